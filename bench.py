@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Flagship training benchmark (driver contract).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric: training samples/sec of the P128 RIS system named in BASELINE.json
+("P128 RIS, 8-qubit QuantumNAT QNN + CNN estimator, bf16"): one step = the QSC scenario
+classifier (8 qubits, 3 layers, QuantumNAT noise) + the HDCE estimator (3 scenario
+experts + shared 4096->2048 FC, per-stream NMSE) forward + backward + optimizer on
+9 streams x 256 samples PER GPU (weak scaling; reference step R:181-204 / R:335-370),
+synthetic DeepMIMO-shaped data resident in HBM, random-init weights.
+
+W untimed warm-up steps, then K timed steps bracketed by barrier + device sync; the
+slowest rank's time is used; rank 0 prints ONE JSON line with the whole-job value.
+The reference publishes no throughput, so vs_baseline is null.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="per-stream batch (batch_size_DML)")
+    ap.add_argument("--qubits", type=int, default=8)
+    ap.add_argument("--data-len", type=int, default=20000)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-quantumnat", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import init_distributed, shutdown
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
+                                                                                                FlagshipTrainer)
+
+    world_env = int(os.environ.get("WORLD_SIZE", 1))
+    if world_env != args.gpus and world_env != 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+    ctx = init_distributed("auto")
+    cfg = FlagshipConfig(n_qubits=args.qubits, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
+                         hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat)
+    tr = FlagshipTrainer(cfg, ctx)
+    sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
+
+    for _ in range(args.warmup):
+        tr.step()
+    sync()
+    ctx.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    sync()
+    ctx.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    elapsed = ctx.max_scalar(elapsed)
+
+    hl = tr.hloss.tolist()
+    ql = float(tr.qloss.item())
+    n = ctx.world
+    samples = tr.samples_per_step * n * args.steps
+    value = samples / elapsed
+    if ctx.is_main:
+        rec = {
+            "metric": "NMSE(dB) vs SNR + samples/sec, P128 RIS estimator at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (DeepMIMO-shaped geometric channels, HBM-resident), random-init weights",
+            "config": {
+                "model": f"P128 RIS, {args.qubits}-qubit QuantumNAT QNN + CNN estimator (HDCE: 3x Conv_P128 + FC_P128)",
+                "global_batch": tr.samples_per_step * n,
+                "per_gpu_batch": tr.samples_per_step,
+                "streams": tr.S,
+                "batch_size_DML": args.batch,
+                "seq_len": None,
+                "parallelism": f"dp{n}",
+                "hip_graphs": bool(tr.graphed.enabled),
+                "quantumnat": cfg.use_quantumnat,
+            },
+            "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
+        }
+        print(json.dumps(rec), flush=True)
+    shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,173 @@
+"""Build and load the framework's native code.
+
+Two shared objects are produced IN-TREE under ``<pkg>/lib`` (so they travel with a
+repo snapshot to a GPU box):
+
+* ``libqdml_hip.so`` -- every ``csrc/hip/*.hip`` kernel, compiled by ``hipcc
+  --offload-arch=gfx950`` (CDNA4 only; no CUDA / hipify / dual paths).  Launchers
+  are ``extern "C"`` functions taking raw device pointers and a ``hipStream_t``;
+  they enqueue on torch's current stream, so they are captured by HIP graphs
+  like any other kernel.
+* ``libqdml_cpu.so`` -- the C++/OpenMP runtime pieces (CPU state-vector simulator,
+  host data utilities).
+
+The HIP library links ``libamdhip64.so.7``; torch must be imported first so the
+dynamic loader binds that SONAME to the HIP runtime torch already loaded (one
+runtime per process, shared streams).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import shutil
+import subprocess
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+OBJ_DIR = os.path.join(LIB_DIR, "obj")
+HIP_LIB = os.path.join(LIB_DIR, "libqdml_hip.so")
+CPU_LIB = os.path.join(LIB_DIR, "libqdml_cpu.so")
+ARCH = os.environ.get("QDML_OFFLOAD_ARCH", "gfx950")
+
+_lock = threading.Lock()
+_hip: Optional[ctypes.CDLL] = None
+_cpu: Optional[ctypes.CDLL] = None
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def _sources(sub: str, ext: str) -> List[str]:
+    d = os.path.join(CSRC, sub)
+    return sorted(os.path.join(d, f) for f in os.listdir(d) if f.endswith(ext))
+
+
+def _headers(sub: str) -> List[str]:
+    d = os.path.join(CSRC, sub)
+    return [os.path.join(d, f) for f in os.listdir(d) if f.endswith((".h", ".hpp", ".cuh"))]
+
+
+def _stale(target: str, deps: List[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: List[str], verbose: bool) -> None:
+    if verbose:
+        print("[qdml build]", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
+
+
+def hipcc() -> Optional[str]:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    return None
+
+
+def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
+    cc = hipcc()
+    if cc is None:
+        raise NativeUnavailable("hipcc not found")
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    srcs = _sources("hip", ".hip")
+    hdrs = _headers("hip")
+    flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
+             "-Wno-unused-result", "-I", os.path.join(CSRC, "hip")]
+    objs = []
+
+    def one(src: str) -> str:
+        obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+        if force or _stale(obj, [src] + hdrs):
+            _run([cc] + flags + ["-c", src, "-o", obj], verbose)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(one, srcs))
+    if force or _stale(HIP_LIB, objs):
+        _run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", HIP_LIB] + objs, verbose)
+    return HIP_LIB
+
+
+def build_cpu(force: bool = False, verbose: bool = True) -> str:
+    cxx = os.environ.get("CXX", shutil.which("g++") or "g++")
+    srcs = _sources("cpu", ".cpp")
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if force or _stale(CPU_LIB, srcs + _headers("cpu")):
+        _run([cxx, "-O3", "-std=c++17", "-fopenmp", "-fPIC", "-shared", "-o", CPU_LIB] + srcs, verbose)
+    return CPU_LIB
+
+
+def build_all(force: bool = False, verbose: bool = True) -> None:
+    build_cpu(force, verbose)
+    build_hip(force, verbose)
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    # All launchers return an int status (hipError_t) and take pointers / ints /
+    # floats; declare argtypes lazily in ops modules via `fn()`.
+    pass
+
+
+def hip_lib(build_if_missing: bool = True) -> ctypes.CDLL:
+    """The HIP kernel library.  Raises if it cannot be loaded (no silent fallback)."""
+    global _hip
+    if _hip is not None:
+        return _hip
+    with _lock:
+        if _hip is not None:
+            return _hip
+        import torch  # noqa: F401  (bind libamdhip64.so.7 to torch's runtime first)
+        if not os.path.exists(HIP_LIB):
+            if not build_if_missing:
+                raise NativeUnavailable(f"{HIP_LIB} missing; run __graft_entry__.build()")
+            build_hip(verbose=False)
+        _hip = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL)
+    return _hip
+
+
+def cpu_lib(build_if_missing: bool = True) -> ctypes.CDLL:
+    global _cpu
+    if _cpu is not None:
+        return _cpu
+    with _lock:
+        if _cpu is not None:
+            return _cpu
+        if not os.path.exists(CPU_LIB):
+            if not build_if_missing:
+                raise NativeUnavailable(f"{CPU_LIB} missing")
+            build_cpu(verbose=False)
+        _cpu = ctypes.CDLL(CPU_LIB)
+    return _cpu
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        raise RuntimeError(f"{what} failed with HIP status {status}")
+
+
+def fn(lib: ctypes.CDLL, name: str, argtypes, restype=ctypes.c_int):
+    f = getattr(lib, name)
+    if getattr(f, "_qd_declared", False) is False:
+        f.argtypes = argtypes
+        f.restype = restype
+        f._qd_declared = True
+    return f
+
+
+def stream_ptr(device=None) -> ctypes.c_void_p:
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())

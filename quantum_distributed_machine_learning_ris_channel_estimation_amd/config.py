@@ -1,0 +1,155 @@
+"""Typed configuration for the framework.
+
+The reference hard-codes its knobs as attributes of ``Y2HRunner.__init__``
+(Runner_P128_QuantumNAT_onchipQNN.py:20-33) and ``model_val.__init__``
+(Test.py:14-21); QSC constructor knobs live at
+Estimators_QuantumNAT_onchipQNN.py:108-119.  We keep *the same attribute names*
+so existing user code that pokes ``runner.lr = ...`` keeps working, and add the
+MI355X-specific knobs (world size, dtype, qubits, HIP graphs, bucket sizes).
+
+Overrides come from ``update_from_dict`` (CLI ``--set key=value`` or a
+YAML/JSON file via ``load_config_file``).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+
+@dataclass
+class RunnerConfig:
+    # --- reference knobs (R:20-33) -------------------------------------------------
+    Pilot_num: int = 128
+    data_len: int = 20000
+    SNRdb: int = 10
+    num_workers: int = 0
+    batch_size: int = 256          # unused by the reference (R:25); kept for parity
+    batch_size_DML: int = 256      # per-stream batch (R:26)
+    lr: float = 1e-3
+    lr_decay: int = 30             # epochs between x0.5 LR steps (HDCE, R:272-283)
+    lr_threshold: float = 1e-6     # LR floor (R:279)
+    n_epochs: int = 100
+    print_freq: int = 50
+    optimizer: str = "adam"        # 'adam' | 'sgd' (R:40-46)
+    train_test_ratio: float = 0.9
+
+    # --- QSC constructor knobs (E:108, runner passes False/False at R:313-316) -----
+    n_qubits: int = 6
+    n_layers: int = 3
+    n_classes: int = 3
+    use_quantumnat: bool = False
+    use_gradient_pruning: bool = False
+    noise_level: float = 0.01       # E:118
+    gradient_threshold: float = 0.1  # E:119
+    qsc_weight_decay: float = 0.01   # AdamW wd (R:320)
+
+    # --- framework knobs (new) -----------------------------------------------------
+    n_scenarios: int = 3
+    n_users: int = 3
+    workspace: str = "./workspace"
+    data_dir: str = "available_data"
+    synthetic: bool = True          # generate DeepMIMO-shaped data when .npy files are absent
+    seed: int = 0
+    dtype: str = "bf16"             # estimator compute dtype: fp32 | bf16
+    device: str = "auto"            # auto | cuda | cpu
+    backend: str = "auto"           # kernel backend: auto | hip | cpu | torch
+    hip_graphs: bool = True
+    overlap_comm: bool = True
+    bucket_mb: float = 32.0
+    world_size: int = 1
+    log_jsonl: Optional[str] = None
+    deterministic: bool = False
+    nan_guard: bool = True
+    resume: bool = False
+
+    def update_from_dict(self, d: Dict[str, Any]) -> "RunnerConfig":
+        names = {f.name: f for f in dataclasses.fields(self)}
+        for k, v in d.items():
+            if k not in names:
+                raise KeyError(f"unknown config key {k!r}")
+            setattr(self, k, _coerce(v, type(getattr(self, k))))
+        return self
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+
+@dataclass
+class EvalConfig:
+    # --- reference knobs (T:14-21, T:66) ----------------------------------------------
+    training_SNRdb: int = 10
+    num_workers: int = 8
+    batch_size: int = 200
+    batch_size_DML: int = 256
+    training_data_len: int = 20000
+    indicator: int = -1
+    data_len_for_test: int = 10000
+    Pilot_num: int = 128
+    snr_list: tuple = (5, 7, 9, 11, 13, 15)
+    # framework knobs
+    workspace: str = "./workspace"
+    results_dir: str = "results"
+    n_qubits: int = 6
+    n_layers: int = 3
+    seed: int = 1234
+    device: str = "auto"
+    backend: str = "auto"
+
+    def update_from_dict(self, d: Dict[str, Any]) -> "EvalConfig":
+        names = {f.name for f in dataclasses.fields(self)}
+        for k, v in d.items():
+            if k not in names:
+                raise KeyError(f"unknown config key {k!r}")
+            cur = getattr(self, k)
+            setattr(self, k, tuple(v) if isinstance(cur, tuple) else _coerce(v, type(cur)))
+        return self
+
+
+def _coerce(v: Any, ty: type) -> Any:
+    if v is None or ty is type(None):
+        return v
+    if isinstance(v, str) and ty is not str:
+        if ty is bool:
+            return v.lower() in ("1", "true", "yes", "on")
+        return ty(v)
+    if ty is float and isinstance(v, int):
+        return float(v)
+    return v
+
+
+def load_config_file(path: str) -> Dict[str, Any]:
+    """Load a YAML (safe loader only) or JSON override file."""
+    with open(path, "r") as f:
+        text = f.read()
+    if path.endswith((".yaml", ".yml")):
+        import yaml
+        return yaml.safe_load(text) or {}
+    return json.loads(text)
+
+
+def parse_overrides(items) -> Dict[str, Any]:
+    """``["lr=1e-3", "n_qubits=8"]`` -> dict (values parsed as JSON when possible)."""
+    out: Dict[str, Any] = {}
+    for it in items or []:
+        k, _, v = it.partition("=")
+        try:
+            out[k] = json.loads(v)
+        except json.JSONDecodeError:
+            out[k] = v
+    return out
+
+
+def resolve_device(device: str = "auto"):
+    import torch
+    if device == "auto":
+        return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    return torch.device(device)
+
+
+def env_rank_info():
+    """torchrun-compatible rank discovery (RANK / WORLD_SIZE / LOCAL_RANK)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))

@@ -1,0 +1,59 @@
+// Shared helpers for the CDNA4 (gfx950) kernels of this framework.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <type_traits>
+
+#define QD_API extern "C" __attribute__((visibility("default")))
+
+namespace qd {
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Orders LDS traffic of ONE wave without a workgroup barrier: LDS instructions of a
+// wave execute in order, so only the compiler must be kept from reordering.
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64); result valid in every thread.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red /* >= NT/64 floats */) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(static_cast<uint32_t>(h) << 16);
+}
+// Round-to-nearest-even f32 -> bf16 (NaN-preserving via the compiler's cvt).
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+
+}  // namespace qd

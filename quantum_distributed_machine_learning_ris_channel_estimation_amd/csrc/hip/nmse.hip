@@ -1,0 +1,175 @@
+// Fused NMSE loss + gradient for the HDCE estimator.
+//
+// Reference: NMSE_cuda / NMSELoss (Estimators_QuantumNAT_onchipQNN.py:282-295) is a
+// batch-GLOBAL ratio sum((x^-x)^2)/sum(x^2); the runner computes it per stream
+// (9 calls) against the LS label and against the perfect channel (R:112-113) and sums
+// loss/9 (R:195-199).
+//
+// MI355X design: the 9 streams are one (rows x 2048) activation.  Pass 1 computes
+// per-row partial sums (err^2, label^2, errperf^2, perf^2) with one wave per row and
+// 16-byte loads; pass 2 (one block) reduces rows by stream in a fixed order
+// (deterministic), forms loss, loss_perf and the per-stream gradient coefficients
+// 2/(S*den_s), and raises the device `skip` flag if the loss is not finite; pass 3
+// writes dY = coef[stream(row)] * (Y - label) directly in the dtype the FC backward
+// GEMM consumes (bf16 or fp32).  For data-parallel training the per-stream
+// numerators/denominators are all-reduced BEFORE pass 2 (global NMSE, not a mean
+// of per-rank ratios) -- see parallel/dp.py.
+#include "common.h"
+
+namespace qd {
+namespace nmse {
+
+template <typename T>
+__device__ __forceinline__ float4 load4(const T* p);
+template <>
+__device__ __forceinline__ float4 load4<float>(const float* p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+template <>
+__device__ __forceinline__ float4 load4<uint16_t>(const uint16_t* p) {
+  const ushort4 h = *reinterpret_cast<const ushort4*>(p);
+  return make_float4(bf16_to_f32(h.x), bf16_to_f32(h.y), bf16_to_f32(h.z), bf16_to_f32(h.w));
+}
+
+// One wave per row; 4 rows per 256-thread block.  out: (rows, 4) fp32.
+template <typename TY>
+__global__ void __launch_bounds__(256) row_sums_kernel(const TY* __restrict__ Y, const float* __restrict__ Lb,
+                                                       const float* __restrict__ Pf, float* __restrict__ out, int rows,
+                                                       int cols) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const TY* y = Y + (size_t)row * cols;
+  const float* l = Lb + (size_t)row * cols;
+  const float* pf = Pf ? Pf + (size_t)row * cols : nullptr;
+  float e = 0.f, pw = 0.f, ep = 0.f, pp = 0.f;
+  for (int c = lane * 4; c < cols; c += 256) {
+    const float4 yv = load4<TY>(y + c);
+    const float4 lv = *reinterpret_cast<const float4*>(l + c);
+    const float d0 = yv.x - lv.x, d1 = yv.y - lv.y, d2 = yv.z - lv.z, d3 = yv.w - lv.w;
+    e += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    pw += lv.x * lv.x + lv.y * lv.y + lv.z * lv.z + lv.w * lv.w;
+    if (pf) {
+      const float4 pv = *reinterpret_cast<const float4*>(pf + c);
+      const float q0 = yv.x - pv.x, q1 = yv.y - pv.y, q2 = yv.z - pv.z, q3 = yv.w - pv.w;
+      ep += q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;
+      pp += pv.x * pv.x + pv.y * pv.y + pv.z * pv.z + pv.w * pv.w;
+    }
+  }
+  e = wave_sum(e);
+  pw = wave_sum(pw);
+  ep = wave_sum(ep);
+  pp = wave_sum(pp);
+  if (lane == 0) {
+    float4 o = make_float4(e, pw, ep, pp);
+    *reinterpret_cast<float4*>(out + (size_t)row * 4) = o;
+  }
+}
+
+// Per-stream reduction (rows in index order -> deterministic).  stream_sums: (S,4).
+__global__ void __launch_bounds__(256) stream_sums_kernel(const float* __restrict__ rowsums,
+                                                          const int* __restrict__ row_stream, float* __restrict__ ss,
+                                                          int rows, int S) {
+  __shared__ float red[4];
+  for (int s = 0; s < S; ++s) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int r = threadIdx.x; r < rows; r += 256) {
+      if (row_stream[r] != s) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += rowsums[(size_t)r * 4 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float t = block_sum<256>(a[k], red);
+      if (threadIdx.x == 0) ss[s * 4 + k] = t;
+    }
+  }
+}
+
+// loss = sum_s num_s/den_s / S (same for perf); coef_s = 2/(S den_s); skip if non-finite.
+__global__ void finalize_kernel(const float* __restrict__ ss, float* __restrict__ loss, float* __restrict__ coef,
+                                int* __restrict__ skip, int S, float loss_scale) {
+  if (threadIdx.x != 0) return;
+  float l = 0.f, lp = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const float den = ss[s * 4 + 1];
+    l += ss[s * 4 + 0] / den;
+    const float denp = ss[s * 4 + 3];
+    lp += denp > 0.f ? ss[s * 4 + 2] / denp : 0.f;
+    coef[s] = loss_scale * 2.f / ((float)S * den);
+  }
+  loss[0] = l / (float)S;
+  loss[1] = lp / (float)S;
+  if (skip) *skip = isfinite(loss[0]) ? 0 : 1;
+}
+
+template <typename TY, typename TD>
+__global__ void __launch_bounds__(256) grad_kernel(const TY* __restrict__ Y, const float* __restrict__ Lb,
+                                                   const float* __restrict__ coef, const int* __restrict__ row_stream,
+                                                   TD* __restrict__ dY, int rows, int cols) {
+  const long n4 = (long)rows * cols / 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long e = i * 4;
+    const int r = (int)(e / cols);
+    const float c = coef[row_stream[r]];
+    const float4 yv = load4<TY>(Y + e);
+    const float4 lv = *reinterpret_cast<const float4*>(Lb + e);
+    const float g0 = c * (yv.x - lv.x), g1 = c * (yv.y - lv.y), g2 = c * (yv.z - lv.z), g3 = c * (yv.w - lv.w);
+    if constexpr (std::is_same<TD, float>::value) {
+      *reinterpret_cast<float4*>(dY + e) = make_float4(g0, g1, g2, g3);
+    } else {
+      ushort4 h;
+      h.x = f32_to_bf16(g0);
+      h.y = f32_to_bf16(g1);
+      h.z = f32_to_bf16(g2);
+      h.w = f32_to_bf16(g3);
+      *reinterpret_cast<ushort4*>(dY + e) = h;
+    }
+  }
+}
+
+}  // namespace nmse
+}  // namespace qd
+
+using namespace qd::nmse;
+
+// y_bf16: 1 if Y is bf16 else fp32.  perf may be null.
+QD_API int qd_nmse_row_sums(const void* Y, int y_bf16, const float* label, const float* perf, float* rowsums, int rows,
+                            int cols, void* stream) {
+  if (cols % 4) return (int)hipErrorInvalidValue;
+  dim3 grid((rows + 3) / 4);
+  if (y_bf16)
+    hipLaunchKernelGGL(row_sums_kernel<uint16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const uint16_t*)Y, label,
+                       perf, rowsums, rows, cols);
+  else
+    hipLaunchKernelGGL(row_sums_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)Y, label, perf,
+                       rowsums, rows, cols);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_nmse_stream_sums(const float* rowsums, const int* row_stream, float* ss, int rows, int S, void* stream) {
+  hipLaunchKernelGGL(stream_sums_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, rowsums, row_stream, ss, rows, S);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_nmse_finalize(const float* ss, float* loss, float* coef, int* skip, int S, float loss_scale,
+                            void* stream) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ss, loss, coef, skip, S, loss_scale);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_nmse_grad(const void* Y, int y_bf16, const float* label, const float* coef, const int* row_stream,
+                        void* dY, int dy_bf16, int rows, int cols, void* stream) {
+  long n4 = (long)rows * cols / 4;
+  int grid = (int)((n4 + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  hipStream_t st = (hipStream_t)stream;
+#define QD_G(TY, TD) hipLaunchKernelGGL((grad_kernel<TY, TD>), dim3(grid), dim3(256), 0, st, (const TY*)Y, label, coef, \
+                                        row_stream, (TD*)dY, rows, cols)
+  if (y_bf16 && dy_bf16) QD_G(uint16_t, uint16_t);
+  else if (y_bf16) QD_G(uint16_t, float);
+  else if (dy_bf16) QD_G(float, uint16_t);
+  else QD_G(float, float);
+#undef QD_G
+  return (int)hipGetLastError();
+}

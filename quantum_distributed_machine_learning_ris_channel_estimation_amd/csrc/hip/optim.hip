@@ -1,0 +1,133 @@
+// Fused flat-buffer optimizers (Adam / AdamW / SGD-momentum) for gfx950.
+//
+// Reference: Y2HRunner.get_optimizer (Runner_P128_QuantumNAT_onchipQNN.py:40-46):
+// Adam(lr) for each of the 4 HDCE modules (R:160-163), SGD(lr, momentum 0.9), and
+// AdamW(lr, wd=0.01) for the QSC (R:320); on-chip gradient pruning
+// g *= (|g| > thr) over all QSC parameters (E:205-228).
+//
+// MI355X design: every parameter of a model lives in ONE flat fp32 buffer (grads,
+// moments likewise), so a whole optimizer step is one launch of a grid-stride
+// kernel at HBM rate.  All step-dependent scalars (step count, learning rate) are
+// read from DEVICE memory, so the launch can be captured once in a HIP graph and
+// replayed every step; `skip` (set by the loss kernel when the loss is not finite)
+// turns the step into a no-op without a host sync.  Gradient pruning and the DP
+// gradient scale (1/world) are fused into the same pass.
+#include "common.h"
+
+namespace qd {
+namespace optim {
+
+struct AdamArgs {
+  float beta1, beta2, eps, weight_decay, grad_scale, prune_thr;
+  int decoupled;  // 1 = AdamW
+};
+
+__global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n,
+                                                   const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr,
+                                                   const int* __restrict__ skip, unsigned int* __restrict__ pruned,
+                                                   AdamArgs a) {
+  if (skip != nullptr && *skip) return;
+  const float lr = *lr_ptr;
+  const float t = *step_ptr + 1.f;  // step about to be taken
+  const float bc1 = 1.f - __powf(a.beta1, t);
+  const float bc2 = 1.f - __powf(a.beta2, t);
+  const float step_size = lr / bc1;
+  const float rbc2 = rsqrtf(bc2);
+  unsigned int cnt = 0;
+  const long stride = (long)gridDim.x * blockDim.x * 4;
+  for (long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < n; i0 += stride) {
+    if (i0 + 3 < n) {
+      float4 pp = *reinterpret_cast<float4*>(p + i0);
+      float4 gg = *reinterpret_cast<float4*>(g + i0);
+      float4 mm = *reinterpret_cast<float4*>(m + i0);
+      float4 vv = *reinterpret_cast<float4*>(v + i0);
+      float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float gj = ga[j] * a.grad_scale;
+        if (a.prune_thr > 0.f && !(fabsf(gj) > a.prune_thr)) { gj = 0.f; ++cnt; }
+        float pj = pa[j];
+        if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
+        else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
+        ma[j] = a.beta1 * ma[j] + (1.f - a.beta1) * gj;
+        va[j] = a.beta2 * va[j] + (1.f - a.beta2) * gj * gj;
+        const float denom = sqrtf(va[j]) * rbc2 + a.eps;
+        pa[j] = pj - step_size * ma[j] / denom;
+        ga[j] = gj;
+      }
+      *reinterpret_cast<float4*>(p + i0) = pp;
+      *reinterpret_cast<float4*>(m + i0) = mm;
+      *reinterpret_cast<float4*>(v + i0) = vv;
+      if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
+    } else {
+      for (long i = i0; i < n; ++i) {
+        float gj = g[i] * a.grad_scale;
+        if (a.prune_thr > 0.f && !(fabsf(gj) > a.prune_thr)) { gj = 0.f; ++cnt; }
+        float pj = p[i];
+        if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
+        else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
+        m[i] = a.beta1 * m[i] + (1.f - a.beta1) * gj;
+        v[i] = a.beta2 * v[i] + (1.f - a.beta2) * gj * gj;
+        const float denom = sqrtf(v[i]) * rbc2 + a.eps;
+        p[i] = pj - step_size * m[i] / denom;
+        g[i] = gj;
+      }
+    }
+  }
+  if (pruned != nullptr && a.prune_thr > 0.f) {
+    // one atomic per wave (the compiler's wave-level atomic coalescing would not sum counts)
+    float c = wave_sum((float)cnt);
+    if ((threadIdx.x & 63) == 0 && c > 0.f) atomicAdd(pruned, (unsigned int)c);
+  }
+}
+
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                  float* __restrict__ buf, long n, const float* __restrict__ lr_ptr,
+                                                  const float* __restrict__ step_ptr, const int* __restrict__ skip,
+                                                  float momentum, float weight_decay, float grad_scale) {
+  if (skip != nullptr && *skip) return;
+  const float lr = *lr_ptr;
+  const bool first = *step_ptr < 0.5f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gj = g[i] * grad_scale + weight_decay * p[i];
+    float b = first ? gj : momentum * buf[i] + gj;
+    buf[i] = b;
+    p[i] -= lr * b;
+  }
+}
+
+__global__ void step_tick_kernel(float* step, const int* skip) {
+  if (skip == nullptr || *skip == 0) *step += 1.f;
+}
+
+inline int grid_for(long n) {
+  long b = (n / 4 + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 2048) b = 2048;
+  return (int)b;
+}
+
+}  // namespace optim
+}  // namespace qd
+
+using namespace qd::optim;
+
+QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const int* skip,
+                        unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
+                        float grad_scale, float prune_thr, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  AdamArgs a{beta1, beta2, eps, weight_decay, grad_scale, prune_thr, decoupled};
+  if (n > 0) hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a);
+  hipLaunchKernelGGL(step_tick_kernel, dim3(1), dim3(1), 0, st, step, skip);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_sgd_step(float* p, float* g, float* buf, long n, const float* lr, float* step, const int* skip,
+                       float momentum, float weight_decay, float grad_scale, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (n > 0) hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, buf, n, lr, step, skip, momentum,
+                                weight_decay, grad_scale);
+  hipLaunchKernelGGL(step_tick_kernel, dim3(1), dim3(1), 0, st, step, skip);
+  return (int)hipGetLastError();
+}

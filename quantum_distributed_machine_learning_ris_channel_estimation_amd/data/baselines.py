@@ -1,0 +1,67 @@
+"""LS and LMMSE channel-estimation baselines.
+
+Reference: ``generate_data.generate_MMSE_estimate(HLS, sigma2)`` (called at Test.py:145,
+not shipped).  It refines the full-grid LS estimate given the pilot noise variance
+``sigma2 = 10^(-snr/10)``.  We implement linear MMSE with a channel covariance learned
+from the synthetic generator:
+
+  H_mmse = W HLS,  W = R (R + s2_LS I)^-1,  s2_LS = sigma2 * 10^(LS_GAIN_DB/10)
+
+``mode='freq'`` (default) uses the 16x16 subcarrier covariance per RIS element (the
+classic OFDM LMMSE); ``mode='full'`` the full 1024x1024 covariance.  The filter is
+applied as a complex GEMM (on the GPU when the input is there).
+"""
+from __future__ import annotations
+
+from functools import lru_cache
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .channel import H_DIM, LS_GAIN_DB, N_ELEM, N_SUBC, generate_mixed
+
+
+def covariance(H: torch.Tensor, mode: str = "freq") -> torch.Tensor:
+    if mode == "freq":
+        h = H.reshape(-1, N_ELEM, N_SUBC).reshape(-1, N_SUBC)
+        return (h.T @ h.conj()) / h.shape[0]          # R[f, f'] = E[h_f h_f'^*]
+    if mode == "full":
+        return (H.T @ H.conj()) / H.shape[0]
+    raise ValueError(mode)
+
+
+def lmmse_matrix(R: torch.Tensor, noise_var: float) -> torch.Tensor:
+    """W = R (R + s2 I)^-1 computed via the Hermitian eigendecomposition."""
+    R = R.to(torch.complex128)
+    evals, U = torch.linalg.eigh(R)
+    evals = evals.clamp_min(0)
+    gain = evals / (evals + noise_var)
+    return (U * gain.to(U.dtype)) @ U.conj().T
+
+
+def apply_lmmse(HLS: torch.Tensor, W: torch.Tensor, mode: str = "freq") -> torch.Tensor:
+    W = W.to(device=HLS.device, dtype=torch.complex64)
+    if mode == "freq":
+        h = HLS.reshape(-1, N_ELEM, N_SUBC)
+        return (h @ W.T).reshape(-1, H_DIM)
+    return HLS @ W.T
+
+
+@lru_cache(maxsize=4)
+def _calibration_covariance(mode: str, n: int = 4096, seed: int = 7) -> torch.Tensor:
+    _, _, H, _ = generate_mixed(n, snr_db=100.0, index=-1, base_seed=seed, split="calib")
+    return covariance(H, mode)
+
+
+def lmmse_estimate(HLS: torch.Tensor, sigma2: float, mode: str = "freq",
+                   R: Optional[torch.Tensor] = None) -> torch.Tensor:
+    R = _calibration_covariance(mode) if R is None else R
+    W = lmmse_matrix(R, sigma2 * 10 ** (LS_GAIN_DB / 10))
+    return apply_lmmse(HLS, W, mode)
+
+
+def generate_MMSE_estimate(HLS_np, sigma2: float, mode: str = "freq"):
+    """Reference-compatible signature (Test.py:145): complex ndarray in, complex ndarray out."""
+    HLS = torch.as_tensor(np.asarray(HLS_np)).to(torch.complex64)
+    return lmmse_estimate(HLS, sigma2, mode).numpy()

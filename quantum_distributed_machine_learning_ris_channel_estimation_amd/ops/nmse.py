@@ -1,0 +1,92 @@
+"""Per-stream NMSE loss with a fused gradient (csrc/hip/nmse.hip).
+
+Reference: ``NMSE_cuda`` (Estimators_QuantumNAT_onchipQNN.py:282-286) applied per
+stream and averaged over the 9 streams (Runner_P128_QuantumNAT_onchipQNN.py:194-199).
+
+``StreamNMSE`` evaluates, for an activation Y whose rows belong to S streams,
+  loss      = (1/S) sum_s sum_{r in s} |Y_r - L_r|^2 / sum_{r in s} |L_r|^2
+  loss_perf = same against the perfect channel (monitor, R:113)
+and returns dY = dloss/dY without autograd (the HDCE engine feeds it straight into
+the FC backward).  The row->stream map is a device int32 tensor, so any row order
+(e.g. the expert-interleaved order of the grouped estimator) works.
+
+In data-parallel runs ``sums()`` + all-reduce + ``finalize()`` give the GLOBAL NMSE
+(sum of errors over sum of powers across ranks), never a mean of per-rank ratios.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _native as nat
+
+_p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+
+
+class StreamNMSE:
+    def __init__(self, row_stream: torch.Tensor, n_streams: int, cols: int = 2048):
+        self.row_stream = row_stream.to(torch.int32).contiguous()
+        self.rows = row_stream.numel()
+        self.S = n_streams
+        self.cols = cols
+        dev = row_stream.device
+        self.rowsums = torch.zeros(self.rows, 4, device=dev)
+        self.ss = torch.zeros(n_streams, 4, device=dev)       # (err, pow, err_perf, pow_perf) per stream
+        self.loss = torch.zeros(2, device=dev)               # (loss, loss_perf)
+        self.coef = torch.zeros(n_streams, device=dev)
+        self.skip = torch.zeros(1, device=dev, dtype=torch.int32)
+        self._rs_long = self.row_stream.long()
+
+    def sums(self, Y: torch.Tensor, label: torch.Tensor, perf: Optional[torch.Tensor]) -> torch.Tensor:
+        assert Y.shape == (self.rows, self.cols) and label.dtype == torch.float32
+        if Y.is_cuda:
+            lib = nat.hip_lib()
+            st = nat.stream_ptr(Y.device)
+            f = nat.fn(lib, "qd_nmse_row_sums", [_p, _i, _p, _p, _p, _i, _i, _p])
+            nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label),
+                        nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowsums), self.rows, self.cols, st),
+                      "nmse_row_sums")
+            g = nat.fn(lib, "qd_nmse_stream_sums", [_p, _p, _p, _i, _i, _p])
+            nat.check(g(nat.ptr(self.rowsums), nat.ptr(self.row_stream), nat.ptr(self.ss), self.rows, self.S, st),
+                      "nmse_stream_sums")
+        else:
+            Yf = Y.float()
+            rs = torch.stack([((Yf - label) ** 2).sum(1), (label ** 2).sum(1),
+                              ((Yf - perf) ** 2).sum(1) if perf is not None else torch.zeros(self.rows),
+                              (perf ** 2).sum(1) if perf is not None else torch.zeros(self.rows)], 1)
+            self.ss.zero_().index_add_(0, self._rs_long, rs)
+        return self.ss
+
+    def finalize(self, loss_scale: float = 1.0) -> torch.Tensor:
+        if self.ss.is_cuda:
+            lib = nat.hip_lib()
+            f = nat.fn(lib, "qd_nmse_finalize", [_p, _p, _p, _p, _i, _f, _p])
+            nat.check(f(nat.ptr(self.ss), nat.ptr(self.loss), nat.ptr(self.coef), nat.ptr(self.skip), self.S,
+                        loss_scale, nat.stream_ptr(self.ss.device)), "nmse_finalize")
+        else:
+            ss = self.ss
+            self.loss[0] = (ss[:, 0] / ss[:, 1]).sum() / self.S
+            self.loss[1] = (ss[:, 2] / ss[:, 3].clamp_min(1e-30)).sum() / self.S
+            self.coef.copy_(loss_scale * 2.0 / (self.S * ss[:, 1]))
+            self.skip.fill_(0 if torch.isfinite(self.loss[0]) else 1)
+        return self.loss
+
+    def grad(self, Y: torch.Tensor, label: torch.Tensor, out_dtype=torch.float32,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        dY = out if out is not None else torch.empty(self.rows, self.cols, device=Y.device, dtype=out_dtype)
+        if Y.is_cuda:
+            lib = nat.hip_lib()
+            f = nat.fn(lib, "qd_nmse_grad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _p])
+            nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label), nat.ptr(self.coef),
+                        nat.ptr(self.row_stream), nat.ptr(dY), int(dY.dtype == torch.bfloat16), self.rows, self.cols,
+                        nat.stream_ptr(Y.device)), "nmse_grad")
+        else:
+            dY.copy_(self.coef[self._rs_long][:, None] * (Y.float() - label))
+        return dY
+
+    def __call__(self, Y, label, perf=None, out_dtype=torch.float32) -> Tuple[torch.Tensor, torch.Tensor]:
+        self.sums(Y, label, perf)
+        self.finalize()
+        return self.loss, self.grad(Y, label, out_dtype)

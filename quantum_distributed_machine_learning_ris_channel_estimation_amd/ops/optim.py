@@ -1,0 +1,217 @@
+"""Flat parameter spaces and the fused optimizers that update them.
+
+Reference optimizers: ``Y2HRunner.get_optimizer`` (Runner_P128_QuantumNAT_onchipQNN.py:40-46),
+four separate ``Adam``s for Conv0/1/2 + CE (R:160-163), ``AdamW(wd=0.01)`` for the QSC
+(R:320), and ``QSC_P128.apply_gradient_pruning`` (E:205-228).
+
+``FlatParamSpace`` re-points every parameter of a set of modules at a view of ONE
+contiguous fp32 buffer (grads likewise), so that
+  * zero_grad is one memset,
+  * the data-parallel gradient all-reduce is one RCCL call per bucket,
+  * the optimizer step is one HIP kernel (csrc/hip/optim.hip) -- four Adams with
+    identical hyper-parameters are exactly one Adam over the concatenation.
+All step-dependent scalars live on the device, so a captured HIP graph replays
+correctly step after step (LR changes are a device write, not a re-capture).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import _native as nat
+
+_p, _i, _f, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
+ALIGN = 16  # elements; keeps every parameter view 64-byte aligned for float4 access
+
+
+class FlatParamSpace:
+    def __init__(self, params: Sequence[Tuple[str, nn.Parameter]], device=None):
+        seen = set()
+        uniq = []
+        for name, p in params:
+            if id(p) in seen:
+                continue
+            seen.add(id(p))
+            uniq.append((name, p))
+        self.names = [n for n, _ in uniq]
+        self.params = [p for _, p in uniq]
+        device = torch.device(device) if device is not None else self.params[0].device
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+        self.offsets = offs
+        self.numel = off
+        self.flat = torch.zeros(off, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(off, device=device, dtype=torch.float32)
+        for p, o in zip(self.params, offs):
+            n = p.numel()
+            view = self.flat[o:o + n].view(p.shape)
+            view.copy_(p.data.to(device, torch.float32))
+            p.data = view
+            p.grad = self.grad[o:o + n].view(p.shape)
+
+    def slice_of(self, p: torch.Tensor) -> slice:
+        for q, o in zip(self.params, self.offsets):
+            if q is p:
+                return slice(o, o + q.numel())
+        raise KeyError("parameter not in space")
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def reattach_grads(self) -> None:
+        """Restore the grad views if user code set ``p.grad = None``."""
+        for p, o in zip(self.params, self.offsets):
+            if p.grad is None or p.grad.data_ptr() != self.grad[o:].data_ptr():
+                p.grad = self.grad[o:o + p.numel()].view(p.shape)
+
+
+class FusedOptimizer:
+    """Adam / AdamW / SGD-momentum over a FlatParamSpace, one kernel per step.
+
+    ``prune_thr`` > 0 fuses on-chip gradient pruning (g *= |g| > thr) into the step,
+    ``grad_scale`` fuses gradient averaging; ``skip`` (device int) makes the step a no-op.
+    """
+
+    def __init__(self, space: FlatParamSpace, kind: str = "adam", lr: float = 1e-3, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.0, momentum: float = 0.9, prune_thr: float = 0.0):
+        if kind not in ("adam", "adamw", "sgd"):
+            raise NotImplementedError(f"Optimizer {kind} not understood.")
+        self.space = space
+        self.kind = kind
+        self.betas = betas
+        self.eps = eps
+        self.weight_decay = weight_decay
+        self.momentum = momentum
+        self.prune_thr = prune_thr
+        dev = space.flat.device
+        self.lr_t = torch.full((1,), lr, device=dev, dtype=torch.float32)
+        self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.pruned = torch.zeros(1, device=dev, dtype=torch.int32)
+        if kind == "sgd":
+            self.buf = torch.zeros_like(space.flat)
+        else:
+            self.m = torch.zeros_like(space.flat)
+            self.v = torch.zeros_like(space.flat)
+        self._lr_host = lr
+        # torch.optim-like view for code that reads/writes param_groups[0]['lr']
+        self.param_groups = [_LRGroup(self)]
+
+    # ---------------------------------------------------------------- lr
+    @property
+    def lr(self) -> float:
+        return self._lr_host
+
+    def set_lr(self, lr: float) -> None:
+        self._lr_host = float(lr)
+        self.lr_t.fill_(float(lr))
+
+    # ---------------------------------------------------------------- step
+    def step(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None) -> None:
+        s = self.space
+        if s.flat.is_cuda:
+            lib = nat.hip_lib()
+            st = nat.stream_ptr(s.flat.device)
+            skp = nat.ptr(skip) if skip is not None else None
+            if self.kind == "sgd":
+                f = nat.fn(lib, "qd_sgd_step", [_p, _p, _p, _l, _p, _p, _p, _f, _f, _f, _p])
+                nat.check(f(nat.ptr(s.flat), nat.ptr(s.grad), nat.ptr(self.buf), s.numel, nat.ptr(self.lr_t),
+                            nat.ptr(self.step_t), skp, self.momentum, self.weight_decay, grad_scale, st), "sgd")
+            else:
+                f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f, _p])
+                nat.check(f(nat.ptr(s.flat), nat.ptr(s.grad), nat.ptr(self.m), nat.ptr(self.v), s.numel,
+                            nat.ptr(self.lr_t), nat.ptr(self.step_t), skp, nat.ptr(self.pruned), self.betas[0],
+                            self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
+                            self.prune_thr, st), "adam")
+            return
+        self._step_host(grad_scale, skip)
+
+    @torch.no_grad()
+    def _step_host(self, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
+        """CPU path (same math as optim.hip; the CPU has no HIP kernels)."""
+        if skip is not None and int(skip.item()) != 0:
+            return
+        s = self.space
+        p, g = s.flat, s.grad
+        if grad_scale != 1.0:
+            g.mul_(grad_scale)
+        if self.prune_thr > 0:
+            mask = g.abs() > self.prune_thr
+            self.pruned += (~mask).sum().to(torch.int32)
+            g.mul_(mask)
+        lr = float(self.lr_t.item())
+        if self.kind == "sgd":
+            d = g + self.weight_decay * p if self.weight_decay else g
+            if self.step_t.item() == 0:
+                self.buf.copy_(d)
+            else:
+                self.buf.mul_(self.momentum).add_(d)
+            p.sub_(lr * self.buf)
+        else:
+            t = float(self.step_t.item()) + 1.0
+            b1, b2 = self.betas
+            if self.kind == "adamw":
+                p.mul_(1 - lr * self.weight_decay)
+                d = g
+            else:
+                d = g + self.weight_decay * p if self.weight_decay else g
+            self.m.mul_(b1).add_(d, alpha=1 - b1)
+            self.v.mul_(b2).addcmul_(d, d, value=1 - b2)
+            denom = (self.v.sqrt() / (1 - b2 ** t) ** 0.5).add_(self.eps)
+            p.addcdiv_(self.m, denom, value=-lr / (1 - b1 ** t))
+        self.step_t += 1
+
+    def zero_grad(self) -> None:
+        self.space.zero_grad()
+
+    # ---------------------------------------------------------------- state
+    def state_dict(self) -> Dict:
+        d = {"kind": self.kind, "lr": self._lr_host, "step": self.step_t.cpu(), "betas": self.betas, "eps": self.eps,
+             "weight_decay": self.weight_decay, "prune_thr": self.prune_thr}
+        if self.kind == "sgd":
+            d["buf"] = self.buf.cpu()
+        else:
+            d["m"], d["v"] = self.m.cpu(), self.v.cpu()
+        return d
+
+    def load_state_dict(self, d: Dict) -> None:
+        self.set_lr(d["lr"])
+        self.step_t.copy_(d["step"])
+        if self.kind == "sgd":
+            self.buf.copy_(d["buf"])
+        else:
+            self.m.copy_(d["m"])
+            self.v.copy_(d["v"])
+
+
+class _LRGroup(dict):
+    def __init__(self, opt: FusedOptimizer):
+        super().__init__()
+        self._opt = opt
+
+    def __getitem__(self, k):
+        if k == "lr":
+            return self._opt.lr
+        return super().__getitem__(k)
+
+    def __setitem__(self, k, v):
+        if k == "lr":
+            self._opt.set_lr(v)
+        else:
+            super().__setitem__(k, v)
+
+
+def make_optimizer(space: FlatParamSpace, name: str, lr: float, **kw) -> FusedOptimizer:
+    """Reference ``get_optimizer`` semantics: 'adam' -> Adam(lr), 'sgd' -> SGD(lr, 0.9), 'adamw'."""
+    name = name.lower()
+    if name == "adam":
+        return FusedOptimizer(space, "adam", lr, **kw)
+    if name == "adamw":
+        return FusedOptimizer(space, "adamw", lr, weight_decay=kw.pop("weight_decay", 0.01), **kw)
+    if name == "sgd":
+        return FusedOptimizer(space, "sgd", lr, momentum=kw.pop("momentum", 0.9), **kw)
+    raise NotImplementedError(f"Optimizer {name} not understood.")

@@ -1,0 +1,195 @@
+"""SPMD data parallelism over RCCL (torch.distributed 'nccl' backend on ROCm) / Gloo on CPU.
+
+Reference: the only multi-GPU mechanism is ``torch.nn.DataParallel`` over 4 GPUs
+(Runner_P128_QuantumNAT_onchipQNN.py:135-153, Test.py:70-97): single process, one
+Python thread per GPU, the module re-replicated on EVERY forward (the 32 MiB FC
+weight broadcast 9x per step), gradients reduced to GPU0 9x per step (one per
+``backward()``), outputs gathered to GPU0.
+
+MI355X design:
+  * one process per GPU (torchrun-compatible env: RANK / WORLD_SIZE / LOCAL_RANK /
+    MASTER_ADDR / MASTER_PORT); weights stay resident -- a single rank-0 broadcast at
+    init replaces the per-call replicate;
+  * each rank owns a contiguous shard of the HBM-resident dataset and samples it
+    independently (weak scaling: per-GPU work fixed);
+  * gradients live in flat buffers; each bucket is ONE all-reduce launched
+    asynchronously the moment backward finalises it (FC bucket first, while the conv
+    backward still runs), the averaging factor 1/world is fused into the optimizer;
+  * xGMI is point-to-point (7 links/GPU): RCCL rings are per-link bound, so we send
+    few, large messages -- the 33.6 MB FC gradient as a single bucket, all small
+    parameter grads coalesced into one second bucket;
+  * metrics (NMSE numerators/denominators, correct/total counts, loss sums) are
+    all-reduced as raw sums -- the global NMSE is sum(err)/sum(pow), never a mean of
+    per-rank ratios.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.distributed:
+            dist.broadcast(t, src)
+        return t
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.distributed:
+            dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                                   "min": dist.ReduceOp.MIN}[op])
+        return t
+
+    def max_scalar(self, v: float) -> float:
+        if not self.distributed:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+_CTX: Optional[DistContext] = None
+
+
+def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
+    """Initialise from torchrun-style env vars; world 1 needs no process group."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    use_cuda = (device in ("auto", "cuda")) and torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    backend = "none"
+    if world > 1:
+        backend = "nccl" if use_cuda else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s),
+                                **kw)
+    _CTX = DistContext(rank, world, local, dev, backend)
+    return _CTX
+
+
+def get_context() -> DistContext:
+    return _CTX if _CTX is not None else DistContext()
+
+
+def shutdown() -> None:
+    global _CTX
+    if _CTX is not None and _CTX.distributed and dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None
+
+
+class GradBuckets:
+    """Asynchronous all-reduce of named gradient buckets.
+
+    A bucket is a list of flat fp32 tensors; a single tensor is reduced in place, several
+    are coalesced through a staging buffer (one collective either way).  ``launch(name)``
+    enqueues the collective after everything already on the current stream (RCCL's stream
+    waits on it); ``wait()`` makes the current stream wait for all launched collectives and
+    scatters coalesced results back -- no host synchronisation anywhere.
+    """
+
+    def __init__(self, ctx: DistContext, buckets: Dict[str, Sequence[torch.Tensor]]):
+        self.ctx = ctx
+        self.buckets = {k: list(v) for k, v in buckets.items()}
+        self.staging: Dict[str, torch.Tensor] = {}
+        for k, ts in self.buckets.items():
+            if len(ts) > 1:
+                self.staging[k] = torch.empty(sum(t.numel() for t in ts), device=ts[0].device, dtype=ts[0].dtype)
+        self.pending: List = []
+
+    def bucket_bytes(self) -> Dict[str, int]:
+        return {k: sum(t.numel() * t.element_size() for t in ts) for k, ts in self.buckets.items()}
+
+    def launch(self, name: str) -> None:
+        if not self.ctx.distributed or name not in self.buckets:
+            return
+        ts = self.buckets[name]
+        if len(ts) == 1:
+            work = dist.all_reduce(ts[0], async_op=True)
+            self.pending.append((work, None, None))
+        else:
+            st = self.staging[name]
+            torch.cat([t.reshape(-1) for t in ts], out=st)
+            work = dist.all_reduce(st, async_op=True)
+            self.pending.append((work, st, ts))
+
+    def launch_all(self) -> None:
+        for k in self.buckets:
+            self.launch(k)
+
+    def wait(self) -> None:
+        for work, st, ts in self.pending:
+            work.wait()
+            if st is not None:
+                o = 0
+                for t in ts:
+                    n = t.numel()
+                    t.view(-1).copy_(st[o:o + n])
+                    o += n
+        self.pending.clear()
+
+
+class DeviceSampler:
+    """Per-rank shuffled mini-batch indices over an HBM-resident shard (reference:
+    DataLoader(shuffle=True) over the zipped 9-stream dataset, R:88-93).  Partial last
+    batches are kept, as with drop_last=False."""
+
+    def __init__(self, n: int, batch: int, device, seed: int = 0, rank: int = 0, shuffle: bool = True,
+                 drop_last: bool = False):
+        self.n, self.batch, self.device = n, batch, device
+        self.seed, self.rank, self.shuffle, self.drop_last = seed, rank, shuffle, drop_last
+        self.epoch = 0
+
+    def __len__(self) -> int:
+        return self.n // self.batch if self.drop_last else (self.n + self.batch - 1) // self.batch
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = epoch
+
+    def __iter__(self):
+        if self.shuffle:
+            g = torch.Generator(device="cpu")
+            g.manual_seed(self.seed * 1000003 + self.epoch * 7919 + self.rank)
+            perm = torch.randperm(self.n, generator=g).to(self.device)
+        else:
+            perm = torch.arange(self.n, device=self.device)
+        for i in range(len(self)):
+            yield perm[i * self.batch:(i + 1) * self.batch]

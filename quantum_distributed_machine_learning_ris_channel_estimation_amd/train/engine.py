@@ -1,0 +1,267 @@
+"""Fused training engines for the HDCE estimator and the scenario classifiers.
+
+Reference hot loops (Runner_P128_QuantumNAT_onchipQNN.py):
+  * HDCE (R:181-204): for each of 9 (scenario, user) streams, pack on the host, H2D,
+    run Conv[sid] then the shared CE under DataParallel (which re-broadcasts the 32 MiB
+    FC weight and reduces its gradient to GPU0 on EVERY call), NMSE loss / 9, and a
+    separate ``backward()`` per stream; then step 4 Adam optimizers.
+  * QSC (R:335-370): 9 serial forwards of the hybrid classifier, one backward, pruning,
+    AdamW.
+
+MI355X design implemented here:
+  * the dataset is HBM-resident (data/datasets.DMLStore); a step gathers its rows on
+    the device -- no host packing, no H2D;
+  * all 9 streams are ONE step.  The three scenario experts run as one grouped
+    convolution: the expert index is folded into the channel axis (input
+    (3*B, 3*2, H, W), groups=3), so one kernel per layer serves all experts and the
+    per-expert activations land, already flattened C-major, as rows of a single
+    (9*B, 4096) FC operand (rows ordered user, batch, expert);
+  * BatchNorm is "ghost" BN over each 256-sample stream batch -- exactly the
+    statistics the reference's per-stream Conv calls see (R:194), including three
+    sequential momentum updates of each expert's running stats per step;
+  * the FC GEMM runs in bf16 with fp32 accumulation; the per-stream NMSE and its
+    gradient come from the fused kernels in ops/nmse.py;
+  * backward is split explicitly at the FC input: FC grads (32 MiB) are complete
+    first, so data-parallel all-reduce of that bucket overlaps the conv backward;
+  * parameters live in FlatParamSpaces; the optimizer step is one kernel.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..models.estimators import Conv_P128, FC_P128, QSC_P128, SC_P128, pilot_grid
+from ..ops.nmse import StreamNMSE
+from ..ops.optim import FlatParamSpace
+
+CONV_PARAM_ORDER = ["cnn.0.weight", "cnn.1.weight", "cnn.1.bias", "cnn.3.weight", "cnn.4.weight", "cnn.4.bias",
+                    "cnn.6.weight", "cnn.7.weight", "cnn.7.bias"]
+BN_IDX = [1, 4, 7]
+
+
+def _dtype(name: str) -> torch.dtype:
+    return {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}[name]
+
+
+class HDCEModel:
+    """3 scenario experts (Conv_P128) + shared FC_P128, stored grouped for one-kernel-per-layer
+    execution.  The reference modules stay the single source of parameters (their tensors are
+    views into the flat buffer), so ``Conv0.state_dict()`` etc. remain reference-compatible."""
+
+    def __init__(self, pilot_num: int = 128, device="cpu", dtype: str = "bf16", n_experts: int = 3):
+        self.device = torch.device(device)
+        self.E = n_experts
+        self.H, self.W = pilot_grid(pilot_num)
+        self.compute_dtype = _dtype(dtype) if self.device.type == "cuda" else torch.float32
+        self.convs = [Conv_P128(pilot_num).to(self.device) for _ in range(n_experts)]
+        self.fc = FC_P128(pilot_num).to(self.device)
+        named = []
+        for pname in CONV_PARAM_ORDER:
+            for e, m in enumerate(self.convs):
+                named.append((f"Conv{e}.{pname}", m.get_parameter(pname)))
+        named += [("CE.FC.weight", self.fc.FC.weight), ("CE.FC.bias", self.fc.FC.bias)]
+        self.space = FlatParamSpace(named, self.device)
+        # grouped leaf views over the expert-consecutive parameter blocks
+        self.conv_w, self.bn_w, self.bn_b = [], [], []
+        for k in range(3):
+            self.conv_w.append(self._group_leaf(f"Conv0.cnn.{3 * k}.weight"))
+            self.bn_w.append(self._group_leaf(f"Conv0.cnn.{3 * k + 1}.weight"))
+            self.bn_b.append(self._group_leaf(f"Conv0.cnn.{3 * k + 1}.bias"))
+        self.fc_w = self._leaf(self.fc.FC.weight)
+        self.fc_b = self._leaf(self.fc.FC.bias)
+        # grouped BN running statistics; the modules' buffers become views
+        C = 32 * n_experts
+        self.run_mean = [torch.zeros(C, device=self.device) for _ in range(3)]
+        self.run_var = [torch.ones(C, device=self.device) for _ in range(3)]
+        for k, idx in enumerate(BN_IDX):
+            for e, m in enumerate(self.convs):
+                bn = m.cnn[idx]
+                bn.running_mean = self.run_mean[k][e * 32:(e + 1) * 32]
+                bn.running_var = self.run_var[k][e * 32:(e + 1) * 32]
+        self.momentum, self.eps = 0.1, 1e-5
+        self._fc_w_lp = None
+
+    # ------------------------------------------------------------------ params
+    def _group_leaf(self, first_name: str) -> torch.Tensor:
+        i = self.space.names.index(first_name)
+        p0 = self.space.params[i]
+        o = self.space.offsets[i]
+        n = p0.numel() * self.E
+        shape = (p0.shape[0] * self.E,) + tuple(p0.shape[1:])
+        leaf = self.space.flat[o:o + n].view(shape)
+        leaf.requires_grad_(True)
+        leaf.grad = self.space.grad[o:o + n].view(shape)
+        return leaf
+
+    def _leaf(self, p: torch.Tensor) -> torch.Tensor:
+        sl = self.space.slice_of(p)
+        leaf = self.space.flat[sl].view(p.shape)
+        leaf.requires_grad_(True)
+        leaf.grad = self.space.grad[sl].view(p.shape)
+        return leaf
+
+    def modules(self) -> List[nn.Module]:
+        return list(self.convs) + [self.fc]
+
+    def train(self, mode: bool = True):
+        for m in self.modules():
+            m.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def count_batches(self, n: int) -> None:
+        with torch.no_grad():
+            for m in self.convs:
+                for idx in BN_IDX:
+                    m.cnn[idx].num_batches_tracked += n
+
+    # ------------------------------------------------------------------ forward pieces
+    def pack_input(self, Yp: torch.Tensor) -> torch.Tensor:
+        """(E, U, B, 2, H, W) stream-major pilots -> (U*B, E*2, H, W) grouped-conv input."""
+        E, U, B = Yp.shape[:3]
+        return Yp.permute(1, 2, 0, 3, 4, 5).reshape(U * B, E * 2, self.H, self.W)
+
+    def conv_stack(self, x: torch.Tensor, n_groups: int, training: bool) -> torch.Tensor:
+        """Grouped 3-layer conv/BN/ReLU; BN statistics per (sample group, channel)."""
+        dt = self.compute_dtype
+        h = x.to(dt)
+        for k in range(3):
+            z = F.conv2d(h, self.conv_w[k].to(dt), padding=1, groups=self.E)
+            h = self._ghost_bn_relu(z, k, n_groups, training).to(dt)
+        return h
+
+    def _ghost_bn_relu(self, z: torch.Tensor, k: int, U: int, training: bool) -> torch.Tensor:
+        NB, C, H, W = z.shape
+        zf = z.float().view(U, NB // U, C, H * W)
+        if training:
+            var, mean = torch.var_mean(zf, dim=(1, 3), unbiased=False, keepdim=True)  # (U,1,C,1)
+            with torch.no_grad():
+                n = zf.shape[1] * zf.shape[3]
+                unb = var.view(U, C) * (n / max(n - 1, 1))
+                rm, rv = self.run_mean[k], self.run_var[k]
+                for u in range(U):  # sequential updates = the reference's per-stream calls
+                    rm.mul_(1 - self.momentum).add_(mean.view(U, C)[u], alpha=self.momentum)
+                    rv.mul_(1 - self.momentum).add_(unb[u], alpha=self.momentum)
+        else:
+            mean = self.run_mean[k].view(1, 1, C, 1)
+            var = self.run_var[k].view(1, 1, C, 1)
+        y = (zf - mean) * torch.rsqrt(var + self.eps) * self.bn_w[k].view(1, 1, C, 1) + self.bn_b[k].view(1, 1, C, 1)
+        return F.relu(y).view(NB, C, H, W)
+
+    def fc_forward(self, a: torch.Tensor) -> torch.Tensor:
+        dt = self.compute_dtype
+        return F.linear(a.to(dt), self.fc_w.to(dt), self.fc_b.to(dt))
+
+    def features(self, Yp: torch.Tensor, training: bool) -> torch.Tensor:
+        """(E, U, B, 2, H, W) -> FC operand (U*B*E, 32*H*W), rows ordered (u, b, e)."""
+        E, U, B = Yp.shape[:3]
+        h = self.conv_stack(self.pack_input(Yp), U, training)
+        return h.reshape(U * B * E, 32 * self.H * self.W)
+
+    @staticmethod
+    def row_stream(E: int, U: int, B: int, device) -> torch.Tensor:
+        """stream id (e*U + u) of every FC row in (u, b, e) order."""
+        u = torch.arange(U, device=device).view(U, 1, 1)
+        e = torch.arange(E, device=device).view(1, 1, E)
+        return (e * U + u).expand(U, B, E).reshape(-1).to(torch.int32)
+
+    @staticmethod
+    def rows_from_streams(t: torch.Tensor) -> torch.Tensor:
+        """(E, U, B, D) stream-major tensor -> (U*B*E, D) in FC row order."""
+        E, U, B, D = t.shape
+        return t.permute(1, 2, 0, 3).reshape(U * B * E, D)
+
+    # ------------------------------------------------------------------ expert routing (eval)
+    @torch.no_grad()
+    def estimate_routed(self, x: torch.Tensor, expert: torch.Tensor) -> torch.Tensor:
+        """Test-time hierarchical routing (Test.py:166-214): sample i -> Conv_{expert[i]} -> CE.
+
+        Samples are bucketed by expert with one sort (no per-sample Python loop); outputs
+        come back in input order."""
+        order = torch.argsort(expert, stable=True)
+        counts = torch.bincount(expert, minlength=self.E).tolist()
+        xs = x[order]
+        out = torch.empty(x.shape[0], self.fc.FC.out_features, device=x.device, dtype=torch.float32)
+        start = 0
+        for e, c in enumerate(counts):
+            if c == 0:
+                continue
+            seg = xs[start:start + c]
+            h = self.convs[e].eval()(seg.float())
+            out[order[start:start + c]] = self.fc.eval()(h).float()
+            start += c
+        return out
+
+
+class HDCEStep:
+    """One fused HDCE training step over 9 stream batches (see module docstring)."""
+
+    def __init__(self, model: HDCEModel, n_users: int, batch: int, grad_hook: Optional[Callable] = None):
+        self.m = model
+        self.U, self.B = n_users, batch
+        dev = model.device
+        self.nmse = StreamNMSE(HDCEModel.row_stream(model.E, n_users, batch, dev), model.E * n_users)
+        self.grad_hook = grad_hook  # called as grad_hook("fc") / grad_hook("conv") when buckets are final
+
+    def __call__(self, Yp: torch.Tensor, HL: torch.Tensor, HP: torch.Tensor) -> torch.Tensor:
+        """Yp (E,U,B,2,H,W), HL/HP (E,U,B,2048) fp32.  Returns device loss[2] (loss, loss_perf)."""
+        m = self.m
+        A = m.features(Yp, training=True)
+        A_det = A.detach().requires_grad_(True)
+        Y = m.fc_forward(A_det)
+        label = HDCEModel.rows_from_streams(HL)
+        perf = HDCEModel.rows_from_streams(HP)
+        self.nmse.sums(Y, label, perf)
+        loss = self.nmse.finalize()
+        dY = self.nmse.grad(Y, label, out_dtype=Y.dtype)
+        torch.autograd.backward(Y, dY)             # FC grads + dA
+        if self.grad_hook:
+            self.grad_hook("fc")
+        torch.autograd.backward(A, A_det.grad)     # conv/BN grads
+        if self.grad_hook:
+            self.grad_hook("conv")
+        m.count_batches(self.U)
+        return loss
+
+    @property
+    def skip(self) -> torch.Tensor:
+        return self.nmse.skip
+
+
+class ClassifierStep:
+    """One fused step of a scenario classifier (QSC_P128 or SC_P128) over all 9 streams.
+
+    The reference sums 9 per-stream ``nll_loss / 9`` (R:362); with equal stream batches that
+    is exactly the mean NLL over the concatenated 9*B samples, computed in one pass.
+    For QSC with QuantumNAT on, each stream gets its own noise draw (the reference draws
+    per forward call) through grouped quantum weights."""
+
+    def __init__(self, model: nn.Module, n_streams: int, grad_hook: Optional[Callable] = None):
+        self.model = model
+        self.S = n_streams
+        self.grad_hook = grad_hook
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        if isinstance(m, QSC_P128):
+            angles = m.preprocess(x)
+            w = m.qlayer.weights
+            if m.training and m.use_quantumnat and m.noise_level > 0:
+                noise = torch.randn((self.S,) + tuple(w.shape), device=w.device, dtype=w.dtype)
+                w = w.unsqueeze(0) + m.noise_level * noise
+            xq = m.qlayer(angles, w)
+            return F.log_softmax(m.classifier(xq), dim=1)
+        return m(x)
+
+    def __call__(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        out = self.forward(x)
+        loss = F.nll_loss(out, labels)
+        loss.backward()
+        if self.grad_hook:
+            self.grad_hook("all")
+        return loss.detach()

@@ -1,0 +1,420 @@
+"""``Y2HRunner``: the training orchestrator (reference: Runner_P128_QuantumNAT_onchipQNN.py).
+
+Public surface kept from the reference:
+  attributes  Pilot_num, data_len, SNRdb, num_workers, batch_size, batch_size_DML, lr,
+              lr_decay, lr_threshold, n_epochs, print_freq, optimizer, train_test_ratio,
+              train_QSC_losses, val_QSC_losses, val_QSC_accuracies          (R:20-38)
+  methods     get_optimizer (R:40-46), get_data (R:48-73), get_dataloader_DML (R:75-95),
+              get_HDCE_loss / get_HDCE_estimate (R:97-132),
+              train_Conv_Linear_of_HDCE (R:134-283), get_SE_loss / get_SE_estimate
+              (R:285-302), train_QSC_P128 (R:307-426)
+  new         train_SC_P128 (the classical-SC trainer Test.py expects but the reference
+              lacks), train_all, resume, DP over RCCL, HIP-graph captured steps.
+
+The training methods run the fused engines of train/engine.py on HBM-resident data;
+the host-side helpers (get_data, get_dataloader_DML, get_*_loss) remain for API
+compatibility and tests.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+import torch.optim as optim
+from torch.utils.data import DataLoader
+
+from ..config import RunnerConfig
+from ..data.channel import pack_channel, pack_pilots
+from ..data.datasets import (DatasetFolder_DML, DMLStore, load_or_generate_stream, make_dml_stores, split_stream)
+from ..models.estimators import NMSELoss, QSC_P128, SC_P128
+from ..ops.optim import FlatParamSpace, make_optimizer
+from ..parallel.dp import DeviceSampler, GradBuckets, init_distributed
+from ..utils.metrics import MetricsLogger, to_db
+from ..utils.profiling import GraphedStep
+from . import checkpoint as ck
+from .engine import ClassifierStep, HDCEModel, HDCEStep
+
+
+class Y2HRunner:
+    def __init__(self, cfg: Optional[RunnerConfig] = None, **overrides):
+        cfg = cfg or RunnerConfig()
+        if overrides:
+            cfg.update_from_dict(overrides)
+        self.cfg = cfg
+        for k, v in cfg.to_dict().items():
+            setattr(self, k, v)
+        self.train_QSC_losses: List[float] = []
+        self.val_QSC_losses: List[float] = []
+        self.val_QSC_accuracies: List[float] = []
+        self.train_SC_losses: List[float] = []
+        self.train_HDCE_losses: List[float] = []
+        self.val_HDCE_nmse: List[float] = []
+        self._stores: Optional[Tuple[DMLStore, DMLStore]] = None
+        self.ctx = None
+
+    # ------------------------------------------------------------------ config sync
+    def _sync_cfg(self) -> RunnerConfig:
+        """Attribute writes (runner.lr = ...) win over the dataclass, as in the reference."""
+        for k in self.cfg.to_dict():
+            setattr(self.cfg, k, getattr(self, k))
+        return self.cfg
+
+    def _context(self):
+        if self.ctx is None:
+            self.ctx = init_distributed(self.device)
+        return self.ctx
+
+    def _log(self) -> MetricsLogger:
+        ctx = self._context()
+        return MetricsLogger(self.log_jsonl, ctx.rank, ctx.world)
+
+    def _print(self, *a, **kw) -> None:
+        if self._context().is_main:
+            print(*a, **kw, flush=True)
+
+    # ------------------------------------------------------------------ reference helpers
+    def get_optimizer(self, parameters, lr):
+        if self.optimizer == "adam":
+            return optim.Adam(parameters, lr=lr)
+        elif self.optimizer == "sgd":
+            return optim.SGD(parameters, lr=lr, momentum=0.9)
+        raise NotImplementedError("Optimizer {} not understood.".format(self.optimizer))
+
+    def get_data(self, data_len, indicator, uid):
+        st = load_or_generate_stream(self.data_dir, indicator, uid, self.Pilot_num, self.SNRdb, data_len,
+                                     self.synthetic, self.seed)
+        print("data loaded for scenario" + str(indicator) + " user" + str(uid) + "!")
+        tr, va = split_stream([a.numpy() for a in st], self.train_test_ratio)
+        return tr, va
+
+    def get_dataloader_DML(self, data_len):
+        tds, vds = [], []
+        for s in range(self.n_scenarios):
+            for u in range(self.n_users):
+                td, vd = self.get_data(data_len, s, u)
+                tds.append(td)
+                vds.append(vd)
+        train_loader = DataLoader(DatasetFolder_DML(*tds), batch_size=self.batch_size_DML, shuffle=True,
+                                  num_workers=self.num_workers, pin_memory=torch.cuda.is_available())
+        val_loader = DataLoader(DatasetFolder_DML(*vds), batch_size=self.batch_size_DML, shuffle=True,
+                                num_workers=self.num_workers, pin_memory=torch.cuda.is_available())
+        return train_loader, val_loader
+
+    def _pack_td(self, td, device):
+        Yp = td[0] if torch.is_tensor(td[0]) else torch.as_tensor(td[0])
+        HL = td[1] if torch.is_tensor(td[1]) else torch.as_tensor(td[1])
+        HP = td[2] if torch.is_tensor(td[2]) else torch.as_tensor(td[2])
+        return (pack_pilots(Yp, self.Pilot_num).to(device), pack_channel(HL).to(device), pack_channel(HP).to(device))
+
+    def get_HDCE_loss(self, td, Conv, CE, criterion, device):
+        Yp_input, label_out, perfect_out = self._pack_td(td, device)
+        Hhat = CE(Conv(Yp_input))
+        return criterion(Hhat, label_out), criterion(Hhat, perfect_out)
+
+    def get_HDCE_estimate(self, vd, Conv, CE, device):
+        Yp_input, label_out, perfect_out = self._pack_td(vd, device)
+        return CE(Conv(Yp_input)), label_out, perfect_out
+
+    def get_SE_loss(self, td, CNN, device):
+        pred, label = self.get_SE_estimate(td, CNN, device)
+        return F.nll_loss(pred, label)
+
+    def get_SE_estimate(self, td, CNN, device):
+        Yp = td[0] if torch.is_tensor(td[0]) else torch.as_tensor(td[0])
+        label_out = torch.as_tensor(td[3]).long().to(device).reshape(-1)
+        return CNN(pack_pilots(Yp, self.Pilot_num).to(device)), label_out
+
+    # ------------------------------------------------------------------ device data
+    def device_stores(self) -> Tuple[DMLStore, DMLStore]:
+        """HBM-resident train/val stores (this rank's shard)."""
+        if self._stores is None:
+            ctx = self._context()
+            tr, va = make_dml_stores(self.data_len, self.Pilot_num, self.SNRdb, self.train_test_ratio, ctx.device,
+                                     self.data_dir, self.synthetic, self.seed, self.n_scenarios, self.n_users)
+            if ctx.world > 1:
+                tr = tr.shard(ctx.rank, ctx.world)
+                va = va.shard(ctx.rank, ctx.world)
+            self._stores = (tr, va)
+            self._print(f"Data Loaded! ({tr.n_streams} streams x {tr.n} train / {va.n} val samples per rank, "
+                        f"device={ctx.device})")
+        return self._stores
+
+    def _graphs_on(self) -> bool:
+        ctx = self._context()
+        return bool(self.hip_graphs) and ctx.device.type == "cuda" and ctx.world == 1
+
+    # ------------------------------------------------------------------ HDCE
+    def build_hdce(self) -> HDCEModel:
+        ctx = self._context()
+        model = HDCEModel(self.Pilot_num, ctx.device, self.dtype, self.n_scenarios)
+        ctx.broadcast_(model.space.flat)
+        return model
+
+    @torch.no_grad()
+    def eval_hdce(self, model: HDCEModel, store: DMLStore, batch: int = 1024) -> Tuple[float, float]:
+        """Global val NMSE vs label and vs perfect (R:216-235): sum err / sum pow over ALL streams."""
+        model.eval()
+        E, U = self.n_scenarios, self.n_users
+        acc = torch.zeros(4, device=store.Yp.device, dtype=torch.float64)
+        for s in range(0, store.n, batch):
+            idx = torch.arange(s, min(s + batch, store.n), device=store.Yp.device)
+            Yp, HL, HP = store.gather(idx)
+            b = idx.numel()
+            A = model.features(Yp.view(E, U, b, *Yp.shape[2:]), training=False)
+            Y = model.fc_forward(A).float()
+            lab = HDCEModel.rows_from_streams(HL.view(E, U, b, -1))
+            per = HDCEModel.rows_from_streams(HP.view(E, U, b, -1))
+            acc += torch.stack([((Y - lab) ** 2).sum(), (lab ** 2).sum(), ((Y - per) ** 2).sum(),
+                                (per ** 2).sum()]).double()
+        self._context().all_reduce_(acc)
+        model.train()
+        return float(acc[0] / acc[1]), float(acc[2] / acc[3])
+
+    def train_Conv_Linear_of_HDCE(self):
+        cfg = self._sync_cfg()
+        ctx = self._context()
+        tr, va = self.device_stores()
+        model = self.build_hdce()
+        opt = make_optimizer(model.space, self.optimizer, self.lr)
+        E, U, B = self.n_scenarios, self.n_users, self.batch_size_DML
+        sp = model.space
+        n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
+        buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "conv": [sp.grad[:n_conv]]})
+        step = HDCEStep(model, U, B, grad_hook=buckets.launch)
+        loss_acc = torch.zeros(2, device=ctx.device)
+        last_loss = torch.zeros(2, device=ctx.device)
+        static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
+        gscale = 1.0 / ctx.world
+
+        def run(idx):
+            sp.zero_grad()
+            Yp, HL, HP = tr.gather(idx)
+            b = idx.numel()
+            hs = step if b == B else HDCEStep(model, U, b, grad_hook=buckets.launch)
+            loss = hs(Yp.view(E, U, b, *Yp.shape[2:]), HL.view(E, U, b, -1), HP.view(E, U, b, -1))
+            last_loss.copy_(loss)
+            loss_acc.add_(loss)
+            buckets.wait()
+            opt.step(grad_scale=gscale, skip=hs.skip)
+
+        graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
+        sampler = DeviceSampler(tr.n, B, ctx.device, self.seed, ctx.rank)
+        d = ck.ckpt_dir(self.workspace, self.Pilot_num) if ctx.is_main else None
+        log = self._log()
+        best_nmse = 1000.0
+        self._print("Everything prepared well, start to train HDCE Conv+Linear...")
+        for epoch in range(self.n_epochs):
+            self._print(f"HDCE Conv+Linear:SNR: {self.SNRdb} Epoch [{epoch}]/[{self.n_epochs}] learning rate: "
+                        f"{opt.lr:.4e}", time.strftime("%Y-%m-%d %H:%M:%S", time.localtime()))
+            model.train()
+            sampler.set_epoch(epoch)
+            loss_acc.zero_()
+            t0 = time.perf_counter()
+            nb = 0
+            for it, idx in enumerate(sampler):
+                if idx.numel() == B:
+                    if graphed.enabled and graphed.graph is None:
+                        _capture_preserving(graphed, [sp.flat, opt.m, opt.v, opt.step_t] + model.run_mean
+                                            + model.run_var + [loss_acc], static_idx, idx)
+                    static_idx.copy_(idx)
+                    graphed()
+                else:
+                    run(idx)
+                nb += 1
+                if it % self.print_freq == 0:
+                    l = last_loss.tolist()
+                    self._print(f"Epoch: [{epoch}/{self.n_epochs}][{it}/{len(sampler)}]\t Loss {l[0]:.5f}\t "
+                                f"Loss_perf {l[1]:.5f}")
+            if ctx.device.type == "cuda":
+                torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            sps = nb * B * E * U * ctx.world / max(dt, 1e-9)
+            tl = (loss_acc / max(nb, 1)).tolist()
+            self.train_HDCE_losses.append(tl[0])
+            nmse, nmse_perf = self.eval_hdce(model, va)
+            self.val_HDCE_nmse.append(nmse)
+            if ctx.is_main:
+                if epoch == self.n_epochs - 1:
+                    ck.save_hdce(d, model.convs, model.fc, B, self.SNRdb, f"epoch{epoch}")
+                    print("HDCE finally saved!")
+                if nmse < best_nmse:
+                    ck.save_hdce(d, model.convs, model.fc, B, self.SNRdb, "best")
+                    print("HDCE saved!")
+            if nmse < best_nmse:
+                best_nmse = nmse
+            self._print(f"Epoch [{epoch}]/[{self.n_epochs}] || NMSE {nmse:.5f}, NMSE_perf {nmse_perf:.5f}, "
+                        f"best nmse: {best_nmse:.5f}")
+            self._print("==============================================================")
+            log.log(kind="hdce_epoch", epoch=epoch, loss=tl[0], loss_perf=tl[1], val_nmse=nmse,
+                    val_nmse_db=to_db(nmse), val_nmse_perf_db=to_db(nmse_perf), lr=opt.lr, samples_per_sec=sps)
+            if epoch > 0:
+                if epoch % self.lr_decay == 0:
+                    opt.set_lr(opt.lr * 0.5)
+                if opt.lr < self.lr_threshold:
+                    opt.set_lr(self.lr_threshold)
+            if ctx.is_main:
+                ck.save_resume(os.path.join(d, f"HDCE_{B}_{self.SNRdb}dB_resume.pth"), epoch=epoch,
+                               best=best_nmse, optimizer=opt.state_dict(), flat=sp.flat.cpu(),
+                               run_mean=[t.cpu() for t in model.run_mean], run_var=[t.cpu() for t in model.run_var],
+                               rng=ck.rng_state())
+        self.hdce_model = model
+        return model
+
+    # ------------------------------------------------------------------ classifiers
+    @torch.no_grad()
+    def eval_classifier(self, cstep: ClassifierStep, store: DMLStore, batch: int) -> Tuple[float, float]:
+        """(avg val loss, accuracy) with the reference's definitions (R:378-414)."""
+        model = cstep.model
+        model.eval()
+        S = store.n_streams
+        loss_sum = torch.zeros(3, device=store.Yp.device, dtype=torch.float64)  # loss sum, correct, total
+        nb = 0
+        for s in range(0, store.n, batch):
+            idx = torch.arange(s, min(s + batch, store.n), device=store.Yp.device)
+            b = idx.numel()
+            x = store.Yp.index_select(1, idx).reshape(S * b, *store.Yp.shape[2:])
+            labels = store.scen.repeat_interleave(b)
+            out = cstep.forward(x)
+            loss_sum[0] += F.nll_loss(out, labels).double()
+            loss_sum[1] += (out.argmax(1) == labels).sum().double()
+            loss_sum[2] += labels.numel()
+            nb += 1
+        ctx = self._context()
+        loss_sum[0] /= max(nb, 1)
+        ctx.all_reduce_(loss_sum)
+        loss_sum[0] /= ctx.world
+        model.train()
+        return float(loss_sum[0]), float(loss_sum[1] / loss_sum[2])
+
+    def _train_classifier(self, model, kind: str, opt_name: str, wd: float, prune_thr: float,
+                          on_epoch, histories: Tuple[List, List, List]):
+        ctx = self._context()
+        tr, va = self.device_stores()
+        model = model.to(ctx.device)
+        space = FlatParamSpace(list(model.named_parameters()), ctx.device)
+        ctx.broadcast_(space.flat)
+        kw = {"prune_thr": prune_thr}
+        if opt_name == "adamw":
+            kw["weight_decay"] = wd
+        opt = make_optimizer(space, opt_name, self.lr, **kw)
+        S, B = tr.n_streams, self.batch_size_DML
+        buckets = GradBuckets(ctx, {"all": [space.grad]})
+        cstep = ClassifierStep(model, S, grad_hook=buckets.launch)
+        loss_acc = torch.zeros(1, device=ctx.device)
+        static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
+        gscale = 1.0 / ctx.world
+
+        def run(idx):
+            space.zero_grad()
+            b = idx.numel()
+            x = tr.Yp.index_select(1, idx).reshape(S * b, *tr.Yp.shape[2:])
+            labels = tr.scen.repeat_interleave(b)
+            loss = cstep(x, labels)
+            loss_acc.add_(loss)
+            buckets.wait()
+            opt.step(grad_scale=gscale)
+
+        graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
+        sampler = DeviceSampler(tr.n, B, ctx.device, self.seed + 17, ctx.rank)
+        log = self._log()
+        train_losses, val_losses, val_accs = histories
+        train_losses.clear()
+        for epoch in range(self.n_epochs):
+            model.train()
+            sampler.set_epoch(epoch)
+            loss_acc.zero_()
+            opt.pruned.zero_()
+            nb = 0
+            t0 = time.perf_counter()
+            for idx in sampler:
+                if idx.numel() == B:
+                    if graphed.enabled and graphed.graph is None:
+                        _capture_preserving(graphed, [space.flat, opt.step_t, loss_acc]
+                                            + ([opt.m, opt.v] if opt.kind != "sgd" else [opt.buf]), static_idx, idx)
+                    static_idx.copy_(idx)
+                    graphed()
+                else:
+                    run(idx)
+                nb += 1
+            avg = float(loss_acc.item()) / max(nb, 1)
+            dt = time.perf_counter() - t0
+            train_losses.append(avg)
+            self._print(f"Epoch {epoch + 1}/{self.n_epochs}, Average Loss: {avg:.4f}")
+            if prune_thr > 0:
+                ratio = float(opt.pruned.item()) / max(nb * space.numel, 1)
+                if ratio > 0.1:
+                    self._print(f"Gradient pruning: {ratio:.1%} gradients pruned")
+            vl, acc = self.eval_classifier(cstep, va, B)
+            val_losses.append(vl)
+            val_accs.append(acc)
+            self._print(f"Validation Loss: {vl:.4f}, Validation Accuracy: {acc:.2%}")
+            log.log(kind=f"{kind}_epoch", epoch=epoch, loss=avg, val_loss=vl, val_acc=acc, lr=opt.lr,
+                    samples_per_sec=nb * B * S * ctx.world / max(dt, 1e-9))
+            on_epoch(epoch, acc, model)
+        return model
+
+    def train_QSC_P128(self):
+        self._sync_cfg()
+        model = QSC_P128(self.n_qubits, self.n_layers, self.n_classes, use_quantumnat=self.use_quantumnat,
+                         use_gradient_pruning=self.use_gradient_pruning, pilot_num=self.Pilot_num,
+                         backend=None if self.backend == "auto" else self.backend, noise_level=self.noise_level,
+                         gradient_threshold=self.gradient_threshold)
+        ctx = self._context()
+        d = ck.ckpt_dir(self.workspace, self.Pilot_num) if ctx.is_main else None
+        state = {"best": 0.0}
+        self._print("Data Loaded for QSC with QuantumNAT + On-chip QNN optimization!")
+
+        def on_epoch(epoch, acc, m):
+            if ctx.is_main and acc > state["best"]:
+                ck.save_qsc(d, m, self.batch_size_DML, self.SNRdb, "best", alias=True)
+                print("Optimized QML saved (best so far).")
+            if acc > state["best"]:
+                state["best"] = acc
+            if ctx.is_main and epoch == self.n_epochs - 1:
+                ck.save_qsc(d, m, self.batch_size_DML, self.SNRdb, f"epoch{epoch}")
+                print("Optimized QSC finally saved!")
+
+        prune = self.gradient_threshold if self.use_gradient_pruning else 0.0
+        self.qsc_model = self._train_classifier(model, "qsc", "adamw", self.qsc_weight_decay, prune, on_epoch,
+                                                (self.train_QSC_losses, self.val_QSC_losses, self.val_QSC_accuracies))
+        return self.qsc_model
+
+    def train_SC_P128(self):
+        """Classical scenario classifier trainer (Test.py:69-73 expects its checkpoint)."""
+        self._sync_cfg()
+        model = SC_P128(self.Pilot_num, self.n_classes)
+        ctx = self._context()
+        d = ck.ckpt_dir(self.workspace, self.Pilot_num) if ctx.is_main else None
+        self.val_SC_losses, self.val_SC_accuracies = [], []
+
+        def on_epoch(epoch, acc, m):
+            if ctx.is_main and epoch == self.n_epochs - 1:
+                ck.save_sc(d, m, self.batch_size_DML, self.SNRdb, f"epoch{epoch}")
+                print("SC finally saved!")
+
+        self.sc_model = self._train_classifier(model, "sc", self.optimizer, 0.0, 0.0, on_epoch,
+                                               (self.train_SC_losses, self.val_SC_losses, self.val_SC_accuracies))
+        return self.sc_model
+
+    def train_all(self):
+        """HDCE estimator + classical SC + quantum SC: everything model_val needs."""
+        self.train_Conv_Linear_of_HDCE()
+        self.train_SC_P128()
+        self.train_QSC_P128()
+
+
+def _capture_preserving(graphed: GraphedStep, state: List[torch.Tensor], static_idx: torch.Tensor,
+                        idx: torch.Tensor) -> None:
+    """Capture the step graph without letting the warm-up iterations change training state:
+    snapshot every stateful tensor, warm up + capture, restore."""
+    snap = [t.clone() for t in state]
+    static_idx.copy_(idx)
+    graphed.capture()
+    with torch.no_grad():
+        for t, s in zip(state, snap):
+            t.copy_(s)

@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU-box validation: build, smoke, pytest -m gpu, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a timeout/abort/segfault (rc >= 124) ends the script.
+set -u
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$ROOT"
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+STEPS=${STEPS:-"build smoke pytest bench prof"}
+run() {
+  local name=$1; shift
+  local t0=$(date +%s)
+  timeout -k 10 "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc $(( $(date +%s) - t0 ))s" | tee -a "$OUT/summary.txt"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ge 124 ]; then echo "fatal rc=$rc in $name; stopping"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    build) run build 600 python __graft_entry__.py build ;;
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    pytest) run pytest 900 python -m pytest tests -m gpu -x -q ;;
+    bench) run bench 600 python bench.py --steps ${BENCH_STEPS:-50} --warmup 10 ;;
+    bench_eager) run bench_eager 600 python bench.py --steps 20 --warmup 5 --no-graphs ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 20 --warmup 5) ;;
+  esac
+done

@@ -1,0 +1,22 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP kernels); run with -m gpu")
+    config.addinivalue_line("markers", "slow: longer CPU tests")
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    nat.hip_lib()  # must load: GPU tests never fall back silently
+    return torch.device("cuda", 0)

@@ -1,0 +1,142 @@
+"""HIP kernel numerics on a real MI355X vs fp32/fp64 CPU references of the same op."""
+import math
+
+import pytest
+import torch
+
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.nmse import StreamNMSE
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.optim import FlatParamSpace, FusedOptimizer
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.quantum import qsim
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("L", [1, 3])
+def test_qsim_hip_matches_cpp(cuda, n, L):
+    g = torch.Generator().manual_seed(100 * n + L)
+    B = 37 if n < 9 else 13  # not a multiple of samples-per-wave
+    x = torch.rand(B, n, generator=g) * 2 - 1
+    w = torch.rand(L, n, 2, generator=g) * 2 * math.pi
+    gE = torch.randn(B, n, generator=g)
+    xc, wc = x.clone().requires_grad_(), w.clone().requires_grad_()
+    Ec = qsim(xc, wc, "cpu")
+    (Ec * gE).sum().backward()
+    xg, wg = x.to(cuda).requires_grad_(), w.to(cuda).requires_grad_()
+    Eg = qsim(xg, wg, "hip")
+    (Eg * gE.to(cuda)).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(Eg.cpu(), Ec, atol=2e-5), (Eg.cpu() - Ec).abs().max()
+    assert torch.allclose(xg.grad.cpu(), xc.grad, atol=5e-5), (xg.grad.cpu() - xc.grad).abs().max()
+    assert torch.allclose(wg.grad.cpu(), wc.grad, atol=5e-4 * max(1, B / 16)), (wg.grad.cpu() - wc.grad).abs().max()
+
+
+def test_qsim_hip_large_batch_and_groups(cuda):
+    n, L, G, b = 8, 3, 9, 256
+    torch.manual_seed(0)
+    x = (torch.rand(G * b, n) * 2 - 1)
+    w = torch.rand(G, L, n, 2) * 6.28
+    Eg = qsim(x.to(cuda), w.to(cuda), "hip").cpu()
+    Ec = torch.cat([qsim(x[i * b:(i + 1) * b], w[i], "cpu") for i in range(G)])
+    assert torch.allclose(Eg, Ec, atol=2e-5)
+    # grouped gradient: master weights receive the sum over groups
+    m = torch.rand(L, n, 2).to(cuda).requires_grad_()
+    noise = torch.randn(G, L, n, 2, device=cuda) * 0.01
+    xs = x.to(cuda).requires_grad_()
+    qsim(xs, m.unsqueeze(0) + noise, "hip").sum().backward()
+    mc = m.detach().cpu().requires_grad_()
+    xc = x.clone().requires_grad_()
+    qsim(xc, mc.unsqueeze(0) + noise.cpu(), "cpu").sum().backward()
+    assert torch.allclose(m.grad.cpu(), mc.grad, rtol=1e-3, atol=1e-2)
+    assert torch.allclose(xs.grad.cpu(), xc.grad, atol=5e-5)
+
+
+def test_qsim_hip_graph_capture(cuda):
+    n, L, B = 8, 3, 512
+    x = (torch.rand(B, n, device=cuda) * 2 - 1).requires_grad_()
+    w = torch.rand(L, n, 2, device=cuda).requires_grad_()
+    out = torch.zeros(1, device=cuda)
+
+    def body():
+        x.grad = None
+        w.grad = None
+        E = qsim(x, w, "hip")
+        E.sum().backward()
+        out.copy_(E.sum())
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        body()
+    torch.cuda.current_stream().wait_stream(s)
+    ref = out.clone()
+    gph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gph):
+        body()
+    gph.replay()
+    torch.cuda.synchronize()
+    assert torch.allclose(out, ref)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_stream_nmse_hip_vs_cpu(cuda, dt):
+    torch.manual_seed(1)
+    S, b, C = 9, 40, 2048
+    rs = torch.arange(S).repeat_interleave(b)[torch.randperm(S * b)]
+    Y = torch.randn(S * b, C).to(dt).float()
+    Lb = torch.randn(S * b, C)
+    Pf = torch.randn(S * b, C)
+    cpu = StreamNMSE(rs, S)
+    lc, gc = cpu(Y, Lb, Pf)
+    gpu = StreamNMSE(rs.to(cuda), S)
+    lg, gg = gpu(Y.to(cuda).to(dt), Lb.to(cuda), Pf.to(cuda), out_dtype=torch.float32)
+    assert torch.allclose(lg.cpu(), lc, rtol=1e-5)
+    assert torch.allclose(gg.cpu(), gc, rtol=1e-4, atol=1e-9)
+    # reference definition: mean over streams of per-stream global ratios
+    ref = sum(((Y[rs == s] - Lb[rs == s]) ** 2).sum() / (Lb[rs == s] ** 2).sum() for s in range(S)) / S
+    assert torch.allclose(lg[0].cpu(), ref, rtol=1e-5)
+    assert int(gpu.skip.item()) == 0
+
+
+@pytest.mark.parametrize("kind", ["adam", "adamw", "sgd"])
+def test_fused_optimizer_hip_vs_torch(cuda, kind):
+    torch.manual_seed(2)
+    shapes = [(33, 7), (5,), (64, 3, 3, 3)]
+    ref_params = [torch.nn.Parameter(torch.randn(s, device=cuda)) for s in shapes]
+    our_params = [torch.nn.Parameter(p.detach().clone()) for p in ref_params]
+    space = FlatParamSpace([(f"p{i}", p) for i, p in enumerate(our_params)], cuda)
+    if kind == "adam":
+        ref = torch.optim.Adam(ref_params, lr=1e-2)
+        opt = FusedOptimizer(space, "adam", lr=1e-2)
+    elif kind == "adamw":
+        ref = torch.optim.AdamW(ref_params, lr=1e-2, weight_decay=0.01)
+        opt = FusedOptimizer(space, "adamw", lr=1e-2, weight_decay=0.01)
+    else:
+        ref = torch.optim.SGD(ref_params, lr=1e-2, momentum=0.9)
+        opt = FusedOptimizer(space, "sgd", lr=1e-2, momentum=0.9)
+    for it in range(5):
+        grads = [torch.randn(s, device=cuda) for s in shapes]
+        for p, g in zip(ref_params, grads):
+            p.grad = g.clone()
+        for p, g in zip(our_params, grads):
+            p.grad.copy_(g)
+        ref.step()
+        opt.step()
+    for a, b in zip(ref_params, our_params):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
+
+
+def test_fused_optimizer_skip_and_prune(cuda):
+    p = torch.nn.Parameter(torch.ones(100, device=cuda))
+    space = FlatParamSpace([("p", p)], cuda)
+    opt = FusedOptimizer(space, "adamw", lr=0.1, weight_decay=0.01, prune_thr=0.5)
+    p.grad.copy_(torch.linspace(-1, 1, 100, device=cuda))
+    skip = torch.ones(1, dtype=torch.int32, device=cuda)
+    opt.step(skip=skip)
+    assert torch.equal(p.detach(), torch.ones(100, device=cuda)) and opt.step_t.item() == 0
+    skip.zero_()
+    opt.step(skip=skip)
+    small = torch.linspace(-1, 1, 100).abs() <= 0.5
+    assert int(opt.pruned.item()) == int(small.sum())
+    moved = (p.detach().cpu() - (1 - 0.1 * 0.01)).abs() > 1e-6
+    assert torch.equal(moved, ~small)
