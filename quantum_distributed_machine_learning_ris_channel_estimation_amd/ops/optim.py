@@ -45,6 +45,7 @@ class FlatParamSpace:
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.offsets = offs
         self.numel = off
+        self.n_real = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(off, device=device, dtype=torch.float32)
         self.grad = torch.zeros(off, device=device, dtype=torch.float32)
         for p, o in zip(self.params, offs):
@@ -167,6 +168,13 @@ class FusedOptimizer:
 
     def zero_grad(self) -> None:
         self.space.zero_grad()
+
+    def pruned_count(self, steps: int) -> int:
+        """Pruned gradient elements over ``steps`` steps (alignment padding excluded; syncs)."""
+        return int(self.pruned.item()) - (self.space.numel - self.space.n_real) * steps
+
+    def pruning_ratio(self, steps: int) -> float:
+        return self.pruned_count(steps) / max(1, self.space.n_real * steps)
 
     # ---------------------------------------------------------------- state
     def state_dict(self) -> Dict:

@@ -179,23 +179,30 @@ class HDCEModel:
     # ------------------------------------------------------------------ expert routing (eval)
     @torch.no_grad()
     def estimate_routed(self, x: torch.Tensor, expert: torch.Tensor) -> torch.Tensor:
-        """Test-time hierarchical routing (Test.py:166-214): sample i -> Conv_{expert[i]} -> CE.
+        return estimate_routed(self.convs, self.fc, x, expert)
 
-        Samples are bucketed by expert with one sort (no per-sample Python loop); outputs
-        come back in input order."""
-        order = torch.argsort(expert, stable=True)
-        counts = torch.bincount(expert, minlength=self.E).tolist()
-        xs = x[order]
-        out = torch.empty(x.shape[0], self.fc.FC.out_features, device=x.device, dtype=torch.float32)
-        start = 0
-        for e, c in enumerate(counts):
-            if c == 0:
-                continue
-            seg = xs[start:start + c]
-            h = self.convs[e].eval()(seg.float())
-            out[order[start:start + c]] = self.fc.eval()(h).float()
-            start += c
-        return out
+
+@torch.no_grad()
+def estimate_routed(convs: Sequence[nn.Module], fc: nn.Module, x: torch.Tensor, expert: torch.Tensor,
+                    chunk: int = 4096) -> torch.Tensor:
+    """Test-time hierarchical routing (Test.py:166-214): sample i -> Conv_{expert[i]} -> shared CE.
+
+    MoE-style top-1 routing: samples are bucketed by expert with ONE stable sort (the
+    reference loops over samples in Python), each bucket runs through its expert, and the
+    outputs are scattered back to input order."""
+    E = len(convs)
+    order = torch.argsort(expert, stable=True)
+    counts = torch.bincount(expert, minlength=E).tolist()
+    xs = x[order]
+    out = torch.empty(x.shape[0], fc.FC.out_features, device=x.device, dtype=torch.float32)
+    start = 0
+    for e, c in enumerate(counts):
+        for s in range(start, start + c, chunk):
+            t = min(s + chunk, start + c)
+            h = convs[e](xs[s:t].float())
+            out[order[s:t]] = fc(h).float()
+        start += c
+    return out
 
 
 class HDCEStep:

@@ -346,7 +346,7 @@ class Y2HRunner:
             train_losses.append(avg)
             self._print(f"Epoch {epoch + 1}/{self.n_epochs}, Average Loss: {avg:.4f}")
             if prune_thr > 0:
-                ratio = float(opt.pruned.item()) / max(nb * space.numel, 1)
+                ratio = opt.pruning_ratio(nb)
                 if ratio > 0.1:
                     self._print(f"Gradient pruning: {ratio:.1%} gradients pruned")
             vl, acc = self.eval_classifier(cstep, va, B)

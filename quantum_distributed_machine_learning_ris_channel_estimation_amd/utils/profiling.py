@@ -2,7 +2,7 @@
 
 Reference: wall-clock only -- ``time.time()`` around QSC training (R:437-440) and a
 timestamp per HDCE epoch (R:173).  Here:
-  * ``range(name)``   -- roctx range (visible in ``rocprofv3 --marker-trace``) when
+  * ``trace_range(name)`` -- roctx range (visible in ``rocprofv3 --marker-trace``) when
                          libroctx64 is loadable, otherwise a no-op;
   * ``EventTimer``    -- HIP-event phase timing without host syncs inside the step;
   * ``GraphedStep``   -- captures a whole training step (gather, forward, backward,
@@ -38,7 +38,7 @@ def _load_roctx():
 
 
 @contextlib.contextmanager
-def range(name: str):
+def trace_range(name: str):
     lib = _load_roctx() if os.environ.get("QDML_ROCTX", "1") == "1" else False
     if lib:
         lib.roctxRangePushA(name.encode())
