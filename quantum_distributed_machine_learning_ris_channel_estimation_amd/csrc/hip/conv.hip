@@ -1,0 +1,693 @@
+// HDCE feature extractor (3 x [conv3x3 -> BatchNorm -> ReLU], 32 channels) for gfx950.
+//
+// Reference: Conv_P128 (Estimators_QuantumNAT_onchipQNN.py:237-268), applied per
+// (scenario, user) stream with the scenario's own expert (Runner:109, R:194); PyTorch runs it
+// through cuDNN conv + BN + ReLU kernels, and the grouped-expert form through MIOpen, whose
+// grouped backward-weight kernel measured 4.7 ms per call on MI355X
+// (profiles/r1_00_baseline_miopen_kernel_stats.md).
+//
+// Data: activations are (N, E*32, H, W) with N = users x batch samples and the E scenario
+// experts folded into the channel axis; a "virtual sample" (n, e) is one sample through one
+// expert.  BatchNorm statistics are per (group u = n / B, channel) -- ghost BN over each
+// 256-sample stream batch, exactly what the reference's per-stream calls compute.
+//
+// Kernels (all MFMA bf16 32x32x16, fp32 accumulate):
+//   conv3x3_kernel   implicit-GEMM conv: M = 32 positions, N = 32 channels, K = 9*CIN ordered
+//                    (tap, channel) so an A fragment is ONE ds_read_b128 from a channel-last
+//                    LDS tile (pixel stride padded to 80 B: conflict-free).  Weights stay in
+//                    VGPRs as B fragments for the whole launch.  Input transforms fused in the
+//                    LDS staging: raw f32 pilots (layer 1), BN+ReLU of the previous layer's
+//                    pre-BN output (forward), or the BN/ReLU backward (dz from dh and z) for the
+//                    data-gradient pass (same kernel with flipped/transposed weights).
+//                    Epilogue: bf16 z + per-(group, channel) sum / sum-of-squares partials, or
+//                    fp32 dgrad output.
+//   conv3x3_wgrad    dW = sum_{samples,positions} im2col(x)^T dz: the 4 waves of a workgroup
+//                    split each sample's positions (K), keep all 9 tap tiles of accumulators
+//                    in registers across samples, and reduce through LDS once per workgroup
+//                    into a deterministic slab (no float atomics).  A operand rows come from 3
+//                    column-shifted copies of the input tile so every read is an aligned
+//                    ds_read_b128.
+//   bn_*             statistics finalisation (+ running-stat momentum updates in stream order),
+//                    backward reductions, and the final BN+ReLU apply that feeds the FC GEMM.
+#include "common.h"
+
+namespace qd {
+namespace conv {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int CO = 32;     // output channels of every layer (per expert)
+constexpr int NST = 8;     // floats per (group, channel) BN state record
+
+// BN state record per (u, channel): {mean, invstd, a=gamma*invstd, b=beta-mean*a, c1, c2, c3, 0}
+enum { ST_MEAN = 0, ST_INV = 1, ST_A = 2, ST_B = 3, ST_C1 = 4, ST_C2 = 5, ST_C3 = 6 };
+
+enum InMode { IN_RAW_F32 = 0, IN_BNRELU = 1, IN_BNBWD = 2 };
+enum OutMode { OUT_Z_STATS = 0, OUT_F32 = 1 };
+
+template <int H, int W>
+struct Geo {
+  static constexpr int HW = H * W;
+  static constexpr int HP = H + 2;
+  static constexpr int WP = W + 2;
+  static constexpr int MT = HW / 32;  // 32-position M tiles
+  static_assert(HW % 64 == 0 && W % 8 == 0, "geometry");
+};
+
+__device__ __forceinline__ float bf(uint16_t h) { return bf16_to_f32(h); }
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, size_t i);
+template <>
+__device__ __forceinline__ float ldf<float>(const float* p, size_t i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ldf<uint16_t>(const uint16_t* p, size_t i) { return bf16_to_f32(p[i]); }
+
+// 8 consecutive values (16- or 32-byte aligned) -> floats
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void load8(const uint16_t* p, float* v) {
+  const uint4 a = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// conv3x3_kernel: forward (and data-gradient) implicit GEMM
+// grid: (U * chunks, E); block 256 (4 waves); each wave owns `spw` consecutive samples.
+// CIN: input channels of THIS pass (layer-1 fwd: 2; else 32).
+// DGRAD: weights used transposed + flipped (W[e*32+k][lane][8-tap]); output fp32.
+// wt: B fragments pre-packed by pack_weights_kernel (fwd or dgrad order).
+// ------------------------------------------------------------------------------------------
+template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN>
+__global__ void __launch_bounds__(256) conv3x3_kernel(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
+                                                      const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
+                                                      void* __restrict__ out, float* __restrict__ stats, int E, int B,
+                                                      int chunks, int spw) {
+  using G = Geo<H, W>;
+  constexpr int CINP = (CIN % 16 == 0) ? CIN + 8 : CIN;  // channel-last pixel stride (bf16)
+  constexpr int KS = (9 * CIN + 15) / 16;                   // 16-deep k steps
+  constexpr int TILE = G::HP * G::WP * CINP;                // bf16 elements per wave tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
+  const int EC_in = E * CIN;
+  __bf16* tile = reinterpret_cast<__bf16*>(smem) + wv * TILE;
+  for (int i = lane; i < TILE; i += 64) tile[i] = (__bf16)0.f;
+
+  // ---- weights -> B fragments (registers): pre-packed [e][s][lane][8] bf16 (pack_weights_kernel) ----
+  bf16x8 bfrag[KS];
+  const bf16x8* wp = reinterpret_cast<const bf16x8*>(wt) + (size_t)e * KS * 64 + lane;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) bfrag[s] = wp[s * 64];
+
+  // per-lane channel for the output/statistics: column of the MFMA tile
+  float s1 = 0.f, s2 = 0.f;
+  const int n0 = u * B + (chunk * 4 + wv) * spw;
+  const int nend = min((u + 1) * B, n0 + spw);
+  const float* st_u = st_in ? st_in + (size_t)u * EC_in * NST : nullptr;
+
+  for (int n = n0; n < nend; ++n) {
+    wave_lds_fence();
+    // ---- stage the (transformed) input tile into LDS, channel-last, with zero halo ----
+    const size_t base = ((size_t)n * E + e) * CIN * G::HW;
+    if constexpr (INM == IN_RAW_F32) {
+      for (int i = lane; i < CIN * G::HW; i += 64) {
+        const int c = i / G::HW, p = i % G::HW;
+        const float v = ldf<TIN>(xin, base + i);
+        tile[((p / W + 1) * G::WP + (p % W) + 1) * CINP + c] = (__bf16)v;
+      }
+    } else {
+      constexpr int CH8 = CIN * G::HW / 8;
+      for (int i = lane; i < CH8; i += 64) {
+        const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
+        float v[8];
+        load8(xin + base + (size_t)c * G::HW + p0, v);
+        const float* sc = st_u + (size_t)(e * CIN + c) * NST;
+        if constexpr (INM == IN_BNRELU) {
+          const float a = sc[ST_A], b = sc[ST_B];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaxf(a * v[j] + b, 0.f);
+        } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
+          float z[8];
+          load8(zaux + base + (size_t)c * G::HW + p0, z);
+          const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+          const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float g = (a * z[j] + b > 0.f) ? v[j] : 0.f;
+            v[j] = c1 * g - c2 - c3 * (z[j] - mu) * inv;
+          }
+        }
+        const int ph = p0 / W, pw = p0 % W;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tile[((ph + 1) * G::WP + pw + j + 1) * CINP + c] = (__bf16)v[j];
+      }
+    }
+    wave_lds_fence();
+    // ---- MFMA over the M tiles ----
+#pragma unroll
+    for (int mt = 0; mt < G::MT; ++mt) {
+      const int p = mt * 32 + l32, ph = p / W, pw = p % W;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        bf16x8 a;
+        if constexpr (CIN % 16 == 0) {
+          const int tap = (16 * s) / CIN, c0 = (16 * s) % CIN + 8 * hh;
+          const int kh = tap / 3, kw = tap % 3;
+          a = *reinterpret_cast<const bf16x8*>(tile + ((ph + kh) * G::WP + pw + kw) * CINP + c0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = 16 * s + 8 * hh + j;
+            if (k < 9 * CIN) {
+              const int tap = k / CIN, c = k % CIN;
+              a[j] = tile[((ph + tap / 3) * G::WP + pw + tap % 3) * CINP + c];
+            } else {
+              a[j] = (__bf16)0.f;
+            }
+          }
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfrag[s], acc, 0, 0, 0);
+      }
+      // ---- epilogue: lane holds channel l32, positions mt*32 + 8g + 4hh + {0..3} ----
+      const size_t obase = ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + mt * 32 + 4 * hh;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v0 = acc[4 * g], v1 = acc[4 * g + 1], v2 = acc[4 * g + 2], v3 = acc[4 * g + 3];
+        if constexpr (OUTM == OUT_Z_STATS) {
+          const uint16_t h0 = f32_to_bf16(v0), h1 = f32_to_bf16(v1), h2 = f32_to_bf16(v2), h3 = f32_to_bf16(v3);
+          uint2 pk = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + obase + 8 * g) = pk;
+          v0 = bf(h0); v1 = bf(h1); v2 = bf(h2); v3 = bf(h3);
+          s1 += v0 + v1 + v2 + v3;
+          s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+        } else {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + obase + 8 * g) = make_float4(v0, v1, v2, v3);
+        }
+      }
+    }
+  }
+  if constexpr (OUTM == OUT_Z_STATS) {
+    // combine the two half-waves (same channel), then the 4 waves through LDS
+    s1 += __shfl_xor(s1, 32);
+    s2 += __shfl_xor(s2, 32);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    if (hh == 0) {
+      red[(wv * 32 + l32) * 2] = s1;
+      red[(wv * 32 + l32) * 2 + 1] = s2;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int c = tid >> 1, k = tid & 1;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
+      stats[(((size_t)u * chunks + chunk) * E * CO + e * CO + c) * 2 + k] = t;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// pack_weights_kernel: fp32 W (E*32, CIN, 3, 3) -> bf16 B fragments [e][s][lane][8] in the
+// exact register order conv3x3_kernel consumes (16-byte coalesced loads per lane).
+// dgrad = 1: transposed + spatially flipped (the data-gradient correlation).
+// ------------------------------------------------------------------------------------------
+__global__ void pack_weights_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, int E, int CIN, int KS,
+                                    int dgrad) {
+  const int lane = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
+  const int hh = lane >> 5, col = lane & 31;
+  uint16_t v8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * s + 8 * hh + j;
+    float v = 0.f;
+    if (!dgrad) {
+      if (k < 9 * CIN) v = w[((size_t)(e * CO + col) * CIN + k % CIN) * 9 + k / CIN];
+    } else {
+      if (k < 9 * CO) v = w[((size_t)(e * CO + k % CO) * CO + col) * 9 + (8 - k / CO)];
+    }
+    v8[j] = f32_to_bf16(v);
+  }
+  uint4 pk = make_uint4(v8[0] | ((uint32_t)v8[1] << 16), v8[2] | ((uint32_t)v8[3] << 16),
+                        v8[4] | ((uint32_t)v8[5] << 16), v8[6] | ((uint32_t)v8[7] << 16));
+  *reinterpret_cast<uint4*>(out + (((size_t)e * KS + s) * 64 + lane) * 8) = pk;
+}
+
+// ------------------------------------------------------------------------------------------
+// conv3x3_wgrad: dW[e][co][ci][tap] partials.  grid (U*chunks, E), block 256, `spb` samples
+// per workgroup; slab[(e * U*chunks + blockIdx.x)][co][ci][tap].
+// x = layer input (raw f32 pilots, or BN+ReLU of the previous z); dz from (dh, z, st).
+// ------------------------------------------------------------------------------------------
+template <int CIN, int H, int W, int INM, typename TIN, typename TDH>
+__global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restrict__ xin,
+                                                            const float* __restrict__ st_prev,
+                                                            const TDH* __restrict__ dh,
+                                                            const uint16_t* __restrict__ z,
+                                                            const float* __restrict__ st, float* __restrict__ slab,
+                                                            int E, int B, int chunks, int spb) {
+  using G = Geo<H, W>;
+  constexpr int MTW = (9 * CIN + 31) / 32;        // accumulator tiles (9 for CIN=32, 1 for CIN=2)
+  constexpr int XCS = G::HP * W + 8;              // channel stride of the shifted copies (bf16)
+  constexpr int DZS = G::HW + 8;                  // channel stride of the dz tile (bf16)
+  constexpr int KSW = G::HW / 16 / 4;             // k-steps per wave per sample (positions split 4 ways)
+  constexpr int XELEMS = 3 * CIN * XCS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __bf16* X = reinterpret_cast<__bf16*>(smem);
+  __bf16* DZ = X + XELEMS;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
+  for (int i = tid; i < XELEMS; i += 256) X[i] = (__bf16)0.f;
+
+  f32x16 acc[MTW];
+#pragma unroll
+  for (int t = 0; t < MTW; ++t) acc[t] = f32x16{};
+  // per-lane A-row mapping (m = l32 within tile t): (tap, ci)
+  const float* stp_u = st_prev ? st_prev + (size_t)u * E * CIN * NST : nullptr;
+  const float* st_u = st + (size_t)u * E * CO * NST;
+  const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
+
+  for (int n = n0; n < nend; ++n) {
+    __syncthreads();
+    // ---- stage x into 3 column-shifted copies: X[kw][ci][row 0..HP-1][w] = x[ci][row-1][w+kw-1] ----
+    // one thread per (channel, image row): W contiguous values -> 3 aligned 16-byte row writes
+    const size_t xb = ((size_t)n * E + e) * CIN * G::HW;
+    for (int i = tid; i < CIN * H; i += 256) {
+      const int c = i / H, ph = i % H;
+      float a = 1.f, b = 0.f;
+      if constexpr (INM == IN_BNRELU) {
+        const float* sc = stp_u + (size_t)(e * CIN + c) * NST;
+        a = sc[ST_A];
+        b = sc[ST_B];
+      }
+      float v[W + 2];
+      v[0] = 0.f;
+      v[W + 1] = 0.f;
+#pragma unroll
+      for (int q = 0; q < W; q += 8) load8(xin + xb + (size_t)c * G::HW + ph * W + q, v + 1 + q);
+      if constexpr (INM == IN_BNRELU) {
+#pragma unroll
+        for (int q = 1; q <= W; ++q) v[q] = fmaxf(a * v[q] + b, 0.f);
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        __bf16* dst = X + (kw * CIN + c) * XCS + (ph + 1) * W;
+#pragma unroll
+        for (int q = 0; q < W; q += 8) {
+          bf16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[q + j + kw];  // column w holds x[w + kw - 1]
+          *reinterpret_cast<bf16x8*>(dst + q) = o;
+        }
+      }
+    }
+    // ---- stage dz (bf16) [co][p] ----
+    const size_t zb = ((size_t)n * E + e) * CO * G::HW;
+    for (int i = tid; i < CO * G::HW / 8; i += 256) {
+      const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
+      float d[8], zz[8];
+      load8(dh + zb + (size_t)c * G::HW + p0, d);
+      load8(z + zb + (size_t)c * G::HW + p0, zz);
+      const float* sc = st_u + (size_t)(e * CO + c) * NST;
+      const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+      const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = (a * zz[j] + b > 0.f) ? d[j] : 0.f;
+        o[j] = (__bf16)(c1 * g - c2 - c3 * (zz[j] - mu) * inv);
+      }
+      *reinterpret_cast<bf16x8*>(DZ + c * DZS + p0) = o;
+    }
+    __syncthreads();
+    // ---- MFMA: this wave's positions p in [wv*HW/4, (wv+1)*HW/4) ----
+#pragma unroll
+    for (int ks = 0; ks < KSW; ++ks) {
+      const int p0 = (wv * KSW + ks) * 16 + 8 * hh;   // 8 consecutive positions (aligned, one row)
+      const int ph = p0 / W, pw0 = p0 % W;
+      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(DZ + l32 * DZS + p0);
+#pragma unroll
+      for (int t = 0; t < MTW; ++t) {
+        const int m = t * 32 + l32;
+        bf16x8 a;
+        if (m < 9 * CIN) {
+          const int tap = m / CIN, c = m % CIN, kh = tap / 3, kw = tap % 3;
+          a = *reinterpret_cast<const bf16x8*>(X + (kw * CIN + c) * XCS + (ph + kh) * W + pw0);
+        } else {
+          a = bf16x8{};
+        }
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr, acc[t], 0, 0, 0);
+      }
+    }
+  }
+  // ---- reduce the 4 waves' accumulators through LDS, write one slab row ----
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // MTW*32*32 floats
+  for (int w = 0; w < 4; ++w) {
+    if (wv == w) {
+#pragma unroll
+      for (int t = 0; t < MTW; ++t) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          float* q = red + (t * 32 + row) * 32 + l32;
+          *q = (w == 0 ? 0.f : *q) + acc[t][r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* srow = slab + ((size_t)e * gridDim.x + blockIdx.x) * CO * CIN * 9;
+  for (int i = tid; i < CO * CIN * 9; i += 256) {
+    const int co = i / (CIN * 9), rem = i % (CIN * 9), c = rem / 9, tap = rem % 9;
+    const int m = tap * CIN + c;
+    srow[i] = red[m * 32 + co];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm pieces
+// ------------------------------------------------------------------------------------------
+// Forward statistics: per (u, ch) mean/invstd/(a,b); running stats updated in u order.
+// One 64-lane block per channel: lanes sum the chunk partials, lane 0 finishes.
+__global__ void __launch_bounds__(64) bn_stats_finalize_kernel(const float* __restrict__ stats,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ beta, float* __restrict__ run_mean,
+                                                               float* __restrict__ run_var, float* __restrict__ st, int U,
+                                                               int chunks, int EC, float count, float momentum, float eps,
+                                                               int training) {
+  const int ch = blockIdx.x, lane = threadIdx.x;
+  const float g = gamma[ch], bt = beta[ch];
+  float rm = run_mean[ch], rv = run_var[ch];
+  for (int u = 0; u < U; ++u) {
+    float mean, var;
+    if (training) {
+      float a = 0.f, b = 0.f;
+      for (int k = lane; k < chunks; k += 64) {
+        a += stats[(((size_t)u * chunks + k) * EC + ch) * 2];
+        b += stats[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
+      }
+      a = wave_sum(a);
+      b = wave_sum(b);
+      mean = a / count;
+      var = fmaxf(b / count - mean * mean, 0.f);
+      rm = (1.f - momentum) * rm + momentum * mean;
+      rv = (1.f - momentum) * rv + momentum * var * count / (count - 1.f);
+    } else {
+      mean = rm;
+      var = rv;
+    }
+    if (lane == 0) {
+      const float inv = rsqrtf(var + eps);
+      float* r = st + ((size_t)u * EC + ch) * NST;
+      r[ST_MEAN] = mean;
+      r[ST_INV] = inv;
+      r[ST_A] = g * inv;
+      r[ST_B] = bt - mean * g * inv;
+    }
+  }
+  if (training && lane == 0) {
+    run_mean[ch] = rm;
+    run_var[ch] = rv;
+  }
+}
+
+// Backward reductions: per (u, chunk, ch): sum g, sum g*xhat.  grid (U*chunks, E), block 256.
+// 16-lane groups each own one (sample, channel) row of HW values (8 per lane per pass); a
+// group's rows alternate between channels g and g+16, so every lane keeps 2 x 2 partials.
+template <int HW, typename TDH>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restrict__ dh, const uint16_t* __restrict__ z,
+                                                            const float* __restrict__ st, float* __restrict__ slab,
+                                                            int E, int B, int chunks, int spb) {
+  const int tid = threadIdx.x, grp = tid >> 4, gl = tid & 15;
+  const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
+  const int EC = E * CO;
+  const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
+  const int rows = (nend - n0) * CO;
+  float sg0 = 0.f, sgx0 = 0.f, sg1 = 0.f, sgx1 = 0.f;  // channels grp and grp+16
+  for (int it = 0; it * 16 < rows; ++it) {
+    const int r = it * 16 + grp;
+    if (r >= rows) break;
+    const int n = n0 + r / CO, c = r % CO, ch = e * CO + c;
+    const float* sc = st + ((size_t)u * EC + ch) * NST;
+    const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+    const size_t rb = ((size_t)n * EC + ch) * HW;
+    float tg = 0.f, tgx = 0.f;
+#pragma unroll
+    for (int q = gl * 8; q < HW; q += 128) {
+      float d[8], zz[8];
+      load8(dh + rb + q, d);
+      load8(z + rb + q, zz);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = (a * zz[j] + b > 0.f) ? d[j] : 0.f;
+        tg += g;
+        tgx += g * (zz[j] - mu) * inv;
+      }
+    }
+    if (it & 1) {
+      sg1 += tg;
+      sgx1 += tgx;
+    } else {
+      sg0 += tg;
+      sgx0 += tgx;
+    }
+  }
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) {
+    sg0 += __shfl_xor(sg0, m);
+    sgx0 += __shfl_xor(sgx0, m);
+    sg1 += __shfl_xor(sg1, m);
+    sgx1 += __shfl_xor(sgx1, m);
+  }
+  if (gl == 0) {
+    float* o = slab + (((size_t)u * chunks + chunk) * EC + e * CO + grp) * 2;
+    o[0] = sg0;
+    o[1] = sgx0;
+    o[32] = sg1;   // channel grp + 16
+    o[33] = sgx1;
+  }
+}
+
+// c1 = gamma*invstd, c2 = c1*Sg/M, c3 = c1*Sgx/M per (u, ch); dgamma += sum_u Sgx, dbeta += sum_u Sg.
+__global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __restrict__ slab,
+                                                             const float* __restrict__ gamma, float* __restrict__ st,
+                                                             float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                             int U, int chunks, int EC, float count) {
+  const int ch = blockIdx.x, lane = threadIdx.x;
+  float tg = 0.f, tgx = 0.f;
+  for (int u = 0; u < U; ++u) {
+    float sg = 0.f, sgx = 0.f;
+    for (int k = lane; k < chunks; k += 64) {
+      sg += slab[(((size_t)u * chunks + k) * EC + ch) * 2];
+      sgx += slab[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
+    }
+    sg = wave_sum(sg);
+    sgx = wave_sum(sgx);
+    if (lane == 0) {
+      float* r = st + ((size_t)u * EC + ch) * NST;
+      const float c1 = gamma[ch] * r[ST_INV];
+      r[ST_C1] = c1;
+      r[ST_C2] = c1 * sg / count;
+      r[ST_C3] = c1 * sgx / count;
+    }
+    tg += sg;
+    tgx += sgx;
+  }
+  if (lane == 0) {
+    dgamma[ch] += tgx;
+    dbeta[ch] += tg;
+  }
+}
+
+// h = relu(a z + b) -> bf16 (the FC operand), 8 elements per thread.
+template <int HW>
+__global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __restrict__ z, const float* __restrict__ st,
+                                                            uint16_t* __restrict__ h, long n8, int EC, int B) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const long e0 = i * 8;
+    const long row = e0 / HW;             // (n, ch)
+    const int ch = (int)(row % EC);
+    const int n = (int)(row / EC);
+    const float* sc = st + ((size_t)(n / B) * EC + ch) * NST;
+    const float a = sc[ST_A], b = sc[ST_B];
+    float v[8];
+    load8(z + e0, v);
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = f32_to_bf16(fmaxf(a * v[2 * j] + b, 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(a * v[2 * j + 1] + b, 0.f)) << 16);
+    *reinterpret_cast<uint4*>(h + e0) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// out[i] += sum_rows slab[g][row][i] for every group g (rows contiguous per group).
+// block = 64 columns x 4 row phases; deterministic order (fixed per-thread row sets + fixed combine).
+__global__ void __launch_bounds__(256) slab_rows_sum_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                            int groups, int rows, int width) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + tx;
+  const int g = blockIdx.y;
+  float t = 0.f;
+  if (i < width) {
+    const float* s = slab + (size_t)g * rows * width + i;
+    for (int r = ty; r < rows; r += 4) t += s[(size_t)r * width];
+  }
+  red[ty][tx] = t;
+  __syncthreads();
+  if (ty == 0 && i < width) out[(size_t)g * width + i] += (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+}
+
+}  // namespace conv
+}  // namespace qd
+
+using namespace qd::conv;
+
+// ---------------------------------------------------------------------------------------------
+// C ABI.  Geometry: H=16 and W in {8, 16} (P128 / P256).  All launches on `stream`.
+// ---------------------------------------------------------------------------------------------
+#define QD_GEOM(W_, ...) \
+  if ((H) == 16 && (W) == 8) { constexpr int W_ = 8; __VA_ARGS__; } \
+  else if ((H) == 16 && (W) == 16) { constexpr int W_ = 16; __VA_ARGS__; } \
+  else return (int)hipErrorInvalidValue;
+
+static size_t fwd_smem(int cin, int H, int W) {
+  const int cinp = (cin % 16 == 0) ? cin + 8 : cin;
+  return 4 * (size_t)(H + 2) * (W + 2) * cinp * 2;
+}
+
+// layer: 1 -> CIN=2 raw f32 input; 2,3 -> CIN=32 bf16 z_prev with BN+ReLU (st_prev).
+QD_API int qd_conv_pack_weights(const float* w, uint16_t* out, int E, int cin, int dgrad, void* stream) {
+  const int KS = dgrad ? 18 : (9 * cin + 15) / 16;
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(KS, E), dim3(64), 0, (hipStream_t)stream, w, out, E, cin, KS, dgrad);
+  return (int)hipGetLastError();
+}
+
+// w: packed B fragments from qd_conv_pack_weights(dgrad=0)
+QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const uint16_t* w, uint16_t* z, float* stats,
+                       int N, int E, int B, int H, int W, int chunks, int spw, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int U = N / B;
+  dim3 grid(U * chunks, E);
+  if (chunks * 4 * spw < B) return (int)hipErrorInvalidValue;
+  if (layer == 1) {
+    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<2, 16, WW, IN_RAW_F32, OUT_Z_STATS, false, float>), grid, dim3(256),
+                                    fwd_smem(2, H, W), s, (const float*)xin, nullptr, nullptr, w, z, stats, E, B, chunks,
+                                    spw))
+  } else {
+    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNRELU, OUT_Z_STATS, false, uint16_t>), grid,
+                                    dim3(256), fwd_smem(32, H, W), s, (const uint16_t*)xin, nullptr, st_prev, w, z,
+                                    stats, E, B, chunks, spw))
+  }
+  return (int)hipGetLastError();
+}
+
+// data gradient of a 32->32 layer: dx (f32) from dh (f32 or bf16) of this layer, z, st.
+// w: packed B fragments from qd_conv_pack_weights(dgrad=1)
+QD_API int qd_conv_dgrad(const void* dh, int dh_bf16, const uint16_t* z, const float* st, const uint16_t* w, float* dx,
+                         int N, int E, int B, int H, int W, int chunks, int spw, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((N / B) * chunks, E);
+  if (chunks * 4 * spw < B) return (int)hipErrorInvalidValue;
+  if (dh_bf16) {
+    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNBWD, OUT_F32, true, uint16_t>), grid, dim3(256),
+                                    fwd_smem(32, H, W), s, (const uint16_t*)dh, z, st, w, dx, nullptr, E, B, chunks,
+                                    spw))
+  } else {
+    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNBWD, OUT_F32, true, float>), grid, dim3(256),
+                                    fwd_smem(32, H, W), s, (const float*)dh, z, st, w, dx, nullptr, E, B, chunks,
+                                    spw))
+  }
+  return (int)hipGetLastError();
+}
+
+static size_t wgrad_smem(int cin, int H, int W) {
+  const size_t stage = (3 * (size_t)cin * ((H + 2) * W + 8) + 32 * (size_t)(H * W + 8)) * 2;
+  const size_t red = (size_t)((9 * cin + 31) / 32) * 32 * 32 * 4;
+  return stage > red ? stage : red;
+}
+
+// weight-gradient partials: slab (E, U*chunks, 32*CIN*9).  layer 1: x = raw f32 (CIN=2);
+// layers 2,3: x = BN+ReLU(z_prev) (st_prev).
+QD_API int qd_conv_wgrad(int layer, const void* xin, const float* st_prev, const void* dh, int dh_bf16,
+                         const uint16_t* z, const float* st, float* slab, int N, int E, int B, int H, int W, int chunks,
+                         int spb, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((N / B) * chunks, E);
+  if (chunks * spb < B) return (int)hipErrorInvalidValue;
+#define QD_WG(CIN_, INM_, TIN_, TDH_)                                                                              \
+  QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_wgrad_kernel<CIN_, 16, WW, INM_, TIN_, TDH_>), grid, dim3(256),         \
+                                  wgrad_smem(CIN_, H, W), s, (const TIN_*)xin, st_prev, (const TDH_*)dh, z, st, slab, \
+                                  E, B, chunks, spb))
+  if (layer == 1) {
+    if (dh_bf16) { QD_WG(2, IN_RAW_F32, float, uint16_t) } else { QD_WG(2, IN_RAW_F32, float, float) }
+  } else {
+    if (dh_bf16) { QD_WG(32, IN_BNRELU, uint16_t, uint16_t) } else { QD_WG(32, IN_BNRELU, uint16_t, float) }
+  }
+#undef QD_WG
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_bn_stats_finalize(const float* stats, const float* gamma, const float* beta, float* run_mean,
+                                float* run_var, float* st, int U, int chunks, int EC, float count, float momentum,
+                                float eps, int training, void* stream) {
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(EC), dim3(64), 0, (hipStream_t)stream, stats, gamma,
+                     beta, run_mean, run_var, st, U, chunks, EC, count, momentum, eps, training);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_bn_bwd_reduce(const void* dh, int dh_bf16, const uint16_t* z, const float* st, float* slab, int N, int E,
+                            int B, int H, int W, int chunks, int spb, void* stream) {
+  dim3 grid((N / B) * chunks, E);
+  hipStream_t s = (hipStream_t)stream;
+  if (chunks * spb < B || H * W % 64) return (int)hipErrorInvalidValue;
+  if (H * W == 128) {
+    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb);
+  } else if (H * W == 256) {
+    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_bn_bwd_finalize(const float* slab, const float* gamma, float* st, float* dgamma, float* dbeta, int U,
+                              int chunks, int EC, float count, void* stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(EC), dim3(64), 0, (hipStream_t)stream, slab, gamma, st,
+                     dgamma, dbeta, U, chunks, EC, count);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int N, int EC, int B, int HW,
+                            void* stream) {
+  const long n8 = (long)N * EC * HW / 8;
+  int grid = (int)((n8 + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  if (HW == 128)
+    hipLaunchKernelGGL((bn_relu_apply_kernel<128>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B);
+  else if (HW == 256)
+    hipLaunchKernelGGL((bn_relu_apply_kernel<256>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_slab_rows_sum(const float* slab, float* out, int groups, int rows, int width, void* stream) {
+  hipLaunchKernelGGL(slab_rows_sum_kernel, dim3((width + 63) / 64, groups), dim3(256), 0, (hipStream_t)stream, slab,
+                     out, groups, rows, width);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,123 @@
+"""HIP conv-BN-ReLU stack of the HDCE experts (csrc/hip/conv.hip), forward + manual backward.
+
+Reference module: ``Conv_P128.cnn`` (Estimators_QuantumNAT_onchipQNN.py:246-261) = 3 x
+[Conv2d 3x3 no-bias -> BatchNorm2d(32) -> ReLU], one instance per scenario expert.
+
+``ConvStackHIP`` runs all experts for a whole 9-stream step with 3 forward conv launches
+(+3 tiny statistics launches) and 3 x (BN reduce, BN finalize, dgrad, wgrad, slab sum)
+backward launches; every buffer is allocated once, so the whole step is capturable in a
+HIP graph.  Gradients are written straight into the model's flat gradient buffer.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+
+from .. import _native as nat
+
+_p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+NST = 8
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return nat.ptr(t) if t is not None else None
+
+
+class ConvStackHIP:
+    """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
+
+    def __init__(self, model, U: int, B: int, spw: int = 1, spb_w: int = 8, spb_r: int = 8):
+        self.m = model
+        self.U, self.B, self.N, self.E = U, B, U * B, model.E
+        self.H, self.W = model.H, model.W
+        self.HW = self.H * self.W
+        self.EC = 32 * self.E
+        dev = model.device
+        self.spw = spw
+        self.chunks = (B + 4 * spw - 1) // (4 * spw)          # forward / dgrad: 4 waves x spw samples
+        self.spb_w = spb_w
+        self.chunks_w = (B + spb_w - 1) // spb_w              # wgrad workgroups per group
+        self.spb_r = spb_r
+        self.chunks_r = (B + spb_r - 1) // spb_r              # BN backward reductions
+        N, EC, HW = self.N, self.EC, self.HW
+        bf = torch.bfloat16
+        self.z = [torch.empty(N, EC, HW, device=dev, dtype=bf) for _ in range(3)]
+        self.h3 = torch.empty(N * self.E, 32 * HW, device=dev, dtype=bf)
+        self.st = [torch.zeros(U, EC, NST, device=dev) for _ in range(3)]
+        self.stats = torch.zeros(U, self.chunks, EC, 2, device=dev)
+        self.rslab = torch.zeros(U, self.chunks_r, EC, 2, device=dev)
+        self.dx = [torch.empty(N, EC, HW, device=dev) for _ in range(2)]   # grads w.r.t. h1, h2
+        self.wslab = [torch.empty(self.E, U * self.chunks_w, 32 * cin * 9, device=dev) for cin in (2, 32, 32)]
+        # bf16 B-fragment images of the weights (re-packed every step; 16-byte coalesced loads in-kernel)
+        self.cins = (2, 32, 32)
+        self.wpk = [torch.empty(self.E, (9 * cin + 15) // 16, 64, 8, device=dev, dtype=bf) for cin in self.cins]
+        self.wpk_t = [None] + [torch.empty(self.E, 18, 64, 8, device=dev, dtype=bf) for _ in range(2)]
+        self.lib = nat.hip_lib()
+        L = self.lib
+        self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
+        self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
+        self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
+        self._fin = nat.fn(L, "qd_bn_stats_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i, _p])
+        self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
+        self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _p])
+        self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p])
+        self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
+        self._pack = nat.fn(L, "qd_conv_pack_weights", [_p, _p, _i, _i, _i, _p])
+
+    def pack_weights(self, st, dgrad: bool) -> None:
+        for k in range(3):
+            if dgrad and k == 0:
+                continue
+            out = self.wpk_t[k] if dgrad else self.wpk[k]
+            nat.check(self._pack(nat.ptr(self.m.conv_w[k]), nat.ptr(out), self.E, self.cins[k], int(dgrad), st),
+                      "conv_pack_weights")
+
+    # --------------------------------------------------------------------- forward
+    def forward(self, x1: torch.Tensor, training: bool) -> torch.Tensor:
+        """x1: (N, E*2, H, W) fp32 contiguous.  Returns the FC operand (N*E, 32*H*W) bf16."""
+        m, st = self.m, nat.stream_ptr(x1.device)
+        assert x1.shape == (self.N, 2 * self.E, self.H, self.W) and x1.dtype == torch.float32 and x1.is_contiguous()
+        self.x1 = x1
+        self.pack_weights(st, dgrad=False)
+        inp, st_prev = x1, None
+        for k in range(3):
+            nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
+                                nat.ptr(self.stats), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw,
+                                st), f"conv_fwd{k + 1}")
+            nat.check(self._fin(nat.ptr(self.stats), nat.ptr(m.bn_w[k]), nat.ptr(m.bn_b[k]), nat.ptr(m.run_mean[k]),
+                                nat.ptr(m.run_var[k]), nat.ptr(self.st[k]), self.U, self.chunks, self.EC,
+                                float(self.B * self.HW), m.momentum, m.eps, int(training), st), f"bn_fin{k + 1}")
+            inp, st_prev = self.z[k], self.st[k]
+        nat.check(self._apply(nat.ptr(self.z[2]), nat.ptr(self.st[2]), nat.ptr(self.h3), self.N, self.EC, self.B,
+                              self.HW, st), "bn_relu_apply")
+        return self.h3
+
+    # --------------------------------------------------------------------- backward
+    def backward(self, dh3: torch.Tensor) -> None:
+        """dh3: dL/dh3 as (N*E, 32*H*W) (bf16 or fp32).  Accumulates conv/BN grads into the flat grad."""
+        m, st = self.m, nat.stream_ptr(dh3.device)
+        self.pack_weights(st, dgrad=True)
+        dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
+        for k in (2, 1, 0):
+            z, bst = self.z[k], self.st[k]
+            nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.rslab), self.N, self.E,
+                                 self.B, self.H, self.W, self.chunks_r, self.spb_r, st), f"bn_bwd_reduce{k + 1}")
+            nat.check(self._bfin(nat.ptr(self.rslab), nat.ptr(m.bn_w[k]), nat.ptr(bst), nat.ptr(m.bn_w[k].grad),
+                                 nat.ptr(m.bn_b[k].grad), self.U, self.chunks_r, self.EC, float(self.B * self.HW), st),
+                      f"bn_bwd_fin{k + 1}")
+            xin = self.x1 if k == 0 else self.z[k - 1]
+            st_prev = None if k == 0 else self.st[k - 1]
+            ws = self.wslab[k]
+            nat.check(self._wgrad(k + 1, nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst),
+                                  nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_w, self.spb_w, st),
+                      f"conv_wgrad{k + 1}")
+            nat.check(self._ssum(nat.ptr(ws), nat.ptr(m.conv_w[k].grad), self.E, ws.shape[1], ws.shape[2], st),
+                      f"wslab_sum{k + 1}")
+            if k > 0:
+                dx = self.dx[k - 1]
+                nat.check(self._dgrad(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.wpk_t[k]),
+                                      nat.ptr(dx), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw, st),
+                          f"conv_dgrad{k + 1}")
+                dh, dh_bf = dx, 0

@@ -206,17 +206,30 @@ def estimate_routed(convs: Sequence[nn.Module], fc: nn.Module, x: torch.Tensor, 
 
 
 class HDCEStep:
-    """One fused HDCE training step over 9 stream batches (see module docstring)."""
+    """One fused HDCE training step over 9 stream batches (see module docstring).
 
-    def __init__(self, model: HDCEModel, n_users: int, batch: int, grad_hook: Optional[Callable] = None):
+    GPU path (``hip=True``): the conv/BN/ReLU stack runs on the hand-written kernels of
+    csrc/hip/conv.hip with a manual backward, the FC on hipBLASLt (bf16 operands, fp32
+    weight-gradient output written straight into the flat gradient buffer), the loss on
+    csrc/hip/nmse.hip.  CPU / reference path: the same math through torch autograd."""
+
+    def __init__(self, model: HDCEModel, n_users: int, batch: int, grad_hook: Optional[Callable] = None,
+                 hip: Optional[bool] = None):
         self.m = model
         self.U, self.B = n_users, batch
         dev = model.device
         self.nmse = StreamNMSE(HDCEModel.row_stream(model.E, n_users, batch, dev), model.E * n_users)
         self.grad_hook = grad_hook  # called as grad_hook("fc") / grad_hook("conv") when buckets are final
+        self.hip = (dev.type == "cuda") if hip is None else hip
+        if self.hip:
+            from ..ops.conv import ConvStackHIP
+            self.conv = ConvStackHIP(model, n_users, batch)
+            self.fc_b_lp = None
 
     def __call__(self, Yp: torch.Tensor, HL: torch.Tensor, HP: torch.Tensor) -> torch.Tensor:
         """Yp (E,U,B,2,H,W), HL/HP (E,U,B,2048) fp32.  Returns device loss[2] (loss, loss_perf)."""
+        if self.hip:
+            return self._step_hip(Yp, HL, HP)
         m = self.m
         A = m.features(Yp, training=True)
         A_det = A.detach().requires_grad_(True)
@@ -235,9 +248,42 @@ class HDCEStep:
         m.count_batches(self.U)
         return loss
 
+    @torch.no_grad()
+    def _step_hip(self, Yp, HL, HP) -> torch.Tensor:
+        m = self.m
+        dt = m.compute_dtype
+        x1 = m.pack_input(Yp).float().contiguous()
+        A = self.conv.forward(x1, training=True)                # (rows, 4096) bf16
+        W = m.fc_w.detach().to(dt)
+        b = m.fc_b.detach().to(dt)
+        Y = torch.nn.functional.linear(A.to(dt), W, b)
+        label = HDCEModel.rows_from_streams(HL)
+        perf = HDCEModel.rows_from_streams(HP)
+        self.nmse.sums(Y, label, perf)
+        loss = self.nmse.finalize()
+        dY = self.nmse.grad(Y, label, out_dtype=dt)
+        _mm_f32(dY.t(), A.to(dt), m.fc_w.grad)               # dW = dY^T A   (fp32 out)
+        torch.sum(dY, dim=0, dtype=torch.float32, out=m.fc_b.grad)
+        if self.grad_hook:
+            self.grad_hook("fc")
+        dA = torch.mm(dY, W)                                   # (rows, 4096) bf16
+        self.conv.backward(dA)
+        if self.grad_hook:
+            self.grad_hook("conv")
+        m.count_batches(self.U)
+        return loss
+
     @property
     def skip(self) -> torch.Tensor:
         return self.nmse.skip
+
+
+def _mm_f32(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> None:
+    """out = a @ b with low-precision operands and an fp32 result (hipBLASLt)."""
+    if a.dtype == torch.float32:
+        torch.mm(a, b, out=out)
+    else:
+        torch.mm(a, b, out_dtype=torch.float32, out=out)
 
 
 class ClassifierStep:
