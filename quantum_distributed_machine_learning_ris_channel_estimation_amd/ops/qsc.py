@@ -1,0 +1,103 @@
+"""Fused QSC training step on the HIP kernels (csrc/hip/qsc.hip + csrc/hip/qsim.hip).
+
+Reference step (Runner_P128_QuantumNAT_onchipQNN.py:341-369): 9 forward calls of
+``QSC_P128`` (preprocess CNN -> PennyLane TorchLayer -> Linear -> log_softmax), summed
+``nll_loss / 9``, one autograd backward, optional pruning, AdamW.
+
+Here one step over all 9*B samples is 6 launches, no autograd:
+  qsc_pre_fwd   CNN preprocess + Linear + tanh            -> angles (B, n)
+  qsim_fwd      variational circuit                         -> E = <Z_i> (B, n)
+  qsc_head      Linear(n, C) + log_softmax + mean NLL + backward -> loss, dE, dWc, dbc
+  qsim_bwd      adjoint differentiation                     -> d angles, weight-grad slab
+  reduce_slab   -> qlayer.weights grad
+  qsc_pre_bwd   recompute + backprop the preprocess         -> slab -> flat grad (one column sum)
+All gradients land in the model's FlatParamSpace; every buffer is static (graph-capturable).
+QuantumNAT: each of the G streams gets its own noise draw w + sigma*N(0,1) (the reference
+draws per forward call), forward AND backward use it, the grads flow to the clean master.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from .. import _native as nat
+from ..ops.optim import FlatParamSpace
+
+_p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+
+
+class QSCStepHIP:
+    def __init__(self, model, space: FlatParamSpace, batch_total: int, n_groups: int = 1,
+                 grid_fwd: int = 512, grid_bwd: int = 256):
+        self.m = model
+        self.space = space
+        dev = space.flat.device
+        self.B = batch_total
+        self.G = n_groups
+        self.n = model.num_qubits
+        self.L = model.n_layers
+        self.C = model.n_classes
+        pre = model.preprocess
+        names = dict(zip(space.names, space.offsets))
+        o = [names["preprocess.0.weight"], names["preprocess.0.bias"], names["preprocess.3.weight"],
+             names["preprocess.3.bias"], names["preprocess.7.weight"], names["preprocess.7.bias"]]
+        row = o[5] + self.n - o[0]
+        self.offs = (ctypes.c_int * 7)(*(o + [row]))
+        self.row0, self.row = o[0], row
+        feat = pre[7].weight.shape[1]
+        self.Hh, self.Ww = (16, 8) if feat == 256 else (16, 16)
+        self.grid_fwd = min(grid_fwd, batch_total)
+        self.grid_bwd = min(grid_bwd, batch_total)
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.angles = torch.empty(batch_total, self.n, **f32)
+        self.E = torch.empty(batch_total, self.n, **f32)
+        self.dE = torch.empty(batch_total, self.n, **f32)
+        self.dang = torch.empty(batch_total, self.n, **f32)
+        self.loss = torch.zeros(1, **f32)
+        self.preslab = torch.empty(self.grid_bwd, row, **f32)
+        L = nat.hip_lib()
+        self.qrows = nat.fn(L, "qd_qsim_bwd_grid", [_i, _i])(self.n, batch_total)
+        self.qslab = torch.empty(self.qrows, 2 * self.n * self.L, **f32)
+        self._pre_fwd = nat.fn(L, "qd_qsc_pre_fwd", [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+        self._pre_bwd = nat.fn(L, "qd_qsc_pre_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+        self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p])
+        self._qf = nat.fn(L, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
+        self._qb = nat.fn(L, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+        self._rs = nat.fn(L, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
+        self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
+
+    def quantum_weights(self) -> torch.Tensor:
+        m = self.m
+        w = m.qlayer.weights.detach()
+        if m.training and m.use_quantumnat and m.noise_level > 0:
+            return w.unsqueeze(0) + m.noise_level * torch.randn((self.G,) + tuple(w.shape), device=w.device)
+        return w
+
+    @torch.no_grad()
+    def __call__(self, x: torch.Tensor, labels: torch.Tensor, loss_acc: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x (B, 2, H, W) fp32 contiguous, labels (B,) int64.  Accumulates grads; returns loss (1,)."""
+        m, sp = self.m, self.space
+        B, n, L = self.B, self.n, self.L
+        assert x.shape[0] == B and x.is_contiguous() and labels.dtype == torch.int64
+        st = nat.stream_ptr(x.device)
+        flat = sp.flat
+        nat.check(self._pre_fwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), B, n, self.Hh, self.Ww,
+                                self.grid_fwd, st), "qsc_pre_fwd")
+        w = self.quantum_weights().contiguous()
+        wgroup = B // w.shape[0] if w.dim() == 4 else 0
+        nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, wgroup, st), "qsim_fwd")
+        cls = m.classifier
+        nat.check(self._head(nat.ptr(self.E), nat.ptr(cls.weight), nat.ptr(cls.bias), nat.ptr(labels),
+                             nat.ptr(self.dE), nat.ptr(cls.weight.grad), nat.ptr(cls.bias.grad), nat.ptr(self.loss),
+                             nat.ptr(loss_acc) if loss_acc is not None else None, B, n, self.C, st), "qsc_head")
+        nat.check(self._qb(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.dE), nat.ptr(self.dang),
+                           nat.ptr(self.qslab), B, n, L, wgroup, st), "qsim_bwd")
+        nat.check(self._rs(nat.ptr(self.qslab), nat.ptr(m.qlayer.weights.grad), self.qrows, 2 * n * L, 1.0, st),
+                  "reduce_slab")
+        nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B, n,
+                                self.Hh, self.Ww, self.grid_bwd, st), "qsc_pre_bwd")
+        nat.check(self._ssum(nat.ptr(self.preslab), nat.ptr(sp.grad[self.row0:]), 1, self.grid_bwd, self.row, st),
+                  "qsc_slab_sum")
+        return self.loss

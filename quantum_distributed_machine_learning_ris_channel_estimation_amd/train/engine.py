@@ -294,10 +294,16 @@ class ClassifierStep:
     For QSC with QuantumNAT on, each stream gets its own noise draw (the reference draws
     per forward call) through grouped quantum weights."""
 
-    def __init__(self, model: nn.Module, n_streams: int, grad_hook: Optional[Callable] = None):
+    def __init__(self, model: nn.Module, n_streams: int, grad_hook: Optional[Callable] = None,
+                 space: Optional[FlatParamSpace] = None, batch_total: Optional[int] = None):
         self.model = model
         self.S = n_streams
         self.grad_hook = grad_hook
+        self.hip = None
+        dev = next(model.parameters()).device
+        if isinstance(model, QSC_P128) and dev.type == "cuda" and space is not None and batch_total:
+            from ..ops.qsc import QSCStepHIP
+            self.hip = QSCStepHIP(model, space, batch_total, n_groups=n_streams)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         m = self.model
@@ -312,6 +318,11 @@ class ClassifierStep:
         return m(x)
 
     def __call__(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        if self.hip is not None and x.shape[0] == self.hip.B:
+            loss = self.hip(x.contiguous(), labels)
+            if self.grad_hook:
+                self.grad_hook("all")
+            return loss
         out = self.forward(x)
         loss = F.nll_loss(out, labels)
         loss.backward()

@@ -73,7 +73,7 @@ class FlagshipTrainer:
         # bucket "fc": 33.6 MB, ready first; bucket "small": conv + QSC grads, coalesced
         self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "small": [sp.grad[:n_conv], self.qspace.grad]})
         self.hstep = HDCEStep(self.hdce, self.U, self.B, grad_hook=self._hdce_hook)
-        self.cstep = ClassifierStep(self.qsc, self.S)
+        self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B)
         self.idx = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.perm = torch.randperm(self.store.n, device=dev)
         self.cursor = 0

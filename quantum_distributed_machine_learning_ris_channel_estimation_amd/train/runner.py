@@ -304,7 +304,7 @@ class Y2HRunner:
         opt = make_optimizer(space, opt_name, self.lr, **kw)
         S, B = tr.n_streams, self.batch_size_DML
         buckets = GradBuckets(ctx, {"all": [space.grad]})
-        cstep = ClassifierStep(model, S, grad_hook=buckets.launch)
+        cstep = ClassifierStep(model, S, grad_hook=buckets.launch, space=space, batch_total=S * B)
         loss_acc = torch.zeros(1, device=ctx.device)
         static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
         gscale = 1.0 / ctx.world
