@@ -1,0 +1,87 @@
+"""The fused 9-stream HDCE engine reproduces the reference's per-stream loop exactly (fp32, CPU):
+9 calls of Conv[sid] -> CE, NMSE / 9 each, one backward per stream (R:181-204), including the
+BatchNorm running statistics after three sequential per-stream updates."""
+import copy
+
+import torch
+
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.models.estimators import NMSELoss
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.optim import FlatParamSpace, FusedOptimizer
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import (
+    ClassifierStep, HDCEModel, HDCEStep)
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.models.estimators import QSC_P128
+
+
+def test_hdce_step_equals_reference_per_stream_loop():
+    torch.manual_seed(0)
+    E, U, B = 3, 3, 8
+    m = HDCEModel(128, "cpu", "fp32")
+    ref_convs = [copy.deepcopy(c) for c in m.convs]
+    ref_fc = copy.deepcopy(m.fc)
+    # detach deep copies from the flat buffers
+    for mod in ref_convs + [ref_fc]:
+        for p in mod.parameters():
+            p.data = p.data.clone()
+            p.grad = None
+        for name, buf in list(mod.named_buffers()):
+            mod.get_buffer(name).data = buf.data.clone()
+    Yp = torch.randn(E, U, B, 2, 16, 8)
+    HL = torch.randn(E, U, B, 2048)
+    HP = HL + 0.1 * torch.randn_like(HL)
+    m.space.zero_grad()
+    loss = HDCEStep(m, U, B, hip=False)(Yp, HL, HP)
+    crit = NMSELoss()
+    tot, totp = 0.0, 0.0
+    for s in range(E):
+        for u in range(U):
+            h = ref_fc(ref_convs[s](Yp[s, u]))
+            l = crit(h, HL[s, u]) / 9
+            tot += float(l)
+            totp += float(crit(h, HP[s, u]) / 9)
+            l.backward()
+    assert abs(float(loss[0]) - tot) < 1e-5 and abs(float(loss[1]) - totp) < 1e-5
+    assert torch.allclose(m.fc.FC.weight.grad, ref_fc.FC.weight.grad, rtol=1e-4, atol=1e-7)
+    for e in range(E):
+        for (n1, p1), (n2, p2) in zip(m.convs[e].named_parameters(), ref_convs[e].named_parameters()):
+            assert torch.allclose(p1.grad, p2.grad, rtol=2e-3, atol=1e-6), (e, n1)
+        for (n1, b1), (n2, b2) in zip(m.convs[e].named_buffers(), ref_convs[e].named_buffers()):
+            assert torch.allclose(b1.float(), b2.float(), rtol=1e-4, atol=1e-6), (e, n1)
+
+
+def test_classifier_step_is_mean_nll_over_streams():
+    torch.manual_seed(1)
+    m = QSC_P128(n_qubits=4, use_quantumnat=False, use_gradient_pruning=False)
+    space = FlatParamSpace(list(m.named_parameters()))
+    S, b = 9, 5
+    x = torch.randn(S * b, 2, 16, 8)
+    y = torch.arange(S).div(3, rounding_mode="floor").repeat_interleave(b)
+    loss = ClassifierStep(m, S)(x, y)
+    ref = sum(torch.nn.functional.nll_loss(m(x[i * b:(i + 1) * b]), y[i * b:(i + 1) * b]) / 9 for i in range(S))
+    assert abs(float(loss) - float(ref)) < 1e-5
+
+
+def test_fused_optimizer_cpu_matches_torch():
+    torch.manual_seed(2)
+    for kind in ("adam", "adamw", "sgd"):
+        ref = [torch.nn.Parameter(torch.randn(7, 3)), torch.nn.Parameter(torch.randn(5))]
+        ours = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+        space = FlatParamSpace([(str(i), p) for i, p in enumerate(ours)])
+        if kind == "adam":
+            o_ref, o = torch.optim.Adam(ref, lr=0.01), FusedOptimizer(space, "adam", 0.01)
+        elif kind == "adamw":
+            o_ref, o = torch.optim.AdamW(ref, lr=0.01, weight_decay=0.01), FusedOptimizer(space, "adamw", 0.01,
+                                                                                         weight_decay=0.01)
+        else:
+            o_ref, o = torch.optim.SGD(ref, lr=0.01, momentum=0.9), FusedOptimizer(space, "sgd", 0.01)
+        for _ in range(4):
+            gs = [torch.randn_like(p) for p in ref]
+            for p, g in zip(ref, gs):
+                p.grad = g.clone()
+            for p, g in zip(ours, gs):
+                p.grad.copy_(g)
+            o_ref.step()
+            o.step()
+        for a, b in zip(ref, ours):
+            assert torch.allclose(a, b, atol=1e-6), kind
+        o.param_groups[0]["lr"] = 0.5
+        assert o.lr == 0.5 and float(o.lr_t) == 0.5
