@@ -32,10 +32,13 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="per-stream batch (batch_size_DML)")
     ap.add_argument("--qubits", type=int, default=8)
+    ap.add_argument("--pilot", type=int, default=128, choices=[128, 256], help="Pilot_num (P128 / P256 configs)")
+    ap.add_argument("--layers", type=int, default=3, help="QNN layers")
     ap.add_argument("--data-len", type=int, default=20000)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-quantumnat", action="store_true")
+    ap.add_argument("--split-graphs", action="store_true", help="3-graph DP plan even at 1 GPU")
     args = ap.parse_args()
 
     import torch
@@ -49,8 +52,9 @@ def main() -> int:
     if world_env != args.gpus and world_env != 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
     ctx = init_distributed("auto")
-    cfg = FlagshipConfig(n_qubits=args.qubits, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
-                         hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat)
+    cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
+                         hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
+                         split_graphs=args.split_graphs)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
@@ -75,7 +79,8 @@ def main() -> int:
     value = samples / elapsed
     if ctx.is_main:
         rec = {
-            "metric": "NMSE(dB) vs SNR + samples/sec, P128 RIS estimator at 1/2/4/8 MI355X",
+            "metric": "NMSE(dB) vs SNR + samples/sec, P128 RIS estimator at 1/2/4/8 MI355X"
+                      if args.pilot == 128 else f"samples/sec, P{args.pilot} RIS estimator",
             "value": round(value, 2),
             "unit": "samples/s",
             "n_gpus": n,
@@ -88,7 +93,8 @@ def main() -> int:
             "dtype": args.dtype,
             "data": "synthetic (DeepMIMO-shaped geometric channels, HBM-resident), random-init weights",
             "config": {
-                "model": f"P128 RIS, {args.qubits}-qubit QuantumNAT QNN + CNN estimator (HDCE: 3x Conv_P128 + FC_P128)",
+                "model": f"P{args.pilot} RIS, {args.qubits}-qubit {'QuantumNAT ' if cfg.use_quantumnat else ''}QNN + CNN "
+                     f"estimator (HDCE: 3x Conv_P{args.pilot} + FC_P{args.pilot})",
                 "global_batch": tr.samples_per_step * n,
                 "per_gpu_batch": tr.samples_per_step,
                 "streams": tr.S,
@@ -96,6 +102,7 @@ def main() -> int:
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "hip_graphs": bool(tr.graphed.enabled),
+                "graphs_per_step": len(tr.graphs),
                 "quantumnat": cfg.use_quantumnat,
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},

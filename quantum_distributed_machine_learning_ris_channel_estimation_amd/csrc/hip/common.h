@@ -56,4 +56,12 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   return *reinterpret_cast<uint16_t*>(&b);
 }
 
+// Opt a kernel in to more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
+template <class K>
+inline hipError_t allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 65536) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes);
+}
+
 }  // namespace qd

@@ -491,18 +491,32 @@ static size_t qsc_smem(int H, int W, bool bwd, int n) {
 }
 
 // offs: [w1, b1, w2, b2, wl, bl, row_width] float offsets into the flat parameter buffer.
+template <int H, int W>
+static int launch_pre_fwd(const float* x, const float* flat, Offs o, float* angles, int B, int n, int grid,
+                          hipStream_t s) {
+  const size_t sm = qsc_smem(H, W, false, n);
+  if (hipError_t e = qd::allow_lds(qsc_pre_fwd_kernel<H, W>, sm)) return (int)e;
+  hipLaunchKernelGGL((qsc_pre_fwd_kernel<H, W>), dim3(grid), dim3(NT), sm, s, x, flat, o, angles, B, n);
+  return (int)hipGetLastError();
+}
+
+template <int H, int W>
+static int launch_pre_bwd(const float* x, const float* flat, Offs o, const float* dang, float* slab, int B, int n,
+                          int grid, hipStream_t s) {
+  const size_t sm = qsc_smem(H, W, true, n);
+  if (hipError_t e = qd::allow_lds(qsc_pre_bwd_kernel<H, W>, sm)) return (int)e;
+  hipLaunchKernelGGL((qsc_pre_bwd_kernel<H, W>), dim3(grid), dim3(NT), sm, s, x, flat, o, dang, slab, B, n);
+  return (int)hipGetLastError();
+}
+
 QD_API int qd_qsc_pre_fwd(const float* x, const float* flat, const int* offs, float* angles, int B, int n, int H, int W,
                           int grid, void* stream) {
   if (n > 16 || B <= 0) return (int)hipErrorInvalidValue;
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8)
-    hipLaunchKernelGGL((qsc_pre_fwd_kernel<16, 8>), dim3(grid), dim3(NT), qsc_smem(H, W, false, n), s, x, flat, o, angles, B, n);
-  else if (H == 16 && W == 16)
-    hipLaunchKernelGGL((qsc_pre_fwd_kernel<16, 16>), dim3(grid), dim3(NT), qsc_smem(H, W, false, n), s, x, flat, o, angles, B, n);
-  else
-    return (int)hipErrorInvalidValue;
-  return (int)hipGetLastError();
+  if (H == 16 && W == 8) return launch_pre_fwd<16, 8>(x, flat, o, angles, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_pre_fwd<16, 16>(x, flat, o, angles, B, n, grid, s);
+  return (int)hipErrorInvalidValue;
 }
 
 // slab: (grid, offs[6]) floats; row layout = flat layout starting at offs[0].
@@ -511,13 +525,9 @@ QD_API int qd_qsc_pre_bwd(const float* x, const float* flat, const int* offs, co
   if (n > 16 || B <= 0 || qsc_smem(H, W, true, n) > 160 * 1024) return (int)hipErrorInvalidValue;
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8)
-    hipLaunchKernelGGL((qsc_pre_bwd_kernel<16, 8>), dim3(grid), dim3(NT), qsc_smem(H, W, true, n), s, x, flat, o, dang, slab, B, n);
-  else if (H == 16 && W == 16)
-    hipLaunchKernelGGL((qsc_pre_bwd_kernel<16, 16>), dim3(grid), dim3(NT), qsc_smem(H, W, true, n), s, x, flat, o, dang, slab, B, n);
-  else
-    return (int)hipErrorInvalidValue;
-  return (int)hipGetLastError();
+  if (H == 16 && W == 8) return launch_pre_bwd<16, 8>(x, flat, o, dang, slab, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_pre_bwd<16, 16>(x, flat, o, dang, slab, B, n, grid, s);
+  return (int)hipErrorInvalidValue;
 }
 
 QD_API int qd_qsc_head(const float* E, const float* wc, const float* bc, const long* labels, float* dE, float* dwc,

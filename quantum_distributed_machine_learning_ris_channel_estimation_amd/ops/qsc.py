@@ -1,4 +1,4 @@
-"""Fused QSC training step on the HIP kernels (csrc/hip/qsc.hip + csrc/hip/qsim.hip).
+"""Fused QSC training step on the HIP kernels (csrc/hip/qsc.hip + csrc/hip/qsim{,_big}.hip).
 
 Reference step (Runner_P128_QuantumNAT_onchipQNN.py:341-369): 9 forward calls of
 ``QSC_P128`` (preprocess CNN -> PennyLane TorchLayer -> Linear -> log_softmax), summed
@@ -24,6 +24,7 @@ import torch
 
 from .. import _native as nat
 from ..ops.optim import FlatParamSpace
+from ..ops.quantum import HIP_REG_MAX_QUBITS
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
@@ -58,13 +59,25 @@ class QSCStepHIP:
         self.loss = torch.zeros(1, **f32)
         self.preslab = torch.empty(self.grid_bwd, row, **f32)
         L = nat.hip_lib()
-        self.qrows = nat.fn(L, "qd_qsim_bwd_grid", [_i, _i])(self.n, batch_total)
+        self.big = self.n > HIP_REG_MAX_QUBITS  # workgroup-per-sample simulator (qsim_big.hip)
+        if self.big:
+            self.qrows = nat.fn(L, "qd_qsim_big_grid", [_i])(batch_total)
+            ws = nat.fn(L, "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)
+            nb = max(ws(self.n, self.qrows, 0), ws(self.n, self.qrows, 1))
+            self.qws = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else None
+        else:
+            self.qrows = nat.fn(L, "qd_qsim_bwd_grid", [_i, _i])(self.n, batch_total)
+            self.qws = None
         self.qslab = torch.empty(self.qrows, 2 * self.n * self.L, **f32)
         self._pre_fwd = nat.fn(L, "qd_qsc_pre_fwd", [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._pre_bwd = nat.fn(L, "qd_qsc_pre_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p])
-        self._qf = nat.fn(L, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
-        self._qb = nat.fn(L, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+        if self.big:
+            self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
+            self._qb = nat.fn(L, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
+        else:
+            self._qf = nat.fn(L, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
+            self._qb = nat.fn(L, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
         self._rs = nat.fn(L, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
         self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
 
@@ -87,13 +100,15 @@ class QSCStepHIP:
                                 self.grid_fwd, st), "qsc_pre_fwd")
         w = self.quantum_weights().contiguous()
         wgroup = B // w.shape[0] if w.dim() == 4 else 0
-        nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, wgroup, st), "qsim_fwd")
+        extra = (nat.ptr(self.qws) if self.qws is not None else None,) if self.big else ()
+        nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, wgroup, *extra, st),
+                  "qsim_fwd")
         cls = m.classifier
         nat.check(self._head(nat.ptr(self.E), nat.ptr(cls.weight), nat.ptr(cls.bias), nat.ptr(labels),
                              nat.ptr(self.dE), nat.ptr(cls.weight.grad), nat.ptr(cls.bias.grad), nat.ptr(self.loss),
                              nat.ptr(loss_acc) if loss_acc is not None else None, B, n, self.C, st), "qsc_head")
         nat.check(self._qb(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.dE), nat.ptr(self.dang),
-                           nat.ptr(self.qslab), B, n, L, wgroup, st), "qsim_bwd")
+                           nat.ptr(self.qslab), B, n, L, wgroup, *extra, st), "qsim_bwd")
         nat.check(self._rs(nat.ptr(self.qslab), nat.ptr(m.qlayer.weights.grad), self.qrows, 2 * n * L, 1.0, st),
                   "reduce_slab")
         nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B, n,

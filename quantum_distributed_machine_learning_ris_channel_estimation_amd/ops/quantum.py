@@ -8,8 +8,10 @@ through its tape ("best" diff method, E:148).
 
 Here three interchangeable backends implement the SAME function:
 
-* ``hip``   -- hand-written CDNA4 kernels (csrc/hip/qsim.hip): register-resident
-               batched state vectors, forward + adjoint backward.  Default on GPU.
+* ``hip``   -- hand-written CDNA4 kernels: csrc/hip/qsim.hip (n <= 10: register-resident
+               state, one wave per sample) and csrc/hip/qsim_big.hip (n = 11..16: one
+               512-thread workgroup per sample, state in LDS or an HBM workspace),
+               forward + adjoint backward.  Default on GPU.
 * ``cpu``   -- C++/OpenMP simulator (csrc/cpu/qsim_cpu.cpp). Default on CPU.
 * ``torch`` -- eager complex-tensor simulator differentiated by autograd: the
                "reference-equivalent" gate-by-gate path used as a baseline and an
@@ -29,31 +31,75 @@ _i = ctypes.c_int
 _f = ctypes.c_float
 _p = ctypes.c_void_p
 
-HIP_MAX_QUBITS = 10
+HIP_REG_MAX_QUBITS = 10   # register-resident kernel
+HIP_MAX_QUBITS = 16       # workgroup-per-sample kernel above that
+
+
+def _big_ws(n: int, grid: int, backward: bool, device) -> Optional[torch.Tensor]:
+    nbytes = nat.fn(nat.hip_lib(), "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)(n, grid, int(backward))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device) if nbytes else None
+
+
+def hip_qsim_fwd(x: torch.Tensor, w: torch.Tensor, E: torch.Tensor, wgroup: int = 0) -> None:
+    """Raw launcher (no autograd): E = <Z>(x, w); x (B, n) fp32, w (L, n, 2) or (G, L, n, 2) fp32."""
+    lib = nat.hip_lib()
+    B, n = x.shape
+    L = w.shape[-3]
+    st = nat.stream_ptr(x.device)
+    if n <= HIP_REG_MAX_QUBITS:
+        f = nat.fn(lib, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
+        nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, st), "qd_qsim_fwd")
+        return
+    grid = nat.fn(lib, "qd_qsim_big_grid", [_i])(B)
+    ws = _big_ws(n, grid, False, x.device)
+    f = nat.fn(lib, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
+    nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, nat.ptr(ws) if ws is not None else None, st),
+              "qd_qsim_big_fwd")
+
+
+def hip_qsim_bwd_slab(x: torch.Tensor, w: torch.Tensor, gE: torch.Tensor, dx: torch.Tensor) -> torch.Tensor:
+    """Raw adjoint backward: writes dx (B, n), returns the (rows, 2nL) weight-grad slab."""
+    lib = nat.hip_lib()
+    B, n = x.shape
+    L = w.shape[-3]
+    P = 2 * n * L
+    st = nat.stream_ptr(x.device)
+    if n <= HIP_REG_MAX_QUBITS:
+        rows = nat.fn(lib, "qd_qsim_bwd_grid", [_i, _i])(n, B)
+        slab = torch.empty(rows, P, device=x.device, dtype=torch.float32)
+        f = nat.fn(lib, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+        nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup_of(x, w), st),
+                  "qd_qsim_bwd")
+        return slab
+    rows = nat.fn(lib, "qd_qsim_big_grid", [_i])(B)
+    slab = torch.empty(rows, P, device=x.device, dtype=torch.float32)
+    ws = _big_ws(n, rows, True, x.device)
+    f = nat.fn(lib, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
+    nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup_of(x, w),
+                nat.ptr(ws) if ws is not None else None, st), "qd_qsim_big_bwd")
+    return slab
+
+
+def wgroup_of(x: torch.Tensor, w: torch.Tensor) -> int:
+    return x.shape[0] // w.shape[0] if w.dim() == 4 else 0
 
 
 # ----------------------------------------------------------------------------- HIP
 class _QSimHIP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x: torch.Tensor, w: torch.Tensor, wgroup: int = 0):
-        lib = nat.hip_lib()
         B, n = x.shape
-        L = w.shape[-3]
         x = x.detach().float().contiguous()
         w = w.detach().float().contiguous()
         E = torch.empty(B, n, device=x.device, dtype=torch.float32)
         if B > 0:
-            f = nat.fn(lib, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
-            nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, nat.stream_ptr(x.device)),
-                      "qd_qsim_fwd")
+            hip_qsim_fwd(x, w, E, wgroup)
         ctx.save_for_backward(x, w)
-        ctx.wgroup = wgroup
         return E
 
     @staticmethod
     def backward(ctx, gE: torch.Tensor):
         x, w = ctx.saved_tensors
-        lib = nat.hip_lib()
         B, n = x.shape
         L = w.shape[-3]
         P = 2 * n * L
@@ -61,14 +107,10 @@ class _QSimHIP(torch.autograd.Function):
         dx = torch.empty_like(x)
         dw = torch.zeros(P, device=x.device, dtype=torch.float32)
         if B > 0:
-            rows = nat.fn(lib, "qd_qsim_bwd_grid", [_i, _i])(n, B)
-            slab = torch.empty(rows, P, device=x.device, dtype=torch.float32)
-            st = nat.stream_ptr(x.device)
-            f = nat.fn(lib, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
-            nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, ctx.wgroup, st),
-                      "qd_qsim_bwd")
-            r = nat.fn(lib, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
-            nat.check(r(nat.ptr(slab), nat.ptr(dw), rows, P, 0.0, st), "qd_reduce_slab")
+            slab = hip_qsim_bwd_slab(x, w, gE, dx)
+            r = nat.fn(nat.hip_lib(), "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
+            nat.check(r(nat.ptr(slab), nat.ptr(dw), slab.shape[0], P, 0.0, nat.stream_ptr(x.device)),
+                      "qd_reduce_slab")
         dw = dw.view(L, n, 2)
         if w.dim() == 4:  # grouped (noisy) weights: every group maps back to the same master weights
             dw = _group_grad(dw, w)
@@ -186,7 +228,9 @@ def qsim(x: torch.Tensor, w: torch.Tensor, backend: Optional[str] = None) -> tor
         if x.device.type != "cuda":
             raise RuntimeError("hip backend needs CUDA/HIP tensors")
         if n > HIP_MAX_QUBITS:
-            raise NotImplementedError(f"HIP register-resident path supports n <= {HIP_MAX_QUBITS}")
+            raise NotImplementedError(f"HIP simulators support n <= {HIP_MAX_QUBITS}")
+        if 2 * n * w.shape[-3] > 256 and n > HIP_REG_MAX_QUBITS:
+            raise NotImplementedError("large-n HIP simulator supports 2*n*L <= 256")
         wgroup = x.shape[0] // w.shape[0] if w.dim() == 4 else 0
         return _QSimHIP.apply(x, w, wgroup)
     if w.dim() == 4:  # host backends: run per group

@@ -228,8 +228,18 @@ class HDCEStep:
 
     def __call__(self, Yp: torch.Tensor, HL: torch.Tensor, HP: torch.Tensor) -> torch.Tensor:
         """Yp (E,U,B,2,H,W), HL/HP (E,U,B,2048) fp32.  Returns device loss[2] (loss, loss_perf)."""
+        loss = self.forward_fc(Yp, HL, HP)
+        if self.grad_hook:
+            self.grad_hook("fc")
+        self.backward_conv()
+        if self.grad_hook:
+            self.grad_hook("conv")
+        return loss
+
+    # Phase 1: forward, fused NMSE, complete FC backward (FC grads final, dA ready).
+    def forward_fc(self, Yp: torch.Tensor, HL: torch.Tensor, HP: torch.Tensor) -> torch.Tensor:
         if self.hip:
-            return self._step_hip(Yp, HL, HP)
+            return self._forward_fc_hip(Yp, HL, HP)
         m = self.m
         A = m.features(Yp, training=True)
         A_det = A.detach().requires_grad_(True)
@@ -240,16 +250,20 @@ class HDCEStep:
         loss = self.nmse.finalize()
         dY = self.nmse.grad(Y, label, out_dtype=Y.dtype)
         torch.autograd.backward(Y, dY)             # FC grads + dA
-        if self.grad_hook:
-            self.grad_hook("fc")
-        torch.autograd.backward(A, A_det.grad)     # conv/BN grads
-        if self.grad_hook:
-            self.grad_hook("conv")
-        m.count_batches(self.U)
+        self._A, self._dA = A, A_det.grad
         return loss
 
+    # Phase 2: conv/BN backward from dA.
+    def backward_conv(self) -> None:
+        if self.hip:
+            self.conv.backward(self._dA)
+        else:
+            torch.autograd.backward(self._A, self._dA)
+            self._A = None
+        self.m.count_batches(self.U)
+
     @torch.no_grad()
-    def _step_hip(self, Yp, HL, HP) -> torch.Tensor:
+    def _forward_fc_hip(self, Yp, HL, HP) -> torch.Tensor:
         m = self.m
         dt = m.compute_dtype
         x1 = m.pack_input(Yp).float().contiguous()
@@ -264,13 +278,7 @@ class HDCEStep:
         dY = self.nmse.grad(Y, label, out_dtype=dt)
         _mm_f32(dY.t(), A.to(dt), m.fc_w.grad)               # dW = dY^T A   (fp32 out)
         torch.sum(dY, dim=0, dtype=torch.float32, out=m.fc_b.grad)
-        if self.grad_hook:
-            self.grad_hook("fc")
-        dA = torch.mm(dY, W)                                   # (rows, 4096) bf16
-        self.conv.backward(dA)
-        if self.grad_hook:
-            self.grad_hook("conv")
-        m.count_batches(self.U)
+        self._dA = torch.mm(dY, W)                             # (rows, 4096) bf16
         return loss
 
     @property

@@ -43,6 +43,7 @@ class FlagshipConfig:
     lr: float = 1e-3
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
+    split_graphs: bool = False   # force the 3-graph DP execution plan even at world 1 (testing)
     seed: int = 0
     n_scenarios: int = 3
     n_users: int = 3
@@ -72,7 +73,7 @@ class FlagshipTrainer:
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
         # bucket "fc": 33.6 MB, ready first; bucket "small": conv + QSC grads, coalesced
         self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "small": [sp.grad[:n_conv], self.qspace.grad]})
-        self.hstep = HDCEStep(self.hdce, self.U, self.B, grad_hook=self._hdce_hook)
+        self.hstep = HDCEStep(self.hdce, self.U, self.B)
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B)
         self.idx = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.perm = torch.randperm(self.store.n, device=dev)
@@ -80,28 +81,47 @@ class FlagshipTrainer:
         self.hloss = torch.zeros(2, device=dev)
         self.qloss = torch.zeros(1, device=dev)
         self.labels = self.store.scen.repeat_interleave(self.B)
-        self.graphed = GraphedStep(self._step_body, enabled=cfg.hip_graphs and dev.type == "cuda" and ctx.world == 1)
+        graphs = cfg.hip_graphs and dev.type == "cuda"
+        if ctx.world == 1 and not cfg.split_graphs:
+            # one graph: gather, both forwards, NMSE, both backwards, both optimizers
+            self.graphs = [GraphedStep(self._step_body, enabled=graphs)]
+        else:
+            # three graphs around the two gradient all-reduces; the FC bucket (33.6 MB) is reduced on
+            # RCCL's stream while graph 2 (conv + QSC backward) runs on the compute stream
+            pool = torch.cuda.graph_pool_handle() if graphs else None
+            self.graphs = [GraphedStep(f, enabled=graphs, pool=pool) for f in (self._phase1, self._phase2, self._phase3)]
 
-    def _hdce_hook(self, name: str) -> None:
-        if name == "fc":
-            self.buckets.launch("fc")   # overlaps the conv + QSC backward below
-
-    def _step_body(self) -> None:
-        E, U, B, S = self.E, self.U, self.B, self.S
+    # -- phases ---------------------------------------------------------------------------
+    def _phase1(self) -> None:
+        E, U, B = self.E, self.U, self.B
         self.hdce.space.zero_grad()
         self.qspace.zero_grad()
-        Yp, HL, HP = self.store.gather(self.idx)
-        # HDCE estimator: fwd, fused NMSE, FC bwd (-> bucket "fc" launched), conv bwd
-        loss = self.hstep(Yp.view(E, U, B, *Yp.shape[2:]), HL.view(E, U, B, -1), HP.view(E, U, B, -1))
+        self.Yp, HL, HP = self.store.gather(self.idx)
+        loss = self.hstep.forward_fc(self.Yp.view(E, U, B, *self.Yp.shape[2:]), HL.view(E, U, B, -1),
+                                     HP.view(E, U, B, -1))
         self.hloss.copy_(loss)
-        # QSC scenario classifier on the same pilots
-        q = self.cstep(Yp.reshape(S * B, *Yp.shape[2:]), self.labels)
+
+    def _phase2(self) -> None:
+        self.hstep.backward_conv()
+        q = self.cstep(self.Yp.reshape(self.S * self.B, *self.Yp.shape[2:]), self.labels)
         self.qloss.copy_(q)
-        self.buckets.launch("small")
-        self.buckets.wait()
+
+    def _phase3(self) -> None:
         g = 1.0 / self.ctx.world
         self.hopt.step(grad_scale=g, skip=self.hstep.skip)
         self.qopt.step(grad_scale=g)
+
+    def _step_body(self) -> None:
+        self._phase1()
+        self.buckets.launch("fc")
+        self._phase2()
+        self.buckets.launch("small")
+        self.buckets.wait()
+        self._phase3()
+
+    @property
+    def graphed(self) -> GraphedStep:
+        return self.graphs[0]
 
     def next_batch(self) -> None:
         if self.cursor + self.B > self.store.n:
@@ -112,7 +132,16 @@ class FlagshipTrainer:
 
     def step(self) -> None:
         self.next_batch()
-        self.graphed()
+        if len(self.graphs) == 1:
+            self.graphs[0]()
+            return
+        g1, g2, g3 = self.graphs
+        g1()
+        self.buckets.launch("fc")
+        g2()
+        self.buckets.launch("small")
+        self.buckets.wait()
+        g3()
 
     @property
     def samples_per_step(self) -> int:

@@ -21,9 +21,13 @@ for s in $STEPS; do
   case $s in
     build) run build 600 python __graft_entry__.py build ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
-    pytest) run pytest 900 python -m pytest tests -m gpu -x -q ;;
+    pytest) run pytest 900 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py --steps ${BENCH_STEPS:-50} --warmup 10 ;;
     bench_eager) run bench_eager 600 python bench.py --steps 20 --warmup 5 --no-graphs ;;
+    bench_p256) run bench_p256 600 python bench.py --steps 20 --warmup 5 --pilot 256 --qubits 12 ;;
+    bench_q16) run bench_q16 600 python bench.py --steps 10 --warmup 3 --qubits 16 ;;
+    train) run train 1200 python scripts/train_eval.py --epochs ${EPOCHS:-100} --qubits 6 --qml-qubits 4,8 --out "$OUT/train" ;;
+    bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 20 --warmup 5) ;;
   esac
 done

@@ -31,6 +31,35 @@ def test_qsim_hip_matches_cpp(cuda, n, L):
     assert torch.allclose(wg.grad.cpu(), wc.grad, atol=5e-4 * max(1, B / 16)), (wg.grad.cpu() - wc.grad).abs().max()
 
 
+@pytest.mark.parametrize("n,L,B", [(11, 3, 9), (12, 3, 7), (13, 2, 5), (14, 3, 4), (16, 3, 3), (16, 8, 2)])
+def test_qsim_big_hip_matches_cpp(cuda, n, L, B):
+    """Workgroup-per-sample kernels (qsim_big.hip): LDS-resident (n<=12 bwd, n<=13 fwd) and HBM paths."""
+    g = torch.Generator().manual_seed(7 * n + L)
+    x = torch.rand(B, n, generator=g) * 2 - 1
+    w = torch.rand(L, n, 2, generator=g) * 2 * math.pi
+    gE = torch.randn(B, n, generator=g)
+    xc, wc = x.clone().requires_grad_(), w.clone().requires_grad_()
+    Ec = qsim(xc, wc, "cpu")
+    (Ec * gE).sum().backward()
+    xg, wg = x.to(cuda).requires_grad_(), w.to(cuda).requires_grad_()
+    Eg = qsim(xg, wg, "hip")
+    (Eg * gE.to(cuda)).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(Eg.cpu(), Ec, atol=5e-5), (Eg.cpu() - Ec).abs().max()
+    assert torch.allclose(xg.grad.cpu(), xc.grad, atol=2e-4), (xg.grad.cpu() - xc.grad).abs().max()
+    assert torch.allclose(wg.grad.cpu(), wc.grad, atol=1e-3), (wg.grad.cpu() - wc.grad).abs().max()
+
+
+def test_qsim_big_hip_groups(cuda):
+    n, L, G, b = 12, 3, 3, 4
+    torch.manual_seed(1)
+    x = torch.rand(G * b, n) * 2 - 1
+    w = torch.rand(G, L, n, 2) * 6.28
+    Eg = qsim(x.to(cuda), w.to(cuda), "hip").cpu()
+    Ec = torch.cat([qsim(x[i * b:(i + 1) * b], w[i], "cpu") for i in range(G)])
+    assert torch.allclose(Eg, Ec, atol=5e-5)
+
+
 def test_qsim_hip_large_batch_and_groups(cuda):
     n, L, G, b = 8, 3, 9, 256
     torch.manual_seed(0)
