@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) stream_sums_kernel(const float* __restric
 
 // loss = sum_s num_s/den_s / S (same for perf); coef_s = 2/(S den_s); skip if non-finite.
 __global__ void finalize_kernel(const float* __restrict__ ss, float* __restrict__ loss, float* __restrict__ coef,
-                                int* __restrict__ skip, int S, float loss_scale) {
+                                float* __restrict__ skip, int S, float loss_scale) {
   if (threadIdx.x != 0) return;
   float l = 0.f, lp = 0.f;
   for (int s = 0; s < S; ++s) {
@@ -100,7 +100,7 @@ __global__ void finalize_kernel(const float* __restrict__ ss, float* __restrict_
   }
   loss[0] = l / (float)S;
   loss[1] = lp / (float)S;
-  if (skip) *skip = isfinite(loss[0]) ? 0 : 1;
+  if (skip) *skip = isfinite(loss[0]) ? 0.f : 1.f;
 }
 
 template <typename TY, typename TD>
@@ -152,7 +152,7 @@ QD_API int qd_nmse_stream_sums(const float* rowsums, const int* row_stream, floa
   return (int)hipGetLastError();
 }
 
-QD_API int qd_nmse_finalize(const float* ss, float* loss, float* coef, int* skip, int S, float loss_scale,
+QD_API int qd_nmse_finalize(const float* ss, float* loss, float* coef, float* skip, int S, float loss_scale,
                             void* stream) {
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ss, loss, coef, skip, S, loss_scale);
   return (int)hipGetLastError();

@@ -25,9 +25,9 @@ struct AdamArgs {
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n,
                                                    const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr,
-                                                   const int* __restrict__ skip, unsigned int* __restrict__ pruned,
+                                                   const float* __restrict__ skip, unsigned int* __restrict__ pruned,
                                                    AdamArgs a) {
-  if (skip != nullptr && *skip) return;
+  if (skip != nullptr && *skip != 0.f) return;
   const float lr = *lr_ptr;
   const float t = *step_ptr + 1.f;  // step about to be taken
   const float bc1 = 1.f - __powf(a.beta1, t);
@@ -84,9 +84,9 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
 
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
                                                   float* __restrict__ buf, long n, const float* __restrict__ lr_ptr,
-                                                  const float* __restrict__ step_ptr, const int* __restrict__ skip,
+                                                  const float* __restrict__ step_ptr, const float* __restrict__ skip,
                                                   float momentum, float weight_decay, float grad_scale) {
-  if (skip != nullptr && *skip) return;
+  if (skip != nullptr && *skip != 0.f) return;
   const float lr = *lr_ptr;
   const bool first = *step_ptr < 0.5f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -97,8 +97,8 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
   }
 }
 
-__global__ void step_tick_kernel(float* step, const int* skip) {
-  if (skip == nullptr || *skip == 0) *step += 1.f;
+__global__ void step_tick_kernel(float* step, const float* skip) {
+  if (skip == nullptr || *skip == 0.f) *step += 1.f;
 }
 
 inline int grid_for(long n) {
@@ -113,7 +113,7 @@ inline int grid_for(long n) {
 
 using namespace qd::optim;
 
-QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const int* skip,
+QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const float* skip,
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
                         float grad_scale, float prune_thr, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -123,7 +123,7 @@ QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const fl
   return (int)hipGetLastError();
 }
 
-QD_API int qd_sgd_step(float* p, float* g, float* buf, long n, const float* lr, float* step, const int* skip,
+QD_API int qd_sgd_step(float* p, float* g, float* buf, long n, const float* lr, float* step, const float* skip,
                        float momentum, float weight_decay, float grad_scale, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (n > 0) hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, buf, n, lr, step, skip, momentum,

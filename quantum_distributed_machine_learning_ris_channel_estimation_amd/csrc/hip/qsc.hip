@@ -412,7 +412,8 @@ __global__ void __launch_bounds__(1024) qsc_head_kernel(const float* __restrict_
                                                         const float* __restrict__ bc, const long* __restrict__ labels,
                                                         float* __restrict__ dE, float* __restrict__ dwc,
                                                         float* __restrict__ dbc, float* __restrict__ loss,
-                                                        float* __restrict__ loss_acc, int B) {
+                                                        float* __restrict__ loss_acc, float* __restrict__ skip,
+                                                        int skip_add, int B) {
   constexpr int P = C * N + C;
   __shared__ float red[16][P + 1];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -475,6 +476,10 @@ __global__ void __launch_bounds__(1024) qsc_head_kernel(const float* __restrict_
     else {
       loss[0] = s * invB;
       if (loss_acc) loss_acc[0] += s * invB;
+      if (skip) {  // NaN guard: a non-finite loss turns the optimizer step into a no-op
+        const float bad = isfinite(s) ? 0.f : 1.f;
+        skip[0] = skip_add ? skip[0] + bad : bad;
+      }
     }
   }
 }
@@ -531,12 +536,13 @@ QD_API int qd_qsc_pre_bwd(const float* x, const float* flat, const int* offs, co
 }
 
 QD_API int qd_qsc_head(const float* E, const float* wc, const float* bc, const long* labels, float* dE, float* dwc,
-                       float* dbc, float* loss, float* loss_acc, int B, int n, int C, void* stream) {
+                       float* dbc, float* loss, float* loss_acc, float* skip, int skip_add, int B, int n, int C,
+                       void* stream) {
   hipStream_t s = (hipStream_t)stream;
 #define QD_HEAD(NN, CC)                                                                                      \
   if (n == NN && C == CC) {                                                                                 \
     hipLaunchKernelGGL((qsc_head_kernel<NN, CC>), dim3(1), dim3(1024), 0, s, E, wc, bc, labels, dE, dwc, dbc, \
-                       loss, loss_acc, B);                                                                  \
+                       loss, loss_acc, skip, skip_add, B);                                                               \
     return (int)hipGetLastError();                                                                          \
   }
 #define QD_HEAD_N(NN) QD_HEAD(NN, 2) QD_HEAD(NN, 3) QD_HEAD(NN, 4)

@@ -36,7 +36,7 @@ class StreamNMSE:
         self.ss = torch.zeros(n_streams, 4, device=dev)       # (err, pow, err_perf, pow_perf) per stream
         self.loss = torch.zeros(2, device=dev)               # (loss, loss_perf)
         self.coef = torch.zeros(n_streams, device=dev)
-        self.skip = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.skip = torch.zeros(1, device=dev, dtype=torch.float32)  # NaN guard flag (all-reduced in DP)
         self._rs_long = self.row_stream.long()
 
     def sums(self, Y: torch.Tensor, label: torch.Tensor, perf: Optional[torch.Tensor]) -> torch.Tensor:
@@ -70,7 +70,7 @@ class StreamNMSE:
             self.loss[0] = (ss[:, 0] / ss[:, 1]).sum() / self.S
             self.loss[1] = (ss[:, 2] / ss[:, 3].clamp_min(1e-30)).sum() / self.S
             self.coef.copy_(loss_scale * 2.0 / (self.S * ss[:, 1]))
-            self.skip.fill_(0 if torch.isfinite(self.loss[0]) else 1)
+            self.skip.fill_(0.0 if torch.isfinite(self.loss[0]) else 1.0)
         return self.loss
 
     def grad(self, Y: torch.Tensor, label: torch.Tensor, out_dtype=torch.float32,

@@ -75,7 +75,7 @@ class FusedOptimizer:
     """Adam / AdamW / SGD-momentum over a FlatParamSpace, one kernel per step.
 
     ``prune_thr`` > 0 fuses on-chip gradient pruning (g *= |g| > thr) into the step,
-    ``grad_scale`` fuses gradient averaging; ``skip`` (device int) makes the step a no-op.
+    ``grad_scale`` fuses gradient averaging; ``skip`` (device fp32, nonzero = skip) makes the step a no-op.
     """
 
     def __init__(self, space: FlatParamSpace, kind: str = "adam", lr: float = 1e-3, betas=(0.9, 0.999),
@@ -134,7 +134,7 @@ class FusedOptimizer:
     @torch.no_grad()
     def _step_host(self, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
         """CPU path (same math as optim.hip; the CPU has no HIP kernels)."""
-        if skip is not None and int(skip.item()) != 0:
+        if skip is not None and float(skip.item()) != 0.0:
             return
         s = self.space
         p, g = s.flat, s.grad

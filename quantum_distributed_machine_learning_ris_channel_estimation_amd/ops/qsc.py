@@ -71,7 +71,7 @@ class QSCStepHIP:
         self.qslab = torch.empty(self.qrows, 2 * self.n * self.L, **f32)
         self._pre_fwd = nat.fn(L, "qd_qsc_pre_fwd", [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._pre_bwd = nat.fn(L, "qd_qsc_pre_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
-        self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p])
+        self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
         if self.big:
             self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
             self._qb = nat.fn(L, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
@@ -89,8 +89,10 @@ class QSCStepHIP:
         return w
 
     @torch.no_grad()
-    def __call__(self, x: torch.Tensor, labels: torch.Tensor, loss_acc: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """x (B, 2, H, W) fp32 contiguous, labels (B,) int64.  Accumulates grads; returns loss (1,)."""
+    def __call__(self, x: torch.Tensor, labels: torch.Tensor, loss_acc: Optional[torch.Tensor] = None,
+                 skip: Optional[torch.Tensor] = None, skip_add: bool = False) -> torch.Tensor:
+        """x (B, 2, H, W) fp32 contiguous, labels (B,) int64.  Accumulates grads; returns loss (1,).
+        ``skip`` (fp32 (1,)): set (or, with skip_add, incremented) to 1 if the loss is not finite."""
         m, sp = self.m, self.space
         B, n, L = self.B, self.n, self.L
         assert x.shape[0] == B and x.is_contiguous() and labels.dtype == torch.int64
@@ -106,7 +108,8 @@ class QSCStepHIP:
         cls = m.classifier
         nat.check(self._head(nat.ptr(self.E), nat.ptr(cls.weight), nat.ptr(cls.bias), nat.ptr(labels),
                              nat.ptr(self.dE), nat.ptr(cls.weight.grad), nat.ptr(cls.bias.grad), nat.ptr(self.loss),
-                             nat.ptr(loss_acc) if loss_acc is not None else None, B, n, self.C, st), "qsc_head")
+                             nat.ptr(loss_acc) if loss_acc is not None else None,
+                             nat.ptr(skip) if skip is not None else None, int(skip_add), B, n, self.C, st), "qsc_head")
         nat.check(self._qb(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.dE), nat.ptr(self.dang),
                            nat.ptr(self.qslab), B, n, L, wgroup, *extra, st), "qsim_bwd")
         nat.check(self._rs(nat.ptr(self.qslab), nat.ptr(m.qlayer.weights.grad), self.qrows, 2 * n * L, 1.0, st),

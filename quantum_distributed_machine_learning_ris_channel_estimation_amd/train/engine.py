@@ -81,6 +81,12 @@ class HDCEModel:
                 bn = m.cnn[idx]
                 bn.running_mean = self.run_mean[k][e * 32:(e + 1) * 32]
                 bn.running_var = self.run_var[k][e * 32:(e + 1) * 32]
+        # all 3x3 num_batches_tracked counters are views of one int64 buffer: one add per step
+        self._nbt = torch.zeros(n_experts * len(BN_IDX), dtype=torch.long, device=self.device)
+        for e, m in enumerate(self.convs):
+            for k, idx in enumerate(BN_IDX):
+                m.cnn[idx].num_batches_tracked = self._nbt[e * len(BN_IDX) + k]
+        self.nbt = [self._nbt]
         self.momentum, self.eps = 0.1, 1e-5
         self._fc_w_lp = None
 
@@ -116,9 +122,7 @@ class HDCEModel:
 
     def count_batches(self, n: int) -> None:
         with torch.no_grad():
-            for m in self.convs:
-                for idx in BN_IDX:
-                    m.cnn[idx].num_batches_tracked += n
+            self._nbt.add_(n)
 
     # ------------------------------------------------------------------ forward pieces
     def pack_input(self, Yp: torch.Tensor) -> torch.Tensor:
@@ -214,11 +218,13 @@ class HDCEStep:
     csrc/hip/nmse.hip.  CPU / reference path: the same math through torch autograd."""
 
     def __init__(self, model: HDCEModel, n_users: int, batch: int, grad_hook: Optional[Callable] = None,
-                 hip: Optional[bool] = None):
+                 hip: Optional[bool] = None, skip: Optional[torch.Tensor] = None):
         self.m = model
         self.U, self.B = n_users, batch
         dev = model.device
         self.nmse = StreamNMSE(HDCEModel.row_stream(model.E, n_users, batch, dev), model.E * n_users)
+        if skip is not None:  # share a NaN-guard flag (e.g. one that rides in a gradient bucket)
+            self.nmse.skip = skip
         self.grad_hook = grad_hook  # called as grad_hook("fc") / grad_hook("conv") when buckets are final
         self.hip = (dev.type == "cuda") if hip is None else hip
         if self.hip:
@@ -303,10 +309,16 @@ class ClassifierStep:
     per forward call) through grouped quantum weights."""
 
     def __init__(self, model: nn.Module, n_streams: int, grad_hook: Optional[Callable] = None,
-                 space: Optional[FlatParamSpace] = None, batch_total: Optional[int] = None):
+                 space: Optional[FlatParamSpace] = None, batch_total: Optional[int] = None,
+                 skip: Optional[torch.Tensor] = None):
+        """``skip``: a shared NaN-guard flag another loss already set this step (it is incremented);
+        by default the step owns its flag (``self.skip``, overwritten every step)."""
         self.model = model
         self.S = n_streams
         self.grad_hook = grad_hook
+        dev0 = next(model.parameters()).device
+        self.skip_add = skip is not None
+        self.skip = skip if skip is not None else torch.zeros(1, device=dev0, dtype=torch.float32)
         self.hip = None
         dev = next(model.parameters()).device
         if isinstance(model, QSC_P128) and dev.type == "cuda" and space is not None and batch_total:
@@ -327,13 +339,18 @@ class ClassifierStep:
 
     def __call__(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         if self.hip is not None and x.shape[0] == self.hip.B:
-            loss = self.hip(x.contiguous(), labels)
+            loss = self.hip(x.contiguous(), labels, skip=self.skip, skip_add=self.skip_add)
             if self.grad_hook:
                 self.grad_hook("all")
             return loss
         out = self.forward(x)
         loss = F.nll_loss(out, labels)
         loss.backward()
+        bad = (~torch.isfinite(loss.detach())).float().reshape(1)
+        if self.skip_add:
+            self.skip.add_(bad)
+        else:
+            self.skip.copy_(bad)
         if self.grad_hook:
             self.grad_hook("all")
         return loss.detach()

@@ -71,10 +71,14 @@ class FlagshipTrainer:
                                    prune_thr=0.1 if cfg.use_gradient_pruning else 0.0)
         sp = self.hdce.space
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
-        # bucket "fc": 33.6 MB, ready first; bucket "small": conv + QSC grads, coalesced
-        self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "small": [sp.grad[:n_conv], self.qspace.grad]})
         self.hstep = HDCEStep(self.hdce, self.U, self.B)
-        self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B)
+        # NaN guard: the NMSE kernel sets the flag, the QSC head adds to it; it travels in the small
+        # bucket so every rank sees the same (summed) flag and skips -- or steps -- in lockstep
+        self.skip = self.hstep.skip
+        self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B, skip=self.skip)
+        # bucket "fc": 33.6 MB, ready first; bucket "small": conv + QSC grads + skip flag, coalesced
+        self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]],
+                                         "small": [sp.grad[:n_conv], self.qspace.grad, self.skip]})
         self.idx = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.perm = torch.randperm(self.store.n, device=dev)
         self.cursor = 0
@@ -108,8 +112,8 @@ class FlagshipTrainer:
 
     def _phase3(self) -> None:
         g = 1.0 / self.ctx.world
-        self.hopt.step(grad_scale=g, skip=self.hstep.skip)
-        self.qopt.step(grad_scale=g)
+        self.hopt.step(grad_scale=g, skip=self.skip)
+        self.qopt.step(grad_scale=g, skip=self.skip)
 
     def _step_body(self) -> None:
         self._phase1()

@@ -67,6 +67,11 @@ class Y2HRunner:
     def _context(self):
         if self.ctx is None:
             self.ctx = init_distributed(self.device)
+            # same seed on every rank: identical init (rank 0 broadcasts anyway); data order differs per rank
+            torch.manual_seed(self.seed)
+            np.random.seed(self.seed % (2 ** 32))
+            if self.deterministic:
+                torch.use_deterministic_algorithms(True, warn_only=True)
         return self.ctx
 
     def _log(self) -> MetricsLogger:
@@ -184,8 +189,11 @@ class Y2HRunner:
         E, U, B = self.n_scenarios, self.n_users, self.batch_size_DML
         sp = model.space
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
-        buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "conv": [sp.grad[:n_conv]]})
-        step = HDCEStep(model, U, B, grad_hook=buckets.launch)
+        step = HDCEStep(model, U, B)
+        skip = step.skip if self.nan_guard else None
+        # the NaN-guard flag rides in the conv bucket: all ranks skip (or step) together
+        buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "conv": [sp.grad[:n_conv]] + ([skip] if skip is not None else [])})
+        step.grad_hook = buckets.launch
         loss_acc = torch.zeros(2, device=ctx.device)
         last_loss = torch.zeros(2, device=ctx.device)
         static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
@@ -195,20 +203,37 @@ class Y2HRunner:
             sp.zero_grad()
             Yp, HL, HP = tr.gather(idx)
             b = idx.numel()
-            hs = step if b == B else HDCEStep(model, U, b, grad_hook=buckets.launch)
+            hs = step if b == B else HDCEStep(model, U, b, grad_hook=buckets.launch, skip=skip)
             loss = hs(Yp.view(E, U, b, *Yp.shape[2:]), HL.view(E, U, b, -1), HP.view(E, U, b, -1))
             last_loss.copy_(loss)
             loss_acc.add_(loss)
             buckets.wait()
-            opt.step(grad_scale=gscale, skip=hs.skip)
+            opt.step(grad_scale=gscale, skip=skip)
 
         graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
         sampler = DeviceSampler(tr.n, B, ctx.device, self.seed, ctx.rank)
         d = ck.ckpt_dir(self.workspace, self.Pilot_num) if ctx.is_main else None
         log = self._log()
         best_nmse = 1000.0
+        resume_path = os.path.join(ck.ckpt_dir(self.workspace, self.Pilot_num), f"HDCE_{B}_{self.SNRdb}dB_resume.pth")
+        start = 0
+        if self.resume:
+            st = ck.load_resume(resume_path)
+            if st is not None:
+                ck.load_into(sp.flat, st["flat"])
+                opt.load_state_dict(st["optimizer"])
+                for t, v in zip(model.run_mean + model.run_var, st["run_mean"] + st["run_var"]):
+                    ck.load_into(t, v)
+                for t, v in zip(model.nbt, st["nbt"]):
+                    ck.load_into(t, v)
+                best_nmse, start = float(st["best"]), int(st["epoch"]) + 1
+                self.train_HDCE_losses[:] = st["train_losses"].tolist()
+                self.val_HDCE_nmse[:] = st["val_nmse"].tolist()
+                if ctx.world == 1:
+                    ck.set_rng_state(st["rng"])
+                self._print(f"Resumed HDCE from {resume_path} at epoch {start}")
         self._print("Everything prepared well, start to train HDCE Conv+Linear...")
-        for epoch in range(self.n_epochs):
+        for epoch in range(start, self.n_epochs):
             self._print(f"HDCE Conv+Linear:SNR: {self.SNRdb} Epoch [{epoch}]/[{self.n_epochs}] learning rate: "
                         f"{opt.lr:.4e}", time.strftime("%Y-%m-%d %H:%M:%S", time.localtime()))
             model.train()
@@ -258,10 +283,12 @@ class Y2HRunner:
                 if opt.lr < self.lr_threshold:
                     opt.set_lr(self.lr_threshold)
             if ctx.is_main:
-                ck.save_resume(os.path.join(d, f"HDCE_{B}_{self.SNRdb}dB_resume.pth"), epoch=epoch,
-                               best=best_nmse, optimizer=opt.state_dict(), flat=sp.flat.cpu(),
-                               run_mean=[t.cpu() for t in model.run_mean], run_var=[t.cpu() for t in model.run_var],
-                               rng=ck.rng_state())
+                ck.save_resume(resume_path, epoch=epoch, best=best_nmse, optimizer=opt.state_dict(),
+                               flat=sp.flat.cpu(), run_mean=[t.cpu() for t in model.run_mean],
+                               run_var=[t.cpu() for t in model.run_var], nbt=[t.cpu() for t in model.nbt],
+                               train_losses=torch.tensor(self.train_HDCE_losses, dtype=torch.float64),
+                               val_nmse=torch.tensor(self.val_HDCE_nmse, dtype=torch.float64), rng=ck.rng_state())
+            _maybe_fault(epoch)
         self.hdce_model = model
         return model
 
@@ -292,7 +319,8 @@ class Y2HRunner:
         return float(loss_sum[0]), float(loss_sum[1] / loss_sum[2])
 
     def _train_classifier(self, model, kind: str, opt_name: str, wd: float, prune_thr: float,
-                          on_epoch, histories: Tuple[List, List, List]):
+                          on_epoch, histories: Tuple[List, List, List], extra: Optional[Dict] = None):
+        """``extra``: small mutable trainer state (e.g. best accuracy) saved in the resume file."""
         ctx = self._context()
         tr, va = self.device_stores()
         model = model.to(ctx.device)
@@ -303,8 +331,10 @@ class Y2HRunner:
             kw["weight_decay"] = wd
         opt = make_optimizer(space, opt_name, self.lr, **kw)
         S, B = tr.n_streams, self.batch_size_DML
-        buckets = GradBuckets(ctx, {"all": [space.grad]})
-        cstep = ClassifierStep(model, S, grad_hook=buckets.launch, space=space, batch_total=S * B)
+        cstep = ClassifierStep(model, S, space=space, batch_total=S * B)
+        skip = cstep.skip if self.nan_guard else None
+        buckets = GradBuckets(ctx, {"all": [space.grad] + ([skip] if skip is not None else [])})
+        cstep.grad_hook = buckets.launch
         loss_acc = torch.zeros(1, device=ctx.device)
         static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
         gscale = 1.0 / ctx.world
@@ -317,14 +347,31 @@ class Y2HRunner:
             loss = cstep(x, labels)
             loss_acc.add_(loss)
             buckets.wait()
-            opt.step(grad_scale=gscale)
+            opt.step(grad_scale=gscale, skip=skip)
 
         graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
         sampler = DeviceSampler(tr.n, B, ctx.device, self.seed + 17, ctx.rank)
         log = self._log()
         train_losses, val_losses, val_accs = histories
-        train_losses.clear()
-        for epoch in range(self.n_epochs):
+        for h in histories:
+            h.clear()
+        extra = extra if extra is not None else {}
+        resume_path = os.path.join(ck.ckpt_dir(self.workspace, self.Pilot_num),
+                                   f"{kind.upper()}_{B}_{self.SNRdb}dB_resume.pth")
+        start = 0
+        if self.resume:
+            st = ck.load_resume(resume_path)
+            if st is not None:
+                ck.load_into(space.flat, st["flat"])
+                opt.load_state_dict(st["optimizer"])
+                for h, v in zip(histories, st["histories"]):
+                    h.extend(v.tolist())
+                extra.update({k: float(v) for k, v in st["extra"].items()})
+                start = int(st["epoch"]) + 1
+                if ctx.world == 1:
+                    ck.set_rng_state(st["rng"])
+                self._print(f"Resumed {kind.upper()} from {resume_path} at epoch {start}")
+        for epoch in range(start, self.n_epochs):
             model.train()
             sampler.set_epoch(epoch)
             loss_acc.zero_()
@@ -356,10 +403,16 @@ class Y2HRunner:
             log.log(kind=f"{kind}_epoch", epoch=epoch, loss=avg, val_loss=vl, val_acc=acc, lr=opt.lr,
                     samples_per_sec=nb * B * S * ctx.world / max(dt, 1e-9))
             on_epoch(epoch, acc, model)
+            if ctx.is_main:
+                ck.save_resume(resume_path, epoch=epoch, flat=space.flat.cpu(), optimizer=opt.state_dict(),
+                               histories=[torch.tensor(h, dtype=torch.float64) for h in histories],
+                               extra={k: torch.tensor(float(v)) for k, v in extra.items()}, rng=ck.rng_state())
+            _maybe_fault(epoch)
         return model
 
     def train_QSC_P128(self):
         self._sync_cfg()
+        self._context()  # seeds before the model is built
         model = QSC_P128(self.n_qubits, self.n_layers, self.n_classes, use_quantumnat=self.use_quantumnat,
                          use_gradient_pruning=self.use_gradient_pruning, pilot_num=self.Pilot_num,
                          backend=None if self.backend == "auto" else self.backend, noise_level=self.noise_level,
@@ -381,12 +434,14 @@ class Y2HRunner:
 
         prune = self.gradient_threshold if self.use_gradient_pruning else 0.0
         self.qsc_model = self._train_classifier(model, "qsc", "adamw", self.qsc_weight_decay, prune, on_epoch,
-                                                (self.train_QSC_losses, self.val_QSC_losses, self.val_QSC_accuracies))
+                                                (self.train_QSC_losses, self.val_QSC_losses, self.val_QSC_accuracies),
+                                                extra=state)
         return self.qsc_model
 
     def train_SC_P128(self):
         """Classical scenario classifier trainer (Test.py:69-73 expects its checkpoint)."""
         self._sync_cfg()
+        self._context()
         model = SC_P128(self.Pilot_num, self.n_classes)
         ctx = self._context()
         d = ck.ckpt_dir(self.workspace, self.Pilot_num) if ctx.is_main else None
@@ -406,6 +461,15 @@ class Y2HRunner:
         self.train_Conv_Linear_of_HDCE()
         self.train_SC_P128()
         self.train_QSC_P128()
+
+
+def _maybe_fault(epoch: int) -> None:
+    """Fault injection for the resume tests: QDML_FAULT_EPOCH=k hard-kills the process right after
+    epoch k's resume file is written (no cleanup, like a node loss)."""
+    k = os.environ.get("QDML_FAULT_EPOCH")
+    if k is not None and int(k) == epoch:
+        print(f"[fault injection] killing the process after epoch {epoch}", flush=True)
+        os._exit(75)
 
 
 def _capture_preserving(graphed: GraphedStep, state: List[torch.Tensor], static_idx: torch.Tensor,
