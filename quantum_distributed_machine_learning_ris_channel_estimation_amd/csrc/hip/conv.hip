@@ -223,9 +223,9 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const TIN* __restrict__ xi
 // exact register order conv3x3_kernel consumes (16-byte coalesced loads per lane).
 // dgrad = 1: transposed + spatially flipped (the data-gradient correlation).
 // ------------------------------------------------------------------------------------------
-__global__ void pack_weights_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, int E, int CIN, int KS,
-                                    int dgrad) {
-  const int lane = threadIdx.x, s = blockIdx.x, e = blockIdx.y;
+__device__ __forceinline__ void pack_weights_body(const float* __restrict__ w, uint16_t* __restrict__ out, int CIN,
+                                                  int KS, int dgrad, int s, int e) {
+  const int lane = threadIdx.x;
   const int hh = lane >> 5, col = lane & 31;
   uint16_t v8[8];
 #pragma unroll
@@ -242,6 +242,23 @@ __global__ void pack_weights_kernel(const float* __restrict__ w, uint16_t* __res
   uint4 pk = make_uint4(v8[0] | ((uint32_t)v8[1] << 16), v8[2] | ((uint32_t)v8[3] << 16),
                         v8[4] | ((uint32_t)v8[5] << 16), v8[6] | ((uint32_t)v8[7] << 16));
   *reinterpret_cast<uint4*>(out + (((size_t)e * KS + s) * 64 + lane) * 8) = pk;
+}
+
+__global__ void pack_weights_kernel(const float* __restrict__ w, uint16_t* __restrict__ out, int E, int CIN, int KS,
+                                    int dgrad) {
+  pack_weights_body(w, out, CIN, KS, dgrad, blockIdx.x, blockIdx.y);
+}
+
+// All packs of a step in one launch (weights only change at the optimizer step).
+struct PackJobs {
+  const float* w[8];
+  uint16_t* out[8];
+  int cin[8], ks[8], dgrad[8];
+};
+__global__ void pack_weights_multi_kernel(PackJobs jobs) {
+  const int j = blockIdx.z, s = blockIdx.x;
+  if (s >= jobs.ks[j]) return;
+  pack_weights_body(jobs.w[j], jobs.out[j], jobs.cin[j], jobs.ks[j], jobs.dgrad[j], s, blockIdx.y);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -572,6 +589,24 @@ static size_t fwd_smem(int cin, int H, int W) {
 QD_API int qd_conv_pack_weights(const float* w, uint16_t* out, int E, int cin, int dgrad, void* stream) {
   const int KS = dgrad ? 18 : (9 * cin + 15) / 16;
   hipLaunchKernelGGL(pack_weights_kernel, dim3(KS, E), dim3(64), 0, (hipStream_t)stream, w, out, E, cin, KS, dgrad);
+  return (int)hipGetLastError();
+}
+
+// n jobs (<= 8): w[j] fp32 (E, 32, cin[j], 3, 3) -> out[j] packed (dgrad[j] selects the dgrad order)
+QD_API int qd_conv_pack_weights_multi(int n, const float* const* w, uint16_t* const* out, const int* cin,
+                                      const int* dgrad, int E, void* stream) {
+  if (n < 1 || n > 8) return (int)hipErrorInvalidValue;
+  PackJobs jobs{};
+  int ksmax = 0;
+  for (int j = 0; j < n; ++j) {
+    jobs.w[j] = w[j];
+    jobs.out[j] = out[j];
+    jobs.cin[j] = cin[j];
+    jobs.dgrad[j] = dgrad[j];
+    jobs.ks[j] = dgrad[j] ? 18 : (9 * cin[j] + 15) / 16;
+    ksmax = jobs.ks[j] > ksmax ? jobs.ks[j] : ksmax;
+  }
+  hipLaunchKernelGGL(pack_weights_multi_kernel, dim3(ksmax, E, n), dim3(64), 0, (hipStream_t)stream, jobs);
   return (int)hipGetLastError();
 }
 

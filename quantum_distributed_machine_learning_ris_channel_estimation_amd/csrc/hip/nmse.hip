@@ -34,14 +34,15 @@ __device__ __forceinline__ float4 load4<uint16_t>(const uint16_t* p) {
 // One wave per row; 4 rows per 256-thread block.  out: (rows, 4) fp32.
 template <typename TY>
 __global__ void __launch_bounds__(256) row_sums_kernel(const TY* __restrict__ Y, const float* __restrict__ Lb,
-                                                       const float* __restrict__ Pf, float* __restrict__ out, int rows,
-                                                       int cols) {
+                                                       const float* __restrict__ Pf, const int* __restrict__ rowoff,
+                                                       float* __restrict__ out, int rows, int cols) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const TY* y = Y + (size_t)row * cols;
-  const float* l = Lb + (size_t)row * cols;
-  const float* pf = Pf ? Pf + (size_t)row * cols : nullptr;
+  const size_t lrow = rowoff ? (size_t)rowoff[row] : (size_t)row;  // labels read in place from the store
+  const float* l = Lb + lrow * cols;
+  const float* pf = Pf ? Pf + lrow * cols : nullptr;
   float e = 0.f, pw = 0.f, ep = 0.f, pp = 0.f;
   for (int c = lane * 4; c < cols; c += 256) {
     const float4 yv = load4<TY>(y + c);
@@ -67,22 +68,61 @@ __global__ void __launch_bounds__(256) row_sums_kernel(const TY* __restrict__ Y,
 }
 
 // Per-stream reduction (rows in index order -> deterministic).  stream_sums: (S,4).
-__global__ void __launch_bounds__(256) stream_sums_kernel(const float* __restrict__ rowsums,
-                                                          const int* __restrict__ row_stream, float* __restrict__ ss,
-                                                          int rows, int S) {
-  __shared__ float red[4];
-  for (int s = 0; s < S; ++s) {
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int r = threadIdx.x; r < rows; r += 256) {
-      if (row_stream[r] != s) continue;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] += rowsums[(size_t)r * 4 + k];
+__global__ void __launch_bounds__(1024) stream_sums_kernel(const float* __restrict__ rowsums,
+                                                           const int* __restrict__ row_stream, float* __restrict__ ss,
+                                                           int rows, int S) {
+  const int s = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  for (int r = lane; r < rows; r += 64) {
+    if (row_stream[r] != s) continue;
+    const float4 v = *reinterpret_cast<const float4*>(rowsums + (size_t)r * 4);
+    a0 += v.x;
+    a1 += v.y;
+    a2 += v.z;
+    a3 += v.w;
+  }
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  a3 = wave_sum(a3);
+  if (lane == 0) *reinterpret_cast<float4*>(ss + s * 4) = make_float4(a0, a1, a2, a3);
+}
+
+// Fused stream reduction + finalize: one wave per stream sums its rows' partials in a fixed order
+// (deterministic), then thread 0 finalises.  blockDim = 64 * S (S <= 16).
+__global__ void __launch_bounds__(1024) stream_reduce_finalize_kernel(const float* __restrict__ rowsums,
+                                                                      const int* __restrict__ row_stream,
+                                                                      float* __restrict__ ss, float* __restrict__ loss,
+                                                                      float* __restrict__ coef, float* __restrict__ skip,
+                                                                      int rows, int S, float loss_scale) {
+  const int s = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  for (int r = lane; r < rows; r += 64) {
+    if (row_stream[r] != s) continue;
+    const float4 v = *reinterpret_cast<const float4*>(rowsums + (size_t)r * 4);
+    a0 += v.x;
+    a1 += v.y;
+    a2 += v.z;
+    a3 += v.w;
+  }
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  a3 = wave_sum(a3);
+  if (lane == 0) *reinterpret_cast<float4*>(ss + s * 4) = make_float4(a0, a1, a2, a3);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f, lp = 0.f;
+    for (int k = 0; k < S; ++k) {
+      const float den = ss[k * 4 + 1];
+      l += ss[k * 4 + 0] / den;
+      const float denp = ss[k * 4 + 3];
+      lp += denp > 0.f ? ss[k * 4 + 2] / denp : 0.f;
+      coef[k] = loss_scale * 2.f / ((float)S * den);
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float t = block_sum<256>(a[k], red);
-      if (threadIdx.x == 0) ss[s * 4 + k] = t;
-    }
+    loss[0] = l / (float)S;
+    loss[1] = lp / (float)S;
+    if (skip) *skip = isfinite(loss[0]) ? 0.f : 1.f;
   }
 }
 
@@ -106,14 +146,16 @@ __global__ void finalize_kernel(const float* __restrict__ ss, float* __restrict_
 template <typename TY, typename TD>
 __global__ void __launch_bounds__(256) grad_kernel(const TY* __restrict__ Y, const float* __restrict__ Lb,
                                                    const float* __restrict__ coef, const int* __restrict__ row_stream,
-                                                   TD* __restrict__ dY, int rows, int cols) {
+                                                   const int* __restrict__ rowoff, TD* __restrict__ dY, int rows,
+                                                   int cols) {
   const long n4 = (long)rows * cols / 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const long e = i * 4;
     const int r = (int)(e / cols);
     const float c = coef[row_stream[r]];
     const float4 yv = load4<TY>(Y + e);
-    const float4 lv = *reinterpret_cast<const float4*>(Lb + e);
+    const size_t le = rowoff ? (size_t)rowoff[r] * cols + (e - (long)r * cols) : (size_t)e;
+    const float4 lv = *reinterpret_cast<const float4*>(Lb + le);
     const float g0 = c * (yv.x - lv.x), g1 = c * (yv.y - lv.y), g2 = c * (yv.z - lv.z), g3 = c * (yv.w - lv.w);
     if constexpr (std::is_same<TD, float>::value) {
       *reinterpret_cast<float4*>(dY + e) = make_float4(g0, g1, g2, g3);
@@ -133,22 +175,33 @@ __global__ void __launch_bounds__(256) grad_kernel(const TY* __restrict__ Y, con
 
 using namespace qd::nmse;
 
-// y_bf16: 1 if Y is bf16 else fp32.  perf may be null.
-QD_API int qd_nmse_row_sums(const void* Y, int y_bf16, const float* label, const float* perf, float* rowsums, int rows,
-                            int cols, void* stream) {
+// y_bf16: 1 if Y is bf16 else fp32.  perf may be null.  rowoff (nullable): label/perf row of
+// output row r (labels gathered in place from the dataset store).
+QD_API int qd_nmse_row_sums(const void* Y, int y_bf16, const float* label, const float* perf, const int* rowoff,
+                            float* rowsums, int rows, int cols, void* stream) {
   if (cols % 4) return (int)hipErrorInvalidValue;
   dim3 grid((rows + 3) / 4);
   if (y_bf16)
     hipLaunchKernelGGL(row_sums_kernel<uint16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const uint16_t*)Y, label,
-                       perf, rowsums, rows, cols);
+                       perf, rowoff, rowsums, rows, cols);
   else
     hipLaunchKernelGGL(row_sums_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)Y, label, perf,
-                       rowsums, rows, cols);
+                       rowoff, rowsums, rows, cols);
   return (int)hipGetLastError();
 }
 
 QD_API int qd_nmse_stream_sums(const float* rowsums, const int* row_stream, float* ss, int rows, int S, void* stream) {
-  hipLaunchKernelGGL(stream_sums_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, rowsums, row_stream, ss, rows, S);
+  if (S < 1 || S > 16) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stream_sums_kernel, dim3(1), dim3(64 * S), 0, (hipStream_t)stream, rowsums, row_stream, ss, rows,
+                     S);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_nmse_reduce_finalize(const float* rowsums, const int* row_stream, float* ss, float* loss, float* coef,
+                                   float* skip, int rows, int S, float loss_scale, void* stream) {
+  if (S < 1 || S > 16) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stream_reduce_finalize_kernel, dim3(1), dim3(64 * S), 0, (hipStream_t)stream, rowsums, row_stream,
+                     ss, loss, coef, skip, rows, S, loss_scale);
   return (int)hipGetLastError();
 }
 
@@ -159,13 +212,14 @@ QD_API int qd_nmse_finalize(const float* ss, float* loss, float* coef, float* sk
 }
 
 QD_API int qd_nmse_grad(const void* Y, int y_bf16, const float* label, const float* coef, const int* row_stream,
-                        void* dY, int dy_bf16, int rows, int cols, void* stream) {
+                        const int* rowoff, void* dY, int dy_bf16, int rows, int cols, void* stream) {
+  if (cols % 4) return (int)hipErrorInvalidValue;
   long n4 = (long)rows * cols / 4;
   int grid = (int)((n4 + 255) / 256);
   if (grid > 4096) grid = 4096;
   hipStream_t st = (hipStream_t)stream;
 #define QD_G(TY, TD) hipLaunchKernelGGL((grad_kernel<TY, TD>), dim3(grid), dim3(256), 0, st, (const TY*)Y, label, coef, \
-                                        row_stream, (TD*)dY, rows, cols)
+                                        row_stream, rowoff, (TD*)dY, rows, cols)
   if (y_bf16 && dy_bf16) QD_G(uint16_t, uint16_t);
   else if (y_bf16) QD_G(uint16_t, float);
   else if (dy_bf16) QD_G(float, uint16_t);

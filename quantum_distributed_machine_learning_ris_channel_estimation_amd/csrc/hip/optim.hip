@@ -11,7 +11,11 @@
 // read from DEVICE memory, so the launch can be captured once in a HIP graph and
 // replayed every step; `skip` (set by the loss kernel when the loss is not finite)
 // turns the step into a no-op without a host sync.  Gradient pruning and the DP
-// gradient scale (1/world) are fused into the same pass.
+// gradient scale (1/world) are fused into the same pass, and so are
+//   * the step-counter increment: the last workgroup to finish (device-wide done counter)
+//     bumps it, so a step is one launch, not two;
+//   * an optional bf16 "shadow" of a parameter range (the FC weight): the forward GEMM reads
+//     the shadow instead of casting 8.4 M fp32 weights every step.
 #include "common.h"
 
 namespace qd {
@@ -22,12 +26,48 @@ struct AdamArgs {
   int decoupled;  // 1 = AdamW
 };
 
+struct Shadow {
+  uint16_t* out;  // bf16 copy of p[lo, hi) (lo, hi multiples of 4), or null
+  long lo, hi;
+};
+
+// Called by every thread at the end of the kernel: the last workgroup to get here increments the
+// step counter and re-arms the done counter.  Every workgroup read *step at its start, before it
+// arrives, so no workgroup can observe the increment of the step it is computing.
+__device__ __forceinline__ void tick_if_last(float* step, unsigned int* done) {
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned int prev = atomicAdd(done, 1u);
+    last = (prev == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    *step += 1.f;
+    *done = 0u;
+    __threadfence();
+  }
+}
+
+__device__ __forceinline__ void store_shadow(const Shadow& sh, long i0, float4 v) {
+  if (sh.out != nullptr && i0 >= sh.lo && i0 < sh.hi) {
+    ushort4 h;
+    h.x = f32_to_bf16(v.x);
+    h.y = f32_to_bf16(v.y);
+    h.z = f32_to_bf16(v.z);
+    h.w = f32_to_bf16(v.w);
+    *reinterpret_cast<ushort4*>(sh.out + (i0 - sh.lo)) = h;
+  }
+}
+
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n,
-                                                   const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr,
+                                                   const float* __restrict__ lr_ptr, const float* step_ptr,
                                                    const float* __restrict__ skip, unsigned int* __restrict__ pruned,
-                                                   AdamArgs a) {
-  if (skip != nullptr && *skip != 0.f) return;
+                                                   AdamArgs a, float* __restrict__ step_out,
+                                                   unsigned int* __restrict__ done, Shadow sh) {
+  if (skip != nullptr && *skip != 0.f) return;  // uniform across the grid: nobody ticks
   const float lr = *lr_ptr;
   const float t = *step_ptr + 1.f;  // step about to be taken
   const float bc1 = 1.f - __powf(a.beta1, t);
@@ -57,6 +97,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         ga[j] = gj;
       }
       *reinterpret_cast<float4*>(p + i0) = pp;
+      store_shadow(sh, i0, pp);
       *reinterpret_cast<float4*>(m + i0) = mm;
       *reinterpret_cast<float4*>(v + i0) = vv;
       if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
@@ -72,6 +113,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         const float denom = sqrtf(v[i]) * rbc2 + a.eps;
         p[i] = pj - step_size * m[i] / denom;
         g[i] = gj;
+        if (sh.out != nullptr && i >= sh.lo && i < sh.hi) sh.out[i - sh.lo] = f32_to_bf16(p[i]);
       }
     }
   }
@@ -80,12 +122,14 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     float c = wave_sum((float)cnt);
     if ((threadIdx.x & 63) == 0 && c > 0.f) atomicAdd(pruned, (unsigned int)c);
   }
+  tick_if_last(step_out, done);
 }
 
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
                                                   float* __restrict__ buf, long n, const float* __restrict__ lr_ptr,
-                                                  const float* __restrict__ step_ptr, const float* __restrict__ skip,
-                                                  float momentum, float weight_decay, float grad_scale) {
+                                                  const float* step_ptr, const float* __restrict__ skip,
+                                                  float momentum, float weight_decay, float grad_scale,
+                                                  float* __restrict__ step_out, unsigned int* __restrict__ done) {
   if (skip != nullptr && *skip != 0.f) return;
   const float lr = *lr_ptr;
   const bool first = *step_ptr < 0.5f;
@@ -95,10 +139,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
     buf[i] = b;
     p[i] -= lr * b;
   }
-}
-
-__global__ void step_tick_kernel(float* step, const float* skip) {
-  if (skip == nullptr || *skip == 0.f) *step += 1.f;
+  tick_if_last(step_out, done);
 }
 
 inline int grid_for(long n) {
@@ -113,21 +154,26 @@ inline int grid_for(long n) {
 
 using namespace qd::optim;
 
+// done: device uint32 counter, zero-initialised once (re-armed by the kernel).
+// shadow: optional bf16 copy of p[lo, hi) (lo, hi multiples of 4), written with the update.
 QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const float* skip,
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
-                        float grad_scale, float prune_thr, void* stream) {
+                        float grad_scale, float prune_thr, unsigned int* done, uint16_t* shadow, long shadow_lo,
+                        long shadow_hi, void* stream) {
+  if (n <= 0 || done == nullptr || (shadow && ((shadow_lo | shadow_hi) & 3))) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   AdamArgs a{beta1, beta2, eps, weight_decay, grad_scale, prune_thr, decoupled};
-  if (n > 0) hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a);
-  hipLaunchKernelGGL(step_tick_kernel, dim3(1), dim3(1), 0, st, step, skip);
+  Shadow sh{shadow, shadow_lo, shadow_hi};
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step,
+                     done, sh);
   return (int)hipGetLastError();
 }
 
 QD_API int qd_sgd_step(float* p, float* g, float* buf, long n, const float* lr, float* step, const float* skip,
-                       float momentum, float weight_decay, float grad_scale, void* stream) {
+                       float momentum, float weight_decay, float grad_scale, unsigned int* done, void* stream) {
+  if (n <= 0 || done == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  if (n > 0) hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, buf, n, lr, step, skip, momentum,
-                                weight_decay, grad_scale);
-  hipLaunchKernelGGL(step_tick_kernel, dim3(1), dim3(1), 0, st, step, skip);
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, buf, n, lr, step, skip, momentum,
+                     weight_decay, grad_scale, step, done);
   return (int)hipGetLastError();
 }

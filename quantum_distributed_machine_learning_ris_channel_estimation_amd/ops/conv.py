@@ -4,7 +4,7 @@ Reference module: ``Conv_P128.cnn`` (Estimators_QuantumNAT_onchipQNN.py:246-261)
 [Conv2d 3x3 no-bias -> BatchNorm2d(32) -> ReLU], one instance per scenario expert.
 
 ``ConvStackHIP`` runs all experts for a whole 9-stream step with 3 forward conv launches
-(+3 tiny statistics launches) and 3 x (BN reduce, BN finalize, dgrad, wgrad, slab sum)
+(+3 tiny statistics launches, +1 weight-pack launch) and 3 x (BN reduce, BN finalize, dgrad, wgrad, slab sum)
 backward launches; every buffer is allocated once, so the whole step is capturable in a
 HIP graph.  Gradients are written straight into the model's flat gradient buffer.
 """
@@ -64,15 +64,16 @@ class ConvStackHIP:
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p])
         self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
-        self._pack = nat.fn(L, "qd_conv_pack_weights", [_p, _p, _i, _i, _i, _p])
+        self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
 
-    def pack_weights(self, st, dgrad: bool) -> None:
-        for k in range(3):
-            if dgrad and k == 0:
-                continue
-            out = self.wpk_t[k] if dgrad else self.wpk[k]
-            nat.check(self._pack(nat.ptr(self.m.conv_w[k]), nat.ptr(out), self.E, self.cins[k], int(dgrad), st),
-                      "conv_pack_weights")
+    def pack_weights(self, st) -> None:
+        """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch."""
+        jobs = [(k, 0) for k in range(3)] + [(k, 1) for k in (1, 2)]
+        w = (ctypes.c_void_p * 8)(*[nat.ptr(self.m.conv_w[k]) for k, _ in jobs])
+        out = (ctypes.c_void_p * 8)(*[nat.ptr(self.wpk_t[k] if d else self.wpk[k]) for k, d in jobs])
+        cin = (ctypes.c_int * 8)(*[self.cins[k] for k, _ in jobs])
+        dg = (ctypes.c_int * 8)(*[d for _, d in jobs])
+        nat.check(self._packm(len(jobs), w, out, cin, dg, self.E, st), "conv_pack_weights")
 
     # --------------------------------------------------------------------- forward
     def forward(self, x1: torch.Tensor, training: bool) -> torch.Tensor:
@@ -80,7 +81,7 @@ class ConvStackHIP:
         m, st = self.m, nat.stream_ptr(x1.device)
         assert x1.shape == (self.N, 2 * self.E, self.H, self.W) and x1.dtype == torch.float32 and x1.is_contiguous()
         self.x1 = x1
-        self.pack_weights(st, dgrad=False)
+        self.pack_weights(st)
         inp, st_prev = x1, None
         for k in range(3):
             nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
@@ -98,7 +99,6 @@ class ConvStackHIP:
     def backward(self, dh3: torch.Tensor) -> None:
         """dh3: dL/dh3 as (N*E, 32*H*W) (bf16 or fp32).  Accumulates conv/BN grads into the flat grad."""
         m, st = self.m, nat.stream_ptr(dh3.device)
-        self.pack_weights(st, dgrad=True)
         dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
         for k in (2, 1, 0):
             z, bst = self.z[k], self.st[k]

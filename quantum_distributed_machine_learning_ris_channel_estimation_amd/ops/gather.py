@@ -1,0 +1,54 @@
+"""One-launch batch assembly from the HBM-resident dataset (csrc/hip/gather.hip).
+
+Reference: the per-step host-side packing + H2D copies of every stream
+(Runner_P128_QuantumNAT_onchipQNN.py:104-108, R:181-199, R:344-346).
+
+``StepGather(E, U, B, H, W)`` owns static buffers (graph-capturable) and, for a shuffled
+index vector ``idx`` (B,) over a ``DMLStore``, fills
+  x1      (U*B, E*2, H, W)  HDCE grouped-conv input
+  xq      (S*B, 2, H, W)    classifier input, stream-major (if ``with_classifier``)
+  rowoff  (U*B*E,) int32    store row of every FC output row (labels are read in place)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .. import _native as nat
+
+_p, _i, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+
+
+class StepGather:
+    def __init__(self, E: int, U: int, B: int, H: int, W: int, device, with_classifier: bool = True):
+        self.E, self.U, self.B, self.H, self.W = E, U, B, H, W
+        self.S = E * U
+        dev = torch.device(device)
+        self.x1 = torch.empty(U * B, E * 2, H, W, device=dev)
+        self.xq = torch.empty(self.S * B, 2, H, W, device=dev) if with_classifier else None
+        self.rowoff = torch.empty(U * B * E, device=dev, dtype=torch.int32)
+        self.plane = 2 * H * W
+
+    def __call__(self, store, idx: torch.Tensor) -> None:
+        Yp, HL = store.Yp, store.Hlabel
+        S, N = Yp.shape[:2]
+        assert S == self.S and idx.shape == (self.B,) and idx.dtype == torch.int64
+        assert Yp.dtype == torch.float32 and Yp[0, 0].is_contiguous() and Yp.stride(1) == self.plane
+        cols = HL.shape[-1]
+        assert HL.stride(1) == cols and HL.stride(0) % cols == 0 and store.Hperf.stride() == HL.stride()
+        if Yp.is_cuda:
+            f = nat.fn(nat.hip_lib(), "qd_gather_step", [_p, _p, _l, _p, _p, _p, _l, _i, _i, _i, _i, _p])
+            nat.check(f(nat.ptr(idx), nat.ptr(Yp), Yp.stride(0), nat.ptr(self.x1),
+                        nat.ptr(self.xq) if self.xq is not None else None, nat.ptr(self.rowoff), HL.stride(0) // cols,
+                        self.E, self.U, self.B, self.plane, nat.stream_ptr(Yp.device)), "gather_step")
+            return
+        E, U, B = self.E, self.U, self.B
+        g = Yp.index_select(1, idx)                                   # (S, B, 2, H, W), s = e*U + u
+        self.x1.copy_(g.view(E, U, B, 2, self.H, self.W).permute(1, 2, 0, 3, 4, 5)
+                      .reshape(U * B, E * 2, self.H, self.W))
+        if self.xq is not None:
+            self.xq.copy_(g.reshape(self.S * B, 2, self.H, self.W))
+        s = (torch.arange(E).view(1, 1, E) * U + torch.arange(U).view(U, 1, 1)).to(idx.device)
+        off = s * (HL.stride(0) // cols) + idx.view(1, B, 1)
+        self.rowoff.copy_(off.expand(U, B, E).reshape(-1).to(torch.int32))

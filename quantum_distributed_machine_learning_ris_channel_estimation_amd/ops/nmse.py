@@ -10,6 +10,10 @@ and returns dY = dloss/dY without autograd (the HDCE engine feeds it straight in
 the FC backward).  The row->stream map is a device int32 tensor, so any row order
 (e.g. the expert-interleaved order of the grouped estimator) works.
 
+Labels can be read in place from the dataset store: set ``rowoff`` (int32, one store row per
+output row, produced by ops/gather.py) and pass the (S, N, cols) label/perf stores instead of
+(rows, cols) tensors -- the kernels index through it, so no permuted label copy is ever made.
+
 In data-parallel runs ``sums()`` + all-reduce + ``finalize()`` give the GLOBAL NMSE
 (sum of errors over sum of powers across ranks), never a mean of per-rank ratios.
 """
@@ -38,26 +42,65 @@ class StreamNMSE:
         self.coef = torch.zeros(n_streams, device=dev)
         self.skip = torch.zeros(1, device=dev, dtype=torch.float32)  # NaN guard flag (all-reduced in DP)
         self._rs_long = self.row_stream.long()
+        self.rowoff: Optional[torch.Tensor] = None
+
+    def _labels(self, t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """Host-path view of the labels in output-row order."""
+        if t is None or self.rowoff is None:
+            return t
+        # (S, N, cols) store, possibly a rank-shard view: rowoff = s * (stride0 / cols) + n
+        sr = t.stride(0) // self.cols
+        o = self.rowoff.long()
+        return t[o // sr, o % sr]
+
+    def _check_labels(self, t: torch.Tensor) -> None:
+        assert t.dtype == torch.float32 and t.shape[-1] == self.cols and t.stride(-1) == 1
+        if self.rowoff is None:
+            assert t.shape == (self.rows, self.cols) and t.is_contiguous()
+
+    def _row_sums_hip(self, Y, label, perf, st) -> None:
+        self._check_labels(label)
+        if perf is not None:
+            self._check_labels(perf)
+        f = nat.fn(nat.hip_lib(), "qd_nmse_row_sums", [_p, _i, _p, _p, _p, _p, _i, _i, _p])
+        nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label),
+                    nat.ptr(perf) if perf is not None else None,
+                    nat.ptr(self.rowoff) if self.rowoff is not None else None, nat.ptr(self.rowsums), self.rows,
+                    self.cols, st), "nmse_row_sums")
 
     def sums(self, Y: torch.Tensor, label: torch.Tensor, perf: Optional[torch.Tensor]) -> torch.Tensor:
-        assert Y.shape == (self.rows, self.cols) and label.dtype == torch.float32
+        assert Y.shape == (self.rows, self.cols)
         if Y.is_cuda:
             lib = nat.hip_lib()
             st = nat.stream_ptr(Y.device)
-            f = nat.fn(lib, "qd_nmse_row_sums", [_p, _i, _p, _p, _p, _i, _i, _p])
-            nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label),
-                        nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowsums), self.rows, self.cols, st),
-                      "nmse_row_sums")
+            self._row_sums_hip(Y, label, perf, st)
             g = nat.fn(lib, "qd_nmse_stream_sums", [_p, _p, _p, _i, _i, _p])
             nat.check(g(nat.ptr(self.rowsums), nat.ptr(self.row_stream), nat.ptr(self.ss), self.rows, self.S, st),
                       "nmse_stream_sums")
         else:
+            label, perf = self._labels(label), self._labels(perf)
             Yf = Y.float()
             rs = torch.stack([((Yf - label) ** 2).sum(1), (label ** 2).sum(1),
                               ((Yf - perf) ** 2).sum(1) if perf is not None else torch.zeros(self.rows),
                               (perf ** 2).sum(1) if perf is not None else torch.zeros(self.rows)], 1)
             self.ss.zero_().index_add_(0, self._rs_long, rs)
         return self.ss
+
+    def sums_finalize(self, Y: torch.Tensor, label: torch.Tensor, perf: Optional[torch.Tensor],
+                      loss_scale: float = 1.0) -> torch.Tensor:
+        """sums() + finalize() for a rank-local loss; on the GPU the stream reduction and the
+        finalisation are one launch."""
+        if not Y.is_cuda:
+            self.sums(Y, label, perf)
+            return self.finalize(loss_scale)
+        assert Y.shape == (self.rows, self.cols)
+        lib = nat.hip_lib()
+        st = nat.stream_ptr(Y.device)
+        self._row_sums_hip(Y, label, perf, st)
+        g = nat.fn(lib, "qd_nmse_reduce_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _f, _p])
+        nat.check(g(nat.ptr(self.rowsums), nat.ptr(self.row_stream), nat.ptr(self.ss), nat.ptr(self.loss),
+                    nat.ptr(self.coef), nat.ptr(self.skip), self.rows, self.S, loss_scale, st), "nmse_reduce_finalize")
+        return self.loss
 
     def finalize(self, loss_scale: float = 1.0) -> torch.Tensor:
         if self.ss.is_cuda:
@@ -78,12 +121,14 @@ class StreamNMSE:
         dY = out if out is not None else torch.empty(self.rows, self.cols, device=Y.device, dtype=out_dtype)
         if Y.is_cuda:
             lib = nat.hip_lib()
-            f = nat.fn(lib, "qd_nmse_grad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _p])
+            self._check_labels(label)
+            f = nat.fn(lib, "qd_nmse_grad", [_p, _i, _p, _p, _p, _p, _p, _i, _i, _i, _p])
             nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label), nat.ptr(self.coef),
-                        nat.ptr(self.row_stream), nat.ptr(dY), int(dY.dtype == torch.bfloat16), self.rows, self.cols,
+                        nat.ptr(self.row_stream), nat.ptr(self.rowoff) if self.rowoff is not None else None,
+                        nat.ptr(dY), int(dY.dtype == torch.bfloat16), self.rows, self.cols,
                         nat.stream_ptr(Y.device)), "nmse_grad")
         else:
-            dY.copy_(self.coef[self._rs_long][:, None] * (Y.float() - label))
+            dY.copy_(self.coef[self._rs_long][:, None] * (Y.float() - self._labels(label)))
         return dY
 
     def __call__(self, Y, label, perf=None, out_dtype=torch.float32) -> Tuple[torch.Tensor, torch.Tensor]:

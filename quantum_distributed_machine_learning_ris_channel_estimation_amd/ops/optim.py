@@ -93,6 +93,9 @@ class FusedOptimizer:
         self.lr_t = torch.full((1,), lr, device=dev, dtype=torch.float32)
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
         self.pruned = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.done = torch.zeros(1, device=dev, dtype=torch.int32)   # last-workgroup counter (step tick)
+        self.shadow: Optional[torch.Tensor] = None                    # bf16 copy of flat[lo:hi]
+        self.shadow_lo = self.shadow_hi = 0
         if kind == "sgd":
             self.buf = torch.zeros_like(space.flat)
         else:
@@ -101,6 +104,20 @@ class FusedOptimizer:
         self._lr_host = lr
         # torch.optim-like view for code that reads/writes param_groups[0]['lr']
         self.param_groups = [_LRGroup(self)]
+
+    def attach_shadow(self, lo: int, hi: int) -> torch.Tensor:
+        """Keep a bf16 copy of flat[lo:hi] up to date with every step (written by the update
+        kernel itself on the GPU).  Returns the shadow, initialised from the current weights."""
+        if lo % 4 or hi % 4:
+            raise ValueError("shadow bounds must be multiples of 4")
+        self.shadow_lo, self.shadow_hi = lo, hi
+        self.shadow = self.space.flat[lo:hi].to(torch.bfloat16)
+        return self.shadow
+
+    def refresh_shadow(self) -> None:
+        """Re-sync the shadow after the weights were changed outside step() (load, broadcast)."""
+        if self.shadow is not None:
+            self.shadow.copy_(self.space.flat[self.shadow_lo:self.shadow_hi])
 
     # ---------------------------------------------------------------- lr
     @property
@@ -119,17 +136,25 @@ class FusedOptimizer:
             st = nat.stream_ptr(s.flat.device)
             skp = nat.ptr(skip) if skip is not None else None
             if self.kind == "sgd":
-                f = nat.fn(lib, "qd_sgd_step", [_p, _p, _p, _l, _p, _p, _p, _f, _f, _f, _p])
+                f = nat.fn(lib, "qd_sgd_step", [_p, _p, _p, _l, _p, _p, _p, _f, _f, _f, _p, _p])
                 nat.check(f(nat.ptr(s.flat), nat.ptr(s.grad), nat.ptr(self.buf), s.numel, nat.ptr(self.lr_t),
-                            nat.ptr(self.step_t), skp, self.momentum, self.weight_decay, grad_scale, st), "sgd")
+                            nat.ptr(self.step_t), skp, self.momentum, self.weight_decay, grad_scale,
+                            nat.ptr(self.done), st), "sgd")
+                if self.shadow is not None:
+                    self.refresh_shadow()
             else:
-                f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f, _p])
+                f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
+                                                 _p, _p, _l, _l, _p])
                 nat.check(f(nat.ptr(s.flat), nat.ptr(s.grad), nat.ptr(self.m), nat.ptr(self.v), s.numel,
                             nat.ptr(self.lr_t), nat.ptr(self.step_t), skp, nat.ptr(self.pruned), self.betas[0],
                             self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
-                            self.prune_thr, st), "adam")
+                            self.prune_thr, nat.ptr(self.done),
+                            nat.ptr(self.shadow) if self.shadow is not None else None, self.shadow_lo,
+                            self.shadow_hi, st), "adam")
             return
         self._step_host(grad_scale, skip)
+        if self.shadow is not None:
+            self.refresh_shadow()
 
     @torch.no_grad()
     def _step_host(self, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
@@ -187,6 +212,7 @@ class FusedOptimizer:
         return d
 
     def load_state_dict(self, d: Dict) -> None:
+        self.refresh_shadow()
         self.set_lr(d["lr"])
         self.step_t.copy_(d["step"])
         if self.kind == "sgd":

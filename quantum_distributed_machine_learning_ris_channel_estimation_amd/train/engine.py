@@ -88,7 +88,26 @@ class HDCEModel:
                 m.cnn[idx].num_batches_tracked = self._nbt[e * len(BN_IDX) + k]
         self.nbt = [self._nbt]
         self.momentum, self.eps = 0.1, 1e-5
-        self._fc_w_lp = None
+        self.fc_shadow: Optional[torch.Tensor] = None  # bf16 FC weight+bias kept fresh by the optimizer
+
+    def attach_fc_shadow(self, opt) -> None:
+        """Let ``opt`` maintain a bf16 copy of the FC weight and bias (GPU, bf16 compute only)."""
+        if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16:
+            return
+        lo = self.space.offsets[self.space.names.index("CE.FC.weight")]
+        ob = self.space.offsets[self.space.names.index("CE.FC.bias")]
+        hi = ob + self.fc_b.numel()
+        sh = opt.attach_shadow(lo, hi + (-hi) % 4)
+        self.fc_shadow = sh
+        self._shadow_w = sh[:self.fc_w.numel()].view(self.fc_w.shape)
+        self._shadow_b = sh[ob - lo:ob - lo + self.fc_b.numel()]
+
+    def fc_weights_lp(self):
+        """(W, b) in the compute dtype: the optimizer-maintained shadow, or a fresh cast."""
+        if self.fc_shadow is not None:
+            return self._shadow_w, self._shadow_b
+        dt = self.compute_dtype
+        return self.fc_w.detach().to(dt), self.fc_b.detach().to(dt)
 
     # ------------------------------------------------------------------ params
     def _group_leaf(self, first_name: str) -> torch.Tensor:
@@ -244,16 +263,25 @@ class HDCEStep:
 
     # Phase 1: forward, fused NMSE, complete FC backward (FC grads final, dA ready).
     def forward_fc(self, Yp: torch.Tensor, HL: torch.Tensor, HP: torch.Tensor) -> torch.Tensor:
+        """From stream-major tensors Yp (E,U,B,2,H,W), HL/HP (E,U,B,2048)."""
+        self.nmse.rowoff = None
+        x1 = self.m.pack_input(Yp).float().contiguous()
+        return self._forward_fc(x1, HDCEModel.rows_from_streams(HL), HDCEModel.rows_from_streams(HP))
+
+    def forward_fc_gathered(self, g, store) -> torch.Tensor:
+        """From a filled ops.gather.StepGather: conv input g.x1, labels read in place from the
+        store through g.rowoff (no permuted label copies)."""
+        self.nmse.rowoff = g.rowoff
+        return self._forward_fc(g.x1, store.Hlabel, store.Hperf)
+
+    def _forward_fc(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
         if self.hip:
-            return self._forward_fc_hip(Yp, HL, HP)
+            return self._forward_fc_hip(x1, label, perf)
         m = self.m
-        A = m.features(Yp, training=True)
+        A = m.conv_stack(x1, self.U, training=True).reshape(x1.shape[0] * m.E, -1)
         A_det = A.detach().requires_grad_(True)
         Y = m.fc_forward(A_det)
-        label = HDCEModel.rows_from_streams(HL)
-        perf = HDCEModel.rows_from_streams(HP)
-        self.nmse.sums(Y, label, perf)
-        loss = self.nmse.finalize()
+        loss = self.nmse.sums_finalize(Y, label, perf)
         dY = self.nmse.grad(Y, label, out_dtype=Y.dtype)
         torch.autograd.backward(Y, dY)             # FC grads + dA
         self._A, self._dA = A, A_det.grad
@@ -269,18 +297,13 @@ class HDCEStep:
         self.m.count_batches(self.U)
 
     @torch.no_grad()
-    def _forward_fc_hip(self, Yp, HL, HP) -> torch.Tensor:
+    def _forward_fc_hip(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
         m = self.m
         dt = m.compute_dtype
-        x1 = m.pack_input(Yp).float().contiguous()
         A = self.conv.forward(x1, training=True)                # (rows, 4096) bf16
-        W = m.fc_w.detach().to(dt)
-        b = m.fc_b.detach().to(dt)
+        W, b = m.fc_weights_lp()
         Y = torch.nn.functional.linear(A.to(dt), W, b)
-        label = HDCEModel.rows_from_streams(HL)
-        perf = HDCEModel.rows_from_streams(HP)
-        self.nmse.sums(Y, label, perf)
-        loss = self.nmse.finalize()
+        loss = self.nmse.sums_finalize(Y, label, perf)
         dY = self.nmse.grad(Y, label, out_dtype=dt)
         _mm_f32(dY.t(), A.to(dt), m.fc_w.grad)               # dW = dY^T A   (fp32 out)
         torch.sum(dY, dim=0, dtype=torch.float32, out=m.fc_b.grad)

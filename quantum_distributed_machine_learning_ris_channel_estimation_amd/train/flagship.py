@@ -22,6 +22,7 @@ import torch
 
 from ..data.datasets import DMLStore, make_dml_stores
 from ..models.estimators import QSC_P128
+from ..ops.gather import StepGather
 from ..ops.optim import FlatParamSpace, make_optimizer
 from ..parallel.dp import DistContext, GradBuckets
 from ..utils.profiling import GraphedStep
@@ -67,6 +68,7 @@ class FlagshipTrainer:
         ctx.broadcast_(self.hdce.space.flat)
         ctx.broadcast_(self.qspace.flat)
         self.hopt = make_optimizer(self.hdce.space, "adam", cfg.lr)
+        self.hdce.attach_fc_shadow(self.hopt)   # after the broadcast: the shadow starts in sync
         self.qopt = make_optimizer(self.qspace, "adamw", cfg.lr, weight_decay=cfg.qsc_weight_decay,
                                    prune_thr=0.1 if cfg.use_gradient_pruning else 0.0)
         sp = self.hdce.space
@@ -80,6 +82,7 @@ class FlagshipTrainer:
         self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]],
                                          "small": [sp.grad[:n_conv], self.qspace.grad, self.skip]})
         self.idx = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)
         self.perm = torch.randperm(self.store.n, device=dev)
         self.cursor = 0
         self.hloss = torch.zeros(2, device=dev)
@@ -100,14 +103,13 @@ class FlagshipTrainer:
         E, U, B = self.E, self.U, self.B
         self.hdce.space.zero_grad()
         self.qspace.zero_grad()
-        self.Yp, HL, HP = self.store.gather(self.idx)
-        loss = self.hstep.forward_fc(self.Yp.view(E, U, B, *self.Yp.shape[2:]), HL.view(E, U, B, -1),
-                                     HP.view(E, U, B, -1))
+        self.gat(self.store, self.idx)           # one launch: conv input, classifier input, label rows
+        loss = self.hstep.forward_fc_gathered(self.gat, self.store)
         self.hloss.copy_(loss)
 
     def _phase2(self) -> None:
         self.hstep.backward_conv()
-        q = self.cstep(self.Yp.reshape(self.S * self.B, *self.Yp.shape[2:]), self.labels)
+        q = self.cstep(self.gat.xq, self.labels)
         self.qloss.copy_(q)
 
     def _phase3(self) -> None:

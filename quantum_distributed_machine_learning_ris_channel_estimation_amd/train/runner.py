@@ -32,6 +32,7 @@ from ..config import RunnerConfig
 from ..data.channel import pack_channel, pack_pilots
 from ..data.datasets import (DatasetFolder_DML, DMLStore, load_or_generate_stream, make_dml_stores, split_stream)
 from ..models.estimators import NMSELoss, QSC_P128, SC_P128
+from ..ops.gather import StepGather
 from ..ops.optim import FlatParamSpace, make_optimizer
 from ..parallel.dp import DeviceSampler, GradBuckets, init_distributed
 from ..utils.metrics import MetricsLogger, to_db
@@ -186,6 +187,7 @@ class Y2HRunner:
         tr, va = self.device_stores()
         model = self.build_hdce()
         opt = make_optimizer(model.space, self.optimizer, self.lr)
+        model.attach_fc_shadow(opt)
         E, U, B = self.n_scenarios, self.n_users, self.batch_size_DML
         sp = model.space
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
@@ -199,12 +201,22 @@ class Y2HRunner:
         static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
         gscale = 1.0 / ctx.world
 
+        gathers = {}
+
         def run(idx):
             sp.zero_grad()
-            Yp, HL, HP = tr.gather(idx)
             b = idx.numel()
+            if b not in gathers:
+                gathers[b] = StepGather(E, U, b, model.H, model.W, ctx.device, with_classifier=False)
+            g = gathers[b]
+            g(tr, idx)
             hs = step if b == B else HDCEStep(model, U, b, grad_hook=buckets.launch, skip=skip)
-            loss = hs(Yp.view(E, U, b, *Yp.shape[2:]), HL.view(E, U, b, -1), HP.view(E, U, b, -1))
+            loss = hs.forward_fc_gathered(g, tr)
+            if hs.grad_hook:
+                hs.grad_hook("fc")
+            hs.backward_conv()
+            if hs.grad_hook:
+                hs.grad_hook("conv")
             last_loss.copy_(loss)
             loss_acc.add_(loss)
             buckets.wait()

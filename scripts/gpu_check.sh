@@ -28,6 +28,7 @@ for s in $STEPS; do
     bench_q16) run bench_q16 600 python bench.py --steps 10 --warmup 3 --qubits 16 ;;
     train) run train 1200 python scripts/train_eval.py --epochs ${EPOCHS:-100} --qubits 6 --qml-qubits 4,8 --out "$OUT/train" ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
-    prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 20 --warmup 5) ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" ;;
+    tune) run tune 900 python scripts/tune_kernels.py ;;
   esac
 done

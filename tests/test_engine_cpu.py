@@ -85,3 +85,36 @@ def test_fused_optimizer_cpu_matches_torch():
             assert torch.allclose(a, b, atol=1e-6), kind
         o.param_groups[0]["lr"] = 0.5
         assert o.lr == 0.5 and float(o.lr_t) == 0.5
+
+
+def test_step_gather_matches_explicit_permutes():
+    """ops.gather.StepGather (one launch on GPU) == gather + pack_input + rows_from_streams, also on
+    a rank shard (non-contiguous sample axis); and the HDCE step gives the same loss both ways."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.data.datasets import make_dml_stores
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.gather import StepGather
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEModel, HDCEStep
+    tr, _ = make_dml_stores(40, 128, 10, 0.9, "cpu", synthetic=True, base_seed=3)
+    tr = tr.shard(1, 2)
+    E, U, B = 3, 3, 5
+    idx = torch.randperm(tr.n)[:B]
+    g = StepGather(E, U, B, 16, 8, "cpu")
+    g(tr, idx)
+    Yp, HL, HP = tr.gather(idx)
+    m = HDCEModel(128, "cpu", "fp32")
+    assert torch.equal(g.x1, m.pack_input(Yp.view(E, U, B, 2, 16, 8)))
+    assert torch.equal(g.xq, Yp.reshape(E * U * B, 2, 16, 8))
+    lab = HDCEModel.rows_from_streams(HL.view(E, U, B, -1))
+    assert torch.equal(_rows(tr.Hlabel, g.rowoff), lab)
+    torch.manual_seed(0)
+    s1 = HDCEStep(m, U, B)
+    l1 = s1.forward_fc(Yp.view(E, U, B, 2, 16, 8), HL.view(E, U, B, -1), HP.view(E, U, B, -1)).clone()
+    s2 = HDCEStep(m, U, B)
+    l2 = s2.forward_fc_gathered(g, tr).clone()
+    assert torch.allclose(l1, l2, rtol=1e-6)
+
+
+def _rows(store_t, rowoff):
+    """Rows of a (S, N, C) possibly non-contiguous view addressed as s*stride0/C + n."""
+    C = store_t.shape[-1]
+    sr = store_t.stride(0) // C
+    return torch.stack([store_t[int(o) // sr, int(o) % sr] for o in rowoff])
