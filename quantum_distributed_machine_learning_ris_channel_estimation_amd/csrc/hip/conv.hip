@@ -567,6 +567,47 @@ __global__ void __launch_bounds__(256) slab_rows_sum_kernel(const float* __restr
   if (ty == 0 && i < width) out[(size_t)g * width + i] += (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
 
+// Vector variant (width % 4 == 0, 16-byte aligned rows): 16 column quads x 16 row phases per
+// block, float4 loads, unrolled so each thread keeps several independent loads in flight.
+__global__ void __launch_bounds__(256) slab_rows_sum4_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                             int groups, int rows, int width) {
+  __shared__ float4 red[16][16];
+  const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int i = (blockIdx.x * 16 + tq) * 4;
+  const int g = blockIdx.y;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < width) {
+    const float* s = slab + (size_t)g * rows * width + i;
+#pragma unroll 4
+    for (int r = ty; r < rows; r += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(s + (size_t)r * width);
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
+    }
+  }
+  red[ty][tq] = t;
+  __syncthreads();
+  if (ty == 0 && i < width) {
+    float4 acc = red[0][tq];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      acc.x += red[k][tq].x;
+      acc.y += red[k][tq].y;
+      acc.z += red[k][tq].z;
+      acc.w += red[k][tq].w;
+    }
+    float4* o = reinterpret_cast<float4*>(out + (size_t)g * width + i);
+    float4 cur = *o;
+    cur.x += acc.x;
+    cur.y += acc.y;
+    cur.z += acc.z;
+    cur.w += acc.w;
+    *o = cur;
+  }
+}
+
 }  // namespace conv
 }  // namespace qd
 
@@ -722,6 +763,11 @@ QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int
 }
 
 QD_API int qd_slab_rows_sum(const float* slab, float* out, int groups, int rows, int width, void* stream) {
+  if (width % 4 == 0 && ((uintptr_t)slab & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+    hipLaunchKernelGGL(slab_rows_sum4_kernel, dim3((width / 4 + 15) / 16, groups), dim3(256), 0, (hipStream_t)stream,
+                       slab, out, groups, rows, width);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(slab_rows_sum_kernel, dim3((width + 63) / 64, groups), dim3(256), 0, (hipStream_t)stream, slab,
                      out, groups, rows, width);
   return (int)hipGetLastError();

@@ -88,18 +88,21 @@ __global__ void __launch_bounds__(1024) stream_sums_kernel(const float* __restri
   if (lane == 0) *reinterpret_cast<float4*>(ss + s * 4) = make_float4(a0, a1, a2, a3);
 }
 
-// Fused stream reduction + finalize: one wave per stream sums its rows' partials in a fixed order
-// (deterministic), then thread 0 finalises.  blockDim = 64 * S (S <= 16).
+// Fused stream reduction + finalize: wave s sums the partials of stream s's rows, listed by a
+// CSR index (order[off[s] .. off[s+1]), built once on the host), in a fixed order
+// (deterministic); thread 0 then finalises.  blockDim = 64 * S (S <= 16).
 __global__ void __launch_bounds__(1024) stream_reduce_finalize_kernel(const float* __restrict__ rowsums,
-                                                                      const int* __restrict__ row_stream,
+                                                                      const int* __restrict__ order,
+                                                                      const int* __restrict__ off,
                                                                       float* __restrict__ ss, float* __restrict__ loss,
                                                                       float* __restrict__ coef, float* __restrict__ skip,
-                                                                      int rows, int S, float loss_scale) {
+                                                                      int S, float loss_scale) {
   const int s = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  for (int r = lane; r < rows; r += 64) {
-    if (row_stream[r] != s) continue;
-    const float4 v = *reinterpret_cast<const float4*>(rowsums + (size_t)r * 4);
+  const int beg = off[s], end = off[s + 1];
+#pragma unroll 4
+  for (int j = beg + lane; j < end; j += 64) {
+    const float4 v = *reinterpret_cast<const float4*>(rowsums + (size_t)order[j] * 4);
     a0 += v.x;
     a1 += v.y;
     a2 += v.z;
@@ -197,11 +200,12 @@ QD_API int qd_nmse_stream_sums(const float* rowsums, const int* row_stream, floa
   return (int)hipGetLastError();
 }
 
-QD_API int qd_nmse_reduce_finalize(const float* rowsums, const int* row_stream, float* ss, float* loss, float* coef,
-                                   float* skip, int rows, int S, float loss_scale, void* stream) {
+// order/off: CSR list of every stream's rows (host-built once).
+QD_API int qd_nmse_reduce_finalize(const float* rowsums, const int* order, const int* off, float* ss, float* loss,
+                                   float* coef, float* skip, int S, float loss_scale, void* stream) {
   if (S < 1 || S > 16) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(stream_reduce_finalize_kernel, dim3(1), dim3(64 * S), 0, (hipStream_t)stream, rowsums, row_stream,
-                     ss, loss, coef, skip, rows, S, loss_scale);
+  hipLaunchKernelGGL(stream_reduce_finalize_kernel, dim3(1), dim3(64 * S), 0, (hipStream_t)stream, rowsums, order, off,
+                     ss, loss, coef, skip, S, loss_scale);
   return (int)hipGetLastError();
 }
 

@@ -484,10 +484,47 @@ __global__ void __launch_bounds__(1024) qsc_head_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// QuantumNAT noise injection (E:175-199: w + noise_level * randn per forward call), for G weight
+// groups (one per data stream) in ONE single-block launch: out[g] = w + sigma * N(0, 1), normals
+// from a counter-based hash of (seed, counter, g, k) -- no RNG state, graph-replay safe.  The
+// device counter is read by every thread and then advanced by thread 0, so every replay draws
+// fresh noise, and forward and backward of the same step see the same noisy weights.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float hash_normal(unsigned long long seed, unsigned long long ctr, unsigned int i) {
+  const unsigned long long h = mix64(seed ^ mix64(ctr * 0x100000001b3ull + i));
+  const float u1 = ((h >> 40) + 1u) * (1.0f / 16777217.0f);          // (0, 1]
+  const float u2 = ((h >> 16) & 0xffffffu) * (1.0f / 16777216.0f);   // [0, 1)
+  return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+__global__ void __launch_bounds__(256) qnoise_kernel(const float* __restrict__ w, float* __restrict__ out, int G,
+                                                     int P, float sigma, unsigned long long seed,
+                                                     unsigned long long* __restrict__ counter) {
+  const unsigned long long ctr = *counter;
+  for (int i = threadIdx.x; i < G * P; i += blockDim.x) out[i] = w[i % P] + sigma * hash_normal(seed, ctr, i);
+  __syncthreads();
+  if (threadIdx.x == 0) *counter = ctr + 1;
+}
+
 }  // namespace qsc
 }  // namespace qd
 
 using namespace qd::qsc;
+
+QD_API int qd_qnoise(const float* w, float* out, int G, int P, float sigma, unsigned long long seed,
+                     unsigned long long* counter, void* stream) {
+  if (G < 1 || P < 1 || counter == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(qnoise_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, w, out, G, P, sigma, seed, counter);
+  return (int)hipGetLastError();
+}
 
 static size_t qsc_smem(int H, int W, bool bwd, int n) {
   if (H == 16 && W == 8)

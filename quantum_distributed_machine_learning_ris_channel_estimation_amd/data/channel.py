@@ -81,11 +81,14 @@ GEO_SCENARIOS: Dict[int, GeoScenario] = {
 SHARED_ANGLES_DEG = (-10.0, 20.0)
 SHARED_DELAYS = (1.5, 2.5)
 SHARED_POWERS_DB = (-2.0, -3.0)
-GEO_ANGLE_JITTER_DEG = 0.1
-GEO_DELAY_JITTER = 0.01
-GEO_LOS_JITTER_DEG = 0.5
-GEO_BLOCK_PROB = 0.1
-GEO_BLOCK_DB = 15.0
+# Knobs of the geometric model (defaults = v3).  Sub-paths: every scatterer is a small cluster of
+# ``n_sub`` rays at fixed offsets (drawn once per (scenario, user, scatterer), spread
+# ``sub_spread_deg`` / ``sub_delay_spread``), each with its own random phase per sample -- more
+# degrees of freedom per user, like the many rays of a ray-traced scene.  ``user_drift_deg``: per
+# sample, ALL angles of a user shift together by U(-1, 1) * drift (position along the user row).
+GEO = dict(angle_jitter_deg=0.1, delay_jitter=0.01, los_jitter_deg=0.5, block_prob=0.1, block_db=15.0,
+           n_sub=1, sub_spread_deg=0.0, sub_delay_spread=0.0, user_drift_deg=0.0, amp_jitter=0.1,
+           user_tilt_db=3.0)
 CHANNEL_MODEL = "geometric"
 
 
@@ -139,8 +142,9 @@ def _steer(amp_phase: torch.Tensor, ang_deg: torch.Tensor, tau: torch.Tensor, de
 
 def generate_channels_geometric(n: int, scenario: int, user: int, seed: int, device="cpu",
                                 chunk: int = 8192) -> torch.Tensor:
-    """v3 fixed-environment model (module docstring)."""
+    """Fixed-environment model (module docstring; knobs in ``GEO``)."""
     spec = GEO_SCENARIOS[scenario]
+    cfg = GEO
     device = torch.device(device)
     g = _gen(seed, device)
     angs, dls, pws = list(spec.angles_deg), list(spec.delays), list(spec.powers_db)
@@ -151,24 +155,37 @@ def generate_channels_geometric(n: int, scenario: int, user: int, seed: int, dev
         pws += list(SHARED_POWERS_DB)
     K = len(angs)
     # user-dependent visibility of the scatterers
-    upw = torch.tensor(pws, device=device) - 3.0 * (torch.arange(K, device=device) - user * (K - 1) / 2).abs() / max(K - 1, 1)
+    upw = torch.tensor(pws, device=device) - cfg["user_tilt_db"] * (
+        torch.arange(K, device=device) - user * (K - 1) / 2).abs() / max(K - 1, 1)
+    # fixed sub-ray geometry of this (scenario, user): a property of the scene, not of the sample
+    ns = int(cfg["n_sub"])
+    gs = _gen(seed_for("geo-sub", scenario, user), torch.device("cpu"))
+    sub_a = (cfg["sub_spread_deg"] * torch.randn(K, ns, generator=gs)).to(device) if ns > 1 else torch.zeros(K, 1, device=device)
+    sub_d = (cfg["sub_delay_spread"] * torch.rand(K, ns, generator=gs)).to(device) if ns > 1 else torch.zeros(K, 1, device=device)
     out = torch.empty(n, H_DIM, dtype=torch.complex64, device=device)
+    base_a = torch.tensor(angs, device=device)
+    base_d = torch.tensor(dls, device=device)
     for s in range(0, n, chunk):
         b = min(chunk, n - s)
-        ang = torch.tensor(angs, device=device).repeat(b, 1) + GEO_ANGLE_JITTER_DEG * torch.randn(b, K, generator=g, device=device)
-        tau = torch.tensor(dls, device=device).repeat(b, 1) + GEO_DELAY_JITTER * torch.rand(b, K, generator=g, device=device)
+        drift = cfg["user_drift_deg"] * (2 * torch.rand(b, 1, generator=g, device=device) - 1)
+        ang = base_a.repeat(b, 1) + cfg["angle_jitter_deg"] * torch.randn(b, K, generator=g, device=device) + drift
+        tau = base_d.repeat(b, 1) + cfg["delay_jitter"] * torch.rand(b, K, generator=g, device=device)
         pw = (10 ** (upw / 10)).repeat(b, 1)
-        if spec.shared and GEO_BLOCK_PROB > 0:
-            blk = torch.rand(b, 1, generator=g, device=device) < GEO_BLOCK_PROB
+        if spec.shared and cfg["block_prob"] > 0:
+            blk = torch.rand(b, 1, generator=g, device=device) < cfg["block_prob"]
             att = torch.ones(b, K, device=device)
-            att[:, :n_own] = 10 ** (-GEO_BLOCK_DB / 10)
+            att[:, :n_own] = 10 ** (-cfg["block_db"] / 10)
             pw = torch.where(blk, pw * att, pw)
         pw = pw / pw.sum(dim=1, keepdim=True)
-        amp = torch.sqrt(pw) * (1 + 0.1 * torch.randn(b, K, generator=g, device=device))
-        ph = 2 * math.pi * torch.rand(b, K, generator=g, device=device)
+        amp = torch.sqrt(pw) * (1 + cfg["amp_jitter"] * torch.randn(b, K, generator=g, device=device))
+        # expand scatterers into sub-rays (equal power split, independent phases)
+        ang = (ang[:, :, None] + sub_a[None]).reshape(b, K * ns)
+        tau = (tau[:, :, None] + sub_d[None]).reshape(b, K * ns)
+        amp = (amp[:, :, None] / math.sqrt(ns)).expand(b, K, ns).reshape(b, K * ns)
+        ph = 2 * math.pi * torch.rand(b, K * ns, generator=g, device=device)
         if spec.los:
             Kf = 10 ** (spec.k_factor_db / 10)
-            la = USER_MEAN_ANGLE_DEG[user] + GEO_LOS_JITTER_DEG * (2 * torch.rand(b, 1, generator=g, device=device) - 1)
+            la = USER_MEAN_ANGLE_DEG[user] + cfg["los_jitter_deg"] * (2 * torch.rand(b, 1, generator=g, device=device) - 1) + drift
             ld = 0.2 * torch.rand(b, 1, generator=g, device=device)
             ang = torch.cat([la, ang], 1)
             tau = torch.cat([ld, tau], 1)

@@ -43,6 +43,10 @@ class StreamNMSE:
         self.skip = torch.zeros(1, device=dev, dtype=torch.float32)  # NaN guard flag (all-reduced in DP)
         self._rs_long = self.row_stream.long()
         self.rowoff: Optional[torch.Tensor] = None
+        # CSR list of each stream's rows (stable order) for the one-launch reduce + finalize
+        self.order = torch.sort(self._rs_long, stable=True).indices.to(torch.int32)
+        cnt = torch.bincount(self._rs_long, minlength=n_streams)
+        self.off = torch.cat([cnt.new_zeros(1), cnt.cumsum(0)]).to(torch.int32)
 
     def _labels(self, t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         """Host-path view of the labels in output-row order."""
@@ -97,9 +101,9 @@ class StreamNMSE:
         lib = nat.hip_lib()
         st = nat.stream_ptr(Y.device)
         self._row_sums_hip(Y, label, perf, st)
-        g = nat.fn(lib, "qd_nmse_reduce_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _f, _p])
-        nat.check(g(nat.ptr(self.rowsums), nat.ptr(self.row_stream), nat.ptr(self.ss), nat.ptr(self.loss),
-                    nat.ptr(self.coef), nat.ptr(self.skip), self.rows, self.S, loss_scale, st), "nmse_reduce_finalize")
+        g = nat.fn(lib, "qd_nmse_reduce_finalize", [_p, _p, _p, _p, _p, _p, _p, _i, _f, _p])
+        nat.check(g(nat.ptr(self.rowsums), nat.ptr(self.order), nat.ptr(self.off), nat.ptr(self.ss), nat.ptr(self.loss),
+                    nat.ptr(self.coef), nat.ptr(self.skip), self.S, loss_scale, st), "nmse_reduce_finalize")
         return self.loss
 
     def finalize(self, loss_scale: float = 1.0) -> torch.Tensor:

@@ -13,7 +13,8 @@ Here one step over all 9*B samples is 6 launches, no autograd:
   qsc_pre_bwd   recompute + backprop the preprocess         -> slab -> flat grad (one column sum)
 All gradients land in the model's FlatParamSpace; every buffer is static (graph-capturable).
 QuantumNAT: each of the G streams gets its own noise draw w + sigma*N(0,1) (the reference
-draws per forward call), forward AND backward use it, the grads flow to the clean master.
+draws per forward call), generated in-kernel (qd_qnoise, one launch per step); forward AND
+backward use it, the grads flow to the clean master.
 """
 from __future__ import annotations
 
@@ -45,6 +46,8 @@ class QSCStepHIP:
         o = [names["preprocess.0.weight"], names["preprocess.0.bias"], names["preprocess.3.weight"],
              names["preprocess.3.bias"], names["preprocess.7.weight"], names["preprocess.7.bias"]]
         row = o[5] + self.n - o[0]
+        row += (-row) % 4   # float4 slab sums; the tail lands in the flat space's alignment padding (zeros)
+        assert o[0] + row <= space.numel
         self.offs = (ctypes.c_int * 7)(*(o + [row]))
         self.row0, self.row = o[0], row
         feat = pre[7].weight.shape[1]
@@ -80,12 +83,21 @@ class QSCStepHIP:
             self._qb = nat.fn(L, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
         self._rs = nat.fn(L, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
         self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
+        self._qnoise = nat.fn(L, "qd_qnoise", [_p, _p, _i, _i, _f, ctypes.c_ulonglong, _p, _p])
+        wq = model.qlayer.weights
+        self.wnoisy = torch.empty((n_groups,) + tuple(wq.shape), **f32)
+        self.noise_ctr = torch.zeros(1, dtype=torch.int64, device=dev)      # advanced by the kernel
+        self.noise_seed = int(torch.randint(0, 2 ** 62, (1,)).item())       # from the (seeded) host RNG
 
     def quantum_weights(self) -> torch.Tensor:
+        """Master weights, or (training + QuantumNAT) G per-stream noisy copies drawn in-kernel
+        (qd_qnoise: counter-based RNG, one launch, no graph RNG state)."""
         m = self.m
         w = m.qlayer.weights.detach()
         if m.training and m.use_quantumnat and m.noise_level > 0:
-            return w.unsqueeze(0) + m.noise_level * torch.randn((self.G,) + tuple(w.shape), device=w.device)
+            nat.check(self._qnoise(nat.ptr(w), nat.ptr(self.wnoisy), self.G, w.numel(), float(m.noise_level),
+                                   self.noise_seed, nat.ptr(self.noise_ctr), nat.stream_ptr(w.device)), "qnoise")
+            return self.wnoisy
         return w
 
     @torch.no_grad()

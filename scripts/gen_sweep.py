@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Synthetic-channel calibration sweep (GPU): for each generator variant, train the HDCE estimator
+and the classical SC briefly and report NMSE / accuracy vs SNR, to pick generator knobs whose
+curves resemble the reference's published FIG1.  One JSON line per variant.
+
+    python scripts/gen_sweep.py --epochs 30 --sc-epochs 8
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+VARIANTS = {
+    "v3": {},
+    "sub4": dict(n_sub=4, sub_spread_deg=1.5, sub_delay_spread=0.3),
+    "sub4_drift2": dict(n_sub=4, sub_spread_deg=1.5, sub_delay_spread=0.3, user_drift_deg=2.0),
+    "sub6_drift3": dict(n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, user_drift_deg=3.0),
+    "drift2": dict(user_drift_deg=2.0),
+    "sub4_block": dict(n_sub=4, sub_spread_deg=1.5, sub_delay_spread=0.3, block_prob=0.2, block_db=30.0,
+                       user_tilt_db=0.0),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=30)
+    ap.add_argument("--sc-epochs", type=int, default=8)
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--test-len", type=int, default=3000)
+    ap.add_argument("--out", default="gpurun_out/gen_sweep")
+    a = ap.parse_args()
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.data import channel
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.evaluate import model_val
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.runner import Y2HRunner
+    base = dict(channel.GEO)
+    os.makedirs(a.out, exist_ok=True)
+    for name in a.variants.split(","):
+        channel.GEO.clear()
+        channel.GEO.update(base)
+        channel.GEO.update(VARIANTS[name])
+        ws = os.path.join("/tmp", f"gensweep_{name}")
+        shutil.rmtree(ws, ignore_errors=True)
+        t0 = time.time()
+        r = Y2HRunner(n_epochs=a.epochs, workspace=ws, hip_graphs=True)
+        r.train_Conv_Linear_of_HDCE()
+        r.n_epochs = a.sc_epochs
+        r.train_SC_P128()
+        rec = {"variant": name, "geo": dict(channel.GEO), "val_hdce_db": [round(10 * __import__("math").log10(v), 2)
+                                                                           for v in r.val_HDCE_nmse[::5]],
+               "sc_val_acc": [round(v, 4) for v in r.val_SC_accuracies]}
+        for tag in (f"epoch{a.epochs - 1}", "best"):
+            mv = model_val(workspace=ws, results_dir=os.path.join(a.out, name), data_len_for_test=a.test_len,
+                           snr_list=(5, 10, 15))
+            mv.epoch_tag = tag
+            mv.test_for_CE_P128_for_all_scenarios()
+            res = mv.results
+            db = lambda xs: [round(10 * __import__("math").log10(x), 2) for x in xs]
+            rec[tag] = {"ls": db(res["nmse_ls"]), "mmse": db(res["nmse_mmse"]), "hdce": db(res["nmse_classical"]),
+                        "acc": [round(x, 4) for x in res["acc_classical"]]}
+        rec["seconds"] = round(time.time() - t0, 1)
+        print(json.dumps(rec), flush=True)
+        with open(os.path.join(a.out, "sweep.jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
+
+if __name__ == "__main__":
+    main()

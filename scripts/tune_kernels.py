@@ -11,8 +11,12 @@ from __future__ import annotations
 import argparse
 import itertools
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def time_graph(fn, iters=50):

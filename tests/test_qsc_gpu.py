@@ -32,3 +32,40 @@ def test_qsc_step_matches_autograd(cuda, pilot_num, n, B):
         assert na == nb
         err = (pa.grad - pb.grad).abs().max() / pb.grad.abs().max().clamp_min(1e-12)
         assert err < 2e-3, (na, float(err))
+
+
+def test_qsc_step_quantumnat_in_kernel_noise(cuda):
+    """QuantumNAT noise drawn in-kernel: N(0, sigma^2) per element, fresh every step, distinct per
+    stream group; the fused step equals autograd through the SAME noisy weights, grads to the master."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.quantum import qsim
+    torch.manual_seed(0)
+    n, G, b = 6, 9, 32
+    B = G * b
+    a = QSC_P128(n_qubits=n, use_quantumnat=True, use_gradient_pruning=False, noise_level=0.05).to(cuda)
+    ref = QSC_P128(n_qubits=n, use_quantumnat=False, use_gradient_pruning=False).to(cuda)
+    ref.load_state_dict(a.state_dict())
+    space = FlatParamSpace(list(a.named_parameters()), cuda)
+    step = QSCStepHIP(a, space, B, n_groups=G)
+    x = torch.randn(B, 2, 16, 8, device=cuda)
+    y = torch.randint(0, 3, (B,), device=cuda)
+    space.zero_grad()
+    loss = step(x, y)
+    wn = step.wnoisy.clone()
+    w0 = a.qlayer.weights.detach()
+    d = (wn - w0.unsqueeze(0)) / 0.05
+    assert abs(float(d.mean())) < 0.1 and abs(float(d.std()) - 1.0) < 0.1
+    assert not torch.equal(wn[0], wn[1])
+    # reference through the same noisy weights
+    angles = ref.preprocess(x)
+    wq = ref.qlayer.weights.unsqueeze(0) + (wn - w0.unsqueeze(0))
+    out = F.log_softmax(ref.classifier(qsim(angles, wq, "hip")), dim=1)
+    rl = F.nll_loss(out, y)
+    rl.backward()
+    torch.cuda.synchronize()
+    assert torch.allclose(loss[0], rl, rtol=1e-4, atol=1e-5)
+    for (na, pa), (nb, pb) in zip(a.named_parameters(), ref.named_parameters()):
+        err = (pa.grad - pb.grad).abs().max() / pb.grad.abs().max().clamp_min(1e-12)
+        assert err < 2e-3, (na, float(err))
+    # next step: fresh noise
+    step(x, y)
+    assert not torch.equal(step.wnoisy, wn)
