@@ -28,7 +28,7 @@ def _ptr(t: Optional[torch.Tensor]):
 class ConvStackHIP:
     """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
 
-    def __init__(self, model, U: int, B: int, spw: int = 1, spb_w: int = 8, spb_r: int = 8):
+    def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 16, spb_r: int = 4):
         self.m = model
         self.U, self.B, self.N, self.E = U, B, U * B, model.E
         self.H, self.W = model.H, model.W

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""HDCE generalisation diagnostic (GPU).
+
+After training, compare on the SAME training batch the train-mode NMSE (ghost-BN batch stats, HIP
+path) with the eval-mode NMSE (running stats, torch path): a large gap would mean a train/eval
+mismatch rather than overfitting.  Also reports the val curve for several data lengths.
+"""
+import argparse
+import json
+import math
+import os
+import shutil
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+@torch.no_grad()
+def nmse_on(model, store, idx, training):
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEModel
+    E, U = 3, 3
+    Yp, HL, HP = store.gather(idx)
+    b = idx.numel()
+    model.train(training)
+    A = model.features(Yp.view(E, U, b, *Yp.shape[2:]), training=training)
+    Y = model.fc_forward(A).float()
+    per = HDCEModel.rows_from_streams(HP.view(E, U, b, -1))
+    model.train(True)
+    return float(((Y - per) ** 2).sum() / (per ** 2).sum())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=20)
+    ap.add_argument("--data-lens", default="20000,100000")
+    a = ap.parse_args()
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.runner import Y2HRunner
+    for dl in [int(x) for x in a.data_lens.split(",")]:
+        ws = f"/tmp/diag_{dl}"
+        shutil.rmtree(ws, ignore_errors=True)
+        r = Y2HRunner(n_epochs=a.epochs, data_len=dl, workspace=ws)
+        m = r.train_Conv_Linear_of_HDCE()
+        tr, va = r.device_stores()
+        idx = torch.arange(0, 256, device=tr.Yp.device)
+        # the torch (non-HIP) train-mode path recomputes batch statistics exactly as the HIP kernels do
+        rec = {"data_len": dl,
+               "train_batch_trainmode_db": round(10 * math.log10(nmse_on(m, tr, idx, True)), 2),
+               "train_batch_evalmode_db": round(10 * math.log10(nmse_on(m, tr, idx, False)), 2),
+               "val_batch_evalmode_db": round(10 * math.log10(nmse_on(m, va, idx[:min(256, va.n)], False)), 2),
+               "val_curve_db": [round(10 * math.log10(v), 2) for v in r.val_HDCE_nmse],
+               "train_loss_db": [round(10 * math.log10(v), 2) for v in r.train_HDCE_losses]}
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
