@@ -1,16 +1,24 @@
-// Batched VQC simulator for LARGE qubit counts (n = 11 .. 16): one workgroup per sample.
+// Batched VQC simulator for LARGE qubit counts (n = 11 .. 16): one 256-thread workgroup per sample,
+// gate-fused passes.
 //
-// Same circuit and adjoint method as csrc/hip/qsim.hip (reference E:125-142); that kernel keeps a
-// sample's state in one wave's registers, which stops at n = 10 (16 amplitudes per lane).  Here a
-// 512-thread workgroup owns a sample and applies the gates as passes over the state:
-//   * state in LDS when it fits (forward: 2 buffers, backward: 4 buffers of 2^n complex fp32 --
-//     n <= 12 backward / n <= 13 forward), otherwise in a per-workgroup HBM workspace (n = 16:
-//     512 KiB per state; at one workgroup per CU the working set is L2/MALL-resident);
-//   * one pass per fused RZ.RY wire rotation (amplitude pairs, no divergence), one gather pass per
-//     CNOT ring (ping-pong buffers: the ring is a GF(2)-linear basis permutation);
-//   * adjoint backward: each gate's two parameter-gradient partials are block-reduced as part of
-//     the pass barrier; layer-0 RY gradients are the per-sample d(angles), the weight gradients are
-//     accumulated over the workgroup's samples and written as one slab row per workgroup.
+// Same circuit and adjoint method as csrc/hip/qsim.hip (reference E:125-142: RY embedding, L x
+// [RY, RZ on every wire, CNOT ring], <Z_i>); that kernel keeps a sample's state in one wave's
+// registers, which stops at n = 10.  Here the state (2^n complex fp32: 16 KiB .. 512 KiB) lives in
+// LDS when it fits (n <= 12) or in a per-workgroup HBM workspace, and a layer is TWO passes over it
+// instead of one pass per gate:
+//   low pass   qubits 0 .. TB-1 (TB = min(n, 12)).  The state is cut into 2^(n-TB) tiles of 2^TB
+//              contiguous amplitudes (32 KiB); a tile is staged in LDS and the TB rotations are
+//              applied three qubits at a time in registers (each thread owns the 8 amplitudes that
+//              differ in those 3 bits): 4 LDS round trips per tile, not TB.
+//   high pass  qubits TB .. n-1 (HB = n - TB <= 4).  A thread owns a "column" of 2^HB amplitudes
+//              (same low bits), applies the HB rotations in registers and stores every amplitude at
+//              its CNOT-ring image f(k): the ring permutation costs nothing extra.
+// Layer 0 (embedding + first rotations) is a product state written directly at its ring images.
+// Forward traffic per layer: ~2 reads + 2 writes of the state (the per-gate version made 17 of
+// each at 16 qubits).  Backward (adjoint): recompute psi, then per layer in reverse: the high pass
+// gathers psi and lambda from f(k) (inverse ring) and undoes the high rotations, the low pass
+// undoes the low ones; lambda = (sum_q g_q Z_q) psi is formed on the fly in the first reverse pass.
+// Per-gate gradient partials stay in registers across tiles and are block-reduced once per pass.
 #include "common.h"
 
 namespace qd {
@@ -21,208 +29,432 @@ struct cf {
 };
 __device__ __forceinline__ cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 
-constexpr int NT = 512;
+constexpr int NT = 256;   // 4 waves: lets the backward use AGPRs instead of scratch (512-thread groups spilled)
 constexpr int NW = NT / 64;
 
-__device__ __forceinline__ int ring_fwd(int k, int n) {
-  for (int i = 0; i < n - 1; ++i) k ^= ((k >> i) & 1) << (i + 1);
-  k ^= (k >> (n - 1)) & 1;
-  return k;
-}
-__device__ __forceinline__ int ring_inv(int k, int n) {
-  k ^= (k >> (n - 1)) & 1;
-  for (int i = n - 2; i >= 0; --i) k ^= ((k >> i) & 1) << (i + 1);
-  return k;
-}
-// insert a zero bit at position q
-__device__ __forceinline__ int ins0(int p, int q) { return ((p >> q) << (q + 1)) | (p & ((1 << q) - 1)); }
+template <int N>
+struct G {
+  static constexpr int D = 1 << N;
+  static constexpr int TB = N < 12 ? N : 12;   // low (tile) qubits
+  static constexpr int HB = N - TB;            // high (column) qubits
+  static constexpr int T = 1 << TB;            // tile size (amplitudes)
+  static constexpr int NTILE = 1 << HB;
+  static constexpr int NGRP = (TB + 2) / 3;    // 3-qubit groups of the low pass
+  static constexpr bool LDS_STATE = N <= 12;
+};
 
-// Block-wide sum of two values; every thread gets the result.  red: >= 2*NW floats.
-__device__ __forceinline__ float2 block_sum2(float a, float b, float* red) {
-  a = wave_sum(a);
-  b = wave_sum(b);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    red[2 * w] = a;
-    red[2 * w + 1] = b;
-  }
-  __syncthreads();
-  float2 r = {0.f, 0.f};
+template <int N>
+__device__ __forceinline__ int ring_fwd(int k) {
 #pragma unroll
-  for (int i = 0; i < NW; ++i) {
-    r.x += red[2 * i];
-    r.y += red[2 * i + 1];
-  }
-  __syncthreads();
-  return r;
+  for (int i = 0; i < N - 1; ++i) k ^= ((k >> i) & 1) << (i + 1);
+  k ^= (k >> (N - 1)) & 1;
+  return k;
+}
+template <int N>
+__device__ __forceinline__ int ring_inv(int k) {
+  k ^= (k >> (N - 1)) & 1;
+#pragma unroll
+  for (int i = N - 2; i >= 0; --i) k ^= ((k >> i) & 1) << (i + 1);
+  return k;
 }
 
-__device__ void product_state(cf* s, const float* xs, const float* w, int n, float* cs) {
-  // cs: 4n floats of LDS: (ch, sh, cp, sp) per wire
-  for (int q = threadIdx.x; q < n; q += NT) {
-    float sh, ch, sp, cp;
-    __sincosf(0.5f * (xs[q] + w[2 * q]), &sh, &ch);
-    __sincosf(0.5f * w[2 * q + 1], &sp, &cp);
-    cs[4 * q] = ch;
-    cs[4 * q + 1] = sh;
-    cs[4 * q + 2] = cp;
-    cs[4 * q + 3] = sp;
+// insert NB zero bits at position P into t
+template <int P, int NB>
+__device__ __forceinline__ int ins_bits(int t) {
+  return ((t >> P) << (P + NB)) | (t & ((1 << P) - 1));
+}
+
+// Per-qubit trig of one layer, (cos, sin) of theta/2 and (cos, sin) of phi/2, into LDS.
+__device__ __forceinline__ void layer_trig(float4* trig, const float* wl, const float* xs, int n) {
+  if (threadIdx.x < n) {
+    const int q = threadIdx.x;
+    float s, c, sp, cp;
+    __sincosf(0.5f * (wl[2 * q] + (xs ? xs[q] : 0.f)), &s, &c);
+    __sincosf(0.5f * wl[2 * q + 1], &sp, &cp);
+    trig[q] = make_float4(c, s, cp, sp);
+  }
+}
+
+// forward gate RZ(phi) RY(theta) on the pair (a0: bit 0, a1: bit 1)
+__device__ __forceinline__ void gate_fwd(cf& a0, cf& a1, float4 t) {
+  const cf t0 = {t.x * a0.x - t.y * a1.x, t.x * a0.y - t.y * a1.y};
+  const cf t1 = {t.y * a0.x + t.x * a1.x, t.y * a0.y + t.x * a1.y};
+  a0 = cmul(t0, cf{t.z, -t.w});
+  a1 = cmul(t1, cf{t.z, t.w});
+}
+
+// adjoint step: given psi, lambda AFTER the gate, accumulate d(theta), d(phi) and undo the gate
+__device__ __forceinline__ void gate_adj(cf& p0, cf& p1, cf& l0, cf& l1, float4 t, float& dth, float& dph) {
+  dph += (l0.x * p0.y - l0.y * p0.x) - (l1.x * p1.y - l1.y * p1.x);   // Im <lam| Z |psi>
+  p0 = cmul(p0, cf{t.z, t.w});
+  l0 = cmul(l0, cf{t.z, t.w});
+  p1 = cmul(p1, cf{t.z, -t.w});
+  l1 = cmul(l1, cf{t.z, -t.w});
+  dth += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y); // Im <lam| Y |psi>
+  const cf q0 = p0, q1 = p1, m0 = l0, m1 = l1;
+  p0 = {t.x * q0.x + t.y * q1.x, t.x * q0.y + t.y * q1.y};
+  p1 = {t.x * q1.x - t.y * q0.x, t.x * q1.y - t.y * q0.y};
+  l0 = {t.x * m0.x + t.y * m1.x, t.x * m0.y + t.y * m1.y};
+  l1 = {t.x * m1.x - t.y * m0.x, t.x * m1.y - t.y * m0.y};
+}
+
+// Block-reduce NV per-thread values; dst[off + i] += sum_i (thread i < NV).  red: NW*NV floats.
+template <int NV>
+__device__ __forceinline__ void block_add(const float (&v)[NV], float* red, float* dst, int off) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float s = wave_sum(v[i]);
+    if (lane == 0) red[w * NV + i] = s;
   }
   __syncthreads();
-  const int D = 1 << n;
-  for (int k = threadIdx.x; k < D; k += NT) {
+  if (threadIdx.x < NV) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s += red[k * NV + threadIdx.x];
+    dst[off + threadIdx.x] += s;
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------- forward passes
+// Layer 0 + ring: A[j] = prod_q c_q(bit_q(f^-1(j))), c(0) = cos(t/2)e^{-ip/2}, c(1) = sin(t/2)e^{ip/2}
+template <int N>
+__device__ void product_pass(cf* A, const float4* trig) {
+  for (int j = threadIdx.x; j < G<N>::D; j += NT) {
+    const int k = ring_inv<N>(j);
     cf a = {1.f, 0.f};
-    for (int q = 0; q < n; ++q) {
-      const float* c = cs + 4 * q;
-      const bool b = (k >> q) & 1;
-      const cf f = b ? cf{c[1] * c[2], c[1] * c[3]} : cf{c[0] * c[2], -c[0] * c[3]};
-      a = cmul(a, f);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const float4 t = trig[q];
+      a = cmul(a, ((k >> q) & 1) ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
     }
-    s[k] = a;
+    A[j] = a;
   }
   __syncthreads();
 }
 
-// dst[j] = src[f^-1(j)] (forward ring) or src[f(j)] (inverse)
-__device__ __forceinline__ void permute(const cf* src, cf* dst, int n, bool inverse) {
-  const int D = 1 << n;
-  for (int j = threadIdx.x; j < D; j += NT) dst[j] = src[inverse ? ring_fwd(j, n) : ring_inv(j, n)];
-  __syncthreads();
-}
-
-__device__ __forceinline__ void rotate(cf* s, int n, int q, float theta, float phi) {
-  float sn, c, sp, cp;
-  __sincosf(0.5f * theta, &sn, &c);
-  __sincosf(0.5f * phi, &sp, &cp);
-  const int half = 1 << (n - 1);
-  for (int p = threadIdx.x; p < half; p += NT) {
-    const int k0 = ins0(p, q), k1 = k0 | (1 << q);
-    const cf a0 = s[k0], a1 = s[k1];
-    s[k0] = cmul(cf{c * a0.x - sn * a1.x, c * a0.y - sn * a1.y}, cf{cp, -sp});
-    s[k1] = cmul(cf{sn * a0.x + c * a1.x, sn * a0.y + c * a1.y}, cf{cp, sp});
-  }
-  __syncthreads();
-}
-
-// Forward circuit; returns the buffer holding psi_final (a or b).
-__device__ cf* run_circuit(cf* a, cf* b, const float* xs, const float* w, int n, int L, float* cs) {
-  product_state(a, xs, w, n, cs);
-  permute(a, b, n, false);
-  cf* cur = b;
-  cf* oth = a;
-  for (int l = 1; l < L; ++l) {
-    for (int q = 0; q < n; ++q) rotate(cur, n, q, w[2 * (l * n + q)], w[2 * (l * n + q) + 1]);
-    permute(cur, oth, n, false);
-    cf* t = cur;
-    cur = oth;
-    oth = t;
-  }
-  return cur;
-}
-
-__global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                          float* __restrict__ E, int B, int n, int L, int wgroup,
-                                                          cf* __restrict__ ws, int use_lds) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem);            // 64 floats
-  float* cs = red + 64;                                   // 64 floats
-  const int D = 1 << n;
-  cf* a = use_lds ? reinterpret_cast<cf*>(smem + 512) : ws + (size_t)blockIdx.x * 2 * D;
-  cf* b = a + D;
-  for (int s = blockIdx.x; s < B; s += gridDim.x) {
-    const float* ws_ = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * n * L : 0);
-    cf* psi = run_circuit(a, b, x + (size_t)s * n, ws_, n, L, cs);
-    float part[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) part[q] = 0.f;
-    for (int k = threadIdx.x; k < D; k += NT) {
-      const float p = psi[k].x * psi[k].x + psi[k].y * psi[k].y;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) part[q] += ((k >> q) & 1) ? -p : p;
+// Low pass (forward): rotations on qubits 0..TB-1 of every tile of A (in place).
+template <int N>
+__device__ void low_pass_fwd(cf* A, cf* tile, const float4* trig) {
+  using C = G<N>;
+  for (int h = 0; h < C::NTILE; ++h) {
+    cf* tl = C::LDS_STATE ? A : tile;
+    if constexpr (!C::LDS_STATE) {
+      const cf* src = A + (size_t)h * C::T;
+      for (int i = threadIdx.x; i < C::T; i += NT) tl[i] = src[i];
+      __syncthreads();
     }
+    static_for<0, C::NGRP>([&](auto gc) {
+      constexpr int g0 = 3 * decltype(gc)::value;
+      constexpr int NB = (C::TB - g0) < 3 ? (C::TB - g0) : 3;
+      constexpr int ACT = C::T >> NB;
+      for (int t = threadIdx.x; t < ACT; t += NT) {
+        const int base = ins_bits<g0, NB>(t);
+        cf a[1 << NB];
 #pragma unroll
-    for (int q = 0; q < 16; q += 2) {  // constant indices keep part[] in registers
-      if (q < n) {                      // uniform branch: every thread reaches the barrier
-        const float2 r = block_sum2(part[q], part[q + 1], red);
-        if (threadIdx.x == 0) {
-          E[(size_t)s * n + q] = r.x;
-          if (q + 1 < n) E[(size_t)s * n + q + 1] = r.y;
+        for (int j = 0; j < (1 << NB); ++j) a[j] = tl[base | (j << g0)];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const float4 tg = trig[g0 + b];
+#pragma unroll
+          for (int j = 0; j < (1 << NB); ++j)
+            if (!((j >> b) & 1)) gate_fwd(a[j], a[j | (1 << b)], tg);
         }
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j) tl[base | (j << g0)] = a[j];
       }
+      __syncthreads();
+    });
+    if constexpr (!C::LDS_STATE) {
+      cf* dst = A + (size_t)h * C::T;
+      for (int i = threadIdx.x; i < C::T; i += NT) dst[i] = tl[i];
+      __syncthreads();
     }
   }
 }
 
-// slab: (gridDim.x, 2*n*L) partial weight grads; dx: (B, n)
+// High pass (forward): rotations on qubits TB..N-1 column-wise, stored at ring images: B[f(k)].
+template <int N>
+__device__ void high_pass_fwd(const cf* A, cf* B, const float4* trig) {
+  using C = G<N>;
+  for (int c = threadIdx.x; c < C::T; c += NT) {
+    cf a[C::NTILE];
+#pragma unroll
+    for (int h = 0; h < C::NTILE; ++h) a[h] = A[c | (h << C::TB)];
+#pragma unroll
+    for (int b = 0; b < C::HB; ++b) {
+      const float4 tg = trig[C::TB + b];
+#pragma unroll
+      for (int h = 0; h < C::NTILE; ++h)
+        if (!((h >> b) & 1)) gate_fwd(a[h], a[h | (1 << b)], tg);
+    }
+#pragma unroll
+    for (int h = 0; h < C::NTILE; ++h) B[ring_fwd<N>(c | (h << C::TB))] = a[h];
+  }
+  __syncthreads();
+}
+
+// Full forward circuit of one sample; returns the buffer holding psi_final (A or B).
+template <int N>
+__device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs, const float* w, int L) {
+  layer_trig(trig, w, xs, N);
+  __syncthreads();
+  product_pass<N>(A, trig);
+  for (int l = 1; l < L; ++l) {
+    layer_trig(trig, w + 2 * N * l, nullptr, N);
+    __syncthreads();
+    low_pass_fwd<N>(A, tile, trig);
+    high_pass_fwd<N>(A, B, trig);
+    cf* t = A;
+    A = B;
+    B = t;
+  }
+  return A;
+}
+
+// ------------------------------------------------------------------------------- kernels
+// LDS carve (bytes): reduction scratch | trig (<= 16 float4) | gE (16) | acc (2nL <= 256) + per-
+// sample layer-0 scratch (2n <= 32) | data (tiles, or the whole state when n <= 12).
+constexpr int O_RED = 0, O_TRIG = 2048, O_G = 2304, O_ACC = 2368, O_TMP = 3392, O_DATA = 3584;
+
+template <int N>
+__global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          float* __restrict__ E, int B, int L, int wgroup,
+                                                          cf* __restrict__ ws) {
+  using C = G<N>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem + O_RED);
+  float4* trig = reinterpret_cast<float4*>(smem + O_TRIG);
+  float* outv = reinterpret_cast<float*>(smem + O_TMP);
+  cf* data = reinterpret_cast<cf*>(smem + O_DATA);
+  cf *A, *Bf, *tile;
+  if constexpr (C::LDS_STATE) {
+    A = data;
+    Bf = data + C::D;
+    tile = nullptr;
+  } else {
+    A = ws + (size_t)blockIdx.x * 2 * C::D;
+    Bf = A + C::D;
+    tile = data;
+  }
+  for (int s = blockIdx.x; s < B; s += gridDim.x) {
+    const float* wsmp = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * N * L : 0);
+    cf* psi = run_circuit<N>(A, Bf, tile, trig, x + (size_t)s * N, wsmp, L);
+    float part[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) part[q] = 0.f;
+    for (int k = threadIdx.x; k < C::D; k += NT) {
+      const cf a = psi[k];
+      const float p = a.x * a.x + a.y * a.y;
+#pragma unroll
+      for (int q = 0; q < N; ++q) part[q] += ((k >> q) & 1) ? -p : p;
+    }
+    if (threadIdx.x < N) outv[threadIdx.x] = 0.f;
+    __syncthreads();
+    block_add<N>(part, red, outv, 0);
+    if (threadIdx.x < N) E[(size_t)s * N + threadIdx.x] = outv[threadIdx.x];
+    __syncthreads();
+  }
+}
+
+// slab: (gridDim.x, 2*N*L) partial weight grads (one row per workgroup); dx: (B, N)
+template <int N>
 __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ gE, float* __restrict__ dx,
-                                                          float* __restrict__ slab, int B, int n, int L, int wgroup,
-                                                          cf* __restrict__ ws, int use_lds) {
+                                                          float* __restrict__ slab, int B, int L, int wgroup,
+                                                          cf* __restrict__ ws) {
+  using C = G<N>;
+  constexpr int HV = C::HB > 0 ? C::HB : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem);            // 64
-  float* cs = red + 64;                                   // 64
-  float* acc = red + 128;                                 // 2*n*L <= 256 (weight grads)
-  float* gq = red + 384;                                  // n <= 16 output cotangents
-  const int D = 1 << n;
-  const int P = 2 * n * L;
-  cf* base = use_lds ? reinterpret_cast<cf*>(smem + 2048) : ws + (size_t)blockIdx.x * 4 * D;
-  cf *pa = base, *pb = base + D, *la = base + 2 * D, *lb = base + 3 * D;
+  float* red = reinterpret_cast<float*>(smem + O_RED);
+  float4* trig = reinterpret_cast<float4*>(smem + O_TRIG);
+  float* gq = reinterpret_cast<float*>(smem + O_G);
+  float* acc = reinterpret_cast<float*>(smem + O_ACC);
+  float* tmp = reinterpret_cast<float*>(smem + O_TMP);
+  cf* data = reinterpret_cast<cf*>(smem + O_DATA);
+  const int P = 2 * N * L;
+  cf *b0, *b1, *b2, *b3, *tp = nullptr, *tq = nullptr;
+  if constexpr (C::LDS_STATE) {
+    b0 = data;
+    b1 = data + C::D;
+    b2 = data + 2 * C::D;
+    b3 = data + 3 * C::D;
+  } else {
+    b0 = ws + (size_t)blockIdx.x * 4 * C::D;
+    b1 = b0 + C::D;
+    b2 = b0 + 2 * C::D;
+    b3 = b0 + 3 * C::D;
+    tp = data;
+    tq = data + C::T;
+  }
   for (int i = threadIdx.x; i < P; i += NT) acc[i] = 0.f;
-  __syncthreads();
   for (int s = blockIdx.x; s < B; s += gridDim.x) {
-    const float* wsmp = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * n * L : 0);
-    const float* xs = x + (size_t)s * n;
-    cf* psi = run_circuit(pa, pb, xs, wsmp, n, L, cs);
-    cf* psi_o = (psi == pa) ? pb : pa;
-    cf* lam = la;
-    cf* lam_o = lb;
-    // lambda = (sum_q g_q Z_q) psi
-    if (threadIdx.x < n) gq[threadIdx.x] = gE[(size_t)s * n + threadIdx.x];
-    __syncthreads();
-    for (int k = threadIdx.x; k < D; k += NT) {
-      float o = 0.f;
-      for (int q = 0; q < n; ++q) o += ((k >> q) & 1) ? -gq[q] : gq[q];
-      lam[k] = {psi[k].x * o, psi[k].y * o};
-    }
-    __syncthreads();
-    const int half = 1 << (n - 1);
+    const float* wsmp = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * N * L : 0);
+    const float* xs = x + (size_t)s * N;
+    if (threadIdx.x < N) gq[threadIdx.x] = gE[(size_t)s * N + threadIdx.x];
+    if (threadIdx.x < 2 * N) tmp[threadIdx.x] = 0.f;
+    cf* psi = run_circuit<N>(b0, b1, tp, trig, xs, wsmp, L);   // its barriers publish gq / tmp
+    cf* psi_o = (psi == b0) ? b1 : b0;
+    cf* lam = b2;
+    cf* lam_o = b3;
     for (int l = L - 1; l >= 0; --l) {
-      permute(psi, psi_o, n, true);
-      permute(lam, lam_o, n, true);
-      cf* t = psi; psi = psi_o; psi_o = t;
-      t = lam; lam = lam_o; lam_o = t;
-      for (int q = n - 1; q >= 0; --q) {
-        const float theta = wsmp[2 * (l * n + q)] + (l == 0 ? xs[q] : 0.f);
-        const float phi = wsmp[2 * (l * n + q) + 1];
-        float sn, c, sp, cp;
-        __sincosf(0.5f * theta, &sn, &c);
-        __sincosf(0.5f * phi, &sp, &cp);
-        float dphi = 0.f, dth = 0.f;
-        for (int p = threadIdx.x; p < half; p += NT) {
-          const int k0 = ins0(p, q), k1 = k0 | (1 << q);
-          cf p0 = psi[k0], p1 = psi[k1], l0 = lam[k0], l1 = lam[k1];
-          // RZ^dagger with dphi = Im <lam| Z |psi>
-          dphi += (l0.x * p0.y - l0.y * p0.x) - (l1.x * p1.y - l1.y * p1.x);
-          p0 = cmul(p0, cf{cp, sp}); l0 = cmul(l0, cf{cp, sp});
-          p1 = cmul(p1, cf{cp, -sp}); l1 = cmul(l1, cf{cp, -sp});
-          // RY^dagger with dtheta = Im <lam| Y |psi>
-          dth += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
-          psi[k0] = {c * p0.x + sn * p1.x, c * p0.y + sn * p1.y};
-          psi[k1] = {c * p1.x - sn * p0.x, c * p1.y - sn * p0.y};
-          lam[k0] = {c * l0.x + sn * l1.x, c * l0.y + sn * l1.y};
-          lam[k1] = {c * l1.x - sn * l0.x, c * l1.y - sn * l0.y};
+      layer_trig(trig, wsmp + 2 * N * l, l == 0 ? xs : nullptr, N);
+      __syncthreads();
+      // layer-0 gradients go to the per-sample scratch first (their theta part is also dx)
+      float* gdst = (l == 0) ? tmp : acc + 2 * N * l;
+      const bool first = (l == L - 1);   // lambda = O psi formed on the fly
+      // ---- high pass (reverse): gather psi/lam at f(k) (inverse ring), undo high rotations
+      {
+        float dth[HV], dph[HV];
+#pragma unroll
+        for (int b = 0; b < HV; ++b) dth[b] = dph[b] = 0.f;
+        for (int c = threadIdx.x; c < C::T; c += NT) {
+          cf p[C::NTILE], m[C::NTILE];
+#pragma unroll
+          for (int h = 0; h < C::NTILE; ++h) {
+            const int src = ring_fwd<N>(c | (h << C::TB));
+            p[h] = psi[src];
+            if (first) {
+              float o = 0.f;
+#pragma unroll
+              for (int q = 0; q < N; ++q) o += ((src >> q) & 1) ? -gq[q] : gq[q];
+              m[h] = {p[h].x * o, p[h].y * o};
+            } else {
+              m[h] = lam[src];
+            }
+          }
+#pragma unroll
+          for (int bb = 0; bb < C::HB; ++bb) {
+            const int b = C::HB - 1 - bb;   // reverse qubit order
+            const float4 tg = trig[C::TB + b];
+#pragma unroll
+            for (int h = 0; h < C::NTILE; ++h)
+              if (!((h >> b) & 1)) gate_adj(p[h], p[h | (1 << b)], m[h], m[h | (1 << b)], tg, dth[b], dph[b]);
+          }
+#pragma unroll
+          for (int h = 0; h < C::NTILE; ++h) {
+            psi_o[c | (h << C::TB)] = p[h];
+            lam_o[c | (h << C::TB)] = m[h];
+          }
         }
-        const float2 r = block_sum2(dth, dphi, red);   // includes the pass barrier
-        if (threadIdx.x == 0) {
-          acc[2 * (l * n + q)] += r.x;
-          acc[2 * (l * n + q) + 1] += r.y;
-          if (l == 0) dx[(size_t)s * n + q] = r.x;
+        __syncthreads();
+        if constexpr (C::HB > 0) {
+          float v[2 * HV];
+#pragma unroll
+          for (int b = 0; b < HV; ++b) {
+            v[2 * b] = dth[b];
+            v[2 * b + 1] = dph[b];
+          }
+          block_add<2 * HV>(v, red, gdst, 2 * C::TB);
         }
+        cf* t = psi;
+        psi = psi_o;
+        psi_o = t;
+        t = lam;
+        lam = lam_o;
+        lam_o = t;
+      }
+      // ---- low pass (reverse): tiles of psi/lam in place, groups and qubits in reverse order
+      {
+        float dth[C::TB], dph[C::TB];
+#pragma unroll
+        for (int q = 0; q < C::TB; ++q) dth[q] = dph[q] = 0.f;
+        for (int h = 0; h < C::NTILE; ++h) {
+          cf* tpp = C::LDS_STATE ? psi : tp;
+          cf* tqq = C::LDS_STATE ? lam : tq;
+          if constexpr (!C::LDS_STATE) {
+            const cf* sp_ = psi + (size_t)h * C::T;
+            const cf* sl_ = lam + (size_t)h * C::T;
+            for (int i = threadIdx.x; i < C::T; i += NT) {
+              tpp[i] = sp_[i];
+              tqq[i] = sl_[i];
+            }
+            __syncthreads();
+          }
+          static_for<0, C::NGRP>([&](auto gc) {
+            constexpr int gi = C::NGRP - 1 - decltype(gc)::value;
+            constexpr int g0 = 3 * gi;
+            constexpr int NB = (C::TB - g0) < 3 ? (C::TB - g0) : 3;
+            constexpr int ACT = C::T >> NB;
+            for (int t = threadIdx.x; t < ACT; t += NT) {
+              const int base = ins_bits<g0, NB>(t);
+              cf p[1 << NB], m[1 << NB];
+#pragma unroll
+              for (int j = 0; j < (1 << NB); ++j) {
+                p[j] = tpp[base | (j << g0)];
+                m[j] = tqq[base | (j << g0)];
+              }
+#pragma unroll
+              for (int bb = 0; bb < NB; ++bb) {
+                const int b = NB - 1 - bb;
+                const float4 tg = trig[g0 + b];
+#pragma unroll
+                for (int j = 0; j < (1 << NB); ++j)
+                  if (!((j >> b) & 1))
+                    gate_adj(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[g0 + b], dph[g0 + b]);
+              }
+#pragma unroll
+              for (int j = 0; j < (1 << NB); ++j) {
+                tpp[base | (j << g0)] = p[j];
+                tqq[base | (j << g0)] = m[j];
+              }
+            }
+            __syncthreads();
+          });
+          if constexpr (!C::LDS_STATE) {
+            if (l > 0) {  // after layer 0 nothing reads the state again
+              cf* dp_ = psi + (size_t)h * C::T;
+              cf* dl_ = lam + (size_t)h * C::T;
+              for (int i = threadIdx.x; i < C::T; i += NT) {
+                dp_[i] = tpp[i];
+                dl_[i] = tqq[i];
+              }
+            }
+            __syncthreads();
+          }
+        }
+        float v[2 * C::TB];
+#pragma unroll
+        for (int q = 0; q < C::TB; ++q) {
+          v[2 * q] = dth[q];
+          v[2 * q + 1] = dph[q];
+        }
+        block_add<2 * C::TB>(v, red, gdst, 0);
       }
     }
+    // layer 0: theta grads are this sample's d(angles); fold the scratch into the slab accumulators
+    if (threadIdx.x < N) {
+      dx[(size_t)s * N + threadIdx.x] = tmp[2 * threadIdx.x];
+      acc[2 * threadIdx.x] += tmp[2 * threadIdx.x];
+      acc[2 * threadIdx.x + 1] += tmp[2 * threadIdx.x + 1];
+    }
+    __syncthreads();
   }
   __syncthreads();
   for (int i = threadIdx.x; i < P; i += NT) slab[(size_t)blockIdx.x * P + i] = acc[i];
+}
+
+template <int N>
+static size_t smem_bytes(bool backward) {
+  using C = G<N>;
+  if (C::LDS_STATE) return O_DATA + (backward ? 4 : 2) * sizeof(cf) * C::D;
+  return O_DATA + (backward ? 2 : 1) * sizeof(cf) * C::T;
+}
+
+template <int N>
+static int launch(bool backward, const float* x, const float* w, const float* gE, float* E_or_dx, float* slab, int B,
+                  int L, int wgroup, cf* ws, int grid, hipStream_t st) {
+  const size_t sm = smem_bytes<N>(backward);
+  if (!G<N>::LDS_STATE && ws == nullptr) return (int)hipErrorInvalidValue;
+  if (backward) {
+    if (hipError_t e = allow_lds(qsim_big_bwd_kernel<N>, sm)) return (int)e;
+    hipLaunchKernelGGL(qsim_big_bwd_kernel<N>, dim3(grid), dim3(NT), sm, st, x, w, gE, E_or_dx, slab, B, L, wgroup, ws);
+  } else {
+    if (hipError_t e = allow_lds(qsim_big_fwd_kernel<N>, sm)) return (int)e;
+    hipLaunchKernelGGL(qsim_big_fwd_kernel<N>, dim3(grid), dim3(NT), sm, st, x, w, E_or_dx, B, L, wgroup, ws);
+  }
+  return (int)hipGetLastError();
 }
 
 }  // namespace qsimbig
@@ -230,39 +462,40 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
 
 using namespace qd::qsimbig;
 
-// Workspace (bytes) the large-n kernels need for a given grid when the state does not fit LDS.
-static bool fwd_lds(int n) { return 512 + 2 * (size_t(8) << n) <= 160 * 1024; }
-static bool bwd_lds(int n) { return 2048 + 4 * (size_t(8) << n) <= 160 * 1024; }
+#define QD_BIG_DISPATCH(n, CALL)            \
+  switch (n) {                              \
+    case 11: return CALL(11);               \
+    case 12: return CALL(12);               \
+    case 13: return CALL(13);               \
+    case 14: return CALL(14);               \
+    case 15: return CALL(15);               \
+    case 16: return CALL(16);               \
+    default: return (int)hipErrorInvalidValue; \
+  }
 
+// Workspace (bytes) for a given grid: zero when the state is LDS-resident (n <= 12).
 QD_API long long qd_qsim_big_workspace(int n, int grid, int backward) {
-  if (backward) return bwd_lds(n) ? 0 : (long long)grid * 4 * (8ll << n);
-  return fwd_lds(n) ? 0 : (long long)grid * 2 * (8ll << n);
+  if (n <= 12) return 0;
+  return (long long)grid * (backward ? 4 : 2) * (8ll << n);
 }
 
-QD_API int qd_qsim_big_grid(int B) { return B < 1024 ? B : 1024; }
+// Workgroups (= slab rows of the backward) for a batch of B: one sample in flight per workgroup.
+QD_API int qd_qsim_big_grid(int B) { return B < 512 ? B : 512; }
 
 QD_API int qd_qsim_big_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
                            void* stream) {
-  if (n < 2 || n > 16 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
+  if (B < 1 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
   const int grid = qd_qsim_big_grid(B);
-  const int lds = fwd_lds(n);
-  if (!lds && ws == nullptr) return (int)hipErrorInvalidValue;
-  const size_t sm = lds ? 512 + 2 * (size_t(8) << n) : 512;
-  if (hipError_t e = qd::allow_lds(qsim_big_fwd_kernel, sm)) return (int)e;
-  hipLaunchKernelGGL(qsim_big_fwd_kernel, dim3(grid), dim3(NT), sm, (hipStream_t)stream, x, w, E, B, n, L, wgroup,
-                     (cf*)ws, lds);
-  return (int)hipGetLastError();
+#define CALL_F(NN) launch<NN>(false, x, w, nullptr, E, nullptr, B, L, wgroup, (cf*)ws, grid, (hipStream_t)stream)
+  QD_BIG_DISPATCH(n, CALL_F)
+#undef CALL_F
 }
 
 QD_API int qd_qsim_big_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n, int L,
                            int wgroup, void* ws, void* stream) {
-  if (n < 2 || n > 16 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
+  if (B < 1 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
   const int grid = qd_qsim_big_grid(B);
-  const int lds = bwd_lds(n);
-  if (!lds && ws == nullptr) return (int)hipErrorInvalidValue;
-  const size_t sm = lds ? 2048 + 4 * (size_t(8) << n) : 2048;
-  if (hipError_t e = qd::allow_lds(qsim_big_bwd_kernel, sm)) return (int)e;
-  hipLaunchKernelGGL(qsim_big_bwd_kernel, dim3(grid), dim3(NT), sm, (hipStream_t)stream, x, w, gE, dx, slab, B, n, L,
-                     wgroup, (cf*)ws, lds);
-  return (int)hipGetLastError();
+#define CALL_B(NN) launch<NN>(true, x, w, gE, dx, slab, B, L, wgroup, (cf*)ws, grid, (hipStream_t)stream)
+  QD_BIG_DISPATCH(n, CALL_B)
+#undef CALL_B
 }

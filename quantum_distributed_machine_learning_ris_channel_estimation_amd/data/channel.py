@@ -86,9 +86,12 @@ SHARED_POWERS_DB = (-2.0, -3.0)
 # ``sub_spread_deg`` / ``sub_delay_spread``), each with its own random phase per sample -- more
 # degrees of freedom per user, like the many rays of a ray-traced scene.  ``user_drift_deg``: per
 # sample, ALL angles of a user shift together by U(-1, 1) * drift (position along the user row).
+# ``user_los_deg``: LoS angle of each user (scenario 0); ``user_tilt_db``: how strongly a user's
+# position re-weights the scatterers.  Users whose statistics differ a lot interact badly with the
+# reference's per-stream BatchNorm (train-mode statistics per user vs one running average at eval).
 GEO = dict(angle_jitter_deg=0.1, delay_jitter=0.01, los_jitter_deg=0.5, block_prob=0.1, block_db=15.0,
            n_sub=1, sub_spread_deg=0.0, sub_delay_spread=0.0, user_drift_deg=0.0, amp_jitter=0.1,
-           user_tilt_db=3.0)
+           user_tilt_db=3.0, user_los_deg=(-25.0, 5.0, 30.0))
 CHANNEL_MODEL = "geometric"
 
 
@@ -185,7 +188,7 @@ def generate_channels_geometric(n: int, scenario: int, user: int, seed: int, dev
         ph = 2 * math.pi * torch.rand(b, K * ns, generator=g, device=device)
         if spec.los:
             Kf = 10 ** (spec.k_factor_db / 10)
-            la = USER_MEAN_ANGLE_DEG[user] + cfg["los_jitter_deg"] * (2 * torch.rand(b, 1, generator=g, device=device) - 1) + drift
+            la = cfg["user_los_deg"][user] + cfg["los_jitter_deg"] * (2 * torch.rand(b, 1, generator=g, device=device) - 1) + drift
             ld = 0.2 * torch.rand(b, 1, generator=g, device=device)
             ang = torch.cat([la, ang], 1)
             tau = torch.cat([ld, tau], 1)

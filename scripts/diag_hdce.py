@@ -43,12 +43,14 @@ def main():
         r = Y2HRunner(n_epochs=a.epochs, data_len=dl, workspace=ws)
         m = r.train_Conv_Linear_of_HDCE()
         tr, va = r.device_stores()
-        idx = torch.arange(0, 256, device=tr.Yp.device)
+        idx = torch.arange(0, min(256, tr.n, va.n), device=tr.Yp.device)
         # the torch (non-HIP) train-mode path recomputes batch statistics exactly as the HIP kernels do
-        rec = {"data_len": dl,
-               "train_batch_trainmode_db": round(10 * math.log10(nmse_on(m, tr, idx, True)), 2),
-               "train_batch_evalmode_db": round(10 * math.log10(nmse_on(m, tr, idx, False)), 2),
-               "val_batch_evalmode_db": round(10 * math.log10(nmse_on(m, va, idx[:min(256, va.n)], False)), 2),
+        db = lambda v: round(10 * math.log10(v), 2)
+        ev_tr, ev_va = nmse_on(m, tr, idx, False), nmse_on(m, va, idx, False)   # eval first: train mode
+        rec = {"data_len": dl,                                                   # updates running stats
+               "train_batch_evalmode_db": db(ev_tr), "val_batch_evalmode_db": db(ev_va),
+               "train_batch_trainmode_db": db(nmse_on(m, tr, idx, True)),
+               "val_batch_trainmode_db": db(nmse_on(m, va, idx, True)),
                "val_curve_db": [round(10 * math.log10(v), 2) for v in r.val_HDCE_nmse],
                "train_loss_db": [round(10 * math.log10(v), 2) for v in r.train_HDCE_losses]}
         print(json.dumps(rec), flush=True)

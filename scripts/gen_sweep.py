@@ -16,12 +16,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 VARIANTS = {
     "v3": {},
-    "sub4": dict(n_sub=4, sub_spread_deg=1.5, sub_delay_spread=0.3),
-    "sub4_drift2": dict(n_sub=4, sub_spread_deg=1.5, sub_delay_spread=0.3, user_drift_deg=2.0),
-    "sub6_drift3": dict(n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, user_drift_deg=3.0),
-    "drift2": dict(user_drift_deg=2.0),
-    "sub4_block": dict(n_sub=4, sub_spread_deg=1.5, sub_delay_spread=0.3, block_prob=0.2, block_db=30.0,
-                       user_tilt_db=0.0),
+    "same_users": dict(user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0)),
+    "same_users_los8": dict(user_tilt_db=0.0, user_los_deg=(-8.0, 0.0, 8.0), los_jitter_deg=2.0),
+    "same_users_drift": dict(user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0), user_drift_deg=2.0),
+    "same_users_sub4": dict(user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0), n_sub=4, sub_spread_deg=1.5,
+                            sub_delay_spread=0.3),
+    "tilt1": dict(user_tilt_db=1.0, user_los_deg=(-5.0, 0.0, 5.0)),
 }
 
 
