@@ -91,7 +91,9 @@ SHARED_POWERS_DB = (-2.0, -3.0)
 # reference's per-stream BatchNorm (train-mode statistics per user vs one running average at eval).
 GEO = dict(angle_jitter_deg=0.1, delay_jitter=0.01, los_jitter_deg=0.5, block_prob=0.1, block_db=15.0,
            n_sub=1, sub_spread_deg=0.0, sub_delay_spread=0.0, user_drift_deg=0.0, amp_jitter=0.1,
-           user_tilt_db=3.0, user_los_deg=(-25.0, 5.0, 30.0))
+           user_tilt_db=3.0, user_los_deg=(-25.0, 5.0, 30.0), own_db=0.0)
+# ``own_db``: power offset of the scenario-specific scatterers of the scenarios that also see the
+# shared ones (1, 2): lower = weaker scenario signature, harder classification at low SNR.
 CHANNEL_MODEL = "geometric"
 
 
@@ -153,6 +155,7 @@ def generate_channels_geometric(n: int, scenario: int, user: int, seed: int, dev
     angs, dls, pws = list(spec.angles_deg), list(spec.delays), list(spec.powers_db)
     n_own = len(angs)
     if spec.shared:
+        pws = [p + cfg["own_db"] for p in pws]
         angs += list(SHARED_ANGLES_DEG)
         dls += list(SHARED_DELAYS)
         pws += list(SHARED_POWERS_DB)

@@ -104,13 +104,16 @@ class QSC_P128(nn.Module):
     weights (straight-through), and the master weights are never mutated.
     On-chip gradient pruning (E:205-228) zeroes every gradient with |g| <= threshold
     for ALL parameters (classical included), as the reference does.
+    ``use_quantum=False`` selects ``classical_fallback`` (referenced at E:168-170 but never
+    defined there): Linear(n, n) + Tanh in place of the VQC, an equal-width classical ablation
+    with the same (-1, 1) output range as <Z_i>.
     """
 
     def __init__(self, n_qubits: int = 6, n_layers: int = 3, n_classes: int = 3, use_quantumnat: bool = True,
                  use_gradient_pruning: bool = True, pilot_num: int = 128, backend: Optional[str] = None,
-                 noise_level: float = 0.01, gradient_threshold: float = 0.1):
+                 noise_level: float = 0.01, gradient_threshold: float = 0.1, use_quantum: bool = True):
         super().__init__()
-        self.use_quantum = True
+        self.use_quantum = use_quantum
         self.num_qubits = n_qubits
         self.n_layers = n_layers
         self.n_classes = n_classes
@@ -135,6 +138,8 @@ class QSC_P128(nn.Module):
             nn.Tanh(),
         )
         self.classifier = nn.Linear(n_qubits, n_classes)
+        if not use_quantum:
+            self.classical_fallback = nn.Sequential(nn.Linear(n_qubits, n_qubits), nn.Tanh())
 
     def quantum_weights(self, generator: Optional[torch.Generator] = None) -> torch.Tensor:
         w = self.qlayer.weights
@@ -145,7 +150,10 @@ class QSC_P128(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         angles = self.preprocess(x)
-        xq = self.qlayer(angles, self.quantum_weights())
+        if self.use_quantum:
+            xq = self.qlayer(angles, self.quantum_weights())
+        else:
+            xq = self.classical_fallback(angles)
         return F.log_softmax(self.classifier(xq), dim=1)
 
     @torch.no_grad()

@@ -344,13 +344,14 @@ class ClassifierStep:
         self.skip = skip if skip is not None else torch.zeros(1, device=dev0, dtype=torch.float32)
         self.hip = None
         dev = next(model.parameters()).device
-        if isinstance(model, QSC_P128) and dev.type == "cuda" and space is not None and batch_total:
+        if (isinstance(model, QSC_P128) and model.use_quantum and dev.type == "cuda" and space is not None
+                and batch_total):
             from ..ops.qsc import QSCStepHIP
             self.hip = QSCStepHIP(model, space, batch_total, n_groups=n_streams)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         m = self.model
-        if isinstance(m, QSC_P128):
+        if isinstance(m, QSC_P128) and m.use_quantum:
             angles = m.preprocess(x)
             w = m.qlayer.weights
             if m.training and m.use_quantumnat and m.noise_level > 0:

@@ -14,14 +14,17 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+_SAME = dict(user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0))
+_SUB4 = dict(n_sub=4, sub_spread_deg=1.5, sub_delay_spread=0.3)
+_BLK = dict(block_prob=0.16, block_db=40.0)
 VARIANTS = {
     "v3": {},
-    "same_users": dict(user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0)),
-    "same_users_los8": dict(user_tilt_db=0.0, user_los_deg=(-8.0, 0.0, 8.0), los_jitter_deg=2.0),
-    "same_users_drift": dict(user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0), user_drift_deg=2.0),
-    "same_users_sub4": dict(user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0), n_sub=4, sub_spread_deg=1.5,
-                            sub_delay_spread=0.3),
-    "tilt1": dict(user_tilt_db=1.0, user_los_deg=(-5.0, 0.0, 5.0)),
+    "same_users": dict(_SAME),
+    "v4a": dict(_SAME, **_SUB4, **_BLK),
+    "v4b": dict(_SAME, **_SUB4, **_BLK, own_db=-4.0),
+    "v4c": dict(_SAME, n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, **_BLK, own_db=-4.0),
+    "v4d": dict(_SAME, **_BLK, own_db=-4.0),
+    "v4e": dict(_SAME, n_sub=8, sub_spread_deg=3.0, sub_delay_spread=0.6, **_BLK, own_db=-6.0),
 }
 
 
@@ -29,7 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=30)
     ap.add_argument("--sc-epochs", type=int, default=8)
-    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--variants", default=",".join(k for k in VARIANTS if k.startswith("v4")))
     ap.add_argument("--test-len", type=int, default=3000)
     ap.add_argument("--out", default="gpurun_out/gen_sweep")
     a = ap.parse_args()

@@ -85,3 +85,19 @@ def test_nmse_is_batch_global_ratio():
     expect = (0.01 + 0.04) / 30.0
     assert abs(NMSE_cuda(xh, x).item() - expect) < 1e-7
     assert abs(NMSELoss()(xh, x).item() - expect) < 1e-7
+
+
+def test_qsc_classical_fallback_ablation():
+    """use_quantum=False runs the classical_fallback the reference references (E:168-170); the
+    default quantum model keeps the reference state_dict keys."""
+    import torch
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.models.estimators import QSC_P128
+    q = QSC_P128(n_qubits=4)
+    assert not any(k.startswith("classical_fallback") for k in q.state_dict())
+    c = QSC_P128(n_qubits=4, use_quantum=False)
+    assert "classical_fallback.0.weight" in c.state_dict()
+    x = torch.randn(5, 2, 16, 8)
+    out = c(x)
+    assert out.shape == (5, 3) and torch.allclose(out.exp().sum(1), torch.ones(5), atol=1e-5)
+    out.sum().backward()
+    assert c.classical_fallback[0].weight.grad is not None and c.qlayer.weights.grad is None
