@@ -163,11 +163,18 @@ def generate_channels_geometric(n: int, scenario: int, user: int, seed: int, dev
     # user-dependent visibility of the scatterers
     upw = torch.tensor(pws, device=device) - cfg["user_tilt_db"] * (
         torch.arange(K, device=device) - user * (K - 1) / 2).abs() / max(K - 1, 1)
-    # fixed sub-ray geometry of this (scenario, user): a property of the scene, not of the sample
+    # fixed sub-ray geometry: a property of each scatterer (the shared scatterers look the same from
+    # every scenario that sees them), not of the sample
     ns = int(cfg["n_sub"])
-    gs = _gen(seed_for("geo-sub", scenario, user), torch.device("cpu"))
-    sub_a = (cfg["sub_spread_deg"] * torch.randn(K, ns, generator=gs)).to(device) if ns > 1 else torch.zeros(K, 1, device=device)
-    sub_d = (cfg["sub_delay_spread"] * torch.rand(K, ns, generator=gs)).to(device) if ns > 1 else torch.zeros(K, 1, device=device)
+    sub_a = torch.zeros(K, ns)
+    sub_d = torch.zeros(K, ns)
+    if ns > 1:
+        for j in range(K):
+            key = ("geo-sub", scenario, j) if j < n_own else ("geo-sub-shared", j - n_own)
+            gs = _gen(seed_for(*key), torch.device("cpu"))
+            sub_a[j] = cfg["sub_spread_deg"] * torch.randn(ns, generator=gs)
+            sub_d[j] = cfg["sub_delay_spread"] * torch.rand(ns, generator=gs)
+    sub_a, sub_d = sub_a.to(device), sub_d.to(device)
     out = torch.empty(n, H_DIM, dtype=torch.complex64, device=device)
     base_a = torch.tensor(angs, device=device)
     base_d = torch.tensor(dls, device=device)

@@ -25,6 +25,11 @@ VARIANTS = {
     "v4c": dict(_SAME, n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, **_BLK, own_db=-4.0),
     "v4d": dict(_SAME, **_BLK, own_db=-4.0),
     "v4e": dict(_SAME, n_sub=8, sub_spread_deg=3.0, sub_delay_spread=0.6, **_BLK, own_db=-6.0),
+    "v5a": dict(_SAME, **_SUB4, **_BLK, own_db=-8.0, angle_jitter_deg=0.05),
+    "v5b": dict(_SAME, n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, **_BLK, own_db=-8.0, angle_jitter_deg=0.05),
+    "v5c": dict(_SAME, n_sub=8, sub_spread_deg=3.0, sub_delay_spread=0.6, **_BLK, own_db=-10.0, angle_jitter_deg=0.05),
+    "v5d": dict(_SAME, **_BLK, own_db=-10.0),
+    "v5e": dict(_SAME, n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, **_BLK, own_db=-12.0, angle_jitter_deg=0.05),
 }
 
 
@@ -32,7 +37,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--epochs", type=int, default=30)
     ap.add_argument("--sc-epochs", type=int, default=8)
-    ap.add_argument("--variants", default=",".join(k for k in VARIANTS if k.startswith("v4")))
+    ap.add_argument("--variants", default=",".join(k for k in VARIANTS if k.startswith("v5")))
     ap.add_argument("--test-len", type=int, default=3000)
     ap.add_argument("--out", default="gpurun_out/gen_sweep")
     a = ap.parse_args()
