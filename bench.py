@@ -35,7 +35,8 @@ def main() -> int:
     ap.add_argument("--pilot", type=int, default=128, choices=[128, 256], help="Pilot_num (P128 / P256 configs)")
     ap.add_argument("--layers", type=int, default=3, help="QNN layers")
     ap.add_argument("--data-len", type=int, default=20000)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="estimator compute dtype (fp8: e4m3 FC forward GEMM, bf16 convs/backward)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-quantumnat", action="store_true")
     ap.add_argument("--split-graphs", action="store_true", help="3-graph DP plan even at 1 GPU")

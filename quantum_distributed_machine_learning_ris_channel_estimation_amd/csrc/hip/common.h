@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <hip/hip_fp8.h>
 #include <stdint.h>
 #include <type_traits>
 
@@ -62,6 +63,22 @@ inline hipError_t allow_lds(K kernel, size_t bytes) {
   if (bytes <= 65536) return hipSuccess;
   return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)bytes);
+}
+
+// fp32 -> OCP fp8 (gfx950 native formats), saturating to the finite range.
+__device__ __forceinline__ uint8_t f32_to_e4m3(float v) {
+  return (uint8_t)__hip_cvt_float_to_fp8(v, __HIP_SATFINITE, __HIP_E4M3);
+}
+__device__ __forceinline__ uint8_t f32_to_e5m2(float v) {
+  return (uint8_t)__hip_cvt_float_to_fp8(v, __HIP_SATFINITE, __HIP_E5M2);
+}
+
+// Running |x| max of non-negative values as float bits (monotone for x >= 0): one atomic per wave.
+__device__ __forceinline__ void amax_update(unsigned int* amax_bits, float local_absmax) {
+  float m = local_absmax;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(amax_bits, __float_as_uint(m));
 }
 
 }  // namespace qd

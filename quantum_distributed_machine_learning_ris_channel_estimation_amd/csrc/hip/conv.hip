@@ -530,8 +530,14 @@ __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __rest
 
 // h = relu(a z + b) -> bf16 (the FC operand), 8 elements per thread.
 template <int HW>
+// FP8 (fp8 estimator): additionally h8 = e4m3(h * qs[0]) for the fp8 FC GEMM, and amax[0] tracks
+// max(h) for the next step's delayed scale (h >= 0 after the ReLU).
 __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __restrict__ z, const float* __restrict__ st,
-                                                            uint16_t* __restrict__ h, long n8, int EC, int B) {
+                                                            uint16_t* __restrict__ h, long n8, int EC, int B,
+                                                            uint8_t* __restrict__ h8, const float* __restrict__ qs,
+                                                            unsigned int* __restrict__ amax) {
+  const float q = h8 ? qs[0] : 0.f;
+  float mx = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     const long e0 = i * 8;
     const long row = e0 / HW;             // (n, ch)
@@ -543,10 +549,22 @@ __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __re
     load8(z + e0, v);
     uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      w[j] = f32_to_bf16(fmaxf(a * v[2 * j] + b, 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(a * v[2 * j + 1] + b, 0.f)) << 16);
+    for (int j = 0; j < 8; ++j) v[j] = fmaxf(a * v[j] + b, 0.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
     *reinterpret_cast<uint4*>(h + e0) = make_uint4(w[0], w[1], w[2], w[3]);
+    if (h8) {
+      uint32_t p0 = 0, p1 = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mx = fmaxf(mx, fmaxf(v[j], v[j + 4]));
+        p0 |= (uint32_t)f32_to_e4m3(v[j] * q) << (8 * j);
+        p1 |= (uint32_t)f32_to_e4m3(v[j + 4] * q) << (8 * j);
+      }
+      *reinterpret_cast<uint2*>(h8 + e0) = make_uint2(p0, p1);
+    }
   }
+  if (h8) amax_update(amax, mx);
 }
 
 // out[i] += sum_rows slab[g][row][i] for every group g (rows contiguous per group).
@@ -748,15 +766,19 @@ QD_API int qd_bn_bwd_finalize(const float* slab, const float* gamma, float* st, 
   return (int)hipGetLastError();
 }
 
+// h8/qs/amax nullable (fp8 estimator only)
 QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int N, int EC, int B, int HW,
-                            void* stream) {
+                            uint8_t* h8, const float* qs, unsigned int* amax, void* stream) {
   const long n8 = (long)N * EC * HW / 8;
   int grid = (int)((n8 + 255) / 256);
   if (grid > 4096) grid = 4096;
+  if (h8 && (!qs || !amax)) return (int)hipErrorInvalidValue;
   if (HW == 128)
-    hipLaunchKernelGGL((bn_relu_apply_kernel<128>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B);
+    hipLaunchKernelGGL((bn_relu_apply_kernel<128>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B,
+                       h8, qs, amax);
   else if (HW == 256)
-    hipLaunchKernelGGL((bn_relu_apply_kernel<256>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B);
+    hipLaunchKernelGGL((bn_relu_apply_kernel<256>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B,
+                       h8, qs, amax);
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();

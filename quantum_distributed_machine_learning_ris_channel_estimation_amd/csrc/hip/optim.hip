@@ -27,8 +27,11 @@ struct AdamArgs {
 };
 
 struct Shadow {
-  uint16_t* out;  // bf16 copy of p[lo, hi) (lo, hi multiples of 4), or null
+  uint16_t* out;        // bf16 copy of p[lo, hi) (lo, hi multiples of 4), or null
   long lo, hi;
+  uint8_t* out8;        // optional e4m3 copy of the same range, scaled by *qs (fp8 estimator)
+  const float* qs;
+  unsigned int* amax;   // running max |p| over the range (next step's delayed scale)
 };
 
 // Called by every thread at the end of the kernel: the last workgroup to get here increments the
@@ -51,7 +54,7 @@ __device__ __forceinline__ void tick_if_last(float* step, unsigned int* done) {
   }
 }
 
-__device__ __forceinline__ void store_shadow(const Shadow& sh, long i0, float4 v) {
+__device__ __forceinline__ float store_shadow(const Shadow& sh, long i0, float4 v) {
   if (sh.out != nullptr && i0 >= sh.lo && i0 < sh.hi) {
     ushort4 h;
     h.x = f32_to_bf16(v.x);
@@ -59,7 +62,15 @@ __device__ __forceinline__ void store_shadow(const Shadow& sh, long i0, float4 v
     h.z = f32_to_bf16(v.z);
     h.w = f32_to_bf16(v.w);
     *reinterpret_cast<ushort4*>(sh.out + (i0 - sh.lo)) = h;
+    if (sh.out8 != nullptr) {
+      const float q = *sh.qs;
+      const uint32_t p = (uint32_t)f32_to_e4m3(v.x * q) | ((uint32_t)f32_to_e4m3(v.y * q) << 8) |
+                         ((uint32_t)f32_to_e4m3(v.z * q) << 16) | ((uint32_t)f32_to_e4m3(v.w * q) << 24);
+      *reinterpret_cast<uint32_t*>(sh.out8 + (i0 - sh.lo)) = p;
+      return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    }
   }
+  return 0.f;
 }
 
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ g,
@@ -76,6 +87,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
   const float step_size = lr / bc1;
   const float rbc2 = rsqrtf(bc2);
   unsigned int cnt = 0;
+  float wmax = 0.f;
   const long stride = (long)gridDim.x * blockDim.x * 4;
   for (long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < n; i0 += stride) {
     if (i0 + 3 < n) {
@@ -98,7 +110,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         ga[j] = gj;
       }
       *reinterpret_cast<float4*>(p + i0) = pp;
-      store_shadow(sh, i0, pp);
+      wmax = fmaxf(wmax, store_shadow(sh, i0, pp));
       *reinterpret_cast<float4*>(m + i0) = mm;
       *reinterpret_cast<float4*>(v + i0) = vv;
       if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
@@ -114,7 +126,13 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         const float denom = sqrtf(v[i]) * rbc2 + a.eps;
         p[i] = pj - step_size * m[i] / denom;
         g[i] = gj;
-        if (sh.out != nullptr && i >= sh.lo && i < sh.hi) sh.out[i - sh.lo] = f32_to_bf16(p[i]);
+        if (sh.out != nullptr && i >= sh.lo && i < sh.hi) {
+          sh.out[i - sh.lo] = f32_to_bf16(p[i]);
+          if (sh.out8 != nullptr) {
+            sh.out8[i - sh.lo] = f32_to_e4m3(p[i] * *sh.qs);
+            wmax = fmaxf(wmax, fabsf(p[i]));
+          }
+        }
       }
     }
   }
@@ -123,6 +141,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     float c = wave_sum((float)cnt);
     if ((threadIdx.x & 63) == 0 && c > 0.f) atomicAdd(pruned, (unsigned int)c);
   }
+  if (sh.out8 != nullptr) amax_update(sh.amax, wmax);
   tick_if_last(step_out, done);
 }
 
@@ -143,6 +162,21 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
   tick_if_last(step_out, done);
 }
 
+// Delayed per-tensor fp8 scaling: scale = amax / (fmax / 2^margin) (dequantisation factor fed to
+// the GEMM), qs = 1 / scale (quantisation factor used by the producers), amax re-armed.
+__global__ void fp8_scale_update_kernel(unsigned int* amax, float* scale, float* qs, int n, float fmax, float margin) {
+  const int i = threadIdx.x;
+  if (i < n) {
+    const float a = __uint_as_float(amax[i]);
+    if (a > 0.f) {   // keep the previous scale if the tensor was not produced this step
+      const float s = fmaxf(a, 1e-30f) * exp2f(margin) / fmax;
+      scale[i] = s;
+      qs[i] = 1.f / s;
+    }
+    amax[i] = 0u;
+  }
+}
+
 inline int grid_for(long n) {
   long b = (n / 4 + 255) / 256;
   if (b < 1) b = 1;
@@ -156,15 +190,17 @@ inline int grid_for(long n) {
 using namespace qd::optim;
 
 // done: device uint32 counter, zero-initialised once (re-armed by the kernel).
-// shadow: optional bf16 copy of p[lo, hi) (lo, hi multiples of 4), written with the update.
+// shadow: optional bf16 copy of p[lo, hi) (lo, hi multiples of 4), written with the update;
+// shadow8/qs/amax: optional e4m3 copy of the same range (fp8 estimator).
 QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const float* skip,
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
                         float grad_scale, float prune_thr, unsigned int* done, uint16_t* shadow, long shadow_lo,
-                        long shadow_hi, void* stream) {
+                        long shadow_hi, uint8_t* shadow8, const float* qs, unsigned int* amax, void* stream) {
   if (n <= 0 || done == nullptr || (shadow && ((shadow_lo | shadow_hi) & 3))) return (int)hipErrorInvalidValue;
+  if (shadow8 && (!shadow || !qs || !amax)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   AdamArgs a{beta1, beta2, eps, weight_decay, grad_scale, prune_thr, decoupled};
-  Shadow sh{shadow, shadow_lo, shadow_hi};
+  Shadow sh{shadow, shadow_lo, shadow_hi, shadow8, qs, amax};
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step,
                      done, sh);
   return (int)hipGetLastError();
@@ -176,5 +212,13 @@ QD_API int qd_sgd_step(float* p, float* g, float* buf, long n, const float* lr, 
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n * 4)), dim3(256), 0, st, p, g, buf, n, lr, step, skip, momentum,
                      weight_decay, grad_scale, step, done);
+  return (int)hipGetLastError();
+}
+
+QD_API int qd_fp8_scale_update(unsigned int* amax, float* scale, float* qs, int n, float fmax, float margin,
+                               void* stream) {
+  if (n < 1 || n > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(fp8_scale_update_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, amax, scale, qs, n, fmax,
+                     margin);
   return (int)hipGetLastError();
 }

@@ -16,14 +16,15 @@ Test.py:7) but does not ship it, nor the DeepMIMO-derived ``available_data/*.npy
 * ``Hperf`` is the noiseless channel.
 
 Propagation: multipath H[m, f] = sum_p a_p e^{-j pi m sin(theta_p)} e^{-j 2 pi f tau_p / 16},
-per-sample normalised to unit mean power.  Default model ("geometric", v3): like a ray-traced
-DeepMIMO scene, each scenario has a FIXED environment -- its scatterers' angles of arrival
-and excess delays at the RIS are fixed (+-0.1 deg / 0.01 jitter for position dependence),
-scenario 0 adds a user-position-dependent LoS ray (Rician K = 6 dB), scenarios 1 and 2 share
-two scatterers and with probability 0.1 their own scatterers are blocked (-15 dB), which
+per-sample normalised to unit mean power.  Default model ("geometric"): like a ray-traced
+DeepMIMO scene, each scenario has a FIXED environment -- its scatterers (each a cluster of
+sub-rays) sit at fixed angles of arrival / excess delays at the RIS (small jitter for position
+dependence), scenario 0 adds a LoS ray (Rician K = 6 dB), scenarios 1 and 2 share two
+scatterers and a fraction of their samples has the scenario-specific scatterers blocked, which
 makes those samples genuinely ambiguous for the scenario classifier (the reference's SC
-accuracy saturates near 0.95).  Users (3 per scenario) differ in LoS angle and in which
-scatterers they see strongly; path phases and +-10% amplitudes are random per sample.
+accuracy saturates near 0.945).  The 3 users of a scenario are statistically alike (the
+reference's per-stream BatchNorm punishes users with different statistics, see README);
+path phases and +-10% amplitudes are random per sample.  Knobs: ``GEO``.
 The alternative "cluster" model (v1: random cluster centre / spread / delays per sample) is
 kept for comparison: its best linear estimator from the pilots only reaches ~-1.5 dB NMSE
 (see reports/r1_gen_v1), i.e. it is not learnable from 128 pilots.
@@ -89,9 +90,15 @@ SHARED_POWERS_DB = (-2.0, -3.0)
 # ``user_los_deg``: LoS angle of each user (scenario 0); ``user_tilt_db``: how strongly a user's
 # position re-weights the scatterers.  Users whose statistics differ a lot interact badly with the
 # reference's per-stream BatchNorm (train-mode statistics per user vs one running average at eval).
-GEO = dict(angle_jitter_deg=0.1, delay_jitter=0.01, los_jitter_deg=0.5, block_prob=0.1, block_db=15.0,
-           n_sub=1, sub_spread_deg=0.0, sub_delay_spread=0.0, user_drift_deg=0.0, amp_jitter=0.1,
-           user_tilt_db=3.0, user_los_deg=(-25.0, 5.0, 30.0), own_db=0.0)
+# Defaults = the calibrated "v5c" scene (scripts/gen_sweep.py; reports/r1_gen_v5): 8 sub-rays per
+# scatterer, statistically alike users, 16% of the scenario-1/2 samples blocked down to the shared
+# scatterers (ambiguous between those scenarios), scenario-specific scatterers 10 dB below the
+# shared ones.  GEO_V3 keeps the first geometric calibration for comparison.
+GEO_V3 = dict(angle_jitter_deg=0.1, delay_jitter=0.01, los_jitter_deg=0.5, block_prob=0.1, block_db=15.0,
+              n_sub=1, sub_spread_deg=0.0, sub_delay_spread=0.0, user_drift_deg=0.0, amp_jitter=0.1,
+              user_tilt_db=3.0, user_los_deg=(-25.0, 5.0, 30.0), own_db=0.0)
+GEO = dict(GEO_V3, angle_jitter_deg=0.05, block_prob=0.16, block_db=40.0, n_sub=8, sub_spread_deg=3.0,
+           sub_delay_spread=0.6, user_tilt_db=0.0, user_los_deg=(-2.0, 0.0, 2.0), own_db=-10.0)
 # ``own_db``: power offset of the scenario-specific scatterers of the scenarios that also see the
 # shared ones (1, 2): lower = weaker scenario signature, harder classification at low SNR.
 CHANNEL_MODEL = "geometric"

@@ -45,6 +45,8 @@ class ConvStackHIP:
         bf = torch.bfloat16
         self.z = [torch.empty(N, EC, HW, device=dev, dtype=bf) for _ in range(3)]
         self.h3 = torch.empty(N * self.E, 32 * HW, device=dev, dtype=bf)
+        self.fp8 = getattr(model, "fp8", False)
+        self.h3_8 = torch.empty(N * self.E, 32 * HW, device=dev, dtype=torch.float8_e4m3fn) if self.fp8 else None
         self.st = [torch.zeros(U, EC, NST, device=dev) for _ in range(3)]
         self.stats = torch.zeros(U, self.chunks, EC, 2, device=dev)
         self.rslab = torch.zeros(U, self.chunks_r, EC, 2, device=dev)
@@ -62,7 +64,7 @@ class ConvStackHIP:
         self._fin = nat.fn(L, "qd_bn_stats_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i, _p])
         self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _p])
-        self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p])
+        self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
         self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
 
@@ -91,8 +93,10 @@ class ConvStackHIP:
                                 nat.ptr(m.run_var[k]), nat.ptr(self.st[k]), self.U, self.chunks, self.EC,
                                 float(self.B * self.HW), m.momentum, m.eps, int(training), st), f"bn_fin{k + 1}")
             inp, st_prev = self.z[k], self.st[k]
+        f8 = self.m.fp8_scales if self.fp8 else None
         nat.check(self._apply(nat.ptr(self.z[2]), nat.ptr(self.st[2]), nat.ptr(self.h3), self.N, self.EC, self.B,
-                              self.HW, st), "bn_relu_apply")
+                              self.HW, _ptr(self.h3_8), nat.ptr(f8.qs) if f8 else None,
+                              nat.ptr(f8.amax) if f8 else None, st), "bn_relu_apply")
         return self.h3
 
     # --------------------------------------------------------------------- backward

@@ -71,6 +71,42 @@ class FlatParamSpace:
                 p.grad = self.grad[o:o + p.numel()].view(p.shape)
 
 
+FP8_E4M3_MAX = 448.0
+
+
+class Fp8Scales:
+    """Delayed per-tensor fp8 scaling state for ``n`` tensors (device-resident, graph-safe).
+
+    ``qs[i]`` is the quantisation factor producers multiply by (x8 = e4m3(x * qs)), ``scale[i]`` =
+    1/qs the dequantisation factor handed to the GEMM, ``amax[i]`` the running max |x| (float bits)
+    the producers accumulate; ``update()`` (one launch) turns amax into the next scales."""
+
+    def __init__(self, n: int, device, margin: float = 1.0):
+        self.n, self.margin = n, margin
+        self.amax = torch.zeros(n, device=device, dtype=torch.int32)
+        self.scale = torch.ones(n, device=device, dtype=torch.float32)
+        self.qs = torch.ones(n, device=device, dtype=torch.float32)
+
+    def set_from_tensor(self, i: int, t: torch.Tensor) -> None:
+        a = float(t.detach().abs().max().clamp_min(1e-30))
+        s = a * 2.0 ** self.margin / FP8_E4M3_MAX
+        self.scale[i] = s
+        self.qs[i] = 1.0 / s
+
+    def update(self) -> None:
+        if self.scale.is_cuda:
+            f = nat.fn(nat.hip_lib(), "qd_fp8_scale_update", [_p, _p, _p, _i, _f, _f, _p])
+            nat.check(f(nat.ptr(self.amax), nat.ptr(self.scale), nat.ptr(self.qs), self.n, FP8_E4M3_MAX,
+                        self.margin, nat.stream_ptr(self.scale.device)), "fp8_scale_update")
+            return
+        a = self.amax.view(torch.float32).clone()
+        upd = a > 0
+        s = a.clamp_min(1e-30) * 2.0 ** self.margin / FP8_E4M3_MAX
+        self.scale.copy_(torch.where(upd, s, self.scale))
+        self.qs.copy_(1.0 / self.scale)
+        self.amax.zero_()
+
+
 class FusedOptimizer:
     """Adam / AdamW / SGD-momentum over a FlatParamSpace, one kernel per step.
 
@@ -96,6 +132,9 @@ class FusedOptimizer:
         self.done = torch.zeros(1, device=dev, dtype=torch.int32)   # last-workgroup counter (step tick)
         self.shadow: Optional[torch.Tensor] = None                    # bf16 copy of flat[lo:hi]
         self.shadow_lo = self.shadow_hi = 0
+        self.shadow8: Optional[torch.Tensor] = None                   # e4m3 copy (fp8 estimator)
+        self.fp8: Optional[Fp8Scales] = None
+        self.fp8_slot = 0
         if kind == "sgd":
             self.buf = torch.zeros_like(space.flat)
         else:
@@ -105,19 +144,30 @@ class FusedOptimizer:
         # torch.optim-like view for code that reads/writes param_groups[0]['lr']
         self.param_groups = [_LRGroup(self)]
 
-    def attach_shadow(self, lo: int, hi: int) -> torch.Tensor:
+    def attach_shadow(self, lo: int, hi: int, fp8: Optional[Fp8Scales] = None, fp8_slot: int = 0) -> torch.Tensor:
         """Keep a bf16 copy of flat[lo:hi] up to date with every step (written by the update
-        kernel itself on the GPU).  Returns the shadow, initialised from the current weights."""
+        kernel itself on the GPU).  Returns the shadow, initialised from the current weights.
+        With ``fp8``, an e4m3 copy (``shadow8``, quantised with fp8.qs[fp8_slot]) is kept too and
+        the kernel accumulates max|w| into fp8.amax[fp8_slot]."""
         if lo % 4 or hi % 4:
             raise ValueError("shadow bounds must be multiples of 4")
         self.shadow_lo, self.shadow_hi = lo, hi
         self.shadow = self.space.flat[lo:hi].to(torch.bfloat16)
+        if fp8 is not None:
+            self.fp8, self.fp8_slot = fp8, fp8_slot
+            fp8.set_from_tensor(fp8_slot, self.space.flat[lo:hi])
+            self.shadow8 = torch.empty(hi - lo, device=self.space.flat.device, dtype=torch.float8_e4m3fn)
+        self.refresh_shadow()
         return self.shadow
 
     def refresh_shadow(self) -> None:
         """Re-sync the shadow after the weights were changed outside step() (load, broadcast)."""
         if self.shadow is not None:
-            self.shadow.copy_(self.space.flat[self.shadow_lo:self.shadow_hi])
+            w = self.space.flat[self.shadow_lo:self.shadow_hi]
+            self.shadow.copy_(w)
+            if self.shadow8 is not None:
+                q = self.fp8.qs[self.fp8_slot]
+                self.shadow8.copy_((w * q).clamp(-FP8_E4M3_MAX, FP8_E4M3_MAX).to(torch.float8_e4m3fn))
 
     # ---------------------------------------------------------------- lr
     @property
@@ -144,13 +194,16 @@ class FusedOptimizer:
                     self.refresh_shadow()
             else:
                 f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
-                                                 _p, _p, _l, _l, _p])
+                                                 _p, _p, _l, _l, _p, _p, _p, _p])
+                f8 = self.shadow8 is not None
                 nat.check(f(nat.ptr(s.flat), nat.ptr(s.grad), nat.ptr(self.m), nat.ptr(self.v), s.numel,
                             nat.ptr(self.lr_t), nat.ptr(self.step_t), skp, nat.ptr(self.pruned), self.betas[0],
                             self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
                             self.prune_thr, nat.ptr(self.done),
                             nat.ptr(self.shadow) if self.shadow is not None else None, self.shadow_lo,
-                            self.shadow_hi, st), "adam")
+                            self.shadow_hi, nat.ptr(self.shadow8) if f8 else None,
+                            nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
+                            nat.ptr(self.fp8.amax[self.fp8_slot:]) if f8 else None, st), "adam")
             return
         self._step_host(grad_scale, skip)
         if self.shadow is not None:

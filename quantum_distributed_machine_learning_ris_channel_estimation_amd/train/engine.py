@@ -43,7 +43,9 @@ BN_IDX = [1, 4, 7]
 
 
 def _dtype(name: str) -> torch.dtype:
-    return {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16}[name]
+    # "fp8": the estimator's FC forward GEMM runs in OCP e4m3 (see HDCEModel); the convs and the
+    # backward GEMMs compute in bf16
+    return {"bf16": torch.bfloat16, "fp32": torch.float32, "fp16": torch.float16, "fp8": torch.bfloat16}[name]
 
 
 class HDCEModel:
@@ -56,6 +58,14 @@ class HDCEModel:
         self.E = n_experts
         self.H, self.W = pilot_grid(pilot_num)
         self.compute_dtype = _dtype(dtype) if self.device.type == "cuda" else torch.float32
+        # fp8 estimator: FC forward = e4m3 x e4m3 (hipBLASLt, fp32 accumulate) with delayed per-tensor
+        # scales; slot 0 = activations (quantised by the conv stack's last BN+ReLU kernel), slot 1 =
+        # FC weights (quantised by the optimizer's shadow write)
+        self.fp8 = dtype == "fp8" and self.device.type == "cuda"
+        self.fp8_scales = None
+        if self.fp8:
+            from ..ops.optim import Fp8Scales
+            self.fp8_scales = Fp8Scales(2, self.device)
         self.convs = [Conv_P128(pilot_num).to(self.device) for _ in range(n_experts)]
         self.fc = FC_P128(pilot_num).to(self.device)
         named = []
@@ -97,10 +107,12 @@ class HDCEModel:
         lo = self.space.offsets[self.space.names.index("CE.FC.weight")]
         ob = self.space.offsets[self.space.names.index("CE.FC.bias")]
         hi = ob + self.fc_b.numel()
-        sh = opt.attach_shadow(lo, hi + (-hi) % 4)
+        sh = opt.attach_shadow(lo, hi + (-hi) % 4, fp8=self.fp8_scales, fp8_slot=1)
         self.fc_shadow = sh
         self._shadow_w = sh[:self.fc_w.numel()].view(self.fc_w.shape)
         self._shadow_b = sh[ob - lo:ob - lo + self.fc_b.numel()]
+        if self.fp8:
+            self._shadow_w8 = opt.shadow8[:self.fc_w.numel()].view(self.fc_w.shape)
 
     def fc_weights_lp(self):
         """(W, b) in the compute dtype: the optimizer-maintained shadow, or a fresh cast."""
@@ -178,6 +190,8 @@ class HDCEModel:
 
     def fc_forward(self, a: torch.Tensor) -> torch.Tensor:
         dt = self.compute_dtype
+        if self.fp8:   # evaluation in the training precision: on-the-fly per-tensor e4m3 scales
+            return fp8_linear(a, self.fc_w.detach(), self.fc_b.detach().to(dt))
         return F.linear(a.to(dt), self.fc_w.to(dt), self.fc_b.to(dt))
 
     def features(self, Yp: torch.Tensor, training: bool) -> torch.Tensor:
@@ -302,7 +316,17 @@ class HDCEStep:
         dt = m.compute_dtype
         A = self.conv.forward(x1, training=True)                # (rows, 4096) bf16
         W, b = m.fc_weights_lp()
-        Y = torch.nn.functional.linear(A.to(dt), W, b)
+        if m.fp8 and m.fc_shadow is None:
+            Y = fp8_linear(A, m.fc_w.detach(), b)
+        elif m.fp8:
+            # fp8 forward GEMM: activations quantised by the conv stack's last kernel, weights by the
+            # optimizer (both with the scales of the previous step); then the scales move on
+            sc = m.fp8_scales.scale
+            Y = torch._scaled_mm(self.conv.h3_8, m._shadow_w8.t(), scale_a=sc[0], scale_b=sc[1], bias=b,
+                                 out_dtype=dt)
+            m.fp8_scales.update()
+        else:
+            Y = torch.nn.functional.linear(A.to(dt), W, b)
         loss = self.nmse.sums_finalize(Y, label, perf)
         dY = self.nmse.grad(Y, label, out_dtype=dt)
         _mm_f32(dY.t(), A.to(dt), m.fc_w.grad)               # dW = dY^T A   (fp32 out)
@@ -313,6 +337,16 @@ class HDCEStep:
     @property
     def skip(self) -> torch.Tensor:
         return self.nmse.skip
+
+
+def fp8_linear(a: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a @ w.T + b with both operands quantised to OCP e4m3 (per-tensor scales computed here)."""
+    from ..ops.optim import FP8_E4M3_MAX
+    sa = (a.detach().abs().amax().float().clamp_min(1e-30) * 2.0 / FP8_E4M3_MAX).reshape(())
+    sw = (w.abs().amax().float().clamp_min(1e-30) * 2.0 / FP8_E4M3_MAX).reshape(())
+    a8 = (a.float() / sa).to(torch.float8_e4m3fn)
+    w8 = (w.float() / sw).to(torch.float8_e4m3fn)
+    return torch._scaled_mm(a8, w8.t(), scale_a=sa, scale_b=sw, bias=b, out_dtype=b.dtype)
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> None:

@@ -28,6 +28,7 @@ VARIANTS = {
     "v5a": dict(_SAME, **_SUB4, **_BLK, own_db=-8.0, angle_jitter_deg=0.05),
     "v5b": dict(_SAME, n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, **_BLK, own_db=-8.0, angle_jitter_deg=0.05),
     "v5c": dict(_SAME, n_sub=8, sub_spread_deg=3.0, sub_delay_spread=0.6, **_BLK, own_db=-10.0, angle_jitter_deg=0.05),
+    # (v5c became the default channel.GEO)
     "v5d": dict(_SAME, **_BLK, own_db=-10.0),
     "v5e": dict(_SAME, n_sub=6, sub_spread_deg=2.0, sub_delay_spread=0.5, **_BLK, own_db=-12.0, angle_jitter_deg=0.05),
 }
@@ -44,7 +45,7 @@ def main():
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.data import channel
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.evaluate import model_val
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.runner import Y2HRunner
-    base = dict(channel.GEO)
+    base = dict(channel.GEO_V3)   # variants are stated relative to the first geometric calibration
     os.makedirs(a.out, exist_ok=True)
     for name in a.variants.split(","):
         channel.GEO.clear()

@@ -26,6 +26,8 @@ for s in $STEPS; do
     bench_eager) run bench_eager 600 python bench.py --steps 20 --warmup 5 --no-graphs ;;
     bench_p256) run bench_p256 600 python bench.py --steps 20 --warmup 5 --pilot 256 --qubits 12 ;;
     bench_q16) run bench_q16 600 python bench.py --steps 10 --warmup 3 --qubits 16 ;;
+    bench_fp8) run bench_fp8 600 python bench.py --steps 50 --warmup 10 --dtype fp8 ;;
+    bench_c5) run bench_c5 600 python bench.py --steps 10 --warmup 3 --qubits 16 --dtype fp8 ;;
     train) run train 1200 python scripts/train_eval.py --epochs ${EPOCHS:-100} --qubits 6 --qml-qubits 4,8 --out "$OUT/train" ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" ;;
