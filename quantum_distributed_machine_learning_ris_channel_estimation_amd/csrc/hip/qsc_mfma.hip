@@ -1,0 +1,468 @@
+// QSC preprocess CNN on fp32 MFMA: one wave per sample, no workgroup barriers in the sample loop.
+//
+// Reference: QSC_P128.preprocess (Estimators_QuantumNAT_onchipQNN.py:152-162)
+//   Conv2d(2,16,3,p=1) -> ReLU -> MaxPool2 -> Conv2d(16,32,3,p=1) -> ReLU -> MaxPool2 -> Flatten
+//   -> Linear(F, n) -> Tanh          (F = 32 * H/4 * W/4: 256 for P128, 512 for P256)
+//
+// The first version (csrc/hip/qsc.hip, kept as the reference path) ran a whole 256-thread
+// workgroup per sample with ~12 barriers per sample and scalar LDS-bound convolutions (0.75 LDS
+// loads per FMA): 46 us forward + 152 us backward for 2304 samples.  Here:
+//   * conv2 (M = positions, N = 32 channels, K = 144) is an implicit GEMM on
+//     v_mfma_f32_32x32x2_f32 (exact fp32, as the reference), operands gathered from the per-wave
+//     LDS image of the padded pool-1 map; conv1 (K = 18) stays on the VALU with a lane owning a
+//     pool window x 8 channels, so pool 1 happens in registers;
+//   * backward: conv2 weight grads accumulate across the wave's samples in MFMA accumulators
+//     (5 tiles of 32x32, K = positions), conv2 data grads are a 16x16x4 MFMA implicit GEMM over
+//     the zero-padded dz2 image (K = 32 channels x 9 flipped taps), conv1 weight grads a 16x16x4
+//     MFMA over positions; the linear layer's weight grads are one GEMM outside the kernel
+//     (dpre^T . p2 over the batch), everything else lands in one slab row per workgroup, summed
+//     in a fixed order (deterministic, no float atomics).
+// Every wave owns its sample from input to output, so waves never wait for each other.
+#include "common.h"
+
+namespace qd {
+namespace qsc2 {
+
+constexpr int C1 = 16, C2 = 32;
+constexpr int K1 = 2 * 9;         // conv1 reduction size
+constexpr int K2 = C1 * 9;        // conv2 reduction size (144)
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+struct Offs {
+  int w1, b1, w2, b2, wl, bl, row;
+};
+
+template <int H, int W>
+struct Geo {
+  static constexpr int HW = H * W;
+  static constexpr int H2 = H / 2, W2 = W / 2, HW2 = H2 * W2;   // pool-1 grid (conv2 positions)
+  static constexpr int H4 = H / 4, W4 = W / 4, HW4 = H4 * W4;   // pool-2 grid
+  static constexpr int F = C2 * HW4;
+  static constexpr int XW = W + 2, XP = (H + 2) * (W + 2);       // padded input plane
+  static constexpr int PW = W2 + 2, PP = (H2 + 2) * (W2 + 2);    // padded pool-1 plane
+  static constexpr int MT2 = HW2 / 32;                           // conv2 32-position tiles
+  static constexpr int MT1 = HW2 / 16;                           // dgrad 16-position tiles
+  // per-wave LDS image (floats)
+  static constexpr int o_x = 0;                                   // 2 x XP
+  static constexpr int o_p1 = o_x + 2 * XP;                       // C1 x PP (padded pool-1 map)
+  static constexpr int o_z2 = o_p1 + C1 * PP;                     // C2 x HW2 (conv2 pre-activation)
+  static constexpr int o_dz2 = o_z2 + C2 * HW2;                   // C2 x PP (padded conv2 grad)
+  static constexpr int o_dp1 = o_dz2 + C2 * PP;                   // C1 x HW2
+  static constexpr int o_dz1 = o_dp1 + C1 * HW2;                  // C1 x HW
+  static constexpr int o_misc = o_dz1 + C1 * HW;                  // 32: dpre / angles
+  static constexpr int FWD = o_dz2;                               // forward needs x, p1, z2
+  static constexpr int BWD = o_misc + 32;
+};
+
+// block-shared weights (floats): W1 [16][18] | b1 [16] | W2 [32][144] | b2 [32]
+constexpr int S_W1 = 0, S_B1 = S_W1 + C1 * K1, S_W2 = S_B1 + C1, S_B2 = S_W2 + C2 * K2, S_WEND = S_B2 + C2;
+
+__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+
+__device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Offs o, float* ws) {
+  const int nt = blockDim.x;
+  for (int i = threadIdx.x; i < C1 * K1; i += nt) ws[S_W1 + i] = flat[o.w1 + i];
+  for (int i = threadIdx.x; i < C1; i += nt) ws[S_B1 + i] = flat[o.b1 + i];
+  for (int i = threadIdx.x; i < C2 * K2; i += nt) ws[S_W2 + i] = flat[o.w2 + i];
+  for (int i = threadIdx.x; i < C2; i += nt) ws[S_B2 + i] = flat[o.b2 + i];
+}
+
+// conv1 pre-activations (+bias) of pool window `win` for channels [8h, 8h+8): acc[c][4 positions]
+template <int H, int W>
+__device__ __forceinline__ void conv1_window(const float* act, const float* ws, int win, int h, float (&acc)[8][4]) {
+  using G = Geo<H, W>;
+  const int qy = win / G::W2, qx = win % G::W2;
+  float patch[2][4][4];
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) patch[ci][dy][dx] = act[G::o_x + ci * G::XP + (2 * qy + dy) * G::XW + 2 * qx + dx];
+#pragma unroll 2   // fully unrolled, the 144 per-lane weight loads get hoisted into VGPRs
+  for (int c = 0; c < 8; ++c) {
+    const int co = 8 * h + c;
+    const float b = ws[S_B1 + co];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[c][p] = b;
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float w = ws[S_W1 + co * K1 + ci * 9 + t];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[c][p] += w * patch[ci][(p >> 1) + t / 3][(p & 1) + t % 3];
+      }
+  }
+}
+
+// Forward of one sample into the wave's LDS image: x -> p1 (padded) -> z2 (pre-activation).
+template <int H, int W>
+__device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane) {
+  using G = Geo<H, W>;
+  for (int i = lane; i < 2 * G::HW; i += 64) {
+    const int c = i / G::HW, p = i % G::HW;
+    act[G::o_x + c * G::XP + (p / W + 1) * G::XW + p % W + 1] = xs[i];
+  }
+  wave_lds_fence();
+  // conv1 + ReLU + pool: lane = (window, channel half)
+  for (int win = lane & 31; win < G::HW2; win += 32) {
+    const int h = lane >> 5;
+    float acc[8][4];
+    conv1_window<H, W>(act, ws, win, h, acc);
+    const int qy = win / G::W2, qx = win % G::W2;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float m = fmaxf(fmaxf(relu(acc[c][0]), relu(acc[c][1])), fmaxf(relu(acc[c][2]), relu(acc[c][3])));
+      act[G::o_p1 + (8 * h + c) * G::PP + (qy + 1) * G::PW + qx + 1] = m;
+    }
+  }
+  wave_lds_fence();
+  // conv2 on MFMA: rows = positions, cols = output channels; k = ci*9 + tap
+  const int col = lane & 31, kh = lane >> 5;
+  for (int mt = 0; mt < G::MT2; ++mt) {
+    const int pos = mt * 32 + col;
+    const int py = pos / G::W2, px = pos % G::W2;
+    f32x16 acc = {};
+#pragma unroll 4
+    for (int kk = 0; kk < K2 / 2; ++kk) {
+      const int k = 2 * kk + kh;
+      const int ci = k / 9, t = k % 9;
+      const float a = act[G::o_p1 + ci * G::PP + (py + t / 3) * G::PW + px + t % 3];
+      const float b = ws[S_W2 + col * K2 + k];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    const float bias = ws[S_B2 + col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
+      act[G::o_z2 + col * G::HW2 + mt * 32 + row] = acc[r] + bias;
+    }
+  }
+  wave_lds_fence();
+}
+
+// pool-2 (after ReLU) value and the winning position of feature f (first max, reference order)
+template <int H, int W>
+__device__ __forceinline__ float pool2(const float* act, int f, int& arg) {
+  using G = Geo<H, W>;
+  const int c = f / G::HW4, q = f % G::HW4, qy = q / G::W4, qx = q % G::W4;
+  const int base = (2 * qy) * G::W2 + 2 * qx;
+  const int idx[4] = {base, base + 1, base + G::W2, base + G::W2 + 1};
+  const float* z = act + G::o_z2 + c * G::HW2;
+  float m = relu(z[idx[0]]);
+  arg = idx[0];
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {
+    const float v = relu(z[idx[r]]);
+    if (v > m) {
+      m = v;
+      arg = idx[r];
+    }
+  }
+  return m;
+}
+
+// angles (B, n) = tanh(preprocess(x)); p2 (B, F) = flattened pool-2 features (for the linear
+// layer's weight-gradient GEMM in the backward).  One wave per sample.
+template <int H, int W, int NWV>
+__global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
+                                                      Offs o, float* __restrict__ angles, float* __restrict__ p2,
+                                                      int B, int n) {
+  using G = Geo<H, W>;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* ws = sm;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* act = sm + S_WEND + wv * G::FWD;
+  stage_weights(flat, o, ws);
+  for (int i = lane; i < G::FWD; i += 64) act[i] = 0.f;   // zero halos once; interiors rewritten per sample
+  __syncthreads();
+  const float* wl = flat + o.wl;
+  for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
+    sample_forward<H, W>(x + (size_t)s * 2 * G::HW, ws, act, lane);
+    float pf[G::F / 64];
+#pragma unroll
+    for (int i = 0; i < G::F / 64; ++i) {
+      int arg;
+      pf[i] = pool2<H, W>(act, lane + 64 * i, arg);
+      p2[(size_t)s * G::F + lane + 64 * i] = pf[i];
+    }
+    for (int j = 0; j < n; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < G::F / 64; ++i) acc += wl[(size_t)j * G::F + lane + 64 * i] * pf[i];
+      acc = wave_sum(acc);
+      if (lane == 0) angles[(size_t)s * n + j] = tanhf(acc + flat[o.bl + j]);
+    }
+  }
+}
+
+// Backward.  dang (B, n) = dL/d(angles).  Outputs: dpre (B, n) = dL/d(pre-tanh) (for the linear
+// weight-gradient GEMM), slab row per workgroup = grads of [w1 | b1 | w2 | b2 | (wl: 0) | bl] in
+// the flat layout starting at o.w1.
+template <int H, int W, int NWV>
+__global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
+                                                      Offs o, const float* __restrict__ angles,
+                                                      const float* __restrict__ dang, float* __restrict__ dpre_out,
+                                                      float* __restrict__ slab, int B, int n) {
+  using G = Geo<H, W>;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* ws = sm;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* act = sm + S_WEND + wv * G::BWD;
+  stage_weights(flat, o, ws);
+  for (int i = lane; i < G::BWD; i += 64) act[i] = 0.f;
+  __syncthreads();
+  const float* wl = flat + o.wl;
+  const int col32 = lane & 31, kh = lane >> 5;     // 32x32x2 operand coordinates
+  const int col16 = lane & 15, kq = lane >> 4;     // 16x16x4 operand coordinates
+  f32x16 gw2[5];                                   // dW2 tiles: rows = co, cols = k in [32t, 32t+32)
+#pragma unroll
+  for (int t = 0; t < 5; ++t) gw2[t] = (f32x16){};
+  f32x4 gw1[2];                                    // dW1 tiles: rows = co, cols = k in [16t, 16t+16)
+  gw1[0] = (f32x4){};
+  gw1[1] = (f32x4){};
+  float gb1[8], gb2 = 0.f, gbl = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) gb1[c] = 0.f;
+
+  for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
+    sample_forward<H, W>(x + (size_t)s * 2 * G::HW, ws, act, lane);
+    float* misc = act + G::o_misc;
+    if (lane < n) {
+      const float th = angles[(size_t)s * n + lane];
+      const float d = dang[(size_t)s * n + lane] * (1.f - th * th);
+      misc[lane] = d;
+      dpre_out[(size_t)s * n + lane] = d;
+      gbl += d;
+    }
+    wave_lds_fence();
+    // linear backward -> dp2, pool-2 backward (+ReLU mask) -> padded dz2
+#pragma unroll
+    for (int i = 0; i < G::F / 64; ++i) {
+      const int f = lane + 64 * i;
+      float dp = 0.f;
+      for (int j = 0; j < n; ++j) dp += wl[(size_t)j * G::F + f] * misc[j];
+      int arg;
+      pool2<H, W>(act, f, arg);
+      const int c = f / G::HW4, q = f % G::HW4, qy = q / G::W4, qx = q % G::W4;
+      const float* z = act + G::o_z2 + c * G::HW2;
+      const bool pass = z[arg] > 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int py = 2 * qy + (r >> 1), px = 2 * qx + (r & 1);
+        const int pidx = py * G::W2 + px;
+        act[G::o_dz2 + c * G::PP + (py + 1) * G::PW + px + 1] = (pidx == arg && pass) ? dp : 0.f;
+      }
+    }
+    wave_lds_fence();
+    // conv2 bias grad: lane (co, half) sums half of the positions
+    {
+      const float* dz = act + G::o_dz2 + col32 * G::PP;
+      for (int p = kh; p < G::HW2; p += 2) gb2 += dz[(p / G::W2 + 1) * G::PW + p % G::W2 + 1];
+    }
+    // conv2 weight grads: dW2[co][k] += sum_pos dz2[co][pos] * im2col(p1)[pos][k]  (K = positions)
+#pragma unroll 2
+    for (int kk = 0; kk < G::HW2 / 2; ++kk) {
+      const int pos = 2 * kk + kh;
+      const int py = pos / G::W2, px = pos % G::W2;
+      const float a = act[G::o_dz2 + col32 * G::PP + (py + 1) * G::PW + px + 1];
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int k = 32 * t + col32;
+        float b = 0.f;
+        if (k < K2) {
+          const int ci = k / 9, tp = k % 9;
+          b = act[G::o_p1 + ci * G::PP + (py + tp / 3) * G::PW + px + tp % 3];
+        }
+        gw2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, gw2[t], 0, 0, 0);
+      }
+    }
+    // conv2 data grads: dp1[ci][pos] = sum_{co,tap} dz2_pad[co][pos + 2 - tap] * W2[co][ci][tap]
+    for (int mt = 0; mt < G::MT1; ++mt) {
+      const int pos = 16 * mt + col16;
+      const int py = pos / G::W2, px = pos % G::W2;
+      f32x4 acc = {};
+#pragma unroll 4
+      for (int kk = 0; kk < 2 * K2 / 4; ++kk) {   // K = 32 co x 9 taps = 288
+        const int k = 4 * kk + kq;
+        const int co = k / 9, tp = k % 9;
+        const float a = act[G::o_dz2 + co * G::PP + (py + 2 - tp / 3) * G::PW + px + 2 - tp % 3];
+        const float b = ws[S_W2 + co * K2 + col16 * 9 + tp];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) act[G::o_dp1 + col16 * G::HW2 + 16 * mt + 4 * kq + r] = acc[r];
+    }
+    wave_lds_fence();
+    // pool-1 backward (+ReLU mask): recompute the window's conv1 pre-activations; dz1 (C1 x HW)
+    for (int win = lane & 31; win < G::HW2; win += 32) {
+      const int h = lane >> 5;
+      float acc[8][4];
+      conv1_window<H, W>(act, ws, win, h, acc);
+      const int qy = win / G::W2, qx = win % G::W2;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int co = 8 * h + c;
+        int am = 0;
+        float mv = relu(acc[c][0]);
+#pragma unroll
+        for (int p = 1; p < 4; ++p)
+          if (relu(acc[c][p]) > mv) {
+            mv = relu(acc[c][p]);
+            am = p;
+          }
+        const float g = (acc[c][am] > 0.f) ? act[G::o_dp1 + co * G::HW2 + win] : 0.f;
+        gb1[c] += g;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int py = 2 * qy + (p >> 1), px = 2 * qx + (p & 1);
+          act[G::o_dz1 + co * G::HW + py * W + px] = (p == am) ? g : 0.f;
+        }
+      }
+    }
+    wave_lds_fence();
+    // conv1 weight grads: dW1[co][k] += sum_pos dz1[co][pos] * im2col(x)[pos][k]  (K = positions)
+#pragma unroll 4
+    for (int kk = 0; kk < G::HW / 4; ++kk) {
+      const int pos = 4 * kk + kq;
+      const int py = pos / W, px = pos % W;
+      const float a = act[G::o_dz1 + col16 * G::HW + pos];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int k = 16 * t + col16;
+        float b = 0.f;
+        if (k < K1) {
+          const int ci = k / 9, tp = k % 9;
+          b = act[G::o_x + ci * G::XP + (py + tp / 3) * G::XW + px + tp % 3];
+        }
+        gw1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, gw1[t], 0, 0, 0);
+      }
+    }
+    wave_lds_fence();
+  }
+
+  // ---- deterministic workgroup reduction -> slab row (w1 | b1 | w2 | b2 | wl = 0 | bl) ----
+  __syncthreads();
+  float* red = sm + S_WEND;   // reuse the activation images: NWV x (C2*K2 + C1*K1 + C1 + C2 + 16)
+  constexpr int RW = C2 * K2 + C1 * K1 + C1 + C2 + 16;
+  float* mine = red + wv * RW;
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * kh, k = 32 * t + col32;
+      if (k < K2) mine[co * K2 + k] = gw2[t][r];
+    }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 4 * kq + r, k = 16 * t + col16;
+      if (k < K1) mine[C2 * K2 + co * K1 + k] = gw1[t][r];
+    }
+  // b1: lanes (win, h) hold 8 channels; combine the 32 windows of each half
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float v = gb1[c];
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) v += __shfl_xor(v, m);
+    if ((lane & 31) == 0) mine[C2 * K2 + C1 * K1 + 8 * kh + c] = v;
+  }
+  {
+    const float v = gb2 + __shfl_xor(gb2, 32);
+    if (kh == 0) mine[C2 * K2 + C1 * K1 + C1 + col32] = v;
+  }
+  if (lane < 16) mine[C2 * K2 + C1 * K1 + C1 + C2 + lane] = lane < n ? gbl : 0.f;
+  __syncthreads();
+  float* row = slab + (size_t)blockIdx.x * o.row;
+  for (int i = threadIdx.x; i < o.row; i += 64 * NWV) {
+    float v = 0.f;
+    int src = -1;
+    if (i >= o.w2 - o.w1 && i < o.w2 - o.w1 + C2 * K2) src = i - (o.w2 - o.w1);
+    else if (i < C1 * K1) src = C2 * K2 + i;
+    else if (i >= o.b1 - o.w1 && i < o.b1 - o.w1 + C1) src = C2 * K2 + C1 * K1 + (i - (o.b1 - o.w1));
+    else if (i >= o.b2 - o.w1 && i < o.b2 - o.w1 + C2) src = C2 * K2 + C1 * K1 + C1 + (i - (o.b2 - o.w1));
+    else if (i >= o.bl - o.w1 && i < o.bl - o.w1 + n) src = C2 * K2 + C1 * K1 + C1 + C2 + (i - (o.bl - o.w1));
+    if (src >= 0) {
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) v += red[w * RW + src];
+    }
+    row[i] = v;
+  }
+}
+
+// waves per workgroup: 4 for P128; P256's backward images are twice as large -> 2
+template <int W>
+constexpr int fwd_waves() { return 4; }
+template <int W>
+constexpr int bwd_waves() { return W == 8 ? 4 : 2; }
+
+template <int H, int W>
+constexpr size_t fwd_smem() {
+  return sizeof(float) * (S_WEND + fwd_waves<W>() * Geo<H, W>::FWD);
+}
+template <int H, int W>
+constexpr size_t bwd_smem() {
+  constexpr size_t act = bwd_waves<W>() * Geo<H, W>::BWD;
+  constexpr size_t red = bwd_waves<W>() * (C2 * K2 + C1 * K1 + C1 + C2 + 16);
+  return sizeof(float) * (S_WEND + (act > red ? act : red));
+}
+
+template <int H, int W>
+int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* p2, int B, int n, int grid,
+               hipStream_t s) {
+  constexpr int NW = fwd_waves<W>();
+  constexpr size_t sm = fwd_smem<H, W>();
+  static_assert(sm <= 160 * 1024, "LDS");
+  if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW>, sm)) return (int)e;
+  hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, B, n);
+  return (int)hipGetLastError();
+}
+
+template <int H, int W>
+int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, const float* dang, float* dpre,
+               float* slab, int B, int n, int grid, hipStream_t s) {
+  constexpr int NW = bwd_waves<W>();
+  constexpr size_t sm = bwd_smem<H, W>();
+  static_assert(sm <= 160 * 1024, "LDS");
+  if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW>, sm)) return (int)e;
+  hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang, dpre,
+                     slab, B, n);
+  return (int)hipGetLastError();
+}
+
+}  // namespace qsc2
+}  // namespace qd
+
+using namespace qd::qsc2;
+
+// offs: [w1, b1, w2, b2, wl, bl, row_width] float offsets into the flat parameter buffer.
+QD_API int qd_qsc2_fwd(const float* x, const float* flat, const int* offs, float* angles, float* p2, int B, int n, int H,
+                       int W, int grid, void* stream) {
+  if (n < 1 || n > 16 || B <= 0 || grid <= 0) return (int)hipErrorInvalidValue;
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, B, n, grid, s);
+  return (int)hipErrorInvalidValue;
+}
+
+// slab: (grid, offs[6]) floats, row layout = flat layout from offs[0] (wl columns left zero).
+QD_API int qd_qsc2_bwd(const float* x, const float* flat, const int* offs, const float* angles, const float* dang,
+                       float* dpre, float* slab, int B, int n, int H, int W, int grid, void* stream) {
+  if (n < 1 || n > 16 || B <= 0 || grid <= 0) return (int)hipErrorInvalidValue;
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, B, n, grid, s);
+  return (int)hipErrorInvalidValue;
+}
+
+// waves (= samples in flight) per workgroup of the two kernels
+QD_API int qd_qsc2_waves(int W, int backward) {
+  if (W == 8) return backward ? bwd_waves<8>() : fwd_waves<8>();
+  if (W == 16) return backward ? bwd_waves<16>() : fwd_waves<16>();
+  return -1;
+}

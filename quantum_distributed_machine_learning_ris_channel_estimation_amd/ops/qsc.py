@@ -32,7 +32,9 @@ _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
 class QSCStepHIP:
     def __init__(self, model, space: FlatParamSpace, batch_total: int, n_groups: int = 1,
-                 grid_fwd: int = 512, grid_bwd: int = 256):
+                 grid_fwd: int = 512, grid_bwd: int = 256, impl: str = "mfma"):
+        """impl: "mfma" (csrc/hip/qsc_mfma.hip: one wave per sample, fp32 MFMA convs; default) or
+        "ref" (csrc/hip/qsc.hip: one workgroup per sample, VALU convs)."""
         self.m = model
         self.space = space
         dev = space.flat.device
@@ -52,9 +54,20 @@ class QSCStepHIP:
         self.row0, self.row = o[0], row
         feat = pre[7].weight.shape[1]
         self.Hh, self.Ww = (16, 8) if feat == 256 else (16, 16)
-        self.grid_fwd = min(grid_fwd, batch_total)
-        self.grid_bwd = min(grid_bwd, batch_total)
+        self.impl = impl
         f32 = dict(device=dev, dtype=torch.float32)
+        self.F = feat
+        if impl == "mfma":
+            wf = nat.fn(nat.hip_lib(), "qd_qsc2_waves", [_i, _i])
+            self.grid_fwd = -(-batch_total // wf(self.Ww, 0))      # one sample per wave
+            self.grid_bwd = min(-(-batch_total // wf(self.Ww, 1)), grid_bwd)
+            self.p2 = torch.empty(batch_total, feat, **f32)        # pool-2 features (linear weight grad)
+            self.dpre = torch.empty(batch_total, self.n, **f32)
+            self.gwl = space.grad[names["preprocess.7.weight"]:names["preprocess.7.weight"] + self.n * feat].view(
+                self.n, feat)
+        else:
+            self.grid_fwd = min(grid_fwd, batch_total)
+            self.grid_bwd = min(grid_bwd, batch_total)
         self.angles = torch.empty(batch_total, self.n, **f32)
         self.E = torch.empty(batch_total, self.n, **f32)
         self.dE = torch.empty(batch_total, self.n, **f32)
@@ -74,6 +87,8 @@ class QSCStepHIP:
         self.qslab = torch.empty(self.qrows, 2 * self.n * self.L, **f32)
         self._pre_fwd = nat.fn(L, "qd_qsc_pre_fwd", [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._pre_bwd = nat.fn(L, "qd_qsc_pre_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+        self._fwd2 = nat.fn(L, "qd_qsc2_fwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+        self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
         if self.big:
             self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
@@ -110,8 +125,12 @@ class QSCStepHIP:
         assert x.shape[0] == B and x.is_contiguous() and labels.dtype == torch.int64
         st = nat.stream_ptr(x.device)
         flat = sp.flat
-        nat.check(self._pre_fwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), B, n, self.Hh, self.Ww,
-                                self.grid_fwd, st), "qsc_pre_fwd")
+        if self.impl == "mfma":
+            nat.check(self._fwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2), B, n,
+                                 self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
+        else:
+            nat.check(self._pre_fwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), B, n, self.Hh,
+                                    self.Ww, self.grid_fwd, st), "qsc_pre_fwd")
         w = self.quantum_weights().contiguous()
         wgroup = B // w.shape[0] if w.dim() == 4 else 0
         extra = (nat.ptr(self.qws) if self.qws is not None else None,) if self.big else ()
@@ -126,8 +145,15 @@ class QSCStepHIP:
                            nat.ptr(self.qslab), B, n, L, wgroup, *extra, st), "qsim_bwd")
         nat.check(self._rs(nat.ptr(self.qslab), nat.ptr(m.qlayer.weights.grad), self.qrows, 2 * n * L, 1.0, st),
                   "reduce_slab")
-        nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B, n,
-                                self.Hh, self.Ww, self.grid_bwd, st), "qsc_pre_bwd")
+        if self.impl == "mfma":
+            nat.check(self._bwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang),
+                                 nat.ptr(self.dpre), nat.ptr(self.preslab), B, n, self.Hh, self.Ww, self.grid_bwd, st),
+                      "qsc2_bwd")
+        else:
+            nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B,
+                                    n, self.Hh, self.Ww, self.grid_bwd, st), "qsc_pre_bwd")
         nat.check(self._ssum(nat.ptr(self.preslab), nat.ptr(sp.grad[self.row0:]), 1, self.grid_bwd, self.row, st),
                   "qsc_slab_sum")
+        if self.impl == "mfma":
+            self.gwl.addmm_(self.dpre.t(), self.p2)   # linear weight grad over the batch (one GEMM)
         return self.loss

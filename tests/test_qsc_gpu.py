@@ -10,9 +10,10 @@ from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.qsc imp
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("impl", ["mfma", "ref"])
 @pytest.mark.parametrize("pilot_num,n,B", [(128, 8, 2304), (128, 4, 300), (128, 6, 64), (256, 6, 96),
                                                    (256, 12, 72), (128, 16, 18)])
-def test_qsc_step_matches_autograd(cuda, pilot_num, n, B):
+def test_qsc_step_matches_autograd(cuda, pilot_num, n, B, impl):
     torch.manual_seed(0)
     H, W = (16, 8) if pilot_num == 128 else (16, 16)
     a = QSC_P128(n_qubits=n, use_quantumnat=False, use_gradient_pruning=False, pilot_num=pilot_num).to(cuda)
@@ -21,7 +22,7 @@ def test_qsc_step_matches_autograd(cuda, pilot_num, n, B):
     space = FlatParamSpace(list(a.named_parameters()), cuda)
     x = torch.randn(B, 2, H, W, device=cuda)
     y = torch.randint(0, 3, (B,), device=cuda)
-    step = QSCStepHIP(a, space, B)
+    step = QSCStepHIP(a, space, B, impl=impl)
     space.zero_grad()
     loss = step(x, y)
     ref = F.nll_loss(b(x), y)
