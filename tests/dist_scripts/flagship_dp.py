@@ -1,0 +1,48 @@
+"""World-N flagship trainer on CPU/gloo: ranks stay bit-identical; a NaN on ONE rank makes every rank
+skip the step (the NaN-guard flag rides in the small gradient bucket)."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import (  # noqa: E402
+    init_distributed, shutdown)
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (  # noqa: E402
+    FlagshipConfig, FlagshipTrainer)
+
+
+def flat_all(tr):
+    return torch.cat([tr.hdce.space.flat, tr.qspace.flat])
+
+
+def same_on_all_ranks(t):
+    g = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(g, t)
+    return all(torch.equal(g[0], x) for x in g[1:])
+
+
+def main(out):
+    ctx = init_distributed("cpu")
+    cfg = FlagshipConfig(n_qubits=4, batch=4, data_len=40, hip_graphs=False, dtype="fp32")
+    tr = FlagshipTrainer(cfg, ctx)
+    ok = [same_on_all_ranks(flat_all(tr))]
+    for _ in range(2):
+        tr.step()
+        ok.append(same_on_all_ranks(flat_all(tr)))
+    before = flat_all(tr).clone()
+    # NaN injected into rank 1's data only
+    if ctx.rank == 1:
+        tr.store.Yp.fill_(float("nan"))
+    tr.step()
+    after = flat_all(tr)
+    skipped = torch.equal(before, after)
+    ok.append(same_on_all_ranks(after))
+    with open(f"{out}.{ctx.rank}", "w") as f:
+        f.write(f"{int(all(ok))} {int(skipped)} {float(tr.skip.item())}\n")
+    shutdown()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

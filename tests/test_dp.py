@@ -22,3 +22,15 @@ def test_dp_equivalence_and_collectives(tmp_path):
 def test_launcher_propagates_failure():
     rc = launch([sys.executable, "-c", "import os,sys; sys.exit(3 if os.environ['RANK']=='1' else 0)"], nproc=2)
     assert rc == 3
+
+
+def test_flagship_dp_lockstep_and_rank_consistent_nan_skip(tmp_path):
+    out = str(tmp_path / "fl")
+    rc = launch([sys.executable, os.path.join(HERE, "dist_scripts", "flagship_dp.py"), out], nproc=2,
+                extra_env={"OMP_NUM_THREADS": "2"})
+    assert rc == 0
+    for r in range(2):
+        same, skipped, flag = open(f"{out}.{r}").read().split()
+        assert same == "1"           # parameters bit-identical across ranks after every step
+        assert skipped == "1"        # the NaN on rank 1 made BOTH ranks skip
+        assert float(flag) >= 1.0    # the summed skip flag
