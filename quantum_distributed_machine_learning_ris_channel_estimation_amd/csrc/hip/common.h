@@ -65,20 +65,36 @@ inline hipError_t allow_lds(K kernel, size_t bytes) {
                              (int)bytes);
 }
 
-// fp32 -> OCP fp8 (gfx950 native formats), saturating to the finite range.
-__device__ __forceinline__ uint8_t f32_to_e4m3(float v) {
-  return (uint8_t)__hip_cvt_float_to_fp8(v, __HIP_SATFINITE, __HIP_E4M3);
+// fp32 -> OCP e4m3 (gfx950 native format) with the packed hardware converter; inputs clamped to
+// the finite range first (saturating semantics).  pack4 returns 4 bytes (a, b, c, d) little-endian.
+constexpr float kE4M3Max = 448.f;
+__device__ __forceinline__ uint32_t e4m3_pack4(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -kE4M3Max), kE4M3Max);
+  b = fminf(fmaxf(b, -kE4M3Max), kE4M3Max);
+  c = fminf(fmaxf(c, -kE4M3Max), kE4M3Max);
+  d = fminf(fmaxf(d, -kE4M3Max), kE4M3Max);
+  int p = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  p = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, p, true);
+  return (uint32_t)p;
 }
-__device__ __forceinline__ uint8_t f32_to_e5m2(float v) {
-  return (uint8_t)__hip_cvt_float_to_fp8(v, __HIP_SATFINITE, __HIP_E5M2);
-}
+__device__ __forceinline__ uint8_t f32_to_e4m3(float v) { return (uint8_t)(e4m3_pack4(v, 0.f, 0.f, 0.f) & 0xffu); }
 
-// Running |x| max of non-negative values as float bits (monotone for x >= 0): one atomic per wave.
-__device__ __forceinline__ void amax_update(unsigned int* amax_bits, float local_absmax) {
+// Per-workgroup |x| max for delayed fp8 scaling: part[blockIdx.x] = max(part[blockIdx.x], block max).
+// No atomics (one contended address per wave serialised ~16k atomics in L2: 8 -> 192 us); the
+// scale-update kernel reduces the partials.  Every thread of the block must call it.
+__device__ __forceinline__ void amax_block_store(float* part, float local_absmax) {
+  __shared__ float wmax[16];
   float m = local_absmax;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(amax_bits, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = 0.f;
+    for (int w = 0; w < (int)(blockDim.x + 63) / 64; ++w) b = fmaxf(b, wmax[w]);
+    part[blockIdx.x] = fmaxf(part[blockIdx.x], b);
+  }
 }
+constexpr int kAmaxParts = 4096;   // partial slots per scaled tensor (>= any producer grid)
 
 }  // namespace qd

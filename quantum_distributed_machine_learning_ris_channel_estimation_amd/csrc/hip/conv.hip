@@ -535,7 +535,7 @@ template <int HW>
 __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __restrict__ z, const float* __restrict__ st,
                                                             uint16_t* __restrict__ h, long n8, int EC, int B,
                                                             uint8_t* __restrict__ h8, const float* __restrict__ qs,
-                                                            unsigned int* __restrict__ amax) {
+                                                            float* __restrict__ amax) {
   const float q = h8 ? qs[0] : 0.f;
   float mx = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
@@ -554,17 +554,14 @@ __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __re
     for (int j = 0; j < 4; ++j) w[j] = f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
     *reinterpret_cast<uint4*>(h + e0) = make_uint4(w[0], w[1], w[2], w[3]);
     if (h8) {
-      uint32_t p0 = 0, p1 = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        mx = fmaxf(mx, fmaxf(v[j], v[j + 4]));
-        p0 |= (uint32_t)f32_to_e4m3(v[j] * q) << (8 * j);
-        p1 |= (uint32_t)f32_to_e4m3(v[j + 4] * q) << (8 * j);
-      }
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j]);
+      const uint32_t p0 = e4m3_pack4(v[0] * q, v[1] * q, v[2] * q, v[3] * q);
+      const uint32_t p1 = e4m3_pack4(v[4] * q, v[5] * q, v[6] * q, v[7] * q);
       *reinterpret_cast<uint2*>(h8 + e0) = make_uint2(p0, p1);
     }
   }
-  if (h8) amax_update(amax, mx);
+  if (h8) amax_block_store(amax, mx);
 }
 
 // out[i] += sum_rows slab[g][row][i] for every group g (rows contiguous per group).
@@ -768,10 +765,10 @@ QD_API int qd_bn_bwd_finalize(const float* slab, const float* gamma, float* st, 
 
 // h8/qs/amax nullable (fp8 estimator only)
 QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int N, int EC, int B, int HW,
-                            uint8_t* h8, const float* qs, unsigned int* amax, void* stream) {
+                            uint8_t* h8, const float* qs, float* amax, void* stream) {
   const long n8 = (long)N * EC * HW / 8;
   int grid = (int)((n8 + 255) / 256);
-  if (grid > 4096) grid = 4096;
+  if (grid > 2048) grid = 2048;   // <= kAmaxParts
   if (h8 && (!qs || !amax)) return (int)hipErrorInvalidValue;
   if (HW == 128)
     hipLaunchKernelGGL((bn_relu_apply_kernel<128>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B,

@@ -31,7 +31,7 @@ struct Shadow {
   long lo, hi;
   uint8_t* out8;        // optional e4m3 copy of the same range, scaled by *qs (fp8 estimator)
   const float* qs;
-  unsigned int* amax;   // running max |p| over the range (next step's delayed scale)
+  float* amax;          // per-workgroup max |p| partials over the range (next step's delayed scale)
 };
 
 // Called by every thread at the end of the kernel: the last workgroup to get here increments the
@@ -64,9 +64,7 @@ __device__ __forceinline__ float store_shadow(const Shadow& sh, long i0, float4 
     *reinterpret_cast<ushort4*>(sh.out + (i0 - sh.lo)) = h;
     if (sh.out8 != nullptr) {
       const float q = *sh.qs;
-      const uint32_t p = (uint32_t)f32_to_e4m3(v.x * q) | ((uint32_t)f32_to_e4m3(v.y * q) << 8) |
-                         ((uint32_t)f32_to_e4m3(v.z * q) << 16) | ((uint32_t)f32_to_e4m3(v.w * q) << 24);
-      *reinterpret_cast<uint32_t*>(sh.out8 + (i0 - sh.lo)) = p;
+      *reinterpret_cast<uint32_t*>(sh.out8 + (i0 - sh.lo)) = e4m3_pack4(v.x * q, v.y * q, v.z * q, v.w * q);
       return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
     }
   }
@@ -141,7 +139,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     float c = wave_sum((float)cnt);
     if ((threadIdx.x & 63) == 0 && c > 0.f) atomicAdd(pruned, (unsigned int)c);
   }
-  if (sh.out8 != nullptr) amax_update(sh.amax, wmax);
+  if (sh.out8 != nullptr) amax_block_store(sh.amax, wmax);
   tick_if_last(step_out, done);
 }
 
@@ -162,18 +160,30 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
   tick_if_last(step_out, done);
 }
 
-// Delayed per-tensor fp8 scaling: scale = amax / (fmax / 2^margin) (dequantisation factor fed to
-// the GEMM), qs = 1 / scale (quantisation factor used by the producers), amax re-armed.
-__global__ void fp8_scale_update_kernel(unsigned int* amax, float* scale, float* qs, int n, float fmax, float margin) {
-  const int i = threadIdx.x;
-  if (i < n) {
-    const float a = __uint_as_float(amax[i]);
-    if (a > 0.f) {   // keep the previous scale if the tensor was not produced this step
-      const float s = fmaxf(a, 1e-30f) * exp2f(margin) / fmax;
+// Delayed per-tensor fp8 scaling, one workgroup per tensor: amax = max of the producers'
+// per-workgroup partials (then re-armed to 0), scale = amax * 2^margin / fmax (dequantisation
+// factor fed to the GEMM), qs = 1 / scale (quantisation factor the producers multiply by).
+__global__ void __launch_bounds__(256) fp8_scale_update_kernel(float* amax_parts, float* scale, float* qs, int nparts,
+                                                               float fmax, float margin) {
+  __shared__ float red[4];
+  const int i = blockIdx.x;
+  float* part = amax_parts + (size_t)i * nparts;
+  float m = 0.f;
+  for (int k = threadIdx.x; k < nparts; k += 256) {
+    m = fmaxf(m, part[k]);
+    part[k] = 0.f;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float a = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (a > 0.f) {   // keep the previous scale if the tensor was not produced since the last update
+      const float s = a * exp2f(margin) / fmax;
       scale[i] = s;
       qs[i] = 1.f / s;
     }
-    amax[i] = 0u;
   }
 }
 
@@ -195,7 +205,7 @@ using namespace qd::optim;
 QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const float* skip,
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
                         float grad_scale, float prune_thr, unsigned int* done, uint16_t* shadow, long shadow_lo,
-                        long shadow_hi, uint8_t* shadow8, const float* qs, unsigned int* amax, void* stream) {
+                        long shadow_hi, uint8_t* shadow8, const float* qs, float* amax, void* stream) {
   if (n <= 0 || done == nullptr || (shadow && ((shadow_lo | shadow_hi) & 3))) return (int)hipErrorInvalidValue;
   if (shadow8 && (!shadow || !qs || !amax)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
@@ -215,10 +225,13 @@ QD_API int qd_sgd_step(float* p, float* g, float* buf, long n, const float* lr, 
   return (int)hipGetLastError();
 }
 
-QD_API int qd_fp8_scale_update(unsigned int* amax, float* scale, float* qs, int n, float fmax, float margin,
+// amax_parts: (n, kAmaxParts) floats
+QD_API int qd_fp8_scale_update(float* amax_parts, float* scale, float* qs, int n, float fmax, float margin,
                                void* stream) {
   if (n < 1 || n > 64) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(fp8_scale_update_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, amax, scale, qs, n, fmax,
-                     margin);
+  hipLaunchKernelGGL(fp8_scale_update_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, amax_parts, scale, qs,
+                     qd::kAmaxParts, fmax, margin);
   return (int)hipGetLastError();
 }
+
+QD_API int qd_amax_parts() { return qd::kAmaxParts; }

@@ -60,12 +60,18 @@ constexpr int S_W1 = 0, S_B1 = S_W1 + C1 * K1, S_W2 = S_B1 + C1, S_B2 = S_W2 + C
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
-__device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Offs o, float* ws) {
+// ... followed by the linear layer: wl [n][F] | bl [16] (LDS: a runtime-n loop over L2 loads of
+// wl serialises one round trip per iteration -- it dominated both kernels before staging)
+__host__ __device__ constexpr int act_base(int n, int F) { return S_WEND + ((n * F + 16 + 3) & ~3); }
+
+__device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Offs o, float* ws, int n, int F) {
   const int nt = blockDim.x;
   for (int i = threadIdx.x; i < C1 * K1; i += nt) ws[S_W1 + i] = flat[o.w1 + i];
   for (int i = threadIdx.x; i < C1; i += nt) ws[S_B1 + i] = flat[o.b1 + i];
   for (int i = threadIdx.x; i < C2 * K2; i += nt) ws[S_W2 + i] = flat[o.w2 + i];
   for (int i = threadIdx.x; i < C2; i += nt) ws[S_B2 + i] = flat[o.b2 + i];
+  for (int i = threadIdx.x; i < n * F; i += nt) ws[S_WEND + i] = flat[o.wl + i];
+  for (int i = threadIdx.x; i < n; i += nt) ws[S_WEND + n * F + i] = flat[o.bl + i];
 }
 
 // conv1 pre-activations (+bias) of pool window `win` for channels [8h, 8h+8): acc[c][4 positions]
@@ -174,11 +180,12 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ws = sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float* act = sm + S_WEND + wv * G::FWD;
-  stage_weights(flat, o, ws);
+  float* act = sm + act_base(n, G::F) + wv * G::FWD;
+  stage_weights(flat, o, ws, n, G::F);
   for (int i = lane; i < G::FWD; i += 64) act[i] = 0.f;   // zero halos once; interiors rewritten per sample
   __syncthreads();
-  const float* wl = flat + o.wl;
+  const float* wl = ws + S_WEND;
+  const float* bl = wl + n * G::F;
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
     sample_forward<H, W>(x + (size_t)s * 2 * G::HW, ws, act, lane);
     float pf[G::F / 64];
@@ -193,7 +200,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
 #pragma unroll
       for (int i = 0; i < G::F / 64; ++i) acc += wl[(size_t)j * G::F + lane + 64 * i] * pf[i];
       acc = wave_sum(acc);
-      if (lane == 0) angles[(size_t)s * n + j] = tanhf(acc + flat[o.bl + j]);
+      if (lane == 0) angles[(size_t)s * n + j] = tanhf(acc + bl[j]);
     }
   }
 }
@@ -210,11 +217,11 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ws = sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float* act = sm + S_WEND + wv * G::BWD;
-  stage_weights(flat, o, ws);
+  float* act = sm + act_base(n, G::F) + wv * G::BWD;
+  stage_weights(flat, o, ws, n, G::F);
   for (int i = lane; i < G::BWD; i += 64) act[i] = 0.f;
   __syncthreads();
-  const float* wl = flat + o.wl;
+  const float* wl = ws + S_WEND;
   const int col32 = lane & 31, kh = lane >> 5;     // 32x32x2 operand coordinates
   const int col16 = lane & 15, kq = lane >> 4;     // 16x16x4 operand coordinates
   f32x16 gw2[5];                                   // dW2 tiles: rows = co, cols = k in [32t, 32t+32)
@@ -400,22 +407,22 @@ template <int W>
 constexpr int bwd_waves() { return W == 8 ? 4 : 2; }
 
 template <int H, int W>
-constexpr size_t fwd_smem() {
-  return sizeof(float) * (S_WEND + fwd_waves<W>() * Geo<H, W>::FWD);
+size_t fwd_smem(int n) {
+  return sizeof(float) * (act_base(n, Geo<H, W>::F) + fwd_waves<W>() * Geo<H, W>::FWD);
 }
 template <int H, int W>
-constexpr size_t bwd_smem() {
-  constexpr size_t act = bwd_waves<W>() * Geo<H, W>::BWD;
-  constexpr size_t red = bwd_waves<W>() * (C2 * K2 + C1 * K1 + C1 + C2 + 16);
-  return sizeof(float) * (S_WEND + (act > red ? act : red));
+size_t bwd_smem(int n) {
+  const size_t act = act_base(n, Geo<H, W>::F) + bwd_waves<W>() * Geo<H, W>::BWD;
+  const size_t red = S_WEND + bwd_waves<W>() * (C2 * K2 + C1 * K1 + C1 + C2 + 16);
+  return sizeof(float) * (act > red ? act : red);
 }
 
 template <int H, int W>
 int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* p2, int B, int n, int grid,
                hipStream_t s) {
   constexpr int NW = fwd_waves<W>();
-  constexpr size_t sm = fwd_smem<H, W>();
-  static_assert(sm <= 160 * 1024, "LDS");
+  const size_t sm = fwd_smem<H, W>(n);
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW>, sm)) return (int)e;
   hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, B, n);
   return (int)hipGetLastError();
@@ -425,8 +432,8 @@ template <int H, int W>
 int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, const float* dang, float* dpre,
                float* slab, int B, int n, int grid, hipStream_t s) {
   constexpr int NW = bwd_waves<W>();
-  constexpr size_t sm = bwd_smem<H, W>();
-  static_assert(sm <= 160 * 1024, "LDS");
+  const size_t sm = bwd_smem<H, W>(n);
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW>, sm)) return (int)e;
   hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang, dpre,
                      slab, B, n);

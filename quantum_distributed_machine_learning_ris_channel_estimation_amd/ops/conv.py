@@ -96,7 +96,7 @@ class ConvStackHIP:
         f8 = self.m.fp8_scales if self.fp8 else None
         nat.check(self._apply(nat.ptr(self.z[2]), nat.ptr(self.st[2]), nat.ptr(self.h3), self.N, self.EC, self.B,
                               self.HW, _ptr(self.h3_8), nat.ptr(f8.qs) if f8 else None,
-                              nat.ptr(f8.amax) if f8 else None, st), "bn_relu_apply")
+                              nat.ptr(f8.amax[0]) if f8 else None, st), "bn_relu_apply")
         return self.h3
 
     # --------------------------------------------------------------------- backward

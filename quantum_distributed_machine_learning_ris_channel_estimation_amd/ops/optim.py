@@ -78,12 +78,17 @@ class Fp8Scales:
     """Delayed per-tensor fp8 scaling state for ``n`` tensors (device-resident, graph-safe).
 
     ``qs[i]`` is the quantisation factor producers multiply by (x8 = e4m3(x * qs)), ``scale[i]`` =
-    1/qs the dequantisation factor handed to the GEMM, ``amax[i]`` the running max |x| (float bits)
-    the producers accumulate; ``update()`` (one launch) turns amax into the next scales."""
+    1/qs the dequantisation factor handed to the GEMM, ``amax[i]`` the per-workgroup max |x|
+    partials the producers write (no atomics); ``update()`` (one launch) reduces them into the
+    next scales and re-arms them."""
+
+    PARTS = 4096   # = kAmaxParts in csrc/hip/common.h
 
     def __init__(self, n: int, device, margin: float = 1.0):
         self.n, self.margin = n, margin
-        self.amax = torch.zeros(n, device=device, dtype=torch.int32)
+        self.amax = torch.zeros(n, self.PARTS, device=device, dtype=torch.float32)
+        if self.amax.is_cuda:
+            assert nat.fn(nat.hip_lib(), "qd_amax_parts", [])() == self.PARTS
         self.scale = torch.ones(n, device=device, dtype=torch.float32)
         self.qs = torch.ones(n, device=device, dtype=torch.float32)
 
@@ -99,7 +104,7 @@ class Fp8Scales:
             nat.check(f(nat.ptr(self.amax), nat.ptr(self.scale), nat.ptr(self.qs), self.n, FP8_E4M3_MAX,
                         self.margin, nat.stream_ptr(self.scale.device)), "fp8_scale_update")
             return
-        a = self.amax.view(torch.float32).clone()
+        a = self.amax.amax(dim=1)
         upd = a > 0
         s = a.clamp_min(1e-30) * 2.0 ** self.margin / FP8_E4M3_MAX
         self.scale.copy_(torch.where(upd, s, self.scale))
@@ -203,7 +208,7 @@ class FusedOptimizer:
                             nat.ptr(self.shadow) if self.shadow is not None else None, self.shadow_lo,
                             self.shadow_hi, nat.ptr(self.shadow8) if f8 else None,
                             nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
-                            nat.ptr(self.fp8.amax[self.fp8_slot:]) if f8 else None, st), "adam")
+                            nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, st), "adam")
             return
         self._step_host(grad_scale, skip)
         if self.shadow is not None:

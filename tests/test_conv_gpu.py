@@ -145,6 +145,19 @@ def test_hdce_fp8_estimator_step(cuda):
     W = m8.fc_w.detach()
     Wq = m8._shadow_w8.float() * float(sc.scale[1])
     assert float((Wq - W).norm() / W.norm()) < 0.05
+    # the kernel's e4m3 bytes are PyTorch's OCP float8_e4m3fn of the same scaled values
+    o8.refresh_shadow()                                          # kernel-free reference path ...
+    ref8 = o8.shadow8.clone()
+    m8.space.grad.zero_()
+    sk = torch.ones(1, device=cuda)
+    o8.step(skip=torch.zeros(1, device=cuda))                    # ... vs the kernel's fused write
+    torch.cuda.synchronize()
+    qs = float(sc.qs[1])
+    W = m8.space.flat[o8.shadow_lo:o8.shadow_hi]
+    torch_e4m3 = (W * qs).clamp(-448, 448).to(torch.float8_e4m3fn)
+    same = (o8.shadow8.view(torch.uint8) == torch_e4m3.view(torch.uint8)).float().mean()
+    assert float(same) > 0.999, float(same)
+    del ref8, sk
     # activations: h3_8 * scale_a ~ h3 (the scale used for the LAST forward was updated after it,
     # so compare the relative shape via the quantisation error of a fresh forward)
     A = s8.conv.h3.float()
