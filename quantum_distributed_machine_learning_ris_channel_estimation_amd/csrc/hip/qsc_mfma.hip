@@ -60,18 +60,46 @@ constexpr int S_W1 = 0, S_B1 = S_W1 + C1 * K1, S_W2 = S_B1 + C1, S_B2 = S_W2 + C
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
+// Diagnostic phase stamps (STAMP builds only): s_memtime with its own lgkmcnt wait, fenced by
+// scheduling barriers so the compiler keeps each phase's work on its side of the stamp.
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+constexpr int NSTAMP = 12;
+
 // ... followed by the linear layer: wl [n][F] | bl [16] (LDS: a runtime-n loop over L2 loads of
 // wl serialises one round trip per iteration -- it dominated both kernels before staging)
 __host__ __device__ constexpr int act_base(int n, int F) { return S_WEND + ((n * F + 16 + 3) & ~3); }
 
+// global -> LDS copy of n floats (both 16-byte aligned, n % 4 == 0): float4 loads, four in flight
+// per thread (a plain strided loop serialises one L2 round trip per iteration)
+__device__ __forceinline__ void stage4(float* dst, const float* __restrict__ src, int n) {
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  const int n4 = n >> 2, nt = blockDim.x;
+  int i = threadIdx.x;
+  for (; i + 3 * nt < n4; i += 4 * nt) {
+    const float4 a = s4[i], b = s4[i + nt], c = s4[i + 2 * nt], d = s4[i + 3 * nt];
+    d4[i] = a;
+    d4[i + nt] = b;
+    d4[i + 2 * nt] = c;
+    d4[i + 3 * nt] = d;
+  }
+  for (; i < n4; i += nt) d4[i] = s4[i];
+}
+
+// (all offsets are multiples of 16 floats: FlatParamSpace ALIGN; LDS slots multiples of 4)
 __device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Offs o, float* ws, int n, int F) {
-  const int nt = blockDim.x;
-  for (int i = threadIdx.x; i < C1 * K1; i += nt) ws[S_W1 + i] = flat[o.w1 + i];
-  for (int i = threadIdx.x; i < C1; i += nt) ws[S_B1 + i] = flat[o.b1 + i];
-  for (int i = threadIdx.x; i < C2 * K2; i += nt) ws[S_W2 + i] = flat[o.w2 + i];
-  for (int i = threadIdx.x; i < C2; i += nt) ws[S_B2 + i] = flat[o.b2 + i];
-  for (int i = threadIdx.x; i < n * F; i += nt) ws[S_WEND + i] = flat[o.wl + i];
-  for (int i = threadIdx.x; i < n; i += nt) ws[S_WEND + n * F + i] = flat[o.bl + i];
+  stage4(ws + S_W1, flat + o.w1, C1 * K1);
+  stage4(ws + S_B1, flat + o.b1, C1);
+  stage4(ws + S_W2, flat + o.w2, C2 * K2);
+  stage4(ws + S_B2, flat + o.b2, C2);
+  stage4(ws + S_WEND, flat + o.wl, n * F);
+  if (threadIdx.x < n) ws[S_WEND + n * F + threadIdx.x] = flat[o.bl + threadIdx.x];
 }
 
 // conv1 pre-activations (+bias) of pool window `win` for channels [8h, 8h+8): acc[c][4 positions]
@@ -104,14 +132,24 @@ __device__ __forceinline__ void conv1_window(const float* act, const float* ws, 
 }
 
 // Forward of one sample into the wave's LDS image: x -> p1 (padded) -> z2 (pre-activation).
-template <int H, int W>
-__device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane) {
+template <int H, int W, bool STAMP = false>
+__device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane,
+                                               unsigned long long* ts = nullptr) {
   using G = Geo<H, W>;
-  for (int i = lane; i < 2 * G::HW; i += 64) {
-    const int c = i / G::HW, p = i % G::HW;
-    act[G::o_x + c * G::XP + (p / W + 1) * G::XW + p % W + 1] = xs[i];
+  static_assert(W % 4 == 0, "float4 rows");
+  const float4* x4 = reinterpret_cast<const float4*>(xs);   // sample planes are 16-byte aligned
+#pragma unroll
+  for (int i = lane; i < 2 * G::HW / 4; i += 64) {
+    const float4 v = x4[i];
+    const int c = (4 * i) / G::HW, p = (4 * i) % G::HW;
+    float* d = act + G::o_x + c * G::XP + (p / W + 1) * G::XW + p % W + 1;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
   }
   wave_lds_fence();
+  if constexpr (STAMP) ts[2] = stamp();
   // conv1 + ReLU + pool: lane = (window, channel half)
   for (int win = lane & 31; win < G::HW2; win += 32) {
     const int h = lane >> 5;
@@ -125,6 +163,7 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
     }
   }
   wave_lds_fence();
+  if constexpr (STAMP) ts[3] = stamp();
   // conv2 on MFMA: rows = positions, cols = output channels; k = ci*9 + tap
   const int col = lane & 31, kh = lane >> 5;
   for (int mt = 0; mt < G::MT2; ++mt) {
@@ -147,6 +186,7 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
     }
   }
   wave_lds_fence();
+  if constexpr (STAMP) ts[4] = stamp();
 }
 
 // pool-2 (after ReLU) value and the winning position of feature f (first max, reference order)
@@ -172,10 +212,12 @@ __device__ __forceinline__ float pool2(const float* act, int f, int& arg) {
 
 // angles (B, n) = tanh(preprocess(x)); p2 (B, F) = flattened pool-2 features (for the linear
 // layer's weight-gradient GEMM in the backward).  One wave per sample.
-template <int H, int W, int NWV>
+template <int H, int W, int NWV, bool STAMP = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                       Offs o, float* __restrict__ angles, float* __restrict__ p2,
-                                                      int B, int n) {
+                                                      int B, int n, unsigned long long* __restrict__ stamps = nullptr) {
+  unsigned long long ts[NSTAMP] = {};
+  if constexpr (STAMP) ts[0] = stamp();
   using G = Geo<H, W>;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ws = sm;
@@ -184,10 +226,13 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   stage_weights(flat, o, ws, n, G::F);
   for (int i = lane; i < G::FWD; i += 64) act[i] = 0.f;   // zero halos once; interiors rewritten per sample
   __syncthreads();
+  if constexpr (STAMP) ts[1] = stamp();
   const float* wl = ws + S_WEND;
   const float* bl = wl + n * G::F;
+  bool first = true;
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
-    sample_forward<H, W>(x + (size_t)s * 2 * G::HW, ws, act, lane);
+    if (STAMP && first) sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, ts);
+    else sample_forward<H, W>(x + (size_t)s * 2 * G::HW, ws, act, lane);
     float pf[G::F / 64];
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {
@@ -202,6 +247,15 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
       acc = wave_sum(acc);
       if (lane == 0) angles[(size_t)s * n + j] = tanhf(acc + bl[j]);
     }
+    if (STAMP && first) {
+      ts[5] = stamp();
+      first = false;
+    }
+  }
+  if constexpr (STAMP) {
+    ts[6] = stamp();
+    if (lane == 0)
+      for (int k = 0; k < NSTAMP; ++k) stamps[(size_t)(blockIdx.x * NWV + wv) * NSTAMP + k] = ts[k];
   }
 }
 
@@ -419,12 +473,19 @@ size_t bwd_smem(int n) {
 
 template <int H, int W>
 int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* p2, int B, int n, int grid,
-               hipStream_t s) {
+               hipStream_t s, unsigned long long* stamps = nullptr) {
   constexpr int NW = fwd_waves<W>();
   const size_t sm = fwd_smem<H, W>(n);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW>, sm)) return (int)e;
-  hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, B, n);
+  if (stamps) {
+    if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW, true>, sm)) return (int)e;
+    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW, true>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, B,
+                       n, stamps);
+  } else {
+    if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW>, sm)) return (int)e;
+    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, B, n,
+                       nullptr);
+  }
   return (int)hipGetLastError();
 }
 
@@ -472,4 +533,15 @@ QD_API int qd_qsc2_waves(int W, int backward) {
   if (W == 8) return backward ? bwd_waves<8>() : fwd_waves<8>();
   if (W == 16) return backward ? bwd_waves<16>() : fwd_waves<16>();
   return -1;
+}
+
+// Diagnostic: forward with per-wave phase stamps (stamps: grid * waves * 12 u64):
+// [0] kernel start [1] weights staged [2] input tile [3] conv1+pool [4] conv2 [5] pool2+linear
+// (first sample of the wave) [6] wave done.
+QD_API int qd_qsc2_fwd_stamped(const float* x, const float* flat, const int* offs, float* angles, float* p2, int B,
+                               int n, int H, int W, int grid, unsigned long long* stamps, void* stream) {
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, B, n, grid, (hipStream_t)stream, stamps);
+  if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, B, n, grid, (hipStream_t)stream, stamps);
+  return (int)hipErrorInvalidValue;
 }
