@@ -41,12 +41,13 @@ struct Geo {
   static constexpr int F = C2 * HW4;
   static constexpr int XW = W + 2, XP = (H + 2) * (W + 2);       // padded input plane
   static constexpr int PW = W2 + 2, PP = (H2 + 2) * (W2 + 2);    // padded pool-1 plane
+  static constexpr int PC = 20;   // pool-1 map is channel-last: 16 channels (+4 pad: ds_read_b128 banks) per position
   static constexpr int MT2 = HW2 / 32;                           // conv2 32-position tiles
   static constexpr int MT1 = HW2 / 16;                           // dgrad 16-position tiles
   // per-wave LDS image (floats)
   static constexpr int o_x = 0;                                   // 2 x XP
   static constexpr int o_p1 = o_x + 2 * XP;                       // C1 x PP (padded pool-1 map)
-  static constexpr int o_z2 = o_p1 + C1 * PP;                     // C2 x HW2 (conv2 pre-activation)
+  static constexpr int o_z2 = o_p1 + PC * PP;                     // C2 x HW2 (conv2 pre-activation)
   static constexpr int o_dz2 = o_z2 + C2 * HW2;                   // C2 x PP (padded conv2 grad)
   static constexpr int o_dp1 = o_dz2 + C2 * PP;                   // C1 x HW2
   static constexpr int o_dz1 = o_dp1 + C1 * HW2;                  // C1 x HW
@@ -132,9 +133,11 @@ __device__ __forceinline__ void conv1_window(const float* act, const float* ws, 
 }
 
 // Forward of one sample into the wave's LDS image: x -> p1 (padded) -> z2 (pre-activation).
-template <int H, int W, bool STAMP = false>
+// wreg (optional): this lane's 72 conv2 weights W2[co = lane&31][ci = 8*(lane>>5) + j][t] at
+// [t*8 + j], register-resident across samples (forward kernel); null = read them from LDS.
+template <int H, int W, bool WREG, bool STAMP = false>
 __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane,
-                                               unsigned long long* ts = nullptr) {
+                                               const float (&wreg)[72], unsigned long long* ts = nullptr) {
   using G = Geo<H, W>;
   static_assert(W % 4 == 0, "float4 rows");
   const float4* x4 = reinterpret_cast<const float4*>(xs);   // sample planes are 16-byte aligned
@@ -156,27 +159,35 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
     float acc[8][4];
     conv1_window<H, W>(act, ws, win, h, acc);
     const int qy = win / G::W2, qx = win % G::W2;
+    float m[8];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float m = fmaxf(fmaxf(relu(acc[c][0]), relu(acc[c][1])), fmaxf(relu(acc[c][2]), relu(acc[c][3])));
-      act[G::o_p1 + (8 * h + c) * G::PP + (qy + 1) * G::PW + qx + 1] = m;
-    }
+    for (int c = 0; c < 8; ++c)
+      m[c] = fmaxf(fmaxf(relu(acc[c][0]), relu(acc[c][1])), fmaxf(relu(acc[c][2]), relu(acc[c][3])));
+    float4* d = reinterpret_cast<float4*>(act + G::o_p1 + ((qy + 1) * G::PW + qx + 1) * G::PC + 8 * h);
+    d[0] = make_float4(m[0], m[1], m[2], m[3]);
+    d[1] = make_float4(m[4], m[5], m[6], m[7]);
   }
   wave_lds_fence();
   if constexpr (STAMP) ts[3] = stamp();
-  // conv2 on MFMA: rows = positions, cols = output channels; k = ci*9 + tap
+  // conv2 on MFMA: rows = positions, cols = output channels.  MFMA step j of tap t sums the k-pair
+  // (t, ci = j) [lane half 0] and (t, ci = 8 + j) [half 1]: a lane's 8 A operands of a tap are 8
+  // consecutive channels of one position of the channel-last map = two ds_read_b128.
   const int col = lane & 31, kh = lane >> 5;
   for (int mt = 0; mt < G::MT2; ++mt) {
     const int pos = mt * 32 + col;
     const int py = pos / G::W2, px = pos % G::W2;
     f32x16 acc = {};
-#pragma unroll 4
-    for (int kk = 0; kk < K2 / 2; ++kk) {
-      const int k = 2 * kk + kh;
-      const int ci = k / 9, t = k % 9;
-      const float a = act[G::o_p1 + ci * G::PP + (py + t / 3) * G::PW + px + t % 3];
-      const float b = ws[S_W2 + col * K2 + k];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4* ap =
+          reinterpret_cast<const float4*>(act + G::o_p1 + ((py + t / 3) * G::PW + px + t % 3) * G::PC + 8 * kh);
+      const float4 a0 = ap[0], a1 = ap[1];
+      const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float b = WREG ? wreg[t * 8 + j] : ws[S_W2 + col * K2 + (8 * kh + j) * 9 + t];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b, acc, 0, 0, 0);
+      }
     }
     const float bias = ws[S_B2 + col];
 #pragma unroll
@@ -229,10 +240,15 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   if constexpr (STAMP) ts[1] = stamp();
   const float* wl = ws + S_WEND;
   const float* bl = wl + n * G::F;
+  float wreg[72];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wreg[t * 8 + j] = ws[S_W2 + (lane & 31) * K2 + (8 * (lane >> 5) + j) * 9 + t];
   bool first = true;
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
-    if (STAMP && first) sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, ts);
-    else sample_forward<H, W>(x + (size_t)s * 2 * G::HW, ws, act, lane);
+    if (STAMP && first) sample_forward<H, W, true, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, ts);
+    else sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg);
     float pf[G::F / 64];
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {
@@ -285,11 +301,12 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   gw1[0] = (f32x4){};
   gw1[1] = (f32x4){};
   float gb1[8], gb2 = 0.f, gbl = 0.f;
+  const float no_wreg[72] = {};   // unused: the backward reads conv2 weights from LDS (register budget)
 #pragma unroll
   for (int c = 0; c < 8; ++c) gb1[c] = 0.f;
 
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
-    sample_forward<H, W>(x + (size_t)s * 2 * G::HW, ws, act, lane);
+    sample_forward<H, W, false>(x + (size_t)s * 2 * G::HW, ws, act, lane, no_wreg);
     float* misc = act + G::o_misc;
     if (lane < n) {
       const float th = angles[(size_t)s * n + lane];
@@ -331,11 +348,11 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
       const float a = act[G::o_dz2 + col32 * G::PP + (py + 1) * G::PW + px + 1];
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
-        const int k = 32 * t + col32;
+        const int k = 32 * t + col32;   // column = tap * 16 + ci (16 lanes read 16 contiguous channels)
         float b = 0.f;
         if (k < K2) {
-          const int ci = k / 9, tp = k % 9;
-          b = act[G::o_p1 + ci * G::PP + (py + tp / 3) * G::PW + px + tp % 3];
+          const int tp = k >> 4, ci = k & 15;
+          b = act[G::o_p1 + ((py + tp / 3) * G::PW + px + tp % 3) * G::PC + ci];
         }
         gw2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, gw2[t], 0, 0, 0);
       }
@@ -414,7 +431,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = (r & 3) + 8 * (r >> 2) + 4 * kh, k = 32 * t + col32;
-      if (k < K2) mine[co * K2 + k] = gw2[t][r];
+      if (k < K2) mine[co * K2 + (k & 15) * 9 + (k >> 4)] = gw2[t][r];   // (tap, ci) -> flat [ci][tap]
     }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
