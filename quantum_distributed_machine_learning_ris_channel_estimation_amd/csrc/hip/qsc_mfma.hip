@@ -8,9 +8,10 @@
 // workgroup per sample with ~12 barriers per sample and scalar LDS-bound convolutions (0.75 LDS
 // loads per FMA): 46 us forward + 152 us backward for 2304 samples.  Here:
 //   * conv2 (M = positions, N = 32 channels, K = 144) is an implicit GEMM on
-//     v_mfma_f32_32x32x2_f32 (exact fp32, as the reference), operands gathered from the per-wave
-//     LDS image of the padded pool-1 map; conv1 (K = 18) stays on the VALU with a lane owning a
-//     pool window x 8 channels, so pool 1 happens in registers;
+//     v_mfma_f32_32x32x2_f32 (exact fp32, as the reference) from a channel-last LDS image of the
+//     padded pool-1 map (two ds_read_b128 feed 8 MFMAs), conv2 weights in registers; conv1
+//     (K = 18) stays on the VALU with a lane owning one row of a pool window x all 16 channels,
+//     so every conv1 weight is wave-uniform (scalar loads) and pool 1 is one lane shuffle;
 //   * backward: conv2 weight grads accumulate across the wave's samples in MFMA accumulators
 //     (5 tiles of 32x32, K = positions), conv2 data grads are a 16x16x4 MFMA implicit GEMM over
 //     the zero-padded dz2 image (K = 32 channels x 9 flipped taps), conv1 weight grads a 16x16x4
@@ -52,7 +53,8 @@ struct Geo {
   static constexpr int o_dp1 = o_dz2 + C2 * PP;                   // C1 x HW2
   static constexpr int o_dz1 = o_dp1 + C1 * HW2;                  // C1 x HW
   static constexpr int o_misc = o_dz1 + C1 * HW;                  // 32: dpre / angles
-  static constexpr int FWD = o_dz2;                               // forward needs x, p1, z2
+  static constexpr int o_p2f = o_dz2;                              // forward only: F pooled features
+  static constexpr int FWD = o_p2f + F;                            // forward needs x, p1, z2, p2
   static constexpr int BWD = o_misc + 32;
 };
 
@@ -72,9 +74,10 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 constexpr int NSTAMP = 12;
 
-// ... followed by the linear layer: wl [n][F] | bl [16] (LDS: a runtime-n loop over L2 loads of
-// wl serialises one round trip per iteration -- it dominated both kernels before staging)
-__host__ __device__ constexpr int act_base(int n, int F) { return S_WEND + ((n * F + 16 + 3) & ~3); }
+// ... followed by the linear layer: wl [n][F + 4] (row pad: conflict-free 4-lanes-per-output reads)
+// | bl [16] (LDS: a runtime-n loop over L2 loads of wl serialises one round trip per iteration)
+__host__ __device__ constexpr int wl_stride(int F) { return F + 4; }
+__host__ __device__ constexpr int act_base(int n, int F) { return S_WEND + ((n * wl_stride(F) + 16 + 3) & ~3); }
 
 // global -> LDS copy of n floats (both 16-byte aligned, n % 4 == 0): float4 loads, four in flight
 // per thread (a plain strided loop serialises one L2 round trip per iteration)
@@ -99,35 +102,38 @@ __device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Of
   stage4(ws + S_B1, flat + o.b1, C1);
   stage4(ws + S_W2, flat + o.w2, C2 * K2);
   stage4(ws + S_B2, flat + o.b2, C2);
-  stage4(ws + S_WEND, flat + o.wl, n * F);
-  if (threadIdx.x < n) ws[S_WEND + n * F + threadIdx.x] = flat[o.bl + threadIdx.x];
+  for (int j = 0; j < n; ++j) stage4(ws + S_WEND + j * wl_stride(F), flat + o.wl + j * F, F);
+  if (threadIdx.x < n) ws[S_WEND + n * wl_stride(F) + threadIdx.x] = flat[o.bl + threadIdx.x];
 }
 
-// conv1 pre-activations (+bias) of pool window `win` for channels [8h, 8h+8): acc[c][4 positions]
+// conv1 pre-activations (+bias) of one ROW of pool window `win` (hw = 0 top, 1 bottom): all 16
+// channels x 2 positions.  The whole wave walks the channels in lockstep, so every weight is
+// wave-uniform: scalar loads straight from the flat buffer (SGPR operands), no LDS traffic.
 template <int H, int W>
-__device__ __forceinline__ void conv1_window(const float* act, const float* ws, int win, int h, float (&acc)[8][4]) {
+__device__ __forceinline__ void conv1_half(const float* act, const float* __restrict__ w1g,
+                                           const float* __restrict__ b1g, int win, int hw, float (&acc)[16][2]) {
   using G = Geo<H, W>;
   const int qy = win / G::W2, qx = win % G::W2;
-  float patch[2][4][4];
+  float patch[2][3][4];
 #pragma unroll
   for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
-    for (int dy = 0; dy < 4; ++dy)
+    for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-      for (int dx = 0; dx < 4; ++dx) patch[ci][dy][dx] = act[G::o_x + ci * G::XP + (2 * qy + dy) * G::XW + 2 * qx + dx];
-#pragma unroll 2   // fully unrolled, the 144 per-lane weight loads get hoisted into VGPRs
-  for (int c = 0; c < 8; ++c) {
-    const int co = 8 * h + c;
-    const float b = ws[S_B1 + co];
+      for (int dx = 0; dx < 4; ++dx)
+        patch[ci][dy][dx] = act[G::o_x + ci * G::XP + (2 * qy + hw + dy) * G::XW + 2 * qx + dx];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) acc[c][p] = b;
+  for (int co = 0; co < C1; ++co) {
+    const float b = b1g[co];
+    acc[co][0] = b;
+    acc[co][1] = b;
 #pragma unroll
     for (int ci = 0; ci < 2; ++ci)
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const float w = ws[S_W1 + co * K1 + ci * 9 + t];
-#pragma unroll
-        for (int p = 0; p < 4; ++p) acc[c][p] += w * patch[ci][(p >> 1) + t / 3][(p & 1) + t % 3];
+        const float w = w1g[co * K1 + ci * 9 + t];
+        acc[co][0] += w * patch[ci][t / 3][t % 3];
+        acc[co][1] += w * patch[ci][t / 3][1 + t % 3];
       }
   }
 }
@@ -137,7 +143,8 @@ __device__ __forceinline__ void conv1_window(const float* act, const float* ws, 
 // [t*8 + j], register-resident across samples (forward kernel); null = read them from LDS.
 template <int H, int W, bool WREG, bool STAMP = false>
 __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane,
-                                               const float (&wreg)[72], unsigned long long* ts = nullptr) {
+                                               const float (&wreg)[72], const float* __restrict__ w1g,
+                                               const float* __restrict__ b1g, unsigned long long* ts = nullptr) {
   using G = Geo<H, W>;
   static_assert(W % 4 == 0, "float4 rows");
   const float4* x4 = reinterpret_cast<const float4*>(xs);   // sample planes are 16-byte aligned
@@ -153,19 +160,22 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
   }
   wave_lds_fence();
   if constexpr (STAMP) ts[2] = stamp();
-  // conv1 + ReLU + pool: lane = (window, channel half)
-  for (int win = lane & 31; win < G::HW2; win += 32) {
-    const int h = lane >> 5;
-    float acc[8][4];
-    conv1_window<H, W>(act, ws, win, h, acc);
-    const int qy = win / G::W2, qx = win % G::W2;
-    float m[8];
+  // conv1 + ReLU + pool: lane = (window, row of the window); the two rows meet with one shuffle
+  static_assert((2 * G::HW2) % 64 == 0, "whole waves per conv1 pass");
+  for (int idx = lane; idx < 2 * G::HW2; idx += 64) {
+    const int win = idx >> 1, hw = idx & 1;
+    float acc[16][2];
+    conv1_half<H, W>(act, w1g, b1g, win, hw, acc);
+    float m[16];
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      m[c] = fmaxf(fmaxf(relu(acc[c][0]), relu(acc[c][1])), fmaxf(relu(acc[c][2]), relu(acc[c][3])));
-    float4* d = reinterpret_cast<float4*>(act + G::o_p1 + ((qy + 1) * G::PW + qx + 1) * G::PC + 8 * h);
-    d[0] = make_float4(m[0], m[1], m[2], m[3]);
-    d[1] = make_float4(m[4], m[5], m[6], m[7]);
+    for (int c = 0; c < 16; ++c) {
+      const float v = fmaxf(relu(acc[c][0]), relu(acc[c][1]));
+      m[c] = fmaxf(v, __shfl_xor(v, 1));
+    }
+    const int qy = win / G::W2, qx = win % G::W2;
+    float4* d = reinterpret_cast<float4*>(act + G::o_p1 + ((qy + 1) * G::PW + qx + 1) * G::PC + 8 * hw);
+    d[0] = make_float4(m[8 * hw + 0], m[8 * hw + 1], m[8 * hw + 2], m[8 * hw + 3]);
+    d[1] = make_float4(m[8 * hw + 4], m[8 * hw + 5], m[8 * hw + 6], m[8 * hw + 7]);
   }
   wave_lds_fence();
   if constexpr (STAMP) ts[3] = stamp();
@@ -239,7 +249,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   __syncthreads();
   if constexpr (STAMP) ts[1] = stamp();
   const float* wl = ws + S_WEND;
-  const float* bl = wl + n * G::F;
+  const float* bl = wl + n * wl_stride(G::F);
   float wreg[72];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -247,21 +257,31 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
     for (int j = 0; j < 8; ++j) wreg[t * 8 + j] = ws[S_W2 + (lane & 31) * K2 + (8 * (lane >> 5) + j) * 9 + t];
   bool first = true;
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
-    if (STAMP && first) sample_forward<H, W, true, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, ts);
-    else sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg);
-    float pf[G::F / 64];
+    if (STAMP && first)
+      sample_forward<H, W, true, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, ts);
+    else
+      sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1);
+    float* p2s = act + G::o_p2f;
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {
       int arg;
-      pf[i] = pool2<H, W>(act, lane + 64 * i, arg);
-      p2[(size_t)s * G::F + lane + 64 * i] = pf[i];
+      const float v = pool2<H, W>(act, lane + 64 * i, arg);
+      p2s[lane + 64 * i] = v;
+      p2[(size_t)s * G::F + lane + 64 * i] = v;
     }
-    for (int j = 0; j < n; ++j) {
+    wave_lds_fence();
+    // linear: 4 lanes per output j (n <= 16), interleaved f (conflict-free), then 2 shuffles
+    {
+      const int j = lane >> 2, part = lane & 3;
       float acc = 0.f;
-#pragma unroll
-      for (int i = 0; i < G::F / 64; ++i) acc += wl[(size_t)j * G::F + lane + 64 * i] * pf[i];
-      acc = wave_sum(acc);
-      if (lane == 0) angles[(size_t)s * n + j] = tanhf(acc + bl[j]);
+      if (j < n) {
+        const float* wj = wl + j * wl_stride(G::F);
+#pragma unroll 8
+        for (int f = part; f < G::F; f += 4) acc += p2s[f] * wj[f];
+      }
+      acc += __shfl_xor(acc, 1);
+      acc += __shfl_xor(acc, 2);
+      if (j < n && part == 0) angles[(size_t)s * n + j] = tanhf(acc + bl[j]);
     }
     if (STAMP && first) {
       ts[5] = stamp();
@@ -300,13 +320,13 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   f32x4 gw1[2];                                    // dW1 tiles: rows = co, cols = k in [16t, 16t+16)
   gw1[0] = (f32x4){};
   gw1[1] = (f32x4){};
-  float gb1[8], gb2 = 0.f, gbl = 0.f;
+  float gb1[16], gb2 = 0.f, gbl = 0.f;
   const float no_wreg[72] = {};   // unused: the backward reads conv2 weights from LDS (register budget)
 #pragma unroll
-  for (int c = 0; c < 8; ++c) gb1[c] = 0.f;
+  for (int c = 0; c < 16; ++c) gb1[c] = 0.f;
 
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
-    sample_forward<H, W, false>(x + (size_t)s * 2 * G::HW, ws, act, lane, no_wreg);
+    sample_forward<H, W, false>(x + (size_t)s * 2 * G::HW, ws, act, lane, no_wreg, flat + o.w1, flat + o.b1);
     float* misc = act + G::o_misc;
     if (lane < n) {
       const float th = angles[(size_t)s * n + lane];
@@ -321,7 +341,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
     for (int i = 0; i < G::F / 64; ++i) {
       const int f = lane + 64 * i;
       float dp = 0.f;
-      for (int j = 0; j < n; ++j) dp += wl[(size_t)j * G::F + f] * misc[j];
+      for (int j = 0; j < n; ++j) dp += wl[j * wl_stride(G::F) + f] * misc[j];
       int arg;
       pool2<H, W>(act, f, arg);
       const int c = f / G::HW4, q = f % G::HW4, qy = q / G::W4, qx = q % G::W4;
@@ -374,30 +394,31 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
       for (int r = 0; r < 4; ++r) act[G::o_dp1 + col16 * G::HW2 + 16 * mt + 4 * kq + r] = acc[r];
     }
     wave_lds_fence();
-    // pool-1 backward (+ReLU mask): recompute the window's conv1 pre-activations; dz1 (C1 x HW)
-    for (int win = lane & 31; win < G::HW2; win += 32) {
-      const int h = lane >> 5;
-      float acc[8][4];
-      conv1_window<H, W>(act, ws, win, h, acc);
+    // pool-1 backward (+ReLU mask): recompute conv1 (lane = window row, all 16 channels, scalar
+    // weights), find each window's first max across the two row lanes, route dp1 -> dz1 (C1 x HW)
+    for (int idx = lane; idx < 2 * G::HW2; idx += 64) {
+      const int win = idx >> 1, hw = idx & 1;
+      float acc[16][2];
+      conv1_half<H, W>(act, flat + o.w1, flat + o.b1, win, hw, acc);
       const int qy = win / G::W2, qx = win % G::W2;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const int co = 8 * h + c;
+      for (int co = 0; co < 16; ++co) {
+        const float o0 = __shfl_xor(acc[co][0], 1), o1 = __shfl_xor(acc[co][1], 1);
+        // window scan order: top-left, top-right, bottom-left, bottom-right (reference argmax)
+        const float v[4] = {hw ? o0 : acc[co][0], hw ? o1 : acc[co][1], hw ? acc[co][0] : o0, hw ? acc[co][1] : o1};
         int am = 0;
-        float mv = relu(acc[c][0]);
+        float mv = relu(v[0]);
 #pragma unroll
         for (int p = 1; p < 4; ++p)
-          if (relu(acc[c][p]) > mv) {
-            mv = relu(acc[c][p]);
+          if (relu(v[p]) > mv) {
+            mv = relu(v[p]);
             am = p;
           }
-        const float g = (acc[c][am] > 0.f) ? act[G::o_dp1 + co * G::HW2 + win] : 0.f;
-        gb1[c] += g;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const int py = 2 * qy + (p >> 1), px = 2 * qx + (p & 1);
-          act[G::o_dz1 + co * G::HW + py * W + px] = (p == am) ? g : 0.f;
-        }
+        const float g = (v[am] > 0.f) ? act[G::o_dp1 + co * G::HW2 + win] : 0.f;
+        if (hw == 0) gb1[co] += g;
+        float* dz = act + G::o_dz1 + co * G::HW + (2 * qy + hw) * W + 2 * qx;
+        dz[0] = (am == 2 * hw) ? g : 0.f;
+        dz[1] = (am == 2 * hw + 1) ? g : 0.f;
       }
     }
     wave_lds_fence();
@@ -442,11 +463,9 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
     }
   // b1: lanes (win, h) hold 8 channels; combine the 32 windows of each half
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    float v = gb1[c];
-#pragma unroll
-    for (int m = 1; m < 32; m <<= 1) v += __shfl_xor(v, m);
-    if ((lane & 31) == 0) mine[C2 * K2 + C1 * K1 + 8 * kh + c] = v;
+  for (int c = 0; c < 16; ++c) {   // b1: per-window lanes hold all 16 channels
+    const float v = wave_sum(gb1[c]);
+    if (lane == 0) mine[C2 * K2 + C1 * K1 + c] = v;
   }
   {
     const float v = gb2 + __shfl_xor(gb2, 32);
