@@ -49,10 +49,12 @@ struct Geo {
   static constexpr int o_x = 0;                                   // 2 x XP
   static constexpr int o_p1 = o_x + 2 * XP;                       // C1 x PP (padded pool-1 map)
   static constexpr int o_z2 = o_p1 + PC * PP;                     // C2 x HW2 (conv2 pre-activation)
-  static constexpr int o_dz2 = o_z2 + C2 * HW2;                   // C2 x PP (padded conv2 grad)
-  static constexpr int o_dp1 = o_dz2 + C2 * PP;                   // C1 x HW2
-  static constexpr int o_dz1 = o_dp1 + C1 * HW2;                  // C1 x HW
-  static constexpr int o_misc = o_dz1 + C1 * HW;                  // 32: dpre / angles
+  static constexpr int DC = 36;  // dz2 is channel-last too: 32 channels (+4 pad) per padded position
+  static constexpr int o_dz2 = o_z2 + C2 * HW2;                   // PP x DC (padded conv2 grad)
+  static constexpr int o_dp1 = o_dz2 + PP * DC;                   // C1 x HW2
+  static constexpr int o_dz1 = o_z2;                              // C1 x HW, aliases z2 + dz2 (dead by then)
+  static_assert(C1 * HW <= C2 * HW2 + PP * DC, "dz1 alias");
+  static constexpr int o_misc = o_dp1 + C1 * HW2;                 // 32: dpre / angles
   static constexpr int o_p2f = o_dz2;                              // forward only: F pooled features
   static constexpr int FWD = o_p2f + F;                            // forward needs x, p1, z2, p2
   static constexpr int BWD = o_misc + 32;
@@ -78,6 +80,10 @@ constexpr int NSTAMP = 12;
 // | bl [16] (LDS: a runtime-n loop over L2 loads of wl serialises one round trip per iteration)
 __host__ __device__ constexpr int wl_stride(int F) { return F + 4; }
 __host__ __device__ constexpr int act_base(int n, int F) { return S_WEND + ((n * wl_stride(F) + 16 + 3) & ~3); }
+// backward only: W2 transposed to [tap][ci][co] (co contiguous, stride 36) after the linear layer
+constexpr int W2T_CS = 36;
+constexpr int W2T_SIZE = 9 * C1 * W2T_CS;
+__host__ __device__ constexpr int act_base_bwd(int n, int F) { return act_base(n, F) + W2T_SIZE; }
 
 // global -> LDS copy of n floats (both 16-byte aligned, n % 4 == 0): float4 loads, four in flight
 // per thread (a plain strided loop serialises one L2 round trip per iteration)
@@ -102,7 +108,14 @@ __device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Of
   stage4(ws + S_B1, flat + o.b1, C1);
   stage4(ws + S_W2, flat + o.w2, C2 * K2);
   stage4(ws + S_B2, flat + o.b2, C2);
-  for (int j = 0; j < n; ++j) stage4(ws + S_WEND + j * wl_stride(F), flat + o.wl + j * F, F);
+  {  // linear weights: one flat loop (a loop of per-row copies serialised ~2k cycles per row)
+    const int q4 = F / 4;
+    const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
+    for (int i = threadIdx.x; i < n * q4; i += blockDim.x) {
+      const int j = i / q4, c = i % q4;
+      *reinterpret_cast<float4*>(ws + S_WEND + j * wl_stride(F) + 4 * c) = src[i];
+    }
+  }
   if (threadIdx.x < n) ws[S_WEND + n * wl_stride(F) + threadIdx.x] = flat[o.bl + threadIdx.x];
 }
 
@@ -298,18 +311,28 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
 // Backward.  dang (B, n) = dL/d(angles).  Outputs: dpre (B, n) = dL/d(pre-tanh) (for the linear
 // weight-gradient GEMM), slab row per workgroup = grads of [w1 | b1 | w2 | b2 | (wl: 0) | bl] in
 // the flat layout starting at o.w1.
-template <int H, int W, int NWV>
+template <int H, int W, int NWV, bool STAMP = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                       Offs o, const float* __restrict__ angles,
                                                       const float* __restrict__ dang, float* __restrict__ dpre_out,
-                                                      float* __restrict__ slab, int B, int n) {
+                                                      float* __restrict__ slab, int B, int n,
+                                                      unsigned long long* __restrict__ stamps = nullptr) {
+  unsigned long long ts[NSTAMP] = {};
+  bool first = true;
+  if constexpr (STAMP) ts[0] = stamp();
   using G = Geo<H, W>;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ws = sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float* act = sm + act_base(n, G::F) + wv * G::BWD;
+  float* act = sm + act_base_bwd(n, G::F) + wv * G::BWD;
+  float* w2t = sm + act_base(n, G::F);
   stage_weights(flat, o, ws, n, G::F);
   for (int i = lane; i < G::BWD; i += 64) act[i] = 0.f;
+  __syncthreads();
+  for (int i = threadIdx.x; i < C2 * K2; i += 64 * NWV) {   // W2 [co][ci][tap] -> W2T [tap][ci][co]
+    const int co = i / K2, ci = (i % K2) / 9, t = i % 9;
+    w2t[(t * C1 + ci) * W2T_CS + co] = ws[S_W2 + i];
+  }
   __syncthreads();
   const float* wl = ws + S_WEND;
   const int col32 = lane & 31, kh = lane >> 5;     // 32x32x2 operand coordinates
@@ -326,7 +349,9 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   for (int c = 0; c < 16; ++c) gb1[c] = 0.f;
 
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
+    if (STAMP && first) ts[1] = stamp();
     sample_forward<H, W, false>(x + (size_t)s * 2 * G::HW, ws, act, lane, no_wreg, flat + o.w1, flat + o.b1);
+    if (STAMP && first) ts[2] = stamp();
     float* misc = act + G::o_misc;
     if (lane < n) {
       const float th = angles[(size_t)s * n + lane];
@@ -351,21 +376,22 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
       for (int r = 0; r < 4; ++r) {
         const int py = 2 * qy + (r >> 1), px = 2 * qx + (r & 1);
         const int pidx = py * G::W2 + px;
-        act[G::o_dz2 + c * G::PP + (py + 1) * G::PW + px + 1] = (pidx == arg && pass) ? dp : 0.f;
+        act[G::o_dz2 + ((py + 1) * G::PW + px + 1) * G::DC + c] = (pidx == arg && pass) ? dp : 0.f;
       }
     }
     wave_lds_fence();
+    if (STAMP && first) ts[3] = stamp();
     // conv2 bias grad: lane (co, half) sums half of the positions
     {
-      const float* dz = act + G::o_dz2 + col32 * G::PP;
-      for (int p = kh; p < G::HW2; p += 2) gb2 += dz[(p / G::W2 + 1) * G::PW + p % G::W2 + 1];
+      const float* dz = act + G::o_dz2 + col32;
+      for (int p = kh; p < G::HW2; p += 2) gb2 += dz[((p / G::W2 + 1) * G::PW + p % G::W2 + 1) * G::DC];
     }
     // conv2 weight grads: dW2[co][k] += sum_pos dz2[co][pos] * im2col(p1)[pos][k]  (K = positions)
 #pragma unroll 2
     for (int kk = 0; kk < G::HW2 / 2; ++kk) {
       const int pos = 2 * kk + kh;
       const int py = pos / G::W2, px = pos % G::W2;
-      const float a = act[G::o_dz2 + col32 * G::PP + (py + 1) * G::PW + px + 1];
+      const float a = act[G::o_dz2 + ((py + 1) * G::PW + px + 1) * G::DC + col32];
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
         const int k = 32 * t + col32;   // column = tap * 16 + ci (16 lanes read 16 contiguous channels)
@@ -377,23 +403,30 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
         gw2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, gw2[t], 0, 0, 0);
       }
     }
-    // conv2 data grads: dp1[ci][pos] = sum_{co,tap} dz2_pad[co][pos + 2 - tap] * W2[co][ci][tap]
+    if (STAMP && first) ts[4] = stamp();
+    // conv2 data grads: dp1[ci][pos] = sum_{tap,co} dz2_pad[pos + 2 - tap][co] * W2[co][ci][tap].
+    // MFMA step j of tap t sums k = (t, co = 8*kq + j) over the four lane groups kq: a lane's 8 A
+    // (dz2, channel-last) and 8 B (W2T, co-contiguous) operands of a tap are 2 + 2 ds_read_b128.
     for (int mt = 0; mt < G::MT1; ++mt) {
       const int pos = 16 * mt + col16;
       const int py = pos / G::W2, px = pos % G::W2;
       f32x4 acc = {};
-#pragma unroll 4
-      for (int kk = 0; kk < 2 * K2 / 4; ++kk) {   // K = 32 co x 9 taps = 288
-        const int k = 4 * kk + kq;
-        const int co = k / 9, tp = k % 9;
-        const float a = act[G::o_dz2 + co * G::PP + (py + 2 - tp / 3) * G::PW + px + 2 - tp % 3];
-        const float b = ws[S_W2 + co * K2 + col16 * 9 + tp];
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float4* ap = reinterpret_cast<const float4*>(
+            act + G::o_dz2 + ((py + 2 - t / 3) * G::PW + px + 2 - t % 3) * G::DC + 8 * kq);
+        const float4* bp = reinterpret_cast<const float4*>(w2t + (t * C1 + col16) * W2T_CS + 8 * kq);
+        const float4 a0 = ap[0], a1 = ap[1], b0 = bp[0], b1 = bp[1];
+        const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) act[G::o_dp1 + col16 * G::HW2 + 16 * mt + 4 * kq + r] = acc[r];
     }
     wave_lds_fence();
+    if (STAMP && first) ts[5] = stamp();
     // pool-1 backward (+ReLU mask): recompute conv1 (lane = window row, all 16 channels, scalar
     // weights), find each window's first max across the two row lanes, route dp1 -> dz1 (C1 x HW)
     for (int idx = lane; idx < 2 * G::HW2; idx += 64) {
@@ -422,6 +455,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
       }
     }
     wave_lds_fence();
+    if (STAMP && first) ts[6] = stamp();
     // conv1 weight grads: dW1[co][k] += sum_pos dz1[co][pos] * im2col(x)[pos][k]  (K = positions)
 #pragma unroll 4
     for (int kk = 0; kk < G::HW / 4; ++kk) {
@@ -440,6 +474,10 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
       }
     }
     wave_lds_fence();
+    if (STAMP && first) {
+      ts[7] = stamp();
+      first = false;
+    }
   }
 
   // ---- deterministic workgroup reduction -> slab row (w1 | b1 | w2 | b2 | wl = 0 | bl) ----
@@ -474,6 +512,11 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   if (lane < 16) mine[C2 * K2 + C1 * K1 + C1 + C2 + lane] = lane < n ? gbl : 0.f;
   __syncthreads();
   float* row = slab + (size_t)blockIdx.x * o.row;
+  if constexpr (STAMP) {
+    ts[8] = stamp();
+    if (lane == 0)
+      for (int k = 0; k < NSTAMP; ++k) stamps[(size_t)(blockIdx.x * NWV + wv) * NSTAMP + k] = ts[k];
+  }
   for (int i = threadIdx.x; i < o.row; i += 64 * NWV) {
     float v = 0.f;
     int src = -1;
@@ -502,7 +545,7 @@ size_t fwd_smem(int n) {
 }
 template <int H, int W>
 size_t bwd_smem(int n) {
-  const size_t act = act_base(n, Geo<H, W>::F) + bwd_waves<W>() * Geo<H, W>::BWD;
+  const size_t act = act_base_bwd(n, Geo<H, W>::F) + bwd_waves<W>() * Geo<H, W>::BWD;
   const size_t red = S_WEND + bwd_waves<W>() * (C2 * K2 + C1 * K1 + C1 + C2 + 16);
   return sizeof(float) * (act > red ? act : red);
 }
@@ -527,13 +570,19 @@ int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* 
 
 template <int H, int W>
 int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, const float* dang, float* dpre,
-               float* slab, int B, int n, int grid, hipStream_t s) {
+               float* slab, int B, int n, int grid, hipStream_t s, unsigned long long* stamps = nullptr) {
   constexpr int NW = bwd_waves<W>();
   const size_t sm = bwd_smem<H, W>(n);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW>, sm)) return (int)e;
-  hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang, dpre,
-                     slab, B, n);
+  if (stamps) {
+    if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW, true>, sm)) return (int)e;
+    hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW, true>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang,
+                       dpre, slab, B, n, stamps);
+  } else {
+    if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW>, sm)) return (int)e;
+    hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang, dpre,
+                       slab, B, n, nullptr);
+  }
   return (int)hipGetLastError();
 }
 
@@ -579,5 +628,19 @@ QD_API int qd_qsc2_fwd_stamped(const float* x, const float* flat, const int* off
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
   if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, B, n, grid, (hipStream_t)stream, stamps);
   if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, B, n, grid, (hipStream_t)stream, stamps);
+  return (int)hipErrorInvalidValue;
+}
+
+// Diagnostic: backward with per-wave phase stamps (stamps: grid * waves * 12 u64): [0] start
+// [1] weights staged [2] forward recompute [3] linear + pool-2 backward [4] conv2 weight grads
+// [5] conv2 data grads [6] pool-1 backward [7] conv1 weight grads (first sample) [8] wave done.
+QD_API int qd_qsc2_bwd_stamped(const float* x, const float* flat, const int* offs, const float* angles,
+                               const float* dang, float* dpre, float* slab, int B, int n, int H, int W, int grid,
+                               unsigned long long* stamps, void* stream) {
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  if (H == 16 && W == 8)
+    return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, B, n, grid, (hipStream_t)stream, stamps);
+  if (H == 16 && W == 16)
+    return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, B, n, grid, (hipStream_t)stream, stamps);
   return (int)hipErrorInvalidValue;
 }
