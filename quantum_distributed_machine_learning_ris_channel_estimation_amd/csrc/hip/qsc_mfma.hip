@@ -102,6 +102,18 @@ __device__ __forceinline__ void stage4(float* dst, const float* __restrict__ src
   for (; i < n4; i += nt) d4[i] = s4[i];
 }
 
+// forward kernel LDS: just the linear layer (wl [n][F+4] | bl), then the per-wave images
+__host__ __device__ constexpr int fwd_act_base(int n, int F) { return (n * (F + 4) + 16 + 3) & ~3; }
+__device__ __forceinline__ void stage_linear(const float* __restrict__ flat, Offs o, float* ws, int n, int F) {
+  const int q4 = F / 4;
+  const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
+  for (int i = threadIdx.x; i < n * q4; i += blockDim.x) {
+    const int j = i / q4, c = i % q4;
+    *reinterpret_cast<float4*>(ws + j * (F + 4) + 4 * c) = src[i];
+  }
+  if (threadIdx.x < n) ws[n * (F + 4) + threadIdx.x] = flat[o.bl + threadIdx.x];
+}
+
 // (all offsets are multiples of 16 floats: FlatParamSpace ALIGN; LDS slots multiples of 4)
 __device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Offs o, float* ws, int n, int F) {
   stage4(ws + S_W1, flat + o.w1, C1 * K1);
@@ -157,7 +169,8 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
 template <int H, int W, bool WREG, bool STAMP = false>
 __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane,
                                                const float (&wreg)[72], const float* __restrict__ w1g,
-                                               const float* __restrict__ b1g, unsigned long long* ts = nullptr) {
+                                               const float* __restrict__ b1g, float bias2,
+                                               unsigned long long* ts = nullptr) {
   using G = Geo<H, W>;
   static_assert(W % 4 == 0, "float4 rows");
   const float4* x4 = reinterpret_cast<const float4*>(xs);   // sample planes are 16-byte aligned
@@ -212,11 +225,10 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b, acc, 0, 0, 0);
       }
     }
-    const float bias = ws[S_B2 + col];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
-      act[G::o_z2 + col * G::HW2 + mt * 32 + row] = acc[r] + bias;
+      act[G::o_z2 + col * G::HW2 + mt * 32 + row] = acc[r] + bias2;
     }
   }
   wave_lds_fence();
@@ -256,24 +268,41 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ws = sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float* act = sm + act_base(n, G::F) + wv * G::FWD;
-  stage_weights(flat, o, ws, n, G::F);
+  // LDS: only the linear layer is staged; conv1 weights are scalar loads, conv2 weights live in
+  // registers (loaded straight from the flat buffer), conv2 bias is one value per lane
+  float* act = sm + fwd_act_base(n, G::F) + wv * G::FWD;
+  stage_linear(flat, o, ws, n, G::F);
   for (int i = lane; i < G::FWD; i += 64) act[i] = 0.f;   // zero halos once; interiors rewritten per sample
+  // this lane's weights W2[co][8h .. 8h+7][0..8] are 72 contiguous floats: 18 float4 loads
+  float wreg[72];
+  {
+    const float4* wp = reinterpret_cast<const float4*>(flat + o.w2 + (lane & 31) * K2 + 72 * (lane >> 5));
+    float tmp[72];
+#pragma unroll
+    for (int q = 0; q < 18; ++q) {
+      const float4 v = wp[q];
+      tmp[4 * q] = v.x;
+      tmp[4 * q + 1] = v.y;
+      tmp[4 * q + 2] = v.z;
+      tmp[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wreg[t * 8 + j] = tmp[j * 9 + t];
+  }
+  const float bias2 = flat[o.b2 + (lane & 31)];
   __syncthreads();
   if constexpr (STAMP) ts[1] = stamp();
-  const float* wl = ws + S_WEND;
+  const float* wl = ws;
   const float* bl = wl + n * wl_stride(G::F);
-  float wreg[72];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) wreg[t * 8 + j] = ws[S_W2 + (lane & 31) * K2 + (8 * (lane >> 5) + j) * 9 + t];
   bool first = true;
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
     if (STAMP && first)
-      sample_forward<H, W, true, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, ts);
+      sample_forward<H, W, true, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, bias2,
+                                       ts);
     else
-      sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1);
+      sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, bias2);
     float* p2s = act + G::o_p2f;
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {
@@ -350,7 +379,8 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
 
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
     if (STAMP && first) ts[1] = stamp();
-    sample_forward<H, W, false>(x + (size_t)s * 2 * G::HW, ws, act, lane, no_wreg, flat + o.w1, flat + o.b1);
+    sample_forward<H, W, false>(x + (size_t)s * 2 * G::HW, ws, act, lane, no_wreg, flat + o.w1, flat + o.b1,
+                                ws[S_B2 + (lane & 31)]);
     if (STAMP && first) ts[2] = stamp();
     float* misc = act + G::o_misc;
     if (lane < n) {
@@ -360,6 +390,9 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
       dpre_out[(size_t)s * n + lane] = d;
       gbl += d;
     }
+    // dz2's zero halo is clobbered by the previous sample's dz1 (aliased): re-zero the image
+    for (int i = lane; i < G::PP * G::DC / 4; i += 64)
+      reinterpret_cast<float4*>(act + G::o_dz2)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     wave_lds_fence();
     // linear backward -> dp2, pool-2 backward (+ReLU mask) -> padded dz2
 #pragma unroll
@@ -541,7 +574,7 @@ constexpr int bwd_waves() { return W == 8 ? 4 : 2; }
 
 template <int H, int W>
 size_t fwd_smem(int n) {
-  return sizeof(float) * (act_base(n, Geo<H, W>::F) + fwd_waves<W>() * Geo<H, W>::FWD);
+  return sizeof(float) * (fwd_act_base(n, Geo<H, W>::F) + fwd_waves<W>() * Geo<H, W>::FWD);
 }
 template <int H, int W>
 size_t bwd_smem(int n) {
