@@ -126,30 +126,48 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const TIN* __restrict__ xi
         tile[((p / W + 1) * G::WP + (p % W) + 1) * CINP + c] = (__bf16)v;
       }
     } else {
+      // batched two-phase staging: issue UNR passes' global loads (8 values each) together, then
+      // transform + scatter to LDS.  A rolled loop waited one L2/HBM round trip per pass, which made
+      // this staging -- not the MFMAs -- the kernel's critical path.
       constexpr int CH8 = CIN * G::HW / 8;
-      for (int i = lane; i < CH8; i += 64) {
-        const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
-        float v[8];
-        load8(xin + base + (size_t)c * G::HW + p0, v);
-        const float* sc = st_u + (size_t)(e * CIN + c) * NST;
-        if constexpr (INM == IN_BNRELU) {
-          const float a = sc[ST_A], b = sc[ST_B];
+      static_assert(CH8 % 64 == 0, "whole waves per staging pass");
+      constexpr int ITER = CH8 / 64;
+      constexpr int UNR0 = INM == IN_BNBWD ? 2 : 4;             // passes in flight (register budget)
+      constexpr int UNR = ITER < UNR0 ? ITER : UNR0;
+      static_assert(ITER % UNR == 0, "staging batches");
+#pragma unroll 1
+      for (int it0 = 0; it0 < ITER; it0 += UNR) {
+        float v[UNR][8];
+        [[maybe_unused]] float z[INM == IN_BNBWD ? UNR : 1][8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaxf(a * v[j] + b, 0.f);
-        } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
-          float z[8];
-          load8(zaux + base + (size_t)c * G::HW + p0, z);
-          const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
-          const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float g = (a * z[j] + b > 0.f) ? v[j] : 0.f;
-            v[j] = c1 * g - c2 - c3 * (z[j] - mu) * inv;
-          }
+        for (int u = 0; u < UNR; ++u) {
+          const int i = lane + 64 * (it0 + u);
+          const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
+          load8(xin + base + (size_t)c * G::HW + p0, v[u]);
+          if constexpr (INM == IN_BNBWD) load8(zaux + base + (size_t)c * G::HW + p0, z[u]);
         }
-        const int ph = p0 / W, pw = p0 % W;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) tile[((ph + 1) * G::WP + pw + j + 1) * CINP + c] = (__bf16)v[j];
+        for (int u = 0; u < UNR; ++u) {
+          const int i = lane + 64 * (it0 + u);
+          const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
+          const float* sc = st_u + (size_t)(e * CIN + c) * NST;
+          if constexpr (INM == IN_BNRELU) {
+            const float a = sc[ST_A], b = sc[ST_B];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[u][j] = fmaxf(a * v[u][j] + b, 0.f);
+          } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
+            const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+            const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float g = (a * z[u][j] + b > 0.f) ? v[u][j] : 0.f;
+              v[u][j] = c1 * g - c2 - c3 * (z[u][j] - mu) * inv;
+            }
+          }
+          const int ph = p0 / W, pw = p0 % W;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) tile[((ph + 1) * G::WP + pw + j + 1) * CINP + c] = (__bf16)v[u][j];
+        }
       }
     }
     wave_lds_fence();

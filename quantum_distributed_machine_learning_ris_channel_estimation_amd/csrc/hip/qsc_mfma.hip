@@ -272,7 +272,9 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   // registers (loaded straight from the flat buffer), conv2 bias is one value per lane
   float* act = sm + fwd_act_base(n, G::F) + wv * G::FWD;
   stage_linear(flat, o, ws, n, G::F);
-  for (int i = lane; i < G::FWD; i += 64) act[i] = 0.f;   // zero halos once; interiors rewritten per sample
+  static_assert(G::FWD % 4 == 0 && G::BWD % 4 == 0, "float4 image fills");
+  for (int i = lane; i < G::FWD / 4; i += 64)   // zero halos once; interiors rewritten per sample
+    reinterpret_cast<float4*>(act)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   // this lane's weights W2[co][8h .. 8h+7][0..8] are 72 contiguous floats: 18 float4 loads
   float wreg[72];
   {
@@ -356,7 +358,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   float* act = sm + act_base_bwd(n, G::F) + wv * G::BWD;
   float* w2t = sm + act_base(n, G::F);
   stage_weights(flat, o, ws, n, G::F);
-  for (int i = lane; i < G::BWD; i += 64) act[i] = 0.f;
+  for (int i = lane; i < G::BWD / 4; i += 64) reinterpret_cast<float4*>(act)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
   for (int i = threadIdx.x; i < C2 * K2; i += 64 * NWV) {   // W2 [co][ci][tap] -> W2T [tap][ci][co]
     const int co = i / K2, ci = (i % K2) / 9, t = i % 9;
