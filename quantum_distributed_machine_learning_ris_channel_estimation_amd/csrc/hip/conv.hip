@@ -29,6 +29,8 @@
 //                    ds_read_b128.
 //   bn_*             statistics finalisation (+ running-stat momentum updates in stream order),
 //                    backward reductions, and the final BN+ReLU apply that feeds the FC GEMM.
+#include <algorithm>
+
 #include "common.h"
 
 namespace qd {
@@ -602,12 +604,31 @@ __global__ void __launch_bounds__(256) slab_rows_sum_kernel(const float* __restr
 
 // Vector variant (width % 4 == 0, 16-byte aligned rows): 16 column quads x 16 row phases per
 // block, float4 loads, unrolled so each thread keeps several independent loads in flight.
+__device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
+                                                    int width, int g, int bx);
 __global__ void __launch_bounds__(256) slab_rows_sum4_kernel(const float* __restrict__ slab, float* __restrict__ out,
                                                              int groups, int rows, int width) {
+  slab_rows_sum4_body(slab, out, rows, width, blockIdx.y, blockIdx.x);
+}
+
+// Several independent slab sums in one launch (blockIdx.z = job): the conv stack's three weight-
+// gradient reductions at the end of its backward.
+struct SlabJobs {
+  const float* slab[4];
+  float* out[4];
+  int groups[4], rows[4], width[4];
+};
+__global__ void __launch_bounds__(256) slab_rows_sum4_multi_kernel(SlabJobs jobs) {
+  const int j = blockIdx.z;
+  if (blockIdx.y >= jobs.groups[j] || blockIdx.x * 64 >= jobs.width[j]) return;
+  slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x);
+}
+
+__device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
+                                                    int width, int g, int bx) {
   __shared__ float4 red[16][16];
   const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int i = (blockIdx.x * 16 + tq) * 4;
-  const int g = blockIdx.y;
+  const int i = (bx * 16 + tq) * 4;
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < width) {
     const float* s = slab + (size_t)g * rows * width + i;
@@ -796,6 +817,26 @@ QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int
                        h8, qs, amax);
   else
     return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// n <= 4 jobs, each as qd_slab_rows_sum (width % 4 == 0, 16-byte aligned), one launch
+QD_API int qd_slab_rows_sum_multi(int n, const float* const* slabs, float* const* outs, const int* groups,
+                                  const int* rows, const int* widths, void* stream) {
+  if (n < 1 || n > 4) return (int)hipErrorInvalidValue;
+  SlabJobs jobs{};
+  int gx = 0, gy = 0;
+  for (int j = 0; j < n; ++j) {
+    if (widths[j] % 4 || ((uintptr_t)slabs[j] & 15) || ((uintptr_t)outs[j] & 15)) return (int)hipErrorInvalidValue;
+    jobs.slab[j] = slabs[j];
+    jobs.out[j] = outs[j];
+    jobs.groups[j] = groups[j];
+    jobs.rows[j] = rows[j];
+    jobs.width[j] = widths[j];
+    gx = std::max(gx, (widths[j] / 4 + 15) / 16);
+    gy = std::max(gy, groups[j]);
+  }
+  hipLaunchKernelGGL(slab_rows_sum4_multi_kernel, dim3(gx, gy, n), dim3(256), 0, (hipStream_t)stream, jobs);
   return (int)hipGetLastError();
 }
 

@@ -66,6 +66,7 @@ class ConvStackHIP:
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
         self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
+        self._ssum_multi = nat.fn(L, "qd_slab_rows_sum_multi", [_i, _p, _p, _p, _p, _p, _p])
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
 
     def pack_weights(self, st) -> None:
@@ -117,11 +118,16 @@ class ConvStackHIP:
             nat.check(self._wgrad(k + 1, nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst),
                                   nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_w, self.spb_w, st),
                       f"conv_wgrad{k + 1}")
-            nat.check(self._ssum(nat.ptr(ws), nat.ptr(m.conv_w[k].grad), self.E, ws.shape[1], ws.shape[2], st),
-                      f"wslab_sum{k + 1}")
             if k > 0:
                 dx = self.dx[k - 1]
                 nat.check(self._dgrad(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.wpk_t[k]),
                                       nat.ptr(dx), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw, st),
                           f"conv_dgrad{k + 1}")
                 dh, dh_bf = dx, 0
+        # the three weight-gradient slabs -> conv_w grads in one launch
+        slabs = (ctypes.c_void_p * 4)(*[nat.ptr(w) for w in self.wslab])
+        outs = (ctypes.c_void_p * 4)(*[nat.ptr(m.conv_w[k].grad) for k in range(3)])
+        groups = (ctypes.c_int * 4)(*[self.E] * 3)
+        rows = (ctypes.c_int * 4)(*[w.shape[1] for w in self.wslab])
+        widths = (ctypes.c_int * 4)(*[w.shape[2] for w in self.wslab])
+        nat.check(self._ssum_multi(3, slabs, outs, groups, rows, widths, st), "wslab_sum")

@@ -85,8 +85,9 @@ class FlagshipTrainer:
         self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)
         self.perm = torch.randperm(self.store.n, device=dev)
         self.cursor = 0
-        self.hloss = torch.zeros(2, device=dev)
-        self.qloss = torch.zeros(1, device=dev)
+        # the loss kernels' own static buffers double as the step's loss outputs (no per-step copies)
+        self.hloss = self.hstep.nmse.loss
+        self.qloss = self.cstep.hip.loss if self.cstep.hip is not None else torch.zeros(1, device=dev)
         self.labels = self.store.scen.repeat_interleave(self.B)
         graphs = cfg.hip_graphs and dev.type == "cuda"
         if ctx.world == 1 and not cfg.split_graphs:
@@ -105,12 +106,14 @@ class FlagshipTrainer:
         self.qspace.zero_grad()
         self.gat(self.store, self.idx)           # one launch: conv input, classifier input, label rows
         loss = self.hstep.forward_fc_gathered(self.gat, self.store)
-        self.hloss.copy_(loss)
+        if loss is not self.hloss:
+            self.hloss.copy_(loss)
 
     def _phase2(self) -> None:
         self.hstep.backward_conv()
         q = self.cstep(self.gat.xq, self.labels)
-        self.qloss.copy_(q)
+        if q is not self.qloss:
+            self.qloss.copy_(q)
 
     def _phase3(self) -> None:
         g = 1.0 / self.ctx.world
