@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restric
 __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __restrict__ slab,
                                                              const float* __restrict__ gamma, float* __restrict__ st,
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                             int U, int chunks, int EC, float count) {
+                                                             int U, int chunks, int EC, float count, int accumulate) {
   const int ch = blockIdx.x, lane = threadIdx.x;
   float tg = 0.f, tgx = 0.f;
   for (int u = 0; u < U; ++u) {
@@ -543,8 +543,8 @@ __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __rest
     tgx += sgx;
   }
   if (lane == 0) {
-    dgamma[ch] += tgx;
-    dbeta[ch] += tg;
+    dgamma[ch] = (accumulate ? dgamma[ch] : 0.f) + tgx;
+    dbeta[ch] = (accumulate ? dbeta[ch] : 0.f) + tg;
   }
 }
 
@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __re
 // out[i] += sum_rows slab[g][row][i] for every group g (rows contiguous per group).
 // block = 64 columns x 4 row phases; deterministic order (fixed per-thread row sets + fixed combine).
 __global__ void __launch_bounds__(256) slab_rows_sum_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                                            int groups, int rows, int width) {
+                                                            int groups, int rows, int width, int accumulate) {
   __shared__ float red[4][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + tx;
@@ -599,16 +599,18 @@ __global__ void __launch_bounds__(256) slab_rows_sum_kernel(const float* __restr
   }
   red[ty][tx] = t;
   __syncthreads();
-  if (ty == 0 && i < width) out[(size_t)g * width + i] += (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+  if (ty == 0 && i < width)
+    out[(size_t)g * width + i] = (accumulate ? out[(size_t)g * width + i] : 0.f) + (red[0][tx] + red[1][tx]) +
+                                 (red[2][tx] + red[3][tx]);
 }
 
 // Vector variant (width % 4 == 0, 16-byte aligned rows): 16 column quads x 16 row phases per
 // block, float4 loads, unrolled so each thread keeps several independent loads in flight.
 __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
-                                                    int width, int g, int bx);
+                                                    int width, int g, int bx, int accumulate);
 __global__ void __launch_bounds__(256) slab_rows_sum4_kernel(const float* __restrict__ slab, float* __restrict__ out,
-                                                             int groups, int rows, int width) {
-  slab_rows_sum4_body(slab, out, rows, width, blockIdx.y, blockIdx.x);
+                                                             int groups, int rows, int width, int accumulate) {
+  slab_rows_sum4_body(slab, out, rows, width, blockIdx.y, blockIdx.x, accumulate);
 }
 
 // Several independent slab sums in one launch (blockIdx.z = job): the conv stack's three weight-
@@ -617,15 +619,16 @@ struct SlabJobs {
   const float* slab[4];
   float* out[4];
   int groups[4], rows[4], width[4];
+  int accumulate;
 };
 __global__ void __launch_bounds__(256) slab_rows_sum4_multi_kernel(SlabJobs jobs) {
   const int j = blockIdx.z;
   if (blockIdx.y >= jobs.groups[j] || blockIdx.x * 64 >= jobs.width[j]) return;
-  slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x);
+  slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x, jobs.accumulate);
 }
 
 __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
-                                                    int width, int g, int bx) {
+                                                    int width, int g, int bx, int accumulate) {
   __shared__ float4 red[16][16];
   const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int i = (bx * 16 + tq) * 4;
@@ -653,7 +656,7 @@ __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ sl
       acc.w += red[k][tq].w;
     }
     float4* o = reinterpret_cast<float4*>(out + (size_t)g * width + i);
-    float4 cur = *o;
+    float4 cur = accumulate ? *o : make_float4(0.f, 0.f, 0.f, 0.f);
     cur.x += acc.x;
     cur.y += acc.y;
     cur.z += acc.z;
@@ -795,10 +798,11 @@ QD_API int qd_bn_bwd_reduce(const void* dh, int dh_bf16, const uint16_t* z, cons
   return (int)hipGetLastError();
 }
 
+// accumulate = 0: overwrite dgamma/dbeta (no zero_grad needed)
 QD_API int qd_bn_bwd_finalize(const float* slab, const float* gamma, float* st, float* dgamma, float* dbeta, int U,
-                              int chunks, int EC, float count, void* stream) {
+                              int chunks, int EC, float count, int accumulate, void* stream) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(EC), dim3(64), 0, (hipStream_t)stream, slab, gamma, st,
-                     dgamma, dbeta, U, chunks, EC, count);
+                     dgamma, dbeta, U, chunks, EC, count, accumulate);
   return (int)hipGetLastError();
 }
 
@@ -822,9 +826,10 @@ QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int
 
 // n <= 4 jobs, each as qd_slab_rows_sum (width % 4 == 0, 16-byte aligned), one launch
 QD_API int qd_slab_rows_sum_multi(int n, const float* const* slabs, float* const* outs, const int* groups,
-                                  const int* rows, const int* widths, void* stream) {
+                                  const int* rows, const int* widths, int accumulate, void* stream) {
   if (n < 1 || n > 4) return (int)hipErrorInvalidValue;
   SlabJobs jobs{};
+  jobs.accumulate = accumulate;
   int gx = 0, gy = 0;
   for (int j = 0; j < n; ++j) {
     if (widths[j] % 4 || ((uintptr_t)slabs[j] & 15) || ((uintptr_t)outs[j] & 15)) return (int)hipErrorInvalidValue;
@@ -840,13 +845,15 @@ QD_API int qd_slab_rows_sum_multi(int n, const float* const* slabs, float* const
   return (int)hipGetLastError();
 }
 
-QD_API int qd_slab_rows_sum(const float* slab, float* out, int groups, int rows, int width, void* stream) {
+// accumulate = 1: out += sum; 0: out = sum
+QD_API int qd_slab_rows_sum(const float* slab, float* out, int groups, int rows, int width, int accumulate,
+                            void* stream) {
   if (width % 4 == 0 && ((uintptr_t)slab & 15) == 0 && ((uintptr_t)out & 15) == 0) {
     hipLaunchKernelGGL(slab_rows_sum4_kernel, dim3((width / 4 + 15) / 16, groups), dim3(256), 0, (hipStream_t)stream,
-                       slab, out, groups, rows, width);
+                       slab, out, groups, rows, width, accumulate);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(slab_rows_sum_kernel, dim3((width + 63) / 64, groups), dim3(256), 0, (hipStream_t)stream, slab,
-                     out, groups, rows, width);
+                     out, groups, rows, width, accumulate);
   return (int)hipGetLastError();
 }

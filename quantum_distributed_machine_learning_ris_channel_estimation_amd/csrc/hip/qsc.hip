@@ -413,7 +413,7 @@ __global__ void __launch_bounds__(1024) qsc_head_kernel(const float* __restrict_
                                                         float* __restrict__ dE, float* __restrict__ dwc,
                                                         float* __restrict__ dbc, float* __restrict__ loss,
                                                         float* __restrict__ loss_acc, float* __restrict__ skip,
-                                                        int skip_add, int B) {
+                                                        int skip_add, int accumulate, int B) {
   constexpr int P = C * N + C;
   __shared__ float red[16][P + 1];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -471,8 +471,8 @@ __global__ void __launch_bounds__(1024) qsc_head_kernel(const float* __restrict_
   if (t <= P) {
     float s = 0.f;
     for (int w = 0; w < 16; ++w) s += red[w][t];
-    if (t < C * N) dwc[t] += s;
-    else if (t < P) dbc[t - C * N] += s;
+    if (t < C * N) dwc[t] = (accumulate ? dwc[t] : 0.f) + s;
+    else if (t < P) dbc[t - C * N] = (accumulate ? dbc[t - C * N] : 0.f) + s;
     else {
       loss[0] = s * invB;
       if (loss_acc) loss_acc[0] += s * invB;
@@ -573,13 +573,13 @@ QD_API int qd_qsc_pre_bwd(const float* x, const float* flat, const int* offs, co
 }
 
 QD_API int qd_qsc_head(const float* E, const float* wc, const float* bc, const long* labels, float* dE, float* dwc,
-                       float* dbc, float* loss, float* loss_acc, float* skip, int skip_add, int B, int n, int C,
-                       void* stream) {
+                       float* dbc, float* loss, float* loss_acc, float* skip, int skip_add, int accumulate, int B,
+                       int n, int C, void* stream) {
   hipStream_t s = (hipStream_t)stream;
 #define QD_HEAD(NN, CC)                                                                                      \
   if (n == NN && C == CC) {                                                                                 \
     hipLaunchKernelGGL((qsc_head_kernel<NN, CC>), dim3(1), dim3(1024), 0, s, E, wc, bc, labels, dE, dwc, dbc, \
-                       loss, loss_acc, skip, skip_add, B);                                                               \
+                       loss, loss_acc, skip, skip_add, accumulate, B);                                                               \
     return (int)hipGetLastError();                                                                          \
   }
 #define QD_HEAD_N(NN) QD_HEAD(NN, 2) QD_HEAD(NN, 3) QD_HEAD(NN, 4)

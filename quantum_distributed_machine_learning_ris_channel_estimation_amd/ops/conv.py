@@ -63,10 +63,9 @@ class ConvStackHIP:
         self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
         self._fin = nat.fn(L, "qd_bn_stats_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i, _p])
         self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
-        self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _p])
+        self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _i, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
-        self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
-        self._ssum_multi = nat.fn(L, "qd_slab_rows_sum_multi", [_i, _p, _p, _p, _p, _p, _p])
+        self._ssum_multi = nat.fn(L, "qd_slab_rows_sum_multi", [_i, _p, _p, _p, _p, _p, _i, _p])
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
 
     def pack_weights(self, st) -> None:
@@ -101,8 +100,9 @@ class ConvStackHIP:
         return self.h3
 
     # --------------------------------------------------------------------- backward
-    def backward(self, dh3: torch.Tensor) -> None:
-        """dh3: dL/dh3 as (N*E, 32*H*W) (bf16 or fp32).  Accumulates conv/BN grads into the flat grad."""
+    def backward(self, dh3: torch.Tensor, accumulate: bool = True) -> None:
+        """dh3: dL/dh3 as (N*E, 32*H*W) (bf16 or fp32).  Adds (accumulate) or writes the conv/BN grads
+        into the flat grad -- writing makes a zero_grad before the step unnecessary."""
         m, st = self.m, nat.stream_ptr(dh3.device)
         dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
         for k in (2, 1, 0):
@@ -110,7 +110,8 @@ class ConvStackHIP:
             nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.rslab), self.N, self.E,
                                  self.B, self.H, self.W, self.chunks_r, self.spb_r, st), f"bn_bwd_reduce{k + 1}")
             nat.check(self._bfin(nat.ptr(self.rslab), nat.ptr(m.bn_w[k]), nat.ptr(bst), nat.ptr(m.bn_w[k].grad),
-                                 nat.ptr(m.bn_b[k].grad), self.U, self.chunks_r, self.EC, float(self.B * self.HW), st),
+                                 nat.ptr(m.bn_b[k].grad), self.U, self.chunks_r, self.EC, float(self.B * self.HW),
+                                 int(accumulate), st),
                       f"bn_bwd_fin{k + 1}")
             xin = self.x1 if k == 0 else self.z[k - 1]
             st_prev = None if k == 0 else self.st[k - 1]
@@ -130,4 +131,4 @@ class ConvStackHIP:
         groups = (ctypes.c_int * 4)(*[self.E] * 3)
         rows = (ctypes.c_int * 4)(*[w.shape[1] for w in self.wslab])
         widths = (ctypes.c_int * 4)(*[w.shape[2] for w in self.wslab])
-        nat.check(self._ssum_multi(3, slabs, outs, groups, rows, widths, st), "wslab_sum")
+        nat.check(self._ssum_multi(3, slabs, outs, groups, rows, widths, int(accumulate), st), "wslab_sum")

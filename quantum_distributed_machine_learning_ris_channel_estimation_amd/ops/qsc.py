@@ -89,7 +89,7 @@ class QSCStepHIP:
         self._pre_bwd = nat.fn(L, "qd_qsc_pre_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._fwd2 = nat.fn(L, "qd_qsc2_fwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
-        self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+        self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
             self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
             self._qb = nat.fn(L, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
@@ -97,7 +97,7 @@ class QSCStepHIP:
             self._qf = nat.fn(L, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
             self._qb = nat.fn(L, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
         self._rs = nat.fn(L, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
-        self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _p])
+        self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _i, _p])
         self._qnoise = nat.fn(L, "qd_qnoise", [_p, _p, _i, _i, _f, ctypes.c_ulonglong, _p, _p])
         wq = model.qlayer.weights
         self.wnoisy = torch.empty((n_groups,) + tuple(wq.shape), **f32)
@@ -117,9 +117,11 @@ class QSCStepHIP:
 
     @torch.no_grad()
     def __call__(self, x: torch.Tensor, labels: torch.Tensor, loss_acc: Optional[torch.Tensor] = None,
-                 skip: Optional[torch.Tensor] = None, skip_add: bool = False) -> torch.Tensor:
-        """x (B, 2, H, W) fp32 contiguous, labels (B,) int64.  Accumulates grads; returns loss (1,).
-        ``skip`` (fp32 (1,)): set (or, with skip_add, incremented) to 1 if the loss is not finite."""
+                 skip: Optional[torch.Tensor] = None, skip_add: bool = False, accumulate: bool = True) -> torch.Tensor:
+        """x (B, 2, H, W) fp32 contiguous, labels (B,) int64.  Returns loss (1,).
+        ``skip`` (fp32 (1,)): set (or, with skip_add, incremented) to 1 if the loss is not finite.
+        ``accumulate``: add into the grads (default) or write them (every grad of the model has exactly
+        one producer per step, so a zero_grad before the step becomes unnecessary)."""
         m, sp = self.m, self.space
         B, n, L = self.B, self.n, self.L
         assert x.shape[0] == B and x.is_contiguous() and labels.dtype == torch.int64
@@ -140,10 +142,12 @@ class QSCStepHIP:
         nat.check(self._head(nat.ptr(self.E), nat.ptr(cls.weight), nat.ptr(cls.bias), nat.ptr(labels),
                              nat.ptr(self.dE), nat.ptr(cls.weight.grad), nat.ptr(cls.bias.grad), nat.ptr(self.loss),
                              nat.ptr(loss_acc) if loss_acc is not None else None,
-                             nat.ptr(skip) if skip is not None else None, int(skip_add), B, n, self.C, st), "qsc_head")
+                             nat.ptr(skip) if skip is not None else None, int(skip_add), int(accumulate), B, n, self.C,
+                             st), "qsc_head")
         nat.check(self._qb(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.dE), nat.ptr(self.dang),
                            nat.ptr(self.qslab), B, n, L, wgroup, *extra, st), "qsim_bwd")
-        nat.check(self._rs(nat.ptr(self.qslab), nat.ptr(m.qlayer.weights.grad), self.qrows, 2 * n * L, 1.0, st),
+        nat.check(self._rs(nat.ptr(self.qslab), nat.ptr(m.qlayer.weights.grad), self.qrows, 2 * n * L,
+                           1.0 if accumulate else 0.0, st),
                   "reduce_slab")
         if self.impl == "mfma":
             nat.check(self._bwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang),
@@ -152,8 +156,13 @@ class QSCStepHIP:
         else:
             nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B,
                                     n, self.Hh, self.Ww, self.grid_bwd, st), "qsc_pre_bwd")
-        nat.check(self._ssum(nat.ptr(self.preslab), nat.ptr(sp.grad[self.row0:]), 1, self.grid_bwd, self.row, st),
+        nat.check(self._ssum(nat.ptr(self.preslab), nat.ptr(sp.grad[self.row0:]), 1, self.grid_bwd, self.row,
+                             int(accumulate), st),
                   "qsc_slab_sum")
         if self.impl == "mfma":
-            self.gwl.addmm_(self.dpre.t(), self.p2)   # linear weight grad over the batch (one GEMM)
+            # linear weight grad over the batch (one GEMM); the slab row left these columns 0 / untouched
+            if accumulate:
+                self.gwl.addmm_(self.dpre.t(), self.p2)
+            else:
+                torch.mm(self.dpre.t(), self.p2, out=self.gwl)
         return self.loss

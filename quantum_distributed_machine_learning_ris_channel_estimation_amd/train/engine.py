@@ -252,6 +252,9 @@ class HDCEStep:
 
     def __init__(self, model: HDCEModel, n_users: int, batch: int, grad_hook: Optional[Callable] = None,
                  hip: Optional[bool] = None, skip: Optional[torch.Tensor] = None):
+        """On the HIP path every gradient of the model is WRITTEN by exactly one kernel or GEMM
+        (FC: GEMM out= / sum out=, conv + BN: overwrite mode) -- ``writes_grads`` -- so callers may
+        skip zero_grad; the CPU/autograd path accumulates as usual."""
         self.m = model
         self.U, self.B = n_users, batch
         dev = model.device
@@ -260,6 +263,7 @@ class HDCEStep:
             self.nmse.skip = skip
         self.grad_hook = grad_hook  # called as grad_hook("fc") / grad_hook("conv") when buckets are final
         self.hip = (dev.type == "cuda") if hip is None else hip
+        self.writes_grads = self.hip
         if self.hip:
             from ..ops.conv import ConvStackHIP
             self.conv = ConvStackHIP(model, n_users, batch)
@@ -304,7 +308,7 @@ class HDCEStep:
     # Phase 2: conv/BN backward from dA.
     def backward_conv(self) -> None:
         if self.hip:
-            self.conv.backward(self._dA)
+            self.conv.backward(self._dA, accumulate=False)
         else:
             torch.autograd.backward(self._A, self._dA)
             self._A = None
@@ -376,6 +380,7 @@ class ClassifierStep:
         dev0 = next(model.parameters()).device
         self.skip_add = skip is not None
         self.skip = skip if skip is not None else torch.zeros(1, device=dev0, dtype=torch.float32)
+        self.writes_grads = False   # set by callers that skip zero_grad (fused HIP step only)
         self.hip = None
         dev = next(model.parameters()).device
         if (isinstance(model, QSC_P128) and model.use_quantum and dev.type == "cuda" and space is not None
@@ -397,7 +402,8 @@ class ClassifierStep:
 
     def __call__(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
         if self.hip is not None and x.shape[0] == self.hip.B:
-            loss = self.hip(x.contiguous(), labels, skip=self.skip, skip_add=self.skip_add)
+            loss = self.hip(x.contiguous(), labels, skip=self.skip, skip_add=self.skip_add,
+                            accumulate=not self.writes_grads)
             if self.grad_hook:
                 self.grad_hook("all")
             return loss

@@ -78,6 +78,7 @@ class FlagshipTrainer:
         # bucket so every rank sees the same (summed) flag and skips -- or steps -- in lockstep
         self.skip = self.hstep.skip
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B, skip=self.skip)
+        self.cstep.writes_grads = self.cstep.hip is not None
         # bucket "fc": 33.6 MB, ready first; bucket "small": conv + QSC grads + skip flag, coalesced
         self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]],
                                          "small": [sp.grad[:n_conv], self.qspace.grad, self.skip]})
@@ -101,9 +102,11 @@ class FlagshipTrainer:
 
     # -- phases ---------------------------------------------------------------------------
     def _phase1(self) -> None:
-        E, U, B = self.E, self.U, self.B
-        self.hdce.space.zero_grad()
-        self.qspace.zero_grad()
+        # the fused GPU kernels WRITE every gradient (one producer per element): no zero_grad fills
+        if not self.hstep.writes_grads:
+            self.hdce.space.zero_grad()
+        if not self.cstep.writes_grads:
+            self.qspace.zero_grad()
         self.gat(self.store, self.idx)           # one launch: conv input, classifier input, label rows
         loss = self.hstep.forward_fc_gathered(self.gat, self.store)
         if loss is not self.hloss:
