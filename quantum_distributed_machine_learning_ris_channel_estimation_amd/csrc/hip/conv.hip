@@ -286,6 +286,26 @@ __global__ void pack_weights_multi_kernel(PackJobs jobs) {
 // per workgroup; slab[(e * U*chunks + blockIdx.x)][co][ci][tap].
 // x = layer input (raw f32 pilots, or BN+ReLU of the previous z); dz from (dh, z, st).
 // ------------------------------------------------------------------------------------------
+// Raw 16-byte vectors kept in registers between a prefetch and its use (no conversion at load
+// time, so the compiler's wait for the data lands at the use, one sample later).
+template <typename T>
+struct PerQ;
+template <>
+struct PerQ<float> { static constexpr int N = 4; };
+template <>
+struct PerQ<uint16_t> { static constexpr int N = 8; };
+__device__ __forceinline__ void unpack_q(const uint4 q, float* v, const float*) {
+  v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+}
+__device__ __forceinline__ void unpack_q(const uint4 q, float* v, const uint16_t*) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
 template <int CIN, int H, int W, int INM, typename TIN, typename TDH>
 __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restrict__ xin,
                                                             const float* __restrict__ st_prev,
@@ -299,6 +319,10 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restric
   constexpr int DZS = G::HW + 8;                  // channel stride of the dz tile (bf16)
   constexpr int KSW = G::HW / 16 / 4;             // k-steps per wave per sample (positions split 4 ways)
   constexpr int XELEMS = 3 * CIN * XCS;
+  // staging items per thread: x = one (channel, image row) of W values; dz = 8 positions of a channel
+  constexpr int XN = CIN * H, XIT = (XN + 255) / 256, XQ = W / PerQ<TIN>::N;
+  constexpr int DN = CO * G::HW / 8, DIT = DN / 256, DQ = 8 / PerQ<TDH>::N;
+  static_assert(DN % 256 == 0, "dz staging items");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __bf16* X = reinterpret_cast<__bf16*>(smem);
   __bf16* DZ = X + XELEMS;
@@ -310,63 +334,104 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restric
   f32x16 acc[MTW];
 #pragma unroll
   for (int t = 0; t < MTW; ++t) acc[t] = f32x16{};
-  // per-lane A-row mapping (m = l32 within tile t): (tap, ci)
-  const float* stp_u = st_prev ? st_prev + (size_t)u * E * CIN * NST : nullptr;
-  const float* st_u = st + (size_t)u * E * CO * NST;
   const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
 
-  for (int n = n0; n < nend; ++n) {
-    __syncthreads();
-    // ---- stage x into 3 column-shifted copies: X[kw][ci][row 0..HP-1][w] = x[ci][row-1][w+kw-1] ----
-    // one thread per (channel, image row): W contiguous values -> 3 aligned 16-byte row writes
+  // ---- per-item BN parameters: the channel of an item is the same for every sample -> registers ----
+  [[maybe_unused]] float xa[XIT], xbb[XIT];
+#pragma unroll
+  for (int k = 0; k < XIT; ++k) {
+    xa[k] = 1.f;
+    xbb[k] = 0.f;
+    const int i = tid + 256 * k;
+    if constexpr (INM == IN_BNRELU) {
+      if (XN % 256 == 0 || i < XN) {
+        const float* sc = st_prev + ((size_t)u * E * CIN + e * CIN + i / H) * NST;
+        xa[k] = sc[ST_A];
+        xbb[k] = sc[ST_B];
+      }
+    }
+  }
+  float da[DIT], db[DIT], dmu[DIT], dinv[DIT], dc1[DIT], dc2[DIT], dc3[DIT];
+#pragma unroll
+  for (int k = 0; k < DIT; ++k) {
+    const float* sc = st + ((size_t)u * E * CO + e * CO + (tid + 256 * k) / (G::HW / 8)) * NST;
+    da[k] = sc[ST_A]; db[k] = sc[ST_B]; dmu[k] = sc[ST_MEAN]; dinv[k] = sc[ST_INV];
+    dc1[k] = sc[ST_C1]; dc2[k] = sc[ST_C2]; dc3[k] = sc[ST_C3];
+  }
+
+  // ---- one-sample-ahead register prefetch: sample n+1's loads fly during sample n's MFMAs ----
+  uint4 xr[XIT][XQ], dr[DIT][DQ], zr[DIT];
+  auto prefetch = [&](int n) {
     const size_t xb = ((size_t)n * E + e) * CIN * G::HW;
-    for (int i = tid; i < CIN * H; i += 256) {
-      const int c = i / H, ph = i % H;
-      float a = 1.f, b = 0.f;
-      if constexpr (INM == IN_BNRELU) {
-        const float* sc = stp_u + (size_t)(e * CIN + c) * NST;
-        a = sc[ST_A];
-        b = sc[ST_B];
+#pragma unroll
+    for (int k = 0; k < XIT; ++k) {
+      const int i = tid + 256 * k;
+      if (XN % 256 == 0 || i < XN) {
+        const uint4* src = reinterpret_cast<const uint4*>(xin + xb + (size_t)(i / H) * G::HW + (i % H) * W);
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) xr[k][q] = src[q];
       }
-      float v[W + 2];
-      v[0] = 0.f;
-      v[W + 1] = 0.f;
+    }
+    const size_t zb = ((size_t)n * E + e) * CO * G::HW;
 #pragma unroll
-      for (int q = 0; q < W; q += 8) load8(xin + xb + (size_t)c * G::HW + ph * W + q, v + 1 + q);
-      if constexpr (INM == IN_BNRELU) {
+    for (int k = 0; k < DIT; ++k) {
+      const size_t off = zb + (size_t)(tid + 256 * k) * 8;   // item i covers elements [8i, 8i+8) of the sample
+      const uint4* sd = reinterpret_cast<const uint4*>(dh + off);
 #pragma unroll
-        for (int q = 1; q <= W; ++q) v[q] = fmaxf(a * v[q] + b, 0.f);
-      }
+      for (int q = 0; q < DQ; ++q) dr[k][q] = sd[q];
+      zr[k] = *reinterpret_cast<const uint4*>(z + off);
+    }
+  };
+  if (n0 < nend) prefetch(n0);
+
+  for (int n = n0; n < nend; ++n) {
+    __syncthreads();   // the previous sample's MFMAs are done reading X / DZ
+    // ---- x -> 3 column-shifted copies: X[kw][ci][row 0..HP-1][w] = x[ci][row-1][w+kw-1] ----
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        __bf16* dst = X + (kw * CIN + c) * XCS + (ph + 1) * W;
+    for (int k = 0; k < XIT; ++k) {
+      const int i = tid + 256 * k;
+      if (XN % 256 == 0 || i < XN) {
+        const int c = i / H, ph = i % H;
+        float v[W + 2];
+        v[0] = 0.f;
+        v[W + 1] = 0.f;
 #pragma unroll
-        for (int q = 0; q < W; q += 8) {
-          bf16x8 o;
+        for (int q = 0; q < XQ; ++q) unpack_q(xr[k][q], v + 1 + q * PerQ<TIN>::N, (const TIN*)nullptr);
+        if constexpr (INM == IN_BNRELU) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[q + j + kw];  // column w holds x[w + kw - 1]
-          *reinterpret_cast<bf16x8*>(dst + q) = o;
+          for (int q = 1; q <= W; ++q) v[q] = fmaxf(xa[k] * v[q] + xbb[k], 0.f);
+        }
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          __bf16* dst = X + (kw * CIN + c) * XCS + (ph + 1) * W;
+#pragma unroll
+          for (int q = 0; q < W; q += 8) {
+            bf16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[q + j + kw];  // column w holds x[w + kw - 1]
+            *reinterpret_cast<bf16x8*>(dst + q) = o;
+          }
         }
       }
     }
-    // ---- stage dz (bf16) [co][p] ----
-    const size_t zb = ((size_t)n * E + e) * CO * G::HW;
-    for (int i = tid; i < CO * G::HW / 8; i += 256) {
+    // ---- dz = BN/ReLU backward of dh (bf16) [co][p] ----
+#pragma unroll
+    for (int k = 0; k < DIT; ++k) {
+      const int i = tid + 256 * k;
       const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
       float d[8], zz[8];
-      load8(dh + zb + (size_t)c * G::HW + p0, d);
-      load8(z + zb + (size_t)c * G::HW + p0, zz);
-      const float* sc = st_u + (size_t)(e * CO + c) * NST;
-      const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
-      const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+#pragma unroll
+      for (int q = 0; q < DQ; ++q) unpack_q(dr[k][q], d + q * PerQ<TDH>::N, (const TDH*)nullptr);
+      unpack_q(zr[k], zz, (const uint16_t*)nullptr);
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float g = (a * zz[j] + b > 0.f) ? d[j] : 0.f;
-        o[j] = (__bf16)(c1 * g - c2 - c3 * (zz[j] - mu) * inv);
+        const float g = (da[k] * zz[j] + db[k] > 0.f) ? d[j] : 0.f;
+        o[j] = (__bf16)(dc1[k] * g - dc2[k] - dc3[k] * (zz[j] - dmu[k]) * dinv[k]);
       }
       *reinterpret_cast<bf16x8*>(DZ + c * DZS + p0) = o;
     }
+    if (n + 1 < nend) prefetch(n + 1);
     __syncthreads();
     // ---- MFMA: this wave's positions p in [wv*HW/4, (wv+1)*HW/4) ----
 #pragma unroll

@@ -28,7 +28,7 @@ def _ptr(t: Optional[torch.Tensor]):
 class ConvStackHIP:
     """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
 
-    def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 16, spb_r: int = 4):
+    def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 16, spb_r: int = 4, spb_w1: int = 4):
         self.m = model
         self.U, self.B, self.N, self.E = U, B, U * B, model.E
         self.H, self.W = model.H, model.W
@@ -39,6 +39,9 @@ class ConvStackHIP:
         self.chunks = (B + 4 * spw - 1) // (4 * spw)          # forward / dgrad: 4 waves x spw samples
         self.spb_w = spb_w
         self.chunks_w = (B + spb_w - 1) // spb_w              # wgrad workgroups per group
+        # layer 1 (2 input channels) is one accumulator tile: staging-bound, so more, shorter workgroups
+        self.spb_wl = (spb_w1, spb_w, spb_w)
+        self.chunks_wl = tuple((B + s - 1) // s for s in self.spb_wl)
         self.spb_r = spb_r
         self.chunks_r = (B + spb_r - 1) // spb_r              # BN backward reductions
         N, EC, HW = self.N, self.EC, self.HW
@@ -51,7 +54,7 @@ class ConvStackHIP:
         self.stats = torch.zeros(U, self.chunks, EC, 2, device=dev)
         self.rslab = torch.zeros(U, self.chunks_r, EC, 2, device=dev)
         self.dx = [torch.empty(N, EC, HW, device=dev) for _ in range(2)]   # grads w.r.t. h1, h2
-        self.wslab = [torch.empty(self.E, U * self.chunks_w, 32 * cin * 9, device=dev) for cin in (2, 32, 32)]
+        self.wslab = [torch.empty(self.E, U * c, 32 * cin * 9, device=dev) for c, cin in zip(self.chunks_wl, (2, 32, 32))]
         # bf16 B-fragment images of the weights (re-packed every step; 16-byte coalesced loads in-kernel)
         self.cins = (2, 32, 32)
         self.wpk = [torch.empty(self.E, (9 * cin + 15) // 16, 64, 8, device=dev, dtype=bf) for cin in self.cins]
@@ -117,7 +120,7 @@ class ConvStackHIP:
             st_prev = None if k == 0 else self.st[k - 1]
             ws = self.wslab[k]
             nat.check(self._wgrad(k + 1, nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst),
-                                  nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_w, self.spb_w, st),
+                                  nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k], st),
                       f"conv_wgrad{k + 1}")
             if k > 0:
                 dx = self.dx[k - 1]

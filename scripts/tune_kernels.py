@@ -80,6 +80,36 @@ def tune_conv(pilot, Bs, combos):
                               "fwd_us": round(f, 1), "fwd_bwd_us": round(fb, 1)}), flush=True)
 
 
+def tune_wgrad(pilot, B, spbs):
+    """Each layer's weight-gradient launch alone, per samples-per-workgroup setting."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.conv import ConvStackHIP, _ptr
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEModel
+    dev = torch.device("cuda")
+    m = HDCEModel(pilot, dev, "bf16")
+    U, E = 3, 3
+    N = U * B
+    x1 = torch.randn(N, 2 * E, m.H, m.W, device=dev)
+    dh = torch.randn(N * E, 32 * m.H * m.W, device=dev).to(torch.bfloat16)
+    dx = torch.randn(N, 32 * E, m.H * m.W, device=dev)
+    for spb in spbs:
+        cs = ConvStackHIP(m, U, B, spb_w=spb, spb_w1=spb)
+        cs.forward(x1, True)
+        st = nat.stream_ptr(dev)
+        for k in range(3):
+            g, gbf = (dh, 1) if k == 2 else (dx, 0)
+            xin = cs.x1 if k == 0 else cs.z[k - 1]
+            sp = None if k == 0 else cs.st[k - 1]
+
+            def run():
+                nat.check(cs._wgrad(k + 1, nat.ptr(xin), _ptr(sp), nat.ptr(g), gbf, nat.ptr(cs.z[k]),
+                                    nat.ptr(cs.st[k]), nat.ptr(cs.wslab[k]), cs.N, cs.E, cs.B, cs.H, cs.W,
+                                    cs.chunks_wl[k], cs.spb_wl[k], st), "wgrad")
+            us = time_graph(run)
+            print(json.dumps({"op": "wgrad", "layer": k + 1, "pilot": pilot, "spb": spb, "us": round(us, 1)}),
+                  flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="qsc,conv")
@@ -88,6 +118,8 @@ def main():
     if "qsc" in what:
         grids = [(512, 256), (1024, 256), (1024, 512), (2304, 512), (2304, 768), (2304, 1152), (1024, 1024)]
         tune_qsc(8, 128, 2304, grids)
+    if "wgrad" in what:
+        tune_wgrad(128, 256, [2, 4, 8, 16, 32])
     if "conv" in what:
         tune_conv(128, [256], list(itertools.product([1, 2], [4, 8, 16], [4, 8, 16])))
 
