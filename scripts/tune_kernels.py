@@ -95,13 +95,13 @@ def tune_wgrad(pilot, B, spbs):
     for spb in spbs:
         cs = ConvStackHIP(m, U, B, spb_w=spb, spb_w1=spb)
         cs.forward(x1, True)
-        st = nat.stream_ptr(dev)
         for k in range(3):
             g, gbf = (dh, 1) if k == 2 else (dx, 0)
             xin = cs.x1 if k == 0 else cs.z[k - 1]
             sp = None if k == 0 else cs.st[k - 1]
 
             def run():
+                st = nat.stream_ptr(dev)   # the capture stream, not the one current outside it
                 nat.check(cs._wgrad(k + 1, nat.ptr(xin), _ptr(sp), nat.ptr(g), gbf, nat.ptr(cs.z[k]),
                                     nat.ptr(cs.st[k]), nat.ptr(cs.wslab[k]), cs.N, cs.E, cs.B, cs.H, cs.W,
                                     cs.chunks_wl[k], cs.spb_wl[k], st), "wgrad")
