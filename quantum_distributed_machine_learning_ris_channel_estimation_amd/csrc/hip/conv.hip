@@ -46,7 +46,7 @@ constexpr int NST = 8;     // floats per (group, channel) BN state record
 enum { ST_MEAN = 0, ST_INV = 1, ST_A = 2, ST_B = 3, ST_C1 = 4, ST_C2 = 5, ST_C3 = 6 };
 
 enum InMode { IN_RAW_F32 = 0, IN_BNRELU = 1, IN_BNBWD = 2 };
-enum OutMode { OUT_Z_STATS = 0, OUT_F32 = 1 };
+enum OutMode { OUT_Z_STATS = 0, OUT_F32 = 1, OUT_BF16 = 2 };
 
 template <int H, int W>
 struct Geo {
@@ -211,6 +211,10 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const TIN* __restrict__ xi
           v0 = bf(h0); v1 = bf(h1); v2 = bf(h2); v3 = bf(h3);
           s1 += v0 + v1 + v2 + v3;
           s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+        } else if constexpr (OUTM == OUT_BF16) {
+          const uint2 pk = make_uint2(f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16),
+                                      f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16));
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + obase + 8 * g) = pk;
         } else {
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + obase + 8 * g) = make_float4(v0, v1, v2, v3);
         }
@@ -307,7 +311,7 @@ __device__ __forceinline__ void unpack_q(const uint4 q, float* v, const uint16_t
 }
 
 template <int CIN, int H, int W, int INM, typename TIN, typename TDH>
-__global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restrict__ xin,
+__global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __restrict__ xin,
                                                             const float* __restrict__ st_prev,
                                                             const TDH* __restrict__ dh,
                                                             const uint16_t* __restrict__ z,
@@ -329,7 +333,11 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restric
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int hh = lane >> 5, l32 = lane & 31;
   const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
-  for (int i = tid; i < XELEMS; i += 256) X[i] = (__bf16)0.f;
+  // zero halo rows (0 and HP-1) of every shifted copy; interior rows are rewritten per sample
+  for (int i = tid; i < 3 * CIN * 2 * (W / 8); i += 256) {
+    const int cc = i / (2 * (W / 8)), r = (i / (W / 8)) & 1, q = i % (W / 8);
+    *reinterpret_cast<bf16x8*>(X + cc * XCS + r * (G::HP - 1) * W + 8 * q) = bf16x8{};
+  }
 
   f32x16 acc[MTW];
 #pragma unroll
@@ -444,7 +452,7 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restric
         const int m = t * 32 + l32;
         bf16x8 a;
         if (m < 9 * CIN) {
-          const int tap = m / CIN, c = m % CIN, kh = tap / 3, kw = tap % 3;
+          const int c = m / 9, tap = m % 9, kh = tap / 3, kw = tap % 3;   // row m = (ci, tap): slab order
           a = *reinterpret_cast<const bf16x8*>(X + (kw * CIN + c) * XCS + (ph + kh) * W + pw0);
         } else {
           a = bf16x8{};
@@ -453,28 +461,33 @@ __global__ void __launch_bounds__(256) conv3x3_wgrad_kernel(const TIN* __restric
       }
     }
   }
-  // ---- reduce the 4 waves' accumulators through LDS, write one slab row ----
+  // ---- reduce the 4 waves' accumulators through LDS (two transposed regions [co][m], odd row
+  // stride: conflict-free), (w0 + w2) + (w1 + w3) in a fixed order, then one contiguous slab row ----
+  constexpr int RS = 9 * CIN + 1;
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // MTW*32*32 floats
-  for (int w = 0; w < 4; ++w) {
-    if (wv == w) {
+  float* red = reinterpret_cast<float*>(smem) + (wv & 1) * 32 * RS;
+#pragma unroll
+  for (int round = 0; round < 2; ++round) {
+    if ((wv >> 1) == round) {
 #pragma unroll
       for (int t = 0; t < MTW; ++t) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * hh;
-          float* q = red + (t * 32 + row) * 32 + l32;
-          *q = (w == 0 ? 0.f : *q) + acc[t][r];
+          const int m = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (m < 9 * CIN) {
+            float* q = red + l32 * RS + m;
+            *q = (round == 0 ? 0.f : *q) + acc[t][r];
+          }
         }
       }
     }
     __syncthreads();
   }
+  const float* r0 = reinterpret_cast<const float*>(smem);
   float* srow = slab + ((size_t)e * gridDim.x + blockIdx.x) * CO * CIN * 9;
   for (int i = tid; i < CO * CIN * 9; i += 256) {
-    const int co = i / (CIN * 9), rem = i % (CIN * 9), c = rem / 9, tap = rem % 9;
-    const int m = tap * CIN + c;
-    srow[i] = red[m * 32 + co];
+    const int co = i / (CIN * 9), m = i % (CIN * 9);
+    srow[i] = r0[co * RS + m] + r0[32 * RS + co * RS + m];
   }
 }
 
@@ -792,28 +805,28 @@ QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const u
   return (int)hipGetLastError();
 }
 
-// data gradient of a 32->32 layer: dx (f32) from dh (f32 or bf16) of this layer, z, st.
-// w: packed B fragments from qd_conv_pack_weights(dgrad=1)
-QD_API int qd_conv_dgrad(const void* dh, int dh_bf16, const uint16_t* z, const float* st, const uint16_t* w, float* dx,
-                         int N, int E, int B, int H, int W, int chunks, int spw, void* stream) {
+// data gradient of a 32->32 layer: dx (f32, or bf16 when dx_bf16) from dh (f32 or bf16) of this
+// layer, z, st.  w: packed B fragments from qd_conv_pack_weights(dgrad=1)
+QD_API int qd_conv_dgrad(const void* dh, int dh_bf16, const uint16_t* z, const float* st, const uint16_t* w, void* dx,
+                         int dx_bf16, int N, int E, int B, int H, int W, int chunks, int spw, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((N / B) * chunks, E);
   if (chunks * 4 * spw < B) return (int)hipErrorInvalidValue;
+#define QD_DG(OUTM_, TIN_)                                                                                         \
+  QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNBWD, OUTM_, true, TIN_>), grid, dim3(256),          \
+                                  fwd_smem(32, H, W), s, (const TIN_*)dh, z, st, w, dx, nullptr, E, B, chunks, spw))
   if (dh_bf16) {
-    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNBWD, OUT_F32, true, uint16_t>), grid, dim3(256),
-                                    fwd_smem(32, H, W), s, (const uint16_t*)dh, z, st, w, dx, nullptr, E, B, chunks,
-                                    spw))
+    if (dx_bf16) { QD_DG(OUT_BF16, uint16_t) } else { QD_DG(OUT_F32, uint16_t) }
   } else {
-    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNBWD, OUT_F32, true, float>), grid, dim3(256),
-                                    fwd_smem(32, H, W), s, (const float*)dh, z, st, w, dx, nullptr, E, B, chunks,
-                                    spw))
+    if (dx_bf16) { QD_DG(OUT_BF16, float) } else { QD_DG(OUT_F32, float) }
   }
+#undef QD_DG
   return (int)hipGetLastError();
 }
 
 static size_t wgrad_smem(int cin, int H, int W) {
   const size_t stage = (3 * (size_t)cin * ((H + 2) * W + 8) + 32 * (size_t)(H * W + 8)) * 2;
-  const size_t red = (size_t)((9 * cin + 31) / 32) * 32 * 32 * 4;
+  const size_t red = 2 * 32 * (size_t)(9 * cin + 1) * 4;
   return stage > red ? stage : red;
 }
 

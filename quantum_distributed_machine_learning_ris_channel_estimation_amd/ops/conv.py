@@ -28,7 +28,8 @@ def _ptr(t: Optional[torch.Tensor]):
 class ConvStackHIP:
     """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
 
-    def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 16, spb_r: int = 4, spb_w1: int = 4):
+    def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 8, spb_r: int = 4, spb_w1: int = 4,
+                 dx_bf16: bool = True):
         self.m = model
         self.U, self.B, self.N, self.E = U, B, U * B, model.E
         self.H, self.W = model.H, model.W
@@ -53,7 +54,10 @@ class ConvStackHIP:
         self.st = [torch.zeros(U, EC, NST, device=dev) for _ in range(3)]
         self.stats = torch.zeros(U, self.chunks, EC, 2, device=dev)
         self.rslab = torch.zeros(U, self.chunks_r, EC, 2, device=dev)
-        self.dx = [torch.empty(N, EC, HW, device=dev) for _ in range(2)]   # grads w.r.t. h1, h2
+        # grads w.r.t. h1, h2: bf16 by default (they only feed bf16 MFMA operands and fp32-accumulated
+        # BN reductions), halving the dgrad write and every re-read of it
+        self.dx_bf16 = dx_bf16
+        self.dx = [torch.empty(N, EC, HW, device=dev, dtype=bf if dx_bf16 else torch.float32) for _ in range(2)]
         self.wslab = [torch.empty(self.E, U * c, 32 * cin * 9, device=dev) for c, cin in zip(self.chunks_wl, (2, 32, 32))]
         # bf16 B-fragment images of the weights (re-packed every step; 16-byte coalesced loads in-kernel)
         self.cins = (2, 32, 32)
@@ -62,7 +66,7 @@ class ConvStackHIP:
         self.lib = nat.hip_lib()
         L = self.lib
         self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
-        self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
+        self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p])
         self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
         self._fin = nat.fn(L, "qd_bn_stats_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i, _p])
         self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
@@ -125,9 +129,9 @@ class ConvStackHIP:
             if k > 0:
                 dx = self.dx[k - 1]
                 nat.check(self._dgrad(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.wpk_t[k]),
-                                      nat.ptr(dx), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw, st),
-                          f"conv_dgrad{k + 1}")
-                dh, dh_bf = dx, 0
+                                      nat.ptr(dx), int(self.dx_bf16), self.N, self.E, self.B, self.H, self.W,
+                                      self.chunks, self.spw, st), f"conv_dgrad{k + 1}")
+                dh, dh_bf = dx, int(self.dx_bf16)
         # the three weight-gradient slabs -> conv_w grads in one launch
         slabs = (ctypes.c_void_p * 4)(*[nat.ptr(w) for w in self.wslab])
         outs = (ctypes.c_void_p * 4)(*[nat.ptr(m.conv_w[k].grad) for k in range(3)])

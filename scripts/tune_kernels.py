@@ -91,12 +91,12 @@ def tune_wgrad(pilot, B, spbs):
     N = U * B
     x1 = torch.randn(N, 2 * E, m.H, m.W, device=dev)
     dh = torch.randn(N * E, 32 * m.H * m.W, device=dev).to(torch.bfloat16)
-    dx = torch.randn(N, 32 * E, m.H * m.W, device=dev)
+    dx = torch.randn(N, 32 * E, m.H * m.W, device=dev).to(torch.bfloat16)
     for spb in spbs:
         cs = ConvStackHIP(m, U, B, spb_w=spb, spb_w1=spb)
         cs.forward(x1, True)
         for k in range(3):
-            g, gbf = (dh, 1) if k == 2 else (dx, 0)
+            g, gbf = (dh, 1) if k == 2 else (dx, 1)
             xin = cs.x1 if k == 0 else cs.z[k - 1]
             sp = None if k == 0 else cs.st[k - 1]
 
@@ -119,7 +119,7 @@ def main():
         grids = [(512, 256), (1024, 256), (1024, 512), (2304, 512), (2304, 768), (2304, 1152), (1024, 1024)]
         tune_qsc(8, 128, 2304, grids)
     if "wgrad" in what:
-        tune_wgrad(128, 256, [2, 4, 8, 16, 32])
+        tune_wgrad(128, 256, [4, 8, 16, 32])
     if "conv" in what:
         tune_conv(128, [256], list(itertools.product([1, 2], [4, 8, 16], [4, 8, 16])))
 
