@@ -34,6 +34,14 @@ struct Offs {
   int w1, b1, w2, b2, wl, bl, row;
 };
 
+// forward -> backward hand-off per sample (the backward routes gradients through the saved pool
+// choices instead of recomputing conv1/conv2): see sample_forward
+struct Saved {
+  float* p1;      // (B, HW2, 16) pool-1 map, channel-last
+  uint32_t* c1;   // (B, HW2) pool-1 argmax codes, 2 bits per channel
+  uint8_t* c2;    // (B, F) pool-2 window-relative argmax
+};
+
 template <int H, int W>
 struct Geo {
   static constexpr int HW = H * W;
@@ -166,10 +174,14 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
 // Forward of one sample into the wave's LDS image: x -> p1 (padded) -> z2 (pre-activation).
 // wreg (optional): this lane's 72 conv2 weights W2[co = lane&31][ci = 8*(lane>>5) + j][t] at
 // [t*8 + j], register-resident across samples (forward kernel); null = read them from LDS.
+// Saved for the backward (per sample): p1g = pool-1 map [window][16 ch]; c1g[window] = 2-bit
+// window-relative argmax per channel (bits 2c..2c+1: 0 top-left, 1 top-right, 2 bottom-left,
+// 3 bottom-right; first max in that scan order, the reference's max_pool2d choice).
 template <int H, int W, bool WREG, bool STAMP = false>
 __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane,
                                                const float (&wreg)[72], const float* __restrict__ w1g,
                                                const float* __restrict__ b1g, float bias2,
+                                               float* __restrict__ p1g, uint32_t* __restrict__ c1g,
                                                unsigned long long* ts = nullptr) {
   using G = Geo<H, W>;
   static_assert(W % 4 == 0, "float4 rows");
@@ -193,15 +205,34 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
     float acc[16][2];
     conv1_half<H, W>(act, w1g, b1g, win, hw, acc);
     float m[16];
+    uint32_t right = 0, bottom = 0;   // per channel: right column wins in this row; bottom row wins
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-      const float v = fmaxf(relu(acc[c][0]), relu(acc[c][1]));
-      m[c] = fmaxf(v, __shfl_xor(v, 1));
+      const float r0 = relu(acc[c][0]), r1 = relu(acc[c][1]);
+      const float v = fmaxf(r0, r1), pv = __shfl_xor(v, 1);
+      m[c] = fmaxf(v, pv);
+      right |= (uint32_t)(r1 > r0) << c;
+      bottom |= (uint32_t)(hw ? (v > pv) : (pv > v)) << c;   // ties go to the top row
     }
+    const uint32_t pright = __shfl_xor(right, 1);
     const int qy = win / G::W2, qx = win % G::W2;
     float4* d = reinterpret_cast<float4*>(act + G::o_p1 + ((qy + 1) * G::PW + qx + 1) * G::PC + 8 * hw);
-    d[0] = make_float4(m[8 * hw + 0], m[8 * hw + 1], m[8 * hw + 2], m[8 * hw + 3]);
-    d[1] = make_float4(m[8 * hw + 4], m[8 * hw + 5], m[8 * hw + 6], m[8 * hw + 7]);
+    const float4 m0 = make_float4(m[8 * hw + 0], m[8 * hw + 1], m[8 * hw + 2], m[8 * hw + 3]);
+    const float4 m1 = make_float4(m[8 * hw + 4], m[8 * hw + 5], m[8 * hw + 6], m[8 * hw + 7]);
+    d[0] = m0;
+    d[1] = m1;
+    float4* g = reinterpret_cast<float4*>(p1g + win * C1 + 8 * hw);
+    g[0] = m0;
+    g[1] = m1;
+    if (hw == 0) {
+      uint32_t code = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const uint32_t b = (bottom >> c) & 1u;
+        code |= (b ? 2u + ((pright >> c) & 1u) : (right >> c) & 1u) << (2 * c);
+      }
+      c1g[win] = code;
+    }
   }
   wave_lds_fence();
   if constexpr (STAMP) ts[3] = stamp();
@@ -237,20 +268,20 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
 
 // pool-2 (after ReLU) value and the winning position of feature f (first max, reference order)
 template <int H, int W>
-__device__ __forceinline__ float pool2(const float* act, int f, int& arg) {
+__device__ __forceinline__ float pool2(const float* act, int f, int& rel) {
   using G = Geo<H, W>;
   const int c = f / G::HW4, q = f % G::HW4, qy = q / G::W4, qx = q % G::W4;
   const int base = (2 * qy) * G::W2 + 2 * qx;
   const int idx[4] = {base, base + 1, base + G::W2, base + G::W2 + 1};
   const float* z = act + G::o_z2 + c * G::HW2;
   float m = relu(z[idx[0]]);
-  arg = idx[0];
+  rel = 0;
 #pragma unroll
   for (int r = 1; r < 4; ++r) {
     const float v = relu(z[idx[r]]);
     if (v > m) {
       m = v;
-      arg = idx[r];
+      rel = r;
     }
   }
   return m;
@@ -261,7 +292,8 @@ __device__ __forceinline__ float pool2(const float* act, int f, int& arg) {
 template <int H, int W, int NWV, bool STAMP = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                       Offs o, float* __restrict__ angles, float* __restrict__ p2,
-                                                      int B, int n, unsigned long long* __restrict__ stamps = nullptr) {
+                                                      Saved sv, int B, int n,
+                                                      unsigned long long* __restrict__ stamps = nullptr) {
   unsigned long long ts[NSTAMP] = {};
   if constexpr (STAMP) ts[0] = stamp();
   using G = Geo<H, W>;
@@ -300,18 +332,22 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   const float* bl = wl + n * wl_stride(G::F);
   bool first = true;
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
+    float* p1g = sv.p1 + (size_t)s * C1 * G::HW2;
+    uint32_t* c1g = sv.c1 + (size_t)s * G::HW2;
     if (STAMP && first)
       sample_forward<H, W, true, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, bias2,
-                                       ts);
+                                       p1g, c1g, ts);
     else
-      sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, bias2);
+      sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, bias2, p1g,
+                                 c1g);
     float* p2s = act + G::o_p2f;
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {
-      int arg;
-      const float v = pool2<H, W>(act, lane + 64 * i, arg);
+      int rel;
+      const float v = pool2<H, W>(act, lane + 64 * i, rel);
       p2s[lane + 64 * i] = v;
       p2[(size_t)s * G::F + lane + 64 * i] = v;
+      sv.c2[(size_t)s * G::F + lane + 64 * i] = (uint8_t)rel;
     }
     wave_lds_fence();
     // linear: 4 lanes per output j (n <= 16), interleaved f (conflict-free), then 2 shuffles
@@ -346,7 +382,8 @@ template <int H, int W, int NWV, bool STAMP = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                       Offs o, const float* __restrict__ angles,
                                                       const float* __restrict__ dang, float* __restrict__ dpre_out,
-                                                      float* __restrict__ slab, int B, int n,
+                                                      float* __restrict__ slab, const float* __restrict__ p2,
+                                                      Saved sv, int B, int n,
                                                       unsigned long long* __restrict__ stamps = nullptr) {
   unsigned long long ts[NSTAMP] = {};
   bool first = true;
@@ -374,44 +411,113 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   f32x4 gw1[2];                                    // dW1 tiles: rows = co, cols = k in [16t, 16t+16)
   gw1[0] = (f32x4){};
   gw1[1] = (f32x4){};
-  float gb1[16], gb2 = 0.f, gbl = 0.f;
-  const float no_wreg[72] = {};   // unused: the backward reads conv2 weights from LDS (register budget)
+  constexpr int FPL = G::F / 64;              // pool-2 features per lane (f = FPL * lane + i)
+  constexpr int XQ = 2 * G::HW / 256;          // float4s of x per lane
+  constexpr int P1Q = C1 * G::HW2 / 256;       // float4s of the saved pool-1 map per lane
+  constexpr int CPL = C1 * G::HW2 / 64;        // pool-1 (channel, window) pairs per lane
+  static_assert(FPL % 4 == 0 && XQ >= 1 && P1Q >= 1 && 64 % G::HW2 == 0, "lane mappings");
+  float gb1[CPL], gb2 = 0.f, gbl = 0.f;
 #pragma unroll
-  for (int c = 0; c < 16; ++c) gb1[c] = 0.f;
+  for (int c = 0; c < CPL; ++c) gb1[c] = 0.f;
 
-  for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
+  // ---- one-sample-ahead register prefetch of everything a sample reads from global memory ----
+  // ext-vector registers (float4 is a struct: arrays of it are copied by memcpy and land in scratch)
+  f32x4 rx[XQ], rp1[P1Q], rp2[FPL / 4];
+  uint32_t rc2[FPL / 4], rc1 = 0;
+  float rth = 0.f, rda = 0.f;
+  auto prefetch = [&](int s) {
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (size_t)s * 2 * G::HW);
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) rx[q] = x4[lane + 64 * q];
+    const f32x4* p4 = reinterpret_cast<const f32x4*>(sv.p1 + (size_t)s * C1 * G::HW2);
+#pragma unroll
+    for (int q = 0; q < P1Q; ++q) rp1[q] = p4[lane + 64 * q];
+    const f32x4* q4 = reinterpret_cast<const f32x4*>(p2 + (size_t)s * G::F + FPL * lane);
+    const uint32_t* c4 = reinterpret_cast<const uint32_t*>(sv.c2 + (size_t)s * G::F + FPL * lane);
+#pragma unroll
+    for (int q = 0; q < FPL / 4; ++q) {
+      rp2[q] = q4[q];
+      rc2[q] = c4[q];
+    }
+    rc1 = sv.c1[(size_t)s * G::HW2 + lane % G::HW2];
+    if (lane < n) {
+      rth = angles[(size_t)s * n + lane];
+      rda = dang[(size_t)s * n + lane];
+    }
+  };
+  const int s0 = blockIdx.x * NWV + wv;
+  if (s0 < B) prefetch(s0);
+
+  for (int s = s0; s < B; s += gridDim.x * NWV) {
     if (STAMP && first) ts[1] = stamp();
-    sample_forward<H, W, false>(x + (size_t)s * 2 * G::HW, ws, act, lane, no_wreg, flat + o.w1, flat + o.b1,
-                                ws[S_B2 + (lane & 31)]);
-    if (STAMP && first) ts[2] = stamp();
+    // ---- this sample's saved state -> LDS images (x padded, p1 padded channel-last) ----
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const int i = lane + 64 * q, c = (4 * i) / G::HW, p = (4 * i) % G::HW;
+      float* d = act + G::o_x + c * G::XP + (p / W + 1) * G::XW + p % W + 1;
+      d[0] = rx[q][0];
+      d[1] = rx[q][1];
+      d[2] = rx[q][2];
+      d[3] = rx[q][3];
+    }
+#pragma unroll
+    for (int q = 0; q < P1Q; ++q) {
+      const int i = lane + 64 * q, win = i >> 2, cq = i & 3;
+      const int qy = win / G::W2, qx = win % G::W2;
+      *reinterpret_cast<f32x4*>(act + G::o_p1 + ((qy + 1) * G::PW + qx + 1) * G::PC + 4 * cq) = rp1[q];
+    }
     float* misc = act + G::o_misc;
     if (lane < n) {
-      const float th = angles[(size_t)s * n + lane];
-      const float d = dang[(size_t)s * n + lane] * (1.f - th * th);
+      const float d = rda * (1.f - rth * rth);
       misc[lane] = d;
       dpre_out[(size_t)s * n + lane] = d;
       gbl += d;
     }
+    float p2v[FPL];
+    uint32_t c2v[FPL / 4], c1v = rc1;
+#pragma unroll
+    for (int q = 0; q < FPL / 4; ++q) {
+      p2v[4 * q] = rp2[q][0];
+      p2v[4 * q + 1] = rp2[q][1];
+      p2v[4 * q + 2] = rp2[q][2];
+      p2v[4 * q + 3] = rp2[q][3];
+      c2v[q] = rc2[q];
+    }
+    if (s + gridDim.x * NWV < B) prefetch(s + gridDim.x * NWV);
     // dz2's zero halo is clobbered by the previous sample's dz1 (aliased): re-zero the image
     for (int i = lane; i < G::PP * G::DC / 4; i += 64)
       reinterpret_cast<float4*>(act + G::o_dz2)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     wave_lds_fence();
-    // linear backward -> dp2, pool-2 backward (+ReLU mask) -> padded dz2
+    if (STAMP && first) ts[2] = stamp();
+    // linear backward -> dp2 (FPL consecutive features per lane: float4 weight reads), pool-2
+    // backward through the saved window choice (+ReLU: passes iff the pooled value is > 0)
+    {
+      float dp[FPL];
 #pragma unroll
-    for (int i = 0; i < G::F / 64; ++i) {
-      const int f = lane + 64 * i;
-      float dp = 0.f;
-      for (int j = 0; j < n; ++j) dp += wl[j * wl_stride(G::F) + f] * misc[j];
-      int arg;
-      pool2<H, W>(act, f, arg);
-      const int c = f / G::HW4, q = f % G::HW4, qy = q / G::W4, qx = q % G::W4;
-      const float* z = act + G::o_z2 + c * G::HW2;
-      const bool pass = z[arg] > 0.f;
+      for (int i = 0; i < FPL; ++i) dp[i] = 0.f;
+      for (int j = 0; j < n; ++j) {
+        const float mj = misc[j];
+        const float4* wr = reinterpret_cast<const float4*>(wl + j * wl_stride(G::F) + FPL * lane);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int py = 2 * qy + (r >> 1), px = 2 * qx + (r & 1);
-        const int pidx = py * G::W2 + px;
-        act[G::o_dz2 + ((py + 1) * G::PW + px + 1) * G::DC + c] = (pidx == arg && pass) ? dp : 0.f;
+        for (int q = 0; q < FPL / 4; ++q) {
+          const float4 w4 = wr[q];
+          dp[4 * q] += w4.x * mj;
+          dp[4 * q + 1] += w4.y * mj;
+          dp[4 * q + 2] += w4.z * mj;
+          dp[4 * q + 3] += w4.w * mj;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FPL; ++i) {
+        const int f = FPL * lane + i;
+        const int c = f / G::HW4, q = f % G::HW4, qy = q / G::W4, qx = q % G::W4;
+        const int rel = (c2v[i / 4] >> (8 * (i % 4))) & 0xff;
+        const float g = p2v[i] > 0.f ? dp[i] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int py = 2 * qy + (r >> 1), px = 2 * qx + (r & 1);
+          act[G::o_dz2 + ((py + 1) * G::PW + px + 1) * G::DC + c] = (r == rel) ? g : 0.f;
+        }
       }
     }
     wave_lds_fence();
@@ -462,31 +568,23 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
     }
     wave_lds_fence();
     if (STAMP && first) ts[5] = stamp();
-    // pool-1 backward (+ReLU mask): recompute conv1 (lane = window row, all 16 channels, scalar
-    // weights), find each window's first max across the two row lanes, route dp1 -> dz1 (C1 x HW)
-    for (int idx = lane; idx < 2 * G::HW2; idx += 64) {
-      const int win = idx >> 1, hw = idx & 1;
-      float acc[16][2];
-      conv1_half<H, W>(act, flat + o.w1, flat + o.b1, win, hw, acc);
+    // pool-1 backward through the saved window choices (+ReLU: passes iff p1 > 0): lane = window,
+    // CPL channels; every 2x2 window of dz1 (C1 x HW) is written whole
+    {
+      const int win = lane % G::HW2, cb = (lane / G::HW2) * CPL;
       const int qy = win / G::W2, qx = win % G::W2;
 #pragma unroll
-      for (int co = 0; co < 16; ++co) {
-        const float o0 = __shfl_xor(acc[co][0], 1), o1 = __shfl_xor(acc[co][1], 1);
-        // window scan order: top-left, top-right, bottom-left, bottom-right (reference argmax)
-        const float v[4] = {hw ? o0 : acc[co][0], hw ? o1 : acc[co][1], hw ? acc[co][0] : o0, hw ? acc[co][1] : o1};
-        int am = 0;
-        float mv = relu(v[0]);
-#pragma unroll
-        for (int p = 1; p < 4; ++p)
-          if (relu(v[p]) > mv) {
-            mv = relu(v[p]);
-            am = p;
-          }
-        const float g = (v[am] > 0.f) ? act[G::o_dp1 + co * G::HW2 + win] : 0.f;
-        if (hw == 0) gb1[co] += g;
-        float* dz = act + G::o_dz1 + co * G::HW + (2 * qy + hw) * W + 2 * qx;
-        dz[0] = (am == 2 * hw) ? g : 0.f;
-        dz[1] = (am == 2 * hw + 1) ? g : 0.f;
+      for (int c = 0; c < CPL; ++c) {
+        const int co = cb + c;
+        const float pv = act[G::o_p1 + ((qy + 1) * G::PW + qx + 1) * G::PC + co];
+        const float g = pv > 0.f ? act[G::o_dp1 + co * G::HW2 + win] : 0.f;
+        gb1[c] += g;
+        const uint32_t code = (c1v >> (2 * co)) & 3u;
+        float* dz = act + G::o_dz1 + co * G::HW + (2 * qy) * W + 2 * qx;
+        dz[0] = code == 0 ? g : 0.f;
+        dz[1] = code == 1 ? g : 0.f;
+        dz[W] = code == 2 ? g : 0.f;
+        dz[W + 1] = code == 3 ? g : 0.f;
       }
     }
     wave_lds_fence();
@@ -534,11 +632,13 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
       const int co = 4 * kq + r, k = 16 * t + col16;
       if (k < K1) mine[C2 * K2 + co * K1 + k] = gw1[t][r];
     }
-  // b1: lanes (win, h) hold 8 channels; combine the 32 windows of each half
+  // b1: lane (window, channel block cb) holds channels cb .. cb+CPL-1; sum over the windows
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {   // b1: per-window lanes hold all 16 channels
-    const float v = wave_sum(gb1[c]);
-    if (lane == 0) mine[C2 * K2 + C1 * K1 + c] = v;
+  for (int c = 0; c < CPL; ++c) {
+    float v = gb1[c];
+#pragma unroll
+    for (int off = 1; off < G::HW2; off <<= 1) v += __shfl_xor(v, off);
+    if (lane % G::HW2 == 0) mine[C2 * K2 + C1 * K1 + (lane / G::HW2) * CPL + c] = v;
   }
   {
     const float v = gb2 + __shfl_xor(gb2, 32);
@@ -586,37 +686,38 @@ size_t bwd_smem(int n) {
 }
 
 template <int H, int W>
-int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* p2, int B, int n, int grid,
+int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* p2, Saved sv, int B, int n, int grid,
                hipStream_t s, unsigned long long* stamps = nullptr) {
   constexpr int NW = fwd_waves<W>();
   const size_t sm = fwd_smem<H, W>(n);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   if (stamps) {
     if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW, true>, sm)) return (int)e;
-    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW, true>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, B,
-                       n, stamps);
+    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW, true>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, sv,
+                       B, n, stamps);
   } else {
     if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW>, sm)) return (int)e;
-    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, B, n,
-                       nullptr);
+    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, sv, B,
+                       n, nullptr);
   }
   return (int)hipGetLastError();
 }
 
 template <int H, int W>
 int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, const float* dang, float* dpre,
-               float* slab, int B, int n, int grid, hipStream_t s, unsigned long long* stamps = nullptr) {
+               float* slab, const float* p2, Saved sv, int B, int n, int grid, hipStream_t s,
+               unsigned long long* stamps = nullptr) {
   constexpr int NW = bwd_waves<W>();
   const size_t sm = bwd_smem<H, W>(n);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   if (stamps) {
     if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW, true>, sm)) return (int)e;
     hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW, true>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang,
-                       dpre, slab, B, n, stamps);
+                       dpre, slab, p2, sv, B, n, stamps);
   } else {
     if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW>, sm)) return (int)e;
     hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang, dpre,
-                       slab, B, n, nullptr);
+                       slab, p2, sv, B, n, nullptr);
   }
   return (int)hipGetLastError();
 }
@@ -627,24 +728,29 @@ int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, c
 using namespace qd::qsc2;
 
 // offs: [w1, b1, w2, b2, wl, bl, row_width] float offsets into the flat parameter buffer.
-QD_API int qd_qsc2_fwd(const float* x, const float* flat, const int* offs, float* angles, float* p2, int B, int n, int H,
-                       int W, int grid, void* stream) {
-  if (n < 1 || n > 16 || B <= 0 || grid <= 0) return (int)hipErrorInvalidValue;
+// Saved for the backward: p1s (B, HW/4, 16) f32, c1 (B, HW/4) u32, c2 (B, F) u8 (see sample_forward).
+QD_API int qd_qsc2_fwd(const float* x, const float* flat, const int* offs, float* angles, float* p2, float* p1s,
+                       uint32_t* c1, uint8_t* c2, int B, int n, int H, int W, int grid, void* stream) {
+  if (n < 1 || n > 16 || B <= 0 || grid <= 0 || !p1s || !c1 || !c2) return (int)hipErrorInvalidValue;
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, B, n, grid, s);
-  if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, B, n, grid, s);
+  if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, sv, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, sv, B, n, grid, s);
   return (int)hipErrorInvalidValue;
 }
 
 // slab: (grid, offs[6]) floats, row layout = flat layout from offs[0] (wl columns left zero).
+// p2 / p1s / c1 / c2: what qd_qsc2_fwd saved for this batch.
 QD_API int qd_qsc2_bwd(const float* x, const float* flat, const int* offs, const float* angles, const float* dang,
-                       float* dpre, float* slab, int B, int n, int H, int W, int grid, void* stream) {
-  if (n < 1 || n > 16 || B <= 0 || grid <= 0) return (int)hipErrorInvalidValue;
+                       float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1, uint8_t* c2, int B, int n,
+                       int H, int W, int grid, void* stream) {
+  if (n < 1 || n > 16 || B <= 0 || grid <= 0 || !p2 || !p1s || !c1 || !c2) return (int)hipErrorInvalidValue;
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, B, n, grid, s);
-  if (H == 16 && W == 16) return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, B, n, grid, s);
+  if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s);
   return (int)hipErrorInvalidValue;
 }
 
@@ -658,24 +764,29 @@ QD_API int qd_qsc2_waves(int W, int backward) {
 // Diagnostic: forward with per-wave phase stamps (stamps: grid * waves * 12 u64):
 // [0] kernel start [1] weights staged [2] input tile [3] conv1+pool [4] conv2 [5] pool2+linear
 // (first sample of the wave) [6] wave done.
-QD_API int qd_qsc2_fwd_stamped(const float* x, const float* flat, const int* offs, float* angles, float* p2, int B,
-                               int n, int H, int W, int grid, unsigned long long* stamps, void* stream) {
+QD_API int qd_qsc2_fwd_stamped(const float* x, const float* flat, const int* offs, float* angles, float* p2,
+                               float* p1s, uint32_t* c1, uint8_t* c2, int B, int n, int H, int W, int grid,
+                               unsigned long long* stamps, void* stream) {
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
-  if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, B, n, grid, (hipStream_t)stream, stamps);
-  if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, B, n, grid, (hipStream_t)stream, stamps);
+  Saved sv{p1s, c1, c2};
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, sv, B, n, grid, s, stamps);
+  if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, sv, B, n, grid, s, stamps);
   return (int)hipErrorInvalidValue;
 }
 
 // Diagnostic: backward with per-wave phase stamps (stamps: grid * waves * 12 u64): [0] start
-// [1] weights staged [2] forward recompute [3] linear + pool-2 backward [4] conv2 weight grads
+// [1] weights staged [2] saved state -> LDS [3] linear + pool-2 backward [4] conv2 weight grads
 // [5] conv2 data grads [6] pool-1 backward [7] conv1 weight grads (first sample) [8] wave done.
 QD_API int qd_qsc2_bwd_stamped(const float* x, const float* flat, const int* offs, const float* angles,
-                               const float* dang, float* dpre, float* slab, int B, int n, int H, int W, int grid,
-                               unsigned long long* stamps, void* stream) {
+                               const float* dang, float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1,
+                               uint8_t* c2, int B, int n, int H, int W, int grid, unsigned long long* stamps,
+                               void* stream) {
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
-  if (H == 16 && W == 8)
-    return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, B, n, grid, (hipStream_t)stream, stamps);
+  Saved sv{p1s, c1, c2};
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s, stamps);
   if (H == 16 && W == 16)
-    return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, B, n, grid, (hipStream_t)stream, stamps);
+    return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s, stamps);
   return (int)hipErrorInvalidValue;
 }

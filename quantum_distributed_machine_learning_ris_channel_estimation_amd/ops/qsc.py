@@ -62,6 +62,11 @@ class QSCStepHIP:
             self.grid_fwd = -(-batch_total // wf(self.Ww, 0))      # one sample per wave
             self.grid_bwd = min(-(-batch_total // wf(self.Ww, 1)), grid_bwd)
             self.p2 = torch.empty(batch_total, feat, **f32)        # pool-2 features (linear weight grad)
+            # saved by the forward for the backward: pool-1 map + both pools' argmax choices
+            hw2 = self.Hh * self.Ww // 4
+            self.p1s = torch.empty(batch_total, hw2 * 16, **f32)
+            self.c1 = torch.empty(batch_total, hw2, device=dev, dtype=torch.int32)
+            self.c2 = torch.empty(batch_total, feat, device=dev, dtype=torch.uint8)
             self.dpre = torch.empty(batch_total, self.n, **f32)
             self.gwl = space.grad[names["preprocess.7.weight"]:names["preprocess.7.weight"] + self.n * feat].view(
                 self.n, feat)
@@ -87,8 +92,8 @@ class QSCStepHIP:
         self.qslab = torch.empty(self.qrows, 2 * self.n * self.L, **f32)
         self._pre_fwd = nat.fn(L, "qd_qsc_pre_fwd", [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._pre_bwd = nat.fn(L, "qd_qsc_pre_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
-        self._fwd2 = nat.fn(L, "qd_qsc2_fwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
-        self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+        self._fwd2 = nat.fn(L, "qd_qsc2_fwd", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+        self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
             self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
@@ -116,6 +121,9 @@ class QSCStepHIP:
         return w
 
     @torch.no_grad()
+    def _saved(self):
+        return nat.ptr(self.p1s), nat.ptr(self.c1), nat.ptr(self.c2)
+
     def __call__(self, x: torch.Tensor, labels: torch.Tensor, loss_acc: Optional[torch.Tensor] = None,
                  skip: Optional[torch.Tensor] = None, skip_add: bool = False, accumulate: bool = True) -> torch.Tensor:
         """x (B, 2, H, W) fp32 contiguous, labels (B,) int64.  Returns loss (1,).
@@ -128,8 +136,8 @@ class QSCStepHIP:
         st = nat.stream_ptr(x.device)
         flat = sp.flat
         if self.impl == "mfma":
-            nat.check(self._fwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2), B, n,
-                                 self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
+            nat.check(self._fwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
+                                 *self._saved(), B, n, self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
         else:
             nat.check(self._pre_fwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), B, n, self.Hh,
                                     self.Ww, self.grid_fwd, st), "qsc_pre_fwd")
@@ -151,8 +159,8 @@ class QSCStepHIP:
                   "reduce_slab")
         if self.impl == "mfma":
             nat.check(self._bwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang),
-                                 nat.ptr(self.dpre), nat.ptr(self.preslab), B, n, self.Hh, self.Ww, self.grid_bwd, st),
-                      "qsc2_bwd")
+                                 nat.ptr(self.dpre), nat.ptr(self.preslab), nat.ptr(self.p2), *self._saved(), B, n,
+                                 self.Hh, self.Ww, self.grid_bwd, st), "qsc2_bwd")
         else:
             nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B,
                                     n, self.Hh, self.Ww, self.grid_bwd, st), "qsc_pre_bwd")

@@ -31,9 +31,10 @@ def main():
     waves = nat.fn(lib, "qd_qsc2_waves", [ctypes.c_int, ctypes.c_int])(8, 0)
     grid = step.grid_fwd
     st = torch.zeros(grid * waves * 12, dtype=torch.int64, device=dev)
-    f = nat.fn(lib, "qd_qsc2_fwd_stamped", [ctypes.c_void_p] * 5 + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2)
+    f = nat.fn(lib, "qd_qsc2_fwd_stamped", [ctypes.c_void_p] * 8 + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2)
     for _ in range(3):
-        nat.check(f(nat.ptr(x), nat.ptr(sp.flat), step.offs, nat.ptr(step.angles), nat.ptr(step.p2), B, n, 16, 8, grid,
+        nat.check(f(nat.ptr(x), nat.ptr(sp.flat), step.offs, nat.ptr(step.angles), nat.ptr(step.p2), *step._saved(), B, n,
+                    16, 8, grid,
                     nat.ptr(st), nat.stream_ptr(dev)), "stamped")
     torch.cuda.synchronize()
     t = st.view(grid * waves, 12).cpu().double()
@@ -52,13 +53,14 @@ def main():
     wb = nat.fn(lib, "qd_qsc2_waves", [ctypes.c_int, ctypes.c_int])(8, 1)
     gb = step.grid_bwd
     sb = torch.zeros(gb * wb * 12, dtype=torch.int64, device=dev)
-    fb = nat.fn(lib, "qd_qsc2_bwd_stamped", [ctypes.c_void_p] * 7 + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2)
+    fb = nat.fn(lib, "qd_qsc2_bwd_stamped", [ctypes.c_void_p] * 11 + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2)
     nat.check(fb(nat.ptr(x), nat.ptr(sp.flat), step.offs, nat.ptr(step.angles), nat.ptr(step.dang), nat.ptr(step.dpre),
-                 nat.ptr(step.preslab), B, n, 16, 8, gb, nat.ptr(sb), nat.stream_ptr(dev)), "bwd stamped")
+                 nat.ptr(step.preslab), nat.ptr(step.p2), *step._saved(), B, n, 16, 8, gb, nat.ptr(sb),
+                 nat.stream_ptr(dev)), "bwd stamped")
     torch.cuda.synchronize()
     tb = sb.view(gb * wb, 12).cpu().double()
-    bn = ["stage weights", "forward recompute", "linear + pool2 bwd", "conv2 wgrad (MFMA)", "conv2 dgrad (MFMA)",
-          "pool1 bwd (conv1 recompute)", "conv1 wgrad (MFMA)", "rest of samples + tail"]
+    bn = ["stage weights", "saved state -> LDS", "linear + pool2 bwd", "conv2 wgrad (MFMA)", "conv2 dgrad (MFMA)",
+          "pool1 bwd (saved argmax)", "conv1 wgrad (MFMA)", "rest of samples + tail"]
     out["backward"] = {nm: float((tb[:, i + 1] - tb[:, i]).median()) for i, nm in enumerate(bn)}
     out["backward"]["wave_lifetime_median_cycles"] = float((tb[:, 8] - tb[:, 0]).median())
     print(json.dumps(out, indent=1))
