@@ -28,6 +28,16 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Diagnostic phase stamp (stamped kernel builds only): s_memtime with its own lgkmcnt wait, fenced
+// by scheduling barriers so the compiler keeps each phase's work on its side of the stamp.
+__device__ __forceinline__ unsigned long long phase_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);

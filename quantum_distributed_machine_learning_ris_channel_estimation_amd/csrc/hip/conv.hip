@@ -81,6 +81,26 @@ __device__ __forceinline__ void load8(const uint16_t* p, float* v) {
   }
 }
 
+// Raw 16-byte vectors kept in registers between a prefetch and its use (no conversion at load
+// time, so the compiler's wait for the data lands at the use, one sample later).
+template <typename T>
+struct PerQ;
+template <>
+struct PerQ<float> { static constexpr int N = 4; };
+template <>
+struct PerQ<uint16_t> { static constexpr int N = 8; };
+__device__ __forceinline__ void unpack_q(const uint4 q, float* v, const float*) {
+  v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+}
+__device__ __forceinline__ void unpack_q(const uint4 q, float* v, const uint16_t*) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // conv3x3_kernel: forward (and data-gradient) implicit GEMM
 // grid: (U * chunks, E); block 256 (4 waves); each wave owns `spw` consecutive samples.
@@ -88,11 +108,16 @@ __device__ __forceinline__ void load8(const uint16_t* p, float* v) {
 // DGRAD: weights used transposed + flipped (W[e*32+k][lane][8-tap]); output fp32.
 // wt: B fragments pre-packed by pack_weights_kernel (fwd or dgrad order).
 // ------------------------------------------------------------------------------------------
-template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN>
-__global__ void __launch_bounds__(256) conv3x3_kernel(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
+template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN, bool STAMP = false>
+__global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
                                                       const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
                                                       void* __restrict__ out, float* __restrict__ stats, int E, int B,
-                                                      int chunks, int spw) {
+                                                      int chunks, int spw,
+                                                      unsigned long long* __restrict__ stamps = nullptr) {
+  // STAMP (diagnostic builds): per wave [0] start [1] weights + BN params staged [2] first sample
+  // staged [3] first sample's MFMAs + epilogue [4] all samples [5] end
+  unsigned long long ts[8] = {};
+  if constexpr (STAMP) ts[0] = phase_stamp();
   using G = Geo<H, W>;
   constexpr int CINP = (CIN % 16 == 0) ? CIN + 8 : CIN;  // channel-last pixel stride (bf16)
   constexpr int KS = (9 * CIN + 15) / 16;                   // 16-deep k steps
@@ -102,125 +127,214 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const TIN* __restrict__ xi
   const int hh = lane >> 5, l32 = lane & 31;
   const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
   const int EC_in = E * CIN;
+  static_assert(TILE % 8 == 0, "16-byte tile fills");
   __bf16* tile = reinterpret_cast<__bf16*>(smem) + wv * TILE;
-  for (int i = lane; i < TILE; i += 64) tile[i] = (__bf16)0.f;
+  for (int i = lane; i < TILE / 8; i += 64) reinterpret_cast<bf16x8*>(tile)[i] = bf16x8{};
 
-  // ---- weights -> B fragments (registers): pre-packed [e][s][lane][8] bf16 (pack_weights_kernel) ----
-  bf16x8 bfrag[KS];
-  const bf16x8* wp = reinterpret_cast<const bf16x8*>(wt) + (size_t)e * KS * 64 + lane;
-#pragma unroll
-  for (int s = 0; s < KS; ++s) bfrag[s] = wp[s * 64];
-
+  bf16x8* wl = reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(smem) + 4 * TILE);   // B fragments
+  constexpr bool RAWIN = INM == IN_RAW_F32;
+  float* stl = reinterpret_cast<float*>(wl + KS * 64);                                     // BN params
   // per-lane channel for the output/statistics: column of the MFMA tile
   float s1 = 0.f, s2 = 0.f;
   const int n0 = u * B + (chunk * 4 + wv) * spw;
   const int nend = min((u + 1) * B, n0 + spw);
-  const float* st_u = st_in ? st_in + (size_t)u * EC_in * NST : nullptr;
+
+  // ---- one-sample-ahead register prefetch of the raw input (converted at use, one sample later).
+  // Where a whole sample does not fit the register budget (P256 dgrad), groups of GR items are
+  // loaded and staged synchronously instead (batched: GR loads in flight per round trip). ----
+  constexpr int CH8 = CIN * G::HW / 8;                  // 8-value staging items per sample
+  constexpr int ITER = RAWIN ? (CIN * G::HW) / 64 : CH8 / 64;
+  static_assert(RAWIN ? (CIN * G::HW) % 64 == 0 : CH8 % 64 == 0, "whole waves per staging pass");
+  constexpr int QV = RAWIN ? 1 : (int)sizeof(TIN) / 2;  // uint4s per 8-value item (bf16: 1, f32: 2)
+  constexpr int HOLD = ITER * (QV + (INM == IN_BNBWD ? 1 : 0));   // 16-byte registers per sample
+  constexpr bool PREF = RAWIN || (HOLD <= 16 && G::HW <= 128);   // (P256: registers go to the MFMA pipeline)
+  constexpr int GR = PREF ? ITER : (INM == IN_BNBWD ? 2 : 4);
+  static_assert(ITER % GR == 0, "staging groups");
+  [[maybe_unused]] uint4 rv[RAWIN ? 1 : GR][QV];
+  [[maybe_unused]] uint4 rz[INM == IN_BNBWD ? GR : 1];
+  [[maybe_unused]] float rr[RAWIN ? GR : 1];
+  auto load_group = [&](int n, int g0) {
+    const size_t base = ((size_t)n * E + e) * CIN * G::HW;
+#pragma unroll
+    for (int k = 0; k < GR; ++k) {
+      const int it = g0 + k;
+      if constexpr (RAWIN) {
+        rr[k] = ldf<TIN>(xin, base + lane + 64 * it);
+      } else {
+        const size_t off = base + (size_t)(lane + 64 * it) * 8;   // item i = elements [8i, 8i+8)
+        const uint4* src = reinterpret_cast<const uint4*>(xin + off);
+#pragma unroll
+        for (int q = 0; q < QV; ++q) rv[k][q] = src[q];
+        if constexpr (INM == IN_BNBWD) rz[k] = *reinterpret_cast<const uint4*>(zaux + off);
+      }
+    }
+  };
+  // transform + scatter a group into the channel-last LDS tile
+  auto store_group = [&](int g0) {
+#pragma unroll
+    for (int k = 0; k < GR; ++k) {
+      const int i = lane + 64 * (g0 + k);
+      if constexpr (RAWIN) {
+        const int c = i / G::HW, p = i % G::HW;
+        tile[((p / W + 1) * G::WP + (p % W) + 1) * CINP + c] = (__bf16)rr[k];
+      } else {
+        const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
+        const float* sc = stl + c * NST;
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < QV; ++q) unpack_q(rv[k][q], v + q * (8 / QV), (const TIN*)nullptr);
+        if constexpr (INM == IN_BNRELU) {
+          const float a = sc[ST_A], b = sc[ST_B];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaxf(a * v[j] + b, 0.f);
+        } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
+          float z[8];
+          unpack_q(rz[k], z, (const uint16_t*)nullptr);
+          const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+          const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float g = (a * z[j] + b > 0.f) ? v[j] : 0.f;
+            v[j] = c1 * g - c2 - c3 * (z[j] - mu) * inv;
+          }
+        }
+        const int ph = p0 / W, pw = p0 % W;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tile[((ph + 1) * G::WP + pw + j + 1) * CINP + c] = (__bf16)v[j];
+      }
+    }
+  };
+  if (PREF && n0 < nend) load_group(n0, 0);   // the first sample's loads fly during the prologue
+  // ---- prologue: weights -> B fragments in LDS, shared by the 4 waves (pre-packed [e][s][lane][8]
+  // bf16 by pack_weights_kernel), and the BN parameters of this block's (group, expert) input
+  // channels; every load in flight at once (a rolled copy loop waited one round trip per pass) ----
+  {
+    constexpr int WPT = (KS * 64 + 255) / 256;
+    const bf16x8* wp = reinterpret_cast<const bf16x8*>(wt) + (size_t)e * KS * 64;
+    bf16x8 tw[WPT];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) tw[k] = wp[tid + 256 * k];
+    [[maybe_unused]] float tp = 0.f;
+    static_assert(CIN * NST <= 256, "one BN parameter per thread");
+    if constexpr (!RAWIN)
+      if (tid < CIN * NST) tp = st_in[((size_t)u * EC_in + e * CIN) * NST + tid];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) wl[tid + 256 * k] = tw[k];
+    if constexpr (!RAWIN)
+      if (tid < CIN * NST) stl[tid] = tp;
+  }
+  __syncthreads();
+  if constexpr (STAMP) ts[1] = phase_stamp();
 
   for (int n = n0; n < nend; ++n) {
     wave_lds_fence();
     // ---- stage the (transformed) input tile into LDS, channel-last, with zero halo ----
-    const size_t base = ((size_t)n * E + e) * CIN * G::HW;
-    if constexpr (INM == IN_RAW_F32) {
-      for (int i = lane; i < CIN * G::HW; i += 64) {
-        const int c = i / G::HW, p = i % G::HW;
-        const float v = ldf<TIN>(xin, base + i);
-        tile[((p / W + 1) * G::WP + (p % W) + 1) * CINP + c] = (__bf16)v;
-      }
+    if constexpr (PREF) {
+      store_group(0);
+      if (n + 1 < nend) load_group(n + 1, 0);
     } else {
-      // batched two-phase staging: issue UNR passes' global loads (8 values each) together, then
-      // transform + scatter to LDS.  A rolled loop waited one L2/HBM round trip per pass, which made
-      // this staging -- not the MFMAs -- the kernel's critical path.
-      constexpr int CH8 = CIN * G::HW / 8;
-      static_assert(CH8 % 64 == 0, "whole waves per staging pass");
-      constexpr int ITER = CH8 / 64;
-      constexpr int UNR0 = INM == IN_BNBWD ? 2 : 4;             // passes in flight (register budget)
-      constexpr int UNR = ITER < UNR0 ? ITER : UNR0;
-      static_assert(ITER % UNR == 0, "staging batches");
 #pragma unroll 1
-      for (int it0 = 0; it0 < ITER; it0 += UNR) {
-        float v[UNR][8];
-        [[maybe_unused]] float z[INM == IN_BNBWD ? UNR : 1][8];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          const int i = lane + 64 * (it0 + u);
-          const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
-          load8(xin + base + (size_t)c * G::HW + p0, v[u]);
-          if constexpr (INM == IN_BNBWD) load8(zaux + base + (size_t)c * G::HW + p0, z[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          const int i = lane + 64 * (it0 + u);
-          const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
-          const float* sc = st_u + (size_t)(e * CIN + c) * NST;
-          if constexpr (INM == IN_BNRELU) {
-            const float a = sc[ST_A], b = sc[ST_B];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[u][j] = fmaxf(a * v[u][j] + b, 0.f);
-          } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
-            const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
-            const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float g = (a * z[u][j] + b > 0.f) ? v[u][j] : 0.f;
-              v[u][j] = c1 * g - c2 - c3 * (z[u][j] - mu) * inv;
-            }
-          }
-          const int ph = p0 / W, pw = p0 % W;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) tile[((ph + 1) * G::WP + pw + j + 1) * CINP + c] = (__bf16)v[u][j];
-        }
+      for (int g0 = 0; g0 < ITER; g0 += GR) {
+        load_group(n, g0);
+        store_group(g0);
       }
     }
     wave_lds_fence();
-    // ---- MFMA over the M tiles ----
-#pragma unroll
-    for (int mt = 0; mt < G::MT; ++mt) {
+    if (STAMP && n == n0) ts[2] = phase_stamp();
+    // ---- MFMA: MG position tiles at once (independent accumulators) with the next k-step's
+    // fragments in flight behind the current MFMAs (a one-tile loop waited out one LDS round trip
+    // per MFMA: ds_read -> lgkmcnt(0) -> mfma) ----
+    auto load_a = [&](int mt, int s) -> bf16x8 {
       const int p = mt * 32 + l32, ph = p / W, pw = p % W;
-      f32x16 acc = {};
+      bf16x8 a;
+      if constexpr (CIN % 16 == 0) {
+        const int tap = (16 * s) / CIN, c0 = (16 * s) % CIN + 8 * hh;
+        const int kh = tap / 3, kw = tap % 3;
+        a = *reinterpret_cast<const bf16x8*>(tile + ((ph + kh) * G::WP + pw + kw) * CINP + c0);
+      } else {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        bf16x8 a;
-        if constexpr (CIN % 16 == 0) {
-          const int tap = (16 * s) / CIN, c0 = (16 * s) % CIN + 8 * hh;
-          const int kh = tap / 3, kw = tap % 3;
-          a = *reinterpret_cast<const bf16x8*>(tile + ((ph + kh) * G::WP + pw + kw) * CINP + c0);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int k = 16 * s + 8 * hh + j;
-            if (k < 9 * CIN) {
-              const int tap = k / CIN, c = k % CIN;
-              a[j] = tile[((ph + tap / 3) * G::WP + pw + tap % 3) * CINP + c];
-            } else {
-              a[j] = (__bf16)0.f;
-            }
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * s + 8 * hh + j;
+          if (k < 9 * CIN) {
+            const int tap = k / CIN, c = k % CIN;
+            a[j] = tile[((ph + tap / 3) * G::WP + pw + tap % 3) * CINP + c];
+          } else {
+            a[j] = (__bf16)0.f;
           }
         }
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfrag[s], acc, 0, 0, 0);
       }
-      // ---- epilogue: lane holds channel l32, positions mt*32 + 8g + 4hh + {0..3} ----
-      const size_t obase = ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + mt * 32 + 4 * hh;
+      return a;
+    };
+    constexpr int MG = G::MT < 4 ? G::MT : 4;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v0 = acc[4 * g], v1 = acc[4 * g + 1], v2 = acc[4 * g + 2], v3 = acc[4 * g + 3];
-        if constexpr (OUTM == OUT_Z_STATS) {
-          const uint16_t h0 = f32_to_bf16(v0), h1 = f32_to_bf16(v1), h2 = f32_to_bf16(v2), h3 = f32_to_bf16(v3);
-          uint2 pk = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + obase + 8 * g) = pk;
-          v0 = bf(h0); v1 = bf(h1); v2 = bf(h2); v3 = bf(h3);
-          s1 += v0 + v1 + v2 + v3;
-          s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
-        } else if constexpr (OUTM == OUT_BF16) {
-          const uint2 pk = make_uint2(f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16),
-                                      f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16));
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + obase + 8 * g) = pk;
+    for (int g0 = 0; g0 < G::MT; g0 += MG) {
+      f32x16 acc[MG];
+      bf16x8 a_cur[MG], b_cur = wl[lane];
+#pragma unroll
+      for (int j = 0; j < MG; ++j) {
+        acc[j] = f32x16{};
+        a_cur[j] = load_a(g0 + j, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        bf16x8 a_nxt[MG], b_nxt;
+        if (s + 1 < KS) {
+          b_nxt = wl[(s + 1) * 64 + lane];
+#pragma unroll
+          for (int j = 0; j < MG; ++j) a_nxt[j] = load_a(g0 + j, s + 1);
+        }
+        // pin the order: the next step's reads are issued before this step's MFMAs (left alone,
+        // the scheduler drains the tiles one after another to save registers)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < MG; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_cur[j], b_cur, acc[j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < KS) {
+          b_cur = b_nxt;
+#pragma unroll
+          for (int j = 0; j < MG; ++j) a_cur[j] = a_nxt[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MG; ++j) {
+        const int mt = g0 + j;
+        // ---- epilogue: lane holds channel l32, positions mt*32 + 8g + 4hh + {0..3}.  bf16 outputs:
+        // the two half-waves swap halves so each lane stores 8 consecutive positions (16 bytes) ----
+        const size_t rbase = ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + mt * 32;
+        if constexpr (OUTM == OUT_F32) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + rbase + 8 * g + 4 * hh) =
+                make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
         } else {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + obase + 8 * g) = make_float4(v0, v1, v2, v3);
+          uint2 pk[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const uint16_t h0 = f32_to_bf16(acc[j][4 * g]), h1 = f32_to_bf16(acc[j][4 * g + 1]);
+            const uint16_t h2 = f32_to_bf16(acc[j][4 * g + 2]), h3 = f32_to_bf16(acc[j][4 * g + 3]);
+            pk[g] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
+            if constexpr (OUTM == OUT_Z_STATS) {   // statistics of the stored (bf16-rounded) values
+              const float v0 = bf(h0), v1 = bf(h1), v2 = bf(h2), v3 = bf(h3);
+              s1 += v0 + v1 + v2 + v3;
+              s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {   // pair (g = 2q, 2q + 1): half-wave hh stores g = 2q + hh
+            const uint2 send = hh ? pk[2 * q] : pk[2 * q + 1];
+            const uint2 recv = make_uint2(__shfl_xor(send.x, 32), __shfl_xor(send.y, 32));
+            const uint2 mine = hh ? pk[2 * q + 1] : pk[2 * q];
+            const uint4 row = hh ? make_uint4(recv.x, recv.y, mine.x, mine.y) : make_uint4(mine.x, mine.y, recv.x, recv.y);
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + rbase + 8 * (2 * q + hh)) = row;
+          }
         }
       }
     }
+    if (STAMP && n == n0) ts[3] = phase_stamp();
   }
+  if constexpr (STAMP) ts[4] = phase_stamp();
   if constexpr (OUTM == OUT_Z_STATS) {
     // combine the two half-waves (same channel), then the 4 waves through LDS
     s1 += __shfl_xor(s1, 32);
@@ -239,6 +353,11 @@ __global__ void __launch_bounds__(256) conv3x3_kernel(const TIN* __restrict__ xi
       for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
       stats[(((size_t)u * chunks + chunk) * E * CO + e * CO + c) * 2 + k] = t;
     }
+  }
+  if constexpr (STAMP) {
+    ts[5] = phase_stamp();
+    if (lane == 0)
+      for (int k = 0; k < 8; ++k) stamps[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wv) * 8 + k] = ts[k];
   }
 }
 
@@ -290,26 +409,6 @@ __global__ void pack_weights_multi_kernel(PackJobs jobs) {
 // per workgroup; slab[(e * U*chunks + blockIdx.x)][co][ci][tap].
 // x = layer input (raw f32 pilots, or BN+ReLU of the previous z); dz from (dh, z, st).
 // ------------------------------------------------------------------------------------------
-// Raw 16-byte vectors kept in registers between a prefetch and its use (no conversion at load
-// time, so the compiler's wait for the data lands at the use, one sample later).
-template <typename T>
-struct PerQ;
-template <>
-struct PerQ<float> { static constexpr int N = 4; };
-template <>
-struct PerQ<uint16_t> { static constexpr int N = 8; };
-__device__ __forceinline__ void unpack_q(const uint4 q, float* v, const float*) {
-  v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
-}
-__device__ __forceinline__ void unpack_q(const uint4 q, float* v, const uint16_t*) {
-  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
 template <int CIN, int H, int W, int INM, typename TIN, typename TDH>
 __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __restrict__ xin,
                                                             const float* __restrict__ st_prev,
@@ -344,27 +443,15 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
   for (int t = 0; t < MTW; ++t) acc[t] = f32x16{};
   const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
 
-  // ---- per-item BN parameters: the channel of an item is the same for every sample -> registers ----
-  [[maybe_unused]] float xa[XIT], xbb[XIT];
-#pragma unroll
-  for (int k = 0; k < XIT; ++k) {
-    xa[k] = 1.f;
-    xbb[k] = 0.f;
-    const int i = tid + 256 * k;
-    if constexpr (INM == IN_BNRELU) {
-      if (XN % 256 == 0 || i < XN) {
-        const float* sc = st_prev + ((size_t)u * E * CIN + e * CIN + i / H) * NST;
-        xa[k] = sc[ST_A];
-        xbb[k] = sc[ST_B];
-      }
-    }
+  // ---- BN parameters of this block's (group, expert) channels -> LDS once: [x: CIN][dz: CO] x NST ----
+  float* prm = reinterpret_cast<float*>(DZ + CO * DZS);
+  if constexpr (INM == IN_BNRELU) {
+    const float* sp = st_prev + ((size_t)u * E * CIN + e * CIN) * NST;
+    for (int i = tid; i < CIN * NST; i += 256) prm[i] = sp[i];
   }
-  float da[DIT], db[DIT], dmu[DIT], dinv[DIT], dc1[DIT], dc2[DIT], dc3[DIT];
-#pragma unroll
-  for (int k = 0; k < DIT; ++k) {
-    const float* sc = st + ((size_t)u * E * CO + e * CO + (tid + 256 * k) / (G::HW / 8)) * NST;
-    da[k] = sc[ST_A]; db[k] = sc[ST_B]; dmu[k] = sc[ST_MEAN]; dinv[k] = sc[ST_INV];
-    dc1[k] = sc[ST_C1]; dc2[k] = sc[ST_C2]; dc3[k] = sc[ST_C3];
+  {
+    const float* sp = st + ((size_t)u * E * CO + e * CO) * NST;
+    for (int i = tid; i < CO * NST; i += 256) prm[CIN * NST + i] = sp[i];
   }
 
   // ---- one-sample-ahead register prefetch: sample n+1's loads fly during sample n's MFMAs ----
@@ -406,8 +493,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
 #pragma unroll
         for (int q = 0; q < XQ; ++q) unpack_q(xr[k][q], v + 1 + q * PerQ<TIN>::N, (const TIN*)nullptr);
         if constexpr (INM == IN_BNRELU) {
+          const float xa = prm[c * NST + ST_A], xb2 = prm[c * NST + ST_B];
 #pragma unroll
-          for (int q = 1; q <= W; ++q) v[q] = fmaxf(xa[k] * v[q] + xbb[k], 0.f);
+          for (int q = 1; q <= W; ++q) v[q] = fmaxf(xa * v[q] + xb2, 0.f);
         }
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
@@ -431,11 +519,14 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
 #pragma unroll
       for (int q = 0; q < DQ; ++q) unpack_q(dr[k][q], d + q * PerQ<TDH>::N, (const TDH*)nullptr);
       unpack_q(zr[k], zz, (const uint16_t*)nullptr);
+      const float* sc = prm + (CIN + c) * NST;
+      const float da = sc[ST_A], db = sc[ST_B], dmu = sc[ST_MEAN], dinv = sc[ST_INV];
+      const float dc1 = sc[ST_C1], dc2 = sc[ST_C2], dc3 = sc[ST_C3];
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float g = (da[k] * zz[j] + db[k] > 0.f) ? d[j] : 0.f;
-        o[j] = (__bf16)(dc1[k] * g - dc2[k] - dc3[k] * (zz[j] - dmu[k]) * dinv[k]);
+        const float g = (da * zz[j] + db > 0.f) ? d[j] : 0.f;
+        o[j] = (__bf16)(dc1 * g - dc2 - dc3 * (zz[j] - dmu) * dinv);
       }
       *reinterpret_cast<bf16x8*>(DZ + c * DZS + p0) = o;
     }
@@ -758,7 +849,9 @@ using namespace qd::conv;
 
 static size_t fwd_smem(int cin, int H, int W) {
   const int cinp = (cin % 16 == 0) ? cin + 8 : cin;
-  return 4 * (size_t)(H + 2) * (W + 2) * cinp * 2;
+  const int ks = (9 * cin + 15) / 16;   // (dgrad: cin = 32 -> 18 = the dgrad pack's k-steps too)
+  // 4 wave tiles | B fragments | BN params
+  return 4 * (size_t)(H + 2) * (W + 2) * cinp * 2 + (size_t)ks * 64 * 16 + (size_t)cin * NST * sizeof(float);
 }
 
 // layer: 1 -> CIN=2 raw f32 input; 2,3 -> CIN=32 bf16 z_prev with BN+ReLU (st_prev).
@@ -824,8 +917,26 @@ QD_API int qd_conv_dgrad(const void* dh, int dh_bf16, const uint16_t* z, const f
   return (int)hipGetLastError();
 }
 
+// Diagnostic: layer-2/3 forward (dgrad = 0) or bf16 data gradient (dgrad = 1) with per-wave phase
+// stamps (stamps: grid * 4 waves * 8 u64; see conv3x3_kernel).  P128 geometry only.
+QD_API int qd_conv_stamped(int dgrad, const void* xin, const uint16_t* zaux, const float* st, const uint16_t* w,
+                           void* out, float* stats, int N, int E, int B, int chunks, int spw,
+                           unsigned long long* stamps, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((N / B) * chunks, E);
+  if (dgrad)
+    hipLaunchKernelGGL((conv3x3_kernel<32, 16, 8, IN_BNBWD, OUT_BF16, true, uint16_t, true>), grid, dim3(256),
+                       fwd_smem(32, 16, 8), s, (const uint16_t*)xin, zaux, st, w, out, nullptr, E, B, chunks, spw,
+                       stamps);
+  else
+    hipLaunchKernelGGL((conv3x3_kernel<32, 16, 8, IN_BNRELU, OUT_Z_STATS, false, uint16_t, true>), grid, dim3(256),
+                       fwd_smem(32, 16, 8), s, (const uint16_t*)xin, nullptr, st, w, out, stats, E, B, chunks, spw,
+                       stamps);
+  return (int)hipGetLastError();
+}
+
 static size_t wgrad_smem(int cin, int H, int W) {
-  const size_t stage = (3 * (size_t)cin * ((H + 2) * W + 8) + 32 * (size_t)(H * W + 8)) * 2;
+  const size_t stage = (3 * (size_t)cin * ((H + 2) * W + 8) + 32 * (size_t)(H * W + 8)) * 2 + (cin + 32) * NST * 4;
   const size_t red = 2 * 32 * (size_t)(9 * cin + 1) * 4;
   return stage > red ? stage : red;
 }

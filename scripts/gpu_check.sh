@@ -33,8 +33,10 @@ for s in $STEPS; do
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" ;;
     prof_fp8) (cd /tmp && export TMPDIR=/tmp && run prof_fp8 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_fp8" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --dtype fp8) && python scripts/prof_summary.py "$OUT/prof_fp8/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_fp8_summary.md" ;;
     stamp) run stamp 300 python scripts/stamp_qsc.py ;;
+    stamp_conv) run stamp_conv 300 python scripts/stamp_conv.py ;;
     tune) run tune 900 python scripts/tune_kernels.py --what ${TUNE_WHAT:-qsc,conv} ;;
     fp8probe) run fp8probe 300 python scripts/probe_fp8.py ;;
+    fcprobe) run fcprobe 300 python scripts/probe_fc_gemm.py ;;
     diag) run diag 900 python scripts/diag_hdce.py --epochs ${DIAG_EPOCHS:-20} ;;
     gensweep) run gensweep 1500 python scripts/gen_sweep.py --epochs ${SWEEP_EPOCHS:-30} --sc-epochs 8 ;;
   esac

@@ -121,7 +121,7 @@ def main():
     if "wgrad" in what:
         tune_wgrad(128, 256, [4, 8, 16, 32])
     if "conv" in what:
-        tune_conv(128, [256], list(itertools.product([1, 2], [4, 8, 16], [4, 8, 16])))
+        tune_conv(128, [256], list(itertools.product([1, 2, 4], [8], [4, 8])))
 
 
 if __name__ == "__main__":
