@@ -587,45 +587,60 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
 // ------------------------------------------------------------------------------------------
 // Forward statistics: per (u, ch) mean/invstd/(a,b); running stats updated in u order.
 // One 64-lane block per channel: lanes sum the chunk partials, lane 0 finishes.
+constexpr int kMaxGroups = 8;   // statistics groups (users) per finalisation launch
 __global__ void __launch_bounds__(64) bn_stats_finalize_kernel(const float* __restrict__ stats,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ beta, float* __restrict__ run_mean,
                                                                float* __restrict__ run_var, float* __restrict__ st, int U,
                                                                int chunks, int EC, float count, float momentum, float eps,
-                                                               int training) {
+                                                               int training, long long* __restrict__ nbt, int n_nbt,
+                                                               long long nbt_inc) {
+  // every global load is issued up front (the per-group loop paid one round trip per group)
   const int ch = blockIdx.x, lane = threadIdx.x;
+  if (nbt && ch == 0 && lane < n_nbt) nbt[lane] += nbt_inc;   // BatchNorm num_batches_tracked
   const float g = gamma[ch], bt = beta[ch];
   float rm = run_mean[ch], rv = run_var[ch];
-  for (int u = 0; u < U; ++u) {
-    float mean, var;
-    if (training) {
-      float a = 0.f, b = 0.f;
+  float a[kMaxGroups], b[kMaxGroups];
+#pragma unroll
+  for (int u = 0; u < kMaxGroups; ++u) {
+    a[u] = 0.f;
+    b[u] = 0.f;
+    if (training && u < U) {
       for (int k = lane; k < chunks; k += 64) {
-        a += stats[(((size_t)u * chunks + k) * EC + ch) * 2];
-        b += stats[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
+        a[u] += stats[(((size_t)u * chunks + k) * EC + ch) * 2];
+        b[u] += stats[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
       }
-      a = wave_sum(a);
-      b = wave_sum(b);
-      mean = a / count;
-      var = fmaxf(b / count - mean * mean, 0.f);
-      rm = (1.f - momentum) * rm + momentum * mean;
-      rv = (1.f - momentum) * rv + momentum * var * count / (count - 1.f);
-    } else {
-      mean = rm;
-      var = rv;
-    }
-    if (lane == 0) {
-      const float inv = rsqrtf(var + eps);
-      float* r = st + ((size_t)u * EC + ch) * NST;
-      r[ST_MEAN] = mean;
-      r[ST_INV] = inv;
-      r[ST_A] = g * inv;
-      r[ST_B] = bt - mean * g * inv;
     }
   }
-  if (training && lane == 0) {
-    run_mean[ch] = rm;
-    run_var[ch] = rv;
+#pragma unroll
+  for (int u = 0; u < kMaxGroups; ++u) {
+    if (training && u < U) {
+      a[u] = wave_sum(a[u]);
+      b[u] = wave_sum(b[u]);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int u = 0; u < kMaxGroups; ++u) {
+      if (u >= U) break;
+      float mean, var;
+      if (training) {
+        mean = a[u] / count;
+        var = fmaxf(b[u] / count - mean * mean, 0.f);
+        rm = (1.f - momentum) * rm + momentum * mean;
+        rv = (1.f - momentum) * rv + momentum * var * count / (count - 1.f);
+      } else {
+        mean = rm;
+        var = rv;
+      }
+      const float inv = rsqrtf(var + eps);
+      float4* r = reinterpret_cast<float4*>(st + ((size_t)u * EC + ch) * NST);
+      r[0] = make_float4(mean, inv, g * inv, bt - mean * g * inv);   // ST_MEAN, ST_INV, ST_A, ST_B
+    }
+    if (training) {
+      run_mean[ch] = rm;
+      run_var[ch] = rv;
+    }
   }
 }
 
@@ -692,28 +707,44 @@ __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __rest
                                                              float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                              int U, int chunks, int EC, float count, int accumulate) {
   const int ch = blockIdx.x, lane = threadIdx.x;
+  const float gm = gamma[ch];
+  const float od = accumulate ? dgamma[ch] : 0.f, ob = accumulate ? dbeta[ch] : 0.f;
+  float sg[kMaxGroups], sgx[kMaxGroups], inv[kMaxGroups];
+#pragma unroll
+  for (int u = 0; u < kMaxGroups; ++u) {
+    sg[u] = 0.f;
+    sgx[u] = 0.f;
+    inv[u] = 0.f;
+    if (u < U) {
+      inv[u] = st[((size_t)u * EC + ch) * NST + ST_INV];
+      for (int k = lane; k < chunks; k += 64) {
+        sg[u] += slab[(((size_t)u * chunks + k) * EC + ch) * 2];
+        sgx[u] += slab[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
+      }
+    }
+  }
   float tg = 0.f, tgx = 0.f;
-  for (int u = 0; u < U; ++u) {
-    float sg = 0.f, sgx = 0.f;
-    for (int k = lane; k < chunks; k += 64) {
-      sg += slab[(((size_t)u * chunks + k) * EC + ch) * 2];
-      sgx += slab[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
+#pragma unroll
+  for (int u = 0; u < kMaxGroups; ++u) {
+    if (u < U) {
+      sg[u] = wave_sum(sg[u]);
+      sgx[u] = wave_sum(sgx[u]);
+      tg += sg[u];
+      tgx += sgx[u];
     }
-    sg = wave_sum(sg);
-    sgx = wave_sum(sgx);
-    if (lane == 0) {
-      float* r = st + ((size_t)u * EC + ch) * NST;
-      const float c1 = gamma[ch] * r[ST_INV];
-      r[ST_C1] = c1;
-      r[ST_C2] = c1 * sg / count;
-      r[ST_C3] = c1 * sgx / count;
-    }
-    tg += sg;
-    tgx += sgx;
   }
   if (lane == 0) {
-    dgamma[ch] = (accumulate ? dgamma[ch] : 0.f) + tgx;
-    dbeta[ch] = (accumulate ? dbeta[ch] : 0.f) + tg;
+#pragma unroll
+    for (int u = 0; u < kMaxGroups; ++u) {
+      if (u >= U) break;
+      const float c1 = gm * inv[u];
+      float* r = st + ((size_t)u * EC + ch) * NST;
+      r[ST_C1] = c1;
+      r[ST_C2] = c1 * sg[u] / count;
+      r[ST_C3] = c1 * sgx[u] / count;
+    }
+    dgamma[ch] = od + tgx;
+    dbeta[ch] = ob + tg;
   }
 }
 
@@ -782,18 +813,47 @@ __global__ void __launch_bounds__(256) slab_rows_sum4_kernel(const float* __rest
   slab_rows_sum4_body(slab, out, rows, width, blockIdx.y, blockIdx.x, accumulate);
 }
 
-// Several independent slab sums in one launch (blockIdx.z = job): the conv stack's three weight-
-// gradient reductions at the end of its backward.
+// Several independent slab sums in one launch (blockIdx.z = job): every gradient-slab reduction of
+// a step phase (conv weight slabs, quantum-layer slab, QSC preprocess slab) at once.  Jobs whose
+// width is not a multiple of 4 (or whose buffers are not 16-byte aligned) take a scalar path.
+constexpr int kSlabJobs = 8;
 struct SlabJobs {
-  const float* slab[4];
-  float* out[4];
-  int groups[4], rows[4], width[4];
+  const float* slab[kSlabJobs];
+  float* out[kSlabJobs];
+  int groups[kSlabJobs], rows[kSlabJobs], width[kSlabJobs], vec[kSlabJobs];
   int accumulate;
 };
+__device__ __forceinline__ void slab_rows_sum1_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
+                                                    int width, int g, int bx, int accumulate) {
+  __shared__ float red1[16][64];
+  const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* s = slab + (size_t)g * rows * width;
+  for (int r = ty; r < rows; r += 16) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = bx * 64 + q * 16 + tq;
+      if (i < width) t[q] += s[(size_t)r * width + i];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red1[ty][q * 16 + tq] = t[q];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int i = bx * 64 + threadIdx.x;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += red1[k][threadIdx.x];
+    if (i < width) out[(size_t)g * width + i] = (accumulate ? out[(size_t)g * width + i] : 0.f) + acc;
+  }
+}
 __global__ void __launch_bounds__(256) slab_rows_sum4_multi_kernel(SlabJobs jobs) {
   const int j = blockIdx.z;
   if (blockIdx.y >= jobs.groups[j] || blockIdx.x * 64 >= jobs.width[j]) return;
-  slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x, jobs.accumulate);
+  if (jobs.vec[j])
+    slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x, jobs.accumulate);
+  else
+    slab_rows_sum1_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x, jobs.accumulate);
 }
 
 __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
@@ -964,9 +1024,11 @@ QD_API int qd_conv_wgrad(int layer, const void* xin, const float* st_prev, const
 
 QD_API int qd_bn_stats_finalize(const float* stats, const float* gamma, const float* beta, float* run_mean,
                                 float* run_var, float* st, int U, int chunks, int EC, float count, float momentum,
-                                float eps, int training, void* stream) {
+                                float eps, int training, long long* nbt, int n_nbt, long long nbt_inc,
+                                void* stream) {
+  if (U < 1 || U > kMaxGroups || n_nbt > 64) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(EC), dim3(64), 0, (hipStream_t)stream, stats, gamma,
-                     beta, run_mean, run_var, st, U, chunks, EC, count, momentum, eps, training);
+                     beta, run_mean, run_var, st, U, chunks, EC, count, momentum, eps, training, nbt, n_nbt, nbt_inc);
   return (int)hipGetLastError();
 }
 
@@ -990,6 +1052,7 @@ QD_API int qd_bn_bwd_reduce(const void* dh, int dh_bf16, const uint16_t* z, cons
 // accumulate = 0: overwrite dgamma/dbeta (no zero_grad needed)
 QD_API int qd_bn_bwd_finalize(const float* slab, const float* gamma, float* st, float* dgamma, float* dbeta, int U,
                               int chunks, int EC, float count, int accumulate, void* stream) {
+  if (U < 1 || U > kMaxGroups) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(EC), dim3(64), 0, (hipStream_t)stream, slab, gamma, st,
                      dgamma, dbeta, U, chunks, EC, count, accumulate);
   return (int)hipGetLastError();
@@ -1016,18 +1079,18 @@ QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int
 // n <= 4 jobs, each as qd_slab_rows_sum (width % 4 == 0, 16-byte aligned), one launch
 QD_API int qd_slab_rows_sum_multi(int n, const float* const* slabs, float* const* outs, const int* groups,
                                   const int* rows, const int* widths, int accumulate, void* stream) {
-  if (n < 1 || n > 4) return (int)hipErrorInvalidValue;
+  if (n < 1 || n > kSlabJobs) return (int)hipErrorInvalidValue;
   SlabJobs jobs{};
   jobs.accumulate = accumulate;
   int gx = 0, gy = 0;
   for (int j = 0; j < n; ++j) {
-    if (widths[j] % 4 || ((uintptr_t)slabs[j] & 15) || ((uintptr_t)outs[j] & 15)) return (int)hipErrorInvalidValue;
+    jobs.vec[j] = !(widths[j] % 4 || ((uintptr_t)slabs[j] & 15) || ((uintptr_t)outs[j] & 15));
     jobs.slab[j] = slabs[j];
     jobs.out[j] = outs[j];
     jobs.groups[j] = groups[j];
     jobs.rows[j] = rows[j];
     jobs.width[j] = widths[j];
-    gx = std::max(gx, (widths[j] / 4 + 15) / 16);
+    gx = std::max(gx, (widths[j] + 63) / 64);
     gy = std::max(gy, groups[j]);
   }
   hipLaunchKernelGGL(slab_rows_sum4_multi_kernel, dim3(gx, gy, n), dim3(256), 0, (hipStream_t)stream, jobs);

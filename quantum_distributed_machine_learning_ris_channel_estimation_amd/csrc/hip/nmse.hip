@@ -173,10 +173,69 @@ __global__ void __launch_bounds__(256) grad_kernel(const TY* __restrict__ Y, con
   }
 }
 
+// Same gradient, column-blocked so the FC bias gradient falls out of it: grid (cols / 1024, RB),
+// thread = 4 columns x the rows of chunk blockIdx.y; colsum slab (RB, cols) gets each chunk's fp32
+// column sums of dY (reduced afterwards by qd_slab_rows_sum: deterministic, no atomics).
+template <typename TY, typename TD>
+__global__ void __launch_bounds__(256) grad_bias_kernel(const TY* __restrict__ Y, const float* __restrict__ Lb,
+                                                        const float* __restrict__ coef,
+                                                        const int* __restrict__ row_stream,
+                                                        const int* __restrict__ rowoff, TD* __restrict__ dY,
+                                                        float* __restrict__ colsum, int rows, int cols, int rpc) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 4;
+  const int r0 = blockIdx.y * rpc, r1 = min(rows, r0 + rpc);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c0 < cols) {
+    for (int r = r0; r < r1; ++r) {
+      const size_t e = (size_t)r * cols + c0;
+      const float c = coef[row_stream[r]];
+      const float4 yv = load4<TY>(Y + e);
+      const size_t le = rowoff ? (size_t)rowoff[r] * cols + c0 : e;
+      const float4 lv = *reinterpret_cast<const float4*>(Lb + le);
+      const float g0 = c * (yv.x - lv.x), g1 = c * (yv.y - lv.y), g2 = c * (yv.z - lv.z), g3 = c * (yv.w - lv.w);
+      acc.x += g0;
+      acc.y += g1;
+      acc.z += g2;
+      acc.w += g3;
+      if constexpr (std::is_same<TD, float>::value) {
+        *reinterpret_cast<float4*>(dY + e) = make_float4(g0, g1, g2, g3);
+      } else {
+        ushort4 h;
+        h.x = f32_to_bf16(g0);
+        h.y = f32_to_bf16(g1);
+        h.z = f32_to_bf16(g2);
+        h.w = f32_to_bf16(g3);
+        *reinterpret_cast<ushort4*>(dY + e) = h;
+      }
+    }
+    *reinterpret_cast<float4*>(colsum + (size_t)blockIdx.y * cols + c0) = acc;
+  }
+}
+
 }  // namespace nmse
 }  // namespace qd
 
 using namespace qd::nmse;
+
+// dY as qd_nmse_grad, plus colsum (chunks, cols) = per-row-chunk column sums of dY (bias gradient
+// partials).  cols % 4 == 0.
+QD_API int qd_nmse_grad_bias(const void* Y, int y_bf16, const float* label, const float* coef, const int* row_stream,
+                             const int* rowoff, void* dY, int dy_bf16, float* colsum, int chunks, int rows, int cols,
+                             void* stream) {
+  if (cols % 4 || chunks < 1) return (int)hipErrorInvalidValue;
+  const int rpc = (rows + chunks - 1) / chunks;
+  dim3 grid((cols / 4 + 255) / 256, chunks);
+  hipStream_t st = (hipStream_t)stream;
+#define QD_G(TY, TD)                                                                                          \
+  hipLaunchKernelGGL((grad_bias_kernel<TY, TD>), grid, dim3(256), 0, st, (const TY*)Y, label, coef, row_stream, \
+                     rowoff, (TD*)dY, colsum, rows, cols, rpc)
+  if (y_bf16 && dy_bf16) QD_G(uint16_t, uint16_t);
+  else if (y_bf16) QD_G(uint16_t, float);
+  else if (dy_bf16) QD_G(float, uint16_t);
+  else QD_G(float, float);
+#undef QD_G
+  return (int)hipGetLastError();
+}
 
 // y_bf16: 1 if Y is bf16 else fp32.  perf may be null.  rowoff (nullable): label/perf row of
 // output row r (labels gathered in place from the dataset store).

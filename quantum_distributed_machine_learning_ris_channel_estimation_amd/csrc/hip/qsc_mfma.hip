@@ -32,6 +32,8 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 struct Offs {
   int w1, b1, w2, b2, wl, bl, row;
+  int base;   // flat offset of slab column 0 (min of the preprocess and quantum-weight offsets)
+  int qw;     // flat offset of the quantum-layer weights (their slab columns: see qsc2_bwd_kernel)
 };
 
 // forward -> backward hand-off per sample (the backward routes gradients through the saved pool
@@ -40,6 +42,13 @@ struct Saved {
   float* p1;      // (B, HW2, 16) pool-1 map, channel-last
   uint32_t* c1;   // (B, HW2) pool-1 argmax codes, 2 bits per channel
   uint8_t* c2;    // (B, F) pool-2 window-relative argmax
+};
+
+// the quantum layer's adjoint-pass slab (rows, width): each backward workgroup also sums its share
+// of rows into the quantum-weight columns of its own slab row (one reduction launch fewer)
+struct QSlab {
+  const float* slab;
+  int rows, width;
 };
 
 template <int H, int W>
@@ -375,15 +384,15 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   }
 }
 
-// Backward.  dang (B, n) = dL/d(angles).  Outputs: dpre (B, n) = dL/d(pre-tanh) (for the linear
-// weight-gradient GEMM), slab row per workgroup = grads of [w1 | b1 | w2 | b2 | (wl: 0) | bl] in
-// the flat layout starting at o.w1.
+// Backward.  dang (B, n) = dL/d(angles).  Outputs: dpre (B, n) = dL/d(pre-tanh), slab row per
+// workgroup = grads of [w1 | b1 | w2 | b2 | wl | bl] in the flat layout starting at o.w1 (wl
+// columns zero when n > 64 / (F / 64): the caller then forms dWl = dpre^T p2 with a GEMM).
 template <int H, int W, int NWV, bool STAMP = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                       Offs o, const float* __restrict__ angles,
                                                       const float* __restrict__ dang, float* __restrict__ dpre_out,
                                                       float* __restrict__ slab, const float* __restrict__ p2,
-                                                      Saved sv, int B, int n,
+                                                      Saved sv, int B, int n, int wlk, QSlab qs,
                                                       unsigned long long* __restrict__ stamps = nullptr) {
   unsigned long long ts[NSTAMP] = {};
   bool first = true;
@@ -419,6 +428,15 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   float gb1[CPL], gb2 = 0.f, gbl = 0.f;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) gb1[c] = 0.f;
+  // linear-layer weight gradient dWl[j][f] += dpre[j] * p2[f], accumulated in registers over the
+  // wave's samples (lane = features FPL*lane ..) when n <= NWL: no separate GEMM launch
+  constexpr int NWL = 64 / FPL;
+  const bool wl_here = wlk != 0;   // host guarantees n <= NWL and the LDS reduction fits
+  float gwl[NWL][FPL];
+#pragma unroll
+  for (int j = 0; j < NWL; ++j)
+#pragma unroll
+    for (int i = 0; i < FPL; ++i) gwl[j][i] = 0.f;
 
   // ---- one-sample-ahead register prefetch of everything a sample reads from global memory ----
   // ext-vector registers (float4 is a struct: arrays of it are copied by memcpy and land in scratch)
@@ -505,6 +523,14 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
           dp[4 * q + 1] += w4.y * mj;
           dp[4 * q + 2] += w4.z * mj;
           dp[4 * q + 3] += w4.w * mj;
+        }
+      }
+      if (wl_here) {
+#pragma unroll
+        for (int j = 0; j < NWL; ++j) {
+          const float mj = j < n ? misc[j] : 0.f;
+#pragma unroll
+          for (int i = 0; i < FPL; ++i) gwl[j][i] += mj * p2v[i];
         }
       }
 #pragma unroll
@@ -615,9 +641,20 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
 
   // ---- deterministic workgroup reduction -> slab row (w1 | b1 | w2 | b2 | wl = 0 | bl) ----
   __syncthreads();
-  float* red = sm + S_WEND;   // reuse the activation images: NWV x (C2*K2 + C1*K1 + C1 + C2 + 16)
-  constexpr int RW = C2 * K2 + C1 * K1 + C1 + C2 + 16;
+  float* red = sm + S_WEND;   // reuse the activation images: NWV x RW
+  constexpr int RW0 = C2 * K2 + C1 * K1 + C1 + C2 + 16;
+  const int RW = RW0 + (wl_here ? n * G::F : 0);   // ... | wl [n][F]
   float* mine = red + wv * RW;
+  if (wl_here) {
+#pragma unroll
+    for (int j = 0; j < NWL; ++j)
+      if (j < n) {
+#pragma unroll
+        for (int q = 0; q < FPL / 4; ++q)
+          *reinterpret_cast<float4*>(mine + RW0 + j * G::F + FPL * lane + 4 * q) =
+              make_float4(gwl[j][4 * q], gwl[j][4 * q + 1], gwl[j][4 * q + 2], gwl[j][4 * q + 3]);
+      }
+  }
 #pragma unroll
   for (int t = 0; t < 5; ++t)
 #pragma unroll
@@ -652,17 +689,26 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
     if (lane == 0)
       for (int k = 0; k < NSTAMP; ++k) stamps[(size_t)(blockIdx.x * NWV + wv) * NSTAMP + k] = ts[k];
   }
+  // this workgroup's share of the quantum-layer slab rows
+  const int q0 = (int)((long long)qs.rows * blockIdx.x / gridDim.x);
+  const int q1 = (int)((long long)qs.rows * (blockIdx.x + 1) / gridDim.x);
   for (int i = threadIdx.x; i < o.row; i += 64 * NWV) {
     float v = 0.f;
     int src = -1;
-    if (i >= o.w2 - o.w1 && i < o.w2 - o.w1 + C2 * K2) src = i - (o.w2 - o.w1);
-    else if (i < C1 * K1) src = C2 * K2 + i;
-    else if (i >= o.b1 - o.w1 && i < o.b1 - o.w1 + C1) src = C2 * K2 + C1 * K1 + (i - (o.b1 - o.w1));
-    else if (i >= o.b2 - o.w1 && i < o.b2 - o.w1 + C2) src = C2 * K2 + C1 * K1 + C1 + (i - (o.b2 - o.w1));
-    else if (i >= o.bl - o.w1 && i < o.bl - o.w1 + n) src = C2 * K2 + C1 * K1 + C1 + C2 + (i - (o.bl - o.w1));
+    const int a = i + o.base;   // flat offset of this column
+    if (a >= o.w2 && a < o.w2 + C2 * K2) src = a - o.w2;
+    else if (a >= o.w1 && a < o.w1 + C1 * K1) src = C2 * K2 + (a - o.w1);
+    else if (a >= o.b1 && a < o.b1 + C1) src = C2 * K2 + C1 * K1 + (a - o.b1);
+    else if (a >= o.b2 && a < o.b2 + C2) src = C2 * K2 + C1 * K1 + C1 + (a - o.b2);
+    else if (a >= o.bl && a < o.bl + n) src = C2 * K2 + C1 * K1 + C1 + C2 + (a - o.bl);
+    else if (wl_here && a >= o.wl && a < o.wl + n * G::F) src = RW0 + (a - o.wl);
     if (src >= 0) {
 #pragma unroll
       for (int w = 0; w < NWV; ++w) v += red[w * RW + src];
+    } else if (qs.slab && a >= o.qw && a < o.qw + qs.width) {
+      const float* qc = qs.slab + (a - o.qw);
+#pragma unroll 4
+      for (int r = q0; r < q1; ++r) v += qc[(size_t)r * qs.width];
     }
     row[i] = v;
   }
@@ -678,10 +724,18 @@ template <int H, int W>
 size_t fwd_smem(int n) {
   return sizeof(float) * (fwd_act_base(n, Geo<H, W>::F) + fwd_waves<W>() * Geo<H, W>::FWD);
 }
+// the backward also reduces the linear weight gradient when its register tile holds n outputs and
+// the larger reduction image still fits the 160 KB of LDS
+template <int H, int W>
+bool wl_in_kernel(int n) {
+  using G = Geo<H, W>;
+  const size_t red = sizeof(float) * (S_WEND + bwd_waves<W>() * (C2 * K2 + C1 * K1 + C1 + C2 + 16 + (size_t)n * G::F));
+  return n <= 64 / (G::F / 64) && red <= 160 * 1024;
+}
 template <int H, int W>
 size_t bwd_smem(int n) {
   const size_t act = act_base_bwd(n, Geo<H, W>::F) + bwd_waves<W>() * Geo<H, W>::BWD;
-  const size_t red = S_WEND + bwd_waves<W>() * (C2 * K2 + C1 * K1 + C1 + C2 + 16);
+  const size_t red = S_WEND + bwd_waves<W>() * (C2 * K2 + C1 * K1 + C1 + C2 + 16 + (wl_in_kernel<H, W>(n) ? n * Geo<H, W>::F : 0));
   return sizeof(float) * (act > red ? act : red);
 }
 
@@ -705,7 +759,7 @@ int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* 
 
 template <int H, int W>
 int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, const float* dang, float* dpre,
-               float* slab, const float* p2, Saved sv, int B, int n, int grid, hipStream_t s,
+               float* slab, const float* p2, Saved sv, QSlab qs, int B, int n, int grid, hipStream_t s,
                unsigned long long* stamps = nullptr) {
   constexpr int NW = bwd_waves<W>();
   const size_t sm = bwd_smem<H, W>(n);
@@ -713,11 +767,11 @@ int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, c
   if (stamps) {
     if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW, true>, sm)) return (int)e;
     hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW, true>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang,
-                       dpre, slab, p2, sv, B, n, stamps);
+                       dpre, slab, p2, sv, B, n, (int)wl_in_kernel<H, W>(n), qs, stamps);
   } else {
     if (hipError_t e = allow_lds(qsc2_bwd_kernel<H, W, NW>, sm)) return (int)e;
     hipLaunchKernelGGL((qsc2_bwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, dang, dpre,
-                       slab, p2, sv, B, n, nullptr);
+                       slab, p2, sv, B, n, (int)wl_in_kernel<H, W>(n), qs, nullptr);
   }
   return (int)hipGetLastError();
 }
@@ -727,12 +781,13 @@ int launch_bwd(const float* x, const float* flat, Offs o, const float* angles, c
 
 using namespace qd::qsc2;
 
-// offs: [w1, b1, w2, b2, wl, bl, row_width] float offsets into the flat parameter buffer.
+// offs: [w1, b1, w2, b2, wl, bl, row_width, base, qw] float offsets into the flat parameter buffer
+// (slab rows cover [base, base + row_width)).
 // Saved for the backward: p1s (B, HW/4, 16) f32, c1 (B, HW/4) u32, c2 (B, F) u8 (see sample_forward).
 QD_API int qd_qsc2_fwd(const float* x, const float* flat, const int* offs, float* angles, float* p2, float* p1s,
                        uint32_t* c1, uint8_t* c2, int B, int n, int H, int W, int grid, void* stream) {
   if (n < 1 || n > 16 || B <= 0 || grid <= 0 || !p1s || !c1 || !c2) return (int)hipErrorInvalidValue;
-  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
   if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, sv, B, n, grid, s);
@@ -743,15 +798,23 @@ QD_API int qd_qsc2_fwd(const float* x, const float* flat, const int* offs, float
 // slab: (grid, offs[6]) floats, row layout = flat layout from offs[0] (wl columns left zero).
 // p2 / p1s / c1 / c2: what qd_qsc2_fwd saved for this batch.
 QD_API int qd_qsc2_bwd(const float* x, const float* flat, const int* offs, const float* angles, const float* dang,
-                       float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1, uint8_t* c2, int B, int n,
-                       int H, int W, int grid, void* stream) {
+                       float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1, uint8_t* c2,
+                       const float* qslab, int qrows, int qwidth, int B, int n, int H, int W, int grid, void* stream) {
   if (n < 1 || n > 16 || B <= 0 || grid <= 0 || !p2 || !p1s || !c1 || !c2) return (int)hipErrorInvalidValue;
-  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s);
-  if (H == 16 && W == 16) return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s);
+  QSlab qs{qslab, qrows, qwidth};
+  if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, p2, sv, qs, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, p2, sv, qs, B, n, grid, s);
   return (int)hipErrorInvalidValue;
+}
+
+// 1 if qd_qsc2_bwd also produces the linear-layer weight gradient (slab wl columns) for n qubits
+QD_API int qd_qsc2_wl_in_kernel(int H, int W, int n) {
+  if (H == 16 && W == 8) return wl_in_kernel<16, 8>(n) ? 1 : 0;
+  if (H == 16 && W == 16) return wl_in_kernel<16, 16>(n) ? 1 : 0;
+  return 0;
 }
 
 // waves (= samples in flight) per workgroup of the two kernels
@@ -767,7 +830,7 @@ QD_API int qd_qsc2_waves(int W, int backward) {
 QD_API int qd_qsc2_fwd_stamped(const float* x, const float* flat, const int* offs, float* angles, float* p2,
                                float* p1s, uint32_t* c1, uint8_t* c2, int B, int n, int H, int W, int grid,
                                unsigned long long* stamps, void* stream) {
-  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
   if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, sv, B, n, grid, s, stamps);
@@ -780,13 +843,15 @@ QD_API int qd_qsc2_fwd_stamped(const float* x, const float* flat, const int* off
 // [5] conv2 data grads [6] pool-1 backward [7] conv1 weight grads (first sample) [8] wave done.
 QD_API int qd_qsc2_bwd_stamped(const float* x, const float* flat, const int* offs, const float* angles,
                                const float* dang, float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1,
-                               uint8_t* c2, int B, int n, int H, int W, int grid, unsigned long long* stamps,
-                               void* stream) {
-  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6]};
+                               uint8_t* c2, const float* qslab, int qrows, int qwidth, int B, int n, int H, int W,
+                               int grid, unsigned long long* stamps, void* stream) {
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s, stamps);
+  QSlab qs{qslab, qrows, qwidth};
+  if (H == 16 && W == 8)
+    return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, p2, sv, qs, B, n, grid, s, stamps);
   if (H == 16 && W == 16)
-    return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, p2, sv, B, n, grid, s, stamps);
+    return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, p2, sv, qs, B, n, grid, s, stamps);
   return (int)hipErrorInvalidValue;
 }

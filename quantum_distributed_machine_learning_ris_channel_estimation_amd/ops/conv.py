@@ -16,6 +16,7 @@ from typing import List, Optional
 import torch
 
 from .. import _native as nat
+from .slabsum import SlabBatch
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 NST = 8
@@ -31,6 +32,9 @@ class ConvStackHIP:
     def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 8, spb_r: int = 4, spb_w1: int = 4,
                  dx_bf16: bool = True):
         self.m = model
+        self.count_batches = False   # set by the owner that stops counting num_batches_tracked itself
+        if not 1 <= U <= 8:
+            raise ValueError(f"ConvStackHIP: {U} BatchNorm groups per step (1..8 supported)")
         self.U, self.B, self.N, self.E = U, B, U * B, model.E
         self.H, self.W = model.H, model.W
         self.HW = self.H * self.W
@@ -68,11 +72,11 @@ class ConvStackHIP:
         self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
         self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p])
         self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
-        self._fin = nat.fn(L, "qd_bn_stats_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i, _p])
+        self._fin = nat.fn(L, "qd_bn_stats_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i, _p, _i,
+                                                          ctypes.c_longlong, _p])
         self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _i, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
-        self._ssum_multi = nat.fn(L, "qd_slab_rows_sum_multi", [_i, _p, _p, _p, _p, _p, _i, _p])
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
 
     def pack_weights(self, st) -> None:
@@ -96,9 +100,12 @@ class ConvStackHIP:
             nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
                                 nat.ptr(self.stats), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw,
                                 st), f"conv_fwd{k + 1}")
+            # the first finalisation also advances every BN layer's num_batches_tracked (training)
+            nbt = getattr(m, "_nbt", None) if (k == 0 and training and self.count_batches) else None
             nat.check(self._fin(nat.ptr(self.stats), nat.ptr(m.bn_w[k]), nat.ptr(m.bn_b[k]), nat.ptr(m.run_mean[k]),
                                 nat.ptr(m.run_var[k]), nat.ptr(self.st[k]), self.U, self.chunks, self.EC,
-                                float(self.B * self.HW), m.momentum, m.eps, int(training), st), f"bn_fin{k + 1}")
+                                float(self.B * self.HW), m.momentum, m.eps, int(training), _ptr(nbt),
+                                nbt.numel() if nbt is not None else 0, self.U, st), f"bn_fin{k + 1}")
             inp, st_prev = self.z[k], self.st[k]
         f8 = self.m.fp8_scales if self.fp8 else None
         nat.check(self._apply(nat.ptr(self.z[2]), nat.ptr(self.st[2]), nat.ptr(self.h3), self.N, self.EC, self.B,
@@ -107,7 +114,7 @@ class ConvStackHIP:
         return self.h3
 
     # --------------------------------------------------------------------- backward
-    def backward(self, dh3: torch.Tensor, accumulate: bool = True) -> None:
+    def backward(self, dh3: torch.Tensor, accumulate: bool = True, slabs: Optional["SlabBatch"] = None) -> None:
         """dh3: dL/dh3 as (N*E, 32*H*W) (bf16 or fp32).  Adds (accumulate) or writes the conv/BN grads
         into the flat grad -- writing makes a zero_grad before the step unnecessary."""
         m, st = self.m, nat.stream_ptr(dh3.device)
@@ -132,10 +139,12 @@ class ConvStackHIP:
                                       nat.ptr(dx), int(self.dx_bf16), self.N, self.E, self.B, self.H, self.W,
                                       self.chunks, self.spw, st), f"conv_dgrad{k + 1}")
                 dh, dh_bf = dx, int(self.dx_bf16)
-        # the three weight-gradient slabs -> conv_w grads in one launch
-        slabs = (ctypes.c_void_p * 4)(*[nat.ptr(w) for w in self.wslab])
-        outs = (ctypes.c_void_p * 4)(*[nat.ptr(m.conv_w[k].grad) for k in range(3)])
-        groups = (ctypes.c_int * 4)(*[self.E] * 3)
-        rows = (ctypes.c_int * 4)(*[w.shape[1] for w in self.wslab])
-        widths = (ctypes.c_int * 4)(*[w.shape[2] for w in self.wslab])
-        nat.check(self._ssum_multi(3, slabs, outs, groups, rows, widths, int(accumulate), st), "wslab_sum")
+        # the three weight-gradient slabs -> conv_w grads: queued on the caller's batch (one launch
+        # for every slab reduction of the step phase) or launched here
+        own = slabs is None
+        batch = SlabBatch() if own else slabs
+        for k in range(3):
+            w = self.wslab[k]
+            batch.add(w, m.conv_w[k].grad, self.E, w.shape[1], w.shape[2])
+        if own:
+            batch.launch(accumulate, st)

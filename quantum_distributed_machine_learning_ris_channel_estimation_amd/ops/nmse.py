@@ -135,6 +135,29 @@ class StreamNMSE:
             dY.copy_(self.coef[self._rs_long][:, None] * (Y.float() - self._labels(label)))
         return dY
 
+    def grad_bias(self, Y: torch.Tensor, label: torch.Tensor, bias_grad: torch.Tensor, out_dtype=torch.float32,
+                  chunks: int = 128) -> torch.Tensor:
+        """dY (as ``grad``) and, fused into the same pass, the FC bias gradient sum_rows dY written
+        (overwritten) into ``bias_grad``: per-row-chunk column sums + one deterministic slab reduce."""
+        dY = torch.empty(self.rows, self.cols, device=Y.device, dtype=out_dtype)
+        if not Y.is_cuda:
+            dY.copy_(self.coef[self._rs_long][:, None] * (Y.float() - self._labels(label)))
+            bias_grad.copy_(dY.float().sum(0))
+            return dY
+        if getattr(self, "_colsum", None) is None or self._colsum.shape[0] != chunks:
+            self._colsum = torch.empty(chunks, self.cols, device=Y.device)
+        lib = nat.hip_lib()
+        self._check_labels(label)
+        f = nat.fn(lib, "qd_nmse_grad_bias", [_p, _i, _p, _p, _p, _p, _p, _i, _p, _i, _i, _i, _p])
+        st = nat.stream_ptr(Y.device)
+        nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label), nat.ptr(self.coef),
+                    nat.ptr(self.row_stream), nat.ptr(self.rowoff) if self.rowoff is not None else None,
+                    nat.ptr(dY), int(dY.dtype == torch.bfloat16), nat.ptr(self._colsum), chunks, self.rows,
+                    self.cols, st), "nmse_grad_bias")
+        ssum = nat.fn(lib, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _i, _p])
+        nat.check(ssum(nat.ptr(self._colsum), nat.ptr(bias_grad), 1, chunks, self.cols, 0, st), "bias_grad_sum")
+        return dY
+
     def __call__(self, Y, label, perf=None, out_dtype=torch.float32) -> Tuple[torch.Tensor, torch.Tensor]:
         self.sums(Y, label, perf)
         self.finalize()

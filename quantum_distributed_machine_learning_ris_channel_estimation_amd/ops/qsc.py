@@ -24,6 +24,7 @@ from typing import Optional
 import torch
 
 from .. import _native as nat
+from .slabsum import SlabBatch
 from ..ops.optim import FlatParamSpace
 from ..ops.quantum import HIP_REG_MAX_QUBITS
 
@@ -47,11 +48,15 @@ class QSCStepHIP:
         names = dict(zip(space.names, space.offsets))
         o = [names["preprocess.0.weight"], names["preprocess.0.bias"], names["preprocess.3.weight"],
              names["preprocess.3.bias"], names["preprocess.7.weight"], names["preprocess.7.bias"]]
-        row = o[5] + self.n - o[0]
+        # slab row = flat columns [base, base + row): the preprocess grads (+ for the MFMA backward, which
+        # also reduces the quantum layer's adjoint slab, the quantum weights in front of them)
+        qoff = names["qlayer.weights"]
+        base = min(o[0], qoff) if impl == "mfma" else o[0]
+        row = o[5] + self.n - base
         row += (-row) % 4   # float4 slab sums; the tail lands in the flat space's alignment padding (zeros)
-        assert o[0] + row <= space.numel
-        self.offs = (ctypes.c_int * 7)(*(o + [row]))
-        self.row0, self.row = o[0], row
+        assert base + row <= space.numel and (impl != "mfma" or qoff + 2 * self.n * self.L <= base + row)
+        self.offs = (ctypes.c_int * 9)(*(o + [row, base, qoff]))
+        self.row0, self.row = base, row
         feat = pre[7].weight.shape[1]
         self.Hh, self.Ww = (16, 8) if feat == 256 else (16, 16)
         self.impl = impl
@@ -70,6 +75,9 @@ class QSCStepHIP:
             self.dpre = torch.empty(batch_total, self.n, **f32)
             self.gwl = space.grad[names["preprocess.7.weight"]:names["preprocess.7.weight"] + self.n * feat].view(
                 self.n, feat)
+            # the backward kernel also reduces dWl = dpre^T p2 into its slab when it fits; else a GEMM
+            self.wl_in_kernel = bool(nat.fn(nat.hip_lib(), "qd_qsc2_wl_in_kernel", [_i, _i, _i])(
+                self.Hh, self.Ww, self.n))
         else:
             self.grid_fwd = min(grid_fwd, batch_total)
             self.grid_bwd = min(grid_bwd, batch_total)
@@ -93,7 +101,8 @@ class QSCStepHIP:
         self._pre_fwd = nat.fn(L, "qd_qsc_pre_fwd", [_p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._pre_bwd = nat.fn(L, "qd_qsc_pre_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._fwd2 = nat.fn(L, "qd_qsc2_fwd", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
-        self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+        self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i,
+                                                   _i, _p])
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
             self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
@@ -125,11 +134,14 @@ class QSCStepHIP:
         return nat.ptr(self.p1s), nat.ptr(self.c1), nat.ptr(self.c2)
 
     def __call__(self, x: torch.Tensor, labels: torch.Tensor, loss_acc: Optional[torch.Tensor] = None,
-                 skip: Optional[torch.Tensor] = None, skip_add: bool = False, accumulate: bool = True) -> torch.Tensor:
+                 skip: Optional[torch.Tensor] = None, skip_add: bool = False, accumulate: bool = True,
+                 slabs: Optional[SlabBatch] = None) -> torch.Tensor:
         """x (B, 2, H, W) fp32 contiguous, labels (B,) int64.  Returns loss (1,).
         ``skip`` (fp32 (1,)): set (or, with skip_add, incremented) to 1 if the loss is not finite.
         ``accumulate``: add into the grads (default) or write them (every grad of the model has exactly
-        one producer per step, so a zero_grad before the step becomes unnecessary)."""
+        one producer per step, so a zero_grad before the step becomes unnecessary).
+        ``slabs``: queue the gradient-slab reductions on this batch (the caller launches it with the
+        same ``accumulate``) instead of launching them here."""
         m, sp = self.m, self.space
         B, n, L = self.B, self.n, self.L
         assert x.shape[0] == B and x.is_contiguous() and labels.dtype == torch.int64
@@ -154,21 +166,24 @@ class QSCStepHIP:
                              st), "qsc_head")
         nat.check(self._qb(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.dE), nat.ptr(self.dang),
                            nat.ptr(self.qslab), B, n, L, wgroup, *extra, st), "qsim_bwd")
-        nat.check(self._rs(nat.ptr(self.qslab), nat.ptr(m.qlayer.weights.grad), self.qrows, 2 * n * L,
-                           1.0 if accumulate else 0.0, st),
-                  "reduce_slab")
+        own = SlabBatch()
+        if self.impl != "mfma":   # (the MFMA preprocess backward folds this reduction into its own slab)
+            (slabs if slabs is not None else own).add(self.qslab, m.qlayer.weights.grad, 1, self.qrows, 2 * n * L)
         if self.impl == "mfma":
             nat.check(self._bwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang),
-                                 nat.ptr(self.dpre), nat.ptr(self.preslab), nat.ptr(self.p2), *self._saved(), B, n,
-                                 self.Hh, self.Ww, self.grid_bwd, st), "qsc2_bwd")
+                                 nat.ptr(self.dpre), nat.ptr(self.preslab), nat.ptr(self.p2), *self._saved(),
+                                 nat.ptr(self.qslab), self.qrows, 2 * n * L, B, n, self.Hh, self.Ww, self.grid_bwd, st),
+                      "qsc2_bwd")
         else:
             nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B,
                                     n, self.Hh, self.Ww, self.grid_bwd, st), "qsc_pre_bwd")
-        nat.check(self._ssum(nat.ptr(self.preslab), nat.ptr(sp.grad[self.row0:]), 1, self.grid_bwd, self.row,
-                             int(accumulate), st),
-                  "qsc_slab_sum")
-        if self.impl == "mfma":
-            # linear weight grad over the batch (one GEMM); the slab row left these columns 0 / untouched
+        # (the linear-weight GEMM below overwrites columns of this slab's output: keep it in order)
+        gemm_wl = self.impl == "mfma" and not self.wl_in_kernel
+        (slabs if slabs is not None and not gemm_wl else own).add(self.preslab, sp.grad[self.row0:], 1,
+                                                                   self.grid_bwd, self.row)
+        own.launch(accumulate, st)
+        if gemm_wl:
+            # linear weight grad over the batch (one GEMM); the slab row left these columns 0
             if accumulate:
                 self.gwl.addmm_(self.dpre.t(), self.p2)
             else:

@@ -1,0 +1,47 @@
+"""Batched deterministic gradient-slab reductions (csrc/hip/conv.hip ``qd_slab_rows_sum_multi``).
+
+Several fused backward kernels (conv weight gradients, the quantum layer's adjoint pass, the QSC
+preprocess backward) write per-workgroup partial rows ("slabs") instead of using float atomics;
+each slab is summed over its rows into the flat gradient buffer.  Every such reduction of a step
+phase is independent, so ``SlabBatch`` collects them and issues ONE launch (up to 8 jobs) -- on
+this GPU a dependent launch costs ~5 us however little it computes.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Tuple
+
+import torch
+
+from .. import _native as nat
+
+_p, _i = ctypes.c_void_p, ctypes.c_int
+MAX_JOBS = 8
+
+
+class SlabBatch:
+    def __init__(self):
+        self.jobs: List[Tuple[torch.Tensor, torch.Tensor, int, int, int]] = []
+        self._f = None
+
+    def add(self, slab: torch.Tensor, out: torch.Tensor, groups: int, rows: int, width: int) -> None:
+        """out[g, :width] (+)= sum_r slab[g, r, :width] for g < groups (both contiguous fp32)."""
+        assert slab.dtype == torch.float32 and out.dtype == torch.float32
+        assert slab.numel() >= groups * rows * width and out.numel() >= groups * width
+        if len(self.jobs) == MAX_JOBS:
+            raise RuntimeError("SlabBatch: more than 8 reductions in one launch")
+        self.jobs.append((slab, out, groups, rows, width))
+
+    def launch(self, accumulate: bool, stream) -> None:
+        if not self.jobs:
+            return
+        if self._f is None:
+            self._f = nat.fn(nat.hip_lib(), "qd_slab_rows_sum_multi", [_i, _p, _p, _p, _p, _p, _i, _p])
+        n = len(self.jobs)
+        slabs = (ctypes.c_void_p * n)(*[nat.ptr(j[0]) for j in self.jobs])
+        outs = (ctypes.c_void_p * n)(*[nat.ptr(j[1]) for j in self.jobs])
+        groups = (ctypes.c_int * n)(*[j[2] for j in self.jobs])
+        rows = (ctypes.c_int * n)(*[j[3] for j in self.jobs])
+        widths = (ctypes.c_int * n)(*[j[4] for j in self.jobs])
+        nat.check(self._f(n, slabs, outs, groups, rows, widths, int(accumulate), stream), "slab_rows_sum_multi")
+        self.jobs = []

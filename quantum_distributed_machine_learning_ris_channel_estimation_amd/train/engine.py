@@ -267,6 +267,7 @@ class HDCEStep:
         if self.hip:
             from ..ops.conv import ConvStackHIP
             self.conv = ConvStackHIP(model, n_users, batch)
+            self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
 
     def __call__(self, Yp: torch.Tensor, HL: torch.Tensor, HP: torch.Tensor) -> torch.Tensor:
@@ -306,13 +307,16 @@ class HDCEStep:
         return loss
 
     # Phase 2: conv/BN backward from dA.
-    def backward_conv(self) -> None:
+    def backward_conv(self, slabs=None) -> None:
+        """``slabs``: queue the conv weight-gradient reductions on this ``SlabBatch`` (HIP path; the
+        caller launches it in overwrite mode)."""
         if self.hip:
-            self.conv.backward(self._dA, accumulate=False)
+            self.conv.backward(self._dA, accumulate=False, slabs=slabs)
         else:
             torch.autograd.backward(self._A, self._dA)
             self._A = None
-        self.m.count_batches(self.U)
+        if not (self.hip and self.conv.count_batches):   # the HIP forward counted them in-kernel
+            self.m.count_batches(self.U)
 
     @torch.no_grad()
     def _forward_fc_hip(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
@@ -332,9 +336,8 @@ class HDCEStep:
         else:
             Y = torch.nn.functional.linear(A.to(dt), W, b)
         loss = self.nmse.sums_finalize(Y, label, perf)
-        dY = self.nmse.grad(Y, label, out_dtype=dt)
+        dY = self.nmse.grad_bias(Y, label, m.fc_b.grad, out_dtype=dt)   # + bias grad, same pass
         _mm_f32(dY.t(), A.to(dt), m.fc_w.grad)               # dW = dY^T A   (fp32 out)
-        torch.sum(dY, dim=0, dtype=torch.float32, out=m.fc_b.grad)
         self._dA = torch.mm(dY, W)                             # (rows, 4096) bf16
         return loss
 
@@ -400,10 +403,12 @@ class ClassifierStep:
             return F.log_softmax(m.classifier(xq), dim=1)
         return m(x)
 
-    def __call__(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, labels: torch.Tensor, slabs=None) -> torch.Tensor:
+        """``slabs`` (HIP path): queue the gradient-slab reductions on this ``SlabBatch`` (launched by
+        the caller, with accumulate = not writes_grads)."""
         if self.hip is not None and x.shape[0] == self.hip.B:
             loss = self.hip(x.contiguous(), labels, skip=self.skip, skip_add=self.skip_add,
-                            accumulate=not self.writes_grads)
+                            accumulate=not self.writes_grads, slabs=slabs)
             if self.grad_hook:
                 self.grad_hook("all")
             return loss

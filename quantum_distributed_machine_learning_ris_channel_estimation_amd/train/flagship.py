@@ -20,10 +20,12 @@ from typing import Optional
 
 import torch
 
+from .. import _native as nat
 from ..data.datasets import DMLStore, make_dml_stores
 from ..models.estimators import QSC_P128
 from ..ops.gather import StepGather
 from ..ops.optim import FlatParamSpace, make_optimizer
+from ..ops.slabsum import SlabBatch
 from ..parallel.dp import DistContext, GradBuckets
 from ..utils.profiling import GraphedStep
 from .engine import ClassifierStep, HDCEModel, HDCEStep
@@ -90,6 +92,7 @@ class FlagshipTrainer:
         self.hloss = self.hstep.nmse.loss
         self.qloss = self.cstep.hip.loss if self.cstep.hip is not None else torch.zeros(1, device=dev)
         self.labels = self.store.scen.repeat_interleave(self.B)
+        self.slabs = SlabBatch()
         graphs = cfg.hip_graphs and dev.type == "cuda"
         if ctx.world == 1 and not cfg.split_graphs:
             # one graph: gather, both forwards, NMSE, both backwards, both optimizers
@@ -113,8 +116,14 @@ class FlagshipTrainer:
             self.hloss.copy_(loss)
 
     def _phase2(self) -> None:
-        self.hstep.backward_conv()
-        q = self.cstep(self.gat.xq, self.labels)
+        # every gradient-slab reduction of the phase (3 conv weight slabs, the quantum layer's and the
+        # QSC preprocess slab) goes out as ONE launch when both steps write (overwrite) their grads
+        share = self.hstep.hip and self.cstep.hip is not None and self.cstep.writes_grads and self.hstep.writes_grads
+        slabs = self.slabs if share else None
+        self.hstep.backward_conv(slabs=slabs)
+        q = self.cstep(self.gat.xq, self.labels, slabs=slabs)
+        if slabs is not None:
+            slabs.launch(accumulate=False, stream=nat.stream_ptr(self.ctx.device))
         if q is not self.qloss:
             self.qloss.copy_(q)
 

@@ -53,9 +53,10 @@ def main():
     wb = nat.fn(lib, "qd_qsc2_waves", [ctypes.c_int, ctypes.c_int])(8, 1)
     gb = step.grid_bwd
     sb = torch.zeros(gb * wb * 12, dtype=torch.int64, device=dev)
-    fb = nat.fn(lib, "qd_qsc2_bwd_stamped", [ctypes.c_void_p] * 11 + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2)
+    fb = nat.fn(lib, "qd_qsc2_bwd_stamped", [ctypes.c_void_p] * 12 + [ctypes.c_int] * 7 + [ctypes.c_void_p] * 2)
     nat.check(fb(nat.ptr(x), nat.ptr(sp.flat), step.offs, nat.ptr(step.angles), nat.ptr(step.dang), nat.ptr(step.dpre),
-                 nat.ptr(step.preslab), nat.ptr(step.p2), *step._saved(), B, n, 16, 8, gb, nat.ptr(sb),
+                 nat.ptr(step.preslab), nat.ptr(step.p2), *step._saved(), nat.ptr(step.qslab), step.qrows,
+                 2 * n * step.L, B, n, 16, 8, gb, nat.ptr(sb),
                  nat.stream_ptr(dev)), "bwd stamped")
     torch.cuda.synchronize()
     tb = sb.view(gb * wb, 12).cpu().double()

@@ -162,3 +162,20 @@ def test_hdce_fp8_estimator_step(cuda):
     # so compare the relative shape via the quantisation error of a fresh forward)
     A = s8.conv.h3.float()
     assert float(A.max()) > 0 and float(sc.scale[0]) > 0
+
+
+def test_hdce_step_counts_batches_and_running_stats(cuda):
+    """The in-kernel BN bookkeeping (num_batches_tracked, running stats) matches the autograd step."""
+    U, B = 3, 64
+    a, b = pair(cuda)
+    Yp = torch.randn(3, U, B, 2, 16, 8, device=cuda)
+    HL = torch.randn(3, U, B, 2048, device=cuda)
+    sa, sb = HDCEStep(a, U, B, hip=True), HDCEStep(b, U, B, hip=False)
+    for _ in range(2):
+        sa(Yp, HL, HL)
+        sb(Yp, HL, HL)
+    torch.cuda.synchronize()
+    assert torch.equal(a._nbt, b._nbt) and int(a._nbt[0]) == 2 * U
+    for k in range(3):
+        assert torch.allclose(a.run_mean[k], b.run_mean[k], rtol=2e-2, atol=2e-3)
+        assert torch.allclose(a.run_var[k], b.run_var[k], rtol=5e-2, atol=2e-3)

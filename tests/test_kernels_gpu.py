@@ -134,6 +134,15 @@ def test_stream_nmse_hip_vs_cpu(cuda, dt):
     Yn[3, 7] = float("nan")
     gpu2.sums_finalize(Yn.to(cuda).to(dt), Lb.to(cuda), Pf.to(cuda))
     assert float(gpu2.skip.item()) == 1.0
+    # gradient + fused FC bias gradient (column sums of dY) == the separate passes
+    gpu3 = StreamNMSE(rs.to(cuda), S)
+    gpu3.sums_finalize(Y.to(cuda).to(dt), Lb.to(cuda), Pf.to(cuda))
+    bg = torch.full((C,), 7.0, device=cuda)   # overwritten
+    dY3 = gpu3.grad_bias(Y.to(cuda).to(dt), Lb.to(cuda), bg, out_dtype=torch.bfloat16)
+    dY1 = gpu3.grad(Y.to(cuda).to(dt), Lb.to(cuda), out_dtype=torch.bfloat16)
+    assert torch.equal(dY3, dY1)
+    ref_b = (gpu3.coef[gpu3._rs_long][:, None] * (Y.to(cuda).to(dt).float() - Lb.to(cuda))).sum(0)
+    assert torch.allclose(bg, ref_b, rtol=1e-4, atol=1e-7)
 
 
 @pytest.mark.parametrize("kind", ["adam", "adamw", "sgd"])
@@ -218,3 +227,22 @@ def test_fused_optimizer_tick_and_shadow(cuda):
     torch.cuda.synchronize()
     assert float(opt.step_t.item()) == 5.0 and int(opt.done.item()) == 0
     assert torch.equal(sh, sp.flat[:2_000_000].to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_slab_batch_multi_reduction(cuda, accumulate):
+    """One launch reducing several slabs (vector and scalar-width jobs) == torch sums."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.slabsum import SlabBatch
+    torch.manual_seed(3)
+    shapes = [(3, 48, 576), (1, 256, 48), (1, 37, 30), (2, 5, 9218)]   # (groups, rows, width)
+    slabs = [torch.randn(g, r, w, device=cuda) for g, r, w in shapes]
+    outs = [torch.randn(g, w, device=cuda) for g, _, w in shapes]
+    refs = [s.sum(1) + (o if accumulate else 0) for s, o in zip(slabs, outs)]
+    b = SlabBatch()
+    for s, o, (g, r, w) in zip(slabs, outs, shapes):
+        b.add(s, o, g, r, w)
+    b.launch(accumulate, nat.stream_ptr(cuda))
+    torch.cuda.synchronize()
+    for o, ref in zip(outs, refs):
+        assert torch.allclose(o, ref, rtol=1e-5, atol=1e-4)
