@@ -102,6 +102,92 @@ __device__ __forceinline__ void unpack_q(const uint4 q, float* v, const uint16_t
 }
 
 // ------------------------------------------------------------------------------------------
+// BatchNorm finalisation inside the consumer kernels.  A consumer workgroup of (group u, expert e)
+// rebuilds the 32-channel BN records it needs straight from the producer's per-chunk partials
+// (every workgroup gets bitwise-identical values: same order), so no separate finalisation launch
+// sits between producer and consumer.  One designated workgroup per expert also does the
+// once-per-step side effects (running statistics / dgamma, dbeta); chunk-0 workgroups publish the
+// record for later kernels.  256 threads: channel c = tid / 8, part j = tid % 8.
+// ------------------------------------------------------------------------------------------
+struct BnFwd {            // forward: (mean, invstd, a, b) from conv statistics partials
+  const float* stats;     // (U, chunks, 2, EC) sum / sum of squares; null: use the st record as is
+  const float* gamma;
+  const float* beta;
+  float* run_mean;
+  float* run_var;
+  float* st_out;          // (U, EC, NST) record published by chunk-0 workgroups
+  int chunks;
+  float count, momentum, eps;
+  int training;
+};
+struct BnBwd {            // backward: (c1, c2, c3) from the BN backward reduction partials
+  const float* rslab;     // (U, chunks, 2, EC) sum g / sum g*xhat; null: use the st record as is
+  const float* gamma;
+  int chunks;
+  float count;
+};
+
+// sums of the two planar partial rows of channel ch over the chunks of group u (8 lanes per
+// channel; up to 64 chunks with every load in flight at once)
+__device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, int u, int chunks, int EC, int ch,
+                                               int j) {
+  float a = 0.f, b = 0.f;
+  const float* p = part + (size_t)u * chunks * 2 * EC + ch;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int k = j + 8 * i;
+    if (k < chunks) {
+      a += p[(size_t)k * 2 * EC];
+      b += p[(size_t)k * 2 * EC + EC];
+    }
+  }
+  for (int k = j + 64; k < chunks; k += 8) {
+    a += p[(size_t)k * 2 * EC];
+    b += p[(size_t)k * 2 * EC + EC];
+  }
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    a += __shfl_xor(a, m);
+    b += __shfl_xor(b, m);
+  }
+  return make_float2(a, b);
+}
+
+// rec[c * NST + ST_MEAN .. ST_B] for the 32 channels of (u, e); publish: also write the record to
+// bn.st_out.  (The running statistics advance once per step in the BN tail launch.)
+__device__ void bn_fwd_build(const BnFwd& bn, float* rec, int u, int e, int EC, bool publish) {
+  const int tid = threadIdx.x, c = tid >> 3, j = tid & 7, ch = e * CO + c;
+  float mean, var;
+  if (bn.training) {
+    const float2 sm = bn_part_sums(bn.stats, u, bn.chunks, EC, ch, j);
+    mean = sm.x / bn.count;
+    var = fmaxf(sm.y / bn.count - mean * mean, 0.f);
+  } else {
+    mean = bn.run_mean[ch];
+    var = bn.run_var[ch];
+  }
+  if (j == 0) {
+    const float g = bn.gamma[ch], inv = rsqrtf(var + bn.eps);
+    const float4 r = make_float4(mean, inv, g * inv, bn.beta[ch] - mean * g * inv);
+    *reinterpret_cast<float4*>(rec + c * NST) = r;
+    if (publish) *reinterpret_cast<float4*>(bn.st_out + ((size_t)u * EC + ch) * NST) = r;
+  }
+}
+
+// rec[c * NST + ...] = the published forward record of (u, e) with c1..c3 of the backward filled
+// in.  (dgamma / dbeta: column sums of the same partials, in the step's batched slab reduction.)
+__device__ void bn_bwd_build(const BnBwd& bn, const float* __restrict__ st, float* rec, int u, int e, int EC) {
+  const int tid = threadIdx.x, c = tid >> 3, j = tid & 7, ch = e * CO + c;
+  const float2 sg = bn_part_sums(bn.rslab, u, bn.chunks, EC, ch, j);
+  if (j == 0) {
+    const float4 f = *reinterpret_cast<const float4*>(st + ((size_t)u * EC + ch) * NST);
+    const float c1 = bn.gamma[ch] * f.y;
+    *reinterpret_cast<float4*>(rec + c * NST) = f;
+    *reinterpret_cast<float4*>(rec + c * NST + 4) = make_float4(c1, c1 * sg.x / bn.count, c1 * sg.y / bn.count, 0.f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // conv3x3_kernel: forward (and data-gradient) implicit GEMM
 // grid: (U * chunks, E); block 256 (4 waves); each wave owns `spw` consecutive samples.
 // CIN: input channels of THIS pass (layer-1 fwd: 2; else 32).
@@ -112,7 +198,7 @@ template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN, bo
 __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
                                                       const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
                                                       void* __restrict__ out, float* __restrict__ stats, int E, int B,
-                                                      int chunks, int spw,
+                                                      int chunks, int spw, BnFwd bnf, BnBwd bnb,
                                                       unsigned long long* __restrict__ stamps = nullptr) {
   // STAMP (diagnostic builds): per wave [0] start [1] weights + BN params staged [2] first sample
   // staged [3] first sample's MFMAs + epilogue [4] all samples [5] end
@@ -217,13 +303,21 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
       if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) tw[k] = wp[tid + 256 * k];
     [[maybe_unused]] float tp = 0.f;
     static_assert(CIN * NST <= 256, "one BN parameter per thread");
+    // BN records of the input channels: rebuilt from the producer's partials (fused finalisation)
+    // or read from the published record
+    const bool build = (INM == IN_BNRELU && bnf.stats) || (INM == IN_BNBWD && bnb.rslab);
     if constexpr (!RAWIN)
-      if (tid < CIN * NST) tp = st_in[((size_t)u * EC_in + e * CIN) * NST + tid];
+      if (!build && tid < CIN * NST) tp = st_in[((size_t)u * EC_in + e * CIN) * NST + tid];
 #pragma unroll
     for (int k = 0; k < WPT; ++k)
       if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) wl[tid + 256 * k] = tw[k];
+    if constexpr (INM == IN_BNRELU) {
+      if (build) bn_fwd_build(bnf, stl, u, e, EC_in, chunk == 0);
+    } else if constexpr (INM == IN_BNBWD) {
+      if (build) bn_bwd_build(bnb, st_in, stl, u, e, EC_in);
+    }
     if constexpr (!RAWIN)
-      if (tid < CIN * NST) stl[tid] = tp;
+      if (!build && tid < CIN * NST) stl[tid] = tp;
   }
   __syncthreads();
   if constexpr (STAMP) ts[1] = phase_stamp();
@@ -351,7 +445,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
-      stats[(((size_t)u * chunks + chunk) * E * CO + e * CO + c) * 2 + k] = t;
+      stats[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;   // planar [2][EC] rows
     }
   }
   if constexpr (STAMP) {
@@ -415,7 +509,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
                                                             const TDH* __restrict__ dh,
                                                             const uint16_t* __restrict__ z,
                                                             const float* __restrict__ st, float* __restrict__ slab,
-                                                            int E, int B, int chunks, int spb) {
+                                                            int E, int B, int chunks, int spb, BnBwd bnb) {
   using G = Geo<H, W>;
   constexpr int MTW = (9 * CIN + 31) / 32;        // accumulator tiles (9 for CIN=32, 1 for CIN=2)
   constexpr int XCS = G::HP * W + 8;              // channel stride of the shifted copies (bf16)
@@ -449,7 +543,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
     const float* sp = st_prev + ((size_t)u * E * CIN + e * CIN) * NST;
     for (int i = tid; i < CIN * NST; i += 256) prm[i] = sp[i];
   }
-  {
+  if (bnb.rslab) {   // fused BN backward finalisation
+    bn_bwd_build(bnb, st, prm + CIN * NST, u, e, E * CO);
+  } else {
     const float* sp = st + ((size_t)u * E * CO + e * CO) * NST;
     for (int i = tid; i < CO * NST; i += 256) prm[CIN * NST + i] = sp[i];
   }
@@ -588,16 +684,30 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
 // Forward statistics: per (u, ch) mean/invstd/(a,b); running stats updated in u order.
 // One 64-lane block per channel: lanes sum the chunk partials, lane 0 finishes.
 constexpr int kMaxGroups = 8;   // statistics groups (users) per finalisation launch
-__global__ void __launch_bounds__(64) bn_stats_finalize_kernel(const float* __restrict__ stats,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ beta, float* __restrict__ run_mean,
-                                                               float* __restrict__ run_var, float* __restrict__ st, int U,
-                                                               int chunks, int EC, float count, float momentum, float eps,
-                                                               int training, long long* __restrict__ nbt, int n_nbt,
+// up to 3 BN layers per launch (blockIdx.y): the step's one BN tail launch advances every layer's
+// running statistics (layers 1/2 had their records built by their consumers) and publishes the last
+// layer's records
+struct FinJobs {
+  const float* stats[3];
+  const float* gamma[3];
+  const float* beta[3];
+  float* run_mean[3];
+  float* run_var[3];
+  float* st[3];
+};
+__global__ void __launch_bounds__(64) bn_stats_finalize_kernel(FinJobs jobs, int U, int chunks, int EC, float count,
+                                                               float momentum, float eps, int training,
+                                                               long long* __restrict__ nbt, int n_nbt,
                                                                long long nbt_inc) {
   // every global load is issued up front (the per-group loop paid one round trip per group)
-  const int ch = blockIdx.x, lane = threadIdx.x;
-  if (nbt && ch == 0 && lane < n_nbt) nbt[lane] += nbt_inc;   // BatchNorm num_batches_tracked
+  const int ch = blockIdx.x, lane = threadIdx.x, l = blockIdx.y;
+  const float* __restrict__ stats = jobs.stats[l];
+  const float* __restrict__ gamma = jobs.gamma[l];
+  const float* __restrict__ beta = jobs.beta[l];
+  float* __restrict__ run_mean = jobs.run_mean[l];
+  float* __restrict__ run_var = jobs.run_var[l];
+  float* __restrict__ st = jobs.st[l];
+  if (nbt && ch == 0 && l == 0 && lane < n_nbt) nbt[lane] += nbt_inc;   // BatchNorm num_batches_tracked
   const float g = gamma[ch], bt = beta[ch];
   float rm = run_mean[ch], rv = run_var[ch];
   float a[kMaxGroups], b[kMaxGroups];
@@ -607,8 +717,8 @@ __global__ void __launch_bounds__(64) bn_stats_finalize_kernel(const float* __re
     b[u] = 0.f;
     if (training && u < U) {
       for (int k = lane; k < chunks; k += 64) {
-        a[u] += stats[(((size_t)u * chunks + k) * EC + ch) * 2];
-        b[u] += stats[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
+        a[u] += stats[((size_t)u * chunks + k) * 2 * EC + ch];
+        b[u] += stats[((size_t)u * chunks + k) * 2 * EC + EC + ch];
       }
     }
   }
@@ -693,11 +803,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restric
     sgx1 += __shfl_xor(sgx1, m);
   }
   if (gl == 0) {
-    float* o = slab + (((size_t)u * chunks + chunk) * EC + e * CO + grp) * 2;
+    float* o = slab + ((size_t)u * chunks + chunk) * 2 * EC + e * CO + grp;   // planar [2][EC] rows
     o[0] = sg0;
-    o[1] = sgx0;
-    o[32] = sg1;   // channel grp + 16
-    o[33] = sgx1;
+    o[EC] = sgx0;
+    o[16] = sg1;   // channel grp + 16
+    o[EC + 16] = sgx1;
   }
 }
 
@@ -718,8 +828,8 @@ __global__ void __launch_bounds__(64) bn_bwd_finalize_kernel(const float* __rest
     if (u < U) {
       inv[u] = st[((size_t)u * EC + ch) * NST + ST_INV];
       for (int k = lane; k < chunks; k += 64) {
-        sg[u] += slab[(((size_t)u * chunks + k) * EC + ch) * 2];
-        sgx[u] += slab[(((size_t)u * chunks + k) * EC + ch) * 2 + 1];
+        sg[u] += slab[((size_t)u * chunks + k) * 2 * EC + ch];
+        sgx[u] += slab[((size_t)u * chunks + k) * 2 * EC + EC + ch];
       }
     }
   }
@@ -806,34 +916,35 @@ __global__ void __launch_bounds__(256) slab_rows_sum_kernel(const float* __restr
 
 // Vector variant (width % 4 == 0, 16-byte aligned rows): 16 column quads x 16 row phases per
 // block, float4 loads, unrolled so each thread keeps several independent loads in flight.
+// ld: row stride of the slab in floats (>= width; a group spans rows * ld floats).
 __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
-                                                    int width, int g, int bx, int accumulate);
+                                                    int width, int ld, int g, int bx, int accumulate);
 __global__ void __launch_bounds__(256) slab_rows_sum4_kernel(const float* __restrict__ slab, float* __restrict__ out,
                                                              int groups, int rows, int width, int accumulate) {
-  slab_rows_sum4_body(slab, out, rows, width, blockIdx.y, blockIdx.x, accumulate);
+  slab_rows_sum4_body(slab, out, rows, width, width, blockIdx.y, blockIdx.x, accumulate);
 }
 
 // Several independent slab sums in one launch (blockIdx.z = job): every gradient-slab reduction of
 // a step phase (conv weight slabs, quantum-layer slab, QSC preprocess slab) at once.  Jobs whose
 // width is not a multiple of 4 (or whose buffers are not 16-byte aligned) take a scalar path.
-constexpr int kSlabJobs = 8;
+constexpr int kSlabJobs = 16;
 struct SlabJobs {
   const float* slab[kSlabJobs];
   float* out[kSlabJobs];
-  int groups[kSlabJobs], rows[kSlabJobs], width[kSlabJobs], vec[kSlabJobs];
+  int groups[kSlabJobs], rows[kSlabJobs], width[kSlabJobs], ld[kSlabJobs], vec[kSlabJobs];
   int accumulate;
 };
 __device__ __forceinline__ void slab_rows_sum1_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
-                                                    int width, int g, int bx, int accumulate) {
+                                                    int width, int ld, int g, int bx, int accumulate) {
   __shared__ float red1[16][64];
   const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
   float t[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* s = slab + (size_t)g * rows * width;
+  const float* s = slab + (size_t)g * rows * ld;
   for (int r = ty; r < rows; r += 16) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = bx * 64 + q * 16 + tq;
-      if (i < width) t[q] += s[(size_t)r * width + i];
+      if (i < width) t[q] += s[(size_t)r * ld + i];
     }
   }
 #pragma unroll
@@ -851,22 +962,24 @@ __global__ void __launch_bounds__(256) slab_rows_sum4_multi_kernel(SlabJobs jobs
   const int j = blockIdx.z;
   if (blockIdx.y >= jobs.groups[j] || blockIdx.x * 64 >= jobs.width[j]) return;
   if (jobs.vec[j])
-    slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x, jobs.accumulate);
+    slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], jobs.ld[j], blockIdx.y, blockIdx.x,
+                        jobs.accumulate);
   else
-    slab_rows_sum1_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], blockIdx.y, blockIdx.x, jobs.accumulate);
+    slab_rows_sum1_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], jobs.ld[j], blockIdx.y, blockIdx.x,
+                        jobs.accumulate);
 }
 
 __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
-                                                    int width, int g, int bx, int accumulate) {
+                                                    int width, int ld, int g, int bx, int accumulate) {
   __shared__ float4 red[16][16];
   const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int i = (bx * 16 + tq) * 4;
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < width) {
-    const float* s = slab + (size_t)g * rows * width + i;
+    const float* s = slab + (size_t)g * rows * ld + i;
 #pragma unroll 4
     for (int r = ty; r < rows; r += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(s + (size_t)r * width);
+      const float4 v = *reinterpret_cast<const float4*>(s + (size_t)r * ld);
       t.x += v.x;
       t.y += v.y;
       t.z += v.z;
@@ -940,34 +1053,43 @@ QD_API int qd_conv_pack_weights_multi(int n, const float* const* w, uint16_t* co
 }
 
 // w: packed B fragments from qd_conv_pack_weights(dgrad=0)
+// bnf (nullable, layers 2/3): build the input BN records from the previous layer's statistics
+// partials in-kernel (fused finalisation; st_prev is then ignored) -- see BnFwd.
 QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const uint16_t* w, uint16_t* z, float* stats,
-                       int N, int E, int B, int H, int W, int chunks, int spw, void* stream) {
+                       int N, int E, int B, int H, int W, int chunks, int spw, const BnFwd* bnf, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  const BnFwd bf = bnf ? *bnf : BnFwd{};
+  const BnBwd bb{};
   const int U = N / B;
   dim3 grid(U * chunks, E);
   if (chunks * 4 * spw < B) return (int)hipErrorInvalidValue;
   if (layer == 1) {
     QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<2, 16, WW, IN_RAW_F32, OUT_Z_STATS, false, float>), grid, dim3(256),
                                     fwd_smem(2, H, W), s, (const float*)xin, nullptr, nullptr, w, z, stats, E, B, chunks,
-                                    spw))
+                                    spw, bf, bb))
   } else {
     QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNRELU, OUT_Z_STATS, false, uint16_t>), grid,
                                     dim3(256), fwd_smem(32, H, W), s, (const uint16_t*)xin, nullptr, st_prev, w, z,
-                                    stats, E, B, chunks, spw))
+                                    stats, E, B, chunks, spw, bf, bb))
   }
   return (int)hipGetLastError();
 }
 
 // data gradient of a 32->32 layer: dx (f32, or bf16 when dx_bf16) from dh (f32 or bf16) of this
 // layer, z, st.  w: packed B fragments from qd_conv_pack_weights(dgrad=1)
+// bnb (nullable): build this layer's BN backward coefficients from the reduction partials in-kernel.
 QD_API int qd_conv_dgrad(const void* dh, int dh_bf16, const uint16_t* z, const float* st, const uint16_t* w, void* dx,
-                         int dx_bf16, int N, int E, int B, int H, int W, int chunks, int spw, void* stream) {
+                         int dx_bf16, int N, int E, int B, int H, int W, int chunks, int spw, const BnBwd* bnb,
+                         void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  const BnFwd bf{};
+  const BnBwd bb = bnb ? *bnb : BnBwd{};
   dim3 grid((N / B) * chunks, E);
   if (chunks * 4 * spw < B) return (int)hipErrorInvalidValue;
 #define QD_DG(OUTM_, TIN_)                                                                                         \
   QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNBWD, OUTM_, true, TIN_>), grid, dim3(256),          \
-                                  fwd_smem(32, H, W), s, (const TIN_*)dh, z, st, w, dx, nullptr, E, B, chunks, spw))
+                                  fwd_smem(32, H, W), s, (const TIN_*)dh, z, st, w, dx, nullptr, E, B, chunks, spw, \
+                                  bf, bb))
   if (dh_bf16) {
     if (dx_bf16) { QD_DG(OUT_BF16, uint16_t) } else { QD_DG(OUT_F32, uint16_t) }
   } else {
@@ -987,11 +1109,11 @@ QD_API int qd_conv_stamped(int dgrad, const void* xin, const uint16_t* zaux, con
   if (dgrad)
     hipLaunchKernelGGL((conv3x3_kernel<32, 16, 8, IN_BNBWD, OUT_BF16, true, uint16_t, true>), grid, dim3(256),
                        fwd_smem(32, 16, 8), s, (const uint16_t*)xin, zaux, st, w, out, nullptr, E, B, chunks, spw,
-                       stamps);
+                       BnFwd{}, BnBwd{}, stamps);
   else
     hipLaunchKernelGGL((conv3x3_kernel<32, 16, 8, IN_BNRELU, OUT_Z_STATS, false, uint16_t, true>), grid, dim3(256),
                        fwd_smem(32, 16, 8), s, (const uint16_t*)xin, nullptr, st, w, out, stats, E, B, chunks, spw,
-                       stamps);
+                       BnFwd{}, BnBwd{}, stamps);
   return (int)hipGetLastError();
 }
 
@@ -1002,17 +1124,19 @@ static size_t wgrad_smem(int cin, int H, int W) {
 }
 
 // weight-gradient partials: slab (E, U*chunks, 32*CIN*9).  layer 1: x = raw f32 (CIN=2);
-// layers 2,3: x = BN+ReLU(z_prev) (st_prev).
+// layers 2,3: x = BN+ReLU(z_prev) (st_prev).  bnb (nullable): this layer's BN backward coefficients
+// from the reduction partials in-kernel, and dgamma / dbeta written by one workgroup per expert.
 QD_API int qd_conv_wgrad(int layer, const void* xin, const float* st_prev, const void* dh, int dh_bf16,
                          const uint16_t* z, const float* st, float* slab, int N, int E, int B, int H, int W, int chunks,
-                         int spb, void* stream) {
+                         int spb, const BnBwd* bnb, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  const BnBwd bb = bnb ? *bnb : BnBwd{};
   dim3 grid((N / B) * chunks, E);
   if (chunks * spb < B) return (int)hipErrorInvalidValue;
 #define QD_WG(CIN_, INM_, TIN_, TDH_)                                                                              \
   QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_wgrad_kernel<CIN_, 16, WW, INM_, TIN_, TDH_>), grid, dim3(256),         \
                                   wgrad_smem(CIN_, H, W), s, (const TIN_*)xin, st_prev, (const TDH_*)dh, z, st, slab, \
-                                  E, B, chunks, spb))
+                                  E, B, chunks, spb, bb))
   if (layer == 1) {
     if (dh_bf16) { QD_WG(2, IN_RAW_F32, float, uint16_t) } else { QD_WG(2, IN_RAW_F32, float, float) }
   } else {
@@ -1027,8 +1151,36 @@ QD_API int qd_bn_stats_finalize(const float* stats, const float* gamma, const fl
                                 float eps, int training, long long* nbt, int n_nbt, long long nbt_inc,
                                 void* stream) {
   if (U < 1 || U > kMaxGroups || n_nbt > 64) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(EC), dim3(64), 0, (hipStream_t)stream, stats, gamma,
-                     beta, run_mean, run_var, st, U, chunks, EC, count, momentum, eps, training, nbt, n_nbt, nbt_inc);
+  FinJobs jobs{};
+  jobs.stats[0] = stats;
+  jobs.gamma[0] = gamma;
+  jobs.beta[0] = beta;
+  jobs.run_mean[0] = run_mean;
+  jobs.run_var[0] = run_var;
+  jobs.st[0] = st;
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(EC, 1), dim3(64), 0, (hipStream_t)stream, jobs, U, chunks, EC,
+                     count, momentum, eps, training, nbt, n_nbt, nbt_inc);
+  return (int)hipGetLastError();
+}
+
+// n (<= 3) layers' finalisations in one launch (arrays of n pointers); nbt as above (layer 0's block).
+QD_API int qd_bn_stats_finalize_multi(int n, const float* const* stats, const float* const* gamma,
+                                      const float* const* beta, float* const* run_mean, float* const* run_var,
+                                      float* const* st, int U, int chunks, int EC, float count, float momentum,
+                                      float eps, int training, long long* nbt, int n_nbt, long long nbt_inc,
+                                      void* stream) {
+  if (n < 1 || n > 3 || U < 1 || U > kMaxGroups || n_nbt > 64) return (int)hipErrorInvalidValue;
+  FinJobs jobs{};
+  for (int l = 0; l < n; ++l) {
+    jobs.stats[l] = stats[l];
+    jobs.gamma[l] = gamma[l];
+    jobs.beta[l] = beta[l];
+    jobs.run_mean[l] = run_mean[l];
+    jobs.run_var[l] = run_var[l];
+    jobs.st[l] = st[l];
+  }
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(EC, n), dim3(64), 0, (hipStream_t)stream, jobs, U, chunks, EC,
+                     count, momentum, eps, training, nbt, n_nbt, nbt_inc);
   return (int)hipGetLastError();
 }
 
@@ -1076,15 +1228,18 @@ QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int
   return (int)hipGetLastError();
 }
 
-// n <= 4 jobs, each as qd_slab_rows_sum (width % 4 == 0, 16-byte aligned), one launch
+// n <= 16 jobs, each as qd_slab_rows_sum, one launch
+// lds (nullable): per-job row strides (default: the width)
 QD_API int qd_slab_rows_sum_multi(int n, const float* const* slabs, float* const* outs, const int* groups,
-                                  const int* rows, const int* widths, int accumulate, void* stream) {
+                                  const int* rows, const int* widths, const int* lds, int accumulate, void* stream) {
   if (n < 1 || n > kSlabJobs) return (int)hipErrorInvalidValue;
   SlabJobs jobs{};
   jobs.accumulate = accumulate;
   int gx = 0, gy = 0;
   for (int j = 0; j < n; ++j) {
-    jobs.vec[j] = !(widths[j] % 4 || ((uintptr_t)slabs[j] & 15) || ((uintptr_t)outs[j] & 15));
+    jobs.ld[j] = lds ? lds[j] : widths[j];
+    if (jobs.ld[j] < widths[j]) return (int)hipErrorInvalidValue;
+    jobs.vec[j] = !(widths[j] % 4 || jobs.ld[j] % 4 || ((uintptr_t)slabs[j] & 15) || ((uintptr_t)outs[j] & 15));
     jobs.slab[j] = slabs[j];
     jobs.out[j] = outs[j];
     jobs.groups[j] = groups[j];

@@ -26,6 +26,17 @@ def _ptr(t: Optional[torch.Tensor]):
     return nat.ptr(t) if t is not None else None
 
 
+class BnFwd(ctypes.Structure):
+    """csrc/hip/conv.hip ``BnFwd``: forward BN finalisation fused into the consuming conv kernel."""
+    _fields_ = [("stats", _p), ("gamma", _p), ("beta", _p), ("run_mean", _p), ("run_var", _p), ("st_out", _p),
+                ("chunks", _i), ("count", _f), ("momentum", _f), ("eps", _f), ("training", _i)]
+
+
+class BnBwd(ctypes.Structure):
+    """csrc/hip/conv.hip ``BnBwd``: BN backward finalisation fused into the wgrad / dgrad kernels."""
+    _fields_ = [("rslab", _p), ("gamma", _p), ("chunks", _i), ("count", _f)]
+
+
 class ConvStackHIP:
     """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
 
@@ -56,8 +67,10 @@ class ConvStackHIP:
         self.fp8 = getattr(model, "fp8", False)
         self.h3_8 = torch.empty(N * self.E, 32 * HW, device=dev, dtype=torch.float8_e4m3fn) if self.fp8 else None
         self.st = [torch.zeros(U, EC, NST, device=dev) for _ in range(3)]
-        self.stats = torch.zeros(U, self.chunks, EC, 2, device=dev)
-        self.rslab = torch.zeros(U, self.chunks_r, EC, 2, device=dev)
+        self.stats = [torch.zeros(U, self.chunks, EC, 2, device=dev) for _ in range(3)]   # per layer
+        # BN backward partials per layer, planar rows [sum g | sum g*xhat] x EC (their column sums are
+        # dbeta / dgamma: jobs of the step's batched slab reduction)
+        self.rslab = [torch.zeros(U, self.chunks_r, 2, EC, device=dev) for _ in range(3)]
         # grads w.r.t. h1, h2: bf16 by default (they only feed bf16 MFMA operands and fp32-accumulated
         # BN reductions), halving the dgrad write and every re-read of it
         self.dx_bf16 = dx_bf16
@@ -69,11 +82,11 @@ class ConvStackHIP:
         self.wpk_t = [None] + [torch.empty(self.E, 18, 64, 8, device=dev, dtype=bf) for _ in range(2)]
         self.lib = nat.hip_lib()
         L = self.lib
-        self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
-        self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p])
-        self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
-        self._fin = nat.fn(L, "qd_bn_stats_finalize", [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i, _p, _i,
-                                                          ctypes.c_longlong, _p])
+        self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
+        self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p])
+        self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
+        self._fin = nat.fn(L, "qd_bn_stats_finalize_multi", [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i,
+                                                                _p, _i, ctypes.c_longlong, _p])
         self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _i, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
@@ -97,16 +110,25 @@ class ConvStackHIP:
         self.pack_weights(st)
         inp, st_prev = x1, None
         for k in range(3):
+            # layers 2, 3 finalise the previous layer's BatchNorm themselves (BnFwd: statistics
+            # partials -> records, running stats, published st); layer 3's own BN keeps a launch
+            bnf = None
+            if k > 0:
+                j = k - 1
+                bnf = BnFwd(nat.ptr(self.stats[j]), nat.ptr(m.bn_w[j]), nat.ptr(m.bn_b[j]), nat.ptr(m.run_mean[j]),
+                            nat.ptr(m.run_var[j]), nat.ptr(self.st[j]), self.chunks, float(self.B * self.HW),
+                            m.momentum, m.eps, int(training))
             nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
-                                nat.ptr(self.stats), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw,
-                                st), f"conv_fwd{k + 1}")
-            # the first finalisation also advances every BN layer's num_batches_tracked (training)
-            nbt = getattr(m, "_nbt", None) if (k == 0 and training and self.count_batches) else None
-            nat.check(self._fin(nat.ptr(self.stats), nat.ptr(m.bn_w[k]), nat.ptr(m.bn_b[k]), nat.ptr(m.run_mean[k]),
-                                nat.ptr(m.run_var[k]), nat.ptr(self.st[k]), self.U, self.chunks, self.EC,
-                                float(self.B * self.HW), m.momentum, m.eps, int(training), _ptr(nbt),
-                                nbt.numel() if nbt is not None else 0, self.U, st), f"bn_fin{k + 1}")
+                                nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw,
+                                ctypes.byref(bnf) if bnf is not None else None, st), f"conv_fwd{k + 1}")
             inp, st_prev = self.z[k], self.st[k]
+        # one BN tail launch: every layer's running statistics (+ num_batches_tracked), and the last
+        # layer's records (layers 1, 2 were built -- bitwise identically -- by their consumers)
+        nbt = getattr(m, "_nbt", None) if (training and self.count_batches) else None
+        arr = lambda xs: (ctypes.c_void_p * 3)(*[nat.ptr(x) for x in xs])
+        nat.check(self._fin(3, arr(self.stats), arr(m.bn_w), arr(m.bn_b), arr(m.run_mean), arr(m.run_var), arr(self.st),
+                            self.U, self.chunks, self.EC, float(self.B * self.HW), m.momentum, m.eps, int(training),
+                            _ptr(nbt), nbt.numel() if nbt is not None else 0, self.U, st), "bn_tail")
         f8 = self.m.fp8_scales if self.fp8 else None
         nat.check(self._apply(nat.ptr(self.z[2]), nat.ptr(self.st[2]), nat.ptr(self.h3), self.N, self.EC, self.B,
                               self.HW, _ptr(self.h3_8), nat.ptr(f8.qs) if f8 else None,
@@ -121,30 +143,32 @@ class ConvStackHIP:
         dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
         for k in (2, 1, 0):
             z, bst = self.z[k], self.st[k]
-            nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.rslab), self.N, self.E,
+            rs = self.rslab[k]
+            nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(rs), self.N, self.E,
                                  self.B, self.H, self.W, self.chunks_r, self.spb_r, st), f"bn_bwd_reduce{k + 1}")
-            nat.check(self._bfin(nat.ptr(self.rslab), nat.ptr(m.bn_w[k]), nat.ptr(bst), nat.ptr(m.bn_w[k].grad),
-                                 nat.ptr(m.bn_b[k].grad), self.U, self.chunks_r, self.EC, float(self.B * self.HW),
-                                 int(accumulate), st),
-                      f"bn_bwd_fin{k + 1}")
+            # BN backward finalisation fused into this layer's wgrad and dgrad kernels
+            bnb = BnBwd(nat.ptr(rs), nat.ptr(m.bn_w[k]), self.chunks_r, float(self.B * self.HW))
             xin = self.x1 if k == 0 else self.z[k - 1]
             st_prev = None if k == 0 else self.st[k - 1]
             ws = self.wslab[k]
             nat.check(self._wgrad(k + 1, nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst),
-                                  nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k], st),
-                      f"conv_wgrad{k + 1}")
+                                  nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k],
+                                  ctypes.byref(bnb), st), f"conv_wgrad{k + 1}")
             if k > 0:
                 dx = self.dx[k - 1]
                 nat.check(self._dgrad(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.wpk_t[k]),
                                       nat.ptr(dx), int(self.dx_bf16), self.N, self.E, self.B, self.H, self.W,
-                                      self.chunks, self.spw, st), f"conv_dgrad{k + 1}")
+                                      self.chunks, self.spw, ctypes.byref(bnb), st), f"conv_dgrad{k + 1}")
                 dh, dh_bf = dx, int(self.dx_bf16)
         # the three weight-gradient slabs -> conv_w grads: queued on the caller's batch (one launch
         # for every slab reduction of the step phase) or launched here
         own = slabs is None
         batch = SlabBatch() if own else slabs
+        EC, R = self.EC, self.U * self.chunks_r
         for k in range(3):
             w = self.wslab[k]
             batch.add(w, m.conv_w[k].grad, self.E, w.shape[1], w.shape[2])
+            batch.add(self.rslab[k], m.bn_b[k].grad, 1, R, EC, ld=2 * EC)              # dbeta = sum g
+            batch.add(self.rslab[k], m.bn_w[k].grad, 1, R, EC, ld=2 * EC, offset=EC)   # dgamma = sum g*xhat
         if own:
             batch.launch(accumulate, st)

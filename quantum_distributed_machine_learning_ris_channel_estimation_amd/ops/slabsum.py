@@ -16,32 +16,36 @@ import torch
 from .. import _native as nat
 
 _p, _i = ctypes.c_void_p, ctypes.c_int
-MAX_JOBS = 8
+MAX_JOBS = 16
 
 
 class SlabBatch:
     def __init__(self):
-        self.jobs: List[Tuple[torch.Tensor, torch.Tensor, int, int, int]] = []
+        self.jobs: List[Tuple[int, torch.Tensor, int, int, int, int]] = []
         self._f = None
 
-    def add(self, slab: torch.Tensor, out: torch.Tensor, groups: int, rows: int, width: int) -> None:
-        """out[g, :width] (+)= sum_r slab[g, r, :width] for g < groups (both contiguous fp32)."""
-        assert slab.dtype == torch.float32 and out.dtype == torch.float32
-        assert slab.numel() >= groups * rows * width and out.numel() >= groups * width
+    def add(self, slab: torch.Tensor, out: torch.Tensor, groups: int, rows: int, width: int, ld: int = 0,
+            offset: int = 0) -> None:
+        """out[g, :width] (+)= sum_r slab[offset + (g * rows + r) * ld : ... + width] for g < groups
+        (fp32; ld = row stride, default width)."""
+        ld = ld or width
+        assert slab.dtype == torch.float32 and out.dtype == torch.float32 and slab.is_contiguous()
+        assert offset + (groups * rows - 1) * ld + width <= slab.numel() and out.numel() >= groups * width
         if len(self.jobs) == MAX_JOBS:
-            raise RuntimeError("SlabBatch: more than 8 reductions in one launch")
-        self.jobs.append((slab, out, groups, rows, width))
+            raise RuntimeError(f"SlabBatch: more than {MAX_JOBS} reductions in one launch")
+        self.jobs.append((slab.data_ptr() + 4 * offset, out, groups, rows, width, ld))
 
     def launch(self, accumulate: bool, stream) -> None:
         if not self.jobs:
             return
         if self._f is None:
-            self._f = nat.fn(nat.hip_lib(), "qd_slab_rows_sum_multi", [_i, _p, _p, _p, _p, _p, _i, _p])
+            self._f = nat.fn(nat.hip_lib(), "qd_slab_rows_sum_multi", [_i, _p, _p, _p, _p, _p, _p, _i, _p])
         n = len(self.jobs)
-        slabs = (ctypes.c_void_p * n)(*[nat.ptr(j[0]) for j in self.jobs])
+        slabs = (ctypes.c_void_p * n)(*[j[0] for j in self.jobs])
         outs = (ctypes.c_void_p * n)(*[nat.ptr(j[1]) for j in self.jobs])
         groups = (ctypes.c_int * n)(*[j[2] for j in self.jobs])
         rows = (ctypes.c_int * n)(*[j[3] for j in self.jobs])
         widths = (ctypes.c_int * n)(*[j[4] for j in self.jobs])
-        nat.check(self._f(n, slabs, outs, groups, rows, widths, int(accumulate), stream), "slab_rows_sum_multi")
+        lds = (ctypes.c_int * n)(*[j[5] for j in self.jobs])
+        nat.check(self._f(n, slabs, outs, groups, rows, widths, lds, int(accumulate), stream), "slab_rows_sum_multi")
         self.jobs = []

@@ -35,7 +35,7 @@ def main():
         for _ in range(3):
             if dg == 0:
                 args = (nat.ptr(cs.z[0]), None, nat.ptr(cs.st[0]), nat.ptr(cs.wpk[1]), nat.ptr(cs.z[1]),
-                        nat.ptr(cs.stats))
+                        nat.ptr(cs.stats[1]))
             else:
                 args = (nat.ptr(dh), nat.ptr(cs.z[2]), nat.ptr(cs.st[2]), nat.ptr(cs.wpk_t[2]), nat.ptr(cs.dx[1]),
                         None)
