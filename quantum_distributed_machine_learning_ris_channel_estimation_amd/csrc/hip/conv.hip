@@ -127,6 +127,15 @@ struct BnBwd {            // backward: (c1, c2, c3) from the BN backward reducti
   float count;
 };
 
+// dgrad epilogue fusion: the BN backward reduction of the PREVIOUS layer (whose output h = relu(a z
+// + b) is this pass's dx): per (u, chunk, channel) sum g and sum g*xhat, g = dx * [a z + b > 0],
+// planar rows (U, chunks, 2, EC) -- what bn_bwd_reduce_kernel would compute in a launch of its own.
+struct BnRed {
+  const uint16_t* z;   // previous layer's pre-BN output (bf16, same layout as dx); null: no fusion
+  const float* st;     // its published BN records (U, EC, NST)
+  float* part;         // (U, chunks, 2, EC)
+};
+
 // sums of the two planar partial rows of channel ch over the chunks of group u (8 lanes per
 // channel; up to 64 chunks with every load in flight at once)
 __device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, int u, int chunks, int EC, int ch,
@@ -198,7 +207,7 @@ template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN, bo
 __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
                                                       const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
                                                       void* __restrict__ out, float* __restrict__ stats, int E, int B,
-                                                      int chunks, int spw, BnFwd bnf, BnBwd bnb,
+                                                      int chunks, int spw, BnFwd bnf, BnBwd bnb, BnRed brd,
                                                       unsigned long long* __restrict__ stamps = nullptr) {
   // STAMP (diagnostic builds): per wave [0] start [1] weights + BN params staged [2] first sample
   // staged [3] first sample's MFMAs + epilogue [4] all samples [5] end
@@ -222,6 +231,15 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
   float* stl = reinterpret_cast<float*>(wl + KS * 64);                                     // BN params
   // per-lane channel for the output/statistics: column of the MFMA tile
   float s1 = 0.f, s2 = 0.f;
+  [[maybe_unused]] float ra = 0.f, rb = 0.f, rmu = 0.f, rinv = 0.f;
+  const bool fuse_red = DGRAD && OUTM == OUT_BF16 && brd.part != nullptr;
+  if (fuse_red) {
+    const float4 r = *reinterpret_cast<const float4*>(brd.st + ((size_t)u * E * CO + e * CO + l32) * NST);
+    rmu = r.x;
+    rinv = r.y;
+    ra = r.z;
+    rb = r.w;
+  }
   const int n0 = u * B + (chunk * 4 + wv) * spw;
   const int nend = min((u + 1) * B, n0 + spw);
 
@@ -233,7 +251,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
   static_assert(RAWIN ? (CIN * G::HW) % 64 == 0 : CH8 % 64 == 0, "whole waves per staging pass");
   constexpr int QV = RAWIN ? 1 : (int)sizeof(TIN) / 2;  // uint4s per 8-value item (bf16: 1, f32: 2)
   constexpr int HOLD = ITER * (QV + (INM == IN_BNBWD ? 1 : 0));   // 16-byte registers per sample
-  constexpr bool PREF = RAWIN || (HOLD <= 16 && G::HW <= 128);   // (P256: registers go to the MFMA pipeline)
+  // (dgrad: registers go to the fused BN-reduction operands; P256: to the MFMA pipeline)
+  constexpr bool PREF = RAWIN || (!DGRAD && HOLD <= 16 && G::HW <= 128);
   constexpr int GR = PREF ? ITER : (INM == IN_BNBWD ? 2 : 4);
   static_assert(ITER % GR == 0, "staging groups");
   [[maybe_unused]] uint4 rv[RAWIN ? 1 : GR][QV];
@@ -364,6 +383,17 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
     constexpr int MG = G::MT < 4 ? G::MT : 4;
 #pragma unroll
     for (int g0 = 0; g0 < G::MT; g0 += MG) {
+      // fused BN reduction: the previous layer's z at this lane's output positions, loaded now so
+      // the round trip hides behind the MFMAs
+      [[maybe_unused]] uint2 zq[MG][4];
+      if (fuse_red) {
+#pragma unroll
+        for (int j = 0; j < MG; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            zq[j][g] = *reinterpret_cast<const uint2*>(
+                brd.z + ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + (g0 + j) * 32 + 8 * g + 4 * hh);
+      }
       f32x16 acc[MG];
       bf16x8 a_cur[MG], b_cur = wl[lane];
 #pragma unroll
@@ -413,6 +443,18 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
               const float v0 = bf(h0), v1 = bf(h1), v2 = bf(h2), v3 = bf(h3);
               s1 += v0 + v1 + v2 + v3;
               s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+            } else if constexpr (DGRAD && OUTM == OUT_BF16) {   // fused BN reduction (stored values)
+              if (fuse_red) {
+                const float d[4] = {bf(h0), bf(h1), bf(h2), bf(h3)};
+                const float zz[4] = {__uint_as_float(zq[j][g].x << 16), __uint_as_float(zq[j][g].x & 0xffff0000u),
+                                     __uint_as_float(zq[j][g].y << 16), __uint_as_float(zq[j][g].y & 0xffff0000u)};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  const float gg = (ra * zz[q] + rb > 0.f) ? d[q] : 0.f;
+                  s1 += gg;
+                  s2 += gg * (zz[q] - rmu) * rinv;
+                }
+              }
             }
           }
 #pragma unroll
@@ -429,7 +471,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
     if (STAMP && n == n0) ts[3] = phase_stamp();
   }
   if constexpr (STAMP) ts[4] = phase_stamp();
-  if constexpr (OUTM == OUT_Z_STATS) {
+  if (OUTM == OUT_Z_STATS || fuse_red) {
     // combine the two half-waves (same channel), then the 4 waves through LDS
     s1 += __shfl_xor(s1, 32);
     s2 += __shfl_xor(s2, 32);
@@ -445,7 +487,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
-      stats[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;   // planar [2][EC] rows
+      float* dst = OUTM == OUT_Z_STATS ? stats : brd.part;
+      dst[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;   // planar [2][EC] rows
     }
   }
   if constexpr (STAMP) {
@@ -1066,11 +1109,11 @@ QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const u
   if (layer == 1) {
     QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<2, 16, WW, IN_RAW_F32, OUT_Z_STATS, false, float>), grid, dim3(256),
                                     fwd_smem(2, H, W), s, (const float*)xin, nullptr, nullptr, w, z, stats, E, B, chunks,
-                                    spw, bf, bb))
+                                    spw, bf, bb, BnRed{}))
   } else {
     QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNRELU, OUT_Z_STATS, false, uint16_t>), grid,
                                     dim3(256), fwd_smem(32, H, W), s, (const uint16_t*)xin, nullptr, st_prev, w, z,
-                                    stats, E, B, chunks, spw, bf, bb))
+                                    stats, E, B, chunks, spw, bf, bb, BnRed{}))
   }
   return (int)hipGetLastError();
 }
@@ -1078,18 +1121,21 @@ QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const u
 // data gradient of a 32->32 layer: dx (f32, or bf16 when dx_bf16) from dh (f32 or bf16) of this
 // layer, z, st.  w: packed B fragments from qd_conv_pack_weights(dgrad=1)
 // bnb (nullable): build this layer's BN backward coefficients from the reduction partials in-kernel.
+// bred (nullable; bf16 dx only): also produce the previous layer's BN backward partials (BnRed).
 QD_API int qd_conv_dgrad(const void* dh, int dh_bf16, const uint16_t* z, const float* st, const uint16_t* w, void* dx,
                          int dx_bf16, int N, int E, int B, int H, int W, int chunks, int spw, const BnBwd* bnb,
-                         void* stream) {
+                         const BnRed* bred, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const BnFwd bf{};
   const BnBwd bb = bnb ? *bnb : BnBwd{};
+  const BnRed br = bred ? *bred : BnRed{};
+  if (br.part && !dx_bf16) return (int)hipErrorInvalidValue;
   dim3 grid((N / B) * chunks, E);
   if (chunks * 4 * spw < B) return (int)hipErrorInvalidValue;
 #define QD_DG(OUTM_, TIN_)                                                                                         \
   QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_kernel<32, 16, WW, IN_BNBWD, OUTM_, true, TIN_>), grid, dim3(256),          \
                                   fwd_smem(32, H, W), s, (const TIN_*)dh, z, st, w, dx, nullptr, E, B, chunks, spw, \
-                                  bf, bb))
+                                  bf, bb, br))
   if (dh_bf16) {
     if (dx_bf16) { QD_DG(OUT_BF16, uint16_t) } else { QD_DG(OUT_F32, uint16_t) }
   } else {
@@ -1109,11 +1155,11 @@ QD_API int qd_conv_stamped(int dgrad, const void* xin, const uint16_t* zaux, con
   if (dgrad)
     hipLaunchKernelGGL((conv3x3_kernel<32, 16, 8, IN_BNBWD, OUT_BF16, true, uint16_t, true>), grid, dim3(256),
                        fwd_smem(32, 16, 8), s, (const uint16_t*)xin, zaux, st, w, out, nullptr, E, B, chunks, spw,
-                       BnFwd{}, BnBwd{}, stamps);
+                       BnFwd{}, BnBwd{}, BnRed{}, stamps);
   else
     hipLaunchKernelGGL((conv3x3_kernel<32, 16, 8, IN_BNRELU, OUT_Z_STATS, false, uint16_t, true>), grid, dim3(256),
                        fwd_smem(32, 16, 8), s, (const uint16_t*)xin, nullptr, st, w, out, stats, E, B, chunks, spw,
-                       BnFwd{}, BnBwd{}, stamps);
+                       BnFwd{}, BnBwd{}, BnRed{}, stamps);
   return (int)hipGetLastError();
 }
 

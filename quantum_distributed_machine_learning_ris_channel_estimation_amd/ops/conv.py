@@ -32,6 +32,11 @@ class BnFwd(ctypes.Structure):
                 ("chunks", _i), ("count", _f), ("momentum", _f), ("eps", _f), ("training", _i)]
 
 
+class BnRed(ctypes.Structure):
+    """csrc/hip/conv.hip ``BnRed``: the previous layer's BN backward reduction fused into dgrad."""
+    _fields_ = [("z", _p), ("st", _p), ("part", _p)]
+
+
 class BnBwd(ctypes.Structure):
     """csrc/hip/conv.hip ``BnBwd``: BN backward finalisation fused into the wgrad / dgrad kernels."""
     _fields_ = [("rslab", _p), ("gamma", _p), ("chunks", _i), ("count", _f)]
@@ -70,7 +75,11 @@ class ConvStackHIP:
         self.stats = [torch.zeros(U, self.chunks, EC, 2, device=dev) for _ in range(3)]   # per layer
         # BN backward partials per layer, planar rows [sum g | sum g*xhat] x EC (their column sums are
         # dbeta / dgamma: jobs of the step's batched slab reduction)
-        self.rslab = [torch.zeros(U, self.chunks_r, 2, EC, device=dev) for _ in range(3)]
+        # (layers 1, 2: produced by the next layer's dgrad kernel, chunked like it; layer 3: by its own
+        # reduction launch over dh3 from the FC GEMM)
+        self.fuse_bn_red = dx_bf16
+        self.rchunks = [self.chunks if self.fuse_bn_red else self.chunks_r] * 2 + [self.chunks_r]
+        self.rslab = [torch.zeros(U, c, 2, EC, device=dev) for c in self.rchunks]
         # grads w.r.t. h1, h2: bf16 by default (they only feed bf16 MFMA operands and fp32-accumulated
         # BN reductions), halving the dgrad write and every re-read of it
         self.dx_bf16 = dx_bf16
@@ -83,7 +92,7 @@ class ConvStackHIP:
         self.lib = nat.hip_lib()
         L = self.lib
         self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
-        self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p])
+        self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p])
         self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
         self._fin = nat.fn(L, "qd_bn_stats_finalize_multi", [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i,
                                                                 _p, _i, ctypes.c_longlong, _p])
@@ -144,10 +153,11 @@ class ConvStackHIP:
         for k in (2, 1, 0):
             z, bst = self.z[k], self.st[k]
             rs = self.rslab[k]
-            nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(rs), self.N, self.E,
-                                 self.B, self.H, self.W, self.chunks_r, self.spb_r, st), f"bn_bwd_reduce{k + 1}")
+            if k == 2 or not self.fuse_bn_red:   # (else the previous dgrad produced these partials)
+                nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(rs), self.N, self.E,
+                                     self.B, self.H, self.W, self.chunks_r, self.spb_r, st), f"bn_bwd_reduce{k + 1}")
             # BN backward finalisation fused into this layer's wgrad and dgrad kernels
-            bnb = BnBwd(nat.ptr(rs), nat.ptr(m.bn_w[k]), self.chunks_r, float(self.B * self.HW))
+            bnb = BnBwd(nat.ptr(rs), nat.ptr(m.bn_w[k]), self.rchunks[k], float(self.B * self.HW))
             xin = self.x1 if k == 0 else self.z[k - 1]
             st_prev = None if k == 0 else self.st[k - 1]
             ws = self.wslab[k]
@@ -156,17 +166,22 @@ class ConvStackHIP:
                                   ctypes.byref(bnb), st), f"conv_wgrad{k + 1}")
             if k > 0:
                 dx = self.dx[k - 1]
+                # ... and the previous layer's BN backward reduction fused into this dgrad's epilogue
+                brd = BnRed(nat.ptr(self.z[k - 1]), nat.ptr(self.st[k - 1]), nat.ptr(self.rslab[k - 1])) \
+                    if self.fuse_bn_red else None
                 nat.check(self._dgrad(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(self.wpk_t[k]),
                                       nat.ptr(dx), int(self.dx_bf16), self.N, self.E, self.B, self.H, self.W,
-                                      self.chunks, self.spw, ctypes.byref(bnb), st), f"conv_dgrad{k + 1}")
+                                      self.chunks, self.spw, ctypes.byref(bnb),
+                                      ctypes.byref(brd) if brd is not None else None, st), f"conv_dgrad{k + 1}")
                 dh, dh_bf = dx, int(self.dx_bf16)
         # the three weight-gradient slabs -> conv_w grads: queued on the caller's batch (one launch
         # for every slab reduction of the step phase) or launched here
         own = slabs is None
         batch = SlabBatch() if own else slabs
-        EC, R = self.EC, self.U * self.chunks_r
+        EC = self.EC
         for k in range(3):
             w = self.wslab[k]
+            R = self.U * self.rchunks[k]
             batch.add(w, m.conv_w[k].grad, self.E, w.shape[1], w.shape[2])
             batch.add(self.rslab[k], m.bn_b[k].grad, 1, R, EC, ld=2 * EC)              # dbeta = sum g
             batch.add(self.rslab[k], m.bn_w[k].grad, 1, R, EC, ld=2 * EC, offset=EC)   # dgamma = sum g*xhat
