@@ -40,6 +40,12 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-quantumnat", action="store_true")
     ap.add_argument("--split-graphs", action="store_true", help="3-graph DP plan even at 1 GPU")
+    ap.add_argument("--steps-per-graph", type=int, default=1,
+                    help="training steps captured per graph replay at world 1 (each gathers its own batch)")
+    ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
+    ap.add_argument("--stream-mode", default="qsc", choices=["serial", "dag", "dagq", "qsc", "full"],
+                    help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
+                         "or a separate QSC graph on its own stream (+ HDCE side branches with 'full')")
     args = ap.parse_args()
 
     import torch
@@ -55,18 +61,19 @@ def main() -> int:
     ctx = init_distributed("auto")
     cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
                          hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
-                         split_graphs=args.split_graphs)
+                         split_graphs=args.split_graphs, stream_mode=args.stream_mode,
+                         qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
-    for _ in range(args.warmup):
-        tr.step()
+    tr.run(args.warmup)
+    tr.prepare(args.steps)   # (graph capture, if the timed run needs a set the warm-up did not)
     sync()
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tr.step()
+    tr.run(args.steps)   # exactly args.steps training steps (steps_per_graph per graph replay)
+    host = time.perf_counter() - t0   # host enqueue time (a launch-bound run shows it ~= wall)
     sync()
     ctx.barrier()
     sync()
@@ -88,6 +95,7 @@ def main() -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "host_ms_per_step": round(host / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -104,6 +112,8 @@ def main() -> int:
                 "parallelism": f"dp{n}",
                 "hip_graphs": bool(tr.graphed.enabled),
                 "graphs_per_step": len(tr.graphs),
+                "stream_mode": tr.mode,
+                "steps_per_graph": args.steps_per_graph if n == 1 else 1,
                 "quantumnat": cfg.use_quantumnat,
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},

@@ -12,6 +12,11 @@
 //                                  stream s = e*U + u, sample idx[b] in the label/perf stores, so
 //                                  the NMSE kernels read labels in place (no permuted copies)
 // One wave per (stream, sample): the 2*H*W-float plane is copied with float4 loads/stores.
+//
+// Device-cursor form (qd_gather_cursor): idx = perm + *cursor, and the grid's last workgroup
+// advances *cursor by B.  A training step's batch selection then lives entirely inside the captured
+// graph(s) -- no per-step host copy of the index slice -- and two graphs replayed on different
+// streams (HDCE: x1 + rowoff, QSC: xq) each advance their own cursor over the same permutation.
 #include "common.h"
 
 namespace qd {
@@ -20,23 +25,43 @@ namespace gather {
 __global__ void __launch_bounds__(256) gather_step_kernel(const long* __restrict__ idx, const float* __restrict__ Yp,
                                                           long yp_stream_stride, float* __restrict__ x1,
                                                           float* __restrict__ xq, int* __restrict__ rowoff,
-                                                          long lab_stream_rows, int E, int U, int B, int plane) {
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                          long lab_stream_rows, int E, int U, int B, int plane,
+                                                          int* __restrict__ cursor, unsigned int* __restrict__ done,
+                                                          long nperm) {
   const int lane = threadIdx.x & 63;
   const int S = E * U;
-  if (wid >= S * B) return;
-  const int s = wid / B, b = wid % B;
-  const int e = s / U, u = s % U;
-  const long n = idx[b];
-  const float4* src = reinterpret_cast<const float4*>(Yp + s * yp_stream_stride + n * plane);
-  float4* d1 = reinterpret_cast<float4*>(x1 + ((size_t)(u * B + b) * E + e) * plane);
-  float4* dq = xq ? reinterpret_cast<float4*>(xq + ((size_t)s * B + b) * plane) : nullptr;
-  for (int i = lane; i < plane / 4; i += 64) {
-    const float4 v = src[i];
-    d1[i] = v;
-    if (dq) dq[i] = v;
+  int c = cursor ? *cursor : 0;
+  if (c < 0 || c + B > nperm) c = 0;   // (never out of the permutation, whatever the host did)
+  // grid-stride over (stream, sample) waves: a capped grid keeps the cursor protocol's
+  // same-address atomics (one per workgroup, serialised in L2) few
+  for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < S * B; wid += gridDim.x * 4) {
+    const int s = wid / B, b = wid % B;
+    const int e = s / U, u = s % U;
+    const long n = idx[c + b];
+    const float4* src = reinterpret_cast<const float4*>(Yp + s * yp_stream_stride + n * plane);
+    float4* d1 = x1 ? reinterpret_cast<float4*>(x1 + ((size_t)(u * B + b) * E + e) * plane) : nullptr;
+    float4* dq = xq ? reinterpret_cast<float4*>(xq + ((size_t)s * B + b) * plane) : nullptr;
+    for (int i = lane; i < plane / 4; i += 64) {
+      const float4 v = src[i];
+      if (d1) d1[i] = v;
+      if (dq) dq[i] = v;
+    }
+    if (lane == 0 && rowoff) rowoff[(size_t)(u * B + b) * E + e] = (int)(s * lab_stream_rows + n);
   }
-  if (lane == 0) rowoff[(size_t)(u * B + b) * E + e] = (int)(s * lab_stream_rows + n);
+  if (cursor == nullptr) return;
+  // the last workgroup to arrive advances the cursor: every workgroup read *cursor before arriving
+  // (same protocol as the optimizer's step tick, csrc/hip/optim.hip)
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (prev == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    *cursor = c + B;
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace gather
@@ -50,6 +75,22 @@ QD_API int qd_gather_step(const long* idx, const float* Yp, long yp_stream_strid
   if (plane % 4 || E < 1 || U < 1 || B < 1) return (int)hipErrorInvalidValue;
   const int waves = E * U * B;
   hipLaunchKernelGGL(gather_step_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, idx, Yp,
-                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane);
+                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, nullptr, nullptr, (long)B);
+  return (int)hipGetLastError();
+}
+
+// perm: (n,) int64 sample permutation; cursor: device int32 (perm offset of this step's batch,
+// advanced by B in-kernel); done: device uint32 zero-initialised once.  x1 / xq / rowoff nullable.
+// The caller guarantees *cursor + B <= n (it re-arms the cursor when it regenerates perm).
+QD_API int qd_gather_cursor(const long* perm, long nperm, int* cursor, unsigned int* done, const float* Yp,
+                            long yp_stream_stride,
+                            float* x1, float* xq, int* rowoff, long lab_stream_rows, int E, int U, int B, int plane,
+                            void* stream) {
+  if (plane % 4 || E < 1 || U < 1 || B < 1 || !cursor || !done || nperm < B) return (int)hipErrorInvalidValue;
+  if ((x1 == nullptr) != (rowoff == nullptr)) return (int)hipErrorInvalidValue;
+  const int waves = E * U * B;
+  const int grid = (waves + 3) / 4 < 128 ? (waves + 3) / 4 : 128;
+  hipLaunchKernelGGL(gather_step_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, perm, Yp,
+                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, cursor, done, nperm);
   return (int)hipGetLastError();
 }

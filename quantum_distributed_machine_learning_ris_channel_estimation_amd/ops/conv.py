@@ -145,10 +145,17 @@ class ConvStackHIP:
         return self.h3
 
     # --------------------------------------------------------------------- backward
-    def backward(self, dh3: torch.Tensor, accumulate: bool = True, slabs: Optional["SlabBatch"] = None) -> None:
+    def backward(self, dh3: torch.Tensor, accumulate: bool = True, slabs: Optional["SlabBatch"] = None,
+                 side: Optional["torch.cuda.Stream"] = None) -> None:
         """dh3: dL/dh3 as (N*E, 32*H*W) (bf16 or fp32).  Adds (accumulate) or writes the conv/BN grads
-        into the flat grad -- writing makes a zero_grad before the step unnecessary."""
+        into the flat grad -- writing makes a zero_grad before the step unnecessary.
+
+        ``side``: a second stream for the weight-gradient kernels of layers 3 and 2.  wgrad(k) and
+        dgrad(k) only share their inputs, so the dgrad chain (the critical path to layer 1) runs on
+        the current stream while wgrad(k) runs beside it; the current stream joins before the slab
+        reduction.  Each of these kernels fills well under the 256 CUs, so they overlap."""
         m, st = self.m, nat.stream_ptr(dh3.device)
+        main = torch.cuda.current_stream(dh3.device) if side is not None else None
         dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
         for k in (2, 1, 0):
             z, bst = self.z[k], self.st[k]
@@ -161,9 +168,13 @@ class ConvStackHIP:
             xin = self.x1 if k == 0 else self.z[k - 1]
             st_prev = None if k == 0 else self.st[k - 1]
             ws = self.wslab[k]
+            on_side = side is not None and k > 0
+            if on_side:
+                side.wait_stream(main)
+            wst = nat.stream_ptr(dh3.device) if not on_side else ctypes.c_void_p(side.cuda_stream)
             nat.check(self._wgrad(k + 1, nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst),
                                   nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k],
-                                  ctypes.byref(bnb), st), f"conv_wgrad{k + 1}")
+                                  ctypes.byref(bnb), wst), f"conv_wgrad{k + 1}")
             if k > 0:
                 dx = self.dx[k - 1]
                 # ... and the previous layer's BN backward reduction fused into this dgrad's epilogue
@@ -174,6 +185,8 @@ class ConvStackHIP:
                                       self.chunks, self.spw, ctypes.byref(bnb),
                                       ctypes.byref(brd) if brd is not None else None, st), f"conv_dgrad{k + 1}")
                 dh, dh_bf = dx, int(self.dx_bf16)
+        if side is not None:
+            main.wait_stream(side)
         # the three weight-gradient slabs -> conv_w grads: queued on the caller's batch (one launch
         # for every slab reduction of the step phase) or launched here
         own = slabs is None

@@ -30,6 +30,44 @@ class StepGather:
         self.rowoff = torch.empty(U * B * E, device=dev, dtype=torch.int32)
         self.plane = 2 * H * W
 
+    def from_cursor(self, store, perm: torch.Tensor, cursor: torch.Tensor, done: torch.Tensor, hdce: bool = True,
+                    classifier: bool = True) -> None:
+        """Batch ``perm[*cursor : *cursor + B]`` (device cursor, int32 (1,)), then ``*cursor += B`` -- all
+        in the one launch, so the batch selection is part of a captured graph.  ``hdce`` fills x1 and
+        rowoff, ``classifier`` fills xq (two graphs on two streams each gather their half with their
+        own cursor).  ``done``: int32 (1,) zero-initialised scratch (last-workgroup counter)."""
+        Yp, HL = store.Yp, store.Hlabel
+        assert perm.dtype == torch.int64 and cursor.dtype == torch.int32 and done.dtype == torch.int32
+        cols = HL.shape[-1]
+        if Yp.is_cuda:
+            assert Yp.dtype == torch.float32 and Yp[0, 0].is_contiguous() and Yp.stride(1) == self.plane
+            assert HL.stride(1) == cols and HL.stride(0) % cols == 0 and store.Hperf.stride() == HL.stride()
+            assert perm.numel() == Yp.shape[1]
+            f = nat.fn(nat.hip_lib(), "qd_gather_cursor", [_p, _l, _p, _p, _p, _l, _p, _p, _p, _l, _i, _i, _i, _i, _p])
+            xq = self.xq if classifier else None
+            assert not classifier or xq is not None
+            nat.check(f(nat.ptr(perm), perm.numel(), nat.ptr(cursor), nat.ptr(done), nat.ptr(Yp), Yp.stride(0),
+                        nat.ptr(self.x1) if hdce else None, nat.ptr(xq) if xq is not None else None,
+                        nat.ptr(self.rowoff) if hdce else None, HL.stride(0) // cols, self.E, self.U, self.B,
+                        self.plane, nat.stream_ptr(Yp.device)), "gather_cursor")
+            return
+        c = int(cursor.item())
+        if c < 0 or c + self.B > perm.numel():
+            c = 0
+        idx = perm[c:c + self.B]
+        xq_saved = self.xq
+        if not classifier:
+            self.xq = None
+        try:
+            if hdce:
+                self(store, idx)
+            elif classifier:
+                g = Yp.index_select(1, idx)
+                self.xq.copy_(g.reshape(self.S * self.B, 2, self.H, self.W))
+        finally:
+            self.xq = xq_saved
+        cursor.fill_(c + self.B)
+
     def __call__(self, store, idx: torch.Tensor) -> None:
         Yp, HL = store.Yp, store.Hlabel
         S, N = Yp.shape[:2]

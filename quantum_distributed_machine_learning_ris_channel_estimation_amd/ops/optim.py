@@ -132,6 +132,10 @@ class FusedOptimizer:
         self.prune_thr = prune_thr
         dev = space.flat.device
         self.lr_t = torch.full((1,), lr, device=dev, dtype=torch.float32)
+        # parts: [lo, hi) ranges of the flat space stepped by separate launches (``step(part=i)``), each
+        # with its own step counter / done counter, so independent ranges can update on different
+        # streams as soon as their gradients are final (they always advance together: equal counts)
+        self.bounds: List[Tuple[int, int]] = [(0, space.numel)]
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
         self.pruned = torch.zeros(1, device=dev, dtype=torch.int32)
         self.done = torch.zeros(1, device=dev, dtype=torch.int32)   # last-workgroup counter (step tick)
@@ -148,6 +152,16 @@ class FusedOptimizer:
         self._lr_host = lr
         # torch.optim-like view for code that reads/writes param_groups[0]['lr']
         self.param_groups = [_LRGroup(self)]
+
+    def partition(self, cuts: Sequence[int]) -> None:
+        """Split the space at the (ALIGN-multiple) offsets ``cuts`` into independently launched parts."""
+        edges = [0] + sorted(int(c) for c in cuts) + [self.space.numel]
+        if any(e % 4 for e in edges) or any(a >= b for a, b in zip(edges, edges[1:])):
+            raise ValueError(f"bad partition {edges}")
+        self.bounds = list(zip(edges, edges[1:]))
+        dev = self.space.flat.device
+        self.step_t = self.step_t[:1].repeat(len(self.bounds)).contiguous()
+        self.done = torch.zeros(len(self.bounds), device=dev, dtype=torch.int32)
 
     def attach_shadow(self, lo: int, hi: int, fp8: Optional[Fp8Scales] = None, fp8_slot: int = 0) -> torch.Tensor:
         """Keep a bf16 copy of flat[lo:hi] up to date with every step (written by the update
@@ -184,35 +198,52 @@ class FusedOptimizer:
         self.lr_t.fill_(float(lr))
 
     # ---------------------------------------------------------------- step
-    def step(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None) -> None:
+    def step(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None, part: Optional[int] = None) -> None:
+        """One optimizer step over every part (``part=None``) or over part ``part`` only."""
         s = self.space
-        if s.flat.is_cuda:
-            lib = nat.hip_lib()
-            st = nat.stream_ptr(s.flat.device)
-            skp = nat.ptr(skip) if skip is not None else None
-            if self.kind == "sgd":
-                f = nat.fn(lib, "qd_sgd_step", [_p, _p, _p, _l, _p, _p, _p, _f, _f, _f, _p, _p])
-                nat.check(f(nat.ptr(s.flat), nat.ptr(s.grad), nat.ptr(self.buf), s.numel, nat.ptr(self.lr_t),
-                            nat.ptr(self.step_t), skp, self.momentum, self.weight_decay, grad_scale,
-                            nat.ptr(self.done), st), "sgd")
-                if self.shadow is not None:
-                    self.refresh_shadow()
-            else:
-                f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
-                                                 _p, _p, _l, _l, _p, _p, _p, _p])
-                f8 = self.shadow8 is not None
-                nat.check(f(nat.ptr(s.flat), nat.ptr(s.grad), nat.ptr(self.m), nat.ptr(self.v), s.numel,
-                            nat.ptr(self.lr_t), nat.ptr(self.step_t), skp, nat.ptr(self.pruned), self.betas[0],
-                            self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
-                            self.prune_thr, nat.ptr(self.done),
-                            nat.ptr(self.shadow) if self.shadow is not None else None, self.shadow_lo,
-                            self.shadow_hi, nat.ptr(self.shadow8) if f8 else None,
-                            nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
-                            nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, st), "adam")
+        if not s.flat.is_cuda:
+            if part not in (None, 0) and len(self.bounds) > 1:
+                # the CPU path steps the whole space at once: only the last part triggers it
+                if part != len(self.bounds) - 1:
+                    return
+            self._step_host(grad_scale, skip)
+            if self.shadow is not None:
+                self.refresh_shadow()
             return
-        self._step_host(grad_scale, skip)
-        if self.shadow is not None:
-            self.refresh_shadow()
+        parts = range(len(self.bounds)) if part is None else (part,)
+        for i in parts:
+            self._step_part(i, grad_scale, skip)
+
+    def _step_part(self, i: int, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
+        s = self.space
+        lo, hi = self.bounds[i]
+        lib = nat.hip_lib()
+        st = nat.stream_ptr(s.flat.device)
+        skp = nat.ptr(skip) if skip is not None else None
+        sp = lambda t: ctypes.c_void_p(t.data_ptr() + 4 * lo)
+        step_p, done_p = nat.ptr(self.step_t[i:]), nat.ptr(self.done[i:])
+        if self.kind == "sgd":
+            f = nat.fn(lib, "qd_sgd_step", [_p, _p, _p, _l, _p, _p, _p, _f, _f, _f, _p, _p])
+            nat.check(f(sp(s.flat), sp(s.grad), nat.ptr(self.buf[lo:]), hi - lo, nat.ptr(self.lr_t), step_p, skp,
+                        self.momentum, self.weight_decay, grad_scale, done_p, st), "sgd")
+            if self.shadow is not None:
+                self.refresh_shadow()
+            return
+        f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
+                                         _p, _p, _l, _l, _p, _p, _p, _p])
+        # the shadow range, clipped to this part and expressed relative to it
+        sh_lo, sh_hi = max(self.shadow_lo, lo), min(self.shadow_hi, hi)
+        has_sh = self.shadow is not None and sh_lo < sh_hi
+        f8 = has_sh and self.shadow8 is not None
+        sh_ptr = ctypes.c_void_p(self.shadow.data_ptr() + 2 * (sh_lo - self.shadow_lo)) \
+            if has_sh else None
+        sh8_ptr = ctypes.c_void_p(self.shadow8.data_ptr() + (sh_lo - self.shadow_lo)) if f8 else None
+        nat.check(f(sp(s.flat), sp(s.grad), nat.ptr(self.m[lo:]), nat.ptr(self.v[lo:]), hi - lo,
+                    nat.ptr(self.lr_t), step_p, skp, nat.ptr(self.pruned), self.betas[0],
+                    self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
+                    self.prune_thr, done_p, sh_ptr, (sh_lo - lo) if has_sh else 0, (sh_hi - lo) if has_sh else 0,
+                    sh8_ptr, nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
+                    nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, st), "adam")
 
     @torch.no_grad()
     def _step_host(self, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
@@ -230,13 +261,13 @@ class FusedOptimizer:
         lr = float(self.lr_t.item())
         if self.kind == "sgd":
             d = g + self.weight_decay * p if self.weight_decay else g
-            if self.step_t.item() == 0:
+            if self.step_t[0].item() == 0:
                 self.buf.copy_(d)
             else:
                 self.buf.mul_(self.momentum).add_(d)
             p.sub_(lr * self.buf)
         else:
-            t = float(self.step_t.item()) + 1.0
+            t = float(self.step_t[0].item()) + 1.0
             b1, b2 = self.betas
             if self.kind == "adamw":
                 p.mul_(1 - lr * self.weight_decay)
@@ -261,7 +292,7 @@ class FusedOptimizer:
 
     # ---------------------------------------------------------------- state
     def state_dict(self) -> Dict:
-        d = {"kind": self.kind, "lr": self._lr_host, "step": self.step_t.cpu(), "betas": self.betas, "eps": self.eps,
+        d = {"kind": self.kind, "lr": self._lr_host, "step": self.step_t[:1].cpu(), "betas": self.betas, "eps": self.eps,
              "weight_decay": self.weight_decay, "prune_thr": self.prune_thr}
         if self.kind == "sgd":
             d["buf"] = self.buf.cpu()
@@ -272,7 +303,7 @@ class FusedOptimizer:
     def load_state_dict(self, d: Dict) -> None:
         self.refresh_shadow()
         self.set_lr(d["lr"])
-        self.step_t.copy_(d["step"])
+        self.step_t.copy_(d["step"].reshape(-1)[:1].expand_as(self.step_t))
         if self.kind == "sgd":
             self.buf.copy_(d["buf"])
         else:

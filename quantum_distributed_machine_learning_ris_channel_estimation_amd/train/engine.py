@@ -264,6 +264,7 @@ class HDCEStep:
         self.grad_hook = grad_hook  # called as grad_hook("fc") / grad_hook("conv") when buckets are final
         self.hip = (dev.type == "cuda") if hip is None else hip
         self.writes_grads = self.hip
+        self.fc_side = None   # optional stream for the FC weight-gradient GEMM (HIP path)
         if self.hip:
             from ..ops.conv import ConvStackHIP
             self.conv = ConvStackHIP(model, n_users, batch)
@@ -307,11 +308,12 @@ class HDCEStep:
         return loss
 
     # Phase 2: conv/BN backward from dA.
-    def backward_conv(self, slabs=None) -> None:
+    def backward_conv(self, slabs=None, side=None) -> None:
         """``slabs``: queue the conv weight-gradient reductions on this ``SlabBatch`` (HIP path; the
-        caller launches it in overwrite mode)."""
+        caller launches it in overwrite mode).  ``side``: stream for the conv weight-gradient kernels
+        (see ConvStackHIP.backward)."""
         if self.hip:
-            self.conv.backward(self._dA, accumulate=False, slabs=slabs)
+            self.conv.backward(self._dA, accumulate=False, slabs=slabs, side=side)
         else:
             torch.autograd.backward(self._A, self._dA)
             self._A = None
@@ -337,7 +339,17 @@ class HDCEStep:
             Y = torch.nn.functional.linear(A.to(dt), W, b)
         loss = self.nmse.sums_finalize(Y, label, perf)
         dY = self.nmse.grad_bias(Y, label, m.fc_b.grad, out_dtype=dt)   # + bias grad, same pass
-        _mm_f32(dY.t(), A.to(dt), m.fc_w.grad)               # dW = dY^T A   (fp32 out)
+        A = A.to(dt)
+        side = self.fc_side
+        if side is not None:
+            # the weight-gradient GEMM runs beside the data-gradient GEMM (and the conv backward that
+            # follows it): both only read dY; the operands stay referenced (no allocator reuse)
+            self._keep = (dY, A)
+            side.wait_stream(torch.cuda.current_stream(A.device))
+            with torch.cuda.stream(side):
+                _mm_f32(dY.t(), A, m.fc_w.grad)               # dW = dY^T A   (fp32 out)
+        else:
+            _mm_f32(dY.t(), A, m.fc_w.grad)
         self._dA = torch.mm(dY, W)                             # (rows, 4096) bf16
         return loss
 

@@ -8,9 +8,21 @@ NLL, AdamW, optional QuantumNAT noise and gradient pruning) and the HDCE estimat
 optimizer, on HBM-resident synthetic data.
 
 Execution plan per step (world = 1): one HIP graph replay containing index gather,
-both forwards, the fused NMSE, both backwards and both optimizer kernels.
-World > 1: the same work eagerly, with the FC gradient bucket all-reduced on RCCL's
-stream while the conv/QSC backward still runs, then the small bucket, then the
+both forwards, the fused NMSE, both backwards and the optimizer kernels, captured from
+FOUR streams so the graph is a DAG, not a chain.  Almost every kernel of this model is
+latency-bound and fills a fraction of the 256 CUs, so independent work overlaps:
+
+  main : gather -> conv fwd x3 -> FC fwd GEMM -> NMSE -> FC dgrad GEMM -> conv bwd (dgrad
+         chain) -> conv slabs -> Adam(conv + BN part)
+  fc   :              (after NMSE) FC wgrad GEMM -> (after dgrad) Adam(FC part)
+  conv :                              (per layer) conv wgrad k=3, 2
+  qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
+         QSC bwd -> slabs -> AdamW
+
+The HDCE and the QSC have separate NaN-guard flags (``skip[0]``, ``skip[1]``), so neither
+optimizer waits for the other model's loss.
+World > 1: three graphs around the two gradient all-reduces (the FC bucket is reduced on
+RCCL's stream while the conv backward runs), the same streams inside each graph, then the
 optimizers (grad averaging fused into them).
 """
 from __future__ import annotations
@@ -47,6 +59,9 @@ class FlagshipConfig:
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
     split_graphs: bool = False   # force the 3-graph DP execution plan even at world 1 (testing)
+    stream_mode: str = "qsc"     # serial | dag | dagq | qsc | full (see FlagshipTrainer.__init__)
+    qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
+    steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     seed: int = 0
     n_scenarios: int = 3
     n_users: int = 3
@@ -70,69 +85,189 @@ class FlagshipTrainer:
         ctx.broadcast_(self.hdce.space.flat)
         ctx.broadcast_(self.qspace.flat)
         self.hopt = make_optimizer(self.hdce.space, "adam", cfg.lr)
+        sp = self.hdce.space
+        n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
+        self.hopt.partition([n_conv])           # part 0: conv + BN params, part 1: FC (own streams)
         self.hdce.attach_fc_shadow(self.hopt)   # after the broadcast: the shadow starts in sync
         self.qopt = make_optimizer(self.qspace, "adamw", cfg.lr, weight_decay=cfg.qsc_weight_decay,
                                    prune_thr=0.1 if cfg.use_gradient_pruning else 0.0)
-        sp = self.hdce.space
-        n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
         self.hstep = HDCEStep(self.hdce, self.U, self.B)
-        # NaN guard: the NMSE kernel sets the flag, the QSC head adds to it; it travels in the small
-        # bucket so every rank sees the same (summed) flag and skips -- or steps -- in lockstep
-        self.skip = self.hstep.skip
-        self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B, skip=self.skip)
+        # NaN guards: the NMSE kernel sets skip[0] (HDCE), the QSC head skip[1]; they travel in the
+        # small bucket so every rank sees the same (summed) flags and skips -- or steps -- in lockstep
+        self.skip = torch.zeros(2, device=dev, dtype=torch.float32)
+        self.hstep.nmse.skip = self.skip[0:1]
+        self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B,
+                                    skip=self.skip[1:2])
+        self.cstep.skip_add = False
         self.cstep.writes_grads = self.cstep.hip is not None
         # bucket "fc": 33.6 MB, ready first; bucket "small": conv + QSC grads + skip flag, coalesced
         self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]],
                                          "small": [sp.grad[:n_conv], self.qspace.grad, self.skip]})
-        self.idx = torch.zeros(self.B, dtype=torch.long, device=dev)
         self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)
+        # batch selection on the device: the gather kernels read perm[cur : cur + B] and advance cur
+        # themselves (cur[0]: HDCE / whole-step gather, cur[1]: the QSC graph's own gather); the host
+        # only tracks the epoch position to regenerate perm in place when it runs out
         self.perm = torch.randperm(self.store.n, device=dev)
-        self.cursor = 0
+        self.cur = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.cur_done = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.cursor = 0   # host mirror of the device cursors (position of the NEXT batch)
         # the loss kernels' own static buffers double as the step's loss outputs (no per-step copies)
         self.hloss = self.hstep.nmse.loss
         self.qloss = self.cstep.hip.loss if self.cstep.hip is not None else torch.zeros(1, device=dev)
         self.labels = self.store.scen.repeat_interleave(self.B)
-        self.slabs = SlabBatch()
+        self.qslabs = SlabBatch()
         graphs = cfg.hip_graphs and dev.type == "cuda"
-        if ctx.world == 1 and not cfg.split_graphs:
-            # one graph: gather, both forwards, NMSE, both backwards, both optimizers
-            self.graphs = [GraphedStep(self._step_body, enabled=graphs)]
+        # side streams (GPU).  stream_mode:
+        #   serial : one stream, one chain
+        #   dag    : ONE graph captured from 4 streams (qsc / fc / conv branches forked off the main chain)
+        #   dagq   : ONE graph, only the QSC branch forked; the HDCE a single chain
+        #   qsc    : the QSC branch is its own graph replayed on its own stream; HDCE one serial graph
+        #   full   : as qsc, and the HDCE graph has its fc / conv side branches
+        # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge
+        # that crosses queues costs a barrier packet, so fewer, longer branches can win)
+        mode = cfg.stream_mode
+        if mode not in ("serial", "dag", "dagq", "qsc", "full"):
+            raise ValueError(f"stream_mode {mode!r}")
+        self.streams = None
+        if dev.type == "cuda" and mode != "serial" and self.hstep.hip and self.cstep.hip is not None:
+            self.streams = {k: torch.cuda.Stream(dev) for k in ("qsc", "fc", "conv")}
         else:
+            mode = "serial"
+        self.mode = mode
+        self.hdce_side = mode in ("dag", "full")
+        self._use_graphs = graphs
+        self._graph_sets = {}            # steps per replay -> list of GraphedStep
+        self.graphs = self._graphs_for(1)
+
+    def _graphs_for(self, k: int):
+        """The graph set that runs ``k`` consecutive training steps per replay (world 1; the DP plan is
+        always one step).  Every step of a replay gathers its own batch through the device cursor, so a
+        k-step replay IS k training steps -- the graph boundary (and, in qsc/full mode, the stream
+        fork/join) is paid once per k steps, and the QSC stream runs k steps beside the HDCE's k."""
+        if k in self._graph_sets:
+            return self._graph_sets[k]
+        graphs, cfg, mode = self._use_graphs, self.cfg, self.mode
+
+        def rep(fn):
+            def body():
+                for _ in range(k):
+                    fn()
+            return body
+
+        if self.ctx.world == 1 and not cfg.split_graphs:
+            if mode in ("qsc", "full"):
+                # (separate memory pools: the two graphs replay CONCURRENTLY, so a block one of them
+                # freed during capture must not be handed to the other)
+                gs = [GraphedStep(rep(self._qsc_graph), enabled=graphs),
+                      GraphedStep(rep(lambda: self._hdce_graph(gather=True)), enabled=graphs)]
+            else:
+                # one graph: gather, both forwards, NMSE, both backwards, the optimizers
+                gs = [GraphedStep(rep(self._step_body), enabled=graphs)]
+        else:
+            if k != 1:
+                raise ValueError("multi-step graphs are a world-1 plan")
             # three graphs around the two gradient all-reduces; the FC bucket (33.6 MB) is reduced on
-            # RCCL's stream while graph 2 (conv + QSC backward) runs on the compute stream
+            # RCCL's stream while graph 2 (conv backward) runs on the compute stream
             pool = torch.cuda.graph_pool_handle() if graphs else None
-            self.graphs = [GraphedStep(f, enabled=graphs, pool=pool) for f in (self._phase1, self._phase2, self._phase3)]
+            gs = [GraphedStep(f, enabled=graphs, pool=pool) for f in (self._phase1, self._phase2, self._phase3)]
+        self._graph_sets[k] = gs
+        return gs
 
     # -- phases ---------------------------------------------------------------------------
-    def _phase1(self) -> None:
+    def _fork(self, s) -> "torch.cuda.StreamContext":
+        s.wait_stream(torch.cuda.current_stream(self.ctx.device))
+        return torch.cuda.stream(s)
+
+    def _join(self, names=("qsc", "fc", "conv")) -> None:
+        cur = torch.cuda.current_stream(self.ctx.device)
+        for n in names:
+            cur.wait_stream(self.streams[n])
+
+    def _gather(self, hdce: bool = True, classifier: bool = True) -> None:
         # the fused GPU kernels WRITE every gradient (one producer per element): no zero_grad fills
-        if not self.hstep.writes_grads:
+        if hdce and not self.hstep.writes_grads:
             self.hdce.space.zero_grad()
-        if not self.cstep.writes_grads:
+        if classifier and not self.cstep.writes_grads:
             self.qspace.zero_grad()
-        self.gat(self.store, self.idx)           # one launch: conv input, classifier input, label rows
+        # one launch: conv input, classifier input, label rows; batch = perm[cur : cur + B], cur += B
+        k = 0 if hdce else 1
+        self.gat.from_cursor(self.store, self.perm, self.cur[k:k + 1], self.cur_done[k:k + 1], hdce=hdce,
+                             classifier=classifier)
+
+    def _qsc_branch(self, with_opt: bool) -> None:
+        q = self.cstep(self.gat.xq, self.labels, slabs=self.qslabs if self.cstep.writes_grads else None)
+        if self.cstep.writes_grads:
+            self.qslabs.launch(accumulate=False, stream=nat.stream_ptr(self.ctx.device))
+        if q is not self.qloss:
+            self.qloss.copy_(q)
+        if with_opt:
+            self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.skip[1:2])
+
+    def _qsc_graph(self) -> None:
+        self._gather(hdce=False, classifier=True)
+        self._qsc_branch(with_opt=True)
+
+    def _hdce_forward(self) -> None:
+        self.hstep.fc_side = self.streams["fc"] if self.hdce_side else None
         loss = self.hstep.forward_fc_gathered(self.gat, self.store)
         if loss is not self.hloss:
             self.hloss.copy_(loss)
 
+    def _hdce_graph(self, gather: bool = False) -> None:
+        """HDCE forward + backward + Adam (world 1); ``gather``: its own batch gather first."""
+        if gather:
+            self._gather(hdce=True, classifier=False)
+        self._hdce_forward()
+        side = self.hdce_side
+        if side:
+            # FC Adam once the dgrad GEMM (which reads the bf16 weight shadow it rewrites) is queued
+            with self._fork(self.streams["fc"]):
+                self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=1)
+        self.hstep.backward_conv(side=self.streams["conv"] if side else None)
+        if side:
+            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=0)
+            self._join(("fc",))
+        else:
+            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1])
+
+    def _phase1(self) -> None:
+        """(DP) gather, QSC fwd+bwd (own stream), HDCE forward, NMSE, FC wgrad + dgrad."""
+        self._gather()
+        if self.streams is not None:
+            with self._fork(self.streams["qsc"]):
+                self._qsc_branch(with_opt=False)
+        self._hdce_forward()
+        if self.streams is not None:
+            self._join(("qsc", "fc") if self.hdce_side else ("qsc",))
+
     def _phase2(self) -> None:
-        # every gradient-slab reduction of the phase (3 conv weight slabs, the quantum layer's and the
-        # QSC preprocess slab) goes out as ONE launch when both steps write (overwrite) their grads
-        share = self.hstep.hip and self.cstep.hip is not None and self.cstep.writes_grads and self.hstep.writes_grads
-        slabs = self.slabs if share else None
-        self.hstep.backward_conv(slabs=slabs)
-        q = self.cstep(self.gat.xq, self.labels, slabs=slabs)
-        if slabs is not None:
-            slabs.launch(accumulate=False, stream=nat.stream_ptr(self.ctx.device))
-        if q is not self.qloss:
-            self.qloss.copy_(q)
+        """(DP) conv backward."""
+        self.hstep.backward_conv(side=self.streams["conv"] if self.hdce_side else None)
+        if self.streams is None:
+            self._qsc_branch(with_opt=False)
 
     def _phase3(self) -> None:
         g = 1.0 / self.ctx.world
-        self.hopt.step(grad_scale=g, skip=self.skip)
-        self.qopt.step(grad_scale=g, skip=self.skip)
+        if self.streams is None:
+            self.hopt.step(grad_scale=g, skip=self.skip[0:1])
+            self.qopt.step(grad_scale=g, skip=self.skip[1:2])
+            return
+        # the three updates are independent: FC Adam (bandwidth-bound, 8.4 M params) beside the rest
+        with self._fork(self.streams["fc"]):
+            self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=1)
+        with self._fork(self.streams["qsc"]):
+            self.qopt.step(grad_scale=g, skip=self.skip[1:2])
+        self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=0)
+        self._join(("qsc", "fc"))
 
     def _step_body(self) -> None:
+        if self.mode in ("dag", "dagq"):
+            self._gather()
+            with self._fork(self.streams["qsc"]):
+                self._qsc_branch(with_opt=True)
+            self._hdce_graph()
+            self._join(("qsc",))
+            return
         self._phase1()
         self.buckets.launch("fc")
         self._phase2()
@@ -140,23 +275,117 @@ class FlagshipTrainer:
         self.buckets.wait()
         self._phase3()
 
+    def mutable_state(self):
+        """Every tensor a step updates in place (weights, optimizer moments/counters, BN running
+        statistics, the fp8 scales, the QuantumNAT RNG counter)."""
+        ts = [self.hdce.space.flat, self.qspace.flat, self.hopt.step_t, self.qopt.step_t]
+        for o in (self.hopt, self.qopt):
+            ts += [o.m, o.v] if o.kind != "sgd" else [o.buf]
+        ts += list(self.hdce.run_mean) + list(self.hdce.run_var) + [self.hdce._nbt]
+        if self.hdce.fc_shadow is not None:
+            ts.append(self.hdce.fc_shadow)
+        if self.hopt.shadow8 is not None:
+            ts.append(self.hopt.shadow8)
+        if getattr(self.hdce, "fp8_scales", None) is not None:
+            f8 = self.hdce.fp8_scales
+            ts += [f8.scale, f8.qs, f8.amax]
+        if self.cstep.hip is not None:
+            ts.append(self.cstep.hip.noise_ctr)
+        return ts
+
+    def capture(self, preserve: bool = True, k: int = 1) -> None:
+        """Capture the ``k``-step graph set now.  Capturing runs warm-up steps; with ``preserve`` the
+        model/optimizer state is restored afterwards, so the first real step is step 1."""
+        gs = self._graphs_for(k)
+        if not any(g.enabled and g.graph is None for g in gs):
+            return
+        # the warm-up runs inside capture advance the device cursors: make room, restore them after
+        if self.cursor + (GraphedStep.WARMUP + 1) * k * self.B > self.store.n:
+            self._new_epoch()
+        if self.cursor + (GraphedStep.WARMUP + 1) * k * self.B > self.store.n:
+            raise ValueError(f"{k} steps per graph need more than the {self.store.n} samples per stream")
+        cur = self.cur.clone()
+        saved = [t.clone() for t in self.mutable_state()] if preserve else None
+        main = torch.cuda.current_stream(self.ctx.device)
+        for i, g in enumerate(gs):
+            if g.enabled and g.graph is None:
+                if len(gs) == 2 and i == 0:   # the QSC graph lives on its stream
+                    self.streams["qsc"].wait_stream(main)
+                    with torch.cuda.stream(self.streams["qsc"]):
+                        g.capture()
+                    main.wait_stream(self.streams["qsc"])
+                else:
+                    g.capture()
+        if saved is not None:
+            for t, c in zip(self.mutable_state(), saved):
+                t.copy_(c)
+        self.cur.copy_(cur)
+
     @property
     def graphed(self) -> GraphedStep:
         return self.graphs[0]
 
-    def next_batch(self) -> None:
-        if self.cursor + self.B > self.store.n:
-            self.perm = torch.randperm(self.store.n, device=self.ctx.device)
-            self.cursor = 0
-        self.idx.copy_(self.perm[self.cursor:self.cursor + self.B])
-        self.cursor += self.B
+    def _new_epoch(self) -> None:
+        # in place: the graphs hold its address; the previous replays were joined on this stream
+        torch.randperm(self.store.n, device=self.ctx.device, out=self.perm)
+        self.cur.zero_()
+        self.cursor = 0
+
+    def next_batch(self, k: int = 1) -> None:
+        """Advance the host mirror of the batch cursor by ``k`` batches; when the permutation cannot
+        hold them, draw a new one and re-arm the device cursors (the short tail is dropped)."""
+        if self.cursor + k * self.B > self.store.n:
+            self._new_epoch()
+        self.cursor += k * self.B
 
     def step(self) -> None:
-        self.next_batch()
-        if len(self.graphs) == 1:
-            self.graphs[0]()
+        """One training step."""
+        self._replay(1)
+
+    def _k(self) -> int:
+        return max(1, self.cfg.steps_per_graph) if (self.ctx.world == 1 and not self.cfg.split_graphs) else 1
+
+    def prepare(self, n: int) -> None:
+        """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""
+        k = self._k()
+        if n // k:
+            self.capture(preserve=False, k=k)
+        if n % k:
+            self.capture(preserve=False, k=1)
+
+    def run(self, n: int) -> None:
+        """``n`` training steps, ``cfg.steps_per_graph`` per graph replay (the remainder one by one)."""
+        k = self._k()
+        for _ in range(n // k):
+            self._replay(k)
+        for _ in range(n % k):
+            self._replay(1)
+
+    def _replay(self, k: int) -> None:
+        gs = self._graphs_for(k)
+        if any(g.enabled and g.graph is None for g in gs):
+            self.capture(preserve=False, k=k)
+        self.next_batch(k)
+        if len(gs) == 1:
+            gs[0]()
             return
-        g1, g2, g3 = self.graphs
+        if len(gs) == 2:
+            # world 1, qsc / full: the QSC graph on its own stream beside the HDCE graph (each gathers
+            # its own inputs); the HDCE graph (the critical path) is enqueued first unless qsc_first
+            gq, gh = gs
+            q = self.streams["qsc"]
+            q.wait_stream(torch.cuda.current_stream(self.ctx.device))
+            if self.cfg.qsc_first:
+                with torch.cuda.stream(q):
+                    gq()
+                gh()
+            else:
+                gh()
+                with torch.cuda.stream(q):
+                    gq()
+            self._join(("qsc",))
+            return
+        g1, g2, g3 = gs
         g1()
         self.buckets.launch("fc")
         g2()

@@ -82,10 +82,12 @@ class GraphedStep:
     replays.  With ``enabled=False`` it simply calls ``fn`` (eager).
     """
 
-    def __init__(self, fn: Callable[[], None], enabled: bool = True, warmup: int = 3, pool=None):
+    WARMUP = 3
+
+    def __init__(self, fn: Callable[[], None], enabled: bool = True, warmup: Optional[int] = None, pool=None):
         self.fn = fn
         self.enabled = enabled and torch.cuda.is_available()
-        self.warmup = warmup
+        self.warmup = self.WARMUP if warmup is None else warmup
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.pool = pool
 

@@ -42,8 +42,23 @@ def from_trace(path, marker, per_step, tail, top):
         a[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     tot = sum(v[1] for v in agg.values())
     span = int(rows[-1]["Start_Timestamp"]) - int(rows[0]["Start_Timestamp"])
+    # union of the kernel intervals: with a multi-stream graph kernels overlap, so the sum of
+    # kernel times ("kernel time") exceeds the time the GPU had any kernel running ("busy")
+    busy, cur_s, cur_e = 0, None, None
+    for r in rows:
+        s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if cur_e is None or s0 > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s0, e0
+        else:
+            cur_e = max(cur_e, e0)
+    if cur_e is not None:
+        busy += cur_e - cur_s
     print(f"steady-state window: {steps:.0f} steps, wall {span / 1e3 / steps:.1f} us/step, "
-          f"GPU busy {tot / 1e3 / steps:.1f} us/step, {sum(v[0] for v in agg.values()) / steps:.0f} launches/step\n")
+          f"GPU busy (interval union) {busy / 1e3 / steps:.1f} us/step, summed kernel time "
+          f"{tot / 1e3 / steps:.1f} us/step (overlap x{tot / max(busy, 1):.2f}), "
+          f"{sum(v[0] for v in agg.values()) / steps:.0f} launches/step\n")
     print("| us/step | calls/step | avg us | % | kernel |\n|---|---|---|---|---|")
     for name, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
         print(f"| {t / 1e3 / steps:.1f} | {c / steps:.2f} | {t / c / 1e3:.1f} | {t / tot * 100:.1f} | `{name[:110]}` |")
@@ -54,8 +69,8 @@ def main():
     ap.add_argument("path")
     ap.add_argument("steps", nargs="?", type=float, default=1.0)
     ap.add_argument("top_pos", nargs="?", type=int, default=None)
-    ap.add_argument("--marker", default="adam_kernel")
-    ap.add_argument("--per-step", type=float, default=2.0)
+    ap.add_argument("--marker", default="gather_step_kernel")
+    ap.add_argument("--per-step", type=float, default=1.0)
     ap.add_argument("--tail", type=float, default=0.5)
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()

@@ -40,7 +40,7 @@ def main(out):
     skipped = torch.equal(before, after)
     ok.append(same_on_all_ranks(after))
     with open(f"{out}.{ctx.rank}", "w") as f:
-        f.write(f"{int(all(ok))} {int(skipped)} {float(tr.skip.item())}\n")
+        f.write(f"{int(all(ok))} {int(skipped)} {float(tr.skip.sum().item())}\n")
     shutdown()
 
 

@@ -210,6 +210,34 @@ def test_step_gather_hip_matches_host(cuda):
     assert torch.equal(d.Hlabel.cpu()[o // sr, o % sr], tr.Hlabel[oh // sr_h, oh % sr_h])
 
 
+def test_gather_device_cursor(cuda):
+    """qd_gather_cursor: batch = perm[*cur : *cur + B] and *cur advances by B in-kernel (last-workgroup
+    protocol), for the HDCE half (x1 + rowoff) and the classifier half (xq) with separate cursors."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.data.datasets import make_dml_stores
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.gather import StepGather
+    st, _ = make_dml_stores(60, 128, 10, 0.9, "cpu", synthetic=True, base_seed=5)
+    d = st.to(cuda)
+    B = 7
+    perm = torch.randperm(d.n, device=cuda)
+    cur = torch.zeros(2, dtype=torch.int32, device=cuda)
+    done = torch.zeros(2, dtype=torch.int32, device=cuda)
+    g = StepGather(3, 3, B, 16, 8, cuda)
+    ref = StepGather(3, 3, B, 16, 8, cuda)
+    for k in range(5):
+        g.from_cursor(d, perm, cur[0:1], done[0:1], hdce=True, classifier=False)
+        g.from_cursor(d, perm, cur[1:2], done[1:2], hdce=False, classifier=True)
+        ref(d, perm[k * B:(k + 1) * B].contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(g.x1, ref.x1) and torch.equal(g.xq, ref.xq) and torch.equal(g.rowoff, ref.rowoff), k
+        assert cur.tolist() == [(k + 1) * B] * 2 and done.tolist() == [0, 0]
+    # an exhausted cursor never reads past the permutation: it restarts at 0
+    cur.fill_(d.n - 3)
+    g.from_cursor(d, perm, cur[0:1], done[0:1], hdce=True, classifier=True)
+    ref(d, perm[:B].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(g.x1, ref.x1) and int(cur[0]) == B
+
+
 def test_fused_optimizer_tick_and_shadow(cuda):
     """Step counter ticks exactly once per launch (last-workgroup pattern) across many workgroups,
     never on a skipped step, and the bf16 shadow tracks the updated weights."""
