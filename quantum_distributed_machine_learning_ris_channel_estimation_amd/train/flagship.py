@@ -43,6 +43,27 @@ from ..utils.profiling import GraphedStep
 from .engine import ClassifierStep, HDCEModel, HDCEStep
 
 
+import os
+
+# hipBLASLt / rocBLAS solution choices for the FC GEMMs, picked on an MI355X by scripts/tune_gemm.py
+# (PyTorch TunableOp); replayed without tuning when present
+TUNABLEOP_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
+                              "tunableop_gfx950.csv")
+
+
+def use_tuned_gemms(path: str = TUNABLEOP_FILE) -> bool:
+    """Replay the stored TunableOp GEMM choices (no tuning at run time).  Returns whether enabled."""
+    if not os.path.exists(path):
+        return False
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.record_untuned_enable(False)
+    tun.set_filename(path, insert_device_ordinal=False)
+    tun.read_file(path)
+    return True
+
+
 @dataclass
 class FlagshipConfig:
     pilot_num: int = 128
@@ -62,6 +83,7 @@ class FlagshipConfig:
     stream_mode: str = "qsc"     # serial | dag | dagq | qsc | full (see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
+    tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
     n_scenarios: int = 3
     n_users: int = 3
@@ -71,6 +93,7 @@ class FlagshipTrainer:
     def __init__(self, cfg: FlagshipConfig, ctx: DistContext):
         self.cfg, self.ctx = cfg, ctx
         dev = ctx.device
+        self.tuned_gemms = dev.type == "cuda" and cfg.tunableop and use_tuned_gemms()
         self.store, _ = make_dml_stores(cfg.data_len, cfg.pilot_num, cfg.snr_db, 0.9, dev, synthetic=True,
                                         base_seed=cfg.seed + 1000 * ctx.rank, n_scenarios=cfg.n_scenarios,
                                         n_users=cfg.n_users)
