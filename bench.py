@@ -43,7 +43,7 @@ def main() -> int:
     ap.add_argument("--steps-per-graph", type=int, default=1,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
-    ap.add_argument("--stream-mode", default="qsc", choices=["serial", "dag", "dagq", "qsc", "full"],
+    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "qsc", "full"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
                          "or a separate QSC graph on its own stream (+ HDCE side branches with 'full')")
     args = ap.parse_args()

@@ -212,10 +212,230 @@ __global__ void __launch_bounds__(256) grad_bias_kernel(const TY* __restrict__ Y
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// One-pass loss + gradient for the grouped estimator's row order r = (u*B + b)*E + e (stream
+// s = e*U + u), labels read in place through rowoff.  The gradient coefficient 2/(S*den_s) only
+// needs den_s = sum |label|^2 over the stream's rows, which is known BEFORE Y: every block sums
+// the precomputed per-row label powers (rowpow_l[rowoff[r]], dataset-constant) of its u-block's
+// E streams itself, in a fixed order (bitwise identical in every block).  So one pass over
+// (Y, label, perf) writes dY, the FC bias-gradient column partials, and the per-stream error
+// partials; nmse_finish_kernel then forms loss / loss_perf / skip and sums the bias partials.
+//
+// block (bx, by): columns 4*(256*bx + t) .. +3, rows [by*rpc, (by+1)*rpc) -- rpc a multiple of E
+// dividing B*E, so a chunk lies in one u-block and walks its rows in e-triples (static indices).
+// part: (gridDim.y, gridDim.x, E, 2) fp32 = (sum err^2, sum errperf^2) of the block per e.
+// dens: (S, 2) = (den, den_perf), written by the blocks with bx == 0 and by at a u-block start.
+template <typename TY, typename TD, int E>
+__global__ void __launch_bounds__(256) nmse_fused_kernel(const TY* __restrict__ Y, const float* __restrict__ Lb,
+                                                         const float* __restrict__ Pf, const int* __restrict__ rowoff,
+                                                         const float* __restrict__ rowpow_l,
+                                                         const float* __restrict__ rowpow_p, TD* __restrict__ dY,
+                                                         float* __restrict__ colsum, float* __restrict__ part,
+                                                         float* __restrict__ dens, int cols, int B, int U, int rpc,
+                                                         float loss_scale) {
+  __shared__ float sden[2 * E];
+  __shared__ float sred[4][2 * E];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int r0 = blockIdx.y * rpc;
+  const int u = r0 / (B * E);
+  const int S = E * U;
+  // per-stream label powers of this u-block (wave e: stream e*U + u), fixed order
+  for (int e = wv; e < E; e += 4) {
+    float a = 0.f, ap = 0.f;
+    for (int b = lane; b < B; b += 64) {
+      const int ro = rowoff[(u * B + b) * E + e];
+      a += rowpow_l[ro];
+      ap += Pf ? rowpow_p[ro] : 0.f;
+    }
+    a = wave_sum(a);
+    ap = wave_sum(ap);
+    if (lane == 0) {
+      sden[e] = a;
+      sden[E + e] = ap;
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && r0 % (B * E) == 0 && t < E) {
+    dens[(t * U + u) * 2 + 0] = sden[t];
+    dens[(t * U + u) * 2 + 1] = sden[E + t];
+  }
+  float coef[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) coef[e] = loss_scale * 2.f / ((float)S * sden[e]);
+  const int c0 = (blockIdx.x * 256 + t) * 4;
+  float num[E], nump[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) num[e] = nump[e] = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c0 < cols) {
+    for (int rb = r0; rb < r0 + rpc; rb += E) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int r = rb + e;
+        const size_t ey = (size_t)r * cols + c0;
+        const size_t le = (size_t)rowoff[r] * cols + c0;
+        const float4 yv = load4<TY>(Y + ey);
+        const float4 lv = *reinterpret_cast<const float4*>(Lb + le);
+        const float d0 = yv.x - lv.x, d1 = yv.y - lv.y, d2 = yv.z - lv.z, d3 = yv.w - lv.w;
+        num[e] += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+        if (Pf) {
+          const float4 pv = *reinterpret_cast<const float4*>(Pf + le);
+          const float q0 = yv.x - pv.x, q1 = yv.y - pv.y, q2 = yv.z - pv.z, q3 = yv.w - pv.w;
+          nump[e] += q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;
+        }
+        const float c = coef[e];
+        const float g0 = c * d0, g1 = c * d1, g2 = c * d2, g3 = c * d3;
+        acc.x += g0;
+        acc.y += g1;
+        acc.z += g2;
+        acc.w += g3;
+        if constexpr (std::is_same<TD, float>::value) {
+          *reinterpret_cast<float4*>(dY + ey) = make_float4(g0, g1, g2, g3);
+        } else {
+          ushort4 h;
+          h.x = f32_to_bf16(g0);
+          h.y = f32_to_bf16(g1);
+          h.z = f32_to_bf16(g2);
+          h.w = f32_to_bf16(g3);
+          *reinterpret_cast<ushort4*>(dY + ey) = h;
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(colsum + (size_t)blockIdx.y * cols + c0) = acc;
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float a = wave_sum(num[e]), b = wave_sum(nump[e]);
+    if (lane == 0) {
+      sred[wv][2 * e] = a;
+      sred[wv][2 * e + 1] = b;
+    }
+  }
+  __syncthreads();
+  if (t < 2 * E) {
+    const float v = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
+    part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 * E + t] = v;
+  }
+}
+
+// blocks 0 .. cols/64-1: 64 bias-gradient columns each (16 threads x float4 per row, 16 row groups,
+// fixed-order LDS combine: deterministic); the LAST block's first wave reduces the error partials
+// per stream and finalises loss, loss_perf and skip.
+template <int E>
+__global__ void __launch_bounds__(256) nmse_finish_kernel(const float* __restrict__ colsum,
+                                                          const float* __restrict__ part,
+                                                          const float* __restrict__ dens, float* __restrict__ bias_grad,
+                                                          float* __restrict__ ss, float* __restrict__ loss,
+                                                          float* __restrict__ skip, int chunks, int gx, int cols,
+                                                          int chunks_per_u, int U) {
+  __shared__ float4 red[16][16];
+  if (blockIdx.x < gridDim.x - 1) {
+    const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int c = blockIdx.x * 64 + tq * 4;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    int k = ty;
+    for (; k + 16 < chunks; k += 32) {   // two independent loads in flight per thread
+      const float4 v = *reinterpret_cast<const float4*>(colsum + (size_t)k * cols + c);
+      const float4 w = *reinterpret_cast<const float4*>(colsum + (size_t)(k + 16) * cols + c);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      b.x += w.x; b.y += w.y; b.z += w.z; b.w += w.w;
+    }
+    if (k < chunks) {
+      const float4 v = *reinterpret_cast<const float4*>(colsum + (size_t)k * cols + c);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    red[ty][tq] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    __syncthreads();
+    if (threadIdx.x < 16) {
+      float4 o = red[0][threadIdx.x];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) {
+        const float4 v = red[j][threadIdx.x];
+        o.x += v.x; o.y += v.y; o.z += v.z; o.w += v.w;
+      }
+      *reinterpret_cast<float4*>(bias_grad + blockIdx.x * 64 + threadIdx.x * 4) = o;
+    }
+    return;
+  }
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  const int S = E * U;
+  float l = 0.f, lp = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const int e = s / U, u = s % U;
+    float n = 0.f, np = 0.f;
+    for (int j = lane; j < chunks_per_u * gx; j += 64) {
+      const int k = u * chunks_per_u + j / gx, x = j % gx;
+      const float* p = part + ((size_t)k * gx + x) * 2 * E + 2 * e;
+      n += p[0];
+      np += p[1];
+    }
+    n = wave_sum(n);
+    np = wave_sum(np);
+    const float den = dens[s * 2], denp = dens[s * 2 + 1];
+    if (lane == 0) {
+      ss[s * 4 + 0] = n;
+      ss[s * 4 + 1] = den;
+      ss[s * 4 + 2] = np;
+      ss[s * 4 + 3] = denp;
+    }
+    l += n / den;
+    lp += denp > 0.f ? np / denp : 0.f;
+  }
+  if (lane == 0) {
+    loss[0] = l / (float)S;
+    loss[1] = lp / (float)S;
+    if (skip) *skip = isfinite(loss[0]) ? 0.f : 1.f;
+  }
+}
+
 }  // namespace nmse
 }  // namespace qd
 
 using namespace qd::nmse;
+
+// One-pass NMSE + dY + bias gradient (see nmse_fused_kernel).  rows = U*B*E; rpc % E == 0 and
+// (B*E) % rpc == 0; cols % 1024 == 0.  colsum: (rows/rpc, cols); part: (rows/rpc, cols/1024, E, 2);
+// dens: (S, 2); ss: (S, 4) as qd_nmse_reduce_finalize's.  perf / rowpow_p nullable together.
+QD_API int qd_nmse_fused(const void* Y, int y_bf16, const float* label, const float* perf, const int* rowoff,
+                         const float* rowpow_l, const float* rowpow_p, void* dY, int dy_bf16, float* colsum,
+                         float* part, float* dens, float* bias_grad, float* ss, float* loss, float* skip, int E, int U,
+                         int B, int cols, int rpc, float loss_scale, void* stream) {
+  if (cols % 1024 || rpc < E || rpc % E || (B * E) % rpc || (perf == nullptr) != (rowpow_p == nullptr))
+    return (int)hipErrorInvalidValue;
+  const int rows = U * B * E;
+  dim3 grid(cols / 1024, rows / rpc);
+  hipStream_t st = (hipStream_t)stream;
+#define QD_F(TY, TD, EE)                                                                                            \
+  hipLaunchKernelGGL((nmse_fused_kernel<TY, TD, EE>), grid, dim3(256), 0, st, (const TY*)Y, label, perf, rowoff,     \
+                     rowpow_l, rowpow_p, (TD*)dY, colsum, part, dens, cols, B, U, rpc, loss_scale)
+#define QD_E(EE)                                          \
+  if (y_bf16 && dy_bf16) QD_F(uint16_t, uint16_t, EE);    \
+  else if (y_bf16) QD_F(uint16_t, float, EE);             \
+  else if (dy_bf16) QD_F(float, uint16_t, EE);            \
+  else QD_F(float, float, EE);
+  switch (E) {
+    case 1: QD_E(1) break;
+    case 2: QD_E(2) break;
+    case 3: QD_E(3) break;
+    case 4: QD_E(4) break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef QD_E
+#undef QD_F
+  const int chunks = rows / rpc;
+#define QD_N(EE)                                                                                                   \
+  hipLaunchKernelGGL((nmse_finish_kernel<EE>), dim3(cols / 64 + 1), dim3(256), 0, st, colsum, part, dens, bias_grad, ss, \
+                     loss, skip, chunks, (int)grid.x, cols, (B * E) / rpc, U)
+  switch (E) {
+    case 1: QD_N(1); break;
+    case 2: QD_N(2); break;
+    case 3: QD_N(3); break;
+    default: QD_N(4); break;
+  }
+#undef QD_N
+  return (int)hipGetLastError();
+}
 
 // dY as qd_nmse_grad, plus colsum (chunks, cols) = per-row-chunk column sums of dY (bias gradient
 // partials).  cols % 4 == 0.

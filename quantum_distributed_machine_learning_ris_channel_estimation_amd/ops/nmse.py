@@ -42,6 +42,7 @@ class StreamNMSE:
         self.coef = torch.zeros(n_streams, device=dev)
         self.skip = torch.zeros(1, device=dev, dtype=torch.float32)  # NaN guard flag (all-reduced in DP)
         self._rs_long = self.row_stream.long()
+        self.rpc_mult = 2   # fused path: rows per block = E * rpc_mult (scripts/probe_nmse.py)
         self.rowoff: Optional[torch.Tensor] = None
         # CSR list of each stream's rows (stable order) for the one-launch reduce + finalize
         self.order = torch.sort(self._rs_long, stable=True).indices.to(torch.int32)
@@ -156,6 +157,52 @@ class StreamNMSE:
                     self.cols, st), "nmse_grad_bias")
         ssum = nat.fn(lib, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _i, _p])
         nat.check(ssum(nat.ptr(self._colsum), nat.ptr(bias_grad), 1, chunks, self.cols, 0, st), "bias_grad_sum")
+        return dY
+
+    # ------------------------------------------------------------------ one-pass GPU path
+    def _row_powers(self, t: torch.Tensor) -> torch.Tensor:
+        """sum |row|^2 of every row of a (S, N, cols) store view, laid out in rowoff's row space
+        (s * stride0/cols + n) -- dataset constants, computed once per store."""
+        key = (t.data_ptr(), tuple(t.shape), tuple(t.stride()))
+        cache = self.__dict__.setdefault("_rowpow", {})
+        if key not in cache:
+            S, N, cols = t.shape
+            sr = t.stride(0) // cols
+            out = torch.zeros(S * sr, device=t.device, dtype=torch.float32)
+            out.view(S, sr)[:, :N] = t.float().pow(2).sum(-1)
+            cache[key] = out
+        return cache[key]
+
+    def fused(self, Y: torch.Tensor, label: torch.Tensor, perf: Optional[torch.Tensor], bias_grad: torch.Tensor,
+              layout: Tuple[int, int, int], out_dtype=torch.bfloat16, loss_scale: float = 1.0,
+              rpc_mult: Optional[int] = None) -> torch.Tensor:
+        """GPU, labels through ``rowoff``, rows in (u, b, e) order with ``layout`` = (E, U, B): loss,
+        loss_perf, skip, dY and the bias gradient (overwritten into ``bias_grad``) in TWO launches
+        (csrc/hip/nmse.hip qd_nmse_fused).  Returns dY; the loss is ``self.loss``."""
+        E, U, B = layout
+        assert Y.is_cuda and self.rowoff is not None and Y.shape == (self.rows, self.cols) and self.rows == E * U * B
+        self._check_labels(label)
+        if perf is not None:
+            self._check_labels(perf)
+        m = rpc_mult or self.rpc_mult
+        rpc = E * m if (B * E) % (E * m) == 0 else E
+        chunks, gx = self.rows // rpc, self.cols // 1024
+        dev = Y.device
+        if getattr(self, "_fz", None) is None or self._fz[0] != (rpc, out_dtype):
+            self._fz = ((rpc, out_dtype), torch.empty(chunks, self.cols, device=dev),
+                        torch.empty(chunks * gx * E * 2, device=dev), torch.empty(self.S, 2, device=dev),
+                        torch.empty(self.rows, self.cols, device=dev, dtype=out_dtype))
+        _, colsum, part, dens, dY = self._fz
+        rl = self._row_powers(label)
+        rp = self._row_powers(perf) if perf is not None else None
+        f = nat.fn(nat.hip_lib(), "qd_nmse_fused", [_p, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p,
+                                                    _i, _i, _i, _i, _i, _f, _p])
+        nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label),
+                    nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowoff), nat.ptr(rl),
+                    nat.ptr(rp) if rp is not None else None, nat.ptr(dY), int(out_dtype == torch.bfloat16),
+                    nat.ptr(colsum), nat.ptr(part), nat.ptr(dens), nat.ptr(bias_grad), nat.ptr(self.ss),
+                    nat.ptr(self.loss), nat.ptr(self.skip), E, U, B, self.cols, rpc, loss_scale,
+                    nat.stream_ptr(dev)), "nmse_fused")
         return dY
 
     def __call__(self, Y, label, perf=None, out_dtype=torch.float32) -> Tuple[torch.Tensor, torch.Tensor]:

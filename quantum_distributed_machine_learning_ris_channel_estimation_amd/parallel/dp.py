@@ -88,13 +88,15 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
     local = int(os.environ.get("LOCAL_RANK", 0))
     use_cuda = (device in ("auto", "cuda")) and torch.cuda.is_available()
     if use_cuda:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        # (QDML_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs: ranks share devices)
+        local_dev = local % torch.cuda.device_count()
+        torch.cuda.set_device(local_dev)
+        dev = torch.device("cuda", local_dev)
     else:
         dev = torch.device("cpu")
     backend = "none"
     if world > 1:
-        backend = "nccl" if use_cuda else "gloo"
+        backend = os.environ.get("QDML_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {}
         if backend == "nccl":
@@ -133,7 +135,7 @@ class GradBuckets:
         for k, ts in self.buckets.items():
             if len(ts) > 1:
                 self.staging[k] = torch.empty(sum(t.numel() for t in ts), device=ts[0].device, dtype=ts[0].dtype)
-        self.pending: List = []
+        self.pending: Dict[str, list] = {}
 
     def bucket_bytes(self) -> Dict[str, int]:
         return {k: sum(t.numel() * t.element_size() for t in ts) for k, ts in self.buckets.items()}
@@ -144,27 +146,33 @@ class GradBuckets:
         ts = self.buckets[name]
         if len(ts) == 1:
             work = dist.all_reduce(ts[0], async_op=True)
-            self.pending.append((work, None, None))
+            self.pending[name] = [work, None, None]
         else:
             st = self.staging[name]
             torch.cat([t.reshape(-1) for t in ts], out=st)
             work = dist.all_reduce(st, async_op=True)
-            self.pending.append((work, st, ts))
+            self.pending[name] = [work, st, ts]
 
     def launch_all(self) -> None:
         for k in self.buckets:
             self.launch(k)
 
-    def wait(self) -> None:
-        for work, st, ts in self.pending:
-            work.wait()
-            if st is not None:
+    def wait(self, names: Optional[Sequence[str]] = None) -> None:
+        """Make the CURRENT stream wait for the named (default: all) launched collectives; a coalesced
+        bucket is scattered back (once) on the first stream that waits for it.  A bucket may be waited
+        for from several streams."""
+        for k in list(self.pending) if names is None else [n for n in names if n in self.pending]:
+            ent = self.pending[k]
+            ent[0].wait()
+            if ent[1] is not None:
                 o = 0
-                for t in ts:
+                for t in ent[2]:
                     n = t.numel()
-                    t.view(-1).copy_(st[o:o + n])
+                    t.view(-1).copy_(ent[1][o:o + n])
                     o += n
-        self.pending.clear()
+                ent[1] = None
+        if names is None:
+            self.pending.clear()
 
 
 class DeviceSampler:

@@ -265,6 +265,8 @@ class HDCEStep:
         self.hip = (dev.type == "cuda") if hip is None else hip
         self.writes_grads = self.hip
         self.fc_side = None   # optional stream for the FC weight-gradient GEMM (HIP path)
+        self.fused_nmse = True  # HIP path: the one-pass NMSE (qd_nmse_fused) when labels come via rowoff
+        self.defer_dgrad = False
         if self.hip:
             from ..ops.conv import ConvStackHIP
             self.conv = ConvStackHIP(model, n_users, batch)
@@ -337,8 +339,13 @@ class HDCEStep:
             m.fp8_scales.update()
         else:
             Y = torch.nn.functional.linear(A.to(dt), W, b)
-        loss = self.nmse.sums_finalize(Y, label, perf)
-        dY = self.nmse.grad_bias(Y, label, m.fc_b.grad, out_dtype=dt)   # + bias grad, same pass
+        if self.nmse.rowoff is not None and self.fused_nmse and self.nmse.cols % 1024 == 0:
+            # one pass: loss, skip, dY, bias-gradient partials (+ one finish launch)
+            dY = self.nmse.fused(Y, label, perf, m.fc_b.grad, (m.E, self.U, self.B), out_dtype=dt)
+            loss = self.nmse.loss
+        else:
+            loss = self.nmse.sums_finalize(Y, label, perf)
+            dY = self.nmse.grad_bias(Y, label, m.fc_b.grad, out_dtype=dt)   # + bias grad, same pass
         A = A.to(dt)
         side = self.fc_side
         if side is not None:
@@ -350,8 +357,16 @@ class HDCEStep:
                 _mm_f32(dY.t(), A, m.fc_w.grad)               # dW = dY^T A   (fp32 out)
         else:
             _mm_f32(dY.t(), A, m.fc_w.grad)
-        self._dA = torch.mm(dY, W)                             # (rows, 4096) bf16
+        self._dYW = (dY, W)
+        if not self.defer_dgrad:
+            self.dgrad()
         return loss
+
+    def dgrad(self) -> None:
+        """dA = dY W (HIP path): issued by the forward unless ``defer_dgrad`` (the DP plan issues it
+        after the FC gradient all-reduce is on its way)."""
+        dY, W = self._dYW
+        self._dA = torch.mm(dY, W)                             # (rows, 4096) bf16
 
     @property
     def skip(self) -> torch.Tensor:

@@ -80,7 +80,7 @@ class FlagshipConfig:
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
     split_graphs: bool = False   # force the 3-graph DP execution plan even at world 1 (testing)
-    stream_mode: str = "qsc"     # serial | dag | dagq | qsc | full (see FlagshipTrainer.__init__)
+    stream_mode: str = "dagq"    # serial | dag | dagq (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
@@ -123,9 +123,10 @@ class FlagshipTrainer:
                                     skip=self.skip[1:2])
         self.cstep.skip_add = False
         self.cstep.writes_grads = self.cstep.hip is not None
-        # bucket "fc": 33.6 MB, ready first; bucket "small": conv + QSC grads + skip flag, coalesced
-        self.buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]],
-                                         "small": [sp.grad[:n_conv], self.qspace.grad, self.skip]})
+        # buckets (see _dp_run): "skip" = the HDCE NaN flag, "fc" = 33.6 MB FC grads (in place), "small"
+        # = conv/BN + QSC grads + the QSC NaN flag (coalesced)
+        self.buckets = GradBuckets(ctx, {"skip": [self.skip[0:1]], "fc": [sp.grad[n_conv:]],
+                                         "small": [sp.grad[:n_conv], self.qspace.grad, self.skip[1:2]]})
         self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)
         # batch selection on the device: the gather kernels read perm[cur : cur + B] and advance cur
         # themselves (cur[0]: HDCE / whole-step gather, cur[1]: the QSC graph's own gather); the host
@@ -146,11 +147,18 @@ class FlagshipTrainer:
         #   dagq   : ONE graph, only the QSC branch forked; the HDCE a single chain
         #   qsc    : the QSC branch is its own graph replayed on its own stream; HDCE one serial graph
         #   full   : as qsc, and the HDCE graph has its fc / conv side branches
+        #   !! qsc / full are kept for diagnosis only: on ROCm 7.x two graphs replayed CONCURRENTLY on two
+        #   streams gave wrong QSC gradients (each graph alone, or both serialised, or the same work as
+        #   branches of ONE graph are bit-exact; scripts/dbg_split.py) -- use dag / dagq
         # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge
         # that crosses queues costs a barrier packet, so fewer, longer branches can win)
         mode = cfg.stream_mode
         if mode not in ("serial", "dag", "dagq", "qsc", "full"):
             raise ValueError(f"stream_mode {mode!r}")
+        if mode in ("qsc", "full"):
+            import warnings
+            warnings.warn(f"stream_mode {mode!r} replays two graphs concurrently: numerically unsafe on ROCm 7.x "
+                          "(see FlagshipTrainer.__init__); use 'dagq'")
         self.streams = None
         if dev.type == "cuda" and mode != "serial" and self.hstep.hip and self.cstep.hip is not None:
             self.streams = {k: torch.cuda.Stream(dev) for k in ("qsc", "fc", "conv")}
@@ -189,10 +197,10 @@ class FlagshipTrainer:
         else:
             if k != 1:
                 raise ValueError("multi-step graphs are a world-1 plan")
-            # three graphs around the two gradient all-reduces; the FC bucket (33.6 MB) is reduced on
-            # RCCL's stream while graph 2 (conv backward) runs on the compute stream
+            # four graphs around the gradient all-reduces (see _dp_run); one memory pool is safe: the
+            # graphs that replay concurrently (gf on the fc stream, gr on main) allocate nothing
             pool = torch.cuda.graph_pool_handle() if graphs else None
-            gs = [GraphedStep(f, enabled=graphs, pool=pool) for f in (self._phase1, self._phase2, self._phase3)]
+            gs = [GraphedStep(f, enabled=graphs, pool=pool) for f in (self._dp_g1, self._dp_g2, self._dp_gf, self._dp_gr)]
         self._graph_sets[k] = gs
         return gs
 
@@ -230,8 +238,9 @@ class FlagshipTrainer:
         self._gather(hdce=False, classifier=True)
         self._qsc_branch(with_opt=True)
 
-    def _hdce_forward(self) -> None:
-        self.hstep.fc_side = self.streams["fc"] if self.hdce_side else None
+    def _hdce_forward(self, side: Optional[bool] = None) -> None:
+        side = self.hdce_side if side is None else side
+        self.hstep.fc_side = self.streams["fc"] if side else None
         loss = self.hstep.forward_fc_gathered(self.gat, self.store)
         if loss is not self.hloss:
             self.hloss.copy_(loss)
@@ -253,35 +262,66 @@ class FlagshipTrainer:
         else:
             self.hopt.step(grad_scale=1.0, skip=self.skip[0:1])
 
-    def _phase1(self) -> None:
-        """(DP) gather, QSC fwd+bwd (own stream), HDCE forward, NMSE, FC wgrad + dgrad."""
+    # -- the data-parallel plan (world > 1; also world 1 'serial' / split_graphs) ---------------
+    #   g1 : gather, HDCE forward, NMSE, FC weight-gradient GEMM
+    #        -> all-reduce 'skip' (HDCE NaN flag) and 'fc' (33.6 MB) start on RCCL's stream
+    #   g2 : FC data-gradient GEMM, conv backward (+ wgrad side stream) and, on the qsc stream, the
+    #        whole QSC forward/backward -- all of it hides the FC all-reduce
+    #        -> all-reduce 'small' (conv/BN + QSC grads + the QSC NaN flag)
+    #   gf : (fc stream) FC Adam once 'skip' + 'fc' arrived and g2's dgrad read the weight shadow,
+    #        beside the 'small' all-reduce;   gr : (main) conv/BN Adam + QSC AdamW after 'small'
+    def _dp_g1(self) -> None:
         self._gather()
-        if self.streams is not None:
+        self.hstep.defer_dgrad = self.hstep.hip
+        self._hdce_forward(side=False)   # (the FC wgrad on main: the all-reduce waits for it first)
+
+    def _dp_g2(self) -> None:
+        # NOTE the first node of a graph must sit on the capturing stream: a branch forked before any
+        # node is a ROOT of the graph, and the HIP graph executor starts root nodes that it places on
+        # its other queues without waiting for the work queued ahead of the graph launch (measured:
+        # the QSC branch then read the previous step's gather output)
+        ms = self.streams is not None
+        if self.hstep.defer_dgrad:
+            self.hstep.dgrad()
+        if ms:
             with self._fork(self.streams["qsc"]):
                 self._qsc_branch(with_opt=False)
-        self._hdce_forward()
-        if self.streams is not None:
-            self._join(("qsc", "fc") if self.hdce_side else ("qsc",))
-
-    def _phase2(self) -> None:
-        """(DP) conv backward."""
-        self.hstep.backward_conv(side=self.streams["conv"] if self.hdce_side else None)
-        if self.streams is None:
+        self.hstep.backward_conv(side=self.streams["conv"] if ms else None)
+        if ms:
+            self._join(("qsc",))
+        else:
             self._qsc_branch(with_opt=False)
 
-    def _phase3(self) -> None:
+    def _dp_gf(self) -> None:
+        self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.skip[0:1], part=1)
+
+    def _dp_gr(self) -> None:
         g = 1.0 / self.ctx.world
-        if self.streams is None:
-            self.hopt.step(grad_scale=g, skip=self.skip[0:1])
-            self.qopt.step(grad_scale=g, skip=self.skip[1:2])
-            return
-        # the three updates are independent: FC Adam (bandwidth-bound, 8.4 M params) beside the rest
-        with self._fork(self.streams["fc"]):
-            self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=1)
-        with self._fork(self.streams["qsc"]):
-            self.qopt.step(grad_scale=g, skip=self.skip[1:2])
         self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=0)
-        self._join(("qsc", "fc"))
+        self.qopt.step(grad_scale=g, skip=self.skip[1:2])
+
+    def _dp_run(self, g1, g2, gf, gr) -> None:
+        b = self.buckets
+        g1()
+        b.launch("skip")
+        b.launch("fc")
+        g2()
+        b.launch("small")
+        if self.streams is None:
+            b.wait()
+            gf()
+            gr()
+            return
+        main = torch.cuda.current_stream(self.ctx.device)
+        fc = self.streams["fc"]
+        fc.wait_stream(main)
+        with torch.cuda.stream(fc):
+            b.wait(("skip", "fc"))
+            gf()
+        b.wait(("skip", "small"))
+        gr()
+        main.wait_stream(fc)
+        b.wait()
 
     def _step_body(self) -> None:
         if self.mode in ("dag", "dagq"):
@@ -291,12 +331,7 @@ class FlagshipTrainer:
             self._hdce_graph()
             self._join(("qsc",))
             return
-        self._phase1()
-        self.buckets.launch("fc")
-        self._phase2()
-        self.buckets.launch("small")
-        self.buckets.wait()
-        self._phase3()
+        self._dp_run(self._dp_g1, self._dp_g2, self._dp_gf, self._dp_gr)
 
     def mutable_state(self):
         """Every tensor a step updates in place (weights, optimizer moments/counters, BN running
@@ -372,9 +407,9 @@ class FlagshipTrainer:
         """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""
         k = self._k()
         if n // k:
-            self.capture(preserve=False, k=k)
+            self.capture(preserve=True, k=k)
         if n % k:
-            self.capture(preserve=False, k=1)
+            self.capture(preserve=True, k=1)
 
     def run(self, n: int) -> None:
         """``n`` training steps, ``cfg.steps_per_graph`` per graph replay (the remainder one by one)."""
@@ -387,7 +422,9 @@ class FlagshipTrainer:
     def _replay(self, k: int) -> None:
         gs = self._graphs_for(k)
         if any(g.enabled and g.graph is None for g in gs):
-            self.capture(preserve=False, k=k)
+            # (preserve: the capture warm-ups run optimizer steps on rank-local gradients; restoring
+            # the state keeps the ranks bit-identical)
+            self.capture(preserve=True, k=k)
         self.next_batch(k)
         if len(gs) == 1:
             gs[0]()
@@ -398,6 +435,16 @@ class FlagshipTrainer:
             gq, gh = gs
             q = self.streams["qsc"]
             q.wait_stream(torch.cuda.current_stream(self.ctx.device))
+            dbg = os.environ.get("QDML_DBG_QSC", "")
+            if dbg:   # (debug: "main" = both graphs on the main stream; "nohdce" = QSC graph only)
+                if dbg == "main":
+                    gh()
+                    gq()
+                else:
+                    with torch.cuda.stream(q):
+                        gq()
+                    self._join(("qsc",))
+                return
             if self.cfg.qsc_first:
                 with torch.cuda.stream(q):
                     gq()
@@ -408,13 +455,7 @@ class FlagshipTrainer:
                     gq()
             self._join(("qsc",))
             return
-        g1, g2, g3 = gs
-        g1()
-        self.buckets.launch("fc")
-        g2()
-        self.buckets.launch("small")
-        self.buckets.wait()
-        g3()
+        self._dp_run(*gs)
 
     @property
     def samples_per_step(self) -> int:

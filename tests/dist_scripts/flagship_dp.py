@@ -1,5 +1,10 @@
-"""World-N flagship trainer on CPU/gloo: ranks stay bit-identical; a NaN on ONE rank makes every rank
-skip the step (the NaN-guard flag rides in the small gradient bucket)."""
+"""World-N flagship trainer: ranks stay bit-identical; a NaN on ONE rank makes every rank skip the step
+(the NaN-guard flags ride in the gradient buckets).
+
+    flagship_dp.py OUT [cpu|cuda]
+
+cpu: gloo, eager.  cuda: the real DP plan (4 HIP graphs, side streams, bucketed async all-reduces)
+with QDML_DIST_BACKEND=gloo so several ranks can share one GPU (RCCL needs a GPU per rank)."""
 import os
 import sys
 
@@ -18,14 +23,18 @@ def flat_all(tr):
 
 
 def same_on_all_ranks(t):
+    t = t.cpu()   # (gloo gathers host tensors)
     g = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(g, t)
     return all(torch.equal(g[0], x) for x in g[1:])
 
 
-def main(out):
-    ctx = init_distributed("cpu")
-    cfg = FlagshipConfig(n_qubits=4, batch=4, data_len=40, hip_graphs=False, dtype="fp32")
+def main(out, device="cpu"):
+    ctx = init_distributed(device)
+    if device == "cuda":
+        cfg = FlagshipConfig(n_qubits=8, batch=32, data_len=800, hip_graphs=True)
+    else:
+        cfg = FlagshipConfig(n_qubits=4, batch=4, data_len=40, hip_graphs=False, dtype="fp32")
     tr = FlagshipTrainer(cfg, ctx)
     ok = [same_on_all_ranks(flat_all(tr))]
     for _ in range(2):
@@ -45,4 +54,4 @@ def main(out):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "cpu")
