@@ -38,6 +38,11 @@ __device__ __forceinline__ unsigned long long phase_stamp() {
   return t;
 }
 
+// torch semantics for non-finite inputs: relu / max propagate NaN (v_max_f32 would return the non-NaN
+// operand and silently turn a NaN batch into zeros -- and a finite loss the NaN guard never sees)
+__device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }
+__device__ __forceinline__ float max_nan(float a, float b) { return (a > b || a != a) ? a : b; }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);

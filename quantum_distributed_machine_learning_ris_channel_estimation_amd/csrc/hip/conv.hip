@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
         if constexpr (INM == IN_BNRELU) {
           const float a = sc[ST_A], b = sc[ST_B];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaxf(a * v[j] + b, 0.f);
+          for (int j = 0; j < 8; ++j) v[j] = relu_nan(a * v[j] + b);
         } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
           float z[8];
           unpack_q(rz[k], z, (const uint16_t*)nullptr);
@@ -634,7 +634,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
         if constexpr (INM == IN_BNRELU) {
           const float xa = prm[c * NST + ST_A], xb2 = prm[c * NST + ST_B];
 #pragma unroll
-          for (int q = 1; q <= W; ++q) v[q] = fmaxf(xa * v[q] + xb2, 0.f);
+          for (int q = 1; q <= W; ++q) v[q] = relu_nan(xa * v[q] + xb2);
         }
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
@@ -922,7 +922,7 @@ __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __re
     load8(z + e0, v);
     uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = fmaxf(a * v[j] + b, 0.f);
+    for (int j = 0; j < 8; ++j) v[j] = relu_nan(a * v[j] + b);
 #pragma unroll
     for (int j = 0; j < 4; ++j) w[j] = f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
     *reinterpret_cast<uint4*>(h + e0) = make_uint4(w[0], w[1], w[2], w[3]);

@@ -61,7 +61,7 @@ struct Lds {
   static constexpr int BWD = o_gwl;                          // + n * F floats (sized at launch)
 };
 
-__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+__device__ __forceinline__ float relu(float v) { return relu_nan(v); }
 
 // ---------------------------------------------------------------------------------------------
 // Forward activations of one sample into LDS (all 256 threads).  Returns nothing; angles (tanh)
@@ -108,7 +108,7 @@ __device__ void sample_forward(const float* __restrict__ xs, const float* wsm, c
   for (int i = t; i < C1 * G::HW2; i += NT) {
     const int c = i / G::HW2, q = i % G::HW2, qh = q / G::W2, qw = q % G::W2;
     const float* a = act + S::o_a1 + c * G::HW + (2 * qh) * W + 2 * qw;
-    const float m = fmaxf(fmaxf(relu(a[0]), relu(a[1])), fmaxf(relu(a[W]), relu(a[W + 1])));
+    const float m = max_nan(max_nan(relu(a[0]), relu(a[1])), max_nan(relu(a[W]), relu(a[W + 1])));
     act[S::o_p1 + c * S::P1P + (qh + 1) * W2P + qw + 1] = m;
   }
   __syncthreads();
@@ -139,7 +139,7 @@ __device__ void sample_forward(const float* __restrict__ xs, const float* wsm, c
   for (int i = t; i < G::F; i += NT) {
     const int c = i / G::HW4, q = i % G::HW4, qh = q / G::W4, qw = q % G::W4;
     const float* a = act + S::o_a2 + c * G::HW2 + (2 * qh) * G::W2 + 2 * qw;
-    act[S::o_p2 + i] = fmaxf(fmaxf(relu(a[0]), relu(a[1])), fmaxf(relu(a[G::W2]), relu(a[G::W2 + 1])));
+    act[S::o_p2 + i] = max_nan(max_nan(relu(a[0]), relu(a[1])), max_nan(relu(a[G::W2]), relu(a[G::W2 + 1])));
   }
   __syncthreads();
   // linear F -> n, tanh.  Each wave reduces a strided slice of features for every output.

@@ -80,7 +80,7 @@ struct Geo {
 // block-shared weights (floats): W1 [16][18] | b1 [16] | W2 [32][144] | b2 [32]
 constexpr int S_W1 = 0, S_B1 = S_W1 + C1 * K1, S_W2 = S_B1 + C1, S_B2 = S_W2 + C2 * K2, S_WEND = S_B2 + C2;
 
-__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+__device__ __forceinline__ float relu(float v) { return relu_nan(v); }
 
 // Diagnostic phase stamps (STAMP builds only): s_memtime with its own lgkmcnt wait, fenced by
 // scheduling barriers so the compiler keeps each phase's work on its side of the stamp.
@@ -218,8 +218,8 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
       const float r0 = relu(acc[c][0]), r1 = relu(acc[c][1]);
-      const float v = fmaxf(r0, r1), pv = __shfl_xor(v, 1);
-      m[c] = fmaxf(v, pv);
+      const float v = max_nan(r0, r1), pv = __shfl_xor(v, 1);
+      m[c] = max_nan(v, pv);
       right |= (uint32_t)(r1 > r0) << c;
       bottom |= (uint32_t)(hw ? (v > pv) : (pv > v)) << c;   // ties go to the top row
     }

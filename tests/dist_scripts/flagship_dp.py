@@ -37,9 +37,14 @@ def main(out, device="cpu"):
         cfg = FlagshipConfig(n_qubits=4, batch=4, data_len=40, hip_graphs=False, dtype="fp32")
     tr = FlagshipTrainer(cfg, ctx)
     ok = [same_on_all_ranks(flat_all(tr))]
-    for _ in range(2):
+    dbg = os.environ.get("QDML_DBG") == "1"
+    for i in range(2):
         tr.step()
         ok.append(same_on_all_ranks(flat_all(tr)))
+        if dbg:
+            print(ctx.rank, "step", i, "same", ok[-1], "skip", tr.skip.tolist(), "h", float(tr.hdce.space.flat.double().sum()),
+                  "q", float(tr.qspace.flat.double().sum()), "hg", float(tr.hdce.space.grad.double().sum()),
+                  "steps", tr.hopt.step_t.tolist(), tr.qopt.step_t.tolist(), flush=True)
     before = flat_all(tr).clone()
     # NaN injected into rank 1's data only
     if ctx.rank == 1:
