@@ -42,6 +42,8 @@ def main() -> int:
     ap.add_argument("--split-graphs", action="store_true", help="3-graph DP plan even at 1 GPU")
     ap.add_argument("--steps-per-graph", type=int, default=1,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
+    ap.add_argument("--hdce-branches", default="", help="(dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam")
+    ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
     ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "qsc", "full"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
@@ -62,7 +64,8 @@ def main() -> int:
     cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
                          hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
                          split_graphs=args.split_graphs, stream_mode=args.stream_mode,
-                         qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph)
+                         qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
+                         hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
@@ -113,6 +116,8 @@ def main() -> int:
                 "hip_graphs": bool(tr.graphed.enabled),
                 "graphs_per_step": len(tr.graphs),
                 "stream_mode": tr.mode,
+                "hdce_branches": "".join(sorted(tr.branches)),
+                "qsc_fork": args.qsc_fork,
                 "steps_per_graph": args.steps_per_graph if n == 1 else 1,
                 "quantumnat": cfg.use_quantumnat,
             },

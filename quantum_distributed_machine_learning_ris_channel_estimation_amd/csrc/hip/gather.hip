@@ -27,7 +27,8 @@ __global__ void __launch_bounds__(256) gather_step_kernel(const long* __restrict
                                                           float* __restrict__ xq, int* __restrict__ rowoff,
                                                           long lab_stream_rows, int E, int U, int B, int plane,
                                                           int* __restrict__ cursor, unsigned int* __restrict__ done,
-                                                          long nperm) {
+                                                          long nperm, const float* __restrict__ rowpow_l,
+                                                          const float* __restrict__ rowpow_p, float2* __restrict__ rowden) {
   const int lane = threadIdx.x & 63;
   const int S = E * U;
   int c = cursor ? *cursor : 0;
@@ -47,6 +48,10 @@ __global__ void __launch_bounds__(256) gather_step_kernel(const long* __restrict
       if (dq) dq[i] = v;
     }
     if (lane == 0 && rowoff) rowoff[(size_t)(u * B + b) * E + e] = (int)(s * lab_stream_rows + n);
+    if (lane == 1 && rowden) {   // per-row label / perfect-channel power for the NMSE kernel's denominators
+      const long ro = s * lab_stream_rows + n;
+      rowden[(size_t)(u * B + b) * E + e] = make_float2(rowpow_l[ro], rowpow_p ? rowpow_p[ro] : 0.f);
+    }
   }
   if (cursor == nullptr) return;
   // the last workgroup to arrive advances the cursor: every workgroup read *cursor before arriving
@@ -75,22 +80,24 @@ QD_API int qd_gather_step(const long* idx, const float* Yp, long yp_stream_strid
   if (plane % 4 || E < 1 || U < 1 || B < 1) return (int)hipErrorInvalidValue;
   const int waves = E * U * B;
   hipLaunchKernelGGL(gather_step_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, idx, Yp,
-                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, nullptr, nullptr, (long)B);
+                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, nullptr, nullptr, (long)B, nullptr, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 
 // perm: (n,) int64 sample permutation; cursor: device int32 (perm offset of this step's batch,
 // advanced by B in-kernel); done: device uint32 zero-initialised once.  x1 / xq / rowoff nullable.
 // The caller guarantees *cursor + B <= n (it re-arms the cursor when it regenerates perm).
-QD_API int qd_gather_cursor(const long* perm, long nperm, int* cursor, unsigned int* done, const float* Yp,
-                            long yp_stream_stride,
+// rowpow_l / rowpow_p / rowden (nullable, HDCE half only): rowden[r] = (|label row|^2, |perf row|^2)
+QD_API int qd_gather_cursor(const long* perm, long nperm, int* cursor, unsigned int* done, const float* rowpow_l,
+                            const float* rowpow_p, float* rowden, const float* Yp, long yp_stream_stride,
                             float* x1, float* xq, int* rowoff, long lab_stream_rows, int E, int U, int B, int plane,
                             void* stream) {
   if (plane % 4 || E < 1 || U < 1 || B < 1 || !cursor || !done || nperm < B) return (int)hipErrorInvalidValue;
-  if ((x1 == nullptr) != (rowoff == nullptr)) return (int)hipErrorInvalidValue;
+  if ((x1 == nullptr) != (rowoff == nullptr) || (rowden && (!rowoff || !rowpow_l))) return (int)hipErrorInvalidValue;
   const int waves = E * U * B;
   const int grid = (waves + 3) / 4 < 128 ? (waves + 3) / 4 : 128;
   hipLaunchKernelGGL(gather_step_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, perm, Yp,
-                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, cursor, done, nperm);
+                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, cursor, done, nperm,
+                     rowpow_l, rowpow_p, reinterpret_cast<float2*>(rowden));
   return (int)hipGetLastError();
 }

@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(256) nmse_fused_kernel(const TY* __restrict__ 
                                                          const float* __restrict__ rowpow_p, TD* __restrict__ dY,
                                                          float* __restrict__ colsum, float* __restrict__ part,
                                                          float* __restrict__ dens, int cols, int B, int U, int rpc,
-                                                         float loss_scale) {
+                                                         float loss_scale, const float2* __restrict__ rowden) {
   __shared__ float sden[2 * E];
   __shared__ float sred[4][2 * E];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -242,10 +242,18 @@ __global__ void __launch_bounds__(256) nmse_fused_kernel(const TY* __restrict__ 
   // per-stream label powers of this u-block (wave e: stream e*U + u), fixed order
   for (int e = wv; e < E; e += 4) {
     float a = 0.f, ap = 0.f;
-    for (int b = lane; b < B; b += 64) {
-      const int ro = rowoff[(u * B + b) * E + e];
-      a += rowpow_l[ro];
-      ap += Pf ? rowpow_p[ro] : 0.f;
+    if (rowden) {   // (gathered per-row powers: independent loads, no rowoff -> rowpow chain)
+      for (int b = lane; b < B; b += 64) {
+        const float2 v = rowden[(u * B + b) * E + e];
+        a += v.x;
+        ap += Pf ? v.y : 0.f;
+      }
+    } else {
+      for (int b = lane; b < B; b += 64) {
+        const int ro = rowoff[(u * B + b) * E + e];
+        a += rowpow_l[ro];
+        ap += Pf ? rowpow_p[ro] : 0.f;
+      }
     }
     a = wave_sum(a);
     ap = wave_sum(ap);
@@ -400,7 +408,7 @@ using namespace qd::nmse;
 QD_API int qd_nmse_fused(const void* Y, int y_bf16, const float* label, const float* perf, const int* rowoff,
                          const float* rowpow_l, const float* rowpow_p, void* dY, int dy_bf16, float* colsum,
                          float* part, float* dens, float* bias_grad, float* ss, float* loss, float* skip, int E, int U,
-                         int B, int cols, int rpc, float loss_scale, void* stream) {
+                         int B, int cols, int rpc, float loss_scale, const float* rowden, void* stream) {
   if (cols % 1024 || rpc < E || rpc % E || (B * E) % rpc || (perf == nullptr) != (rowpow_p == nullptr))
     return (int)hipErrorInvalidValue;
   const int rows = U * B * E;
@@ -408,7 +416,8 @@ QD_API int qd_nmse_fused(const void* Y, int y_bf16, const float* label, const fl
   hipStream_t st = (hipStream_t)stream;
 #define QD_F(TY, TD, EE)                                                                                            \
   hipLaunchKernelGGL((nmse_fused_kernel<TY, TD, EE>), grid, dim3(256), 0, st, (const TY*)Y, label, perf, rowoff,     \
-                     rowpow_l, rowpow_p, (TD*)dY, colsum, part, dens, cols, B, U, rpc, loss_scale)
+                     rowpow_l, rowpow_p, (TD*)dY, colsum, part, dens, cols, B, U, rpc, loss_scale,              \
+                     reinterpret_cast<const float2*>(rowden))
 #define QD_E(EE)                                          \
   if (y_bf16 && dy_bf16) QD_F(uint16_t, uint16_t, EE);    \
   else if (y_bf16) QD_F(uint16_t, float, EE);             \

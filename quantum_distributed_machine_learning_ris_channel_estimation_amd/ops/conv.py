@@ -49,6 +49,7 @@ class ConvStackHIP:
                  dx_bf16: bool = True):
         self.m = model
         self.count_batches = False   # set by the owner that stops counting num_batches_tracked itself
+        self.stage_hook = None       # optional callable(stage name) between forward launches
         if not 1 <= U <= 8:
             raise ValueError(f"ConvStackHIP: {U} BatchNorm groups per step (1..8 supported)")
         self.U, self.B, self.N, self.E = U, B, U * B, model.E
@@ -117,6 +118,9 @@ class ConvStackHIP:
         assert x1.shape == (self.N, 2 * self.E, self.H, self.W) and x1.dtype == torch.float32 and x1.is_contiguous()
         self.x1 = x1
         self.pack_weights(st)
+        hook = self.stage_hook
+        if hook is not None:
+            hook("packed")
         inp, st_prev = x1, None
         for k in range(3):
             # layers 2, 3 finalise the previous layer's BatchNorm themselves (BnFwd: statistics
@@ -131,6 +135,8 @@ class ConvStackHIP:
                                 nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw,
                                 ctypes.byref(bnf) if bnf is not None else None, st), f"conv_fwd{k + 1}")
             inp, st_prev = self.z[k], self.st[k]
+            if hook is not None:
+                hook(f"conv{k + 1}")
         # one BN tail launch: every layer's running statistics (+ num_batches_tracked), and the last
         # layer's records (layers 1, 2 were built -- bitwise identically -- by their consumers)
         nbt = getattr(m, "_nbt", None) if (training and self.count_batches) else None

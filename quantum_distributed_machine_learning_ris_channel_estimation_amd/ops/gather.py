@@ -29,6 +29,10 @@ class StepGather:
         self.xq = torch.empty(self.S * B, 2, H, W, device=dev) if with_classifier else None
         self.rowoff = torch.empty(U * B * E, device=dev, dtype=torch.int32)
         self.plane = 2 * H * W
+        # optional (GPU, HDCE half): per-row label / perf powers of the store (rowoff's row space); the
+        # cursor gather then also writes rowden (U*B*E, 2) for the one-pass NMSE's denominators
+        self.rowpow = None
+        self.rowden = torch.zeros(U * B * E, 2, device=dev)
 
     def from_cursor(self, store, perm: torch.Tensor, cursor: torch.Tensor, done: torch.Tensor, hdce: bool = True,
                     classifier: bool = True) -> None:
@@ -43,10 +47,14 @@ class StepGather:
             assert Yp.dtype == torch.float32 and Yp[0, 0].is_contiguous() and Yp.stride(1) == self.plane
             assert HL.stride(1) == cols and HL.stride(0) % cols == 0 and store.Hperf.stride() == HL.stride()
             assert perm.numel() == Yp.shape[1]
-            f = nat.fn(nat.hip_lib(), "qd_gather_cursor", [_p, _l, _p, _p, _p, _l, _p, _p, _p, _l, _i, _i, _i, _i, _p])
+            f = nat.fn(nat.hip_lib(), "qd_gather_cursor", [_p, _l, _p, _p, _p, _p, _p, _p, _l, _p, _p, _p, _l, _i, _i, _i,
+                                                            _i, _p])
+            rp = self.rowpow if (hdce and self.rowpow is not None) else None
             xq = self.xq if classifier else None
             assert not classifier or xq is not None
-            nat.check(f(nat.ptr(perm), perm.numel(), nat.ptr(cursor), nat.ptr(done), nat.ptr(Yp), Yp.stride(0),
+            nat.check(f(nat.ptr(perm), perm.numel(), nat.ptr(cursor), nat.ptr(done),
+                        nat.ptr(rp[0]) if rp else None, nat.ptr(rp[1]) if rp and rp[1] is not None else None,
+                        nat.ptr(self.rowden) if rp else None, nat.ptr(Yp), Yp.stride(0),
                         nat.ptr(self.x1) if hdce else None, nat.ptr(xq) if xq is not None else None,
                         nat.ptr(self.rowoff) if hdce else None, HL.stride(0) // cols, self.E, self.U, self.B,
                         self.plane, nat.stream_ptr(Yp.device)), "gather_cursor")
@@ -61,6 +69,10 @@ class StepGather:
         try:
             if hdce:
                 self(store, idx)
+                if self.rowpow is not None:
+                    o = self.rowoff.long()
+                    self.rowden[:, 0] = self.rowpow[0][o]
+                    self.rowden[:, 1] = self.rowpow[1][o] if self.rowpow[1] is not None else 0.0
             elif classifier:
                 g = Yp.index_select(1, idx)
                 self.xq.copy_(g.reshape(self.S * self.B, 2, self.H, self.W))

@@ -267,6 +267,7 @@ class HDCEStep:
         self.fc_side = None   # optional stream for the FC weight-gradient GEMM (HIP path)
         self.fused_nmse = True  # HIP path: the one-pass NMSE (qd_nmse_fused) when labels come via rowoff
         self.defer_dgrad = False
+        self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         if self.hip:
             from ..ops.conv import ConvStackHIP
             self.conv = ConvStackHIP(model, n_users, batch)
@@ -294,6 +295,7 @@ class HDCEStep:
         """From a filled ops.gather.StepGather: conv input g.x1, labels read in place from the
         store through g.rowoff (no permuted label copies)."""
         self.nmse.rowoff = g.rowoff
+        self._rowden = g.rowden if getattr(g, "rowpow", None) is not None else None
         return self._forward_fc(g.x1, store.Hlabel, store.Hperf)
 
     def _forward_fc(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
@@ -326,7 +328,11 @@ class HDCEStep:
     def _forward_fc_hip(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
         m = self.m
         dt = m.compute_dtype
+        hook = self.stage_hook
+        self.conv.stage_hook = hook
         A = self.conv.forward(x1, training=True)                # (rows, 4096) bf16
+        if hook is not None:
+            hook("conv")
         W, b = m.fc_weights_lp()
         if m.fp8 and m.fc_shadow is None:
             Y = fp8_linear(A, m.fc_w.detach(), b)
@@ -339,9 +345,12 @@ class HDCEStep:
             m.fp8_scales.update()
         else:
             Y = torch.nn.functional.linear(A.to(dt), W, b)
+        if hook is not None:
+            hook("fc")
         if self.nmse.rowoff is not None and self.fused_nmse and self.nmse.cols % 1024 == 0:
             # one pass: loss, skip, dY, bias-gradient partials (+ one finish launch)
-            dY = self.nmse.fused(Y, label, perf, m.fc_b.grad, (m.E, self.U, self.B), out_dtype=dt)
+            dY = self.nmse.fused(Y, label, perf, m.fc_b.grad, (m.E, self.U, self.B), out_dtype=dt,
+                                 rowden=getattr(self, "_rowden", None))
             loss = self.nmse.loss
         else:
             loss = self.nmse.sums_finalize(Y, label, perf)

@@ -82,6 +82,8 @@ class FlagshipConfig:
     split_graphs: bool = False   # force the 3-graph DP execution plan even at world 1 (testing)
     stream_mode: str = "dagq"    # serial | dag | dagq (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
+    hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
+    qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
@@ -128,6 +130,9 @@ class FlagshipTrainer:
         self.buckets = GradBuckets(ctx, {"skip": [self.skip[0:1]], "fc": [sp.grad[n_conv:]],
                                          "small": [sp.grad[:n_conv], self.qspace.grad, self.skip[1:2]]})
         self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)
+        if dev.type == "cuda" and self.hstep.hip:   # per-row label powers ride along with the gather
+            nm = self.hstep.nmse
+            self.gat.rowpow = (nm._row_powers(self.store.Hlabel), nm._row_powers(self.store.Hperf))
         # batch selection on the device: the gather kernels read perm[cur : cur + B] and advance cur
         # themselves (cur[0]: HDCE / whole-step gather, cur[1]: the QSC graph's own gather); the host
         # only tracks the epoch position to regenerate perm in place when it runs out
@@ -165,7 +170,11 @@ class FlagshipTrainer:
         else:
             mode = "serial"
         self.mode = mode
-        self.hdce_side = mode in ("dag", "full")
+        # HDCE side branches: w = FC weight-gradient GEMM, c = conv weight-gradient kernels, a = FC Adam
+        self.branches = set("wca") if mode in ("dag", "full") else set(cfg.hdce_branches)
+        if self.streams is None:
+            self.branches = set()
+        self.hdce_side = "w" in self.branches
         self._use_graphs = graphs
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
@@ -250,16 +259,18 @@ class FlagshipTrainer:
         if gather:
             self._gather(hdce=True, classifier=False)
         self._hdce_forward()
-        side = self.hdce_side
-        if side:
+        br = self.branches
+        if "a" in br:
             # FC Adam once the dgrad GEMM (which reads the bf16 weight shadow it rewrites) is queued
             with self._fork(self.streams["fc"]):
                 self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=1)
-        self.hstep.backward_conv(side=self.streams["conv"] if side else None)
-        if side:
+        self.hstep.backward_conv(side=self.streams["conv"] if "c" in br else None)
+        if "a" in br:
             self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=0)
             self._join(("fc",))
         else:
+            if self.hdce_side:
+                self._join(("fc",))
             self.hopt.step(grad_scale=1.0, skip=self.skip[0:1])
 
     # -- the data-parallel plan (world > 1; also world 1 'serial' / split_graphs) ---------------
@@ -286,7 +297,7 @@ class FlagshipTrainer:
         if ms:
             with self._fork(self.streams["qsc"]):
                 self._qsc_branch(with_opt=False)
-        self.hstep.backward_conv(side=self.streams["conv"] if ms else None)
+        self.hstep.backward_conv(side=self.streams["conv"] if "c" in self.branches else None)
         if ms:
             self._join(("qsc",))
         else:
@@ -326,9 +337,23 @@ class FlagshipTrainer:
     def _step_body(self) -> None:
         if self.mode in ("dag", "dagq"):
             self._gather()
-            with self._fork(self.streams["qsc"]):
-                self._qsc_branch(with_opt=True)
-            self._hdce_graph()
+            # the QSC branch forks at a chosen point of the HDCE forward (cfg.qsc_fork): its latency-
+            # bound kernels then share the GPU with the later, larger HDCE kernels
+            forked = []
+
+            def fork_qsc(stage: str) -> None:
+                if not forked and stage == self.cfg.qsc_fork:
+                    forked.append(True)
+                    with self._fork(self.streams["qsc"]):
+                        self._qsc_branch(with_opt=True)
+
+            fork_qsc("gather")
+            self.hstep.stage_hook = fork_qsc
+            try:
+                self._hdce_graph()
+            finally:
+                self.hstep.stage_hook = None
+            fork_qsc(self.cfg.qsc_fork)   # (a stage the forward does not have: fork at its end)
             self._join(("qsc",))
             return
         self._dp_run(self._dp_g1, self._dp_g2, self._dp_gf, self._dp_gr)

@@ -30,6 +30,8 @@ for s in $STEPS; do
     bench_c5) run bench_c5 600 python bench.py --steps 10 --warmup 3 --qubits 16 --dtype fp8 ;;
     train) run train 1200 python scripts/train_eval.py --epochs ${EPOCHS:-100} --qubits 6 --qml-qubits 4,8 --out "$OUT/train" ;;
     bench_k) for m in ${MODES:-dagq qsc}; do for k in ${KS:-1 2 5 10}; do run bench_${m}_k$k 300 python bench.py --steps 100 --warmup 10 --stream-mode $m --steps-per-graph $k; done; done ;;
+    bench_br) for b in ${BRS:-x a c w ac wa wca}; do run bench_br_$b 300 python bench.py --steps 100 --warmup 10 --stream-mode dagq --hdce-branches=${b/x/}; done ;;
+    bench_fork) for f in ${FORKS:-gather packed conv1 conv2 conv fc}; do run bench_fork_$f 300 python bench.py --steps 100 --warmup 10 --qsc-fork $f; done ;;
     bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
@@ -41,6 +43,7 @@ for s in $STEPS; do
     fp8probe) run fp8probe 300 python scripts/probe_fp8.py ;;
     fcprobe) run fcprobe 300 python scripts/probe_fc_gemm.py ;;
     nmseprobe) run nmseprobe 300 python scripts/probe_nmse.py ;;
+    fchand) run fchand 300 python scripts/probe_fc_hand.py ;;
     tunegemm) run tunegemm 900 python scripts/tune_gemm.py --out "$OUT/tunableop_gfx950.csv" ;;
     diag) run diag 900 python scripts/diag_hdce.py --epochs ${DIAG_EPOCHS:-20} ;;
     gensweep) run gensweep 1500 python scripts/gen_sweep.py --epochs ${SWEEP_EPOCHS:-30} --sc-epochs 8 ;;

@@ -223,12 +223,18 @@ def test_gather_device_cursor(cuda):
     done = torch.zeros(2, dtype=torch.int32, device=cuda)
     g = StepGather(3, 3, B, 16, 8, cuda)
     ref = StepGather(3, 3, B, 16, 8, cuda)
+    cols = d.Hlabel.shape[-1]
+    rp = (d.Hlabel.pow(2).sum(-1).reshape(-1).contiguous(), d.Hperf.pow(2).sum(-1).reshape(-1).contiguous())
+    g.rowpow = rp   # (contiguous store: rowoff row space = s * N + n)
+    assert d.Hlabel.stride(0) == d.n * cols
     for k in range(5):
         g.from_cursor(d, perm, cur[0:1], done[0:1], hdce=True, classifier=False)
         g.from_cursor(d, perm, cur[1:2], done[1:2], hdce=False, classifier=True)
         ref(d, perm[k * B:(k + 1) * B].contiguous())
         torch.cuda.synchronize()
         assert torch.equal(g.x1, ref.x1) and torch.equal(g.xq, ref.xq) and torch.equal(g.rowoff, ref.rowoff), k
+        o = g.rowoff.long()
+        assert torch.equal(g.rowden[:, 0], rp[0][o]) and torch.equal(g.rowden[:, 1], rp[1][o])
         assert cur.tolist() == [(k + 1) * B] * 2 and done.tolist() == [0, 0]
     # an exhausted cursor never reads past the permutation: it restarts at 0
     cur.fill_(d.n - 3)
