@@ -40,9 +40,10 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-quantumnat", action="store_true")
     ap.add_argument("--split-graphs", action="store_true", help="3-graph DP plan even at 1 GPU")
-    ap.add_argument("--steps-per-graph", type=int, default=1,
+    ap.add_argument("--steps-per-graph", type=int, default=5,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
     ap.add_argument("--hdce-branches", default="", help="(dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam")
+    ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
     ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
     ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "qsc", "full"],
@@ -65,7 +66,8 @@ def main() -> int:
                          hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
                          split_graphs=args.split_graphs, stream_mode=args.stream_mode,
                          qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
-                         hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork)
+                         hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
+                         fc_adam_grid=args.fc_adam_grid)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
@@ -118,6 +120,7 @@ def main() -> int:
                 "stream_mode": tr.mode,
                 "hdce_branches": "".join(sorted(tr.branches)),
                 "qsc_fork": args.qsc_fork,
+                "fc_adam_grid": args.fc_adam_grid,
                 "steps_per_graph": args.steps_per_graph if n == 1 else 1,
                 "quantumnat": cfg.use_quantumnat,
             },

@@ -187,10 +187,10 @@ __global__ void __launch_bounds__(256) fp8_scale_update_kernel(float* amax_parts
   }
 }
 
-inline int grid_for(long n) {
+inline int grid_for(long n, int max_grid = 2048) {
   long b = (n / 4 + 255) / 256;
   if (b < 1) b = 1;
-  if (b > 2048) b = 2048;
+  if (b > max_grid) b = max_grid;
   return (int)b;
 }
 
@@ -205,13 +205,15 @@ using namespace qd::optim;
 QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const float* skip,
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
                         float grad_scale, float prune_thr, unsigned int* done, uint16_t* shadow, long shadow_lo,
-                        long shadow_hi, uint8_t* shadow8, const float* qs, float* amax, void* stream) {
+                        long shadow_hi, uint8_t* shadow8, const float* qs, float* amax, int max_grid, void* stream) {
   if (n <= 0 || done == nullptr || (shadow && ((shadow_lo | shadow_hi) & 3))) return (int)hipErrorInvalidValue;
   if (shadow8 && (!shadow || !qs || !amax)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   AdamArgs a{beta1, beta2, eps, weight_decay, grad_scale, prune_thr, decoupled};
   Shadow sh{shadow, shadow_lo, shadow_hi, shadow8, qs, amax};
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step,
+  // max_grid (0 = 2048): fewer workgroups stream the update more slowly but leave most CUs to
+  // kernels running beside it (the FC Adam as a side branch of the step graph)
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, max_grid > 0 ? max_grid : 2048)), dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step,
                      done, sh);
   return (int)hipGetLastError();
 }

@@ -136,6 +136,7 @@ class FusedOptimizer:
         # with its own step counter / done counter, so independent ranges can update on different
         # streams as soon as their gradients are final (they always advance together: equal counts)
         self.bounds: List[Tuple[int, int]] = [(0, space.numel)]
+        self.max_grid: Dict[int, int] = {}   # part -> workgroup cap of its update launch (0: default)
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
         self.pruned = torch.zeros(1, device=dev, dtype=torch.int32)
         self.done = torch.zeros(1, device=dev, dtype=torch.int32)   # last-workgroup counter (step tick)
@@ -230,7 +231,7 @@ class FusedOptimizer:
                 self.refresh_shadow()
             return
         f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
-                                         _p, _p, _l, _l, _p, _p, _p, _p])
+                                         _p, _p, _l, _l, _p, _p, _p, _i, _p])
         # the shadow range, clipped to this part and expressed relative to it
         sh_lo, sh_hi = max(self.shadow_lo, lo), min(self.shadow_hi, hi)
         has_sh = self.shadow is not None and sh_lo < sh_hi
@@ -243,7 +244,8 @@ class FusedOptimizer:
                     self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
                     self.prune_thr, done_p, sh_ptr, (sh_lo - lo) if has_sh else 0, (sh_hi - lo) if has_sh else 0,
                     sh8_ptr, nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
-                    nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, st), "adam")
+                    nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, int(self.max_grid.get(i, 0)), st),
+                  "adam")
 
     @torch.no_grad()
     def _step_host(self, grad_scale: float, skip: Optional[torch.Tensor]) -> None:

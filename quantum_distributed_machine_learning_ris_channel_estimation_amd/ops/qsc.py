@@ -19,6 +19,7 @@ backward use it, the grads flow to the clean master.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -90,6 +91,8 @@ class QSCStepHIP:
         L = nat.hip_lib()
         self.big = self.n > HIP_REG_MAX_QUBITS  # workgroup-per-sample simulator (qsim_big.hip)
         if self.big:
+            cap = int(os.environ.get("QDML_QSIM_BIG_GRID", "0"))   # (0: the library default)
+            nat.fn(L, "qd_qsim_big_set_grid_cap", [_i], None)(cap)
             self.qrows = nat.fn(L, "qd_qsim_big_grid", [_i])(batch_total)
             ws = nat.fn(L, "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)
             nb = max(ws(self.n, self.qrows, 0), ws(self.n, self.qrows, 1))

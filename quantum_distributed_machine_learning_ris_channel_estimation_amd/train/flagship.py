@@ -83,6 +83,7 @@ class FlagshipConfig:
     stream_mode: str = "dagq"    # serial | dag | dagq (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
+    fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
     qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
@@ -113,6 +114,8 @@ class FlagshipTrainer:
         sp = self.hdce.space
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
         self.hopt.partition([n_conv])           # part 0: conv + BN params, part 1: FC (own streams)
+        if cfg.fc_adam_grid:
+            self.hopt.max_grid[1] = cfg.fc_adam_grid
         self.hdce.attach_fc_shadow(self.hopt)   # after the broadcast: the shadow starts in sync
         self.qopt = make_optimizer(self.qspace, "adamw", cfg.lr, weight_decay=cfg.qsc_weight_decay,
                                    prune_thr=0.1 if cfg.use_gradient_pruning else 0.0)

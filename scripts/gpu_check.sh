@@ -32,6 +32,8 @@ for s in $STEPS; do
     bench_k) for m in ${MODES:-dagq qsc}; do for k in ${KS:-1 2 5 10}; do run bench_${m}_k$k 300 python bench.py --steps 100 --warmup 10 --stream-mode $m --steps-per-graph $k; done; done ;;
     bench_br) for b in ${BRS:-x a c w ac wa wca}; do run bench_br_$b 300 python bench.py --steps 100 --warmup 10 --stream-mode dagq --hdce-branches=${b/x/}; done ;;
     bench_fork) for f in ${FORKS:-gather packed conv1 conv2 conv fc}; do run bench_fork_$f 300 python bench.py --steps 100 --warmup 10 --qsc-fork $f; done ;;
+    bench_adam) for g in ${GRIDS:-0 64 128 256 512}; do run bench_adam_$g 300 python bench.py --steps 100 --warmup 10 --hdce-branches=a --fc-adam-grid $g; done ;;
+    q16grid) for g in ${GRIDS:-512 1152 2304}; do QDML_QSIM_BIG_GRID=$g run bench_q16_$g 300 python bench.py --steps 6 --warmup 2 --steps-per-graph 1 --qubits 16 --dtype fp8; done ;;
     bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
@@ -49,3 +51,7 @@ for s in $STEPS; do
     gensweep) run gensweep 1500 python scripts/gen_sweep.py --epochs ${SWEEP_EPOCHS:-30} --sc-epochs 8 ;;
   esac
 done
+# (extra profiles) prof_cfg: PROF_NAME / PROF_ARGS select the bench configuration
+if [[ " $STEPS " == *" prof_cfg "* ]]; then
+  (cd /tmp && export TMPDIR=/tmp && run prof_${PROF_NAME:-cfg} 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${PROF_NAME:-cfg}" -o run -- python "$ROOT/bench.py" ${PROF_ARGS:-}) && python scripts/prof_summary.py "$OUT/prof_${PROF_NAME:-cfg}/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_${PROF_NAME:-cfg}_summary.md" && python scripts/prof_timeline.py "$OUT/prof_${PROF_NAME:-cfg}/run_kernel_trace.csv" --back 3 > "$OUT/prof_${PROF_NAME:-cfg}_timeline.md"
+fi
