@@ -27,6 +27,8 @@ MI355X design implemented here:
 """
 from __future__ import annotations
 
+import os
+
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -270,7 +272,11 @@ class HDCEStep:
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         if self.hip:
             from ..ops.conv import ConvStackHIP
-            self.conv = ConvStackHIP(model, n_users, batch)
+            # launch knobs (samples per wave / per wgrad workgroup / per BN-reduction workgroup / layer-1
+            # wgrad); QDML_CONV_KNOBS="spw,spb_w,spb_r,spb_w1" overrides them for sweeps
+            kn = os.environ.get("QDML_CONV_KNOBS")
+            kw = dict(zip(("spw", "spb_w", "spb_r", "spb_w1"), map(int, kn.split(",")))) if kn else {}
+            self.conv = ConvStackHIP(model, n_users, batch, **kw)
             self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
 
