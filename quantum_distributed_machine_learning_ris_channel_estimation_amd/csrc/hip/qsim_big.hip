@@ -196,8 +196,10 @@ __device__ void high_pass_fwd(const cf* A, cf* B, const float4* trig) {
 }
 
 // Full forward circuit of one sample; returns the buffer holding psi_final (A or B).
+// final_out (HBM-state builds, L > 1): the last high pass stores psi_final there instead of B.
 template <int N>
-__device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs, const float* w, int L) {
+__device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs, const float* w, int L,
+                           cf* final_out = nullptr) {
   layer_trig(trig, w, xs, N);
   __syncthreads();
   product_pass<N>(A, trig);
@@ -205,10 +207,15 @@ __device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs
     layer_trig(trig, w + 2 * N * l, nullptr, N);
     __syncthreads();
     low_pass_fwd<N>(A, tile, trig);
-    high_pass_fwd<N>(A, B, trig);
-    cf* t = A;
-    A = B;
-    B = t;
+    cf* dst = (final_out != nullptr && l == L - 1) ? final_out : B;
+    high_pass_fwd<N>(A, dst, trig);
+    if (dst == B) {
+      cf* t = A;
+      A = B;
+      B = t;
+    } else {
+      A = dst;
+    }
   }
   return A;
 }
@@ -219,9 +226,11 @@ __device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs
 constexpr int O_RED = 0, O_TRIG = 2048, O_G = 2304, O_ACC = 2368, O_TMP = 3392, O_DATA = 3584;
 
 template <int N>
+// psave (nullable): (B, 2^N) per-sample psi_final, kept for the backward (which then skips its
+// forward recompute: ~1/3 of its state traffic at n = 16)
 __global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           float* __restrict__ E, int B, int L, int wgroup,
-                                                          cf* __restrict__ ws) {
+                                                          cf* __restrict__ ws, cf* __restrict__ psave) {
   using C = G<N>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem + O_RED);
@@ -240,7 +249,11 @@ __global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restric
   }
   for (int s = blockIdx.x; s < B; s += gridDim.x) {
     const float* wsmp = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * N * L : 0);
-    cf* psi = run_circuit<N>(A, Bf, tile, trig, x + (size_t)s * N, wsmp, L);
+    cf* sv = psave ? psave + (size_t)s * C::D : nullptr;
+    cf* psi = run_circuit<N>(A, Bf, tile, trig, x + (size_t)s * N, wsmp, L, C::LDS_STATE ? nullptr : sv);
+    if (sv != nullptr && psi != sv) {   // (LDS-resident state, or L == 1)
+      for (int k = threadIdx.x; k < C::D; k += NT) sv[k] = psi[k];
+    }
     float part[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) part[q] = 0.f;
@@ -260,10 +273,12 @@ __global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restric
 
 // slab: (gridDim.x, 2*N*L) partial weight grads (one row per workgroup); dx: (B, N)
 template <int N>
+// psave (nullable): psi_final of every sample from qsim_big_fwd_kernel (same x, w); the backward
+// starts from it instead of re-running the circuit (the buffer is consumed: it may be overwritten)
 __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ gE, float* __restrict__ dx,
                                                           float* __restrict__ slab, int B, int L, int wgroup,
-                                                          cf* __restrict__ ws) {
+                                                          cf* __restrict__ ws, cf* __restrict__ psave) {
   using C = G<N>;
   constexpr int HV = C::HB > 0 ? C::HB : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -294,8 +309,23 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
     const float* xs = x + (size_t)s * N;
     if (threadIdx.x < N) gq[threadIdx.x] = gE[(size_t)s * N + threadIdx.x];
     if (threadIdx.x < 2 * N) tmp[threadIdx.x] = 0.f;
-    cf* psi = run_circuit<N>(b0, b1, tp, trig, xs, wsmp, L);   // its barriers publish gq / tmp
-    cf* psi_o = (psi == b0) ? b1 : b0;
+    cf* psi;
+    cf* psi_o;
+    if (psave != nullptr) {
+      cf* sv = psave + (size_t)s * C::D;
+      if constexpr (C::LDS_STATE) {
+        for (int k = threadIdx.x; k < C::D; k += NT) b0[k] = sv[k];
+        psi = b0;
+        psi_o = b1;
+      } else {
+        psi = sv;       // read in place; the first reverse pass writes b1 and the ping-pong
+        psi_o = b1;     // continues over (sv, b1) -- the saved state is consumed
+      }
+      __syncthreads();  // (publishes gq / tmp, as run_circuit's barriers do)
+    } else {
+      psi = run_circuit<N>(b0, b1, tp, trig, xs, wsmp, L);   // its barriers publish gq / tmp
+      psi_o = (psi == b0) ? b1 : b0;
+    }
     cf* lam = b2;
     cf* lam_o = b3;
     for (int l = L - 1; l >= 0; --l) {
@@ -444,15 +474,16 @@ static size_t smem_bytes(bool backward) {
 
 template <int N>
 static int launch(bool backward, const float* x, const float* w, const float* gE, float* E_or_dx, float* slab, int B,
-                  int L, int wgroup, cf* ws, int grid, hipStream_t st) {
+                  int L, int wgroup, cf* ws, int grid, hipStream_t st, cf* psave = nullptr) {
   const size_t sm = smem_bytes<N>(backward);
   if (!G<N>::LDS_STATE && ws == nullptr) return (int)hipErrorInvalidValue;
   if (backward) {
     if (hipError_t e = allow_lds(qsim_big_bwd_kernel<N>, sm)) return (int)e;
-    hipLaunchKernelGGL(qsim_big_bwd_kernel<N>, dim3(grid), dim3(NT), sm, st, x, w, gE, E_or_dx, slab, B, L, wgroup, ws);
+    hipLaunchKernelGGL(qsim_big_bwd_kernel<N>, dim3(grid), dim3(NT), sm, st, x, w, gE, E_or_dx, slab, B, L, wgroup, ws,
+                       psave);
   } else {
     if (hipError_t e = allow_lds(qsim_big_fwd_kernel<N>, sm)) return (int)e;
-    hipLaunchKernelGGL(qsim_big_fwd_kernel<N>, dim3(grid), dim3(NT), sm, st, x, w, E_or_dx, B, L, wgroup, ws);
+    hipLaunchKernelGGL(qsim_big_fwd_kernel<N>, dim3(grid), dim3(NT), sm, st, x, w, E_or_dx, B, L, wgroup, ws, psave);
   }
   return (int)hipGetLastError();
 }
@@ -487,20 +518,24 @@ static int g_big_grid_cap = 512;
 QD_API void qd_qsim_big_set_grid_cap(int cap) { g_big_grid_cap = cap > 0 ? cap : 512; }
 QD_API int qd_qsim_big_grid(int B) { return B < g_big_grid_cap ? B : g_big_grid_cap; }
 
+// psave (nullable): (B, 2^n) complex64 buffer keeping every sample's psi_final for qd_qsim_big_bwd.
 QD_API int qd_qsim_big_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
-                           void* stream) {
+                           void* psave, void* stream) {
   if (B < 1 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
   const int grid = qd_qsim_big_grid(B);
-#define CALL_F(NN) launch<NN>(false, x, w, nullptr, E, nullptr, B, L, wgroup, (cf*)ws, grid, (hipStream_t)stream)
+#define CALL_F(NN) \
+  launch<NN>(false, x, w, nullptr, E, nullptr, B, L, wgroup, (cf*)ws, grid, (hipStream_t)stream, (cf*)psave)
   QD_BIG_DISPATCH(n, CALL_F)
 #undef CALL_F
 }
 
+// psave (nullable): the forward's saved psi_final (same x, w); consumed (may be overwritten).
 QD_API int qd_qsim_big_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n, int L,
-                           int wgroup, void* ws, void* stream) {
+                           int wgroup, void* ws, void* psave, void* stream) {
   if (B < 1 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
   const int grid = qd_qsim_big_grid(B);
-#define CALL_B(NN) launch<NN>(true, x, w, gE, dx, slab, B, L, wgroup, (cf*)ws, grid, (hipStream_t)stream)
+#define CALL_B(NN) \
+  launch<NN>(true, x, w, gE, dx, slab, B, L, wgroup, (cf*)ws, grid, (hipStream_t)stream, (cf*)psave)
   QD_BIG_DISPATCH(n, CALL_B)
 #undef CALL_B
 }

@@ -97,6 +97,10 @@ class QSCStepHIP:
             ws = nat.fn(L, "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)
             nb = max(ws(self.n, self.qrows, 0), ws(self.n, self.qrows, 1))
             self.qws = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else None
+            # every sample's final state, kept by the forward for the adjoint backward (which then
+            # skips re-running the circuit): 2304 x 2^16 x 8 B = 1.2 GB at 16 qubits -- HBM has room
+            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev) \
+                if os.environ.get("QDML_QSIM_SAVE_STATE", "1") != "0" else None
         else:
             self.qrows = nat.fn(L, "qd_qsim_bwd_grid", [_i, _i])(self.n, batch_total)
             self.qws = None
@@ -108,8 +112,8 @@ class QSCStepHIP:
                                                    _i, _p])
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
-            self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
-            self._qb = nat.fn(L, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
+            self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+            self._qb = nat.fn(L, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
         else:
             self._qf = nat.fn(L, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
             self._qb = nat.fn(L, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
@@ -158,7 +162,8 @@ class QSCStepHIP:
                                     self.Ww, self.grid_fwd, st), "qsc_pre_fwd")
         w = self.quantum_weights().contiguous()
         wgroup = B // w.shape[0] if w.dim() == 4 else 0
-        extra = (nat.ptr(self.qws) if self.qws is not None else None,) if self.big else ()
+        extra = (nat.ptr(self.qws) if self.qws is not None else None,
+                 nat.ptr(self.psave) if self.psave is not None else None) if self.big else ()
         nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, wgroup, *extra, st),
                   "qsim_fwd")
         cls = m.classifier

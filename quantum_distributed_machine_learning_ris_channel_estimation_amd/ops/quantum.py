@@ -52,9 +52,9 @@ def hip_qsim_fwd(x: torch.Tensor, w: torch.Tensor, E: torch.Tensor, wgroup: int 
         return
     grid = nat.fn(lib, "qd_qsim_big_grid", [_i])(B)
     ws = _big_ws(n, grid, False, x.device)
-    f = nat.fn(lib, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
-    nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, nat.ptr(ws) if ws is not None else None, st),
-              "qd_qsim_big_fwd")
+    f = nat.fn(lib, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+    nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, nat.ptr(ws) if ws is not None else None, None,
+                st), "qd_qsim_big_fwd")
 
 
 def hip_qsim_bwd_slab(x: torch.Tensor, w: torch.Tensor, gE: torch.Tensor, dx: torch.Tensor) -> torch.Tensor:
@@ -74,9 +74,9 @@ def hip_qsim_bwd_slab(x: torch.Tensor, w: torch.Tensor, gE: torch.Tensor, dx: to
     rows = nat.fn(lib, "qd_qsim_big_grid", [_i])(B)
     slab = torch.empty(rows, P, device=x.device, dtype=torch.float32)
     ws = _big_ws(n, rows, True, x.device)
-    f = nat.fn(lib, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
+    f = nat.fn(lib, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
     nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup_of(x, w),
-                nat.ptr(ws) if ws is not None else None, st), "qd_qsim_big_bwd")
+                nat.ptr(ws) if ws is not None else None, None, st), "qd_qsim_big_bwd")
     return slab
 
 

@@ -330,3 +330,37 @@ def test_nmse_fused_matches_two_pass(cuda, with_perf):
     b.fused(Y, L, perf, bg_b, (E, U, B), out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
     assert float(b.skip) == 1.0
+
+
+@pytest.mark.parametrize("n,L,B", [(12, 3, 7), (14, 3, 5), (16, 2, 3), (13, 1, 4)])
+def test_qsim_big_saved_state_backward(cuda, n, L, B):
+    """qsim_big with the forward's psi_final kept for the adjoint backward (no recompute) == the
+    recomputing backward, bitwise: same E, dx and weight-gradient slab."""
+    import ctypes
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    lib = nat.hip_lib()
+    _p, _i = ctypes.c_void_p, ctypes.c_int
+    torch.manual_seed(n)
+    x = torch.rand(B, n, device=cuda) * 3.0
+    w = torch.rand(L, n, 2, device=cuda) * 6.28
+    gE = torch.randn(B, n, device=cuda)
+    grid = nat.fn(lib, "qd_qsim_big_grid", [_i])(B)
+    wsb = nat.fn(lib, "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)(n, grid, 1)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=cuda)
+    ps = torch.empty(B * (8 << n), dtype=torch.uint8, device=cuda)
+    f = nat.fn(lib, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+    b = nat.fn(lib, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+    st = nat.stream_ptr(cuda)
+    out = []
+    for save in (False, True):
+        E = torch.empty(B, n, device=cuda)
+        dx = torch.empty(B, n, device=cuda)
+        slab = torch.empty(grid, 2 * n * L, device=cuda)
+        sp = nat.ptr(ps) if save else None
+        nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, 0, nat.ptr(ws), sp, st), "fwd")
+        nat.check(b(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, 0, nat.ptr(ws), sp, st),
+                  "bwd")
+        torch.cuda.synchronize()
+        out.append((E, dx, slab))
+    for a, c in zip(*out):
+        assert torch.equal(a, c), float((a - c).abs().max())
