@@ -163,8 +163,11 @@ __device__ __forceinline__ float sample_sum(float v) {
 }
 
 template <int N>
+// psave (nullable): every sample's final state, [sample][r][lane-in-sample] (coalesced), for the
+// backward to start from instead of re-running the circuit
 __global__ void __launch_bounds__(64) qsim_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                      float* __restrict__ E, int B, int L, int wgroup) {
+                                                      float* __restrict__ E, int B, int L, int wgroup,
+                                                      cf* __restrict__ psave) {
   using C = Cfg<N>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cf* lds = reinterpret_cast<cf*>(smem);
@@ -181,6 +184,10 @@ __global__ void __launch_bounds__(64) qsim_fwd_kernel(const float* __restrict__ 
     const float* ws = w + (wgroup > 0 ? (size_t)(sld / wgroup) * 2 * N * L : 0);
     cf a[C::R];
     run_circuit<N>(a, xs, ws, L, lds, sbase, li);
+    if (psave != nullptr && smp < B) {
+#pragma unroll
+      for (int r = 0; r < C::R; ++r) psave[(size_t)smp * C::D + r * C::LPS + li] = a[r];
+    }
     float p[C::R], ptot = 0.f;
 #pragma unroll
     for (int r = 0; r < C::R; ++r) {
@@ -207,7 +214,8 @@ __global__ void __launch_bounds__(64) qsim_fwd_kernel(const float* __restrict__ 
 template <int N>
 __global__ void __launch_bounds__(64) qsim_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                       const float* __restrict__ gE, float* __restrict__ dx,
-                                                      float* __restrict__ slab, int B, int L, int wgroup) {
+                                                      float* __restrict__ slab, int B, int L, int wgroup,
+                                                      const cf* __restrict__ psave) {
   using C = Cfg<N>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   cf* lds = reinterpret_cast<cf*>(smem);
@@ -231,7 +239,12 @@ __global__ void __launch_bounds__(64) qsim_bwd_kernel(const float* __restrict__ 
     }
     const float* ws = w + (wgroup > 0 ? (size_t)(sld / wgroup) * 2 * N * L : 0);
     cf psi[C::R], lam[C::R];
-    run_circuit<N>(psi, xs, ws, L, lds, sbase, li);
+    if (psave != nullptr) {   // the forward's final state (same x, w): no recompute
+#pragma unroll
+      for (int r = 0; r < C::R; ++r) psi[r] = psave[(size_t)sld * C::D + r * C::LPS + li];
+    } else {
+      run_circuit<N>(psi, xs, ws, L, lds, sbase, li);
+    }
     // lambda = (sum_q g_q Z_q) psi
 #pragma unroll
     for (int r = 0; r < C::R; ++r) {
@@ -323,22 +336,23 @@ __global__ void __launch_bounds__(256) reduce_slab_kernel(const float* __restric
 }
 
 template <int N>
-static int launch_fwd(const float* x, const float* w, float* E, int B, int L, int wgroup, int grid, hipStream_t st) {
+static int launch_fwd(const float* x, const float* w, float* E, int B, int L, int wgroup, int grid, hipStream_t st,
+                      cf* psave = nullptr) {
   using C = Cfg<N>;
   const int need = (B + C::SPW - 1) / C::SPW;
   if (grid <= 0 || grid > need) grid = need;
   const size_t sm = sizeof(cf) * C::SLOTS;
-  hipLaunchKernelGGL(qsim_fwd_kernel<N>, dim3(grid), dim3(64), sm, st, x, w, E, B, L, wgroup);
+  hipLaunchKernelGGL(qsim_fwd_kernel<N>, dim3(grid), dim3(64), sm, st, x, w, E, B, L, wgroup, psave);
   return (int)hipGetLastError();
 }
 
 template <int N>
 static int launch_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int L,
-                      int wgroup, int grid, hipStream_t st) {
+                      int wgroup, int grid, hipStream_t st, const cf* psave = nullptr) {
   using C = Cfg<N>;
   const size_t sm = sizeof(cf) * C::SLOTS + sizeof(float) * 2 * N * L * kWave;
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(qsim_bwd_kernel<N>, dim3(grid), dim3(64), sm, st, x, w, gE, dx, slab, B, L, wgroup);
+  hipLaunchKernelGGL(qsim_bwd_kernel<N>, dim3(grid), dim3(64), sm, st, x, w, gE, dx, slab, B, L, wgroup, psave);
   return (int)hipGetLastError();
 }
 
@@ -384,6 +398,25 @@ QD_API int qd_qsim_bwd(const float* x, const float* w, const float* gE, float* d
   hipStream_t st = (hipStream_t)stream;
   const int grid = qd_qsim_bwd_grid(n, B);
 #define CALL_B(NN) launch_bwd<NN>(x, w, gE, dx, slab, B, L, wgroup, grid, st)
+  QD_DISPATCH_N(n, CALL_B)
+#undef CALL_B
+}
+
+// As qd_qsim_fwd / qd_qsim_bwd, with psave = (B, 2^n) complex64 scratch: the forward keeps each
+// sample's final state there and the backward starts from it (no circuit recompute).
+QD_API int qd_qsim_fwd_save(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* psave,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+#define CALL_F(NN) launch_fwd<NN>(x, w, E, B, L, wgroup, 0, st, (cf*)psave)
+  QD_DISPATCH_N(n, CALL_F)
+#undef CALL_F
+}
+
+QD_API int qd_qsim_bwd_saved(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n,
+                             int L, int wgroup, const void* psave, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = qd_qsim_bwd_grid(n, B);
+#define CALL_B(NN) launch_bwd<NN>(x, w, gE, dx, slab, B, L, wgroup, grid, st, (const cf*)psave)
   QD_DISPATCH_N(n, CALL_B)
 #undef CALL_B
 }

@@ -115,8 +115,12 @@ class QSCStepHIP:
             self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
             self._qb = nat.fn(L, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
         else:
-            self._qf = nat.fn(L, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
-            self._qb = nat.fn(L, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+            # the forward keeps every sample's final state (2^n complex, 4.7 MB at 8 qubits) for the
+            # adjoint backward, which then skips re-running the circuit
+            save = os.environ.get("QDML_QSIM_SAVE_STATE", "1") != "0"
+            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev) if save else None
+            self._qf = nat.fn(L, "qd_qsim_fwd_save", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
+            self._qb = nat.fn(L, "qd_qsim_bwd_saved", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
         self._rs = nat.fn(L, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
         self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _i, _p])
         self._qnoise = nat.fn(L, "qd_qnoise", [_p, _p, _i, _i, _f, ctypes.c_ulonglong, _p, _p])
@@ -163,7 +167,8 @@ class QSCStepHIP:
         w = self.quantum_weights().contiguous()
         wgroup = B // w.shape[0] if w.dim() == 4 else 0
         extra = (nat.ptr(self.qws) if self.qws is not None else None,
-                 nat.ptr(self.psave) if self.psave is not None else None) if self.big else ()
+                 nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
+            (nat.ptr(self.psave) if self.psave is not None else None,)
         nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, wgroup, *extra, st),
                   "qsim_fwd")
         cls = m.classifier

@@ -364,3 +364,40 @@ def test_qsim_big_saved_state_backward(cuda, n, L, B):
         out.append((E, dx, slab))
     for a, c in zip(*out):
         assert torch.equal(a, c), float((a - c).abs().max())
+
+
+@pytest.mark.parametrize("n,L,B", [(4, 3, 37), (6, 2, 9), (8, 3, 33), (10, 3, 5)])
+def test_qsim_saved_state_backward(cuda, n, L, B):
+    """Register-resident simulator: the backward from the forward's saved final state == the
+    recomputing backward (to fp32 rounding: the two kernels' circuit code may contract differently)."""
+    import ctypes
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    lib = nat.hip_lib()
+    _p, _i = ctypes.c_void_p, ctypes.c_int
+    torch.manual_seed(n)
+    x = torch.rand(B, n, device=cuda) * 3.0
+    w = torch.rand(L, n, 2, device=cuda) * 6.28
+    gE = torch.randn(B, n, device=cuda)
+    rows = nat.fn(lib, "qd_qsim_bwd_grid", [_i, _i])(n, B)
+    ps = torch.empty(B * (8 << n), dtype=torch.uint8, device=cuda)
+    st = nat.stream_ptr(cuda)
+    out = []
+    for save in (False, True):
+        E = torch.empty(B, n, device=cuda)
+        dx = torch.empty(B, n, device=cuda)
+        slab = torch.empty(rows, 2 * n * L, device=cuda)
+        if save:
+            f = nat.fn(lib, "qd_qsim_fwd_save", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
+            b = nat.fn(lib, "qd_qsim_bwd_saved", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
+            nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, 0, nat.ptr(ps), st), "fwd")
+            nat.check(b(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, 0, nat.ptr(ps), st),
+                      "bwd")
+        else:
+            f = nat.fn(lib, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
+            b = nat.fn(lib, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+            nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, 0, st), "fwd")
+            nat.check(b(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, 0, st), "bwd")
+        torch.cuda.synchronize()
+        out.append((E, dx, slab))
+    for a, c in zip(*out):
+        assert torch.allclose(a, c, rtol=1e-5, atol=1e-6), float((a - c).abs().max())
