@@ -83,6 +83,7 @@ class FlagshipConfig:
     stream_mode: str = "dagq"    # serial | dag | dagq (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
+    dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1) or the conv backward (2)
     fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
     qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
@@ -287,7 +288,13 @@ class FlagshipTrainer:
     def _dp_g1(self) -> None:
         self._gather()
         self.hstep.defer_dgrad = self.hstep.hip
+        early = self.streams is not None and self.cfg.dp_qsc_phase == 1
+        if early:   # QSC forward/backward beside the HDCE forward (as in the world-1 plan)
+            with self._fork(self.streams["qsc"]):
+                self._qsc_branch(with_opt=False)
         self._hdce_forward(side=False)   # (the FC wgrad on main: the all-reduce waits for it first)
+        if early:
+            self._join(("qsc",))
 
     def _dp_g2(self) -> None:
         # NOTE the first node of a graph must sit on the capturing stream: a branch forked before any
@@ -297,13 +304,14 @@ class FlagshipTrainer:
         ms = self.streams is not None
         if self.hstep.defer_dgrad:
             self.hstep.dgrad()
-        if ms:
+        late = ms and self.cfg.dp_qsc_phase == 2
+        if late:
             with self._fork(self.streams["qsc"]):
                 self._qsc_branch(with_opt=False)
         self.hstep.backward_conv(side=self.streams["conv"] if "c" in self.branches else None)
-        if ms:
+        if late:
             self._join(("qsc",))
-        else:
+        elif not ms:
             self._qsc_branch(with_opt=False)
 
     def _dp_gf(self) -> None:

@@ -36,6 +36,7 @@ for s in $STEPS; do
     q16grid) for g in ${GRIDS:-512 1152 2304}; do QDML_QSIM_BIG_GRID=$g run bench_q16_$g 300 python bench.py --steps 6 --warmup 2 --steps-per-graph 1 --qubits 16 --dtype fp8; done ;;
     convknobs) for k in ${KNOBS:-2,8,4,4 1,8,4,4 4,8,4,4 2,16,4,4 2,4,4,4 2,8,2,4 2,8,8,4 2,8,4,2 2,8,4,8}; do QDML_CONV_KNOBS=$k run bench_conv_${k//,/_} 300 python bench.py --steps 50 --warmup 10; done ;;
     savestate) for v in 1 0 1 0; do QDML_QSIM_SAVE_STATE=$v run bench_save_$v 300 python bench.py --steps 100 --warmup 10; done ;;
+    dpphase) for v in 1 2 1 2; do run bench_dpq_$v 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
     bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
