@@ -43,6 +43,7 @@ def main() -> int:
     ap.add_argument("--steps-per-graph", type=int, default=5,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
     ap.add_argument("--hdce-branches", default="", help="(dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam")
+    ap.add_argument("--stream-priority", action="store_true", help="HDCE chain high priority, QSC branch low")
     ap.add_argument("--dp-qsc-phase", type=int, default=2, choices=[1, 2],
                     help="DP plan: run the QSC beside the HDCE forward (1) or beside the conv backward (2)")
     ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
@@ -69,7 +70,8 @@ def main() -> int:
                          split_graphs=args.split_graphs, stream_mode=args.stream_mode,
                          qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
                          hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
-                         fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase)
+                         fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase,
+                         stream_priority=args.stream_priority)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
@@ -124,6 +126,7 @@ def main() -> int:
                 "qsc_fork": args.qsc_fork,
                 "fc_adam_grid": args.fc_adam_grid,
                 "dp_qsc_phase": args.dp_qsc_phase,
+                "stream_priority": args.stream_priority,
                 "steps_per_graph": args.steps_per_graph if n == 1 else 1,
                 "quantumnat": cfg.use_quantumnat,
             },

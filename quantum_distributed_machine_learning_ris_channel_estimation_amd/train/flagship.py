@@ -83,6 +83,7 @@ class FlagshipConfig:
     stream_mode: str = "dagq"    # serial | dag | dagq (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
+    stream_priority: bool = False  # capture the HDCE chain on a high-priority stream, the QSC branch low
     dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1) or the conv backward (2)
     fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
     qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
@@ -169,8 +170,15 @@ class FlagshipTrainer:
             warnings.warn(f"stream_mode {mode!r} replays two graphs concurrently: numerically unsafe on ROCm 7.x "
                           "(see FlagshipTrainer.__init__); use 'dagq'")
         self.streams = None
+        self.capture_stream = None
         if dev.type == "cuda" and mode != "serial" and self.hstep.hip and self.cstep.hip is not None:
             self.streams = {k: torch.cuda.Stream(dev) for k in ("qsc", "fc", "conv")}
+            if cfg.stream_priority:
+                # the critical HDCE chain is captured on a high-priority stream, the QSC branch on a
+                # low-priority one (lower number = higher priority)
+                lo, hi = torch.cuda.Stream.priority_range()
+                self.capture_stream = torch.cuda.Stream(dev, priority=hi)
+                self.streams["qsc"] = torch.cuda.Stream(dev, priority=lo)
         else:
             mode = "serial"
         self.mode = mode
@@ -206,7 +214,7 @@ class FlagshipTrainer:
                       GraphedStep(rep(lambda: self._hdce_graph(gather=True)), enabled=graphs)]
             else:
                 # one graph: gather, both forwards, NMSE, both backwards, the optimizers
-                gs = [GraphedStep(rep(self._step_body), enabled=graphs)]
+                gs = [GraphedStep(rep(self._step_body), enabled=graphs, capture_stream=self.capture_stream)]
         else:
             if k != 1:
                 raise ValueError("multi-step graphs are a world-1 plan")

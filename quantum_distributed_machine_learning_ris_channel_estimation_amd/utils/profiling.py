@@ -84,7 +84,11 @@ class GraphedStep:
 
     WARMUP = 3
 
-    def __init__(self, fn: Callable[[], None], enabled: bool = True, warmup: Optional[int] = None, pool=None):
+    def __init__(self, fn: Callable[[], None], enabled: bool = True, warmup: Optional[int] = None, pool=None,
+                 capture_stream: Optional["torch.cuda.Stream"] = None):
+        """``capture_stream``: the stream the graph is captured on (e.g. a high-priority one, so the
+        nodes of its chain keep that priority over side branches forked from lower-priority streams)."""
+        self.capture_stream = capture_stream
         self.fn = fn
         self.enabled = enabled and torch.cuda.is_available()
         self.warmup = self.WARMUP if warmup is None else warmup
@@ -99,7 +103,9 @@ class GraphedStep:
                 self.fn()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
+        if self.capture_stream is not None:
+            self.capture_stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.graph(g, pool=self.pool, stream=self.capture_stream):
             self.fn()
         self.graph = g
 

@@ -37,11 +37,12 @@ for s in $STEPS; do
     convknobs) for k in ${KNOBS:-2,8,4,4 1,8,4,4 4,8,4,4 2,16,4,4 2,4,4,4 2,8,2,4 2,8,8,4 2,8,4,2 2,8,4,8}; do QDML_CONV_KNOBS=$k run bench_conv_${k//,/_} 300 python bench.py --steps 50 --warmup 10; done ;;
     savestate) for v in 1 0 1 0; do QDML_QSIM_SAVE_STATE=$v run bench_save_$v 300 python bench.py --steps 100 --warmup 10; done ;;
     dpphase) for v in 1 2 1 2; do run bench_dpq_$v 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
+    prio) for v in "" "--stream-priority" "" "--stream-priority" "--dtype fp8" "--dtype fp8 --stream-priority"; do run bench_prio_${v// /_} 300 python bench.py --steps 100 --warmup 10 $v; done ;;
     bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace ${PROF_EXTRA:-} --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --stream-mode ${MODE:-dagq} ${BENCH_EXTRA:-}) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" && python scripts/prof_timeline.py "$OUT/prof/run_kernel_trace.csv" > "$OUT/prof_timeline.md" ;;
-    prof_fp8) (cd /tmp && export TMPDIR=/tmp && run prof_fp8 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_fp8" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --dtype fp8) && python scripts/prof_summary.py "$OUT/prof_fp8/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_fp8_summary.md" ;;
+    prof_fp8) (cd /tmp && export TMPDIR=/tmp && run prof_fp8 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_fp8" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --dtype fp8 --steps-per-graph 1) && python scripts/prof_summary.py "$OUT/prof_fp8/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_fp8_summary.md" && python scripts/prof_timeline.py "$OUT/prof_fp8/run_kernel_trace.csv" > "$OUT/prof_fp8_timeline.md" ;;
     stamp) run stamp 300 python scripts/stamp_qsc.py ;;
     stamp_conv) run stamp_conv 300 python scripts/stamp_conv.py ;;
     tune) run tune 900 python scripts/tune_kernels.py --what ${TUNE_WHAT:-qsc,conv} ;;
