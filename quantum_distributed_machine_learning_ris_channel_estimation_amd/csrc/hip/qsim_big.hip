@@ -195,6 +195,79 @@ __device__ void high_pass_fwd(const cf* A, cf* B, const float4* trig) {
   __syncthreads();
 }
 
+// Low pass of layer 1 with the layer-0 product state GENERATED per tile (HBM-state builds): the
+// product amplitudes are never written to and re-read from HBM.  trig0: layer-0 (embedding) trig.
+template <int N>
+__device__ void low_pass_fwd_gen(cf* A, cf* tile, const float4* trig, const float4* trig0) {
+  using C = G<N>;
+  static_assert(!C::LDS_STATE, "HBM-state builds");
+  for (int h = 0; h < C::NTILE; ++h) {
+    for (int i = threadIdx.x; i < C::T; i += NT) {
+      const int k = ring_inv<N>(i | (h << C::TB));
+      cf a = {1.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < N; ++q) {
+        const float4 t = trig0[q];
+        a = cmul(a, ((k >> q) & 1) ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
+      }
+      tile[i] = a;
+    }
+    __syncthreads();
+    static_for<0, C::NGRP>([&](auto gc) {
+      constexpr int g0 = 3 * decltype(gc)::value;
+      constexpr int NB = (C::TB - g0) < 3 ? (C::TB - g0) : 3;
+      constexpr int ACT = C::T >> NB;
+      for (int t = threadIdx.x; t < ACT; t += NT) {
+        const int base = ins_bits<g0, NB>(t);
+        cf a[1 << NB];
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j) a[j] = tile[base | (j << g0)];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const float4 tg = trig[g0 + b];
+#pragma unroll
+          for (int j = 0; j < (1 << NB); ++j)
+            if (!((j >> b) & 1)) gate_fwd(a[j], a[j | (1 << b)], tg);
+        }
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j) tile[base | (j << g0)] = a[j];
+      }
+      __syncthreads();
+    });
+    cf* dst = A + (size_t)h * C::T;
+    for (int i = threadIdx.x; i < C::T; i += NT) dst[i] = tile[i];
+    __syncthreads();
+  }
+}
+
+// Last high pass with the <Z_q> reduction fused in: part[q] accumulates sum |psi_k|^2 (+-1) at
+// the ring images k; the state is stored (for the backward) only when B != null.
+template <int N>
+__device__ void high_pass_fwd_expect(const cf* A, cf* B, const float4* trig, float (&part)[N]) {
+  using C = G<N>;
+  for (int c = threadIdx.x; c < C::T; c += NT) {
+    cf a[C::NTILE];
+#pragma unroll
+    for (int h = 0; h < C::NTILE; ++h) a[h] = A[c | (h << C::TB)];
+#pragma unroll
+    for (int b = 0; b < C::HB; ++b) {
+      const float4 tg = trig[C::TB + b];
+#pragma unroll
+      for (int h = 0; h < C::NTILE; ++h)
+        if (!((h >> b) & 1)) gate_fwd(a[h], a[h | (1 << b)], tg);
+    }
+#pragma unroll
+    for (int h = 0; h < C::NTILE; ++h) {
+      const int k = ring_fwd<N>(c | (h << C::TB));
+      if (B != nullptr) B[k] = a[h];
+      const float p = a[h].x * a[h].x + a[h].y * a[h].y;
+#pragma unroll
+      for (int q = 0; q < N; ++q) part[q] += ((k >> q) & 1) ? -p : p;
+    }
+  }
+  __syncthreads();
+}
+
 // Full forward circuit of one sample; returns the buffer holding psi_final (A or B).
 // final_out (HBM-state builds, L > 1): the last high pass stores psi_final there instead of B.
 template <int N>
@@ -250,19 +323,47 @@ __global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restric
   for (int s = blockIdx.x; s < B; s += gridDim.x) {
     const float* wsmp = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * N * L : 0);
     cf* sv = psave ? psave + (size_t)s * C::D : nullptr;
-    cf* psi = run_circuit<N>(A, Bf, tile, trig, x + (size_t)s * N, wsmp, L, C::LDS_STATE ? nullptr : sv);
-    if (sv != nullptr && psi != sv) {   // (LDS-resident state, or L == 1)
-      for (int k = threadIdx.x; k < C::D; k += NT) sv[k] = psi[k];
-    }
     float part[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) part[q] = 0.f;
-    for (int k = threadIdx.x; k < C::D; k += NT) {
-      const cf a = psi[k];
-      const float p = a.x * a.x + a.y * a.y;
-#pragma unroll
-      for (int q = 0; q < N; ++q) part[q] += ((k >> q) & 1) ? -p : p;
+    if constexpr (!C::LDS_STATE) {
+      if (L >= 2) {
+        // HBM-resident state: layer 0 generated inside layer 1's low pass, <Z> reduced inside the
+        // last high pass -- 3 state reads + 4 writes (3 without psave) instead of 5 + 5
+        float4* trig0 = reinterpret_cast<float4*>(smem + O_ACC);
+        layer_trig(trig0, wsmp, x + (size_t)s * N, N);
+        cf* Acur = A;
+        cf* Bcur = Bf;
+        for (int l = 1; l < L; ++l) {
+          layer_trig(trig, wsmp + 2 * N * l, nullptr, N);
+          __syncthreads();
+          if (l == 1) low_pass_fwd_gen<N>(Acur, tile, trig, trig0);
+          else low_pass_fwd<N>(Acur, tile, trig);
+          if (l == L - 1) {
+            high_pass_fwd_expect<N>(Acur, sv, trig, part);
+          } else {
+            high_pass_fwd<N>(Acur, Bcur, trig);
+            cf* t = Acur;
+            Acur = Bcur;
+            Bcur = t;
+          }
+        }
+        goto reduce;
+      }
     }
+    {
+      cf* psi = run_circuit<N>(A, Bf, tile, trig, x + (size_t)s * N, wsmp, L, C::LDS_STATE ? nullptr : sv);
+      if (sv != nullptr && psi != sv) {   // (LDS-resident state, or L == 1)
+        for (int k = threadIdx.x; k < C::D; k += NT) sv[k] = psi[k];
+      }
+      for (int k = threadIdx.x; k < C::D; k += NT) {
+        const cf a = psi[k];
+        const float p = a.x * a.x + a.y * a.y;
+#pragma unroll
+        for (int q = 0; q < N; ++q) part[q] += ((k >> q) & 1) ? -p : p;
+      }
+    }
+  reduce:
     if (threadIdx.x < N) outv[threadIdx.x] = 0.f;
     __syncthreads();
     block_add<N>(part, red, outv, 0);
@@ -272,9 +373,9 @@ __global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restric
 }
 
 // slab: (gridDim.x, 2*N*L) partial weight grads (one row per workgroup); dx: (B, N)
-template <int N>
 // psave (nullable): psi_final of every sample from qsim_big_fwd_kernel (same x, w); the backward
 // starts from it instead of re-running the circuit (the buffer is consumed: it may be overwritten)
+template <int N>
 __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ gE, float* __restrict__ dx,
                                                           float* __restrict__ slab, int B, int L, int wgroup,
