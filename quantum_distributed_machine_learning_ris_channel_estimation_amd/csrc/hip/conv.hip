@@ -204,11 +204,11 @@ __device__ void bn_bwd_build(const BnBwd& bn, const float* __restrict__ st, floa
 // wt: B fragments pre-packed by pack_weights_kernel (fwd or dgrad order).
 // ------------------------------------------------------------------------------------------
 template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN, bool STAMP = false>
-__global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
-                                                      const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
-                                                      void* __restrict__ out, float* __restrict__ stats, int E, int B,
-                                                      int chunks, int spw, BnFwd bnf, BnBwd bnb, BnRed brd,
-                                                      unsigned long long* __restrict__ stamps = nullptr) {
+__device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
+                                             const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
+                                             void* __restrict__ out, float* __restrict__ stats, int E, int B,
+                                             int chunks, int spw, BnFwd bnf, BnBwd bnb, BnRed brd,
+                                             unsigned long long* __restrict__ stamps, int bx, int by, int gdx) {
   // STAMP (diagnostic builds): per wave [0] start [1] weights + BN params staged [2] first sample
   // staged [3] first sample's MFMAs + epilogue [4] all samples [5] end
   unsigned long long ts[8] = {};
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int hh = lane >> 5, l32 = lane & 31;
-  const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
+  const int u = bx / chunks, chunk = bx % chunks, e = by;
   const int EC_in = E * CIN;
   static_assert(TILE % 8 == 0, "16-byte tile fills");
   __bf16* tile = reinterpret_cast<__bf16*>(smem) + wv * TILE;
@@ -494,8 +494,18 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
   if constexpr (STAMP) {
     ts[5] = phase_stamp();
     if (lane == 0)
-      for (int k = 0; k < 8; ++k) stamps[((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wv) * 8 + k] = ts[k];
+      for (int k = 0; k < 8; ++k) stamps[((size_t)(by * gdx + bx) * 4 + wv) * 8 + k] = ts[k];
   }
+}
+
+template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN, bool STAMP = false>
+__global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
+                                                      const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
+                                                      void* __restrict__ out, float* __restrict__ stats, int E, int B,
+                                                      int chunks, int spw, BnFwd bnf, BnBwd bnb, BnRed brd,
+                                                      unsigned long long* __restrict__ stamps = nullptr) {
+  conv3x3_body<CIN, H, W, INM, OUTM, DGRAD, TIN, STAMP>(xin, zaux, st_in, wt, out, stats, E, B, chunks, spw, bnf, bnb,
+                                                        brd, stamps, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -547,12 +557,10 @@ __global__ void pack_weights_multi_kernel(PackJobs jobs) {
 // x = layer input (raw f32 pilots, or BN+ReLU of the previous z); dz from (dh, z, st).
 // ------------------------------------------------------------------------------------------
 template <int CIN, int H, int W, int INM, typename TIN, typename TDH>
-__global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __restrict__ xin,
-                                                            const float* __restrict__ st_prev,
-                                                            const TDH* __restrict__ dh,
-                                                            const uint16_t* __restrict__ z,
-                                                            const float* __restrict__ st, float* __restrict__ slab,
-                                                            int E, int B, int chunks, int spb, BnBwd bnb) {
+__device__ __forceinline__ void conv3x3_wgrad_body(const TIN* __restrict__ xin, const float* __restrict__ st_prev,
+                                                   const TDH* __restrict__ dh, const uint16_t* __restrict__ z,
+                                                   const float* __restrict__ st, float* __restrict__ slab, int E, int B,
+                                                   int chunks, int spb, BnBwd bnb, int bx, int by, int gdx) {
   using G = Geo<H, W>;
   constexpr int MTW = (9 * CIN + 31) / 32;        // accumulator tiles (9 for CIN=32, 1 for CIN=2)
   constexpr int XCS = G::HP * W + 8;              // channel stride of the shifted copies (bf16)
@@ -568,7 +576,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
   __bf16* DZ = X + XELEMS;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int hh = lane >> 5, l32 = lane & 31;
-  const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
+  const int u = bx / chunks, chunk = bx % chunks, e = by;
   // zero halo rows (0 and HP-1) of every shifted copy; interior rows are rewritten per sample
   for (int i = tid; i < 3 * CIN * 2 * (W / 8); i += 256) {
     const int cc = i / (2 * (W / 8)), r = (i / (W / 8)) & 1, q = i % (W / 8);
@@ -714,10 +722,43 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __rest
     __syncthreads();
   }
   const float* r0 = reinterpret_cast<const float*>(smem);
-  float* srow = slab + ((size_t)e * gridDim.x + blockIdx.x) * CO * CIN * 9;
+  float* srow = slab + ((size_t)e * gdx + bx) * CO * CIN * 9;
   for (int i = tid; i < CO * CIN * 9; i += 256) {
     const int co = i / (CIN * 9), m = i % (CIN * 9);
     srow[i] = r0[co * RS + m] + r0[32 * RS + co * RS + m];
+  }
+}
+
+template <int CIN, int H, int W, int INM, typename TIN, typename TDH>
+__global__ void __launch_bounds__(256, 2) conv3x3_wgrad_kernel(const TIN* __restrict__ xin,
+                                                            const float* __restrict__ st_prev,
+                                                            const TDH* __restrict__ dh,
+                                                            const uint16_t* __restrict__ z,
+                                                            const float* __restrict__ st, float* __restrict__ slab,
+                                                            int E, int B, int chunks, int spb, BnBwd bnb) {
+  conv3x3_wgrad_body<CIN, H, W, INM, TIN, TDH>(xin, st_prev, dh, z, st, slab, E, B, chunks, spb, bnb, blockIdx.x,
+                                               blockIdx.y, gridDim.x);
+}
+
+// One launch for a 32-channel layer's weight gradient AND data gradient (bf16 dh / dx): the two are
+// independent (they share only their inputs), so their workgroups run side by side -- blocks
+// [0, gx_w) take the wgrad body, the rest the dgrad body -- without a graph branch (whose cross-
+// queue edges cost more than the overlap wins).  Each body is exactly its own kernel's.
+template <int W>
+__global__ void __launch_bounds__(256, 2) conv3x3_wd_kernel(const uint16_t* __restrict__ xin,
+                                                         const float* __restrict__ st_prev,
+                                                         const uint16_t* __restrict__ dh,
+                                                         const uint16_t* __restrict__ z, const float* __restrict__ st,
+                                                         float* __restrict__ slab, int chunks_w, int spb, BnBwd bnb,
+                                                         const uint16_t* __restrict__ wt, uint16_t* __restrict__ dx,
+                                                         int chunks_d, int spw, BnRed brd, int E, int B, int gx_w) {
+  if ((int)blockIdx.x < gx_w) {
+    conv3x3_wgrad_body<32, 16, W, IN_BNRELU, uint16_t, uint16_t>(xin, st_prev, dh, z, st, slab, E, B, chunks_w, spb,
+                                                                 bnb, blockIdx.x, blockIdx.y, gx_w);
+  } else {
+    conv3x3_body<32, 16, W, IN_BNBWD, OUT_BF16, true, uint16_t>(dh, z, st, wt, dx, nullptr, E, B, chunks_d, spw,
+                                                                 BnFwd{}, bnb, brd, nullptr, blockIdx.x - gx_w,
+                                                                 blockIdx.y, gridDim.x - gx_w);
   }
 }
 
@@ -1189,6 +1230,28 @@ QD_API int qd_conv_wgrad(int layer, const void* xin, const float* st_prev, const
     if (dh_bf16) { QD_WG(32, IN_BNRELU, uint16_t, uint16_t) } else { QD_WG(32, IN_BNRELU, uint16_t, float) }
   }
 #undef QD_WG
+  return (int)hipGetLastError();
+}
+
+// wgrad + dgrad of a 32-channel layer in ONE launch (bf16 dh and dx; see conv3x3_wd_kernel).  Arguments
+// as qd_conv_wgrad (layer 2 / 3) and qd_conv_dgrad.
+QD_API int qd_conv_wgrad_dgrad(const uint16_t* xin, const float* st_prev, const uint16_t* dh, const uint16_t* z,
+                               const float* st, float* slab, int chunks_w, int spb, const uint16_t* w, uint16_t* dx,
+                               int chunks_d, int spw, int N, int E, int B, int H, int W, const BnBwd* bnb,
+                               const BnRed* bred, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const BnBwd bb = bnb ? *bnb : BnBwd{};
+  const BnRed br = bred ? *bred : BnRed{};
+  if (chunks_w * spb < B || chunks_d * 4 * spw < B) return (int)hipErrorInvalidValue;
+  const int gx_w = (N / B) * chunks_w, gx_d = (N / B) * chunks_d;
+  dim3 grid(gx_w + gx_d, E);
+  const size_t sm_w = wgrad_smem(32, H, W), sm_d = fwd_smem(32, H, W);
+  const size_t sm = sm_w > sm_d ? sm_w : sm_d;
+  QD_GEOM(WW, {
+    if (hipError_t e = qd::allow_lds(conv3x3_wd_kernel<WW>, sm)) return (int)e;
+    hipLaunchKernelGGL((conv3x3_wd_kernel<WW>), grid, dim3(256), sm, s, xin, st_prev, dh, z, st, slab, chunks_w, spb, bb,
+                       w, dx, chunks_d, spw, br, E, B, gx_w);
+  })
   return (int)hipGetLastError();
 }
 

@@ -101,6 +101,11 @@ class ConvStackHIP:
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _i, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
+        self._wd = nat.fn(L, "qd_conv_wgrad_dgrad", [_p, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i,
+                                                        _p, _p, _p])
+        # wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate launches)
+        import os
+        self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
 
     def pack_weights(self, st) -> None:
         """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch."""
@@ -174,6 +179,17 @@ class ConvStackHIP:
             xin = self.x1 if k == 0 else self.z[k - 1]
             st_prev = None if k == 0 else self.st[k - 1]
             ws = self.wslab[k]
+            if k > 0 and self.fuse_wd and dh_bf and self.dx_bf16 and side is None:
+                # weight AND data gradient of this layer in one launch (independent: side by side)
+                dx = self.dx[k - 1]
+                brd = BnRed(nat.ptr(self.z[k - 1]), nat.ptr(self.st[k - 1]), nat.ptr(self.rslab[k - 1])) \
+                    if self.fuse_bn_red else None
+                nat.check(self._wd(nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), nat.ptr(z), nat.ptr(bst), nat.ptr(ws),
+                                   self.chunks_wl[k], self.spb_wl[k], nat.ptr(self.wpk_t[k]), nat.ptr(dx), self.chunks,
+                                   self.spw, self.N, self.E, self.B, self.H, self.W, ctypes.byref(bnb),
+                                   ctypes.byref(brd) if brd is not None else None, st), f"conv_wgrad_dgrad{k + 1}")
+                dh, dh_bf = dx, 1
+                continue
             on_side = side is not None and k > 0
             if on_side:
                 side.wait_stream(main)

@@ -38,6 +38,7 @@ for s in $STEPS; do
     savestate) for v in 1 0 1 0; do QDML_QSIM_SAVE_STATE=$v run bench_save_$v 300 python bench.py --steps 100 --warmup 10; done ;;
     dpphase) for v in 1 2 1 2; do run bench_dpq_$v 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
     prio) for v in "" "--stream-priority" "" "--stream-priority" "--dtype fp8" "--dtype fp8 --stream-priority"; do run bench_prio_${v// /_} 300 python bench.py --steps 100 --warmup 10 $v; done ;;
+    fusewd) for v in 1 0 1 0; do QDML_CONV_FUSE_WD=$v run bench_fwd_$v 300 python bench.py --steps 100 --warmup 10; mv $OUT/bench_fwd_$v.log $OUT/bench_fwd_${v}_$RANDOM.log; done ;;
     bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
