@@ -544,9 +544,12 @@ struct PackJobs {
   const float* w[8];
   uint16_t* out[8];
   int cin[8], ks[8], dgrad[8];
+  int* cursor;      // optional: *cursor += cursor_inc (the step's batch cursor, advanced here when the
+  int cursor_inc;   // pack runs at the END of a step, after everything that read the cursor)
 };
 __global__ void pack_weights_multi_kernel(PackJobs jobs) {
   const int j = blockIdx.z, s = blockIdx.x;
+  if (jobs.cursor != nullptr && j == 0 && s == 0 && blockIdx.y == 0 && threadIdx.x == 0) *jobs.cursor += jobs.cursor_inc;
   if (s >= jobs.ks[j]) return;
   pack_weights_body(jobs.w[j], jobs.out[j], jobs.cin[j], jobs.ks[j], jobs.dgrad[j], s, blockIdx.y);
 }
@@ -1119,10 +1122,19 @@ QD_API int qd_conv_pack_weights(const float* w, uint16_t* out, int E, int cin, i
 }
 
 // n jobs (<= 8): w[j] fp32 (E, 32, cin[j], 3, 3) -> out[j] packed (dgrad[j] selects the dgrad order)
+QD_API int qd_conv_pack_weights_multi2(int n, const float* const* w, uint16_t* const* out, const int* cin,
+                                       const int* dgrad, int E, int* cursor, int cursor_inc, void* stream);
 QD_API int qd_conv_pack_weights_multi(int n, const float* const* w, uint16_t* const* out, const int* cin,
                                       const int* dgrad, int E, void* stream) {
+  return qd_conv_pack_weights_multi2(n, w, out, cin, dgrad, E, nullptr, 0, stream);
+}
+// cursor (nullable): advanced by cursor_inc in the same launch (see PackJobs)
+QD_API int qd_conv_pack_weights_multi2(int n, const float* const* w, uint16_t* const* out, const int* cin,
+                                       const int* dgrad, int E, int* cursor, int cursor_inc, void* stream) {
   if (n < 1 || n > 8) return (int)hipErrorInvalidValue;
   PackJobs jobs{};
+  jobs.cursor = cursor;
+  jobs.cursor_inc = cursor_inc;
   int ksmax = 0;
   for (int j = 0; j < n; ++j) {
     jobs.w[j] = w[j];

@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(256) gather_step_kernel(const long* __restrict
       rowden[(size_t)(u * B + b) * E + e] = make_float2(rowpow_l[ro], rowpow_p ? rowpow_p[ro] : 0.f);
     }
   }
-  if (cursor == nullptr) return;
+  if (cursor == nullptr || done == nullptr) return;   // (read-only cursor: someone else advances it)
   // the last workgroup to arrive advances the cursor: every workgroup read *cursor before arriving
   // (same protocol as the optimizer's step tick, csrc/hip/optim.hip)
   __shared__ bool last;
@@ -92,10 +92,13 @@ QD_API int qd_gather_cursor(const long* perm, long nperm, int* cursor, unsigned 
                             const float* rowpow_p, float* rowden, const float* Yp, long yp_stream_stride,
                             float* x1, float* xq, int* rowoff, long lab_stream_rows, int E, int U, int B, int plane,
                             void* stream) {
-  if (plane % 4 || E < 1 || U < 1 || B < 1 || !cursor || !done || nperm < B) return (int)hipErrorInvalidValue;
+  // done == null: the cursor is only read (the caller advances it later in the step, e.g. the
+  // end-of-step weight pack) -- no same-address atomics, so the grid need not be capped
+  if (plane % 4 || E < 1 || U < 1 || B < 1 || !cursor || nperm < B) return (int)hipErrorInvalidValue;
   if ((x1 == nullptr) != (rowoff == nullptr) || (rowden && (!rowoff || !rowpow_l))) return (int)hipErrorInvalidValue;
   const int waves = E * U * B;
-  const int grid = (waves + 3) / 4 < 128 ? (waves + 3) / 4 : 128;
+  const int cap = done ? 128 : 4096;
+  const int grid = (waves + 3) / 4 < cap ? (waves + 3) / 4 : cap;
   hipLaunchKernelGGL(gather_step_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, perm, Yp,
                      yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, cursor, done, nperm,
                      rowpow_l, rowpow_p, reinterpret_cast<float2*>(rowden));

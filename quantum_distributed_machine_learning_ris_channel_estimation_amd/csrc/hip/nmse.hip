@@ -365,11 +365,11 @@ __global__ void __launch_bounds__(256) nmse_finish_kernel(const float* __restric
     }
     return;
   }
-  if (threadIdx.x >= 64) return;
-  const int lane = threadIdx.x;
+  // per-stream sums: wave w takes streams w, w + waves, ... (each in a fixed order); then thread 0
+  // forms the loss over the streams in order (deterministic)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int S = E * U;
-  float l = 0.f, lp = 0.f;
-  for (int s = 0; s < S; ++s) {
+  for (int s = wv; s < S; s += nw) {
     const int e = s / U, u = s % U;
     float n = 0.f, np = 0.f;
     for (int j = lane; j < chunks_per_u * gx; j += 64) {
@@ -380,17 +380,20 @@ __global__ void __launch_bounds__(256) nmse_finish_kernel(const float* __restric
     }
     n = wave_sum(n);
     np = wave_sum(np);
-    const float den = dens[s * 2], denp = dens[s * 2 + 1];
     if (lane == 0) {
       ss[s * 4 + 0] = n;
-      ss[s * 4 + 1] = den;
+      ss[s * 4 + 1] = dens[s * 2];
       ss[s * 4 + 2] = np;
-      ss[s * 4 + 3] = denp;
+      ss[s * 4 + 3] = dens[s * 2 + 1];
     }
-    l += n / den;
-    lp += denp > 0.f ? np / denp : 0.f;
   }
-  if (lane == 0) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f, lp = 0.f;
+    for (int s = 0; s < S; ++s) {
+      l += ss[s * 4 + 0] / ss[s * 4 + 1];
+      lp += ss[s * 4 + 3] > 0.f ? ss[s * 4 + 2] / ss[s * 4 + 3] : 0.f;
+    }
     loss[0] = l / (float)S;
     loss[1] = lp / (float)S;
     if (skip) *skip = isfinite(loss[0]) ? 0.f : 1.f;
@@ -405,10 +408,13 @@ using namespace qd::nmse;
 // One-pass NMSE + dY + bias gradient (see nmse_fused_kernel).  rows = U*B*E; rpc % E == 0 and
 // (B*E) % rpc == 0; cols % 1024 == 0.  colsum: (rows/rpc, cols); part: (rows/rpc, cols/1024, E, 2);
 // dens: (S, 2); ss: (S, 4) as qd_nmse_reduce_finalize's.  perf / rowpow_p nullable together.
+// finish_bias = 0: the finish launch only forms the loss; the caller reduces colsum -> bias_grad itself
+// (e.g. as one job of a later batched slab reduction, off the critical path).
 QD_API int qd_nmse_fused(const void* Y, int y_bf16, const float* label, const float* perf, const int* rowoff,
                          const float* rowpow_l, const float* rowpow_p, void* dY, int dy_bf16, float* colsum,
                          float* part, float* dens, float* bias_grad, float* ss, float* loss, float* skip, int E, int U,
-                         int B, int cols, int rpc, float loss_scale, const float* rowden, void* stream) {
+                         int B, int cols, int rpc, float loss_scale, const float* rowden, int finish_bias,
+                         void* stream) {
   if (cols % 1024 || rpc < E || rpc % E || (B * E) % rpc || (perf == nullptr) != (rowpow_p == nullptr))
     return (int)hipErrorInvalidValue;
   const int rows = U * B * E;
@@ -434,7 +440,8 @@ QD_API int qd_nmse_fused(const void* Y, int y_bf16, const float* label, const fl
 #undef QD_F
   const int chunks = rows / rpc;
 #define QD_N(EE)                                                                                                   \
-  hipLaunchKernelGGL((nmse_finish_kernel<EE>), dim3(cols / 64 + 1), dim3(256), 0, st, colsum, part, dens, bias_grad, ss, \
+  hipLaunchKernelGGL((nmse_finish_kernel<EE>), dim3(finish_bias ? cols / 64 + 1 : 1),                          \
+                     dim3(256), 0, st, colsum, part, dens, bias_grad, ss, \
                      loss, skip, chunks, (int)grid.x, cols, (B * E) / rpc, U)
   switch (E) {
     case 1: QD_N(1); break;

@@ -101,20 +101,26 @@ class ConvStackHIP:
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _i, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
+        self._packm2 = nat.fn(L, "qd_conv_pack_weights_multi2", [_i, _p, _p, _p, _p, _i, _p, _i, _p])
+        # pack_at_tail: the owner packs the weights at the END of each step (after the optimizer) and
+        # the forward reads the packed images as they are (one launch less at the head of the chain)
+        self.pack_at_tail = False
         self._wd = nat.fn(L, "qd_conv_wgrad_dgrad", [_p, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i,
                                                         _p, _p, _p])
         # wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate launches)
         import os
         self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
 
-    def pack_weights(self, st) -> None:
-        """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch."""
+    def pack_weights(self, st, cursor: Optional[torch.Tensor] = None, cursor_inc: int = 0) -> None:
+        """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch.
+        ``cursor`` (int32 device, optional): advanced by ``cursor_inc`` in the same launch."""
         jobs = [(k, 0) for k in range(3)] + [(k, 1) for k in (1, 2)]
         w = (ctypes.c_void_p * 8)(*[nat.ptr(self.m.conv_w[k]) for k, _ in jobs])
         out = (ctypes.c_void_p * 8)(*[nat.ptr(self.wpk_t[k] if d else self.wpk[k]) for k, d in jobs])
         cin = (ctypes.c_int * 8)(*[self.cins[k] for k, _ in jobs])
         dg = (ctypes.c_int * 8)(*[d for _, d in jobs])
-        nat.check(self._packm(len(jobs), w, out, cin, dg, self.E, st), "conv_pack_weights")
+        nat.check(self._packm2(len(jobs), w, out, cin, dg, self.E, _ptr(cursor), int(cursor_inc), st),
+                  "conv_pack_weights")
 
     # --------------------------------------------------------------------- forward
     def forward(self, x1: torch.Tensor, training: bool) -> torch.Tensor:
@@ -122,7 +128,8 @@ class ConvStackHIP:
         m, st = self.m, nat.stream_ptr(x1.device)
         assert x1.shape == (self.N, 2 * self.E, self.H, self.W) and x1.dtype == torch.float32 and x1.is_contiguous()
         self.x1 = x1
-        self.pack_weights(st)
+        if not self.pack_at_tail:
+            self.pack_weights(st)
         hook = self.stage_hook
         if hook is not None:
             hook("packed")

@@ -12,6 +12,7 @@ index vector ``idx`` (B,) over a ``DMLStore``, fills
 from __future__ import annotations
 
 import ctypes
+from typing import Optional
 
 import torch
 
@@ -34,14 +35,16 @@ class StepGather:
         self.rowpow = None
         self.rowden = torch.zeros(U * B * E, 2, device=dev)
 
-    def from_cursor(self, store, perm: torch.Tensor, cursor: torch.Tensor, done: torch.Tensor, hdce: bool = True,
-                    classifier: bool = True) -> None:
+    def from_cursor(self, store, perm: torch.Tensor, cursor: torch.Tensor, done: Optional[torch.Tensor],
+                    hdce: bool = True, classifier: bool = True) -> None:
         """Batch ``perm[*cursor : *cursor + B]`` (device cursor, int32 (1,)), then ``*cursor += B`` -- all
         in the one launch, so the batch selection is part of a captured graph.  ``hdce`` fills x1 and
         rowoff, ``classifier`` fills xq (two graphs on two streams each gather their half with their
-        own cursor).  ``done``: int32 (1,) zero-initialised scratch (last-workgroup counter)."""
+        own cursor).  ``done``: int32 (1,) zero-initialised scratch (last-workgroup counter); None = only
+        READ the cursor (the caller advances it later in the step)."""
         Yp, HL = store.Yp, store.Hlabel
-        assert perm.dtype == torch.int64 and cursor.dtype == torch.int32 and done.dtype == torch.int32
+        assert perm.dtype == torch.int64 and cursor.dtype == torch.int32
+        assert done is None or done.dtype == torch.int32
         cols = HL.shape[-1]
         if Yp.is_cuda:
             assert Yp.dtype == torch.float32 and Yp[0, 0].is_contiguous() and Yp.stride(1) == self.plane
@@ -52,7 +55,7 @@ class StepGather:
             rp = self.rowpow if (hdce and self.rowpow is not None) else None
             xq = self.xq if classifier else None
             assert not classifier or xq is not None
-            nat.check(f(nat.ptr(perm), perm.numel(), nat.ptr(cursor), nat.ptr(done),
+            nat.check(f(nat.ptr(perm), perm.numel(), nat.ptr(cursor), nat.ptr(done) if done is not None else None,
                         nat.ptr(rp[0]) if rp else None, nat.ptr(rp[1]) if rp and rp[1] is not None else None,
                         nat.ptr(self.rowden) if rp else None, nat.ptr(Yp), Yp.stride(0),
                         nat.ptr(self.x1) if hdce else None, nat.ptr(xq) if xq is not None else None,
@@ -78,7 +81,8 @@ class StepGather:
                 self.xq.copy_(g.reshape(self.S * self.B, 2, self.H, self.W))
         finally:
             self.xq = xq_saved
-        cursor.fill_(c + self.B)
+        if done is not None:
+            cursor.fill_(c + self.B)
 
     def __call__(self, store, idx: torch.Tensor) -> None:
         Yp, HL = store.Yp, store.Hlabel

@@ -175,10 +175,13 @@ class StreamNMSE:
 
     def fused(self, Y: torch.Tensor, label: torch.Tensor, perf: Optional[torch.Tensor], bias_grad: torch.Tensor,
               layout: Tuple[int, int, int], out_dtype=torch.bfloat16, loss_scale: float = 1.0,
-              rpc_mult: Optional[int] = None, rowden: Optional[torch.Tensor] = None) -> torch.Tensor:
+              rpc_mult: Optional[int] = None, rowden: Optional[torch.Tensor] = None,
+              bias_slabs=None) -> torch.Tensor:
         """GPU, labels through ``rowoff``, rows in (u, b, e) order with ``layout`` = (E, U, B): loss,
         loss_perf, skip, dY and the bias gradient (overwritten into ``bias_grad``) in TWO launches
-        (csrc/hip/nmse.hip qd_nmse_fused).  Returns dY; the loss is ``self.loss``."""
+        (csrc/hip/nmse.hip qd_nmse_fused).  Returns dY; the loss is ``self.loss``.
+        ``bias_slabs`` (ops.slabsum.SlabBatch): queue the bias-gradient column reduction on it instead
+        (the caller launches it in overwrite mode later in the step)."""
         E, U, B = layout
         assert Y.is_cuda and self.rowoff is not None and Y.shape == (self.rows, self.cols) and self.rows == E * U * B
         self._check_labels(label)
@@ -196,13 +199,16 @@ class StreamNMSE:
         rl = self._row_powers(label)
         rp = self._row_powers(perf) if perf is not None else None
         f = nat.fn(nat.hip_lib(), "qd_nmse_fused", [_p, _i, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p,
-                                                    _i, _i, _i, _i, _i, _f, _p, _p])
+                                                    _i, _i, _i, _i, _i, _f, _p, _i, _p])
         nat.check(f(nat.ptr(Y), int(Y.dtype == torch.bfloat16), nat.ptr(label),
                     nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowoff), nat.ptr(rl),
                     nat.ptr(rp) if rp is not None else None, nat.ptr(dY), int(out_dtype == torch.bfloat16),
                     nat.ptr(colsum), nat.ptr(part), nat.ptr(dens), nat.ptr(bias_grad), nat.ptr(self.ss),
                     nat.ptr(self.loss), nat.ptr(self.skip), E, U, B, self.cols, rpc, loss_scale,
-                    nat.ptr(rowden) if rowden is not None else None, nat.stream_ptr(dev)), "nmse_fused")
+                    nat.ptr(rowden) if rowden is not None else None, int(bias_slabs is None), nat.stream_ptr(dev)),
+                  "nmse_fused")
+        if bias_slabs is not None:
+            bias_slabs.add(colsum, bias_grad, 1, chunks, self.cols)
         return dY
 
     def __call__(self, Y, label, perf=None, out_dtype=torch.float32) -> Tuple[torch.Tensor, torch.Tensor]:

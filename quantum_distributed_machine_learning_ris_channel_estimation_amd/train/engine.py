@@ -35,6 +35,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import _native as nat
 from ..models.estimators import Conv_P128, FC_P128, QSC_P128, SC_P128, pilot_grid
 from ..ops.nmse import StreamNMSE
 from ..ops.optim import FlatParamSpace
@@ -269,6 +270,9 @@ class HDCEStep:
         self.fc_side = None   # optional stream for the FC weight-gradient GEMM (HIP path)
         self.fused_nmse = True  # HIP path: the one-pass NMSE (qd_nmse_fused) when labels come via rowoff
         self.defer_dgrad = False
+        # world-1 plans: the FC bias gradient's column reduction rides in the conv backward's slab launch
+        # (never in DP: the FC gradient bucket is all-reduced before the conv backward runs)
+        self.bias_via_conv_slabs = False
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         if self.hip:
             from ..ops.conv import ConvStackHIP
@@ -323,7 +327,16 @@ class HDCEStep:
         caller launches it in overwrite mode).  ``side``: stream for the conv weight-gradient kernels
         (see ConvStackHIP.backward)."""
         if self.hip:
-            self.conv.backward(self._dA, accumulate=False, slabs=slabs, side=side)
+            pending = getattr(self, "_slabs", None)
+            self._slabs = None
+            if pending is not None and slabs is None:
+                # the conv weight / BN slabs and the pending FC bias reduction: one overwrite launch
+                self.conv.backward(self._dA, accumulate=False, slabs=pending, side=side)
+                pending.launch(accumulate=False, stream=nat.stream_ptr(self._dA.device))
+            else:
+                if pending is not None:
+                    pending.launch(accumulate=False, stream=nat.stream_ptr(self._dA.device))
+                self.conv.backward(self._dA, accumulate=False, slabs=slabs, side=side)
         else:
             torch.autograd.backward(self._A, self._dA)
             self._A = None
@@ -355,8 +368,12 @@ class HDCEStep:
             hook("fc")
         if self.nmse.rowoff is not None and self.fused_nmse and self.nmse.cols % 1024 == 0:
             # one pass: loss, skip, dY, bias-gradient partials (+ one finish launch)
+            # (the FC bias gradient's column reduction joins the conv backward's slab batch: one launch less
+            # between the loss and the FC gradient GEMMs)
+            from ..ops.slabsum import SlabBatch
+            self._slabs = SlabBatch() if (self.writes_grads and self.bias_via_conv_slabs) else None
             dY = self.nmse.fused(Y, label, perf, m.fc_b.grad, (m.E, self.U, self.B), out_dtype=dt,
-                                 rowden=getattr(self, "_rowden", None))
+                                 rowden=getattr(self, "_rowden", None), bias_slabs=self._slabs)
             loss = self.nmse.loss
         else:
             loss = self.nmse.sums_finalize(Y, label, perf)

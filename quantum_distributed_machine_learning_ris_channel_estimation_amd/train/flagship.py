@@ -7,23 +7,27 @@ NLL, AdamW, optional QuantumNAT noise and gradient pruning) and the HDCE estimat
 (3 scenario experts + shared FC, per-stream NMSE, Adam), both forward + backward +
 optimizer, on HBM-resident synthetic data.
 
-Execution plan per step (world = 1): one HIP graph replay containing index gather,
-both forwards, the fused NMSE, both backwards and the optimizer kernels, captured from
-FOUR streams so the graph is a DAG, not a chain.  Almost every kernel of this model is
-latency-bound and fills a fraction of the 256 CUs, so independent work overlaps:
+Execution plan per step (world = 1, default ``stream_mode="dagq"``): one HIP graph replay
+(``steps_per_graph`` consecutive steps per replay in bench) captured from two streams, so the
+graph is a DAG.  Almost every kernel of this model is latency-bound and fills a fraction of
+the 256 CUs, so the independent QSC branch overlaps the HDCE chain:
 
-  main : gather -> conv fwd x3 -> FC fwd GEMM -> NMSE -> FC dgrad GEMM -> conv bwd (dgrad
-         chain) -> conv slabs -> Adam(conv + BN part)
-  fc   :              (after NMSE) FC wgrad GEMM -> (after dgrad) Adam(FC part)
-  conv :                              (per layer) conv wgrad k=3, 2
+  main : gather -> conv fwd x3 -> BN tail -> BN/ReLU apply -> FC fwd GEMM -> one-pass NMSE ->
+         loss finish -> FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce -> [wgrad|dgrad] L3 ->
+         [wgrad|dgrad] L2 -> wgrad L1 -> slab sums (conv, BN, FC bias) -> Adam(conv part) ->
+         conv weight pack for the NEXT step (+ batch cursor) -> Adam(FC part)
   qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
          QSC bwd -> slabs -> AdamW
 
+([wgrad|dgrad] = one launch running both independent gradients side by side.)  More side
+branches, later fork points, stream priorities and two concurrently replayed graphs were all
+measured and are kept as options (see ``__init__`` and README).
+
 The HDCE and the QSC have separate NaN-guard flags (``skip[0]``, ``skip[1]``), so neither
 optimizer waits for the other model's loss.
-World > 1: three graphs around the two gradient all-reduces (the FC bucket is reduced on
-RCCL's stream while the conv backward runs), the same streams inside each graph, then the
-optimizers (grad averaging fused into them).
+World > 1: four graphs around the gradient all-reduces (``_dp_run``): the FC bucket starts right
+after the forward + FC weight gradient and is hidden by the FC data gradient, the conv backward
+and the QSC branch; the FC Adam runs on its own stream beside the small-bucket all-reduce.
 """
 from __future__ import annotations
 
@@ -83,6 +87,7 @@ class FlagshipConfig:
     stream_mode: str = "dagq"    # serial | dag | dagq (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
+    tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
     stream_priority: bool = False  # capture the HDCE chain on a high-priority stream, the QSC branch low
     dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1) or the conv backward (2)
     fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
@@ -122,6 +127,7 @@ class FlagshipTrainer:
         self.qopt = make_optimizer(self.qspace, "adamw", cfg.lr, weight_decay=cfg.qsc_weight_decay,
                                    prune_thr=0.1 if cfg.use_gradient_pruning else 0.0)
         self.hstep = HDCEStep(self.hdce, self.U, self.B)
+        self.hstep.bias_via_conv_slabs = ctx.world == 1 and not cfg.split_graphs
         # NaN guards: the NMSE kernel sets skip[0] (HDCE), the QSC head skip[1]; they travel in the
         # small bucket so every rank sees the same (summed) flags and skips -- or steps -- in lockstep
         self.skip = torch.zeros(2, device=dev, dtype=torch.float32)
@@ -187,6 +193,13 @@ class FlagshipTrainer:
         if self.streams is None:
             self.branches = set()
         self.hdce_side = "w" in self.branches
+        if "a" in self.branches:   # (the FC Adam branch reads the bias gradient before the conv slabs run)
+            self.hstep.bias_via_conv_slabs = False
+        # end-of-step weight pack (GPU fused path; the qsc / full diagnosis modes keep the forward pack)
+        self.tail_pack = bool(self.hstep.hip and cfg.tail_pack and mode not in ("qsc", "full"))
+        if self.tail_pack:
+            self.hstep.conv.pack_at_tail = True
+            self._tail_pack_launch(advance=False)   # the first step's images
         self._use_graphs = graphs
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
@@ -241,10 +254,18 @@ class FlagshipTrainer:
             self.hdce.space.zero_grad()
         if classifier and not self.cstep.writes_grads:
             self.qspace.zero_grad()
-        # one launch: conv input, classifier input, label rows; batch = perm[cur : cur + B], cur += B
+        # one launch: conv input, classifier input, label rows; batch = perm[cur : cur + B].  With the
+        # end-of-step weight pack (tail_pack) the pack advances cur[0]; else the gather itself does
         k = 0 if hdce else 1
-        self.gat.from_cursor(self.store, self.perm, self.cur[k:k + 1], self.cur_done[k:k + 1], hdce=hdce,
-                             classifier=classifier)
+        advance = not (self.tail_pack and k == 0)
+        self.gat.from_cursor(self.store, self.perm, self.cur[k:k + 1], self.cur_done[k:k + 1] if advance else None,
+                             hdce=hdce, classifier=classifier)
+
+    def _tail_pack_launch(self, advance: bool = True) -> None:
+        """Pack the (just updated) conv weights into the MFMA B-fragment images the next forward reads,
+        and advance the batch cursor -- one launch at the end of the step."""
+        self.hstep.conv.pack_weights(nat.stream_ptr(self.ctx.device), cursor=self.cur[0:1] if advance else None,
+                                     cursor_inc=self.B if advance else 0)
 
     def _qsc_branch(self, with_opt: bool) -> None:
         q = self.cstep(self.gat.xq, self.labels, slabs=self.qslabs if self.cstep.writes_grads else None)
@@ -279,11 +300,16 @@ class FlagshipTrainer:
         self.hstep.backward_conv(side=self.streams["conv"] if "c" in br else None)
         if "a" in br:
             self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=0)
+            if self.tail_pack:
+                self._tail_pack_launch()
             self._join(("fc",))
         else:
             if self.hdce_side:
                 self._join(("fc",))
-            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1])
+            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=0)
+            if self.tail_pack:
+                self._tail_pack_launch()
+            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=1)
 
     # -- the data-parallel plan (world > 1; also world 1 'serial' / split_graphs) ---------------
     #   g1 : gather, HDCE forward, NMSE, FC weight-gradient GEMM
@@ -328,6 +354,8 @@ class FlagshipTrainer:
     def _dp_gr(self) -> None:
         g = 1.0 / self.ctx.world
         self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=0)
+        if self.tail_pack:
+            self._tail_pack_launch()
         self.qopt.step(grad_scale=g, skip=self.skip[1:2])
 
     def _dp_run(self, g1, g2, gf, gr) -> None:
@@ -422,6 +450,8 @@ class FlagshipTrainer:
             for t, c in zip(self.mutable_state(), saved):
                 t.copy_(c)
         self.cur.copy_(cur)
+        if self.tail_pack:   # (the packed images are derived from the weights: rebuild them)
+            self._tail_pack_launch(advance=False)
 
     @property
     def graphed(self) -> GraphedStep:
