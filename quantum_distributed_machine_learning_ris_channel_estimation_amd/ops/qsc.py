@@ -66,6 +66,7 @@ class QSCStepHIP:
         if impl == "mfma":
             wf = nat.fn(nat.hip_lib(), "qd_qsc2_waves", [_i, _i])
             self.grid_fwd = -(-batch_total // wf(self.Ww, 0))      # one sample per wave
+            grid_bwd = int(os.environ.get("QDML_QSC_GRID_BWD", grid_bwd))   # (tuning knob)
             self.grid_bwd = min(-(-batch_total // wf(self.Ww, 1)), grid_bwd)
             self.p2 = torch.empty(batch_total, feat, **f32)        # pool-2 features (linear weight grad)
             # saved by the forward for the backward: pool-1 map + both pools' argmax choices

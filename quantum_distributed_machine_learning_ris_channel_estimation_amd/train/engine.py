@@ -433,9 +433,10 @@ class ClassifierStep:
 
     def __init__(self, model: nn.Module, n_streams: int, grad_hook: Optional[Callable] = None,
                  space: Optional[FlatParamSpace] = None, batch_total: Optional[int] = None,
-                 skip: Optional[torch.Tensor] = None):
+                 skip: Optional[torch.Tensor] = None, hip_kw: Optional[dict] = None):
         """``skip``: a shared NaN-guard flag another loss already set this step (it is incremented);
-        by default the step owns its flag (``self.skip``, overwritten every step)."""
+        by default the step owns its flag (``self.skip``, overwritten every step).  ``hip_kw``: extra
+        QSCStepHIP arguments (launch grids)."""
         self.model = model
         self.S = n_streams
         self.grad_hook = grad_hook
@@ -448,7 +449,7 @@ class ClassifierStep:
         if (isinstance(model, QSC_P128) and model.use_quantum and dev.type == "cuda" and space is not None
                 and batch_total):
             from ..ops.qsc import QSCStepHIP
-            self.hip = QSCStepHIP(model, space, batch_total, n_groups=n_streams)
+            self.hip = QSCStepHIP(model, space, batch_total, n_groups=n_streams, **(hip_kw or {}))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         m = self.model

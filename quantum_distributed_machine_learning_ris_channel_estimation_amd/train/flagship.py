@@ -7,10 +7,13 @@ NLL, AdamW, optional QuantumNAT noise and gradient pruning) and the HDCE estimat
 (3 scenario experts + shared FC, per-stream NMSE, Adam), both forward + backward +
 optimizer, on HBM-resident synthetic data.
 
-Execution plan per step (world = 1, default ``stream_mode="dagq"``): one HIP graph replay
-(``steps_per_graph`` consecutive steps per replay in bench) captured from two streams, so the
-graph is a DAG.  Almost every kernel of this model is latency-bound and fills a fraction of
-the 256 CUs, so the independent QSC branch overlaps the HDCE chain:
+Execution plan (world = 1, default ``stream_mode="dagi"``): one HIP graph replay runs
+``steps_per_graph`` consecutive training steps (5 in bench) as TWO independent chains captured
+from two streams.  Almost every kernel of this model is latency-bound and fills a fraction of
+the 256 CUs, so the QSC chain overlaps the HDCE chain; the chains share nothing but the batch
+permutation (each has its own device cursor), so they meet only at the replay's head and tail
+(``dagq``, the earlier default, forks and joins the QSC branch every step: ~1.5% slower).
+Per step:
 
   main : gather -> conv fwd x3 -> BN tail -> BN/ReLU apply -> FC fwd GEMM -> one-pass NMSE ->
          loss finish -> FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce -> [wgrad|dgrad] L3 ->
@@ -84,7 +87,7 @@ class FlagshipConfig:
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
     split_graphs: bool = False   # force the 3-graph DP execution plan even at world 1 (testing)
-    stream_mode: str = "dagq"    # serial | dag | dagq (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
+    stream_mode: str = "dagi"    # serial | dag | dagq | dagi (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
@@ -92,6 +95,9 @@ class FlagshipConfig:
     dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1) or the conv backward (2)
     fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
     qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
+    qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
+    dagi_order: str = "inter"    # (dagi) capture order: inter (QSC step i after HDCE step i) | qfirst | mainfirst
+    qsc_late_capture: bool = False  # (qsc_fork gather) capture the QSC branch AFTER the HDCE chain
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
@@ -132,8 +138,11 @@ class FlagshipTrainer:
         # small bucket so every rank sees the same (summed) flags and skips -- or steps -- in lockstep
         self.skip = torch.zeros(2, device=dev, dtype=torch.float32)
         self.hstep.nmse.skip = self.skip[0:1]
+        # QSC backward grid: off the critical path (dagi) fewer, longer-running workgroups interfere
+        # less with the HDCE chain (measured 0.4486 vs 0.4515 ms/step at 128 vs 256)
+        gb = cfg.qsc_grid_bwd or (128 if cfg.stream_mode == "dagi" else 256)
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B,
-                                    skip=self.skip[1:2])
+                                    skip=self.skip[1:2], hip_kw={"grid_bwd": gb})
         self.cstep.skip_add = False
         self.cstep.writes_grads = self.cstep.hip is not None
         # buckets (see _dp_run): "skip" = the HDCE NaN flag, "fc" = 33.6 MB FC grads (in place), "small"
@@ -161,6 +170,7 @@ class FlagshipTrainer:
         #   serial : one stream, one chain
         #   dag    : ONE graph captured from 4 streams (qsc / fc / conv branches forked off the main chain)
         #   dagq   : ONE graph, only the QSC branch forked; the HDCE a single chain
+        #   dagi   : ONE graph, the HDCE and QSC chains independent within a replay (see _indep_body)
         #   qsc    : the QSC branch is its own graph replayed on its own stream; HDCE one serial graph
         #   full   : as qsc, and the HDCE graph has its fc / conv side branches
         #   !! qsc / full are kept for diagnosis only: on ROCm 7.x two graphs replayed CONCURRENTLY on two
@@ -169,7 +179,7 @@ class FlagshipTrainer:
         # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge
         # that crosses queues costs a barrier packet, so fewer, longer branches can win)
         mode = cfg.stream_mode
-        if mode not in ("serial", "dag", "dagq", "qsc", "full"):
+        if mode not in ("serial", "dag", "dagq", "dagi", "qsc", "full"):
             raise ValueError(f"stream_mode {mode!r}")
         if mode in ("qsc", "full"):
             import warnings
@@ -225,6 +235,8 @@ class FlagshipTrainer:
                 # freed during capture must not be handed to the other)
                 gs = [GraphedStep(rep(self._qsc_graph), enabled=graphs),
                       GraphedStep(rep(lambda: self._hdce_graph(gather=True)), enabled=graphs)]
+            elif mode == "dagi":
+                gs = [GraphedStep(lambda: self._indep_body(k), enabled=graphs, capture_stream=self.capture_stream)]
             else:
                 # one graph: gather, both forwards, NMSE, both backwards, the optimizers
                 gs = [GraphedStep(rep(self._step_body), enabled=graphs, capture_stream=self.capture_stream)]
@@ -384,6 +396,19 @@ class FlagshipTrainer:
     def _step_body(self) -> None:
         if self.mode in ("dag", "dagq"):
             self._gather()
+            if self.cfg.qsc_late_capture and self.cfg.qsc_fork == "gather":
+                # same DAG, other node order: the HIP graph executor keeps a node's FIRST child on the
+                # node's queue and starts later children on other queues (each cross-queue edge costs
+                # ~10 us).  Capturing the HDCE chain first keeps the critical path on one queue
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.ctx.device))
+                self._hdce_graph()
+                q = self.streams["qsc"]
+                q.wait_event(ev)
+                with torch.cuda.stream(q):
+                    self._qsc_branch(with_opt=True)
+                self._join(("qsc",))
+                return
             # the QSC branch forks at a chosen point of the HDCE forward (cfg.qsc_fork): its latency-
             # bound kernels then share the GPU with the later, larger HDCE kernels
             forked = []
@@ -404,6 +429,34 @@ class FlagshipTrainer:
             self._join(("qsc",))
             return
         self._dp_run(self._dp_g1, self._dp_g2, self._dp_gf, self._dp_gr)
+
+    def _indep_body(self, k: int) -> None:
+        """(dagi) ``k`` steps as TWO independent chains of one graph: the HDCE chain on the capturing
+        stream, the QSC chain (each step with its own batch gather, cursor ``cur[1]``) on the qsc stream.
+        The chains meet only at the replay's head and tail -- no per-step fork / join edges, which the
+        HIP graph executor pays as cross-queue barrier packets (~10 us each).  Both chains read the
+        same perm with cursors advanced by B per step, so step i of either model sees the same batch."""
+        main = torch.cuda.current_stream(self.ctx.device)
+        q = self.streams["qsc"]
+        order = os.environ.get("QDML_DAGI_ORDER", self.cfg.dagi_order)
+        ev = torch.cuda.Event()
+        for i in range(k):
+            self._gather(hdce=True, classifier=False)
+            if i == 0:   # (a node on the capturing stream first: a branch forked before it is a ROOT)
+                ev.record(main)
+                q.wait_event(ev)
+            if order == "qfirst":
+                with torch.cuda.stream(q):
+                    self._qsc_graph()
+            self._hdce_graph()
+            if order == "inter":
+                with torch.cuda.stream(q):
+                    self._qsc_graph()
+        if order == "mainfirst":
+            with torch.cuda.stream(q):
+                for i in range(k):
+                    self._qsc_graph()
+        self._join(("qsc",))
 
     def mutable_state(self):
         """Every tensor a step updates in place (weights, optimizer moments/counters, BN running

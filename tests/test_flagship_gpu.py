@@ -44,7 +44,7 @@ def _all_state(tr):
 
 
 @pytest.mark.parametrize("mode,split,k", [("dag", False, 1), ("dag", True, 1), ("dagq", True, 1), ("dagq", False, 1),
-                                          ("dagq", False, 3), ("dag", False, 2)])
+                                          ("dagq", False, 3), ("dag", False, 2), ("dagi", False, 1), ("dagi", False, 3)])
 def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     """The 4-stream DAG step (captured in one graph, or the 3-graph DP plan) computes exactly what the
     single-stream eager step computes: every kernel is deterministic (slab reductions, no float
