@@ -17,9 +17,9 @@ Per step:
 
   main : gather -> conv fwd x3 -> BN tail -> BN/ReLU apply -> FC fwd GEMM -> one-pass NMSE ->
          loss finish -> FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce -> [wgrad|dgrad] L3 ->
-         [wgrad|dgrad] L2 -> wgrad L1 -> slab sums (conv, BN, FC bias) -> Adam(conv part) ->
-         conv weight pack for the NEXT step (+ batch cursor) -> Adam(FC part)
-  qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
+         [wgrad|dgrad] L2 -> wgrad L1 -> slab sums (conv, BN, FC bias) -> Adam (one launch over all
+         HDCE parameters, writes the bf16 FC shadow) -> conv weight pack for the NEXT step (+ cursor)
+  qsc  : gather (own cursor) -> QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
          QSC bwd -> slabs -> AdamW
 
 ([wgrad|dgrad] = one launch running both independent gradients side by side.)  More side
@@ -126,7 +126,11 @@ class FlagshipTrainer:
         self.hopt = make_optimizer(self.hdce.space, "adam", cfg.lr)
         sp = self.hdce.space
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
-        self.hopt.partition([n_conv])           # part 0: conv + BN params, part 1: FC (own streams)
+        # part 0: conv + BN params, part 1: FC -- for the plans that step them apart (the DP plan, the FC
+        # Adam side branch); the world-1 chain steps the whole space in ONE launch
+        if (ctx.world > 1 or cfg.split_graphs or cfg.stream_mode in ("dag", "qsc", "full")
+                or "a" in cfg.hdce_branches):
+            self.hopt.partition([n_conv])
         if cfg.fc_adam_grid:
             self.hopt.max_grid[1] = cfg.fc_adam_grid
         self.hdce.attach_fc_shadow(self.hopt)   # after the broadcast: the shadow starts in sync
@@ -318,6 +322,11 @@ class FlagshipTrainer:
         else:
             if self.hdce_side:
                 self._join(("fc",))
+            if len(self.hopt.bounds) == 1:
+                self.hopt.step(grad_scale=1.0, skip=self.skip[0:1])
+                if self.tail_pack:
+                    self._tail_pack_launch()
+                return
             self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=0)
             if self.tail_pack:
                 self._tail_pack_launch()
@@ -361,11 +370,12 @@ class FlagshipTrainer:
             self._qsc_branch(with_opt=False)
 
     def _dp_gf(self) -> None:
-        self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.skip[0:1], part=1)
+        if len(self.hopt.bounds) > 1:   # (unpartitioned -- serial world 1 -- gr steps everything)
+            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.skip[0:1], part=1)
 
     def _dp_gr(self) -> None:
         g = 1.0 / self.ctx.world
-        self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=0)
+        self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=0 if len(self.hopt.bounds) > 1 else None)
         if self.tail_pack:
             self._tail_pack_launch()
         self.qopt.step(grad_scale=g, skip=self.skip[1:2])

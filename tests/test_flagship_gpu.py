@@ -50,7 +50,8 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     single-stream eager step computes: every kernel is deterministic (slab reductions, no float
     atomics) and the DAG only reorders independent work."""
     ctx = DistContext(device=cuda)
-    base = dict(batch=32, data_len=800, use_quantumnat=True)
+    # (the same QSC backward grid on both sides: it fixes the slab reduction order)
+    base = dict(batch=32, data_len=800, use_quantumnat=True, qsc_grid_bwd=128)
     ref = FlagshipTrainer(FlagshipConfig(hip_graphs=False, stream_mode="serial", **base), ctx)
     dag = FlagshipTrainer(FlagshipConfig(hip_graphs=True, stream_mode=mode, split_graphs=split,
                                          steps_per_graph=k, **base), ctx)
@@ -65,7 +66,7 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     for i, (a, b) in enumerate(zip(_all_state(ref), _all_state(dag))):
         assert torch.allclose(a.float(), b.float(), rtol=1e-6, atol=1e-7), (i, float((a.float() - b.float()).abs().max()))
     assert torch.allclose(ref.hloss, dag.hloss, rtol=1e-6) and torch.allclose(ref.qloss, dag.qloss, rtol=1e-6)
-    assert torch.equal(ref.hopt.step_t, dag.hopt.step_t) and float(dag.hopt.step_t[0]) == 4.0
+    assert float(ref.hopt.step_t[0]) == 4.0 and bool((dag.hopt.step_t == 4.0).all())
 
 
 def test_dp_plan_two_ranks_on_one_gpu(tmp_path):
