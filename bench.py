@@ -44,8 +44,9 @@ def main() -> int:
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
     ap.add_argument("--hdce-branches", default="", help="(dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam")
     ap.add_argument("--stream-priority", action="store_true", help="HDCE chain high priority, QSC branch low")
-    ap.add_argument("--dp-qsc-phase", type=int, default=2, choices=[1, 2],
-                    help="DP plan: run the QSC beside the HDCE forward (1) or beside the conv backward (2)")
+    ap.add_argument("--dp-qsc-phase", type=int, default=2, choices=[1, 2, 3],
+                    help="DP plan: run the QSC beside the HDCE forward (1), beside the conv backward (2), or "
+                         "its forward half beside the HDCE forward and its backward half beside the conv backward (3)")
     ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
     ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
     ap.add_argument("--qsc-late-capture", action="store_true",

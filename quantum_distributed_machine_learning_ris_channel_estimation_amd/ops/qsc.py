@@ -154,6 +154,14 @@ class QSCStepHIP:
         one producer per step, so a zero_grad before the step becomes unnecessary).
         ``slabs``: queue the gradient-slab reductions on this batch (the caller launches it with the
         same ``accumulate``) instead of launching them here."""
+        self.forward_part(x, labels, loss_acc, skip, skip_add, accumulate)
+        return self.backward_part(x, accumulate, slabs)
+
+    def forward_part(self, x: torch.Tensor, labels: torch.Tensor, loss_acc: Optional[torch.Tensor] = None,
+                     skip: Optional[torch.Tensor] = None, skip_add: bool = False, accumulate: bool = True) -> None:
+        """First half of ``__call__``: preprocess, noise draw, simulator forward, head (loss, dE and
+        the head's grads).  ``backward_part`` (same x) finishes the step -- the two halves can sit in
+        different graphs of an execution plan."""
         m, sp = self.m, self.space
         B, n, L = self.B, self.n, self.L
         assert x.shape[0] == B and x.is_contiguous() and labels.dtype == torch.int64
@@ -178,6 +186,18 @@ class QSCStepHIP:
                              nat.ptr(loss_acc) if loss_acc is not None else None,
                              nat.ptr(skip) if skip is not None else None, int(skip_add), int(accumulate), B, n, self.C,
                              st), "qsc_head")
+        self._w_cur = w
+
+    def backward_part(self, x: torch.Tensor, accumulate: bool = True, slabs: Optional[SlabBatch] = None) -> torch.Tensor:
+        m, sp = self.m, self.space
+        B, n, L = self.B, self.n, self.L
+        st = nat.stream_ptr(x.device)
+        flat = sp.flat
+        w = self._w_cur
+        wgroup = B // w.shape[0] if w.dim() == 4 else 0
+        extra = (nat.ptr(self.qws) if self.qws is not None else None,
+                 nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
+            (nat.ptr(self.psave) if self.psave is not None else None,)
         nat.check(self._qb(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.dE), nat.ptr(self.dang),
                            nat.ptr(self.qslab), B, n, L, wgroup, *extra, st), "qsim_bwd")
         own = SlabBatch()

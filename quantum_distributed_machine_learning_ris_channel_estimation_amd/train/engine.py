@@ -463,6 +463,18 @@ class ClassifierStep:
             return F.log_softmax(m.classifier(xq), dim=1)
         return m(x)
 
+    def forward_part(self, x: torch.Tensor, labels: torch.Tensor) -> None:
+        """(HIP path) the step's forward half: loss, NaN flag, head grads (see QSCStepHIP.forward_part)."""
+        self.hip.forward_part(x.contiguous(), labels, skip=self.skip, skip_add=self.skip_add,
+                              accumulate=not self.writes_grads)
+
+    def backward_part(self, x: torch.Tensor, slabs=None) -> torch.Tensor:
+        """(HIP path) the step's backward half; returns the loss."""
+        loss = self.hip.backward_part(x.contiguous(), accumulate=not self.writes_grads, slabs=slabs)
+        if self.grad_hook:
+            self.grad_hook("all")
+        return loss
+
     def __call__(self, x: torch.Tensor, labels: torch.Tensor, slabs=None) -> torch.Tensor:
         """``slabs`` (HIP path): queue the gradient-slab reductions on this ``SlabBatch`` (launched by
         the caller, with accumulate = not writes_grads)."""

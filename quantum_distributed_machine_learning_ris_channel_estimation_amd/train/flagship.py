@@ -92,7 +92,11 @@ class FlagshipConfig:
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
     stream_priority: bool = False  # capture the HDCE chain on a high-priority stream, the QSC branch low
-    dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1) or the conv backward (2)
+    dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1), the conv backward (2),
+    #                              or its forward half beside the HDCE forward and its backward half beside
+    #                              the conv backward (3).  World-1 rehearsal: 0.492 / 0.517 / 0.557 ms;
+    #                              2 is kept: it leaves the most work (QSC + conv backward) behind the 33.6 MB
+    #                              FC all-reduce, which at 2-8 ranks over xGMI is expected to take 0.2-0.4 ms
     fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
     qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
     qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
@@ -144,7 +148,8 @@ class FlagshipTrainer:
         self.hstep.nmse.skip = self.skip[0:1]
         # QSC backward grid: off the critical path (dagi) fewer, longer-running workgroups interfere
         # less with the HDCE chain (measured 0.4486 vs 0.4515 ms/step at 128 vs 256)
-        gb = cfg.qsc_grid_bwd or (128 if cfg.stream_mode == "dagi" else 256)
+        # (the DP plan runs the QSC inside a graph whose length it sets: there the full grid)
+        gb = cfg.qsc_grid_bwd or (128 if cfg.stream_mode == "dagi" and ctx.world == 1 and not cfg.split_graphs else 256)
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B,
                                     skip=self.skip[1:2], hip_kw={"grid_bwd": gb})
         self.cstep.skip_add = False
@@ -283,8 +288,15 @@ class FlagshipTrainer:
         self.hstep.conv.pack_weights(nat.stream_ptr(self.ctx.device), cursor=self.cur[0:1] if advance else None,
                                      cursor_inc=self.B if advance else 0)
 
-    def _qsc_branch(self, with_opt: bool) -> None:
-        q = self.cstep(self.gat.xq, self.labels, slabs=self.qslabs if self.cstep.writes_grads else None)
+    def _qsc_branch(self, with_opt: bool, part: str = "all") -> None:
+        """The QSC step (+ AdamW with ``with_opt``); ``part`` "fwd" / "bwd": only that half (HIP path)."""
+        if part == "fwd":
+            self.cstep.forward_part(self.gat.xq, self.labels)
+            return
+        if part == "bwd":
+            q = self.cstep.backward_part(self.gat.xq, slabs=self.qslabs if self.cstep.writes_grads else None)
+        else:
+            q = self.cstep(self.gat.xq, self.labels, slabs=self.qslabs if self.cstep.writes_grads else None)
         if self.cstep.writes_grads:
             self.qslabs.launch(accumulate=False, stream=nat.stream_ptr(self.ctx.device))
         if q is not self.qloss:
@@ -343,10 +355,11 @@ class FlagshipTrainer:
     def _dp_g1(self) -> None:
         self._gather()
         self.hstep.defer_dgrad = self.hstep.hip
-        early = self.streams is not None and self.cfg.dp_qsc_phase == 1
-        if early:   # QSC forward/backward beside the HDCE forward (as in the world-1 plan)
+        ph = self.cfg.dp_qsc_phase
+        early = self.streams is not None and ph in (1, 3)
+        if early:   # QSC forward (+ backward: phase 1) beside the HDCE forward
             with self._fork(self.streams["qsc"]):
-                self._qsc_branch(with_opt=False)
+                self._qsc_branch(with_opt=False, part="fwd" if ph == 3 else "all")
         self._hdce_forward(side=False)   # (the FC wgrad on main: the all-reduce waits for it first)
         if early:
             self._join(("qsc",))
@@ -359,10 +372,11 @@ class FlagshipTrainer:
         ms = self.streams is not None
         if self.hstep.defer_dgrad:
             self.hstep.dgrad()
-        late = ms and self.cfg.dp_qsc_phase == 2
+        ph = self.cfg.dp_qsc_phase
+        late = ms and ph in (2, 3)
         if late:
             with self._fork(self.streams["qsc"]):
-                self._qsc_branch(with_opt=False)
+                self._qsc_branch(with_opt=False, part="bwd" if ph == 3 else "all")
         self.hstep.backward_conv(side=self.streams["conv"] if "c" in self.branches else None)
         if late:
             self._join(("qsc",))

@@ -43,7 +43,7 @@ for s in $STEPS; do
     dagicmp) for r in 1 2 3; do for o in dagq inter qfirst; do if [ $o = dagq ]; then m=dagq; else m=dagi; fi; QDML_DAGI_ORDER=$o timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode $m > $OUT/cmp.log 2>&1 || exit 1; echo "$o $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/dagicmp.txt; done; done ;;
     qscgrid) for r in 1 2; do for g in 256 128 64 576; do QDML_QSC_GRID_BWD=$g timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode dagi > $OUT/cmp.log 2>&1 || exit 1; echo "$g $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/qscgrid.txt; done; done ;;
     dagiorder) for o in inter qfirst mainfirst inter qfirst mainfirst; do QDML_DAGI_ORDER=$o run bench_order_${o}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --stream-mode dagi; done ;;
-    dpphase) for v in 1 2 1 2; do run bench_dpq_$v 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
+    dpphase) for v in 1 2 3 1 2 3; do run bench_dpq_${v}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
     prio) for v in "" "--stream-priority" "" "--stream-priority" "--dtype fp8" "--dtype fp8 --stream-priority"; do run bench_prio_${v// /_} 300 python bench.py --steps 100 --warmup 10 $v; done ;;
     fusewd) for v in 1 0 1 0; do QDML_CONV_FUSE_WD=$v run bench_fwd_$v 300 python bench.py --steps 100 --warmup 10; mv $OUT/bench_fwd_$v.log $OUT/bench_fwd_${v}_$RANDOM.log; done ;;
     bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
