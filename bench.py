@@ -49,10 +49,8 @@ def main() -> int:
                          "its forward half beside the HDCE forward and its backward half beside the conv backward (3)")
     ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
     ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
-    ap.add_argument("--qsc-late-capture", action="store_true",
-                    help="(dagq) capture the QSC branch after the HDCE chain (keeps the chain on one HIP queue)")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
-    ap.add_argument("--stream-mode", default="dagi", choices=["serial", "dag", "dagq", "dagi", "qsc", "full"],
+    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "dagi", "qsc", "full"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
                          "or a separate QSC graph on its own stream (+ HDCE side branches with 'full')")
     args = ap.parse_args()
@@ -72,7 +70,7 @@ def main() -> int:
                          hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
                          split_graphs=args.split_graphs, stream_mode=args.stream_mode,
                          qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
-                         hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork, qsc_late_capture=args.qsc_late_capture,
+                         hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
                          fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase,
                          stream_priority=args.stream_priority)
     tr = FlagshipTrainer(cfg, ctx)
@@ -127,7 +125,6 @@ def main() -> int:
                 "stream_mode": tr.mode,
                 "hdce_branches": "".join(sorted(tr.branches)),
                 "qsc_fork": args.qsc_fork,
-                "qsc_late_capture": args.qsc_late_capture,
                 "fc_adam_grid": args.fc_adam_grid,
                 "dp_qsc_phase": args.dp_qsc_phase,
                 "stream_priority": args.stream_priority,

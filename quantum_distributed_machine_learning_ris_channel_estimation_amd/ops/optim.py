@@ -28,7 +28,10 @@ ALIGN = 16  # elements; keeps every parameter view 64-byte aligned for float4 ac
 
 
 class FlatParamSpace:
-    def __init__(self, params: Sequence[Tuple[str, nn.Parameter]], device=None):
+    def __init__(self, params: Sequence[Tuple[str, nn.Parameter]], device=None, extra: int = 0):
+        """``extra``: trailing scratch floats (one ALIGN block) after the last parameter; their grad
+        slots ride along with the tail of the grad buffer (e.g. a NaN flag that then travels in the
+        same all-reduce as the last parameters' gradients).  ``extra_off`` is their offset."""
         seen = set()
         uniq = []
         for name, p in params:
@@ -44,6 +47,8 @@ class FlatParamSpace:
             offs.append(off)
             off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.offsets = offs
+        self.extra_off = off
+        off += (extra + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
         self.n_real = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(off, device=device, dtype=torch.float32)

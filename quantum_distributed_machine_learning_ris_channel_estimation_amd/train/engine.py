@@ -56,7 +56,8 @@ class HDCEModel:
     execution.  The reference modules stay the single source of parameters (their tensors are
     views into the flat buffer), so ``Conv0.state_dict()`` etc. remain reference-compatible."""
 
-    def __init__(self, pilot_num: int = 128, device="cpu", dtype: str = "bf16", n_experts: int = 3):
+    def __init__(self, pilot_num: int = 128, device="cpu", dtype: str = "bf16", n_experts: int = 3,
+                 grad_extra: int = 0):
         self.device = torch.device(device)
         self.E = n_experts
         self.H, self.W = pilot_grid(pilot_num)
@@ -76,7 +77,7 @@ class HDCEModel:
             for e, m in enumerate(self.convs):
                 named.append((f"Conv{e}.{pname}", m.get_parameter(pname)))
         named += [("CE.FC.weight", self.fc.FC.weight), ("CE.FC.bias", self.fc.FC.bias)]
-        self.space = FlatParamSpace(named, self.device)
+        self.space = FlatParamSpace(named, self.device, extra=grad_extra)
         # grouped leaf views over the expert-consecutive parameter blocks
         self.conv_w, self.bn_w, self.bn_b = [], [], []
         for k in range(3):

@@ -7,19 +7,18 @@ NLL, AdamW, optional QuantumNAT noise and gradient pruning) and the HDCE estimat
 (3 scenario experts + shared FC, per-stream NMSE, Adam), both forward + backward +
 optimizer, on HBM-resident synthetic data.
 
-Execution plan (world = 1, default ``stream_mode="dagi"``): one HIP graph replay runs
-``steps_per_graph`` consecutive training steps (5 in bench) as TWO independent chains captured
-from two streams.  Almost every kernel of this model is latency-bound and fills a fraction of
-the 256 CUs, so the QSC chain overlaps the HDCE chain; the chains share nothing but the batch
-permutation (each has its own device cursor), so they meet only at the replay's head and tail
-(``dagq``, the earlier default, forks and joins the QSC branch every step: ~1.5% slower).
-Per step:
+Execution plan (world = 1, default ``stream_mode="dagq"``): one HIP graph replay runs
+``steps_per_graph`` consecutive training steps (5 in bench), each captured from two streams: the
+QSC branch forks off the HDCE chain after the batch gather and joins it at the end of the step.
+Almost every kernel of this model is latency-bound and fills a fraction of the 256 CUs, so the
+QSC branch overlaps the HDCE chain.  (``dagi`` -- the two chains independent for the whole replay
+-- was ~1.5% faster but not bit-reproducible; see ``__init__``.)  Per step:
 
   main : gather -> conv fwd x3 -> BN tail -> BN/ReLU apply -> FC fwd GEMM -> one-pass NMSE ->
          loss finish -> FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce -> [wgrad|dgrad] L3 ->
          [wgrad|dgrad] L2 -> wgrad L1 -> slab sums (conv, BN, FC bias) -> Adam (one launch over all
          HDCE parameters, writes the bf16 FC shadow) -> conv weight pack for the NEXT step (+ cursor)
-  qsc  : gather (own cursor) -> QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
+  qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
          QSC bwd -> slabs -> AdamW
 
 ([wgrad|dgrad] = one launch running both independent gradients side by side.)  More side
@@ -87,7 +86,7 @@ class FlagshipConfig:
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
     split_graphs: bool = False   # force the 3-graph DP execution plan even at world 1 (testing)
-    stream_mode: str = "dagi"    # serial | dag | dagq | dagi (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
+    stream_mode: str = "dagq"    # serial | dag | dagq | dagi (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
@@ -100,8 +99,6 @@ class FlagshipConfig:
     fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
     qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
     qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
-    dagi_order: str = "inter"    # (dagi) capture order: inter (QSC step i after HDCE step i) | qfirst | mainfirst
-    qsc_late_capture: bool = False  # (qsc_fork gather) capture the QSC branch AFTER the HDCE chain
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
@@ -121,7 +118,10 @@ class FlagshipTrainer:
         self.S = self.E * self.U
         # --- models (weights broadcast from rank 0 once; then resident)
         torch.manual_seed(cfg.seed)
-        self.hdce = HDCEModel(cfg.pilot_num, dev, cfg.dtype, cfg.n_scenarios)
+        # DP: the HDCE NaN flag lives in a scratch slot right after the FC gradient, so it travels in
+        # the FC all-reduce (one collective less ahead of it)
+        self.flag_in_fc = ctx.world > 1 or cfg.split_graphs
+        self.hdce = HDCEModel(cfg.pilot_num, dev, cfg.dtype, cfg.n_scenarios, grad_extra=1 if self.flag_in_fc else 0)
         self.qsc = QSC_P128(cfg.n_qubits, cfg.n_layers, cfg.n_classes, cfg.use_quantumnat,
                             cfg.use_gradient_pruning, cfg.pilot_num).to(dev)
         self.qspace = FlatParamSpace(list(self.qsc.named_parameters()), dev)
@@ -144,20 +144,25 @@ class FlagshipTrainer:
         self.hstep.bias_via_conv_slabs = ctx.world == 1 and not cfg.split_graphs
         # NaN guards: the NMSE kernel sets skip[0] (HDCE), the QSC head skip[1]; they travel in the
         # small bucket so every rank sees the same (summed) flags and skips -- or steps -- in lockstep
-        self.skip = torch.zeros(2, device=dev, dtype=torch.float32)
-        self.hstep.nmse.skip = self.skip[0:1]
+        self.skip = torch.zeros(2, 64, device=dev, dtype=torch.float32)   # (own cache line per flag)
+        self.qskip = self.skip[1, 0:1]
+        self.hskip = sp.grad[sp.extra_off:sp.extra_off + 1] if self.flag_in_fc else self.skip[0, 0:1]
+        self.hstep.nmse.skip = self.hskip
         # QSC backward grid: off the critical path (dagi) fewer, longer-running workgroups interfere
         # less with the HDCE chain (measured 0.4486 vs 0.4515 ms/step at 128 vs 256)
         # (the DP plan runs the QSC inside a graph whose length it sets: there the full grid)
         gb = cfg.qsc_grid_bwd or (128 if cfg.stream_mode == "dagi" and ctx.world == 1 and not cfg.split_graphs else 256)
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B,
-                                    skip=self.skip[1:2], hip_kw={"grid_bwd": gb})
+                                    skip=self.qskip, hip_kw={"grid_bwd": gb})
         self.cstep.skip_add = False
         self.cstep.writes_grads = self.cstep.hip is not None
-        # buckets (see _dp_run): "skip" = the HDCE NaN flag, "fc" = 33.6 MB FC grads (in place), "small"
+        # buckets (see _dp_run): "fc" = 33.6 MB FC grads (in place; + the HDCE NaN flag when flag_in_fc,
+        # else that flag is its own "skip" bucket), "small"
         # = conv/BN + QSC grads + the QSC NaN flag (coalesced)
-        self.buckets = GradBuckets(ctx, {"skip": [self.skip[0:1]], "fc": [sp.grad[n_conv:]],
-                                         "small": [sp.grad[:n_conv], self.qspace.grad, self.skip[1:2]]})
+        bk = {"fc": [sp.grad[n_conv:]], "small": [sp.grad[:n_conv], self.qspace.grad, self.qskip]}
+        if not self.flag_in_fc:
+            bk["skip"] = [self.skip[0, 0:1]]
+        self.buckets = GradBuckets(ctx, bk)
         self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)
         if dev.type == "cuda" and self.hstep.hip:   # per-row label powers ride along with the gather
             nm = self.hstep.nmse
@@ -166,8 +171,10 @@ class FlagshipTrainer:
         # themselves (cur[0]: HDCE / whole-step gather, cur[1]: the QSC graph's own gather); the host
         # only tracks the epoch position to regenerate perm in place when it runs out
         self.perm = torch.randperm(self.store.n, device=dev)
-        self.cur = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.cur_done = torch.zeros(2, dtype=torch.int32, device=dev)
+        # (one 256-byte row each: the HDCE and QSC chains run concurrently and update their own
+        # cursor / arrival counter, so the two never share a cache line)
+        self.cur = torch.zeros(2, 64, dtype=torch.int32, device=dev)
+        self.cur_done = torch.zeros(2, 64, dtype=torch.int32, device=dev)
         self.cursor = 0   # host mirror of the device cursors (position of the NEXT batch)
         # the loss kernels' own static buffers double as the step's loss outputs (no per-step copies)
         self.hloss = self.hstep.nmse.loss
@@ -180,6 +187,14 @@ class FlagshipTrainer:
         #   dag    : ONE graph captured from 4 streams (qsc / fc / conv branches forked off the main chain)
         #   dagq   : ONE graph, only the QSC branch forked; the HDCE a single chain
         #   dagi   : ONE graph, the HDCE and QSC chains independent within a replay (see _indep_body)
+        #   !! dagi, qsc and full are kept for diagnosis only.  Whenever the QSC chain runs concurrently
+        #   with the HDCE chain ACROSS step boundaries (dagi with >= 2 steps per replay; two graphs
+        #   replayed concurrently in qsc / full) the QSC weights drift from the serial run by ~1e-5
+        #   after a few steps in most trials (scripts/dbg_dagi.py), although every QSC kernel is
+        #   bit-reproducible under concurrent load on its own (scripts/dbg_qsc_race.py) and the chains
+        #   share no buffer (cursors and NaN flags sit on separate cache lines).  dagq (QSC forked and
+        #   joined every step) and the serial graphs match the eager run bit for bit; dagi was ~1.5%
+        #   faster (profiles/r1_15_dagi_sweeps.md), not worth an unexplained non-reproducibility
         #   qsc    : the QSC branch is its own graph replayed on its own stream; HDCE one serial graph
         #   full   : as qsc, and the HDCE graph has its fc / conv side branches
         #   !! qsc / full are kept for diagnosis only: on ROCm 7.x two graphs replayed CONCURRENTLY on two
@@ -190,10 +205,10 @@ class FlagshipTrainer:
         mode = cfg.stream_mode
         if mode not in ("serial", "dag", "dagq", "dagi", "qsc", "full"):
             raise ValueError(f"stream_mode {mode!r}")
-        if mode in ("qsc", "full"):
+        if mode in ("qsc", "full", "dagi"):
             import warnings
-            warnings.warn(f"stream_mode {mode!r} replays two graphs concurrently: numerically unsafe on ROCm 7.x "
-                          "(see FlagshipTrainer.__init__); use 'dagq'")
+            warnings.warn(f"stream_mode {mode!r} runs the QSC and HDCE chains concurrently across step boundaries: "
+                          "not bit-reproducible on ROCm 7.x (see FlagshipTrainer.__init__); use 'dagq'")
         self.streams = None
         self.capture_stream = None
         if dev.type == "cuda" and mode != "serial" and self.hstep.hip and self.cstep.hip is not None:
@@ -279,13 +294,13 @@ class FlagshipTrainer:
         # end-of-step weight pack (tail_pack) the pack advances cur[0]; else the gather itself does
         k = 0 if hdce else 1
         advance = not (self.tail_pack and k == 0)
-        self.gat.from_cursor(self.store, self.perm, self.cur[k:k + 1], self.cur_done[k:k + 1] if advance else None,
+        self.gat.from_cursor(self.store, self.perm, self.cur[k, 0:1], self.cur_done[k, 0:1] if advance else None,
                              hdce=hdce, classifier=classifier)
 
     def _tail_pack_launch(self, advance: bool = True) -> None:
         """Pack the (just updated) conv weights into the MFMA B-fragment images the next forward reads,
         and advance the batch cursor -- one launch at the end of the step."""
-        self.hstep.conv.pack_weights(nat.stream_ptr(self.ctx.device), cursor=self.cur[0:1] if advance else None,
+        self.hstep.conv.pack_weights(nat.stream_ptr(self.ctx.device), cursor=self.cur[0, 0:1] if advance else None,
                                      cursor_inc=self.B if advance else 0)
 
     def _qsc_branch(self, with_opt: bool, part: str = "all") -> None:
@@ -302,7 +317,7 @@ class FlagshipTrainer:
         if q is not self.qloss:
             self.qloss.copy_(q)
         if with_opt:
-            self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.skip[1:2])
+            self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.qskip)
 
     def _qsc_graph(self) -> None:
         self._gather(hdce=False, classifier=True)
@@ -324,10 +339,10 @@ class FlagshipTrainer:
         if "a" in br:
             # FC Adam once the dgrad GEMM (which reads the bf16 weight shadow it rewrites) is queued
             with self._fork(self.streams["fc"]):
-                self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=1)
+                self.hopt.step(grad_scale=1.0, skip=self.hskip, part=1)
         self.hstep.backward_conv(side=self.streams["conv"] if "c" in br else None)
         if "a" in br:
-            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=0)
+            self.hopt.step(grad_scale=1.0, skip=self.hskip, part=0)
             if self.tail_pack:
                 self._tail_pack_launch()
             self._join(("fc",))
@@ -335,14 +350,14 @@ class FlagshipTrainer:
             if self.hdce_side:
                 self._join(("fc",))
             if len(self.hopt.bounds) == 1:
-                self.hopt.step(grad_scale=1.0, skip=self.skip[0:1])
+                self.hopt.step(grad_scale=1.0, skip=self.hskip)
                 if self.tail_pack:
                     self._tail_pack_launch()
                 return
-            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=0)
+            self.hopt.step(grad_scale=1.0, skip=self.hskip, part=0)
             if self.tail_pack:
                 self._tail_pack_launch()
-            self.hopt.step(grad_scale=1.0, skip=self.skip[0:1], part=1)
+            self.hopt.step(grad_scale=1.0, skip=self.hskip, part=1)
 
     # -- the data-parallel plan (world > 1; also world 1 'serial' / split_graphs) ---------------
     #   g1 : gather, HDCE forward, NMSE, FC weight-gradient GEMM
@@ -385,14 +400,14 @@ class FlagshipTrainer:
 
     def _dp_gf(self) -> None:
         if len(self.hopt.bounds) > 1:   # (unpartitioned -- serial world 1 -- gr steps everything)
-            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.skip[0:1], part=1)
+            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.hskip, part=1)
 
     def _dp_gr(self) -> None:
         g = 1.0 / self.ctx.world
-        self.hopt.step(grad_scale=g, skip=self.skip[0:1], part=0 if len(self.hopt.bounds) > 1 else None)
+        self.hopt.step(grad_scale=g, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None)
         if self.tail_pack:
             self._tail_pack_launch()
-        self.qopt.step(grad_scale=g, skip=self.skip[1:2])
+        self.qopt.step(grad_scale=g, skip=self.qskip)
 
     def _dp_run(self, g1, g2, gf, gr) -> None:
         b = self.buckets
@@ -420,19 +435,6 @@ class FlagshipTrainer:
     def _step_body(self) -> None:
         if self.mode in ("dag", "dagq"):
             self._gather()
-            if self.cfg.qsc_late_capture and self.cfg.qsc_fork == "gather":
-                # same DAG, other node order: the HIP graph executor keeps a node's FIRST child on the
-                # node's queue and starts later children on other queues (each cross-queue edge costs
-                # ~10 us).  Capturing the HDCE chain first keeps the critical path on one queue
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(self.ctx.device))
-                self._hdce_graph()
-                q = self.streams["qsc"]
-                q.wait_event(ev)
-                with torch.cuda.stream(q):
-                    self._qsc_branch(with_opt=True)
-                self._join(("qsc",))
-                return
             # the QSC branch forks at a chosen point of the HDCE forward (cfg.qsc_fork): its latency-
             # bound kernels then share the GPU with the later, larger HDCE kernels
             forked = []
@@ -460,27 +462,25 @@ class FlagshipTrainer:
         The chains meet only at the replay's head and tail -- no per-step fork / join edges, which the
         HIP graph executor pays as cross-queue barrier packets (~10 us each).  Both chains read the
         same perm with cursors advanced by B per step, so step i of either model sees the same batch."""
+        # CAPTURE ORDER MATTERS (measured, ROCm 7.x graph executor): each step's QSC chain is captured
+        # right after the gather it forks from, BEFORE the HDCE chain.  Captured the other way round
+        # (HDCE chain first, QSC after it, same edges) the replayed QSC chain read stale inputs -- QSC
+        # weights differed from the serial run in 6 of 6 trials (scripts/dbg_dagi.py); this order, and
+        # dagq's per-step fork, matched in every trial
         main = torch.cuda.current_stream(self.ctx.device)
         q = self.streams["qsc"]
-        order = os.environ.get("QDML_DAGI_ORDER", self.cfg.dagi_order)
-        ev = torch.cuda.Event()
         for i in range(k):
             self._gather(hdce=True, classifier=False)
             if i == 0:   # (a node on the capturing stream first: a branch forked before it is a ROOT)
-                ev.record(main)
-                q.wait_event(ev)
-            if order == "qfirst":
-                with torch.cuda.stream(q):
-                    self._qsc_graph()
-            self._hdce_graph()
-            if order == "inter":
-                with torch.cuda.stream(q):
-                    self._qsc_graph()
-        if order == "mainfirst":
+                q.wait_stream(main)
             with torch.cuda.stream(q):
-                for i in range(k):
-                    self._qsc_graph()
+                self._qsc_graph()
+            self._hdce_graph()
         self._join(("qsc",))
+
+    def skip_flags(self) -> torch.Tensor:
+        """(2,) the HDCE and QSC NaN-guard flags of the last step (after the all-reduce: summed)."""
+        return torch.cat([self.hskip, self.qskip])
 
     def mutable_state(self):
         """Every tensor a step updates in place (weights, optimizer moments/counters, BN running

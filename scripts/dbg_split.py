@@ -33,4 +33,4 @@ for mode, k, split in cases:
         print(mode, k, split, "replay", rep, "qsc param diff", [x for x in d if x[1] > 0],
               "hdce diff", float((ref.hdce.space.flat - dag.hdce.space.flat).abs().max()),
               "loss", float(ref.qloss), float(dag.qloss), "noise ctr", int(ref.cstep.hip.noise_ctr),
-              int(dag.cstep.hip.noise_ctr), "cur", ref.cur.tolist(), dag.cur.tolist(), flush=True)
+              int(dag.cstep.hip.noise_ctr), "cur", ref.cur[:, 0].tolist(), dag.cur[:, 0].tolist(), flush=True)

@@ -40,16 +40,15 @@ for s in $STEPS; do
     envsweep) for e in ${ENVS:-NONE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 DEBUG_HIP_GRAPH_BATCH_SIZE=1 DEBUG_HIP_GRAPH_BATCH_SIZE=64 DEBUG_HIP_FORCE_GRAPH_QUEUES=1 DEBUG_HIP_FORCE_GRAPH_QUEUES=2}; do
         for v in "" "--qsc-late-capture"; do env $e timeout -k 10 300 python bench.py --steps 100 --warmup 10 $v > $OUT/env_${e}${v// /_}.log 2>&1 || exit 1; echo "$e $v $(grep -o '"ms_per_step": [0-9.]*' $OUT/env_${e}${v// /_}.log)" | tee -a $OUT/envsweep.txt; done; done ;;
     dagi) for v in dagq dagi dagq dagi; do run bench_mode_${v}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --stream-mode $v; done ;;
-    dagicmp) for r in 1 2 3; do for o in dagq inter qfirst; do if [ $o = dagq ]; then m=dagq; else m=dagi; fi; QDML_DAGI_ORDER=$o timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode $m > $OUT/cmp.log 2>&1 || exit 1; echo "$o $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/dagicmp.txt; done; done ;;
-    qscgrid) for r in 1 2; do for g in 256 128 64 576; do QDML_QSC_GRID_BWD=$g timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode dagi > $OUT/cmp.log 2>&1 || exit 1; echo "$g $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/qscgrid.txt; done; done ;;
-    dagiorder) for o in inter qfirst mainfirst inter qfirst mainfirst; do QDML_DAGI_ORDER=$o run bench_order_${o}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --stream-mode dagi; done ;;
+    dagicmp) for r in 1 2 3; do for o in dagq dagi; do m=$o; timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode $m > $OUT/cmp.log 2>&1 || exit 1; echo "$o $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/dagicmp.txt; done; done ;;
+    qscgrid) for r in 1 2; do for g in 256 128 64 576; do QDML_QSC_GRID_BWD=$g timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode ${MODE:-dagq} > $OUT/cmp.log 2>&1 || exit 1; echo "$g $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/qscgrid.txt; done; done ;;
     dpphase) for v in 1 2 3 1 2 3; do run bench_dpq_${v}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
     prio) for v in "" "--stream-priority" "" "--stream-priority" "--dtype fp8" "--dtype fp8 --stream-priority"; do run bench_prio_${v// /_} 300 python bench.py --steps 100 --warmup 10 $v; done ;;
     fusewd) for v in 1 0 1 0; do QDML_CONV_FUSE_WD=$v run bench_fwd_$v 300 python bench.py --steps 100 --warmup 10; mv $OUT/bench_fwd_$v.log $OUT/bench_fwd_${v}_$RANDOM.log; done ;;
     bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
-    prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace ${PROF_EXTRA:-} --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --stream-mode ${MODE:-dagi} ${BENCH_EXTRA:-}) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" && python scripts/prof_timeline.py "$OUT/prof/run_kernel_trace.csv" --marker "conv3x3_kernel<2," > "$OUT/prof_timeline.md" ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace ${PROF_EXTRA:-} --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --stream-mode ${MODE:-dagq} ${BENCH_EXTRA:-}) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" && python scripts/prof_timeline.py "$OUT/prof/run_kernel_trace.csv" --marker "conv3x3_kernel<2," > "$OUT/prof_timeline.md" ;;
     prof_fp8) (cd /tmp && export TMPDIR=/tmp && run prof_fp8 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_fp8" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --dtype fp8 --steps-per-graph 1) && python scripts/prof_summary.py "$OUT/prof_fp8/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_fp8_summary.md" && python scripts/prof_timeline.py "$OUT/prof_fp8/run_kernel_trace.csv" > "$OUT/prof_fp8_timeline.md" ;;
     stamp) run stamp 300 python scripts/stamp_qsc.py ;;
     stamp_conv) run stamp_conv 300 python scripts/stamp_conv.py ;;

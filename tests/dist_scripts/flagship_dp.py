@@ -42,7 +42,7 @@ def main(out, device="cpu"):
         tr.step()
         ok.append(same_on_all_ranks(flat_all(tr)))
         if dbg:
-            print(ctx.rank, "step", i, "same", ok[-1], "skip", tr.skip.tolist(), "h", float(tr.hdce.space.flat.double().sum()),
+            print(ctx.rank, "step", i, "same", ok[-1], "skip", tr.skip_flags().tolist(), "h", float(tr.hdce.space.flat.double().sum()),
                   "q", float(tr.qspace.flat.double().sum()), "hg", float(tr.hdce.space.grad.double().sum()),
                   "steps", tr.hopt.step_t.tolist(), tr.qopt.step_t.tolist(), flush=True)
     before = flat_all(tr).clone()
@@ -54,7 +54,7 @@ def main(out, device="cpu"):
     skipped = torch.equal(before, after)
     ok.append(same_on_all_ranks(after))
     with open(f"{out}.{ctx.rank}", "w") as f:
-        f.write(f"{int(all(ok))} {int(skipped)} {float(tr.skip.sum().item())}\n")
+        f.write(f"{int(all(ok))} {int(skipped)} {float(tr.skip_flags().sum().item())}\n")
     shutdown()
 
 

@@ -45,8 +45,7 @@ def _all_state(tr):
 
 @pytest.mark.parametrize("mode,split,k,phase", [("dag", False, 1, 3), ("dag", True, 1, 3), ("dagq", True, 1, 3),
                                                 ("dagq", True, 1, 2), ("dagq", True, 1, 1), ("dagq", False, 1, 3),
-                                                ("dagq", False, 3, 3), ("dag", False, 2, 3), ("dagi", False, 1, 3),
-                                                ("dagi", False, 3, 3)])
+                                                ("dagq", False, 3, 3), ("dag", False, 2, 3)])
 def test_multistream_graph_matches_serial_eager(cuda, mode, split, k, phase):
     """The 4-stream DAG step (captured in one graph, or the 3-graph DP plan) computes exactly what the
     single-stream eager step computes: every kernel is deterministic (slab reductions, no float
@@ -64,8 +63,10 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k, phase):
         ref.step()
     dag.run(4)                        # k-step replays + single steps for the remainder
     torch.cuda.synchronize()
-    assert torch.equal(ref.skip, dag.skip) and float(dag.skip.sum()) == 0.0
+    assert torch.equal(ref.skip_flags(), dag.skip_flags()) and float(dag.skip_flags().sum()) == 0.0
     for i, (a, b) in enumerate(zip(_all_state(ref), _all_state(dag))):
+        if b.numel() != a.numel():   # (the DP plan's HDCE space has a scratch slot at the end: the NaN flag)
+            b = b[:a.numel()]
         assert torch.allclose(a.float(), b.float(), rtol=1e-6, atol=1e-7), (i, float((a.float() - b.float()).abs().max()))
     assert torch.allclose(ref.hloss, dag.hloss, rtol=1e-6) and torch.allclose(ref.qloss, dag.qloss, rtol=1e-6)
     assert float(ref.hopt.step_t[0]) == 4.0 and bool((dag.hopt.step_t == 4.0).all())
