@@ -112,4 +112,52 @@ __device__ __forceinline__ void amax_block_store(float* part, float local_absmax
 }
 constexpr int kAmaxParts = 4096;   // partial slots per scaled tensor (>= any producer grid)
 
+// HDCE loss finish (nmse.hip's one-pass kernel leaves per-block error partials): per-stream sums,
+// loss = mean_s err_s / den_s (and the perfect-channel variant), NaN-guard flag.  A block-wide body
+// (every thread of a 256-thread block calls it) so that any later launch of the step can host it as
+// one extra workgroup -- nmse_finish_kernel, or the BN backward reduction (one launch fewer).
+struct LossFinish {
+  const float* part;   // (chunks, gx, E, 2)
+  const float* dens;   // (S, 2)
+  float* ss;           // (S, 4) scratch
+  float* loss;         // (2,)
+  float* skip;         // (1,) nullable
+  int gx, chunks_per_u, U, E;
+};
+__device__ inline void loss_finish_body(const LossFinish& f) {
+  // wave w takes streams w, w + waves, ... (each in a fixed order); then thread 0 forms the loss over
+  // the streams in order (deterministic)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int E = f.E, U = f.U, S = E * U;
+  for (int s = wv; s < S; s += nw) {
+    const int e = s / U, u = s % U;
+    float n = 0.f, np = 0.f;
+    for (int j = lane; j < f.chunks_per_u * f.gx; j += 64) {
+      const int k = u * f.chunks_per_u + j / f.gx, x = j % f.gx;
+      const float* p = f.part + ((size_t)k * f.gx + x) * 2 * E + 2 * e;
+      n += p[0];
+      np += p[1];
+    }
+    n = wave_sum(n);
+    np = wave_sum(np);
+    if (lane == 0) {
+      f.ss[s * 4 + 0] = n;
+      f.ss[s * 4 + 1] = f.dens[s * 2];
+      f.ss[s * 4 + 2] = np;
+      f.ss[s * 4 + 3] = f.dens[s * 2 + 1];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f, lp = 0.f;
+    for (int s = 0; s < S; ++s) {
+      l += f.ss[s * 4 + 0] / f.ss[s * 4 + 1];
+      lp += f.ss[s * 4 + 3] > 0.f ? f.ss[s * 4 + 2] / f.ss[s * 4 + 3] : 0.f;
+    }
+    f.loss[0] = l / (float)S;
+    f.loss[1] = lp / (float)S;
+    if (f.skip) *f.skip = isfinite(f.loss[0]) ? 0.f : 1.f;
+  }
+}
+
 }  // namespace qd

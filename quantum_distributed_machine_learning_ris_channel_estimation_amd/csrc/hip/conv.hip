@@ -847,7 +847,11 @@ __global__ void __launch_bounds__(64) bn_stats_finalize_kernel(FinJobs jobs, int
 template <int HW, typename TDH>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restrict__ dh, const uint16_t* __restrict__ z,
                                                             const float* __restrict__ st, float* __restrict__ slab,
-                                                            int E, int B, int chunks, int spb) {
+                                                            int E, int B, int chunks, int spb, LossFinish lf) {
+  if ((int)blockIdx.y == E) {   // the extra row (lf.part set): block 0 hosts the HDCE loss finish
+    if (blockIdx.x == 0) loss_finish_body(lf);
+    return;
+  }
   const int tid = threadIdx.x, grp = tid >> 4, gl = tid & 15;
   const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
   const int EC = E * CO;
@@ -1305,17 +1309,19 @@ QD_API int qd_bn_stats_finalize_multi(int n, const float* const* stats, const fl
   return (int)hipGetLastError();
 }
 
+// lf (nullable): also run this loss finish (see common.h) as one extra workgroup
 QD_API int qd_bn_bwd_reduce(const void* dh, int dh_bf16, const uint16_t* z, const float* st, float* slab, int N, int E,
-                            int B, int H, int W, int chunks, int spb, void* stream) {
-  dim3 grid((N / B) * chunks, E);
+                            int B, int H, int W, int chunks, int spb, const qd::LossFinish* lf_in, void* stream) {
+  const qd::LossFinish lf = (lf_in && lf_in->part) ? *lf_in : qd::LossFinish{};
+  dim3 grid((N / B) * chunks, E + (lf.part ? 1 : 0));
   hipStream_t s = (hipStream_t)stream;
   if (chunks * spb < B || H * W % 64) return (int)hipErrorInvalidValue;
   if (H * W == 128) {
-    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb);
-    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb);
+    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb, lf);
   } else if (H * W == 256) {
-    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb);
-    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb);
+    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
+    else hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb, lf);
   } else {
     return (int)hipErrorInvalidValue;
   }

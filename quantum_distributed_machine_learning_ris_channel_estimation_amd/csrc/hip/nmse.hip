@@ -365,39 +365,7 @@ __global__ void __launch_bounds__(256) nmse_finish_kernel(const float* __restric
     }
     return;
   }
-  // per-stream sums: wave w takes streams w, w + waves, ... (each in a fixed order); then thread 0
-  // forms the loss over the streams in order (deterministic)
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int S = E * U;
-  for (int s = wv; s < S; s += nw) {
-    const int e = s / U, u = s % U;
-    float n = 0.f, np = 0.f;
-    for (int j = lane; j < chunks_per_u * gx; j += 64) {
-      const int k = u * chunks_per_u + j / gx, x = j % gx;
-      const float* p = part + ((size_t)k * gx + x) * 2 * E + 2 * e;
-      n += p[0];
-      np += p[1];
-    }
-    n = wave_sum(n);
-    np = wave_sum(np);
-    if (lane == 0) {
-      ss[s * 4 + 0] = n;
-      ss[s * 4 + 1] = dens[s * 2];
-      ss[s * 4 + 2] = np;
-      ss[s * 4 + 3] = dens[s * 2 + 1];
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float l = 0.f, lp = 0.f;
-    for (int s = 0; s < S; ++s) {
-      l += ss[s * 4 + 0] / ss[s * 4 + 1];
-      lp += ss[s * 4 + 3] > 0.f ? ss[s * 4 + 2] / ss[s * 4 + 3] : 0.f;
-    }
-    loss[0] = l / (float)S;
-    loss[1] = lp / (float)S;
-    if (skip) *skip = isfinite(loss[0]) ? 0.f : 1.f;
-  }
+  loss_finish_body(LossFinish{part, dens, ss, loss, skip, gx, chunks_per_u, U, E});
 }
 
 }  // namespace nmse
@@ -409,7 +377,9 @@ using namespace qd::nmse;
 // (B*E) % rpc == 0; cols % 1024 == 0.  colsum: (rows/rpc, cols); part: (rows/rpc, cols/1024, E, 2);
 // dens: (S, 2); ss: (S, 4) as qd_nmse_reduce_finalize's.  perf / rowpow_p nullable together.
 // finish_bias = 0: the finish launch only forms the loss; the caller reduces colsum -> bias_grad itself
-// (e.g. as one job of a later batched slab reduction, off the critical path).
+// (e.g. as one job of a later batched slab reduction, off the critical path).  finish_bias = 2: no
+// finish launch at all -- the caller runs the loss finish (LossFinish over part / dens / ss / loss /
+// skip, gx = cols / 1024, chunks_per_u = B*E / rpc) in a later launch (qd_bn_bwd_reduce's lf).
 QD_API int qd_nmse_fused(const void* Y, int y_bf16, const float* label, const float* perf, const int* rowoff,
                          const float* rowpow_l, const float* rowpow_p, void* dY, int dy_bf16, float* colsum,
                          float* part, float* dens, float* bias_grad, float* ss, float* loss, float* skip, int E, int U,
@@ -438,6 +408,7 @@ QD_API int qd_nmse_fused(const void* Y, int y_bf16, const float* label, const fl
   }
 #undef QD_E
 #undef QD_F
+  if (finish_bias == 2) return (int)hipGetLastError();
   const int chunks = rows / rpc;
 #define QD_N(EE)                                                                                                   \
   hipLaunchKernelGGL((nmse_finish_kernel<EE>), dim3(finish_bias ? cols / 64 + 1 : 1),                          \

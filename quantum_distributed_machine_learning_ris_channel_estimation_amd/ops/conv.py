@@ -97,7 +97,7 @@ class ConvStackHIP:
         self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
         self._fin = nat.fn(L, "qd_bn_stats_finalize_multi", [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i,
                                                                 _p, _i, ctypes.c_longlong, _p])
-        self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p])
+        self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _i, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
@@ -164,14 +164,16 @@ class ConvStackHIP:
 
     # --------------------------------------------------------------------- backward
     def backward(self, dh3: torch.Tensor, accumulate: bool = True, slabs: Optional["SlabBatch"] = None,
-                 side: Optional["torch.cuda.Stream"] = None) -> None:
+                 side: Optional["torch.cuda.Stream"] = None, loss_finish=None) -> None:
         """dh3: dL/dh3 as (N*E, 32*H*W) (bf16 or fp32).  Adds (accumulate) or writes the conv/BN grads
         into the flat grad -- writing makes a zero_grad before the step unnecessary.
 
         ``side``: a second stream for the weight-gradient kernels of layers 3 and 2.  wgrad(k) and
         dgrad(k) only share their inputs, so the dgrad chain (the critical path to layer 1) runs on
         the current stream while wgrad(k) runs beside it; the current stream joins before the slab
-        reduction.  Each of these kernels fills well under the 256 CUs, so they overlap."""
+        reduction.  Each of these kernels fills well under the 256 CUs, so they overlap.
+        ``loss_finish`` (ops.nmse.LossFinish): the deferred HDCE loss finish, hosted by layer 3's BN
+        reduction launch as one extra workgroup."""
         m, st = self.m, nat.stream_ptr(dh3.device)
         main = torch.cuda.current_stream(dh3.device) if side is not None else None
         dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
@@ -179,8 +181,9 @@ class ConvStackHIP:
             z, bst = self.z[k], self.st[k]
             rs = self.rslab[k]
             if k == 2 or not self.fuse_bn_red:   # (else the previous dgrad produced these partials)
+                lf = ctypes.byref(loss_finish) if (loss_finish is not None and k == 2) else None
                 nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(rs), self.N, self.E,
-                                     self.B, self.H, self.W, self.chunks_r, self.spb_r, st), f"bn_bwd_reduce{k + 1}")
+                                     self.B, self.H, self.W, self.chunks_r, self.spb_r, lf, st), f"bn_bwd_reduce{k + 1}")
             # BN backward finalisation fused into this layer's wgrad and dgrad kernels
             bnb = BnBwd(nat.ptr(rs), nat.ptr(m.bn_w[k]), self.rchunks[k], float(self.B * self.HW))
             xin = self.x1 if k == 0 else self.z[k - 1]

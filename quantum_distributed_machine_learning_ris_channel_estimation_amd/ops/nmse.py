@@ -29,6 +29,13 @@ from .. import _native as nat
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
 
+class LossFinish(ctypes.Structure):
+    """csrc/hip/common.h LossFinish: the HDCE loss finish a later launch can host."""
+    _fields_ = [("part", ctypes.c_void_p), ("dens", ctypes.c_void_p), ("ss", ctypes.c_void_p),
+                ("loss", ctypes.c_void_p), ("skip", ctypes.c_void_p), ("gx", ctypes.c_int),
+                ("chunks_per_u", ctypes.c_int), ("U", ctypes.c_int), ("E", ctypes.c_int)]
+
+
 class StreamNMSE:
     def __init__(self, row_stream: torch.Tensor, n_streams: int, cols: int = 2048):
         self.row_stream = row_stream.to(torch.int32).contiguous()
@@ -176,12 +183,14 @@ class StreamNMSE:
     def fused(self, Y: torch.Tensor, label: torch.Tensor, perf: Optional[torch.Tensor], bias_grad: torch.Tensor,
               layout: Tuple[int, int, int], out_dtype=torch.bfloat16, loss_scale: float = 1.0,
               rpc_mult: Optional[int] = None, rowden: Optional[torch.Tensor] = None,
-              bias_slabs=None) -> torch.Tensor:
+              bias_slabs=None, defer_loss: bool = False) -> torch.Tensor:
         """GPU, labels through ``rowoff``, rows in (u, b, e) order with ``layout`` = (E, U, B): loss,
         loss_perf, skip, dY and the bias gradient (overwritten into ``bias_grad``) in TWO launches
         (csrc/hip/nmse.hip qd_nmse_fused).  Returns dY; the loss is ``self.loss``.
         ``bias_slabs`` (ops.slabsum.SlabBatch): queue the bias-gradient column reduction on it instead
-        (the caller launches it in overwrite mode later in the step)."""
+        (the caller launches it in overwrite mode later in the step).  ``defer_loss`` (with
+        ``bias_slabs``): no finish launch; ``self.pending_finish`` (a LossFinish) must be handed to a
+        later launch of the step (ConvStackHIP.backward's ``loss_finish``), which forms loss and skip."""
         E, U, B = layout
         assert Y.is_cuda and self.rowoff is not None and Y.shape == (self.rows, self.cols) and self.rows == E * U * B
         self._check_labels(label)
@@ -205,8 +214,15 @@ class StreamNMSE:
                     nat.ptr(rp) if rp is not None else None, nat.ptr(dY), int(out_dtype == torch.bfloat16),
                     nat.ptr(colsum), nat.ptr(part), nat.ptr(dens), nat.ptr(bias_grad), nat.ptr(self.ss),
                     nat.ptr(self.loss), nat.ptr(self.skip), E, U, B, self.cols, rpc, loss_scale,
-                    nat.ptr(rowden) if rowden is not None else None, int(bias_slabs is None), nat.stream_ptr(dev)),
+                    nat.ptr(rowden) if rowden is not None else None,
+                    2 if defer_loss else int(bias_slabs is None), nat.stream_ptr(dev)),
                   "nmse_fused")
+        self.pending_finish = None
+        if defer_loss:
+            assert bias_slabs is not None, "defer_loss needs the bias reduction queued elsewhere"
+            self.pending_finish = LossFinish(nat.ptr(part), nat.ptr(dens), nat.ptr(self.ss), nat.ptr(self.loss),
+                                             nat.ptr(self.skip) if self.skip is not None else None,
+                                             gx, (B * E) // rpc, U, E)
         if bias_slabs is not None:
             bias_slabs.add(colsum, bias_grad, 1, chunks, self.cols)
         return dY

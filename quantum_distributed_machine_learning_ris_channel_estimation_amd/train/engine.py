@@ -274,6 +274,7 @@ class HDCEStep:
         # world-1 plans: the FC bias gradient's column reduction rides in the conv backward's slab launch
         # (never in DP: the FC gradient bucket is all-reduced before the conv backward runs)
         self.bias_via_conv_slabs = False
+        self.defer_loss = True   # (with bias_via_conv_slabs) loss finish hosted by the conv backward
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         if self.hip:
             from ..ops.conv import ConvStackHIP
@@ -330,14 +331,16 @@ class HDCEStep:
         if self.hip:
             pending = getattr(self, "_slabs", None)
             self._slabs = None
+            lf = getattr(self.nmse, "pending_finish", None)
+            self.nmse.pending_finish = None
             if pending is not None and slabs is None:
                 # the conv weight / BN slabs and the pending FC bias reduction: one overwrite launch
-                self.conv.backward(self._dA, accumulate=False, slabs=pending, side=side)
+                self.conv.backward(self._dA, accumulate=False, slabs=pending, side=side, loss_finish=lf)
                 pending.launch(accumulate=False, stream=nat.stream_ptr(self._dA.device))
             else:
                 if pending is not None:
                     pending.launch(accumulate=False, stream=nat.stream_ptr(self._dA.device))
-                self.conv.backward(self._dA, accumulate=False, slabs=slabs, side=side)
+                self.conv.backward(self._dA, accumulate=False, slabs=slabs, side=side, loss_finish=lf)
         else:
             torch.autograd.backward(self._A, self._dA)
             self._A = None
@@ -373,8 +376,11 @@ class HDCEStep:
             # between the loss and the FC gradient GEMMs)
             from ..ops.slabsum import SlabBatch
             self._slabs = SlabBatch() if (self.writes_grads and self.bias_via_conv_slabs) else None
+            # (with the bias in the conv slab batch, the loss finish rides in the conv backward too:
+            # nothing between here and there reads loss or skip)
             dY = self.nmse.fused(Y, label, perf, m.fc_b.grad, (m.E, self.U, self.B), out_dtype=dt,
-                                 rowden=getattr(self, "_rowden", None), bias_slabs=self._slabs)
+                                 rowden=getattr(self, "_rowden", None), bias_slabs=self._slabs,
+                                 defer_loss=self._slabs is not None and self.defer_loss)
             loss = self.nmse.loss
         else:
             loss = self.nmse.sums_finalize(Y, label, perf)

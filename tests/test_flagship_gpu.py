@@ -87,3 +87,21 @@ def test_dp_plan_two_ranks_on_one_gpu(tmp_path):
     for r in range(2):
         same, skipped, flag = open(f"{out}.{r}").read().split()
         assert same == "1" and skipped == "1" and float(flag) >= 1.0, (r, same, skipped, flag)
+
+
+def test_deferred_loss_finish_matches_finish_launch(cuda):
+    """The HDCE loss finish hosted by the conv backward's BN-reduction launch (default at world 1)
+    gives the same loss, NaN flag and training state as the separate finish launch."""
+    ctx = DistContext(device=cuda)
+    base = dict(batch=32, data_len=800, use_quantumnat=True, hip_graphs=False)
+    a = FlagshipTrainer(FlagshipConfig(**base), ctx)
+    b = FlagshipTrainer(FlagshipConfig(**base), ctx)
+    b.hstep.defer_loss = False
+    for _ in range(3):
+        a.step()
+        b.step()
+        torch.cuda.synchronize()
+        assert a.hstep.nmse.pending_finish is None
+        assert torch.equal(a.hloss, b.hloss) and torch.equal(a.skip_flags(), b.skip_flags())
+    for x, y in zip(_all_state(a), _all_state(b)):
+        assert torch.equal(x, y)
