@@ -16,6 +16,8 @@
 //     bumps it, so a step is one launch, not two;
 //   * an optional bf16 "shadow" of a parameter range (the FC weight): the forward GEMM reads
 //     the shadow instead of casting 8.4 M fp32 weights every step.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace qd {
@@ -71,6 +73,29 @@ __device__ __forceinline__ float store_shadow(const Shadow& sh, long i0, float4 
   return 0.f;
 }
 
+// NT: streaming (non-temporal) loads / stores for the big parameter ranges (each element is touched
+// once per step: keeping it in L2 / MALL only evicts the activations the next kernels re-read)
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ldv(const float* a) {
+  if constexpr (NT) {
+    const f32x4v r = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(a));
+    return make_float4(r.x, r.y, r.z, r.w);
+  } else {
+    return *reinterpret_cast<const float4*>(a);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void stv(float* a, float4 v) {
+  if constexpr (NT) {
+    const f32x4v r = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(r, reinterpret_cast<f32x4v*>(a));
+  } else {
+    *reinterpret_cast<float4*>(a) = v;
+  }
+}
+
+template <bool NT>
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n,
                                                    const float* __restrict__ lr_ptr, const float* step_ptr,
@@ -89,10 +114,10 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
   const long stride = (long)gridDim.x * blockDim.x * 4;
   for (long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < n; i0 += stride) {
     if (i0 + 3 < n) {
-      float4 pp = *reinterpret_cast<float4*>(p + i0);
-      float4 gg = *reinterpret_cast<float4*>(g + i0);
-      float4 mm = *reinterpret_cast<float4*>(m + i0);
-      float4 vv = *reinterpret_cast<float4*>(v + i0);
+      float4 pp = ldv<NT>(p + i0);
+      float4 gg = ldv<NT>(g + i0);
+      float4 mm = ldv<NT>(m + i0);
+      float4 vv = ldv<NT>(v + i0);
       float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -107,10 +132,10 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         pa[j] = pj - step_size * ma[j] / denom;
         ga[j] = gj;
       }
-      *reinterpret_cast<float4*>(p + i0) = pp;
+      stv<NT>(p + i0, pp);
       wmax = fmaxf(wmax, store_shadow(sh, i0, pp));
-      *reinterpret_cast<float4*>(m + i0) = mm;
-      *reinterpret_cast<float4*>(v + i0) = vv;
+      stv<NT>(m + i0, mm);
+      stv<NT>(v + i0, vv);
       if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
     } else {
       for (long i = i0; i < n; ++i) {
@@ -213,8 +238,14 @@ QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const fl
   Shadow sh{shadow, shadow_lo, shadow_hi, shadow8, qs, amax};
   // max_grid (0 = 2048): fewer workgroups stream the update more slowly but leave most CUs to
   // kernels running beside it (the FC Adam as a side branch of the step graph)
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, max_grid > 0 ? max_grid : 2048)), dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step,
-                     done, sh);
+  // streaming loads/stores for large ranges (QDML_ADAM_NT=0/1 overrides; measured in scripts/gpu_check.sh adamnt)
+  static const int nt_env = [] { const char* e = getenv("QDML_ADAM_NT"); return e ? atoi(e) : -1; }();
+  const bool nt = nt_env >= 0 ? nt_env != 0 : n >= (1L << 20);
+  const dim3 grid(grid_for(n, max_grid > 0 ? max_grid : 2048));
+  if (nt)
+    hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh);
+  else
+    hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh);
   return (int)hipGetLastError();
 }
 
