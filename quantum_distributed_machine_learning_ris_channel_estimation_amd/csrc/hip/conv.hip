@@ -782,12 +782,11 @@ struct FinJobs {
   float* run_var[3];
   float* st[3];
 };
-__global__ void __launch_bounds__(64) bn_stats_finalize_kernel(FinJobs jobs, int U, int chunks, int EC, float count,
-                                                               float momentum, float eps, int training,
-                                                               long long* __restrict__ nbt, int n_nbt,
-                                                               long long nbt_inc) {
+// one (layer l, channel ch) per wave; st[l] null: running statistics only (no records)
+__device__ __forceinline__ void bn_fin_body(const FinJobs& jobs, int ch, int l, int lane, int U, int chunks, int EC,
+                                            float count, float momentum, float eps, int training,
+                                            long long* __restrict__ nbt, int n_nbt, long long nbt_inc) {
   // every global load is issued up front (the per-group loop paid one round trip per group)
-  const int ch = blockIdx.x, lane = threadIdx.x, l = blockIdx.y;
   const float* __restrict__ stats = jobs.stats[l];
   const float* __restrict__ gamma = jobs.gamma[l];
   const float* __restrict__ beta = jobs.beta[l];
@@ -831,14 +830,24 @@ __global__ void __launch_bounds__(64) bn_stats_finalize_kernel(FinJobs jobs, int
         var = rv;
       }
       const float inv = rsqrtf(var + eps);
-      float4* r = reinterpret_cast<float4*>(st + ((size_t)u * EC + ch) * NST);
-      r[0] = make_float4(mean, inv, g * inv, bt - mean * g * inv);   // ST_MEAN, ST_INV, ST_A, ST_B
+      if (st) {
+        float4* r = reinterpret_cast<float4*>(st + ((size_t)u * EC + ch) * NST);
+        r[0] = make_float4(mean, inv, g * inv, bt - mean * g * inv);   // ST_MEAN, ST_INV, ST_A, ST_B
+      }
     }
     if (training) {
       run_mean[ch] = rm;
       run_var[ch] = rv;
     }
   }
+}
+
+__global__ void __launch_bounds__(64) bn_stats_finalize_kernel(FinJobs jobs, int U, int chunks, int EC, float count,
+                                                               float momentum, float eps, int training,
+                                                               long long* __restrict__ nbt, int n_nbt,
+                                                               long long nbt_inc) {
+  bn_fin_body(jobs, blockIdx.x, blockIdx.y, threadIdx.x, U, chunks, EC, count, momentum, eps, training, nbt, n_nbt,
+              nbt_inc);
 }
 
 // Backward reductions: per (u, chunk, ch): sum g, sum g*xhat.  grid (U*chunks, E), block 256.
@@ -966,6 +975,60 @@ __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __re
     const int n = (int)(row / EC);
     const float* sc = st + ((size_t)(n / B) * EC + ch) * NST;
     const float a = sc[ST_A], b = sc[ST_B];
+    float v[8];
+    load8(z + e0, v);
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = relu_nan(a * v[j] + b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+    *reinterpret_cast<uint4*>(h + e0) = make_uint4(w[0], w[1], w[2], w[3]);
+    if (h8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j]);
+      const uint32_t p0 = e4m3_pack4(v[0] * q, v[1] * q, v[2] * q, v[3] * q);
+      const uint32_t p1 = e4m3_pack4(v[4] * q, v[5] * q, v[6] * q, v[7] * q);
+      *reinterpret_cast<uint2*>(h8 + e0) = make_uint2(p0, p1);
+    }
+  }
+  if (h8) amax_block_store(amax, mx);
+}
+
+// Layer-3 BN + ReLU apply with the BN tail folded in: one launch instead of two.
+// Workgroups [0, U*ach*E), (u, chunk, e): build the (u, e) records from the conv's statistics partials
+// (bn_fwd_build, as the conv kernels do for layers 1 / 2; chunk 0 publishes them for the backward), then
+// h = relu(a z + b) for spb samples x 32 channels (32*HW contiguous bf16 per sample).  Workgroups
+// beyond: every layer's running statistics (+ num_batches_tracked), one (layer, channel) per wave --
+// jobs.st[2] is null there, the records of layer 3 come from the apply workgroups only.
+template <int HW>
+__global__ void __launch_bounds__(256) bn_apply_tail_kernel(const uint16_t* __restrict__ z, uint16_t* __restrict__ h,
+                                                            BnFwd bnf, FinJobs jobs, int U, int E, int B, int spb,
+                                                            int ach, int chunks, int training,
+                                                            long long* __restrict__ nbt, int n_nbt, long long nbt_inc,
+                                                            uint8_t* __restrict__ h8, const float* __restrict__ qs,
+                                                            float* __restrict__ amax) {
+  const int EC = E * CO;
+  const int napply = U * ach * E;
+  if ((int)blockIdx.x >= napply) {
+    const int idx = ((int)blockIdx.x - napply) * 4 + (threadIdx.x >> 6);
+    if (idx < 3 * EC)
+      bn_fin_body(jobs, idx % EC, idx / EC, threadIdx.x & 63, U, chunks, EC, bnf.count, bnf.momentum, bnf.eps,
+                  training, nbt, n_nbt, nbt_inc);
+    return;
+  }
+  __shared__ float stl[CO * NST];
+  const int e = blockIdx.x % E, rest = blockIdx.x / E, chunk = rest % ach, u = rest / ach;
+  bn_fwd_build(bnf, stl, u, e, EC, chunk == 0);
+  __syncthreads();
+  const float q = h8 ? qs[0] : 0.f;
+  float mx = 0.f;
+  const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
+  constexpr int ITEMS = CO * HW / 8;   // 8-value items per sample
+  for (int t = threadIdx.x; t < (nend - n0) * ITEMS; t += 256) {
+    const int n = n0 + t / ITEMS, i = t % ITEMS;
+    const size_t e0 = ((size_t)n * EC + e * CO) * HW + (size_t)i * 8;
+    const int c = (i * 8) / HW;
+    const float a = stl[c * NST + ST_A], b = stl[c * NST + ST_B];
     float v[8];
     load8(z + e0, v);
     uint32_t w[4];
@@ -1350,6 +1413,42 @@ QD_API int qd_bn_relu_apply(const uint16_t* z, const float* st, uint16_t* h, int
   else if (HW == 256)
     hipLaunchKernelGGL((bn_relu_apply_kernel<256>), dim3(grid), dim3(256), 0, (hipStream_t)stream, z, st, h, n8, EC, B,
                        h8, qs, amax);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// Layer-3 BN tail + BN/ReLU apply in one launch (bn_apply_tail_kernel).  bnf: layer 3's BnFwd (records
+// published to bnf->st_out); stats/gamma/beta/run_mean/run_var/st: the 3 layers' arrays as in
+// qd_bn_stats_finalize_multi (st[2] is ignored: layer 3's records come from bnf).  spb: samples per
+// apply workgroup (divides B).
+QD_API int qd_bn_apply_tail(const uint16_t* z, uint16_t* h, const BnFwd* bnf, const float* const* stats,
+                            const float* const* gamma, const float* const* beta, float* const* run_mean,
+                            float* const* run_var, float* const* st, int U, int E, int B, int HW, int spb, int chunks,
+                            int training, long long* nbt, int n_nbt, long long nbt_inc, uint8_t* h8, const float* qs,
+                            float* amax, void* stream) {
+  if (!bnf || U < 1 || U > kMaxGroups || n_nbt > 64 || spb < 1 || B % spb || (h8 && (!qs || !amax)))
+    return (int)hipErrorInvalidValue;
+  FinJobs jobs{};
+  for (int l = 0; l < 3; ++l) {
+    jobs.stats[l] = stats[l];
+    jobs.gamma[l] = gamma[l];
+    jobs.beta[l] = beta[l];
+    jobs.run_mean[l] = run_mean[l];
+    jobs.run_var[l] = run_var[l];
+    jobs.st[l] = l == 2 ? nullptr : st[l];
+  }
+  const int ach = B / spb, EC = E * CO;
+  const int napply = U * ach * E, nfin = (3 * EC + 3) / 4;
+  if (napply > qd::kAmaxParts) return (int)hipErrorInvalidValue;
+  const dim3 grid(napply + nfin);
+  hipStream_t s = (hipStream_t)stream;
+  if (HW == 128)
+    hipLaunchKernelGGL((bn_apply_tail_kernel<128>), grid, dim3(256), 0, s, z, h, *bnf, jobs, U, E, B, spb, ach, chunks,
+                       training, nbt, n_nbt, nbt_inc, h8, qs, amax);
+  else if (HW == 256)
+    hipLaunchKernelGGL((bn_apply_tail_kernel<256>), grid, dim3(256), 0, s, z, h, *bnf, jobs, U, E, B, spb, ach, chunks,
+                       training, nbt, n_nbt, nbt_inc, h8, qs, amax);
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();

@@ -11,6 +11,7 @@ HIP graph.  Gradients are written straight into the model's flat gradient buffer
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional
 
 import torch
@@ -100,6 +101,12 @@ class ConvStackHIP:
         self._bred = nat.fn(L, "qd_bn_bwd_reduce", [_p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
         self._bfin = nat.fn(L, "qd_bn_bwd_finalize", [_p, _p, _p, _p, _p, _i, _i, _i, _f, _i, _p])
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
+        self._apply_tail = nat.fn(L, "qd_bn_apply_tail", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i,
+                                                           _i, _p, _i, ctypes.c_longlong, _p, _p, _p, _p])
+        # the BN tail (running statistics) and layer 3's BN/ReLU apply as ONE launch (QDML_BN_APPLY_TAIL=0:
+        # two launches, the tail publishing layer 3's records)
+        self.apply_tail = os.environ.get("QDML_BN_APPLY_TAIL", "1") != "0"
+        self.spb_a = 8 if B % 8 == 0 else 1
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
         self._packm2 = nat.fn(L, "qd_conv_pack_weights_multi2", [_i, _p, _p, _p, _p, _i, _p, _i, _p])
         # pack_at_tail: the owner packs the weights at the END of each step (after the optimizer) and
@@ -108,7 +115,6 @@ class ConvStackHIP:
         self._wd = nat.fn(L, "qd_conv_wgrad_dgrad", [_p, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i,
                                                         _p, _p, _p])
         # wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate launches)
-        import os
         self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
 
     def pack_weights(self, st, cursor: Optional[torch.Tensor] = None, cursor_inc: int = 0) -> None:
@@ -153,10 +159,21 @@ class ConvStackHIP:
         # layer's records (layers 1, 2 were built -- bitwise identically -- by their consumers)
         nbt = getattr(m, "_nbt", None) if (training and self.count_batches) else None
         arr = lambda xs: (ctypes.c_void_p * 3)(*[nat.ptr(x) for x in xs])
+        f8 = self.m.fp8_scales if self.fp8 else None
+        if self.apply_tail:
+            bnf3 = BnFwd(nat.ptr(self.stats[2]), nat.ptr(m.bn_w[2]), nat.ptr(m.bn_b[2]), nat.ptr(m.run_mean[2]),
+                         nat.ptr(m.run_var[2]), nat.ptr(self.st[2]), self.chunks, float(self.B * self.HW),
+                         m.momentum, m.eps, int(training))
+            nat.check(self._apply_tail(nat.ptr(self.z[2]), nat.ptr(self.h3), ctypes.byref(bnf3), arr(self.stats),
+                                       arr(m.bn_w), arr(m.bn_b), arr(m.run_mean), arr(m.run_var), arr(self.st),
+                                       self.U, self.E, self.B, self.HW, self.spb_a, self.chunks, int(training),
+                                       _ptr(nbt), nbt.numel() if nbt is not None else 0, self.U, _ptr(self.h3_8),
+                                       nat.ptr(f8.qs) if f8 else None, nat.ptr(f8.amax[0]) if f8 else None, st),
+                      "bn_apply_tail")
+            return self.h3
         nat.check(self._fin(3, arr(self.stats), arr(m.bn_w), arr(m.bn_b), arr(m.run_mean), arr(m.run_var), arr(self.st),
                             self.U, self.chunks, self.EC, float(self.B * self.HW), m.momentum, m.eps, int(training),
                             _ptr(nbt), nbt.numel() if nbt is not None else 0, self.U, st), "bn_tail")
-        f8 = self.m.fp8_scales if self.fp8 else None
         nat.check(self._apply(nat.ptr(self.z[2]), nat.ptr(self.st[2]), nat.ptr(self.h3), self.N, self.EC, self.B,
                               self.HW, _ptr(self.h3_8), nat.ptr(f8.qs) if f8 else None,
                               nat.ptr(f8.amax[0]) if f8 else None, st), "bn_relu_apply")
