@@ -36,13 +36,44 @@ struct Shadow {
   float* amax;          // per-workgroup max |p| partials over the range (next step's delayed scale)
 };
 
+// Conv weight images written by the update itself: csrc/hip/conv.hip pack_weights_body's B-fragment
+// layouts as a scatter (forward image of each layer, dgrad image of layers 2 / 3), so the updated
+// weights need no separate pack launch; the step's batch cursor advances with the step tick.
+struct PackScatter {
+  long lo[3];           // offsets (relative to this launch's p) of the 3 layers' weights (E*32*CIN*9 each)
+  int n[3], cin[3];     // n[k] = 0: layer k not in this launch
+  uint16_t* fwd[3];     // [e][KS][64][8] bf16, KS = (9*CIN + 15) / 16 (padding written once at init)
+  uint16_t* dg[3];      // [e][18][64][8] bf16 (CIN = 32 only), nullable
+  int* cursor;          // nullable: *cursor += cursor_inc once per launch (also when the step is skipped)
+  int cursor_inc;
+};
+
+__device__ __forceinline__ void pack_scatter(const PackScatter& ps, long i0, const float* v4) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (ps.n[k] == 0 || i0 < ps.lo[k] || i0 >= ps.lo[k] + ps.n[k]) continue;
+    const int CIN = ps.cin[k], per = 32 * CIN * 9, KS = (9 * CIN + 15) / 16;
+    for (int q = 0; q < 4; ++q) {
+      const int idx = (int)(i0 - ps.lo[k]) + q;
+      const int e = idx / per, r = idx % per, co = r / (CIN * 9), ci = (r % (CIN * 9)) / 9, tap = r % 9;
+      const uint16_t b = f32_to_bf16(v4[q]);
+      int kk = tap * CIN + ci;   // forward: W[e*32 + col][k % CIN][k / CIN], col = co
+      ps.fwd[k][(((size_t)e * KS + kk / 16) * 64 + ((kk % 16) / 8) * 32 + co) * 8 + kk % 8] = b;
+      if (ps.dg[k]) {            // dgrad: W[e*32 + k % 32][col][8 - k / 32], col = ci
+        kk = (8 - tap) * 32 + co;
+        ps.dg[k][(((size_t)e * 18 + kk / 16) * 64 + ((kk % 16) / 8) * 32 + ci) * 8 + kk % 8] = b;
+      }
+    }
+  }
+}
+
 // Called by every thread at the end of the kernel: the last workgroup to get here increments the
 // step counter and re-arms the done counter.  Every workgroup consumed *step (its value feeds the
 // update it already stored) before it arrives, so no workgroup can observe the increment of the
 // step it is computing.  Deliberately NO __threadfence(): only the counter itself is shared, and
 // on gfx950 an agent-scope release per workgroup writes back the XCD's whole dirty L2 -- measured
 // 3x slower for this kernel (47 -> 145 us).  The next kernel sees *step via kernel-boundary ordering.
-__device__ __forceinline__ void tick_if_last(float* step, unsigned int* done) {
+__device__ __forceinline__ void tick_if_last(float* step, unsigned int* done, int* cursor = nullptr, int inc = 0) {
   __shared__ bool last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -52,6 +83,7 @@ __device__ __forceinline__ void tick_if_last(float* step, unsigned int* done) {
   __syncthreads();
   if (last && threadIdx.x == 0) {
     *step += 1.f;
+    if (cursor) *cursor += inc;
     __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -101,8 +133,11 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    const float* __restrict__ lr_ptr, const float* step_ptr,
                                                    const float* __restrict__ skip, unsigned int* __restrict__ pruned,
                                                    AdamArgs a, float* __restrict__ step_out,
-                                                   unsigned int* __restrict__ done, Shadow sh) {
-  if (skip != nullptr && *skip != 0.f) return;  // uniform across the grid: nobody ticks
+                                                   unsigned int* __restrict__ done, Shadow sh, PackScatter ps) {
+  if (skip != nullptr && *skip != 0.f) {   // uniform across the grid: nobody ticks (the cursor still moves)
+    if (ps.cursor && blockIdx.x == 0 && threadIdx.x == 0) *ps.cursor += ps.cursor_inc;
+    return;
+  }
   const float lr = *lr_ptr;
   const float t = *step_ptr + 1.f;  // step about to be taken
   const float bc1 = 1.f - __powf(a.beta1, t);
@@ -134,6 +169,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
       }
       stv<NT>(p + i0, pp);
       wmax = fmaxf(wmax, store_shadow(sh, i0, pp));
+      pack_scatter(ps, i0, &pp.x);
       stv<NT>(m + i0, mm);
       stv<NT>(v + i0, vv);
       if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
@@ -165,7 +201,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     if ((threadIdx.x & 63) == 0 && c > 0.f) atomicAdd(pruned, (unsigned int)c);
   }
   if (sh.out8 != nullptr) amax_block_store(sh.amax, wmax);
-  tick_if_last(step_out, done);
+  tick_if_last(step_out, done, ps.cursor, ps.cursor_inc);
 }
 
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
@@ -230,7 +266,12 @@ using namespace qd::optim;
 QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const float* skip,
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
                         float grad_scale, float prune_thr, unsigned int* done, uint16_t* shadow, long shadow_lo,
-                        long shadow_hi, uint8_t* shadow8, const float* qs, float* amax, int max_grid, void* stream) {
+                        long shadow_hi, uint8_t* shadow8, const float* qs, float* amax, int max_grid,
+                        const PackScatter* ps_in, void* stream) {
+  const PackScatter ps = ps_in ? *ps_in : PackScatter{};
+  for (int k = 0; k < 3; ++k)
+    if (ps.n[k] && (ps.lo[k] < 0 || ps.lo[k] + ps.n[k] > n || (ps.lo[k] & 3) || (ps.n[k] & 3) || !ps.fwd[k]))
+      return (int)hipErrorInvalidValue;
   if (n <= 0 || done == nullptr || (shadow && ((shadow_lo | shadow_hi) & 3))) return (int)hipErrorInvalidValue;
   if (shadow8 && (!shadow || !qs || !amax)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
@@ -243,9 +284,9 @@ QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const fl
   const bool nt = nt_env >= 0 ? nt_env != 0 : n >= (1L << 20);
   const dim3 grid(grid_for(n, max_grid > 0 ? max_grid : 2048));
   if (nt)
-    hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh);
+    hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh, ps);
   else
-    hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh);
+    hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh, ps);
   return (int)hipGetLastError();
 }
 

@@ -128,6 +128,25 @@ class ConvStackHIP:
         nat.check(self._packm2(len(jobs), w, out, cin, dg, self.E, _ptr(cursor), int(cursor_inc), st),
                   "conv_pack_weights")
 
+    def pack_scatter(self, flat: torch.Tensor, lo: int, hi: int, cursor: Optional[torch.Tensor] = None,
+                     cursor_inc: int = 0):
+        """PackScatter for an optimizer launch over flat[lo:hi]: the update kernel writes the forward
+        (3 layers) and dgrad (layers 2, 3) images of the conv weights it updates -- the same bytes as
+        pack_weights -- and advances ``cursor``.  The images' zero padding comes from pack_weights (init)."""
+        from .optim import PackScatter
+        ps = PackScatter()
+        base = flat.data_ptr()
+        for k in range(3):
+            w = self.m.conv_w[k]
+            o = (w.data_ptr() - base) // 4
+            if lo <= o and o + w.numel() <= hi:
+                ps.lo[k], ps.n[k], ps.cin[k] = o - lo, w.numel(), self.cins[k]
+                ps.fwd[k] = nat.ptr(self.wpk[k])
+                ps.dg[k] = nat.ptr(self.wpk_t[k]) if self.wpk_t[k] is not None else None
+        ps.cursor = nat.ptr(cursor) if cursor is not None else None
+        ps.cursor_inc = int(cursor_inc)
+        return ps
+
     # --------------------------------------------------------------------- forward
     def forward(self, x1: torch.Tensor, training: bool) -> torch.Tensor:
         """x1: (N, E*2, H, W) fp32 contiguous.  Returns the FC operand (N*E, 32*H*W) bf16."""

@@ -27,6 +27,13 @@ _p, _i, _f, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 ALIGN = 16  # elements; keeps every parameter view 64-byte aligned for float4 access
 
 
+class PackScatter(ctypes.Structure):
+    """csrc/hip/optim.hip ``PackScatter``: conv weight images written by the update kernel itself."""
+    _fields_ = [("lo", ctypes.c_long * 3), ("n", ctypes.c_int * 3), ("cin", ctypes.c_int * 3),
+                ("fwd", ctypes.c_void_p * 3), ("dg", ctypes.c_void_p * 3), ("cursor", ctypes.c_void_p),
+                ("cursor_inc", ctypes.c_int)]
+
+
 class FlatParamSpace:
     def __init__(self, params: Sequence[Tuple[str, nn.Parameter]], device=None, extra: int = 0):
         """``extra``: trailing scratch floats (one ALIGN block) after the last parameter; their grad
@@ -204,8 +211,10 @@ class FusedOptimizer:
         self.lr_t.fill_(float(lr))
 
     # ---------------------------------------------------------------- step
-    def step(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None, part: Optional[int] = None) -> None:
-        """One optimizer step over every part (``part=None``) or over part ``part`` only."""
+    def step(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None, part: Optional[int] = None,
+             pack=None) -> None:
+        """One optimizer step over every part (``part=None``) or over part ``part`` only.  ``pack`` (GPU):
+        a callable (lo, hi) -> PackScatter for the range a launch updates (see ConvStackHIP.pack_scatter)."""
         s = self.space
         if not s.flat.is_cuda:
             if part not in (None, 0) and len(self.bounds) > 1:
@@ -218,9 +227,9 @@ class FusedOptimizer:
             return
         parts = range(len(self.bounds)) if part is None else (part,)
         for i in parts:
-            self._step_part(i, grad_scale, skip)
+            self._step_part(i, grad_scale, skip, pack)
 
-    def _step_part(self, i: int, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
+    def _step_part(self, i: int, grad_scale: float, skip: Optional[torch.Tensor], pack=None) -> None:
         s = self.space
         lo, hi = self.bounds[i]
         lib = nat.hip_lib()
@@ -236,7 +245,8 @@ class FusedOptimizer:
                 self.refresh_shadow()
             return
         f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
-                                         _p, _p, _l, _l, _p, _p, _p, _i, _p])
+                                         _p, _p, _l, _l, _p, _p, _p, _i, _p, _p])
+        ps = pack(lo, hi) if pack is not None else None
         # the shadow range, clipped to this part and expressed relative to it
         sh_lo, sh_hi = max(self.shadow_lo, lo), min(self.shadow_hi, hi)
         has_sh = self.shadow is not None and sh_lo < sh_hi
@@ -249,7 +259,8 @@ class FusedOptimizer:
                     self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
                     self.prune_thr, done_p, sh_ptr, (sh_lo - lo) if has_sh else 0, (sh_hi - lo) if has_sh else 0,
                     sh8_ptr, nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
-                    nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, int(self.max_grid.get(i, 0)), st),
+                    nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, int(self.max_grid.get(i, 0)),
+                    ctypes.byref(ps) if ps is not None else None, st),
                   "adam")
 
     @torch.no_grad()

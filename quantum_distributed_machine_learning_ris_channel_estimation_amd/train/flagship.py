@@ -297,6 +297,14 @@ class FlagshipTrainer:
         self.gat.from_cursor(self.store, self.perm, self.cur[k, 0:1], self.cur_done[k, 0:1] if advance else None,
                              hdce=hdce, classifier=classifier)
 
+    def _adam_pack(self):
+        """(tail_pack) the HDCE update writes the conv weight images and advances the batch cursor
+        itself (QDML_ADAM_PACK=0: a separate pack launch after it)."""
+        if not (self.tail_pack and os.environ.get("QDML_ADAM_PACK", "1") != "0"):
+            return None
+        conv, flat, cur = self.hstep.conv, self.hdce.space.flat, self.cur[0, 0:1]
+        return lambda lo, hi: conv.pack_scatter(flat, lo, hi, cursor=cur, cursor_inc=self.B)
+
     def _tail_pack_launch(self, advance: bool = True) -> None:
         """Pack the (just updated) conv weights into the MFMA B-fragment images the next forward reads,
         and advance the batch cursor -- one launch at the end of the step."""
@@ -350,8 +358,9 @@ class FlagshipTrainer:
             if self.hdce_side:
                 self._join(("fc",))
             if len(self.hopt.bounds) == 1:
-                self.hopt.step(grad_scale=1.0, skip=self.hskip)
-                if self.tail_pack:
+                pk = self._adam_pack()
+                self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
+                if self.tail_pack and pk is None:
                     self._tail_pack_launch()
                 return
             self.hopt.step(grad_scale=1.0, skip=self.hskip, part=0)
@@ -404,8 +413,9 @@ class FlagshipTrainer:
 
     def _dp_gr(self) -> None:
         g = 1.0 / self.ctx.world
-        self.hopt.step(grad_scale=g, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None)
-        if self.tail_pack:
+        pk = self._adam_pack()
+        self.hopt.step(grad_scale=g, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None, pack=pk)
+        if self.tail_pack and pk is None:
             self._tail_pack_launch()
         self.qopt.step(grad_scale=g, skip=self.qskip)
 

@@ -105,3 +105,23 @@ def test_deferred_loss_finish_matches_finish_launch(cuda):
         assert torch.equal(a.hloss, b.hloss) and torch.equal(a.skip_flags(), b.skip_flags())
     for x, y in zip(_all_state(a), _all_state(b)):
         assert torch.equal(x, y)
+
+
+def test_update_kernel_writes_the_conv_weight_images(cuda):
+    """The HDCE Adam launch writes the conv weights' forward / dgrad B-fragment images (PackScatter)
+    and advances the batch cursor: the images equal a fresh pack_weights of the updated weights."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    ctx = DistContext(device=cuda)
+    tr = FlagshipTrainer(FlagshipConfig(batch=32, data_len=800, hip_graphs=False), ctx)
+    assert tr._adam_pack() is not None
+    conv = tr.hstep.conv
+    for i in range(3):
+        tr.step()
+    torch.cuda.synchronize()
+    assert int(tr.cur[0, 0]) == 3 * tr.B
+    got = [t.clone() for t in conv.wpk] + [t.clone() for t in conv.wpk_t if t is not None]
+    conv.pack_weights(nat.stream_ptr(cuda))
+    torch.cuda.synchronize()
+    ref = list(conv.wpk) + [t for t in conv.wpk_t if t is not None]
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
