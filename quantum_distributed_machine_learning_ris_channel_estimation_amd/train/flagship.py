@@ -14,10 +14,11 @@ Almost every kernel of this model is latency-bound and fills a fraction of the 2
 QSC branch overlaps the HDCE chain.  (``dagi`` -- the two chains independent for the whole replay
 -- was ~1.5% faster but not bit-reproducible; see ``__init__``.)  Per step:
 
-  main : gather -> conv fwd x3 -> BN tail -> BN/ReLU apply -> FC fwd GEMM -> one-pass NMSE ->
-         loss finish -> FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce -> [wgrad|dgrad] L3 ->
+  main : gather -> conv fwd x3 -> BN/ReLU apply (+ BN tail) -> FC fwd GEMM -> one-pass NMSE ->
+         FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce (+ loss finish) -> [wgrad|dgrad] L3 ->
          [wgrad|dgrad] L2 -> wgrad L1 -> slab sums (conv, BN, FC bias) -> Adam (one launch over all
-         HDCE parameters, writes the bf16 FC shadow) -> conv weight pack for the NEXT step (+ cursor)
+         HDCE parameters; also writes the bf16 FC shadow and the conv weights' MFMA B-fragment images
+         for the NEXT step, and advances the batch cursor)
   qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
          QSC bwd -> slabs -> AdamW
 
