@@ -246,17 +246,22 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
   // ---- one-sample-ahead register prefetch of the raw input (converted at use, one sample later).
   // Where a whole sample does not fit the register budget (P256 dgrad), groups of GR items are
   // loaded and staged synchronously instead (batched: GR loads in flight per round trip). ----
-  constexpr int CH8 = CIN * G::HW / 8;                  // 8-value staging items per sample
-  constexpr int ITER = RAWIN ? (CIN * G::HW) / 64 : CH8 / 64;
-  static_assert(RAWIN ? (CIN * G::HW) % 64 == 0 : CH8 % 64 == 0, "whole waves per staging pass");
-  constexpr int QV = RAWIN ? 1 : (int)sizeof(TIN) / 2;  // uint4s per 8-value item (bf16: 1, f32: 2)
-  constexpr int HOLD = ITER * (QV + (INM == IN_BNBWD ? 1 : 0));   // 16-byte registers per sample
+  // staging item (non-raw input): 8 consecutive positions of a channel PAIR (c, c+1), so the
+  // channel-last LDS tile is written as bf16x2 words -- 16 lanes of a pass write 16 consecutive
+  // words of one pixel (a single-channel item wrote 2-byte values 640 bytes apart: 4-8-way bank
+  // conflicts, profiles/r1_19_pmc.md)
+  constexpr int CH8 = CIN * G::HW / 8;                  // 8-value (single channel) units per sample
+  constexpr int NPAIR = CIN / 2;
+  constexpr int ITER = RAWIN ? (CIN * G::HW) / 64 : CH8 / 128;
+  static_assert(RAWIN ? (CIN * G::HW) % 64 == 0 : CH8 % 128 == 0, "whole waves per staging pass");
+  constexpr int QV = RAWIN ? 1 : (int)sizeof(TIN) / 2;  // uint4s per 8-value unit (bf16: 1, f32: 2)
+  constexpr int HOLD = ITER * (2 * QV + (INM == IN_BNBWD ? 2 : 0));   // 16-byte registers per sample
   // (dgrad: registers go to the fused BN-reduction operands; P256: to the MFMA pipeline)
   constexpr bool PREF = RAWIN || (!DGRAD && HOLD <= 16 && G::HW <= 128);
   constexpr int GR = PREF ? ITER : (INM == IN_BNBWD ? 2 : 4);
   static_assert(ITER % GR == 0, "staging groups");
-  [[maybe_unused]] uint4 rv[RAWIN ? 1 : GR][QV];
-  [[maybe_unused]] uint4 rz[INM == IN_BNBWD ? GR : 1];
+  [[maybe_unused]] uint4 rv[RAWIN ? 1 : GR][2][QV];
+  [[maybe_unused]] uint4 rz[INM == IN_BNBWD ? GR : 1][2];
   [[maybe_unused]] float rr[RAWIN ? GR : 1];
   auto load_group = [&](int n, int g0) {
     const size_t base = ((size_t)n * E + e) * CIN * G::HW;
@@ -266,11 +271,16 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
       if constexpr (RAWIN) {
         rr[k] = ldf<TIN>(xin, base + lane + 64 * it);
       } else {
-        const size_t off = base + (size_t)(lane + 64 * it) * 8;   // item i = elements [8i, 8i+8)
-        const uint4* src = reinterpret_cast<const uint4*>(xin + off);
+        // item i: channel pair i % NPAIR, positions [8 (i / NPAIR), +8)
+        const int i = lane + 64 * it, pr = i % NPAIR, sg = i / NPAIR;
 #pragma unroll
-        for (int q = 0; q < QV; ++q) rv[k][q] = src[q];
-        if constexpr (INM == IN_BNBWD) rz[k] = *reinterpret_cast<const uint4*>(zaux + off);
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const size_t off = base + (size_t)(2 * pr + h2) * G::HW + 8 * sg;
+          const uint4* src = reinterpret_cast<const uint4*>(xin + off);
+#pragma unroll
+          for (int q = 0; q < QV; ++q) rv[k][h2][q] = src[q];
+          if constexpr (INM == IN_BNBWD) rz[k][h2] = *reinterpret_cast<const uint4*>(zaux + off);
+        }
       }
     }
   };
@@ -283,29 +293,36 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
         const int c = i / G::HW, p = i % G::HW;
         tile[((p / W + 1) * G::WP + (p % W) + 1) * CINP + c] = (__bf16)rr[k];
       } else {
-        const int c = i / (G::HW / 8), p0 = (i % (G::HW / 8)) * 8;
-        const float* sc = stl + c * NST;
-        float v[8];
+        const int pr = i % NPAIR, p0 = (i / NPAIR) * 8;
+        float v2[2][8];
 #pragma unroll
-        for (int q = 0; q < QV; ++q) unpack_q(rv[k][q], v + q * (8 / QV), (const TIN*)nullptr);
-        if constexpr (INM == IN_BNRELU) {
-          const float a = sc[ST_A], b = sc[ST_B];
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const float* sc = stl + (2 * pr + h2) * NST;
+          float* v = v2[h2];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = relu_nan(a * v[j] + b);
-        } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
-          float z[8];
-          unpack_q(rz[k], z, (const uint16_t*)nullptr);
-          const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
-          const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+          for (int q = 0; q < QV; ++q) unpack_q(rv[k][h2][q], v + q * (8 / QV), (const TIN*)nullptr);
+          if constexpr (INM == IN_BNRELU) {
+            const float a = sc[ST_A], b = sc[ST_B];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float g = (a * z[j] + b > 0.f) ? v[j] : 0.f;
-            v[j] = c1 * g - c2 - c3 * (z[j] - mu) * inv;
+            for (int j = 0; j < 8; ++j) v[j] = relu_nan(a * v[j] + b);
+          } else {  // IN_BNBWD: v = dh; dz = c1*g - c2 - c3*xhat, g = dh * [a z + b > 0]
+            float z[8];
+            unpack_q(rz[k][h2], z, (const uint16_t*)nullptr);
+            const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+            const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float g = (a * z[j] + b > 0.f) ? v[j] : 0.f;
+              v[j] = c1 * g - c2 - c3 * (z[j] - mu) * inv;
+            }
           }
         }
         const int ph = p0 / W, pw = p0 % W;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) tile[((ph + 1) * G::WP + pw + j + 1) * CINP + c] = (__bf16)v[j];
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t w2 = f32_to_bf16(v2[0][j]) | ((uint32_t)f32_to_bf16(v2[1][j]) << 16);
+          *reinterpret_cast<uint32_t*>(tile + ((ph + 1) * G::WP + pw + j + 1) * CINP + 2 * pr) = w2;
+        }
       }
     }
   };
