@@ -37,7 +37,7 @@ for s in $STEPS; do
     convknobs) for k in ${KNOBS:-2,8,4,4 1,8,4,4 4,8,4,4 2,16,4,4 2,4,4,4 2,8,2,4 2,8,8,4 2,8,4,2 2,8,4,8}; do QDML_CONV_KNOBS=$k run bench_conv_${k//,/_} 300 python bench.py --steps 50 --warmup 10; done ;;
     savestate) for v in 1 0 1 0; do QDML_QSIM_SAVE_STATE=$v run bench_save_$v 300 python bench.py --steps 100 --warmup 10; done ;;
     envsweep) for e in ${ENVS:-NONE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 DEBUG_HIP_GRAPH_BATCH_SIZE=1 DEBUG_HIP_GRAPH_BATCH_SIZE=64 DEBUG_HIP_FORCE_GRAPH_QUEUES=1 DEBUG_HIP_FORCE_GRAPH_QUEUES=2}; do
-        for v in "" "--qsc-late-capture"; do env $e timeout -k 10 300 python bench.py --steps 100 --warmup 10 $v > $OUT/env_${e}${v// /_}.log 2>&1 || exit 1; echo "$e $v $(grep -o '"ms_per_step": [0-9.]*' $OUT/env_${e}${v// /_}.log)" | tee -a $OUT/envsweep.txt; done; done ;;
+        for v in "" "--stream-mode dagi"; do env $e timeout -k 10 300 python bench.py --steps 100 --warmup 10 $v > $OUT/env_${e}${v// /_}.log 2>&1 || exit 1; echo "$e $v $(grep -o '"ms_per_step": [0-9.]*' $OUT/env_${e}${v// /_}.log)" | tee -a $OUT/envsweep.txt; done; done ;;
     dagi) for v in dagq dagi dagq dagi; do run bench_mode_${v}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --stream-mode $v; done ;;
     dagicmp) for r in 1 2 3; do for o in dagq dagi; do m=$o; timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode $m > $OUT/cmp.log 2>&1 || exit 1; echo "$o $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/dagicmp.txt; done; done ;;
     qscgrid) for r in 1 2; do for g in 256 128 64 576; do QDML_QSC_GRID_BWD=$g timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode ${MODE:-dagq} > $OUT/cmp.log 2>&1 || exit 1; echo "$g $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/qscgrid.txt; done; done ;;
