@@ -83,6 +83,7 @@ def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     hdrs = _headers("hip")
     flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
              "-Wno-unused-result", "-I", os.path.join(CSRC, "hip")]
+    flags += os.environ.get("QDML_HIPCC_EXTRA", "").split()   # (tuning sweeps: e.g. -DQD_CINP_PAD=16)
     objs = []
 
     def one(src: str) -> str:

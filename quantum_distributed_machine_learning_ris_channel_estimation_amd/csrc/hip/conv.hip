@@ -33,6 +33,10 @@
 
 #include "common.h"
 
+#ifndef QD_CINP_PAD
+#define QD_CINP_PAD 8   // bf16 padding of the channel-last conv tile pixels (multiple of 8: 16-byte reads)
+#endif
+
 namespace qd {
 namespace conv {
 
@@ -214,7 +218,7 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
   unsigned long long ts[8] = {};
   if constexpr (STAMP) ts[0] = phase_stamp();
   using G = Geo<H, W>;
-  constexpr int CINP = (CIN % 16 == 0) ? CIN + 8 : CIN;  // channel-last pixel stride (bf16)
+  constexpr int CINP = (CIN % 16 == 0) ? CIN + QD_CINP_PAD : CIN;  // channel-last pixel stride (bf16)
   constexpr int KS = (9 * CIN + 15) / 16;                   // 16-deep k steps
   constexpr int TILE = G::HP * G::WP * CINP;                // bf16 elements per wave tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1192,7 +1196,7 @@ using namespace qd::conv;
   else return (int)hipErrorInvalidValue;
 
 static size_t fwd_smem(int cin, int H, int W) {
-  const int cinp = (cin % 16 == 0) ? cin + 8 : cin;
+  const int cinp = (cin % 16 == 0) ? cin + QD_CINP_PAD : cin;
   const int ks = (9 * cin + 15) / 16;   // (dgrad: cin = 32 -> 18 = the dgrad pack's k-steps too)
   // 4 wave tiles | B fragments | BN params
   return 4 * (size_t)(H + 2) * (W + 2) * cinp * 2 + (size_t)ks * 64 * 16 + (size_t)cin * NST * sizeof(float);
