@@ -15,6 +15,13 @@ synthetic DeepMIMO-shaped data resident in HBM, random-init weights.
 W untimed warm-up steps, then K timed steps bracketed by barrier + device sync; the
 slowest rank's time is used; rank 0 prints ONE JSON line with the whole-job value.
 The reference publishes no throughput, so vs_baseline is null.
+
+``python bench.py --gpus N`` (N > 1) without a torchrun environment starts the N ranks itself
+(one child process per GPU through parallel/launch.py, BEFORE this process imports torch or
+touches a GPU), relays rank 0's JSON line on stdout and exits non-zero if any rank fails.  Under
+torchrun, WORLD_SIZE must equal --gpus (a mismatch is an error, never a silent 1-rank run).
+At N > 1 the JSON line also carries ``phases_ms``: per-phase HIP-event times of the DP step
+(max over ranks), measured on extra steps AFTER the timed region.
 """
 from __future__ import annotations
 
@@ -49,29 +56,39 @@ def main() -> int:
                          "its forward half beside the HDCE forward and its backward half beside the conv backward (3)")
     ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
     ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
+    ap.add_argument("--dp-plan", default="zero", choices=["zero", "allreduce"],
+                    help="world > 1: ZeRO-1 FC optimizer (reduce-scatter / shard Adam / all-gather) or all-reduce")
+    ap.add_argument("--phase-steps", type=int, default=20,
+                    help="N > 1: extra steps (after the timed region) timed per phase with HIP events; 0 = off")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
     ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "dagi", "qsc", "full"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
                          "or a separate QSC graph on its own stream (+ HDCE side branches with 'full')")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return self_launch(args.gpus)
+    world_env = int(os.environ.get("WORLD_SIZE", 1))
+    if world_env != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        return 2
+
     import torch
-    import torch.distributed as dist
 
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import init_distributed, shutdown
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
                                                                                                 FlagshipTrainer)
 
-    world_env = int(os.environ.get("WORLD_SIZE", 1))
-    if world_env != args.gpus and world_env != 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
     ctx = init_distributed("auto")
+    if ctx.world != args.gpus:
+        print(f"error: --gpus {args.gpus} but the process group has {ctx.world} rank(s)", file=sys.stderr)
+        return 2
     cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
                          hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
                          split_graphs=args.split_graphs, stream_mode=args.stream_mode,
                          qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
                          hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
-                         fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase,
+                         fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase, dp_plan=args.dp_plan,
                          stream_priority=args.stream_priority)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
@@ -95,6 +112,10 @@ def main() -> int:
     n = ctx.world
     samples = tr.samples_per_step * n * args.steps
     value = samples / elapsed
+    phases = tr.phase_times(args.phase_steps) if args.phase_steps > 0 and len(tr.graphs) == 4 else None
+    if phases is not None:
+        keys = sorted(phases)
+        phases = dict(zip(keys, (round(v, 4) for v in ctx.max_vector([phases[k] for k in keys]))))
     if ctx.is_main:
         rec = {
             "metric": "NMSE(dB) vs SNR + samples/sec, P128 RIS estimator at 1/2/4/8 MI355X"
@@ -127,15 +148,36 @@ def main() -> int:
                 "qsc_fork": args.qsc_fork,
                 "fc_adam_grid": args.fc_adam_grid,
                 "dp_qsc_phase": args.dp_qsc_phase,
+                "dp_plan": ("zero" if tr.zero else "allreduce") if len(tr.graphs) == 4 else None,
+                "dist_backend": ctx.backend,
                 "stream_priority": args.stream_priority,
                 "steps_per_graph": args.steps_per_graph if n == 1 else 1,
                 "quantumnat": cfg.use_quantumnat,
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
         }
+        if phases is not None:
+            rec["phases_ms"] = phases
         print(json.dumps(rec), flush=True)
     shutdown()
     return 0
+
+
+def self_launch(n: int) -> int:
+    """Start ``n`` ranks of this same command (torchrun environment contract) and wait for them.
+    Only the standard library is imported here: no torch, no GPU, before the children exist."""
+    import importlib.util
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    path = os.path.join(here, "quantum_distributed_machine_learning_ris_channel_estimation_amd", "parallel", "launch.py")
+    spec = importlib.util.spec_from_file_location("_qdml_launch", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    rc = mod.launch([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], nproc=n,
+                    extra_env={"QDML_SELF_LAUNCHED": "1"})
+    if rc != 0:
+        print(f"error: a rank of the {n}-rank bench failed (exit {rc})", file=sys.stderr)
+    return rc
 
 
 if __name__ == "__main__":

@@ -16,6 +16,7 @@ datasets below exist for API compatibility and tests.
 from __future__ import annotations
 
 import os
+import warnings
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -74,11 +75,15 @@ def generate_datapair(Ns: int, Pilot_num: int = 128, index: int = -1, SNRdb: flo
     return Yp.cpu().numpy(), HLS.cpu().numpy(), H.cpu().numpy(), ind.cpu().numpy()
 
 
+def stream_paths(data_dir: str, scenario: int, user: int, pilot_num: int, snr_db: int, data_len: int) -> List[str]:
+    return [os.path.join(data_dir, npy_name(k, scenario, pilot_num, snr_db, user, data_len))
+            for k in ("Yp", "Hlabel", "Hperf")]
+
+
 def load_or_generate_stream(data_dir: str, scenario: int, user: int, pilot_num: int, snr_db: int, data_len: int,
                             synthetic: bool = True, base_seed: int = 0, device="cpu"):
     """Reference .npy file pattern when present, else the synthetic generator."""
-    paths = [os.path.join(data_dir, npy_name(k, scenario, pilot_num, snr_db, user, data_len))
-             for k in ("Yp", "Hlabel", "Hperf")]
+    paths = stream_paths(data_dir, scenario, user, pilot_num, snr_db, data_len)
     if all(os.path.exists(p) for p in paths):
         Yp, HL, HP = (torch.from_numpy(np.load(p)).to(device) for p in paths)  # allow_pickle=False (default)
         n = min(len(Yp), data_len)
@@ -127,10 +132,16 @@ class DMLStore:
                         self.Hperf.to(device, ld) if ld else self.Hperf.to(device),
                         self.scen.to(device), self.user.to(device))
 
-    def shard(self, rank: int, world: int) -> "DMLStore":
-        """Contiguous per-rank shard of the sample axis (distributed DML sampler)."""
-        per = self.n // world
-        s = slice(rank * per, (rank + 1) * per)
+    def shard(self, rank: int, world: int, drop_remainder: bool = True) -> "DMLStore":
+        """Contiguous per-rank shard of the sample axis (distributed DML sampler).  Training shards are
+        equal (``drop_remainder``: every rank runs the same number of lock-step batches); validation
+        shards (``drop_remainder=False``) cover every sample, the first ``n % world`` ranks one more."""
+        per, rem = divmod(self.n, world)
+        if drop_remainder:
+            s = slice(rank * per, (rank + 1) * per)
+        else:
+            lo = rank * per + min(rank, rem)
+            s = slice(lo, lo + per + (rank < rem))
         return DMLStore(self.Yp[:, s], self.Hlabel[:, s], self.Hperf[:, s], self.scen, self.user)
 
     def gather(self, idx: torch.Tensor):
@@ -149,7 +160,25 @@ def build_store(streams: List, scen_ids: List[int], user_ids: List[int], pilot_n
 def make_dml_stores(data_len: int, pilot_num: int, snr_db: int, ratio: float, device, data_dir: str = "available_data",
                     synthetic: bool = True, base_seed: int = 0, n_scenarios: int = 3, n_users: int = 3,
                     label_dtype=torch.float32) -> Tuple[DMLStore, DMLStore]:
-    """Train / val stores for all (scenario, user) streams in reference order (R:76-84)."""
+    """Train / val stores for all (scenario, user) streams in reference order (R:76-84).
+
+    Real data (the reference's 27 .npy files under ``data_dir``) is all-or-nothing: some streams on
+    disk and others missing is an error (never a silent real/synthetic mix), and falling back to the
+    synthetic generator is announced with a warning unless ``data_dir`` is None (synthetic by intent)."""
+    if data_dir is not None:
+        have = [all(os.path.exists(p) for p in stream_paths(data_dir, s, u, pilot_num, snr_db, data_len))
+                for s in range(n_scenarios) for u in range(n_users)]
+        if any(have) and not all(have):
+            missing = [i for i, h in enumerate(have) if not h]
+            raise FileNotFoundError(f"{data_dir}: data files for streams {missing} (scenario*{n_users}+user) are "
+                                    f"missing while the others exist; refusing to mix real and synthetic data")
+        if not any(have):
+            if not synthetic:
+                raise FileNotFoundError(stream_paths(data_dir, 0, 0, pilot_num, snr_db, data_len)[0])
+            warnings.warn(f"no reference data files under {data_dir!r}: using the synthetic DeepMIMO-shaped "
+                          "generator for all streams", stacklevel=2)
+    else:
+        data_dir = ""
     tr, va, sids, uids = [], [], [], []
     for s in range(n_scenarios):
         for u in range(n_users):

@@ -216,16 +216,13 @@ class FusedOptimizer:
         """One optimizer step over every part (``part=None``) or over part ``part`` only.  ``pack`` (GPU):
         a callable (lo, hi) -> PackScatter for the range a launch updates (see ConvStackHIP.pack_scatter)."""
         s = self.space
+        parts = range(len(self.bounds)) if part is None else (part,)
         if not s.flat.is_cuda:
-            if part not in (None, 0) and len(self.bounds) > 1:
-                # the CPU path steps the whole space at once: only the last part triggers it
-                if part != len(self.bounds) - 1:
-                    return
-            self._step_host(grad_scale, skip)
+            for i in parts:
+                self._step_host(i, grad_scale, skip)
             if self.shadow is not None:
                 self.refresh_shadow()
             return
-        parts = range(len(self.bounds)) if part is None else (part,)
         for i in parts:
             self._step_part(i, grad_scale, skip, pack)
 
@@ -264,12 +261,13 @@ class FusedOptimizer:
                   "adam")
 
     @torch.no_grad()
-    def _step_host(self, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
-        """CPU path (same math as optim.hip; the CPU has no HIP kernels)."""
+    def _step_host(self, i: int, grad_scale: float, skip: Optional[torch.Tensor]) -> None:
+        """CPU path for part ``i`` (same math as optim.hip; the CPU has no HIP kernels)."""
         if skip is not None and float(skip.item()) != 0.0:
             return
         s = self.space
-        p, g = s.flat, s.grad
+        lo, hi = self.bounds[i]
+        p, g = s.flat[lo:hi], s.grad[lo:hi]
         if grad_scale != 1.0:
             g.mul_(grad_scale)
         if self.prune_thr > 0:
@@ -278,25 +276,27 @@ class FusedOptimizer:
             g.mul_(mask)
         lr = float(self.lr_t.item())
         if self.kind == "sgd":
+            buf = self.buf[lo:hi]
             d = g + self.weight_decay * p if self.weight_decay else g
-            if self.step_t[0].item() == 0:
-                self.buf.copy_(d)
+            if self.step_t[i].item() == 0:
+                buf.copy_(d)
             else:
-                self.buf.mul_(self.momentum).add_(d)
-            p.sub_(lr * self.buf)
+                buf.mul_(self.momentum).add_(d)
+            p.sub_(lr * buf)
         else:
-            t = float(self.step_t[0].item()) + 1.0
+            m, v = self.m[lo:hi], self.v[lo:hi]
+            t = float(self.step_t[i].item()) + 1.0
             b1, b2 = self.betas
             if self.kind == "adamw":
                 p.mul_(1 - lr * self.weight_decay)
                 d = g
             else:
                 d = g + self.weight_decay * p if self.weight_decay else g
-            self.m.mul_(b1).add_(d, alpha=1 - b1)
-            self.v.mul_(b2).addcmul_(d, d, value=1 - b2)
-            denom = (self.v.sqrt() / (1 - b2 ** t) ** 0.5).add_(self.eps)
-            p.addcdiv_(self.m, denom, value=-lr / (1 - b1 ** t))
-        self.step_t += 1
+            m.mul_(b1).add_(d, alpha=1 - b1)
+            v.mul_(b2).addcmul_(d, d, value=1 - b2)
+            denom = (v.sqrt() / (1 - b2 ** t) ** 0.5).add_(self.eps)
+            p.addcdiv_(m, denom, value=-lr / (1 - b1 ** t))
+        self.step_t[i] += 1
 
     def zero_grad(self) -> None:
         self.space.zero_grad()

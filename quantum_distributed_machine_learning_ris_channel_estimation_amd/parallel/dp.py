@@ -68,11 +68,15 @@ class DistContext:
         return t
 
     def max_scalar(self, v: float) -> float:
+        return self.max_vector([v])[0]
+
+    def max_vector(self, vs: Sequence[float]) -> List[float]:
+        """Element-wise max over ranks of a short host vector (one collective)."""
         if not self.distributed:
-            return v
-        t = torch.tensor([v], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+            return [float(v) for v in vs]
+        t = torch.tensor(list(vs), dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return [float(x) for x in t.tolist()]
 
 
 _CTX: Optional[DistContext] = None
@@ -97,6 +101,9 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
     backend = "none"
     if world > 1:
         backend = os.environ.get("QDML_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
+        if backend == "nccl" and world > torch.cuda.device_count():
+            raise RuntimeError(f"RCCL needs one GPU per rank: WORLD_SIZE={world} but {torch.cuda.device_count()} "
+                               "visible GPU(s) (QDML_DIST_BACKEND=gloo rehearses several ranks per GPU)")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {}
         if backend == "nccl":
@@ -156,6 +163,35 @@ class GradBuckets:
     def launch_all(self) -> None:
         for k in self.buckets:
             self.launch(k)
+
+    # -- sharded (ZeRO-1 style) collectives: one flat region split into `world` equal shards ----
+    def _shard_staging(self, key: str, full: torch.Tensor) -> torch.Tensor:
+        w = self.ctx.world
+        if full.numel() % w:
+            raise ValueError(f"sharded region of {full.numel()} elements not divisible by world {w}")
+        st = self.staging.get(key)
+        if st is None or st.numel() * w != full.numel() or st.dtype != full.dtype:
+            st = self.staging[key] = torch.empty(full.numel() // w, device=full.device, dtype=full.dtype)
+        return st
+
+    def launch_reduce_scatter(self, name: str, full: torch.Tensor) -> None:
+        """Sum ``full`` over ranks keeping only this rank's shard ``full.view(world, -1)[rank]`` (the
+        other shards are left as they were).  The collective writes a shard-sized staging buffer that
+        ``wait`` copies back into the shard (out of place: no reliance on in-place aliasing rules)."""
+        if not self.ctx.distributed:
+            return
+        st = self._shard_staging("rs:" + name, full)
+        work = dist.reduce_scatter_tensor(st, full, async_op=True)
+        self.pending[name] = [work, st, [full.view(self.ctx.world, -1)[self.ctx.rank]]]
+
+    def launch_all_gather(self, name: str, full: torch.Tensor) -> None:
+        """Every rank's shard of ``full`` to every rank (the inverse of the reduce-scatter layout).
+        This rank's shard is staged first, so the collective never reads the buffer it writes."""
+        if not self.ctx.distributed:
+            return
+        st = self._shard_staging("ag:" + name, full)
+        st.copy_(full.view(self.ctx.world, -1)[self.ctx.rank])
+        self.pending[name] = [dist.all_gather_into_tensor(full, st, async_op=True), None, None]
 
     def wait(self, names: Optional[Sequence[str]] = None) -> None:
         """Make the CURRENT stream wait for the named (default: all) launched collectives; a coalesced

@@ -38,7 +38,7 @@ import torch.nn.functional as F
 from .. import _native as nat
 from ..models.estimators import Conv_P128, FC_P128, QSC_P128, SC_P128, pilot_grid
 from ..ops.nmse import StreamNMSE
-from ..ops.optim import FlatParamSpace
+from ..ops.optim import ALIGN, FlatParamSpace
 
 CONV_PARAM_ORDER = ["cnn.0.weight", "cnn.1.weight", "cnn.1.bias", "cnn.3.weight", "cnn.4.weight", "cnn.4.bias",
                     "cnn.6.weight", "cnn.7.weight", "cnn.7.bias"]
@@ -57,7 +57,9 @@ class HDCEModel:
     views into the flat buffer), so ``Conv0.state_dict()`` etc. remain reference-compatible."""
 
     def __init__(self, pilot_num: int = 128, device="cpu", dtype: str = "bf16", n_experts: int = 3,
-                 grad_extra: int = 0):
+                 grad_extra: int = 0, fc_pad_multiple: int = 1):
+        """``fc_pad_multiple``: pad the flat space after the FC parameters so that the FC region
+        [FC.weight offset, end) has a multiple of this many elements (ZeRO-1 sharding over ranks)."""
         self.device = torch.device(device)
         self.E = n_experts
         self.H, self.W = pilot_grid(pilot_num)
@@ -77,6 +79,10 @@ class HDCEModel:
             for e, m in enumerate(self.convs):
                 named.append((f"Conv{e}.{pname}", m.get_parameter(pname)))
         named += [("CE.FC.weight", self.fc.FC.weight), ("CE.FC.bias", self.fc.FC.bias)]
+        if fc_pad_multiple > 1:
+            al = lambda n: (n + ALIGN - 1) // ALIGN * ALIGN
+            fc_len = al(self.fc.FC.weight.numel()) + al(self.fc.FC.bias.numel()) + al(grad_extra)
+            grad_extra += (-fc_len) % (fc_pad_multiple * ALIGN)   # (every shard ALIGN-aligned)
         self.space = FlatParamSpace(named, self.device, extra=grad_extra)
         # grouped leaf views over the expert-consecutive parameter blocks
         self.conv_w, self.bn_w, self.bn_b = [], [], []
@@ -104,14 +110,16 @@ class HDCEModel:
         self.momentum, self.eps = 0.1, 1e-5
         self.fc_shadow: Optional[torch.Tensor] = None  # bf16 FC weight+bias kept fresh by the optimizer
 
-    def attach_fc_shadow(self, opt) -> None:
-        """Let ``opt`` maintain a bf16 copy of the FC weight and bias (GPU, bf16 compute only)."""
+    def attach_fc_shadow(self, opt, to_end: bool = False) -> None:
+        """Let ``opt`` maintain a bf16 copy of the FC weight and bias (GPU, bf16 compute only);
+        ``to_end``: the shadow spans the whole FC region up to the end of the flat space (sharded)."""
         if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16:
             return
         lo = self.space.offsets[self.space.names.index("CE.FC.weight")]
         ob = self.space.offsets[self.space.names.index("CE.FC.bias")]
         hi = ob + self.fc_b.numel()
-        sh = opt.attach_shadow(lo, hi + (-hi) % 4, fp8=self.fp8_scales, fp8_slot=1)
+        hi = self.space.numel if to_end else hi + (-hi) % 4
+        sh = opt.attach_shadow(lo, hi, fp8=self.fp8_scales, fp8_slot=1)
         self.fc_shadow = sh
         self._shadow_w = sh[:self.fc_w.numel()].view(self.fc_w.shape)
         self._shadow_b = sh[ob - lo:ob - lo + self.fc_b.numel()]

@@ -98,6 +98,9 @@ class FlagshipConfig:
     #                              2 is kept: it leaves the most work (QSC + conv backward) behind the 33.6 MB
     #                              FC all-reduce, which at 2-8 ranks over xGMI is expected to take 0.2-0.4 ms
     fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
+    dp_plan: str = "zero"        # world > 1: "zero" = ZeRO-1 FC optimizer (reduce-scatter the FC gradient,
+    #                              Adam on this rank's 1/world shard, all-gather the bf16 weight shadow) or
+    #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
     qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
     qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
@@ -112,17 +115,25 @@ class FlagshipTrainer:
         self.cfg, self.ctx = cfg, ctx
         dev = ctx.device
         self.tuned_gemms = dev.type == "cuda" and cfg.tunableop and use_tuned_gemms()
-        self.store, _ = make_dml_stores(cfg.data_len, cfg.pilot_num, cfg.snr_db, 0.9, dev, synthetic=True,
+        self.store, _ = make_dml_stores(cfg.data_len, cfg.pilot_num, cfg.snr_db, 0.9, dev, data_dir=None, synthetic=True,
                                         base_seed=cfg.seed + 1000 * ctx.rank, n_scenarios=cfg.n_scenarios,
                                         n_users=cfg.n_users)
         self.E, self.U, self.B = cfg.n_scenarios, cfg.n_users, cfg.batch
         self.S = self.E * self.U
         # --- models (weights broadcast from rank 0 once; then resident)
         torch.manual_seed(cfg.seed)
-        # DP: the HDCE NaN flag lives in a scratch slot right after the FC gradient, so it travels in
-        # the FC all-reduce (one collective less ahead of it)
-        self.flag_in_fc = ctx.world > 1 or cfg.split_graphs
-        self.hdce = HDCEModel(cfg.pilot_num, dev, cfg.dtype, cfg.n_scenarios, grad_extra=1 if self.flag_in_fc else 0)
+        dp = ctx.world > 1 or cfg.split_graphs
+        if cfg.dp_plan not in ("zero", "allreduce"):
+            raise ValueError(f"dp_plan {cfg.dp_plan!r}")
+        # ZeRO-1 plan (see _dp_run); not with the fp8 estimator (its weight scale is a max over the
+        # whole FC weight, which a sharded update would have to all-reduce)
+        self.zero = dp and cfg.dp_plan == "zero" and cfg.dtype != "fp8"
+        # all-reduce plan: the HDCE NaN flag lives in a scratch slot right after the FC gradient, so it
+        # travels in the FC all-reduce (one collective less ahead of it); ZeRO plan: in the small bucket
+        # (every rank needs the summed flag, a reduce-scatter leaves it on one rank only)
+        self.flag_in_fc = dp and not self.zero
+        self.hdce = HDCEModel(cfg.pilot_num, dev, cfg.dtype, cfg.n_scenarios, grad_extra=1 if self.flag_in_fc else 0,
+                              fc_pad_multiple=ctx.world if self.zero else 1)
         self.qsc = QSC_P128(cfg.n_qubits, cfg.n_layers, cfg.n_classes, cfg.use_quantumnat,
                             cfg.use_gradient_pruning, cfg.pilot_num).to(dev)
         self.qspace = FlatParamSpace(list(self.qsc.named_parameters()), dev)
@@ -133,12 +144,17 @@ class FlagshipTrainer:
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
         # part 0: conv + BN params, part 1: FC -- for the plans that step them apart (the DP plan, the FC
         # Adam side branch); the world-1 chain steps the whole space in ONE launch
-        if (ctx.world > 1 or cfg.split_graphs or cfg.stream_mode in ("dag", "qsc", "full")
-                or "a" in cfg.hdce_branches):
+        # ZeRO: parts 1..world = the FC region [n_conv, end) in equal shards; this rank steps 1 + rank
+        self.fc_region = (n_conv, sp.numel)
+        self.shard_len = (sp.numel - n_conv) // ctx.world
+        if self.zero:
+            self.hopt.partition([n_conv + i * self.shard_len for i in range(ctx.world)])
+        elif (dp or cfg.stream_mode in ("dag", "qsc", "full") or "a" in cfg.hdce_branches):
             self.hopt.partition([n_conv])
         if cfg.fc_adam_grid:
-            self.hopt.max_grid[1] = cfg.fc_adam_grid
-        self.hdce.attach_fc_shadow(self.hopt)   # after the broadcast: the shadow starts in sync
+            self.hopt.max_grid[1 + (ctx.rank if self.zero else 0)] = cfg.fc_adam_grid
+        # after the broadcast: the shadow starts in sync
+        self.hdce.attach_fc_shadow(self.hopt, to_end=self.zero)
         self.qopt = make_optimizer(self.qspace, "adamw", cfg.lr, weight_decay=cfg.qsc_weight_decay,
                                    prune_thr=0.1 if cfg.use_gradient_pruning else 0.0)
         self.hstep = HDCEStep(self.hdce, self.U, self.B)
@@ -161,7 +177,9 @@ class FlagshipTrainer:
         # else that flag is its own "skip" bucket), "small"
         # = conv/BN + QSC grads + the QSC NaN flag (coalesced)
         bk = {"fc": [sp.grad[n_conv:]], "small": [sp.grad[:n_conv], self.qspace.grad, self.qskip]}
-        if not self.flag_in_fc:
+        if self.zero:
+            bk = {"small": bk["small"] + [self.hskip]}
+        elif not self.flag_in_fc:
             bk["skip"] = [self.skip[0, 0:1]]
         self.buckets = GradBuckets(ctx, bk)
         self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)
@@ -236,6 +254,7 @@ class FlagshipTrainer:
             self.hstep.conv.pack_at_tail = True
             self._tail_pack_launch(advance=False)   # the first step's images
         self._use_graphs = graphs
+        self._phases = None   # (phase_times) per-step dicts of HIP events
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
 
@@ -409,7 +428,9 @@ class FlagshipTrainer:
             self._qsc_branch(with_opt=False)
 
     def _dp_gf(self) -> None:
-        if len(self.hopt.bounds) > 1:   # (unpartitioned -- serial world 1 -- gr steps everything)
+        if self.zero:   # this rank's shard of the FC region only
+            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.hskip, part=1 + self.ctx.rank)
+        elif len(self.hopt.bounds) > 1:   # (unpartitioned -- serial world 1 -- gr steps everything)
             self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.hskip, part=1)
 
     def _dp_gr(self) -> None:
@@ -420,28 +441,108 @@ class FlagshipTrainer:
             self._tail_pack_launch()
         self.qopt.step(grad_scale=g, skip=self.qskip)
 
+    def _fc_weights_lp(self) -> torch.Tensor:
+        """(ZeRO) the FC region's copy the forward / data gradient read: the bf16 shadow (GPU bf16),
+        else the fp32 master weights themselves."""
+        lo, hi = self.fc_region
+        return self.hdce.fc_shadow if self.hdce.fc_shadow is not None else self.hdce.space.flat[lo:hi]
+
+    def sync_master(self) -> None:
+        """(ZeRO, bf16 shadow) each rank's fp32 FC master weights are current on its own shard only;
+        all-gather them (checkpointing, cross-rank comparisons).  No-op otherwise."""
+        if self.zero and self.ctx.distributed and self.hdce.fc_shadow is not None:
+            lo, hi = self.fc_region
+            self.buckets.launch_all_gather("master", self.hdce.space.flat[lo:hi])
+            self.buckets.wait(("master",))
+
+    def _mark(self, name: str, stream=None) -> None:
+        """(phase timing) a HIP event on ``stream`` (default: current) under ``name``."""
+        if self._phases is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            self._phases[-1][name] = e
+
     def _dp_run(self, g1, g2, gf, gr) -> None:
-        b = self.buckets
+        """The DP step around the collectives.  RCCL runs every collective of the process group on one
+        stream, in launch order: fc gradient (all-reduce, or reduce-scatter in the ZeRO plan), small
+        bucket, (ZeRO) the shadow all-gather.
+          allreduce : g1 | AR fc | g2 | AR small | fc stream: FC Adam (whole FC) | main: conv/QSC Adam
+          zero      : g1 | RS fc | g2 | AR small | fc stream: FC Adam on 1/world, AG shadow | main: ..."""
+        b, zero = self.buckets, self.zero
+        timed = self._phases is not None
+        if timed:
+            self._phases.append({})
+            self._mark("start")
         g1()
-        b.launch("skip")
-        b.launch("fc")
+        self._mark("g1")
+        lo, hi = self.fc_region
+        if zero:
+            b.launch_reduce_scatter("fc", self.hdce.space.grad[lo:hi])
+        else:
+            b.launch("skip")
+            b.launch("fc")
         g2()
+        self._mark("g2")
         b.launch("small")
+        fc_wait = ("fc", "small") if zero else ("skip", "fc")
         if self.streams is None:
-            b.wait()
+            b.wait(fc_wait)
             gf()
+            if zero:
+                b.launch_all_gather("ag", self._fc_weights_lp())
+            b.wait()
             gr()
             return
         main = torch.cuda.current_stream(self.ctx.device)
         fc = self.streams["fc"]
         fc.wait_stream(main)
         with torch.cuda.stream(fc):
-            b.wait(("skip", "fc"))
+            b.wait(fc_wait)
+            self._mark("fc_ready", fc)
             gf()
-        b.wait(("skip", "small"))
+            self._mark("gf", fc)
+            if zero:
+                b.launch_all_gather("ag", self._fc_weights_lp())
+                b.wait(("ag",))
+                self._mark("ag", fc)
+        # (allreduce plan: the HDCE NaN flag rides in the fc bucket -- wait for it before the conv Adam
+        # reads it; free under RCCL, whose in-order stream finished fc before small)
+        b.wait(("small",) if zero else ("skip", "fc", "small"))
+        self._mark("small_ready")
         gr()
+        self._mark("gr")
         main.wait_stream(fc)
         b.wait()
+        self._mark("end")
+
+    def phase_times(self, steps: int):
+        """Run ``steps`` DP steps with HIP events around the phases and return the mean milliseconds of
+        each (diagnostic; GPU DP plan only, else None): g1 (forward + FC wgrad), g2 (FC dgrad + conv
+        backward + QSC, hiding the FC collective), fc_exposed (FC collective time left after g2),
+        small_exposed, fc_adam, all_gather (ZeRO), conv_qsc_adam, step."""
+        if self.ctx.device.type != "cuda" or len(self.graphs) != 4 or self.streams is None:
+            return None
+        self._phases = []
+        try:
+            for _ in range(steps):
+                self.step()
+            torch.cuda.synchronize(self.ctx.device)
+            rows = self._phases
+        finally:
+            self._phases = None
+        el = lambda r, a, b_: r[a].elapsed_time(r[b_])
+        out = {"g1": [], "g2": [], "fc_exposed": [], "small_exposed": [], "fc_adam": [], "all_gather": [],
+               "conv_qsc_adam": [], "step": []}
+        for r in rows:
+            out["g1"].append(el(r, "start", "g1"))
+            out["g2"].append(el(r, "g1", "g2"))
+            out["fc_exposed"].append(max(0.0, el(r, "g2", "fc_ready")))
+            out["small_exposed"].append(max(0.0, el(r, "g2", "small_ready")))
+            out["fc_adam"].append(el(r, "fc_ready", "gf"))
+            out["all_gather"].append(el(r, "gf", "ag") if "ag" in r else 0.0)
+            out["conv_qsc_adam"].append(el(r, "small_ready", "gr"))
+            out["step"].append(el(r, "start", "end"))
+        return {k: sum(v) / len(v) for k, v in out.items()}
 
     def _step_body(self) -> None:
         if self.mode in ("dag", "dagq"):

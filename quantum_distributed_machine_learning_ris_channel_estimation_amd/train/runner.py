@@ -144,7 +144,7 @@ class Y2HRunner:
                                      self.data_dir, self.synthetic, self.seed, self.n_scenarios, self.n_users)
             if ctx.world > 1:
                 tr = tr.shard(ctx.rank, ctx.world)
-                va = va.shard(ctx.rank, ctx.world)
+                va = va.shard(ctx.rank, ctx.world, drop_remainder=False)   # (metrics are global sums)
             self._stores = (tr, va)
             self._print(f"Data Loaded! ({tr.n_streams} streams x {tr.n} train / {va.n} val samples per rank, "
                         f"device={ctx.device})")
@@ -256,8 +256,12 @@ class Y2HRunner:
             for it, idx in enumerate(sampler):
                 if idx.numel() == B:
                     if graphed.enabled and graphed.graph is None:
+                        # (every tensor a step updates: incl. the optimizer-written bf16 FC shadow and
+                        # the BN batch counters)
                         _capture_preserving(graphed, [sp.flat, opt.m, opt.v, opt.step_t] + model.run_mean
-                                            + model.run_var + [loss_acc], static_idx, idx)
+                                            + model.run_var + [model._nbt, loss_acc]
+                                            + ([model.fc_shadow] if model.fc_shadow is not None else []),
+                                            static_idx, idx)
                     static_idx.copy_(idx)
                     graphed()
                 else:
@@ -311,7 +315,7 @@ class Y2HRunner:
         model = cstep.model
         model.eval()
         S = store.n_streams
-        loss_sum = torch.zeros(3, device=store.Yp.device, dtype=torch.float64)  # loss sum, correct, total
+        loss_sum = torch.zeros(4, device=store.Yp.device, dtype=torch.float64)  # loss sum, correct, total, batches
         nb = 0
         for s in range(0, store.n, batch):
             idx = torch.arange(s, min(s + batch, store.n), device=store.Yp.device)
@@ -324,9 +328,9 @@ class Y2HRunner:
             loss_sum[2] += labels.numel()
             nb += 1
         ctx = self._context()
-        loss_sum[0] /= max(nb, 1)
-        ctx.all_reduce_(loss_sum)
-        loss_sum[0] /= ctx.world
+        loss_sum[3] = nb
+        ctx.all_reduce_(loss_sum)   # (per-rank val shards may differ in size: divide global sums)
+        loss_sum[0] /= loss_sum[3].clamp_min(1)
         model.train()
         return float(loss_sum[0]), float(loss_sum[1] / loss_sum[2])
 
@@ -393,8 +397,10 @@ class Y2HRunner:
             for idx in sampler:
                 if idx.numel() == B:
                     if graphed.enabled and graphed.graph is None:
-                        _capture_preserving(graphed, [space.flat, opt.step_t, loss_acc]
-                                            + ([opt.m, opt.v] if opt.kind != "sgd" else [opt.buf]), static_idx, idx)
+                        _capture_preserving(graphed, [space.flat, opt.step_t, loss_acc, opt.pruned]
+                                            + ([opt.m, opt.v] if opt.kind != "sgd" else [opt.buf])
+                                            + ([cstep.hip.noise_ctr] if cstep.hip is not None else []),
+                                            static_idx, idx)
                     static_idx.copy_(idx)
                     graphed()
                 else:

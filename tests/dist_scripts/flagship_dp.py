@@ -19,7 +19,11 @@ from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flags
 
 
 def flat_all(tr):
-    return torch.cat([tr.hdce.space.flat, tr.qspace.flat])
+    tr.sync_master()   # (ZeRO plan: each rank's fp32 FC master is current on its own shard only)
+    ts = [tr.hdce.space.flat, tr.qspace.flat]
+    if tr.hdce.fc_shadow is not None:   # the bf16 weights the forward reads
+        ts.append(tr.hdce.fc_shadow.float())
+    return torch.cat(ts)
 
 
 def same_on_all_ranks(t):
@@ -31,10 +35,11 @@ def same_on_all_ranks(t):
 
 def main(out, device="cpu"):
     ctx = init_distributed(device)
+    plan = os.environ.get("QDML_DP_PLAN", "zero")
     if device == "cuda":
-        cfg = FlagshipConfig(n_qubits=8, batch=32, data_len=800, hip_graphs=True)
+        cfg = FlagshipConfig(n_qubits=8, batch=32, data_len=800, hip_graphs=True, dp_plan=plan)
     else:
-        cfg = FlagshipConfig(n_qubits=4, batch=4, data_len=40, hip_graphs=False, dtype="fp32")
+        cfg = FlagshipConfig(n_qubits=4, batch=4, data_len=40, hip_graphs=False, dtype="fp32", dp_plan=plan)
     tr = FlagshipTrainer(cfg, ctx)
     ok = [same_on_all_ranks(flat_all(tr))]
     dbg = os.environ.get("QDML_DBG") == "1"

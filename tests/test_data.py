@@ -81,3 +81,31 @@ def test_split_and_stores():
     assert trs.scen.tolist() == [0, 0, 0, 1, 1, 1, 2, 2, 2]
     sh = trs.shard(1, 2)
     assert sh.n == 18 and torch.equal(sh.Yp[:, 0], trs.Yp[:, 18])
+
+
+def test_real_and_synthetic_streams_never_mix(tmp_path):
+    """Some reference .npy streams on disk and others missing is an error; none on disk warns."""
+    import warnings
+
+    import pytest
+
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.data.datasets import (
+        generate_stream, make_dml_stores, save_stream_npy)
+    d = str(tmp_path / "avail")
+    save_stream_npy(d, generate_stream(20, 0, 0, 10, 128, "train", 0, "cpu"), 0, 0, 128, 10, 20)
+    with pytest.raises(FileNotFoundError, match="mix"):
+        make_dml_stores(20, 128, 10, 0.9, "cpu", data_dir=d)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        make_dml_stores(20, 128, 10, 0.9, "cpu", data_dir=str(tmp_path / "none"))
+    assert any("synthetic" in str(x.message) for x in w)
+
+
+def test_val_shards_cover_every_sample():
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.data.datasets import make_dml_stores
+    _, va = make_dml_stores(70, 128, 10, 0.9, "cpu", data_dir=None)   # 7 val samples per stream
+    shards = [va.shard(r, 3, drop_remainder=False) for r in range(3)]
+    assert sum(s.n for s in shards) == va.n
+    import torch
+    assert torch.equal(torch.cat([s.Yp for s in shards], 1), va.Yp)
+    assert len({va.shard(r, 3).n for r in range(3)}) == 1   # training shards stay equal

@@ -24,13 +24,61 @@ def test_launcher_propagates_failure():
     assert rc == 3
 
 
-def test_flagship_dp_lockstep_and_rank_consistent_nan_skip(tmp_path):
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("plan", ["zero", "allreduce"])
+def test_flagship_dp_lockstep_and_rank_consistent_nan_skip(tmp_path, plan):
     out = str(tmp_path / "fl")
     rc = launch([sys.executable, os.path.join(HERE, "dist_scripts", "flagship_dp.py"), out], nproc=2,
-                extra_env={"OMP_NUM_THREADS": "2"})
+                extra_env={"OMP_NUM_THREADS": "2", "QDML_DP_PLAN": plan})
     assert rc == 0
     for r in range(2):
         same, skipped, flag = open(f"{out}.{r}").read().split()
         assert same == "1"           # parameters bit-identical across ranks after every step
         assert skipped == "1"        # the NaN on rank 1 made BOTH ranks skip
         assert float(flag) >= 1.0    # the summed skip flag
+
+
+def test_zero_plan_bit_identical_to_allreduce_plan(tmp_path):
+    """ZeRO-1 FC optimizer (reduce-scatter, Adam on a 1/world shard, all-gather) == all-reduce plan."""
+    out = str(tmp_path / "z")
+    rc = launch([sys.executable, os.path.join(HERE, "dist_scripts", "zero_vs_allreduce.py"), out], nproc=2,
+                extra_env={"OMP_NUM_THREADS": "2"})
+    assert rc == 0
+    for r in range(2):
+        ok, diff = open(f"{out}.{r}").read().split()
+        assert ok == "1", diff
+
+
+def _bench(args, env_extra=None, timeout=600):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update({"OMP_NUM_THREADS": "2", "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+    env.update(env_extra or {})
+    root = os.path.dirname(HERE)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True, text=True,
+                       env=env, timeout=timeout, cwd=root)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, [json.loads(ln) for ln in lines], p.stderr
+
+
+SMALL = ["--steps", "2", "--warmup", "1", "--batch", "4", "--data-len", "200", "--qubits", "4", "--dtype", "fp32"]
+
+
+def test_bench_self_launches_n_ranks():
+    """`python bench.py --gpus 2` without torchrun starts 2 ranks itself and reports dp2 (one JSON line)."""
+    rc, recs, err = _bench(["--gpus", "2"] + SMALL + ["--phase-steps", "0"])
+    assert rc == 0, err[-2000:]
+    assert len(recs) == 1, recs
+    r = recs[0]
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2"
+    assert r["config"]["global_batch"] == 2 * r["config"]["per_gpu_batch"]
+    assert r["config"]["dp_plan"] == "zero"
+
+
+def test_bench_world_mismatch_is_an_error():
+    rc, recs, err = _bench(["--gpus", "2"] + SMALL, env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and not recs
+    assert "WORLD_SIZE" in err

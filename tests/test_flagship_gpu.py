@@ -72,7 +72,8 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k, phase):
     assert float(ref.hopt.step_t[0]) == 4.0 and bool((dag.hopt.step_t == 4.0).all())
 
 
-def test_dp_plan_two_ranks_on_one_gpu(tmp_path):
+@pytest.mark.parametrize("plan", ["zero", "allreduce"])
+def test_dp_plan_two_ranks_on_one_gpu(tmp_path, plan):
     """The DP execution plan on the GPU (4 graphs, side streams, async bucketed all-reduces) with 2 ranks
     sharing the card over gloo: ranks stay bit-identical step after step and a NaN on one rank makes both
     skip.  (The 8-GPU RCCL run is the driver's; this covers the same code path on one device.)"""
@@ -82,11 +83,48 @@ def test_dp_plan_two_ranks_on_one_gpu(tmp_path):
     here = os.path.dirname(os.path.abspath(__file__))
     out = str(tmp_path / "fl")
     rc = launch([sys.executable, os.path.join(here, "dist_scripts", "flagship_dp.py"), out, "cuda"], nproc=2,
-                extra_env={"OMP_NUM_THREADS": "2", "QDML_DIST_BACKEND": "gloo"})
+                extra_env={"OMP_NUM_THREADS": "2", "QDML_DIST_BACKEND": "gloo", "QDML_DP_PLAN": plan})
     assert rc == 0
     for r in range(2):
         same, skipped, flag = open(f"{out}.{r}").read().split()
         assert same == "1" and skipped == "1" and float(flag) >= 1.0, (r, same, skipped, flag)
+
+
+def test_zero_plan_matches_allreduce_plan_on_gpu(tmp_path):
+    """ZeRO-1 FC optimizer == all-reduce plan bit for bit on the GPU plan (2 ranks sharing the card over
+    gloo): reduce-scatter, Adam on each rank's FC shard writing its slice of the bf16 shadow, all-gather."""
+    import os
+    import sys
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.launch import launch
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = str(tmp_path / "z")
+    rc = launch([sys.executable, os.path.join(here, "dist_scripts", "zero_vs_allreduce.py"), out, "cuda"], nproc=2,
+                extra_env={"OMP_NUM_THREADS": "2", "QDML_DIST_BACKEND": "gloo"})
+    assert rc == 0
+    for r in range(2):
+        ok, diff = open(f"{out}.{r}").read().split()
+        assert ok == "1", (r, diff)
+
+
+def test_bench_two_ranks_one_gpu_reports_phases(tmp_path):
+    """`bench.py --gpus 2` self-launches 2 ranks (gloo on one card) and reports dp2 with per-phase times."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update({"QDML_DIST_BACKEND": "gloo", "OMP_NUM_THREADS": "2"})
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "5", "--warmup", "2",
+                        "--phase-steps", "3"], capture_output=True, text=True, env=env, timeout=300, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(recs) == 1
+    r = recs[0]
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["dp_plan"] == "zero"
+    ph = r["phases_ms"]
+    assert set(ph) >= {"g1", "g2", "fc_exposed", "fc_adam", "all_gather", "conv_qsc_adam", "step"}
+    assert ph["step"] > 0 and ph["g1"] > 0
 
 
 def test_deferred_loss_finish_matches_finish_launch(cuda):
