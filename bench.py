@@ -85,7 +85,7 @@ def main() -> int:
         return 2
     cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
                          hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
-                         split_graphs=args.split_graphs, stream_mode=args.stream_mode,
+                         split_graphs=args.split_graphs or ctx.forced, stream_mode=args.stream_mode,
                          qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
                          hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
                          fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase, dp_plan=args.dp_plan,

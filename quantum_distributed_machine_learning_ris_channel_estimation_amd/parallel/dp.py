@@ -40,6 +40,7 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    forced: bool = False   # a process group even at world 1 (QDML_FORCE_DIST=1: rehearses the collectives)
 
     @property
     def is_main(self) -> bool:
@@ -47,7 +48,7 @@ class DistContext:
 
     @property
     def distributed(self) -> bool:
-        return self.world > 1
+        return self.world > 1 or self.forced
 
     def barrier(self) -> None:
         if self.distributed:
@@ -99,18 +100,24 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
     else:
         dev = torch.device("cpu")
     backend = "none"
-    if world > 1:
+    forced = world == 1 and os.environ.get("QDML_FORCE_DIST") == "1"
+    if world > 1 or forced:
         backend = os.environ.get("QDML_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
         if backend == "nccl" and world > torch.cuda.device_count():
             raise RuntimeError(f"RCCL needs one GPU per rank: WORLD_SIZE={world} but {torch.cuda.device_count()} "
                                "visible GPU(s) (QDML_DIST_BACKEND=gloo rehearses several ranks per GPU)")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if forced and "MASTER_PORT" not in os.environ:
+            import socket
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
         kw = {}
         if backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s),
                                 **kw)
-    _CTX = DistContext(rank, world, local, dev, backend)
+    _CTX = DistContext(rank, world, local, dev, backend, forced)
     return _CTX
 
 
@@ -120,7 +127,7 @@ def get_context() -> DistContext:
 
 def shutdown() -> None:
     global _CTX
-    if _CTX is not None and _CTX.distributed and dist.is_initialized():
+    if _CTX is not None and dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None
 
