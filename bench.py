@@ -46,7 +46,7 @@ def main() -> int:
                     help="estimator compute dtype (fp8: e4m3 FC forward GEMM, bf16 convs/backward)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-quantumnat", action="store_true")
-    ap.add_argument("--split-graphs", action="store_true", help="3-graph DP plan even at 1 GPU")
+    ap.add_argument("--split-graphs", action="store_true", help="the DP plan (5 graphs around the collectives) even at 1 GPU")
     ap.add_argument("--steps-per-graph", type=int, default=5,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
     ap.add_argument("--hdce-branches", default="", help="(dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam")
@@ -112,7 +112,7 @@ def main() -> int:
     n = ctx.world
     samples = tr.samples_per_step * n * args.steps
     value = samples / elapsed
-    phases = tr.phase_times(args.phase_steps) if args.phase_steps > 0 and len(tr.graphs) == 4 else None
+    phases = tr.phase_times(args.phase_steps) if args.phase_steps > 0 and len(tr.graphs) == 5 else None
     if phases is not None:
         keys = sorted(phases)
         phases = dict(zip(keys, (round(v, 4) for v in ctx.max_vector([phases[k] for k in keys]))))
@@ -148,7 +148,7 @@ def main() -> int:
                 "qsc_fork": args.qsc_fork,
                 "fc_adam_grid": args.fc_adam_grid,
                 "dp_qsc_phase": args.dp_qsc_phase,
-                "dp_plan": ("zero" if tr.zero else "allreduce") if len(tr.graphs) == 4 else None,
+                "dp_plan": ("zero" if tr.zero else "allreduce") if len(tr.graphs) == 5 else None,
                 "dist_backend": ctx.backend,
                 "stream_priority": args.stream_priority,
                 "steps_per_graph": args.steps_per_graph if n == 1 else 1,

@@ -318,6 +318,23 @@ class HDCEStep:
         self._rowden = g.rowden if getattr(g, "rowpow", None) is not None else None
         return self._forward_fc(g.x1, store.Hlabel, store.Hperf)
 
+    # the same forward in two halves (HIP path; the DP plan replays them as separate graphs, so the FC
+    # weights' update from the previous step -- an all-gather or the FC Adam -- overlaps the conv forward)
+    def forward_conv_gathered(self, g) -> None:
+        """Half 1: the conv / BN / ReLU stack on g.x1 (no FC weight read)."""
+        assert self.hip
+        self.nmse.rowoff = g.rowoff
+        self._rowden = g.rowden if getattr(g, "rowpow", None) is not None else None
+        self.conv.stage_hook = self.stage_hook
+        self._A_conv = self.conv.forward(g.x1, training=True)
+        if self.stage_hook is not None:
+            self.stage_hook("conv")
+
+    def forward_fc_after_conv(self, store) -> torch.Tensor:
+        """Half 2: FC forward, loss, FC weight gradient (+ data gradient unless deferred)."""
+        A, self._A_conv = self._A_conv, None
+        return self._fc_hip(A, store.Hlabel, store.Hperf)
+
     def _forward_fc(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
         if self.hip:
             return self._forward_fc_hip(x1, label, perf)
@@ -357,13 +374,18 @@ class HDCEStep:
 
     @torch.no_grad()
     def _forward_fc_hip(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
-        m = self.m
-        dt = m.compute_dtype
         hook = self.stage_hook
         self.conv.stage_hook = hook
         A = self.conv.forward(x1, training=True)                # (rows, 4096) bf16
         if hook is not None:
             hook("conv")
+        return self._fc_hip(A, label, perf)
+
+    @torch.no_grad()
+    def _fc_hip(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
+        m = self.m
+        dt = m.compute_dtype
+        hook = self.stage_hook
         W, b = m.fc_weights_lp()
         if m.fp8 and m.fc_shadow is None:
             Y = fp8_linear(A, m.fc_w.detach(), b)

@@ -28,9 +28,11 @@ measured and are kept as options (see ``__init__`` and README).
 
 The HDCE and the QSC have separate NaN-guard flags (``skip[0]``, ``skip[1]``), so neither
 optimizer waits for the other model's loss.
-World > 1: four graphs around the gradient all-reduces (``_dp_run``): the FC bucket starts right
-after the forward + FC weight gradient and is hidden by the FC data gradient, the conv backward
-and the QSC branch; the FC Adam runs on its own stream beside the small-bucket all-reduce.
+World > 1: five graphs around the gradient collectives (``_dp_run``): the FC gradient's collective
+(reduce-scatter in the default ZeRO-1 plan, all-reduce otherwise) starts right after the forward +
+FC weight gradient and is hidden by the FC data gradient, the conv backward and the QSC branch; the
+FC update (Adam on this rank's shard + the bf16 weight all-gather, or Adam on all of it) runs on
+its own stream and overlaps the next step's gather + conv forward.
 """
 from __future__ import annotations
 
@@ -86,7 +88,7 @@ class FlagshipConfig:
     lr: float = 1e-3
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
-    split_graphs: bool = False   # force the 3-graph DP execution plan even at world 1 (testing)
+    split_graphs: bool = False   # force the DP execution plan (5 graphs) even at world 1 (testing)
     stream_mode: str = "dagq"    # serial | dag | dagq | dagi (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
     qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
     hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
@@ -287,10 +289,12 @@ class FlagshipTrainer:
         else:
             if k != 1:
                 raise ValueError("multi-step graphs are a world-1 plan")
-            # four graphs around the gradient all-reduces (see _dp_run); one memory pool is safe: the
-            # graphs that replay concurrently (gf on the fc stream, gr on main) allocate nothing
+            # five graphs around the gradient collectives (see _dp_run); one memory pool is safe: the
+            # graphs that replay concurrently (gf on the fc stream beside gr / the next g1a on main)
+            # allocate nothing
             pool = torch.cuda.graph_pool_handle() if graphs else None
-            gs = [GraphedStep(f, enabled=graphs, pool=pool) for f in (self._dp_g1, self._dp_g2, self._dp_gf, self._dp_gr)]
+            gs = [GraphedStep(f, enabled=graphs, pool=pool)
+                  for f in (self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)]
         self._graph_sets[k] = gs
         return gs
 
@@ -396,7 +400,8 @@ class FlagshipTrainer:
     #        -> all-reduce 'small' (conv/BN + QSC grads + the QSC NaN flag)
     #   gf : (fc stream) FC Adam once 'skip' + 'fc' arrived and g2's dgrad read the weight shadow,
     #        beside the 'small' all-reduce;   gr : (main) conv/BN Adam + QSC AdamW after 'small'
-    def _dp_g1(self) -> None:
+    def _dp_g1a(self) -> None:
+        """gather + conv forward (reads no FC weight: overlaps the previous step's FC update)."""
         self._gather()
         self.hstep.defer_dgrad = self.hstep.hip
         ph = self.cfg.dp_qsc_phase
@@ -404,9 +409,23 @@ class FlagshipTrainer:
         if early:   # QSC forward (+ backward: phase 1) beside the HDCE forward
             with self._fork(self.streams["qsc"]):
                 self._qsc_branch(with_opt=False, part="fwd" if ph == 3 else "all")
-        self._hdce_forward(side=False)   # (the FC wgrad on main: the all-reduce waits for it first)
+        if self.hstep.hip:
+            self.hstep.forward_conv_gathered(self.gat)
+        else:
+            self._hdce_forward(side=False)
         if early:
             self._join(("qsc",))
+
+    def _dp_g1b(self) -> None:
+        """FC forward, loss, FC weight gradient (on main: the FC collective waits for it first)."""
+        if self.hstep.hip:
+            loss = self.hstep.forward_fc_after_conv(self.store)
+            if loss is not self.hloss:
+                self.hloss.copy_(loss)
+
+    def _dp_g1(self) -> None:
+        self._dp_g1a()
+        self._dp_g1b()
 
     def _dp_g2(self) -> None:
         # NOTE the first node of a graph must sit on the capturing stream: a branch forked before any
@@ -462,18 +481,27 @@ class FlagshipTrainer:
             e.record(stream)
             self._phases[-1][name] = e
 
-    def _dp_run(self, g1, g2, gf, gr) -> None:
+    def _dp_run(self, g1a, g1b, g2, gf, gr, fence: bool = True) -> None:
         """The DP step around the collectives.  RCCL runs every collective of the process group on one
         stream, in launch order: fc gradient (all-reduce, or reduce-scatter in the ZeRO plan), small
         bucket, (ZeRO) the shadow all-gather.
-          allreduce : g1 | AR fc | g2 | AR small | fc stream: FC Adam (whole FC) | main: conv/QSC Adam
-          zero      : g1 | RS fc | g2 | AR small | fc stream: FC Adam on 1/world, AG shadow | main: ..."""
+          allreduce : g1a g1b | AR fc | g2 | AR small | fc stream: FC Adam (whole FC) | main: conv/QSC Adam
+          zero      : g1a g1b | RS fc | g2 | AR small | fc stream: FC Adam on 1/world, AG shadow | main: ...
+        The FC update (fc stream) of step i overlaps step i+1's gather + conv forward (g1a): main waits
+        for the fc stream only before g1b reads the FC weights.  ``fence``: main also waits for it at the
+        end of the step (the last step of a run(), every step()): afterwards the state is complete."""
         b, zero = self.buckets, self.zero
         timed = self._phases is not None
         if timed:
             self._phases.append({})
             self._mark("start")
-        g1()
+        g1a()
+        self._mark("g1a")
+        main = torch.cuda.current_stream(self.ctx.device) if self.streams is not None else None
+        if main is not None:
+            main.wait_stream(self.streams["fc"])   # (the previous step's FC update, when not fenced)
+        self._mark("fc_prev")
+        g1b()
         self._mark("g1")
         lo, hi = self.fc_region
         if zero:
@@ -493,7 +521,6 @@ class FlagshipTrainer:
             b.wait()
             gr()
             return
-        main = torch.cuda.current_stream(self.ctx.device)
         fc = self.streams["fc"]
         fc.wait_stream(main)
         with torch.cuda.stream(fc):
@@ -511,8 +538,9 @@ class FlagshipTrainer:
         self._mark("small_ready")
         gr()
         self._mark("gr")
-        main.wait_stream(fc)
-        b.wait()
+        b.pending.clear()   # (every collective has been waited for by the stream that consumes it)
+        if fence:
+            main.wait_stream(fc)
         self._mark("end")
 
     def phase_times(self, steps: int):
@@ -520,20 +548,21 @@ class FlagshipTrainer:
         each (diagnostic; GPU DP plan only, else None): g1 (forward + FC wgrad), g2 (FC dgrad + conv
         backward + QSC, hiding the FC collective), fc_exposed (FC collective time left after g2),
         small_exposed, fc_adam, all_gather (ZeRO), conv_qsc_adam, step."""
-        if self.ctx.device.type != "cuda" or len(self.graphs) != 4 or self.streams is None:
+        if self.ctx.device.type != "cuda" or len(self.graphs) != 5 or self.streams is None:
             return None
         self._phases = []
         try:
-            for _ in range(steps):
-                self.step()
+            self.run(steps)
             torch.cuda.synchronize(self.ctx.device)
             rows = self._phases
         finally:
             self._phases = None
         el = lambda r, a, b_: r[a].elapsed_time(r[b_])
-        out = {"g1": [], "g2": [], "fc_exposed": [], "small_exposed": [], "fc_adam": [], "all_gather": [],
-               "conv_qsc_adam": [], "step": []}
-        for r in rows:
+        out = {"g1a": [], "fc_prev_wait": [], "g1": [], "g2": [], "fc_exposed": [], "small_exposed": [],
+               "fc_adam": [], "all_gather": [], "conv_qsc_adam": [], "step": []}
+        for i, r in enumerate(rows):
+            out["g1a"].append(el(r, "start", "g1a"))
+            out["fc_prev_wait"].append(el(r, "g1a", "fc_prev"))
             out["g1"].append(el(r, "start", "g1"))
             out["g2"].append(el(r, "g1", "g2"))
             out["fc_exposed"].append(max(0.0, el(r, "g2", "fc_ready")))
@@ -541,7 +570,8 @@ class FlagshipTrainer:
             out["fc_adam"].append(el(r, "fc_ready", "gf"))
             out["all_gather"].append(el(r, "gf", "ag") if "ag" in r else 0.0)
             out["conv_qsc_adam"].append(el(r, "small_ready", "gr"))
-            out["step"].append(el(r, "start", "end"))
+            # step = start to the next step's start (the FC update overlaps it), the last to its end
+            out["step"].append(el(r, "start", rows[i + 1]["start"]) if i + 1 < len(rows) else el(r, "start", "end"))
         return {k: sum(v) / len(v) for k, v in out.items()}
 
     def _step_body(self) -> None:
@@ -566,7 +596,7 @@ class FlagshipTrainer:
             fork_qsc(self.cfg.qsc_fork)   # (a stage the forward does not have: fork at its end)
             self._join(("qsc",))
             return
-        self._dp_run(self._dp_g1, self._dp_g2, self._dp_gf, self._dp_gr)
+        self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)
 
     def _indep_body(self, k: int) -> None:
         """(dagi) ``k`` steps as TWO independent chains of one graph: the HDCE chain on the capturing
@@ -677,12 +707,11 @@ class FlagshipTrainer:
     def run(self, n: int) -> None:
         """``n`` training steps, ``cfg.steps_per_graph`` per graph replay (the remainder one by one)."""
         k = self._k()
-        for _ in range(n // k):
-            self._replay(k)
-        for _ in range(n % k):
-            self._replay(1)
+        reps = [k] * (n // k) + [1] * (n % k)
+        for i, kk in enumerate(reps):   # (DP plan: consecutive steps overlap; the last one is fenced)
+            self._replay(kk, fence=i == len(reps) - 1)
 
-    def _replay(self, k: int) -> None:
+    def _replay(self, k: int, fence: bool = True) -> None:
         gs = self._graphs_for(k)
         if any(g.enabled and g.graph is None for g in gs):
             # (preserve: the capture warm-ups run optimizer steps on rank-local gradients; restoring
@@ -718,7 +747,7 @@ class FlagshipTrainer:
                     gq()
             self._join(("qsc",))
             return
-        self._dp_run(*gs)
+        self._dp_run(*gs, fence=fence)
 
     @property
     def samples_per_step(self) -> int:
