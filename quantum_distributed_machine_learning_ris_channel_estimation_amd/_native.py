@@ -74,6 +74,11 @@ def hipcc() -> Optional[str]:
     return None
 
 
+# gemm.hip: MFMA accumulators in VGPRs (the default AGPR form made hipcc shuttle the 18-36 accumulator
+# tiles between the register files every K step)
+PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     cc = hipcc()
     if cc is None:
@@ -89,7 +94,7 @@ def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     def one(src: str) -> str:
         obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
         if force or _stale(obj, [src] + hdrs):
-            _run([cc] + flags + ["-c", src, "-o", obj], verbose)
+            _run([cc] + flags + PER_FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj], verbose)
         return obj
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:

@@ -1,0 +1,558 @@
+// The three FC_P128 GEMMs of a training step, hand-written for gfx950 (bf16 MFMA 16x16x32, fp32
+// accumulation), and the inference FC:
+//
+//   forward   Y[M, N]  = A[M, K] . W[N, K]^T (+ b)     A = conv features, W = bf16 weight shadow
+//   wgrad     dW[N, K] = dY[M, N]^T . A[M, K]          fp32 out, straight into the flat gradient
+//   dgrad     dA[M, K] = dY[M, N] . W[N, K]            bf16 out, the conv backward's input
+//
+// Reference: FC_P128 (Estimators_QuantumNAT_onchipQNN.py:272-279) trained through autograd
+// (Runner_P128_QuantumNAT_onchipQNN.py:109-113, 194-199): Linear 4096 -> 2048, 78% of the HDCE FLOPs.
+// At the flagship shape M = 2304 (9 streams x 256), N = 2048, K = 4096 each GEMM is 38.7 GFLOP.
+//
+// One kernel template, C[I, J] = sum_k P[i, k] Q[j, k], each operand in one of two layouts:
+//   KC  k-contiguous   X[i * ld + k]     (forward A and W, dgrad dY)
+//   MC  i-contiguous   X[k * ld + i]     (wgrad dY^T and A, dgrad W)
+// so the forward is KC x KC, dgrad KC x MC and wgrad MC x MC -- no transposed copies anywhere.
+//
+// Tiles and waves.  BM x BN output tile, WM x WN waves each owning (16 MF) x (16 NJ).  The shapes
+// are chosen so that one tile lands on each CU (256 tiles for 256 CUs): forward 144 x 128
+// (16 x 16 tiles), dgrad 144 x 256 (16 x 16), wgrad 128 x 256 (16 x 16).  BK = 64.
+//
+// LDS images (one 1-KiB global_load_lds_dwordx4 per wave-instruction, lane-linear destination, the
+// swizzle applied on the per-lane SOURCE address and on the read -- guide §5.4 rule 21):
+//   KC  [rows][64 bf16]: 128-B rows, 16-B chunk c of row r stored at slot c ^ (r & 7).  An MFMA
+//       fragment is one ds_read_b128 per lane; conflict-free for ds_read_b128's lane groups.
+//   MC  [panel of 128 columns][64 k][256 B]: chunk c of k-row k at slot c ^ swt(k),
+//       swt(k) = 2 ((k & 3) | ((k >> 1) & 4)).  A fragment is two ds_read_b64_tr_b16 per lane (the
+//       hardware transpose read: lane i of a 16-lane group receives column i of 4 k-rows);
+//       conflict-free over each 32-lane half.  (Both checked exhaustively by scripts/lds_banks.py.)
+//
+// Pipeline (1 workgroup per CU): NSTAGE LDS stages filled by global_load_lds (NSTAGE - 1 tiles in
+// flight), counted `s_waitcnt vmcnt` + raw `s_barrier` (a __syncthreads() would drain the ring), and
+// two register sets of MFMA fragments: the fragments of sub-step s + 1 (32 k) are read from LDS
+// while the MFMAs of sub-step s issue.  One barrier per K step.  XCD-aware tile order: the blocks
+// of one XCD take a compact group of tiles, so their A / W slabs are shared in that XCD's L2.
+//
+// Epilogues (accumulators -> fp32 tile in LDS -> whole rows with 8/16-B stores):
+//   EPI_F32   C fp32                                     (wgrad)
+//   EPI_BF16  C bf16 (+ bias)                            (dgrad, inference forward)
+//   EPI_NMSE  the HDCE training loss (forward): per row r (stream s, label row rowoff[r]) with
+//             coef_s = 2 / (S den_s): dY = coef_s (Y - L) -> bf16 (Y itself is never stored),
+//             per-row error partials vs label and perfect channel in the layout of common.h's
+//             LossFinish (chunks of E rows: part[(r / E, tile_j, r % E)]), the per-stream label
+//             powers (dens), and per-tile column sums of dY (the bias gradient's partials) -- so
+//             the loss finish and the bias reduction run exactly as after csrc/hip/nmse.hip's
+//             one-pass kernel (qd_nmse_finish, or deferred into a later launch of the step).
+#include <type_traits>
+
+#include "common.h"
+
+namespace qd {
+namespace gemm {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short v4s;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+enum { KC = 0, MC = 1 };
+enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2 };
+constexpr int BK = 64;
+
+__device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
+__device__ __forceinline__ int mc_swt(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+
+struct NmseArgs {
+  const float* label;      // (rows of the store, N) fp32, row rowoff[r]
+  const float* perf;       // same, or null
+  const int* rowoff;       // (M,)
+  const float2* rowden;    // (M,) per-row (|label|^2, |perf|^2)
+  uint16_t* dY;            // (M, N) bf16
+  float* part;             // (M / E, n_tiles_n, E, 2): row partials (err^2, errperf^2) per N-tile
+  float* colsum;           // (n_tiles_m, N): per-M-tile column sums of dY
+  float* dens;             // (S, 2): per-stream (sum |label|^2, sum |perf|^2)
+  int E, U, B;             // row r = (u*B + b)*E + e, stream s = e*U + u
+  float loss_scale;
+};
+
+template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_>
+struct Geo {
+  static constexpr int MF = MF_, NJ = NJ_, WM = WM_, WN = WN_, LA = LA_, LB = LB_, NSTAGE = NSTAGE_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = 16 * MF * WM, BN = 16 * NJ * WN;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  static constexpr int PA = A_BYTES / 1024, PB = B_BYTES / 1024, P = PA + PB;   // 1-KiB pieces per tile
+  static constexpr int NPER = (P + NW - 1) / NW;      // pieces each wave issues per tile
+  static constexpr int PITCH = BN + 4;               // fp32 epilogue tile row pitch
+  static constexpr int LDS = (NSTAGE * STAGE > BM * PITCH * 4 + 8192) ? NSTAGE * STAGE : BM * PITCH * 4 + 8192;
+  static_assert(LA == KC || BM % 128 == 0, "MC operand tiles are whole 128-column panels");
+  static_assert(LB == KC || BN % 128 == 0, "MC operand tiles are whole 128-column panels");
+  static_assert(BN % 128 == 0, "epilogue rows are 2 or 4 columns per lane");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+// source address of this lane's 16 bytes of 1-KiB piece q of operand X (tile rows r0.., k0..k0+63)
+template <int L>
+__device__ __forceinline__ const uint16_t* piece_src(const uint16_t* __restrict__ X, int ld, int r0, int k0, int q,
+                                                     int lane) {
+  if constexpr (L == KC) {
+    const int row = q * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ (row & 7);
+    return X + (size_t)(r0 + row) * ld + k0 + ch * 8;
+  } else {
+    const int panel = q >> 4;
+    const int kr = ((q & 15) << 2) + (lane >> 4);
+    const int ch = (lane & 15) ^ mc_swt(kr);
+    return X + (size_t)(k0 + kr) * ld + r0 + panel * 128 + ch * 8;
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void vm_wait(int tiles) {   // leave `tiles` tiles of NPER pieces in flight
+  constexpr int N = G::NPER;
+  if (tiles >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * N) : "memory");
+  else if (tiles == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory");
+  else if (tiles == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// LDS reads as inline asm: the compiler's own LDS wait counting turned conservative in this loop
+// (lgkmcnt(0) before every MFMA group, i.e. no read/MFMA overlap), so the K loop places its waits
+// itself -- the counts are exact because LDS reads return in issue order -- each followed by a
+// sched_barrier so no MFMA is hoisted above its wait (guide §5.4 rule 18).  Addresses: one per-lane
+// base VGPR per (operand, sub-step) computed once, the fragment index in the instruction's offset.
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_b128(uint32_t addr) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ v4s lds_tr16(uint32_t addr) {
+  v4s r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N < 15 ? N : 15) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Per-lane read addressing of one operand image (image byte offset IMG within a stage; the wave's
+// fragments start at tile row R0w).
+//   KC: fragment f (rows R0w + 16 f ..) of sub-step s at  base[s] + 2048 f            (immediate)
+//   MC: fragment f at  base[s] + panel(f) * 16384 + ((cc(f) * 2) ^ x)  (+ 1024 for its second half),
+//       cc(f) = (R0w + 16 f) & 127 -- wave-uniform -- and x the lane's swizzle bits
+template <int L>
+struct Reader {
+  uint32_t base[2];
+  uint32_t x;
+  int r0w;
+  __device__ __forceinline__ void init(int img, int r0w_, int fr, int fq) {
+    r0w = r0w_;
+    if constexpr (L == KC) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) base[s] = img + (r0w + fr) * 128 + (((4 * s + fq) ^ (fr & 7)) << 4);
+      x = 0;
+    } else {
+      const int q = fr >> 2, p = fr & 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) base[s] = img + (32 * s + 8 * fq + q) * 256 + 8 * (p & 1) + 16 * (p >> 1);
+      x = (uint32_t)mc_swt(8 * fq + q) << 4;
+    }
+  }
+  // fragment f of sub-step s in the stage at byte offset st
+  template <int F>
+  __device__ __forceinline__ bf16x8 frag(uint32_t st, int s) const {
+    if constexpr (L == KC) {
+      return lds_b128<F * 2048>(st + base[s]);
+    } else {
+      const int r = r0w + 16 * F;
+      const uint32_t a = st + base[s] + (r >> 7) * (BK * 256) + ((uint32_t)((r & 127) * 2) ^ x);
+      const v4s lo = lds_tr16<0>(a);
+      const v4s hi = lds_tr16<1024>(a);
+      typedef __attribute__((ext_vector_type(8))) short v8s;
+      const v8s v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      return __builtin_bit_cast(bf16x8, v);
+    }
+  }
+};
+
+template <class G>
+struct Frags {
+  bf16x8 a[G::MF], b[G::NJ];
+};
+
+template <class G>
+struct Readers {
+  Reader<G::LA> ra;
+  Reader<G::LB> rb;
+  static constexpr int RA = G::LA == KC ? 1 : 2, RB = G::LB == KC ? 1 : 2;   // ds_read instrs per fragment
+  // LDS reads that may stay in flight when an MFMA group of the woven schedule starts (see mma_read)
+  static constexpr int ALLOW = (G::MF - 1) * RA + G::NJ * RB;
+
+  template <int J = 0>
+  __device__ __forceinline__ void read_b(Frags<G>& f, uint32_t st, int s) const {
+    if constexpr (J < G::NJ) {
+      f.b[J] = rb.template frag<J>(st, s);
+      read_b<J + 1>(f, st, s);
+    }
+  }
+  template <int I = 0>
+  __device__ __forceinline__ void read_a(Frags<G>& f, uint32_t st, int s) const {
+    if constexpr (I < G::MF) {
+      f.a[I] = ra.template frag<I>(st, s);
+      read_a<I + 1>(f, st, s);
+    }
+  }
+  // The MFMAs of set `cur` with the LDS reads of set `nxt` (stage st, sub-step s) woven in: nxt's B
+  // fragments first, then after the NJ MFMAs of each cur.a[i] the read of nxt.a[i].  cur was read in
+  // the same order one phase earlier, so before MFMA group i exactly (MF-1-i) RA reads of cur plus
+  // this phase's NJ RB + i RA reads may still be in flight: a constant ALLOW, and each group waits only
+  // for its own fragments.  (lgkmcnt holds 15 at most: schedules with ALLOW > 15 over-wait a little.)
+  template <bool READ, int I = 0>
+  __device__ __forceinline__ void mma_read(f32x4 (&acc)[G::MF][G::NJ], const Frags<G>& cur, Frags<G>& nxt,
+                                           uint32_t st, int s) const {
+    if constexpr (I == 0 && READ) read_b(nxt, st, s);
+    if constexpr (I < G::MF) {
+      lgkm_wait<READ ? ALLOW : (G::MF - 1 - I) * RA>();
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j)
+        acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.a[I], cur.b[j], acc[I][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (READ) nxt.a[I] = ra.template frag<I>(st, s);
+      mma_read<READ, I + 1>(acc, cur, nxt, st, s);
+    }
+  }
+};
+
+// This wave's glds pieces of one tile: every wave issues exactly NPER of them (the last piece is
+// loaded twice when NW does not divide P -- identical bytes to the same LDS slots), so the vmcnt
+// counts are uniform; source pointers advance by one K tile per stage() call, the LDS destinations
+// are wave-uniform (SGPR) offsets within a stage.
+template <class G>
+struct Stager {
+  const uint16_t* src[G::NPER];
+  int dst[G::NPER];
+  int adv[G::NPER];   // elements to advance per K tile
+  __device__ __forceinline__ void init(const uint16_t* Pm, int ldp, const uint16_t* Qm, int ldq, int i0, int j0,
+                                       int wave, int lane) {
+#pragma unroll
+    for (int it = 0; it < G::NPER; ++it) {
+      int q = wave + it * G::NW;
+      q = q < G::P ? q : G::P - 1;
+      const bool isA = q < G::PA;
+      const int qq = isA ? q : q - G::PA;
+      const uint16_t* sa = piece_src<G::LA>(Pm, ldp, i0, 0, isA ? qq : 0, lane);
+      const uint16_t* sb = piece_src<G::LB>(Qm, ldq, j0, 0, isA ? 0 : qq, lane);
+      src[it] = isA ? sa : sb;
+      dst[it] = isA ? q * 1024 : G::A_BYTES + qq * 1024;
+      const int la = G::LA == KC ? BK : BK * ldp, lb = G::LB == KC ? BK : BK * ldq;
+      adv[it] = isA ? la : lb;
+    }
+  }
+  __device__ __forceinline__ void issue(char* st) {
+#pragma unroll
+    for (int it = 0; it < G::NPER; ++it) {
+      __builtin_amdgcn_global_load_lds((glb_void*)src[it], (lds_void*)(st + dst[it]), 16, 0, 0);
+      src[it] += adv[it];
+    }
+  }
+};
+
+struct Args {
+  const uint16_t* P;
+  const uint16_t* Q;
+  int ldp, ldq;
+  int I, J, K;
+  void* C;              // fp32 (EPI_F32) or bf16 (EPI_BF16)
+  int ldc;
+  const uint16_t* bias; // EPI_BF16: per output column j, nullable
+  NmseArgs na;          // EPI_NMSE
+};
+
+// tile order: blocks b, b+8, ... share an XCD; each XCD takes whole GM x GN tile groups (row-major
+// within the group) when the grid splits that way, else plain row-major
+template <int GM, int GN>
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_i, int tiles_j, int& ti, int& tj) {
+  if (nwg % 8 == 0 && tiles_i % GM == 0 && tiles_j % GN == 0 && (nwg / 8) % (GM * GN) == 0) {
+    const int xcd = bid & 7, loc = bid >> 3;
+    const int per = nwg / 8;                          // tiles per XCD
+    const int g = xcd * (per / (GM * GN)) + loc / (GM * GN);
+    const int in = loc % (GM * GN);
+    const int gi = tiles_i / GM;
+    ti = (g % gi) * GM + in / GN;
+    tj = (g / gi) * GN + in % GN;
+  } else {
+    ti = bid / tiles_j;
+    tj = bid % tiles_j;
+  }
+}
+
+template <class G, int EPI, int GM, int GN>
+__global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / G::WN, wn = wave % G::WN;
+  const int tiles_i = a.I / G::BM, tiles_j = a.J / G::BN;
+  int ti, tj;
+  tile_of<GM, GN>(blockIdx.x, gridDim.x, tiles_i, tiles_j, ti, tj);
+  const int i0 = ti * G::BM, j0 = tj * G::BN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[G::MF][G::NJ];
+#pragma unroll
+  for (int i = 0; i < G::MF; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = a.K / BK;
+  constexpr int NS = G::NSTAGE;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  Stager<G> stg;
+  stg.init(a.P, a.ldp, a.Q, a.ldq, i0, j0, __builtin_amdgcn_readfirstlane(wave), lane);
+  Readers<G> rd;
+  rd.ra.init(0, wm * G::MF * 16, fr, fq);
+  rd.rb.init(G::A_BYTES, wn * G::NJ * 16, fr, fq);
+  // prologue: tiles 0 .. NS-2 in flight; wait for tile 0; its first fragments
+  for (int t = 0; t < NS - 1 && t < nk; ++t) stg.issue(smem + t * G::STAGE);
+  vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
+  __builtin_amdgcn_s_barrier();
+  Frags<G> f0, f1;
+  rd.read_b(f0, lds0, 0);
+  rd.read_a(f0, lds0, 0);
+
+  // Each K step t: MFMAs of sub-step 0 of tile t with sub-step 1's reads woven in; wait for tile t+1
+  // (counted vmcnt) + barrier; refill the stage tile t-1 used; MFMAs of sub-step 1 with tile t+1's
+  // sub-step-0 reads woven in.  Steady-state steps (refill always, a constant wait) form a loop with no
+  // branch inside; the last NS-1 steps are peeled (no refill, shrinking waits).
+  auto step = [&](int t, auto refill, int ahead) {
+    const uint32_t cur = lds0 + (t % NS) * G::STAGE, nxt = lds0 + ((t + 1) % NS) * G::STAGE;
+    rd.template mma_read<true>(acc, f0, f1, cur, 1);
+    vm_wait<G>(ahead);
+    __builtin_amdgcn_s_barrier();
+    if constexpr (decltype(refill)::value) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
+    __builtin_amdgcn_sched_barrier(0);
+    rd.template mma_read<true>(acc, f1, f0, nxt, 0);
+  };
+  int t = 0;
+  for (; t < nk - (NS - 1); ++t) step(t, std::true_type{}, NS - 3 < 0 ? 0 : NS - 3);
+  for (; t < nk - 1; ++t) step(t, std::false_type{}, nk - 2 - t);
+  rd.template mma_read<true>(acc, f0, f1, lds0 + (t % NS) * G::STAGE, 1);
+  rd.template mma_read<false>(acc, f1, f0, 0, 0);
+
+  // ---------------------------------------------------------------- epilogue
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();   // (every wave is done with the stage ring: it becomes the fp32 tile)
+  float* ct = reinterpret_cast<float*>(smem);
+  constexpr int PITCH = G::PITCH;
+#pragma unroll
+  for (int j = 0; j < G::NJ; ++j) {
+    const int cl = (wn * G::NJ + j) * 16 + fr;
+#pragma unroll
+    for (int i = 0; i < G::MF; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ct[((wm * G::MF + i) * 16 + fq * 4 + r) * PITCH + cl] = acc[i][j][r];
+  }
+  __syncthreads();
+  constexpr int VEC = G::BN / 64;   // columns per lane in a row pass (2 or 4)
+  const int c0 = VEC * lane;
+  if constexpr (EPI == EPI_F32) {
+    float* C = reinterpret_cast<float*>(a.C);
+    for (int row = wave; row < G::BM; row += G::NW) {
+      float* dst = C + (size_t)(i0 + row) * a.ldc + j0 + c0;
+      if constexpr (VEC == 4) *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(ct + row * PITCH + c0);
+      else *reinterpret_cast<float2*>(dst) = *reinterpret_cast<const float2*>(ct + row * PITCH + c0);
+    }
+  } else if constexpr (EPI == EPI_BF16) {
+    uint16_t* C = reinterpret_cast<uint16_t*>(a.C);
+    float bv[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) bv[v] = a.bias ? bf16_to_f32(a.bias[j0 + c0 + v]) : 0.f;
+    for (int row = wave; row < G::BM; row += G::NW) {
+      const float* src = ct + row * PITCH + c0;
+      uint16_t* dst = C + (size_t)(i0 + row) * a.ldc + j0 + c0;
+      if constexpr (VEC == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        uint2 w;
+        w.x = (uint32_t)f32_to_bf16(v.x + bv[0]) | ((uint32_t)f32_to_bf16(v.y + bv[1]) << 16);
+        w.y = (uint32_t)f32_to_bf16(v.z + bv[2]) | ((uint32_t)f32_to_bf16(v.w + bv[3]) << 16);
+        *reinterpret_cast<uint2*>(dst) = w;
+      } else {
+        const float2 v = *reinterpret_cast<const float2*>(src);
+        *reinterpret_cast<uint32_t*>(dst) =
+            (uint32_t)f32_to_bf16(v.x + bv[0]) | ((uint32_t)f32_to_bf16(v.y + bv[1]) << 16);
+      }
+    }
+  } else {
+    static_assert(EPI != EPI_NMSE || VEC == 2, "the NMSE epilogue walks 128-column tiles");
+    // HDCE loss: per-stream coefficients of the streams this tile touches (den_s summed over the
+    // stream's B rows in a fixed order: every block gets bitwise-identical values)
+    const NmseArgs& na = a.na;
+    const int N = a.J;
+    float* red = ct + G::BM * PITCH;                  // 64 floats after the tile
+    const float bv0 = a.bias ? bf16_to_f32(a.bias[j0 + c0]) : 0.f;
+    const float bv1 = a.bias ? bf16_to_f32(a.bias[j0 + c0 + 1]) : 0.f;
+    const int E = na.E, B = na.B, U = na.U, S = E * U;
+    const int ub = B * E;
+    const int u_lo = i0 / ub, u_hi = (i0 + G::BM - 1) / ub;
+    const int nst = (u_hi - u_lo + 1) * E;
+    for (int q = wave; q < nst; q += G::NW) {
+      const int u = u_lo + q / E, e = q % E;
+      float s = 0.f, sp = 0.f;
+      for (int b = lane; b < B; b += 64) {
+        const float2 v = na.rowden[(u * B + b) * E + e];
+        s += v.x;
+        sp += na.perf ? v.y : 0.f;
+      }
+      s = wave_sum(s);
+      sp = wave_sum(sp);
+      if (lane == 0) {
+        red[q] = na.loss_scale * 2.f / ((float)S * s);
+        if (tj == 0 && u * ub >= i0) *reinterpret_cast<float2*>(na.dens + (e * U + u) * 2) = make_float2(s, sp);
+      }
+    }
+    __syncthreads();
+    float cs0 = 0.f, cs1 = 0.f;
+    constexpr int RU = 4;                             // rows per batch (independent loads)
+    static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
+    for (int r0 = wave * RU; r0 < G::BM; r0 += G::NW * RU) {
+      float2 l[RU], pv[RU];
+      int ro[RU];
+#pragma unroll
+      for (int q = 0; q < RU; ++q) ro[q] = na.rowoff[i0 + r0 + q];
+#pragma unroll
+      for (int q = 0; q < RU; ++q) {
+        const size_t o = (size_t)ro[q] * N + j0 + c0;
+        l[q] = *reinterpret_cast<const float2*>(na.label + o);
+        pv[q] = na.perf ? *reinterpret_cast<const float2*>(na.perf + o) : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < RU; ++q) {
+        const int row = i0 + r0 + q;
+        float2 y = *reinterpret_cast<const float2*>(ct + (r0 + q) * PITCH + c0);
+        y.x += bv0;
+        y.y += bv1;
+        const float coef = red[(row / ub - u_lo) * E + row % E];
+        const float d0 = y.x - l[q].x, d1 = y.y - l[q].y;
+        float se = d0 * d0 + d1 * d1, sp = 0.f;
+        if (na.perf) {
+          const float p0 = y.x - pv[q].x, p1 = y.y - pv[q].y;
+          sp = p0 * p0 + p1 * p1;
+        }
+        const float g0 = coef * d0, g1 = coef * d1;
+        cs0 += g0;
+        cs1 += g1;
+        *reinterpret_cast<uint32_t*>(na.dY + (size_t)row * N + j0 + c0) =
+            (uint32_t)f32_to_bf16(g0) | ((uint32_t)f32_to_bf16(g1) << 16);
+        se = wave_sum(se);
+        sp = wave_sum(sp);
+        if (lane == 0)
+          *reinterpret_cast<float2*>(na.part + (((size_t)(row / E) * tiles_j + tj) * E + row % E) * 2) = make_float2(se, sp);
+      }
+    }
+    // column sums of dY over the tile: the waves' partials combined in a fixed order
+    __syncthreads();
+    float2* cpart = reinterpret_cast<float2*>(red + 64);
+    cpart[wave * 64 + lane] = make_float2(cs0, cs1);
+    __syncthreads();
+    if (wave == 0) {
+      float2 o = cpart[lane];
+#pragma unroll
+      for (int w = 1; w < G::NW; ++w) {
+        const float2 v = cpart[w * 64 + lane];
+        o.x += v.x;
+        o.y += v.y;
+      }
+      *reinterpret_cast<float2*>(na.colsum + (size_t)ti * N + j0 + c0) = o;
+    }
+  }
+}
+
+template <class G, int EPI, int GM, int GN>
+int launch(const Args& a, hipStream_t st) {
+  if (a.I % G::BM || a.J % G::BN || a.K % BK || a.K < BK) return (int)hipErrorInvalidValue;
+  auto kern = &gemm_kernel<G, EPI, GM, GN>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    attr = true;
+  }
+  const int grid = (a.I / G::BM) * (a.J / G::BN);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), G::LDS, st, a);
+  return (int)hipGetLastError();
+}
+
+// configurations (cfg index -> geometry); 0 = default
+//   forward  KC x KC  : 0: 144 x 128, 4 waves (1 x 4), 4 stages      1: 192 x 128, 8 waves (2 x 4), 3 stages
+//   dgrad    KC x MC  : 0: 144 x 256, 4 waves (1 x 4), 3 stages      1: 144 x 128, 4 waves, 4 stages
+//   wgrad    MC x MC  : 0: 128 x 256, 4 waves (1 x 4), 3 stages      1: 128 x 256, 8 waves (2 x 4), 3 stages
+using FwdA = Geo<9, 2, 1, 4, KC, KC, 4>;
+using FwdB = Geo<6, 2, 2, 4, KC, KC, 3>;
+using DgrA = Geo<9, 4, 1, 4, KC, MC, 3>;
+using DgrB = Geo<9, 2, 1, 4, KC, MC, 4>;
+using WgrA = Geo<8, 4, 1, 4, MC, MC, 3>;
+using WgrB = Geo<4, 4, 2, 4, MC, MC, 3>;
+
+}  // namespace gemm
+}  // namespace qd
+
+using namespace qd::gemm;
+
+// Which forward config applies to (M, N, K): 1 + cfg, or 0 (unsupported)
+QD_API int qd_gemm_tile_m(int cfg) { return cfg == 1 ? FwdB::BM : FwdA::BM; }
+
+QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
+  if (K % BK || N % 128) return 0;
+  if (cfg == 0) return M % FwdA::BM == 0;
+  if (cfg == 1) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
+  return 0;
+}
+
+// Y = A W^T (+ bias) bf16: A (M, K), W (N, K), Y (M, N), all row-major
+QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t* bias, uint16_t* Y, int M, int N,
+                            int K, int cfg, void* stream) {
+  Args a{A, W, K, K, M, N, K, Y, N, bias, {}};
+  hipStream_t st = (hipStream_t)stream;
+  if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
+  if (M % FwdA::BM) return (int)hipErrorInvalidValue;
+  return launch<FwdA, EPI_BF16, 4, 8>(a, st);
+}
+
+// The training forward with the HDCE-loss epilogue (see the header).  rows M = U*B*E in (u, b, e)
+// order; part (M / E, N / 128, E, 2), colsum (M / tile_m, N), dens (S, 2) -- then qd_nmse_finish
+// (chunks = M / tile_m, gx = N / 128, chunks_per_u = B) or a deferred LossFinish.
+QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t* bias, const float* label,
+                            const float* perf, const int* rowoff, const float* rowden, uint16_t* dY, float* part,
+                            float* colsum, float* dens, int M, int N, int K, int E, int U, int B, float loss_scale,
+                            int cfg, void* stream) {
+  if (M != U * B * E || E < 1 || E > 4) return (int)hipErrorInvalidValue;
+  NmseArgs na{label, perf, rowoff, reinterpret_cast<const float2*>(rowden), dY, part, colsum, dens, E, U, B,
+              loss_scale};
+  Args a{A, W, K, K, M, N, K, nullptr, N, bias, na};
+  hipStream_t st = (hipStream_t)stream;
+  const int bm = cfg == 1 ? FwdB::BM : FwdA::BM;
+  if (M % bm || (bm / (B * E) + 2) * E > 64) return (int)hipErrorInvalidValue;
+  if (cfg == 1) return launch<FwdB, EPI_NMSE, 1, 4>(a, st);
+  return launch<FwdA, EPI_NMSE, 4, 8>(a, st);
+}
+
+// dW (N, K) fp32 = dY^T A: dY (M, N) bf16, A (M, K) bf16 row-major; reduction over M
+QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M, int N, int K, int ldw, int cfg,
+                         void* stream) {
+  Args a{dY, A, N, K, N, K, M, dW, ldw, nullptr, {}};
+  hipStream_t st = (hipStream_t)stream;
+  if (cfg == 1) return launch<WgrB, EPI_F32, 2, 8>(a, st);
+  return launch<WgrA, EPI_F32, 2, 8>(a, st);
+}
+
+// dA (M, K) bf16 = dY W: dY (M, N) bf16, W (N, K) bf16 row-major; reduction over N
+QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, int M, int N, int K, int cfg,
+                         void* stream) {
+  Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}};
+  hipStream_t st = (hipStream_t)stream;
+  if (cfg == 1) return launch<DgrB, EPI_BF16, 4, 8>(a, st);
+  return launch<DgrA, EPI_BF16, 4, 4>(a, st);
+}

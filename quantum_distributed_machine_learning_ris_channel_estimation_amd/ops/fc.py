@@ -79,3 +79,59 @@ class FcNmse:
                           self.M, self.N, self.K, self.E, self.U, self.B, loss_scale, nat.stream_ptr(A.device)),
                   "fc_gemm_nmse")
         return self.dY
+
+
+# ---------------------------------------------------------------------------------------------------
+# csrc/hip/gemm.hip: the hand-written forward / weight-gradient / data-gradient GEMMs of FC_P128
+# (cfg selects a tile configuration; 0 = the default chosen by measurement, see gemm.hip's header)
+
+def _gemm_fn(name, argtypes):
+    return nat.fn(nat.hip_lib(), name, argtypes)
+
+
+def gemm_fwd_ok(M: int, N: int, K: int, cfg: int = 0) -> bool:
+    return bool(_gemm_fn("qd_gemm_fwd_ok", [_i, _i, _i, _i])(M, N, K, cfg))
+
+
+def gemm_tile_m(cfg: int = 0) -> int:
+    return int(_gemm_fn("qd_gemm_tile_m", [_i])(cfg))
+
+
+def gemm_fwd(A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+             cfg: int = 0) -> torch.Tensor:
+    """Y = A W^T (+ b), bf16 (A (M, K), W (N, K) row-major)."""
+    M, K = A.shape
+    N = W.shape[0]
+    assert A.dtype == W.dtype == torch.bfloat16 and A.is_contiguous() and W.is_contiguous() and W.shape[1] == K
+    assert b is None or (b.dtype == torch.bfloat16 and b.numel() == N and b.is_contiguous())
+    if not gemm_fwd_ok(M, N, K, cfg):
+        raise ValueError(f"gemm_fwd: shape {(M, N, K)} not supported by cfg {cfg}")
+    Y = out if out is not None else torch.empty(M, N, device=A.device, dtype=torch.bfloat16)
+    f = _gemm_fn("qd_gemm_fwd_bias", [_p, _p, _p, _p, _i, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(b) if b is not None else None, nat.ptr(Y), M, N, K, cfg,
+                nat.stream_ptr(A.device)), "gemm_fwd_bias")
+    return Y
+
+
+def gemm_wgrad(dY: torch.Tensor, A: torch.Tensor, out: Optional[torch.Tensor] = None, cfg: int = 0) -> torch.Tensor:
+    """dW = dY^T A in fp32 (dY (M, N), A (M, K) bf16 row-major; the reduction runs over M)."""
+    M, N = dY.shape
+    K = A.shape[1]
+    assert dY.dtype == A.dtype == torch.bfloat16 and dY.is_contiguous() and A.is_contiguous() and A.shape[0] == M
+    W = out if out is not None else torch.empty(N, K, device=A.device, dtype=torch.float32)
+    assert W.dtype == torch.float32 and W.shape == (N, K) and W.stride(1) == 1
+    f = _gemm_fn("qd_gemm_wgrad", [_p, _p, _p, _i, _i, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(dY), nat.ptr(A), nat.ptr(W), M, N, K, W.stride(0), cfg, nat.stream_ptr(A.device)),
+              "gemm_wgrad")
+    return W
+
+
+def gemm_dgrad(dY: torch.Tensor, W: torch.Tensor, out: Optional[torch.Tensor] = None, cfg: int = 0) -> torch.Tensor:
+    """dA = dY W, bf16 (dY (M, N), W (N, K) row-major; the reduction runs over N)."""
+    M, N = dY.shape
+    K = W.shape[1]
+    assert dY.dtype == W.dtype == torch.bfloat16 and dY.is_contiguous() and W.is_contiguous() and W.shape[0] == N
+    dA = out if out is not None else torch.empty(M, K, device=W.device, dtype=torch.bfloat16)
+    f = _gemm_fn("qd_gemm_dgrad", [_p, _p, _p, _i, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(dY), nat.ptr(W), nat.ptr(dA), M, N, K, cfg, nat.stream_ptr(W.device)), "gemm_dgrad")
+    return dA

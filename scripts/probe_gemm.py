@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Time the hand-written FC GEMMs (csrc/hip/gemm.hip, every cfg) against hipBLASLt (TunableOp choices when
+the shipped file exists) at the flagship shape M=2304, N=2048, K=4096, on uniform random operands.
+Rounds interleave the variants in one process (guide §5.4 rule 24); the median and min are printed."""
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import (  # noqa: E402
+    gemm_dgrad, gemm_fwd, gemm_wgrad)
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import use_tuned_gemms  # noqa: E402
+
+
+def timeit(fn, iters=30):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters * 1e3
+
+
+def main():
+    print("tuned gemms:", use_tuned_gemms())
+    dev = torch.device("cuda")
+    M, N, K = 2304, 2048, 4096
+    A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
+    W = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
+    b = (torch.rand(N, device=dev) * 2 - 1).bfloat16()
+    dY = (torch.rand(M, N, device=dev) * 2 - 1).bfloat16()
+    Y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    dW = torch.empty(N, K, device=dev)
+    dA = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    fl = 2 * M * N * K
+    var = {
+        "fwd_hipblaslt": lambda: torch.nn.functional.linear(A, W, b),
+        "fwd_hand0": lambda: gemm_fwd(A, W, b, out=Y, cfg=0),
+        "fwd_hand1": lambda: gemm_fwd(A, W, b, out=Y, cfg=1),
+        "wgrad_hipblaslt": lambda: torch.mm(dY.t(), A, out_dtype=torch.float32, out=dW),
+        "wgrad_hand0": lambda: gemm_wgrad(dY, A, out=dW, cfg=0),
+        "wgrad_hand1": lambda: gemm_wgrad(dY, A, out=dW, cfg=1),
+        "dgrad_hipblaslt": lambda: torch.mm(dY, W, out=dA),
+        "dgrad_hand0": lambda: gemm_dgrad(dY, W, out=dA, cfg=0),
+        "dgrad_hand1": lambda: gemm_dgrad(dY, W, out=dA, cfg=1),
+    }
+    res = {k: [] for k in var}
+    for _ in range(5):
+        for k, f in var.items():
+            res[k].append(timeit(f))
+    for k, v in res.items():
+        med = statistics.median(v)
+        print(f"{k:18s} median {med:8.2f} us  min {min(v):8.2f} us  {fl / med / 1e6:7.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
