@@ -332,8 +332,8 @@ class HDCEStep:
 
     def forward_fc_after_conv(self, store) -> torch.Tensor:
         """Half 2: FC forward, loss, FC weight gradient (+ data gradient unless deferred)."""
-        A, self._A_conv = self._A_conv, None
-        return self._fc_hip(A, store.Hlabel, store.Hperf)
+        # (the conv output is a static buffer: graph capture replays this half on its own several times)
+        return self._fc_hip(self._A_conv, store.Hlabel, store.Hperf)
 
     def _forward_fc(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
         if self.hip:
