@@ -497,3 +497,24 @@ QD_API int qd_nmse_grad(const void* Y, int y_bf16, const float* label, const flo
 #undef QD_G
   return (int)hipGetLastError();
 }
+
+// The finish launch alone, for producers other than qd_nmse_fused (csrc/hip/gemm.hip's forward GEMM
+// with the loss epilogue): colsum (chunks, cols) -> bias_grad when finish_bias, and the loss finish
+// over part (chunks_per_u * U, gx, E, 2) / dens (S, 2).
+QD_API int qd_nmse_finish(const float* colsum, int chunks, const float* part, int gx, int chunks_per_u,
+                          const float* dens, float* bias_grad, float* ss, float* loss, float* skip, int cols, int U,
+                          int E, int finish_bias, void* stream) {
+  if (cols % 64 || E < 1 || E > 4) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+#define QD_N(EE)                                                                                               \
+  hipLaunchKernelGGL((nmse_finish_kernel<EE>), dim3(finish_bias ? cols / 64 + 1 : 1), dim3(256), 0, st, colsum, \
+                     part, dens, bias_grad, ss, loss, skip, chunks, gx, cols, chunks_per_u, U)
+  switch (E) {
+    case 1: QD_N(1); break;
+    case 2: QD_N(2); break;
+    case 3: QD_N(3); break;
+    default: QD_N(4); break;
+  }
+#undef QD_N
+  return (int)hipGetLastError();
+}

@@ -227,6 +227,52 @@ class StreamNMSE:
             bias_slabs.add(colsum, bias_grad, 1, chunks, self.cols)
         return dY
 
+    def gemm_fused(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], label: torch.Tensor,
+                   perf: Optional[torch.Tensor], bias_grad: torch.Tensor, layout: Tuple[int, int, int],
+                   rowden: torch.Tensor, loss_scale: float = 1.0, bias_slabs=None, defer_loss: bool = False,
+                   cfg: int = 0) -> torch.Tensor:
+        """The FC forward GEMM with this loss as its epilogue (csrc/hip/gemm.hip qd_gemm_fwd_nmse): Y = A W^T
+        + b is never written; dY (bf16), the error partials, the per-stream label powers and the bias
+        gradient's per-tile column sums come out of the GEMM, then the same finish as ``fused`` (a launch,
+        or ``pending_finish`` for a later launch of the step with ``defer_loss``; the bias column reduction
+        queued on ``bias_slabs`` when given).  Returns dY; the loss is ``self.loss``."""
+        from .fc import gemm_tile_m
+        E, U, B = layout
+        M, K = A.shape
+        N = W.shape[0]
+        assert A.is_cuda and self.rowoff is not None and M == self.rows == E * U * B and N == self.cols
+        assert A.dtype == W.dtype == torch.bfloat16 and A.is_contiguous() and W.is_contiguous()
+        self._check_labels(label)
+        if perf is not None:
+            self._check_labels(perf)
+        tm = gemm_tile_m(cfg)
+        gx = N // 128
+        dev = A.device
+        if getattr(self, "_gz", None) is None or self._gz[0] != (tm, N):
+            self._gz = ((tm, N), torch.empty(M, N, device=dev, dtype=torch.bfloat16),
+                        torch.empty(M // E * gx * E * 2, device=dev), torch.empty(M // tm, N, device=dev),
+                        torch.empty(self.S, 2, device=dev))
+        _, dY, part, colsum, dens = self._gz
+        f = nat.fn(nat.hip_lib(), "qd_gemm_fwd_nmse", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i,
+                                                       _i, _f, _i, _p])
+        nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(b) if b is not None else None, nat.ptr(label),
+                    nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowoff), nat.ptr(rowden), nat.ptr(dY),
+                    nat.ptr(part), nat.ptr(colsum), nat.ptr(dens), M, N, K, E, U, B, loss_scale, cfg,
+                    nat.stream_ptr(dev)), "gemm_fwd_nmse")
+        self.pending_finish = None
+        if defer_loss:
+            assert bias_slabs is not None, "defer_loss needs the bias reduction queued elsewhere"
+            self.pending_finish = LossFinish(nat.ptr(part), nat.ptr(dens), nat.ptr(self.ss), nat.ptr(self.loss),
+                                             nat.ptr(self.skip) if self.skip is not None else None, gx, B, U, E)
+        else:
+            fin = nat.fn(nat.hip_lib(), "qd_nmse_finish", [_p, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+            nat.check(fin(nat.ptr(colsum), M // tm, nat.ptr(part), gx, B, nat.ptr(dens), nat.ptr(bias_grad),
+                          nat.ptr(self.ss), nat.ptr(self.loss), nat.ptr(self.skip) if self.skip is not None else None,
+                          N, U, E, int(bias_slabs is None), nat.stream_ptr(dev)), "nmse_finish")
+        if bias_slabs is not None:
+            bias_slabs.add(colsum, bias_grad, 1, M // tm, N)
+        return dY
+
     def __call__(self, Y, label, perf=None, out_dtype=torch.float32) -> Tuple[torch.Tensor, torch.Tensor]:
         self.sums(Y, label, perf)
         self.finalize()

@@ -284,6 +284,10 @@ class HDCEStep:
         self.bias_via_conv_slabs = False
         self.defer_loss = True   # (with bias_via_conv_slabs) loss finish hosted by the conv backward
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
+        # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; QDML_HAND_GEMM=0: hipBLASLt) and their
+        # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d")
+        self.hand_gemm = self.hip and os.environ.get("QDML_HAND_GEMM", "1") != "0"
+        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,0,0").split(","))
         if self.hip:
             from ..ops.conv import ConvStackHIP
             # launch knobs (samples per wave / per wgrad workgroup / per BN-reduction workgroup / layer-1
@@ -381,8 +385,51 @@ class HDCEStep:
             hook("conv")
         return self._fc_hip(A, label, perf)
 
+    def _hand_gemm_ok(self, A: torch.Tensor) -> bool:
+        """The hand-written FC GEMMs (csrc/hip/gemm.hip) apply: bf16 estimator, labels gathered through
+        rowoff with per-row powers, a shape the kernels tile (QDML_HAND_GEMM=0: hipBLASLt instead)."""
+        m = self.m
+        if not (self.hand_gemm and m.compute_dtype == torch.bfloat16 and not m.fp8 and self.nmse.rowoff is not None
+                and getattr(self, "_rowden", None) is not None):
+            return False
+        from ..ops.fc import gemm_fwd_ok, gemm_tile_m
+        M, K = A.shape
+        N = m.fc_w.shape[0]
+        c = self.gemm_cfg
+        return (gemm_fwd_ok(M, N, K, c[0]) and N % 256 == 0 and M % 128 == 0 and K % 256 == 0
+                and (gemm_tile_m(c[0]) // (self.B * m.E) + 2) * m.E <= 64)
+
+    @torch.no_grad()
+    def _fc_hand(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
+        """FC forward with the loss fused into its epilogue, then the weight and data gradients -- all
+        three GEMMs hand-written (csrc/hip/gemm.hip), no Y in memory."""
+        from ..ops.fc import gemm_dgrad, gemm_wgrad
+        from ..ops.slabsum import SlabBatch
+        m = self.m
+        W, b = m.fc_weights_lp()
+        if self.stage_hook is not None:
+            self.stage_hook("fc")
+        self._slabs = SlabBatch() if (self.writes_grads and self.bias_via_conv_slabs) else None
+        dY = self.nmse.gemm_fused(A, W, b, label, perf, m.fc_b.grad, (m.E, self.U, self.B), self._rowden,
+                                  bias_slabs=self._slabs, defer_loss=self._slabs is not None and self.defer_loss,
+                                  cfg=self.gemm_cfg[0])
+        side = self.fc_side
+        if side is not None:
+            self._keep = (dY, A)
+            side.wait_stream(torch.cuda.current_stream(A.device))
+            with torch.cuda.stream(side):
+                gemm_wgrad(dY, A, out=m.fc_w.grad, cfg=self.gemm_cfg[1])
+        else:
+            gemm_wgrad(dY, A, out=m.fc_w.grad, cfg=self.gemm_cfg[1])
+        self._dYW = (dY, W)
+        if not self.defer_dgrad:
+            self.dgrad()
+        return self.nmse.loss
+
     @torch.no_grad()
     def _fc_hip(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
+        if self._hand_gemm_ok(A):
+            return self._fc_hand(A, label, perf)
         m = self.m
         dt = m.compute_dtype
         hook = self.stage_hook
@@ -435,7 +482,14 @@ class HDCEStep:
         """dA = dY W (HIP path): issued by the forward unless ``defer_dgrad`` (the DP plan issues it
         after the FC gradient all-reduce is on its way)."""
         dY, W = self._dYW
-        self._dA = torch.mm(dY, W)                             # (rows, 4096) bf16
+        from ..ops.fc import gemm_dgrad
+        if self.hand_gemm and dY.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 \
+                and dY.shape[0] % 144 == 0 and W.shape[1] % 256 == 0 and W.shape[0] % 64 == 0:
+            if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
+                self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)
+            self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
+        else:
+            self._dA = torch.mm(dY, W)                         # (rows, 4096) bf16
 
     @property
     def skip(self) -> torch.Tensor:

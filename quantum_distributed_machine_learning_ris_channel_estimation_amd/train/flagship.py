@@ -571,7 +571,7 @@ class FlagshipTrainer:
             out["all_gather"].append(el(r, "gf", "ag") if "ag" in r else 0.0)
             out["conv_qsc_adam"].append(el(r, "small_ready", "gr"))
             # step = start to the next step's start (the FC update overlaps it), the last to its end
-            out["step"].append(el(r, "start", rows[i + 1]["start"]) if i + 1 < len(rows) else el(r, "start", "end"))
+            out["step"].append(r["start"].elapsed_time(rows[i + 1]["start"]) if i + 1 < len(rows) else el(r, "start", "end"))
         return {k: sum(v) / len(v) for k, v in out.items()}
 
     def _step_body(self) -> None:
