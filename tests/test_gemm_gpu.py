@@ -76,3 +76,83 @@ def test_gemm_dgrad_matches_fp32(cuda, cfg, M, N, K):
     torch.cuda.synchronize()
     assert torch.equal(dA2[:, 5], dY[:, N - 1]) and torch.equal(dA2[:, K - 1], dY[:, 0])
     assert float(dA2[:, :5].abs().sum()) == 0.0
+
+
+def _rows(E, U, B, N_store, cols, device):
+    S = E * U
+    L = torch.randn(S, N_store, cols, device=device)
+    P = L + 0.3 * torch.randn_like(L)
+    idx = torch.randint(0, N_store, (B,), device=device)
+    u = torch.arange(U, device=device).view(U, 1, 1)
+    e = torch.arange(E, device=device).view(1, 1, E)
+    rowoff = ((e * U + u).expand(U, B, E) * N_store + idx.view(1, B, 1)).reshape(-1).to(torch.int32)
+    lab = L.reshape(-1, cols)[rowoff.long()]
+    per = P.reshape(-1, cols)[rowoff.long()]
+    rowden = torch.stack([lab.pow(2).sum(1), per.pow(2).sum(1)], 1).contiguous()
+    stream = (e * U + u).expand(U, B, E).reshape(-1)
+    return L, P, rowoff, rowden, lab, per, stream
+
+
+@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("E,U,B,N,K", [(3, 3, 64, 256, 320), (3, 3, 256, 2048, 4096)])
+def test_gemm_nmse_epilogue_matches_fp32(cuda, cfg, E, U, B, N, K):
+    """Forward GEMM with the HDCE loss epilogue + finish: loss, loss_perf, dY, bias gradient, NaN flag."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import gemm_tile_m
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.nmse import StreamNMSE
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEModel
+    torch.manual_seed(1)
+    M, S = E * U * B, E * U
+    if M % gemm_tile_m(cfg) or not gemm_fwd_ok(M, N, K, cfg):
+        pytest.skip("shape not tiled by this cfg")
+    A = torch.randn(M, K, device=cuda).bfloat16()
+    W = (torch.randn(N, K, device=cuda) * K ** -0.5).bfloat16()
+    b = (0.1 * torch.randn(N, device=cuda)).bfloat16()
+    L, P, rowoff, rowden, lab, per, stream = _rows(E, U, B, 40, N, cuda)
+    nm = StreamNMSE(HDCEModel.row_stream(E, U, B, cuda), S, N)
+    nm.rowoff = rowoff
+    bg = torch.full((N,), 1e30, device=cuda)
+    dY = nm.gemm_fused(A, W, b, L, P, bg, (E, U, B), rowden, cfg=cfg)
+    torch.cuda.synchronize()
+    Y = A.float() @ W.float().t() + b.float()
+    num = torch.zeros(S, device=cuda).index_add_(0, stream, ((Y - lab) ** 2).sum(1))
+    den = torch.zeros(S, device=cuda).index_add_(0, stream, (lab ** 2).sum(1))
+    nump = torch.zeros(S, device=cuda).index_add_(0, stream, ((Y - per) ** 2).sum(1))
+    denp = torch.zeros(S, device=cuda).index_add_(0, stream, (per ** 2).sum(1))
+    ref_loss = torch.stack([(num / den).mean(), (nump / denp).mean()])
+    ref_dY = (2.0 / (S * den))[stream][:, None] * (Y - lab)
+    assert torch.allclose(nm.loss, ref_loss, rtol=2e-3), (nm.loss, ref_loss)
+    assert _rel(dY, ref_dY) <= 2e-2
+    assert torch.allclose(bg, ref_dY.sum(0), rtol=2e-2, atol=2e-2 * float(ref_dY.sum(0).abs().max()))
+    assert float(nm.skip) == 0.0 and torch.allclose(nm.ss[:, 1], den, rtol=1e-4)
+    A[3, 3] = float("nan")
+    nm.gemm_fused(A, W, b, L, P, bg, (E, U, B), rowden, cfg=cfg)
+    torch.cuda.synchronize()
+    assert float(nm.skip) == 1.0
+
+
+def test_flagship_hand_gemm_matches_hipblaslt_path(cuda, monkeypatch):
+    """One flagship step with the hand-written FC GEMMs (loss fused into the forward's epilogue) vs the
+    hipBLASLt + one-pass NMSE path: loss and every gradient agree to bf16 accuracy."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
+                                                                                                FlagshipTrainer)
+    ctx = DistContext(device=cuda)
+    cfg = dict(batch=64, data_len=800, hip_graphs=False, use_quantumnat=False, stream_mode="serial")
+    trs = []
+    for hand in ("1", "0"):
+        monkeypatch.setenv("QDML_HAND_GEMM", hand)
+        tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
+        assert tr.hstep.hand_gemm == (hand == "1")
+        tr.next_batch()
+        tr._dp_g1()
+        tr._dp_g2()
+        torch.cuda.synchronize()
+        trs.append(tr)
+    a, b = trs
+    assert torch.allclose(a.hloss, b.hloss, rtol=1e-2), (a.hloss, b.hloss)
+    ga, gb = a.hdce.space.grad, b.hdce.space.grad
+    sp = a.hdce.space
+    for name, p in zip(sp.names, sp.params):
+        sl = sp.slice_of(p)
+        x, y = ga[sl], gb[sl]
+        assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
