@@ -38,8 +38,8 @@
 //   EPI_BF16  C bf16 (+ bias)                            (dgrad, inference forward)
 //   EPI_NMSE  the HDCE training loss (forward): per row r (stream s, label row rowoff[r]) with
 //             coef_s = 2 / (S den_s): dY = coef_s (Y - L) -> bf16 (Y itself is never stored),
-//             per-row error partials vs label and perfect channel in the layout of common.h's
-//             LossFinish (chunks of E rows: part[(r / E, tile_j, r % E)]), the per-stream label
+//             error partials vs label and perfect channel per (chunk of 16 samples = 16 E rows, e)
+//             in the layout of common.h's LossFinish (part[(r / 16E, tile_j, e)]), the per-stream label
 //             powers (dens), and per-tile column sums of dY (the bias gradient's partials) -- so
 //             the loss finish and the bias reduction run exactly as after csrc/hip/nmse.hip's
 //             one-pass kernel (qd_nmse_finish, or deferred into a later launch of the step).
@@ -415,6 +415,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
       }
     }
     __syncthreads();
+    float2* rsum = reinterpret_cast<float2*>(red + 64 + G::NW * 128);   // per-row (err^2, errperf^2)
     float cs0 = 0.f, cs1 = 0.f;
     constexpr int RU = 4;                             // rows per batch (independent loads)
     static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
@@ -449,12 +450,23 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
             (uint32_t)f32_to_bf16(g0) | ((uint32_t)f32_to_bf16(g1) << 16);
         se = wave_sum(se);
         sp = wave_sum(sp);
-        if (lane == 0)
-          *reinterpret_cast<float2*>(na.part + (((size_t)(row / E) * tiles_j + tj) * E + row % E) * 2) = make_float2(se, sp);
+        if (lane == 0) rsum[r0 + q] = make_float2(se, sp);
       }
     }
     // column sums of dY over the tile: the waves' partials combined in a fixed order
     __syncthreads();
+    // row error partials -> per (chunk of 16 samples, e) sums in a fixed order: part (M / CR, gx, E, 2)
+    const int CR = 16 * E;
+    for (int sl = tid; sl < (G::BM / CR) * E; sl += G::NT) {
+      const int c = sl / E, e = sl % E;
+      float2 o = make_float2(0.f, 0.f);
+      for (int b = 0; b < 16; ++b) {
+        const float2 v = rsum[c * CR + b * E + e];
+        o.x += v.x;
+        o.y += v.y;
+      }
+      *reinterpret_cast<float2*>(na.part + (((size_t)((i0 + c * CR) / CR) * tiles_j + tj) * E + e) * 2) = o;
+    }
     float2* cpart = reinterpret_cast<float2*>(red + 64);
     cpart[wave * 64 + lane] = make_float2(cs0, cs1);
     __syncthreads();
@@ -522,8 +534,8 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
 }
 
 // The training forward with the HDCE-loss epilogue (see the header).  rows M = U*B*E in (u, b, e)
-// order; part (M / E, N / 128, E, 2), colsum (M / tile_m, N), dens (S, 2) -- then qd_nmse_finish
-// (chunks = M / tile_m, gx = N / 128, chunks_per_u = B) or a deferred LossFinish.
+// order, B % 16 == 0; part (M / 16E, N / 128, E, 2), colsum (M / tile_m, N), dens (S, 2) -- then
+// qd_nmse_finish (chunks = M / tile_m, gx = N / 128, chunks_per_u = B / 16) or a deferred LossFinish.
 QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t* bias, const float* label,
                             const float* perf, const int* rowoff, const float* rowden, uint16_t* dY, float* part,
                             float* colsum, float* dens, int M, int N, int K, int E, int U, int B, float loss_scale,
@@ -534,7 +546,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   Args a{A, W, K, K, M, N, K, nullptr, N, bias, na};
   hipStream_t st = (hipStream_t)stream;
   const int bm = cfg == 1 ? FwdB::BM : FwdA::BM;
-  if (M % bm || (bm / (B * E) + 2) * E > 64) return (int)hipErrorInvalidValue;
+  if (M % bm || (bm / (B * E) + 2) * E > 64 || B % 16 || bm % (16 * E)) return (int)hipErrorInvalidValue;
   if (cfg == 1) return launch<FwdB, EPI_NMSE, 1, 4>(a, st);
   return launch<FwdA, EPI_NMSE, 4, 8>(a, st);
 }

@@ -250,7 +250,7 @@ class StreamNMSE:
         dev = A.device
         if getattr(self, "_gz", None) is None or self._gz[0] != (tm, N):
             self._gz = ((tm, N), torch.empty(M, N, device=dev, dtype=torch.bfloat16),
-                        torch.empty(M // E * gx * E * 2, device=dev), torch.empty(M // tm, N, device=dev),
+                        torch.empty(M // 16 * gx * 2, device=dev), torch.empty(M // tm, N, device=dev),
                         torch.empty(self.S, 2, device=dev))
         _, dY, part, colsum, dens = self._gz
         f = nat.fn(nat.hip_lib(), "qd_gemm_fwd_nmse", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i,
@@ -263,10 +263,10 @@ class StreamNMSE:
         if defer_loss:
             assert bias_slabs is not None, "defer_loss needs the bias reduction queued elsewhere"
             self.pending_finish = LossFinish(nat.ptr(part), nat.ptr(dens), nat.ptr(self.ss), nat.ptr(self.loss),
-                                             nat.ptr(self.skip) if self.skip is not None else None, gx, B, U, E)
+                                             nat.ptr(self.skip) if self.skip is not None else None, gx, B // 16, U, E)
         else:
             fin = nat.fn(nat.hip_lib(), "qd_nmse_finish", [_p, _i, _p, _i, _i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
-            nat.check(fin(nat.ptr(colsum), M // tm, nat.ptr(part), gx, B, nat.ptr(dens), nat.ptr(bias_grad),
+            nat.check(fin(nat.ptr(colsum), M // tm, nat.ptr(part), gx, B // 16, nat.ptr(dens), nat.ptr(bias_grad),
                           nat.ptr(self.ss), nat.ptr(self.loss), nat.ptr(self.skip) if self.skip is not None else None,
                           N, U, E, int(bias_slabs is None), nat.stream_ptr(dev)), "nmse_finish")
         if bias_slabs is not None:

@@ -396,8 +396,9 @@ class HDCEStep:
         M, K = A.shape
         N = m.fc_w.shape[0]
         c = self.gemm_cfg
+        tm = gemm_tile_m(c[0])
         return (gemm_fwd_ok(M, N, K, c[0]) and N % 256 == 0 and M % 128 == 0 and K % 256 == 0
-                and (gemm_tile_m(c[0]) // (self.B * m.E) + 2) * m.E <= 64)
+                and (tm // (self.B * m.E) + 2) * m.E <= 64 and self.B % 16 == 0 and tm % (16 * m.E) == 0)
 
     @torch.no_grad()
     def _fc_hand(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
@@ -490,6 +491,8 @@ class HDCEStep:
             self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
         else:
             self._dA = torch.mm(dY, W)                         # (rows, 4096) bf16
+        if self.stage_hook is not None:
+            self.stage_hook("dgrad")
 
     @property
     def skip(self) -> torch.Tensor:

@@ -103,7 +103,10 @@ class FlagshipConfig:
     dp_plan: str = "zero"        # world > 1: "zero" = ZeRO-1 FC optimizer (reduce-scatter the FC gradient,
     #                              Adam on this rank's 1/world shard, all-gather the bf16 weight shadow) or
     #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
-    qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc
+    qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc, or
+    #                              "split": its forward half beside the conv forward (joined before the FC
+    #                              GEMMs, which take whole CUs), its backward half + AdamW beside the conv
+    #                              backward (forked once the FC data gradient is issued)
     qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
@@ -575,6 +578,26 @@ class FlagshipTrainer:
         return {k: sum(v) / len(v) for k, v in out.items()}
 
     def _step_body(self) -> None:
+        if self.mode in ("dag", "dagq") and self.cfg.qsc_fork == "split" and self.cstep.hip is not None:
+            self._gather()
+            q = self.streams["qsc"]
+            with self._fork(q):
+                self._qsc_branch(with_opt=False, part="fwd")
+
+            def hook(stage: str) -> None:
+                if stage == "fc":          # the FC GEMMs need whole CUs: the QSC forward half is done by now
+                    self._join(("qsc",))
+                elif stage == "dgrad":     # the QSC backward half beside the conv backward
+                    with self._fork(q):
+                        self._qsc_branch(with_opt=True, part="bwd")
+
+            self.hstep.stage_hook = hook
+            try:
+                self._hdce_graph()
+            finally:
+                self.hstep.stage_hook = None
+            self._join(("qsc",))
+            return
         if self.mode in ("dag", "dagq"):
             self._gather()
             # the QSC branch forks at a chosen point of the HDCE forward (cfg.qsc_fork): its latency-
