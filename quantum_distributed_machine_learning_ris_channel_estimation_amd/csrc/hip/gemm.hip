@@ -417,7 +417,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     __syncthreads();
     float2* rsum = reinterpret_cast<float2*>(red + 64 + G::NW * 128);   // per-row (err^2, errperf^2)
     float cs0 = 0.f, cs1 = 0.f;
-    constexpr int RU = 4;                             // rows per batch (independent loads)
+    constexpr int RU = 12;                            // rows per batch (independent loads in flight)
     static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
     for (int r0 = wave * RU; r0 < G::BM; r0 += G::NW * RU) {
       float2 l[RU], pv[RU];

@@ -408,12 +408,12 @@ class HDCEStep:
         from ..ops.slabsum import SlabBatch
         m = self.m
         W, b = m.fc_weights_lp()
-        if self.stage_hook is not None:
-            self.stage_hook("fc")
         self._slabs = SlabBatch() if (self.writes_grads and self.bias_via_conv_slabs) else None
         dY = self.nmse.gemm_fused(A, W, b, label, perf, m.fc_b.grad, (m.E, self.U, self.B), self._rowden,
                                   bias_slabs=self._slabs, defer_loss=self._slabs is not None and self.defer_loss,
                                   cfg=self.gemm_cfg[0])
+        if self.stage_hook is not None:
+            self.stage_hook("fc")
         side = self.fc_side
         if side is not None:
             self._keep = (dY, A)
@@ -429,6 +429,8 @@ class HDCEStep:
 
     @torch.no_grad()
     def _fc_hip(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
+        if self.stage_hook is not None:
+            self.stage_hook("fc_pre")   # (before anything reads the FC weights)
         if self._hand_gemm_ok(A):
             return self._fc_hand(A, label, perf)
         m = self.m

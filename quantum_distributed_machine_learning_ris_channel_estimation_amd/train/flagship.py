@@ -108,6 +108,10 @@ class FlagshipConfig:
     #                              GEMMs, which take whole CUs), its backward half + AdamW beside the conv
     #                              backward (forked once the FC data gradient is issued)
     qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
+    fc_adam_overlap: bool = True  # (world 1, dag / dagq) the FC part of the HDCE Adam runs on a side stream
+    #                               and overlaps the NEXT step's gather + conv forward (+ QSC); that step's FC
+    #                               GEMM waits for it.  The conv part (and the weight-image pack) stays on
+    #                               the chain: the next conv forward reads those weights
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
@@ -154,7 +158,8 @@ class FlagshipTrainer:
         self.shard_len = (sp.numel - n_conv) // ctx.world
         if self.zero:
             self.hopt.partition([n_conv + i * self.shard_len for i in range(ctx.world)])
-        elif (dp or cfg.stream_mode in ("dag", "qsc", "full") or "a" in cfg.hdce_branches):
+        elif (dp or cfg.stream_mode in ("dag", "qsc", "full") or "a" in cfg.hdce_branches
+              or (cfg.fc_adam_overlap and cfg.stream_mode in ("dag", "dagq") and dev.type == "cuda")):
             self.hopt.partition([n_conv])
         if cfg.fc_adam_grid:
             self.hopt.max_grid[1 + (ctx.rank if self.zero else 0)] = cfg.fc_adam_grid
@@ -259,6 +264,10 @@ class FlagshipTrainer:
             self.hstep.conv.pack_at_tail = True
             self._tail_pack_launch(advance=False)   # the first step's images
         self._use_graphs = graphs
+        # FC Adam overlapping the next step (see FlagshipConfig.fc_adam_overlap): pending on the fc stream
+        self.fc_overlap = bool(cfg.fc_adam_overlap and self.streams is not None and mode in ("dag", "dagq")
+                               and ctx.world == 1 and not cfg.split_graphs and not self.branches)
+        self._fc_pending = False
         self._phases = None   # (phase_times) per-step dicts of HIP events
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
@@ -276,6 +285,9 @@ class FlagshipTrainer:
             def body():
                 for _ in range(k):
                     fn()
+                if self._fc_pending:   # (a captured graph must rejoin every stream it forked)
+                    self._join(("fc",))
+                    self._fc_pending = False
             return body
 
         if self.ctx.world == 1 and not cfg.split_graphs:
@@ -384,6 +396,17 @@ class FlagshipTrainer:
         else:
             if self.hdce_side:
                 self._join(("fc",))
+            if self.fc_overlap:
+                # conv part (+ the next step's weight images and batch cursor) on the chain; the FC part on
+                # the fc stream, overlapping the next step up to its FC forward (see _fc_wait)
+                pk = self._adam_pack()
+                self.hopt.step(grad_scale=1.0, skip=self.hskip, part=0, pack=pk)
+                if self.tail_pack and pk is None:
+                    self._tail_pack_launch()
+                with self._fork(self.streams["fc"]):
+                    self.hopt.step(grad_scale=1.0, skip=self.hskip, part=1)
+                self._fc_pending = True
+                return
             if len(self.hopt.bounds) == 1:
                 pk = self._adam_pack()
                 self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
@@ -577,6 +600,12 @@ class FlagshipTrainer:
             out["step"].append(r["start"].elapsed_time(rows[i + 1]["start"]) if i + 1 < len(rows) else el(r, "start", "end"))
         return {k: sum(v) / len(v) for k, v in out.items()}
 
+    def _fc_wait(self) -> None:
+        """Before the FC forward: the previous step's FC Adam (fc_overlap) must have rewritten the weights."""
+        if self._fc_pending:
+            self._join(("fc",))
+            self._fc_pending = False
+
     def _step_body(self) -> None:
         if self.mode in ("dag", "dagq") and self.cfg.qsc_fork == "split" and self.cstep.hip is not None:
             self._gather()
@@ -585,7 +614,8 @@ class FlagshipTrainer:
                 self._qsc_branch(with_opt=False, part="fwd")
 
             def hook(stage: str) -> None:
-                if stage == "fc":          # the FC GEMMs need whole CUs: the QSC forward half is done by now
+                if stage == "fc_pre":      # the FC GEMMs need whole CUs: the QSC forward half is done by now
+                    self._fc_wait()
                     self._join(("qsc",))
                 elif stage == "dgrad":     # the QSC backward half beside the conv backward
                     with self._fork(q):
@@ -605,6 +635,8 @@ class FlagshipTrainer:
             forked = []
 
             def fork_qsc(stage: str) -> None:
+                if stage == "fc_pre":
+                    self._fc_wait()
                 if not forked and stage == self.cfg.qsc_fork:
                     forked.append(True)
                     with self._fork(self.streams["qsc"]):
