@@ -286,7 +286,10 @@ class HDCEStep:
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; QDML_HAND_GEMM=0: hipBLASLt) and their
         # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d")
-        self.hand_gemm = self.hip and os.environ.get("QDML_HAND_GEMM", "1") != "0"
+        hg = os.environ.get("QDML_HAND_GEMM", "1").strip()
+        hg = {"1": "fwd,wgrad,dgrad", "all": "fwd,wgrad,dgrad", "0": "", "none": ""}.get(hg, hg)
+        self.hand_gemm = set(x for x in hg.split(",") if x) if self.hip else set()
+        assert self.hand_gemm <= {"fwd", "wgrad", "dgrad"}, self.hand_gemm
         self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,0,0").split(","))
         if self.hip:
             from ..ops.conv import ConvStackHIP
@@ -389,7 +392,7 @@ class HDCEStep:
         """The hand-written FC GEMMs (csrc/hip/gemm.hip) apply: bf16 estimator, labels gathered through
         rowoff with per-row powers, a shape the kernels tile (QDML_HAND_GEMM=0: hipBLASLt instead)."""
         m = self.m
-        if not (self.hand_gemm and m.compute_dtype == torch.bfloat16 and not m.fp8 and self.nmse.rowoff is not None
+        if not ("fwd" in self.hand_gemm and m.compute_dtype == torch.bfloat16 and not m.fp8 and self.nmse.rowoff is not None
                 and getattr(self, "_rowden", None) is not None):
             return False
         from ..ops.fc import gemm_fwd_ok, gemm_tile_m
@@ -414,14 +417,7 @@ class HDCEStep:
                                   cfg=self.gemm_cfg[0])
         if self.stage_hook is not None:
             self.stage_hook("fc")
-        side = self.fc_side
-        if side is not None:
-            self._keep = (dY, A)
-            side.wait_stream(torch.cuda.current_stream(A.device))
-            with torch.cuda.stream(side):
-                gemm_wgrad(dY, A, out=m.fc_w.grad, cfg=self.gemm_cfg[1])
-        else:
-            gemm_wgrad(dY, A, out=m.fc_w.grad, cfg=self.gemm_cfg[1])
+        self._wgrad(dY, A)
         self._dYW = (dY, W)
         if not self.defer_dgrad:
             self.dgrad()
@@ -466,27 +462,42 @@ class HDCEStep:
             loss = self.nmse.sums_finalize(Y, label, perf)
             dY = self.nmse.grad_bias(Y, label, m.fc_b.grad, out_dtype=dt)   # + bias grad, same pass
         A = A.to(dt)
-        side = self.fc_side
-        if side is not None:
-            # the weight-gradient GEMM runs beside the data-gradient GEMM (and the conv backward that
-            # follows it): both only read dY; the operands stay referenced (no allocator reuse)
-            self._keep = (dY, A)
-            side.wait_stream(torch.cuda.current_stream(A.device))
-            with torch.cuda.stream(side):
-                _mm_f32(dY.t(), A, m.fc_w.grad)               # dW = dY^T A   (fp32 out)
-        else:
-            _mm_f32(dY.t(), A, m.fc_w.grad)
+        self._wgrad(dY, A)
         self._dYW = (dY, W)
         if not self.defer_dgrad:
             self.dgrad()
         return loss
+
+    def _wgrad(self, dY: torch.Tensor, A: torch.Tensor) -> None:
+        """dW = dY^T A (fp32, straight into the flat gradient): the hand-written GEMM for bf16 operands of a
+        tiled shape, else hipBLASLt; on ``fc_side`` when set (beside the data gradient and the conv backward,
+        which only read dY; the operands stay referenced: no allocator reuse)."""
+        from ..ops.fc import gemm_wgrad
+        m = self.m
+        hand = ("wgrad" in self.hand_gemm and dY.dtype == A.dtype == torch.bfloat16 and dY.shape[0] % 64 == 0
+                and dY.shape[1] % 128 == 0 and A.shape[1] % 256 == 0)
+
+        def run():
+            if hand:
+                gemm_wgrad(dY, A, out=m.fc_w.grad, cfg=self.gemm_cfg[1])
+            else:
+                _mm_f32(dY.t(), A, m.fc_w.grad)
+
+        side = self.fc_side
+        if side is not None:
+            self._keep = (dY, A)
+            side.wait_stream(torch.cuda.current_stream(A.device))
+            with torch.cuda.stream(side):
+                run()
+        else:
+            run()
 
     def dgrad(self) -> None:
         """dA = dY W (HIP path): issued by the forward unless ``defer_dgrad`` (the DP plan issues it
         after the FC gradient all-reduce is on its way)."""
         dY, W = self._dYW
         from ..ops.fc import gemm_dgrad
-        if self.hand_gemm and dY.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 \
+        if "dgrad" in self.hand_gemm and dY.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 \
                 and dY.shape[0] % 144 == 0 and W.shape[1] % 256 == 0 and W.shape[0] % 64 == 0:
             if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
                 self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)

@@ -142,7 +142,7 @@ def test_flagship_hand_gemm_matches_hipblaslt_path(cuda, monkeypatch):
     for hand in ("1", "0"):
         monkeypatch.setenv("QDML_HAND_GEMM", hand)
         tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
-        assert tr.hstep.hand_gemm == (hand == "1")
+        assert bool(tr.hstep.hand_gemm) == (hand == "1")
         tr.next_batch()
         tr._dp_g1()
         tr._dp_g2()
