@@ -76,9 +76,11 @@ struct NmseArgs {
   float loss_scale;
 };
 
-template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_>
+// DBG (diagnosis builds, scripts/probe_gemm.py): 1 = no global loads in the K loop (MFMAs on whatever the
+// stages hold), 2 = no MFMAs (loads and LDS reads only)
+template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int DBG_ = 0>
 struct Geo {
-  static constexpr int MF = MF_, NJ = NJ_, WM = WM_, WN = WN_, LA = LA_, LB = LB_, NSTAGE = NSTAGE_;
+  static constexpr int MF = MF_, NJ = NJ_, WM = WM_, WN = WN_, LA = LA_, LB = LB_, NSTAGE = NSTAGE_, DBG = DBG_;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int BM = 16 * MF * WM, BN = 16 * NJ * WN;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -220,7 +222,8 @@ struct Readers {
       lgkm_wait<READ ? ALLOW : (G::MF - 1 - I) * RA>();
 #pragma unroll
       for (int j = 0; j < G::NJ; ++j)
-        acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.a[I], cur.b[j], acc[I][j], 0, 0, 0);
+        if constexpr (G::DBG == 2) asm volatile("" ::"v"(cur.a[I]), "v"(cur.b[j]));
+        else acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.a[I], cur.b[j], acc[I][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (READ) nxt.a[I] = ra.template frag<I>(st, s);
       mma_read<READ, I + 1>(acc, cur, nxt, st, s);
@@ -331,9 +334,9 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   auto step = [&](int t, auto refill, int ahead) {
     const uint32_t cur = lds0 + (t % NS) * G::STAGE, nxt = lds0 + ((t + 1) % NS) * G::STAGE;
     rd.template mma_read<true>(acc, f0, f1, cur, 1);
-    vm_wait<G>(ahead);
+    if constexpr (G::DBG != 1) vm_wait<G>(ahead);
     __builtin_amdgcn_s_barrier();
-    if constexpr (decltype(refill)::value) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
+    if constexpr (decltype(refill)::value && G::DBG != 1) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
     __builtin_amdgcn_sched_barrier(0);
     rd.template mma_read<true>(acc, f1, f0, nxt, 0);
   };
@@ -518,6 +521,7 @@ QD_API int qd_gemm_tile_m(int cfg) { return cfg == 1 ? FwdB::BM : FwdA::BM; }
 
 QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (K % BK || N % 128) return 0;
+  if (cfg == 101 || cfg == 102) return M % FwdA::BM == 0;
   if (cfg == 0) return M % FwdA::BM == 0;
   if (cfg == 1) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
   return 0;
@@ -530,6 +534,8 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
   if (M % FwdA::BM) return (int)hipErrorInvalidValue;
+  if (cfg == 101) return launch<Geo<9, 2, 1, 4, KC, KC, 4, 1>, EPI_BF16, 4, 8>(a, st);   // (diagnosis builds)
+  if (cfg == 102) return launch<Geo<9, 2, 1, 4, KC, KC, 4, 2>, EPI_BF16, 4, 8>(a, st);
   return launch<FwdA, EPI_BF16, 4, 8>(a, st);
 }
 

@@ -41,6 +41,8 @@ def main():
         "fwd_hipblaslt": lambda: torch.nn.functional.linear(A, W, b),
         "fwd_hand0": lambda: gemm_fwd(A, W, b, out=Y, cfg=0),
         "fwd_hand1": lambda: gemm_fwd(A, W, b, out=Y, cfg=1),
+        "fwd_hand0_noload": lambda: gemm_fwd(A, W, b, out=Y, cfg=101),
+        "fwd_hand0_nomfma": lambda: gemm_fwd(A, W, b, out=Y, cfg=102),
         "wgrad_hipblaslt": lambda: torch.mm(dY.t(), A, out_dtype=torch.float32, out=dW),
         "wgrad_hand0": lambda: gemm_wgrad(dY, A, out=dW, cfg=0),
         "wgrad_hand1": lambda: gemm_wgrad(dY, A, out=dW, cfg=1),
