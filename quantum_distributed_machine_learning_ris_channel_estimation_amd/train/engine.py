@@ -286,7 +286,10 @@ class HDCEStep:
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; QDML_HAND_GEMM=0: hipBLASLt) and their
         # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d")
-        hg = os.environ.get("QDML_HAND_GEMM", "1").strip()
+        # default: the hand-written weight-gradient GEMM; the forward (with the loss epilogue) and data-gradient
+        # kernels are exact and as fast in isolation (scripts/probe_gemm.py) but take whole CUs (140-160 KB of
+        # LDS), so beside the QSC branch the step measured 0.465 vs 0.440 ms with them (profiles/r2_*)
+        hg = os.environ.get("QDML_HAND_GEMM", "wgrad").strip()
         hg = {"1": "fwd,wgrad,dgrad", "all": "fwd,wgrad,dgrad", "0": "", "none": ""}.get(hg, hg)
         self.hand_gemm = set(x for x in hg.split(",") if x) if self.hip else set()
         assert self.hand_gemm <= {"fwd", "wgrad", "dgrad"}, self.hand_gemm

@@ -108,10 +108,11 @@ class FlagshipConfig:
     #                              GEMMs, which take whole CUs), its backward half + AdamW beside the conv
     #                              backward (forked once the FC data gradient is issued)
     qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
-    fc_adam_overlap: bool = True  # (world 1, dag / dagq) the FC part of the HDCE Adam runs on a side stream
+    fc_adam_overlap: bool = False  # (world 1, dag / dagq) the FC part of the HDCE Adam runs on a side stream
     #                               and overlaps the NEXT step's gather + conv forward (+ QSC); that step's FC
     #                               GEMM waits for it.  The conv part (and the weight-image pack) stays on
-    #                               the chain: the next conv forward reads those weights
+    #                               the chain: the next conv forward reads those weights.  Measured no gain:
+    #                               the bandwidth-bound Adam slows the next step's (latency-bound) gather
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
