@@ -63,6 +63,7 @@ class SC_P128(nn.Module):
     def __init__(self, pilot_num: int = 128, n_classes: int = 3):
         super().__init__()
         H, W = pilot_grid(pilot_num)
+        self.pilot_num = pilot_num
         self.flat = 32 * (H // 4) * (W // 4)
         self.conv1 = nn.Conv2d(2, 32, kernel_size=3, padding=1, bias=False)
         self.conv2 = nn.Conv2d(32, 32, kernel_size=3, padding=1, bias=False)

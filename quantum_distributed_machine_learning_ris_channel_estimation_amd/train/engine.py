@@ -560,9 +560,15 @@ class ClassifierStep:
                 and batch_total):
             from ..ops.qsc import QSCStepHIP
             self.hip = QSCStepHIP(model, space, batch_total, n_groups=n_streams, **(hip_kw or {}))
+        elif isinstance(model, SC_P128) and dev.type == "cuda" and space is not None:
+            from ..ops.sc import SCStepHIP   # (any batch size: the kernels take B per call)
+            self.hip = SCStepHIP(model, space, batch_total or 0)
+        self.is_sc = isinstance(model, SC_P128)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         m = self.model
+        if self.is_sc and self.hip is not None:
+            return self.hip.forward(x)
         if isinstance(m, QSC_P128) and m.use_quantum:
             angles = m.preprocess(x)
             w = m.qlayer.weights
@@ -588,7 +594,7 @@ class ClassifierStep:
     def __call__(self, x: torch.Tensor, labels: torch.Tensor, slabs=None) -> torch.Tensor:
         """``slabs`` (HIP path): queue the gradient-slab reductions on this ``SlabBatch`` (launched by
         the caller, with accumulate = not writes_grads)."""
-        if self.hip is not None and x.shape[0] == self.hip.B:
+        if self.hip is not None and (self.is_sc or x.shape[0] == self.hip.B):
             loss = self.hip(x.contiguous(), labels, skip=self.skip, skip_add=self.skip_add,
                             accumulate=not self.writes_grads, slabs=slabs)
             if self.grad_hook:

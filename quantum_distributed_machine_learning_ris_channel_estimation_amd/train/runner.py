@@ -399,7 +399,8 @@ class Y2HRunner:
                     if graphed.enabled and graphed.graph is None:
                         _capture_preserving(graphed, [space.flat, opt.step_t, loss_acc, opt.pruned]
                                             + ([opt.m, opt.v] if opt.kind != "sgd" else [opt.buf])
-                                            + ([cstep.hip.noise_ctr] if cstep.hip is not None else []),
+                                            + ([cstep.hip.noise_ctr] if getattr(cstep.hip, "noise_ctr", None)
+                                               is not None else []),
                                             static_idx, idx)
                     static_idx.copy_(idx)
                     graphed()
