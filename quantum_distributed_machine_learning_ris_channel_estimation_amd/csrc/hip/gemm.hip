@@ -95,13 +95,15 @@ struct Geo {
 };
 
 // source address of this lane's 16 bytes of 1-KiB piece q of operand X (tile rows r0.., k0..k0+63)
+// (KC only: with an expert map, tile row r reads source row r * re + expert[r] -- the routed operand)
 template <int L>
 __device__ __forceinline__ const uint16_t* piece_src(const uint16_t* __restrict__ X, int ld, int r0, int k0, int q,
-                                                     int lane) {
+                                                     int lane, const long* __restrict__ expert = nullptr, int re = 0) {
   if constexpr (L == KC) {
     const int row = q * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ (row & 7);
-    return X + (size_t)(r0 + row) * ld + k0 + ch * 8;
+    const size_t src_row = expert ? (size_t)(r0 + row) * re + expert[r0 + row] : (size_t)(r0 + row);
+    return X + src_row * ld + k0 + ch * 8;
   } else {
     const int panel = q >> 4;
     const int kr = ((q & 15) << 2) + (lane >> 4);
@@ -241,14 +243,14 @@ struct Stager {
   int dst[G::NPER];
   int adv[G::NPER];   // elements to advance per K tile
   __device__ __forceinline__ void init(const uint16_t* Pm, int ldp, const uint16_t* Qm, int ldq, int i0, int j0,
-                                       int wave, int lane) {
+                                       int wave, int lane, const long* pexp, int pe) {
 #pragma unroll
     for (int it = 0; it < G::NPER; ++it) {
       int q = wave + it * G::NW;
       q = q < G::P ? q : G::P - 1;
       const bool isA = q < G::PA;
       const int qq = isA ? q : q - G::PA;
-      const uint16_t* sa = piece_src<G::LA>(Pm, ldp, i0, 0, isA ? qq : 0, lane);
+      const uint16_t* sa = piece_src<G::LA>(Pm, ldp, i0, 0, isA ? qq : 0, lane, pexp, pe);
       const uint16_t* sb = piece_src<G::LB>(Qm, ldq, j0, 0, isA ? 0 : qq, lane);
       src[it] = isA ? sa : sb;
       dst[it] = isA ? q * 1024 : G::A_BYTES + qq * 1024;
@@ -274,6 +276,8 @@ struct Args {
   int ldc;
   const uint16_t* bias; // EPI_BF16: per output column j, nullable
   NmseArgs na;          // EPI_NMSE
+  const long* pexp;     // nullable: row i of P is P[i * pe + pexp[i]] (KC P only: expert-routed rows)
+  int pe;
 };
 
 // tile order: blocks b, b+8, ... share an XCD; each XCD takes whole GM x GN tile groups (row-major
@@ -315,7 +319,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   constexpr int NS = G::NSTAGE;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   Stager<G> stg;
-  stg.init(a.P, a.ldp, a.Q, a.ldq, i0, j0, __builtin_amdgcn_readfirstlane(wave), lane);
+  stg.init(a.P, a.ldp, a.Q, a.ldq, i0, j0, __builtin_amdgcn_readfirstlane(wave), lane, a.pexp, a.pe);
   Readers<G> rd;
   rd.ra.init(0, wm * G::MF * 16, fr, fq);
   rd.rb.init(G::A_BYTES, wn * G::NJ * 16, fr, fq);
@@ -527,10 +531,12 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   return 0;
 }
 
-// Y = A W^T (+ bias) bf16: A (M, K), W (N, K), Y (M, N), all row-major
+// Y = A W^T (+ bias) bf16: A (M, K), W (N, K), Y (M, N), all row-major.  expert (nullable, (M,) int64,
+// values < E): row i of the product uses A[i * E + expert[i]] -- the test-time routing's expert selection
+// (Test.py:166-214) fused into the operand loads, A holding every expert's features per sample.
 QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t* bias, uint16_t* Y, int M, int N,
-                            int K, int cfg, void* stream) {
-  Args a{A, W, K, K, M, N, K, Y, N, bias, {}};
+                            int K, int cfg, const long* expert, int E, void* stream) {
+  Args a{A, W, K, K, M, N, K, Y, N, bias, {}, expert, E};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
   if (M % FwdA::BM) return (int)hipErrorInvalidValue;
@@ -549,7 +555,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   if (M != U * B * E || E < 1 || E > 4) return (int)hipErrorInvalidValue;
   NmseArgs na{label, perf, rowoff, reinterpret_cast<const float2*>(rowden), dY, part, colsum, dens, E, U, B,
               loss_scale};
-  Args a{A, W, K, K, M, N, K, nullptr, N, bias, na};
+  Args a{A, W, K, K, M, N, K, nullptr, N, bias, na, nullptr, 0};
   hipStream_t st = (hipStream_t)stream;
   const int bm = cfg == 1 ? FwdB::BM : FwdA::BM;
   if (M % bm || (bm / (B * E) + 2) * E > 64 || B % 16 || bm % (16 * E)) return (int)hipErrorInvalidValue;
@@ -560,7 +566,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
 // dW (N, K) fp32 = dY^T A: dY (M, N) bf16, A (M, K) bf16 row-major; reduction over M
 QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M, int N, int K, int ldw, int cfg,
                          void* stream) {
-  Args a{dY, A, N, K, N, K, M, dW, ldw, nullptr, {}};
+  Args a{dY, A, N, K, N, K, M, dW, ldw, nullptr, {}, nullptr, 0};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<WgrB, EPI_F32, 2, 8>(a, st);
   return launch<WgrA, EPI_F32, 2, 8>(a, st);
@@ -569,7 +575,7 @@ QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M
 // dA (M, K) bf16 = dY W: dY (M, N) bf16, W (N, K) bf16 row-major; reduction over N
 QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, int M, int N, int K, int cfg,
                          void* stream) {
-  Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}};
+  Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}, nullptr, 0};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<DgrB, EPI_BF16, 4, 8>(a, st);
   return launch<DgrA, EPI_BF16, 4, 4>(a, st);

@@ -589,3 +589,60 @@ QD_API int qd_qsc_head(const float* E, const float* wc, const float* bc, const l
 #undef QD_HEAD
   return (int)hipErrorInvalidValue;
 }
+
+// Inference head (eval / Test.py routing): per sample, logits = Wc E + bc -> log_softmax (logp, nullable)
+// and the argmax (pred, nullable).  A thread per sample (the training head above is one workgroup: it
+// also reduces the weight gradients).
+namespace qd {
+namespace qsc {
+template <int N, int C>
+__global__ void __launch_bounds__(256) qsc_infer_head_kernel(const float* __restrict__ E, const float* __restrict__ wc,
+                                                             const float* __restrict__ bc, float* __restrict__ logp,
+                                                             long* __restrict__ pred, int B) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  float e[N], lg[C], mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < N; ++j) e[j] = E[(size_t)b * N + j];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    float s = bc[c];
+#pragma unroll
+    for (int j = 0; j < N; ++j) s += wc[c * N + j] * e[j];
+    lg[c] = s;
+    mx = fmaxf(mx, s);
+  }
+  float se = 0.f;
+  int am = 0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    se += __expf(lg[c] - mx);
+    if (lg[c] > lg[am]) am = c;
+  }
+  const float lse = mx + __logf(se);
+  if (logp) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) logp[(size_t)b * C + c] = lg[c] - lse;
+  }
+  if (pred) pred[b] = am;
+}
+}  // namespace qsc
+}  // namespace qd
+
+QD_API int qd_qsc_infer_head(const float* E, const float* wc, const float* bc, float* logp, long* pred, int B, int n,
+                             int C, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (B + 255) / 256;
+#define QD_IH(NN, CC)                                                                                      \
+  if (n == NN && C == CC) {                                                                                \
+    hipLaunchKernelGGL((qd::qsc::qsc_infer_head_kernel<NN, CC>), dim3(grid), dim3(256), 0, s, E, wc, bc, logp, \
+                       pred, B);                                                                           \
+    return (int)hipGetLastError();                                                                         \
+  }
+#define QD_IH_N(NN) QD_IH(NN, 2) QD_IH(NN, 3) QD_IH(NN, 4)
+  QD_IH_N(2) QD_IH_N(3) QD_IH_N(4) QD_IH_N(5) QD_IH_N(6) QD_IH_N(7) QD_IH_N(8) QD_IH_N(9)
+  QD_IH_N(10) QD_IH_N(11) QD_IH_N(12) QD_IH_N(13) QD_IH_N(14) QD_IH_N(15) QD_IH_N(16)
+#undef QD_IH_N
+#undef QD_IH
+  return (int)hipErrorInvalidValue;
+}

@@ -98,18 +98,24 @@ def gemm_tile_m(cfg: int = 0) -> int:
 
 
 def gemm_fwd(A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-             cfg: int = 0) -> torch.Tensor:
-    """Y = A W^T (+ b), bf16 (A (M, K), W (N, K) row-major)."""
+             cfg: int = 0, expert: Optional[torch.Tensor] = None, n_experts: int = 0) -> torch.Tensor:
+    """Y = A W^T (+ b), bf16 (A (M_A, K), W (N, K) row-major).  ``expert`` ((M,) int64, values <
+    ``n_experts``): row i of the product uses A[i * n_experts + expert[i]] -- expert-routed rows, the
+    selection fused into the GEMM's operand loads (A holds every expert's features per sample)."""
     M, K = A.shape
     N = W.shape[0]
+    if expert is not None:
+        assert expert.dtype == torch.int64 and expert.is_contiguous() and expert.device == A.device
+        M = expert.numel()
+        assert A.shape[0] >= M * n_experts
     assert A.dtype == W.dtype == torch.bfloat16 and A.is_contiguous() and W.is_contiguous() and W.shape[1] == K
     assert b is None or (b.dtype == torch.bfloat16 and b.numel() == N and b.is_contiguous())
     if not gemm_fwd_ok(M, N, K, cfg):
         raise ValueError(f"gemm_fwd: shape {(M, N, K)} not supported by cfg {cfg}")
     Y = out if out is not None else torch.empty(M, N, device=A.device, dtype=torch.bfloat16)
-    f = _gemm_fn("qd_gemm_fwd_bias", [_p, _p, _p, _p, _i, _i, _i, _i, _p])
+    f = _gemm_fn("qd_gemm_fwd_bias", [_p, _p, _p, _p, _i, _i, _i, _i, _p, _i, _p])
     nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(b) if b is not None else None, nat.ptr(Y), M, N, K, cfg,
-                nat.stream_ptr(A.device)), "gemm_fwd_bias")
+                nat.ptr(expert) if expert is not None else None, n_experts, nat.stream_ptr(A.device)), "gemm_fwd_bias")
     return Y
 
 

@@ -188,6 +188,28 @@ class QSCStepHIP:
                              st), "qsc_head")
         self._w_cur = w
 
+    @torch.no_grad()
+    def infer(self, x: torch.Tensor, pred: Optional[torch.Tensor] = None,
+              logp: Optional[torch.Tensor] = None) -> None:
+        """Inference on the HIP kernels (x.shape[0] == B): preprocess CNN, the circuit with the clean
+        master weights (no QuantumNAT noise), then a thread-per-sample head -> log-probabilities (B, C)
+        and / or the argmax (B,) int64."""
+        m = self.m
+        B, n, L = self.B, self.n, self.L
+        assert x.shape[0] == B and x.is_contiguous() and self.impl == "mfma"
+        st = nat.stream_ptr(x.device)
+        nat.check(self._fwd2(nat.ptr(x), nat.ptr(self.space.flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
+                             *self._saved(), B, n, self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
+        w = m.qlayer.weights.detach().contiguous()
+        extra = (nat.ptr(self.qws) if self.qws is not None else None,
+                 nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
+            (nat.ptr(self.psave) if self.psave is not None else None,)
+        nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, 0, *extra, st), "qsim_fwd")
+        cls = m.classifier
+        f = nat.fn(nat.hip_lib(), "qd_qsc_infer_head", [_p, _p, _p, _p, _p, _i, _i, _i, _p])
+        nat.check(f(nat.ptr(self.E), nat.ptr(cls.weight), nat.ptr(cls.bias), nat.ptr(logp) if logp is not None else None,
+                    nat.ptr(pred) if pred is not None else None, B, n, self.C, st), "qsc_infer_head")
+
     def backward_part(self, x: torch.Tensor, accumulate: bool = True, slabs: Optional[SlabBatch] = None) -> torch.Tensor:
         m, sp = self.m, self.space
         B, n, L = self.B, self.n, self.L

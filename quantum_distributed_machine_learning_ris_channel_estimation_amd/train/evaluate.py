@@ -108,15 +108,35 @@ class model_val:
         x = pack_pilots(Yp, self.Pilot_num)
         out = {"nmse_ls": float(criterion(pack_channel(HLS), perf)),
                "nmse_mmse": float(criterion(pack_channel(HMMSE), perf))}
+        eng = self._hip_engine(sc, qsc, convs, fc)
         for tag, clf in (("classical", sc), ("quantum", qsc)):
             if clf is None:
                 out[f"nmse_{tag}"], out[f"acc_{tag}"] = float("nan"), float("nan")
                 continue
-            pred = torch.cat([clf(x[i:i + chunk]).argmax(1) for i in range(0, x.shape[0], chunk)])
-            Hhat = estimate_routed(convs, fc, x, pred)
+            if eng is not None:   # the HIP kernels: classifier, experts, routed FC (train/infer.py)
+                if (eng.sc if tag == "classical" else eng.qsc) is not None:
+                    pred = eng.classify(x, tag)
+                else:   # (the classical-fallback QSC ablation: torch)
+                    pred = torch.cat([clf(x[i:i + chunk]).argmax(1) for i in range(0, x.shape[0], chunk)])
+                Hhat = eng.estimate(x, pred)
+            else:
+                pred = torch.cat([clf(x[i:i + chunk]).argmax(1) for i in range(0, x.shape[0], chunk)])
+                Hhat = estimate_routed(convs, fc, x, pred)
             out[f"nmse_{tag}"] = float(criterion(Hhat, perf))
             out[f"acc_{tag}"] = float((pred == ind).float().mean())
         return out
+
+    def _hip_engine(self, sc, qsc, convs, fc):
+        """The HIP inference engine for these models (GPU; None on the CPU, or with QDML_EVAL_TORCH=1)."""
+        if self.device.type != "cuda" or os.environ.get("QDML_EVAL_TORCH") == "1":
+            return None
+        key = (id(sc), id(qsc), tuple(id(c) for c in convs), id(fc))
+        if getattr(self, "_eng_key", None) != key:
+            from .infer import HIPInference
+            self._eng = HIPInference(convs, fc, self.Pilot_num, self.device, sc=sc,
+                                     qsc=qsc if (qsc is not None and qsc.use_quantum) else None)
+            self._eng_key = key
+        return self._eng
 
     def test_for_CE_P128_for_all_scenarios(self):
         sc, qsc, convs, fc = self.load_models()
