@@ -23,6 +23,8 @@ def plot_fig1(res: Dict, path: str) -> None:
     plt.subplot(1, 2, 1)
     plt.plot(snr, res["NMSE_LS_dB"], "k--", linewidth=2, marker="o", markersize=8, label="LS Algorithm")
     plt.plot(snr, res["NMSE_MMSE_dB"], "r--", linewidth=2, marker="s", markersize=8, label="MMSE Algorithm")
+    if "NMSE_LMMSE_dB" in res:
+        plt.plot(snr, res["NMSE_LMMSE_dB"], "m:", linewidth=2, marker="x", markersize=8, label="LMMSE (Wiener)")
     plt.plot(snr, res["NMSE_HDCE_Classical_dB"], "b-", linewidth=3, marker="^", markersize=10,
              label="HDCE (Classical SC)")
     if any(v == v for v in res["NMSE_HDCE_Quantum_dB"]):

@@ -68,7 +68,7 @@ def main():
             mv.test_for_CE_P128_for_all_scenarios()
             res = mv.results
             db = lambda xs: [round(10 * __import__("math").log10(x), 2) for x in xs]
-            rec[tag] = {"ls": db(res["nmse_ls"]), "mmse": db(res["nmse_mmse"]), "hdce": db(res["nmse_classical"]),
+            rec[tag] = {"ls": db(res["nmse_ls"]), "mmse": db(res["nmse_mmse"]), "lmmse": db(res["nmse_lmmse"]), "hdce": db(res["nmse_classical"]),
                         "acc": [round(x, 4) for x in res["acc_classical"]]}
         rec["seconds"] = round(time.time() - t0, 1)
         print(json.dumps(rec), flush=True)
