@@ -97,6 +97,9 @@ class EvalConfig:
     seed: int = 1234
     device: str = "auto"
     backend: str = "auto"
+    # test-time BN adaptation: re-estimate each expert's BN statistics on the test pilots routed to it
+    # (unsupervised; the reference keeps the 10 dB training statistics -- reports/r2_hdce_snr.md)
+    bn_adapt: bool = False
 
     def update_from_dict(self, d: Dict[str, Any]) -> "EvalConfig":
         names = {f.name for f in dataclasses.fields(self)}

@@ -32,6 +32,41 @@ from . import checkpoint as ck
 from .engine import estimate_routed
 
 
+@torch.no_grad()
+def recalibrate_bn(convs, x: torch.Tensor, expert: torch.Tensor, chunk: int = 4096) -> list:
+    """Re-estimate every expert's BN running statistics (cumulative average over the inputs routed to it);
+    returns the previous statistics for ``restore_bn``.  An expert that receives no input keeps its own."""
+    saved = []
+    for e, conv in enumerate(convs):
+        bns = [m for m in conv.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+        saved.append([(m.momentum, m.running_mean.clone(), m.running_var.clone(), m.num_batches_tracked.clone())
+                      for m in bns])
+        xe = x[expert == e]
+        if xe.shape[0] < 2:
+            continue
+        for m in bns:
+            m.reset_running_stats()
+            m.momentum = None
+        was = conv.training
+        conv.train()
+        for s in range(0, xe.shape[0], chunk):
+            if xe.shape[0] - s >= 2:
+                conv(xe[s:s + chunk].float())
+        conv.train(was)
+    return saved
+
+
+@torch.no_grad()
+def restore_bn(convs, saved: list) -> None:
+    for conv, st in zip(convs, saved):
+        bns = [m for m in conv.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+        for m, (mom, rm, rv, nb) in zip(bns, st):
+            m.momentum = mom
+            m.running_mean.copy_(rm)
+            m.running_var.copy_(rv)
+            m.num_batches_tracked.copy_(nb)
+
+
 def _epoch_file(d: str, pattern_fmt: str, prefer: str) -> Optional[str]:
     """The reference hard-codes 'epoch99'; fall back to the latest epoch present."""
     p = os.path.join(d, pattern_fmt.format(tag=prefer))
@@ -117,15 +152,19 @@ class model_val:
             if clf is None:
                 out[f"nmse_{tag}"], out[f"acc_{tag}"] = float("nan"), float("nan")
                 continue
-            if eng is not None:   # the HIP kernels: classifier, experts, routed FC (train/infer.py)
-                if (eng.sc if tag == "classical" else eng.qsc) is not None:
-                    pred = eng.classify(x, tag)
-                else:   # (the classical-fallback QSC ablation: torch)
-                    pred = torch.cat([clf(x[i:i + chunk]).argmax(1) for i in range(0, x.shape[0], chunk)])
+            if eng is not None and (eng.sc if tag == "classical" else eng.qsc) is not None:
+                pred = eng.classify(x, tag)   # the HIP kernels: classifier, experts, routed FC (train/infer.py)
+            else:   # (CPU, or the classical-fallback QSC ablation: torch)
+                pred = torch.cat([clf(x[i:i + chunk]).argmax(1) for i in range(0, x.shape[0], chunk)])
+            saved = recalibrate_bn(convs, x, pred) if self.bn_adapt else None
+            if eng is not None:
+                if saved is not None:
+                    eng.load_bn_stats(convs)
                 Hhat = eng.estimate(x, pred)
             else:
-                pred = torch.cat([clf(x[i:i + chunk]).argmax(1) for i in range(0, x.shape[0], chunk)])
                 Hhat = estimate_routed(convs, fc, x, pred)
+            if saved is not None:
+                restore_bn(convs, saved)
             out[f"nmse_{tag}"] = float(criterion(Hhat, perf))
             out[f"acc_{tag}"] = float((pred == ind).float().mean())
         return out

@@ -71,6 +71,17 @@ class HIPInference:
         self._gather = nat.fn(nat.hip_lib(), "qd_gather_step", [_p, _p, _l, _p, _p, _p, _l, _i, _i, _i, _i, _p])
         self._plane = plane
 
+    @torch.no_grad()
+    def load_bn_stats(self, convs: Sequence[nn.Module]) -> None:
+        """Refresh the experts' BN running statistics (views into the grouped buffers the conv kernels
+        read) from ``convs``, e.g. after a test-time BN re-estimation."""
+        for e in range(self.E):
+            src = [m for m in convs[e].modules() if isinstance(m, nn.BatchNorm2d)]
+            dst = [m for m in self.model.convs[e].modules() if isinstance(m, nn.BatchNorm2d)]
+            for d, s_ in zip(dst, src):
+                d.running_mean.copy_(s_.running_mean)
+                d.running_var.copy_(s_.running_var)
+
     def _load(self, x: torch.Tensor, lo: int, n: int) -> None:
         """Samples x[lo:lo+n] -> the classifier input (xq) and the experts-in-channels conv input (x1); the
         chunk's tail (n < chunk) repeats sample lo (its outputs are dropped)."""

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--out", default="reports")
     ap.add_argument("--workspace", default="./workspace")
+    ap.add_argument("--bn-adapt", action="store_true", help="also run the sweep with test-time BN re-estimation "
+                    "(written under <out>/bn_adapt)")
     a = ap.parse_args()
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.evaluate import model_val
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.runner import Y2HRunner
@@ -55,7 +57,19 @@ def main():
     mv.epoch_tag = f"epoch{a.epochs - 1}"
     t0 = time.time()
     mv.test_for_CE_P128_for_all_scenarios()
-    print(json.dumps({"eval_s": time.time() - t0, **t}))
+    t["eval_s"] = time.time() - t0
+    if a.bn_adapt:
+        mva = model_val(workspace=a.workspace, results_dir=os.path.join(a.out, "bn_adapt"), data_len_for_test=a.test_len,
+                        training_data_len=a.data_len, batch_size_DML=a.batch, n_qubits=a.qubits, bn_adapt=True)
+        mva.epoch_tag = mv.epoch_tag
+        t0 = time.time()
+        mva.test_for_CE_P128_for_all_scenarios()
+        t["eval_bn_adapt_s"] = time.time() - t0
+    summary = {**{k: round(v, 2) for k, v in t.items()},
+               "eval_engine": "torch" if os.environ.get("QDML_EVAL_TORCH") == "1" else "hip"}
+    with open(os.path.join(a.out, "run_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps(summary))
 
 
 if __name__ == "__main__":
