@@ -222,7 +222,9 @@ class FlagshipTrainer:
         #   replayed concurrently in qsc / full) the QSC weights drift from the serial run by ~1e-5
         #   after a few steps in most trials (scripts/dbg_dagi.py), although every QSC kernel is
         #   bit-reproducible under concurrent load on its own (scripts/dbg_qsc_race.py) and the chains
-        #   share no buffer (cursors and NaN flags sit on separate cache lines).  dagq (QSC forked and
+        #   share no buffer (cursors and NaN flags sit on separate cache lines).  Localised and bounded
+        #   in docs/CONCURRENCY.md: the simulator forward computes 1-3 samples from stale inputs although
+        #   its producer finished microseconds earlier; not the step-counter protocol, not a stray write.  dagq (QSC forked and
         #   joined every step) and the serial graphs match the eager run bit for bit; dagi was ~1.5%
         #   faster (profiles/r1_15_dagi_sweeps.md), not worth an unexplained non-reproducibility
         #   qsc    : the QSC branch is its own graph replayed on its own stream; HDCE one serial graph

@@ -21,7 +21,7 @@ for s in $STEPS; do
   case $s in
     build) run build 600 python __graft_entry__.py build ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
-    pytest) run pytest 900 python -m pytest tests -m gpu -q ;;
+    pytest) run pytest 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps ${BENCH_STEPS:-50} --warmup 10 ;;
     bench_eager) run bench_eager 600 python bench.py --steps 20 --warmup 5 --no-graphs ;;
     bench_p256) run bench_p256 600 python bench.py --steps 20 --warmup 5 --pilot 256 --qubits 12 ;;

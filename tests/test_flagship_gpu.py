@@ -72,6 +72,30 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k, phase):
     assert float(ref.hopt.step_t[0]) == 4.0 and bool((dag.hopt.step_t == 4.0).all())
 
 
+@pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1)])
+def test_shipped_plans_bit_exact_over_12_steps(cuda, mode, split, k):
+    """The plans bench.py / the DP path run -- dagq (QSC branch forked and joined every step, k steps per
+    replay) and the 5-graph data-parallel plan -- reproduce the serial eager run BIT FOR BIT over 12
+    steps, in every one of 3 fresh trainer pairs (docs/CONCURRENCY.md: the independent-chains plan dagi
+    does not, in 10-25 of 25 trials on the boxes measured)."""
+    ctx = DistContext(device=cuda)
+    base = dict(batch=32, data_len=800, use_quantumnat=True, qsc_grid_bwd=128)
+    for trial in range(3):
+        ref = FlagshipTrainer(FlagshipConfig(hip_graphs=False, stream_mode="serial", **base), ctx)
+        dag = FlagshipTrainer(FlagshipConfig(hip_graphs=True, stream_mode=mode, split_graphs=split,
+                                             steps_per_graph=k, **base), ctx)
+        dag.capture(preserve=True, k=k)
+        for rep in range(12 // k):
+            for _ in range(k):
+                ref.step()
+            dag.run(k)
+            torch.cuda.synchronize()
+            for i, (a, b) in enumerate(zip(_all_state(ref), _all_state(dag))):
+                b = b[:a.numel()] if b.numel() != a.numel() else b
+                assert torch.equal(a, b), (trial, rep, i, float((a.float() - b.float()).abs().max()))
+        assert torch.equal(ref.qloss, dag.qloss) and torch.equal(ref.hloss, dag.hloss)
+
+
 @pytest.mark.parametrize("plan", ["zero", "allreduce"])
 def test_dp_plan_two_ranks_on_one_gpu(tmp_path, plan):
     """The DP execution plan on the GPU (4 graphs, side streams, async bucketed all-reduces) with 2 ranks
