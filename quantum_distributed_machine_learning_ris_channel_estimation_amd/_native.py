@@ -89,6 +89,11 @@ def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
              "-Wno-unused-result", "-I", os.path.join(CSRC, "hip")]
     flags += os.environ.get("QDML_HIPCC_EXTRA", "").split()   # (tuning sweeps: e.g. -DQD_CINP_PAD=16)
+    # a changed flag set (a tuning build, then the default again) rebuilds every object
+    stamp = os.path.join(OBJ_DIR, "flags.txt")
+    want = " ".join(f for f in flags if not f.startswith("/"))   # (not the include path: the tree moves)
+    if not force and (not os.path.exists(stamp) or open(stamp).read() != want):
+        force = True
     objs = []
 
     def one(src: str) -> str:
@@ -101,6 +106,8 @@ def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
         objs = list(ex.map(one, srcs))
     if force or _stale(HIP_LIB, objs):
         _run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", HIP_LIB] + objs, verbose)
+    with open(stamp, "w") as f:
+        f.write(want)
     return HIP_LIB
 
 

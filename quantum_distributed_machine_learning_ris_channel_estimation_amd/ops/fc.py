@@ -1,14 +1,9 @@
-"""Hand-written MFMA FC_P128 GEMM (csrc/hip/fc_gemm.hip) with the HDCE loss fused into its epilogue.
+"""Hand-written MFMA FC_P128 GEMMs (csrc/hip/gemm.hip): the training forward with the HDCE loss fused
+into its epilogue (dY, per-row error partials, bias-gradient partials; Y never written), the weight
+and data gradients, and the inference forward (bias, optional expert-routed rows).
 
 Reference: FC_P128 (Estimators_QuantumNAT_onchipQNN.py:272-279) + NMSE_cuda (E:282-286) per stream
 (Runner_P128_QuantumNAT_onchipQNN.py:109-113, 194-199).
-
-``fc_linear(A, W, b)``             Y = A W^T + b, bf16 (tile 144 x 128, one workgroup per CU)
-``FcNmse(...)(A, W, b, ...)``      the training forward: the GEMM epilogue turns the accumulator
-                                   straight into dY = 2 (Y - L) / (S den_s) (bf16), per-row error
-                                   partials and per-tile bias-gradient partials; one small finish
-                                   launch forms loss / loss_perf / the NaN flag / the bias gradient.
-                                   Y is never written to memory.
 """
 from __future__ import annotations
 
@@ -21,69 +16,6 @@ from .. import _native as nat
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
-
-def tile_m(M: int, N: int, K: int) -> int:
-    """M tile the kernel uses for this shape (144 or 128), 0 if unsupported."""
-    return int(nat.fn(nat.hip_lib(), "qd_fc_gemm_tile_m", [_i, _i, _i])(M, N, K))
-
-
-def fc_linear(A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    M, K = A.shape
-    N = W.shape[0]
-    assert A.dtype == W.dtype == torch.bfloat16 and A.is_contiguous() and W.is_contiguous() and W.shape[1] == K
-    assert b is None or (b.dtype == torch.bfloat16 and b.numel() == N and b.is_contiguous())
-    if not tile_m(M, N, K):
-        raise ValueError(f"fc_linear: shape {(M, N, K)} not supported")
-    Y = out if out is not None else torch.empty(M, N, device=A.device, dtype=torch.bfloat16)
-    f = nat.fn(nat.hip_lib(), "qd_fc_gemm_bias", [_p, _p, _p, _p, _i, _i, _i, _p])
-    nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(b) if b is not None else None, nat.ptr(Y), M, N, K,
-                nat.stream_ptr(A.device)), "fc_gemm_bias")
-    return Y
-
-
-class FcNmse:
-    """FC forward + per-stream NMSE loss + dY + bias gradient for rows in (u, b, e) order.
-
-    ``layout`` = (E, U, B); labels (S, N_store, cols) read in place through ``rowoff`` (int32, one
-    store row per output row); ``rowden`` (M, 2) fp32 per-row label / perf powers (ops/gather.py)."""
-
-    def __init__(self, M: int, N: int, K: int, layout, device):
-        self.M, self.N, self.K = M, N, K
-        self.E, self.U, self.B = layout
-        assert M == self.E * self.U * self.B
-        self.tm = tile_m(M, N, K)
-        if not self.tm:
-            raise ValueError(f"FcNmse: shape {(M, N, K)} not supported")
-        S = self.E * self.U
-        self.dY = torch.empty(M, N, device=device, dtype=torch.bfloat16)
-        self.rowpart = torch.empty(M, N // 128, 2, device=device)
-        self.colpart = torch.empty(M // self.tm, N, device=device)
-        self.ss = torch.zeros(S, 4, device=device)
-        self._f = nat.fn(nat.hip_lib(), "qd_fc_gemm_nmse", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
-                                                            _i, _i, _i, _i, _i, _i, _f, _p])
-
-    @staticmethod
-    def supported(M: int, N: int, K: int) -> bool:
-        return bool(tile_m(M, N, K)) and N % 64 == 0
-
-    def __call__(self, A, W, b, label, perf, rowoff, rowden, bias_grad, loss, skip, loss_scale: float = 1.0):
-        assert A.shape == (self.M, self.K) and W.shape == (self.N, self.K)
-        assert A.dtype == W.dtype == torch.bfloat16 and A.is_contiguous() and W.is_contiguous()
-        assert label.dtype == torch.float32 and label.stride(-1) == 1 and label.shape[-1] == self.N
-        assert rowoff.dtype == torch.int32 and rowoff.numel() == self.M and rowden.shape == (self.M, 2)
-        nat.check(self._f(nat.ptr(A), nat.ptr(W), nat.ptr(b) if b is not None else None, nat.ptr(label),
-                          nat.ptr(perf) if perf is not None else None, nat.ptr(rowoff), nat.ptr(rowden),
-                          nat.ptr(self.dY), nat.ptr(self.rowpart), nat.ptr(self.colpart), nat.ptr(bias_grad),
-                          nat.ptr(self.ss), nat.ptr(loss), nat.ptr(skip) if skip is not None else None,
-                          self.M, self.N, self.K, self.E, self.U, self.B, loss_scale, nat.stream_ptr(A.device)),
-                  "fc_gemm_nmse")
-        return self.dY
-
-
-# ---------------------------------------------------------------------------------------------------
-# csrc/hip/gemm.hip: the hand-written forward / weight-gradient / data-gradient GEMMs of FC_P128
-# (cfg selects a tile configuration; 0 = the default chosen by measurement, see gemm.hip's header)
 
 def _gemm_fn(name, argtypes):
     return nat.fn(nat.hip_lib(), name, argtypes)

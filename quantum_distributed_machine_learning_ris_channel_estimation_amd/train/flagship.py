@@ -231,7 +231,7 @@ class FlagshipTrainer:
         #   full   : as qsc, and the HDCE graph has its fc / conv side branches
         #   !! qsc / full are kept for diagnosis only: on ROCm 7.x two graphs replayed CONCURRENTLY on two
         #   streams gave wrong QSC gradients (each graph alone, or both serialised, or the same work as
-        #   branches of ONE graph are bit-exact; scripts/dbg_split.py) -- use dag / dagq
+        #   branches of ONE graph are bit-exact; scripts/dbg_bisect.py qsc) -- use dag / dagq
         # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge
         # that crosses queues costs a barrier packet, so fewer, longer branches can win)
         mode = cfg.stream_mode

@@ -57,7 +57,6 @@ for s in $STEPS; do
     fp8probe) run fp8probe 300 python scripts/probe_fp8.py ;;
     fcprobe) run fcprobe 300 python scripts/probe_fc_gemm.py ;;
     nmseprobe) run nmseprobe 300 python scripts/probe_nmse.py ;;
-    fchand) run fchand 300 python scripts/probe_fc_hand.py ;;
     tunegemm) run tunegemm 900 python scripts/tune_gemm.py --out "$OUT/tunableop_gfx950.csv" ;;
     diag) run diag 900 python scripts/diag_hdce.py --epochs ${DIAG_EPOCHS:-20} ;;
     gensweep) run gensweep 1500 python scripts/gen_sweep.py --epochs ${SWEEP_EPOCHS:-30} --sc-epochs 8 ;;
