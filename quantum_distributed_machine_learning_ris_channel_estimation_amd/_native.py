@@ -76,7 +76,9 @@ def hipcc() -> Optional[str]:
 
 # gemm.hip: MFMA accumulators in VGPRs (the default AGPR form made hipcc shuttle the 18-36 accumulator
 # tiles between the register files every K step)
-PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+# qsim_stream.hip: no SLP vectorisation (packed-f32 pairs of the complex gate math doubled the register
+# demand: the adjoint passes spilled at 256 VGPRs, 86-92 without)
+PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "qsim_stream.hip": ["-fno-slp-vectorize"]}
 
 
 def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:

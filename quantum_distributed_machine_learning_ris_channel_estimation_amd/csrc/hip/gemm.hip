@@ -78,9 +78,15 @@ struct NmseArgs {
 
 // DBG (diagnosis builds, scripts/probe_gemm.py): 1 = no global loads in the K loop (MFMAs on whatever the
 // stages hold), 2 = no MFMAs (loads and LDS reads only)
-template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int DBG_ = 0>
+// F8: OCP e4m3 operands (KC x KC only).  The kernel still moves 2-byte "elements" (a row of K e4m3
+// values is K / 2 of them), so staging, LDS images and fragment reads are the bf16 ones unchanged; each
+// 16-byte fragment holds 16 k and feeds TWO mfma_f32_16x16x32_fp8_fp8 (its low and high 8 bytes).  The
+// k order this implies is the same permutation for A and B, so the dot products are exact sums over K.
+template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int DBG_ = 0, int F8_ = 0>
 struct Geo {
   static constexpr int MF = MF_, NJ = NJ_, WM = WM_, WN = WN_, LA = LA_, LB = LB_, NSTAGE = NSTAGE_, DBG = DBG_;
+  static constexpr int F8 = F8_;
+  static_assert(!F8 || (LA == KC && LB == KC), "e4m3 operands: k-contiguous layouts");
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int BM = 16 * MF * WM, BN = 16 * NJ * WN;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -224,8 +230,16 @@ struct Readers {
       lgkm_wait<READ ? ALLOW : (G::MF - 1 - I) * RA>();
 #pragma unroll
       for (int j = 0; j < G::NJ; ++j)
-        if constexpr (G::DBG == 2) asm volatile("" ::"v"(cur.a[I]), "v"(cur.b[j]));
-        else acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.a[I], cur.b[j], acc[I][j], 0, 0, 0);
+        if constexpr (G::DBG == 2) {
+          asm volatile("" ::"v"(cur.a[I]), "v"(cur.b[j]));
+        } else if constexpr (G::F8) {
+          typedef __attribute__((ext_vector_type(2))) long l2;
+          const l2 av = __builtin_bit_cast(l2, cur.a[I]), bv = __builtin_bit_cast(l2, cur.b[j]);
+          acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av.x, bv.x, acc[I][j], 0, 0, 0);
+          acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(av.y, bv.y, acc[I][j], 0, 0, 0);
+        } else {
+          acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.a[I], cur.b[j], acc[I][j], 0, 0, 0);
+        }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (READ) nxt.a[I] = ra.template frag<I>(st, s);
       mma_read<READ, I + 1>(acc, cur, nxt, st, s);
@@ -278,6 +292,7 @@ struct Args {
   NmseArgs na;          // EPI_NMSE
   const long* pexp;     // nullable: row i of P is P[i * pe + pexp[i]] (KC P only: expert-routed rows)
   int pe;
+  const float* deq;     // nullable: (2,) dequantisation scales; the accumulators are multiplied by their product
 };
 
 // tile order: blocks b, b+8, ... share an XCD; each XCD takes whole GM x GN tile groups (row-major
@@ -355,13 +370,14 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   __syncthreads();   // (every wave is done with the stage ring: it becomes the fp32 tile)
   float* ct = reinterpret_cast<float*>(smem);
   constexpr int PITCH = G::PITCH;
+  const float dq = a.deq ? a.deq[0] * a.deq[1] : 1.f;
 #pragma unroll
   for (int j = 0; j < G::NJ; ++j) {
     const int cl = (wn * G::NJ + j) * 16 + fr;
 #pragma unroll
     for (int i = 0; i < G::MF; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ct[((wm * G::MF + i) * 16 + fq * 4 + r) * PITCH + cl] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) ct[((wm * G::MF + i) * 16 + fq * 4 + r) * PITCH + cl] = acc[i][j][r] * dq;
   }
   __syncthreads();
   constexpr int VEC = G::BN / 64;   // columns per lane in a row pass (2 or 4)
@@ -514,6 +530,7 @@ using DgrA = Geo<9, 4, 1, 4, KC, MC, 3>;
 using DgrB = Geo<9, 2, 1, 4, KC, MC, 4>;
 using WgrA = Geo<8, 4, 1, 4, MC, MC, 3>;
 using WgrB = Geo<4, 4, 2, 4, MC, MC, 3>;
+using FwdA8 = Geo<9, 2, 1, 4, KC, KC, 4, 0, 1>;   // e4m3 forward: the FwdA geometry, 128 k per stage
 
 }  // namespace gemm
 }  // namespace qd
@@ -536,7 +553,7 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
 // (Test.py:166-214) fused into the operand loads, A holding every expert's features per sample.
 QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t* bias, uint16_t* Y, int M, int N,
                             int K, int cfg, const long* expert, int E, void* stream) {
-  Args a{A, W, K, K, M, N, K, Y, N, bias, {}, expert, E};
+  Args a{A, W, K, K, M, N, K, Y, N, bias, {}, expert, E, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
   if (M % FwdA::BM) return (int)hipErrorInvalidValue;
@@ -555,7 +572,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   if (M != U * B * E || E < 1 || E > 4) return (int)hipErrorInvalidValue;
   NmseArgs na{label, perf, rowoff, reinterpret_cast<const float2*>(rowden), dY, part, colsum, dens, E, U, B,
               loss_scale};
-  Args a{A, W, K, K, M, N, K, nullptr, N, bias, na, nullptr, 0};
+  Args a{A, W, K, K, M, N, K, nullptr, N, bias, na, nullptr, 0, nullptr};
   hipStream_t st = (hipStream_t)stream;
   const int bm = cfg == 1 ? FwdB::BM : FwdA::BM;
   if (M % bm || (bm / (B * E) + 2) * E > 64 || B % 16 || bm % (16 * E)) return (int)hipErrorInvalidValue;
@@ -566,7 +583,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
 // dW (N, K) fp32 = dY^T A: dY (M, N) bf16, A (M, K) bf16 row-major; reduction over M
 QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M, int N, int K, int ldw, int cfg,
                          void* stream) {
-  Args a{dY, A, N, K, N, K, M, dW, ldw, nullptr, {}, nullptr, 0};
+  Args a{dY, A, N, K, N, K, M, dW, ldw, nullptr, {}, nullptr, 0, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<WgrB, EPI_F32, 2, 8>(a, st);
   return launch<WgrA, EPI_F32, 2, 8>(a, st);
@@ -575,8 +592,36 @@ QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M
 // dA (M, K) bf16 = dY W: dY (M, N) bf16, W (N, K) bf16 row-major; reduction over N
 QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, int M, int N, int K, int cfg,
                          void* stream) {
-  Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}, nullptr, 0};
+  Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}, nullptr, 0, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<DgrB, EPI_BF16, 4, 8>(a, st);
   return launch<DgrA, EPI_BF16, 4, 4>(a, st);
+}
+
+// e4m3 forward with the HDCE-loss epilogue: A8 (M, K) e4m3 activations, W8 (N, K) e4m3 weights (both
+// row-major, K bytes per row), deq (2,) their dequantisation scales (the accumulators are scaled by the
+// product before the bias); everything else as qd_gemm_fwd_nmse.
+QD_API int qd_gemm_fwd_nmse_f8(const uint8_t* A8, const uint8_t* W8, const float* deq, const uint16_t* bias,
+                               const float* label, const float* perf, const int* rowoff, const float* rowden,
+                               uint16_t* dY, float* part, float* colsum, float* dens, int M, int N, int K, int E, int U,
+                               int B, float loss_scale, void* stream) {
+  if (M != U * B * E || E < 1 || E > 4 || K % 128 || !deq) return (int)hipErrorInvalidValue;
+  NmseArgs na{label, perf, rowoff, reinterpret_cast<const float2*>(rowden), dY, part, colsum, dens, E, U, B,
+              loss_scale};
+  const int K2 = K / 2;   // 2-byte units of an e4m3 row
+  Args a{reinterpret_cast<const uint16_t*>(A8), reinterpret_cast<const uint16_t*>(W8), K2, K2, M, N, K2, nullptr, N,
+         bias, na, nullptr, 0, deq};
+  if (M % FwdA8::BM || (FwdA8::BM / (B * E) + 2) * E > 64 || B % 16 || FwdA8::BM % (16 * E))
+    return (int)hipErrorInvalidValue;
+  return launch<FwdA8, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
+}
+
+// Y (M, N) bf16 = deq[0] deq[1] A8 W8^T (+ bias): the e4m3 inference / test forward
+QD_API int qd_gemm_fwd_bias_f8(const uint8_t* A8, const uint8_t* W8, const float* deq, const uint16_t* bias,
+                               uint16_t* Y, int M, int N, int K, void* stream) {
+  if (K % 128 || !deq || M % FwdA8::BM) return (int)hipErrorInvalidValue;
+  const int K2 = K / 2;
+  Args a{reinterpret_cast<const uint16_t*>(A8), reinterpret_cast<const uint16_t*>(W8), K2, K2, M, N, K2, Y, N, bias, {},
+         nullptr, 0, deq};
+  return launch<FwdA8, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
 }

@@ -1,0 +1,579 @@
+// Streamed VQC simulator for HBM-resident states (n = 13 .. 16 qubits, L >= 2 layers).
+//
+// Same circuit and adjoint method as csrc/hip/qsim.hip / qsim_big.hip (reference E:125-142: RY
+// angle embedding, L x [RY, RZ on every wire, CNOT ring], <Z_i>).  qsim_big.hip gives each sample ONE
+// 256-thread workgroup that walks its 2^n-amplitude state (512 KiB at n = 16) pass after pass: a few
+// KiB in flight per CU, measured 1.2-1.8 TB/s on the forward and backward of the 16-qubit flagship
+// config (profiles/r2_11_q16_*).  Here every pass is its own launch over ALL samples at once, one
+// workgroup per (sample, 4096-amplitude brick) -- 36,864 workgroups at n = 16, B = 2304 -- so each
+// pass streams the whole batch's state at HBM rate:
+//
+//   pass A   qubits {0..7} u {12..n-1}: the brick is 2^(n-12) runs of 256 contiguous amplitudes
+//            (bits 8..11 fixed = brick index), staged in LDS, rotated three qubits at a time.
+//   pass B   qubits {8..11} + the CNOT ring: the brick is the contiguous tile of bits 0..11 (one
+//            thread owns the 16 amplitudes that differ in bits 8..11: the 4 rotations stay in
+//            registers).  The ring f is GF(2)-linear (bit j of f(k) = parity of bits 0..j, bit 0 =
+//            parity of bits 1..n-1), so f maps a tile onto exactly TWO runs of 2048 contiguous
+//            amplitudes (selected by bit 11 of the image): the permutation is an LDS scatter, and
+//            every global load and store of both passes is coalesced.
+//
+// Forward (L layers): pass A of layer 1 GENERATES its input (the ring image of the layer-0 product
+// state) instead of loading it, then B, A, B, ...; the last pass B stores psi_final (kept for the
+// backward) and per-tile <Z_q> partials.  Backward: per layer in reverse, pass B (gather at the
+// ring image, undo rotations 11..8 with d(theta), d(phi) partials) and pass A (undo the rest; layer 0
+// stores nothing).  lambda = (sum_q g_q Z_q) psi is formed while loading the first pass.  Gradient
+// partials go to a slab of 16 rows per sample (every column written once per row): the caller's
+// slab reduction sums them; dx = the layer-0 theta columns, reduced per sample here.
+//
+// State traffic at n = 16, L = 3: forward 7 state passes (1 write + 3 read/write pairs), backward
+// 19 (both psi and lambda) -- vs the per-sample kernel's ~7 and ~26 passes at a third of the rate.
+#include "common.h"
+
+namespace qd {
+namespace qstream {
+
+struct cf {
+  float x, y;
+};
+__device__ __forceinline__ cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+
+constexpr int NT = 256;
+constexpr int NWV = NT / 64;
+constexpr int ROWS = 16;   // slab rows (workgroups of pass A) per sample
+
+
+template <int N>
+struct SG {
+  static constexpr int HB = N - 12;        // bits above the 4096-amplitude tile
+  static constexpr int D = 1 << N;
+  static constexpr int AB = 8 + HB;        // pass-A brick bits (qubits 0..7 and 12..N-1)
+  static constexpr int AS = 1 << AB;       // pass-A brick size
+  static constexpr int NTILE = 1 << HB;    // pass-B tiles per sample
+  static constexpr int NGRP = (AB + 2) / 3;
+  // threads of the adjoint pass A: one 3-qubit set (8 amplitudes) each, at most 512
+  static constexpr int NTA = AS / 8 < 512 ? AS / 8 : 512;
+  static_assert(N >= 13 && N <= 16, "streamed simulator: 13..16 qubits");
+};
+
+// The CNOT ring f and its inverse in closed form: bit j >= 1 of f(k) is the prefix parity of bits
+// 0..j (a log-step XOR scan), bit 0 is k_0 ^ parity(all); f^-1(j): restore bit 0 (= j_0 ^ j_{n-1}),
+// then k_i = j_i ^ j_{i-1}.
+template <int N>
+__device__ __forceinline__ int ring_fwd(int k) {
+  int p = k ^ (k << 1);
+  p ^= p << 2;
+  p ^= p << 4;
+  p ^= p << 8;
+  p &= (1 << N) - 1;
+  return (p & ~1) | ((k ^ (p >> (N - 1))) & 1);
+}
+template <int N>
+__device__ __forceinline__ int ring_inv(int j) {
+  const int j2 = j ^ ((j >> (N - 1)) & 1);
+  return j2 ^ ((j2 << 1) & ((1 << N) - 1));
+}
+template <int P, int NB>
+__device__ __forceinline__ int ins_bits(int t) {
+  return ((t >> P) << (P + NB)) | (t & ((1 << P) - 1));
+}
+// pass-A brick element e -> state index (brick = bits 8..11)
+__device__ __forceinline__ int brick_k(int e, int br) { return (e & 255) | (br << 8) | ((e >> 8) << 12); }
+// pass-A brick bit -> qubit
+__device__ __forceinline__ constexpr int brick_q(int b) { return b < 8 ? b : b + 4; }
+
+// RZ(phi) RY(theta) on the pair (a0: bit 0, a1: bit 1); t = (cos th/2, sin th/2, cos ph/2, sin ph/2)
+__device__ __forceinline__ void gate_fwd(cf& a0, cf& a1, float4 t) {
+  const cf t0 = {t.x * a0.x - t.y * a1.x, t.x * a0.y - t.y * a1.y};
+  const cf t1 = {t.y * a0.x + t.x * a1.x, t.y * a0.y + t.x * a1.y};
+  a0 = cmul(t0, cf{t.z, -t.w});
+  a1 = cmul(t1, cf{t.z, t.w});
+}
+// adjoint step on psi / lambda AFTER the gate: accumulate d(theta), d(phi), undo the gate on both
+__device__ __forceinline__ void gate_adj(cf& p0, cf& p1, cf& l0, cf& l1, float4 t, float& dth, float& dph) {
+  dph += (l0.x * p0.y - l0.y * p0.x) - (l1.x * p1.y - l1.y * p1.x);
+  p0 = cmul(p0, cf{t.z, t.w});
+  l0 = cmul(l0, cf{t.z, t.w});
+  p1 = cmul(p1, cf{t.z, -t.w});
+  l1 = cmul(l1, cf{t.z, -t.w});
+  dth += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+  const cf q0 = p0, q1 = p1, m0 = l0, m1 = l1;
+  p0 = {t.x * q0.x + t.y * q1.x, t.x * q0.y + t.y * q1.y};
+  p1 = {t.x * q1.x - t.y * q0.x, t.x * q1.y - t.y * q0.y};
+  l0 = {t.x * m0.x + t.y * m1.x, t.x * m0.y + t.y * m1.y};
+  l1 = {t.x * m1.x - t.y * m0.x, t.x * m1.y - t.y * m0.y};
+}
+
+// (cos, sin) of theta/2 and phi/2 of layer l for every qubit of sample s (theta + x at layer 0)
+template <int N>
+__device__ __forceinline__ void load_trig(float4* trig, const float* x, const float* w, int s, int L, int l,
+                                          int wgroup) {
+  if (threadIdx.x < N) {
+    const int q = threadIdx.x;
+    const float* wl = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * N * L : 0) + 2 * N * l;
+    float sn, c, sp, cp;
+    __sincosf(0.5f * (wl[2 * q] + (l == 0 ? x[(size_t)s * N + q] : 0.f)), &sn, &c);
+    __sincosf(0.5f * wl[2 * q + 1], &sp, &cp);
+    trig[q] = make_float4(c, sn, cp, sp);
+  }
+}
+
+// dst[i] = sum over the workgroup of v[i] (thread 0..NV-1 hold the results); red: NWV * NV floats
+template <int NV, int NTH = NT>
+__device__ __forceinline__ void block_sum_vec(const float (&v)[NV], float* red, float* out) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float s = wave_sum(v[i]);
+    if (lane == 0) red[w * NV + i] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NTH / 64; ++k) s += red[k * NV + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+}
+
+// Rotations on bits [LO, LO + NBITS) of an LDS brick of 2^TOT amplitudes, three bits at a time (a
+// thread owns the 2^NB amplitudes differing in a group's bits): forward, or (ADJ) the adjoint sweep
+// in reverse order with gradient partials dth / dph indexed by (bit - LO).  IDQ: bit b is qubit b,
+// else the pass-A map (brick_q).
+template <int TOT, int LO, int NBITS, bool IDQ, bool ADJ, int NTH = NT>
+__device__ __forceinline__ void lds_gates(cf* tp, cf* tq, const float4* trig, float (&dth)[NBITS],
+                                          float (&dph)[NBITS]) {
+  constexpr int NGRP = (NBITS + 2) / 3;
+  static_for<0, NGRP>([&](auto gc) {
+    constexpr int gi = ADJ ? NGRP - 1 - decltype(gc)::value : decltype(gc)::value;
+    constexpr int r0 = 3 * gi;                       // first bit of the group, relative to LO
+    constexpr int g0 = LO + r0;
+    constexpr int NB = (NBITS - r0) < 3 ? (NBITS - r0) : 3;
+    constexpr int ACT = (1 << TOT) >> NB;
+#pragma unroll 1
+    for (int t = threadIdx.x; t < ACT; t += NTH) {
+      const int base = ins_bits<g0, NB>(t);
+      cf p[1 << NB], m[1 << NB];
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) {
+        p[j] = tp[base | (j << g0)];
+        if constexpr (ADJ) m[j] = tq[base | (j << g0)];
+      }
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb) {
+        const int b = ADJ ? NB - 1 - bb : bb;
+        const float4 tg = trig[IDQ ? g0 + b : brick_q(g0 + b)];
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j)
+          if (!((j >> b) & 1)) {
+            if constexpr (ADJ) gate_adj(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[r0 + b], dph[r0 + b]);
+            else gate_fwd(p[j], p[j | (1 << b)], tg);
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) {
+        tp[base | (j << g0)] = p[j];
+        if constexpr (ADJ) tq[base | (j << g0)] = m[j];
+      }
+    }
+    __syncthreads();
+  });
+}
+
+// ------------------------------------------------------------------------------------------ forward
+// pass A of layer l (GEN: layer 1, its input generated: the ring image of the layer-0 product state)
+template <int N, bool GEN>
+__global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x, const float* __restrict__ w, int L,
+                                                 int l, int wgroup, cf* __restrict__ state) {
+  using C = SG<N>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* trig = reinterpret_cast<float4*>(smem);          // 16
+  float4* trig0 = trig + 16;                                 // 16 (GEN)
+  cf* tp = reinterpret_cast<cf*>(smem + 512);
+  const int br = blockIdx.x, s = blockIdx.y;
+  load_trig<N>(trig, x, w, s, L, l, wgroup);
+  if constexpr (GEN) load_trig<N>(trig0, x, w, s, L, 0, wgroup);
+  __syncthreads();
+  cf* st = state + (size_t)s * C::D;
+  if constexpr (GEN) {
+    // product amplitude of basis state k = PL[k & 255] * PH[k >> 8] (tables over 8 / n-8 qubits)
+    cf* PL = tp + C::AS;
+    cf* PH = PL + 256;
+    {
+      const int i = threadIdx.x;   // (NT == 256 entries of each table)
+      cf a = {1.f, 0.f}, h = {1.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 t = trig0[q];
+        a = cmul(a, ((i >> q) & 1) ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
+      }
+#pragma unroll
+      for (int q = 8; q < N; ++q) {
+        const float4 t = trig0[q];
+        h = cmul(h, ((i >> (q - 8)) & 1) ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
+      }
+      PL[i] = a;
+      if (i < (1 << (N - 8))) PH[i] = h;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < C::AS; e += NT) {
+      const int k = ring_inv<N>(brick_k(e, br));
+      tp[e] = cmul(PL[k & 255], PH[k >> 8]);
+    }
+  } else {
+    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NT)
+      *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(st + brick_k(e, br));
+  }
+  __syncthreads();
+  float dth[C::AB], dph[C::AB];
+  lds_gates<C::AB, 0, C::AB, false, false>(tp, nullptr, trig, dth, dph);
+  for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NT)
+    *reinterpret_cast<float4*>(st + brick_k(e, br)) = *reinterpret_cast<const float4*>(tp + e);
+}
+
+// pass B of layer l: qubits 8..11 in registers, the ring as an LDS scatter, two coalesced output runs.
+// LAST: also the per-tile <Z_q> partials epart[(s * NTILE + t) * N + q].
+template <int N, bool LAST>
+__global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x, const float* __restrict__ w, int L,
+                                                 int l, int wgroup, const cf* __restrict__ in, cf* __restrict__ out,
+                                                 float* __restrict__ epart) {
+  using C = SG<N>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* trig = reinterpret_cast<float4*>(smem);
+  float* red = reinterpret_cast<float*>(smem + 256);          // NWV * N floats
+  cf* tp = reinterpret_cast<cf*>(smem + 512);
+  const int t = blockIdx.x, s = blockIdx.y, c = threadIdx.x;
+  load_trig<N>(trig, x, w, s, L, l, wgroup);
+  const cf* src = in + (size_t)s * C::D + ((size_t)t << 12);
+  cf a[16];
+#pragma unroll
+  for (int h = 0; h < 16; ++h) a[h] = src[(h << 8) | c];
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const float4 tg = trig[8 + b];
+#pragma unroll
+    for (int h = 0; h < 16; ++h)
+      if (!((h >> b) & 1)) gate_fwd(a[h], a[h | (1 << b)], tg);
+  }
+#pragma unroll
+  for (int h = 0; h < 16; ++h) tp[ring_fwd<N>((t << 12) | (h << 8) | c) & 4095] = a[h];
+  __syncthreads();
+  const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
+  cf* dst = out + (size_t)s * C::D;
+  float part[N];
+#pragma unroll
+  for (int q = 0; q < N; ++q) part[q] = 0.f;
+  for (int i = 2 * threadIdx.x; i < 4096; i += 2 * NT) {
+    const int j = i | ((i & 2048 ? A1 : A0) << 12);
+    const float4 v = *reinterpret_cast<const float4*>(tp + i);
+    *reinterpret_cast<float4*>(dst + j) = v;
+    if constexpr (LAST) {
+      const float p0 = v.x * v.x + v.y * v.y, p1 = v.z * v.z + v.w * v.w;
+#pragma unroll
+      for (int q = 0; q < N; ++q) {
+        const float z0 = ((j >> q) & 1) ? -p0 : p0;
+        const float z1 = (((j + 1) >> q) & 1) ? -p1 : p1;
+        part[q] += z0 + z1;
+      }
+    }
+  }
+  if constexpr (LAST) {
+    float o[N];
+    block_sum_vec<N>(part, red, o);
+    if (threadIdx.x < N) epart[((size_t)s * C::NTILE + t) * N + threadIdx.x] = o[threadIdx.x];
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(256) reduce_e(const float* __restrict__ epart, float* __restrict__ E, int B) {
+  using C = SG<N>;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * N) return;
+  const int s = i / N, q = i % N;
+  float acc = 0.f;
+  for (int t = 0; t < C::NTILE; ++t) acc += epart[((size_t)s * C::NTILE + t) * N + q];
+  E[i] = acc;
+}
+
+// ----------------------------------------------------------------------------------------- backward
+// Reverse pass B of layer l: gather psi (and lambda, or FIRST: form it from psi and gE) at the ring
+// images, undo rotations 11..8, store tile order.  Slab row s*16 + t*(16/NTILE) gets the 8 partials
+// of qubits 8..11 (the other rows of the tile's group get zeros in those columns).
+template <int N, bool FIRST>
+__global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x, const float* __restrict__ w,
+                                                 const float* __restrict__ gE, int L, int l, int wgroup,
+                                                 const cf* __restrict__ pin, const cf* __restrict__ lin,
+                                                 cf* __restrict__ pout, cf* __restrict__ lout, float* __restrict__ slab) {
+  using C = SG<N>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* trig = reinterpret_cast<float4*>(smem);
+  float* gq = reinterpret_cast<float*>(smem + 256);       // 16
+  float* red = reinterpret_cast<float*>(smem + 320);      // NWV * 8
+  cf* tp = reinterpret_cast<cf*>(smem + 512);
+  cf* tq = tp + 4096;
+  const int t = blockIdx.x, s = blockIdx.y;
+  load_trig<N>(trig, x, w, s, L, l, wgroup);
+  // (FIRST) o(j) = sum_q g_q (1 - 2 bit_q(j)) = OL[j & 255] + OH[j >> 8]
+  float* OL = reinterpret_cast<float*>(tq + 4096);
+  float* OH = OL + 256;
+  if (FIRST && threadIdx.x < N) gq[threadIdx.x] = gE[(size_t)s * N + threadIdx.x];
+  __syncthreads();
+  if constexpr (FIRST) {
+    const int i = threadIdx.x;
+    float ol = 0.f, oh = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ol += ((i >> q) & 1) ? -gq[q] : gq[q];
+#pragma unroll
+    for (int q = 8; q < N; ++q) oh += ((i >> (q - 8)) & 1) ? -gq[q] : gq[q];
+    OL[i] = ol;
+    if (i < (1 << (N - 8))) OH[i] = oh;
+    __syncthreads();
+  }
+  const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
+  const cf* ps = pin + (size_t)s * C::D;
+  const cf* ls = FIRST ? nullptr : lin + (size_t)s * C::D;
+#pragma unroll 2
+  for (int i = threadIdx.x; i < 4096; i += NT) {
+    const int j = i | ((i & 2048 ? A1 : A0) << 12);
+    const int kk = ring_inv<N>(j) & 4095;
+    const cf p = ps[j];
+    cf m;
+    if constexpr (FIRST) {
+      const float o = OL[j & 255] + OH[j >> 8];
+      m = {p.x * o, p.y * o};
+    } else {
+      m = ls[j];
+    }
+    tp[kk] = p;
+    tq[kk] = m;
+  }
+  __syncthreads();
+  // undo rotations 11..8 on the tile in LDS (two groups: bits 11 .. 9, bit 8)
+  float dth[4], dph[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) dth[b] = dph[b] = 0.f;
+  lds_gates<12, 8, 4, true, true>(tp, tq, trig, dth, dph);
+  cf* po = pout + (size_t)s * C::D + ((size_t)t << 12);
+  cf* lo = lout + (size_t)s * C::D + ((size_t)t << 12);
+  for (int i = 2 * threadIdx.x; i < 4096; i += 2 * NT) {
+    *reinterpret_cast<float4*>(po + i) = *reinterpret_cast<const float4*>(tp + i);
+    *reinterpret_cast<float4*>(lo + i) = *reinterpret_cast<const float4*>(tq + i);
+  }
+  float v[8];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    v[2 * b] = dth[b];
+    v[2 * b + 1] = dph[b];
+  }
+  float o[8];
+  block_sum_vec<8>(v, red, o);
+  if (threadIdx.x < 8) {
+    constexpr int PER = ROWS / C::NTILE;
+    const int P = 2 * N * L;
+    const int col = (l * N + 8 + threadIdx.x / 2) * 2 + (threadIdx.x & 1);
+    float* row = slab + ((size_t)s * ROWS + t * PER) * P + col;
+    row[0] = o[threadIdx.x];
+#pragma unroll
+    for (int r = 1; r < PER; ++r) row[(size_t)r * P] = 0.f;
+  }
+}
+
+// Reverse pass A of layer l (in place; STORE = false for layer 0, whose result nothing reads).  512
+// threads: the adjoint sweep is latency-bound (dependent gradient sums), and the 64 KiB of psi + lambda
+// per workgroup allow only 2 workgroups per CU -- twice the waves hide it better.
+template <int N, bool STORE>
+__global__ void __launch_bounds__(SG<N>::NTA, 4) pass_a_bwd(const float* __restrict__ x, const float* __restrict__ w, int L,
+                                                 int l, int wgroup, cf* __restrict__ pst, cf* __restrict__ lst,
+                                                 float* __restrict__ slab) {
+  using C = SG<N>;
+  constexpr int NTA = C::NTA;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* trig = reinterpret_cast<float4*>(smem);
+  float* red = reinterpret_cast<float*>(smem + 256);      // (NTA / 64) * 2AB floats <= 768 B
+  cf* tp = reinterpret_cast<cf*>(smem + 1024);
+  cf* tq = tp + C::AS;
+  const int br = blockIdx.x, s = blockIdx.y;
+  load_trig<N>(trig, x, w, s, L, l, wgroup);
+  cf* ps = pst + (size_t)s * C::D;
+  cf* ls = lst + (size_t)s * C::D;
+  for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
+    const int k = brick_k(e, br);
+    *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(ps + k);
+    *reinterpret_cast<float4*>(tq + e) = *reinterpret_cast<const float4*>(ls + k);
+  }
+  __syncthreads();
+  float dth[C::AB], dph[C::AB];
+#pragma unroll
+  for (int b = 0; b < C::AB; ++b) dth[b] = dph[b] = 0.f;
+  lds_gates<C::AB, 0, C::AB, false, true, NTA>(tp, tq, trig, dth, dph);
+  if constexpr (STORE) {
+    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
+      const int k = brick_k(e, br);
+      *reinterpret_cast<float4*>(ps + k) = *reinterpret_cast<const float4*>(tp + e);
+      *reinterpret_cast<float4*>(ls + k) = *reinterpret_cast<const float4*>(tq + e);
+    }
+  }
+  float v[2 * C::AB], o[2 * C::AB];
+#pragma unroll
+  for (int b = 0; b < C::AB; ++b) {
+    v[2 * b] = dth[b];
+    v[2 * b + 1] = dph[b];
+  }
+  block_sum_vec<2 * C::AB, NTA>(v, red, o);
+  if (threadIdx.x < 2 * C::AB) {
+    const int P = 2 * N * L;
+    const int q = brick_q(threadIdx.x / 2);
+    slab[((size_t)s * ROWS + br) * P + (l * N + q) * 2 + (threadIdx.x & 1)] = o[threadIdx.x];
+  }
+}
+
+// dx[s][q] = sum over the sample's 16 slab rows of the layer-0 theta column
+__global__ void __launch_bounds__(256) reduce_dx(const float* __restrict__ slab, float* __restrict__ dx, int B, int N,
+                                                 int P) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * N) return;
+  const int s = i / N, q = i % N;
+  float acc = 0.f;
+  for (int r = 0; r < ROWS; ++r) acc += slab[((size_t)s * ROWS + r) * P + 2 * q];
+  dx[i] = acc;
+}
+
+// ------------------------------------------------------------------------------------------ host
+template <int N>
+struct Smem {
+  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + 512);   // (+ the GEN product tables)
+  static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
+  static constexpr size_t B_BWD = 512 + 2 * sizeof(cf) * 4096 + 2048;   // (+ the FIRST observable tables)
+  static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * SG<N>::AS;
+};
+
+inline size_t state_bytes(int n, int B) { return (size_t)B * (8ull << n); }
+
+template <int N>
+static int fwd(const float* x, const float* w, float* E, int B, int L, int wgroup, char* ws, cf* psave,
+               hipStream_t st) {
+  using C = SG<N>;
+  using S = Smem<N>;
+  cf* U = psave ? psave : reinterpret_cast<cf*>(ws);
+  cf* V = reinterpret_cast<cf*>(ws + state_bytes(N, B));
+  float* epart = reinterpret_cast<float*>(ws + 2 * state_bytes(N, B));
+  // (L-1) pass-B swaps: start where the final state must land (U)
+  cf* cur = ((L - 1) % 2 == 0) ? U : V;
+  cf* oth = (cur == U) ? V : U;
+  static bool attr = false;
+  if (!attr) {
+    (void)allow_lds(pass_a_fwd<N, true>, S::A_FWD);
+    (void)allow_lds(pass_a_fwd<N, false>, S::A_FWD);
+    (void)allow_lds(pass_b_fwd<N, true>, S::B_FWD);
+    (void)allow_lds(pass_b_fwd<N, false>, S::B_FWD);
+    attr = true;
+  }
+  const dim3 ga(ROWS, B), gb(C::NTILE, B);
+  for (int l = 1; l < L; ++l) {
+    if (l == 1)
+      hipLaunchKernelGGL((pass_a_fwd<N, true>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, cur);
+    else
+      hipLaunchKernelGGL((pass_a_fwd<N, false>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, cur);
+    if (l == L - 1)
+      hipLaunchKernelGGL((pass_b_fwd<N, true>), gb, dim3(NT), S::B_FWD, st, x, w, L, l, wgroup, cur, oth, epart);
+    else
+      hipLaunchKernelGGL((pass_b_fwd<N, false>), gb, dim3(NT), S::B_FWD, st, x, w, L, l, wgroup, cur, oth, epart);
+    cf* tmp = cur;
+    cur = oth;
+    oth = tmp;
+  }
+  if (E) hipLaunchKernelGGL(reduce_e<N>, dim3((B * N + 255) / 256), dim3(256), 0, st, epart, E, B);
+  return (int)hipGetLastError();
+}
+
+template <int N>
+static int bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int L, int wgroup,
+               char* ws, cf* psave, hipStream_t st) {
+  using C = SG<N>;
+  using S = Smem<N>;
+  const size_t sb = state_bytes(N, B);
+  cf* W1 = reinterpret_cast<cf*>(ws);
+  cf* W2 = reinterpret_cast<cf*>(ws + sb);
+  cf* W3 = reinterpret_cast<cf*>(ws + 2 * sb);
+  if (psave == nullptr) {   // no kept state: run the forward into the 4th slot (its own scratch: slots 1, 2)
+    psave = reinterpret_cast<cf*>(ws + 3 * sb);
+    if (int e = fwd<N>(x, w, nullptr, B, L, wgroup, ws, psave, st)) return e;
+  }
+  static bool attr = false;
+  if (!attr) {
+    (void)allow_lds(pass_b_bwd<N, true>, S::B_BWD);
+    (void)allow_lds(pass_b_bwd<N, false>, S::B_BWD);
+    (void)allow_lds(pass_a_bwd<N, true>, S::A_BWD);
+    (void)allow_lds(pass_a_bwd<N, false>, S::A_BWD);
+    attr = true;
+  }
+  const dim3 ga(ROWS, B), gb(C::NTILE, B);
+  // (psi, lambda) buffers: psave -> (W1, W2) -> (psave, W3) -> (W1, W2) -> ...
+  cf* pin = psave;
+  cf* lin = nullptr;
+  for (int l = L - 1; l >= 0; --l) {
+    const bool even = ((L - 1 - l) % 2) == 0;
+    cf* po = even ? W1 : psave;
+    cf* lo = even ? W2 : W3;
+    if (l == L - 1)
+      hipLaunchKernelGGL((pass_b_bwd<N, true>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, pin, lin, po, lo,
+                         slab);
+    else
+      hipLaunchKernelGGL((pass_b_bwd<N, false>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, pin, lin, po, lo,
+                         slab);
+    if (l > 0)
+      hipLaunchKernelGGL((pass_a_bwd<N, true>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, po, lo, slab);
+    else
+      hipLaunchKernelGGL((pass_a_bwd<N, false>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, po, lo, slab);
+    pin = po;
+    lin = lo;
+  }
+  hipLaunchKernelGGL(reduce_dx, dim3((B * N + 255) / 256), dim3(256), 0, st, slab, dx, B, N, 2 * N * L);
+  return (int)hipGetLastError();
+}
+
+}  // namespace qstream
+}  // namespace qd
+
+using namespace qd::qstream;
+
+#define QD_STREAM_DISPATCH(n, CALL)         \
+  switch (n) {                              \
+    case 13: return CALL(13);               \
+    case 14: return CALL(14);               \
+    case 15: return CALL(15);               \
+    case 16: return CALL(16);               \
+    default: return (int)hipErrorInvalidValue; \
+  }
+
+// Whether (n, L) runs on the streamed simulator (else qsim_big.hip's workgroup-per-sample kernels).
+QD_API int qd_qsim_stream_ok(int n, int L) { return n >= 13 && n <= 16 && L >= 2 && 2 * n * L <= 1024; }
+
+// Slab rows of the backward's weight-gradient partials: 16 per sample.
+QD_API int qd_qsim_stream_rows(int B) { return B * ROWS; }
+
+// Workspace bytes: forward 2 states + the <Z> partials; backward 4 states (3 + one for a forward
+// recompute when the caller kept no state).
+QD_API long long qd_qsim_stream_workspace(int n, int B, int backward) {
+  const long long sb = (long long)state_bytes(n, B);
+  const long long ep = (long long)B * (1ll << (n - 12)) * n * 4;
+  return backward ? 4 * sb + ep : 2 * sb + ep;
+}
+
+// E (B, n) = <Z>; psave (nullable): (B, 2^n) complex64 psi_final for qd_qsim_stream_bwd.
+QD_API int qd_qsim_stream_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
+                              void* psave, void* stream) {
+  if (!qd_qsim_stream_ok(n, L) || B < 1 || ws == nullptr) return (int)hipErrorInvalidValue;
+#define CALL_F(NN) fwd<NN>(x, w, E, B, L, wgroup, (char*)ws, (cf*)psave, (hipStream_t)stream)
+  QD_STREAM_DISPATCH(n, CALL_F)
+#undef CALL_F
+}
+
+// dx (B, n), slab (16 B, 2 n L) weight-gradient partials; psave (nullable) is consumed.
+QD_API int qd_qsim_stream_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n,
+                              int L, int wgroup, void* ws, void* psave, void* stream) {
+  if (!qd_qsim_stream_ok(n, L) || B < 1 || ws == nullptr) return (int)hipErrorInvalidValue;
+#define CALL_B(NN) bwd<NN>(x, w, gE, dx, slab, B, L, wgroup, (char*)ws, (cf*)psave, (hipStream_t)stream)
+  QD_STREAM_DISPATCH(n, CALL_B)
+#undef CALL_B
+}

@@ -73,3 +73,18 @@ def gemm_dgrad(dY: torch.Tensor, W: torch.Tensor, out: Optional[torch.Tensor] = 
     f = _gemm_fn("qd_gemm_dgrad", [_p, _p, _p, _i, _i, _i, _i, _p])
     nat.check(f(nat.ptr(dY), nat.ptr(W), nat.ptr(dA), M, N, K, cfg, nat.stream_ptr(W.device)), "gemm_dgrad")
     return dA
+
+
+def gemm_fwd_f8(A8: torch.Tensor, W8: torch.Tensor, deq: torch.Tensor, b: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Y (M, N) bf16 = deq[0] deq[1] A8 W8^T (+ b): OCP e4m3 operands (torch.float8_e4m3fn, row-major,
+    K % 128 == 0), fp32 accumulation (csrc/hip/gemm.hip qd_gemm_fwd_bias_f8, mfma_f32_16x16x32_fp8_fp8)."""
+    M, K = A8.shape
+    N = W8.shape[0]
+    assert A8.dtype == W8.dtype == torch.float8_e4m3fn and A8.is_contiguous() and W8.is_contiguous()
+    assert deq.dtype == torch.float32 and deq.numel() >= 2
+    Y = out if out is not None else torch.empty(M, N, device=A8.device, dtype=torch.bfloat16)
+    f = _gemm_fn("qd_gemm_fwd_bias_f8", [_p, _p, _p, _p, _p, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(A8), nat.ptr(W8), nat.ptr(deq), nat.ptr(b) if b is not None else None, nat.ptr(Y), M, N, K,
+                nat.stream_ptr(A8.device)), "gemm_fwd_bias_f8")
+    return Y

@@ -230,18 +230,24 @@ class StreamNMSE:
     def gemm_fused(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], label: torch.Tensor,
                    perf: Optional[torch.Tensor], bias_grad: torch.Tensor, layout: Tuple[int, int, int],
                    rowden: torch.Tensor, loss_scale: float = 1.0, bias_slabs=None, defer_loss: bool = False,
-                   cfg: int = 0) -> torch.Tensor:
+                   cfg: int = 0, deq: Optional[torch.Tensor] = None) -> torch.Tensor:
         """The FC forward GEMM with this loss as its epilogue (csrc/hip/gemm.hip qd_gemm_fwd_nmse): Y = A W^T
         + b is never written; dY (bf16), the error partials, the per-stream label powers and the bias
         gradient's per-tile column sums come out of the GEMM, then the same finish as ``fused`` (a launch,
         or ``pending_finish`` for a later launch of the step with ``defer_loss``; the bias column reduction
-        queued on ``bias_slabs`` when given).  Returns dY; the loss is ``self.loss``."""
+        queued on ``bias_slabs`` when given).  Returns dY; the loss is ``self.loss``.
+        ``deq`` (2,) fp32: A and W are OCP e4m3 (torch.float8_e4m3fn) with these dequantisation scales
+        (qd_gemm_fwd_nmse_f8, the fp8 estimator); the rest of the contract is unchanged."""
         from .fc import gemm_tile_m
         E, U, B = layout
         M, K = A.shape
         N = W.shape[0]
+        f8 = deq is not None
         assert A.is_cuda and self.rowoff is not None and M == self.rows == E * U * B and N == self.cols
-        assert A.dtype == W.dtype == torch.bfloat16 and A.is_contiguous() and W.is_contiguous()
+        want = torch.float8_e4m3fn if f8 else torch.bfloat16
+        assert A.dtype == W.dtype == want and A.is_contiguous() and W.is_contiguous()
+        if f8:
+            cfg = 0   # (the e4m3 kernel has the cfg-0 tile)
         self._check_labels(label)
         if perf is not None:
             self._check_labels(perf)
@@ -253,12 +259,20 @@ class StreamNMSE:
                         torch.empty(M // 16 * gx * 2, device=dev), torch.empty(M // tm, N, device=dev),
                         torch.empty(self.S, 2, device=dev))
         _, dY, part, colsum, dens = self._gz
-        f = nat.fn(nat.hip_lib(), "qd_gemm_fwd_nmse", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i,
-                                                       _i, _f, _i, _p])
-        nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(b) if b is not None else None, nat.ptr(label),
-                    nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowoff), nat.ptr(rowden), nat.ptr(dY),
-                    nat.ptr(part), nat.ptr(colsum), nat.ptr(dens), M, N, K, E, U, B, loss_scale, cfg,
-                    nat.stream_ptr(dev)), "gemm_fwd_nmse")
+        if f8:
+            f = nat.fn(nat.hip_lib(), "qd_gemm_fwd_nmse_f8", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i,
+                                                              _i, _i, _i, _i, _f, _p])
+            nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(deq), nat.ptr(b) if b is not None else None, nat.ptr(label),
+                        nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowoff), nat.ptr(rowden),
+                        nat.ptr(dY), nat.ptr(part), nat.ptr(colsum), nat.ptr(dens), M, N, K, E, U, B, loss_scale,
+                        nat.stream_ptr(dev)), "gemm_fwd_nmse_f8")
+        else:
+            f = nat.fn(nat.hip_lib(), "qd_gemm_fwd_nmse", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i,
+                                                           _i, _i, _f, _i, _p])
+            nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(b) if b is not None else None, nat.ptr(label),
+                        nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowoff), nat.ptr(rowden),
+                        nat.ptr(dY), nat.ptr(part), nat.ptr(colsum), nat.ptr(dens), M, N, K, E, U, B, loss_scale, cfg,
+                        nat.stream_ptr(dev)), "gemm_fwd_nmse")
         self.pending_finish = None
         if defer_loss:
             assert bias_slabs is not None, "defer_loss needs the bias reduction queued elsewhere"

@@ -27,7 +27,7 @@ import torch
 from .. import _native as nat
 from .slabsum import SlabBatch
 from ..ops.optim import FlatParamSpace
-from ..ops.quantum import HIP_REG_MAX_QUBITS
+from ..ops.quantum import HIP_REG_MAX_QUBITS, stream_sim_ok
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
@@ -91,7 +91,17 @@ class QSCStepHIP:
         self.preslab = torch.empty(self.grid_bwd, row, **f32)
         L = nat.hip_lib()
         self.big = self.n > HIP_REG_MAX_QUBITS  # workgroup-per-sample simulator (qsim_big.hip)
-        if self.big:
+        # n = 13..16 with >= 2 layers: the streamed simulator (csrc/hip/qsim_stream.hip, one workgroup per
+        # (sample, 4096-amplitude brick) per pass); else qsim_big.hip's workgroup-per-sample kernels
+        self.stream = self.big and stream_sim_ok(self.n, self.L)
+        if self.stream:
+            self.qrows = nat.fn(L, "qd_qsim_stream_rows", [_i])(batch_total)
+            ws = nat.fn(L, "qd_qsim_stream_workspace", [_i, _i, _i], ctypes.c_longlong)
+            nb = max(ws(self.n, batch_total, 0), ws(self.n, batch_total, 1))
+            self.qws = torch.empty(nb, dtype=torch.uint8, device=dev)
+            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev) \
+                if os.environ.get("QDML_QSIM_SAVE_STATE", "1") != "0" else None
+        elif self.big:
             cap = int(os.environ.get("QDML_QSIM_BIG_GRID", "0"))   # (0: the library default)
             nat.fn(L, "qd_qsim_big_set_grid_cap", [_i], None)(cap)
             self.qrows = nat.fn(L, "qd_qsim_big_grid", [_i])(batch_total)
@@ -113,8 +123,9 @@ class QSCStepHIP:
                                                    _i, _p])
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
-            self._qf = nat.fn(L, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
-            self._qb = nat.fn(L, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+            pre = "qd_qsim_stream" if self.stream else "qd_qsim_big"
+            self._qf = nat.fn(L, pre + "_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+            self._qb = nat.fn(L, pre + "_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
         else:
             # the forward keeps every sample's final state (2^n complex, 4.7 MB at 8 qubits) for the
             # adjoint backward, which then skips re-running the circuit

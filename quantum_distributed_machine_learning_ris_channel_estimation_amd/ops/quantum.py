@@ -20,6 +20,7 @@ Here three interchangeable backends implement the SAME function:
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from typing import Optional
 
@@ -33,6 +34,20 @@ _p = ctypes.c_void_p
 
 HIP_REG_MAX_QUBITS = 10   # register-resident kernel
 HIP_MAX_QUBITS = 16       # workgroup-per-sample kernel above that
+
+
+def stream_sim_ok(n: int, L: int) -> bool:
+    """(n, L) runs on the streamed simulator (csrc/hip/qsim_stream.hip: n = 13..16, L >= 2, one
+    workgroup per (sample, 4096-amplitude brick) per pass); QDML_QSIM_STREAM=0 keeps qsim_big.hip's
+    workgroup-per-sample kernels."""
+    if os.environ.get("QDML_QSIM_STREAM", "1") == "0":
+        return False
+    return bool(nat.fn(nat.hip_lib(), "qd_qsim_stream_ok", [_i, _i])(n, L))
+
+
+def _stream_ws(n: int, B: int, backward: bool, device) -> torch.Tensor:
+    nbytes = nat.fn(nat.hip_lib(), "qd_qsim_stream_workspace", [_i, _i, _i], ctypes.c_longlong)(n, B, int(backward))
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
 def _big_ws(n: int, grid: int, backward: bool, device) -> Optional[torch.Tensor]:
@@ -49,6 +64,11 @@ def hip_qsim_fwd(x: torch.Tensor, w: torch.Tensor, E: torch.Tensor, wgroup: int 
     if n <= HIP_REG_MAX_QUBITS:
         f = nat.fn(lib, "qd_qsim_fwd", [_p, _p, _p, _i, _i, _i, _i, _p])
         nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, st), "qd_qsim_fwd")
+        return
+    if stream_sim_ok(n, L):
+        ws = _stream_ws(n, B, False, x.device)
+        f = nat.fn(lib, "qd_qsim_stream_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+        nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, nat.ptr(ws), None, st), "qd_qsim_stream_fwd")
         return
     grid = nat.fn(lib, "qd_qsim_big_grid", [_i])(B)
     ws = _big_ws(n, grid, False, x.device)
@@ -70,6 +90,13 @@ def hip_qsim_bwd_slab(x: torch.Tensor, w: torch.Tensor, gE: torch.Tensor, dx: to
         f = nat.fn(lib, "qd_qsim_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
         nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup_of(x, w), st),
                   "qd_qsim_bwd")
+        return slab
+    if stream_sim_ok(n, L):
+        slab = torch.empty(nat.fn(lib, "qd_qsim_stream_rows", [_i])(B), P, device=x.device, dtype=torch.float32)
+        ws = _stream_ws(n, B, True, x.device)
+        f = nat.fn(lib, "qd_qsim_stream_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
+        nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup_of(x, w),
+                    nat.ptr(ws), None, st), "qd_qsim_stream_bwd")
         return slab
     rows = nat.fn(lib, "qd_qsim_big_grid", [_i])(B)
     slab = torch.empty(rows, P, device=x.device, dtype=torch.float32)

@@ -426,12 +426,54 @@ class HDCEStep:
             self.dgrad()
         return self.nmse.loss
 
+    def _hand_f8_ok(self, A: torch.Tensor) -> bool:
+        """The fp8 estimator's forward on the hand-written e4m3 GEMM with the loss epilogue
+        (qd_gemm_fwd_nmse_f8): e4m3 activations from the conv stack, e4m3 weight shadow from the
+        optimizer, rowoff-gathered labels.  QDML_HAND_FP8=0: hipBLASLt (torch._scaled_mm) + the NMSE kernel."""
+        m = self.m
+        if not (m.fp8 and m.fc_shadow is not None and os.environ.get("QDML_HAND_FP8", "1") != "0"
+                and self.nmse.rowoff is not None and getattr(self, "_rowden", None) is not None
+                and getattr(self.conv, "h3_8", None) is not None):
+            return False
+        from ..ops.fc import gemm_tile_m
+        M, K = A.shape
+        N = m.fc_w.shape[0]
+        tm = gemm_tile_m(0)
+        return (M % tm == 0 and N % 128 == 0 and K % 128 == 0 and (tm // (self.B * m.E) + 2) * m.E <= 64
+                and self.B % 16 == 0 and tm % (16 * m.E) == 0)
+
+    @torch.no_grad()
+    def _fc_hand_f8(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
+        """fp8 estimator: e4m3 forward GEMM with the loss fused into its epilogue (per-tensor delayed
+        scales of the previous step), bf16 weight / data gradients."""
+        from ..ops.slabsum import SlabBatch
+        m = self.m
+        W, b = m.fc_weights_lp()
+        self._slabs = SlabBatch() if (self.writes_grads and self.bias_via_conv_slabs) else None
+        dY = self.nmse.gemm_fused(self.conv.h3_8, m._shadow_w8, b, label, perf, m.fc_b.grad, (m.E, self.U, self.B),
+                                  self._rowden, bias_slabs=self._slabs,
+                                  defer_loss=self._slabs is not None and self.defer_loss, deq=m.fp8_scales.scale)
+        m.fp8_scales.update()
+        if self.stage_hook is not None:
+            self.stage_hook("fc")
+        A = A.to(m.compute_dtype)
+        self._wgrad(dY, A)
+        self._dYW = (dY, W)
+        if not self.defer_dgrad:
+            self.dgrad()
+        return self.nmse.loss
+
     @torch.no_grad()
     def _fc_hip(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
         if self.stage_hook is not None:
             self.stage_hook("fc_pre")   # (before anything reads the FC weights)
         if self._hand_gemm_ok(A):
+            self.fc_path = "hand"
             return self._fc_hand(A, label, perf)
+        if self._hand_f8_ok(A):
+            self.fc_path = "hand_f8"
+            return self._fc_hand_f8(A, label, perf)
+        self.fc_path = "library"   # (which FC forward the last step ran: hand / hand_f8 / library)
         m = self.m
         dt = m.compute_dtype
         hook = self.stage_hook

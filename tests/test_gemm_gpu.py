@@ -156,3 +156,59 @@ def test_flagship_hand_gemm_matches_hipblaslt_path(cuda, monkeypatch):
         sl = sp.slice_of(p)
         x, y = ga[sl], gb[sl]
         assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
+
+
+@pytest.mark.parametrize("M,N,K", [(576, 256, 256), (2304, 2048, 4096)])
+def test_gemm_fwd_f8_matches_fp32(cuda, M, N, K):
+    """e4m3 forward (mfma_f32_16x16x32_fp8_fp8, two per 16-byte fragment) == the fp32 product of the SAME
+    dequantised operands (the only error left is fp32 accumulation order + the bf16 output), and exact
+    one-hot layout checks."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import gemm_fwd_f8
+    torch.manual_seed(2)
+    A = torch.randn(M, K, device=cuda)
+    W = torch.randn(N, K, device=cuda) * K ** -0.5
+    sa, sw = float(A.abs().max()) / 448.0, float(W.abs().max()) / 448.0
+    A8 = (A / sa).to(torch.float8_e4m3fn)
+    W8 = (W / sw).to(torch.float8_e4m3fn)
+    deq = torch.tensor([sa, sw], device=cuda)
+    b = torch.randn(N, device=cuda).bfloat16()
+    Y = gemm_fwd_f8(A8, W8, deq, b)
+    ref = (A8.float() * sa) @ (W8.float() * sw).t() + b.float()
+    torch.cuda.synchronize()
+    assert _rel(Y, ref) < 8e-3, _rel(Y, ref)
+    W2 = torch.zeros(N, K, device=cuda)
+    W2[5, 7] = 1.0
+    W2[N - 3, K - 1] = 2.0
+    Y2 = gemm_fwd_f8(A8, W2.to(torch.float8_e4m3fn), torch.tensor([1.0, 1.0], device=cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(Y2[:, 5].float(), A8[:, 7].float().bfloat16().float())
+    assert torch.equal(Y2[:, N - 3].float(), (2 * A8[:, K - 1].float()).bfloat16().float())
+    assert float(Y2[:, :5].float().abs().sum()) == 0.0
+
+
+def test_flagship_fp8_hand_gemm_matches_scaled_mm_path(cuda, monkeypatch):
+    """fp8 estimator step: the hand-written e4m3 GEMM with the loss epilogue vs hipBLASLt's scaled GEMM +
+    the one-pass NMSE kernel, from the same e4m3 operands and scales: loss and every gradient agree."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
+                                                                                                FlagshipTrainer)
+    ctx = DistContext(device=cuda)
+    cfg = dict(batch=64, data_len=800, hip_graphs=False, use_quantumnat=False, stream_mode="serial", dtype="fp8")
+    trs = []
+    for hand in ("1", "0"):
+        monkeypatch.setenv("QDML_HAND_FP8", hand)
+        tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
+        tr.next_batch()
+        tr._dp_g1()
+        tr._dp_g2()
+        torch.cuda.synchronize()
+        assert tr.hstep.fc_path == ("hand_f8" if hand == "1" else "library")
+        trs.append(tr)
+    a, b = trs
+    assert torch.allclose(a.hloss, b.hloss, rtol=1e-2), (a.hloss, b.hloss)
+    ga, gb = a.hdce.space.grad, b.hdce.space.grad
+    sp = a.hdce.space
+    for name, p in zip(sp.names, sp.params):
+        sl = sp.slice_of(p)
+        x, y = ga[sl], gb[sl]
+        assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
