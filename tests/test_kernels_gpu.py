@@ -449,3 +449,46 @@ def test_qsim_stream_matches_per_sample_kernel(cuda, n, L, B, G):
         assert torch.allclose(dx1, dx0, atol=1e-4), float((dx1 - dx0).abs().max())
         g0, g1 = slab0.sum(0), slab1.sum(0)
         assert torch.allclose(g1, g0, atol=2e-4 * B * G, rtol=1e-4), float((g1 - g0).abs().max())
+
+
+def _mfma_fwd(cuda, x, w, wgroup, save):
+    import ctypes
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    lib = nat.hip_lib()
+    _p, _i = ctypes.c_void_p, ctypes.c_int
+    G, L = w.shape[0], w.shape[1]
+    B = x.shape[0]
+    nh = nat.fn(lib, "qd_qsim_mfma_ops_halves", [_i, _i], ctypes.c_longlong)(G, L)
+    ops = torch.empty(nh, dtype=torch.float16, device=cuda)
+    E = torch.empty(B, 8, device=cuda)
+    ps = torch.zeros(B * 256 * 2, device=cuda) if save else None
+    st = nat.stream_ptr(cuda)
+    nat.check(nat.fn(lib, "qd_qsim_mfma_prep", [_p, _p, _i, _i, _p])(nat.ptr(w), nat.ptr(ops), G, L, st), "prep")
+    nat.check(nat.fn(lib, "qd_qsim_mfma_fwd", [_p, _p, _p, _p, _i, _i, _i, _p, _p])(
+        nat.ptr(x), nat.ptr(w), nat.ptr(ops), nat.ptr(E), B, L, wgroup, nat.ptr(ps) if save else None, st), "fwd")
+    return E, ps
+
+
+@pytest.mark.parametrize("L,G,b", [(2, 1, 37), (3, 9, 16), (5, 3, 7)])
+def test_qsim_mfma_forward_matches_register_kernel(cuda, L, G, b):
+    """8-qubit forward on the matrix cores (qsim_mfma.hip: Kronecker-factored layer unitaries as
+    complex MFMA GEMMs, fp16 hi/lo split) == the register kernel (qsim.hip) and the fp64 CPU oracle:
+    <Z> and the saved final state (the adjoint backward's input)."""
+    import ctypes
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    lib = nat.hip_lib()
+    _p, _i = ctypes.c_void_p, ctypes.c_int
+    torch.manual_seed(L * 10 + G)
+    B = G * b
+    x = torch.rand(B, 8, device=cuda) * 2 - 1
+    w = torch.rand(G, L, 8, 2, device=cuda) * 6.28
+    E1, ps1 = _mfma_fwd(cuda, x, w, b if G > 1 else 0, True)
+    E0 = torch.empty(B, 8, device=cuda)
+    ps0 = torch.zeros(B * 256 * 2, device=cuda)
+    nat.check(nat.fn(lib, "qd_qsim_fwd_save", [_p, _p, _p, _i, _i, _i, _i, _p, _p])(
+        nat.ptr(x), nat.ptr(w), nat.ptr(E0), B, 8, L, b if G > 1 else 0, nat.ptr(ps0), nat.stream_ptr(cuda)), "reg")
+    torch.cuda.synchronize()
+    assert torch.allclose(E1, E0, atol=3e-6), float((E1 - E0).abs().max())
+    assert torch.allclose(ps1, ps0, atol=2e-6), float((ps1 - ps0).abs().max())
+    Ec = torch.cat([qsim(x[i * b:(i + 1) * b].cpu(), w[i].cpu(), "cpu") for i in range(G)])
+    assert torch.allclose(E1.cpu(), Ec, atol=5e-6), float((E1.cpu() - Ec).abs().max())
