@@ -89,6 +89,16 @@ def test_conv_stack_backward(cuda, pilot_num, B):
             assert rel(ga, gb) < 3e-2, (k, name, rel(ga, gb))
 
 
+# Whole-step conv weight-gradient error vs the fp32 autograd step, measured on MI355X (seed 0):
+# relative Frobenius 0.088 / 0.065 / 0.034 and cosine 0.99614 / 0.99787 / 0.99942 for conv1..3.
+# fro^2 ~= 2(1 - cos) there, i.e. the difference is noise, not a scale or direction error; it grows
+# toward the input because every BN backward compounds the bf16 storage error of z and the ~0.2%
+# of ReLU masks it flips (test_conv_stack_backward pins the kernels' own arithmetic at < 3%).
+# Bounds are ~1.5x the measured error.
+FRO_BOUND = (0.13, 0.10, 0.05)
+COS_BOUND = (0.992, 0.996, 0.9988)
+
+
 def test_hdce_step_hip_vs_torch(cuda):
     """Whole step (conv kernels + hipBLASLt FC + fused NMSE) vs the fp32 autograd step."""
     U, B = 3, 64
@@ -104,11 +114,25 @@ def test_hdce_step_hip_vs_torch(cuda):
     lb = sb(Yp, HL, HP)
     torch.cuda.synchronize()
     assert torch.allclose(la, lb, rtol=2e-2), (la, lb)
+    fr = lambda x, y: float((x.float() - y.float()).norm() / y.float().norm())
+    print(f"loss {la.tolist()} {lb.tolist()} fc_w fro {fr(a.fc_w.grad, b.fc_w.grad):.5f} fc_b {fr(a.fc_b.grad, b.fc_b.grad):.5f}")
+    for k in range(3):
+        print(f"bn{k + 1}: gamma fro {fr(a.bn_w[k].grad, b.bn_w[k].grad):.5f} beta fro {fr(a.bn_b[k].grad, b.bn_b[k].grad):.5f} "
+              f"gamma ratio {float((a.bn_w[k].grad * b.bn_w[k].grad).sum() / (b.bn_w[k].grad ** 2).sum()):.5f} "
+              f"convw ratio {float((a.conv_w[k].grad * b.conv_w[k].grad).sum() / (b.conv_w[k].grad ** 2).sum()):.5f}")
     assert rel(a.fc_w.grad, b.fc_w.grad) < 3e-2
     assert rel(a.fc_b.grad, b.fc_b.grad) < 3e-2
-    # conv grads see bf16 activations end to end: looser bound (see module docstring)
+    # conv grads see bf16 activations end to end: bound the relative Frobenius error and the
+    # direction (cosine) per layer, calibrated above
+    vals = []
     for k in range(3):
-        assert rel(a.conv_w[k].grad, b.conv_w[k].grad) < 0.15
+        ga, gb = a.conv_w[k].grad.float().flatten(), b.conv_w[k].grad.float().flatten()
+        fro = float((ga - gb).norm() / gb.norm())
+        cos = float(torch.nn.functional.cosine_similarity(ga, gb, dim=0))
+        print(f"conv{k + 1} weight grad: fro-rel {fro:.5f} cos {cos:.6f}")
+        vals.append((fro, cos))
+    for k, (fro, cos) in enumerate(vals):
+        assert fro < FRO_BOUND[k] and cos > COS_BOUND[k], (k, fro, cos)
 
 
 def test_hdce_fp8_estimator_step(cuda):
