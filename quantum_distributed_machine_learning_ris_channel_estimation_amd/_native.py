@@ -91,7 +91,7 @@ def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     hdrs = _headers("hip")
     flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
              "-Wno-unused-result", "-I", os.path.join(CSRC, "hip")]
-    flags += os.environ.get("QDML_HIPCC_EXTRA", "").split()   # (tuning sweeps: e.g. -DQD_CINP_PAD=16)
+    flags += os.environ.get("QDML_HIPCC_EXTRA", "").split()   # (tuning sweeps: extra -D defines)
     # a changed flag set (a tuning build, then the default again) rebuilds every object
     stamp = os.path.join(OBJ_DIR, "flags.txt")
     want = " ".join(f for f in flags if not f.startswith("/"))   # (not the include path: the tree moves)

@@ -14,7 +14,8 @@
 // Kernels (all MFMA bf16 32x32x16, fp32 accumulate):
 //   conv3x3_kernel   implicit-GEMM conv: M = 32 positions, N = 32 channels, K = 9*CIN ordered
 //                    (tap, channel) so an A fragment is ONE ds_read_b128 from a channel-last
-//                    LDS tile (pixel stride padded to 80 B: conflict-free).  Weights stay in
+//                    LDS tile (64-byte pixels, 16-byte channel chunks XOR-swizzled per pixel:
+//                    conflict-free for every tap, see tile_swz).  Weights stay in
 //                    VGPRs as B fragments for the whole launch.  Input transforms fused in the
 //                    LDS staging: raw f32 pilots (layer 1), BN+ReLU of the previous layer's
 //                    pre-BN output (forward), or the BN/ReLU backward (dz from dh and z) for the
@@ -26,16 +27,13 @@
 //                    in registers across samples, and reduce through LDS once per workgroup
 //                    into a deterministic slab (no float atomics).  A operand rows come from 3
 //                    column-shifted copies of the input tile so every read is an aligned
-//                    ds_read_b128.
+//                    ds_read_b128; rows are ordered (tap, channel) so the 32 rows of an MFMA tile
+//                    are one tap's 32 channels at an odd 16-byte-slot stride (conflict-free).
 //   bn_*             statistics finalisation (+ running-stat momentum updates in stream order),
 //                    backward reductions, and the final BN+ReLU apply that feeds the FC GEMM.
 #include <algorithm>
 
 #include "common.h"
-
-#ifndef QD_CINP_PAD
-#define QD_CINP_PAD 8   // bf16 padding of the channel-last conv tile pixels (multiple of 8: 16-byte reads)
-#endif
 
 namespace qd {
 namespace conv {
@@ -62,6 +60,13 @@ struct Geo {
 };
 
 __device__ __forceinline__ float bf(uint16_t h) { return bf16_to_f32(h); }
+
+// 32-channel conv tiles: padded pixel (R, C) is 64 bytes = four 16-byte channel chunks, chunk q stored
+// at position q ^ tile_swz(R, C).  Pixel P's chunks sit in bank-row slot group P mod 4; the XOR makes
+// the 16 lanes of every ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) hit 16
+// distinct 16-byte slots for every tap of both geometries (W = 8, 16).  The previous layout (pixels
+// padded to 80 bytes) took 8 (W = 8) / 4 (W = 16) extra LDS cycles per 4-cycle read.
+__device__ __forceinline__ int tile_swz(int R, int C) { return (2 * R + (C >> 2) + 2 * (C >> 3)) & 3; }
 
 template <typename T>
 __device__ __forceinline__ float ldf(const T* p, size_t i);
@@ -218,7 +223,8 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
   unsigned long long ts[8] = {};
   if constexpr (STAMP) ts[0] = phase_stamp();
   using G = Geo<H, W>;
-  constexpr int CINP = (CIN % 16 == 0) ? CIN + QD_CINP_PAD : CIN;  // channel-last pixel stride (bf16)
+  constexpr int CINP = CIN;                                 // channel-last pixel stride (bf16)
+  static_assert(CIN % 16 != 0 || CIN == 32, "the tile swizzle is for 4-chunk (32-channel) pixels");
   constexpr int KS = (9 * CIN + 15) / 16;                   // 16-deep k steps
   constexpr int TILE = G::HP * G::WP * CINP;                // bf16 elements per wave tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -262,7 +268,7 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
   constexpr int HOLD = ITER * (2 * QV + (INM == IN_BNBWD ? 2 : 0));   // 16-byte registers per sample
   // (dgrad: registers go to the fused BN-reduction operands; P256: to the MFMA pipeline)
   constexpr bool PREF = RAWIN || (!DGRAD && HOLD <= 16 && G::HW <= 128);
-  constexpr int GR = PREF ? ITER : (INM == IN_BNBWD ? 2 : 4);
+  constexpr int GR = PREF ? ITER : (INM == IN_BNBWD && ITER > 4 ? 2 : 4);
   static_assert(ITER % GR == 0, "staging groups");
   [[maybe_unused]] uint4 rv[RAWIN ? 1 : GR][2][QV];
   [[maybe_unused]] uint4 rz[INM == IN_BNBWD ? GR : 1][2];
@@ -325,7 +331,9 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const uint32_t w2 = f32_to_bf16(v2[0][j]) | ((uint32_t)f32_to_bf16(v2[1][j]) << 16);
-          *reinterpret_cast<uint32_t*>(tile + ((ph + 1) * G::WP + pw + j + 1) * CINP + 2 * pr) = w2;
+          const int R = ph + 1, C = pw + j + 1;
+          *reinterpret_cast<uint32_t*>(tile + (R * G::WP + C) * CINP + 8 * ((pr >> 2) ^ tile_swz(R, C)) +
+                                       2 * (pr & 3)) = w2;
         }
       }
     }
@@ -384,9 +392,9 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
       const int p = mt * 32 + l32, ph = p / W, pw = p % W;
       bf16x8 a;
       if constexpr (CIN % 16 == 0) {
-        const int tap = (16 * s) / CIN, c0 = (16 * s) % CIN + 8 * hh;
-        const int kh = tap / 3, kw = tap % 3;
-        a = *reinterpret_cast<const bf16x8*>(tile + ((ph + kh) * G::WP + pw + kw) * CINP + c0);
+        const int tap = (16 * s) / CIN, q = ((16 * s) % CIN) / 8 + hh;
+        const int R = ph + tap / 3, C = pw + tap % 3;
+        a = *reinterpret_cast<const bf16x8*>(tile + (R * G::WP + C) * CINP + 8 * (q ^ tile_swz(R, C)));
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -714,7 +722,7 @@ __device__ __forceinline__ void conv3x3_wgrad_body(const TIN* __restrict__ xin, 
         const int m = t * 32 + l32;
         bf16x8 a;
         if (m < 9 * CIN) {
-          const int c = m / 9, tap = m % 9, kh = tap / 3, kw = tap % 3;   // row m = (ci, tap): slab order
+          const int c = m % CIN, tap = m / CIN, kh = tap / 3, kw = tap % 3;   // row m = (tap, ci)
           a = *reinterpret_cast<const bf16x8*>(X + (kw * CIN + c) * XCS + (ph + kh) * W + pw0);
         } else {
           a = bf16x8{};
@@ -735,9 +743,9 @@ __device__ __forceinline__ void conv3x3_wgrad_body(const TIN* __restrict__ xin, 
       for (int t = 0; t < MTW; ++t) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int m = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;   // (tap, ci) -> slab column ci * 9 + tap
           if (m < 9 * CIN) {
-            float* q = red + l32 * RS + m;
+            float* q = red + l32 * RS + (m % CIN) * 9 + m / CIN;
             *q = (round == 0 ? 0.f : *q) + acc[t][r];
           }
         }
@@ -783,6 +791,290 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wd_kernel(const uint16_t* __re
     conv3x3_body<32, 16, W, IN_BNBWD, OUT_BF16, true, uint16_t>(dh, z, st, wt, dx, nullptr, E, B, chunks_d, spw,
                                                                  BnFwd{}, bnb, brd, nullptr, blockIdx.x - gx_w,
                                                                  blockIdx.y, gridDim.x - gx_w);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// conv3x3_bwd_kernel: a 32-channel layer's weight gradient, data gradient and the previous layer's
+// BN backward reduction from ONE staging of each sample.  conv3x3_wd_kernel runs the wgrad and dgrad
+// bodies as separate workgroups, and each of them reads dh, z and z_prev of every sample: per layer
+// at P128 / 9 streams that is 2 x 3 x 18.9 MB of reads + 18.9 MB of dx.  Here a workgroup stages a
+// sample once --
+//   dz = BN/ReLU backward of (dh, z) into two LDS images: channel-major rows (the wgrad B operand)
+//        and the swizzled channel-last tile (the dgrad A operand, tile_swz);
+//   x  = BN+ReLU(z_prev) into the three column-shifted copies (the wgrad A operand)
+// -- and its 4 waves run both GEMMs on it, interleaved (the dependent dgrad chain beside the wgrad
+// accumulators):
+//   dgrad  wave w: position tiles w, w+4, ... (M = 32 positions, N = 32 input channels, K = 288),
+//          epilogue = bf16 dx + the previous layer's BN backward partials (z_prev re-read from L2);
+//   wgrad  dW rows are (tap, ci) tiles of 32: wave w owns taps w and w+4 over ALL positions (no
+//          cross-wave sum) and a quarter of tap 8's positions -- 18 MFMAs per dgrad tile, same as
+//          the dgrad, 3 accumulator tiles instead of 9; accumulated across the workgroup's samples.
+// P128: the next sample's dh / z / z_prev loads are in flight during the MFMAs.
+// grid (U * chunks, E), block 256, spb samples per workgroup.  Outputs are exactly the two bodies':
+// dx, slab rows (e * gridDim.x + bx) and part rows (u, chunk) -- same arithmetic, same order.
+// ------------------------------------------------------------------------------------------
+template <int W>
+struct BwdGeo {
+  using G = Geo<16, W>;
+  static constexpr int XCS = G::HP * W + 8;    // channel stride of the shifted x copies (bf16)
+  static constexpr int DZS = G::HW + 8;        // channel stride of the channel-major dz rows (bf16)
+  static constexpr int X_EL = 3 * CO * XCS, DZ_EL = CO * DZS, T_EL = G::HP * G::WP * CO;
+  static constexpr int KSD = 18;               // dgrad k-steps (9 taps x 32 channels / 16)
+  static constexpr size_t STAGE = (size_t)(X_EL + DZ_EL + T_EL) * 2 + KSD * 64 * 16 + 2 * CO * NST * 4;
+  static constexpr size_t RED = (CO * (size_t)(9 * CO + 1) + 4 * CO * CO) * 4;   // dW rows | tap-8 partials
+  static constexpr size_t SMEM = STAGE > RED ? STAGE : RED;
+};
+
+template <int W>
+__global__ void __launch_bounds__(256, 2) conv3x3_bwd_kernel(const uint16_t* __restrict__ zprev,
+                                                          const float* __restrict__ st_prev,
+                                                          const uint16_t* __restrict__ dh,
+                                                          const uint16_t* __restrict__ z, const float* __restrict__ st,
+                                                          float* __restrict__ slab, const uint16_t* __restrict__ wt,
+                                                          uint16_t* __restrict__ dx, float* __restrict__ part, int E,
+                                                          int B, int chunks, int spb, BnBwd bnb) {
+  using BG = BwdGeo<W>;
+  using G = typename BG::G;
+  constexpr int HW = G::HW, HP = G::HP, WP = G::WP, XCS = BG::XCS, DZS = BG::DZS;
+  constexpr int KSA = HW / 16;                  // wgrad k-steps (16 positions) per sample
+  constexpr int TPW = G::MT / 4;               // dgrad position tiles per wave
+  constexpr int NDI = HW / 128;                // dz items (channel pair x 8 positions) per thread
+  constexpr int NXI = CO * 16 / 256;           // x items (channel, image row) per thread
+  constexpr int XQ = W / 8;                    // 16-byte vectors per image row
+  constexpr bool PREF = HW <= 128;             // one-sample-ahead register prefetch (P128)
+  static_assert(2 * KSA + KSA / 4 == 18 * TPW, "wgrad steps pair with dgrad k-steps");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __bf16* X = reinterpret_cast<__bf16*>(smem);       // [kw][ci][row][w]
+  __bf16* DZ = X + BG::X_EL;                         // [co][p]
+  __bf16* T = DZ + BG::DZ_EL;                        // [pixel][32] swizzled
+  bf16x8* WB = reinterpret_cast<bf16x8*>(T + BG::T_EL);
+  float* prm = reinterpret_cast<float*>(WB + BG::KSD * 64);   // this layer's records (dz)
+  float* prp = prm + CO * NST;                               // previous layer's records (x, reduction)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int bx = blockIdx.x, e = blockIdx.y, u = bx / chunks, chunk = bx % chunks;
+  const int EC = E * CO;
+  const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
+
+  // ---- zero the tile (its halo stays zero) and the halo rows of the shifted copies ----
+  for (int i = tid; i < BG::T_EL / 8; i += 256) reinterpret_cast<bf16x8*>(T)[i] = bf16x8{};
+  for (int i = tid; i < 3 * CO * 2 * XQ; i += 256) {
+    const int cc = i / (2 * XQ), r = (i / XQ) & 1, q = i % XQ;
+    *reinterpret_cast<bf16x8*>(X + cc * XCS + r * (HP - 1) * W + 8 * q) = bf16x8{};
+  }
+
+  uint4 rd[NDI][2], rz[NDI][2], rx[NXI][XQ];
+  auto load = [&](int n) {
+    const size_t sb = ((size_t)n * E + e) * CO * HW;
+#pragma unroll
+    for (int j = 0; j < NDI; ++j) {
+      const int i = tid + 256 * j, pr = i & 15, sg = i >> 4;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const size_t off = sb + (size_t)(2 * pr + h2) * HW + 8 * sg;
+        rd[j][h2] = *reinterpret_cast<const uint4*>(dh + off);
+        rz[j][h2] = *reinterpret_cast<const uint4*>(z + off);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NXI; ++j) {
+      const int i = tid + 256 * j, c = i >> 4, ph = i & 15;
+      const uint4* src = reinterpret_cast<const uint4*>(zprev + sb + (size_t)c * HW + ph * W);
+#pragma unroll
+      for (int q = 0; q < XQ; ++q) rx[j][q] = src[q];
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < NDI; ++j) {
+      const int i = tid + 256 * j, pr = i & 15, p0 = (i >> 4) * 8;
+      float v[2][8];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int c = 2 * pr + h2;
+        const float* sc = prm + c * NST;
+        const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+        const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+        float d[8], zz[8];
+        unpack_q(rd[j][h2], d, (const uint16_t*)nullptr);
+        unpack_q(rz[j][h2], zz, (const uint16_t*)nullptr);
+        uint32_t w4[4];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = (a * zz[k] + b > 0.f) ? d[k] : 0.f;
+          v[h2][k] = c1 * g - c2 - c3 * (zz[k] - mu) * inv;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          w4[k] = f32_to_bf16(v[h2][2 * k]) | ((uint32_t)f32_to_bf16(v[h2][2 * k + 1]) << 16);
+        *reinterpret_cast<uint4*>(DZ + c * DZS + p0) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+      const int ph = p0 / W, pw = p0 % W;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t w2 = f32_to_bf16(v[0][k]) | ((uint32_t)f32_to_bf16(v[1][k]) << 16);
+        const int R = ph + 1, C = pw + k + 1;
+        *reinterpret_cast<uint32_t*>(T + (R * WP + C) * CO + 8 * ((pr >> 2) ^ tile_swz(R, C)) + 2 * (pr & 3)) = w2;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NXI; ++j) {
+      const int i = tid + 256 * j, c = i >> 4, ph = i & 15;
+      float v[W + 2];
+      v[0] = 0.f;
+      v[W + 1] = 0.f;
+#pragma unroll
+      for (int q = 0; q < XQ; ++q) unpack_q(rx[j][q], v + 1 + 8 * q, (const uint16_t*)nullptr);
+      const float xa = prp[c * NST + ST_A], xb = prp[c * NST + ST_B];
+#pragma unroll
+      for (int q = 1; q <= W; ++q) v[q] = relu_nan(xa * v[q] + xb);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        __bf16* dst = X + (kw * CO + c) * XCS + (ph + 1) * W;
+#pragma unroll
+        for (int q = 0; q < W; q += 8) {
+          bf16x8 o;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = (__bf16)v[q + k + kw];   // column w holds x[w + kw - 1]
+          *reinterpret_cast<bf16x8*>(dst + q) = o;
+        }
+      }
+    }
+  };
+
+  // ---- prologue: first sample's loads, dgrad B fragments, both layers' BN records ----
+  if (PREF && n0 < nend) load(n0);
+  {
+    constexpr int NW = BG::KSD * 64, WPT = (NW + 255) / 256;
+    const bf16x8* wp = reinterpret_cast<const bf16x8*>(wt) + (size_t)e * NW;
+    bf16x8 tw[WPT];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (tid + 256 * k < NW) tw[k] = wp[tid + 256 * k];
+    const float pv = st_prev[((size_t)u * EC + e * CO) * NST + tid];   // 32 channels x NST = one per thread
+    float cv = 0.f;
+    if (bnb.rslab) bn_bwd_build(bnb, st, prm, u, e, EC);
+    else cv = st[((size_t)u * EC + e * CO) * NST + tid];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (tid + 256 * k < NW) WB[tid + 256 * k] = tw[k];
+    prp[tid] = pv;
+    if (!bnb.rslab) prm[tid] = cv;
+  }
+  __syncthreads();
+  const float rmu = prp[l32 * NST + ST_MEAN], rinv = prp[l32 * NST + ST_INV];
+  const float ra = prp[l32 * NST + ST_A], rb = prp[l32 * NST + ST_B];
+
+  f32x16 accw[3];   // taps wv, wv + 4, and this wave's share of tap 8
+#pragma unroll
+  for (int t = 0; t < 3; ++t) accw[t] = f32x16{};
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = n0; n < nend; ++n) {
+    __syncthreads();   // the previous sample's MFMAs are done reading X / DZ / T
+    if (!PREF) load(n);
+    store();
+    if (PREF && n + 1 < nend) load(n + 1);
+    __syncthreads();
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+      const int mt = wv + 4 * tt;
+      // the previous layer's z at this lane's dx positions (L2: staged above), for the reduction
+      uint2 zq[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        zq[g] = *reinterpret_cast<const uint2*>(zprev + ((size_t)n * E + e) * CO * HW + (size_t)l32 * HW + mt * 32 +
+                                                8 * g + 4 * hh);
+      const int p = mt * 32 + l32, ph = p / W, pw = p % W;
+      f32x16 acc = f32x16{};
+#pragma unroll
+      for (int s = 0; s < BG::KSD; ++s) {
+        const int tap = s >> 1, q = ((s & 1) << 1) + hh;
+        const int R = ph + tap / 3, C = pw + tap % 3;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(T + (R * WP + C) * CO + 8 * (q ^ tile_swz(R, C)));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, WB[s * 64 + lane], acc, 0, 0, 0);
+        // wgrad step ws: taps wv / wv + 4 at k-step ws / 2, then tap 8 at this wave's k-steps
+        const int ws = tt * BG::KSD + s;
+        const int j = ws < 2 * KSA ? (ws & 1) : 2;
+        const int wt = j == 0 ? wv : (j == 1 ? wv + 4 : 8);
+        const int ks = ws < 2 * KSA ? (ws >> 1) : wv * (KSA / 4) + ws - 2 * KSA;
+        const int p0 = ks * 16 + 8 * hh, xh = p0 / W, xw = p0 % W;
+        const bf16x8 bz = *reinterpret_cast<const bf16x8*>(DZ + l32 * DZS + p0);
+        const bf16x8 ax =
+            *reinterpret_cast<const bf16x8*>(X + ((wt % 3) * CO + l32) * XCS + (xh + wt / 3) * W + xw);
+        accw[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, bz, accw[j], 0, 0, 0);
+      }
+      // ---- dgrad epilogue: lane holds input channel l32, positions mt*32 + 8g + 4hh + {0..3} ----
+      const size_t rbase = ((size_t)n * E + e) * CO * HW + (size_t)l32 * HW + mt * 32;
+      uint2 pk[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint16_t h0 = f32_to_bf16(acc[4 * g]), h1 = f32_to_bf16(acc[4 * g + 1]);
+        const uint16_t h2 = f32_to_bf16(acc[4 * g + 2]), h3 = f32_to_bf16(acc[4 * g + 3]);
+        pk[g] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
+        const float d[4] = {bf(h0), bf(h1), bf(h2), bf(h3)};
+        const float zz[4] = {__uint_as_float(zq[g].x << 16), __uint_as_float(zq[g].x & 0xffff0000u),
+                             __uint_as_float(zq[g].y << 16), __uint_as_float(zq[g].y & 0xffff0000u)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float gg = (ra * zz[k] + rb > 0.f) ? d[k] : 0.f;
+          s1 += gg;
+          s2 += gg * (zz[k] - rmu) * rinv;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {   // pair (g = 2q, 2q + 1): half-wave hh stores g = 2q + hh
+        const uint2 send = hh ? pk[2 * q] : pk[2 * q + 1];
+        const uint2 recv = make_uint2(__shfl_xor(send.x, 32), __shfl_xor(send.y, 32));
+        const uint2 mine = hh ? pk[2 * q + 1] : pk[2 * q];
+        const uint4 row = hh ? make_uint4(recv.x, recv.y, mine.x, mine.y) : make_uint4(mine.x, mine.y, recv.x, recv.y);
+        *reinterpret_cast<uint4*>(dx + rbase + 8 * (2 * q + hh)) = row;
+      }
+    }
+  }
+
+  // ---- the previous layer's BN backward partials: half-waves, then the 4 waves through LDS ----
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 32);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  if (hh == 0) {
+    red[(wv * 32 + l32) * 2] = s1;
+    red[(wv * 32 + l32) * 2 + 1] = s2;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = tid >> 1, k = tid & 1;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
+    part[(((size_t)u * chunks + chunk) * 2 + k) * EC + e * CO + c] = t;   // planar [2][EC] rows
+  }
+  // ---- weight gradient: [co][ci * 9 + tap] rows in LDS (taps wv, wv + 4 written by their owner;
+  // tap 8 = the 4 waves' partials, summed in wave order), then one coalesced slab row ----
+  constexpr int RS = 9 * CO + 1;
+  __syncthreads();
+  float* wr = reinterpret_cast<float*>(smem);
+  float* p8 = wr + CO * RS;   // [wave][co][ci]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ci = (r & 3) + 8 * (r >> 2) + 4 * hh;   // accumulator row = ci, column = co = l32
+    wr[l32 * RS + ci * 9 + wv] = accw[0][r];
+    wr[l32 * RS + ci * 9 + wv + 4] = accw[1][r];
+    p8[(wv * CO + l32) * CO + ci] = accw[2][r];
+  }
+  __syncthreads();
+  float* srow = slab + ((size_t)e * gridDim.x + bx) * CO * CO * 9;
+  for (int i = tid; i < CO * CO * 9; i += 256) {
+    const int co = i / (CO * 9), m = i % (CO * 9);
+    float v;
+    if (m % 9 == 8) {
+      const int ci = m / 9;
+      v = ((p8[co * CO + ci] + p8[(CO + co) * CO + ci]) + p8[(2 * CO + co) * CO + ci]) + p8[(3 * CO + co) * CO + ci];
+    } else {
+      v = wr[co * RS + m];
+    }
+    srow[i] = v;
   }
 }
 
@@ -1196,7 +1488,7 @@ using namespace qd::conv;
   else return (int)hipErrorInvalidValue;
 
 static size_t fwd_smem(int cin, int H, int W) {
-  const int cinp = (cin % 16 == 0) ? cin + QD_CINP_PAD : cin;
+  const int cinp = cin;
   const int ks = (9 * cin + 15) / 16;   // (dgrad: cin = 32 -> 18 = the dgrad pack's k-steps too)
   // 4 wave tiles | B fragments | BN params
   return 4 * (size_t)(H + 2) * (W + 2) * cinp * 2 + (size_t)ks * 64 * 16 + (size_t)cin * NST * sizeof(float);
@@ -1351,6 +1643,26 @@ QD_API int qd_conv_wgrad_dgrad(const uint16_t* xin, const float* st_prev, const 
     if (hipError_t e = qd::allow_lds(conv3x3_wd_kernel<WW>, sm)) return (int)e;
     hipLaunchKernelGGL((conv3x3_wd_kernel<WW>), grid, dim3(256), sm, s, xin, st_prev, dh, z, st, slab, chunks_w, spb, bb,
                        w, dx, chunks_d, spw, br, E, B, gx_w);
+  })
+  return (int)hipGetLastError();
+}
+
+// wgrad + dgrad + the previous layer's BN backward partials of a 32-channel layer from one staging
+// per sample (see conv3x3_bwd_kernel).  zprev / st_prev: the previous layer's pre-BN output and its
+// records (x = BN+ReLU(zprev)); wt: dgrad B fragments; part: (U, chunks, 2, EC); slab rows as
+// qd_conv_wgrad's with the same chunking.
+QD_API int qd_conv_bwd_fused(const uint16_t* zprev, const float* st_prev, const uint16_t* dh, const uint16_t* z,
+                             const float* st, float* slab, const uint16_t* w, uint16_t* dx, float* part, int N, int E,
+                             int B, int H, int W, int chunks, int spb, const BnBwd* bnb, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const BnBwd bb = bnb ? *bnb : BnBwd{};
+  if (chunks * spb < B || N % B) return (int)hipErrorInvalidValue;
+  dim3 grid((N / B) * chunks, E);
+  QD_GEOM(WW, {
+    const size_t sm = BwdGeo<WW>::SMEM;
+    if (hipError_t e = qd::allow_lds(conv3x3_bwd_kernel<WW>, sm)) return (int)e;
+    hipLaunchKernelGGL((conv3x3_bwd_kernel<WW>), grid, dim3(256), sm, s, zprev, st_prev, dh, z, st, slab, w, dx, part,
+                       E, B, chunks, spb, bb);
   })
   return (int)hipGetLastError();
 }

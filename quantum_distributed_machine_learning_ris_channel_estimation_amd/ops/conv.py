@@ -116,6 +116,11 @@ class ConvStackHIP:
                                                         _p, _p, _p])
         # wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate launches)
         self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
+        # ... and from ONE staging of each sample (conv3x3_bwd_kernel: dh / z / z_prev read once for both
+        # GEMMs; QDML_CONV_BWD_FUSED=0: the side-by-side wd kernel).  Its chunking serves both the wgrad
+        # slab and the previous layer's BN partials, so it needs chunks_wl[k] == the partials' chunks.
+        self.bwd_fused = os.environ.get("QDML_CONV_BWD_FUSED", "1") != "0"
+        self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p])
 
     def pack_weights(self, st, cursor: Optional[torch.Tensor] = None, cursor_inc: int = 0) -> None:
         """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch.
@@ -225,6 +230,15 @@ class ConvStackHIP:
             xin = self.x1 if k == 0 else self.z[k - 1]
             st_prev = None if k == 0 else self.st[k - 1]
             ws = self.wslab[k]
+            if (k > 0 and self.bwd_fused and dh_bf and self.dx_bf16 and self.fuse_bn_red and side is None
+                    and self.chunks_wl[k] == self.rchunks[k - 1]):
+                dx = self.dx[k - 1]
+                nat.check(self._bwdf(nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), nat.ptr(z), nat.ptr(bst), nat.ptr(ws),
+                                     nat.ptr(self.wpk_t[k]), nat.ptr(dx), nat.ptr(self.rslab[k - 1]), self.N, self.E,
+                                     self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k], ctypes.byref(bnb), st),
+                          f"conv_bwd_fused{k + 1}")
+                dh, dh_bf = dx, 1
+                continue
             if k > 0 and self.fuse_wd and dh_bf and self.dx_bf16 and side is None:
                 # weight AND data gradient of this layer in one launch (independent: side by side)
                 dx = self.dx[k - 1]

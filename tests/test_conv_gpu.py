@@ -89,6 +89,36 @@ def test_conv_stack_backward(cuda, pilot_num, B):
             assert rel(ga, gb) < 3e-2, (k, name, rel(ga, gb))
 
 
+@pytest.mark.parametrize("pilot_num,B", [(128, 256), (128, 40), (256, 64)])
+def test_conv_bwd_fused_matches_side_by_side(cuda, pilot_num, B):
+    """conv3x3_bwd_kernel (one staging per sample feeds wgrad, dgrad and the previous layer's BN
+    partials) vs conv3x3_wd_kernel (the two bodies as separate workgroups): dx and the BN partials are
+    the same arithmetic in the same order (bitwise); dW sums the positions in a different grouping."""
+    U = 3
+    outs = []
+    for fused in (True, False):
+        a, _ = pair(cuda, pilot_num)
+        torch.manual_seed(1)
+        Yp = torch.randn(3, U, B, 2, a.H, a.W, device=cuda)
+        conv = ConvStackHIP(a, U, B)
+        conv.bwd_fused = fused
+        conv.forward(a.pack_input(Yp).contiguous(), training=True)
+        dh = torch.randn(U * B * 3, 32 * a.H * a.W, device=cuda).to(torch.bfloat16)
+        a.space.zero_grad()
+        conv.backward(dh)
+        torch.cuda.synchronize()
+        outs.append(dict(dx0=conv.dx[0].clone(), dx1=conv.dx[1].clone(),
+                         **{f"W{k}": a.conv_w[k].grad.clone() for k in range(3)},
+                         **{f"g{k}": a.bn_w[k].grad.clone() for k in range(3)},
+                         **{f"b{k}": a.bn_b[k].grad.clone() for k in range(3)}))
+    f, r = outs
+    for name in f:
+        if name.startswith("W"):
+            assert rel(f[name], r[name]) < 1e-5, (name, rel(f[name], r[name]))
+        else:
+            assert torch.equal(f[name], r[name]), (name, rel(f[name], r[name]))
+
+
 # Whole-step conv weight-gradient error vs the fp32 autograd step, measured on MI355X (seed 0):
 # relative Frobenius 0.088 / 0.065 / 0.034 and cosine 0.99614 / 0.99787 / 0.99942 for conv1..3.
 # fro^2 ~= 2(1 - cos) there, i.e. the difference is noise, not a scale or direction error; it grows
