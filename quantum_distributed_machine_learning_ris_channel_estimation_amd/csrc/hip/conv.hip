@@ -806,7 +806,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_wd_kernel(const uint16_t* __re
 // -- and its 4 waves run both GEMMs on it, interleaved (the dependent dgrad chain beside the wgrad
 // accumulators):
 //   dgrad  wave w: position tiles w, w+4, ... (M = 32 positions, N = 32 input channels, K = 288),
-//          epilogue = bf16 dx + the previous layer's BN backward partials (z_prev re-read from L2);
+//          epilogue = bf16 dx + the previous layer's BN backward partials (raw z_prev kept in LDS: a
+//          global re-read there would wait out the next sample's prefetch, vmcnt being in order);
 //   wgrad  dW rows are (tap, ci) tiles of 32: wave w owns taps w and w+4 over ALL positions (no
 //          cross-wave sum) and a quarter of tap 8's positions -- 18 MFMAs per dgrad tile, same as
 //          the dgrad, 3 accumulator tiles instead of 9; accumulated across the workgroup's samples.
@@ -819,15 +820,16 @@ struct BwdGeo {
   using G = Geo<16, W>;
   static constexpr int XCS = G::HP * W + 8;    // channel stride of the shifted x copies (bf16)
   static constexpr int DZS = G::HW + 8;        // channel stride of the channel-major dz rows (bf16)
-  static constexpr int X_EL = 3 * CO * XCS, DZ_EL = CO * DZS, T_EL = G::HP * G::WP * CO;
+  static constexpr int ZPS = G::HW + 4;        // raw z_prev rows [ci][p] (ds_read_b64: 66 dwords per row)
+  static constexpr int X_EL = 3 * CO * XCS, DZ_EL = CO * DZS, T_EL = G::HP * G::WP * CO, ZP_EL = CO * ZPS;
   static constexpr int KSD = 18;               // dgrad k-steps (9 taps x 32 channels / 16)
-  static constexpr size_t STAGE = (size_t)(X_EL + DZ_EL + T_EL) * 2 + KSD * 64 * 16 + 2 * CO * NST * 4;
+  static constexpr size_t STAGE = (size_t)(X_EL + DZ_EL + T_EL + ZP_EL) * 2 + KSD * 64 * 16 + 2 * CO * NST * 4;
   static constexpr size_t RED = (CO * (size_t)(9 * CO + 1) + 4 * CO * CO) * 4;   // dW rows | tap-8 partials
   static constexpr size_t SMEM = STAGE > RED ? STAGE : RED;
 };
 
 template <int W>
-__global__ void __launch_bounds__(256, 2) conv3x3_bwd_kernel(const uint16_t* __restrict__ zprev,
+__global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const uint16_t* __restrict__ zprev,
                                                           const float* __restrict__ st_prev,
                                                           const uint16_t* __restrict__ dh,
                                                           const uint16_t* __restrict__ z, const float* __restrict__ st,
@@ -848,7 +850,8 @@ __global__ void __launch_bounds__(256, 2) conv3x3_bwd_kernel(const uint16_t* __r
   __bf16* X = reinterpret_cast<__bf16*>(smem);       // [kw][ci][row][w]
   __bf16* DZ = X + BG::X_EL;                         // [co][p]
   __bf16* T = DZ + BG::DZ_EL;                        // [pixel][32] swizzled
-  bf16x8* WB = reinterpret_cast<bf16x8*>(T + BG::T_EL);
+  uint16_t* ZP = reinterpret_cast<uint16_t*>(T + BG::T_EL);   // [ci][p] raw z_prev
+  bf16x8* WB = reinterpret_cast<bf16x8*>(ZP + BG::ZP_EL);
   float* prm = reinterpret_cast<float*>(WB + BG::KSD * 64);   // this layer's records (dz)
   float* prp = prm + CO * NST;                               // previous layer's records (x, reduction)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -925,7 +928,12 @@ __global__ void __launch_bounds__(256, 2) conv3x3_bwd_kernel(const uint16_t* __r
       v[0] = 0.f;
       v[W + 1] = 0.f;
 #pragma unroll
-      for (int q = 0; q < XQ; ++q) unpack_q(rx[j][q], v + 1 + 8 * q, (const uint16_t*)nullptr);
+      for (int q = 0; q < XQ; ++q) {
+        unpack_q(rx[j][q], v + 1 + 8 * q, (const uint16_t*)nullptr);
+        uint2* zp = reinterpret_cast<uint2*>(ZP + c * BG::ZPS + ph * W + 8 * q);   // (8-byte aligned rows)
+        zp[0] = make_uint2(rx[j][q].x, rx[j][q].y);
+        zp[1] = make_uint2(rx[j][q].z, rx[j][q].w);
+      }
       const float xa = prp[c * NST + ST_A], xb = prp[c * NST + ST_B];
 #pragma unroll
       for (int q = 1; q <= W; ++q) v[q] = relu_nan(xa * v[q] + xb);
@@ -965,6 +973,9 @@ __global__ void __launch_bounds__(256, 2) conv3x3_bwd_kernel(const uint16_t* __r
   __syncthreads();
   const float rmu = prp[l32 * NST + ST_MEAN], rinv = prp[l32 * NST + ST_INV];
   const float ra = prp[l32 * NST + ST_A], rb = prp[l32 * NST + ST_B];
+  bf16x8 wreg[BG::KSD];   // the dgrad B fragments stay in registers (each wave reads them once)
+#pragma unroll
+  for (int k = 0; k < BG::KSD; ++k) wreg[k] = WB[k * 64 + lane];
 
   f32x16 accw[3];   // taps wv, wv + 4, and this wave's share of tap 8
 #pragma unroll
@@ -979,12 +990,10 @@ __global__ void __launch_bounds__(256, 2) conv3x3_bwd_kernel(const uint16_t* __r
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt) {
       const int mt = wv + 4 * tt;
-      // the previous layer's z at this lane's dx positions (L2: staged above), for the reduction
+      // the previous layer's z at this lane's dx positions (for the reduction)
       uint2 zq[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        zq[g] = *reinterpret_cast<const uint2*>(zprev + ((size_t)n * E + e) * CO * HW + (size_t)l32 * HW + mt * 32 +
-                                                8 * g + 4 * hh);
+      for (int g = 0; g < 4; ++g) zq[g] = *reinterpret_cast<const uint2*>(ZP + l32 * BG::ZPS + mt * 32 + 8 * g + 4 * hh);
       const int p = mt * 32 + l32, ph = p / W, pw = p % W;
       f32x16 acc = f32x16{};
 #pragma unroll
@@ -992,7 +1001,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_bwd_kernel(const uint16_t* __r
         const int tap = s >> 1, q = ((s & 1) << 1) + hh;
         const int R = ph + tap / 3, C = pw + tap % 3;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(T + (R * WP + C) * CO + 8 * (q ^ tile_swz(R, C)));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, WB[s * 64 + lane], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, wreg[s], acc, 0, 0, 0);
         // wgrad step ws: taps wv / wv + 4 at k-step ws / 2, then tap 8 at this wave's k-steps
         const int ws = tt * BG::KSD + s;
         const int j = ws < 2 * KSA ? (ws & 1) : 2;

@@ -47,7 +47,7 @@ class ConvStackHIP:
     """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
 
     def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 8, spb_r: int = 4, spb_w1: int = 4,
-                 dx_bf16: bool = True):
+                 dx_bf16: bool = True, bwd_fused: Optional[bool] = None, spb_f: int = 5):
         self.m = model
         self.count_batches = False   # set by the owner that stops counting num_batches_tracked itself
         self.stage_hook = None       # optional callable(stage name) between forward launches
@@ -62,8 +62,16 @@ class ConvStackHIP:
         self.chunks = (B + 4 * spw - 1) // (4 * spw)          # forward / dgrad: 4 waves x spw samples
         self.spb_w = spb_w
         self.chunks_w = (B + spb_w - 1) // spb_w              # wgrad workgroups per group
+        # backward of layers 3 and 2 (dx bf16): conv3x3_bwd_kernel computes wgrad, dgrad and the previous
+        # layer's BN partials from ONE staging of each sample, spb_f samples per workgroup (5: 468
+        # workgroups, two resident per CU, one staging while the other computes; 8 = 288 workgroups
+        # left half the CUs with one and measured slower than the side-by-side wd kernel).
+        # QDML_CONV_BWD_FUSED=0: wgrad and dgrad as separate workgroups of the wd kernel.
+        if bwd_fused is None:
+            bwd_fused = os.environ.get("QDML_CONV_BWD_FUSED", "1") != "0"
+        self.bwd_fused = bool(bwd_fused) and dx_bf16
         # layer 1 (2 input channels) is one accumulator tile: staging-bound, so more, shorter workgroups
-        self.spb_wl = (spb_w1, spb_w, spb_w)
+        self.spb_wl = (spb_w1, spb_f, spb_f) if self.bwd_fused else (spb_w1, spb_w, spb_w)
         self.chunks_wl = tuple((B + s - 1) // s for s in self.spb_wl)
         self.spb_r = spb_r
         self.chunks_r = (B + spb_r - 1) // spb_r              # BN backward reductions
@@ -77,10 +85,13 @@ class ConvStackHIP:
         self.stats = [torch.zeros(U, self.chunks, EC, 2, device=dev) for _ in range(3)]   # per layer
         # BN backward partials per layer, planar rows [sum g | sum g*xhat] x EC (their column sums are
         # dbeta / dgamma: jobs of the step's batched slab reduction)
-        # (layers 1, 2: produced by the next layer's dgrad kernel, chunked like it; layer 3: by its own
-        # reduction launch over dh3 from the FC GEMM)
+        # (layers 1, 2: produced by the next layer's fused backward / dgrad kernel, chunked like it;
+        # layer 3: by its own reduction launch over dh3 from the FC GEMM)
         self.fuse_bn_red = dx_bf16
-        self.rchunks = [self.chunks if self.fuse_bn_red else self.chunks_r] * 2 + [self.chunks_r]
+        if self.bwd_fused:
+            self.rchunks = [self.chunks_wl[1], self.chunks_wl[2], self.chunks_r]
+        else:
+            self.rchunks = [self.chunks if self.fuse_bn_red else self.chunks_r] * 2 + [self.chunks_r]
         self.rslab = [torch.zeros(U, c, 2, EC, device=dev) for c in self.rchunks]
         # grads w.r.t. h1, h2: bf16 by default (they only feed bf16 MFMA operands and fp32-accumulated
         # BN reductions), halving the dgrad write and every re-read of it
@@ -114,12 +125,8 @@ class ConvStackHIP:
         self.pack_at_tail = False
         self._wd = nat.fn(L, "qd_conv_wgrad_dgrad", [_p, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i,
                                                         _p, _p, _p])
-        # wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate launches)
+        # (bwd_fused off) wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate)
         self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
-        # ... and from ONE staging of each sample (conv3x3_bwd_kernel: dh / z / z_prev read once for both
-        # GEMMs; QDML_CONV_BWD_FUSED=0: the side-by-side wd kernel).  Its chunking serves both the wgrad
-        # slab and the previous layer's BN partials, so it needs chunks_wl[k] == the partials' chunks.
-        self.bwd_fused = os.environ.get("QDML_CONV_BWD_FUSED", "1") != "0"
         self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p])
 
     def pack_weights(self, st, cursor: Optional[torch.Tensor] = None, cursor_inc: int = 0) -> None:
@@ -218,6 +225,7 @@ class ConvStackHIP:
         m, st = self.m, nat.stream_ptr(dh3.device)
         main = torch.cuda.current_stream(dh3.device) if side is not None else None
         dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
+        side_used = False
         for k in (2, 1, 0):
             z, bst = self.z[k], self.st[k]
             rs = self.rslab[k]
@@ -230,8 +238,8 @@ class ConvStackHIP:
             xin = self.x1 if k == 0 else self.z[k - 1]
             st_prev = None if k == 0 else self.st[k - 1]
             ws = self.wslab[k]
-            if (k > 0 and self.bwd_fused and dh_bf and self.dx_bf16 and self.fuse_bn_red and side is None
-                    and self.chunks_wl[k] == self.rchunks[k - 1]):
+            # (the fused kernel has no separate weight-gradient launch to put on ``side``)
+            if k > 0 and self.bwd_fused and dh_bf:
                 dx = self.dx[k - 1]
                 nat.check(self._bwdf(nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), nat.ptr(z), nat.ptr(bst), nat.ptr(ws),
                                      nat.ptr(self.wpk_t[k]), nat.ptr(dx), nat.ptr(self.rslab[k - 1]), self.N, self.E,
@@ -253,6 +261,7 @@ class ConvStackHIP:
             on_side = side is not None and k > 0
             if on_side:
                 side.wait_stream(main)
+                side_used = True
             wst = nat.stream_ptr(dh3.device) if not on_side else ctypes.c_void_p(side.cuda_stream)
             nat.check(self._wgrad(k + 1, nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst),
                                   nat.ptr(ws), self.N, self.E, self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k],
@@ -267,7 +276,7 @@ class ConvStackHIP:
                                       self.chunks, self.spw, ctypes.byref(bnb),
                                       ctypes.byref(brd) if brd is not None else None, st), f"conv_dgrad{k + 1}")
                 dh, dh_bf = dx, int(self.dx_bf16)
-        if side is not None:
+        if side_used:
             main.wait_stream(side)
         # the three weight-gradient slabs -> conv_w grads: queued on the caller's batch (one launch
         # for every slab reduction of the step phase) or launched here
