@@ -538,6 +538,228 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------
+// conv3x3_f8_kernel: the fp8 estimator's 32-channel forward (layers 2, 3) on e4m3 operands.
+// conv3x3_body's structure with an e4m3 channel-last tile -- 32-byte pixels, 8-byte chunks at
+// q ^ tile8_swz(R, C): conflict-free ds_read_b64 fragment reads (lane halves of 32) for every tap
+// of both geometries -- e4m3 B fragments (qd_conv_pack_f8) and mfma_f32_32x32x16_fp8_fp8 (lane l:
+// A[row l&31][k = 8(l>>5) + j], the bf16 form's map; K order (tap, channel) as the bf16 pack).
+// Input transform h = BN+ReLU(z_prev) -> e4m3(h * qs_a) with the delayed activation scale; the
+// epilogue scales the accumulators by deq = scale_a * scale_w, then writes bf16 z + statistics
+// exactly as the bf16 body (the BN backward still sees bf16 z).  amax_a[block] = max h of the
+// block for the next step's scale.  W = 8: the next sample's loads fly during the MFMAs.
+// ------------------------------------------------------------------------------------------
+template <int W>
+__device__ __forceinline__ int tile8_swz(int R, int C) {
+  if constexpr (W == 8) return R & 3;
+  else return (R + 2 * (C >> 3)) & 3;
+}
+constexpr int KS8 = 18;   // 16-deep k-steps of a 32-channel layer
+
+template <int W>
+__global__ void __launch_bounds__(256, 2) conv3x3_f8_kernel(const uint16_t* __restrict__ xin,
+                                                         const uint8_t* __restrict__ wt8, uint16_t* __restrict__ out,
+                                                         float* __restrict__ stats, int E, int B, int chunks, int spw,
+                                                         BnFwd bnf, const float* __restrict__ qs,
+                                                         const float* __restrict__ scale, float* __restrict__ amax_a) {
+  using G = Geo<16, W>;
+  constexpr int CIN = 32, PIX = 32;
+  constexpr int TILE = G::HP * G::WP * PIX;     // bytes per wave tile
+  constexpr int ITER = 8 * G::HW / 8 / 64;      // staging items (channel quad x 8 positions) per lane
+  constexpr bool PREF = G::HW <= 128;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int bx = blockIdx.x, e = blockIdx.y, u = bx / chunks, chunk = bx % chunks;
+  const int EC_in = E * CIN;
+  uint8_t* tile = reinterpret_cast<uint8_t*>(smem) + wv * TILE;
+  for (int i = lane; i < TILE / 16; i += 64) reinterpret_cast<uint4*>(tile)[i] = make_uint4(0u, 0u, 0u, 0u);
+  uint2* wl = reinterpret_cast<uint2*>(smem + 4 * TILE);   // [s][lane] 8-byte B fragments
+  float* stl = reinterpret_cast<float*>(wl + KS8 * 64);    // BN records of the input channels
+  const float qa = qs[0], deq = scale[0] * scale[1];
+  const int n0 = u * B + (chunk * 4 + wv) * spw;
+  const int nend = min((u + 1) * B, n0 + spw);
+
+  // staging item: 8 positions x 4 channels (bf16), one dword per pixel in the e4m3 tile
+  auto load_item = [&](int n, int it, uint4 (&r)[4]) {
+    const size_t base = ((size_t)n * E + e) * CIN * G::HW;
+    const int i = lane + 64 * it, qd = i & 7, sg = i >> 3;
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4)
+      r[c4] = *reinterpret_cast<const uint4*>(xin + base + (size_t)(4 * qd + c4) * G::HW + 8 * sg);
+  };
+  float mx = 0.f;
+  auto store_item = [&](int it, const uint4 (&r)[4]) {
+    {
+      const int i = lane + 64 * it, qd = i & 7, p0 = (i >> 3) * 8;
+      float v[4][8];
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const float* sc = stl + (4 * qd + c4) * NST;
+        const float a = sc[ST_A], b = sc[ST_B];
+        unpack_q(r[c4], v[c4], (const uint16_t*)nullptr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[c4][j] = relu_nan(a * v[c4][j] + b);
+          mx = fmaxf(mx, v[c4][j]);
+        }
+      }
+      const int ph = p0 / W, pw = p0 % W;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int R = ph + 1, C = pw + j + 1;
+        const uint32_t q4 = e4m3_pack4(v[0][j] * qa, v[1][j] * qa, v[2][j] * qa, v[3][j] * qa);
+        *reinterpret_cast<uint32_t*>(tile + (R * G::WP + C) * PIX + 8 * ((qd >> 1) ^ tile8_swz<W>(R, C)) +
+                                     4 * (qd & 1)) = q4;
+      }
+    }
+  };
+  uint4 rv[PREF ? ITER : 1][4];   // (P128) the next sample's items
+  auto load = [&](int n) {
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) load_item(n, it, rv[it]);
+  };
+  auto stage = [&](int n) {
+    if constexpr (PREF) {
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) store_item(it, rv[it]);
+    } else {
+#pragma unroll 1
+      for (int it = 0; it < ITER; ++it) {   // one item in registers at a time (P256)
+        load_item(n, it, rv[0]);
+        store_item(it, rv[0]);
+      }
+    }
+  };
+  if (PREF && n0 < nend) load(n0);
+  {
+    const uint2* wp = reinterpret_cast<const uint2*>(wt8) + (size_t)e * KS8 * 64;
+    uint2 tw[(KS8 * 64 + 255) / 256];
+#pragma unroll
+    for (int k = 0; k < (KS8 * 64 + 255) / 256; ++k)
+      if (tid + 256 * k < KS8 * 64) tw[k] = wp[tid + 256 * k];
+    float tp = 0.f;
+    if (!bnf.stats) tp = bnf.st_out[((size_t)u * EC_in + e * CIN) * NST + tid];   // (records given as is)
+#pragma unroll
+    for (int k = 0; k < (KS8 * 64 + 255) / 256; ++k)
+      if (tid + 256 * k < KS8 * 64) wl[tid + 256 * k] = tw[k];
+    if (bnf.stats) bn_fwd_build(bnf, stl, u, e, EC_in, chunk == 0);
+    else stl[tid] = tp;
+  }
+  __syncthreads();
+
+  float s1 = 0.f, s2 = 0.f;
+  for (int n = n0; n < nend; ++n) {
+    wave_lds_fence();
+    stage(n);
+    if (PREF && n + 1 < nend) load(n + 1);
+    wave_lds_fence();
+    auto load_a = [&](int mt, int s) -> long {
+      const int p = mt * 32 + l32, ph = p / W, pw = p % W;
+      const int tap = s >> 1, q = ((s & 1) << 1) + hh;
+      const int R = ph + tap / 3, C = pw + tap % 3;
+      const uint2 v = *reinterpret_cast<const uint2*>(tile + (R * G::WP + C) * PIX + 8 * (q ^ tile8_swz<W>(R, C)));
+      return (long)(((unsigned long)v.y << 32) | v.x);
+    };
+    constexpr int MG = G::MT < 4 ? G::MT : 4;
+#pragma unroll
+    for (int g0 = 0; g0 < G::MT; g0 += MG) {
+      f32x16 acc[MG];
+#pragma unroll
+      for (int j = 0; j < MG; ++j) acc[j] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < KS8; ++s) {
+        const uint2 bw = wl[s * 64 + lane];
+        const long b = (long)(((unsigned long)bw.y << 32) | bw.x);
+#pragma unroll
+        for (int j = 0; j < MG; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(load_a(g0 + j, s), b, acc[j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < MG; ++j) {
+        const int mt = g0 + j;
+        const size_t rbase = ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + mt * 32;
+        uint2 pk[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint16_t h0 = f32_to_bf16(acc[j][4 * g] * deq), h1 = f32_to_bf16(acc[j][4 * g + 1] * deq);
+          const uint16_t h2 = f32_to_bf16(acc[j][4 * g + 2] * deq), h3 = f32_to_bf16(acc[j][4 * g + 3] * deq);
+          pk[g] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
+          const float v0 = bf(h0), v1 = bf(h1), v2 = bf(h2), v3 = bf(h3);
+          s1 += v0 + v1 + v2 + v3;
+          s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint2 send = hh ? pk[2 * q] : pk[2 * q + 1];
+          const uint2 recv = make_uint2(__shfl_xor(send.x, 32), __shfl_xor(send.y, 32));
+          const uint2 mine = hh ? pk[2 * q + 1] : pk[2 * q];
+          const uint4 row = hh ? make_uint4(recv.x, recv.y, mine.x, mine.y) : make_uint4(mine.x, mine.y, recv.x, recv.y);
+          *reinterpret_cast<uint4*>(out + rbase + 8 * (2 * q + hh)) = row;
+        }
+      }
+    }
+  }
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 32);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  if (hh == 0) {
+    red[(wv * 32 + l32) * 2] = s1;
+    red[(wv * 32 + l32) * 2 + 1] = s2;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = tid >> 1, k = tid & 1;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
+    stats[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;
+  }
+  // the block's max h (h >= 0) -> its amax partial (index: the flat block id; < kAmaxParts)
+  float m = mx;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __syncthreads();
+  if (lane == 0) red[wv] = m;
+  __syncthreads();
+  if (tid == 0) {
+    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float* ap = amax_a + (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    *ap = fmaxf(*ap, bm);
+  }
+}
+
+// fp8 weight images of layers 2, 3 (blockIdx.z = job): e4m3(W * qs_w) B fragments [e][s][lane][8] in
+// conv3x3_f8_kernel's k order, and the block's max |W| into the weight amax partials.
+struct PackF8Jobs {
+  const float* w[2];
+  uint8_t* out[2];
+  const float* qs[2];     // weight quantisation factors
+  float* amax[2];         // weight amax partials
+};
+__global__ void __launch_bounds__(64) pack_weights_f8_kernel(PackF8Jobs jobs) {
+  const int s = blockIdx.x, e = blockIdx.y, jb = blockIdx.z, lane = threadIdx.x;
+  const int hh = lane >> 5, col = lane & 31;
+  const float* w = jobs.w[jb];
+  const float q = jobs.qs[jb][0];
+  float v[8], mx = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * s + 8 * hh + j;   // (tap k / 32, input channel k % 32)
+    v[j] = w[((size_t)(e * CO + col) * CO + k % CO) * 9 + k / CO];
+    mx = fmaxf(mx, fabsf(v[j]));
+  }
+  const uint32_t lo = e4m3_pack4(v[0] * q, v[1] * q, v[2] * q, v[3] * q);
+  const uint32_t hi = e4m3_pack4(v[4] * q, v[5] * q, v[6] * q, v[7] * q);
+  reinterpret_cast<uint2*>(jobs.out[jb])[((size_t)e * KS8 + s) * 64 + lane] = make_uint2(lo, hi);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) {
+    float* ap = jobs.amax[jb] + (size_t)e * gridDim.x + s;
+    *ap = fmaxf(*ap, mx);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // pack_weights_kernel: fp32 W (E*32, CIN, 3, 3) -> bf16 B fragments [e][s][lane][8] in the
 // exact register order conv3x3_kernel consumes (16-byte coalesced loads per lane).
 // dgrad = 1: transposed + spatially flipped (the data-gradient correlation).
@@ -1557,6 +1779,34 @@ QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const u
                                     dim3(256), fwd_smem(32, H, W), s, (const uint16_t*)xin, nullptr, st_prev, w, z,
                                     stats, E, B, chunks, spw, bf, bb, BnRed{}))
   }
+  return (int)hipGetLastError();
+}
+
+// fp8 forward of a 32->32 layer (see conv3x3_f8_kernel).  w8: qd_conv_pack_f8's image; qs / scale: the
+// layer's (activation, weight) pair of quantisation / dequantisation factors; amax_a: the activation
+// amax partials (indexed by the flat block id).
+QD_API int qd_conv_fwd_f8(const uint16_t* xin, const uint8_t* w8, uint16_t* z, float* stats, int N, int E, int B, int H,
+                          int W, int chunks, int spw, const BnFwd* bnf, const float* qs, const float* scale,
+                          float* amax_a, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!bnf || chunks * 4 * spw < B || (N / B) * chunks * E > qd::kAmaxParts) return (int)hipErrorInvalidValue;
+  const BnFwd bf = *bnf;
+  dim3 grid((N / B) * chunks, E);
+  QD_GEOM(WW, {
+    const size_t sm = 4 * (size_t)(16 + 2) * (WW + 2) * 32 + (size_t)KS8 * 64 * 8 + 32 * NST * sizeof(float);
+    hipLaunchKernelGGL((conv3x3_f8_kernel<WW>), grid, dim3(256), sm, s, xin, w8, z, stats, E, B, chunks, spw, bf, qs,
+                       scale, amax_a);
+  })
+  return (int)hipGetLastError();
+}
+
+// e4m3 weight images of layers 2 and 3 in one launch: w[j] fp32 (E, 32, 32, 3, 3) -> out[j]
+// (E, 18, 64, 8) bytes with qs[j][0]; amax[j]: that weight's amax partials (E * 18 used).
+QD_API int qd_conv_pack_f8(const float* w2, const float* w3, uint8_t* o2, uint8_t* o3, const float* qs2,
+                           const float* qs3, float* amax2, float* amax3, int E, void* stream) {
+  if (E * KS8 > qd::kAmaxParts) return (int)hipErrorInvalidValue;
+  PackF8Jobs j{{w2, w3}, {o2, o3}, {qs2, qs3}, {amax2, amax3}};
+  hipLaunchKernelGGL(pack_weights_f8_kernel, dim3(KS8, E, 2), dim3(64), 0, (hipStream_t)stream, j);
   return (int)hipGetLastError();
 }
 

@@ -81,6 +81,23 @@ class ConvStackHIP:
         self.h3 = torch.empty(N * self.E, 32 * HW, device=dev, dtype=bf)
         self.fp8 = getattr(model, "fp8", False)
         self.h3_8 = torch.empty(N * self.E, 32 * HW, device=dev, dtype=torch.float8_e4m3fn) if self.fp8 else None
+        # fp8 estimator: the 32-channel forward convs (layers 2, 3) on e4m3 MFMA (conv3x3_f8_kernel) with
+        # delayed per-tensor scales: slots 2..5 = [act2, w2, act3, w3] of the model's Fp8Scales (updated
+        # with the FC's after the FC forward).  QDML_FP8_CONV=0: bf16 convs, e4m3 FC only.
+        f8m = getattr(model, "fp8_scales", None)
+        self.f8conv = (self.fp8 and dev.type == "cuda" and f8m is not None and f8m.n >= 6
+                       and os.environ.get("QDML_FP8_CONV", "1") != "0")
+        self.wpk8 = [None] + [torch.empty(self.E, 18, 64, 8, device=dev, dtype=torch.uint8) for _ in range(2)] \
+            if self.f8conv else None
+        self.f8s, self.f8o = (f8m, 2) if self.f8conv else (None, 0)
+        if self.f8conv:
+            from .optim import FP8_E4M3_MAX
+            for j in range(2):
+                self.f8s.set_from_tensor(2 + 2 * j + 1, model.conv_w[j + 1])
+                # activations: BN-normalised ReLU outputs; the first step's guess, then the delayed amax
+                a = 8.0 * 2.0 ** self.f8s.margin / FP8_E4M3_MAX
+                self.f8s.scale[2 + 2 * j] = a
+                self.f8s.qs[2 + 2 * j] = 1.0 / a
         self.st = [torch.zeros(U, EC, NST, device=dev) for _ in range(3)]
         self.stats = [torch.zeros(U, self.chunks, EC, 2, device=dev) for _ in range(3)]   # per layer
         # BN backward partials per layer, planar rows [sum g | sum g*xhat] x EC (their column sums are
@@ -128,6 +145,8 @@ class ConvStackHIP:
         # (bwd_fused off) wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate)
         self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
         self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p])
+        self._fwd8 = nat.fn(L, "qd_conv_fwd_f8", [_p] * 4 + [_i] * 7 + [_p] * 5)
+        self._pack8 = nat.fn(L, "qd_conv_pack_f8", [_p] * 8 + [_i, _p])
 
     def pack_weights(self, st, cursor: Optional[torch.Tensor] = None, cursor_inc: int = 0) -> None:
         """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch.
@@ -170,6 +189,11 @@ class ConvStackHIP:
         hook = self.stage_hook
         if hook is not None:
             hook("packed")
+        f8 = self.f8s
+        if self.f8conv:   # e4m3 images of the current layer-2/3 weights (+ their amax for the next step)
+            nat.check(self._pack8(nat.ptr(m.conv_w[1]), nat.ptr(m.conv_w[2]), nat.ptr(self.wpk8[1]),
+                                  nat.ptr(self.wpk8[2]), nat.ptr(f8.qs[3:]), nat.ptr(f8.qs[5:]), nat.ptr(f8.amax[3]),
+                                  nat.ptr(f8.amax[5]), self.E, st), "conv_pack_f8")
         inp, st_prev = x1, None
         for k in range(3):
             # layers 2, 3 finalise the previous layer's BatchNorm themselves (BnFwd: statistics
@@ -180,9 +204,16 @@ class ConvStackHIP:
                 bnf = BnFwd(nat.ptr(self.stats[j]), nat.ptr(m.bn_w[j]), nat.ptr(m.bn_b[j]), nat.ptr(m.run_mean[j]),
                             nat.ptr(m.run_var[j]), nat.ptr(self.st[j]), self.chunks, float(self.B * self.HW),
                             m.momentum, m.eps, int(training))
-            nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
-                                nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw,
-                                ctypes.byref(bnf) if bnf is not None else None, st), f"conv_fwd{k + 1}")
+            if self.f8conv and k > 0:
+                j = 2 + 2 * (k - 1)
+                nat.check(self._fwd8(nat.ptr(inp), nat.ptr(self.wpk8[k]), nat.ptr(self.z[k]), nat.ptr(self.stats[k]),
+                                     self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw, ctypes.byref(bnf),
+                                     nat.ptr(f8.qs[j:]), nat.ptr(f8.scale[j:]), nat.ptr(f8.amax[j]), st),
+                          f"conv_fwd_f8_{k + 1}")
+            else:
+                nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
+                                    nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks,
+                                    self.spw, ctypes.byref(bnf) if bnf is not None else None, st), f"conv_fwd{k + 1}")
             inp, st_prev = self.z[k], self.st[k]
             if hook is not None:
                 hook(f"conv{k + 1}")

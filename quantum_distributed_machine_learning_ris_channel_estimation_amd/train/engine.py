@@ -64,14 +64,15 @@ class HDCEModel:
         self.E = n_experts
         self.H, self.W = pilot_grid(pilot_num)
         self.compute_dtype = _dtype(dtype) if self.device.type == "cuda" else torch.float32
-        # fp8 estimator: FC forward = e4m3 x e4m3 (hipBLASLt, fp32 accumulate) with delayed per-tensor
-        # scales; slot 0 = activations (quantised by the conv stack's last BN+ReLU kernel), slot 1 =
-        # FC weights (quantised by the optimizer's shadow write)
+        # fp8 estimator: FC forward = e4m3 x e4m3 (fp32 accumulate) with delayed per-tensor scales; slot
+        # 0 = FC activations (quantised by the conv stack's last BN+ReLU kernel), slot 1 = FC weights
+        # (quantised by the optimizer's shadow write), slots 2..5 = the e4m3 convs of layers 2 / 3
+        # (activation, weight) -- one scale-update launch per step (after the FC forward) for all six
         self.fp8 = dtype == "fp8" and self.device.type == "cuda"
         self.fp8_scales = None
         if self.fp8:
             from ..ops.optim import Fp8Scales
-            self.fp8_scales = Fp8Scales(2, self.device)
+            self.fp8_scales = Fp8Scales(6, self.device)
         self.convs = [Conv_P128(pilot_num).to(self.device) for _ in range(n_experts)]
         self.fc = FC_P128(pilot_num).to(self.device)
         named = []

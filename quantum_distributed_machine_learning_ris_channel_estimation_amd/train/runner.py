@@ -260,7 +260,9 @@ class Y2HRunner:
                         # the BN batch counters)
                         _capture_preserving(graphed, [sp.flat, opt.m, opt.v, opt.step_t] + model.run_mean
                                             + model.run_var + [model._nbt, loss_acc]
-                                            + ([model.fc_shadow] if model.fc_shadow is not None else []),
+                                            + ([model.fc_shadow] if model.fc_shadow is not None else [])
+                                            + ([model.fp8_scales.amax, model.fp8_scales.scale, model.fp8_scales.qs]
+                                               if model.fp8_scales is not None else []),
                                             static_idx, idx)
                     static_idx.copy_(idx)
                     graphed()

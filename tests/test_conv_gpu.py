@@ -116,6 +116,41 @@ def test_conv_bwd_fused_matches_side_by_side(cuda, pilot_num, B):
         assert rel(f[name], r[name]) < 1e-4, (name, rel(f[name], r[name]))
 
 
+def test_conv_f8_forward_matches_quantised_reference(cuda):
+    """fp8 estimator: layers 2 and 3 on e4m3 MFMA (conv3x3_f8_kernel) vs an fp32 torch conv of the
+    same e4m3-quantised operands (h = BN+ReLU(z_prev) with the kernel's records, scaled by the delayed
+    activation factor; W scaled by the weight factor) -- the kernel's tile swizzle, k order and
+    dequantisation -- and the whole fp8 feature stack vs the fp32 model within e4m3 error."""
+    U, B = 3, 64
+    a, b = pair(cuda)
+    a8 = HDCEModel(128, cuda, "fp8")
+    a8.space.flat.copy_(a.space.flat)
+    Yp = torch.randn(3, U, B, 2, a8.H, a8.W, device=cuda)
+    conv = ConvStackHIP(a8, U, B)
+    assert conv.f8conv
+    x = a8.pack_input(Yp).contiguous()
+    conv.forward(x, training=True)          # (settles the delayed scales: the step's update launch)
+    a8.fp8_scales.update()
+    qs, sc = conv.f8s.qs.clone(), conv.f8s.scale.clone()
+    h3 = conv.forward(x, training=True)
+    torch.cuda.synchronize()
+    E, H, W = a8.E, a8.H, a8.W
+    for k in (1, 2):
+        j = 2 + 2 * (k - 1)
+        st = conv.st[k - 1]                                        # (U, EC, NST) records of layer k
+        zp = conv.z[k - 1].float().view(U, B, E * 32, H * W)
+        h = torch.relu(st[:, None, :, 2:3] * zp + st[:, None, :, 3:4]).view(U * B, E * 32, H, W)
+        hq = (h * qs[j]).clamp(-448, 448).to(torch.float8_e4m3fn).float() * sc[j]
+        wq = (a8.conv_w[k] * qs[j + 1]).clamp(-448, 448).to(torch.float8_e4m3fn).float() * sc[j + 1]
+        ref = F.conv2d(hq, wq, padding=1, groups=E)
+        err = rel(conv.z[k], ref.view_as(conv.z[k]))
+        print(f"layer {k + 1}: fp8 kernel vs quantised fp32 conv: rel {err:.2e}")
+        assert err < 1e-2, (k, err)
+    full = rel(h3, b.features(Yp, training=True))
+    print(f"fp8 feature stack vs fp32 model: rel {full:.3e}")
+    assert full < 8e-2, full
+
+
 # Whole-step conv weight-gradient error vs the fp32 autograd step, measured on MI355X (seed 0):
 # relative Frobenius 0.088 / 0.065 / 0.034 and cosine 0.99614 / 0.99787 / 0.99942 for conv1..3.
 # fro^2 ~= 2(1 - cos) there, i.e. the difference is noise, not a scale or direction error; it grows
