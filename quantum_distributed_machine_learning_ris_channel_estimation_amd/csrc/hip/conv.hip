@@ -542,7 +542,10 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
 // conv3x3_body's structure with an e4m3 channel-last tile -- 32-byte pixels, 8-byte chunks at
 // q ^ tile8_swz(R, C): conflict-free ds_read_b64 fragment reads (lane halves of 32) for every tap
 // of both geometries -- e4m3 B fragments (qd_conv_pack_f8) and mfma_f32_32x32x16_fp8_fp8 (lane l:
-// A[row l&31][k = 8(l>>5) + j], the bf16 form's map; K order (tap, channel) as the bf16 pack).
+// A[row l&31][k = 8(l>>5) + j], the bf16 form's map; K order (tap, channel) as the bf16 pack), built in
+// the prologue straight from the fp32 weights with the delayed weight factor (no pack launch: the
+// separate pack sat on the critical path at 16 us); the bx == 0 block of each expert records the
+// expert's max |W| (amax_w[e]) for the next step's factor.
 // Input transform h = BN+ReLU(z_prev) -> e4m3(h * qs_a) with the delayed activation scale; the
 // epilogue scales the accumulators by deq = scale_a * scale_w, then writes bf16 z + statistics
 // exactly as the bf16 body (the BN backward still sees bf16 z).  amax_a[block] = max h of the
@@ -557,10 +560,11 @@ constexpr int KS8 = 18;   // 16-deep k-steps of a 32-channel layer
 
 template <int W>
 __global__ void __launch_bounds__(256, 2) conv3x3_f8_kernel(const uint16_t* __restrict__ xin,
-                                                         const uint8_t* __restrict__ wt8, uint16_t* __restrict__ out,
+                                                         const float* __restrict__ w32, uint16_t* __restrict__ out,
                                                          float* __restrict__ stats, int E, int B, int chunks, int spw,
                                                          BnFwd bnf, const float* __restrict__ qs,
-                                                         const float* __restrict__ scale, float* __restrict__ amax_a) {
+                                                         const float* __restrict__ scale, float* __restrict__ amax_a,
+                                                         float* __restrict__ amax_w) {
   using G = Geo<16, W>;
   constexpr int CIN = 32, PIX = 32;
   constexpr int TILE = G::HP * G::WP * PIX;     // bytes per wave tile
@@ -631,17 +635,33 @@ __global__ void __launch_bounds__(256, 2) conv3x3_f8_kernel(const uint16_t* __re
     }
   };
   if (PREF && n0 < nend) load(n0);
+  float wmx = 0.f;
   {
-    const uint2* wp = reinterpret_cast<const uint2*>(wt8) + (size_t)e * KS8 * 64;
-    uint2 tw[(KS8 * 64 + 255) / 256];
+    constexpr int NF = KS8 * 64, FPT = (NF + 255) / 256;   // fragments (s, lane) per thread
+    const float qw = qs[1];
+    float tv[FPT][8];
 #pragma unroll
-    for (int k = 0; k < (KS8 * 64 + 255) / 256; ++k)
-      if (tid + 256 * k < KS8 * 64) tw[k] = wp[tid + 256 * k];
+    for (int t = 0; t < FPT; ++t) {
+      const int f = tid + 256 * t, s8 = f >> 6, h = (f >> 5) & 1, col = f & 31;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * s8 + 8 * h + j;   // (tap k / 32, input channel k % 32)
+        tv[t][j] = f < NF ? w32[((size_t)(e * CO + col) * CO + k % CO) * 9 + k / CO] : 0.f;
+      }
+    }
     float tp = 0.f;
     if (!bnf.stats) tp = bnf.st_out[((size_t)u * EC_in + e * CIN) * NST + tid];   // (records given as is)
 #pragma unroll
-    for (int k = 0; k < (KS8 * 64 + 255) / 256; ++k)
-      if (tid + 256 * k < KS8 * 64) wl[tid + 256 * k] = tw[k];
+    for (int t = 0; t < FPT; ++t) {
+      const int f = tid + 256 * t;
+      if (f < NF) {
+        const float* v = tv[t];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wmx = fmaxf(wmx, fabsf(v[j]));
+        wl[f] = make_uint2(e4m3_pack4(v[0] * qw, v[1] * qw, v[2] * qw, v[3] * qw),
+                           e4m3_pack4(v[4] * qw, v[5] * qw, v[6] * qw, v[7] * qw));
+      }
+    }
     if (bnf.stats) bn_fwd_build(bnf, stl, u, e, EC_in, chunk == 0);
     else stl[tid] = tp;
   }
@@ -714,48 +734,25 @@ __global__ void __launch_bounds__(256, 2) conv3x3_f8_kernel(const uint16_t* __re
     for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
     stats[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;
   }
-  // the block's max h (h >= 0) -> its amax partial (index: the flat block id; < kAmaxParts)
-  float m = mx;
+  // the block's max h (h >= 0) -> its amax partial (index: the flat block id; < kAmaxParts); the
+  // expert's max |W| from its bx == 0 block
+  float m = mx, mw = wmx;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  for (int o = 32; o > 0; o >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, o));
+    mw = fmaxf(mw, __shfl_xor(mw, o));
+  }
   __syncthreads();
-  if (lane == 0) red[wv] = m;
+  if (lane == 0) {
+    red[wv] = m;
+    red[4 + wv] = mw;
+  }
   __syncthreads();
   if (tid == 0) {
     const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     float* ap = amax_a + (size_t)blockIdx.y * gridDim.x + blockIdx.x;
     *ap = fmaxf(*ap, bm);
-  }
-}
-
-// fp8 weight images of layers 2, 3 (blockIdx.z = job): e4m3(W * qs_w) B fragments [e][s][lane][8] in
-// conv3x3_f8_kernel's k order, and the block's max |W| into the weight amax partials.
-struct PackF8Jobs {
-  const float* w[2];
-  uint8_t* out[2];
-  const float* qs[2];     // weight quantisation factors
-  float* amax[2];         // weight amax partials
-};
-__global__ void __launch_bounds__(64) pack_weights_f8_kernel(PackF8Jobs jobs) {
-  const int s = blockIdx.x, e = blockIdx.y, jb = blockIdx.z, lane = threadIdx.x;
-  const int hh = lane >> 5, col = lane & 31;
-  const float* w = jobs.w[jb];
-  const float q = jobs.qs[jb][0];
-  float v[8], mx = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 16 * s + 8 * hh + j;   // (tap k / 32, input channel k % 32)
-    v[j] = w[((size_t)(e * CO + col) * CO + k % CO) * 9 + k / CO];
-    mx = fmaxf(mx, fabsf(v[j]));
-  }
-  const uint32_t lo = e4m3_pack4(v[0] * q, v[1] * q, v[2] * q, v[3] * q);
-  const uint32_t hi = e4m3_pack4(v[4] * q, v[5] * q, v[6] * q, v[7] * q);
-  reinterpret_cast<uint2*>(jobs.out[jb])[((size_t)e * KS8 + s) * 64 + lane] = make_uint2(lo, hi);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if (lane == 0) {
-    float* ap = jobs.amax[jb] + (size_t)e * gridDim.x + s;
-    *ap = fmaxf(*ap, mx);
+    if (bx == 0) amax_w[e] = fmaxf(amax_w[e], fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7])));
   }
 }
 
@@ -1782,31 +1779,21 @@ QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const u
   return (int)hipGetLastError();
 }
 
-// fp8 forward of a 32->32 layer (see conv3x3_f8_kernel).  w8: qd_conv_pack_f8's image; qs / scale: the
-// layer's (activation, weight) pair of quantisation / dequantisation factors; amax_a: the activation
-// amax partials (indexed by the flat block id).
-QD_API int qd_conv_fwd_f8(const uint16_t* xin, const uint8_t* w8, uint16_t* z, float* stats, int N, int E, int B, int H,
+// fp8 forward of a 32->32 layer (see conv3x3_f8_kernel).  w: the layer's fp32 weights (E*32, 32, 3, 3);
+// qs / scale: its (activation, weight) pair of quantisation / dequantisation factors; amax_a / amax_w:
+// the activation amax partials (indexed by the flat block id) / the weight's (indexed by expert).
+QD_API int qd_conv_fwd_f8(const uint16_t* xin, const float* w, uint16_t* z, float* stats, int N, int E, int B, int H,
                           int W, int chunks, int spw, const BnFwd* bnf, const float* qs, const float* scale,
-                          float* amax_a, void* stream) {
+                          float* amax_a, float* amax_w, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (!bnf || chunks * 4 * spw < B || (N / B) * chunks * E > qd::kAmaxParts) return (int)hipErrorInvalidValue;
   const BnFwd bf = *bnf;
   dim3 grid((N / B) * chunks, E);
   QD_GEOM(WW, {
     const size_t sm = 4 * (size_t)(16 + 2) * (WW + 2) * 32 + (size_t)KS8 * 64 * 8 + 32 * NST * sizeof(float);
-    hipLaunchKernelGGL((conv3x3_f8_kernel<WW>), grid, dim3(256), sm, s, xin, w8, z, stats, E, B, chunks, spw, bf, qs,
-                       scale, amax_a);
+    hipLaunchKernelGGL((conv3x3_f8_kernel<WW>), grid, dim3(256), sm, s, xin, w, z, stats, E, B, chunks, spw, bf, qs,
+                       scale, amax_a, amax_w);
   })
-  return (int)hipGetLastError();
-}
-
-// e4m3 weight images of layers 2 and 3 in one launch: w[j] fp32 (E, 32, 32, 3, 3) -> out[j]
-// (E, 18, 64, 8) bytes with qs[j][0]; amax[j]: that weight's amax partials (E * 18 used).
-QD_API int qd_conv_pack_f8(const float* w2, const float* w3, uint8_t* o2, uint8_t* o3, const float* qs2,
-                           const float* qs3, float* amax2, float* amax3, int E, void* stream) {
-  if (E * KS8 > qd::kAmaxParts) return (int)hipErrorInvalidValue;
-  PackF8Jobs j{{w2, w3}, {o2, o3}, {qs2, qs3}, {amax2, amax3}};
-  hipLaunchKernelGGL(pack_weights_f8_kernel, dim3(KS8, E, 2), dim3(64), 0, (hipStream_t)stream, j);
   return (int)hipGetLastError();
 }
 

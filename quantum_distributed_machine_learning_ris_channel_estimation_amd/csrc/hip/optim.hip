@@ -230,9 +230,21 @@ __global__ void __launch_bounds__(256) fp8_scale_update_kernel(float* amax_parts
   const int i = blockIdx.x;
   float* part = amax_parts + (size_t)i * nparts;
   float m = 0.f;
-  for (int k = threadIdx.x; k < nparts; k += 256) {
-    m = fmaxf(m, part[k]);
-    part[k] = 0.f;
+  if (nparts == 4096) {   // every load in flight before the re-arming stores (a load / store pair per
+    float4* p4 = reinterpret_cast<float4*>(part);   // iteration serialised 16 round trips)
+    float4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = p4[threadIdx.x + 256 * q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      m = fmaxf(m, fmaxf(fmaxf(v[q].x, v[q].y), fmaxf(v[q].z, v[q].w)));
+      p4[threadIdx.x + 256 * q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  } else {
+    for (int k = threadIdx.x; k < nparts; k += 256) {
+      m = fmaxf(m, part[k]);
+      part[k] = 0.f;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));

@@ -87,8 +87,6 @@ class ConvStackHIP:
         f8m = getattr(model, "fp8_scales", None)
         self.f8conv = (self.fp8 and dev.type == "cuda" and f8m is not None and f8m.n >= 6
                        and os.environ.get("QDML_FP8_CONV", "1") != "0")
-        self.wpk8 = [None] + [torch.empty(self.E, 18, 64, 8, device=dev, dtype=torch.uint8) for _ in range(2)] \
-            if self.f8conv else None
         self.f8s, self.f8o = (f8m, 2) if self.f8conv else (None, 0)
         if self.f8conv:
             from .optim import FP8_E4M3_MAX
@@ -145,8 +143,7 @@ class ConvStackHIP:
         # (bwd_fused off) wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate)
         self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
         self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p])
-        self._fwd8 = nat.fn(L, "qd_conv_fwd_f8", [_p] * 4 + [_i] * 7 + [_p] * 5)
-        self._pack8 = nat.fn(L, "qd_conv_pack_f8", [_p] * 8 + [_i, _p])
+        self._fwd8 = nat.fn(L, "qd_conv_fwd_f8", [_p] * 4 + [_i] * 7 + [_p] * 6)
 
     def pack_weights(self, st, cursor: Optional[torch.Tensor] = None, cursor_inc: int = 0) -> None:
         """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch.
@@ -190,10 +187,6 @@ class ConvStackHIP:
         if hook is not None:
             hook("packed")
         f8 = self.f8s
-        if self.f8conv:   # e4m3 images of the current layer-2/3 weights (+ their amax for the next step)
-            nat.check(self._pack8(nat.ptr(m.conv_w[1]), nat.ptr(m.conv_w[2]), nat.ptr(self.wpk8[1]),
-                                  nat.ptr(self.wpk8[2]), nat.ptr(f8.qs[3:]), nat.ptr(f8.qs[5:]), nat.ptr(f8.amax[3]),
-                                  nat.ptr(f8.amax[5]), self.E, st), "conv_pack_f8")
         inp, st_prev = x1, None
         for k in range(3):
             # layers 2, 3 finalise the previous layer's BatchNorm themselves (BnFwd: statistics
@@ -206,10 +199,10 @@ class ConvStackHIP:
                             m.momentum, m.eps, int(training))
             if self.f8conv and k > 0:
                 j = 2 + 2 * (k - 1)
-                nat.check(self._fwd8(nat.ptr(inp), nat.ptr(self.wpk8[k]), nat.ptr(self.z[k]), nat.ptr(self.stats[k]),
+                nat.check(self._fwd8(nat.ptr(inp), nat.ptr(m.conv_w[k]), nat.ptr(self.z[k]), nat.ptr(self.stats[k]),
                                      self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw, ctypes.byref(bnf),
-                                     nat.ptr(f8.qs[j:]), nat.ptr(f8.scale[j:]), nat.ptr(f8.amax[j]), st),
-                          f"conv_fwd_f8_{k + 1}")
+                                     nat.ptr(f8.qs[j:]), nat.ptr(f8.scale[j:]), nat.ptr(f8.amax[j]),
+                                     nat.ptr(f8.amax[j + 1]), st), f"conv_fwd_f8_{k + 1}")
             else:
                 nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
                                     nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks,
