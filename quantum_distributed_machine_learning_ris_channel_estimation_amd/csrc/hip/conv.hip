@@ -1043,7 +1043,7 @@ struct BwdGeo {
   static constexpr int X_EL = 3 * CO * XCS, DZ_EL = CO * DZS, T_EL = G::HP * G::WP * CO, ZP_EL = CO * ZPS;
   static constexpr int KSD = 18;               // dgrad k-steps (9 taps x 32 channels / 16)
   static constexpr size_t STAGE = (size_t)(X_EL + DZ_EL + T_EL + ZP_EL) * 2 + KSD * 64 * 16 + 2 * CO * NST * 4;
-  static constexpr size_t RED = (CO * (size_t)(9 * CO + 1) + 4 * CO * CO) * 4;   // dW rows | tap-8 partials
+  static constexpr size_t RED = (CO * (size_t)(9 * CO + 1) + 4 * CO * (CO + 1)) * 4;   // dW rows | tap-8 partials
   static constexpr size_t SMEM = STAGE > RED ? STAGE : RED;
 };
 
@@ -1283,13 +1283,13 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
   constexpr int RS = 9 * CO + 1;
   __syncthreads();
   float* wr = reinterpret_cast<float*>(smem);
-  float* p8 = wr + CO * RS;   // [wave][co][ci]
+  float* p8 = wr + CO * RS;   // [wave][co][ci], rows padded to 33: the 32 lanes (co) on distinct banks
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int ci = (r & 3) + 8 * (r >> 2) + 4 * hh;   // accumulator row = ci, column = co = l32
     wr[l32 * RS + ci * 9 + wv] = accw[0][r];
     wr[l32 * RS + ci * 9 + wv + 4] = accw[1][r];
-    p8[(wv * CO + l32) * CO + ci] = accw[2][r];
+    p8[(wv * CO + l32) * (CO + 1) + ci] = accw[2][r];
   }
   __syncthreads();
   float* srow = slab + ((size_t)e * gridDim.x + bx) * CO * CO * 9;
@@ -1298,7 +1298,8 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
     float v;
     if (m % 9 == 8) {
       const int ci = m / 9;
-      v = ((p8[co * CO + ci] + p8[(CO + co) * CO + ci]) + p8[(2 * CO + co) * CO + ci]) + p8[(3 * CO + co) * CO + ci];
+      constexpr int P8 = CO + 1;
+      v = ((p8[co * P8 + ci] + p8[(CO + co) * P8 + ci]) + p8[(2 * CO + co) * P8 + ci]) + p8[(3 * CO + co) * P8 + ci];
     } else {
       v = wr[co * RS + m];
     }
