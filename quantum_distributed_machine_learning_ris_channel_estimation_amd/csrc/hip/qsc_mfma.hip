@@ -714,6 +714,418 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// qsc2_bwd3_kernel (P128): the backward with every matrix product on bf16 MFMAs at fp32-grade
+// accuracy ("bf16x3": each fp32 operand v = hi + lo, hi = bf16(v), lo = bf16(v - hi), and
+// a.b ~= ah.bh + ah.bl + al.bh with fp32 accumulation; relative error ~1e-5).  The f32-input MFMA
+// it replaces runs at 1/16 of the bf16 rate (64 cycles per 32x32x2): three bf16 products per fp32
+// product are still 5x fewer MFMA cycles, and the operands come as whole 8/16-byte fragments
+// instead of one float per lane per instruction.  Same phases, outputs and slab row as
+// qsc2_bwd_kernel (the f32 kernel stays the P256 path and the reference of the GPU test).
+// Per-wave LDS images, bf16 [part = hi | lo]:
+//   XS  [2][kw][ci 2][18][8]    input x, three column-shifted copies      (conv1 wgrad B)
+//   P1S [2][kw][ci 16][10][4]   pool-1 map, three column-shifted copies   (conv2 wgrad B, pool-1 mask)
+//   DZT [2][co 32][40]          dz2 co-major                              (conv2 wgrad A)   } aliased
+//   DZC [2][60][32]             dz2 channel-last, padded 10 x 6           (conv2 dgrad A)   } by DZ1
+//   DZ1 [2][ci 16][136]         dz1 co-major                              (conv1 wgrad A)
+//   DP1 [16][32] fp32           conv2 data gradient
+// block-shared: the linear layer (fp32, as qsc2_bwd_kernel) and W2T [2][tap][ci][co 32] (dgrad B).
+// ----------------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+
+struct B3 {   // P128 geometry of the bf16 images (elements)
+  static constexpr int XS_PART = 3 * 2 * 18 * 8, XS = 2 * XS_PART;
+  static constexpr int P1S_PART = 3 * 16 * 10 * 4, P1S = 2 * P1S_PART;
+  static constexpr int DZT_RS = 40, DZT_PART = 32 * DZT_RS, DZT = 2 * DZT_PART;
+  static constexpr int DZC_PART = 60 * 32, DZC = 2 * DZC_PART;
+  static constexpr int DZ1_RS = 136, DZ1_PART = 16 * DZ1_RS, DZ1 = 2 * DZ1_PART;
+  static_assert(DZ1 <= DZT + DZC, "dz1 alias");
+  static constexpr int BF = XS + P1S + DZT + DZC;                   // bf16 elements per wave
+  static constexpr int WAVE_BYTES = BF * 2 + 16 * 32 * 4 + 32 * 4;  // + DP1 + misc
+  static constexpr int W2T_PART = 9 * 16 * 32, W2T = 2 * W2T_PART;
+};
+static_assert(B3::WAVE_BYTES % 16 == 0, "16-byte wave images");
+
+__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)v;
+  lo = (__bf16)(v - (float)hi);
+}
+
+template <int NWV>
+__global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __restrict__ x, const float* __restrict__ flat,
+                                                         Offs o, const float* __restrict__ angles,
+                                                         const float* __restrict__ dang, float* __restrict__ dpre_out,
+                                                         float* __restrict__ slab, const float* __restrict__ p2, Saved sv,
+                                                         int B, int n, int wlk, QSlab qs) {
+  using G = Geo<16, 8>;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // ---- block-shared: linear layer (fp32) | W2T hi / lo ----
+  float* wl = sm;
+  const int wl_floats = (n * wl_stride(G::F) + 16 + 3) & ~3;
+  __bf16* w2t = reinterpret_cast<__bf16*>(sm + wl_floats);
+  char* wbase = reinterpret_cast<char*>(w2t + B3::W2T) + wv * B3::WAVE_BYTES;
+  __bf16* XS = reinterpret_cast<__bf16*>(wbase);
+  __bf16* P1S = XS + B3::XS;
+  __bf16* DZT = P1S + B3::P1S;
+  __bf16* DZC = DZT + B3::DZT;
+  __bf16* DZ1 = DZT;   // (alias: dz2 images are dead once the conv2 data gradient is done)
+  float* DP1 = reinterpret_cast<float*>(DZC + B3::DZC);
+  float* misc = DP1 + 16 * 32;
+  {
+    const int q4 = G::F / 4;
+    const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
+    for (int i = threadIdx.x; i < n * q4; i += blockDim.x) {
+      const int j = i / q4, c = i % q4;
+      *reinterpret_cast<float4*>(wl + j * wl_stride(G::F) + 4 * c) = src[i];
+    }
+    for (int i = threadIdx.x; i < C2 * K2; i += blockDim.x) {   // W2 [co][ci][tap] -> W2T [tap][ci][co]
+      const int co = i / K2, ci = (i % K2) / 9, t = i % 9;
+      __bf16 h, l;
+      split_bf16(flat[o.w2 + i], h, l);
+      w2t[(t * C1 + ci) * 32 + co] = h;
+      w2t[B3::W2T_PART + (t * C1 + ci) * 32 + co] = l;
+    }
+  }
+  for (int i = lane; i < B3::WAVE_BYTES / 16; i += 64) reinterpret_cast<uint4*>(wbase)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const int col32 = lane & 31, kh = lane >> 5;
+  const int col16 = lane & 15, kq = lane >> 4;
+  f32x16 gw2[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) gw2[t] = (f32x16){};
+  f32x4 gw1[2];
+  gw1[0] = (f32x4){};
+  gw1[1] = (f32x4){};
+  constexpr int FPL = G::F / 64;   // 4 pool-2 features per lane: channel lane / 2, cells 4 (lane & 1) + i
+  float gb2 = 0.f, gbl = 0.f, gb1[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NWL = 64 / FPL;
+  const bool wl_here = wlk != 0;
+  float gwl[NWL][FPL];
+#pragma unroll
+  for (int j = 0; j < NWL; ++j)
+#pragma unroll
+    for (int i = 0; i < FPL; ++i) gwl[j][i] = 0.f;
+
+  // ---- one-sample-ahead register prefetch ----
+  f32x4 rx[2];           // lanes 0..31: x row (c = lane / 16, image row lane % 16)
+  float rp1[2][4];       // (ci, pool-1 row) pairs lane, lane + 64: 4 columns
+  f32x4 rp2;
+  uint32_t rc2 = 0, rc1 = 0;
+  float rth = 0.f, rda = 0.f;
+  auto prefetch = [&](int s) {
+    if (lane < 32) {
+      const f32x4* x4 = reinterpret_cast<const f32x4*>(x + (size_t)s * 2 * G::HW + lane * 8);
+      rx[0] = x4[0];
+      rx[1] = x4[1];
+    }
+    const float* p1 = sv.p1 + (size_t)s * C1 * G::HW2;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int pr = lane + 64 * r, ci = pr >> 3, qy = pr & 7;
+#pragma unroll
+      for (int qx = 0; qx < 4; ++qx) rp1[r][qx] = p1[(qy * 4 + qx) * C1 + ci];
+    }
+    rp2 = *reinterpret_cast<const f32x4*>(p2 + (size_t)s * G::F + FPL * lane);
+    rc2 = *reinterpret_cast<const uint32_t*>(sv.c2 + (size_t)s * G::F + FPL * lane);
+    rc1 = sv.c1[(size_t)s * G::HW2 + (lane & 31)];
+    if (lane < n) {
+      rth = angles[(size_t)s * n + lane];
+      rda = dang[(size_t)s * n + lane];
+    }
+  };
+  const int s0 = blockIdx.x * NWV + wv;
+  if (s0 < B) prefetch(s0);
+
+  for (int s = s0; s < B; s += gridDim.x * NWV) {
+    // ---- saved state -> shifted bf16 copies ----
+    if (lane < 32) {
+      const int c = lane >> 4, ph = lane & 15;
+      float v[10];
+      v[0] = 0.f;
+      v[9] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[1 + q] = rx[0][q];
+        v[5 + q] = rx[1][q];
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        bf16x8_t h, l;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 a, b;
+          split_bf16(v[j + kw], a, b);
+          h[j] = a;
+          l[j] = b;
+        }
+        const int off = ((kw * 2 + c) * 18 + ph + 1) * 8;
+        *reinterpret_cast<bf16x8_t*>(XS + off) = h;
+        *reinterpret_cast<bf16x8_t*>(XS + B3::XS_PART + off) = l;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int pr = lane + 64 * r, ci = pr >> 3, qy = pr & 7;
+      float v[6] = {0.f, rp1[r][0], rp1[r][1], rp1[r][2], rp1[r][3], 0.f};
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        bf16x4_t h, l;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          __bf16 a, b;
+          split_bf16(v[j + kw], a, b);
+          h[j] = a;
+          l[j] = b;
+        }
+        const int off = ((kw * 16 + ci) * 10 + qy + 1) * 4;
+        *reinterpret_cast<bf16x4_t*>(P1S + off) = h;
+        *reinterpret_cast<bf16x4_t*>(P1S + B3::P1S_PART + off) = l;
+      }
+    }
+    if (lane < n) {
+      const float d = rda * (1.f - rth * rth);
+      misc[lane] = d;
+      dpre_out[(size_t)s * n + lane] = d;
+      gbl += d;
+    }
+    const f32x4 p2v = rp2;
+    const uint32_t c2v = rc2, c1v = rc1;
+    if (s + gridDim.x * NWV < B) prefetch(s + gridDim.x * NWV);
+    // dz2's channel-last image is rewritten sparsely: clear it (dz1 of the previous sample aliased it)
+    for (int i = lane; i < B3::DZC * 2 / 16; i += 64) reinterpret_cast<uint4*>(DZC)[i] = make_uint4(0, 0, 0, 0);
+    wave_lds_fence();
+    // ---- linear backward -> dp2; pool-2 backward through the saved choice (+ReLU) -> dz2 ----
+    {
+      float dp[FPL];
+#pragma unroll
+      for (int i = 0; i < FPL; ++i) dp[i] = 0.f;
+      for (int j = 0; j < n; ++j) {
+        const float mj = misc[j];
+        const float4 w4 = *reinterpret_cast<const float4*>(wl + j * wl_stride(G::F) + FPL * lane);
+        dp[0] += w4.x * mj;
+        dp[1] += w4.y * mj;
+        dp[2] += w4.z * mj;
+        dp[3] += w4.w * mj;
+      }
+      if (wl_here) {
+#pragma unroll
+        for (int j = 0; j < NWL; ++j) {
+          const float mj = j < n ? misc[j] : 0.f;
+#pragma unroll
+          for (int i = 0; i < FPL; ++i) gwl[j][i] += mj * p2v[i];
+        }
+      }
+      // lane: channel c = lane / 2, pool-1 rows 4 (lane & 1) .. +3 (16 positions, co-major contiguous)
+      const int c = lane >> 1, hb = lane & 1;
+      float v16[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v16[k] = 0.f;
+#pragma unroll
+      for (int i = 0; i < FPL; ++i) {
+        const int rel = (c2v >> (8 * i)) & 0xff;
+        const float g = p2v[i] > 0.f ? dp[i] : 0.f;
+        gb2 += g;
+        const int lr = 2 * (i >> 1) + (rel >> 1), px = 2 * (i & 1) + (rel & 1);   // local pool-1 row, column
+        v16[lr * 4 + px] = g;
+        __bf16 h, l;
+        split_bf16(g, h, l);
+        const int py = 4 * hb + lr;
+        DZC[((py + 1) * 6 + px + 1) * 32 + c] = h;
+        DZC[B3::DZC_PART + ((py + 1) * 6 + px + 1) * 32 + c] = l;
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        bf16x8_t h, l;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 a, b;
+          split_bf16(v16[8 * hh + j], a, b);
+          h[j] = a;
+          l[j] = b;
+        }
+        const int off = c * B3::DZT_RS + 16 * hb + 8 * hh;
+        *reinterpret_cast<bf16x8_t*>(DZT + off) = h;
+        *reinterpret_cast<bf16x8_t*>(DZT + B3::DZT_PART + off) = l;
+      }
+    }
+    wave_lds_fence();
+    // ---- conv2 weight grads: dW2[co][k] += sum_pos dz2[co][pos] * im2col(p1)[pos][k], K = positions;
+    // A = DZT rows (co), B = P1S (k = tap * 16 + ci): two 8-byte rows of 4 positions per fragment ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p0 = 16 * ks + 8 * kh;   // 8 positions = pool-1 rows p0 / 4, p0 / 4 + 1
+      const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(DZT + col32 * B3::DZT_RS + p0);
+      const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(DZT + B3::DZT_PART + col32 * B3::DZT_RS + p0);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const int k = 32 * t + col32;
+        bf16x8_t bh = {}, bl = {};
+        if (k < K2) {
+          const int tp = k >> 4, ci = k & 15, ky = tp / 3, kx = tp % 3;
+          const int off = ((kx * 16 + ci) * 10 + p0 / 4 + ky) * 4;
+          const bf16x4_t h0 = *reinterpret_cast<const bf16x4_t*>(P1S + off);
+          const bf16x4_t h1 = *reinterpret_cast<const bf16x4_t*>(P1S + off + 4);
+          const bf16x4_t l0 = *reinterpret_cast<const bf16x4_t*>(P1S + B3::P1S_PART + off);
+          const bf16x4_t l1 = *reinterpret_cast<const bf16x4_t*>(P1S + B3::P1S_PART + off + 4);
+          bh = (bf16x8_t){h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+          bl = (bf16x8_t){l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+        }
+        gw2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, gw2[t], 0, 0, 0);
+        gw2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, gw2[t], 0, 0, 0);
+        gw2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, gw2[t], 0, 0, 0);
+      }
+    }
+    // ---- conv2 data grads: dp1[ci][pos] = sum_{tap, co} dz2_pad[pos + 2 - tap][co] W2[co][ci][tap];
+    // 16x16x32: rows = 16 positions, cols = ci, K = one tap's 32 co ----
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int pos = 16 * mt + col16, py = pos >> 2, px = pos & 3;
+      f32x4 acc = {};
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ao = ((py + 2 - t / 3) * 6 + px + 2 - t % 3) * 32 + 8 * kq;
+        const int bo = (t * C1 + col16) * 32 + 8 * kq;
+        const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(DZC + ao);
+        const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(DZC + B3::DZC_PART + ao);
+        const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(w2t + bo);
+        const bf16x8_t bl = *reinterpret_cast<const bf16x8_t*>(w2t + B3::W2T_PART + bo);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) DP1[col16 * 32 + 16 * mt + 4 * kq + r] = acc[r];
+    }
+    wave_lds_fence();
+    // ---- pool-1 backward (+ReLU: passes iff p1 > 0): lane = (channel, image row) pairs, 8 positions
+    // per pair written whole -> DZ1 (co-major); window codes from the lanes holding them ----
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int pr = lane + 64 * r, co = pr >> 4, row = pr & 15, qy = row >> 1, dy = row & 1;
+      float v[8];
+#pragma unroll
+      for (int qx = 0; qx < 4; ++qx) {
+        const int win = qy * 4 + qx;
+        const float pv = (float)P1S[((16 + co) * 10 + qy + 1) * 4 + qx];   // kw = 1 copy, hi part
+        const float g = pv > 0.f ? DP1[co * 32 + win] : 0.f;
+        if (dy == 0) gb1[r] += g;
+        const uint32_t code = (__shfl(c1v, win) >> (2 * co)) & 3u;
+        v[2 * qx] = ((code >> 1) == (uint32_t)dy && (code & 1u) == 0u) ? g : 0.f;
+        v[2 * qx + 1] = ((code >> 1) == (uint32_t)dy && (code & 1u) == 1u) ? g : 0.f;
+      }
+      bf16x8_t h, l;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 a, b;
+        split_bf16(v[j], a, b);
+        h[j] = a;
+        l[j] = b;
+      }
+      *reinterpret_cast<bf16x8_t*>(DZ1 + co * B3::DZ1_RS + row * 8) = h;
+      *reinterpret_cast<bf16x8_t*>(DZ1 + B3::DZ1_PART + co * B3::DZ1_RS + row * 8) = l;
+    }
+    wave_lds_fence();
+    // ---- conv1 weight grads: dW1[co][k] += sum_pos dz1[co][pos] * im2col(x)[pos][k], k = ci * 9 + tap;
+    // 16x16x32: K = 32 positions = 4 image rows, a lane's 8 = one row ----
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int row = 4 * ks + kq;
+      const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(DZ1 + col16 * B3::DZ1_RS + row * 8);
+      const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(DZ1 + B3::DZ1_PART + col16 * B3::DZ1_RS + row * 8);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int k = 16 * t + col16;
+        bf16x8_t bh = {}, bl = {};
+        if (k < K1) {
+          const int ci = k / 9, tp = k % 9;
+          const int off = (((tp % 3) * 2 + ci) * 18 + row + tp / 3) * 8;
+          bh = *reinterpret_cast<const bf16x8_t*>(XS + off);
+          bl = *reinterpret_cast<const bf16x8_t*>(XS + B3::XS_PART + off);
+        }
+        gw1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, gw1[t], 0, 0, 0);
+        gw1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, gw1[t], 0, 0, 0);
+        gw1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, gw1[t], 0, 0, 0);
+      }
+    }
+    wave_lds_fence();
+  }
+
+  // ---- deterministic workgroup reduction -> slab row (w1 | b1 | w2 | b2 | wl | bl), as qsc2_bwd_kernel ----
+  __syncthreads();
+  float* red = sm;
+  constexpr int RW0 = C2 * K2 + C1 * K1 + C1 + C2 + 16;
+  const int RW = RW0 + (wl_here ? n * G::F : 0);
+  float* mine = red + wv * RW;
+  if (wl_here) {
+#pragma unroll
+    for (int j = 0; j < NWL; ++j)
+      if (j < n)
+        *reinterpret_cast<float4*>(mine + RW0 + j * G::F + FPL * lane) =
+            make_float4(gwl[j][0], gwl[j][1], gwl[j][2], gwl[j][3]);
+  }
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * kh, k = 32 * t + col32;
+      if (k < K2) mine[co * K2 + (k & 15) * 9 + (k >> 4)] = gw2[t][r];   // (tap, ci) -> flat [ci][tap]
+    }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 4 * kq + r, k = 16 * t + col16;
+      if (k < K1) mine[C2 * K2 + co * K1 + k] = gw1[t][r];
+    }
+  // b1: lanes 16k .. 16k+15 hold channel k + 4r's windows
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = gb1[r];
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off);
+    if (col16 == 0) mine[C2 * K2 + C1 * K1 + (lane >> 4) + 4 * r] = v;
+  }
+  {
+    const float v = gb2 + __shfl_xor(gb2, 1);   // channel lane / 2 over both row halves
+    if ((lane & 1) == 0) mine[C2 * K2 + C1 * K1 + C1 + (lane >> 1)] = v;
+  }
+  if (lane < 16) mine[C2 * K2 + C1 * K1 + C1 + C2 + lane] = lane < n ? gbl : 0.f;
+  __syncthreads();
+  float* row = slab + (size_t)blockIdx.x * o.row;
+  const int q0 = (int)((long long)qs.rows * blockIdx.x / gridDim.x);
+  const int q1 = (int)((long long)qs.rows * (blockIdx.x + 1) / gridDim.x);
+  for (int i = threadIdx.x; i < o.row; i += 64 * NWV) {
+    float v = 0.f;
+    int src = -1;
+    const int a = i + o.base;
+    if (a >= o.w2 && a < o.w2 + C2 * K2) src = a - o.w2;
+    else if (a >= o.w1 && a < o.w1 + C1 * K1) src = C2 * K2 + (a - o.w1);
+    else if (a >= o.b1 && a < o.b1 + C1) src = C2 * K2 + C1 * K1 + (a - o.b1);
+    else if (a >= o.b2 && a < o.b2 + C2) src = C2 * K2 + C1 * K1 + C1 + (a - o.b2);
+    else if (a >= o.bl && a < o.bl + n) src = C2 * K2 + C1 * K1 + C1 + C2 + (a - o.bl);
+    else if (wl_here && a >= o.wl && a < o.wl + n * G::F) src = RW0 + (a - o.wl);
+    if (src >= 0) {
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) v += red[w * RW + src];
+    } else if (qs.slab && a >= o.qw && a < o.qw + qs.width) {
+      const float* qc = qs.slab + (a - o.qw);
+#pragma unroll 4
+      for (int r = q0; r < q1; ++r) v += qc[(size_t)r * qs.width];
+    }
+    row[i] = v;
+  }
+}
+
+inline size_t bwd3_smem(int n) {
+  using G = Geo<16, 8>;
+  const size_t shared = (size_t)((n * wl_stride(G::F) + 16 + 3) & ~3) * 4 + (size_t)B3::W2T * 2;
+  const size_t act = shared + 4 * (size_t)B3::WAVE_BYTES;
+  const size_t red = sizeof(float) * 4 * (C2 * K2 + C1 * K1 + C1 + C2 + 16 + (size_t)n * G::F);
+  return act > red ? act : red;
+}
+
 // waves per workgroup: 4 for P128; P256's backward images are twice as large -> 2
 template <int W>
 constexpr int fwd_waves() { return 4; }
@@ -808,6 +1220,22 @@ QD_API int qd_qsc2_bwd(const float* x, const float* flat, const int* offs, const
   if (H == 16 && W == 8) return launch_bwd<16, 8>(x, flat, o, angles, dang, dpre, slab, p2, sv, qs, B, n, grid, s);
   if (H == 16 && W == 16) return launch_bwd<16, 16>(x, flat, o, angles, dang, dpre, slab, p2, sv, qs, B, n, grid, s);
   return (int)hipErrorInvalidValue;
+}
+
+// The P128 backward on bf16x3 MFMAs (qsc2_bwd3_kernel): same arguments and outputs as qd_qsc2_bwd.
+QD_API int qd_qsc2_bwd3(const float* x, const float* flat, const int* offs, const float* angles, const float* dang,
+                        float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1, uint8_t* c2,
+                        const float* qslab, int qrows, int qwidth, int B, int n, int H, int W, int grid, void* stream) {
+  if (H != 16 || W != 8 || n < 1 || n > 16 || B <= 0 || grid <= 0 || !p2 || !p1s || !c1 || !c2)
+    return (int)hipErrorInvalidValue;
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
+  Saved sv{p1s, c1, c2};
+  const size_t sm = bwd3_smem(n);
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (hipError_t e = qd::allow_lds(qsc2_bwd3_kernel<4>, sm)) return (int)e;
+  hipLaunchKernelGGL((qsc2_bwd3_kernel<4>), dim3(grid), dim3(256), sm, (hipStream_t)stream, x, flat, o, angles, dang,
+                     dpre, slab, p2, sv, B, n, (int)wl_in_kernel<16, 8>(n), QSlab{qslab, qrows, qwidth});
+  return (int)hipGetLastError();
 }
 
 // 1 if qd_qsc2_bwd also produces the linear-layer weight gradient (slab wl columns) for n qubits

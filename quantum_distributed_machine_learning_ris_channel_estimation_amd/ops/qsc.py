@@ -121,6 +121,10 @@ class QSCStepHIP:
         self._fwd2 = nat.fn(L, "qd_qsc2_fwd", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i,
                                                    _i, _p])
+        # P128: the backward's products on bf16x3 MFMAs (qsc2_bwd3_kernel, fp32-grade; QDML_QSC_BWD=f32: the
+        # f32-MFMA kernel, 1/16 of the bf16 rate)
+        self._bwd3 = nat.fn(L, "qd_qsc2_bwd3", [_p] * 12 + [_i] * 7 + [_p])
+        self.bwd_x3 = (self.Hh, self.Ww) == (16, 8) and os.environ.get("QDML_QSC_BWD", "bf16x3") != "f32"
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
             pre = "qd_qsim_stream" if self.stream else "qd_qsim_big"
@@ -237,7 +241,8 @@ class QSCStepHIP:
         if self.impl != "mfma":   # (the MFMA preprocess backward folds this reduction into its own slab)
             (slabs if slabs is not None else own).add(self.qslab, m.qlayer.weights.grad, 1, self.qrows, 2 * n * L)
         if self.impl == "mfma":
-            nat.check(self._bwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang),
+            bwd = self._bwd3 if self.bwd_x3 else self._bwd2
+            nat.check(bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang),
                                  nat.ptr(self.dpre), nat.ptr(self.preslab), nat.ptr(self.p2), *self._saved(),
                                  nat.ptr(self.qslab), self.qrows, 2 * n * L, B, n, self.Hh, self.Ww, self.grid_bwd, st),
                       "qsc2_bwd")

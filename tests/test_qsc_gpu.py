@@ -70,3 +70,29 @@ def test_qsc_step_quantumnat_in_kernel_noise(cuda):
     # next step: fresh noise
     step(x, y)
     assert not torch.equal(step.wnoisy, wn)
+
+
+@pytest.mark.parametrize("n,B", [(8, 2304), (4, 300), (16, 18)])
+def test_qsc_bwd_bf16x3_matches_f32_kernel(cuda, n, B):
+    """P128 backward on bf16x3 MFMAs (qsc2_bwd3_kernel: hi/lo bf16 operands, three products) vs the
+    f32-MFMA kernel on the same forward: fp32-grade agreement on every parameter gradient."""
+    torch.manual_seed(0)
+    a = QSC_P128(n_qubits=n, use_quantumnat=False, use_gradient_pruning=False).to(cuda)
+    space = FlatParamSpace(list(a.named_parameters()), cuda)
+    x = torch.randn(B, 2, 16, 8, device=cuda)
+    y = torch.randint(0, 3, (B,), device=cuda)
+    step = QSCStepHIP(a, space, B)
+    assert step.bwd_x3
+    out = []
+    for x3 in (True, False):
+        step.bwd_x3 = x3
+        space.zero_grad()
+        loss = step(x, y).clone()
+        torch.cuda.synchronize()
+        out.append((loss, {k: p.grad.clone() for k, p in a.named_parameters()}))
+    (l3, g3), (l32, g32) = out
+    assert torch.equal(l3, l32)
+    for k in g32:
+        err = float((g3[k] - g32[k]).abs().max() / g32[k].abs().max().clamp_min(1e-12))
+        print(f"{k}: bf16x3 vs f32 max-rel {err:.2e}")
+        assert err < 1e-4, (k, err)
