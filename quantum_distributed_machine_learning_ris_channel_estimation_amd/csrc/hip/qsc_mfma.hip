@@ -724,29 +724,37 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
 // qsc2_bwd_kernel (the f32 kernel stays the P256 path and the reference of the GPU test).
 // Per-wave LDS images, bf16 [part = hi | lo]:
 //   XS  [2][kw][ci 2][18][8]    input x, three column-shifted copies      (conv1 wgrad B)
-//   P1S [2][kw][ci 16][10][4]   pool-1 map, three column-shifted copies   (conv2 wgrad B, pool-1 mask)
+//   P1S [2][kw (644)][ci 16][10][4]  pool-1 map, three column-shifted copies (conv2 wgrad B, pool-1 mask)
 //   DZT [2][co 32][40]          dz2 co-major                              (conv2 wgrad A)   } aliased
-//   DZC [2][60][32]             dz2 channel-last, padded 10 x 6           (conv2 dgrad A)   } by DZ1
-//   DZ1 [2][ci 16][136]         dz1 co-major                              (conv1 wgrad A)
+//   DZC [2][60][32]             dz2 channel-last, padded 10 x 6, 8-co chunk q at q ^ 2 (row & 1)
+//                                                                          (conv2 dgrad A)   } by DZ1
+//   DZ1 [2][ci 16][144]         dz1 co-major                              (conv1 wgrad A)
 //   DP1 [16][32] fp32           conv2 data gradient
-// block-shared: the linear layer (fp32, as qsc2_bwd_kernel) and W2T [2][tap][ci][co 32] (dgrad B).
+// block-shared: the linear layer (fp32, as qsc2_bwd_kernel) and W2T [2][tap][ci (48)][co 32] (dgrad B).
+// Strides, pads and the DZC swizzle make every MFMA operand read conflict-free (modelled exhaustively
+// with the ds_read_b64 / b128 lane groups before the build; the first layout measured 2.5 conflict
+// cycles per LDS instruction).
 // ----------------------------------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
 
 struct B3 {   // P128 geometry of the bf16 images (elements)
   static constexpr int XS_PART = 3 * 2 * 18 * 8, XS = 2 * XS_PART;
-  static constexpr int P1S_PART = 3 * 16 * 10 * 4, P1S = 2 * P1S_PART;
+  static constexpr int P1S_CS = 644;   // kw-copy stride (16 * 40 + 4: the two taps of a 32-lane half apart)
+  static constexpr int P1S_PART = 3 * P1S_CS, P1S = 2 * P1S_PART;
   static constexpr int DZT_RS = 40, DZT_PART = 32 * DZT_RS, DZT = 2 * DZT_PART;
   static constexpr int DZC_PART = 60 * 32, DZC = 2 * DZC_PART;
-  static constexpr int DZ1_RS = 136, DZ1_PART = 16 * DZ1_RS, DZ1 = 2 * DZ1_PART;
+  static constexpr int DZ1_RS = 144, DZ1_PART = 16 * DZ1_RS, DZ1 = 2 * DZ1_PART;
   static_assert(DZ1 <= DZT + DZC, "dz1 alias");
   static constexpr int BF = XS + P1S + DZT + DZC;                   // bf16 elements per wave
   static constexpr int WAVE_BYTES = BF * 2 + 16 * 32 * 4 + 32 * 4;  // + DP1 + misc
-  static constexpr int W2T_PART = 9 * 16 * 32, W2T = 2 * W2T_PART;
+  static constexpr int W2T_CS = 48, W2T_PART = 9 * 16 * W2T_CS, W2T = 2 * W2T_PART;
 };
 static_assert(B3::WAVE_BYTES % 16 == 0, "16-byte wave images");
 
+__device__ __forceinline__ int dzc_off(int P, int c) {   // padded position P (= row * 6 + col), channel c
+  return P * 32 + (((c >> 3) ^ (2 * ((P / 6) & 1))) << 3) + (c & 7);
+}
 __device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
   hi = (__bf16)v;
   lo = (__bf16)(v - (float)hi);
@@ -780,12 +788,19 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
       const int j = i / q4, c = i % q4;
       *reinterpret_cast<float4*>(wl + j * wl_stride(G::F) + 4 * c) = src[i];
     }
-    for (int i = threadIdx.x; i < C2 * K2; i += blockDim.x) {   // W2 [co][ci][tap] -> W2T [tap][ci][co]
-      const int co = i / K2, ci = (i % K2) / 9, t = i % 9;
-      __bf16 h, l;
-      split_bf16(flat[o.w2 + i], h, l);
-      w2t[(t * C1 + ci) * 32 + co] = h;
-      w2t[B3::W2T_PART + (t * C1 + ci) * 32 + co] = l;
+    // W2 [co][ci][tap] -> W2T [tap][ci][co]: iterate in DESTINATION order, two co per dword (in source
+    // order the 2-byte writes of a wave landed 64 B apart: 32-way bank conflicts, ~5 us per workgroup)
+#pragma unroll 3
+    for (int i = threadIdx.x; i < 9 * C1 * 16; i += blockDim.x) {
+      const int t = i / (C1 * 16), ci = (i / 16) % C1, cp = i % 16;
+      __bf16 h0, l0, h1, l1;
+      split_bf16(flat[o.w2 + ((2 * cp) * C1 + ci) * 9 + t], h0, l0);
+      split_bf16(flat[o.w2 + ((2 * cp + 1) * C1 + ci) * 9 + t], h1, l1);
+      const int d = ((t * C1 + ci) * B3::W2T_CS + 2 * cp) >> 1;
+      reinterpret_cast<uint32_t*>(w2t)[d] = (uint32_t)__builtin_bit_cast(uint16_t, h0) |
+                                            ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+      reinterpret_cast<uint32_t*>(w2t + B3::W2T_PART)[d] = (uint32_t)__builtin_bit_cast(uint16_t, l0) |
+                                                           ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
     }
   }
   for (int i = lane; i < B3::WAVE_BYTES / 16; i += 64) reinterpret_cast<uint4*>(wbase)[i] = make_uint4(0, 0, 0, 0);
@@ -879,7 +894,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
           h[j] = a;
           l[j] = b;
         }
-        const int off = ((kw * 16 + ci) * 10 + qy + 1) * 4;
+        const int off = kw * B3::P1S_CS + (ci * 10 + qy + 1) * 4;
         *reinterpret_cast<bf16x4_t*>(P1S + off) = h;
         *reinterpret_cast<bf16x4_t*>(P1S + B3::P1S_PART + off) = l;
       }
@@ -932,8 +947,8 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
         __bf16 h, l;
         split_bf16(g, h, l);
         const int py = 4 * hb + lr;
-        DZC[((py + 1) * 6 + px + 1) * 32 + c] = h;
-        DZC[B3::DZC_PART + ((py + 1) * 6 + px + 1) * 32 + c] = l;
+        DZC[dzc_off((py + 1) * 6 + px + 1, c)] = h;
+        DZC[B3::DZC_PART + dzc_off((py + 1) * 6 + px + 1, c)] = l;
       }
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
@@ -964,7 +979,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
         bf16x8_t bh = {}, bl = {};
         if (k < K2) {
           const int tp = k >> 4, ci = k & 15, ky = tp / 3, kx = tp % 3;
-          const int off = ((kx * 16 + ci) * 10 + p0 / 4 + ky) * 4;
+          const int off = kx * B3::P1S_CS + (ci * 10 + p0 / 4 + ky) * 4;
           const bf16x4_t h0 = *reinterpret_cast<const bf16x4_t*>(P1S + off);
           const bf16x4_t h1 = *reinterpret_cast<const bf16x4_t*>(P1S + off + 4);
           const bf16x4_t l0 = *reinterpret_cast<const bf16x4_t*>(P1S + B3::P1S_PART + off);
@@ -985,8 +1000,8 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
       f32x4 acc = {};
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int ao = ((py + 2 - t / 3) * 6 + px + 2 - t % 3) * 32 + 8 * kq;
-        const int bo = (t * C1 + col16) * 32 + 8 * kq;
+        const int ao = dzc_off((py + 2 - t / 3) * 6 + px + 2 - t % 3, 8 * kq);
+        const int bo = (t * C1 + col16) * B3::W2T_CS + 8 * kq;
         const bf16x8_t ah = *reinterpret_cast<const bf16x8_t*>(DZC + ao);
         const bf16x8_t al = *reinterpret_cast<const bf16x8_t*>(DZC + B3::DZC_PART + ao);
         const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(w2t + bo);
@@ -1008,7 +1023,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
 #pragma unroll
       for (int qx = 0; qx < 4; ++qx) {
         const int win = qy * 4 + qx;
-        const float pv = (float)P1S[((16 + co) * 10 + qy + 1) * 4 + qx];   // kw = 1 copy, hi part
+        const float pv = (float)P1S[B3::P1S_CS + (co * 10 + qy + 1) * 4 + qx];   // kw = 1 copy, hi part
         const float g = pv > 0.f ? DP1[co * 32 + win] : 0.f;
         if (dy == 0) gb1[r] += g;
         const uint32_t code = (__shfl(c1v, win) >> (2 * co)) & 3u;
