@@ -29,6 +29,14 @@ constexpr int K1 = 2 * 9;         // conv1 reduction size
 constexpr int K2 = C1 * 9;        // conv2 reduction size (144)
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+
+// bf16x3: an fp32 value as hi + lo bf16 pair; a.b ~= ah.bh + ah.bl + al.bh (relative error ~1e-5)
+__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)v;
+  lo = (__bf16)(v - (float)hi);
+}
 
 struct Offs {
   int w1, b1, w2, b2, wl, bl, row;
@@ -186,12 +194,14 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
 // Saved for the backward (per sample): p1g = pool-1 map [window][16 ch]; c1g[window] = 2-bit
 // window-relative argmax per channel (bits 2c..2c+1: 0 top-left, 1 top-right, 2 bottom-left,
 // 3 bottom-right; first max in that scan order, the reference's max_pool2d choice).
-template <int H, int W, bool WREG, bool STAMP = false>
+// X3: conv2 on bf16x3 MFMAs (mfma_f32_32x32x16_bf16, K = one tap's 16 channels; wx3 = this lane's
+// W2 column as bf16 hi [tap 0..8] | lo [9..17]) instead of the f32 32x32x2 form (1/16 of the rate).
+template <int H, int W, bool WREG, bool STAMP = false, bool X3 = false>
 __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, const float* ws, float* act, int lane,
                                                const float (&wreg)[72], const float* __restrict__ w1g,
                                                const float* __restrict__ b1g, float bias2,
                                                float* __restrict__ p1g, uint32_t* __restrict__ c1g,
-                                               unsigned long long* ts = nullptr) {
+                                               unsigned long long* ts = nullptr, const bf16x8_t* wx3 = nullptr) {
   using G = Geo<H, W>;
   static_assert(W % 4 == 0, "float4 rows");
   const float4* x4 = reinterpret_cast<const float4*>(xs);   // sample planes are 16-byte aligned
@@ -259,10 +269,24 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
           reinterpret_cast<const float4*>(act + G::o_p1 + ((py + t / 3) * G::PW + px + t % 3) * G::PC + 8 * kh);
       const float4 a0 = ap[0], a1 = ap[1];
       const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      if constexpr (X3) {   // k = 8 kh + j = channel: the same pairing as wx3's column
+        bf16x8_t ah, al;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float b = WREG ? wreg[t * 8 + j] : ws[S_W2 + col * K2 + (8 * kh + j) * 9 + t];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b, acc, 0, 0, 0);
+        for (int j = 0; j < 8; ++j) {
+          __bf16 h, l;
+          split_bf16(a[j], h, l);
+          ah[j] = h;
+          al[j] = l;
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, wx3[t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, wx3[9 + t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, wx3[t], acc, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float b = WREG ? wreg[t * 8 + j] : ws[S_W2 + col * K2 + (8 * kh + j) * 9 + t];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b, acc, 0, 0, 0);
+        }
       }
     }
 #pragma unroll
@@ -298,7 +322,7 @@ __device__ __forceinline__ float pool2(const float* act, int f, int& rel) {
 
 // angles (B, n) = tanh(preprocess(x)); p2 (B, F) = flattened pool-2 features (for the linear
 // layer's weight-gradient GEMM in the backward).  One wave per sample.
-template <int H, int W, int NWV, bool STAMP = false>
+template <int H, int W, int NWV, bool STAMP = false, bool X3 = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                       Offs o, float* __restrict__ angles, float* __restrict__ p2,
                                                       Saved sv, int B, int n,
@@ -335,6 +359,18 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
       for (int t = 0; t < 9; ++t) wreg[t * 8 + j] = tmp[j * 9 + t];
   }
   const float bias2 = flat[o.b2 + (lane & 31)];
+  [[maybe_unused]] bf16x8_t wx3[X3 ? 18 : 1];
+  if constexpr (X3) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 h, l;
+        split_bf16(wreg[t * 8 + j], h, l);
+        wx3[t][j] = h;
+        wx3[9 + t][j] = l;
+      }
+  }
   __syncthreads();
   if constexpr (STAMP) ts[1] = stamp();
   const float* wl = ws;
@@ -344,11 +380,11 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
     float* p1g = sv.p1 + (size_t)s * C1 * G::HW2;
     uint32_t* c1g = sv.c1 + (size_t)s * G::HW2;
     if (STAMP && first)
-      sample_forward<H, W, true, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, bias2,
-                                       p1g, c1g, ts);
+      sample_forward<H, W, true, true, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1,
+                                           bias2, p1g, c1g, ts, wx3);
     else
-      sample_forward<H, W, true>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1, bias2, p1g,
-                                 c1g);
+      sample_forward<H, W, true, false, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1,
+                                            bias2, p1g, c1g, nullptr, wx3);
     float* p2s = act + G::o_p2f;
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {
@@ -735,9 +771,6 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
 // with the ds_read_b64 / b128 lane groups before the build; the first layout measured 2.5 conflict
 // cycles per LDS instruction).
 // ----------------------------------------------------------------------------------------------
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
-
 struct B3 {   // P128 geometry of the bf16 images (elements)
   static constexpr int XS_PART = 3 * 2 * 18 * 8, XS = 2 * XS_PART;
   static constexpr int P1S_CS = 644;   // kw-copy stride (16 * 40 + 4: the two taps of a 32-lane half apart)
@@ -755,17 +788,18 @@ static_assert(B3::WAVE_BYTES % 16 == 0, "16-byte wave images");
 __device__ __forceinline__ int dzc_off(int P, int c) {   // padded position P (= row * 6 + col), channel c
   return P * 32 + (((c >> 3) ^ (2 * ((P / 6) & 1))) << 3) + (c & 7);
 }
-__device__ __forceinline__ void split_bf16(float v, __bf16& hi, __bf16& lo) {
-  hi = (__bf16)v;
-  lo = (__bf16)(v - (float)hi);
-}
-
-template <int NWV>
+template <int NWV, bool STAMP = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                          Offs o, const float* __restrict__ angles,
                                                          const float* __restrict__ dang, float* __restrict__ dpre_out,
                                                          float* __restrict__ slab, const float* __restrict__ p2, Saved sv,
-                                                         int B, int n, int wlk, QSlab qs) {
+                                                         int B, int n, int wlk, QSlab qs,
+                                                         unsigned long long* __restrict__ stamps = nullptr) {
+  // STAMP (diagnostic builds): [0] start [1] prologue [2] staging [3] linear + pool-2 bwd [4] conv2 wgrad
+  // [5] conv2 dgrad [6] pool-1 bwd [7] conv1 wgrad (first sample) [8] samples done [9] end
+  unsigned long long ts[NSTAMP] = {};
+  bool first = true;
+  if constexpr (STAMP) ts[0] = stamp();
   using G = Geo<16, 8>;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -805,6 +839,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
   }
   for (int i = lane; i < B3::WAVE_BYTES / 16; i += 64) reinterpret_cast<uint4*>(wbase)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
+  if constexpr (STAMP) ts[1] = stamp();
   const int col32 = lane & 31, kh = lane >> 5;
   const int col16 = lane & 15, kq = lane >> 4;
   f32x16 gw2[5];
@@ -911,6 +946,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
     // dz2's channel-last image is rewritten sparsely: clear it (dz1 of the previous sample aliased it)
     for (int i = lane; i < B3::DZC * 2 / 16; i += 64) reinterpret_cast<uint4*>(DZC)[i] = make_uint4(0, 0, 0, 0);
     wave_lds_fence();
+    if (STAMP && first) ts[2] = stamp();
     // ---- linear backward -> dp2; pool-2 backward through the saved choice (+ReLU) -> dz2 ----
     {
       float dp[FPL];
@@ -966,6 +1002,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
       }
     }
     wave_lds_fence();
+    if (STAMP && first) ts[3] = stamp();
     // ---- conv2 weight grads: dW2[co][k] += sum_pos dz2[co][pos] * im2col(p1)[pos][k], K = positions;
     // A = DZT rows (co), B = P1S (k = tap * 16 + ci): two 8-byte rows of 4 positions per fragment ----
 #pragma unroll
@@ -992,6 +1029,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
         gw2[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, gw2[t], 0, 0, 0);
       }
     }
+    if (STAMP && first) ts[4] = stamp();
     // ---- conv2 data grads: dp1[ci][pos] = sum_{tap, co} dz2_pad[pos + 2 - tap][co] W2[co][ci][tap];
     // 16x16x32: rows = 16 positions, cols = ci, K = one tap's 32 co ----
 #pragma unroll
@@ -1014,6 +1052,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
       for (int r = 0; r < 4; ++r) DP1[col16 * 32 + 16 * mt + 4 * kq + r] = acc[r];
     }
     wave_lds_fence();
+    if (STAMP && first) ts[5] = stamp();
     // ---- pool-1 backward (+ReLU: passes iff p1 > 0): lane = (channel, image row) pairs, 8 positions
     // per pair written whole -> DZ1 (co-major); window codes from the lanes holding them ----
 #pragma unroll
@@ -1042,6 +1081,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
       *reinterpret_cast<bf16x8_t*>(DZ1 + B3::DZ1_PART + co * B3::DZ1_RS + row * 8) = l;
     }
     wave_lds_fence();
+    if (STAMP && first) ts[6] = stamp();
     // ---- conv1 weight grads: dW1[co][k] += sum_pos dz1[co][pos] * im2col(x)[pos][k], k = ci * 9 + tap;
     // 16x16x32: K = 32 positions = 4 image rows, a lane's 8 = one row ----
 #pragma unroll
@@ -1065,7 +1105,12 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
       }
     }
     wave_lds_fence();
+    if (STAMP && first) {
+      ts[7] = stamp();
+      first = false;
+    }
   }
+  if constexpr (STAMP) ts[8] = stamp();
 
   // ---- deterministic workgroup reduction -> slab row (w1 | b1 | w2 | b2 | wl | bl), as qsc2_bwd_kernel ----
   __syncthreads();
@@ -1131,6 +1176,11 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
     }
     row[i] = v;
   }
+  if constexpr (STAMP) {
+    ts[9] = stamp();
+    if (lane == 0)
+      for (int k = 0; k < NSTAMP; ++k) stamps[(size_t)(blockIdx.x * NWV + wv) * NSTAMP + k] = ts[k];
+  }
 }
 
 inline size_t bwd3_smem(int n) {
@@ -1166,20 +1216,20 @@ size_t bwd_smem(int n) {
   return sizeof(float) * (act > red ? act : red);
 }
 
-template <int H, int W>
+template <int H, int W, bool X3 = false>
 int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* p2, Saved sv, int B, int n, int grid,
                hipStream_t s, unsigned long long* stamps = nullptr) {
   constexpr int NW = fwd_waves<W>();
   const size_t sm = fwd_smem<H, W>(n);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   if (stamps) {
-    if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW, true>, sm)) return (int)e;
-    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW, true>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, sv,
-                       B, n, stamps);
+    if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW, true, X3>, sm)) return (int)e;
+    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW, true, X3>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2,
+                       sv, B, n, stamps);
   } else {
-    if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW>, sm)) return (int)e;
-    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles, p2, sv, B,
-                       n, nullptr);
+    if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW, false, X3>, sm)) return (int)e;
+    hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW, false, X3>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles,
+                       p2, sv, B, n, nullptr);
   }
   return (int)hipGetLastError();
 }
@@ -1222,6 +1272,18 @@ QD_API int qd_qsc2_fwd(const float* x, const float* flat, const int* offs, float
   return (int)hipErrorInvalidValue;
 }
 
+// qd_qsc2_fwd with conv2 on bf16x3 MFMAs (sample_forward X3): same arguments and outputs.
+QD_API int qd_qsc2_fwd3(const float* x, const float* flat, const int* offs, float* angles, float* p2, float* p1s,
+                        uint32_t* c1, uint8_t* c2, int B, int n, int H, int W, int grid, void* stream) {
+  if (n < 1 || n > 16 || B <= 0 || grid <= 0 || !p1s || !c1 || !c2) return (int)hipErrorInvalidValue;
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
+  Saved sv{p1s, c1, c2};
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 16 && W == 8) return launch_fwd<16, 8, true>(x, flat, o, angles, p2, sv, B, n, grid, s);
+  if (H == 16 && W == 16) return launch_fwd<16, 16, true>(x, flat, o, angles, p2, sv, B, n, grid, s);
+  return (int)hipErrorInvalidValue;
+}
+
 // slab: (grid, offs[6]) floats, row layout = flat layout from offs[0] (wl columns left zero).
 // p2 / p1s / c1 / c2: what qd_qsc2_fwd saved for this batch.
 QD_API int qd_qsc2_bwd(const float* x, const float* flat, const int* offs, const float* angles, const float* dang,
@@ -1249,7 +1311,22 @@ QD_API int qd_qsc2_bwd3(const float* x, const float* flat, const int* offs, cons
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   if (hipError_t e = qd::allow_lds(qsc2_bwd3_kernel<4>, sm)) return (int)e;
   hipLaunchKernelGGL((qsc2_bwd3_kernel<4>), dim3(grid), dim3(256), sm, (hipStream_t)stream, x, flat, o, angles, dang,
-                     dpre, slab, p2, sv, B, n, (int)wl_in_kernel<16, 8>(n), QSlab{qslab, qrows, qwidth});
+                     dpre, slab, p2, sv, B, n, (int)wl_in_kernel<16, 8>(n), QSlab{qslab, qrows, qwidth}, nullptr);
+  return (int)hipGetLastError();
+}
+
+// Diagnostic: qd_qsc2_bwd3 with per-wave phase stamps (stamps: grid * 4 * 12 u64; see qsc2_bwd3_kernel).
+QD_API int qd_qsc2_bwd3_stamped(const float* x, const float* flat, const int* offs, const float* angles,
+                                const float* dang, float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1,
+                                uint8_t* c2, const float* qslab, int qrows, int qwidth, int B, int n, int grid,
+                                unsigned long long* stamps, void* stream) {
+  Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
+  Saved sv{p1s, c1, c2};
+  const size_t sm = bwd3_smem(n);
+  if (sm > 160 * 1024 || !stamps) return (int)hipErrorInvalidValue;
+  if (hipError_t e = qd::allow_lds(qsc2_bwd3_kernel<4, true>, sm)) return (int)e;
+  hipLaunchKernelGGL((qsc2_bwd3_kernel<4, true>), dim3(grid), dim3(256), sm, (hipStream_t)stream, x, flat, o, angles,
+                     dang, dpre, slab, p2, sv, B, n, (int)wl_in_kernel<16, 8>(n), QSlab{qslab, qrows, qwidth}, stamps);
   return (int)hipGetLastError();
 }
 

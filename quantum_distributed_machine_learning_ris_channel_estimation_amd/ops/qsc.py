@@ -121,10 +121,14 @@ class QSCStepHIP:
         self._fwd2 = nat.fn(L, "qd_qsc2_fwd", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._bwd2 = nat.fn(L, "qd_qsc2_bwd", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i,
                                                    _i, _p])
-        # P128: the backward's products on bf16x3 MFMAs (qsc2_bwd3_kernel, fp32-grade; QDML_QSC_BWD=f32: the
-        # f32-MFMA kernel, 1/16 of the bf16 rate)
+        # the preprocess CNN's products on bf16x3 MFMAs (fp32-grade: hi/lo bf16 operands, three products):
+        # the forward's conv2 (qd_qsc2_fwd3) and, at P128, the whole backward (qsc2_bwd3_kernel); the f32
+        # MFMA they replace runs at 1/16 of the bf16 rate.  QDML_QSC_F32=1: the f32-MFMA kernels.
+        self._fwd3 = nat.fn(L, "qd_qsc2_fwd3", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         self._bwd3 = nat.fn(L, "qd_qsc2_bwd3", [_p] * 12 + [_i] * 7 + [_p])
-        self.bwd_x3 = (self.Hh, self.Ww) == (16, 8) and os.environ.get("QDML_QSC_BWD", "bf16x3") != "f32"
+        x3 = os.environ.get("QDML_QSC_F32", "0") == "0"
+        self.fwd_x3 = x3 and (self.Hh, self.Ww) == (16, 8)   # (P256 at 256 VGPRs halves its occupancy)
+        self.bwd_x3 = x3 and (self.Hh, self.Ww) == (16, 8)
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
             pre = "qd_qsim_stream" if self.stream else "qd_qsim_big"
@@ -183,7 +187,7 @@ class QSCStepHIP:
         st = nat.stream_ptr(x.device)
         flat = sp.flat
         if self.impl == "mfma":
-            nat.check(self._fwd2(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
+            nat.check((self._fwd3 if self.fwd_x3 else self._fwd2)(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
                                  *self._saved(), B, n, self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
         else:
             nat.check(self._pre_fwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), B, n, self.Hh,
@@ -213,7 +217,7 @@ class QSCStepHIP:
         B, n, L = self.B, self.n, self.L
         assert x.shape[0] == B and x.is_contiguous() and self.impl == "mfma"
         st = nat.stream_ptr(x.device)
-        nat.check(self._fwd2(nat.ptr(x), nat.ptr(self.space.flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
+        nat.check((self._fwd3 if self.fwd_x3 else self._fwd2)(nat.ptr(x), nat.ptr(self.space.flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
                              *self._saved(), B, n, self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
         w = m.qlayer.weights.detach().contiguous()
         extra = (nat.ptr(self.qws) if self.qws is not None else None,

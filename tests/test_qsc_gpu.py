@@ -92,6 +92,16 @@ def test_qsc_bwd_bf16x3_matches_f32_kernel(cuda, n, B):
         out.append((loss, {k: p.grad.clone() for k, p in a.named_parameters()}))
     (l3, g3), (l32, g32) = out
     assert torch.equal(l3, l32)
+    # forward: conv2 on bf16x3 (qd_qsc2_fwd3) vs f32 MFMAs -- the angles the circuit consumes
+    angles = []
+    for x3 in (True, False):
+        step.fwd_x3 = x3
+        step(x, y)
+        torch.cuda.synchronize()
+        angles.append(step.angles.clone())
+    err = float((angles[0] - angles[1]).abs().max() / angles[1].abs().max())
+    print(f"angles: bf16x3 vs f32 forward max-rel {err:.2e}")
+    assert err < 1e-4, err
     for k in g32:
         err = float((g3[k] - g32[k]).abs().max() / g32[k].abs().max().clamp_min(1e-12))
         print(f"{k}: bf16x3 vs f32 max-rel {err:.2e}")
