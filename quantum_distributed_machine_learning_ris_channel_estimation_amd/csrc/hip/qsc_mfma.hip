@@ -201,13 +201,14 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
                                                const float (&wreg)[72], const float* __restrict__ w1g,
                                                const float* __restrict__ b1g, float bias2,
                                                float* __restrict__ p1g, uint32_t* __restrict__ c1g,
-                                               unsigned long long* ts = nullptr, const bf16x8_t* wx3 = nullptr) {
+                                               unsigned long long* ts = nullptr, const bf16x8_t* wx3 = nullptr,
+                                               const float4* xpre = nullptr) {
   using G = Geo<H, W>;
   static_assert(W % 4 == 0, "float4 rows");
   const float4* x4 = reinterpret_cast<const float4*>(xs);   // sample planes are 16-byte aligned
 #pragma unroll
   for (int i = lane; i < 2 * G::HW / 4; i += 64) {
-    const float4 v = x4[i];
+    const float4 v = (xpre && i < 64) ? *xpre : x4[i];   // (xpre: this lane's first float4, loaded early)
     const int c = (4 * i) / G::HW, p = (4 * i) % G::HW;
     float* d = act + G::o_x + c * G::XP + (p / W + 1) * G::XW + p % W + 1;
     d[0] = v.x;
@@ -326,13 +327,21 @@ template <int H, int W, int NWV, bool STAMP = false, bool X3 = false>
 __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ flat,
                                                       Offs o, float* __restrict__ angles, float* __restrict__ p2,
                                                       Saved sv, int B, int n,
-                                                      unsigned long long* __restrict__ stamps = nullptr) {
+                                                      unsigned long long* __restrict__ stamps = nullptr,
+                                                      __bf16* __restrict__ w2t_img = nullptr) {
   unsigned long long ts[NSTAMP] = {};
   if constexpr (STAMP) ts[0] = stamp();
   using G = Geo<H, W>;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* ws = sm;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // the first sample's input (one float4 per lane at P128) is loaded before the prologue: its
+  // latency hides behind the weight staging instead of opening the sample
+  float4 xpre = make_float4(0.f, 0.f, 0.f, 0.f);
+  {
+    const int s0 = blockIdx.x * NWV + wv;
+    if (s0 < B) xpre = reinterpret_cast<const float4*>(x + (size_t)s0 * 2 * G::HW)[lane];
+  }
   // LDS: only the linear layer is staged; conv1 weights are scalar loads, conv2 weights live in
   // registers (loaded straight from the flat buffer), conv2 bias is one value per lane
   float* act = sm + fwd_act_base(n, G::F) + wv * G::FWD;
@@ -370,6 +379,18 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
         wx3[t][j] = h;
         wx3[9 + t][j] = l;
       }
+    // the backward's W2T hi / lo image [part][tap][ci (48)][co] (qsc2_bwd3_kernel copies it instead of
+    // transposing W2 in every workgroup): block 0's first wave holds the whole W2, lane = (co, ci half)
+    if (w2t_img && blockIdx.x == 0 && wv == 0) {
+      const int co = lane & 31, c8 = 8 * (lane >> 5);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          w2t_img[(t * C1 + c8 + j) * 48 + co] = wx3[t][j];
+          w2t_img[9 * C1 * 48 + (t * C1 + c8 + j) * 48 + co] = wx3[9 + t][j];
+        }
+    }
   }
   __syncthreads();
   if constexpr (STAMP) ts[1] = stamp();
@@ -379,12 +400,13 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   for (int s = blockIdx.x * NWV + wv; s < B; s += gridDim.x * NWV) {
     float* p1g = sv.p1 + (size_t)s * C1 * G::HW2;
     uint32_t* c1g = sv.c1 + (size_t)s * G::HW2;
+    const float4* xp = s == blockIdx.x * NWV + wv ? &xpre : nullptr;
     if (STAMP && first)
       sample_forward<H, W, true, true, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1,
-                                           bias2, p1g, c1g, ts, wx3);
+                                           bias2, p1g, c1g, ts, wx3, xp);
     else
       sample_forward<H, W, true, false, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1,
-                                            bias2, p1g, c1g, nullptr, wx3);
+                                            bias2, p1g, c1g, nullptr, wx3, xp);
     float* p2s = act + G::o_p2f;
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {
@@ -794,7 +816,8 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
                                                          const float* __restrict__ dang, float* __restrict__ dpre_out,
                                                          float* __restrict__ slab, const float* __restrict__ p2, Saved sv,
                                                          int B, int n, int wlk, QSlab qs,
-                                                         unsigned long long* __restrict__ stamps = nullptr) {
+                                                         unsigned long long* __restrict__ stamps = nullptr,
+                                                         const __bf16* __restrict__ w2t_img = nullptr) {
   // STAMP (diagnostic builds): [0] start [1] prologue [2] staging [3] linear + pool-2 bwd [4] conv2 wgrad
   // [5] conv2 dgrad [6] pool-1 bwd [7] conv1 wgrad (first sample) [8] samples done [9] end
   unsigned long long ts[NSTAMP] = {};
@@ -803,62 +826,8 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
   using G = Geo<16, 8>;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // ---- block-shared: linear layer (fp32) | W2T hi / lo ----
-  float* wl = sm;
-  const int wl_floats = (n * wl_stride(G::F) + 16 + 3) & ~3;
-  __bf16* w2t = reinterpret_cast<__bf16*>(sm + wl_floats);
-  char* wbase = reinterpret_cast<char*>(w2t + B3::W2T) + wv * B3::WAVE_BYTES;
-  __bf16* XS = reinterpret_cast<__bf16*>(wbase);
-  __bf16* P1S = XS + B3::XS;
-  __bf16* DZT = P1S + B3::P1S;
-  __bf16* DZC = DZT + B3::DZT;
-  __bf16* DZ1 = DZT;   // (alias: dz2 images are dead once the conv2 data gradient is done)
-  float* DP1 = reinterpret_cast<float*>(DZC + B3::DZC);
-  float* misc = DP1 + 16 * 32;
-  {
-    const int q4 = G::F / 4;
-    const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
-    for (int i = threadIdx.x; i < n * q4; i += blockDim.x) {
-      const int j = i / q4, c = i % q4;
-      *reinterpret_cast<float4*>(wl + j * wl_stride(G::F) + 4 * c) = src[i];
-    }
-    // W2 [co][ci][tap] -> W2T [tap][ci][co]: iterate in DESTINATION order, two co per dword (in source
-    // order the 2-byte writes of a wave landed 64 B apart: 32-way bank conflicts, ~5 us per workgroup)
-#pragma unroll 3
-    for (int i = threadIdx.x; i < 9 * C1 * 16; i += blockDim.x) {
-      const int t = i / (C1 * 16), ci = (i / 16) % C1, cp = i % 16;
-      __bf16 h0, l0, h1, l1;
-      split_bf16(flat[o.w2 + ((2 * cp) * C1 + ci) * 9 + t], h0, l0);
-      split_bf16(flat[o.w2 + ((2 * cp + 1) * C1 + ci) * 9 + t], h1, l1);
-      const int d = ((t * C1 + ci) * B3::W2T_CS + 2 * cp) >> 1;
-      reinterpret_cast<uint32_t*>(w2t)[d] = (uint32_t)__builtin_bit_cast(uint16_t, h0) |
-                                            ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-      reinterpret_cast<uint32_t*>(w2t + B3::W2T_PART)[d] = (uint32_t)__builtin_bit_cast(uint16_t, l0) |
-                                                           ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
-    }
-  }
-  for (int i = lane; i < B3::WAVE_BYTES / 16; i += 64) reinterpret_cast<uint4*>(wbase)[i] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  if constexpr (STAMP) ts[1] = stamp();
-  const int col32 = lane & 31, kh = lane >> 5;
-  const int col16 = lane & 15, kq = lane >> 4;
-  f32x16 gw2[5];
-#pragma unroll
-  for (int t = 0; t < 5; ++t) gw2[t] = (f32x16){};
-  f32x4 gw1[2];
-  gw1[0] = (f32x4){};
-  gw1[1] = (f32x4){};
+  // ---- one-sample-ahead register prefetch (the first sample's loads fly during the prologue) ----
   constexpr int FPL = G::F / 64;   // 4 pool-2 features per lane: channel lane / 2, cells 4 (lane & 1) + i
-  float gb2 = 0.f, gbl = 0.f, gb1[4] = {0.f, 0.f, 0.f, 0.f};
-  constexpr int NWL = 64 / FPL;
-  const bool wl_here = wlk != 0;
-  float gwl[NWL][FPL];
-#pragma unroll
-  for (int j = 0; j < NWL; ++j)
-#pragma unroll
-    for (int i = 0; i < FPL; ++i) gwl[j][i] = 0.f;
-
-  // ---- one-sample-ahead register prefetch ----
   f32x4 rx[2];           // lanes 0..31: x row (c = lane / 16, image row lane % 16)
   float rp1[2][4];       // (ci, pool-1 row) pairs lane, lane + 64: 4 columns
   f32x4 rp2;
@@ -887,6 +856,69 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
   };
   const int s0 = blockIdx.x * NWV + wv;
   if (s0 < B) prefetch(s0);
+  // ---- block-shared: linear layer (fp32) | W2T hi / lo ----
+  float* wl = sm;
+  const int wl_floats = (n * wl_stride(G::F) + 16 + 3) & ~3;
+  __bf16* w2t = reinterpret_cast<__bf16*>(sm + wl_floats);
+  char* wbase = reinterpret_cast<char*>(w2t + B3::W2T) + wv * B3::WAVE_BYTES;
+  __bf16* XS = reinterpret_cast<__bf16*>(wbase);
+  __bf16* P1S = XS + B3::XS;
+  __bf16* DZT = P1S + B3::P1S;
+  __bf16* DZC = DZT + B3::DZT;
+  __bf16* DZ1 = DZT;   // (alias: dz2 images are dead once the conv2 data gradient is done)
+  float* DP1 = reinterpret_cast<float*>(DZC + B3::DZC);
+  float* misc = DP1 + 16 * 32;
+  {
+    const int q4 = G::F / 4;
+    const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
+    for (int i = threadIdx.x; i < n * q4; i += blockDim.x) {
+      const int j = i / q4, c = i % q4;
+      *reinterpret_cast<float4*>(wl + j * wl_stride(G::F) + 4 * c) = src[i];
+    }
+    if (w2t_img) {   // this step's image from the forward (qd_qsc2_fwd3): one copy, one round trip
+      const uint4* src = reinterpret_cast<const uint4*>(w2t_img);
+      uint4* dst = reinterpret_cast<uint4*>(w2t);
+#pragma unroll
+      for (int k = 0; k < (B3::W2T * 2 / 16 + 255) / 256; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < B3::W2T * 2 / 16) dst[i] = src[i];
+      }
+    } else
+    // W2 [co][ci][tap] -> W2T [tap][ci][co]: iterate in DESTINATION order, two co per dword (in source
+    // order the 2-byte writes of a wave landed 64 B apart: 32-way bank conflicts, ~5 us per workgroup)
+#pragma unroll 3
+    for (int i = threadIdx.x; i < 9 * C1 * 16; i += blockDim.x) {
+      const int t = i / (C1 * 16), ci = (i / 16) % C1, cp = i % 16;
+      __bf16 h0, l0, h1, l1;
+      split_bf16(flat[o.w2 + ((2 * cp) * C1 + ci) * 9 + t], h0, l0);
+      split_bf16(flat[o.w2 + ((2 * cp + 1) * C1 + ci) * 9 + t], h1, l1);
+      const int d = ((t * C1 + ci) * B3::W2T_CS + 2 * cp) >> 1;
+      reinterpret_cast<uint32_t*>(w2t)[d] = (uint32_t)__builtin_bit_cast(uint16_t, h0) |
+                                            ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+      reinterpret_cast<uint32_t*>(w2t + B3::W2T_PART)[d] = (uint32_t)__builtin_bit_cast(uint16_t, l0) |
+                                                           ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+    }
+  }
+  for (int i = lane; i < B3::WAVE_BYTES / 16; i += 64) reinterpret_cast<uint4*>(wbase)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  if constexpr (STAMP) ts[1] = stamp();
+  const int col32 = lane & 31, kh = lane >> 5;
+  const int col16 = lane & 15, kq = lane >> 4;
+  f32x16 gw2[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) gw2[t] = (f32x16){};
+  f32x4 gw1[2];
+  gw1[0] = (f32x4){};
+  gw1[1] = (f32x4){};
+  float gb2 = 0.f, gbl = 0.f, gb1[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NWL = 64 / FPL;
+  const bool wl_here = wlk != 0;
+  float gwl[NWL][FPL];
+#pragma unroll
+  for (int j = 0; j < NWL; ++j)
+#pragma unroll
+    for (int i = 0; i < FPL; ++i) gwl[j][i] = 0.f;
+
 
   for (int s = s0; s < B; s += gridDim.x * NWV) {
     // ---- saved state -> shifted bf16 copies ----
@@ -1218,7 +1250,7 @@ size_t bwd_smem(int n) {
 
 template <int H, int W, bool X3 = false>
 int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* p2, Saved sv, int B, int n, int grid,
-               hipStream_t s, unsigned long long* stamps = nullptr) {
+               hipStream_t s, unsigned long long* stamps = nullptr, __bf16* w2t_img = nullptr) {
   constexpr int NW = fwd_waves<W>();
   const size_t sm = fwd_smem<H, W>(n);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
@@ -1229,7 +1261,7 @@ int launch_fwd(const float* x, const float* flat, Offs o, float* angles, float* 
   } else {
     if (hipError_t e = allow_lds(qsc2_fwd_kernel<H, W, NW, false, X3>, sm)) return (int)e;
     hipLaunchKernelGGL((qsc2_fwd_kernel<H, W, NW, false, X3>), dim3(grid), dim3(64 * NW), sm, s, x, flat, o, angles,
-                       p2, sv, B, n, nullptr);
+                       p2, sv, B, n, nullptr, w2t_img);
   }
   return (int)hipGetLastError();
 }
@@ -1273,13 +1305,15 @@ QD_API int qd_qsc2_fwd(const float* x, const float* flat, const int* offs, float
 }
 
 // qd_qsc2_fwd with conv2 on bf16x3 MFMAs (sample_forward X3): same arguments and outputs.
+// w2t_img (nullable): also write the backward's W2T hi / lo image (B3::W2T bf16) from these weights.
 QD_API int qd_qsc2_fwd3(const float* x, const float* flat, const int* offs, float* angles, float* p2, float* p1s,
-                        uint32_t* c1, uint8_t* c2, int B, int n, int H, int W, int grid, void* stream) {
+                        uint32_t* c1, uint8_t* c2, int B, int n, int H, int W, int grid, void* w2t_img, void* stream) {
   if (n < 1 || n > 16 || B <= 0 || grid <= 0 || !p1s || !c1 || !c2) return (int)hipErrorInvalidValue;
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8) return launch_fwd<16, 8, true>(x, flat, o, angles, p2, sv, B, n, grid, s);
+  if (H == 16 && W == 8)
+    return launch_fwd<16, 8, true>(x, flat, o, angles, p2, sv, B, n, grid, s, nullptr, (__bf16*)w2t_img);
   if (H == 16 && W == 16) return launch_fwd<16, 16, true>(x, flat, o, angles, p2, sv, B, n, grid, s);
   return (int)hipErrorInvalidValue;
 }
@@ -1300,9 +1334,11 @@ QD_API int qd_qsc2_bwd(const float* x, const float* flat, const int* offs, const
 }
 
 // The P128 backward on bf16x3 MFMAs (qsc2_bwd3_kernel): same arguments and outputs as qd_qsc2_bwd.
+// w2t_img (nullable): the W2T image the forward wrote this step (qd_qsc2_fwd3), else built in-kernel.
 QD_API int qd_qsc2_bwd3(const float* x, const float* flat, const int* offs, const float* angles, const float* dang,
                         float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1, uint8_t* c2,
-                        const float* qslab, int qrows, int qwidth, int B, int n, int H, int W, int grid, void* stream) {
+                        const float* qslab, int qrows, int qwidth, int B, int n, int H, int W, int grid,
+                        const void* w2t_img, void* stream) {
   if (H != 16 || W != 8 || n < 1 || n > 16 || B <= 0 || grid <= 0 || !p2 || !p1s || !c1 || !c2)
     return (int)hipErrorInvalidValue;
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
@@ -1311,7 +1347,8 @@ QD_API int qd_qsc2_bwd3(const float* x, const float* flat, const int* offs, cons
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   if (hipError_t e = qd::allow_lds(qsc2_bwd3_kernel<4>, sm)) return (int)e;
   hipLaunchKernelGGL((qsc2_bwd3_kernel<4>), dim3(grid), dim3(256), sm, (hipStream_t)stream, x, flat, o, angles, dang,
-                     dpre, slab, p2, sv, B, n, (int)wl_in_kernel<16, 8>(n), QSlab{qslab, qrows, qwidth}, nullptr);
+                     dpre, slab, p2, sv, B, n, (int)wl_in_kernel<16, 8>(n), QSlab{qslab, qrows, qwidth}, nullptr,
+                     (const __bf16*)w2t_img);
   return (int)hipGetLastError();
 }
 

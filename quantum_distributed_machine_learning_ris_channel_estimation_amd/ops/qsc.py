@@ -124,11 +124,15 @@ class QSCStepHIP:
         # the preprocess CNN's products on bf16x3 MFMAs (fp32-grade: hi/lo bf16 operands, three products):
         # the forward's conv2 (qd_qsc2_fwd3) and, at P128, the whole backward (qsc2_bwd3_kernel); the f32
         # MFMA they replace runs at 1/16 of the bf16 rate.  QDML_QSC_F32=1: the f32-MFMA kernels.
-        self._fwd3 = nat.fn(L, "qd_qsc2_fwd3", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
-        self._bwd3 = nat.fn(L, "qd_qsc2_bwd3", [_p] * 12 + [_i] * 7 + [_p])
+        self._fwd3 = nat.fn(L, "qd_qsc2_fwd3", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p])
+        self._bwd3 = nat.fn(L, "qd_qsc2_bwd3", [_p] * 12 + [_i] * 7 + [_p, _p])
         x3 = os.environ.get("QDML_QSC_F32", "0") == "0"
         self.fwd_x3 = x3 and (self.Hh, self.Ww) == (16, 8)   # (P256 at 256 VGPRs halves its occupancy)
         self.bwd_x3 = x3 and (self.Hh, self.Ww) == (16, 8)
+        # the backward's bf16 hi / lo transposed conv2 weights, written by the bf16x3 forward each step
+        self.w2t_img = torch.empty(2 * 9 * 16 * 48, device=self.p2.device, dtype=torch.bfloat16) \
+            if (self.bwd_x3 and impl == "mfma") else None
+        self._img_step = False   # the image holds this step's weights (the last forward was fwd3)
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
             pre = "qd_qsim_stream" if self.stream else "qd_qsim_big"
@@ -161,6 +165,18 @@ class QSCStepHIP:
         return w
 
     @torch.no_grad()
+    def _fwd_mfma(self, x, flat, st) -> None:
+        """The preprocess forward (f32 or bf16x3 conv2); the bf16x3 one also refreshes the backward's W2T image."""
+        args = (nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2), *self._saved(), self.B,
+                self.n, self.Hh, self.Ww, self.grid_fwd)
+        if self.fwd_x3:
+            img = self.w2t_img if self.bwd_x3 else None
+            nat.check(self._fwd3(*args, nat.ptr(img) if img is not None else None, st), "qsc2_fwd3")
+            self._img_step = img is not None
+        else:
+            nat.check(self._fwd2(*args, st), "qsc2_fwd")
+            self._img_step = False
+
     def _saved(self):
         return nat.ptr(self.p1s), nat.ptr(self.c1), nat.ptr(self.c2)
 
@@ -187,8 +203,7 @@ class QSCStepHIP:
         st = nat.stream_ptr(x.device)
         flat = sp.flat
         if self.impl == "mfma":
-            nat.check((self._fwd3 if self.fwd_x3 else self._fwd2)(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
-                                 *self._saved(), B, n, self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
+            self._fwd_mfma(x, flat, st)
         else:
             nat.check(self._pre_fwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), B, n, self.Hh,
                                     self.Ww, self.grid_fwd, st), "qsc_pre_fwd")
@@ -217,8 +232,7 @@ class QSCStepHIP:
         B, n, L = self.B, self.n, self.L
         assert x.shape[0] == B and x.is_contiguous() and self.impl == "mfma"
         st = nat.stream_ptr(x.device)
-        nat.check((self._fwd3 if self.fwd_x3 else self._fwd2)(nat.ptr(x), nat.ptr(self.space.flat), self.offs, nat.ptr(self.angles), nat.ptr(self.p2),
-                             *self._saved(), B, n, self.Hh, self.Ww, self.grid_fwd, st), "qsc2_fwd")
+        self._fwd_mfma(x, self.space.flat, st)
         w = m.qlayer.weights.detach().contiguous()
         extra = (nat.ptr(self.qws) if self.qws is not None else None,
                  nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
@@ -245,11 +259,13 @@ class QSCStepHIP:
         if self.impl != "mfma":   # (the MFMA preprocess backward folds this reduction into its own slab)
             (slabs if slabs is not None else own).add(self.qslab, m.qlayer.weights.grad, 1, self.qrows, 2 * n * L)
         if self.impl == "mfma":
-            bwd = self._bwd3 if self.bwd_x3 else self._bwd2
-            nat.check(bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang),
-                                 nat.ptr(self.dpre), nat.ptr(self.preslab), nat.ptr(self.p2), *self._saved(),
-                                 nat.ptr(self.qslab), self.qrows, 2 * n * L, B, n, self.Hh, self.Ww, self.grid_bwd, st),
-                      "qsc2_bwd")
+            args = (nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.angles), nat.ptr(self.dang), nat.ptr(self.dpre),
+                    nat.ptr(self.preslab), nat.ptr(self.p2), *self._saved(), nat.ptr(self.qslab), self.qrows, 2 * n * L,
+                    B, n, self.Hh, self.Ww, self.grid_bwd)
+            if self.bwd_x3:
+                nat.check(self._bwd3(*args, nat.ptr(self.w2t_img) if self._img_step else None, st), "qsc2_bwd3")
+            else:
+                nat.check(self._bwd2(*args, st), "qsc2_bwd")
         else:
             nat.check(self._pre_bwd(nat.ptr(x), nat.ptr(flat), self.offs, nat.ptr(self.dang), nat.ptr(self.preslab), B,
                                     n, self.Hh, self.Ww, self.grid_bwd, st), "qsc_pre_bwd")

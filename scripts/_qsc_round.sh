@@ -12,4 +12,3 @@ for i in 1 2; do
   timeout -k 10 120 python bench.py --steps 300 --warmup 10 > $O/b$i.log 2>&1 || exit 1
   QDML_QSC_F32=1 timeout -k 10 120 python bench.py --steps 300 --warmup 10 > $O/c$i.log 2>&1 || exit 1
 done
-STEPS=prof bash scripts/gpu_check.sh
