@@ -128,7 +128,11 @@ __device__ __forceinline__ void stage4(float* dst, const float* __restrict__ src
 }
 
 // forward kernel LDS: just the linear layer (wl [n][F+4] | bl), then the per-wave images
-__host__ __device__ constexpr int fwd_act_base(int n, int F) { return (n * (F + 4) + 16 + 3) & ~3; }
+// ... then conv1's weights and bias (C1 * K1 + C1 floats: read as wave-uniform LDS broadcasts -- as scalar
+// loads the 288 weights overflowed the SGPRs and the compiler spilled them through VGPR lanes, ~1800
+// v_readlane / v_writelane per sample), then the per-wave images
+__host__ __device__ constexpr int fwd_w1_base(int n, int F) { return (n * (F + 4) + 16 + 3) & ~3; }
+__host__ __device__ constexpr int fwd_act_base(int n, int F) { return fwd_w1_base(n, F) + ((C1 * K1 + C1 + 3) & ~3); }
 __device__ __forceinline__ void stage_linear(const float* __restrict__ flat, Offs o, float* ws, int n, int F) {
   const int q4 = F / 4;
   const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
@@ -158,33 +162,39 @@ __device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Of
 
 // conv1 pre-activations (+bias) of one ROW of pool window `win` (hw = 0 top, 1 bottom): all 16
 // channels x 2 positions.  The whole wave walks the channels in lockstep, so every weight is
-// wave-uniform: scalar loads straight from the flat buffer (SGPR operands), no LDS traffic.
+// wave-uniform: LDS broadcast reads of the workgroup's staged copy (w1g = W1 transposed [k][co], b1g).
 template <int H, int W>
 __device__ __forceinline__ void conv1_half(const float* act, const float* __restrict__ w1g,
                                            const float* __restrict__ b1g, int win, int hw, float (&acc)[16][2]) {
   using G = Geo<H, W>;
   const int qy = win / G::W2, qx = win % G::W2;
-  float patch[2][3][4];
-#pragma unroll
-  for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 4; ++dx)
-        patch[ci][dy][dx] = act[G::o_x + ci * G::XP + (2 * qy + hw + dy) * G::XW + 2 * qx + dx];
 #pragma unroll
   for (int co = 0; co < C1; ++co) {
     const float b = b1g[co];
     acc[co][0] = b;
     acc[co][1] = b;
+  }
+  // k = (ci, tap) outer as a rolled loop, channels inner: each k's 16 weights are four broadcast
+  // ds_read_b128 of the transposed copy [k][co] and its two input values two LDS reads, consumed right
+  // away (unrolled, the compiler hoisted all 288 weights into VGPRs and halved the occupancy)
+#pragma unroll 2
+  for (int k = 0; k < K1; ++k) {
+    const int ci = k / 9, t = k % 9;
+    const float* px = act + G::o_x + ci * G::XP + (2 * qy + hw + t / 3) * G::XW + 2 * qx + t % 3;
+    const float p0 = px[0], p1 = px[1];
+    const float4* wk = reinterpret_cast<const float4*>(w1g + k * C1);
 #pragma unroll
-    for (int ci = 0; ci < 2; ++ci)
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const float w = w1g[co * K1 + ci * 9 + t];
-        acc[co][0] += w * patch[ci][t / 3][t % 3];
-        acc[co][1] += w * patch[ci][t / 3][1 + t % 3];
-      }
+    for (int q = 0; q < 4; ++q) {
+      const float4 w = wk[q];
+      acc[4 * q][0] += w.x * p0;
+      acc[4 * q][1] += w.x * p1;
+      acc[4 * q + 1][0] += w.y * p0;
+      acc[4 * q + 1][1] += w.y * p1;
+      acc[4 * q + 2][0] += w.z * p0;
+      acc[4 * q + 2][1] += w.z * p1;
+      acc[4 * q + 3][0] += w.w * p0;
+      acc[4 * q + 3][1] += w.w * p1;
+    }
   }
 }
 
@@ -345,7 +355,10 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   // LDS: only the linear layer is staged; conv1 weights are scalar loads, conv2 weights live in
   // registers (loaded straight from the flat buffer), conv2 bias is one value per lane
   float* act = sm + fwd_act_base(n, G::F) + wv * G::FWD;
+  float* w1s = sm + fwd_w1_base(n, G::F);
   stage_linear(flat, o, ws, n, G::F);
+  for (int i = threadIdx.x; i < C1 * K1 + C1; i += blockDim.x)   // W1 [co][k] -> [k][co] (+ bias)
+    w1s[i < C1 * K1 ? (i % K1) * C1 + i / K1 : i] = i < C1 * K1 ? flat[o.w1 + i] : flat[o.b1 + i - C1 * K1];
   static_assert(G::FWD % 4 == 0 && G::BWD % 4 == 0, "float4 image fills");
   for (int i = lane; i < G::FWD / 4; i += 64)   // zero halos once; interiors rewritten per sample
     reinterpret_cast<float4*>(act)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -402,10 +415,10 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
     uint32_t* c1g = sv.c1 + (size_t)s * G::HW2;
     const float4* xp = s == blockIdx.x * NWV + wv ? &xpre : nullptr;
     if (STAMP && first)
-      sample_forward<H, W, true, true, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1,
+      sample_forward<H, W, true, true, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, w1s, w1s + C1 * K1,
                                            bias2, p1g, c1g, ts, wx3, xp);
     else
-      sample_forward<H, W, true, false, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, flat + o.w1, flat + o.b1,
+      sample_forward<H, W, true, false, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, w1s, w1s + C1 * K1,
                                             bias2, p1g, c1g, nullptr, wx3, xp);
     float* p2s = act + G::o_p2f;
 #pragma unroll
@@ -1390,7 +1403,7 @@ QD_API int qd_qsc2_fwd_stamped(const float* x, const float* flat, const int* off
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   hipStream_t s = (hipStream_t)stream;
-  if (H == 16 && W == 8) return launch_fwd<16, 8>(x, flat, o, angles, p2, sv, B, n, grid, s, stamps);
+  if (H == 16 && W == 8) return launch_fwd<16, 8, true>(x, flat, o, angles, p2, sv, B, n, grid, s, stamps);   // (bf16x3)
   if (H == 16 && W == 16) return launch_fwd<16, 16>(x, flat, o, angles, p2, sv, B, n, grid, s, stamps);
   return (int)hipErrorInvalidValue;
 }
