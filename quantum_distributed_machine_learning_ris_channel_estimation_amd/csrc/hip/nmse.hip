@@ -239,6 +239,32 @@ __global__ void __launch_bounds__(256) nmse_fused_kernel(const TY* __restrict__ 
   const int r0 = blockIdx.y * rpc;
   const int u = r0 / (B * E);
   const int S = E * U;
+  const int c0 = (blockIdx.x * 256 + t) * 4;
+  const bool act = c0 < cols;
+  // The block's rows in batches of RT: a batch's rowoff, Y, label and perf loads are all issued before
+  // any of them is used (rowoff -> label is the only dependent pair), and the first batch is issued
+  // BEFORE the per-stream label powers below, so the whole block pays ~2 memory round trips instead of
+  // one per phase (rowden -> barrier -> rowoff -> label, per batch).
+  constexpr int RT = 2 * E;
+  const int r1 = r0 + rpc;
+  int ro[RT];
+  float4 yv[RT], lv[RT], pv[RT];
+  auto issue = [&](int rb) {
+#pragma unroll
+    for (int q = 0; q < RT; ++q)
+      if (rb + q < r1) ro[q] = rowoff[rb + q];
+#pragma unroll
+    for (int q = 0; q < RT; ++q)
+      if (rb + q < r1) yv[q] = load4<TY>(Y + (size_t)(rb + q) * cols + c0);
+#pragma unroll
+    for (int q = 0; q < RT; ++q)
+      if (rb + q < r1) {
+        const size_t le = (size_t)ro[q] * cols + c0;
+        lv[q] = *reinterpret_cast<const float4*>(Lb + le);
+        pv[q] = Pf ? *reinterpret_cast<const float4*>(Pf + le) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  };
+  if (act) issue(r0);
   // per-stream label powers of this u-block (wave e: stream e*U + u), fixed order
   for (int e = wv; e < E; e += 4) {
     float a = 0.f, ap = 0.f;
@@ -270,25 +296,24 @@ __global__ void __launch_bounds__(256) nmse_fused_kernel(const TY* __restrict__ 
   float coef[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) coef[e] = loss_scale * 2.f / ((float)S * sden[e]);
-  const int c0 = (blockIdx.x * 256 + t) * 4;
   float num[E], nump[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) num[e] = nump[e] = 0.f;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (c0 < cols) {
-    for (int rb = r0; rb < r0 + rpc; rb += E) {
+  if (act) {
+    for (int rb = r0; rb < r1; rb += RT) {
+      if (rb != r0) issue(rb);
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int r = rb + e;
-        const size_t ey = (size_t)r * cols + c0;
-        const size_t le = (size_t)rowoff[r] * cols + c0;
-        const float4 yv = load4<TY>(Y + ey);
-        const float4 lv = *reinterpret_cast<const float4*>(Lb + le);
-        const float d0 = yv.x - lv.x, d1 = yv.y - lv.y, d2 = yv.z - lv.z, d3 = yv.w - lv.w;
+      for (int q = 0; q < RT; ++q) {
+        if (rb + q >= r1) break;   // (rpc % E == 0: whole e-triples)
+        const int e = q % E;
+        const size_t ey = (size_t)(rb + q) * cols + c0;
+        const float4 y = yv[q], l = lv[q];
+        const float d0 = y.x - l.x, d1 = y.y - l.y, d2 = y.z - l.z, d3 = y.w - l.w;
         num[e] += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
         if (Pf) {
-          const float4 pv = *reinterpret_cast<const float4*>(Pf + le);
-          const float q0 = yv.x - pv.x, q1 = yv.y - pv.y, q2 = yv.z - pv.z, q3 = yv.w - pv.w;
+          const float4 p = pv[q];
+          const float q0 = y.x - p.x, q1 = y.y - p.y, q2 = y.z - p.z, q3 = y.w - p.w;
           nump[e] += q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3;
         }
         const float c = coef[e];

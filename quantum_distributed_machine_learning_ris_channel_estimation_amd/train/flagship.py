@@ -271,6 +271,10 @@ class FlagshipTrainer:
         self.fc_overlap = bool(cfg.fc_adam_overlap and self.streams is not None and mode in ("dag", "dagq")
                                and ctx.world == 1 and not cfg.split_graphs and not self.branches)
         self._fc_pending = False
+        # where the QSC branch joins the HDCE chain in a dagq step: "end" (after the Adam), "adam" or "bwd"
+        self._qsc_join_at = os.environ.get("QDML_QSC_JOIN", "end")
+        assert self._qsc_join_at in ("end", "adam", "bwd"), self._qsc_join_at
+        self._qsc_joined = False
         self._phases = None   # (phase_times) per-step dicts of HIP events
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
@@ -324,7 +328,18 @@ class FlagshipTrainer:
     def _join(self, names=("qsc", "fc", "conv")) -> None:
         cur = torch.cuda.current_stream(self.ctx.device)
         for n in names:
+            if n == "qsc" and self._qsc_joined:   # (already joined earlier in this step: no second edge)
+                self._qsc_joined = False
+                continue
             cur.wait_stream(self.streams[n])
+
+    def _early_join(self) -> None:
+        """(dagq) join the QSC branch into the HDCE chain before its backward / Adam instead of at the
+        end of the step (QDML_QSC_JOIN=bwd|adam): the branch has long finished by then, and the next
+        step's gather then follows the HDCE Adam on the same queue."""
+        if self.mode in ("dag", "dagq") and self.cfg.qsc_fork == "gather" and not self._qsc_joined:
+            self._join(("qsc",))
+            self._qsc_joined = True
 
     def _gather(self, hdce: bool = True, classifier: bool = True) -> None:
         # the fused GPU kernels WRITE every gradient (one producer per element): no zero_grad fills
@@ -386,6 +401,8 @@ class FlagshipTrainer:
             self._gather(hdce=True, classifier=False)
         self._hdce_forward()
         br = self.branches
+        if self._qsc_join_at == "bwd":
+            self._early_join()
         if "a" in br:
             # FC Adam once the dgrad GEMM (which reads the bf16 weight shadow it rewrites) is queued
             with self._fork(self.streams["fc"]):
@@ -411,6 +428,8 @@ class FlagshipTrainer:
                 self._fc_pending = True
                 return
             if len(self.hopt.bounds) == 1:
+                if self._qsc_join_at == "adam":
+                    self._early_join()
                 pk = self._adam_pack()
                 self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
                 if self.tail_pack and pk is None:
