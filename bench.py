@@ -61,7 +61,7 @@ def main() -> int:
     ap.add_argument("--phase-steps", type=int, default=20,
                     help="N > 1: extra steps (after the timed region) timed per phase with HIP events; 0 = off")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
-    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "dagi", "qsc", "full"],
+    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "dagi", "dagf", "qsc", "full"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
                          "or a separate QSC graph on its own stream (+ HDCE side branches with 'full')")
     args = ap.parse_args()

@@ -217,6 +217,9 @@ class FlagshipTrainer:
         #   dag    : ONE graph captured from 4 streams (qsc / fc / conv branches forked off the main chain)
         #   dagq   : ONE graph, only the QSC branch forked; the HDCE a single chain
         #   dagi   : ONE graph, the HDCE and QSC chains independent within a replay (see _indep_body)
+        #   dagf   : as dagi, but the QSC chain of every step forks from that step's HDCE gather (a per-step
+        #            cross-queue edge, no per-step join): the step boundary (Adam -> gather -> conv1) stays on
+        #            the HDCE queue (profiles/r2_19_*)
         #   !! dagi, qsc and full are kept for diagnosis only.  Whenever the QSC chain runs concurrently
         #   with the HDCE chain ACROSS step boundaries (dagi with >= 2 steps per replay; two graphs
         #   replayed concurrently in qsc / full) the QSC weights drift from the serial run by ~1e-5
@@ -235,7 +238,7 @@ class FlagshipTrainer:
         # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge
         # that crosses queues costs a barrier packet, so fewer, longer branches can win)
         mode = cfg.stream_mode
-        if mode not in ("serial", "dag", "dagq", "dagi", "qsc", "full"):
+        if mode not in ("serial", "dag", "dagq", "dagi", "dagf", "qsc", "full"):
             raise ValueError(f"stream_mode {mode!r}")
         if mode in ("qsc", "full", "dagi"):
             import warnings
@@ -275,6 +278,7 @@ class FlagshipTrainer:
         self._qsc_join_at = os.environ.get("QDML_QSC_JOIN", "end")
         assert self._qsc_join_at in ("end", "adam", "bwd"), self._qsc_join_at
         self._qsc_joined = False
+        self._join_rev = os.environ.get("QDML_JOIN_ORDER", "") == "rev"
         self._phases = None   # (phase_times) per-step dicts of HIP events
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
@@ -303,8 +307,9 @@ class FlagshipTrainer:
                 # freed during capture must not be handed to the other)
                 gs = [GraphedStep(rep(self._qsc_graph), enabled=graphs),
                       GraphedStep(rep(lambda: self._hdce_graph(gather=True)), enabled=graphs)]
-            elif mode == "dagi":
-                gs = [GraphedStep(lambda: self._indep_body(k), enabled=graphs, capture_stream=self.capture_stream)]
+            elif mode in ("dagi", "dagf"):
+                gs = [GraphedStep(lambda: self._indep_body(k, fork_each=mode == "dagf"), enabled=graphs,
+                                  capture_stream=self.capture_stream)]
             else:
                 # one graph: gather, both forwards, NMSE, both backwards, the optimizers
                 gs = [GraphedStep(rep(self._step_body), enabled=graphs, capture_stream=self.capture_stream)]
@@ -332,6 +337,14 @@ class FlagshipTrainer:
                 self._qsc_joined = False
                 continue
             cur.wait_stream(self.streams[n])
+            if n == "qsc" and self._join_rev and self.mode in ("dag", "dagq"):
+                # the node after the join has parents on two queues: reverse their order so the graph
+                # executor keeps it (and the next step's chain) on the HDCE queue (csrc/hip/graph.hip)
+                import ctypes
+                f = nat.fn(nat.hip_lib(), "qd_capture_deps", [ctypes.c_void_p, ctypes.c_int])
+                rc = f(nat.stream_ptr(self.ctx.device), 1)
+                if rc < 0:
+                    raise RuntimeError(f"qd_capture_deps failed: hip error {-rc}")
 
     def _early_join(self) -> None:
         """(dagq) join the QSC branch into the HDCE chain before its backward / Adam instead of at the
@@ -675,7 +688,7 @@ class FlagshipTrainer:
             return
         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)
 
-    def _indep_body(self, k: int) -> None:
+    def _indep_body(self, k: int, fork_each: bool = False) -> None:
         """(dagi) ``k`` steps as TWO independent chains of one graph: the HDCE chain on the capturing
         stream, the QSC chain (each step with its own batch gather, cursor ``cur[1]``) on the qsc stream.
         The chains meet only at the replay's head and tail -- no per-step fork / join edges, which the
@@ -690,7 +703,9 @@ class FlagshipTrainer:
         q = self.streams["qsc"]
         for i in range(k):
             self._gather(hdce=True, classifier=False)
-            if i == 0:   # (a node on the capturing stream first: a branch forked before it is a ROOT)
+            if i == 0 or fork_each:   # (a node on the capturing stream first: a branch forked before it is a ROOT)
+                # dagf: the QSC chain of step i forks from the HDCE chain's gather of step i (no per-step join:
+                # nothing in the HDCE chain waits for the QSC branch, so the step boundary stays on one queue)
                 q.wait_stream(main)
             with torch.cuda.stream(q):
                 self._qsc_graph()

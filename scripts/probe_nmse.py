@@ -47,8 +47,18 @@ def main():
     res = {"three_kernels": timeit(old)}
     for m in (1, 2, 4, 8):
         res[f"fused_rpc{E * m}"] = timeit(lambda: nm.fused(Y, L, P, bg, (E, U, B), rpc_mult=m))
+    # the same rows gathered into contiguous buffers first (rowoff = identity): what the random
+    # 8 KB-row reads out of the 2 x 1.3 GB label stores cost
+    Lg = L.view(-1, cols)[rowoff.long()].contiguous()
+    Pg = P.view(-1, cols)[rowoff.long()].contiguous()
+    nm.rowoff = torch.arange(U * B * E, device=dev, dtype=torch.int32)
+    res["fused_rpc6_contiguous"] = timeit(lambda: nm.fused(Y, Lg.view(S, -1, cols), Pg.view(S, -1, cols), bg, (E, U, B), rpc_mult=2))
+    nm.rowoff = rowoff
+    # a pre-gather copy itself (torch index_select of both stores)
+    res["torch_pregather_copy"] = timeit(lambda: (torch.index_select(L.view(-1, cols), 0, rowoff.long(), out=Lg),
+                                                  torch.index_select(P.view(-1, cols), 0, rowoff.long(), out=Pg)))
     for k, v in res.items():
-        print(f"{k:16s} {v:7.1f} us")
+        print(f"{k:22s} {v:7.1f} us")
 
 
 if __name__ == "__main__":
