@@ -147,48 +147,32 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
   unsigned int cnt = 0;
   float wmax = 0.f;
   const long stride = (long)gridDim.x * blockDim.x * 4;
-  // one float4 chunk of every array: update + stores (the loads are issued by the caller)
-  auto upd4 = [&](long i0, float4 pp, float4 gg, float4 mm, float4 vv) {
-    float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gj = ga[j] * a.grad_scale;
-      if (a.prune_thr > 0.f && !(fabsf(gj) > a.prune_thr)) { gj = 0.f; ++cnt; }
-      float pj = pa[j];
-      if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
-      else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
-      ma[j] = a.beta1 * ma[j] + (1.f - a.beta1) * gj;
-      va[j] = a.beta2 * va[j] + (1.f - a.beta2) * gj * gj;
-      const float denom = sqrtf(va[j]) * rbc2 + a.eps;
-      pa[j] = pj - step_size * ma[j] / denom;
-      ga[j] = gj;
-    }
-    stv<NT>(p + i0, pp);
-    wmax = fmaxf(wmax, store_shadow(sh, i0, pp));
-    pack_scatter(ps, i0, &pp.x);
-    stv<NT>(m + i0, mm);
-    stv<NT>(v + i0, vv);
-    if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
-  };
-  long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  // UN chunks per thread per iteration, every load issued before the first update: 4 x UN x 16 B in
-  // flight per thread (one chunk per iteration left the grid's in-flight bytes latency-bound)
-  constexpr int UN = 4;
-  for (; i0 + (UN - 1) * stride + 3 < n; i0 += UN * stride) {
-    float4 pp[UN], gg[UN], mm[UN], vv[UN];
-#pragma unroll
-    for (int u = 0; u < UN; ++u) {
-      pp[u] = ldv<NT>(p + i0 + u * stride);
-      gg[u] = ldv<NT>(g + i0 + u * stride);
-      mm[u] = ldv<NT>(m + i0 + u * stride);
-      vv[u] = ldv<NT>(v + i0 + u * stride);
-    }
-#pragma unroll
-    for (int u = 0; u < UN; ++u) upd4(i0 + u * stride, pp[u], gg[u], mm[u], vv[u]);
-  }
-  for (; i0 < n; i0 += stride) {
+  for (long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < n; i0 += stride) {
     if (i0 + 3 < n) {
-      upd4(i0, ldv<NT>(p + i0), ldv<NT>(g + i0), ldv<NT>(m + i0), ldv<NT>(v + i0));
+      float4 pp = ldv<NT>(p + i0);
+      float4 gg = ldv<NT>(g + i0);
+      float4 mm = ldv<NT>(m + i0);
+      float4 vv = ldv<NT>(v + i0);
+      float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float gj = ga[j] * a.grad_scale;
+        if (a.prune_thr > 0.f && !(fabsf(gj) > a.prune_thr)) { gj = 0.f; ++cnt; }
+        float pj = pa[j];
+        if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
+        else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
+        ma[j] = a.beta1 * ma[j] + (1.f - a.beta1) * gj;
+        va[j] = a.beta2 * va[j] + (1.f - a.beta2) * gj * gj;
+        const float denom = sqrtf(va[j]) * rbc2 + a.eps;
+        pa[j] = pj - step_size * ma[j] / denom;
+        ga[j] = gj;
+      }
+      stv<NT>(p + i0, pp);
+      wmax = fmaxf(wmax, store_shadow(sh, i0, pp));
+      pack_scatter(ps, i0, &pp.x);
+      stv<NT>(m + i0, mm);
+      stv<NT>(v + i0, vv);
+      if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
     } else {
       for (long i = i0; i < n; ++i) {
         float gj = g[i] * a.grad_scale;

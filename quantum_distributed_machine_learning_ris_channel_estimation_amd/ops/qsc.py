@@ -66,8 +66,10 @@ class QSCStepHIP:
         if impl == "mfma":
             wf = nat.fn(nat.hip_lib(), "qd_qsc2_waves", [_i, _i])
             self.grid_fwd = -(-batch_total // wf(self.Ww, 0))      # one sample per wave
-            if os.environ.get("QDML_QSC_GRID_FWD"):   # (tuning knob: fewer workgroups, a grid-stride loop)
-                self.grid_fwd = min(self.grid_fwd, int(os.environ["QDML_QSC_GRID_FWD"]))
+            # at most 256 workgroups (grid-stride loop over the samples): the forward runs beside the HDCE
+            # conv forward and leaves it more CUs -- 1 % per step over one sample per wave (576 workgroups
+            # at 2304 samples) in 4 of 4 same-box rounds (profiles/r2_20_*); QDML_QSC_GRID_FWD overrides
+            self.grid_fwd = min(self.grid_fwd, int(os.environ.get("QDML_QSC_GRID_FWD", "256")))
             grid_bwd = int(os.environ.get("QDML_QSC_GRID_BWD", grid_bwd))   # (tuning knob)
             self.grid_bwd = min(-(-batch_total // wf(self.Ww, 1)), grid_bwd)
             self.p2 = torch.empty(batch_total, feat, **f32)        # pool-2 features (linear weight grad)
