@@ -524,6 +524,7 @@ int launch(const Args& a, hipStream_t st) {
 //   forward  KC x KC  : 0: 144 x 128, 4 waves (1 x 4), 4 stages      1: 192 x 128, 8 waves (2 x 4), 3 stages
 //   dgrad    KC x MC  : 0: 144 x 256, 4 waves (1 x 4), 3 stages      1: 144 x 128, 4 waves, 4 stages
 //   wgrad    MC x MC  : 0: 128 x 256, 4 waves (1 x 4), 3 stages      1: 128 x 256, 8 waves (2 x 4), 3 stages
+//   (the training step's wgrad runs cfg 1: measured faster in the step, profiles/r2_20_variants.md)
 using FwdA = Geo<9, 2, 1, 4, KC, KC, 4>;
 using FwdB = Geo<6, 2, 2, 4, KC, KC, 3>;
 using DgrA = Geo<9, 4, 1, 4, KC, MC, 3>;

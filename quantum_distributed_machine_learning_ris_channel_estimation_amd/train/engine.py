@@ -294,7 +294,9 @@ class HDCEStep:
         hg = {"1": "fwd,wgrad,dgrad", "all": "fwd,wgrad,dgrad", "0": "", "none": ""}.get(hg, hg)
         self.hand_gemm = set(x for x in hg.split(",") if x) if self.hip else set()
         assert self.hand_gemm <= {"fwd", "wgrad", "dgrad"}, self.hand_gemm
-        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,0,0").split(","))
+        # (wgrad cfg 1 = 128 x 256 tiles on 8 waves: 1.1-1.6 % per step over cfg 0 in 2 of 2 same-box rounds,
+        # profiles/r2_20_variants.md)
+        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,1,0").split(","))
         if self.hip:
             from ..ops.conv import ConvStackHIP
             # launch knobs (samples per wave / per wgrad workgroup / per BN-reduction workgroup / layer-1
