@@ -20,6 +20,7 @@ In data-parallel runs ``sums()`` + all-reduce + ``finalize()`` give the GLOBAL N
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -49,7 +50,9 @@ class StreamNMSE:
         self.coef = torch.zeros(n_streams, device=dev)
         self.skip = torch.zeros(1, device=dev, dtype=torch.float32)  # NaN guard flag (all-reduced in DP)
         self._rs_long = self.row_stream.long()
-        self.rpc_mult = 2   # fused path: rows per block = E * rpc_mult (scripts/probe_nmse.py)
+        # fused path: rows per block = E * rpc_mult (scripts/probe_nmse.py: 22.7 vs 24.2 us isolated at 4 vs 2;
+        # 0.7 % per step in 2 of 2 rounds, profiles/r2_20_variants.md; QDML_NMSE_RPC_MULT for sweeps)
+        self.rpc_mult = int(os.environ.get("QDML_NMSE_RPC_MULT", "4"))
         self.rowoff: Optional[torch.Tensor] = None
         # CSR list of each stream's rows (stable order) for the one-launch reduce + finalize
         self.order = torch.sort(self._rs_long, stable=True).indices.to(torch.int32)
