@@ -240,6 +240,10 @@ class FlagshipTrainer:
         mode = cfg.stream_mode
         if mode not in ("serial", "dag", "dagq", "dagi", "dagf", "qsc", "full"):
             raise ValueError(f"stream_mode {mode!r}")
+        if mode == "dagf":
+            import warnings
+            warnings.warn("stream_mode 'dagf' is a diagnosis mode: slower than 'dagq', and one graph replay of it "
+                          "crashed inside the HIP runtime (docs/CONCURRENCY.md); use 'dagq'")
         if mode in ("qsc", "full", "dagi"):
             import warnings
             warnings.warn(f"stream_mode {mode!r} runs the QSC and HDCE chains concurrently across step boundaries: "

@@ -72,7 +72,7 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k, phase):
     assert float(ref.hopt.step_t[0]) == 4.0 and bool((dag.hopt.step_t == 4.0).all())
 
 
-@pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1), ("dagf", False, 4)])
+@pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1)])
 def test_shipped_plans_bit_exact_over_12_steps(cuda, mode, split, k):
     """The plans bench.py / the DP path run -- dagq (QSC branch forked and joined every step, k steps per
     replay) and the 5-graph data-parallel plan -- reproduce the same plan run eagerly on one stream
