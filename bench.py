@@ -58,6 +58,8 @@ def main() -> int:
     ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
     ap.add_argument("--dp-plan", default="zero", choices=["zero", "allreduce"],
                     help="world > 1: ZeRO-1 FC optimizer (reduce-scatter / shard Adam / all-gather) or all-reduce")
+    ap.add_argument("--dp-one-graph", action="store_true",
+                    help="DP plan: capture the whole step, RCCL collectives included, in one HIP graph")
     ap.add_argument("--phase-steps", type=int, default=20,
                     help="N > 1: extra steps (after the timed region) timed per phase with HIP events; 0 = off")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
@@ -89,7 +91,7 @@ def main() -> int:
                          qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
                          hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
                          fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase, dp_plan=args.dp_plan,
-                         stream_priority=args.stream_priority)
+                         stream_priority=args.stream_priority, dp_one_graph=args.dp_one_graph)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
@@ -112,6 +114,7 @@ def main() -> int:
     n = ctx.world
     samples = tr.samples_per_step * n * args.steps
     value = samples / elapsed
+    dp = len(tr.graphs) == 5 or (args.dp_one_graph and (ctx.world > 1 or cfg.split_graphs))
     phases = tr.phase_times(args.phase_steps) if args.phase_steps > 0 and len(tr.graphs) == 5 else None
     if phases is not None:
         keys = sorted(phases)
@@ -148,7 +151,8 @@ def main() -> int:
                 "qsc_fork": args.qsc_fork,
                 "fc_adam_grid": args.fc_adam_grid,
                 "dp_qsc_phase": args.dp_qsc_phase,
-                "dp_plan": ("zero" if tr.zero else "allreduce") if len(tr.graphs) == 5 else None,
+                "dp_plan": ("zero" if tr.zero else "allreduce") if dp else None,
+                "dp_one_graph": bool(args.dp_one_graph and dp),
                 "dist_backend": ctx.backend,
                 "stream_priority": args.stream_priority,
                 "steps_per_graph": args.steps_per_graph if n == 1 else 1,

@@ -114,6 +114,10 @@ class FlagshipConfig:
     #                               the chain: the next conv forward reads those weights.  Measured no gain:
     #                               the bandwidth-bound Adam slows the next step's (latency-bound) gather
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
+    dp_one_graph: bool = False   # DP plan: capture the whole step -- its RCCL collectives included -- in ONE
+    #                              graph (the 5-graph plan launches the collectives between graph replays and
+    #                              pays a graph boundary at each; this one pays one per step but fences the
+    #                              FC update at the end of the step instead of overlapping the next gather)
     tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
     n_scenarios: int = 3
@@ -284,6 +288,8 @@ class FlagshipTrainer:
         self._qsc_joined = False
         self._join_rev = os.environ.get("QDML_JOIN_ORDER", "") == "rev"
         self._phases = None   # (phase_times) per-step dicts of HIP events
+        _af = os.environ.get("QDML_OG_AG_FIRST", "")   # (one-graph ZeRO plan) all-gather before gr: 1 / 0
+        self._og_ag_first = None if _af == "" else _af == "1"
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
 
@@ -323,6 +329,14 @@ class FlagshipTrainer:
             # five graphs around the gradient collectives (see _dp_run); one memory pool is safe: the
             # graphs that replay concurrently (gf on the fc stream beside gr / the next g1a on main)
             # allocate nothing
+            if cfg.dp_one_graph and graphs:
+                # the collectives are captured too: RCCL kernels become graph nodes on the PG's stream,
+                # ordered by the captured event edges exactly as the eager plan orders them
+                gs = [GraphedStep(lambda: self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf,
+                                                       self._dp_gr, fence=True), enabled=graphs,
+                                  capture_error_mode="thread_local")]
+                self._graph_sets[k] = gs
+                return gs
             pool = torch.cuda.graph_pool_handle() if graphs else None
             gs = [GraphedStep(f, enabled=graphs, pool=pool)
                   for f in (self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)]
@@ -563,8 +577,10 @@ class FlagshipTrainer:
         g1a()
         self._mark("g1a")
         main = torch.cuda.current_stream(self.ctx.device) if self.streams is not None else None
-        if main is not None:
-            main.wait_stream(self.streams["fc"])   # (the previous step's FC update, when not fenced)
+        if main is not None and not self.cfg.dp_one_graph:
+            # (the previous step's FC update, when not fenced; the one-graph plan always fences, and a
+            # capturing stream must not wait on an event recorded outside the capture)
+            main.wait_stream(self.streams["fc"])
         self._mark("fc_prev")
         g1b()
         self._mark("g1")
@@ -593,7 +609,11 @@ class FlagshipTrainer:
             self._mark("fc_ready", fc)
             gf()
             self._mark("gf", fc)
-            if zero:
+            if zero and self.cfg.dp_one_graph:
+                # (captured: a collective launched from a forked stream crashes hipStreamEndCapture --
+                # scripts/probe_rccl_capture.py -- so main launches the all-gather; see below)
+                pass
+            elif zero:
                 b.launch_all_gather("ag", self._fc_weights_lp())
                 b.wait(("ag",))
                 self._mark("ag", fc)
@@ -601,8 +621,20 @@ class FlagshipTrainer:
         # reads it; free under RCCL, whose in-order stream finished fc before small)
         b.wait(("small",) if zero else ("skip", "fc", "small"))
         self._mark("small_ready")
+        og_ag = zero and self.cfg.dp_one_graph
+        # the shadow all-gather from main once the shard is updated: before gr (it overlaps gr; the shard
+        # Adam is 1/world of the FC) or after it (world 1: the whole-FC Adam on fc overlaps gr instead)
+        ag_first = og_ag and (self.ctx.world > 1 if self._og_ag_first is None else self._og_ag_first)
+        if ag_first:
+            main.wait_stream(fc)
+            b.launch_all_gather("ag", self._fc_weights_lp())
         gr()
         self._mark("gr")
+        if og_ag:
+            if not ag_first:
+                main.wait_stream(fc)
+                b.launch_all_gather("ag", self._fc_weights_lp())
+            b.wait(("ag",))
         b.pending.clear()   # (every collective has been waited for by the stream that consumes it)
         if fence:
             main.wait_stream(fc)

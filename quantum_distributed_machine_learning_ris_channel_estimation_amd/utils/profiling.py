@@ -85,10 +85,13 @@ class GraphedStep:
     WARMUP = 3
 
     def __init__(self, fn: Callable[[], None], enabled: bool = True, warmup: Optional[int] = None, pool=None,
-                 capture_stream: Optional["torch.cuda.Stream"] = None):
+                 capture_stream: Optional["torch.cuda.Stream"] = None, capture_error_mode: str = "global"):
         """``capture_stream``: the stream the graph is captured on (e.g. a high-priority one, so the
         nodes of its chain keep that priority over side branches forked from lower-priority streams)."""
         self.capture_stream = capture_stream
+        # "thread_local" when the captured body launches RCCL collectives: the process group's
+        # watchdog thread polls the events of earlier collectives, which a "global" capture forbids
+        self.capture_error_mode = capture_error_mode
         self.fn = fn
         self.enabled = enabled and torch.cuda.is_available()
         self.warmup = self.WARMUP if warmup is None else warmup
@@ -105,7 +108,8 @@ class GraphedStep:
         g = torch.cuda.CUDAGraph()
         if self.capture_stream is not None:
             self.capture_stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, pool=self.pool, stream=self.capture_stream):
+        with torch.cuda.graph(g, pool=self.pool, stream=self.capture_stream,
+                              capture_error_mode=self.capture_error_mode):
             self.fn()
         self.graph = g
 

@@ -1,0 +1,47 @@
+"""DP plan captured as ONE graph (RCCL collectives inside it) == the 5-graph DP plan, bit for bit.
+
+    dp_one_graph.py OUT [zero|allreduce]
+
+Run with QDML_FORCE_DIST=1 at world 1 on one GPU (a real RCCL process group of one rank: the
+collectives are launched and captured exactly as at world N) or with N ranks.  Both plans train the
+same model on the same batches for 6 steps; weights, moments and the bf16 FC shadow must agree
+exactly (the graphs hold the same kernels in the same dependency order)."""
+import faulthandler
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import (  # noqa: E402
+    init_distributed, shutdown)
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (  # noqa: E402
+    FlagshipConfig, FlagshipTrainer)
+
+
+def run(ctx, plan, one, steps=6):
+    cfg = FlagshipConfig(n_qubits=8, batch=32, data_len=800, hip_graphs=True, dp_plan=plan,
+                         split_graphs=True, dp_one_graph=one)
+    tr = FlagshipTrainer(cfg, ctx)
+    tr.run(steps)
+    tr.sync_master()
+    torch.cuda.synchronize()
+    return len(tr.graphs), [t.cpu().clone() for t in tr.mutable_state()], tr.hloss.cpu().clone()
+
+
+def main(out, plan="zero"):
+    faulthandler.enable()
+    ctx = init_distributed("cuda")
+    n5, s5, l5 = run(ctx, plan, False)
+    print("five-graph plan done", flush=True)
+    n1, s1, l1 = run(ctx, plan, True)
+    print("one-graph plan done", flush=True)
+    same = [torch.equal(a, b) for a, b in zip(s5, s1)]
+    ok = ctx.distributed and n5 == 5 and n1 == 1 and all(same) and torch.equal(l5, l1) and bool(torch.isfinite(l1).all())
+    with open(f"{out}.{ctx.rank}", "w") as f:
+        f.write(f"{int(ok)} {n5} {n1} {''.join(str(int(x)) for x in same)} {l5.tolist()} {l1.tolist()}\n")
+    shutdown()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "zero")
