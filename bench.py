@@ -56,8 +56,13 @@ def main() -> int:
                          "its forward half beside the HDCE forward and its backward half beside the conv backward (3)")
     ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
     ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
-    ap.add_argument("--dp-plan", default="zero", choices=["zero", "allreduce"],
-                    help="world > 1: ZeRO-1 FC optimizer (reduce-scatter / shard Adam / all-gather) or all-reduce")
+    ap.add_argument("--dp-plan", default="auto", choices=["auto", "zero", "allreduce"],
+                    help="world > 1: ZeRO-1 FC optimizer (reduce-scatter / shard Adam / all-gather) or all-reduce; "
+                         "auto = allreduce with the one-graph step, zero with the 5-graph step")
+    ap.add_argument("--dp-graph", default="auto", choices=["auto", "one", "five"],
+                    help="world > 1: the DP step as one HIP graph with the RCCL collectives captured, or 5 graphs "
+                         "with the collectives launched between them; auto = one if every rank's capture "
+                         "pre-flight (parallel/capture_probe.py) succeeds, else five")
     ap.add_argument("--dp-one-graph", action="store_true",
                     help="DP plan: capture the whole step, RCCL collectives included, in one HIP graph")
     ap.add_argument("--phase-steps", type=int, default=20,
@@ -75,6 +80,23 @@ def main() -> int:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
 
+    capture_ok = None
+    one_graph = args.dp_one_graph or args.dp_graph == "one"
+    forced = world_env == 1 and os.environ.get("QDML_FORCE_DIST") == "1"   # (a one-rank RCCL group: rehearsal)
+    if args.dp_graph == "auto" and not args.dp_one_graph and (world_env > 1 or forced) and not args.no_graphs \
+            and os.environ.get("QDML_DIST_BACKEND", "nccl") == "nccl":
+        # (before this process touches the GPU: the probe runs in a child of every rank)
+        import torch
+        n_dev = torch.cuda.device_count()   # (no GPU initialisation on this image)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.capture_probe import preflight
+        capture_ok = preflight()
+        one_graph = capture_ok
+        if n_dev > 0 and torch._C._cuda_getDeviceCount() == 0:
+            print(f"error: {n_dev} GPU(s) visible before the capture pre-flight, none after", file=sys.stderr)
+            return 3
+    dp_plan = args.dp_plan if args.dp_plan != "auto" else ("allreduce" if one_graph else "zero")
+
     import torch
 
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import init_distributed, shutdown
@@ -90,8 +112,8 @@ def main() -> int:
                          split_graphs=args.split_graphs or ctx.forced, stream_mode=args.stream_mode,
                          qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
                          hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
-                         fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase, dp_plan=args.dp_plan,
-                         stream_priority=args.stream_priority, dp_one_graph=args.dp_one_graph)
+                         fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase, dp_plan=dp_plan,
+                         stream_priority=args.stream_priority, dp_one_graph=one_graph)
     tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
@@ -114,8 +136,8 @@ def main() -> int:
     n = ctx.world
     samples = tr.samples_per_step * n * args.steps
     value = samples / elapsed
-    dp = len(tr.graphs) == 5 or (args.dp_one_graph and (ctx.world > 1 or cfg.split_graphs))
-    phases = tr.phase_times(args.phase_steps) if args.phase_steps > 0 and len(tr.graphs) == 5 else None
+    dp = len(tr.graphs) == 5 or (one_graph and (ctx.world > 1 or cfg.split_graphs))
+    phases = tr.phase_times(args.phase_steps) if args.phase_steps > 0 and dp else None
     if phases is not None:
         keys = sorted(phases)
         phases = dict(zip(keys, (round(v, 4) for v in ctx.max_vector([phases[k] for k in keys]))))
@@ -152,10 +174,11 @@ def main() -> int:
                 "fc_adam_grid": args.fc_adam_grid,
                 "dp_qsc_phase": args.dp_qsc_phase,
                 "dp_plan": ("zero" if tr.zero else "allreduce") if dp else None,
-                "dp_one_graph": bool(args.dp_one_graph and dp),
+                "dp_graph": ("one" if one_graph else "five") if dp else None,
+                "capture_preflight": capture_ok,
                 "dist_backend": ctx.backend,
                 "stream_priority": args.stream_priority,
-                "steps_per_graph": args.steps_per_graph if n == 1 else 1,
+                "steps_per_graph": tr._k(),
                 "quantumnat": cfg.use_quantumnat,
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},

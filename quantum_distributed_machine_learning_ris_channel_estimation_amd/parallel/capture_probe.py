@@ -1,0 +1,107 @@
+"""Pre-flight check: do RCCL collectives survive HIP graph capture on THIS node, at THIS world size?
+
+The one-graph data-parallel plan (``FlagshipConfig.dp_one_graph``) captures the step's all-reduces
+into its HIP graph.  That path is measured bit-exact over a one-rank RCCL group
+(``tests/test_flagship_gpu.py::test_dp_one_graph_matches_five_graphs_over_rccl``), but a runtime that
+cannot capture a collective fails hard (a segfault in ``hipStreamEndCapture``,
+``scripts/probe_rccl_capture.py``), not with an exception.  So before a multi-rank run commits to it,
+every rank starts a CHILD process (the parent has not touched the GPU yet) that captures the plan's
+collective pattern -- two async all-reduces launched from the capturing stream, one waited for on a
+forked stream -- replays it and checks the sums.  The ranks then agree through a TCPStore: the plan is
+used only if every child succeeded, so all ranks make the same choice.
+
+    ok = preflight(timeout=120)   # call before anything touches the GPU; True on every rank or none
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import subprocess
+import sys
+import time
+
+
+def _child() -> int:
+    import torch
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    a = torch.full((1 << 20,), float(rank + 1), device=dev)
+    b = torch.full((4096,), 1.0, device=dev)
+    out = torch.empty_like(a)
+    side = torch.cuda.Stream(dev)
+
+    def body():
+        a.mul_(1.0)
+        w1 = dist.all_reduce(a, async_op=True)
+        w2 = dist.all_reduce(b, async_op=True)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            w1.wait()
+            out.copy_(a)
+        w2.wait()
+        torch.cuda.current_stream(dev).wait_stream(side)
+
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        body()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    g = torch.cuda.CUDAGraph()
+    a.fill_(float(rank + 1))
+    b.fill_(1.0)
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        body()
+    a.fill_(float(rank + 1))
+    b.fill_(1.0)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    tri = world * (world + 1) / 2
+    ok = bool((out == tri).all()) and bool((b == world).all())
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0 if ok else 3
+
+
+def preflight(timeout: float = 120.0, port_offset: int = 7) -> bool:
+    """Run the capture probe in a child of every rank and agree on the result (see module docstring).
+    Must be called before this process touches the GPU.  False on every rank if any rank's probe
+    failed, crashed or timed out."""
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    base = int(os.environ.get("MASTER_PORT", "29500"))
+    env = dict(os.environ, MASTER_ADDR=host, MASTER_PORT=str(base + port_offset))
+    # (under torchrun the env:// rendezvous would join the elastic agent's store at MASTER_PORT -- nobody
+    # serves the probe's port: the child hosts its own store instead)
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    t0 = time.time()
+    try:
+        p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--child"], env=env,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout, text=True)
+        rc = p.returncode
+        if rc != 0:
+            tail = [ln for ln in p.stderr.splitlines() if ln.strip() and "Cannot find the function" not in ln][-6:]
+            print(f"[capture preflight] rank {rank}: probe exit {rc}:\n  " + "\n  ".join(tail), file=sys.stderr, flush=True)
+    except subprocess.TimeoutExpired:
+        rc = 124
+    store = dist.TCPStore(host, base + port_offset + 1, world, rank == 0, timeout=datetime.timedelta(seconds=timeout + 60))
+    store.set(f"qdml_capture_ok_{rank}", "1" if rc == 0 else "0")
+    ok = all(store.get(f"qdml_capture_ok_{r}") == b"1" for r in range(world))
+    store.set(f"qdml_capture_done_{rank}", "1")   # (rank 0 hosts the store: it must outlive every read)
+    if rank == 0:
+        for r in range(world):
+            store.wait([f"qdml_capture_done_{r}"])
+    if rank == 0:
+        import torch
+        print(f"[capture preflight] world {world}: {'ok' if ok else f'FAILED (rank 0 rc={rc})'} "
+              f"in {time.time() - t0:.1f}s; devices visible after the probe: {torch._C._cuda_getDeviceCount()}",
+              file=sys.stderr, flush=True)
+    return ok
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "--child":
+    sys.exit(_child())

@@ -324,19 +324,22 @@ class FlagshipTrainer:
                 # one graph: gather, both forwards, NMSE, both backwards, the optimizers
                 gs = [GraphedStep(rep(self._step_body), enabled=graphs, capture_stream=self.capture_stream)]
         else:
+            if cfg.dp_one_graph and graphs:
+                # the collectives are captured too: RCCL kernels become graph nodes on the PG's stream,
+                # ordered by the captured event edges exactly as the eager plan orders them.  k steps per
+                # replay: step i's FC update (fc stream) overlaps step i + 1's gather + conv forward
+                def body():
+                    for i in range(k):
+                        self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr,
+                                     fence=i == k - 1, first=i == 0)
+                gs = [GraphedStep(body, enabled=graphs, capture_error_mode="thread_local")]
+                self._graph_sets[k] = gs
+                return gs
             if k != 1:
-                raise ValueError("multi-step graphs are a world-1 plan")
+                raise ValueError("multi-step graphs are a world-1 plan (and the one-graph DP plan's)")
             # five graphs around the gradient collectives (see _dp_run); one memory pool is safe: the
             # graphs that replay concurrently (gf on the fc stream beside gr / the next g1a on main)
             # allocate nothing
-            if cfg.dp_one_graph and graphs:
-                # the collectives are captured too: RCCL kernels become graph nodes on the PG's stream,
-                # ordered by the captured event edges exactly as the eager plan orders them
-                gs = [GraphedStep(lambda: self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf,
-                                                       self._dp_gr, fence=True), enabled=graphs,
-                                  capture_error_mode="thread_local")]
-                self._graph_sets[k] = gs
-                return gs
             pool = torch.cuda.graph_pool_handle() if graphs else None
             gs = [GraphedStep(f, enabled=graphs, pool=pool)
                   for f in (self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)]
@@ -560,7 +563,7 @@ class FlagshipTrainer:
             e.record(stream)
             self._phases[-1][name] = e
 
-    def _dp_run(self, g1a, g1b, g2, gf, gr, fence: bool = True) -> None:
+    def _dp_run(self, g1a, g1b, g2, gf, gr, fence: bool = True, first: bool = True) -> None:
         """The DP step around the collectives.  RCCL runs every collective of the process group on one
         stream, in launch order: fc gradient (all-reduce, or reduce-scatter in the ZeRO plan), small
         bucket, (ZeRO) the shadow all-gather.
@@ -577,7 +580,7 @@ class FlagshipTrainer:
         g1a()
         self._mark("g1a")
         main = torch.cuda.current_stream(self.ctx.device) if self.streams is not None else None
-        if main is not None and not self.cfg.dp_one_graph:
+        if main is not None and not (self.cfg.dp_one_graph and first):
             # (the previous step's FC update, when not fenced; the one-graph plan always fences, and a
             # capturing stream must not wait on an event recorded outside the capture)
             main.wait_stream(self.streams["fc"])
@@ -645,7 +648,14 @@ class FlagshipTrainer:
         each (diagnostic; GPU DP plan only, else None): g1 (forward + FC wgrad), g2 (FC dgrad + conv
         backward + QSC, hiding the FC collective), fc_exposed (FC collective time left after g2),
         small_exposed, fc_adam, all_gather (ZeRO), conv_qsc_adam, step."""
-        if self.ctx.device.type != "cuda" or len(self.graphs) != 5 or self.streams is None:
+        if self.ctx.device.type != "cuda" or self.streams is None:
+            return None
+        swap = self.cfg.dp_one_graph and len(self.graphs) == 1 and (self.ctx.world > 1 or self.cfg.split_graphs)
+        if swap:   # (one-graph plan: its phases are timed on the 5-graph plan, which has host-visible boundaries)
+            saved = (self._graph_sets, self.graphs)
+            self.cfg.dp_one_graph, self._graph_sets = False, {}
+            self.graphs = self._graphs_for(1)
+        if len(self.graphs) != 5:
             return None
         self._phases = []
         try:
@@ -654,6 +664,9 @@ class FlagshipTrainer:
             rows = self._phases
         finally:
             self._phases = None
+            if swap:
+                self.cfg.dp_one_graph = True
+                self._graph_sets, self.graphs = saved
         el = lambda r, a, b_: r[a].elapsed_time(r[b_])
         out = {"g1a": [], "fc_prev_wait": [], "g1": [], "g2": [], "fc_exposed": [], "small_exposed": [],
                "fc_adam": [], "all_gather": [], "conv_qsc_adam": [], "step": []}
@@ -822,7 +835,8 @@ class FlagshipTrainer:
         self._replay(1)
 
     def _k(self) -> int:
-        return max(1, self.cfg.steps_per_graph) if (self.ctx.world == 1 and not self.cfg.split_graphs) else 1
+        one = (self.ctx.world == 1 and not self.cfg.split_graphs) or (self.cfg.dp_one_graph and self._use_graphs)
+        return max(1, self.cfg.steps_per_graph) if one else 1
 
     def prepare(self, n: int) -> None:
         """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""

@@ -82,3 +82,17 @@ def test_bench_world_mismatch_is_an_error():
     rc, recs, err = _bench(["--gpus", "2"] + SMALL, env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert rc != 0 and not recs
     assert "WORLD_SIZE" in err
+
+
+def test_capture_preflight_ranks_agree_and_fall_back(tmp_path):
+    """bench.py's RCCL capture pre-flight (parallel/capture_probe.py): each rank's child probe fails here
+    (no GPU) and both ranks agree on False -- the 5-graph DP plan -- without touching a GPU themselves."""
+    import os
+    import sys
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.launch import launch
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = str(tmp_path / "pf")
+    rc = launch([sys.executable, os.path.join(here, "dist_scripts", "preflight_agree.py"), out], nproc=2,
+                extra_env={"OMP_NUM_THREADS": "1"})
+    assert rc == 0
+    assert [open(f"{out}.{r}").read().strip() for r in range(2)] == ["0", "0"]

@@ -131,17 +131,18 @@ def test_zero_plan_matches_allreduce_plan_on_gpu(tmp_path):
         assert ok == "1", (r, diff)
 
 
-@pytest.mark.parametrize("plan", ["zero", "allreduce"])
-def test_dp_one_graph_matches_five_graphs_over_rccl(tmp_path, plan):
+@pytest.mark.parametrize("plan,k", [("zero", 1), ("allreduce", 1), ("allreduce", 3)])
+def test_dp_one_graph_matches_five_graphs_over_rccl(tmp_path, plan, k):
     """The DP step captured as ONE graph with its RCCL collectives inside == the 5-graph DP plan (which
     launches the collectives between replays), bit for bit over 6 steps: a real RCCL process group of
-    one rank (QDML_FORCE_DIST=1), so the reduce-scatter / all-reduce / all-gather are captured."""
+    one rank (QDML_FORCE_DIST=1), so the reduce-scatter / all-reduce / all-gather are captured.  k = 3:
+    three steps per replay, each step's FC update overlapping the next step's conv forward."""
     import os
     import sys
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.launch import launch
     here = os.path.dirname(os.path.abspath(__file__))
     out = str(tmp_path / "og")
-    rc = launch([sys.executable, os.path.join(here, "dist_scripts", "dp_one_graph.py"), out, plan], nproc=1,
+    rc = launch([sys.executable, os.path.join(here, "dist_scripts", "dp_one_graph.py"), out, plan, str(k)], nproc=1,
                 extra_env={"OMP_NUM_THREADS": "2", "QDML_FORCE_DIST": "1"})
     assert rc == 0
     rec = open(f"{out}.0").read().split()
