@@ -202,7 +202,8 @@ class GradBuckets:
 
     def wait(self, names: Optional[Sequence[str]] = None) -> None:
         """Make the CURRENT stream wait for the named (default: all) launched collectives; a coalesced
-        bucket is scattered back (once) on the first stream that waits for it.  A bucket may be waited
+        bucket is scattered back (once) on the first stream that waits for it, and a later waiter on another
+        stream waits for that scatter-back (an event) -- not only for the collective.  A bucket may be waited
         for from several streams."""
         for k in list(self.pending) if names is None else [n for n in names if n in self.pending]:
             ent = self.pending[k]
@@ -213,6 +214,12 @@ class GradBuckets:
                 sizes = [t.numel() for t in ent[2]]
                 torch._foreach_copy_([t.view(-1) for t in ent[2]], list(ent[1][:sum(sizes)].split(sizes)))
                 ent[1] = None
+                if ent[2][0].is_cuda:   # later waiters on OTHER streams must wait for the scatter-back too
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    ent.append(ev)
+            elif len(ent) > 3:
+                torch.cuda.current_stream().wait_event(ent[3])
         if names is None:
             self.pending.clear()
 

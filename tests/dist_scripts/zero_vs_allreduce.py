@@ -41,15 +41,18 @@ def main(out, device="cpu"):
     ctx = init_distributed(device)
     za, fa, qa, sa, la = run(ctx, "allreduce", device)
     zz, fz, qz, sz, lz = run(ctx, "zero", device)
-    ok = (not za) and zz and torch.equal(fa, fz) and torch.equal(qa, qz) and torch.equal(la, lz)
+    checks = {"plans": (not za) and zz, "hdce": torch.equal(fa, fz), "qsc": torch.equal(qa, qz),
+              "loss": torch.equal(la, lz)}
     if sa is not None:
-        ok = ok and torch.equal(sa[:fa.numel() - (fa.numel() - sa.numel())], sz[:sa.numel()])
+        checks["shadow"] = torch.equal(sa[:fa.numel() - (fa.numel() - sa.numel())], sz[:sa.numel()])
     g = [torch.empty_like(fz) for _ in range(ctx.world)]
     dist.all_gather(g, fz)
-    ok = ok and all(torch.equal(g[0], x) for x in g[1:])   # every rank holds the same weights
+    checks["ranks"] = all(torch.equal(g[0], x) for x in g[1:])   # every rank holds the same weights
+    ok = all(checks.values())
     diff = float((fa - fz).abs().max())
+    failed = ",".join(k for k, v in checks.items() if not v) or "-"
     with open(f"{out}.{ctx.rank}", "w") as f:
-        f.write(f"{int(ok)} {diff}\n")
+        f.write(f"{int(ok)} {diff} {failed} qdiff={float((qa - qz).abs().max())} loss={la.tolist()}/{lz.tolist()}\n")
     shutdown()
 
 
