@@ -132,6 +132,9 @@ def shutdown() -> None:
     _CTX = None
 
 
+_FOREACH_ALWAYS = os.environ.get("QDML_BUCKET_FOREACH") == "1"   # (A/B: the single multi-tensor scatter-back)
+
+
 class GradBuckets:
     """Asynchronous all-reduce of named gradient buckets.
 
@@ -141,6 +144,8 @@ class GradBuckets:
     waits on it); ``wait()`` makes the current stream wait for all launched collectives and
     scatters coalesced results back -- no host synchronisation anywhere.
     """
+
+    FOREACH_MIN = 8   # members up to which a coalesced bucket is scattered back one copy launch per member
 
     def __init__(self, ctx: DistContext, buckets: Dict[str, Sequence[torch.Tensor]]):
         self.ctx = ctx
@@ -209,10 +214,17 @@ class GradBuckets:
             ent = self.pending[k]
             ent[0].wait()
             if ent[1] is not None:
-                # every member back from the staging buffer in ONE multi-tensor launch (the step's
-                # critical path waits on it: a launch per member cost ~5 us each)
+                # every member back from the staging buffer.  Few members: one copy launch each -- the
+                # multi-tensor launch gives each 64K-element chunk ONE workgroup, so the conv gradient
+                # member (~60K floats) was a single-workgroup copy of 40 us on the step's critical path
+                # (profiles/r2_23_dp_one_graph_world1_kernel_stats.md); many members: one launch
                 sizes = [t.numel() for t in ent[2]]
-                torch._foreach_copy_([t.view(-1) for t in ent[2]], list(ent[1][:sum(sizes)].split(sizes)))
+                parts = list(ent[1][:sum(sizes)].split(sizes))
+                if len(sizes) <= self.FOREACH_MIN and not _FOREACH_ALWAYS:
+                    for t, src in zip(ent[2], parts):
+                        t.view(-1).copy_(src)
+                else:
+                    torch._foreach_copy_([t.view(-1) for t in ent[2]], parts)
                 ent[1] = None
                 if ent[2][0].is_cuda:   # later waiters on OTHER streams must wait for the scatter-back too
                     ev = torch.cuda.Event()
