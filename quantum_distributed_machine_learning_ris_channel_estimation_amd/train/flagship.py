@@ -606,6 +606,12 @@ class FlagshipTrainer:
             gr()
             return
         fc = self.streams["fc"]
+        if zero:
+            # ZeRO: main takes the small bucket (collective + scatter-back) BEFORE forking the fc stream,
+            # which needs its HDCE NaN flag: one stream owns each scatter-back, and the fc stream inherits
+            # it through the fork (no second-waiter path across streams)
+            b.wait(("small",))
+            fc_wait = ("fc",)
         fc.wait_stream(main)
         with torch.cuda.stream(fc):
             b.wait(fc_wait)
