@@ -145,7 +145,11 @@ class GradBuckets:
     scatters coalesced results back -- no host synchronisation anywhere.
     """
 
-    FOREACH_MIN = 8   # members up to which a coalesced bucket is scattered back one copy launch per member
+    # members up to which a coalesced bucket is scattered back one copy launch per member.  0: always the
+    # single multi-tensor launch -- measured no slower in the step (it is off the critical path:
+    # world-1 RCCL one-graph 0.4677/0.4722 vs 0.4705/0.4709 ms, 5-graph 0.5673/0.5678 vs 0.5726/0.5727,
+    # profiles/r2_24_bucket_ab.txt)
+    FOREACH_MIN = 0
 
     def __init__(self, ctx: DistContext, buckets: Dict[str, Sequence[torch.Tensor]]):
         self.ctx = ctx
