@@ -93,14 +93,17 @@ def preflight(timeout: float = 120.0, port_offset: int = 7) -> bool:
                               timeout=datetime.timedelta(seconds=timeout + 60))
         store.set(f"qdml_capture_ok_{rank}", "1" if rc == 0 else "0")
         ok = all(store.get(f"qdml_capture_ok_{r}") == b"1" for r in range(world))
+    except Exception as e:   # (no agreement possible -- e.g. the port is taken: every rank ends up here)
+        print(f"[capture preflight] rank {rank}: store failed ({e}); using the 5-graph plan", file=sys.stderr,
+              flush=True)
+        return False
+    try:   # (after the decision: a failure here must not change it -- the other ranks already have theirs)
         store.set(f"qdml_capture_done_{rank}", "1")   # (rank 0 hosts the store: it must outlive every read)
         if rank == 0:
             for r in range(world):
                 store.wait([f"qdml_capture_done_{r}"])
-    except Exception as e:   # (no agreement possible -- e.g. the port is taken: every rank ends up here)
-        print(f"[capture preflight] rank {rank}: store failed ({e}); using the 5-graph plan", file=sys.stderr,
-              flush=True)
-        ok = False
+    except Exception:
+        pass
     if rank == 0:
         import torch
         print(f"[capture preflight] world {world}: {'ok' if ok else f'FAILED (rank 0 rc={rc})'} "
