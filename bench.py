@@ -20,8 +20,18 @@ The reference publishes no throughput, so vs_baseline is null.
 (one child process per GPU through parallel/launch.py, BEFORE this process imports torch or
 touches a GPU), relays rank 0's JSON line on stdout and exits non-zero if any rank fails.  Under
 torchrun, WORLD_SIZE must equal --gpus (a mismatch is an error, never a silent 1-rank run).
-At N > 1 the JSON line also carries ``phases_ms``: per-phase HIP-event times of the DP step
-(max over ranks), measured on extra steps AFTER the timed region.
+At N > 1:
+  * every rank is a SUPERVISOR that runs the benchmark in a child process (it never touches the GPU
+    itself).  If any rank's child fails (exit, crash, timeout) all supervisors stop their children
+    and start a second attempt with the 5-graph DP plan (``--dp-graph five``: no captured collectives);
+    the JSON line then carries ``dp_fallback`` with the reason.  Only a fully successful attempt's
+    JSON line is printed (rank 0's supervisor relays it), so stdout never holds two.
+  * the DP plan is CHOSEN AT THE REAL WORLD SIZE: with ``--dp-plan auto`` both plans (ZeRO-1 and
+    all-reduce) are built on the graph mode the capture pre-flight allows, each timed over
+    ``--select-steps`` steps after its warm-up (max over ranks), and the faster one is benchmarked;
+    ``plan_select_ms`` records both.
+  * ``phases_ms``: per-phase HIP-event times (max over ranks) on extra steps AFTER the timed region --
+    for the 5-graph plan only; the one-graph plan reports null (no host-visible phase boundaries).
 """
 from __future__ import annotations
 
@@ -67,6 +77,9 @@ def main() -> int:
                     help="DP plan: capture the whole step, RCCL collectives included, in one HIP graph")
     ap.add_argument("--phase-steps", type=int, default=20,
                     help="N > 1: extra steps (after the timed region) timed per phase with HIP events; 0 = off")
+    ap.add_argument("--select-steps", type=int, default=10,
+                    help="N > 1, --dp-plan auto: steps timed per candidate plan to choose the faster one (0 = no timing: "
+                         "allreduce with the one-graph step, zero with the 5-graph step)")
     ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
     ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "dagi", "dagf", "qsc", "full"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
@@ -79,7 +92,13 @@ def main() -> int:
     if world_env != args.gpus:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
         return 2
+    if world_env > 1 and os.environ.get("QDML_BENCH_WORKER") != "1":
+        return supervise(sys.argv[1:], args)
 
+    inj = os.environ.get("QDML_BENCH_FAIL_RANK")   # (fault injection for the supervisor tests)
+    if inj is not None and os.environ.get("RANK") == inj and not os.environ.get("QDML_DP_FALLBACK"):
+        print(f"[bench] rank {inj}: injected failure", file=sys.stderr, flush=True)
+        return 7
     capture_ok = None
     one_graph = args.dp_one_graph or args.dp_graph == "one"
     forced = world_env == 1 and os.environ.get("QDML_FORCE_DIST") == "1"   # (a one-rank RCCL group: rehearsal)
@@ -95,41 +114,77 @@ def main() -> int:
         if n_dev > 0 and torch._C._cuda_getDeviceCount() == 0:
             print(f"error: {n_dev} GPU(s) visible before the capture pre-flight, none after", file=sys.stderr)
             return 3
-    dp_plan = args.dp_plan if args.dp_plan != "auto" else ("allreduce" if one_graph else "zero")
-
     import torch
 
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import init_distributed, shutdown
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
                                                                                                 FlagshipTrainer)
 
-    ctx = init_distributed("auto")
+    ctx = init_distributed("auto", timeout_s=int(os.environ.get("QDML_PG_TIMEOUT", "600")))
     if ctx.world != args.gpus:
         print(f"error: --gpus {args.gpus} but the process group has {ctx.world} rank(s)", file=sys.stderr)
         return 2
-    cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch, data_len=args.data_len, dtype=args.dtype,
-                         hip_graphs=not args.no_graphs, use_quantumnat=not args.no_quantumnat,
-                         split_graphs=args.split_graphs or ctx.forced, stream_mode=args.stream_mode,
-                         qsc_first=args.qsc_first, steps_per_graph=args.steps_per_graph,
-                         hdce_branches=args.hdce_branches, qsc_fork=args.qsc_fork,
-                         fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase, dp_plan=dp_plan,
-                         stream_priority=args.stream_priority, dp_one_graph=one_graph)
-    tr = FlagshipTrainer(cfg, ctx)
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
+    def make(plan: str, og: bool, store=None) -> FlagshipTrainer:
+        cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch,
+                             data_len=args.data_len, dtype=args.dtype, hip_graphs=not args.no_graphs,
+                             use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
+                             stream_mode=args.stream_mode, qsc_first=args.qsc_first,
+                             steps_per_graph=args.steps_per_graph, hdce_branches=args.hdce_branches,
+                             qsc_fork=args.qsc_fork, fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase,
+                             dp_plan=plan, stream_priority=args.stream_priority, dp_one_graph=og)
+        return FlagshipTrainer(cfg, ctx, store=store)
+
+    def timed(tr: FlagshipTrainer, n: int):
+        """(seconds of n timed steps, max over ranks; host enqueue seconds)"""
+        tr.prepare(n)   # (graph capture, if the timed run needs a set the warm-up did not)
+        sync()
+        ctx.barrier()
+        sync()
+        t0 = time.perf_counter()
+        tr.run(n)
+        host = time.perf_counter() - t0   # host enqueue time (a launch-bound run shows it ~= wall)
+        sync()
+        ctx.barrier()
+        sync()
+        return ctx.max_scalar(time.perf_counter() - t0), host
+
+    # the DP plan: chosen at THIS world size by timing every candidate (ZeRO-1 vs all-reduce) on the graph
+    # mode the pre-flight allows; a user-fixed plan is a single candidate
+    dp_run = ctx.world > 1 or ctx.forced or args.split_graphs
+    if not dp_run:
+        cands = ["allreduce"]   # (world 1: the plan field is unused)
+    elif args.dp_plan != "auto":
+        cands = [args.dp_plan]
+    elif args.select_steps <= 0 or args.dtype == "fp8":   # (fp8: no ZeRO plan, see FlagshipTrainer)
+        cands = ["allreduce" if one_graph or args.dtype == "fp8" else "zero"]
+    else:
+        cands = ["allreduce", "zero"]
+    select = {}
+    tr, store = None, None
+    for plan in cands:
+        t = make(plan, one_graph, store)
+        store = t.store
+        if len(cands) > 1:
+            t.run(args.warmup)
+            el, _ = timed(t, args.select_steps)
+            select[plan] = round(el / args.select_steps * 1e3, 4)
+            if tr is None or select[plan] < select[tr_plan]:
+                if tr is not None:
+                    del tr
+                tr, tr_plan = t, plan
+            else:
+                del t
+        else:
+            tr, tr_plan = t, plan
+    cfg = tr.cfg
+    t = None
+    if len(cands) > 1 and ctx.device.type == "cuda":
+        torch.cuda.empty_cache()
+
     tr.run(args.warmup)
-    tr.prepare(args.steps)   # (graph capture, if the timed run needs a set the warm-up did not)
-    sync()
-    ctx.barrier()
-    sync()
-    t0 = time.perf_counter()
-    tr.run(args.steps)   # exactly args.steps training steps (steps_per_graph per graph replay)
-    host = time.perf_counter() - t0   # host enqueue time (a launch-bound run shows it ~= wall)
-    sync()
-    ctx.barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
-    elapsed = ctx.max_scalar(elapsed)
+    elapsed, host = timed(tr, args.steps)
 
     hl = tr.hloss.tolist()
     ql = float(tr.qloss.item())
@@ -137,8 +192,9 @@ def main() -> int:
     samples = tr.samples_per_step * n * args.steps
     value = samples / elapsed
     dp = len(tr.graphs) == 5 or (one_graph and (ctx.world > 1 or cfg.split_graphs))
-    phases = tr.phase_times(args.phase_steps) if args.phase_steps > 0 and dp else None
-    if phases is not None:
+    phases = None
+    if args.phase_steps > 0 and dp and len(tr.graphs) == 5:   # (the 5-graph plan only: see FlagshipTrainer.phase_times)
+        phases = tr.phase_times(args.phase_steps)
         keys = sorted(phases)
         phases = dict(zip(keys, (round(v, 4) for v in ctx.max_vector([phases[k] for k in keys]))))
     if ctx.is_main:
@@ -176,6 +232,7 @@ def main() -> int:
                 "dp_plan": ("zero" if tr.zero else "allreduce") if dp else None,
                 "dp_graph": ("one" if one_graph else "five") if dp else None,
                 "capture_preflight": capture_ok,
+                "plan_select_ms": select or None,
                 "dist_backend": ctx.backend,
                 "stream_priority": args.stream_priority,
                 "steps_per_graph": tr._k(),
@@ -183,11 +240,88 @@ def main() -> int:
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
         }
-        if phases is not None:
+        if dp:
             rec["phases_ms"] = phases
-        print(json.dumps(rec), flush=True)
+        fb = os.environ.get("QDML_DP_FALLBACK")
+        if ctx.world > 1:
+            rec["dp_fallback"] = fb or None
+        line = json.dumps(rec)
+        dest = os.environ.get("QDML_BENCH_JSON")
+        if dest:   # (supervised rank: the supervisor prints it once every rank has succeeded)
+            with open(dest, "w") as f:
+                f.write(line + "\n")
+        else:
+            print(line, flush=True)
     shutdown()
     return 0
+
+
+def supervise(argv, args) -> int:
+    """Run this rank's benchmark in a child process (this process never touches the GPU) and agree with
+    the other ranks' supervisors, through a TCPStore, on whether the attempt succeeded.  On any rank's
+    failure every supervisor stops its child and all start the fallback attempt (the 5-graph DP plan,
+    no captured collectives) on a fresh rendezvous port.  Children are started as new processes (never an
+    exec).  Rank 0 prints the successful attempt's JSON line; returns the exit code."""
+    import datetime
+    import signal
+    import subprocess
+    import tempfile
+
+    from torch.distributed import TCPStore   # (no GPU initialisation)
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    base = int(os.environ.get("MASTER_PORT", "29500"))
+    store = TCPStore(host, base + 11, world, rank == 0, timeout=datetime.timedelta(seconds=3600))
+    attempts = [(list(argv), None)]
+    if args.dp_graph != "five" or args.dp_one_graph:
+        fb = [a for a in argv if a != "--dp-one-graph"]
+        attempts.append((fb + ["--dp-graph", "five"], "first attempt failed on rank {r} (exit {rc}); 5-graph DP plan"))
+    limit = float(os.environ.get("QDML_BENCH_ATTEMPT_TIMEOUT", "900"))
+    json_path = os.path.join(tempfile.gettempdir(), f"qdml_bench_{os.getpid()}.json")
+    rc = 1
+    for i, (av, why) in enumerate(attempts):
+        env = dict(os.environ, QDML_BENCH_WORKER="1", MASTER_PORT=str(base + 20 + 10 * i), QDML_BENCH_JSON=json_path)
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # (the worker's process group hosts its own store)
+        if why:
+            env["QDML_DP_FALLBACK"] = why.format(r=fail_rank, rc=fail_rc)
+        if os.path.exists(json_path):
+            os.remove(json_path)
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + av, env=env, start_new_session=True)
+        key, t0, killed = f"qdml_bench_fail_{i}", time.time(), None
+        while True:
+            rc = p.poll()
+            if rc is not None:
+                break
+            if killed is None and (store.check([key]) or time.time() - t0 > limit):
+                if not store.check([key]):   # (this rank timed out: tell the others)
+                    store.set(key, f"{rank} 124")
+                os.killpg(p.pid, signal.SIGTERM)
+                killed = time.time()
+            elif killed is not None and time.time() - killed > 20:
+                os.killpg(p.pid, signal.SIGKILL)
+            time.sleep(0.2)
+        if rc != 0 and killed is None:
+            store.set(key, f"{rank} {rc}")
+        store.set(f"qdml_bench_rc_{i}_{rank}", str(rc))
+        rcs = [int(store.get(f"qdml_bench_rc_{i}_{r}")) for r in range(world)]   # (blocks until every rank is done)
+        if all(c == 0 for c in rcs):
+            if rank == 0:
+                with open(json_path) as f:
+                    sys.stdout.write(f.read())
+                sys.stdout.flush()
+            rc = 0
+            break
+        fail_rank, fail_rc = (store.get(key).decode().split() + ["?", "?"])[:2] if store.check([key]) else ("?", "?")
+        print(f"[bench supervisor] rank {rank}: attempt {i} failed (exit codes {rcs})", file=sys.stderr, flush=True)
+        rc = next(c for c in rcs if c != 0)
+    if os.path.exists(json_path):
+        os.remove(json_path)
+    # (rank 0 hosts the store: the others must be done with it first)
+    store.set(f"qdml_bench_exit_{rank}", "1")
+    if rank == 0:
+        store.wait([f"qdml_bench_exit_{r}" for r in range(world)])
+    return rc
 
 
 def self_launch(n: int) -> int:

@@ -82,12 +82,17 @@ struct NmseArgs {
 // values is K / 2 of them), so staging, LDS images and fragment reads are the bf16 ones unchanged; each
 // 16-byte fragment holds 16 k and feeds TWO mfma_f32_16x16x32_fp8_fp8 (its low and high 8 bytes).  The
 // k order this implies is the same permutation for A and B, so the dot products are exact sums over K.
-template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int DBG_ = 0, int F8_ = 0>
+// KS: waves along K inside the workgroup.  KS = 2 doubles the waves (2 per SIMD) without shrinking the
+// per-wave output tile: wave group wk computes sub-step wk (32 k) of every K step, the two partial tiles
+// are summed (in a fixed order) in the epilogue.  Each SIMD then interleaves two waves' MFMA, LDS-read,
+// glds-issue and barrier streams, and each wave issues half the staging pieces per K step.
+template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int DBG_ = 0, int F8_ = 0, int KS_ = 1>
 struct Geo {
   static constexpr int MF = MF_, NJ = NJ_, WM = WM_, WN = WN_, LA = LA_, LB = LB_, NSTAGE = NSTAGE_, DBG = DBG_;
-  static constexpr int F8 = F8_;
+  static constexpr int F8 = F8_, KS = KS_;
   static_assert(!F8 || (LA == KC && LB == KC), "e4m3 operands: k-contiguous layouts");
-  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static_assert(KS == 1 || KS == 2, "KS");
+  static constexpr int NW = WM * WN * KS, NT = 64 * NW;
   static constexpr int BM = 16 * MF * WM, BN = 16 * NJ * WN;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   static constexpr int PA = A_BYTES / 1024, PB = B_BYTES / 1024, P = PA + PB;   // 1-KiB pieces per tile
@@ -98,6 +103,7 @@ struct Geo {
   static_assert(LB == KC || BN % 128 == 0, "MC operand tiles are whole 128-column panels");
   static_assert(BN % 128 == 0, "epilogue rows are 2 or 4 columns per lane");
   static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(NSTAGE >= 3, "the refill of step t targets the stage read two steps earlier");
 };
 
 // source address of this lane's 16 bytes of 1-KiB piece q of operand X (tile rows r0.., k0..k0+63)
@@ -317,7 +323,8 @@ template <class G, int EPI, int GM, int GN>
 __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / G::WN, wn = wave % G::WN;
+  const int wk = wave / (G::WM * G::WN), wmn = wave % (G::WM * G::WN);   // (wk = 0 unless KS = 2)
+  const int wm = wmn / G::WN, wn = wmn % G::WN;
   const int tiles_i = a.I / G::BM, tiles_j = a.J / G::BN;
   int ti, tj;
   tile_of<GM, GN>(blockIdx.x, gridDim.x, tiles_i, tiles_j, ti, tj);
@@ -343,27 +350,56 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
   __builtin_amdgcn_s_barrier();
   Frags<G> f0, f1;
-  rd.read_b(f0, lds0, 0);
-  rd.read_a(f0, lds0, 0);
+  if constexpr (G::KS == 1) {
+    rd.read_b(f0, lds0, 0);
+    rd.read_a(f0, lds0, 0);
 
-  // Each K step t: MFMAs of sub-step 0 of tile t with sub-step 1's reads woven in; wait for tile t+1
-  // (counted vmcnt) + barrier; refill the stage tile t-1 used; MFMAs of sub-step 1 with tile t+1's
-  // sub-step-0 reads woven in.  Steady-state steps (refill always, a constant wait) form a loop with no
-  // branch inside; the last NS-1 steps are peeled (no refill, shrinking waits).
-  auto step = [&](int t, auto refill, int ahead) {
-    const uint32_t cur = lds0 + (t % NS) * G::STAGE, nxt = lds0 + ((t + 1) % NS) * G::STAGE;
-    rd.template mma_read<true>(acc, f0, f1, cur, 1);
-    if constexpr (G::DBG != 1) vm_wait<G>(ahead);
-    __builtin_amdgcn_s_barrier();
-    if constexpr (decltype(refill)::value && G::DBG != 1) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
-    __builtin_amdgcn_sched_barrier(0);
-    rd.template mma_read<true>(acc, f1, f0, nxt, 0);
-  };
-  int t = 0;
-  for (; t < nk - (NS - 1); ++t) step(t, std::true_type{}, NS - 3 < 0 ? 0 : NS - 3);
-  for (; t < nk - 1; ++t) step(t, std::false_type{}, nk - 2 - t);
-  rd.template mma_read<true>(acc, f0, f1, lds0 + (t % NS) * G::STAGE, 1);
-  rd.template mma_read<false>(acc, f1, f0, 0, 0);
+    // Each K step t: MFMAs of sub-step 0 of tile t with sub-step 1's reads woven in; wait for tile t+1
+    // (counted vmcnt) + barrier; refill the stage tile t-1 used; MFMAs of sub-step 1 with tile t+1's
+    // sub-step-0 reads woven in.  Steady-state steps (refill always, a constant wait) form a loop with no
+    // branch inside; the last NS-1 steps are peeled (no refill, shrinking waits).
+    auto step = [&](int t, auto refill, int ahead) {
+      const uint32_t cur = lds0 + (t % NS) * G::STAGE, nxt = lds0 + ((t + 1) % NS) * G::STAGE;
+      rd.template mma_read<true>(acc, f0, f1, cur, 1);
+      if constexpr (G::DBG != 1) vm_wait<G>(ahead);
+      __builtin_amdgcn_s_barrier();
+      if constexpr (decltype(refill)::value && G::DBG != 1) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
+      __builtin_amdgcn_sched_barrier(0);
+      rd.template mma_read<true>(acc, f1, f0, nxt, 0);
+    };
+    int t = 0;
+    for (; t < nk - (NS - 1); ++t) step(t, std::true_type{}, NS - 3 < 0 ? 0 : NS - 3);
+    for (; t < nk - 1; ++t) step(t, std::false_type{}, nk - 2 - t);
+    rd.template mma_read<true>(acc, f0, f1, lds0 + (t % NS) * G::STAGE, 1);
+    rd.template mma_read<false>(acc, f1, f0, 0, 0);
+  } else {
+    // KS = 2: this wave's sub-step sk of every tile.  Step t: wait for tile t+1 + barrier; refill the
+    // stage of tile t-1 (every wave finished reading it during step t-1); the MFMAs of tile t with tile
+    // t+1's fragments read in between.  Two steps per loop iteration keep the fragment sets static.
+    // (the wave's sub-step becomes sub-step 0 of its readers: a runtime index into base[] would put the
+    // readers in scratch -- guide §5.4 rule 20)
+    rd.ra.base[0] = wk ? rd.ra.base[1] : rd.ra.base[0];
+    rd.rb.base[0] = wk ? rd.rb.base[1] : rd.rb.base[0];
+    constexpr int sk = 0;
+    rd.read_b(f0, lds0, sk);
+    rd.read_a(f0, lds0, sk);
+    auto step = [&](int t, Frags<G>& cur, Frags<G>& nxt) __attribute__((always_inline)) {
+      const int ahead = nk - 2 - t < NS - 3 ? nk - 2 - t : NS - 3;
+      if constexpr (G::DBG != 1) vm_wait<G>(ahead);
+      __builtin_amdgcn_s_barrier();
+      if (G::DBG != 1 && t + NS - 1 < nk) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
+      __builtin_amdgcn_sched_barrier(0);
+      rd.template mma_read<true>(acc, cur, nxt, lds0 + ((t + 1) % NS) * G::STAGE, sk);
+    };
+    // (nk even: checked by the launcher)
+    int t = 0;
+    for (; t < nk - 2; t += 2) {
+      step(t, f0, f1);
+      step(t + 1, f1, f0);
+    }
+    step(t, f0, f1);
+    rd.template mma_read<false>(acc, f1, f0, 0, 0);
+  }
 
   // ---------------------------------------------------------------- epilogue
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -371,15 +407,24 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   float* ct = reinterpret_cast<float*>(smem);
   constexpr int PITCH = G::PITCH;
   const float dq = a.deq ? a.deq[0] * a.deq[1] : 1.f;
+  // (KS = 2: wave group 0 stores its partial tile, group 1 adds its own -- a fixed summation order)
 #pragma unroll
-  for (int j = 0; j < G::NJ; ++j) {
-    const int cl = (wn * G::NJ + j) * 16 + fr;
+  for (int kk = 0; kk < G::KS; ++kk) {
+    if (wk == kk) {
 #pragma unroll
-    for (int i = 0; i < G::MF; ++i)
+      for (int j = 0; j < G::NJ; ++j) {
+        const int cl = (wn * G::NJ + j) * 16 + fr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ct[((wm * G::MF + i) * 16 + fq * 4 + r) * PITCH + cl] = acc[i][j][r] * dq;
+        for (int i = 0; i < G::MF; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* c = &ct[((wm * G::MF + i) * 16 + fq * 4 + r) * PITCH + cl];
+            *c = kk == 0 ? acc[i][j][r] * dq : *c + acc[i][j][r] * dq;
+          }
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   constexpr int VEC = G::BN / 64;   // columns per lane in a row pass (2 or 4)
   const int c0 = VEC * lane;
   if constexpr (EPI == EPI_F32) {
@@ -440,7 +485,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     __syncthreads();
     float2* rsum = reinterpret_cast<float2*>(red + 64 + G::NW * 128);   // per-row (err^2, errperf^2)
     float cs0 = 0.f, cs1 = 0.f;
-    constexpr int RU = 12;                            // rows per batch (independent loads in flight)
+    constexpr int RU = G::BM % (G::NW * 12) == 0 ? 12 : G::BM % (G::NW * 9) == 0 ? 9 : 6;   // rows per batch
     static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
     for (int r0 = wave * RU; r0 < G::BM; r0 += G::NW * RU) {
       float2 l[RU], pv[RU];
@@ -509,6 +554,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
 template <class G, int EPI, int GM, int GN>
 int launch(const Args& a, hipStream_t st) {
   if (a.I % G::BM || a.J % G::BN || a.K % BK || a.K < BK) return (int)hipErrorInvalidValue;
+  if (G::KS == 2 && (a.K / BK) % 2) return (int)hipErrorInvalidValue;   // (the KS = 2 loop runs K steps in pairs)
   auto kern = &gemm_kernel<G, EPI, GM, GN>;
   static bool attr = false;
   if (!attr) {
@@ -532,6 +578,12 @@ using DgrB = Geo<9, 2, 1, 4, KC, MC, 4>;
 using WgrA = Geo<8, 4, 1, 4, MC, MC, 3>;
 using WgrB = Geo<4, 4, 2, 4, MC, MC, 3>;
 using FwdA8 = Geo<9, 2, 1, 4, KC, KC, 4, 0, 1>;   // e4m3 forward: the FwdA geometry, 128 k per stage
+// two waves per SIMD (round 3): the same output tiles, K split over two wave groups (KS = 2), or 8 waves
+// along N
+using FwdC = Geo<9, 2, 1, 4, KC, KC, 4, 0, 0, 2>;   // fwd 144 x 128, 8 waves (1 x 4 x K2)
+using DgrC = Geo<9, 2, 1, 8, KC, MC, 3>;            // dgrad 144 x 256, 8 waves (1 x 8)
+using DgrD = Geo<9, 4, 1, 4, KC, MC, 3, 0, 0, 2>;   // dgrad 144 x 256, 8 waves (1 x 4 x K2)
+using WgrC = Geo<8, 4, 1, 4, MC, MC, 3, 0, 0, 2>;   // wgrad 128 x 256, 8 waves (1 x 4 x K2)
 
 }  // namespace gemm
 }  // namespace qd
@@ -545,6 +597,7 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (K % BK || N % 128) return 0;
   if (cfg == 101 || cfg == 102) return M % FwdA::BM == 0;
   if (cfg == 0) return M % FwdA::BM == 0;
+  if (cfg == 2) return M % FwdC::BM == 0 && K % (2 * BK) == 0;
   if (cfg == 1) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
   return 0;
 }
@@ -558,6 +611,7 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
   if (M % FwdA::BM) return (int)hipErrorInvalidValue;
+  if (cfg == 2) return launch<FwdC, EPI_BF16, 4, 8>(a, st);
   if (cfg == 101) return launch<Geo<9, 2, 1, 4, KC, KC, 4, 1>, EPI_BF16, 4, 8>(a, st);   // (diagnosis builds)
   if (cfg == 102) return launch<Geo<9, 2, 1, 4, KC, KC, 4, 2>, EPI_BF16, 4, 8>(a, st);
   return launch<FwdA, EPI_BF16, 4, 8>(a, st);
@@ -578,6 +632,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   const int bm = cfg == 1 ? FwdB::BM : FwdA::BM;
   if (M % bm || (bm / (B * E) + 2) * E > 64 || B % 16 || bm % (16 * E)) return (int)hipErrorInvalidValue;
   if (cfg == 1) return launch<FwdB, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 2) return launch<FwdC, EPI_NMSE, 4, 8>(a, st);
   return launch<FwdA, EPI_NMSE, 4, 8>(a, st);
 }
 
@@ -587,6 +642,7 @@ QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M
   Args a{dY, A, N, K, N, K, M, dW, ldw, nullptr, {}, nullptr, 0, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<WgrB, EPI_F32, 2, 8>(a, st);
+  if (cfg == 2) return launch<WgrC, EPI_F32, 2, 8>(a, st);
   return launch<WgrA, EPI_F32, 2, 8>(a, st);
 }
 
@@ -596,6 +652,8 @@ QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, in
   Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}, nullptr, 0, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<DgrB, EPI_BF16, 4, 8>(a, st);
+  if (cfg == 2) return launch<DgrC, EPI_BF16, 4, 4>(a, st);
+  if (cfg == 3) return launch<DgrD, EPI_BF16, 4, 4>(a, st);
   return launch<DgrA, EPI_BF16, 4, 4>(a, st);
 }
 

@@ -7,8 +7,9 @@ cannot capture a collective fails hard (a segfault in ``hipStreamEndCapture``,
 ``scripts/probe_rccl_capture.py``), not with an exception.  So before a multi-rank run commits to it,
 every rank starts a CHILD process (the parent has not touched the GPU yet) that captures the plan's
 collective pattern -- two async all-reduces launched from the capturing stream, one waited for on a
-forked stream -- replays it and checks the sums.  The ranks then agree through a TCPStore: the plan is
-used only if every child succeeded, so all ranks make the same choice.
+forked stream, and the ZeRO plan's reduce-scatter + all-gather -- replays it and checks the sums.  The
+ranks then agree through a TCPStore: rank 0 publishes one decision (the plan is used only if every
+child succeeded) and every rank reads it; a rank that cannot read it exits non-zero.
 
     ok = preflight(timeout=120)   # call before anything touches the GPU; True on every rank or none
 """
@@ -31,18 +32,33 @@ def _child() -> int:
     a = torch.full((1 << 20,), float(rank + 1), device=dev)
     b = torch.full((4096,), 1.0, device=dev)
     out = torch.empty_like(a)
+    # the ZeRO one-graph plan's collectives too: reduce-scatter of a region, all-gather of the shards
+    full = torch.full((world * 8192,), float(rank + 1), device=dev)
+    shard = torch.empty(8192, device=dev)
+    gath = torch.empty(world * 8192, device=dev)
     side = torch.cuda.Stream(dev)
 
     def body():
         a.mul_(1.0)
         w1 = dist.all_reduce(a, async_op=True)
         w2 = dist.all_reduce(b, async_op=True)
+        w3 = dist.reduce_scatter_tensor(shard, full, async_op=True)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             w1.wait()
             out.copy_(a)
         w2.wait()
+        w3.wait()
+        w4 = dist.all_gather_into_tensor(gath, shard, async_op=True)
+        w4.wait()
         torch.cuda.current_stream(dev).wait_stream(side)
+
+    def reset():
+        a.fill_(float(rank + 1))
+        b.fill_(1.0)
+        full.fill_(float(rank + 1))
+        shard.zero_()
+        gath.zero_()
 
     s = torch.cuda.Stream(dev)
     s.wait_stream(torch.cuda.current_stream(dev))
@@ -51,16 +67,15 @@ def _child() -> int:
     torch.cuda.current_stream(dev).wait_stream(s)
     torch.cuda.synchronize(dev)
     g = torch.cuda.CUDAGraph()
-    a.fill_(float(rank + 1))
-    b.fill_(1.0)
+    reset()
     with torch.cuda.graph(g, capture_error_mode="thread_local"):
         body()
-    a.fill_(float(rank + 1))
-    b.fill_(1.0)
+    reset()
     g.replay()
     torch.cuda.synchronize(dev)
     tri = world * (world + 1) / 2
-    ok = bool((out == tri).all()) and bool((b == world).all())
+    ok = (bool((out == tri).all()) and bool((b == world).all()) and bool((shard == tri).all())
+          and bool((gath == tri).all()))
     dist.barrier()
     dist.destroy_process_group()
     return 0 if ok else 3
@@ -69,7 +84,7 @@ def _child() -> int:
 def preflight(timeout: float = 120.0, port_offset: int = 7) -> bool:
     """Run the capture probe in a child of every rank and agree on the result (see module docstring).
     Must be called before this process touches the GPU.  False on every rank if any rank's probe
-    failed, crashed or timed out."""
+    failed, crashed or timed out; SystemExit on a rank that cannot obtain the agreed decision."""
     import torch.distributed as dist
     rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
@@ -88,22 +103,24 @@ def preflight(timeout: float = 120.0, port_offset: int = 7) -> bool:
             print(f"[capture preflight] rank {rank}: probe exit {rc}:\n  " + "\n  ".join(tail), file=sys.stderr, flush=True)
     except subprocess.TimeoutExpired:
         rc = 124
+    # Agreement: every rank publishes its probe result; rank 0 alone decides and publishes ONE decision
+    # key that every rank reads.  A rank that cannot take part (store unreachable, a read that fails
+    # after the vote) exits non-zero instead of falling back to a default of its own: ranks running
+    # different plans would issue different collective sequences (a hang or silent corruption).
     try:
         store = dist.TCPStore(host, base + port_offset + 1, world, rank == 0,
                               timeout=datetime.timedelta(seconds=timeout + 60))
         store.set(f"qdml_capture_ok_{rank}", "1" if rc == 0 else "0")
-        ok = all(store.get(f"qdml_capture_ok_{r}") == b"1" for r in range(world))
-    except Exception as e:   # (no agreement possible -- e.g. the port is taken: every rank ends up here)
-        print(f"[capture preflight] rank {rank}: store failed ({e}); using the 5-graph plan", file=sys.stderr,
-              flush=True)
-        return False
-    try:   # (after the decision: a failure here must not change it -- the other ranks already have theirs)
+        if rank == 0:
+            ok = all(store.get(f"qdml_capture_ok_{r}") == b"1" for r in range(world))
+            store.set("qdml_capture_decision", "1" if ok else "0")
+        ok = store.get("qdml_capture_decision") == b"1"
         store.set(f"qdml_capture_done_{rank}", "1")   # (rank 0 hosts the store: it must outlive every read)
         if rank == 0:
             for r in range(world):
                 store.wait([f"qdml_capture_done_{r}"])
-    except Exception:
-        pass
+    except Exception as e:
+        raise SystemExit(f"[capture preflight] rank {rank}: no agreed decision ({e}); exiting") from e
     if rank == 0:
         import torch
         print(f"[capture preflight] world {world}: {'ok' if ok else f'FAILED (rank 0 rc={rc})'} "

@@ -83,6 +83,16 @@ class DistContext:
 _CTX: Optional[DistContext] = None
 
 
+def check_local_gpus(local_rank: int, local_world: int, n_gpus: int) -> None:
+    """RCCL needs one GPU per rank OF THIS NODE: the ranks of a node (LOCAL_WORLD_SIZE, torchrun's
+    per-node count) must fit its visible GPUs.  The global WORLD_SIZE is irrelevant -- a 2 x 8 job has
+    WORLD_SIZE 16 on 8-GPU nodes."""
+    if local_rank >= n_gpus or local_world > n_gpus:
+        raise RuntimeError(f"RCCL needs one GPU per rank: LOCAL_RANK={local_rank}, LOCAL_WORLD_SIZE={local_world} "
+                           f"but {n_gpus} visible GPU(s) on this node (QDML_DIST_BACKEND=gloo rehearses several "
+                           "ranks per GPU)")
+
+
 def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
     """Initialise from torchrun-style env vars; world 1 needs no process group."""
     global _CTX
@@ -103,9 +113,8 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
     forced = world == 1 and os.environ.get("QDML_FORCE_DIST") == "1"
     if world > 1 or forced:
         backend = os.environ.get("QDML_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
-        if backend == "nccl" and world > torch.cuda.device_count():
-            raise RuntimeError(f"RCCL needs one GPU per rank: WORLD_SIZE={world} but {torch.cuda.device_count()} "
-                               "visible GPU(s) (QDML_DIST_BACKEND=gloo rehearses several ranks per GPU)")
+        if backend == "nccl":
+            check_local_gpus(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)), torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if forced and "MASTER_PORT" not in os.environ:
             import socket

@@ -125,13 +125,16 @@ class FlagshipConfig:
 
 
 class FlagshipTrainer:
-    def __init__(self, cfg: FlagshipConfig, ctx: DistContext):
+    def __init__(self, cfg: FlagshipConfig, ctx: DistContext, store: Optional[DMLStore] = None):
+        """``store``: share another trainer's HBM-resident dataset (same data_len / pilots / SNR / seed)."""
         self.cfg, self.ctx = cfg, ctx
         dev = ctx.device
         self.tuned_gemms = dev.type == "cuda" and cfg.tunableop and use_tuned_gemms()
-        self.store, _ = make_dml_stores(cfg.data_len, cfg.pilot_num, cfg.snr_db, 0.9, dev, data_dir=None, synthetic=True,
-                                        base_seed=cfg.seed + 1000 * ctx.rank, n_scenarios=cfg.n_scenarios,
-                                        n_users=cfg.n_users)
+        if store is None:
+            store, _ = make_dml_stores(cfg.data_len, cfg.pilot_num, cfg.snr_db, 0.9, dev, data_dir=None, synthetic=True,
+                                       base_seed=cfg.seed + 1000 * ctx.rank, n_scenarios=cfg.n_scenarios,
+                                       n_users=cfg.n_users)
+        self.store = store
         self.E, self.U, self.B = cfg.n_scenarios, cfg.n_users, cfg.batch
         self.S = self.E * self.U
         # --- models (weights broadcast from rank 0 once; then resident)
@@ -651,17 +654,12 @@ class FlagshipTrainer:
 
     def phase_times(self, steps: int):
         """Run ``steps`` DP steps with HIP events around the phases and return the mean milliseconds of
-        each (diagnostic; GPU DP plan only, else None): g1 (forward + FC wgrad), g2 (FC dgrad + conv
+        each (diagnostic; the GPU 5-graph DP plan only): g1 (forward + FC wgrad), g2 (FC dgrad + conv
         backward + QSC, hiding the FC collective), fc_exposed (FC collective time left after g2),
-        small_exposed, fc_adam, all_gather (ZeRO), conv_qsc_adam, step."""
-        if self.ctx.device.type != "cuda" or self.streams is None:
-            return None
-        swap = self.cfg.dp_one_graph and len(self.graphs) == 1 and (self.ctx.world > 1 or self.cfg.split_graphs)
-        if swap:   # (one-graph plan: its phases are timed on the 5-graph plan, which has host-visible boundaries)
-            saved = (self._graph_sets, self.graphs)
-            self.cfg.dp_one_graph, self._graph_sets = False, {}
-            self.graphs = self._graphs_for(1)
-        if len(self.graphs) != 5:
+        small_exposed, fc_adam, all_gather (ZeRO), conv_qsc_adam, step.  None for every other plan -- in
+        particular the one-graph DP plan, whose phases have no host-visible boundaries (its whole-step
+        time is what bench.py measures; the phases of a different plan are never reported for it)."""
+        if self.ctx.device.type != "cuda" or self.streams is None or len(self.graphs) != 5:
             return None
         self._phases = []
         try:
@@ -670,9 +668,6 @@ class FlagshipTrainer:
             rows = self._phases
         finally:
             self._phases = None
-            if swap:
-                self.cfg.dp_one_graph = True
-                self._graph_sets, self.graphs = saved
         el = lambda r, a, b_: r[a].elapsed_time(r[b_])
         out = {"g1a": [], "fc_prev_wait": [], "g1": [], "g2": [], "fc_exposed": [], "small_exposed": [],
                "fc_adam": [], "all_gather": [], "conv_qsc_adam": [], "step": []}

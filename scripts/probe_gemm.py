@@ -41,14 +41,18 @@ def main():
         "fwd_hipblaslt": lambda: torch.nn.functional.linear(A, W, b),
         "fwd_hand0": lambda: gemm_fwd(A, W, b, out=Y, cfg=0),
         "fwd_hand1": lambda: gemm_fwd(A, W, b, out=Y, cfg=1),
+        "fwd_hand2_ks2": lambda: gemm_fwd(A, W, b, out=Y, cfg=2),
         "fwd_hand0_noload": lambda: gemm_fwd(A, W, b, out=Y, cfg=101),
         "fwd_hand0_nomfma": lambda: gemm_fwd(A, W, b, out=Y, cfg=102),
         "wgrad_hipblaslt": lambda: torch.mm(dY.t(), A, out_dtype=torch.float32, out=dW),
         "wgrad_hand0": lambda: gemm_wgrad(dY, A, out=dW, cfg=0),
         "wgrad_hand1": lambda: gemm_wgrad(dY, A, out=dW, cfg=1),
+        "wgrad_hand2_ks2": lambda: gemm_wgrad(dY, A, out=dW, cfg=2),
         "dgrad_hipblaslt": lambda: torch.mm(dY, W, out=dA),
         "dgrad_hand0": lambda: gemm_dgrad(dY, W, out=dA, cfg=0),
         "dgrad_hand1": lambda: gemm_dgrad(dY, W, out=dA, cfg=1),
+        "dgrad_hand2_1x8": lambda: gemm_dgrad(dY, W, out=dA, cfg=2),
+        "dgrad_hand3_ks2": lambda: gemm_dgrad(dY, W, out=dA, cfg=3),
     }
     res = {k: [] for k in var}
     for _ in range(5):

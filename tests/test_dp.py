@@ -75,7 +75,21 @@ def test_bench_self_launches_n_ranks():
     r = recs[0]
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2"
     assert r["config"]["global_batch"] == 2 * r["config"]["per_gpu_batch"]
-    assert r["config"]["dp_plan"] == "zero"
+    # the plan is chosen at the real world size by timing both candidates
+    sel = r["config"]["plan_select_ms"]
+    assert set(sel) == {"zero", "allreduce"} and r["config"]["dp_plan"] == min(sel, key=sel.get)
+    assert r["dp_fallback"] is None
+
+
+def test_bench_supervisor_falls_back_when_a_rank_fails():
+    """A rank that fails in the first attempt makes EVERY rank restart with the 5-graph plan; exactly one
+    JSON line (the successful attempt's) is printed, and it names the fallback."""
+    rc, recs, err = _bench(["--gpus", "2"] + SMALL + ["--phase-steps", "0", "--dp-plan", "allreduce"],
+                           env_extra={"QDML_BENCH_FAIL_RANK": "1"})
+    assert rc == 0, err[-2000:]
+    assert len(recs) == 1, recs
+    assert recs[0]["dp_fallback"] and "rank 1" in recs[0]["dp_fallback"], recs[0]
+    assert recs[0]["config"]["dp_graph"] == "five"
 
 
 def test_bench_world_mismatch_is_an_error():

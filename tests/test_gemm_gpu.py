@@ -14,8 +14,8 @@ def _rel(a, b):
     return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
-@pytest.mark.parametrize("M,N,K", [(576, 256, 192), (2304, 2048, 4096)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(576, 256, 192), (576, 256, 256), (2304, 2048, 4096)])
 def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     if not gemm_fwd_ok(M, N, K, cfg):
         pytest.skip("shape not tiled by this cfg")
@@ -36,9 +36,11 @@ def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     assert float(Y2[:, :5].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
-@pytest.mark.parametrize("M,N,K", [(192, 256, 512), (2304, 2048, 4096)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(192, 256, 512), (256, 256, 512), (2304, 2048, 4096)])
 def test_gemm_wgrad_matches_fp32(cuda, cfg, M, N, K):
+    if cfg == 2 and M % 128:
+        pytest.skip("cfg 2 (K split over two wave groups) runs the M reduction in pairs of 64")
     torch.manual_seed(1)
     dY = (torch.randn(M, N, device=cuda) * 1e-2).bfloat16()
     A = torch.randn(M, K, device=cuda).bfloat16()
@@ -57,11 +59,13 @@ def test_gemm_wgrad_matches_fp32(cuda, cfg, M, N, K):
     assert float(dW2[4:N - 1].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
-@pytest.mark.parametrize("M,N,K", [(288, 192, 256), (2304, 2048, 4096)])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(288, 192, 256), (288, 256, 256), (2304, 2048, 4096)])
 def test_gemm_dgrad_matches_fp32(cuda, cfg, M, N, K):
-    if cfg == 0 and K % 256:
-        pytest.skip("cfg 0 tiles K by 256")
+    if cfg in (0, 2, 3) and K % 256:
+        pytest.skip("cfg 0 / 2 / 3 tile K by 256")
+    if cfg == 3 and N % 128:
+        pytest.skip("cfg 3 (K split over two wave groups) runs the N reduction in pairs of 64")
     torch.manual_seed(2)
     dY = (torch.randn(M, N, device=cuda) * 1e-2).bfloat16()
     W = (torch.randn(N, K, device=cuda) * N ** -0.5).bfloat16()
@@ -93,8 +97,8 @@ def _rows(E, U, B, N_store, cols, device):
     return L, P, rowoff, rowden, lab, per, stream
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
-@pytest.mark.parametrize("E,U,B,N,K", [(3, 3, 64, 256, 320), (3, 3, 256, 2048, 4096)])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("E,U,B,N,K", [(3, 3, 64, 256, 320), (3, 3, 64, 256, 384), (3, 3, 256, 2048, 4096)])
 def test_gemm_nmse_epilogue_matches_fp32(cuda, cfg, E, U, B, N, K):
     """Forward GEMM with the HDCE loss epilogue + finish: loss, loss_perf, dY, bias gradient, NaN flag."""
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import gemm_tile_m
