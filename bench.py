@@ -60,12 +60,10 @@ def main() -> int:
     ap.add_argument("--steps-per-graph", type=int, default=5,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
     ap.add_argument("--hdce-branches", default="", help="(dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam")
-    ap.add_argument("--stream-priority", action="store_true", help="HDCE chain high priority, QSC branch low")
     ap.add_argument("--dp-qsc-phase", type=int, default=2, choices=[1, 2, 3],
                     help="DP plan: run the QSC beside the HDCE forward (1), beside the conv backward (2), or "
                          "its forward half beside the HDCE forward and its backward half beside the conv backward (3)")
     ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
-    ap.add_argument("--qsc-fork", default="gather", help="(dagq) HDCE forward stage the QSC branch forks at")
     ap.add_argument("--dp-plan", default="auto", choices=["auto", "zero", "allreduce"],
                     help="world > 1: ZeRO-1 FC optimizer (reduce-scatter / shard Adam / all-gather) or all-reduce; "
                          "auto = allreduce with the one-graph step, zero with the 5-graph step")
@@ -80,10 +78,13 @@ def main() -> int:
     ap.add_argument("--select-steps", type=int, default=10,
                     help="N > 1, --dp-plan auto: steps timed per candidate plan to choose the faster one (0 = no timing: "
                          "allreduce with the one-graph step, zero with the 5-graph step)")
-    ap.add_argument("--qsc-first", action="store_true", help="(qsc/full) enqueue the QSC graph first")
-    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq", "dagi", "dagf", "qsc", "full"],
-                    help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph, "
-                         "or a separate QSC graph on its own stream (+ HDCE side branches with 'full')")
+    ap.add_argument("--settle-steps", type=int, default=25,
+                    help="untimed steps replayed right before the timed region, after the warm-up and the graph "
+                         "capture (rounded up to whole graph replays): the first replays of a fresh graph run "
+                         "slower (profiles/r3_01_window.txt); reported in the JSON line")
+    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq"],
+                    help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph "
+                         "(QSC + HDCE side branches), or the QSC branch forked off the HDCE chain")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -130,15 +131,18 @@ def main() -> int:
         cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch,
                              data_len=args.data_len, dtype=args.dtype, hip_graphs=not args.no_graphs,
                              use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
-                             stream_mode=args.stream_mode, qsc_first=args.qsc_first,
-                             steps_per_graph=args.steps_per_graph, hdce_branches=args.hdce_branches,
-                             qsc_fork=args.qsc_fork, fc_adam_grid=args.fc_adam_grid, dp_qsc_phase=args.dp_qsc_phase,
-                             dp_plan=plan, stream_priority=args.stream_priority, dp_one_graph=og)
+                             stream_mode=args.stream_mode, steps_per_graph=args.steps_per_graph,
+                             hdce_branches=args.hdce_branches, fc_adam_grid=args.fc_adam_grid,
+                             dp_qsc_phase=args.dp_qsc_phase, dp_plan=plan, dp_one_graph=og)
         return FlagshipTrainer(cfg, ctx, store=store)
 
-    def timed(tr: FlagshipTrainer, n: int):
-        """(seconds of n timed steps, max over ranks; host enqueue seconds)"""
+    def timed(tr: FlagshipTrainer, n: int, settle: int = 0):
+        """(seconds of n timed steps, max over ranks; host enqueue seconds).  ``settle``: untimed steps
+        replayed first, after any capture (every rank runs the same count: they hold collectives)."""
         tr.prepare(n)   # (graph capture, if the timed run needs a set the warm-up did not)
+        if settle > 0:
+            k = tr._k()
+            tr.run((settle + k - 1) // k * k)
         sync()
         ctx.barrier()
         sync()
@@ -184,7 +188,9 @@ def main() -> int:
         torch.cuda.empty_cache()
 
     tr.run(args.warmup)
-    elapsed, host = timed(tr, args.steps)
+    k = tr._k()
+    settle = (max(0, args.settle_steps) + k - 1) // k * k
+    elapsed, host = timed(tr, args.steps, settle)
 
     hl = tr.hloss.tolist()
     ql = float(tr.qloss.item())
@@ -206,6 +212,7 @@ def main() -> int:
             "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": settle,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "host_ms_per_step": round(host / args.steps * 1e3, 4),
             "higher_is_better": True,
@@ -226,7 +233,6 @@ def main() -> int:
                 "graphs_per_step": len(tr.graphs),
                 "stream_mode": tr.mode,
                 "hdce_branches": "".join(sorted(tr.branches)),
-                "qsc_fork": args.qsc_fork,
                 "fc_adam_grid": args.fc_adam_grid,
                 "dp_qsc_phase": args.dp_qsc_phase,
                 "dp_plan": ("zero" if tr.zero else "allreduce") if dp else None,
@@ -234,7 +240,6 @@ def main() -> int:
                 "capture_preflight": capture_ok,
                 "plan_select_ms": select or None,
                 "dist_backend": ctx.backend,
-                "stream_priority": args.stream_priority,
                 "steps_per_graph": tr._k(),
                 "quantumnat": cfg.use_quantumnat,
             },

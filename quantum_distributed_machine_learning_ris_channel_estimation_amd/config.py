@@ -54,12 +54,18 @@ class RunnerConfig:
     synthetic: bool = True          # generate DeepMIMO-shaped data when .npy files are absent
     seed: int = 0
     dtype: str = "bf16"             # estimator compute dtype: fp32 | bf16
+    hdce_engine: str = "hip"        # HDCE training step: hip (fused kernels, bf16 MFMA) | torch (autograd; with
+    #                                 dtype fp32: an all-fp32 reference run of the same step, FIG1 attribution)
     device: str = "auto"            # auto | cuda | cpu
     backend: str = "auto"           # kernel backend: auto | hip | cpu | torch
     hip_graphs: bool = True
     overlap_comm: bool = True
     bucket_mb: float = 32.0
     world_size: int = 1
+    dp_semantics: str = "weak"      # N > 1: weak (every rank runs batch_size_DML per stream on its own data shard:
+    #                                 the benchmark's weak scaling) | reference (DataParallel's split: one global
+    #                                 batch of batch_size_DML per stream cut into world parts, global NMSE
+    #                                 denominators, per-replica BatchNorm -- R:144-148)
     log_jsonl: Optional[str] = None
     deterministic: bool = False
     nan_guard: bool = True

@@ -54,6 +54,11 @@ class StreamNMSE:
         # 0.7 % per step in 2 of 2 rounds, profiles/r2_20_variants.md; QDML_NMSE_RPC_MULT for sweeps)
         self.rpc_mult = int(os.environ.get("QDML_NMSE_RPC_MULT", "4"))
         self.rowoff: Optional[torch.Tensor] = None
+        # (S, 2) per-stream (label, perf) denominators of the GLOBAL batch, when this rank computes only part
+        # of it (data parallelism with the reference's DataParallel semantics): the loss becomes this
+        # rank's share sum_s num_s / den_global_s / S and the gradient coefficients 2 / (S den_global_s).
+        # CPU path: used by finalize; GPU one-pass path: the caller scales its per-row powers instead.
+        self.den_global: Optional[torch.Tensor] = None
         # CSR list of each stream's rows (stable order) for the one-launch reduce + finalize
         self.order = torch.sort(self._rs_long, stable=True).indices.to(torch.int32)
         cnt = torch.bincount(self._rs_long, minlength=n_streams)
@@ -125,9 +130,10 @@ class StreamNMSE:
                         loss_scale, nat.stream_ptr(self.ss.device)), "nmse_finalize")
         else:
             ss = self.ss
-            self.loss[0] = (ss[:, 0] / ss[:, 1]).sum() / self.S
-            self.loss[1] = (ss[:, 2] / ss[:, 3].clamp_min(1e-30)).sum() / self.S
-            self.coef.copy_(loss_scale * 2.0 / (self.S * ss[:, 1]))
+            den, denp = (ss[:, 1], ss[:, 3]) if self.den_global is None else (self.den_global[:, 0], self.den_global[:, 1])
+            self.loss[0] = (ss[:, 0] / den).sum() / self.S
+            self.loss[1] = (ss[:, 2] / denp.clamp_min(1e-30)).sum() / self.S
+            self.coef.copy_(loss_scale * 2.0 / (self.S * den))
             self.skip.fill_(0.0 if torch.isfinite(self.loss[0]) else 1.0)
         return self.loss
 

@@ -142,6 +142,9 @@ def shutdown() -> None:
 
 
 _FOREACH_ALWAYS = os.environ.get("QDML_BUCKET_FOREACH") == "1"   # (A/B: the single multi-tensor scatter-back)
+# (diagnosis of the gloo-on-one-GPU rehearsal, docs/CONCURRENCY.md: a host synchronisation of the waiting
+# stream after every gloo work.wait() -- separates gloo's device-copy completion semantics from our ordering)
+_GLOO_HOST_SYNC = os.environ.get("QDML_GLOO_HOST_SYNC") == "1"
 
 
 class GradBuckets:
@@ -226,6 +229,8 @@ class GradBuckets:
         for k in list(self.pending) if names is None else [n for n in names if n in self.pending]:
             ent = self.pending[k]
             ent[0].wait()
+            if _GLOO_HOST_SYNC and self.ctx.backend == "gloo" and torch.cuda.is_available():
+                torch.cuda.current_stream().synchronize()
             if ent[1] is not None:
                 # every member back from the staging buffer.  Few members: one copy launch each -- the
                 # multi-tensor launch gives each 64K-element chunk ONE workgroup, so the conv gradient

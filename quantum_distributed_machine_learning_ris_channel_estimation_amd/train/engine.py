@@ -286,17 +286,17 @@ class HDCEStep:
         self.defer_loss = True   # (with bias_via_conv_slabs) loss finish hosted by the conv backward
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; QDML_HAND_GEMM=0: hipBLASLt) and their
-        # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d")
-        # default: the hand-written weight-gradient GEMM; the forward (with the loss epilogue) and data-gradient
-        # kernels are exact and as fast in isolation (scripts/probe_gemm.py) but take whole CUs (140-160 KB of
-        # LDS), so beside the QSC branch the step measured 0.465 vs 0.440 ms with them (profiles/r2_*)
-        hg = os.environ.get("QDML_HAND_GEMM", "wgrad").strip()
+        # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d").  Default: the hand-written weight
+        # gradient (128 x 256 tiles, 8 waves) and data gradient (144 x 256 tiles, 8 waves along N: cfg 2) --
+        # in the step 0.4115 / 0.4116 vs 0.4180 / 0.4161 ms with the hipBLASLt data gradient (same box, 2
+        # rounds, profiles/r3_02_gemm_variants.txt).  The hand forward (with the loss epilogue; 8 waves as two
+        # K halves: cfg 2, 38.4 us isolated vs hipBLASLt 39.5) stays off: beside the concurrent QSC branch its
+        # whole-CU tiles and epilogue cost more than the separate loss pass (all-hand 0.4225-0.4238)
+        hg = os.environ.get("QDML_HAND_GEMM", "wgrad,dgrad").strip()
         hg = {"1": "fwd,wgrad,dgrad", "all": "fwd,wgrad,dgrad", "0": "", "none": ""}.get(hg, hg)
         self.hand_gemm = set(x for x in hg.split(",") if x) if self.hip else set()
         assert self.hand_gemm <= {"fwd", "wgrad", "dgrad"}, self.hand_gemm
-        # (wgrad cfg 1 = 128 x 256 tiles on 8 waves: 1.1-1.6 % per step over cfg 0 in 2 of 2 same-box rounds,
-        # profiles/r2_20_variants.md)
-        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,1,0").split(","))
+        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,1,2").split(","))
         if self.hip:
             from ..ops.conv import ConvStackHIP
             # launch knobs (samples per wave / per wgrad workgroup / per BN-reduction workgroup / layer-1
@@ -329,7 +329,18 @@ class HDCEStep:
         store through g.rowoff (no permuted label copies)."""
         self.nmse.rowoff = g.rowoff
         self._rowden = g.rowden if getattr(g, "rowpow", None) is not None else None
+        self._apply_den_global()
         return self._forward_fc(g.x1, store.Hlabel, store.Hperf)
+
+    def _apply_den_global(self) -> None:
+        """(DataParallel semantics) this rank holds part of each stream's batch: scale its per-row label
+        powers so that the one-pass NMSE kernels' per-stream sums ARE the global batch's denominators."""
+        dg = self.nmse.den_global
+        if dg is None or self._rowden is None:
+            return
+        rs = self.nmse._rs_long
+        loc = torch.zeros(self.nmse.S, 2, device=dg.device).index_add_(0, rs, self._rowden)
+        self._rowden.mul_((dg / loc.clamp_min(1e-30))[rs])
 
     # the same forward in two halves (HIP path; the DP plan replays them as separate graphs, so the FC
     # weights' update from the previous step -- an all-gather or the FC Adam -- overlaps the conv forward)
@@ -338,6 +349,7 @@ class HDCEStep:
         assert self.hip
         self.nmse.rowoff = g.rowoff
         self._rowden = g.rowden if getattr(g, "rowpow", None) is not None else None
+        self._apply_den_global()
         self.conv.stage_hook = self.stage_hook
         self._A_conv = self.conv.forward(g.x1, training=True)
         if self.stage_hook is not None:

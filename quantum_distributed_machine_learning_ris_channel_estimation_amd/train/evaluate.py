@@ -173,8 +173,16 @@ class model_val:
         """The HIP inference engine for these models (GPU; None on the CPU, or with QDML_EVAL_TORCH=1)."""
         if self.device.type != "cuda" or os.environ.get("QDML_EVAL_TORCH") == "1":
             return None
-        key = (id(sc), id(qsc), tuple(id(c) for c in convs), id(fc))
-        if getattr(self, "_eng_key", None) != key:
+        # the engine keeps COPIES of the weights: key it on the modules themselves (strong references, so a
+        # freed module's id can never be reused by a later model) and on the version counter of every
+        # parameter (an in-place update -- more training, a load_state_dict -- rebuilds it; BN statistics
+        # the sweep itself adapts are handed over by load_bn_stats)
+        mods = [m for m in (sc, qsc, *convs, fc) if m is not None]
+        ver = tuple(t._version for m in mods for t in m.parameters())
+        key = (tuple(mods), ver)
+        old = getattr(self, "_eng_key", None)
+        if old is None or len(old[0]) != len(key[0]) or any(a is not b for a, b in zip(old[0], key[0])) \
+                or old[1] != ver:
             from .infer import HIPInference
             self._eng = HIPInference(convs, fc, self.Pilot_num, self.device, sc=sc,
                                      qsc=qsc if (qsc is not None and qsc.use_quantum) else None)

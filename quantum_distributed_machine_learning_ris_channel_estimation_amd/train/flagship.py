@@ -11,8 +11,9 @@ Execution plan (world = 1, default ``stream_mode="dagq"``): one HIP graph replay
 ``steps_per_graph`` consecutive training steps (5 in bench), each captured from two streams: the
 QSC branch forks off the HDCE chain after the batch gather and joins it at the end of the step.
 Almost every kernel of this model is latency-bound and fills a fraction of the 256 CUs, so the
-QSC branch overlaps the HDCE chain.  (``dagi`` -- the two chains independent for the whole replay
--- was ~1.5% faster but not bit-reproducible; see ``__init__``.)  Per step:
+QSC branch overlaps the HDCE chain.  (Plans that let the two chains run independently across step
+boundaries were ~1.5% faster but not bit-reproducible on ROCm 7.x; they were measured and removed --
+docs/CONCURRENCY.md keeps the findings.)  Per step:
 
   main : gather -> conv fwd x3 -> BN/ReLU apply (+ BN tail) -> FC fwd GEMM -> one-pass NMSE ->
          FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce (+ loss finish) -> [wgrad|dgrad] L3 ->
@@ -22,9 +23,8 @@ QSC branch overlaps the HDCE chain.  (``dagi`` -- the two chains independent for
   qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
          QSC bwd -> slabs -> AdamW
 
-([wgrad|dgrad] = one launch running both independent gradients side by side.)  More side
-branches, later fork points, stream priorities and two concurrently replayed graphs were all
-measured and are kept as options (see ``__init__`` and README).
+([wgrad|dgrad] = one launch running both independent gradients side by side.)  ``dag`` adds HDCE
+side branches (FC weight gradient, conv weight gradients, FC Adam) on their own streams.
 
 The HDCE and the QSC have separate NaN-guard flags (``skip[0]``, ``skip[1]``), so neither
 optimizer waits for the other model's loss.
@@ -89,11 +89,9 @@ class FlagshipConfig:
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
     split_graphs: bool = False   # force the DP execution plan (5 graphs) even at world 1 (testing)
-    stream_mode: str = "dagq"    # serial | dag | dagq | dagi (| qsc | full: diagnosis only, see FlagshipTrainer.__init__)
-    qsc_first: bool = False      # (qsc / full) enqueue the QSC graph before the HDCE graph
-    hdce_branches: str = ""      # (dagq / qsc) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
+    stream_mode: str = "dagq"    # serial | dag | dagq (see FlagshipTrainer.__init__)
+    hdce_branches: str = ""      # (dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
-    stream_priority: bool = False  # capture the HDCE chain on a high-priority stream, the QSC branch low
     dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1), the conv backward (2),
     #                              or its forward half beside the HDCE forward and its backward half beside
     #                              the conv backward (3).  World-1 rehearsal: 0.492 / 0.517 / 0.557 ms;
@@ -103,16 +101,7 @@ class FlagshipConfig:
     dp_plan: str = "zero"        # world > 1: "zero" = ZeRO-1 FC optimizer (reduce-scatter the FC gradient,
     #                              Adam on this rank's 1/world shard, all-gather the bf16 weight shadow) or
     #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
-    qsc_fork: str = "gather"     # (dag / dagq) where the QSC branch forks: gather packed conv1..3 conv fc, or
-    #                              "split": its forward half beside the conv forward (joined before the FC
-    #                              GEMMs, which take whole CUs), its backward half + AdamW beside the conv
-    #                              backward (forked once the FC data gradient is issued)
-    qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 128 in dagi mode, else 256)
-    fc_adam_overlap: bool = False  # (world 1, dag / dagq) the FC part of the HDCE Adam runs on a side stream
-    #                               and overlaps the NEXT step's gather + conv forward (+ QSC); that step's FC
-    #                               GEMM waits for it.  The conv part (and the weight-image pack) stays on
-    #                               the chain: the next conv forward reads those weights.  Measured no gain:
-    #                               the bandwidth-bound Adam slows the next step's (latency-bound) gather
+    qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 256)
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     dp_one_graph: bool = False   # DP plan: capture the whole step -- its RCCL collectives included -- in ONE
     #                              graph (the 5-graph plan launches the collectives between graph replays and
@@ -166,8 +155,7 @@ class FlagshipTrainer:
         self.shard_len = (sp.numel - n_conv) // ctx.world
         if self.zero:
             self.hopt.partition([n_conv + i * self.shard_len for i in range(ctx.world)])
-        elif (dp or cfg.stream_mode in ("dag", "qsc", "full") or "a" in cfg.hdce_branches
-              or (cfg.fc_adam_overlap and cfg.stream_mode in ("dag", "dagq") and dev.type == "cuda")):
+        elif dp or cfg.stream_mode == "dag" or "a" in cfg.hdce_branches:
             self.hopt.partition([n_conv])
         if cfg.fc_adam_grid:
             self.hopt.max_grid[1 + (ctx.rank if self.zero else 0)] = cfg.fc_adam_grid
@@ -183,10 +171,7 @@ class FlagshipTrainer:
         self.qskip = self.skip[1, 0:1]
         self.hskip = sp.grad[sp.extra_off:sp.extra_off + 1] if self.flag_in_fc else self.skip[0, 0:1]
         self.hstep.nmse.skip = self.hskip
-        # QSC backward grid: off the critical path (dagi) fewer, longer-running workgroups interfere
-        # less with the HDCE chain (measured 0.4486 vs 0.4515 ms/step at 128 vs 256)
-        # (the DP plan runs the QSC inside a graph whose length it sets: there the full grid)
-        gb = cfg.qsc_grid_bwd or (128 if cfg.stream_mode == "dagi" and ctx.world == 1 and not cfg.split_graphs else 256)
+        gb = cfg.qsc_grid_bwd or 256   # (QSC backward workgroups: fewer measured slower, profiles/r2_20_variants.md)
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B,
                                     skip=self.qskip, hip_kw={"grid_bwd": gb})
         self.cstep.skip_add = False
@@ -222,85 +207,43 @@ class FlagshipTrainer:
         # side streams (GPU).  stream_mode:
         #   serial : one stream, one chain
         #   dag    : ONE graph captured from 4 streams (qsc / fc / conv branches forked off the main chain)
-        #   dagq   : ONE graph, only the QSC branch forked; the HDCE a single chain
-        #   dagi   : ONE graph, the HDCE and QSC chains independent within a replay (see _indep_body)
-        #   dagf   : as dagi, but the QSC chain of every step forks from that step's HDCE gather (a per-step
-        #            cross-queue edge, no per-step join): the step boundary (Adam -> gather -> conv1) stays on
-        #            the HDCE queue (profiles/r2_19_*)
-        #   !! dagi, qsc and full are kept for diagnosis only.  Whenever the QSC chain runs concurrently
-        #   with the HDCE chain ACROSS step boundaries (dagi with >= 2 steps per replay; two graphs
-        #   replayed concurrently in qsc / full) the QSC weights drift from the serial run by ~1e-5
-        #   after a few steps in most trials (scripts/dbg_dagi.py), although every QSC kernel is
-        #   bit-reproducible under concurrent load on its own (scripts/dbg_qsc_race.py) and the chains
-        #   share no buffer (cursors and NaN flags sit on separate cache lines).  Localised and bounded
-        #   in docs/CONCURRENCY.md: the simulator forward computes 1-3 samples from stale inputs although
-        #   its producer finished microseconds earlier; not the step-counter protocol, not a stray write.  dagq (QSC forked and
-        #   joined every step) and the serial graphs match the eager run bit for bit; dagi was ~1.5%
-        #   faster (profiles/r1_15_dagi_sweeps.md), not worth an unexplained non-reproducibility
-        #   qsc    : the QSC branch is its own graph replayed on its own stream; HDCE one serial graph
-        #   full   : as qsc, and the HDCE graph has its fc / conv side branches
-        #   !! qsc / full are kept for diagnosis only: on ROCm 7.x two graphs replayed CONCURRENTLY on two
-        #   streams gave wrong QSC gradients (each graph alone, or both serialised, or the same work as
-        #   branches of ONE graph are bit-exact; scripts/dbg_bisect.py qsc) -- use dag / dagq
-        # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge
-        # that crosses queues costs a barrier packet, so fewer, longer branches can win)
+        #   dagq   : ONE graph, only the QSC branch forked (after the gather, joined at the end of the step);
+        #            the HDCE a single chain
+        # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge that
+        # crosses queues costs a barrier packet, so fewer, longer branches win.  Plans whose QSC and HDCE
+        # chains ran concurrently ACROSS step boundaries -- independent chains in one graph, or two graphs
+        # replayed on two streams -- were 1-1.5% faster but not bit-reproducible on ROCm 7.x; removed in
+        # round 3, the bisection is in docs/CONCURRENCY.md)
         mode = cfg.stream_mode
-        if mode not in ("serial", "dag", "dagq", "dagi", "dagf", "qsc", "full"):
+        if mode not in ("serial", "dag", "dagq"):
             raise ValueError(f"stream_mode {mode!r}")
-        if mode == "dagf":
-            import warnings
-            warnings.warn("stream_mode 'dagf' is a diagnosis mode: slower than 'dagq', and one graph replay of it "
-                          "crashed inside the HIP runtime (docs/CONCURRENCY.md); use 'dagq'")
-        if mode in ("qsc", "full", "dagi"):
-            import warnings
-            warnings.warn(f"stream_mode {mode!r} runs the QSC and HDCE chains concurrently across step boundaries: "
-                          "not bit-reproducible on ROCm 7.x (see FlagshipTrainer.__init__); use 'dagq'")
         self.streams = None
-        self.capture_stream = None
         if dev.type == "cuda" and mode != "serial" and self.hstep.hip and self.cstep.hip is not None:
             self.streams = {k: torch.cuda.Stream(dev) for k in ("qsc", "fc", "conv")}
-            if cfg.stream_priority:
-                # the critical HDCE chain is captured on a high-priority stream, the QSC branch on a
-                # low-priority one (lower number = higher priority)
-                lo, hi = torch.cuda.Stream.priority_range()
-                self.capture_stream = torch.cuda.Stream(dev, priority=hi)
-                self.streams["qsc"] = torch.cuda.Stream(dev, priority=lo)
         else:
             mode = "serial"
         self.mode = mode
         # HDCE side branches: w = FC weight-gradient GEMM, c = conv weight-gradient kernels, a = FC Adam
-        self.branches = set("wca") if mode in ("dag", "full") else set(cfg.hdce_branches)
+        self.branches = set("wca") if mode == "dag" else set(cfg.hdce_branches)
         if self.streams is None:
             self.branches = set()
         self.hdce_side = "w" in self.branches
         if "a" in self.branches:   # (the FC Adam branch reads the bias gradient before the conv slabs run)
             self.hstep.bias_via_conv_slabs = False
-        # end-of-step weight pack (GPU fused path; the qsc / full diagnosis modes keep the forward pack)
-        self.tail_pack = bool(self.hstep.hip and cfg.tail_pack and mode not in ("qsc", "full"))
+        # end-of-step weight pack (GPU fused path)
+        self.tail_pack = bool(self.hstep.hip and cfg.tail_pack)
         if self.tail_pack:
             self.hstep.conv.pack_at_tail = True
             self._tail_pack_launch(advance=False)   # the first step's images
         self._use_graphs = graphs
-        # FC Adam overlapping the next step (see FlagshipConfig.fc_adam_overlap): pending on the fc stream
-        self.fc_overlap = bool(cfg.fc_adam_overlap and self.streams is not None and mode in ("dag", "dagq")
-                               and ctx.world == 1 and not cfg.split_graphs and not self.branches)
-        self._fc_pending = False
-        # where the QSC branch joins the HDCE chain in a dagq step: "end" (after the Adam), "adam" or "bwd"
-        self._qsc_join_at = os.environ.get("QDML_QSC_JOIN", "end")
-        assert self._qsc_join_at in ("end", "adam", "bwd"), self._qsc_join_at
-        self._qsc_joined = False
-        self._join_rev = os.environ.get("QDML_JOIN_ORDER", "") == "rev"
         self._phases = None   # (phase_times) per-step dicts of HIP events
-        _af = os.environ.get("QDML_OG_AG_FIRST", "")   # (one-graph ZeRO plan) all-gather before gr: 1 / 0
-        self._og_ag_first = None if _af == "" else _af == "1"
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
 
     def _graphs_for(self, k: int):
         """The graph set that runs ``k`` consecutive training steps per replay (world 1; the DP plan is
         always one step).  Every step of a replay gathers its own batch through the device cursor, so a
-        k-step replay IS k training steps -- the graph boundary (and, in qsc/full mode, the stream
-        fork/join) is paid once per k steps, and the QSC stream runs k steps beside the HDCE's k."""
+        k-step replay IS k training steps: the graph boundary is paid once per k steps."""
         if k in self._graph_sets:
             return self._graph_sets[k]
         graphs, cfg, mode = self._use_graphs, self.cfg, self.mode
@@ -309,23 +252,11 @@ class FlagshipTrainer:
             def body():
                 for _ in range(k):
                     fn()
-                if self._fc_pending:   # (a captured graph must rejoin every stream it forked)
-                    self._join(("fc",))
-                    self._fc_pending = False
             return body
 
         if self.ctx.world == 1 and not cfg.split_graphs:
-            if mode in ("qsc", "full"):
-                # (separate memory pools: the two graphs replay CONCURRENTLY, so a block one of them
-                # freed during capture must not be handed to the other)
-                gs = [GraphedStep(rep(self._qsc_graph), enabled=graphs),
-                      GraphedStep(rep(lambda: self._hdce_graph(gather=True)), enabled=graphs)]
-            elif mode in ("dagi", "dagf"):
-                gs = [GraphedStep(lambda: self._indep_body(k, fork_each=mode == "dagf"), enabled=graphs,
-                                  capture_stream=self.capture_stream)]
-            else:
-                # one graph: gather, both forwards, NMSE, both backwards, the optimizers
-                gs = [GraphedStep(rep(self._step_body), enabled=graphs, capture_stream=self.capture_stream)]
+            # one graph: gather, both forwards, NMSE, both backwards, the optimizers
+            gs = [GraphedStep(rep(self._step_body), enabled=graphs)]
         else:
             if cfg.dp_one_graph and graphs:
                 # the collectives are captured too: RCCL kernels become graph nodes on the PG's stream,
@@ -357,26 +288,7 @@ class FlagshipTrainer:
     def _join(self, names=("qsc", "fc", "conv")) -> None:
         cur = torch.cuda.current_stream(self.ctx.device)
         for n in names:
-            if n == "qsc" and self._qsc_joined:   # (already joined earlier in this step: no second edge)
-                self._qsc_joined = False
-                continue
             cur.wait_stream(self.streams[n])
-            if n == "qsc" and self._join_rev and self.mode in ("dag", "dagq"):
-                # the node after the join has parents on two queues: reverse their order so the graph
-                # executor keeps it (and the next step's chain) on the HDCE queue (csrc/hip/graph.hip)
-                import ctypes
-                f = nat.fn(nat.hip_lib(), "qd_capture_deps", [ctypes.c_void_p, ctypes.c_int])
-                rc = f(nat.stream_ptr(self.ctx.device), 1)
-                if rc < 0:
-                    raise RuntimeError(f"qd_capture_deps failed: hip error {-rc}")
-
-    def _early_join(self) -> None:
-        """(dagq) join the QSC branch into the HDCE chain before its backward / Adam instead of at the
-        end of the step (QDML_QSC_JOIN=bwd|adam): the branch has long finished by then, and the next
-        step's gather then follows the HDCE Adam on the same queue."""
-        if self.mode in ("dag", "dagq") and self.cfg.qsc_fork == "gather" and not self._qsc_joined:
-            self._join(("qsc",))
-            self._qsc_joined = True
 
     def _gather(self, hdce: bool = True, classifier: bool = True) -> None:
         # the fused GPU kernels WRITE every gradient (one producer per element): no zero_grad fills
@@ -421,10 +333,6 @@ class FlagshipTrainer:
         if with_opt:
             self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.qskip)
 
-    def _qsc_graph(self) -> None:
-        self._gather(hdce=False, classifier=True)
-        self._qsc_branch(with_opt=True)
-
     def _hdce_forward(self, side: Optional[bool] = None) -> None:
         side = self.hdce_side if side is None else side
         self.hstep.fc_side = self.streams["fc"] if side else None
@@ -438,8 +346,6 @@ class FlagshipTrainer:
             self._gather(hdce=True, classifier=False)
         self._hdce_forward()
         br = self.branches
-        if self._qsc_join_at == "bwd":
-            self._early_join()
         if "a" in br:
             # FC Adam once the dgrad GEMM (which reads the bf16 weight shadow it rewrites) is queued
             with self._fork(self.streams["fc"]):
@@ -453,20 +359,7 @@ class FlagshipTrainer:
         else:
             if self.hdce_side:
                 self._join(("fc",))
-            if self.fc_overlap:
-                # conv part (+ the next step's weight images and batch cursor) on the chain; the FC part on
-                # the fc stream, overlapping the next step up to its FC forward (see _fc_wait)
-                pk = self._adam_pack()
-                self.hopt.step(grad_scale=1.0, skip=self.hskip, part=0, pack=pk)
-                if self.tail_pack and pk is None:
-                    self._tail_pack_launch()
-                with self._fork(self.streams["fc"]):
-                    self.hopt.step(grad_scale=1.0, skip=self.hskip, part=1)
-                self._fc_pending = True
-                return
             if len(self.hopt.bounds) == 1:
-                if self._qsc_join_at == "adam":
-                    self._early_join()
                 pk = self._adam_pack()
                 self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
                 if self.tail_pack and pk is None:
@@ -636,7 +529,7 @@ class FlagshipTrainer:
         og_ag = zero and self.cfg.dp_one_graph
         # the shadow all-gather from main once the shard is updated: before gr (it overlaps gr; the shard
         # Adam is 1/world of the FC) or after it (world 1: the whole-FC Adam on fc overlaps gr instead)
-        ag_first = og_ag and (self.ctx.world > 1 if self._og_ag_first is None else self._og_ag_first)
+        ag_first = og_ag and self.ctx.world > 1
         if ag_first:
             main.wait_stream(fc)
             b.launch_all_gather("ag", self._fc_weights_lp())
@@ -685,82 +578,17 @@ class FlagshipTrainer:
             out["step"].append(r["start"].elapsed_time(rows[i + 1]["start"]) if i + 1 < len(rows) else el(r, "start", "end"))
         return {k: sum(v) / len(v) for k, v in out.items()}
 
-    def _fc_wait(self) -> None:
-        """Before the FC forward: the previous step's FC Adam (fc_overlap) must have rewritten the weights."""
-        if self._fc_pending:
-            self._join(("fc",))
-            self._fc_pending = False
-
     def _step_body(self) -> None:
-        if self.mode in ("dag", "dagq") and self.cfg.qsc_fork == "split" and self.cstep.hip is not None:
-            self._gather()
-            q = self.streams["qsc"]
-            with self._fork(q):
-                self._qsc_branch(with_opt=False, part="fwd")
-
-            def hook(stage: str) -> None:
-                if stage == "fc_pre":      # the FC GEMMs need whole CUs: the QSC forward half is done by now
-                    self._fc_wait()
-                    self._join(("qsc",))
-                elif stage == "dgrad":     # the QSC backward half beside the conv backward
-                    with self._fork(q):
-                        self._qsc_branch(with_opt=True, part="bwd")
-
-            self.hstep.stage_hook = hook
-            try:
-                self._hdce_graph()
-            finally:
-                self.hstep.stage_hook = None
-            self._join(("qsc",))
-            return
         if self.mode in ("dag", "dagq"):
+            # the QSC branch forks right after the batch gather: its latency-bound kernels share the GPU with
+            # the HDCE chain's, and it joins at the end of the step
             self._gather()
-            # the QSC branch forks at a chosen point of the HDCE forward (cfg.qsc_fork): its latency-
-            # bound kernels then share the GPU with the later, larger HDCE kernels
-            forked = []
-
-            def fork_qsc(stage: str) -> None:
-                if stage == "fc_pre":
-                    self._fc_wait()
-                if not forked and stage == self.cfg.qsc_fork:
-                    forked.append(True)
-                    with self._fork(self.streams["qsc"]):
-                        self._qsc_branch(with_opt=True)
-
-            fork_qsc("gather")
-            self.hstep.stage_hook = fork_qsc
-            try:
-                self._hdce_graph()
-            finally:
-                self.hstep.stage_hook = None
-            fork_qsc(self.cfg.qsc_fork)   # (a stage the forward does not have: fork at its end)
+            with self._fork(self.streams["qsc"]):
+                self._qsc_branch(with_opt=True)
+            self._hdce_graph()
             self._join(("qsc",))
             return
         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)
-
-    def _indep_body(self, k: int, fork_each: bool = False) -> None:
-        """(dagi) ``k`` steps as TWO independent chains of one graph: the HDCE chain on the capturing
-        stream, the QSC chain (each step with its own batch gather, cursor ``cur[1]``) on the qsc stream.
-        The chains meet only at the replay's head and tail -- no per-step fork / join edges, which the
-        HIP graph executor pays as cross-queue barrier packets (~10 us each).  Both chains read the
-        same perm with cursors advanced by B per step, so step i of either model sees the same batch."""
-        # CAPTURE ORDER MATTERS (measured, ROCm 7.x graph executor): each step's QSC chain is captured
-        # right after the gather it forks from, BEFORE the HDCE chain.  Captured the other way round
-        # (HDCE chain first, QSC after it, same edges) the replayed QSC chain read stale inputs -- QSC
-        # weights differed from the serial run in 6 of 6 trials (scripts/dbg_dagi.py); this order, and
-        # dagq's per-step fork, matched in every trial
-        main = torch.cuda.current_stream(self.ctx.device)
-        q = self.streams["qsc"]
-        for i in range(k):
-            self._gather(hdce=True, classifier=False)
-            if i == 0 or fork_each:   # (a node on the capturing stream first: a branch forked before it is a ROOT)
-                # dagf: the QSC chain of step i forks from the HDCE chain's gather of step i (no per-step join:
-                # nothing in the HDCE chain waits for the QSC branch, so the step boundary stays on one queue)
-                q.wait_stream(main)
-            with torch.cuda.stream(q):
-                self._qsc_graph()
-            self._hdce_graph()
-        self._join(("qsc",))
 
     def skip_flags(self) -> torch.Tensor:
         """(2,) the HDCE and QSC NaN-guard flags of the last step (after the all-reduce: summed)."""
@@ -797,16 +625,9 @@ class FlagshipTrainer:
             raise ValueError(f"{k} steps per graph need more than the {self.store.n} samples per stream")
         cur = self.cur.clone()
         saved = [t.clone() for t in self.mutable_state()] if preserve else None
-        main = torch.cuda.current_stream(self.ctx.device)
-        for i, g in enumerate(gs):
+        for g in gs:
             if g.enabled and g.graph is None:
-                if len(gs) == 2 and i == 0:   # the QSC graph lives on its stream
-                    self.streams["qsc"].wait_stream(main)
-                    with torch.cuda.stream(self.streams["qsc"]):
-                        g.capture()
-                    main.wait_stream(self.streams["qsc"])
-                else:
-                    g.capture()
+                g.capture()
         if saved is not None:
             for t, c in zip(self.mutable_state(), saved):
                 t.copy_(c)
@@ -863,32 +684,6 @@ class FlagshipTrainer:
         self.next_batch(k)
         if len(gs) == 1:
             gs[0]()
-            return
-        if len(gs) == 2:
-            # world 1, qsc / full: the QSC graph on its own stream beside the HDCE graph (each gathers
-            # its own inputs); the HDCE graph (the critical path) is enqueued first unless qsc_first
-            gq, gh = gs
-            q = self.streams["qsc"]
-            q.wait_stream(torch.cuda.current_stream(self.ctx.device))
-            dbg = os.environ.get("QDML_DBG_QSC", "")
-            if dbg:   # (debug: "main" = both graphs on the main stream; "nohdce" = QSC graph only)
-                if dbg == "main":
-                    gh()
-                    gq()
-                else:
-                    with torch.cuda.stream(q):
-                        gq()
-                    self._join(("qsc",))
-                return
-            if self.cfg.qsc_first:
-                with torch.cuda.stream(q):
-                    gq()
-                gh()
-            else:
-                gh()
-                with torch.cuda.stream(q):
-                    gq()
-            self._join(("qsc",))
             return
         self._dp_run(*gs, fence=fence)
 

@@ -72,6 +72,16 @@ class HIPInference:
         self._plane = plane
 
     @torch.no_grad()
+    def refresh(self, convs: Sequence[nn.Module], fc: nn.Module) -> None:
+        """Reload the estimator weights and BN statistics (e.g. once per epoch of a training run: the
+        engine's buffers and static launch shapes are kept, the conv weights are re-packed by every forward)."""
+        for e in range(self.E):
+            self.model.convs[e].load_state_dict(convs[e].state_dict())
+        self.model.fc.load_state_dict(fc.state_dict())
+        self.W_lp.copy_(self.model.fc_w.detach())
+        self.b_lp.copy_(self.model.fc_b.detach())
+
+    @torch.no_grad()
     def load_bn_stats(self, convs: Sequence[nn.Module]) -> None:
         """Refresh the experts' BN running statistics (views into the grouped buffers the conv kernels
         read) from ``convs``, e.g. after a test-time BN re-estimation."""

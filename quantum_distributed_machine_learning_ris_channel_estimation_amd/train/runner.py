@@ -143,12 +143,26 @@ class Y2HRunner:
             tr, va = make_dml_stores(self.data_len, self.Pilot_num, self.SNRdb, self.train_test_ratio, ctx.device,
                                      self.data_dir, self.synthetic, self.seed, self.n_scenarios, self.n_users)
             if ctx.world > 1:
-                tr = tr.shard(ctx.rank, ctx.world)
+                if not self._dp_reference():   # (reference semantics: every rank slices the same global batches)
+                    tr = tr.shard(ctx.rank, ctx.world)
                 va = va.shard(ctx.rank, ctx.world, drop_remainder=False)   # (metrics are global sums)
             self._stores = (tr, va)
             self._print(f"Data Loaded! ({tr.n_streams} streams x {tr.n} train / {va.n} val samples per rank, "
                         f"device={ctx.device})")
         return self._stores
+
+    def _dp_reference(self) -> bool:
+        """DataParallel semantics (dp_semantics="reference"): each step is ONE global batch of batch_size_DML
+        per stream, drawn from the same permutation on every rank and cut into world contiguous parts
+        (torch.nn.DataParallel's scatter, R:144-148); the loss is that global batch's."""
+        if self.dp_semantics not in ("weak", "reference"):
+            raise ValueError(f"dp_semantics {self.dp_semantics!r}")
+        return self.dp_semantics == "reference" and self._context().world > 1
+
+    def _local_part(self, idx: torch.Tensor) -> torch.Tensor:
+        """(reference semantics) this rank's contiguous part of a global batch of indices."""
+        ctx = self._context()
+        return idx.tensor_split(ctx.world)[ctx.rank] if self._dp_reference() else idx
 
     def _graphs_on(self) -> bool:
         ctx = self._context()
@@ -163,10 +177,28 @@ class Y2HRunner:
 
     @torch.no_grad()
     def eval_hdce(self, model: HDCEModel, store: DMLStore, batch: int = 1024) -> Tuple[float, float]:
-        """Global val NMSE vs label and vs perfect (R:216-235): sum err / sum pow over ALL streams."""
-        model.eval()
+        """Global val NMSE vs label and vs perfect (R:216-235): sum err / sum pow over ALL streams.  On the
+        GPU (hdce_engine "hip") through the HIP inference engine (train/infer.py: conv / BN / ReLU kernels,
+        the routed FC GEMM); elsewhere through the model's torch forward."""
         E, U = self.n_scenarios, self.n_users
         acc = torch.zeros(4, device=store.Yp.device, dtype=torch.float64)
+        if store.Yp.is_cuda and self.hdce_engine == "hip" and store.n > 0:
+            from .infer import HIPInference
+            eng = getattr(self, "_val_engine", None)
+            if eng is None or eng.model.E != model.E:
+                eng = self._val_engine = HIPInference(model.convs, model.fc, self.Pilot_num, store.Yp.device,
+                                                      chunk=min(2304, 144 * ((store.n + 143) // 144)))
+            else:
+                eng.refresh(model.convs, model.fc)
+            for s in range(store.n_streams):
+                expert = torch.full((store.n,), int(store.scen[s]), device=store.Yp.device, dtype=torch.int64)
+                Y = eng.estimate(store.Yp[s], expert)
+                lab, per = store.Hlabel[s], store.Hperf[s]
+                acc += torch.stack([((Y - lab) ** 2).sum(), (lab ** 2).sum(), ((Y - per) ** 2).sum(),
+                                    (per ** 2).sum()]).double()
+            self._context().all_reduce_(acc)
+            return float(acc[0] / acc[1]), float(acc[2] / acc[3])
+        model.eval()
         for s in range(0, store.n, batch):
             idx = torch.arange(s, min(s + batch, store.n), device=store.Yp.device)
             Yp, HL, HP = store.gather(idx)
@@ -191,26 +223,47 @@ class Y2HRunner:
         E, U, B = self.n_scenarios, self.n_users, self.batch_size_DML
         sp = model.space
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
-        step = HDCEStep(model, U, B)
+        if self.hdce_engine not in ("hip", "torch"):
+            raise ValueError(f"hdce_engine {self.hdce_engine!r}")
+        hip = None if self.hdce_engine == "hip" else False
+        ref = self._dp_reference()
+        Bl = (B + ctx.world - 1) // ctx.world if ref else B   # (the first ranks' part of a global batch)
+        step = HDCEStep(model, U, Bl, hip=hip)
         skip = step.skip if self.nan_guard else None
+        # reference semantics: the global batch's per-stream NMSE denominators (every rank computes them from
+        # the global indices); the ranks' losses are shares of ONE loss, so the gradients are SUMMED
+        den_global = torch.zeros(E * U, 2, device=ctx.device) if ref else None
+        rowpow = None
+        if ref and ctx.device.type == "cuda" and step.hip:
+            rowpow = (step.nmse._row_powers(tr.Hlabel), step.nmse._row_powers(tr.Hperf))
         # the NaN-guard flag rides in the conv bucket: all ranks skip (or step) together
         buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "conv": [sp.grad[:n_conv]] + ([skip] if skip is not None else [])})
         step.grad_hook = buckets.launch
         loss_acc = torch.zeros(2, device=ctx.device)
         last_loss = torch.zeros(2, device=ctx.device)
         static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
-        gscale = 1.0 / ctx.world
+        gscale = 1.0 if ref else 1.0 / ctx.world
 
         gathers = {}
 
         def run(idx):
             sp.zero_grad()
+            if ref:
+                den_global[:, 0] = tr.Hlabel.index_select(1, idx).pow(2).sum((1, 2))
+                den_global[:, 1] = tr.Hperf.index_select(1, idx).pow(2).sum((1, 2))
+                idx = self._local_part(idx)
             b = idx.numel()
             if b not in gathers:
                 gathers[b] = StepGather(E, U, b, model.H, model.W, ctx.device, with_classifier=False)
             g = gathers[b]
             g(tr, idx)
-            hs = step if b == B else HDCEStep(model, U, b, grad_hook=buckets.launch, skip=skip)
+            hs = step if b == Bl else HDCEStep(model, U, b, grad_hook=buckets.launch, skip=skip, hip=hip)
+            hs.nmse.den_global = den_global
+            if rowpow is not None:   # (the one-pass NMSE reads per-row label powers, scaled to global sums)
+                g.rowpow = rowpow
+                o = g.rowoff.long()
+                g.rowden[:, 0] = rowpow[0][o]
+                g.rowden[:, 1] = rowpow[1][o]
             loss = hs.forward_fc_gathered(g, tr)
             if hs.grad_hook:
                 hs.grad_hook("fc")
@@ -223,7 +276,8 @@ class Y2HRunner:
             opt.step(grad_scale=gscale, skip=skip)
 
         graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
-        sampler = DeviceSampler(tr.n, B, ctx.device, self.seed, ctx.rank)
+        # (reference semantics: one permutation for every rank -- each takes its part of each global batch)
+        sampler = DeviceSampler(tr.n, B, ctx.device, self.seed, 0 if ref else ctx.rank)
         d = ck.ckpt_dir(self.workspace, self.Pilot_num) if ctx.is_main else None
         log = self._log()
         best_nmse = 1000.0
@@ -276,8 +330,10 @@ class Y2HRunner:
             if ctx.device.type == "cuda":
                 torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            sps = nb * B * E * U * ctx.world / max(dt, 1e-9)
-            tl = (loss_acc / max(nb, 1)).tolist()
+            sps = nb * B * E * U * (1 if ref else ctx.world) / max(dt, 1e-9)
+            # the epoch's loss over every rank: reference semantics -- shares of one loss (sum); weak -- mean
+            ctx.all_reduce_(loss_acc)
+            tl = (loss_acc / (max(nb, 1) * (1 if ref else ctx.world))).tolist()
             self.train_HDCE_losses.append(tl[0])
             nmse, nmse_perf = self.eval_hdce(model, va)
             self.val_HDCE_nmse.append(nmse)
@@ -349,7 +405,9 @@ class Y2HRunner:
             kw["weight_decay"] = wd
         opt = make_optimizer(space, opt_name, self.lr, **kw)
         S, B = tr.n_streams, self.batch_size_DML
-        cstep = ClassifierStep(model, S, space=space, batch_total=S * B)
+        ref = self._dp_reference()
+        Bl = (B + ctx.world - 1) // ctx.world if ref else B
+        cstep = ClassifierStep(model, S, space=space, batch_total=S * Bl)
         skip = cstep.skip if self.nan_guard else None
         buckets = GradBuckets(ctx, {"all": [space.grad] + ([skip] if skip is not None else [])})
         cstep.grad_hook = buckets.launch
@@ -359,16 +417,27 @@ class Y2HRunner:
 
         def run(idx):
             space.zero_grad()
+            if ref:   # (mean NLL of the global batch = sum over ranks of (n_r / n) x the rank's mean)
+                n_glob = idx.numel()
+                idx = self._local_part(idx)
+                share = idx.numel() * ctx.world / n_glob
+                if share != 1.0:
+                    cstep.grad_hook = None
             b = idx.numel()
             x = tr.Yp.index_select(1, idx).reshape(S * b, *tr.Yp.shape[2:])
             labels = tr.scen.repeat_interleave(b)
             loss = cstep(x, labels)
+            if ref and share != 1.0:   # (uneven parts: weight this rank's mean before the reduction)
+                space.grad.mul_(share)
+                loss = loss * share
+                cstep.grad_hook = buckets.launch
+                buckets.launch_all()
             loss_acc.add_(loss)
             buckets.wait()
             opt.step(grad_scale=gscale, skip=skip)
 
         graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
-        sampler = DeviceSampler(tr.n, B, ctx.device, self.seed + 17, ctx.rank)
+        sampler = DeviceSampler(tr.n, B, ctx.device, self.seed + 17, 0 if ref else ctx.rank)
         log = self._log()
         train_losses, val_losses, val_accs = histories
         for h in histories:
@@ -409,7 +478,8 @@ class Y2HRunner:
                 else:
                     run(idx)
                 nb += 1
-            avg = float(loss_acc.item()) / max(nb, 1)
+            ctx.all_reduce_(loss_acc)   # (the epoch's mean loss over every rank)
+            avg = float(loss_acc.item()) / (max(nb, 1) * ctx.world)
             dt = time.perf_counter() - t0
             train_losses.append(avg)
             self._print(f"Epoch {epoch + 1}/{self.n_epochs}, Average Loss: {avg:.4f}")

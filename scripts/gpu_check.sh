@@ -29,30 +29,18 @@ for s in $STEPS; do
     bench_fp8) run bench_fp8 600 python bench.py --steps 50 --warmup 10 --dtype fp8 ;;
     bench_c5) run bench_c5 600 python bench.py --steps 10 --warmup 3 --qubits 16 --dtype fp8 ;;
     train) run train 1200 python scripts/train_eval.py --epochs ${EPOCHS:-100} --qubits 6 --qml-qubits 4,8 --out "$OUT/train" ;;
-    bench_k) for m in ${MODES:-dagq qsc}; do for k in ${KS:-1 2 5 10}; do run bench_${m}_k$k 300 python bench.py --steps 100 --warmup 10 --stream-mode $m --steps-per-graph $k; done; done ;;
-    bench_br) for b in ${BRS:-x a c w ac wa wca}; do run bench_br_$b 300 python bench.py --steps 100 --warmup 10 --stream-mode dagq --hdce-branches=${b/x/}; done ;;
-    bench_fork) for f in ${FORKS:-gather packed conv1 conv2 conv fc}; do run bench_fork_$f 300 python bench.py --steps 100 --warmup 10 --qsc-fork $f; done ;;
-    bench_adam) for g in ${GRIDS:-0 64 128 256 512}; do run bench_adam_$g 300 python bench.py --steps 100 --warmup 10 --hdce-branches=a --fc-adam-grid $g; done ;;
     q16grid) for g in ${GRIDS:-512 1152 2304}; do QDML_QSIM_BIG_GRID=$g run bench_q16_$g 300 python bench.py --steps 6 --warmup 2 --steps-per-graph 1 --qubits 16 --dtype fp8; done ;;
     convknobs) for k in ${KNOBS:-2,8,4,4 1,8,4,4 4,8,4,4 2,16,4,4 2,4,4,4 2,8,2,4 2,8,8,4 2,8,4,2 2,8,4,8}; do QDML_CONV_KNOBS=$k run bench_conv_${k//,/_} 300 python bench.py --steps 50 --warmup 10; done ;;
     savestate) for v in 1 0 1 0; do QDML_QSIM_SAVE_STATE=$v run bench_save_$v 300 python bench.py --steps 100 --warmup 10; done ;;
-    envsweep) for e in ${ENVS:-NONE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 DEBUG_HIP_GRAPH_BATCH_SIZE=1 DEBUG_HIP_GRAPH_BATCH_SIZE=64 DEBUG_HIP_FORCE_GRAPH_QUEUES=1 DEBUG_HIP_FORCE_GRAPH_QUEUES=2}; do
-        for v in "" "--stream-mode dagi"; do env $e timeout -k 10 300 python bench.py --steps 100 --warmup 10 $v > $OUT/env_${e}${v// /_}.log 2>&1 || exit 1; echo "$e $v $(grep -o '"ms_per_step": [0-9.]*' $OUT/env_${e}${v// /_}.log)" | tee -a $OUT/envsweep.txt; done; done ;;
-    dagi) for v in dagq dagi dagq dagi; do run bench_mode_${v}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --stream-mode $v; done ;;
-    dagicmp) for r in 1 2 3; do for o in dagq dagi; do m=$o; timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode $m > $OUT/cmp.log 2>&1 || exit 1; echo "$o $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/dagicmp.txt; done; done ;;
-    qscgrid) for r in 1 2; do for g in 256 128 64 576; do QDML_QSC_GRID_BWD=$g timeout -k 10 300 python bench.py --steps 200 --warmup 10 --stream-mode ${MODE:-dagq} > $OUT/cmp.log 2>&1 || exit 1; echo "$g $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/qscgrid.txt; done; done ;;
+    qscgrid) for r in 1 2; do for g in 256 128 64 576; do QDML_QSC_GRID_BWD=$g timeout -k 10 300 python bench.py --steps 200 --warmup 10 > $OUT/cmp.log 2>&1 || exit 1; echo "$g $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/qscgrid.txt; done; done ;;
     adamnt) for v in 0 1 0 1; do (cd /tmp && export TMPDIR=/tmp && QDML_ADAM_NT=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/adamnt_$v" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 > "$OUT/adamnt_$v.log" 2>&1) || exit 1; python scripts/prof_summary.py "$OUT/adamnt_$v/run_kernel_trace.csv" --tail 0.6 > "$OUT/adamnt_${v}_$RANDOM.md"; rm -rf "$OUT/adamnt_$v"; done ;;
     pmc) for pc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do n=${pc%% *}; (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $pc --output-format csv -d "$OUT/pmc_$n" -o run -- python "$ROOT/bench.py" --steps 10 --warmup 2 --steps-per-graph 1 > "$OUT/pmc_$n.log" 2>&1) || { echo "pmc $pc failed"; tail -5 "$OUT/pmc_$n.log"; exit 1; }; done; python scripts/pmc_summary.py "$OUT"/pmc_* > "$OUT/pmc_summary.md"; rm -rf "$OUT"/pmc_*/ ;;
-    join) for v in ${JOINS:-end adam bwd end adam bwd}; do QDML_QSC_JOIN=$v timeout -k 10 300 python bench.py --steps 300 --warmup 10 > $OUT/cmp.log 2>&1 || exit 1; echo "join=$v $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/join.txt; done ;;
     variants) IFS=';' read -ra VS <<< "${VARIANTS:-NONE=0|}"; for r in 1 2; do for v in "${VS[@]}"; do env ${v%%|*} timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-300} --warmup 10 ${v#*|} > $OUT/cmp.log 2>&1 || exit 1; echo "$v $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/variants.txt; done; done ;;
-    prof_join)(cd /tmp && export TMPDIR=/tmp && QDML_QSC_JOIN=${JOIN:-adam} run prof_join 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_join" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5) && python scripts/prof_summary.py "$OUT/prof_join/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_join_summary.md" && python scripts/prof_timeline.py "$OUT/prof_join/run_kernel_trace.csv" --marker "conv3x3_kernel<2," > "$OUT/prof_join_timeline.md" ;;
     dpphase)for v in 1 2 3 1 2 3; do run bench_dpq_${v}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
-    prio) for v in "" "--stream-priority" "" "--stream-priority" "--dtype fp8" "--dtype fp8 --stream-priority"; do run bench_prio_${v// /_} 300 python bench.py --steps 100 --warmup 10 $v; done ;;
     fusewd) for v in 1 0 1 0; do QDML_CONV_FUSE_WD=$v run bench_fwd_$v 300 python bench.py --steps 100 --warmup 10; mv $OUT/bench_fwd_$v.log $OUT/bench_fwd_${v}_$RANDOM.log; done ;;
-    bench_modes) for m in ${MODES:-serial dag dagq qsc full}; do run bench_$m 300 python bench.py --steps 100 --warmup 10 --stream-mode $m; done; run bench_qscfirst 300 python bench.py --steps 100 --warmup 10 --stream-mode qsc --qsc-first ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
-    prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace ${PROF_EXTRA:-} --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --stream-mode ${MODE:-dagq} ${BENCH_EXTRA:-}) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" && python scripts/prof_timeline.py "$OUT/prof/run_kernel_trace.csv" --marker "conv3x3_kernel<2," > "$OUT/prof_timeline.md" ;;
+    prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace ${PROF_EXTRA:-} --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 ${BENCH_EXTRA:-}) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" && python scripts/prof_timeline.py "$OUT/prof/run_kernel_trace.csv" --marker "conv3x3_kernel<2," > "$OUT/prof_timeline.md" ;;
     prof_fp8) (cd /tmp && export TMPDIR=/tmp && run prof_fp8 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_fp8" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --dtype fp8 --steps-per-graph 1) && python scripts/prof_summary.py "$OUT/prof_fp8/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_fp8_summary.md" && python scripts/prof_timeline.py "$OUT/prof_fp8/run_kernel_trace.csv" > "$OUT/prof_fp8_timeline.md" ;;
     stamp) run stamp 300 python scripts/stamp_qsc.py ;;
     stamp_conv) run stamp_conv 300 python scripts/stamp_conv.py ;;

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--workspace", default="./workspace")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="HDCE estimator compute dtype (fp8: e4m3 FC forward GEMM, bf16 convs / backward)")
+    ap.add_argument("--hdce-engine", default="hip", choices=["hip", "torch"],
+                    help="HDCE training step: the fused HIP kernels, or torch autograd (with --dtype fp32: all fp32)")
     ap.add_argument("--bn-adapt", action="store_true", help="also run the sweep with test-time BN re-estimation "
                     "(written under <out>/bn_adapt)")
     a = ap.parse_args()
@@ -32,6 +34,7 @@ def main():
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.utils.plots import plot_fig2
     os.makedirs(a.out, exist_ok=True)
     common = dict(n_epochs=a.epochs, data_len=a.data_len, batch_size_DML=a.batch, workspace=a.workspace, dtype=a.dtype,
+                  hdce_engine=a.hdce_engine,
                   log_jsonl=os.path.join(a.out, "train_metrics.jsonl"))
     r = Y2HRunner(n_qubits=a.qubits, **common)
     t = {}

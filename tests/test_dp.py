@@ -110,3 +110,33 @@ def test_capture_preflight_ranks_agree_and_fall_back(tmp_path):
                 extra_env={"OMP_NUM_THREADS": "1"})
     assert rc == 0
     assert [open(f"{out}.{r}").read().strip() for r in range(2)] == ["0", "0"]
+
+
+def test_rccl_gpu_check_is_per_node():
+    """One GPU per rank OF THIS NODE: a 2 x 8 job (WORLD_SIZE 16) on 8-GPU nodes is fine; 9 local ranks,
+    or a LOCAL_RANK past the node's GPUs, are not."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import check_local_gpus
+    check_local_gpus(local_rank=7, local_world=8, n_gpus=8)   # (WORLD_SIZE is not an argument at all)
+    for lr, lw in ((8, 8), (0, 9)):
+        with pytest.raises(RuntimeError):
+            check_local_gpus(local_rank=lr, local_world=lw, n_gpus=8)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_reference_dp_semantics_matches_one_process(tmp_path, world):
+    """dp_semantics="reference" (DataParallel's split of one global batch, R:144-148) == one process on the
+    whole batch, for the BN-free classical SC; the HDCE trainer runs in lockstep (rank-identical weights)."""
+    import torch
+    one = str(tmp_path / "one")
+    assert launch([sys.executable, os.path.join(HERE, "dist_scripts", "ref_semantics.py"), one], nproc=1,
+                  extra_env={"OMP_NUM_THREADS": "2", "PYTHONWARNINGS": "ignore"}) == 0
+    many = str(tmp_path / "many")
+    assert launch([sys.executable, os.path.join(HERE, "dist_scripts", "ref_semantics.py"), many], nproc=world,
+                  extra_env={"OMP_NUM_THREADS": "1", "PYTHONWARNINGS": "ignore"}) == 0
+    a = torch.load(f"{one}.0.pt", weights_only=True)
+    for r in range(world):
+        b = torch.load(f"{many}.{r}.pt", weights_only=True)
+        assert torch.allclose(a["sc"], b["sc"], rtol=1e-4, atol=1e-6), float((a["sc"] - b["sc"]).abs().max())
+        assert torch.allclose(a["sc_loss"], b["sc_loss"], rtol=1e-5)
+        same, hl, _ = open(f"{many}.{r}").read().split()
+        assert same == "1" and float(hl) == float(hl)

@@ -118,3 +118,28 @@ def _rows(store_t, rowoff):
     C = store_t.shape[-1]
     sr = store_t.stride(0) // C
     return torch.stack([store_t[int(o) // sr, int(o) % sr] for o in rowoff])
+
+
+def test_nmse_global_denominators_split_equals_whole():
+    """DataParallel semantics: each part of a batch computed with the GLOBAL per-stream denominators gives
+    losses that sum to the whole batch's NMSE loss, and gradients equal to the whole batch's rows."""
+    import torch
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.nmse import StreamNMSE
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEModel
+    torch.manual_seed(0)
+    E, U, B, cols = 3, 3, 8, 64
+    Y, L, P = (torch.randn(E, U, B, cols) for _ in range(3))
+    rows = lambda t: HDCEModel.rows_from_streams(t)
+    whole = StreamNMSE(HDCEModel.row_stream(E, U, B, "cpu"), E * U, cols)
+    lw = whole.sums_finalize(rows(Y), rows(L), rows(P)).clone()
+    gw = whole.grad(rows(Y), rows(L)).view(U, B, E, cols)
+    den = torch.stack([(L ** 2).sum((2, 3)).reshape(-1), (P ** 2).sum((2, 3)).reshape(-1)], 1)   # (S, 2)
+    loss_sum = torch.zeros(2)
+    for lo, hi in ((0, 3), (3, 8)):   # uneven parts of every stream's batch
+        part = StreamNMSE(HDCEModel.row_stream(E, U, hi - lo, "cpu"), E * U, cols)
+        part.den_global = den
+        sl = lambda t: rows(t[:, :, lo:hi].contiguous())
+        loss_sum += part.sums_finalize(sl(Y), sl(L), sl(P))
+        g = part.grad(sl(Y), sl(L)).view(U, hi - lo, E, cols)
+        assert torch.allclose(g, gw[:, lo:hi], rtol=1e-5, atol=1e-7)
+    assert torch.allclose(loss_sum, lw, rtol=1e-5)

@@ -167,7 +167,10 @@ def test_bench_two_ranks_one_gpu_reports_phases(tmp_path):
     recs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(recs) == 1
     r = recs[0]
-    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["config"]["dp_plan"] == "zero"
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2"
+    sel = r["config"]["plan_select_ms"]   # (both plans timed at world 2, the faster one benchmarked)
+    assert set(sel) == {"zero", "allreduce"} and r["config"]["dp_plan"] == min(sel, key=sel.get)
+    assert r["config"]["dp_graph"] == "five"   # (gloo: no captured collectives, so its phases are reported)
     ph = r["phases_ms"]
     assert set(ph) >= {"g1", "g2", "fc_exposed", "fc_adam", "all_gather", "conv_qsc_adam", "step"}
     assert ph["step"] > 0 and ph["g1"] > 0
