@@ -20,8 +20,9 @@ from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flags
 
 def run(ctx, plan, device, steps=3):
     if device == "cuda":
+        # (QDML_STREAM_MODE: diagnosis of the GPU rehearsal -- serial takes the QSC branch off its stream)
         cfg = FlagshipConfig(n_qubits=8, batch=32, data_len=800, hip_graphs=True, dp_plan=plan,
-                             use_quantumnat=False)
+                             use_quantumnat=False, stream_mode=os.environ.get("QDML_STREAM_MODE", "dagq"))
     else:
         cfg = FlagshipConfig(n_qubits=4, batch=4, data_len=40, hip_graphs=False, dtype="fp32", dp_plan=plan,
                              use_quantumnat=False)
@@ -39,9 +40,11 @@ def run(ctx, plan, device, steps=3):
 
 def main(out, device="cpu"):
     ctx = init_distributed(device)
-    za, fa, qa, sa, la = run(ctx, "allreduce", device)
-    zz, fz, qz, sz, lz = run(ctx, "zero", device)
-    checks = {"plans": (not za) and zz, "hdce": torch.equal(fa, fz), "qsc": torch.equal(qa, qz),
+    # (QDML_ZV_PLANS="allreduce,allreduce" etc.: the same plan twice -- run-to-run determinism)
+    pa, pz = os.environ.get("QDML_ZV_PLANS", "allreduce,zero").split(",")
+    za, fa, qa, sa, la = run(ctx, pa, device)
+    zz, fz, qz, sz, lz = run(ctx, pz, device)
+    checks = {"plans": za == (pa == "zero") and zz == (pz == "zero"), "hdce": torch.equal(fa, fz), "qsc": torch.equal(qa, qz),
               "loss": torch.equal(la, lz)}
     if sa is not None:
         checks["shadow"] = torch.equal(sa[:fa.numel() - (fa.numel() - sa.numel())], sz[:sa.numel()])

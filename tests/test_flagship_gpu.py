@@ -115,22 +115,33 @@ def test_dp_plan_two_ranks_on_one_gpu(tmp_path, plan):
         assert same == "1" and skipped == "1" and float(flag) >= 1.0, (r, same, skipped, flag)
 
 
-@pytest.mark.xfail(strict=False, reason="gloo-on-one-card rehearsal: QSC weights differ by ~1e-4 in about half "
-                   "the runs (HDCE bit-equal) after the small-bucket hand-off fixes; the RCCL comparison "
-                   "(test_dp_one_graph_matches_five_graphs_over_rccl) is bit-exact -- docs/CONCURRENCY.md")
-def test_zero_plan_matches_allreduce_plan_on_gpu(tmp_path):
-    """ZeRO-1 FC optimizer == all-reduce plan bit for bit on the GPU plan (2 ranks sharing the card over
-    gloo): reduce-scatter, Adam on each rank's FC shard writing its slice of the bf16 shadow, all-gather."""
+def _two_ranks_one_gpu(tmp_path, script, env):
     import os
     import sys
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.launch import launch
     here = os.path.dirname(os.path.abspath(__file__))
     out = str(tmp_path / "z")
-    rc = launch([sys.executable, os.path.join(here, "dist_scripts", "zero_vs_allreduce.py"), out, "cuda"], nproc=2,
-                extra_env={"OMP_NUM_THREADS": "2", "QDML_DIST_BACKEND": "gloo"})
+    rc = launch([sys.executable, os.path.join(here, "dist_scripts", script), out, "cuda"], nproc=2,
+                extra_env={"OMP_NUM_THREADS": "2", "QDML_DIST_BACKEND": "gloo", **env})
     assert rc == 0
-    for r in range(2):
-        rec = open(f"{out}.{r}").read().split()
+    return [open(f"{out}.{r}").read().split() for r in range(2)]
+
+
+def test_zero_plan_matches_allreduce_plan_on_gpu(tmp_path):
+    """ZeRO-1 FC optimizer == all-reduce plan bit for bit on the GPU DP plan (2 ranks sharing the card over
+    gloo): reduce-scatter, Adam on each rank's FC shard writing its slice of the bf16 shadow, all-gather.
+    The QSC branch runs on the main stream here (stream_mode serial): with it forked (dagq) the DP plan on a
+    SHARED card is not run-to-run deterministic in the QSC weights -- the same plan twice differs as often
+    as the two plans do (profiles/r3_03_zero_diag.txt, docs/CONCURRENCY.md); that is the next test."""
+    for r, rec in enumerate(_two_ranks_one_gpu(tmp_path, "zero_vs_allreduce.py", {"QDML_STREAM_MODE": "serial"})):
+        assert rec[0] == "1", (r, rec)
+
+
+@pytest.mark.xfail(strict=False, reason="OPEN (docs/CONCURRENCY.md): 2 processes sharing one GPU, QSC branch forked: "
+                   "the same DP plan twice differs in the QSC weights in ~1 of 8 runs (HDCE bit-equal); not gloo's "
+                   "completion semantics (a host sync after every wait changes nothing), not ZeRO vs all-reduce")
+def test_dp_plan_run_to_run_on_shared_gpu(tmp_path):
+    for r, rec in enumerate(_two_ranks_one_gpu(tmp_path, "zero_vs_allreduce.py", {"QDML_ZV_PLANS": "allreduce,allreduce"})):
         assert rec[0] == "1", (r, rec)
 
 
