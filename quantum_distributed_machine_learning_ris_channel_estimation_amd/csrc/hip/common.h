@@ -28,6 +28,18 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// One element of an Adam step (moments and weight in place; g already scaled / decayed / pruned).  Every
+// rounding step is an explicit intrinsic, so no FMA contraction choice of the compiler can differ between
+// the kernels that apply it: csrc/hip/optim.hip's update kernel and csrc/hip/gemm.hip's fused
+// weight-gradient epilogue give bitwise-identical weights and moments.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float beta1, float beta2, float eps,
+                                          float step_size, float rbc2) {
+  m = __fmaf_rn(beta1, m, __fmul_rn(1.f - beta1, g));
+  v = __fmaf_rn(beta2, v, __fmul_rn(__fmul_rn(1.f - beta2, g), g));
+  const float denom = __fmaf_rn(__fsqrt_rn(v), rbc2, eps);
+  p = __fmaf_rn(-step_size, __fdiv_rn(m, denom), p);
+}
+
 // Diagnostic phase stamp (stamped kernel builds only): s_memtime with its own lgkmcnt wait, fenced
 // by scheduling barriers so the compiler keeps each phase's work on its side of the stamp.
 __device__ __forceinline__ unsigned long long phase_stamp() {

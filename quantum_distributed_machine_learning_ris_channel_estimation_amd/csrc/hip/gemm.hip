@@ -57,7 +57,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
 enum { KC = 0, MC = 1 };
-enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2 };
+enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2, EPI_ADAM = 3 };
 constexpr int BK = 64;
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
@@ -74,6 +74,22 @@ struct NmseArgs {
   float* dens;             // (S, 2): per-stream (sum |label|^2, sum |perf|^2)
   int E, U, B;             // row r = (u*B + b)*E + e, stream s = e*U + u
   float loss_scale;
+};
+
+// EPI_ADAM (the weight gradient at world 1): the FC weight's Adam step applied to the gradient tile straight
+// from the accumulators -- dW is never written.  p / m / v / shadow are the FC weight's fp32 master, moments and
+// bf16 copy, row-major like dW (ld = ldc); the same arithmetic as csrc/hip/optim.hip adam_kernel (Adam, no
+// weight decay, no pruning).  The last workgroup advances the step counter (optim.hip tick_if_last's protocol).
+struct AdamEpi {
+  float* p;
+  float* m;
+  float* v;
+  uint16_t* shadow;         // nullable
+  const float* lr;
+  const float* step;        // steps taken so far (read), advanced by the last workgroup
+  const float* skip;        // nullable: nonzero = skip the update (NaN guard)
+  float beta1, beta2, eps, grad_scale;
+  unsigned int* done;       // zero-initialised arrival counter (re-armed by the last workgroup)
 };
 
 // DBG (diagnosis builds, scripts/probe_gemm.py): 1 = no global loads in the K loop (MFMAs on whatever the
@@ -299,6 +315,7 @@ struct Args {
   const long* pexp;     // nullable: row i of P is P[i * pe + pexp[i]] (KC P only: expert-routed rows)
   int pe;
   const float* deq;     // nullable: (2,) dequantisation scales; the accumulators are multiplied by their product
+  AdamEpi ad;           // EPI_ADAM
 };
 
 // tile order: blocks b, b+8, ... share an XCD; each XCD takes whole GM x GN tile groups (row-major
@@ -433,6 +450,52 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
       float* dst = C + (size_t)(i0 + row) * a.ldc + j0 + c0;
       if constexpr (VEC == 4) *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(ct + row * PITCH + c0);
       else *reinterpret_cast<float2*>(dst) = *reinterpret_cast<const float2*>(ct + row * PITCH + c0);
+    }
+  } else if constexpr (EPI == EPI_ADAM) {
+    static_assert(VEC == 4, "the Adam epilogue walks 256-column tiles");
+    const AdamEpi& ad = a.ad;
+    const bool skip = ad.skip != nullptr && *ad.skip != 0.f;
+    if (!skip) {
+      const float lr = *ad.lr;
+      const float t = *ad.step + 1.f;  // step about to be taken
+      const float bc1 = 1.f - __powf(ad.beta1, t);
+      const float bc2 = 1.f - __powf(ad.beta2, t);
+      const float step_size = lr / bc1;
+      const float rbc2 = rsqrtf(bc2);
+      for (int row = wave; row < G::BM; row += G::NW) {
+        const size_t o = (size_t)(i0 + row) * a.ldc + j0 + c0;
+        const float4 g4 = *reinterpret_cast<const float4*>(ct + row * PITCH + c0);
+        float4 pp = *reinterpret_cast<const float4*>(ad.p + o);
+        float4 mm = *reinterpret_cast<const float4*>(ad.m + o);
+        float4 vv = *reinterpret_cast<const float4*>(ad.v + o);
+        const float* ga = &g4.x;
+        float* pa = &pp.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          adam_elem(pa[j], ma[j], va[j], ga[j] * ad.grad_scale, ad.beta1, ad.beta2, ad.eps, step_size, rbc2);
+        }
+        *reinterpret_cast<float4*>(ad.p + o) = pp;
+        *reinterpret_cast<float4*>(ad.m + o) = mm;
+        *reinterpret_cast<float4*>(ad.v + o) = vv;
+        if (ad.shadow != nullptr) {
+          uint2 w;
+          w.x = (uint32_t)f32_to_bf16(pp.x) | ((uint32_t)f32_to_bf16(pp.y) << 16);
+          w.y = (uint32_t)f32_to_bf16(pp.z) | ((uint32_t)f32_to_bf16(pp.w) << 16);
+          *reinterpret_cast<uint2*>(ad.shadow + o) = w;
+        }
+      }
+      // step tick: the last workgroup to arrive (every workgroup read *step above, before its arrival)
+      __syncthreads();
+      unsigned int* flag = reinterpret_cast<unsigned int*>(smem);   // (the ct tile is no longer read)
+      if (tid == 0) {
+        const unsigned int prev = __hip_atomic_fetch_add(ad.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = prev == gridDim.x - 1;
+      }
+      __syncthreads();
+      if (tid == 0 && flag[0]) {
+        *const_cast<float*>(ad.step) += 1.f;
+        __hip_atomic_store(ad.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   } else if constexpr (EPI == EPI_BF16) {
     uint16_t* C = reinterpret_cast<uint16_t*>(a.C);
@@ -644,6 +707,20 @@ QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M
   if (cfg == 1) return launch<WgrB, EPI_F32, 2, 8>(a, st);
   if (cfg == 2) return launch<WgrC, EPI_F32, 2, 8>(a, st);
   return launch<WgrA, EPI_F32, 2, 8>(a, st);
+}
+
+// The weight gradient with the FC weight's Adam step as its epilogue (EPI_ADAM): dW (N, K) = dY^T A is never
+// stored; p / m / v / shadow (N, K) row-major with row stride ldw (see AdamEpi).
+QD_API int qd_gemm_wgrad_adam(const uint16_t* dY, const uint16_t* A, int M, int N, int K, int ldw, float* p, float* m,
+                              float* v, uint16_t* shadow, const float* lr, float* step, const float* skip, float beta1,
+                              float beta2, float eps, float grad_scale, unsigned int* done, int cfg, void* stream) {
+  if (!p || !m || !v || !lr || !step || !done || (ldw & 3)) return (int)hipErrorInvalidValue;
+  Args a{dY, A, N, K, N, K, M, nullptr, ldw, nullptr, {}, nullptr, 0, nullptr,
+         AdamEpi{p, m, v, shadow, lr, step, skip, beta1, beta2, eps, grad_scale, done}};
+  hipStream_t st = (hipStream_t)stream;
+  if (cfg == 1) return launch<WgrB, EPI_ADAM, 2, 8>(a, st);
+  if (cfg == 2) return launch<WgrC, EPI_ADAM, 2, 8>(a, st);
+  return launch<WgrA, EPI_ADAM, 2, 8>(a, st);
 }
 
 // dA (M, K) bf16 = dY W: dY (M, N) bf16, W (N, K) bf16 row-major; reduction over N

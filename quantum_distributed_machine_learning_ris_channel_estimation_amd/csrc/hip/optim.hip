@@ -133,7 +133,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
                                                    const float* __restrict__ lr_ptr, const float* step_ptr,
                                                    const float* __restrict__ skip, unsigned int* __restrict__ pruned,
                                                    AdamArgs a, float* __restrict__ step_out,
-                                                   unsigned int* __restrict__ done, Shadow sh, PackScatter ps) {
+                                                   unsigned int* __restrict__ done, Shadow sh, PackScatter ps,
+                                                   long hole_lo, long hole_n) {
   if (skip != nullptr && *skip != 0.f) {   // uniform across the grid: nobody ticks (the cursor still moves)
     if (ps.cursor && blockIdx.x == 0 && threadIdx.x == 0) *ps.cursor += ps.cursor_inc;
     return;
@@ -147,7 +148,10 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
   unsigned int cnt = 0;
   float wmax = 0.f;
   const long stride = (long)gridDim.x * blockDim.x * 4;
-  for (long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 < n; i0 += stride) {
+  // [hole_lo, hole_lo + hole_n) (multiples of 4) is skipped: a range another kernel updates (the FC weight,
+  // stepped inside its weight-gradient GEMM's epilogue); the loop runs over n - hole_n logical elements
+  for (long il = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; il < n - hole_n; il += stride) {
+    const long i0 = il < hole_lo ? il : il + hole_n;
     if (i0 + 3 < n) {
       float4 pp = ldv<NT>(p + i0);
       float4 gg = ldv<NT>(g + i0);
@@ -161,10 +165,8 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         float pj = pa[j];
         if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
         else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
-        ma[j] = a.beta1 * ma[j] + (1.f - a.beta1) * gj;
-        va[j] = a.beta2 * va[j] + (1.f - a.beta2) * gj * gj;
-        const float denom = sqrtf(va[j]) * rbc2 + a.eps;
-        pa[j] = pj - step_size * ma[j] / denom;
+        adam_elem(pj, ma[j], va[j], gj, a.beta1, a.beta2, a.eps, step_size, rbc2);
+        pa[j] = pj;
         ga[j] = gj;
       }
       stv<NT>(p + i0, pp);
@@ -180,10 +182,11 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         float pj = p[i];
         if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
         else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
-        m[i] = a.beta1 * m[i] + (1.f - a.beta1) * gj;
-        v[i] = a.beta2 * v[i] + (1.f - a.beta2) * gj * gj;
-        const float denom = sqrtf(v[i]) * rbc2 + a.eps;
-        p[i] = pj - step_size * m[i] / denom;
+        float mi = m[i], vi = v[i];
+        adam_elem(pj, mi, vi, gj, a.beta1, a.beta2, a.eps, step_size, rbc2);
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pj;
         g[i] = gj;
         if (sh.out != nullptr && i >= sh.lo && i < sh.hi) {
           sh.out[i - sh.lo] = f32_to_bf16(p[i]);
@@ -279,13 +282,15 @@ QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const fl
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
                         float grad_scale, float prune_thr, unsigned int* done, uint16_t* shadow, long shadow_lo,
                         long shadow_hi, uint8_t* shadow8, const float* qs, float* amax, int max_grid,
-                        const PackScatter* ps_in, void* stream) {
+                        const PackScatter* ps_in, long hole_lo, long hole_n, void* stream) {
   const PackScatter ps = ps_in ? *ps_in : PackScatter{};
   for (int k = 0; k < 3; ++k)
     if (ps.n[k] && (ps.lo[k] < 0 || ps.lo[k] + ps.n[k] > n || (ps.lo[k] & 3) || (ps.n[k] & 3) || !ps.fwd[k]))
       return (int)hipErrorInvalidValue;
   if (n <= 0 || done == nullptr || (shadow && ((shadow_lo | shadow_hi) & 3))) return (int)hipErrorInvalidValue;
   if (shadow8 && (!shadow || !qs || !amax)) return (int)hipErrorInvalidValue;
+  if (hole_n < 0 || hole_lo < 0 || ((hole_lo | hole_n) & 3) || hole_lo + hole_n > n || (hole_n && shadow8))
+    return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   AdamArgs a{beta1, beta2, eps, weight_decay, grad_scale, prune_thr, decoupled};
   Shadow sh{shadow, shadow_lo, shadow_hi, shadow8, qs, amax};
@@ -293,12 +298,14 @@ QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const fl
   // kernels running beside it (the FC Adam as a side branch of the step graph)
   // streaming loads/stores for large ranges (QDML_ADAM_NT=0/1 overrides; measured in scripts/gpu_check.sh adamnt)
   static const int nt_env = [] { const char* e = getenv("QDML_ADAM_NT"); return e ? atoi(e) : -1; }();
-  const bool nt = nt_env >= 0 ? nt_env != 0 : n >= (1L << 20);
-  const dim3 grid(grid_for(n, max_grid > 0 ? max_grid : 2048));
+  const bool nt = nt_env >= 0 ? nt_env != 0 : n - hole_n >= (1L << 20);
+  const dim3 grid(grid_for(n - hole_n, max_grid > 0 ? max_grid : 2048));
   if (nt)
-    hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh, ps);
+    hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh,
+                       ps, hole_lo, hole_n);
   else
-    hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh, ps);
+    hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done,
+                       sh, ps, hole_lo, hole_n);
   return (int)hipGetLastError();
 }
 

@@ -195,6 +195,22 @@ __device__ void high_pass_fwd(const cf* A, cf* B, const float4* trig) {
   __syncthreads();
 }
 
+// LDS-resident states with no high qubits (n <= 12): the high pass is the bare CNOT-ring permutation,
+// done IN PLACE through registers (every thread holds its D / NT amplitudes across one barrier), so the
+// forward needs one state buffer instead of two and the adjoint two instead of four -- 2x / 4x fewer
+// bytes of LDS per workgroup, hence 2x the resident workgroups per CU (round 3).
+template <int N>
+__device__ void ring_fwd_inplace(cf* A) {
+  constexpr int PER = G<N>::D / NT;
+  cf a[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) a[i] = A[threadIdx.x + i * NT];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PER; ++i) A[ring_fwd<N>(threadIdx.x + i * NT)] = a[i];
+  __syncthreads();
+}
+
 // Low pass of layer 1 with the layer-0 product state GENERATED per tile (HBM-state builds): the
 // product amplitudes are never written to and re-read from HBM.  trig0: layer-0 (embedding) trig.
 template <int N>
@@ -276,6 +292,15 @@ __device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs
   layer_trig(trig, w, xs, N);
   __syncthreads();
   product_pass<N>(A, trig);
+  if constexpr (G<N>::HB == 0 && G<N>::LDS_STATE) {   // (one buffer: see ring_fwd_inplace)
+    for (int l = 1; l < L; ++l) {
+      layer_trig(trig, w + 2 * N * l, nullptr, N);
+      __syncthreads();
+      low_pass_fwd<N>(A, tile, trig);
+      ring_fwd_inplace<N>(A);
+    }
+    return A;
+  }
   for (int l = 1; l < L; ++l) {
     layer_trig(trig, w + 2 * N * l, nullptr, N);
     __syncthreads();
@@ -391,7 +416,11 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
   cf* data = reinterpret_cast<cf*>(smem + O_DATA);
   const int P = 2 * N * L;
   cf *b0, *b1, *b2, *b3, *tp = nullptr, *tq = nullptr;
-  if constexpr (C::LDS_STATE) {
+  if constexpr (C::LDS_STATE && C::HB == 0) {   // in-place ring passes: psi in b0, lambda in b2
+    b0 = data;
+    b2 = data + C::D;
+    b1 = b3 = nullptr;
+  } else if constexpr (C::LDS_STATE) {
     b0 = data;
     b1 = data + C::D;
     b2 = data + 2 * C::D;
@@ -436,7 +465,30 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
       float* gdst = (l == 0) ? tmp : acc + 2 * N * l;
       const bool first = (l == L - 1);   // lambda = O psi formed on the fly
       // ---- high pass (reverse): gather psi/lam at f(k) (inverse ring), undo high rotations
-      {
+      if constexpr (C::HB == 0 && C::LDS_STATE) {   // the bare inverse ring, in place (ring_fwd_inplace)
+        constexpr int PER = C::D / NT;
+        cf p[PER], m[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+          const int src = ring_fwd<N>(threadIdx.x + i * NT);
+          p[i] = psi[src];
+          if (first) {
+            float o = 0.f;
+#pragma unroll
+            for (int q = 0; q < N; ++q) o += ((src >> q) & 1) ? -gq[q] : gq[q];
+            m[i] = {p[i].x * o, p[i].y * o};
+          } else {
+            m[i] = lam[src];
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+          psi[threadIdx.x + i * NT] = p[i];
+          lam[threadIdx.x + i * NT] = m[i];
+        }
+        __syncthreads();
+      } else {
         float dth[HV], dph[HV];
 #pragma unroll
         for (int b = 0; b < HV; ++b) dth[b] = dph[b] = 0.f;
@@ -569,6 +621,7 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
 template <int N>
 static size_t smem_bytes(bool backward) {
   using C = G<N>;
+  if (C::LDS_STATE && C::HB == 0) return O_DATA + (backward ? 2 : 1) * sizeof(cf) * C::D;   // in-place rings
   if (C::LDS_STATE) return O_DATA + (backward ? 4 : 2) * sizeof(cf) * C::D;
   return O_DATA + (backward ? 2 : 1) * sizeof(cf) * C::T;
 }
@@ -623,7 +676,8 @@ QD_API int qd_qsim_big_grid(int B) { return B < g_big_grid_cap ? B : g_big_grid_
 QD_API int qd_qsim_big_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
                            void* psave, void* stream) {
   if (B < 1 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
-  const int grid = qd_qsim_big_grid(B);
+  // (n <= 12: one 32 KiB state per workgroup, 4 resident per CU -- 768 workgroups, 3 samples each at B = 2304)
+  const int grid = n <= 12 ? (B < 768 ? B : 768) : qd_qsim_big_grid(B);
 #define CALL_F(NN) \
   launch<NN>(false, x, w, nullptr, E, nullptr, B, L, wgroup, (cf*)ws, grid, (hipStream_t)stream, (cf*)psave)
   QD_BIG_DISPATCH(n, CALL_F)

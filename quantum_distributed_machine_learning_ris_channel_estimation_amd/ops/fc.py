@@ -64,6 +64,27 @@ def gemm_wgrad(dY: torch.Tensor, A: torch.Tensor, out: Optional[torch.Tensor] = 
     return W
 
 
+def gemm_wgrad_adam(dY: torch.Tensor, A: torch.Tensor, opt, lo: int, slot: int, skip: Optional[torch.Tensor] = None,
+                    grad_scale: float = 1.0, cfg: int = 0, shape=None) -> None:
+    """dW = dY^T A with the Adam step of the flat range ``[lo, lo + N*K)`` of ``opt`` (ops.optim.FusedOptimizer,
+    its ``fuse_range`` slot ``slot``) applied in the GEMM's epilogue: the weight, moments and the bf16 shadow
+    are updated, dW itself is never stored (csrc/hip/gemm.hip qd_gemm_wgrad_adam)."""
+    M, N = dY.shape
+    K = A.shape[1]
+    assert dY.dtype == A.dtype == torch.bfloat16 and dY.is_contiguous() and A.is_contiguous() and A.shape[0] == M
+    assert opt.kind == "adam" and opt.fused == (lo, lo + N * K)
+    sp = opt.space
+    sh = None
+    if opt.shadow is not None:
+        assert opt.shadow_lo <= lo and lo + N * K <= opt.shadow_hi
+        sh = ctypes.c_void_p(opt.shadow.data_ptr() + 2 * (lo - opt.shadow_lo))
+    f = _gemm_fn("qd_gemm_wgrad_adam", [_p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _f, _f, _f, _f, _p, _i, _p])
+    at = lambda t: ctypes.c_void_p(t.data_ptr() + 4 * lo)
+    nat.check(f(nat.ptr(dY), nat.ptr(A), M, N, K, K, at(sp.flat), at(opt.m), at(opt.v), sh, nat.ptr(opt.lr_t),
+                nat.ptr(opt.step_t[slot:]), nat.ptr(skip) if skip is not None else None, opt.betas[0], opt.betas[1],
+                opt.eps, grad_scale, nat.ptr(opt.done[slot:]), cfg, nat.stream_ptr(A.device)), "gemm_wgrad_adam")
+
+
 def gemm_dgrad(dY: torch.Tensor, W: torch.Tensor, out: Optional[torch.Tensor] = None, cfg: int = 0) -> torch.Tensor:
     """dA = dY W, bf16 (dY (M, N), W (N, K) row-major; the reduction runs over N)."""
     M, N = dY.shape

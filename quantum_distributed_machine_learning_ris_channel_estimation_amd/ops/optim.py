@@ -163,6 +163,9 @@ class FusedOptimizer:
             self.m = torch.zeros_like(space.flat)
             self.v = torch.zeros_like(space.flat)
         self._lr_host = lr
+        # (GPU) a range [lo, hi) stepped by ANOTHER kernel (the FC weight, inside its weight-gradient GEMM's
+        # epilogue, ops/fc.gemm_wgrad_adam): every launch here skips it; it has its own step / done slot
+        self.fused: Optional[Tuple[int, int]] = None
         # torch.optim-like view for code that reads/writes param_groups[0]['lr']
         self.param_groups = [_LRGroup(self)]
 
@@ -175,6 +178,19 @@ class FusedOptimizer:
         dev = self.space.flat.device
         self.step_t = self.step_t[:1].repeat(len(self.bounds)).contiguous()
         self.done = torch.zeros(len(self.bounds), device=dev, dtype=torch.int32)
+
+    def fuse_range(self, lo: int, hi: int) -> int:
+        """Hand [lo, hi) (inside ONE part) to an external update kernel; returns the index of its step / done
+        slot (step_t[i], done[i]).  GPU only; Adam without weight decay or pruning, no e4m3 shadow."""
+        if not self.space.flat.is_cuda or self.kind != "adam" or self.weight_decay or self.prune_thr or self.fp8:
+            raise ValueError("fused ranges: GPU Adam (no weight decay / pruning / e4m3 shadow) only")
+        if lo % 4 or hi % 4 or not any(a <= lo and hi <= b for a, b in self.bounds):
+            raise ValueError(f"fused range {(lo, hi)} must be 4-aligned and inside one part of {self.bounds}")
+        self.fused = (lo, hi)
+        dev = self.space.flat.device
+        self.step_t = torch.cat([self.step_t, self.step_t[:1].clone()]).contiguous()
+        self.done = torch.cat([self.done, torch.zeros(1, device=dev, dtype=torch.int32)])
+        return len(self.bounds)
 
     def attach_shadow(self, lo: int, hi: int, fp8: Optional[Fp8Scales] = None, fp8_slot: int = 0) -> torch.Tensor:
         """Keep a bf16 copy of flat[lo:hi] up to date with every step (written by the update
@@ -242,7 +258,10 @@ class FusedOptimizer:
                 self.refresh_shadow()
             return
         f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
-                                         _p, _p, _l, _l, _p, _p, _p, _i, _p, _p])
+                                         _p, _p, _l, _l, _p, _p, _p, _i, _p, _l, _l, _p])
+        hole_lo = hole_n = 0
+        if self.fused is not None and lo <= self.fused[0] and self.fused[1] <= hi:
+            hole_lo, hole_n = self.fused[0] - lo, self.fused[1] - self.fused[0]
         ps = pack(lo, hi) if pack is not None else None
         # the shadow range, clipped to this part and expressed relative to it
         sh_lo, sh_hi = max(self.shadow_lo, lo), min(self.shadow_hi, hi)
@@ -257,7 +276,7 @@ class FusedOptimizer:
                     self.prune_thr, done_p, sh_ptr, (sh_lo - lo) if has_sh else 0, (sh_hi - lo) if has_sh else 0,
                     sh8_ptr, nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
                     nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, int(self.max_grid.get(i, 0)),
-                    ctypes.byref(ps) if ps is not None else None, st),
+                    ctypes.byref(ps) if ps is not None else None, hole_lo, hole_n, st),
                   "adam")
 
     @torch.no_grad()

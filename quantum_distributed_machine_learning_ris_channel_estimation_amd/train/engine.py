@@ -280,6 +280,10 @@ class HDCEStep:
         self.fc_side = None   # optional stream for the FC weight-gradient GEMM (HIP path)
         self.fused_nmse = True  # HIP path: the one-pass NMSE (qd_nmse_fused) when labels come via rowoff
         self.defer_dgrad = False
+        # (world 1, GPU) FusedAdam: the FC weight's Adam step runs in the weight-gradient GEMM's epilogue
+        # (ops/fc.gemm_wgrad_adam) -- dW is never written; the data gradient then runs first (it reads the
+        # bf16 weight copy the fused update rewrites)
+        self.fused_adam = None
         # world-1 plans: the FC bias gradient's column reduction rides in the conv backward's slab launch
         # (never in DP: the FC gradient bucket is all-reduced before the conv backward runs)
         self.bias_via_conv_slabs = False
@@ -435,11 +439,20 @@ class HDCEStep:
                                   cfg=self.gemm_cfg[0])
         if self.stage_hook is not None:
             self.stage_hook("fc")
-        self._wgrad(dY, A)
+        self._fc_backward(dY, A, W)
+        return self.nmse.loss
+
+    def _fc_backward(self, dY: torch.Tensor, A: torch.Tensor, W: torch.Tensor) -> None:
+        """The FC weight gradient (or its fused Adam step) and the data gradient (unless deferred)."""
         self._dYW = (dY, W)
+        if self.fused_adam is not None:
+            assert not self.defer_dgrad
+            self.dgrad()
+            self._wgrad(dY, A)
+            return
+        self._wgrad(dY, A)
         if not self.defer_dgrad:
             self.dgrad()
-        return self.nmse.loss
 
     def _hand_f8_ok(self, A: torch.Tensor) -> bool:
         """The fp8 estimator's forward on the hand-written e4m3 GEMM with the loss epilogue
@@ -522,10 +535,7 @@ class HDCEStep:
             loss = self.nmse.sums_finalize(Y, label, perf)
             dY = self.nmse.grad_bias(Y, label, m.fc_b.grad, out_dtype=dt)   # + bias grad, same pass
         A = A.to(dt)
-        self._wgrad(dY, A)
-        self._dYW = (dY, W)
-        if not self.defer_dgrad:
-            self.dgrad()
+        self._fc_backward(dY, A, W)
         return loss
 
     def _wgrad(self, dY: torch.Tensor, A: torch.Tensor) -> None:
@@ -537,8 +547,15 @@ class HDCEStep:
         hand = ("wgrad" in self.hand_gemm and dY.dtype == A.dtype == torch.bfloat16 and dY.shape[0] % 64 == 0
                 and dY.shape[1] % 128 == 0 and A.shape[1] % 256 == 0)
 
+        fa = self.fused_adam
+        if fa is not None and not hand:
+            raise RuntimeError("the fused FC Adam needs the hand-written weight-gradient GEMM for this shape")
+
         def run():
-            if hand:
+            if fa is not None:
+                from ..ops.fc import gemm_wgrad_adam
+                gemm_wgrad_adam(dY, A, fa["opt"], fa["lo"], fa["slot"], skip=fa["skip"], cfg=self.gemm_cfg[1])
+            elif hand:
                 gemm_wgrad(dY, A, out=m.fc_w.grad, cfg=self.gemm_cfg[1])
             else:
                 _mm_f32(dY.t(), A, m.fc_w.grad)

@@ -92,6 +92,11 @@ class FlagshipConfig:
     stream_mode: str = "dagq"    # serial | dag | dagq (see FlagshipTrainer.__init__)
     hdce_branches: str = ""      # (dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
+    fused_fc_adam: bool = False  # (world 1, GPU, bf16) the FC weight's Adam step in the weight-gradient GEMM's
+    #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
+    #                              separate (profiles/r3_04_fused_adam.txt) -- 256 one-per-CU workgroups stream
+    #                              the Adam state far slower than the 2048-workgroup update kernel
+    #                              (QDML_FUSED_ADAM=1 turns it on)
     dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1), the conv backward (2),
     #                              or its forward half beside the HDCE forward and its backward half beside
     #                              the conv backward (3).  World-1 rehearsal: 0.492 / 0.517 / 0.557 ms;
@@ -230,6 +235,20 @@ class FlagshipTrainer:
         self.hdce_side = "w" in self.branches
         if "a" in self.branches:   # (the FC Adam branch reads the bias gradient before the conv slabs run)
             self.hstep.bias_via_conv_slabs = False
+        # the FC weight's Adam in the weight-gradient GEMM's epilogue (world 1: no gradient collective between)
+        self.fused_adam = bool((cfg.fused_fc_adam or os.environ.get("QDML_FUSED_ADAM") == "1")
+                               and os.environ.get("QDML_FUSED_ADAM") != "0"
+                               and dev.type == "cuda" and ctx.world == 1 and not cfg.split_graphs
+                               and self.hstep.hip and "wgrad" in self.hstep.hand_gemm and not self.hdce.fp8
+                               and cfg.dtype == "bf16" and "a" not in self.branches and len(self.hopt.bounds) == 1
+                               and self.S * self.B % 64 == 0)   # (the hand weight-gradient GEMM's M tiling)
+        if self.fused_adam:
+            lo = sp.offsets[sp.names.index("CE.FC.weight")]
+            slot = self.hopt.fuse_range(lo, lo + self.hdce.fc_w.numel())
+            self.hstep.fused_adam = {"opt": self.hopt, "lo": lo, "slot": slot, "skip": self.hskip}
+            # the fused update reads this step's NaN flag: the loss finish (which sets it) runs right after the
+            # loss pass, not deferred into the conv backward
+            self.hstep.defer_loss = False
         # end-of-step weight pack (GPU fused path)
         self.tail_pack = bool(self.hstep.hip and cfg.tail_pack)
         if self.tail_pack:

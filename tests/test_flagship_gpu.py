@@ -223,3 +223,28 @@ def test_update_kernel_writes_the_conv_weight_images(cuda):
     ref = list(conv.wpk) + [t for t in conv.wpk_t if t is not None]
     for a, b in zip(got, ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_fused_fc_adam_matches_separate_adam(cuda, graphs):
+    """The FC weight's Adam step inside the weight-gradient GEMM's epilogue (dW never written) == the separate
+    gradient GEMM + Adam launch BIT FOR BIT over 4 steps (both apply common.h adam_elem): weights, moments,
+    bf16 shadow, step counters; and a NaN loss skips the fused update too."""
+    ctx = DistContext(device=cuda)
+    base = dict(batch=64, data_len=800, use_quantumnat=False, hip_graphs=graphs)
+    ref = FlagshipTrainer(FlagshipConfig(fused_fc_adam=False, **base), ctx)
+    fus = FlagshipTrainer(FlagshipConfig(fused_fc_adam=True, **base), ctx)
+    assert fus.fused_adam and not ref.fused_adam
+    ref.run(4)
+    fus.run(4)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(_all_state(ref), _all_state(fus))):
+        assert torch.equal(a, b), (i, float((a.float() - b.float()).abs().max()))
+    assert bool((fus.hopt.step_t == 4.0).all()), fus.hopt.step_t
+    before = [t.clone() for t in _all_state(fus)[:7]]   # (weights, moments, shadow: not the BN statistics)
+    fus.store.Yp.fill_(float("nan"))
+    fus.run(1)
+    torch.cuda.synchronize()
+    assert float(fus.hskip) != 0.0
+    for i, (a, b) in enumerate(zip(before, _all_state(fus)[:7])):
+        assert torch.equal(a, b), i   # (the whole HDCE step skipped, the fused FC update included)

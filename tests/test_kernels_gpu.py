@@ -31,7 +31,8 @@ def test_qsim_hip_matches_cpp(cuda, n, L):
     assert torch.allclose(wg.grad.cpu(), wc.grad, atol=5e-4 * max(1, B / 16)), (wg.grad.cpu() - wc.grad).abs().max()
 
 
-@pytest.mark.parametrize("n,L,B", [(11, 3, 9), (12, 3, 7), (13, 2, 5), (14, 3, 4), (16, 3, 3), (16, 8, 2)])
+@pytest.mark.parametrize("n,L,B", [(11, 3, 9), (12, 3, 7), (13, 2, 5), (14, 3, 4), (16, 3, 3), (16, 8, 2),
+                                   (12, 3, 1000), (11, 2, 800)])
 def test_qsim_big_hip_matches_cpp(cuda, n, L, B):
     """Workgroup-per-sample kernels (qsim_big.hip): LDS-resident (n<=12 bwd, n<=13 fwd) and HBM paths."""
     g = torch.Generator().manual_seed(7 * n + L)
@@ -332,7 +333,7 @@ def test_nmse_fused_matches_two_pass(cuda, with_perf):
     assert float(b.skip) == 1.0
 
 
-@pytest.mark.parametrize("n,L,B", [(12, 3, 7), (14, 3, 5), (16, 2, 3), (13, 1, 4)])
+@pytest.mark.parametrize("n,L,B", [(12, 3, 7), (14, 3, 5), (16, 2, 3), (13, 1, 4), (12, 3, 1100)])
 def test_qsim_big_saved_state_backward(cuda, n, L, B):
     """qsim_big with the forward's psi_final kept for the adjoint backward (no recompute) == the
     recomputing backward: same E, dx and weight-gradient slab (to fp32 rounding: the fused forward
