@@ -30,6 +30,14 @@ struct cf {
 __device__ __forceinline__ cf cmul(cf a, cf b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 
 constexpr int NT = 256;   // 4 waves: lets the backward use AGPRs instead of scratch (512-thread groups spilled)
+// waves per SIMD the register allocation must allow (launch-bounds hint; the n <= 12 LDS state fits 4 forward /
+// 2 backward workgroups per CU)
+#ifndef QD_BIG_FWD_WAVES
+#define QD_BIG_FWD_WAVES 4
+#endif
+#ifndef QD_BIG_BWD_WAVES
+#define QD_BIG_BWD_WAVES 2
+#endif
 constexpr int NW = NT / 64;
 
 template <int N>
@@ -42,6 +50,11 @@ struct G {
   static constexpr int NGRP = (TB + 2) / 3;    // 3-qubit groups of the low pass
   static constexpr bool LDS_STATE = N <= 12;
 };
+
+// LDS carve (bytes): reduction scratch | trig (<= 16 float4) | gE (16) | acc (2nL <= 256) + per-sample
+// layer-0 scratch (2n <= 32) | phase table PI (n <= 12: <= 16 complex) | data (tiles, or the whole state
+// when n <= 12).
+constexpr int O_RED = 0, O_TRIG = 2048, O_G = 2304, O_ACC = 2368, O_TMP = 3392, O_PHI = 3584, O_DATA = 3712;
 
 template <int N>
 __device__ __forceinline__ int ring_fwd(int k) {
@@ -211,6 +224,99 @@ __device__ void ring_fwd_inplace(cf* A) {
   __syncthreads();
 }
 
+// ---- n <= 12 (LDS-resident, no high qubits): the diagonal-RZ formulation (round 3) -------------------------
+// The 2n gates of a layer act on n DIFFERENT wires, so they commute: layer = D . Y with Y = prod_q RY_q (real
+// 2x2 rotations of amplitude pairs) and D = prod_q RZ_q = diag_k prod_q e^{+-i phi_q / 2} (+ for bit_q(k) = 1).
+// The forward applies Y in the 3-qubit register groups WITHOUT phases and D once per amplitude, inside the
+// in-place ring pass -- where thread t holds amplitudes c = t + i * NT (bits 0..7 = t, bits 8.. = i), so
+// D(c) = PT(t) * PI(i): one per-thread factor and a PER-entry table.  The adjoint takes every phi_q gradient
+// Im<lam|Z_q|psi> at ONE point (after the layer, before the ring: Z_q commutes with the layer's other gates),
+// undoes D on psi and lambda there, then every theta_q gradient Im<lam|Y_q|psi> inside the RY-only reverse
+// groups (Y_q commutes with every RY of the layer).  Per amplitude and layer: ~60 (forward) and ~140
+// (adjoint) vector operations instead of ~110 and ~250 with per-gate RZ phases.
+
+__device__ __forceinline__ cf rz_factor(float4 t, bool one) { return one ? cf{t.z, t.w} : cf{t.z, -t.w}; }
+
+// PI(i) = prod over the qubits 8.. of rz_factor(bit of i) for i < PER (threads < PER; trig must be visible)
+template <int N>
+__device__ __forceinline__ void phase_table(cf* phi, const float4* trig) {
+  constexpr int PER = G<N>::D / NT;
+  if (threadIdx.x < PER) {
+    cf p = {1.f, 0.f};
+#pragma unroll
+    for (int b = 0; 8 + b < N; ++b) p = cmul(p, rz_factor(trig[8 + b], (threadIdx.x >> b) & 1));
+    phi[threadIdx.x] = p;
+  }
+}
+// PT(t): this thread's factor over qubits 0..7
+__device__ __forceinline__ cf phase_thread(const float4* trig) {
+  cf p = {1.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) p = cmul(p, rz_factor(trig[q], (threadIdx.x >> q) & 1));
+  return p;
+}
+
+// forward RY on the pair (bit 0: a0, bit 1: a1)
+__device__ __forceinline__ void ry_fwd(cf& a0, cf& a1, float c, float s) {
+  const cf t0 = {c * a0.x - s * a1.x, c * a0.y - s * a1.y};
+  a1 = {s * a0.x + c * a1.x, s * a0.y + c * a1.y};
+  a0 = t0;
+}
+// adjoint RY step: theta gradient Im<lam|Y|psi> of the pair, then RY^-1 on psi and lambda
+__device__ __forceinline__ void ry_adj(cf& p0, cf& p1, cf& l0, cf& l1, float c, float s, float& dth) {
+  dth += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+  const cf q0 = p0, m0 = l0;
+  p0 = {c * q0.x + s * p1.x, c * q0.y + s * p1.y};
+  p1 = {c * p1.x - s * q0.x, c * p1.y - s * q0.y};
+  l0 = {c * m0.x + s * l1.x, c * m0.y + s * l1.y};
+  l1 = {c * l1.x - s * m0.x, c * l1.y - s * m0.y};
+}
+
+// RY of every qubit on the LDS state A, three qubits per register round trip (no phases: see above)
+template <int N>
+__device__ void low_pass_ry(cf* A, const float4* trig) {
+  using C = G<N>;
+  static_for<0, C::NGRP>([&](auto gc) {
+    constexpr int g0 = 3 * decltype(gc)::value;
+    constexpr int NB = (C::TB - g0) < 3 ? (C::TB - g0) : 3;
+    constexpr int ACT = C::T >> NB;
+    float cs[NB], sn[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      cs[b] = trig[g0 + b].x;
+      sn[b] = trig[g0 + b].y;
+    }
+    for (int t = threadIdx.x; t < ACT; t += NT) {
+      const int base = ins_bits<g0, NB>(t);
+      cf a[1 << NB];
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) a[j] = A[base | (j << g0)];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j)
+          if (!((j >> b) & 1)) ry_fwd(a[j], a[j | (1 << b)], cs[b], sn[b]);
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) A[base | (j << g0)] = a[j];
+    }
+    __syncthreads();
+  });
+}
+
+// D (the layer's RZ phases), then the CNOT ring, in place: A'[f(c)] = D(c) A[c]
+template <int N>
+__device__ void ring_phase_fwd(cf* A, const float4* trig, const cf* phi) {
+  constexpr int PER = G<N>::D / NT;
+  const cf pt = phase_thread(trig);
+  cf a[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) a[i] = cmul(A[threadIdx.x + i * NT], cmul(pt, phi[i]));
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PER; ++i) A[ring_fwd<N>(threadIdx.x + i * NT)] = a[i];
+  __syncthreads();
+}
+
 // Low pass of layer 1 with the layer-0 product state GENERATED per tile (HBM-state builds): the
 // product amplitudes are never written to and re-read from HBM.  trig0: layer-0 (embedding) trig.
 template <int N>
@@ -292,12 +398,14 @@ __device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs
   layer_trig(trig, w, xs, N);
   __syncthreads();
   product_pass<N>(A, trig);
-  if constexpr (G<N>::HB == 0 && G<N>::LDS_STATE) {   // (one buffer: see ring_fwd_inplace)
+  if constexpr (G<N>::HB == 0 && G<N>::LDS_STATE) {   // (one buffer, diagonal RZ: see low_pass_ry)
+    cf* phi = reinterpret_cast<cf*>(reinterpret_cast<char*>(trig) - O_TRIG + O_PHI);
     for (int l = 1; l < L; ++l) {
       layer_trig(trig, w + 2 * N * l, nullptr, N);
       __syncthreads();
-      low_pass_fwd<N>(A, tile, trig);
-      ring_fwd_inplace<N>(A);
+      phase_table<N>(phi, trig);
+      low_pass_ry<N>(A, trig);   // (its barriers publish phi)
+      ring_phase_fwd<N>(A, trig, phi);
     }
     return A;
   }
@@ -319,14 +427,11 @@ __device__ cf* run_circuit(cf* A, cf* B, cf* tile, float4* trig, const float* xs
 }
 
 // ------------------------------------------------------------------------------- kernels
-// LDS carve (bytes): reduction scratch | trig (<= 16 float4) | gE (16) | acc (2nL <= 256) + per-
-// sample layer-0 scratch (2n <= 32) | data (tiles, or the whole state when n <= 12).
-constexpr int O_RED = 0, O_TRIG = 2048, O_G = 2304, O_ACC = 2368, O_TMP = 3392, O_DATA = 3584;
 
 template <int N>
 // psave (nullable): (B, 2^N) per-sample psi_final, kept for the backward (which then skips its
 // forward recompute: ~1/3 of its state traffic at n = 16)
-__global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ void __launch_bounds__(NT, G<N>::LDS_STATE ? QD_BIG_FWD_WAVES : 1) qsim_big_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           float* __restrict__ E, int B, int L, int wgroup,
                                                           cf* __restrict__ ws, cf* __restrict__ psave) {
   using C = G<N>;
@@ -401,7 +506,7 @@ __global__ void __launch_bounds__(NT) qsim_big_fwd_kernel(const float* __restric
 // psave (nullable): psi_final of every sample from qsim_big_fwd_kernel (same x, w); the backward
 // starts from it instead of re-running the circuit (the buffer is consumed: it may be overwritten)
 template <int N>
-__global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+__global__ void __launch_bounds__(NT, G<N>::LDS_STATE ? QD_BIG_BWD_WAVES : 1) qsim_big_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ gE, float* __restrict__ dx,
                                                           float* __restrict__ slab, int B, int L, int wgroup,
                                                           cf* __restrict__ ws, cf* __restrict__ psave) {
@@ -464,10 +569,23 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
       // layer-0 gradients go to the per-sample scratch first (their theta part is also dx)
       float* gdst = (l == 0) ? tmp : acc + 2 * N * l;
       const bool first = (l == L - 1);   // lambda = O psi formed on the fly
+      constexpr bool DIAG = C::HB == 0 && C::LDS_STATE;   // (the diagonal-RZ adjoint: phi gradients in dph_l)
+      float dph_l[N];
+#pragma unroll
+      for (int q = 0; q < N; ++q) dph_l[q] = 0.f;
       // ---- high pass (reverse): gather psi/lam at f(k) (inverse ring), undo high rotations
-      if constexpr (C::HB == 0 && C::LDS_STATE) {   // the bare inverse ring, in place (ring_fwd_inplace)
+      if constexpr (C::HB == 0 && C::LDS_STATE) {
+        // diagonal-RZ adjoint (see low_pass_ry): gather psi / lam at the ring images (the point after the
+        // layer), every phi gradient there, undo D on both, store in place; then the RY-only reverse groups
         constexpr int PER = C::D / NT;
+        cf* phi = reinterpret_cast<cf*>(smem + O_PHI);
+        phase_table<N>(phi, trig);
+        __syncthreads();
+        const cf pt = phase_thread(trig);
         cf p[PER], m[PER];
+        float wsum = 0.f, whi[N > 8 ? N - 8 : 1];
+#pragma unroll
+        for (int b = 0; 8 + b < N; ++b) whi[b] = 0.f;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
           const int src = ring_fwd<N>(threadIdx.x + i * NT);
@@ -480,7 +598,20 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
           } else {
             m[i] = lam[src];
           }
+          // Im<lam|Z_q|psi> summand (sign + for bit_q = 0): qubits 0..7 are this thread's fixed bits
+          const float wv = m[i].x * p[i].y - m[i].y * p[i].x;
+          wsum += wv;
+#pragma unroll
+          for (int b = 0; 8 + b < N; ++b) whi[b] += ((i >> b) & 1) ? -wv : wv;
+          const cf dc = cmul(pt, phi[i]);
+          const cf dinv = {dc.x, -dc.y};
+          p[i] = cmul(p[i], dinv);
+          m[i] = cmul(m[i], dinv);
         }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) dph_l[q] = ((threadIdx.x >> q) & 1) ? -wsum : wsum;
+#pragma unroll
+        for (int b = 0; 8 + b < N; ++b) dph_l[8 + b] = whi[b];
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
@@ -574,8 +705,10 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
                 const float4 tg = trig[g0 + b];
 #pragma unroll
                 for (int j = 0; j < (1 << NB); ++j)
-                  if (!((j >> b) & 1))
-                    gate_adj(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[g0 + b], dph[g0 + b]);
+                  if (!((j >> b) & 1)) {
+                    if constexpr (DIAG) ry_adj(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg.x, tg.y, dth[g0 + b]);
+                    else gate_adj(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[g0 + b], dph[g0 + b]);
+                  }
               }
 #pragma unroll
               for (int j = 0; j < (1 << NB); ++j) {
@@ -601,7 +734,8 @@ __global__ void __launch_bounds__(NT) qsim_big_bwd_kernel(const float* __restric
 #pragma unroll
         for (int q = 0; q < C::TB; ++q) {
           v[2 * q] = dth[q];
-          v[2 * q + 1] = dph[q];
+          if constexpr (DIAG) v[2 * q + 1] = dph_l[q];
+          else v[2 * q + 1] = dph[q];
         }
         block_add<2 * C::TB>(v, red, gdst, 0);
       }
