@@ -228,6 +228,16 @@ class FlagshipTrainer:
         else:
             mode = "serial"
         self.mode = mode
+        # (experiment) spatial partitioning: QDML_QSC_CUS / QDML_MAIN_CUS = CU sets (ops/streams.py:parse_cus)
+        # for the QSC branch's stream and for the stream the step is launched on
+        self.main_stream = None
+        if dev.type == "cuda" and (os.environ.get("QDML_QSC_CUS") or os.environ.get("QDML_MAIN_CUS")):
+            from ..ops import streams as cus
+            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+            if os.environ.get("QDML_QSC_CUS") and self.streams is not None:
+                self.streams["qsc"] = cus.masked_stream(cus.parse_cus(os.environ["QDML_QSC_CUS"], n_cu), dev)
+            if os.environ.get("QDML_MAIN_CUS"):
+                self.main_stream = cus.masked_stream(cus.parse_cus(os.environ["QDML_MAIN_CUS"], n_cu), dev)
         # HDCE side branches: w = FC weight-gradient GEMM, c = conv weight-gradient kernels, a = FC Adam
         self.branches = set("wca") if mode == "dag" else set(cfg.hdce_branches)
         if self.streams is None:
@@ -695,6 +705,16 @@ class FlagshipTrainer:
             self._replay(kk, fence=i == len(reps) - 1)
 
     def _replay(self, k: int, fence: bool = True) -> None:
+        if self.main_stream is not None:
+            cur = torch.cuda.current_stream(self.ctx.device)
+            self.main_stream.wait_stream(cur)
+            with torch.cuda.stream(self.main_stream):
+                self._replay_on(k, fence)
+            cur.wait_stream(self.main_stream)
+            return
+        self._replay_on(k, fence)
+
+    def _replay_on(self, k: int, fence: bool) -> None:
         gs = self._graphs_for(k)
         if any(g.enabled and g.graph is None for g in gs):
             # (preserve: the capture warm-ups run optimizer steps on rank-local gradients; restoring
