@@ -60,6 +60,11 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
   return v;
 }
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+  return v;
+}
 
 // Block-wide sum for blockDim.x == NT (multiple of 64); result valid in every thread.
 template <int NT>

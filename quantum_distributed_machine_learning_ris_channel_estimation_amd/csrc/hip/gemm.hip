@@ -53,15 +53,21 @@ namespace gemm {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) short v4s;
+typedef __attribute__((ext_vector_type(8))) int v8i;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
-enum { KC = 0, MC = 1 };
+enum { KC = 0, MC = 1, MC8 = 2 };
 enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2, EPI_ADAM = 3 };
 constexpr int BK = 64;
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
 __device__ __forceinline__ int mc_swt(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+// MC8 (e4m3, i-contiguous) image: [panel of 128 columns][128 k-rows][128 B], 16-byte chunk c of k-row k at slot
+// c ^ s8(k).  A fragment is four ds_read_b64_tr_b8 (lane 2q + p of a 16-lane group addresses k-row q, bytes
+// 8p .. 8p + 7 of a 16-byte column block; lane i receives column i of the 8 rows -- measured,
+// scripts/probe_tr_b8.py); with s8 the 16 k-rows a 32-lane half reads land on 16 distinct 4-bank groups.
+__device__ __forceinline__ int s8_swz(int k) { return ((k >> 1) & 3) | (((k >> 4) & 1) << 2); }
 
 struct NmseArgs {
   const float* label;      // (rows of the store, N) fp32, row rowoff[r]
@@ -74,6 +80,12 @@ struct NmseArgs {
   float* dens;             // (S, 2): per-stream (sum |label|^2, sum |perf|^2)
   int E, U, B;             // row r = (u*B + b)*E + e, stream s = e*U + u
   float loss_scale;
+  // (fp8 backward, nullable) dY also as e4m3 -- row-major dY8 (M, N) and transposed dYt8 (N, M) -- quantised
+  // with the delayed factor *qs8; the workgroup's max |dY| goes to amax8[blockIdx.x] (fp8 scale partials)
+  uint8_t* dY8;
+  uint8_t* dYt8;
+  const float* qs8;
+  float* amax8;
 };
 
 // EPI_ADAM (the weight gradient at world 1): the FC weight's Adam step applied to the gradient tile straight
@@ -98,6 +110,11 @@ struct AdamEpi {
 // values is K / 2 of them), so staging, LDS images and fragment reads are the bf16 ones unchanged; each
 // 16-byte fragment holds 16 k and feeds TWO mfma_f32_16x16x32_fp8_fp8 (its low and high 8 bytes).  The
 // k order this implies is the same permutation for A and B, so the dot products are exact sums over K.
+// F8 = 2 (MX): the same e4m3 staging, but a fragment is 32 bytes (the two 16-byte chunks fq and 4 + fq of a row,
+// i.e. both sub-steps of a K step = 128 k) feeding ONE v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales
+// (e8m0 127): twice the MFMA rate of the non-scaled fp8 / bf16 forms.  A and B fragments take their k in the same
+// lane / byte order, so the product is again an exact sum over K.  A whole K step per fragment set: the K loop
+// is the KS = 2 one (one barrier and one woven fragment read per K step).
 // KS: waves along K inside the workgroup.  KS = 2 doubles the waves (2 per SIMD) without shrinking the
 // per-wave output tile: wave group wk computes sub-step wk (32 k) of every K step, the two partial tiles
 // are summed (in a fixed order) in the epilogue.  Each SIMD then interleaves two waves' MFMA, LDS-read,
@@ -106,8 +123,13 @@ template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int
 struct Geo {
   static constexpr int MF = MF_, NJ = NJ_, WM = WM_, WN = WN_, LA = LA_, LB = LB_, NSTAGE = NSTAGE_, DBG = DBG_;
   static constexpr int F8 = F8_, KS = KS_;
-  static_assert(!F8 || (LA == KC && LB == KC), "e4m3 operands: k-contiguous layouts");
+  static_assert(!F8 || ((LA == KC || (F8 == 2 && LA == MC8)) && (LB == KC || (F8 == 2 && LB == MC8))),
+                "e4m3 operands: k-contiguous layouts (MX: also MC8)");
+  static_assert((LA != MC8 && LB != MC8) || F8 == 2, "MC8 = e4m3 operands");
   static_assert(KS == 1 || KS == 2, "KS");
+  static_assert(F8 != 2 || KS == 1, "MX fragments already span the K step");
+  static constexpr bool MX = F8 == 2;
+  static constexpr bool STEP_LOOP = KS == 2 || MX;   // one fragment set per K step (see gemm_kernel)
   static constexpr int NW = WM * WN * KS, NT = 64 * NW;
   static constexpr int BM = 16 * MF * WM, BN = 16 * NJ * WN;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -132,11 +154,16 @@ __device__ __forceinline__ const uint16_t* piece_src(const uint16_t* __restrict_
     const int ch = (lane & 7) ^ (row & 7);
     const size_t src_row = expert ? (size_t)(r0 + row) * re + expert[r0 + row] : (size_t)(r0 + row);
     return X + src_row * ld + k0 + ch * 8;
-  } else {
+  } else if constexpr (L == MC) {
     const int panel = q >> 4;
     const int kr = ((q & 15) << 2) + (lane >> 4);
     const int ch = (lane & 15) ^ mc_swt(kr);
     return X + (size_t)(k0 + kr) * ld + r0 + panel * 128 + ch * 8;
+  } else {   // MC8: X, ld, r0 in 2-byte units of an e4m3 (k, i) matrix; piece = 8 k-rows x 128 bytes of a panel
+    const int panel = q >> 4;
+    const int kr = ((q & 15) << 3) + (lane >> 3);
+    const int ch = (lane & 7) ^ s8_swz(kr);
+    return X + (size_t)(k0 + kr) * ld + r0 / 2 + panel * 64 + ch * 8;
   }
 }
 
@@ -158,6 +185,12 @@ template <int OFF>
 __device__ __forceinline__ bf16x8 lds_b128(uint32_t addr) {
   bf16x8 r;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ long lds_tr8(uint32_t addr) {
+  long r;
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF) : "memory");
   return r;
 }
 template <int OFF>
@@ -188,12 +221,35 @@ struct Reader {
 #pragma unroll
       for (int s = 0; s < 2; ++s) base[s] = img + (r0w + fr) * 128 + (((4 * s + fq) ^ (fr & 7)) << 4);
       x = 0;
+    } else if constexpr (L == MC8) {
+      // k-rows 16 fq + q (+ 8, + 64, + 72 for the fragment's other three reads), bytes 8p of the column block
+      const int q = fr >> 1, p = fr & 1;
+      base[0] = base[1] = img + (16 * fq + q) * 128 + 8 * p;
+      x = (uint32_t)(((q >> 1) & 3) | ((fq & 1) << 2));   // = s8_swz of every k-row this lane addresses
     } else {
       const int q = fr >> 2, p = fr & 3;
 #pragma unroll
       for (int s = 0; s < 2; ++s) base[s] = img + (32 * s + 8 * fq + q) * 256 + 8 * (p & 1) + 16 * (p >> 1);
       x = (uint32_t)mc_swt(8 * fq + q) << 4;
     }
+  }
+  // MX: fragment f of the whole K step (KC): chunks fq and 4 + fq of the lane's row, 32 bytes
+  template <int F>
+  __device__ __forceinline__ v8i frag32(uint32_t st) const {
+    if constexpr (L == MC8) {
+      // k order as the KC fragment's: bytes 0..15 = k 16 fq .., bytes 16..31 = k 64 + 16 fq ..
+      const int r = r0w + 16 * F;
+      const uint32_t a = st + base[0] + (r >> 7) * 16384 + ((((uint32_t)(r & 127) >> 4) ^ x) << 4);
+      typedef __attribute__((ext_vector_type(4))) long v4l;
+      const v4l v = {lds_tr8<0>(a), lds_tr8<1024>(a), lds_tr8<8192>(a), lds_tr8<9216>(a)};
+      return __builtin_bit_cast(v8i, v);
+    }
+    static_assert(L == KC || L == MC8, "MX fragments: KC or MC8 images");
+    const bf16x8 lo = lds_b128<F * 2048>(st + base[0]);
+    const bf16x8 hi = lds_b128<F * 2048>(st + base[1]);
+    typedef __attribute__((ext_vector_type(4))) int v4i;
+    const v4i l4 = __builtin_bit_cast(v4i, lo), h4 = __builtin_bit_cast(v4i, hi);
+    return __builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
   }
   // fragment f of sub-step s in the stage at byte offset st
   template <int F>
@@ -214,28 +270,32 @@ struct Reader {
 
 template <class G>
 struct Frags {
-  bf16x8 a[G::MF], b[G::NJ];
+  using T = std::conditional_t<G::MX, v8i, bf16x8>;
+  T a[G::MF], b[G::NJ];
 };
 
 template <class G>
 struct Readers {
   Reader<G::LA> ra;
   Reader<G::LB> rb;
-  static constexpr int RA = G::LA == KC ? 1 : 2, RB = G::LB == KC ? 1 : 2;   // ds_read instrs per fragment
+  static constexpr int RA = G::LA == MC8 ? 4 : (G::LA == KC && !G::MX) ? 1 : 2;   // ds_reads per fragment
+  static constexpr int RB = G::LB == MC8 ? 4 : (G::LB == KC && !G::MX) ? 1 : 2;
   // LDS reads that may stay in flight when an MFMA group of the woven schedule starts (see mma_read)
   static constexpr int ALLOW = (G::MF - 1) * RA + G::NJ * RB;
 
   template <int J = 0>
   __device__ __forceinline__ void read_b(Frags<G>& f, uint32_t st, int s) const {
     if constexpr (J < G::NJ) {
-      f.b[J] = rb.template frag<J>(st, s);
+      if constexpr (G::MX) f.b[J] = rb.template frag32<J>(st);
+      else f.b[J] = rb.template frag<J>(st, s);
       read_b<J + 1>(f, st, s);
     }
   }
   template <int I = 0>
   __device__ __forceinline__ void read_a(Frags<G>& f, uint32_t st, int s) const {
     if constexpr (I < G::MF) {
-      f.a[I] = ra.template frag<I>(st, s);
+      if constexpr (G::MX) f.a[I] = ra.template frag32<I>(st);
+      else f.a[I] = ra.template frag<I>(st, s);
       read_a<I + 1>(f, st, s);
     }
   }
@@ -254,6 +314,9 @@ struct Readers {
       for (int j = 0; j < G::NJ; ++j)
         if constexpr (G::DBG == 2) {
           asm volatile("" ::"v"(cur.a[I]), "v"(cur.b[j]));
+        } else if constexpr (G::MX) {
+          // (e4m3 x e4m3, unit e8m0 block scales)
+          acc[I][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(cur.a[I], cur.b[j], acc[I][j], 0, 0, 0, 127, 0, 127);
         } else if constexpr (G::F8) {
           typedef __attribute__((ext_vector_type(2))) long l2;
           const l2 av = __builtin_bit_cast(l2, cur.a[I]), bv = __builtin_bit_cast(l2, cur.b[j]);
@@ -263,7 +326,10 @@ struct Readers {
           acc[I][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.a[I], cur.b[j], acc[I][j], 0, 0, 0);
         }
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (READ) nxt.a[I] = ra.template frag<I>(st, s);
+      if constexpr (READ) {
+        if constexpr (G::MX) nxt.a[I] = ra.template frag32<I>(st);
+        else nxt.a[I] = ra.template frag<I>(st, s);
+      }
       mma_read<READ, I + 1>(acc, cur, nxt, st, s);
     }
   }
@@ -290,7 +356,9 @@ struct Stager {
       const uint16_t* sb = piece_src<G::LB>(Qm, ldq, j0, 0, isA ? 0 : qq, lane);
       src[it] = isA ? sa : sb;
       dst[it] = isA ? q * 1024 : G::A_BYTES + qq * 1024;
-      const int la = G::LA == KC ? BK : BK * ldp, lb = G::LB == KC ? BK : BK * ldq;
+      // (MC8: a K step is 128 k-rows of bytes = 2 BK rows)
+      const int la = G::LA == KC ? BK : (G::LA == MC8 ? 2 : 1) * BK * ldp;
+      const int lb = G::LB == KC ? BK : (G::LB == MC8 ? 2 : 1) * BK * ldq;
       adv[it] = isA ? la : lb;
     }
   }
@@ -316,6 +384,7 @@ struct Args {
   int pe;
   const float* deq;     // nullable: (2,) dequantisation scales; the accumulators are multiplied by their product
   AdamEpi ad;           // EPI_ADAM
+  const float* deq2;    // nullable: with deq, the scales are deq[0] and deq2[0] (two separate scale slots)
 };
 
 // tile order: blocks b, b+8, ... share an XCD; each XCD takes whole GM x GN tile groups (row-major
@@ -367,7 +436,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
   __builtin_amdgcn_s_barrier();
   Frags<G> f0, f1;
-  if constexpr (G::KS == 1) {
+  if constexpr (!G::STEP_LOOP) {
     rd.read_b(f0, lds0, 0);
     rd.read_a(f0, lds0, 0);
 
@@ -395,8 +464,10 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     // t+1's fragments read in between.  Two steps per loop iteration keep the fragment sets static.
     // (the wave's sub-step becomes sub-step 0 of its readers: a runtime index into base[] would put the
     // readers in scratch -- guide §5.4 rule 20)
-    rd.ra.base[0] = wk ? rd.ra.base[1] : rd.ra.base[0];
-    rd.rb.base[0] = wk ? rd.rb.base[1] : rd.rb.base[0];
+    if constexpr (G::KS == 2) {
+      rd.ra.base[0] = wk ? rd.ra.base[1] : rd.ra.base[0];
+      rd.rb.base[0] = wk ? rd.rb.base[1] : rd.rb.base[0];
+    }
     constexpr int sk = 0;
     rd.read_b(f0, lds0, sk);
     rd.read_a(f0, lds0, sk);
@@ -423,7 +494,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   __syncthreads();   // (every wave is done with the stage ring: it becomes the fp32 tile)
   float* ct = reinterpret_cast<float*>(smem);
   constexpr int PITCH = G::PITCH;
-  const float dq = a.deq ? a.deq[0] * a.deq[1] : 1.f;
+  const float dq = a.deq ? a.deq[0] * (a.deq2 ? a.deq2[0] : a.deq[1]) : 1.f;
   // (KS = 2: wave group 0 stores its partial tile, group 1 adds its own -- a fixed summation order)
 #pragma unroll
   for (int kk = 0; kk < G::KS; ++kk) {
@@ -548,6 +619,8 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     __syncthreads();
     float2* rsum = reinterpret_cast<float2*>(red + 64 + G::NW * 128);   // per-row (err^2, errperf^2)
     float cs0 = 0.f, cs1 = 0.f;
+    const float q8 = na.dY8 != nullptr ? *na.qs8 : 0.f;
+    float mx8 = 0.f;
     constexpr int RU = G::BM % (G::NW * 12) == 0 ? 12 : G::BM % (G::NW * 9) == 0 ? 9 : 6;   // rows per batch
     static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
     for (int r0 = wave * RU; r0 < G::BM; r0 += G::NW * RU) {
@@ -579,6 +652,12 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
         cs1 += g1;
         *reinterpret_cast<uint32_t*>(na.dY + (size_t)row * N + j0 + c0) =
             (uint32_t)f32_to_bf16(g0) | ((uint32_t)f32_to_bf16(g1) << 16);
+        if (na.dY8 != nullptr) {
+          mx8 = fmaxf(mx8, fmaxf(fabsf(g0), fabsf(g1)));
+          *reinterpret_cast<uint16_t*>(na.dY8 + (size_t)row * N + j0 + c0) =
+              (uint16_t)(e4m3_pack4(g0 * q8, g1 * q8, 0.f, 0.f) & 0xffffu);
+          *reinterpret_cast<float2*>(ct + (r0 + q) * PITCH + c0) = make_float2(g0, g1);   // (for the dYt8 pass)
+        }
         se = wave_sum(se);
         sp = wave_sum(sp);
         if (lane == 0) rsum[r0 + q] = make_float2(se, sp);
@@ -586,6 +665,33 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     }
     // column sums of dY over the tile: the waves' partials combined in a fixed order
     __syncthreads();
+    if (na.dYt8 != nullptr) {
+      // the tile's dY (now in ct) transposed: column j -> 16-byte runs of dYt8 row j0 + j (lanes take consecutive
+      // columns: conflict-free LDS reads)
+      const int M = a.I;
+      for (int it = tid; it < G::BN * (G::BM / 16); it += G::NT) {
+        const int j = it % G::BN, g = it / G::BN;
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float* cp = ct + (g * 16 + 4 * k) * PITCH + j;
+          w[k] = e4m3_pack4(cp[0] * q8, cp[PITCH] * q8, cp[2 * PITCH] * q8, cp[3 * PITCH] * q8);
+        }
+        *reinterpret_cast<uint4*>(na.dYt8 + (size_t)(j0 + j) * M + i0 + g * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+    if (na.amax8 != nullptr) {   // (scratch after rsum; one partial per workgroup)
+      float* wm = red + 64 + G::NW * 128 + 2 * G::BM;
+      const float m = wave_max(mx8);
+      if (lane == 0) wm[wave] = m;
+      __syncthreads();
+      if (tid == 0) {
+        float b = 0.f;
+#pragma unroll
+        for (int w = 0; w < G::NW; ++w) b = fmaxf(b, wm[w]);
+        na.amax8[blockIdx.x] = fmaxf(na.amax8[blockIdx.x], b);
+      }
+    }
     // row error partials -> per (chunk of 16 samples, e) sums in a fixed order: part (M / CR, gx, E, 2)
     const int CR = 16 * E;
     for (int sl = tid; sl < (G::BM / CR) * E; sl += G::NT) {
@@ -617,7 +723,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
 template <class G, int EPI, int GM, int GN>
 int launch(const Args& a, hipStream_t st) {
   if (a.I % G::BM || a.J % G::BN || a.K % BK || a.K < BK) return (int)hipErrorInvalidValue;
-  if (G::KS == 2 && (a.K / BK) % 2) return (int)hipErrorInvalidValue;   // (the KS = 2 loop runs K steps in pairs)
+  if (G::STEP_LOOP && (a.K / BK) % 2) return (int)hipErrorInvalidValue;   // (that loop runs K steps in pairs)
   auto kern = &gemm_kernel<G, EPI, GM, GN>;
   static bool attr = false;
   if (!attr) {
@@ -641,6 +747,10 @@ using DgrB = Geo<9, 2, 1, 4, KC, MC, 4>;
 using WgrA = Geo<8, 4, 1, 4, MC, MC, 3>;
 using WgrB = Geo<4, 4, 2, 4, MC, MC, 3>;
 using FwdA8 = Geo<9, 2, 1, 4, KC, KC, 4, 0, 1>;   // e4m3 forward: the FwdA geometry, 128 k per stage
+using FwdM8 = Geo<9, 2, 1, 4, KC, KC, 4, 0, 2>;   // e4m3 forward on the MX-scaled MFMA (unit scales)
+using WgrM8 = Geo<4, 4, 2, 4, KC, KC, 3, 0, 2>;   // e4m3 128 x 256 tiles, 8 waves (2 x 4): the transposed-operand wgrad
+using WgrM8C = Geo<4, 4, 2, 4, MC8, MC8, 3, 0, 2>;  // e4m3 wgrad straight from the row-major dY8 and A8 (no copies)
+using DgrM8C = Geo<9, 2, 1, 4, KC, MC8, 4, 0, 2>;   // e4m3 dgrad from dY8 and the row-major W8 (144 x 128 tiles)
 // two waves per SIMD (round 3): the same output tiles, K split over two wave groups (KS = 2), or 8 waves
 // along N
 using FwdC = Geo<9, 2, 1, 4, KC, KC, 4, 0, 0, 2>;   // fwd 144 x 128, 8 waves (1 x 4 x K2)
@@ -736,28 +846,114 @@ QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, in
 
 // e4m3 forward with the HDCE-loss epilogue: A8 (M, K) e4m3 activations, W8 (N, K) e4m3 weights (both
 // row-major, K bytes per row), deq (2,) their dequantisation scales (the accumulators are scaled by the
-// product before the bias); everything else as qd_gemm_fwd_nmse.
+// product before the bias); everything else as qd_gemm_fwd_nmse.  cfg 0: non-scaled fp8 MFMA (bf16 rate),
+// 1: MX-scaled MFMA with unit scales (2x that rate; K % 256 == 0).
+// dY8 / qs8 / amax8 (nullable, all or none; dYt8 nullable): dY also as e4m3 (row-major, and transposed when dYt8)
+// for the fp8 backward GEMMs, quantised with *qs8, max |dY| partials in amax8 (one per workgroup).
 QD_API int qd_gemm_fwd_nmse_f8(const uint8_t* A8, const uint8_t* W8, const float* deq, const uint16_t* bias,
                                const float* label, const float* perf, const int* rowoff, const float* rowden,
                                uint16_t* dY, float* part, float* colsum, float* dens, int M, int N, int K, int E, int U,
-                               int B, float loss_scale, void* stream) {
+                               int B, float loss_scale, int cfg, uint8_t* dY8, uint8_t* dYt8, const float* qs8,
+                               float* amax8, void* stream) {
   if (M != U * B * E || E < 1 || E > 4 || K % 128 || !deq) return (int)hipErrorInvalidValue;
+  if ((dYt8 != nullptr && dY8 == nullptr) || (dY8 != nullptr && (!qs8 || !amax8 || M % 16)))
+    return (int)hipErrorInvalidValue;
   NmseArgs na{label, perf, rowoff, reinterpret_cast<const float2*>(rowden), dY, part, colsum, dens, E, U, B,
-              loss_scale};
+              loss_scale, dY8, dYt8, qs8, amax8};
   const int K2 = K / 2;   // 2-byte units of an e4m3 row
   Args a{reinterpret_cast<const uint16_t*>(A8), reinterpret_cast<const uint16_t*>(W8), K2, K2, M, N, K2, nullptr, N,
          bias, na, nullptr, 0, deq};
   if (M % FwdA8::BM || (FwdA8::BM / (B * E) + 2) * E > 64 || B % 16 || FwdA8::BM % (16 * E))
     return (int)hipErrorInvalidValue;
+  if (cfg == 1) return launch<FwdM8, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
   return launch<FwdA8, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
 }
 
 // Y (M, N) bf16 = deq[0] deq[1] A8 W8^T (+ bias): the e4m3 inference / test forward
 QD_API int qd_gemm_fwd_bias_f8(const uint8_t* A8, const uint8_t* W8, const float* deq, const uint16_t* bias,
-                               uint16_t* Y, int M, int N, int K, void* stream) {
+                               uint16_t* Y, int M, int N, int K, int cfg, void* stream) {
   if (K % 128 || !deq || M % FwdA8::BM) return (int)hipErrorInvalidValue;
   const int K2 = K / 2;
   Args a{reinterpret_cast<const uint16_t*>(A8), reinterpret_cast<const uint16_t*>(W8), K2, K2, M, N, K2, Y, N, bias, {},
          nullptr, 0, deq};
+  if (cfg == 1) return launch<FwdM8, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
   return launch<FwdA8, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
 }
+
+// C[I, J] = sP sQ sum_k P8[i, k] Q8[j, k] on the MX-scaled e4m3 MFMA: P8 (I, K), Q8 (J, K) row-major e4m3 (the
+// fp8 estimator's backward GEMMs on transposed operand copies: dgrad = dY8 . Wt8^T, wgrad = dYt8 . At8^T).
+// sP / sQ: device dequantisation scales; C fp32 (f32 = 1) or bf16, row stride ldc.  cfg 1: 144 x 128 tiles
+// (4 waves), 2: 128 x 256 tiles (8 waves).  K % 256 == 0.
+QD_API int qd_gemm_nt_f8(const uint8_t* P8, const uint8_t* Q8, const float* sP, const float* sQ, void* C, int I, int J,
+                         int K, int ldc, int f32, int cfg, void* stream) {
+  if (K % 256 || !sP || !sQ) return (int)hipErrorInvalidValue;
+  const int K2 = K / 2;
+  Args a{reinterpret_cast<const uint16_t*>(P8), reinterpret_cast<const uint16_t*>(Q8), K2, K2, I, J, K2, C, ldc,
+         nullptr, {}, nullptr, 0, sP, {}, sQ};
+  hipStream_t st = (hipStream_t)stream;
+  if (cfg == 2) return f32 ? launch<WgrM8, EPI_F32, 2, 8>(a, st) : launch<WgrM8, EPI_BF16, 2, 8>(a, st);
+  return f32 ? launch<FwdM8, EPI_F32, 4, 8>(a, st) : launch<FwdM8, EPI_BF16, 4, 8>(a, st);
+}
+
+namespace qd {
+namespace gemm {
+// dst (C, R) = src (R, C)^T for bytes (the e4m3 operand copies of the fp8 backward), R % 64 == 0, C % 256 == 0.
+// No LDS: in a 64 x 256 tile, thread t owns four 4 x 4 byte blocks (rows 4 (t / 16) .., cols 4 (t % 16) + 64 m):
+// sixteen dword loads in flight (16 threads cover 64 contiguous bytes of a row), 4 x 4 byte transposes in
+// registers (v_perm), sixteen dword stores (16 threads cover 64 contiguous bytes of an output row).
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__global__ void __launch_bounds__(256) transpose_u8_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                           int R, int C) {
+  const int tc = C / 256;
+  const int r0 = (blockIdx.x / tc) * 64, c0 = (blockIdx.x % tc) * 256;
+  const int br = threadIdx.x >> 4, bc = threadIdx.x & 15;
+  uint32_t x[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      x[m][i] = __builtin_nontemporal_load(
+          reinterpret_cast<const uint32_t*>(src + (size_t)(r0 + 4 * br + i) * C + c0 + 64 * m + 4 * bc));
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    // y[j] byte i = x[i] byte j
+    const uint32_t a01 = perm(x[m][1], x[m][0], 0x05010400), a23 = perm(x[m][3], x[m][2], 0x05010400);
+    const uint32_t b01 = perm(x[m][1], x[m][0], 0x07030602), b23 = perm(x[m][3], x[m][2], 0x07030602);
+    const uint32_t y[4] = {perm(a23, a01, 0x05040100), perm(a23, a01, 0x07060302), perm(b23, b01, 0x05040100),
+                           perm(b23, b01, 0x07060302)};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<uint32_t*>(dst + (size_t)(c0 + 64 * m + 4 * bc + j) * R + r0 + 4 * br) = y[j];
+  }
+}
+}  // namespace gemm
+}  // namespace qd
+
+QD_API int qd_transpose_u8(const uint8_t* src, uint8_t* dst, int R, int C, void* stream) {
+  if (R % 64 || C % 256 || R < 64 || C < 256) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(qd::gemm::transpose_u8_kernel, dim3((R / 64) * (C / 256)), dim3(256), 0, (hipStream_t)stream, src,
+                     dst, R, C);
+  return (int)hipGetLastError();
+}
+
+// The fp8 estimator's backward GEMMs straight from the row-major e4m3 tensors (MC8 operands, no transposed
+// copies).  sdy / sa / sw: device dequantisation scales.  M % 256 == 0 (wgrad), N % 256 == 0 (dgrad).
+// dW (N, K) fp32 (row stride ldw) = sdy sa dY8^T A8: dY8 (M, N), A8 (M, K)
+QD_API int qd_gemm_wgrad_f8(const uint8_t* dY8, const uint8_t* A8, const float* sdy, const float* sa, float* dW, int M,
+                            int N, int K, int ldw, void* stream) {
+  if (M % 256 || N % 128 || K % 256 || !sdy || !sa) return (int)hipErrorInvalidValue;
+  Args a{reinterpret_cast<const uint16_t*>(dY8), reinterpret_cast<const uint16_t*>(A8), N / 2, K / 2, N, K, M / 2,
+         dW, ldw, nullptr, {}, nullptr, 0, sdy, {}, sa};
+  return launch<WgrM8C, EPI_F32, 2, 8>(a, (hipStream_t)stream);
+}
+// dA (M, K) bf16 = sdy sw dY8 W8: dY8 (M, N), W8 (N, K)
+QD_API int qd_gemm_dgrad_f8(const uint8_t* dY8, const uint8_t* W8, const float* sdy, const float* sw, uint16_t* dA, int M,
+                            int N, int K, void* stream) {
+  if (N % 256 || M % 144 || K % 128 || !sdy || !sw) return (int)hipErrorInvalidValue;
+  Args a{reinterpret_cast<const uint16_t*>(dY8), reinterpret_cast<const uint16_t*>(W8), N / 2, K / 2, M, K, N / 2,
+         dA, K, nullptr, {}, nullptr, 0, sdy, {}, sw};
+  return launch<DgrM8C, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
+}
+

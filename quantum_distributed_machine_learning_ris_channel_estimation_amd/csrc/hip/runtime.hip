@@ -48,3 +48,26 @@ int qd_cu_probe(unsigned* out, int nblocks, int spin, void* stream) {
 }
 
 }  // extern "C"
+
+// ds_read_b64_tr_b8 layout probe: LDS holds bytes b[a] = a & 0xff over 4 KiB (a 256-byte row pitch, 16 rows);
+// lane l reads at byte address addr[l] (host-chosen), the 8 returned bytes land in out[8 l .. 8 l + 7]
+namespace qd {
+namespace rt {
+__global__ void __launch_bounds__(64) tr_b8_probe_kernel(const int* __restrict__ addr, uint8_t* __restrict__ out,
+                                                         const uint8_t* __restrict__ fill) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4096];
+  for (int i = threadIdx.x; i < 4096; i += 64) lds[i] = fill[i];
+  __syncthreads();
+  const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds;
+  typedef __attribute__((ext_vector_type(2))) int v2i;
+  v2i r;
+  asm volatile("ds_read_b64_tr_b8 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(base + (uint32_t)addr[threadIdx.x]) : "memory");
+  *reinterpret_cast<v2i*>(out + 8 * threadIdx.x) = r;
+}
+}  // namespace rt
+}  // namespace qd
+
+extern "C" int qd_tr_b8_probe(const int* addr, uint8_t* out, const uint8_t* fill, void* stream) {
+  hipLaunchKernelGGL(qd::rt::tr_b8_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, addr, out, fill);
+  return (int)hipGetLastError();
+}

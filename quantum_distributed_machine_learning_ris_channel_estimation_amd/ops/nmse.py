@@ -239,14 +239,16 @@ class StreamNMSE:
     def gemm_fused(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], label: torch.Tensor,
                    perf: Optional[torch.Tensor], bias_grad: torch.Tensor, layout: Tuple[int, int, int],
                    rowden: torch.Tensor, loss_scale: float = 1.0, bias_slabs=None, defer_loss: bool = False,
-                   cfg: int = 0, deq: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   cfg: int = 0, deq: Optional[torch.Tensor] = None, f8_out=None) -> torch.Tensor:
         """The FC forward GEMM with this loss as its epilogue (csrc/hip/gemm.hip qd_gemm_fwd_nmse): Y = A W^T
         + b is never written; dY (bf16), the error partials, the per-stream label powers and the bias
         gradient's per-tile column sums come out of the GEMM, then the same finish as ``fused`` (a launch,
         or ``pending_finish`` for a later launch of the step with ``defer_loss``; the bias column reduction
         queued on ``bias_slabs`` when given).  Returns dY; the loss is ``self.loss``.
         ``deq`` (2,) fp32: A and W are OCP e4m3 (torch.float8_e4m3fn) with these dequantisation scales
-        (qd_gemm_fwd_nmse_f8, the fp8 estimator); the rest of the contract is unchanged."""
+        (qd_gemm_fwd_nmse_f8, the fp8 estimator); the rest of the contract is unchanged.  ``f8_out`` (with
+        ``deq``): (dY8 (M, N), dYt8 (N, M) or None, qs (1,), amax partials (4096,)) -- dY also written as e4m3,
+        row-major (and transposed), for the fp8 backward GEMMs."""
         from .fc import gemm_tile_m
         E, U, B = layout
         M, K = A.shape
@@ -255,8 +257,11 @@ class StreamNMSE:
         assert A.is_cuda and self.rowoff is not None and M == self.rows == E * U * B and N == self.cols
         want = torch.float8_e4m3fn if f8 else torch.bfloat16
         assert A.dtype == W.dtype == want and A.is_contiguous() and W.is_contiguous()
+        f8cfg = 0
         if f8:
-            cfg = 0   # (the e4m3 kernel has the cfg-0 tile)
+            # (the e4m3 kernels have the cfg-0 tile; f8 cfg 1 = the MX-scaled MFMA when K allows, QDML_F8_MX=0: off)
+            f8cfg = 1 if (K % 256 == 0 and os.environ.get("QDML_F8_MX", "1") != "0") else 0
+            cfg = 0
         self._check_labels(label)
         if perf is not None:
             self._check_labels(perf)
@@ -270,11 +275,17 @@ class StreamNMSE:
         _, dY, part, colsum, dens = self._gz
         if f8:
             f = nat.fn(nat.hip_lib(), "qd_gemm_fwd_nmse_f8", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i,
-                                                              _i, _i, _i, _i, _f, _p])
+                                                              _i, _i, _i, _i, _f, _i, _p, _p, _p, _p, _p])
+            d8 = [None] * 4
+            if f8_out is not None:
+                dY8, dYt8, qs8, am8 = f8_out
+                assert dY8.shape == (M, N) and dY8.element_size() == 1
+                assert dYt8 is None or (dYt8.shape == (N, M) and dYt8.element_size() == 1)
+                d8 = [nat.ptr(dY8), nat.ptr(dYt8) if dYt8 is not None else None, nat.ptr(qs8), nat.ptr(am8)]
             nat.check(f(nat.ptr(A), nat.ptr(W), nat.ptr(deq), nat.ptr(b) if b is not None else None, nat.ptr(label),
                         nat.ptr(perf) if perf is not None else None, nat.ptr(self.rowoff), nat.ptr(rowden),
                         nat.ptr(dY), nat.ptr(part), nat.ptr(colsum), nat.ptr(dens), M, N, K, E, U, B, loss_scale,
-                        nat.stream_ptr(dev)), "gemm_fwd_nmse_f8")
+                        f8cfg, *d8, nat.stream_ptr(dev)), "gemm_fwd_nmse_f8")
         else:
             f = nat.fn(nat.hip_lib(), "qd_gemm_fwd_nmse", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i,
                                                            _i, _i, _f, _i, _p])

@@ -67,12 +67,13 @@ class HDCEModel:
         # fp8 estimator: FC forward = e4m3 x e4m3 (fp32 accumulate) with delayed per-tensor scales; slot
         # 0 = FC activations (quantised by the conv stack's last BN+ReLU kernel), slot 1 = FC weights
         # (quantised by the optimizer's shadow write), slots 2..5 = the e4m3 convs of layers 2 / 3
-        # (activation, weight) -- one scale-update launch per step (after the FC forward) for all six
+        # (activation, weight), slot 6 = the loss gradient dY (the e4m3 FC backward GEMMs) -- one scale-update
+        # launch per step for all seven
         self.fp8 = dtype == "fp8" and self.device.type == "cuda"
         self.fp8_scales = None
         if self.fp8:
             from ..ops.optim import Fp8Scales
-            self.fp8_scales = Fp8Scales(6, self.device)
+            self.fp8_scales = Fp8Scales(7, self.device)
         self.convs = [Conv_P128(pilot_num).to(self.device) for _ in range(n_experts)]
         self.fc = FC_P128(pilot_num).to(self.device)
         named = []
@@ -301,6 +302,8 @@ class HDCEStep:
         self.hand_gemm = set(x for x in hg.split(",") if x) if self.hip else set()
         assert self.hand_gemm <= {"fwd", "wgrad", "dgrad"}, self.hand_gemm
         self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,1,2").split(","))
+        # fp8 estimator: the FC weight / data gradients in e4m3 as well (see _fc_hand_f8; QDML_F8_BWD=0: bf16)
+        self.f8_bwd = os.environ.get("QDML_F8_BWD", "1") != "0"
         if self.hip:
             from ..ops.conv import ConvStackHIP
             # launch knobs (samples per wave / per wgrad workgroup / per BN-reduction workgroup / layer-1
@@ -470,22 +473,46 @@ class HDCEStep:
         return (M % tm == 0 and N % 128 == 0 and K % 128 == 0 and (tm // (self.B * m.E) + 2) * m.E <= 64
                 and self.B % 16 == 0 and tm % (16 * m.E) == 0)
 
+    def _f8_bwd_ok(self, M: int, N: int, K: int) -> bool:
+        """The FC weight / data gradients in e4m3 too (QDML_F8_BWD=0: bf16): shapes the MX-scaled GEMMs tile
+        (dgrad 144 x 128 tiles over K = N, wgrad 128 x 256 tiles over K = M)."""
+        return self.f8_bwd and M % 256 == 0 and N % 256 == 0 and K % 256 == 0 and M % 144 == 0
+
     @torch.no_grad()
     def _fc_hand_f8(self, A: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:
         """fp8 estimator: e4m3 forward GEMM with the loss fused into its epilogue (per-tensor delayed
-        scales of the previous step), bf16 weight / data gradients."""
+        scales of the previous step).  The weight and data gradients run in e4m3 as well when the shapes allow
+        (_f8_bwd_ok): the loss epilogue also writes dY as e4m3 (delayed scale slot 6), and both gradients run on
+        the MX-scaled MFMA straight from the row-major e4m3 tensors -- dW = dY8^T A8 and dA = dY8 W8, the
+        i-contiguous operands read through ds_read_b64_tr_b8, no transposed copies; else bf16 gradients.  The
+        scale update runs after the data gradient then (every e4m3 operand of the step is dequantised with the
+        scale it was quantised with)."""
         from ..ops.slabsum import SlabBatch
         m = self.m
         W, b = m.fc_weights_lp()
+        M, K = A.shape
+        N = m.fc_w.shape[0]
+        bwd8 = self._f8_bwd_ok(M, N, K)
+        f8o = None
+        sc = m.fp8_scales
+        if bwd8:
+            if getattr(self, "_dY8", None) is None or self._dY8.shape != (M, N):
+                self._dY8 = torch.empty(M, N, device=A.device, dtype=torch.float8_e4m3fn)
+            f8o = (self._dY8, None, sc.qs[6:7], sc.amax[6])
         self._slabs = SlabBatch() if (self.writes_grads and self.bias_via_conv_slabs) else None
         dY = self.nmse.gemm_fused(self.conv.h3_8, m._shadow_w8, b, label, perf, m.fc_b.grad, (m.E, self.U, self.B),
                                   self._rowden, bias_slabs=self._slabs,
-                                  defer_loss=self._slabs is not None and self.defer_loss, deq=m.fp8_scales.scale)
-        m.fp8_scales.update()
+                                  defer_loss=self._slabs is not None and self.defer_loss, deq=sc.scale, f8_out=f8o)
+        if not bwd8:
+            sc.update()
         if self.stage_hook is not None:
             self.stage_hook("fc")
-        A = A.to(m.compute_dtype)
-        self._wgrad(dY, A)
+        self._f8_bwd = bwd8
+        if bwd8:
+            from ..ops.fc import gemm_wgrad_f8
+            gemm_wgrad_f8(self._dY8, self.conv.h3_8.view(M, K), sc.scale[6:7], sc.scale[0:1], out=m.fc_w.grad)
+        else:
+            self._wgrad(dY, A.to(m.compute_dtype))
         self._dYW = (dY, W)
         if not self.defer_dgrad:
             self.dgrad()
@@ -574,6 +601,17 @@ class HDCEStep:
         after the FC gradient all-reduce is on its way)."""
         dY, W = self._dYW
         from ..ops.fc import gemm_dgrad
+        if getattr(self, "_f8_bwd", False):   # (fp8 estimator, see _fc_hand_f8)
+            from ..ops.fc import gemm_dgrad_f8
+            m = self.m
+            sc = m.fp8_scales
+            if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
+                self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)
+            self._dA = gemm_dgrad_f8(self._dY8, m._shadow_w8, sc.scale[6:7], sc.scale[1:2], out=self._dA_buf)
+            sc.update()
+            if self.stage_hook is not None:
+                self.stage_hook("dgrad")
+            return
         if "dgrad" in self.hand_gemm and dY.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 \
                 and dY.shape[0] % 144 == 0 and W.shape[1] % 256 == 0 and W.shape[0] % 64 == 0:
             if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):

@@ -234,7 +234,9 @@ class Y2HRunner:
         # the global indices); the ranks' losses are shares of ONE loss, so the gradients are SUMMED
         den_global = torch.zeros(E * U, 2, device=ctx.device) if ref else None
         rowpow = None
-        if ref and ctx.device.type == "cuda" and step.hip:
+        # per-row label powers (GPU): the one-pass loss kernels and the FC GEMM's loss epilogue read them (the
+        # hand-written FC paths -- incl. the fp8 estimator's e4m3 GEMMs -- need them)
+        if ctx.device.type == "cuda" and step.hip:
             rowpow = (step.nmse._row_powers(tr.Hlabel), step.nmse._row_powers(tr.Hperf))
         # the NaN-guard flag rides in the conv bucket: all ranks skip (or step) together
         buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "conv": [sp.grad[:n_conv]] + ([skip] if skip is not None else [])})
@@ -350,7 +352,8 @@ class Y2HRunner:
                         f"best nmse: {best_nmse:.5f}")
             self._print("==============================================================")
             log.log(kind="hdce_epoch", epoch=epoch, loss=tl[0], loss_perf=tl[1], val_nmse=nmse,
-                    val_nmse_db=to_db(nmse), val_nmse_perf_db=to_db(nmse_perf), lr=opt.lr, samples_per_sec=sps)
+                    val_nmse_db=to_db(nmse), val_nmse_perf_db=to_db(nmse_perf), lr=opt.lr, samples_per_sec=sps,
+                    fc_path=getattr(step, "fc_path", None), f8_bwd=bool(getattr(step, "_f8_bwd", False)))
             if epoch > 0:
                 if epoch % self.lr_decay == 0:
                     opt.set_lr(opt.lr * 0.5)

@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import (  # noqa: E402
-    gemm_dgrad, gemm_fwd, gemm_wgrad)
+    gemm_dgrad, gemm_dgrad_f8, gemm_fwd, gemm_fwd_f8, gemm_nt_f8, gemm_wgrad, gemm_wgrad_f8, transpose_u8)
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import use_tuned_gemms  # noqa: E402
 
 
@@ -37,7 +37,22 @@ def main():
     dW = torch.empty(N, K, device=dev)
     dA = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
     fl = 2 * M * N * K
+    A8, W8 = A.to(torch.float8_e4m3fn), W.to(torch.float8_e4m3fn)
+    deq = torch.ones(2, device=dev)
+    one = torch.ones(1, device=dev)
+    dY8 = dY.to(torch.float8_e4m3fn)
+    Wt8, dYt8, At8 = W8.t().contiguous(), dY8.t().contiguous(), A8.t().contiguous()
+    dW8o = torch.empty(N, K, device=dev)
     var = {
+        "wgrad_f8_rowmajor": lambda: gemm_wgrad_f8(dY8, A8, one, one, out=dW8o),
+        "dgrad_f8_rowmajor": lambda: gemm_dgrad_f8(dY8, W8, one, one, out=dA),
+        "dgrad_f8mx_c1": lambda: gemm_nt_f8(dY8, Wt8, one, one, out=dA, cfg=1),
+        "dgrad_f8mx_c2": lambda: gemm_nt_f8(dY8, Wt8, one, one, out=dA, cfg=2),
+        "wgrad_f8mx_c2": lambda: gemm_nt_f8(dYt8, At8, one, one, out=dW8o, cfg=2),
+        "transpose_A8": lambda: transpose_u8(A8, out=At8),
+        "transpose_W8": lambda: transpose_u8(W8, out=Wt8),
+        "fwd_f8_0": lambda: gemm_fwd_f8(A8, W8, deq, b, out=Y, cfg=0),
+        "fwd_f8_mx": lambda: gemm_fwd_f8(A8, W8, deq, b, out=Y, cfg=1),
         "fwd_hipblaslt": lambda: torch.nn.functional.linear(A, W, b),
         "fwd_hand0": lambda: gemm_fwd(A, W, b, out=Y, cfg=0),
         "fwd_hand1": lambda: gemm_fwd(A, W, b, out=Y, cfg=1),

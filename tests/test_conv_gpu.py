@@ -116,11 +116,12 @@ def test_conv_bwd_fused_matches_side_by_side(cuda, pilot_num, B):
         assert rel(f[name], r[name]) < 1e-4, (name, rel(f[name], r[name]))
 
 
-def test_conv_f8_forward_matches_quantised_reference(cuda):
+def test_conv_f8_forward_matches_quantised_reference(cuda, monkeypatch):
     """fp8 estimator: layers 2 and 3 on e4m3 MFMA (conv3x3_f8_kernel) vs an fp32 torch conv of the
     same e4m3-quantised operands (h = BN+ReLU(z_prev) with the kernel's records, scaled by the delayed
     activation factor; W scaled by the weight factor) -- the kernel's tile swizzle, k order and
     dequantisation -- and the whole fp8 feature stack vs the fp32 model within e4m3 error."""
+    monkeypatch.setenv("QDML_FP8_CONV", "1")   # (opt-in: see ops/conv.py)
     U, B = 3, 64
     a, b = pair(cuda)
     a8 = HDCEModel(128, cuda, "fp8")

@@ -162,8 +162,9 @@ def test_flagship_hand_gemm_matches_hipblaslt_path(cuda, monkeypatch):
         assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
 
 
+@pytest.mark.parametrize("cfg", [0, 1])
 @pytest.mark.parametrize("M,N,K", [(576, 256, 256), (2304, 2048, 4096)])
-def test_gemm_fwd_f8_matches_fp32(cuda, M, N, K):
+def test_gemm_fwd_f8_matches_fp32(cuda, M, N, K, cfg):
     """e4m3 forward (mfma_f32_16x16x32_fp8_fp8, two per 16-byte fragment) == the fp32 product of the SAME
     dequantised operands (the only error left is fp32 accumulation order + the bf16 output), and exact
     one-hot layout checks."""
@@ -176,14 +177,14 @@ def test_gemm_fwd_f8_matches_fp32(cuda, M, N, K):
     W8 = (W / sw).to(torch.float8_e4m3fn)
     deq = torch.tensor([sa, sw], device=cuda)
     b = torch.randn(N, device=cuda).bfloat16()
-    Y = gemm_fwd_f8(A8, W8, deq, b)
+    Y = gemm_fwd_f8(A8, W8, deq, b, cfg=cfg)
     ref = (A8.float() * sa) @ (W8.float() * sw).t() + b.float()
     torch.cuda.synchronize()
     assert _rel(Y, ref) < 8e-3, _rel(Y, ref)
     W2 = torch.zeros(N, K, device=cuda)
     W2[5, 7] = 1.0
     W2[N - 3, K - 1] = 2.0
-    Y2 = gemm_fwd_f8(A8, W2.to(torch.float8_e4m3fn), torch.tensor([1.0, 1.0], device=cuda))
+    Y2 = gemm_fwd_f8(A8, W2.to(torch.float8_e4m3fn), torch.tensor([1.0, 1.0], device=cuda), cfg=cfg)
     torch.cuda.synchronize()
     assert torch.equal(Y2[:, 5].float(), A8[:, 7].float().bfloat16().float())
     assert torch.equal(Y2[:, N - 3].float(), (2 * A8[:, K - 1].float()).bfloat16().float())
@@ -199,6 +200,7 @@ def test_flagship_fp8_hand_gemm_matches_scaled_mm_path(cuda, monkeypatch):
     ctx = DistContext(device=cuda)
     cfg = dict(batch=64, data_len=800, hip_graphs=False, use_quantumnat=False, stream_mode="serial", dtype="fp8")
     trs = []
+    monkeypatch.setenv("QDML_F8_BWD", "0")   # (bf16 gradients on both sides; the e4m3 backward: next test)
     for hand in ("1", "0"):
         monkeypatch.setenv("QDML_HAND_FP8", hand)
         tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
@@ -216,3 +218,95 @@ def test_flagship_fp8_hand_gemm_matches_scaled_mm_path(cuda, monkeypatch):
         sl = sp.slice_of(p)
         x, y = ga[sl], gb[sl]
         assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
+
+
+@pytest.mark.parametrize("cfg,I,J,K", [(1, 2304, 4096, 2048), (2, 2048, 4096, 2304), (2, 256, 256, 256), (1, 144, 128, 512)])
+@pytest.mark.parametrize("f32", [False, True])
+def test_gemm_nt_f8_matches_fp32(cuda, cfg, I, J, K, f32):
+    """The fp8 backward GEMM form (MX-scaled e4m3 MFMA, two separate device scales) == the fp32 product of
+    the same dequantised operands; transpose_u8 is an exact byte transpose."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import gemm_nt_f8, transpose_u8
+    torch.manual_seed(3)
+    P = torch.randn(I, K, device=cuda)
+    Q = torch.randn(J, K, device=cuda) * K ** -0.5
+    sp, sq = float(P.abs().max()) / 448.0, float(Q.abs().max()) / 448.0
+    P8, Q8 = (P / sp).to(torch.float8_e4m3fn), (Q / sq).to(torch.float8_e4m3fn)
+    C = gemm_nt_f8(P8, Q8, torch.tensor([sp], device=cuda), torch.tensor([sq], device=cuda),
+                   out_dtype=torch.float32 if f32 else torch.bfloat16, cfg=cfg)
+    ref = (P8.float() * sp) @ (Q8.float() * sq).t()
+    torch.cuda.synchronize()
+    assert _rel(C, ref) < (1e-4 if f32 else 8e-3), _rel(C, ref)
+    if I % 64 == 0 and K % 256 == 0:
+        T = transpose_u8(P8)
+        assert torch.equal(T.view(torch.uint8), P8.view(torch.uint8).t().contiguous())
+
+
+def test_flagship_fp8_backward_matches_bf16_backward(cuda, monkeypatch):
+    """fp8 estimator, full shape (M = 2304): the e4m3 FC weight / data gradients (MX-scaled NT GEMMs over the
+    transposed e4m3 copies the loss epilogue and the byte transposes write) vs the bf16 gradient GEMMs, same
+    forward, dY scale calibrated from the bf16 run: every HDCE gradient agrees to e4m3 accuracy."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
+                                                                                                FlagshipTrainer)
+    ctx = DistContext(device=cuda)
+    cfg = dict(batch=256, data_len=600, hip_graphs=False, use_quantumnat=False, stream_mode="serial", dtype="fp8")
+    trs = {}
+    for bwd in ("0", "1"):
+        monkeypatch.setenv("QDML_F8_BWD", bwd)
+        trs[bwd] = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
+    b16, b8 = trs["0"], trs["1"]
+    b16.next_batch()
+    b16._dp_g1()
+    b16._dp_g2()
+    torch.cuda.synchronize()
+    assert not getattr(b16.hstep, "_f8_bwd", False)
+    dY = b16.hstep._dYW[0]
+    b8.hdce.fp8_scales.set_from_tensor(6, dY)
+    b8.next_batch()
+    b8._dp_g1()
+    b8._dp_g2()
+    torch.cuda.synchronize()
+    assert b8.hstep._f8_bwd
+    assert torch.equal(b8.hloss, b16.hloss)
+    assert float(b8.hdce.fp8_scales.scale[6]) != 1.0
+    ga, gb = b8.hdce.space.grad, b16.hdce.space.grad
+    sp = b8.hdce.space
+    for name, p in zip(sp.names, sp.params):
+        sl = sp.slice_of(p)
+        x, y = ga[sl].float(), gb[sl].float()
+        cos = float(torch.nn.functional.cosine_similarity(x.flatten(), y.flatten(), dim=0))
+        assert cos > 0.99, (name, cos)
+        assert float((x - y).abs().max()) <= 0.15 * float(y.abs().max()) + 1e-8, name
+
+
+@pytest.mark.parametrize("M,N,K", [(2304, 2048, 4096), (2304, 256, 512), (256, 256, 256)])
+def test_gemm_f8_grads_from_row_major(cuda, M, N, K):
+    """The fp8 backward GEMMs on the row-major e4m3 tensors (i-contiguous operands through ds_read_b64_tr_b8):
+    dW = s s dY8^T A8 (fp32) and dA = s s dY8 W8 (bf16) == the fp32 products of the same dequantised operands;
+    one-hot operands check the layouts exactly."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import gemm_dgrad_f8, gemm_wgrad_f8
+    torch.manual_seed(4)
+    q = lambda t, s: (t / s).to(torch.float8_e4m3fn)
+    dY, A, W = torch.randn(M, N, device=cuda), torch.randn(M, K, device=cuda), torch.randn(N, K, device=cuda)
+    sy, sa, sw = (float(t.abs().max()) / 448.0 for t in (dY, A, W))
+    dY8, A8, W8 = q(dY, sy), q(A, sa), q(W, sw)
+    t = lambda v: torch.tensor([v], device=cuda)
+    dW = torch.empty(N, K, device=cuda)
+    gemm_wgrad_f8(dY8, A8, t(sy), t(sa), out=dW)
+    ref_w = (dY8.float() * sy).t() @ (A8.float() * sa)
+    torch.cuda.synchronize()
+    assert _rel(dW, ref_w) < 1e-4, _rel(dW, ref_w)
+    if M % 144 == 0:
+        dA = gemm_dgrad_f8(dY8, W8, t(sy), t(sw))
+        ref_a = (dY8.float() * sy) @ (W8.float() * sw)
+        torch.cuda.synchronize()
+        assert _rel(dA, ref_a) < 8e-3, _rel(dA, ref_a)
+    # exact layout: one-hot dY picks rows of A / W
+    oh = torch.zeros(M, N, device=cuda)
+    oh[M - 1, 3] = 1.0
+    oh[5, N - 2] = 2.0
+    gemm_wgrad_f8(oh.to(torch.float8_e4m3fn), A8, t(1.0), t(1.0), out=dW)
+    torch.cuda.synchronize()
+    assert torch.equal(dW[3], A8[M - 1].float()) and torch.equal(dW[N - 2], 2 * A8[5].float())
+    assert float(dW[4].abs().sum()) == 0.0
+
