@@ -59,11 +59,6 @@ def main() -> int:
     ap.add_argument("--split-graphs", action="store_true", help="the DP plan (5 graphs around the collectives) even at 1 GPU")
     ap.add_argument("--steps-per-graph", type=int, default=5,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
-    ap.add_argument("--hdce-branches", default="", help="(dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam")
-    ap.add_argument("--dp-qsc-phase", type=int, default=2, choices=[1, 2, 3],
-                    help="DP plan: run the QSC beside the HDCE forward (1), beside the conv backward (2), or "
-                         "its forward half beside the HDCE forward and its backward half beside the conv backward (3)")
-    ap.add_argument("--fc-adam-grid", type=int, default=0, help="workgroup cap of the FC Adam launch")
     ap.add_argument("--dp-plan", default="auto", choices=["auto", "zero", "allreduce"],
                     help="world > 1: ZeRO-1 FC optimizer (reduce-scatter / shard Adam / all-gather) or all-reduce; "
                          "auto = allreduce with the one-graph step, zero with the 5-graph step")
@@ -82,9 +77,9 @@ def main() -> int:
                     help="untimed steps replayed right before the timed region, after the warm-up and the graph "
                          "capture (rounded up to whole graph replays): the first replays of a fresh graph run "
                          "slower (profiles/r3_01_window.txt); reported in the JSON line")
-    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dag", "dagq"],
-                    help="how the step's independent branches run (FlagshipTrainer): one chain, one 4-stream graph "
-                         "(QSC + HDCE side branches), or the QSC branch forked off the HDCE chain")
+    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dagq"],
+                    help="how the step's independent branches run (FlagshipTrainer): one chain, or the QSC branch "
+                         "forked off the HDCE chain")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -132,8 +127,7 @@ def main() -> int:
                              data_len=args.data_len, dtype=args.dtype, hip_graphs=not args.no_graphs,
                              use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
                              stream_mode=args.stream_mode, steps_per_graph=args.steps_per_graph,
-                             hdce_branches=args.hdce_branches, fc_adam_grid=args.fc_adam_grid,
-                             dp_qsc_phase=args.dp_qsc_phase, dp_plan=plan, dp_one_graph=og)
+                             dp_plan=plan, dp_one_graph=og)
         return FlagshipTrainer(cfg, ctx, store=store)
 
     def timed(tr: FlagshipTrainer, n: int, settle: int = 0):
@@ -232,9 +226,6 @@ def main() -> int:
                 "hip_graphs": bool(tr.graphed.enabled),
                 "graphs_per_step": len(tr.graphs),
                 "stream_mode": tr.mode,
-                "hdce_branches": "".join(sorted(tr.branches)),
-                "fc_adam_grid": args.fc_adam_grid,
-                "dp_qsc_phase": args.dp_qsc_phase,
                 "dp_plan": ("zero" if tr.zero else "allreduce") if dp else None,
                 "dp_graph": ("one" if one_graph else "five") if dp else None,
                 "capture_preflight": capture_ok,

@@ -70,6 +70,11 @@ def main(argv=None) -> int:
                 save_stream_npy(cfg.data_dir, st, s, u, cfg.Pilot_num, cfg.SNRdb, cfg.data_len)
                 print(f"wrote scenario {s} user {u} -> {cfg.data_dir}")
         return 0
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and cfg.dp_graphs == "auto" and cfg.hip_graphs \
+            and cfg.device != "cpu" and os.environ.get("QDML_DIST_BACKEND", "nccl") == "nccl":
+        # (before anything touches the GPU: every rank's child captures the collective pattern, rank 0 decides)
+        from .parallel.capture_probe import preflight
+        os.environ["QDML_DP_GRAPHS"] = "1" if preflight() else "0"
     from .train.runner import Y2HRunner
     r = Y2HRunner(cfg)
     {"train-qsc": r.train_QSC_P128, "train-hdce": r.train_Conv_Linear_of_HDCE, "train-sc": r.train_SC_P128,

@@ -177,12 +177,49 @@ def fn(lib: ctypes.CDLL, name: str, argtypes, restype=ctypes.c_int):
         f.argtypes = argtypes
         f.restype = restype
         f._qd_declared = True
-    return f
+    if _POISON is None or name.startswith("qd_lds_poison"):
+        return f
+    return _poisoned(f)
+
+
+# ---------------------------------------------------------------- LDS poisoning (sanitizer)
+# Uninitialised-LDS detector.  LDS is not cleared between workgroups, so a kernel that reads LDS it
+# did not write this launch sees whatever the CU's previous workgroup left there -- usually the same
+# kernel's data (a pad row zeroed by its predecessor), but a different kernel's when two streams
+# interleave on the CUs: a run-to-run difference that appears only under concurrency.  In poison mode
+# every launch made through fn() on a stream handed out by stream_ptr() is preceded, on that stream, by
+# a grid that fills the whole LDS of every CU with a pattern (csrc/hip/runtime.hip lds_poison_kernel);
+# results must be bit-identical to an unpoisoned run (tests/test_lds_poison_gpu.py).
+_POISON = None            # None, or the 32-bit fill pattern
+_POISON_STREAMS = set()   # stream handles stream_ptr() returned while poisoning
+
+
+def set_lds_poison(pattern) -> None:
+    """Enable (a 32-bit pattern, e.g. 0xFFFFFFFF = NaN in fp32 / bf16 / e4m3) or disable (None) LDS
+    poisoning for the launchers declared from now on (ops objects cache their launchers at construction:
+    build them after this call)."""
+    global _POISON
+    _POISON = None if pattern is None else int(pattern) & 0xFFFFFFFF
+    _POISON_STREAMS.clear()
+
+
+def _poisoned(f):
+    def call(*args):
+        st = args[-1] if args else None
+        if _POISON is not None and isinstance(st, ctypes.c_void_p) and st.value in _POISON_STREAMS:
+            lp = fn(hip_lib(), "qd_lds_poison", [ctypes.c_uint32, ctypes.c_void_p])
+            check(lp(_POISON, st), "qd_lds_poison")
+        return f(*args)
+    return call
 
 
 def stream_ptr(device=None) -> ctypes.c_void_p:
     import torch
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    h = torch.cuda.current_stream(device).cuda_stream
+    v = ctypes.c_void_p(h)
+    if _POISON is not None:
+        _POISON_STREAMS.add(v.value)   # (the null stream's handle is 0: c_void_p(0).value is None)
+    return v
 
 
 def ptr(t) -> ctypes.c_void_p:

@@ -59,6 +59,9 @@ class RunnerConfig:
     device: str = "auto"            # auto | cuda | cpu
     backend: str = "auto"           # kernel backend: auto | hip | cpu | torch
     hip_graphs: bool = True
+    dp_graphs: str = "auto"         # N > 1 with RCCL: capture each training step -- its bucketed all-reduces
+    #                                 included -- in a HIP graph (on | off | auto: on when the entry point's
+    #                                 capture pre-flight, parallel/capture_probe.py, passed on every rank)
     overlap_comm: bool = True
     bucket_mb: float = 32.0
     world_size: int = 1

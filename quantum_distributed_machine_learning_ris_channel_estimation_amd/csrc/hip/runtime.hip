@@ -71,3 +71,51 @@ extern "C" int qd_tr_b8_probe(const int* addr, uint8_t* out, const uint8_t* fill
   hipLaunchKernelGGL(qd::rt::tr_b8_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, addr, out, fill);
   return (int)hipGetLastError();
 }
+
+// LDS poisoning (sanitizer, _native.set_lds_poison): every workgroup takes the whole 160 KiB of its CU's LDS
+// and fills it with `pattern`; 8 workgroups per CU so that every CU of every XCD runs at least one.  A kernel
+// that reads LDS it did not write in its own launch then sees the pattern instead of a predecessor's data.
+namespace qd {
+namespace rt {
+constexpr int POISON_LDS = 160 * 1024;
+__global__ void __launch_bounds__(256) lds_poison_kernel(uint32_t pattern) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_all[];
+  const uint4 v = make_uint4(pattern, pattern, pattern, pattern);
+  uint4* l4 = reinterpret_cast<uint4*>(lds_all);
+  for (int i = threadIdx.x; i < POISON_LDS / 16; i += 256) l4[i] = v;
+  __syncthreads();
+  asm volatile("" ::"v"(l4) : "memory");   // (the stores are the kernel's whole effect: keep them)
+}
+}  // namespace rt
+}  // namespace qd
+
+extern "C" int qd_lds_poison(uint32_t pattern, void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)qd::rt::lds_poison_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, qd::rt::POISON_LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(qd::rt::lds_poison_kernel, dim3(8 * 256), dim3(256), qd::rt::POISON_LDS, (hipStream_t)stream,
+                     pattern);
+  return (int)hipGetLastError();
+}
+
+// (sanitizer self-test) one wave reads LDS dwords 0..63 it never wrote: after a poison launch, the pattern
+namespace qd {
+namespace rt {
+__global__ void __launch_bounds__(64) lds_peek_kernel(uint32_t* __restrict__ out) {
+  __shared__ uint32_t scratch[64];   // (allocates the range; read through asm so the compiler cannot fold it)
+  const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)scratch;
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(base + 4u * threadIdx.x) : "memory");
+  out[threadIdx.x] = v;
+}
+}  // namespace rt
+}  // namespace qd
+
+extern "C" int qd_lds_peek(uint32_t* out, void* stream) {
+  hipLaunchKernelGGL(qd::rt::lds_peek_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+  return (int)hipGetLastError();
+}

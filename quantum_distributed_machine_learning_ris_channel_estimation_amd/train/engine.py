@@ -278,7 +278,6 @@ class HDCEStep:
         self.grad_hook = grad_hook  # called as grad_hook("fc") / grad_hook("conv") when buckets are final
         self.hip = (dev.type == "cuda") if hip is None else hip
         self.writes_grads = self.hip
-        self.fc_side = None   # optional stream for the FC weight-gradient GEMM (HIP path)
         self.fused_nmse = True  # HIP path: the one-pass NMSE (qd_nmse_fused) when labels come via rowoff
         self.defer_dgrad = False
         # (world 1, GPU) FusedAdam: the FC weight's Adam step runs in the weight-gradient GEMM's epilogue
@@ -567,8 +566,7 @@ class HDCEStep:
 
     def _wgrad(self, dY: torch.Tensor, A: torch.Tensor) -> None:
         """dW = dY^T A (fp32, straight into the flat gradient): the hand-written GEMM for bf16 operands of a
-        tiled shape, else hipBLASLt; on ``fc_side`` when set (beside the data gradient and the conv backward,
-        which only read dY; the operands stay referenced: no allocator reuse)."""
+        tiled shape, else hipBLASLt."""
         from ..ops.fc import gemm_wgrad
         m = self.m
         hand = ("wgrad" in self.hand_gemm and dY.dtype == A.dtype == torch.bfloat16 and dY.shape[0] % 64 == 0
@@ -587,14 +585,7 @@ class HDCEStep:
             else:
                 _mm_f32(dY.t(), A, m.fc_w.grad)
 
-        side = self.fc_side
-        if side is not None:
-            self._keep = (dY, A)
-            side.wait_stream(torch.cuda.current_stream(A.device))
-            with torch.cuda.stream(side):
-                run()
-        else:
-            run()
+        run()
 
     def dgrad(self) -> None:
         """dA = dY W (HIP path): issued by the forward unless ``defer_dgrad`` (the DP plan issues it

@@ -23,8 +23,7 @@ docs/CONCURRENCY.md keeps the findings.)  Per step:
   qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
          QSC bwd -> slabs -> AdamW
 
-([wgrad|dgrad] = one launch running both independent gradients side by side.)  ``dag`` adds HDCE
-side branches (FC weight gradient, conv weight gradients, FC Adam) on their own streams.
+([wgrad|dgrad] = one launch running both independent gradients side by side.)
 
 The HDCE and the QSC have separate NaN-guard flags (``skip[0]``, ``skip[1]``), so neither
 optimizer waits for the other model's loss.
@@ -89,20 +88,13 @@ class FlagshipConfig:
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
     split_graphs: bool = False   # force the DP execution plan (5 graphs) even at world 1 (testing)
-    stream_mode: str = "dagq"    # serial | dag | dagq (see FlagshipTrainer.__init__)
-    hdce_branches: str = ""      # (dagq) HDCE side branches: w FC wgrad, c conv wgrads, a FC Adam
+    stream_mode: str = "dagq"    # serial | dagq (see FlagshipTrainer.__init__)
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
     fused_fc_adam: bool = False  # (world 1, GPU, bf16) the FC weight's Adam step in the weight-gradient GEMM's
     #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
     #                              separate (profiles/r3_04_fused_adam.txt) -- 256 one-per-CU workgroups stream
     #                              the Adam state far slower than the 2048-workgroup update kernel
     #                              (QDML_FUSED_ADAM=1 turns it on)
-    dp_qsc_phase: int = 2        # DP plan: QSC fwd/bwd beside the HDCE forward (1), the conv backward (2),
-    #                              or its forward half beside the HDCE forward and its backward half beside
-    #                              the conv backward (3).  World-1 rehearsal: 0.492 / 0.517 / 0.557 ms;
-    #                              2 is kept: it leaves the most work (QSC + conv backward) behind the 33.6 MB
-    #                              FC all-reduce, which at 2-8 ranks over xGMI is expected to take 0.2-0.4 ms
-    fc_adam_grid: int = 0        # workgroup cap of the FC Adam launch (0: default; for the 'a' branch)
     dp_plan: str = "zero"        # world > 1: "zero" = ZeRO-1 FC optimizer (reduce-scatter the FC gradient,
     #                              Adam on this rank's 1/world shard, all-gather the bf16 weight shadow) or
     #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
@@ -160,10 +152,8 @@ class FlagshipTrainer:
         self.shard_len = (sp.numel - n_conv) // ctx.world
         if self.zero:
             self.hopt.partition([n_conv + i * self.shard_len for i in range(ctx.world)])
-        elif dp or cfg.stream_mode == "dag" or "a" in cfg.hdce_branches:
+        elif dp:
             self.hopt.partition([n_conv])
-        if cfg.fc_adam_grid:
-            self.hopt.max_grid[1 + (ctx.rank if self.zero else 0)] = cfg.fc_adam_grid
         # after the broadcast: the shadow starts in sync
         self.hdce.attach_fc_shadow(self.hopt, to_end=self.zero)
         self.qopt = make_optimizer(self.qspace, "adamw", cfg.lr, weight_decay=cfg.qsc_weight_decay,
@@ -211,46 +201,29 @@ class FlagshipTrainer:
         graphs = cfg.hip_graphs and dev.type == "cuda"
         # side streams (GPU).  stream_mode:
         #   serial : one stream, one chain
-        #   dag    : ONE graph captured from 4 streams (qsc / fc / conv branches forked off the main chain)
-        #   dagq   : ONE graph, only the QSC branch forked (after the gather, joined at the end of the step);
-        #            the HDCE a single chain
+        #   dagq   : ONE graph, the QSC branch forked after the gather and joined at the end of the step; the
+        #            HDCE a single chain.  (The DP plan also forks the FC update onto the "fc" stream.)
         # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge that
-        # crosses queues costs a barrier packet, so fewer, longer branches win.  Plans whose QSC and HDCE
-        # chains ran concurrently ACROSS step boundaries -- independent chains in one graph, or two graphs
-        # replayed on two streams -- were 1-1.5% faster but not bit-reproducible on ROCm 7.x; removed in
-        # round 3, the bisection is in docs/CONCURRENCY.md)
+        # crosses queues costs a barrier packet, so fewer, longer branches win.  Measured and removed in round 3
+        # (docs/CONCURRENCY.md): HDCE side branches (FC wgrad / conv wgrads / FC Adam on their own streams),
+        # QSC and HDCE chains independent across step boundaries (1-1.5% faster, not bit-reproducible),
+        # CU-masked streams for the two chains (ops/streams.py: every partition slower), and the DP plan's
+        # QSC branch split around the HDCE forward.)
         mode = cfg.stream_mode
-        if mode not in ("serial", "dag", "dagq"):
+        if mode not in ("serial", "dagq"):
             raise ValueError(f"stream_mode {mode!r}")
         self.streams = None
         if dev.type == "cuda" and mode != "serial" and self.hstep.hip and self.cstep.hip is not None:
-            self.streams = {k: torch.cuda.Stream(dev) for k in ("qsc", "fc", "conv")}
+            self.streams = {k: torch.cuda.Stream(dev) for k in ("qsc", "fc")}
         else:
             mode = "serial"
         self.mode = mode
-        # (experiment) spatial partitioning: QDML_QSC_CUS / QDML_MAIN_CUS = CU sets (ops/streams.py:parse_cus)
-        # for the QSC branch's stream and for the stream the step is launched on
-        self.main_stream = None
-        if dev.type == "cuda" and (os.environ.get("QDML_QSC_CUS") or os.environ.get("QDML_MAIN_CUS")):
-            from ..ops import streams as cus
-            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-            if os.environ.get("QDML_QSC_CUS") and self.streams is not None:
-                self.streams["qsc"] = cus.masked_stream(cus.parse_cus(os.environ["QDML_QSC_CUS"], n_cu), dev)
-            if os.environ.get("QDML_MAIN_CUS"):
-                self.main_stream = cus.masked_stream(cus.parse_cus(os.environ["QDML_MAIN_CUS"], n_cu), dev)
-        # HDCE side branches: w = FC weight-gradient GEMM, c = conv weight-gradient kernels, a = FC Adam
-        self.branches = set("wca") if mode == "dag" else set(cfg.hdce_branches)
-        if self.streams is None:
-            self.branches = set()
-        self.hdce_side = "w" in self.branches
-        if "a" in self.branches:   # (the FC Adam branch reads the bias gradient before the conv slabs run)
-            self.hstep.bias_via_conv_slabs = False
         # the FC weight's Adam in the weight-gradient GEMM's epilogue (world 1: no gradient collective between)
         self.fused_adam = bool((cfg.fused_fc_adam or os.environ.get("QDML_FUSED_ADAM") == "1")
                                and os.environ.get("QDML_FUSED_ADAM") != "0"
                                and dev.type == "cuda" and ctx.world == 1 and not cfg.split_graphs
                                and self.hstep.hip and "wgrad" in self.hstep.hand_gemm and not self.hdce.fp8
-                               and cfg.dtype == "bf16" and "a" not in self.branches and len(self.hopt.bounds) == 1
+                               and cfg.dtype == "bf16" and len(self.hopt.bounds) == 1
                                and self.S * self.B % 64 == 0)   # (the hand weight-gradient GEMM's M tiling)
         if self.fused_adam:
             lo = sp.offsets[sp.names.index("CE.FC.weight")]
@@ -314,7 +287,7 @@ class FlagshipTrainer:
         s.wait_stream(torch.cuda.current_stream(self.ctx.device))
         return torch.cuda.stream(s)
 
-    def _join(self, names=("qsc", "fc", "conv")) -> None:
+    def _join(self, names=("qsc", "fc")) -> None:
         cur = torch.cuda.current_stream(self.ctx.device)
         for n in names:
             cur.wait_stream(self.streams[n])
@@ -346,15 +319,9 @@ class FlagshipTrainer:
         self.hstep.conv.pack_weights(nat.stream_ptr(self.ctx.device), cursor=self.cur[0, 0:1] if advance else None,
                                      cursor_inc=self.B if advance else 0)
 
-    def _qsc_branch(self, with_opt: bool, part: str = "all") -> None:
-        """The QSC step (+ AdamW with ``with_opt``); ``part`` "fwd" / "bwd": only that half (HIP path)."""
-        if part == "fwd":
-            self.cstep.forward_part(self.gat.xq, self.labels)
-            return
-        if part == "bwd":
-            q = self.cstep.backward_part(self.gat.xq, slabs=self.qslabs if self.cstep.writes_grads else None)
-        else:
-            q = self.cstep(self.gat.xq, self.labels, slabs=self.qslabs if self.cstep.writes_grads else None)
+    def _qsc_branch(self, with_opt: bool) -> None:
+        """The QSC step (+ AdamW with ``with_opt``)."""
+        q = self.cstep(self.gat.xq, self.labels, slabs=self.qslabs if self.cstep.writes_grads else None)
         if self.cstep.writes_grads:
             self.qslabs.launch(accumulate=False, stream=nat.stream_ptr(self.ctx.device))
         if q is not self.qloss:
@@ -362,42 +329,20 @@ class FlagshipTrainer:
         if with_opt:
             self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.qskip)
 
-    def _hdce_forward(self, side: Optional[bool] = None) -> None:
-        side = self.hdce_side if side is None else side
-        self.hstep.fc_side = self.streams["fc"] if side else None
+    def _hdce_forward(self) -> None:
         loss = self.hstep.forward_fc_gathered(self.gat, self.store)
         if loss is not self.hloss:
             self.hloss.copy_(loss)
 
-    def _hdce_graph(self, gather: bool = False) -> None:
-        """HDCE forward + backward + Adam (world 1); ``gather``: its own batch gather first."""
-        if gather:
-            self._gather(hdce=True, classifier=False)
+    def _hdce_graph(self) -> None:
+        """HDCE forward + backward + Adam (world 1): one Adam launch over the whole space, which also packs
+        the next step's conv weight images and advances the batch cursor (tail_pack)."""
         self._hdce_forward()
-        br = self.branches
-        if "a" in br:
-            # FC Adam once the dgrad GEMM (which reads the bf16 weight shadow it rewrites) is queued
-            with self._fork(self.streams["fc"]):
-                self.hopt.step(grad_scale=1.0, skip=self.hskip, part=1)
-        self.hstep.backward_conv(side=self.streams["conv"] if "c" in br else None)
-        if "a" in br:
-            self.hopt.step(grad_scale=1.0, skip=self.hskip, part=0)
-            if self.tail_pack:
-                self._tail_pack_launch()
-            self._join(("fc",))
-        else:
-            if self.hdce_side:
-                self._join(("fc",))
-            if len(self.hopt.bounds) == 1:
-                pk = self._adam_pack()
-                self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
-                if self.tail_pack and pk is None:
-                    self._tail_pack_launch()
-                return
-            self.hopt.step(grad_scale=1.0, skip=self.hskip, part=0)
-            if self.tail_pack:
-                self._tail_pack_launch()
-            self.hopt.step(grad_scale=1.0, skip=self.hskip, part=1)
+        self.hstep.backward_conv()
+        pk = self._adam_pack()
+        self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
+        if self.tail_pack and pk is None:
+            self._tail_pack_launch()
 
     # -- the data-parallel plan (world > 1; also world 1 'serial' / split_graphs) ---------------
     #   g1 : gather, HDCE forward, NMSE, FC weight-gradient GEMM
@@ -411,17 +356,10 @@ class FlagshipTrainer:
         """gather + conv forward (reads no FC weight: overlaps the previous step's FC update)."""
         self._gather()
         self.hstep.defer_dgrad = self.hstep.hip
-        ph = self.cfg.dp_qsc_phase
-        early = self.streams is not None and ph in (1, 3)
-        if early:   # QSC forward (+ backward: phase 1) beside the HDCE forward
-            with self._fork(self.streams["qsc"]):
-                self._qsc_branch(with_opt=False, part="fwd" if ph == 3 else "all")
         if self.hstep.hip:
             self.hstep.forward_conv_gathered(self.gat)
         else:
-            self._hdce_forward(side=False)
-        if early:
-            self._join(("qsc",))
+            self._hdce_forward()
 
     def _dp_g1b(self) -> None:
         """FC forward, loss, FC weight gradient (on main: the FC collective waits for it first)."""
@@ -435,23 +373,24 @@ class FlagshipTrainer:
         self._dp_g1b()
 
     def _dp_g2(self) -> None:
+        """FC data gradient, conv backward and, on the qsc stream, the whole QSC forward/backward: the work
+        that hides the FC gradient collective.  (World-1 rehearsal of the QSC placement: beside the conv
+        backward 0.517 ms, beside the HDCE forward 0.492, split 0.557 -- this one leaves the most work behind
+        the 33.6 MB FC collective, expected at 0.2-0.4 ms over xGMI at 2-8 ranks.)"""
         # NOTE the first node of a graph must sit on the capturing stream: a branch forked before any
         # node is a ROOT of the graph, and the HIP graph executor starts root nodes that it places on
         # its other queues without waiting for the work queued ahead of the graph launch (measured:
         # the QSC branch then read the previous step's gather output)
-        ms = self.streams is not None
         if self.hstep.defer_dgrad:
             self.hstep.dgrad()
-        ph = self.cfg.dp_qsc_phase
-        late = ms and ph in (2, 3)
-        if late:
-            with self._fork(self.streams["qsc"]):
-                self._qsc_branch(with_opt=False, part="bwd" if ph == 3 else "all")
-        self.hstep.backward_conv(side=self.streams["conv"] if "c" in self.branches else None)
-        if late:
-            self._join(("qsc",))
-        elif not ms:
+        if self.streams is None:
+            self.hstep.backward_conv()
             self._qsc_branch(with_opt=False)
+            return
+        with self._fork(self.streams["qsc"]):
+            self._qsc_branch(with_opt=False)
+        self.hstep.backward_conv()
+        self._join(("qsc",))
 
     def _dp_gf(self) -> None:
         if self.zero:   # this rank's shard of the FC region only
@@ -608,7 +547,7 @@ class FlagshipTrainer:
         return {k: sum(v) / len(v) for k, v in out.items()}
 
     def _step_body(self) -> None:
-        if self.mode in ("dag", "dagq"):
+        if self.mode == "dagq":
             # the QSC branch forks right after the batch gather: its latency-bound kernels share the GPU with
             # the HDCE chain's, and it joins at the end of the step
             self._gather()
@@ -705,16 +644,6 @@ class FlagshipTrainer:
             self._replay(kk, fence=i == len(reps) - 1)
 
     def _replay(self, k: int, fence: bool = True) -> None:
-        if self.main_stream is not None:
-            cur = torch.cuda.current_stream(self.ctx.device)
-            self.main_stream.wait_stream(cur)
-            with torch.cuda.stream(self.main_stream):
-                self._replay_on(k, fence)
-            cur.wait_stream(self.main_stream)
-            return
-        self._replay_on(k, fence)
-
-    def _replay_on(self, k: int, fence: bool) -> None:
         gs = self._graphs_for(k)
         if any(g.enabled and g.graph is None for g in gs):
             # (preserve: the capture warm-ups run optimizer steps on rank-local gradients; restoring

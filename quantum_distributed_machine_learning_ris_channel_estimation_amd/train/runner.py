@@ -165,8 +165,19 @@ class Y2HRunner:
         return idx.tensor_split(ctx.world)[ctx.rank] if self._dp_reference() else idx
 
     def _graphs_on(self) -> bool:
+        """HIP-graph captured training steps: world 1, or N > 1 over RCCL with ``dp_graphs`` on (the bucketed
+        all-reduces are launched from and waited for on the capturing stream, so they become graph nodes --
+        the flagship one-graph DP plan's pattern).  ``auto`` means on only when the entry point's capture
+        pre-flight passed on every rank (it sets QDML_DP_GRAPHS=1 before anything touched the GPU)."""
         ctx = self._context()
-        return bool(self.hip_graphs) and ctx.device.type == "cuda" and ctx.world == 1
+        if not (self.hip_graphs and ctx.device.type == "cuda"):
+            return False
+        if ctx.world == 1:
+            return True
+        if self.dp_graphs not in ("on", "off", "auto"):
+            raise ValueError(f"dp_graphs {self.dp_graphs!r}")
+        on = self.dp_graphs == "on" or (self.dp_graphs == "auto" and os.environ.get("QDML_DP_GRAPHS") == "1")
+        return on and ctx.backend == "nccl"
 
     # ------------------------------------------------------------------ HDCE
     def build_hdce(self) -> HDCEModel:

@@ -36,8 +36,8 @@ for s in $STEPS; do
     adamnt) for v in 0 1 0 1; do (cd /tmp && export TMPDIR=/tmp && QDML_ADAM_NT=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/adamnt_$v" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 > "$OUT/adamnt_$v.log" 2>&1) || exit 1; python scripts/prof_summary.py "$OUT/adamnt_$v/run_kernel_trace.csv" --tail 0.6 > "$OUT/adamnt_${v}_$RANDOM.md"; rm -rf "$OUT/adamnt_$v"; done ;;
     pmc) for pc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do n=${pc%% *}; (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $pc --output-format csv -d "$OUT/pmc_$n" -o run -- python "$ROOT/bench.py" --steps 10 --warmup 2 --steps-per-graph 1 > "$OUT/pmc_$n.log" 2>&1) || { echo "pmc $pc failed"; tail -5 "$OUT/pmc_$n.log"; exit 1; }; done; python scripts/pmc_summary.py "$OUT"/pmc_* > "$OUT/pmc_summary.md"; rm -rf "$OUT"/pmc_*/ ;;
     variants) IFS=';' read -ra VS <<< "${VARIANTS:-NONE=0|}"; for r in 1 2; do for v in "${VS[@]}"; do env ${v%%|*} timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-300} --warmup 10 ${v#*|} > $OUT/cmp.log 2>&1 || exit 1; echo "$v $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/variants.txt; done; done ;;
-    dpphase)for v in 1 2 3 1 2 3; do run bench_dpq_${v}_$RANDOM 300 python bench.py --steps 100 --warmup 10 --split-graphs --dp-qsc-phase $v; done ;;
     fusewd) for v in 1 0 1 0; do QDML_CONV_FUSE_WD=$v run bench_fwd_$v 300 python bench.py --steps 100 --warmup 10; mv $OUT/bench_fwd_$v.log $OUT/bench_fwd_${v}_$RANDOM.log; done ;;
+    poison) run poison 600 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_lds_poison_gpu.py -m gpu ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace ${PROF_EXTRA:-} --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 ${BENCH_EXTRA:-}) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" && python scripts/prof_timeline.py "$OUT/prof/run_kernel_trace.csv" --marker "conv3x3_kernel<2," > "$OUT/prof_timeline.md" ;;
