@@ -47,6 +47,8 @@ for s in $STEPS; do
     tune) run tune 900 python scripts/tune_kernels.py --what ${TUNE_WHAT:-qsc,conv} ;;
     fp8probe) run fp8probe 300 python scripts/probe_fp8.py ;;
     fcprobe) run fcprobe 300 python scripts/probe_fc_gemm.py ;;
+    gemmprobe) run gemmprobe 300 python scripts/probe_gemm.py ;;
+    gemmtest) run gemmtest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_gpu.py -m gpu ;;
     nmseprobe) run nmseprobe 300 python scripts/probe_nmse.py ;;
     tunegemm) run tunegemm 900 python scripts/tune_gemm.py --out "$OUT/tunableop_gfx950.csv" ;;
     diag) run diag 900 python scripts/diag_hdce.py --epochs ${DIAG_EPOCHS:-20} ;;
