@@ -49,6 +49,7 @@ from ..ops.slabsum import SlabBatch
 from ..parallel.dp import DistContext, GradBuckets
 from ..utils.profiling import GraphedStep
 from .engine import ClassifierStep, HDCEModel, HDCEStep
+from .flagship_dp import DPPlan
 
 
 import os
@@ -110,7 +111,7 @@ class FlagshipConfig:
     n_users: int = 3
 
 
-class FlagshipTrainer:
+class FlagshipTrainer(DPPlan):
     def __init__(self, cfg: FlagshipConfig, ctx: DistContext, store: Optional[DMLStore] = None):
         """``store``: share another trainer's HBM-resident dataset (same data_len / pilots / SNR / seed)."""
         self.cfg, self.ctx = cfg, ctx
@@ -343,208 +344,6 @@ class FlagshipTrainer:
         self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
         if self.tail_pack and pk is None:
             self._tail_pack_launch()
-
-    # -- the data-parallel plan (world > 1; also world 1 'serial' / split_graphs) ---------------
-    #   g1 : gather, HDCE forward, NMSE, FC weight-gradient GEMM
-    #        -> all-reduce 'skip' (HDCE NaN flag) and 'fc' (33.6 MB) start on RCCL's stream
-    #   g2 : FC data-gradient GEMM, conv backward (+ wgrad side stream) and, on the qsc stream, the
-    #        whole QSC forward/backward -- all of it hides the FC all-reduce
-    #        -> all-reduce 'small' (conv/BN + QSC grads + the QSC NaN flag)
-    #   gf : (fc stream) FC Adam once 'skip' + 'fc' arrived and g2's dgrad read the weight shadow,
-    #        beside the 'small' all-reduce;   gr : (main) conv/BN Adam + QSC AdamW after 'small'
-    def _dp_g1a(self) -> None:
-        """gather + conv forward (reads no FC weight: overlaps the previous step's FC update)."""
-        self._gather()
-        self.hstep.defer_dgrad = self.hstep.hip
-        if self.hstep.hip:
-            self.hstep.forward_conv_gathered(self.gat)
-        else:
-            self._hdce_forward()
-
-    def _dp_g1b(self) -> None:
-        """FC forward, loss, FC weight gradient (on main: the FC collective waits for it first)."""
-        if self.hstep.hip:
-            loss = self.hstep.forward_fc_after_conv(self.store)
-            if loss is not self.hloss:
-                self.hloss.copy_(loss)
-
-    def _dp_g1(self) -> None:
-        self._dp_g1a()
-        self._dp_g1b()
-
-    def _dp_g2(self) -> None:
-        """FC data gradient, conv backward and, on the qsc stream, the whole QSC forward/backward: the work
-        that hides the FC gradient collective.  (World-1 rehearsal of the QSC placement: beside the conv
-        backward 0.517 ms, beside the HDCE forward 0.492, split 0.557 -- this one leaves the most work behind
-        the 33.6 MB FC collective, expected at 0.2-0.4 ms over xGMI at 2-8 ranks.)"""
-        # NOTE the first node of a graph must sit on the capturing stream: a branch forked before any
-        # node is a ROOT of the graph, and the HIP graph executor starts root nodes that it places on
-        # its other queues without waiting for the work queued ahead of the graph launch (measured:
-        # the QSC branch then read the previous step's gather output)
-        if self.hstep.defer_dgrad:
-            self.hstep.dgrad()
-        if self.streams is None:
-            self.hstep.backward_conv()
-            self._qsc_branch(with_opt=False)
-            return
-        with self._fork(self.streams["qsc"]):
-            self._qsc_branch(with_opt=False)
-        self.hstep.backward_conv()
-        self._join(("qsc",))
-
-    def _dp_gf(self) -> None:
-        if self.zero:   # this rank's shard of the FC region only
-            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.hskip, part=1 + self.ctx.rank)
-        elif len(self.hopt.bounds) > 1:   # (unpartitioned -- serial world 1 -- gr steps everything)
-            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.hskip, part=1)
-
-    def _dp_gr(self) -> None:
-        g = 1.0 / self.ctx.world
-        pk = self._adam_pack()
-        self.hopt.step(grad_scale=g, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None, pack=pk)
-        if self.tail_pack and pk is None:
-            self._tail_pack_launch()
-        self.qopt.step(grad_scale=g, skip=self.qskip)
-
-    def _fc_weights_lp(self) -> torch.Tensor:
-        """(ZeRO) the FC region's copy the forward / data gradient read: the bf16 shadow (GPU bf16),
-        else the fp32 master weights themselves."""
-        lo, hi = self.fc_region
-        return self.hdce.fc_shadow if self.hdce.fc_shadow is not None else self.hdce.space.flat[lo:hi]
-
-    def sync_master(self) -> None:
-        """(ZeRO, bf16 shadow) each rank's fp32 FC master weights are current on its own shard only;
-        all-gather them (checkpointing, cross-rank comparisons).  No-op otherwise."""
-        if self.zero and self.ctx.distributed and self.hdce.fc_shadow is not None:
-            lo, hi = self.fc_region
-            self.buckets.launch_all_gather("master", self.hdce.space.flat[lo:hi])
-            self.buckets.wait(("master",))
-
-    def _mark(self, name: str, stream=None) -> None:
-        """(phase timing) a HIP event on ``stream`` (default: current) under ``name``."""
-        if self._phases is not None:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(stream)
-            self._phases[-1][name] = e
-
-    def _dp_run(self, g1a, g1b, g2, gf, gr, fence: bool = True, first: bool = True) -> None:
-        """The DP step around the collectives.  RCCL runs every collective of the process group on one
-        stream, in launch order: fc gradient (all-reduce, or reduce-scatter in the ZeRO plan), small
-        bucket, (ZeRO) the shadow all-gather.
-          allreduce : g1a g1b | AR fc | g2 | AR small | fc stream: FC Adam (whole FC) | main: conv/QSC Adam
-          zero      : g1a g1b | RS fc | g2 | AR small | fc stream: FC Adam on 1/world, AG shadow | main: ...
-        The FC update (fc stream) of step i overlaps step i+1's gather + conv forward (g1a): main waits
-        for the fc stream only before g1b reads the FC weights.  ``fence``: main also waits for it at the
-        end of the step (the last step of a run(), every step()): afterwards the state is complete."""
-        b, zero = self.buckets, self.zero
-        timed = self._phases is not None
-        if timed:
-            self._phases.append({})
-            self._mark("start")
-        g1a()
-        self._mark("g1a")
-        main = torch.cuda.current_stream(self.ctx.device) if self.streams is not None else None
-        if main is not None and not (self.cfg.dp_one_graph and first):
-            # (the previous step's FC update, when not fenced; the one-graph plan always fences, and a
-            # capturing stream must not wait on an event recorded outside the capture)
-            main.wait_stream(self.streams["fc"])
-        self._mark("fc_prev")
-        g1b()
-        self._mark("g1")
-        lo, hi = self.fc_region
-        if zero:
-            b.launch_reduce_scatter("fc", self.hdce.space.grad[lo:hi])
-        else:
-            b.launch("skip")
-            b.launch("fc")
-        g2()
-        self._mark("g2")
-        b.launch("small")
-        fc_wait = ("fc", "small") if zero else ("skip", "fc")
-        if self.streams is None:
-            b.wait(fc_wait)
-            gf()
-            if zero:
-                b.launch_all_gather("ag", self._fc_weights_lp())
-            b.wait()
-            gr()
-            return
-        fc = self.streams["fc"]
-        if zero:
-            # ZeRO: main takes the small bucket (collective + scatter-back) BEFORE forking the fc stream,
-            # which needs its HDCE NaN flag: one stream owns each scatter-back, and the fc stream inherits
-            # it through the fork (no second-waiter path across streams)
-            b.wait(("small",))
-            fc_wait = ("fc",)
-        fc.wait_stream(main)
-        with torch.cuda.stream(fc):
-            b.wait(fc_wait)
-            self._mark("fc_ready", fc)
-            gf()
-            self._mark("gf", fc)
-            if zero and self.cfg.dp_one_graph:
-                # (captured: a collective launched from a forked stream crashes hipStreamEndCapture --
-                # scripts/probe_rccl_capture.py -- so main launches the all-gather; see below)
-                pass
-            elif zero:
-                b.launch_all_gather("ag", self._fc_weights_lp())
-                b.wait(("ag",))
-                self._mark("ag", fc)
-        # (allreduce plan: the HDCE NaN flag rides in the fc bucket -- wait for it before the conv Adam
-        # reads it; free under RCCL, whose in-order stream finished fc before small)
-        b.wait(("small",) if zero else ("skip", "fc", "small"))
-        self._mark("small_ready")
-        og_ag = zero and self.cfg.dp_one_graph
-        # the shadow all-gather from main once the shard is updated: before gr (it overlaps gr; the shard
-        # Adam is 1/world of the FC) or after it (world 1: the whole-FC Adam on fc overlaps gr instead)
-        ag_first = og_ag and self.ctx.world > 1
-        if ag_first:
-            main.wait_stream(fc)
-            b.launch_all_gather("ag", self._fc_weights_lp())
-        gr()
-        self._mark("gr")
-        if og_ag:
-            if not ag_first:
-                main.wait_stream(fc)
-                b.launch_all_gather("ag", self._fc_weights_lp())
-            b.wait(("ag",))
-        b.pending.clear()   # (every collective has been waited for by the stream that consumes it)
-        if fence:
-            main.wait_stream(fc)
-        self._mark("end")
-
-    def phase_times(self, steps: int):
-        """Run ``steps`` DP steps with HIP events around the phases and return the mean milliseconds of
-        each (diagnostic; the GPU 5-graph DP plan only): g1 (forward + FC wgrad), g2 (FC dgrad + conv
-        backward + QSC, hiding the FC collective), fc_exposed (FC collective time left after g2),
-        small_exposed, fc_adam, all_gather (ZeRO), conv_qsc_adam, step.  None for every other plan -- in
-        particular the one-graph DP plan, whose phases have no host-visible boundaries (its whole-step
-        time is what bench.py measures; the phases of a different plan are never reported for it)."""
-        if self.ctx.device.type != "cuda" or self.streams is None or len(self.graphs) != 5:
-            return None
-        self._phases = []
-        try:
-            self.run(steps)
-            torch.cuda.synchronize(self.ctx.device)
-            rows = self._phases
-        finally:
-            self._phases = None
-        el = lambda r, a, b_: r[a].elapsed_time(r[b_])
-        out = {"g1a": [], "fc_prev_wait": [], "g1": [], "g2": [], "fc_exposed": [], "small_exposed": [],
-               "fc_adam": [], "all_gather": [], "conv_qsc_adam": [], "step": []}
-        for i, r in enumerate(rows):
-            out["g1a"].append(el(r, "start", "g1a"))
-            out["fc_prev_wait"].append(el(r, "g1a", "fc_prev"))
-            out["g1"].append(el(r, "start", "g1"))
-            out["g2"].append(el(r, "g1", "g2"))
-            out["fc_exposed"].append(max(0.0, el(r, "g2", "fc_ready")))
-            out["small_exposed"].append(max(0.0, el(r, "g2", "small_ready")))
-            out["fc_adam"].append(el(r, "fc_ready", "gf"))
-            out["all_gather"].append(el(r, "gf", "ag") if "ag" in r else 0.0)
-            out["conv_qsc_adam"].append(el(r, "small_ready", "gr"))
-            # step = start to the next step's start (the FC update overlaps it), the last to its end
-            out["step"].append(r["start"].elapsed_time(rows[i + 1]["start"]) if i + 1 < len(rows) else el(r, "start", "end"))
-        return {k: sum(v) / len(v) for k, v in out.items()}
 
     def _step_body(self) -> None:
         if self.mode == "dagq":
