@@ -646,3 +646,51 @@ QD_API int qd_qsc_infer_head(const float* E, const float* wc, const float* bc, f
 #undef QD_IH
   return (int)hipErrorInvalidValue;
 }
+
+// The QSC preprocess linear layer's weight gradient when the MFMA backward cannot reduce it in its own slab
+// (large n / P256 feature maps): dWl (n, F) = dpre^T p2 over the batch, dpre (B, n), p2 (B, F) fp32.  A tall-K
+// outer-product sum (K = B = 2304, n <= 16): phase 1 here writes per-sample-chunk partials slab (S, n, F) --
+// block (x, s) takes 256 columns of chunk s, each thread one column with n accumulators, the chunk's dpre rows
+// staged in LDS -- and the caller's slab_rows_sum reduces over S in a fixed order (deterministic, no atomics).
+namespace qd {
+namespace qsc {
+constexpr int OUTER_MAXN = 16;
+__global__ void __launch_bounds__(256) outer_partial_kernel(const float* __restrict__ D, const float* __restrict__ P,
+                                                            float* __restrict__ slab, int B, int n, int F, int bs) {
+  __shared__ float ds[64 * OUTER_MAXN];
+  const int s = blockIdx.y, f = blockIdx.x * 256 + threadIdx.x;
+  const int b0 = s * bs, b1 = min(B, b0 + bs);
+  float acc[OUTER_MAXN];
+#pragma unroll
+  for (int i = 0; i < OUTER_MAXN; ++i) acc[i] = 0.f;
+  for (int c0 = b0; c0 < b1; c0 += 64) {
+    const int cn = min(64, b1 - c0);
+    __syncthreads();
+    for (int t = threadIdx.x; t < cn * n; t += 256) ds[t] = D[(size_t)c0 * n + t];
+    __syncthreads();
+    if (f < F) {
+      for (int b = 0; b < cn; ++b) {
+        const float p = P[(size_t)(c0 + b) * F + f];
+#pragma unroll
+        for (int i = 0; i < OUTER_MAXN; ++i)
+          if (i < n) acc[i] += ds[b * n + i] * p;
+      }
+    }
+  }
+  if (f < F) {
+#pragma unroll
+    for (int i = 0; i < OUTER_MAXN; ++i)
+      if (i < n) slab[((size_t)s * n + i) * F + f] = acc[i];
+  }
+}
+}  // namespace qsc
+}  // namespace qd
+
+// phase 1 of dWl = D^T P (see above): slab (S, n, F) with S = ceil(B / bs)
+QD_API int qd_outer_partial(const float* D, const float* P, float* slab, int B, int n, int F, int bs, void* stream) {
+  if (n < 1 || n > qd::qsc::OUTER_MAXN || bs < 1 || B < 1 || F < 1) return (int)hipErrorInvalidValue;
+  const int S = (B + bs - 1) / bs;
+  hipLaunchKernelGGL(qd::qsc::outer_partial_kernel, dim3((F + 255) / 256, S), dim3(256), 0, (hipStream_t)stream, D, P,
+                     slab, B, n, F, bs);
+  return (int)hipGetLastError();
+}

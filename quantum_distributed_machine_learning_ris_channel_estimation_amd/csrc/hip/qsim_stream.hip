@@ -18,15 +18,21 @@
 //            every global load and store of both passes is coalesced.
 //
 // Forward (L layers): pass A of layer 1 GENERATES its input (the ring image of the layer-0 product
-// state) instead of loading it, then B, A, B, ...; the last pass B stores psi_final (kept for the
-// backward) and per-tile <Z_q> partials.  Backward: per layer in reverse, pass B (gather at the
-// ring image, undo rotations 11..8 with d(theta), d(phi) partials) and pass A (undo the rest; layer 0
-// stores nothing).  lambda = (sum_q g_q Z_q) psi is formed while loading the first pass.  Gradient
-// partials go to a slab of 16 rows per sample (every column written once per row): the caller's
-// slab reduction sums them; dx = the layer-0 theta columns, reduced per sample here.
+// state) instead of loading it, then B, A, B, ...; every pass A's output S_l is KEPT (the backward's
+// psi, round 3: HBM has room -- 1.2 GB per state at n = 16, B = 2304), the passes B write a scratch
+// state, and the last pass B stores nothing: it only reduces the per-tile <Z_q> partials.
+// Backward: per layer in reverse, pass B (lambda gathered at the ring image, psi = S_l with the layer's
+// rotations 8..11 re-applied in registers; undo rotations 11..8 with d(theta), d(phi) partials) and pass A
+// (psi = S_l, undo the rest); only lambda is written -- psi is never un-applied back to memory.  Layer 0's
+// psi is the product state, generated in-kernel; once its qubits 8..11 are undone it is zero outside the
+// brick whose bits 8..11 are 0, so layer 0's pass B stores only that part of lambda and its pass A reads
+// only that brick.  lambda = (sum_q g_q Z_q) psi_final is formed in registers by the first pass B (psi_final
+// at the ring image of a tile = that tile's rotated psi).  Gradient partials go to a slab of 16 rows per
+// sample (every column written once per row): the caller's slab reduction sums them; dx = the layer-0
+// theta columns, reduced per sample here.
 //
-// State traffic at n = 16, L = 3: forward 7 state passes (1 write + 3 read/write pairs), backward
-// 19 (both psi and lambda) -- vs the per-sample kernel's ~7 and ~26 passes at a third of the rate.
+// State traffic at n = 16, L = 3 (1.2 GB per state): forward 6 state passes, backward ~12 (round 2: 7 and
+// 21, with psi un-applied and re-stored in every backward pass).
 #include "common.h"
 
 namespace qd {
@@ -80,6 +86,35 @@ __device__ __forceinline__ int ins_bits(int t) {
 __device__ __forceinline__ int brick_k(int e, int br) { return (e & 255) | (br << 8) | ((e >> 8) << 12); }
 // pass-A brick bit -> qubit
 __device__ __forceinline__ constexpr int brick_q(int b) { return b < 8 ? b : b + 4; }
+
+// Layer-0 product state (embedding + layer-0 rotations on |0..0>, BEFORE its ring) as two tables: amplitude
+// of basis state k = PL[k & 255] * PH[k >> 8] (qubits 0..7 / 8..N-1).  Qubits in `zero` (a mask) are taken
+// back to |0> (their gates already undone by the adjoint).  trig0: layer-0 (cos, sin) per qubit.  NTH threads
+// (any count: the 256 entries are strided over them).
+template <int N, int NTH>
+__device__ __forceinline__ void product_tables(const float4* trig0, cf* PL, cf* PH, int zero) {
+  for (int i = threadIdx.x; i < 256; i += NTH) {
+    cf a = {1.f, 0.f}, h = {1.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 t = trig0[q];
+      const bool one = (i >> q) & 1;
+      const cf f = ((zero >> q) & 1) ? cf{one ? 0.f : 1.f, 0.f}
+                                     : (one ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
+      a = cmul(a, f);
+    }
+#pragma unroll
+    for (int q = 8; q < N; ++q) {
+      const float4 t = trig0[q];
+      const bool one = (i >> (q - 8)) & 1;
+      const cf f = ((zero >> q) & 1) ? cf{one ? 0.f : 1.f, 0.f}
+                                     : (one ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
+      h = cmul(h, f);
+    }
+    PL[i] = a;
+    if (i < (1 << (N - 8))) PH[i] = h;
+  }
+}
 
 // RZ(phi) RY(theta) on the pair (a0: bit 0, a1: bit 1); t = (cos th/2, sin th/2, cos ph/2, sin ph/2)
 __device__ __forceinline__ void gate_fwd(cf& a0, cf& a1, float4 t) {
@@ -183,7 +218,7 @@ __device__ __forceinline__ void lds_gates(cf* tp, cf* tq, const float4* trig, fl
 // pass A of layer l (GEN: layer 1, its input generated: the ring image of the layer-0 product state)
 template <int N, bool GEN>
 __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x, const float* __restrict__ w, int L,
-                                                 int l, int wgroup, cf* __restrict__ state) {
+                                                 int l, int wgroup, const cf* __restrict__ in, cf* __restrict__ out) {
   using C = SG<N>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float4* trig = reinterpret_cast<float4*>(smem);          // 16
@@ -193,35 +228,21 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
   load_trig<N>(trig, x, w, s, L, l, wgroup);
   if constexpr (GEN) load_trig<N>(trig0, x, w, s, L, 0, wgroup);
   __syncthreads();
-  cf* st = state + (size_t)s * C::D;
+  cf* st = out + (size_t)s * C::D;
   if constexpr (GEN) {
-    // product amplitude of basis state k = PL[k & 255] * PH[k >> 8] (tables over 8 / n-8 qubits)
+    // the ring image of the layer-0 product state: amplitude at k = product at ring^-1(k)
     cf* PL = tp + C::AS;
     cf* PH = PL + 256;
-    {
-      const int i = threadIdx.x;   // (NT == 256 entries of each table)
-      cf a = {1.f, 0.f}, h = {1.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float4 t = trig0[q];
-        a = cmul(a, ((i >> q) & 1) ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
-      }
-#pragma unroll
-      for (int q = 8; q < N; ++q) {
-        const float4 t = trig0[q];
-        h = cmul(h, ((i >> (q - 8)) & 1) ? cf{t.y * t.z, t.y * t.w} : cf{t.x * t.z, -t.x * t.w});
-      }
-      PL[i] = a;
-      if (i < (1 << (N - 8))) PH[i] = h;
-    }
+    product_tables<N, NT>(trig0, PL, PH, 0);
     __syncthreads();
     for (int e = threadIdx.x; e < C::AS; e += NT) {
       const int k = ring_inv<N>(brick_k(e, br));
       tp[e] = cmul(PL[k & 255], PH[k >> 8]);
     }
   } else {
+    const cf* si = in + (size_t)s * C::D;
     for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NT)
-      *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(st + brick_k(e, br));
+      *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(si + brick_k(e, br));
   }
   __syncthreads();
   float dth[C::AB], dph[C::AB];
@@ -231,7 +252,7 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
 }
 
 // pass B of layer l: qubits 8..11 in registers, the ring as an LDS scatter, two coalesced output runs.
-// LAST: also the per-tile <Z_q> partials epart[(s * NTILE + t) * N + q].
+// LAST: only the per-tile <Z_q> partials epart[(s * NTILE + t) * N + q] (no state store).
 template <int N, bool LAST>
 __global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x, const float* __restrict__ w, int L,
                                                  int l, int wgroup, const cf* __restrict__ in, cf* __restrict__ out,
@@ -266,7 +287,7 @@ __global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x,
   for (int i = 2 * threadIdx.x; i < 4096; i += 2 * NT) {
     const int j = i | ((i & 2048 ? A1 : A0) << 12);
     const float4 v = *reinterpret_cast<const float4*>(tp + i);
-    *reinterpret_cast<float4*>(dst + j) = v;
+    if constexpr (!LAST) *reinterpret_cast<float4*>(dst + j) = v;   // (the last pass keeps no state)
     if constexpr (LAST) {
       const float p0 = v.x * v.x + v.y * v.y, p1 = v.z * v.z + v.w * v.w;
 #pragma unroll
@@ -296,29 +317,34 @@ __global__ void __launch_bounds__(256) reduce_e(const float* __restrict__ epart,
 }
 
 // ----------------------------------------------------------------------------------------- backward
-// Reverse pass B of layer l: gather psi (and lambda, or FIRST: form it from psi and gE) at the ring
-// images, undo rotations 11..8, store tile order.  Slab row s*16 + t*(16/NTILE) gets the 8 partials
-// of qubits 8..11 (the other rows of the tile's group get zeros in those columns).
-template <int N, bool FIRST>
+// Reverse pass B of layer l.  psi of the tile (pre-ring order, thread c owns the 16 amplitudes that differ in
+// bits 8..11): S_l with the layer's rotations 8..11 re-applied in registers, or (GEN0, layer 0) the product
+// state.  lambda: gathered at the ring images (two coalesced runs, LDS scatter into pre-ring order), or
+// (FIRST) formed in registers as O(ring(k)) psi(k).  Rotations 11..8 undone in registers with their
+// d(theta), d(phi); lambda stored in pre-ring tile order (GEN0: only its bits-8..11 = 0 part, the only one
+// layer 0's pass A reads).  Slab row s*16 + t*(16/NTILE) gets the 8 partials of qubits 8..11 (the other rows
+// of the tile's group get zeros in those columns).
+template <int N, bool FIRST, bool GEN0>
 __global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x, const float* __restrict__ w,
                                                  const float* __restrict__ gE, int L, int l, int wgroup,
-                                                 const cf* __restrict__ pin, const cf* __restrict__ lin,
-                                                 cf* __restrict__ pout, cf* __restrict__ lout, float* __restrict__ slab) {
+                                                 const cf* __restrict__ psi, const cf* __restrict__ lin,
+                                                 cf* __restrict__ lout, float* __restrict__ slab) {
   using C = SG<N>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float4* trig = reinterpret_cast<float4*>(smem);
   float* gq = reinterpret_cast<float*>(smem + 256);       // 16
   float* red = reinterpret_cast<float*>(smem + 320);      // NWV * 8
-  cf* tp = reinterpret_cast<cf*>(smem + 512);
-  cf* tq = tp + 4096;
-  const int t = blockIdx.x, s = blockIdx.y;
-  load_trig<N>(trig, x, w, s, L, l, wgroup);
-  // (FIRST) o(j) = sum_q g_q (1 - 2 bit_q(j)) = OL[j & 255] + OH[j >> 8]
-  float* OL = reinterpret_cast<float*>(tq + 4096);
+  cf* tp = reinterpret_cast<cf*>(smem + 512);             // psi, pre-ring tile order
+  cf* tq = tp + 4096;                                     // lambda, pre-ring tile order
+  float* OL = reinterpret_cast<float*>(tq + 4096);        // (FIRST) observable tables
   float* OH = OL + 256;
+  cf* PL = reinterpret_cast<cf*>(OH + 256);               // (GEN0) product tables
+  cf* PH = PL + 256;
+  const int t = blockIdx.x, s = blockIdx.y, c = threadIdx.x;
+  load_trig<N>(trig, x, w, s, L, l, wgroup);
   if (FIRST && threadIdx.x < N) gq[threadIdx.x] = gE[(size_t)s * N + threadIdx.x];
   __syncthreads();
-  if constexpr (FIRST) {
+  if constexpr (FIRST) {   // o(j) = sum_q g_q (1 - 2 bit_q(j)) = OL[j & 255] + OH[j >> 8]
     const int i = threadIdx.x;
     float ol = 0.f, oh = 0.f;
 #pragma unroll
@@ -327,38 +353,53 @@ __global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x,
     for (int q = 8; q < N; ++q) oh += ((i >> (q - 8)) & 1) ? -gq[q] : gq[q];
     OL[i] = ol;
     if (i < (1 << (N - 8))) OH[i] = oh;
-    __syncthreads();
   }
-  const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
-  const cf* ps = pin + (size_t)s * C::D;
-  const cf* ls = FIRST ? nullptr : lin + (size_t)s * C::D;
-#pragma unroll 2
-  for (int i = threadIdx.x; i < 4096; i += NT) {
-    const int j = i | ((i & 2048 ? A1 : A0) << 12);
-    const int kk = ring_inv<N>(j) & 4095;
-    const cf p = ps[j];
-    cf m;
-    if constexpr (FIRST) {
-      const float o = OL[j & 255] + OH[j >> 8];
-      m = {p.x * o, p.y * o};
-    } else {
-      m = ls[j];
+  if constexpr (GEN0) product_tables<N, NT>(trig, PL, PH, 0);
+  if constexpr (!FIRST) {   // lambda at the ring images -> pre-ring order in LDS
+    const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
+    const cf* ls = lin + (size_t)s * C::D;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < 4096; i += NT) {
+      const int j = i | ((i & 2048 ? A1 : A0) << 12);
+      tq[ring_inv<N>(j) & 4095] = ls[j];
     }
-    tp[kk] = p;
-    tq[kk] = m;
+  }
+  if constexpr (!GEN0) {   // psi = S_l with this layer's rotations 8..11 re-applied (registers)
+    const cf* src = psi + (size_t)s * C::D + ((size_t)t << 12);
+    cf p[16];
+#pragma unroll
+    for (int h = 0; h < 16; ++h) p[h] = src[(h << 8) | c];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const float4 tg = trig[8 + b];
+#pragma unroll
+      for (int h = 0; h < 16; ++h)
+        if (!((h >> b) & 1)) gate_fwd(p[h], p[h | (1 << b)], tg);
+    }
+#pragma unroll
+    for (int h = 0; h < 16; ++h) tp[(h << 8) | c] = p[h];
   }
   __syncthreads();
+  if constexpr (GEN0) {
+    for (int i = threadIdx.x; i < 4096; i += NT) tp[i] = cmul(PL[i & 255], PH[(t << 4) | (i >> 8)]);
+  }
+  if constexpr (FIRST) {   // lambda = O psi_final, psi_final(ring(k)) = psi(k)
+    for (int i = threadIdx.x; i < 4096; i += NT) {
+      const int j = ring_fwd<N>((t << 12) | i);
+      const float o = OL[j & 255] + OH[j >> 8];
+      const cf p = tp[i];
+      tq[i] = {p.x * o, p.y * o};
+    }
+  }
+  if constexpr (GEN0 || FIRST) __syncthreads();
   // undo rotations 11..8 on the tile in LDS (two groups: bits 11 .. 9, bit 8)
   float dth[4], dph[4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) dth[b] = dph[b] = 0.f;
   lds_gates<12, 8, 4, true, true>(tp, tq, trig, dth, dph);
-  cf* po = pout + (size_t)s * C::D + ((size_t)t << 12);
   cf* lo = lout + (size_t)s * C::D + ((size_t)t << 12);
-  for (int i = 2 * threadIdx.x; i < 4096; i += 2 * NT) {
-    *reinterpret_cast<float4*>(po + i) = *reinterpret_cast<const float4*>(tp + i);
+  for (int i = 2 * threadIdx.x; i < (GEN0 ? 256 : 4096); i += 2 * NT)
     *reinterpret_cast<float4*>(lo + i) = *reinterpret_cast<const float4*>(tq + i);
-  }
   float v[8];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -378,12 +419,14 @@ __global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x,
   }
 }
 
-// Reverse pass A of layer l (in place; STORE = false for layer 0, whose result nothing reads).  512
-// threads: the adjoint sweep is latency-bound (dependent gradient sums), and the 64 KiB of psi + lambda
-// per workgroup allow only 2 workgroups per CU -- twice the waves hide it better.
-template <int N, bool STORE>
+// Reverse pass A of layer l: psi = S_l (read only; GEN0: layer 0's product state with qubits 8..11 back at
+// |0>, which is zero outside brick 0 -- the other bricks only write zero partials), lambda in place (STORE
+// = false for layer 0, whose result nothing reads).  512 threads: the adjoint sweep is latency-bound
+// (dependent gradient sums), and the 64 KiB of psi + lambda per workgroup allow only 2 workgroups per CU --
+// twice the waves hide it better.
+template <int N, bool STORE, bool GEN0>
 __global__ void __launch_bounds__(SG<N>::NTA, 4) pass_a_bwd(const float* __restrict__ x, const float* __restrict__ w, int L,
-                                                 int l, int wgroup, cf* __restrict__ pst, cf* __restrict__ lst,
+                                                 int l, int wgroup, const cf* __restrict__ pst, cf* __restrict__ lst,
                                                  float* __restrict__ slab) {
   using C = SG<N>;
   constexpr int NTA = C::NTA;
@@ -393,13 +436,32 @@ __global__ void __launch_bounds__(SG<N>::NTA, 4) pass_a_bwd(const float* __restr
   cf* tp = reinterpret_cast<cf*>(smem + 1024);
   cf* tq = tp + C::AS;
   const int br = blockIdx.x, s = blockIdx.y;
+  const int P = 2 * N * L;
+  if (GEN0 && br != 0) {   // psi = 0 on this brick: no gradient contribution
+    if (threadIdx.x < 2 * C::AB)
+      slab[((size_t)s * ROWS + br) * P + (l * N + brick_q(threadIdx.x / 2)) * 2 + (threadIdx.x & 1)] = 0.f;
+    return;
+  }
   load_trig<N>(trig, x, w, s, L, l, wgroup);
-  cf* ps = pst + (size_t)s * C::D;
   cf* ls = lst + (size_t)s * C::D;
-  for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
-    const int k = brick_k(e, br);
-    *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(ps + k);
-    *reinterpret_cast<float4*>(tq + e) = *reinterpret_cast<const float4*>(ls + k);
+  if constexpr (GEN0) {
+    cf* PL = tq + C::AS;
+    cf* PH = PL + 256;
+    __syncthreads();
+    product_tables<N, NTA>(trig, PL, PH, 0xF00);
+    __syncthreads();
+    for (int e = threadIdx.x; e < C::AS; e += NTA) {
+      const int k = brick_k(e, 0);
+      tp[e] = cmul(PL[k & 255], PH[k >> 8]);
+      tq[e] = ls[k];
+    }
+  } else {
+    const cf* ps = pst + (size_t)s * C::D;
+    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
+      const int k = brick_k(e, br);
+      *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(ps + k);
+      *reinterpret_cast<float4*>(tq + e) = *reinterpret_cast<const float4*>(ls + k);
+    }
   }
   __syncthreads();
   float dth[C::AB], dph[C::AB];
@@ -407,11 +469,8 @@ __global__ void __launch_bounds__(SG<N>::NTA, 4) pass_a_bwd(const float* __restr
   for (int b = 0; b < C::AB; ++b) dth[b] = dph[b] = 0.f;
   lds_gates<C::AB, 0, C::AB, false, true, NTA>(tp, tq, trig, dth, dph);
   if constexpr (STORE) {
-    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
-      const int k = brick_k(e, br);
-      *reinterpret_cast<float4*>(ps + k) = *reinterpret_cast<const float4*>(tp + e);
-      *reinterpret_cast<float4*>(ls + k) = *reinterpret_cast<const float4*>(tq + e);
-    }
+    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA)
+      *reinterpret_cast<float4*>(ls + brick_k(e, br)) = *reinterpret_cast<const float4*>(tq + e);
   }
   float v[2 * C::AB], o[2 * C::AB];
 #pragma unroll
@@ -421,7 +480,6 @@ __global__ void __launch_bounds__(SG<N>::NTA, 4) pass_a_bwd(const float* __restr
   }
   block_sum_vec<2 * C::AB, NTA>(v, red, o);
   if (threadIdx.x < 2 * C::AB) {
-    const int P = 2 * N * L;
     const int q = brick_q(threadIdx.x / 2);
     slab[((size_t)s * ROWS + br) * P + (l * N + q) * 2 + (threadIdx.x & 1)] = o[threadIdx.x];
   }
@@ -443,23 +501,24 @@ template <int N>
 struct Smem {
   static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + 512);   // (+ the GEN product tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
-  static constexpr size_t B_BWD = 512 + 2 * sizeof(cf) * 4096 + 2048;   // (+ the FIRST observable tables)
-  static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * SG<N>::AS;
+  static constexpr size_t B_BWD = 512 + 2 * sizeof(cf) * 4096 + 2048 + sizeof(cf) * 512;   // (+ FIRST / GEN0 tables)
+  static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * SG<N>::AS + sizeof(cf) * 512;  // (+ GEN0 tables)
 };
 
 inline size_t state_bytes(int n, int B) { return (size_t)B * (8ull << n); }
+inline size_t epart_bytes(int n, int B) { return ((size_t)B * (1ull << (n - 12)) * n * 4 + 255) & ~(size_t)255; }
 
+// Forward.  ws: [T: pass-B outputs][<Z> partials][S: pass-A outputs when psave is null].  psave (nullable):
+// L - 1 states, S_l = pass A of layer l's output (the backward's psi).
 template <int N>
 static int fwd(const float* x, const float* w, float* E, int B, int L, int wgroup, char* ws, cf* psave,
                hipStream_t st) {
   using C = SG<N>;
   using S = Smem<N>;
-  cf* U = psave ? psave : reinterpret_cast<cf*>(ws);
-  cf* V = reinterpret_cast<cf*>(ws + state_bytes(N, B));
-  float* epart = reinterpret_cast<float*>(ws + 2 * state_bytes(N, B));
-  // (L-1) pass-B swaps: start where the final state must land (U)
-  cf* cur = ((L - 1) % 2 == 0) ? U : V;
-  cf* oth = (cur == U) ? V : U;
+  const size_t sb = state_bytes(N, B);
+  cf* T = reinterpret_cast<cf*>(ws);
+  float* epart = reinterpret_cast<float*>(ws + sb);
+  cf* S0 = reinterpret_cast<cf*>(ws + sb + epart_bytes(N, B));
   static bool attr = false;
   if (!attr) {
     (void)allow_lds(pass_a_fwd<N, true>, S::A_FWD);
@@ -470,62 +529,61 @@ static int fwd(const float* x, const float* w, float* E, int B, int L, int wgrou
   }
   const dim3 ga(ROWS, B), gb(C::NTILE, B);
   for (int l = 1; l < L; ++l) {
+    cf* a_out = psave ? reinterpret_cast<cf*>(reinterpret_cast<char*>(psave) + (size_t)(l - 1) * sb) : S0;
     if (l == 1)
-      hipLaunchKernelGGL((pass_a_fwd<N, true>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, cur);
+      hipLaunchKernelGGL((pass_a_fwd<N, true>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, nullptr, a_out);
     else
-      hipLaunchKernelGGL((pass_a_fwd<N, false>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, cur);
+      hipLaunchKernelGGL((pass_a_fwd<N, false>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, T, a_out);
     if (l == L - 1)
-      hipLaunchKernelGGL((pass_b_fwd<N, true>), gb, dim3(NT), S::B_FWD, st, x, w, L, l, wgroup, cur, oth, epart);
+      hipLaunchKernelGGL((pass_b_fwd<N, true>), gb, dim3(NT), S::B_FWD, st, x, w, L, l, wgroup, a_out, nullptr, epart);
     else
-      hipLaunchKernelGGL((pass_b_fwd<N, false>), gb, dim3(NT), S::B_FWD, st, x, w, L, l, wgroup, cur, oth, epart);
-    cf* tmp = cur;
-    cur = oth;
-    oth = tmp;
+      hipLaunchKernelGGL((pass_b_fwd<N, false>), gb, dim3(NT), S::B_FWD, st, x, w, L, l, wgroup, a_out, T, epart);
   }
   if (E) hipLaunchKernelGGL(reduce_e<N>, dim3((B * N + 255) / 256), dim3(256), 0, st, epart, E, B);
   return (int)hipGetLastError();
 }
 
+// Backward.  ws: [lambda 1][lambda 2][forward ws: T, <Z> partials][L - 1 kept states when psave is null].
 template <int N>
 static int bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int L, int wgroup,
                char* ws, cf* psave, hipStream_t st) {
   using C = SG<N>;
   using S = Smem<N>;
   const size_t sb = state_bytes(N, B);
-  cf* W1 = reinterpret_cast<cf*>(ws);
-  cf* W2 = reinterpret_cast<cf*>(ws + sb);
-  cf* W3 = reinterpret_cast<cf*>(ws + 2 * sb);
-  if (psave == nullptr) {   // no kept state: run the forward into the 4th slot (its own scratch: slots 1, 2)
-    psave = reinterpret_cast<cf*>(ws + 3 * sb);
-    if (int e = fwd<N>(x, w, nullptr, B, L, wgroup, ws, psave, st)) return e;
+  cf* L1 = reinterpret_cast<cf*>(ws);
+  cf* L2 = reinterpret_cast<cf*>(ws + sb);
+  if (psave == nullptr) {   // no kept states: run the forward first
+    psave = reinterpret_cast<cf*>(ws + 3 * sb + epart_bytes(N, B));
+    if (int e = fwd<N>(x, w, nullptr, B, L, wgroup, ws + 2 * sb, psave, st)) return e;
   }
   static bool attr = false;
   if (!attr) {
-    (void)allow_lds(pass_b_bwd<N, true>, S::B_BWD);
-    (void)allow_lds(pass_b_bwd<N, false>, S::B_BWD);
-    (void)allow_lds(pass_a_bwd<N, true>, S::A_BWD);
-    (void)allow_lds(pass_a_bwd<N, false>, S::A_BWD);
+    (void)allow_lds(pass_b_bwd<N, true, false>, S::B_BWD);
+    (void)allow_lds(pass_b_bwd<N, false, false>, S::B_BWD);
+    (void)allow_lds(pass_b_bwd<N, false, true>, S::B_BWD);
+    (void)allow_lds(pass_a_bwd<N, true, false>, S::A_BWD);
+    (void)allow_lds(pass_a_bwd<N, false, true>, S::A_BWD);
     attr = true;
   }
   const dim3 ga(ROWS, B), gb(C::NTILE, B);
-  // (psi, lambda) buffers: psave -> (W1, W2) -> (psave, W3) -> (W1, W2) -> ...
-  cf* pin = psave;
-  cf* lin = nullptr;
+  const cf* lin = nullptr;
   for (int l = L - 1; l >= 0; --l) {
-    const bool even = ((L - 1 - l) % 2) == 0;
-    cf* po = even ? W1 : psave;
-    cf* lo = even ? W2 : W3;
+    cf* lo = ((L - 1 - l) % 2 == 0) ? L1 : L2;
+    const cf* ps = l > 0 ? reinterpret_cast<const cf*>(reinterpret_cast<const char*>(psave) + (size_t)(l - 1) * sb)
+                         : nullptr;
     if (l == L - 1)
-      hipLaunchKernelGGL((pass_b_bwd<N, true>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, pin, lin, po, lo,
+      hipLaunchKernelGGL((pass_b_bwd<N, true, false>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, ps, lin, lo,
+                         slab);
+    else if (l > 0)
+      hipLaunchKernelGGL((pass_b_bwd<N, false, false>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, ps, lin, lo,
                          slab);
     else
-      hipLaunchKernelGGL((pass_b_bwd<N, false>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, pin, lin, po, lo,
+      hipLaunchKernelGGL((pass_b_bwd<N, false, true>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, ps, lin, lo,
                          slab);
     if (l > 0)
-      hipLaunchKernelGGL((pass_a_bwd<N, true>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, po, lo, slab);
+      hipLaunchKernelGGL((pass_a_bwd<N, true, false>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps, lo, slab);
     else
-      hipLaunchKernelGGL((pass_a_bwd<N, false>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, po, lo, slab);
-    pin = po;
+      hipLaunchKernelGGL((pass_a_bwd<N, false, true>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps, lo, slab);
     lin = lo;
   }
   hipLaunchKernelGGL(reduce_dx, dim3((B * N + 255) / 256), dim3(256), 0, st, slab, dx, B, N, 2 * N * L);
@@ -552,15 +610,21 @@ QD_API int qd_qsim_stream_ok(int n, int L) { return n >= 13 && n <= 16 && L >= 2
 // Slab rows of the backward's weight-gradient partials: 16 per sample.
 QD_API int qd_qsim_stream_rows(int B) { return B * ROWS; }
 
-// Workspace bytes: forward 2 states + the <Z> partials; backward 4 states (3 + one for a forward
-// recompute when the caller kept no state).
-QD_API long long qd_qsim_stream_workspace(int n, int B, int backward) {
-  const long long sb = (long long)state_bytes(n, B);
-  const long long ep = (long long)B * (1ll << (n - 12)) * n * 4;
-  return backward ? 4 * sb + ep : 2 * sb + ep;
+// Workspace bytes (see fwd / bwd): forward 2 states + the <Z> partials; backward 3 states + the partials +
+// the L - 1 kept states of a forward recompute (used when the caller kept none).
+QD_API long long qd_qsim_stream_workspace(int n, int B, int L, int backward) {
+  if (n < 13 || n > 16 || B < 1 || L < 2) return 0;
+  const long long sb = (long long)state_bytes(n, B), ep = (long long)epart_bytes(n, B);
+  return backward ? (3 + (long long)(L - 1)) * sb + ep : 2 * sb + ep;
 }
 
-// E (B, n) = <Z>; psave (nullable): (B, 2^n) complex64 psi_final for qd_qsim_stream_bwd.
+// Bytes of the forward's kept states (psave): L - 1 states of B x 2^n complex64.
+QD_API long long qd_qsim_stream_save_bytes(int n, int B, int L) {
+  if (n < 13 || n > 16 || B < 1 || L < 2) return 0;
+  return (long long)(L - 1) * (long long)state_bytes(n, B);
+}
+
+// E (B, n) = <Z>; psave (nullable): qd_qsim_stream_save_bytes of kept states for qd_qsim_stream_bwd.
 QD_API int qd_qsim_stream_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
                               void* psave, void* stream) {
   if (!qd_qsim_stream_ok(n, L) || B < 1 || ws == nullptr) return (int)hipErrorInvalidValue;

@@ -84,6 +84,9 @@ class QSCStepHIP:
             # the backward kernel also reduces dWl = dpre^T p2 into its slab when it fits; else a GEMM
             self.wl_in_kernel = bool(nat.fn(nat.hip_lib(), "qd_qsc2_wl_in_kernel", [_i, _i, _i])(
                 self.Hh, self.Ww, self.n))
+            if not self.wl_in_kernel:   # (the outer-product partials of qd_outer_partial: 36 samples per chunk)
+                self.wl_bs = 36
+                self.wlslab = torch.empty(-(-batch_total // self.wl_bs), self.n * feat, **f32)
         else:
             self.grid_fwd = min(grid_fwd, batch_total)
             self.grid_bwd = min(grid_bwd, batch_total)
@@ -100,10 +103,12 @@ class QSCStepHIP:
         self.stream = self.big and stream_sim_ok(self.n, self.L)
         if self.stream:
             self.qrows = nat.fn(L, "qd_qsim_stream_rows", [_i])(batch_total)
-            ws = nat.fn(L, "qd_qsim_stream_workspace", [_i, _i, _i], ctypes.c_longlong)
-            nb = max(ws(self.n, batch_total, 0), ws(self.n, batch_total, 1))
+            ws = nat.fn(L, "qd_qsim_stream_workspace", [_i, _i, _i, _i], ctypes.c_longlong)
+            nb = max(ws(self.n, batch_total, self.L, 0), ws(self.n, batch_total, self.L, 1))
             self.qws = torch.empty(nb, dtype=torch.uint8, device=dev)
-            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev) \
+            # the forward keeps every layer's pass-A output (L - 1 states: the backward's psi, never un-applied)
+            sv = nat.fn(L, "qd_qsim_stream_save_bytes", [_i, _i, _i], ctypes.c_longlong)(self.n, batch_total, self.L)
+            self.psave = torch.empty(sv, dtype=torch.uint8, device=dev) \
                 if os.environ.get("QDML_QSIM_SAVE_STATE", "1") != "0" else None
         elif self.big:
             cap = int(os.environ.get("QDML_QSIM_BIG_GRID", "0"))   # (0: the library default)
@@ -151,6 +156,7 @@ class QSCStepHIP:
             self._qb = nat.fn(L, "qd_qsim_bwd_saved", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
         self._rs = nat.fn(L, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
         self._ssum = nat.fn(L, "qd_slab_rows_sum", [_p, _p, _i, _i, _i, _i, _p])
+        self._outer = nat.fn(L, "qd_outer_partial", [_p, _p, _p, _i, _i, _i, _i, _p])
         self._qnoise = nat.fn(L, "qd_qnoise", [_p, _p, _i, _i, _f, ctypes.c_ulonglong, _p, _p])
         wq = model.qlayer.weights
         self.wnoisy = torch.empty((n_groups,) + tuple(wq.shape), **f32)
@@ -279,9 +285,11 @@ class QSCStepHIP:
                                                                    self.grid_bwd, self.row)
         own.launch(accumulate, st)
         if gemm_wl:
-            # linear weight grad over the batch (one GEMM); the slab row left these columns 0
-            if accumulate:
-                self.gwl.addmm_(self.dpre.t(), self.p2)
-            else:
-                torch.mm(self.dpre.t(), self.p2, out=self.gwl)
+            # linear weight grad over the batch, dWl = dpre^T p2 (the slab row left these columns 0): per-chunk
+            # outer-product partials + one slab reduction over the chunks (csrc/hip/qsc.hip qd_outer_partial)
+            Bt, F = self.p2.shape
+            nat.check(self._outer(nat.ptr(self.dpre), nat.ptr(self.p2), nat.ptr(self.wlslab), Bt, self.n, F,
+                                  self.wl_bs, st), "qsc_outer_partial")
+            nat.check(self._ssum(nat.ptr(self.wlslab), nat.ptr(self.gwl), 1, self.wlslab.shape[0], self.n * F,
+                                 int(accumulate), st), "qsc_wl_slab_sum")
         return self.loss

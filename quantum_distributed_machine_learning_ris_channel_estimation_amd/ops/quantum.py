@@ -45,8 +45,9 @@ def stream_sim_ok(n: int, L: int) -> bool:
     return bool(nat.fn(nat.hip_lib(), "qd_qsim_stream_ok", [_i, _i])(n, L))
 
 
-def _stream_ws(n: int, B: int, backward: bool, device) -> torch.Tensor:
-    nbytes = nat.fn(nat.hip_lib(), "qd_qsim_stream_workspace", [_i, _i, _i], ctypes.c_longlong)(n, B, int(backward))
+def _stream_ws(n: int, B: int, L: int, backward: bool, device) -> torch.Tensor:
+    nbytes = nat.fn(nat.hip_lib(), "qd_qsim_stream_workspace", [_i, _i, _i, _i], ctypes.c_longlong)(n, B, L,
+                                                                                                 int(backward))
     return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
 
@@ -66,7 +67,7 @@ def hip_qsim_fwd(x: torch.Tensor, w: torch.Tensor, E: torch.Tensor, wgroup: int 
         nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, st), "qd_qsim_fwd")
         return
     if stream_sim_ok(n, L):
-        ws = _stream_ws(n, B, False, x.device)
+        ws = _stream_ws(n, B, L, False, x.device)
         f = nat.fn(lib, "qd_qsim_stream_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
         nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, nat.ptr(ws), None, st), "qd_qsim_stream_fwd")
         return
@@ -93,7 +94,7 @@ def hip_qsim_bwd_slab(x: torch.Tensor, w: torch.Tensor, gE: torch.Tensor, dx: to
         return slab
     if stream_sim_ok(n, L):
         slab = torch.empty(nat.fn(lib, "qd_qsim_stream_rows", [_i])(B), P, device=x.device, dtype=torch.float32)
-        ws = _stream_ws(n, B, True, x.device)
+        ws = _stream_ws(n, B, L, True, x.device)
         f = nat.fn(lib, "qd_qsim_stream_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
         nat.check(f(nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup_of(x, w),
                     nat.ptr(ws), None, st), "qd_qsim_stream_bwd")

@@ -156,7 +156,9 @@ class model_val:
                 pred = eng.classify(x, tag)   # the HIP kernels: classifier, experts, routed FC (train/infer.py)
             else:   # (CPU, or the classical-fallback QSC ablation: torch)
                 pred = torch.cat([clf(x[i:i + chunk]).argmax(1) for i in range(0, x.shape[0], chunk)])
-            saved = recalibrate_bn(convs, x, pred) if self.bn_adapt else None
+            saved = None
+            if self.bn_adapt:   # (GPU: the HIP training conv forward computes the statistics, no MIOpen)
+                saved = eng.recalibrate_bn(convs, x, pred) if eng is not None else recalibrate_bn(convs, x, pred)
             if eng is not None:
                 if saved is not None:
                     eng.load_bn_stats(convs)
@@ -165,6 +167,8 @@ class model_val:
                 Hhat = estimate_routed(convs, fc, x, pred)
             if saved is not None:
                 restore_bn(convs, saved)
+                if eng is not None:
+                    eng.load_bn_stats(convs)   # (the engine keeps copies: hand the restored statistics back)
             out[f"nmse_{tag}"] = float(criterion(Hhat, perf))
             out[f"acc_{tag}"] = float((pred == ind).float().mean())
         return out

@@ -42,6 +42,7 @@ class HIPInference:
         self.chunk = chunk
         self.H, self.W = pilot_grid(pilot_num)
         self.E = len(convs)
+        self.pilot_num = pilot_num
         # the estimator: an HDCEModel holding the checkpoint's experts + FC (its grouped buffers are what
         # the conv kernels read), eval mode
         m = HDCEModel(pilot_num, self.dev, "bf16", self.E)
@@ -91,6 +92,59 @@ class HIPInference:
             for d, s_ in zip(dst, src):
                 d.running_mean.copy_(s_.running_mean)
                 d.running_var.copy_(s_.running_var)
+
+    @torch.no_grad()
+    def recalibrate_bn(self, convs: Sequence[nn.Module], x: torch.Tensor, expert: torch.Tensor,
+                       chunk: int = 4096) -> list:
+        """Test-time BN re-estimation (``evaluate.recalibrate_bn``, the sweep's bn_adapt option) on the HIP
+        training conv forward instead of MIOpen: every expert's BN running statistics become the cumulative
+        average of its per-chunk batch statistics over the samples routed to it (torch's momentum=None rule,
+        reproduced exactly as momentum 1/k for the k-th chunk of the kernels' running-stat update; chunks
+        of fewer than 2 samples are skipped, as there).  Runs on a scratch copy of the experts (the other
+        experts' channels of a launch get the same samples and are discarded), writes the new statistics
+        into ``convs`` and returns their previous ones for ``evaluate.restore_bn``."""
+        from ..ops.conv import ConvStackHIP
+        from .engine import HDCEModel
+        if getattr(self, "_rc_model", None) is None:
+            self._rc_model = HDCEModel(self.pilot_num, self.dev, "bf16", self.E)
+        m = self._rc_model
+        stacks = {}
+        x = x.to(self.dev).contiguous().float()
+        expert = expert.to(self.dev)
+        saved = []
+        for e, conv in enumerate(convs):
+            bns = [b for b in conv.modules() if isinstance(b, nn.BatchNorm2d)]
+            saved.append([(b.momentum, b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone())
+                          for b in bns])
+            xe = x[expert == e]
+            n = xe.shape[0]
+            if n < 2:
+                continue
+            m.convs[e].load_state_dict(conv.state_dict())
+            dst = [b for b in m.convs[e].modules() if isinstance(b, nn.BatchNorm2d)]
+            for d in dst:
+                d.running_mean.zero_()
+                d.running_var.fill_(1.0)
+            k = 0
+            for lo in range(0, n, chunk):
+                c = min(chunk, n - lo)
+                if c < 2:
+                    continue
+                k += 1
+                if c not in stacks:
+                    stacks[c] = (ConvStackHIP(m, 1, c),
+                                 torch.empty(c, 2 * self.E, self.H, self.W, device=self.dev))
+                stk, x1 = stacks[c]
+                x1.view(c, self.E, 2, self.H, self.W).copy_(xe[lo:lo + c].view(c, 1, 2, self.H, self.W)
+                                                            .expand(c, self.E, 2, self.H, self.W))
+                m.momentum = 1.0 / k
+                stk.forward(x1, training=True)
+            m.momentum = 0.1
+            for b, d in zip(bns, dst):
+                b.running_mean.copy_(d.running_mean)
+                b.running_var.copy_(d.running_var)
+                b.num_batches_tracked.fill_(k)
+        return saved
 
     def _load(self, x: torch.Tensor, lo: int, n: int) -> None:
         """Samples x[lo:lo+n] -> the classifier input (xq) and the experts-in-channels conv input (x1); the

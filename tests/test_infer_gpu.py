@@ -52,3 +52,35 @@ def test_hip_inference_matches_torch_routing(cuda):
     H2 = eng.estimate(x, e2)
     torch.cuda.synchronize()
     assert float((H2 - estimate_routed(convs, fc, x, e2)).norm() / ref.norm()) < 1e-2
+
+
+def test_hip_bn_recalibration_matches_torch(cuda):
+    """Test-time BN re-estimation (Test.py's bn_adapt) on the HIP training conv forward == the torch
+    (MIOpen) cumulative-average rule to bf16-conv accuracy; the expert with < 2 samples keeps its own
+    statistics; restore_bn undoes both."""
+    import copy
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.evaluate import recalibrate_bn, restore_bn
+    convs, fc, _, _ = _models(cuda)
+    ref_convs, hip_convs = copy.deepcopy(convs), copy.deepcopy(convs)
+    eng = HIPInference(hip_convs, fc, 128, cuda, chunk=576)
+    torch.manual_seed(1)
+    N = 2500
+    x = torch.randn(N, 2, 16, 8, device=cuda) * 0.7 + 0.1
+    expert = torch.randint(0, 2, (N,), device=cuda)   # expert 2 gets nothing
+    expert[:1] = 2                                     # ... one sample: < 2, skipped
+    saved_ref = recalibrate_bn(ref_convs, x, expert, chunk=1000)
+    saved_hip = eng.recalibrate_bn(hip_convs, x, expert, chunk=1000)
+    bn = lambda cs: [m for c in cs for m in c.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    for i, (a, b, o) in enumerate(zip(bn(ref_convs), bn(hip_convs), bn(convs))):
+        e = i // 3
+        if e == 2:
+            assert torch.equal(b.running_mean, o.running_mean) and torch.equal(b.running_var, o.running_var)
+            continue
+        assert int(b.num_batches_tracked) == int(a.num_batches_tracked) >= 2
+        s = a.running_var.sqrt().mean()
+        assert torch.allclose(b.running_mean, a.running_mean, atol=0.02 * float(s), rtol=0.02), (i, float((b.running_mean - a.running_mean).abs().max()))
+        assert torch.allclose(b.running_var, a.running_var, rtol=0.04, atol=1e-4), (i, float((b.running_var / a.running_var - 1).abs().max()))
+    restore_bn(hip_convs, saved_hip)
+    restore_bn(ref_convs, saved_ref)
+    for a, o in zip(bn(hip_convs), bn(convs)):
+        assert torch.equal(a.running_mean, o.running_mean) and torch.equal(a.running_var, o.running_var)

@@ -408,8 +408,9 @@ def test_qsim_saved_state_backward(cuda, n, L, B):
 @pytest.mark.parametrize("n,L,B,G", [(13, 2, 6, 2), (14, 3, 4, 1), (15, 3, 6, 3), (16, 3, 4, 2), (16, 5, 2, 1)])
 def test_qsim_stream_matches_per_sample_kernel(cuda, n, L, B, G):
     """Streamed simulator (qsim_stream.hip: one workgroup per (sample, brick) per pass, ring as an LDS
-    scatter) == the workgroup-per-sample kernels (qsim_big.hip): E, dx and the summed weight gradient,
-    per-group (QuantumNAT) weights, with and without the forward's kept state."""
+    scatter; the backward reads the forward's kept pass-A states and generates layer 0) == the
+    workgroup-per-sample kernels (qsim_big.hip): E, dx and the summed weight gradient, per-group
+    (QuantumNAT) weights, with and without the forward's kept states."""
     import ctypes
     from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
     lib = nat.hip_lib()
@@ -432,9 +433,10 @@ def test_qsim_stream_matches_per_sample_kernel(cuda, n, L, B, G):
         nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx0), nat.ptr(slab0), BB, n, L, B, nat.ptr(ws), None, st), "big bwd")
     assert bool(nat.fn(lib, "qd_qsim_stream_ok", [_i, _i])(n, L))
     rows = nat.fn(lib, "qd_qsim_stream_rows", [_i])(BB)
-    wss = nat.fn(lib, "qd_qsim_stream_workspace", [_i, _i, _i], ctypes.c_longlong)(n, BB, 1)
+    wss = nat.fn(lib, "qd_qsim_stream_workspace", [_i, _i, _i, _i], ctypes.c_longlong)(n, BB, L, 1)
     ws2 = torch.empty(wss, dtype=torch.uint8, device=cuda)
-    ps = torch.empty(BB * (8 << n), dtype=torch.uint8, device=cuda)
+    ps = torch.empty(nat.fn(lib, "qd_qsim_stream_save_bytes", [_i, _i, _i], ctypes.c_longlong)(n, BB, L),
+                     dtype=torch.uint8, device=cuda)
     sf = nat.fn(lib, "qd_qsim_stream_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
     sb = nat.fn(lib, "qd_qsim_stream_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
     for save in (True, False):
