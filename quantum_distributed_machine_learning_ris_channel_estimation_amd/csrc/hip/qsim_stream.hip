@@ -56,8 +56,8 @@ struct SG {
   static constexpr int AS = 1 << AB;       // pass-A brick size
   static constexpr int NTILE = 1 << HB;    // pass-B tiles per sample
   static constexpr int NGRP = (AB + 2) / 3;
-  // threads of the adjoint pass A: one 3-qubit set (8 amplitudes) each, at most 512
-  static constexpr int NTA = AS / 8 < 512 ? AS / 8 : 512;
+  // threads of the adjoint pass A: one 3-qubit set (8 amplitudes) each, at most 256 (a set-loop beyond)
+  static constexpr int NTA = AS / 8 < 256 ? AS / 8 : 256;
   static_assert(N >= 13 && N <= 16, "streamed simulator: 13..16 qubits");
 };
 
@@ -208,6 +208,62 @@ __device__ __forceinline__ void lds_gates(cf* tp, cf* tq, const float4* trig, fl
       for (int j = 0; j < (1 << NB); ++j) {
         tp[base | (j << g0)] = p[j];
         if constexpr (ADJ) tq[base | (j << g0)] = m[j];
+      }
+    }
+    __syncthreads();
+  });
+}
+
+// The adjoint sweep of pass A (bits 0 .. NBITS-1 of the LDS brick, brick_q qubit map) with the gradient
+// partials of each 3-qubit group reduced over the wave right after the group and added to this wave's slot of
+// wacc (2 NBITS floats per wave, zeroed by the caller; lane 0 of a wave is its slot's only writer): six live
+// accumulators per thread instead of 2 NBITS (the 512-thread kernel's 128-register budget spilled them).
+// LDS image of pass A's backward: one pad amplitude per 8 (element e at e + e / 8), so the 3-qubit groups on
+// bits 0..2 and 3..5 -- whose threads own 8 contiguous / 8-strided amplitudes -- read and write conflict-free
+// (unpadded, a wave's 8-byte accesses 64 bytes apart hit 4 bank pairs: 8-way conflicts)
+__device__ __forceinline__ int padx(int e) { return e + (e >> 3); }
+
+template <int TOT, int NBITS, int NTH>
+__device__ __forceinline__ void lds_gates_adj_acc(cf* tp, cf* tq, const float4* trig, float* wacc) {
+  constexpr int NGRP = (NBITS + 2) / 3;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  static_for<0, NGRP>([&](auto gc) {
+    constexpr int gi = NGRP - 1 - decltype(gc)::value;
+    constexpr int r0 = 3 * gi;
+    constexpr int NB = (NBITS - r0) < 3 ? (NBITS - r0) : 3;
+    constexpr int ACT = (1 << TOT) >> NB;
+    float dth[NB], dph[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) dth[b] = dph[b] = 0.f;
+#pragma unroll 1
+    for (int t = threadIdx.x; t < ACT; t += NTH) {
+      const int base = ins_bits<r0, NB>(t);
+      cf p[1 << NB], m[1 << NB];
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) {
+        p[j] = tp[padx(base | (j << r0))];
+        m[j] = tq[padx(base | (j << r0))];
+      }
+#pragma unroll
+      for (int bb = 0; bb < NB; ++bb) {
+        const int b = NB - 1 - bb;
+        const float4 tg = trig[brick_q(r0 + b)];
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j)
+          if (!((j >> b) & 1)) gate_adj(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[b], dph[b]);
+      }
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) {
+        tp[padx(base | (j << r0))] = p[j];
+        tq[padx(base | (j << r0))] = m[j];
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float s1 = wave_sum(dth[b]), s2 = wave_sum(dph[b]);
+      if (lane == 0) {
+        wacc[wv * 2 * NBITS + 2 * (r0 + b)] += s1;
+        wacc[wv * 2 * NBITS + 2 * (r0 + b) + 1] += s2;
       }
     }
     __syncthreads();
@@ -420,68 +476,74 @@ __global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x,
 }
 
 // Reverse pass A of layer l: psi = S_l (read only; GEN0: layer 0's product state with qubits 8..11 back at
-// |0>, which is zero outside brick 0 -- the other bricks only write zero partials), lambda in place (STORE
-// = false for layer 0, whose result nothing reads).  512 threads: the adjoint sweep is latency-bound
-// (dependent gradient sums), and the 64 KiB of psi + lambda per workgroup allow only 2 workgroups per CU --
-// twice the waves hide it better.
-template <int N, bool STORE, bool GEN0>
-__global__ void __launch_bounds__(SG<N>::NTA, 4) pass_a_bwd(const float* __restrict__ x, const float* __restrict__ w, int L,
+// |0>, which is zero outside brick 0: one workgroup per sample, the other bricks' partials written zero),
+// lambda in place (STORE = false for layer 0, whose result nothing reads).  A workgroup walks BPB bricks of
+// one sample in turn: the pass is bound by workgroup / wave dispatch rather than bytes (profiles/r3_10: 36,864
+// one-brick workgroups of 8 waves took 1.6 ms, and 34,560 workgroups that only wrote zeros 1.4 ms), so fewer,
+// longer-lived workgroups of 4 waves carry the same bricks.
+template <int N, bool STORE, bool GEN0, int BPB>
+__global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restrict__ x, const float* __restrict__ w, int L,
                                                  int l, int wgroup, const cf* __restrict__ pst, cf* __restrict__ lst,
                                                  float* __restrict__ slab) {
   using C = SG<N>;
   constexpr int NTA = C::NTA;
+  static_assert(!GEN0 || BPB == 1, "layer 0: brick 0 only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float4* trig = reinterpret_cast<float4*>(smem);
   float* red = reinterpret_cast<float*>(smem + 256);      // (NTA / 64) * 2AB floats <= 768 B
-  cf* tp = reinterpret_cast<cf*>(smem + 1024);
-  cf* tq = tp + C::AS;
-  const int br = blockIdx.x, s = blockIdx.y;
+  cf* tp = reinterpret_cast<cf*>(smem + 1024);   // (padded images, see padx)
+  cf* tq = tp + C::AS + C::AS / 8;
+  const int s = blockIdx.y;
   const int P = 2 * N * L;
-  if (GEN0 && br != 0) {   // psi = 0 on this brick: no gradient contribution
-    if (threadIdx.x < 2 * C::AB)
-      slab[((size_t)s * ROWS + br) * P + (l * N + brick_q(threadIdx.x / 2)) * 2 + (threadIdx.x & 1)] = 0.f;
-    return;
+  if constexpr (GEN0) {   // psi = 0 on bricks 1..15: zero partials
+    for (int i = threadIdx.x; i < (ROWS - 1) * 2 * C::AB; i += NTA) {
+      const int r = 1 + i / (2 * C::AB), j = i % (2 * C::AB);
+      slab[((size_t)s * ROWS + r) * P + (l * N + brick_q(j / 2)) * 2 + (j & 1)] = 0.f;
+    }
   }
   load_trig<N>(trig, x, w, s, L, l, wgroup);
   cf* ls = lst + (size_t)s * C::D;
-  if constexpr (GEN0) {
-    cf* PL = tq + C::AS;
-    cf* PH = PL + 256;
-    __syncthreads();
-    product_tables<N, NTA>(trig, PL, PH, 0xF00);
-    __syncthreads();
-    for (int e = threadIdx.x; e < C::AS; e += NTA) {
-      const int k = brick_k(e, 0);
-      tp[e] = cmul(PL[k & 255], PH[k >> 8]);
-      tq[e] = ls[k];
+  const cf* ps = GEN0 ? nullptr : pst + (size_t)s * C::D;
+#pragma unroll 1
+  for (int bi = 0; bi < BPB; ++bi) {
+    const int br = blockIdx.x * BPB + bi;
+    __syncthreads();   // (the previous brick's stores and partial sums are done with LDS)
+    if constexpr (GEN0) {
+      cf* PL = tq + C::AS + C::AS / 8;
+      cf* PH = PL + 256;
+      product_tables<N, NTA>(trig, PL, PH, 0xF00);
+      __syncthreads();
+      for (int e = threadIdx.x; e < C::AS; e += NTA) {
+        const int k = brick_k(e, 0);
+        tp[padx(e)] = cmul(PL[k & 255], PH[k >> 8]);
+        tq[padx(e)] = ls[k];
+      }
+    } else {
+      for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
+        const int k = brick_k(e, br);
+        const float4 a = *reinterpret_cast<const float4*>(ps + k), b = *reinterpret_cast<const float4*>(ls + k);
+        tp[padx(e)] = cf{a.x, a.y};
+        tp[padx(e) + 1] = cf{a.z, a.w};
+        tq[padx(e)] = cf{b.x, b.y};
+        tq[padx(e) + 1] = cf{b.z, b.w};
+      }
     }
-  } else {
-    const cf* ps = pst + (size_t)s * C::D;
-    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
-      const int k = brick_k(e, br);
-      *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(ps + k);
-      *reinterpret_cast<float4*>(tq + e) = *reinterpret_cast<const float4*>(ls + k);
+    if (threadIdx.x < (NTA / 64) * 2 * C::AB) red[threadIdx.x] = 0.f;   // (per-wave gradient slots)
+    __syncthreads();
+    lds_gates_adj_acc<C::AB, C::AB, NTA>(tp, tq, trig, red);
+    if constexpr (STORE) {
+      for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
+        const cf u = tq[padx(e)], v = tq[padx(e) + 1];
+        *reinterpret_cast<float4*>(ls + brick_k(e, br)) = make_float4(u.x, u.y, v.x, v.y);
+      }
     }
-  }
-  __syncthreads();
-  float dth[C::AB], dph[C::AB];
+    if (threadIdx.x < 2 * C::AB) {   // (the sweep ended with a barrier: every wave's slot is final)
+      float o = 0.f;
 #pragma unroll
-  for (int b = 0; b < C::AB; ++b) dth[b] = dph[b] = 0.f;
-  lds_gates<C::AB, 0, C::AB, false, true, NTA>(tp, tq, trig, dth, dph);
-  if constexpr (STORE) {
-    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA)
-      *reinterpret_cast<float4*>(ls + brick_k(e, br)) = *reinterpret_cast<const float4*>(tq + e);
-  }
-  float v[2 * C::AB], o[2 * C::AB];
-#pragma unroll
-  for (int b = 0; b < C::AB; ++b) {
-    v[2 * b] = dth[b];
-    v[2 * b + 1] = dph[b];
-  }
-  block_sum_vec<2 * C::AB, NTA>(v, red, o);
-  if (threadIdx.x < 2 * C::AB) {
-    const int q = brick_q(threadIdx.x / 2);
-    slab[((size_t)s * ROWS + br) * P + (l * N + q) * 2 + (threadIdx.x & 1)] = o[threadIdx.x];
+      for (int k = 0; k < NTA / 64; ++k) o += red[k * 2 * C::AB + threadIdx.x];
+      const int q = brick_q(threadIdx.x / 2);
+      slab[((size_t)s * ROWS + br) * P + (l * N + q) * 2 + (threadIdx.x & 1)] = o;
+    }
   }
 }
 
@@ -502,7 +564,7 @@ struct Smem {
   static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + 512);   // (+ the GEN product tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
   static constexpr size_t B_BWD = 512 + 2 * sizeof(cf) * 4096 + 2048 + sizeof(cf) * 512;   // (+ FIRST / GEN0 tables)
-  static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * SG<N>::AS + sizeof(cf) * 512;  // (+ GEN0 tables)
+  static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * (SG<N>::AS + SG<N>::AS / 8) + sizeof(cf) * 512;  // (+ GEN0 tables)
 };
 
 inline size_t state_bytes(int n, int B) { return (size_t)B * (8ull << n); }
@@ -561,11 +623,19 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     (void)allow_lds(pass_b_bwd<N, true, false>, S::B_BWD);
     (void)allow_lds(pass_b_bwd<N, false, false>, S::B_BWD);
     (void)allow_lds(pass_b_bwd<N, false, true>, S::B_BWD);
-    (void)allow_lds(pass_a_bwd<N, true, false>, S::A_BWD);
-    (void)allow_lds(pass_a_bwd<N, false, true>, S::A_BWD);
+    (void)allow_lds(pass_a_bwd<N, true, false, 1>, S::A_BWD);
+    (void)allow_lds(pass_a_bwd<N, true, false, 2>, S::A_BWD);
+    (void)allow_lds(pass_a_bwd<N, true, false, 4>, S::A_BWD);
+    (void)allow_lds(pass_a_bwd<N, false, true, 1>, S::A_BWD);
     attr = true;
   }
   const dim3 ga(ROWS, B), gb(C::NTILE, B);
+  // bricks per workgroup of the reverse pass A (QDML_QS_BPB: 1, 2, 4; tuning knob)
+  static const int bpb = [] {
+    const char* e = getenv("QDML_QS_BPB");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4) ? v : 2;
+  }();
   const cf* lin = nullptr;
   for (int l = L - 1; l >= 0; --l) {
     cf* lo = ((L - 1 - l) % 2 == 0) ? L1 : L2;
@@ -580,10 +650,20 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     else
       hipLaunchKernelGGL((pass_b_bwd<N, false, true>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, ps, lin, lo,
                          slab);
-    if (l > 0)
-      hipLaunchKernelGGL((pass_a_bwd<N, true, false>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps, lo, slab);
-    else
-      hipLaunchKernelGGL((pass_a_bwd<N, false, true>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps, lo, slab);
+    if (l > 0) {
+      if (bpb == 4)
+        hipLaunchKernelGGL((pass_a_bwd<N, true, false, 4>), dim3(ROWS / 4, B), dim3(C::NTA), S::A_BWD, st, x, w, L, l,
+                           wgroup, ps, lo, slab);
+      else if (bpb == 2)
+        hipLaunchKernelGGL((pass_a_bwd<N, true, false, 2>), dim3(ROWS / 2, B), dim3(C::NTA), S::A_BWD, st, x, w, L, l,
+                           wgroup, ps, lo, slab);
+      else
+        hipLaunchKernelGGL((pass_a_bwd<N, true, false, 1>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps, lo,
+                           slab);
+    } else {
+      hipLaunchKernelGGL((pass_a_bwd<N, false, true, 1>), dim3(1, B), dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps,
+                         lo, slab);
+    }
     lin = lo;
   }
   hipLaunchKernelGGL(reduce_dx, dim3((B * N + 255) / 256), dim3(256), 0, st, slab, dx, B, N, 2 * N * L);
