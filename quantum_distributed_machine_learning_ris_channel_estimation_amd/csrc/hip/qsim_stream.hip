@@ -138,6 +138,16 @@ __device__ __forceinline__ void gate_adj(cf& p0, cf& p1, cf& l0, cf& l1, float4 
   l1 = {t.x * m1.x - t.y * m0.x, t.x * m1.y - t.y * m0.y};
 }
 
+// adjoint of the RY half only (the pass's RZ phases already undone, see pass_a_bwd): d(theta) and undo RY
+__device__ __forceinline__ void gate_adj_ry(cf& p0, cf& p1, cf& l0, cf& l1, float4 t, float& dth) {
+  dth += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+  const cf q0 = p0, q1 = p1, m0 = l0, m1 = l1;
+  p0 = {t.x * q0.x + t.y * q1.x, t.x * q0.y + t.y * q1.y};
+  p1 = {t.x * q1.x - t.y * q0.x, t.x * q1.y - t.y * q0.y};
+  l0 = {t.x * m0.x + t.y * m1.x, t.x * m0.y + t.y * m1.y};
+  l1 = {t.x * m1.x - t.y * m0.x, t.x * m1.y - t.y * m0.y};
+}
+
 // (cos, sin) of theta/2 and phi/2 of layer l for every qubit of sample s (theta + x at layer 0)
 template <int N>
 __device__ __forceinline__ void load_trig(float4* trig, const float* x, const float* w, int s, int L, int l,
@@ -214,10 +224,10 @@ __device__ __forceinline__ void lds_gates(cf* tp, cf* tq, const float4* trig, fl
   });
 }
 
-// The adjoint sweep of pass A (bits 0 .. NBITS-1 of the LDS brick, brick_q qubit map) with the gradient
-// partials of each 3-qubit group reduced over the wave right after the group and added to this wave's slot of
-// wacc (2 NBITS floats per wave, zeroed by the caller; lane 0 of a wave is its slot's only writer): six live
-// accumulators per thread instead of 2 NBITS (the 512-thread kernel's 128-register budget spilled them).
+// The adjoint RY sweep of pass A (bits 0 .. NBITS-1 of the LDS brick, brick_q qubit map; the pass's RZ phases
+// were undone -- and every d(phi) taken -- when the brick was loaded) with the d(theta) partials of each
+// 3-qubit group reduced over the wave right after the group and added to this wave's slot of wacc (2 NBITS
+// floats per wave, lane 0 of a wave its slot's only writer): three live accumulators per thread.
 // LDS image of pass A's backward: one pad amplitude per 8 (element e at e + e / 8), so the 3-qubit groups on
 // bits 0..2 and 3..5 -- whose threads own 8 contiguous / 8-strided amplitudes -- read and write conflict-free
 // (unpadded, a wave's 8-byte accesses 64 bytes apart hit 4 bank pairs: 8-way conflicts)
@@ -232,9 +242,9 @@ __device__ __forceinline__ void lds_gates_adj_acc(cf* tp, cf* tq, const float4* 
     constexpr int r0 = 3 * gi;
     constexpr int NB = (NBITS - r0) < 3 ? (NBITS - r0) : 3;
     constexpr int ACT = (1 << TOT) >> NB;
-    float dth[NB], dph[NB];
+    float dth[NB];
 #pragma unroll
-    for (int b = 0; b < NB; ++b) dth[b] = dph[b] = 0.f;
+    for (int b = 0; b < NB; ++b) dth[b] = 0.f;
 #pragma unroll 1
     for (int t = threadIdx.x; t < ACT; t += NTH) {
       const int base = ins_bits<r0, NB>(t);
@@ -250,7 +260,7 @@ __device__ __forceinline__ void lds_gates_adj_acc(cf* tp, cf* tq, const float4* 
         const float4 tg = trig[brick_q(r0 + b)];
 #pragma unroll
         for (int j = 0; j < (1 << NB); ++j)
-          if (!((j >> b) & 1)) gate_adj(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[b], dph[b]);
+          if (!((j >> b) & 1)) gate_adj_ry(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[b]);
       }
 #pragma unroll
       for (int j = 0; j < (1 << NB); ++j) {
@@ -260,11 +270,8 @@ __device__ __forceinline__ void lds_gates_adj_acc(cf* tp, cf* tq, const float4* 
     }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const float s1 = wave_sum(dth[b]), s2 = wave_sum(dph[b]);
-      if (lane == 0) {
-        wacc[wv * 2 * NBITS + 2 * (r0 + b)] += s1;
-        wacc[wv * 2 * NBITS + 2 * (r0 + b) + 1] += s2;
-      }
+      const float s1 = wave_sum(dth[b]);
+      if (lane == 0) wacc[wv * 2 * NBITS + 2 * (r0 + b)] += s1;
     }
     __syncthreads();
   });
@@ -504,10 +511,46 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
   load_trig<N>(trig, x, w, s, L, l, wgroup);
   cf* ls = lst + (size_t)s * C::D;
   const cf* ps = GEN0 ? nullptr : pst + (size_t)s * C::D;
+  // the pass's RZ phases as one diagonal: amplitude e (brick order) is multiplied by ZL[e & 255] * ZH[e >> 8] when
+  // they are undone (qubit q's factor cos(phi/2) +- i sin(phi/2), + for bit 0) -- after the table barrier below
+  cf* ZL = reinterpret_cast<cf*>(smem + 1024 + 2 * sizeof(cf) * (C::AS + C::AS / 8) + sizeof(cf) * 512);
+  cf* ZH = ZL + 256;
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += NTA) {
+    cf a = {1.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const float4 t = trig[b];
+      a = cmul(a, cf{t.z, ((i >> b) & 1) ? -t.w : t.w});
+    }
+    ZL[i] = a;
+    if (i < (1 << (C::AB - 8))) {
+      cf h = {1.f, 0.f};
+#pragma unroll
+      for (int b = 8; b < C::AB; ++b) {
+        const float4 t = trig[brick_q(b)];
+        h = cmul(h, cf{t.z, ((i >> (b - 8)) & 1) ? -t.w : t.w});
+      }
+      ZH[i] = h;
+    }
+  }
 #pragma unroll 1
   for (int bi = 0; bi < BPB; ++bi) {
     const int br = blockIdx.x * BPB + bi;
     __syncthreads();   // (the previous brick's stores and partial sums are done with LDS)
+    // load psi / lambda; every d(phi) of the pass at this point (Im<lam| Z_q |psi>: the RZ of other qubits
+    // commute with Z_q), then all the pass's RZ undone at once
+    float dz[C::AB];
+#pragma unroll
+    for (int b = 0; b < C::AB; ++b) dz[b] = 0.f;
+    auto take = [&](int e, cf p, cf m) __attribute__((always_inline)) {
+      const float c = m.x * p.y - m.y * p.x;
+#pragma unroll
+      for (int b = 0; b < C::AB; ++b) dz[b] += ((e >> b) & 1) ? -c : c;
+      const cf z = cmul(ZL[e & 255], ZH[e >> 8]);
+      tp[padx(e)] = cmul(p, z);
+      tq[padx(e)] = cmul(m, z);
+    };
     if constexpr (GEN0) {
       cf* PL = tq + C::AS + C::AS / 8;
       cf* PH = PL + 256;
@@ -515,21 +558,27 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
       __syncthreads();
       for (int e = threadIdx.x; e < C::AS; e += NTA) {
         const int k = brick_k(e, 0);
-        tp[padx(e)] = cmul(PL[k & 255], PH[k >> 8]);
-        tq[padx(e)] = ls[k];
+        take(e, cmul(PL[k & 255], PH[k >> 8]), ls[k]);
       }
     } else {
+      __syncthreads();   // (the phase tables)
       for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
         const int k = brick_k(e, br);
         const float4 a = *reinterpret_cast<const float4*>(ps + k), b = *reinterpret_cast<const float4*>(ls + k);
-        tp[padx(e)] = cf{a.x, a.y};
-        tp[padx(e) + 1] = cf{a.z, a.w};
-        tq[padx(e)] = cf{b.x, b.y};
-        tq[padx(e) + 1] = cf{b.z, b.w};
+        take(e, cf{a.x, a.y}, cf{b.x, b.y});
+        take(e + 1, cf{a.z, a.w}, cf{b.z, b.w});
       }
     }
     if (threadIdx.x < (NTA / 64) * 2 * C::AB) red[threadIdx.x] = 0.f;   // (per-wave gradient slots)
     __syncthreads();
+    {
+      const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+      for (int b = 0; b < C::AB; ++b) {
+        const float sz = wave_sum(dz[b]);
+        if (lane == 0) red[wv * 2 * C::AB + 2 * b + 1] = sz;
+      }
+    }
     lds_gates_adj_acc<C::AB, C::AB, NTA>(tp, tq, trig, red);
     if constexpr (STORE) {
       for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
@@ -564,7 +613,8 @@ struct Smem {
   static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + 512);   // (+ the GEN product tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
   static constexpr size_t B_BWD = 512 + 2 * sizeof(cf) * 4096 + 2048 + sizeof(cf) * 512;   // (+ FIRST / GEN0 tables)
-  static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * (SG<N>::AS + SG<N>::AS / 8) + sizeof(cf) * 512;  // (+ GEN0 tables)
+  static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * (SG<N>::AS + SG<N>::AS / 8) + sizeof(cf) * 512   // (+ GEN0 tables)
+                                  + sizeof(cf) * (256 + 16);                                           // (+ RZ tables)
 };
 
 inline size_t state_bytes(int n, int B) { return (size_t)B * (8ull << n); }
