@@ -534,6 +534,19 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
       ZH[i] = h;
     }
   }
+  // (not GEN0) this thread's psi / lambda pairs of the NEXT brick, loaded into registers while the current one is
+  // swept: the loads of brick i + 1 overlap brick i's LDS work (two workgroups per CU leave little else in flight)
+  constexpr int NPAIR = GEN0 ? 1 : C::AS / (2 * NTA);
+  float4 na[NPAIR], nb[NPAIR];
+  auto prefetch = [&](int brn) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      const int k = brick_k(2 * threadIdx.x + 2 * NTA * i, brn);
+      na[i] = *reinterpret_cast<const float4*>(ps + k);
+      nb[i] = *reinterpret_cast<const float4*>(ls + k);
+    }
+  };
+  if constexpr (!GEN0) prefetch(blockIdx.x * BPB);
 #pragma unroll 1
   for (int bi = 0; bi < BPB; ++bi) {
     const int br = blockIdx.x * BPB + bi;
@@ -562,12 +575,13 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
       }
     } else {
       __syncthreads();   // (the phase tables)
-      for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
-        const int k = brick_k(e, br);
-        const float4 a = *reinterpret_cast<const float4*>(ps + k), b = *reinterpret_cast<const float4*>(ls + k);
-        take(e, cf{a.x, a.y}, cf{b.x, b.y});
-        take(e + 1, cf{a.z, a.w}, cf{b.z, b.w});
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i) {
+        const int e = 2 * threadIdx.x + 2 * NTA * i;
+        take(e, cf{na[i].x, na[i].y}, cf{nb[i].x, nb[i].y});
+        take(e + 1, cf{na[i].z, na[i].w}, cf{nb[i].z, nb[i].w});
       }
+      if (bi + 1 < BPB) prefetch(br + 1);
     }
     if (threadIdx.x < (NTA / 64) * 2 * C::AB) red[threadIdx.x] = 0.f;   // (per-wave gradient slots)
     __syncthreads();
@@ -683,8 +697,8 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
   // bricks per workgroup of the reverse pass A (QDML_QS_BPB: 1, 2, 4; tuning knob)
   static const int bpb = [] {
     const char* e = getenv("QDML_QS_BPB");
-    const int v = e ? atoi(e) : 2;
-    return (v == 1 || v == 2 || v == 4) ? v : 2;
+    const int v = e ? atoi(e) : 4;
+    return (v == 1 || v == 2 || v == 4) ? v : 4;
   }();
   const cf* lin = nullptr;
   for (int l = L - 1; l >= 0; --l) {
