@@ -101,6 +101,9 @@ class FlagshipConfig:
     #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
     qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 256)
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
+    lead_in: int = 1             # run(): the first lead_in steps replayed one step per graph -- a run that starts on
+    #                              an idle GPU waits for its first graph's launch to be submitted, and a 1-step graph
+    #                              is submitted in a fifth of a k-step one's time
     dp_one_graph: bool = False   # DP plan: capture the whole step -- its RCCL collectives included -- in ONE
     #                              graph (the 5-graph plan launches the collectives between graph replays and
     #                              pays a graph boundary at each; this one pays one per step but fences the
@@ -427,18 +430,24 @@ class FlagshipTrainer(DPPlan):
         one = (self.ctx.world == 1 and not self.cfg.split_graphs) or (self.cfg.dp_one_graph and self._use_graphs)
         return max(1, self.cfg.steps_per_graph) if one else 1
 
+    def _reps(self, n: int):
+        """Steps per replay of ``run(n)``: lead_in single steps, then k-step replays, then the remainder as ONE
+        replay of a (n - lead_in) % k-step graph (single-step replays cost ~3 % more per step:
+        profiles/r3_12_window.txt)."""
+        k = self._k()
+        lead = min(n, max(0, self.cfg.lead_in)) if k > 1 else 0
+        r = (n - lead) % k
+        return [1] * lead + [k] * ((n - lead) // k) + ([r] if r else [])
+
     def prepare(self, n: int) -> None:
         """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""
-        k = self._k()
-        if n // k:
-            self.capture(preserve=True, k=k)
-        if n % k:
-            self.capture(preserve=True, k=1)
+        for kk in sorted(set(self._reps(n)), reverse=True):
+            self.capture(preserve=True, k=kk)
 
     def run(self, n: int) -> None:
-        """``n`` training steps, ``cfg.steps_per_graph`` per graph replay (the remainder one by one)."""
-        k = self._k()
-        reps = [k] * (n // k) + [1] * (n % k)
+        """``n`` training steps, ``cfg.steps_per_graph`` per graph replay (lead_in single steps first, the
+        remainder as one shorter graph)."""
+        reps = self._reps(n)
         for i, kk in enumerate(reps):   # (DP plan: consecutive steps overlap; the last one is fenced)
             self._replay(kk, fence=i == len(reps) - 1)
 
