@@ -57,7 +57,7 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-quantumnat", action="store_true")
     ap.add_argument("--split-graphs", action="store_true", help="the DP plan (5 graphs around the collectives) even at 1 GPU")
-    ap.add_argument("--steps-per-graph", type=int, default=5,
+    ap.add_argument("--steps-per-graph", type=int, default=10,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
     ap.add_argument("--dp-plan", default="auto", choices=["auto", "zero", "allreduce"],
                     help="world > 1: ZeRO-1 FC optimizer (reduce-scatter / shard Adam / all-gather) or all-reduce; "
