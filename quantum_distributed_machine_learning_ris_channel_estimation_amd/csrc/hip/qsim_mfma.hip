@@ -20,12 +20,16 @@
 // psi_final in the layout qsim.hip's adjoint backward reads (psave[s][r][lane], k = r | lane << 2).
 //
 // qd_qsim_mfma_prep builds every (group, layer) operand image once per step (fp16 hi / lo, per-lane
-// register order); the forward streams them from L2.
+// register order); the forward streams them from L2.  In training with QuantumNAT the build rides in the noise
+// draw's launch (qd_qsim_mfma_prep_noise replaces qsc.hip's single-block qd_qnoise): no extra launch per step.
 //
 // Measured (scripts/probe_qsim_mfma.py, 9 groups x 256 samples, 3 layers, MI355X): forward 11.1 us vs
-// 12.4 us for the register kernel (qsim.hip), but the operand build adds 4 us per step (a separate
-// small launch), so the flagship keeps the register kernel; exact to 3e-6 against it and the fp64 CPU
-// oracle (tests/test_kernels_gpu.py::test_qsim_mfma_forward_matches_register_kernel).
+// 12.4 us for the register kernel (qsim.hip); a separate operand build would add a 4 us launch, so in the
+// training step the build rides in the QuantumNAT draw's launch and this forward is the flagship's default
+// (ops/qsc.py; step 0.4044 / 0.4100 vs 0.4096 / 0.4100 ms with the register forward, profiles/r3_14_*).
+// Exact to 3e-6 against the register kernel and the fp64 CPU oracle
+// (tests/test_kernels_gpu.py::test_qsim_mfma_forward_matches_register_kernel,
+// tests/test_qsc_gpu.py::test_qsc_circuit_forward_on_mfma_matches_register_kernel).
 #include <cstdlib>
 
 #include "common.h"
@@ -69,15 +73,63 @@ __device__ __forceinline__ void split(float v, _Float16& hi, _Float16& lo) {
   lo = (_Float16)((v - (float)hi) * LO_SCALE);
 }
 
-// grid (G, L-1), block 64: operand images of layer l = 1 + blockIdx.y for weight group blockIdx.x
-__global__ void __launch_bounds__(64) prep_kernel(const float* __restrict__ w, _Float16* __restrict__ ops, int L) {
+// QuantumNAT noise draw of qsc.hip's qnoise_kernel, element i of the (G, L, N, 2) noisy-weight tensor (the same
+// counter-based hash: the fused prep below writes bit-identical noisy weights)
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float hash_normal(unsigned long long seed, unsigned long long ctr, unsigned int i) {
+  const unsigned long long h = mix64(seed ^ mix64(ctr * 0x100000001b3ull + i));
+  const float u1 = ((h >> 40) + 1u) * (1.0f / 16777217.0f);          // (0, 1]
+  const float u2 = ((h >> 16) & 0xffffffu) * (1.0f / 16777216.0f);   // [0, 1)
+  return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+struct Noise {
+  const float* w;                 // (L, N, 2) master weights, shared by the G groups
+  float* out;                     // (G, L, N, 2) noisy copies (the forward's layer 0 and the adjoint read them)
+  float sigma;
+  unsigned long long seed;
+  unsigned long long* counter;    // draws so far: read by every block, advanced by the last one to finish
+  unsigned int* done;             // zero-initialised arrival counter (re-armed by the last block)
+};
+
+// grid (G, L), block 64: block (g, l) builds the operand images of layer l >= 1 of weight group g.  w (G, L, N, 2),
+// or with nz.out the noisy weights of that layer drawn here first (QuantumNAT: one launch for the draw and the
+// images, the draw's counter advanced by the last block).  Blocks with l = 0 only draw.
+__global__ void __launch_bounds__(64) prep_kernel(const float* __restrict__ w, _Float16* __restrict__ ops, int L,
+                                                  Noise nz) {
   __shared__ float4 tr[N];
-  const int g = blockIdx.x, l = 1 + blockIdx.y, lane = threadIdx.x;
+  __shared__ float wn[2 * N];
+  const int g = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
+  if (nz.out != nullptr) {
+    const unsigned long long ctr = *nz.counter;
+    if (lane < 2 * N) {
+      const int P = L * 2 * N, j = l * 2 * N + lane;
+      const float v = nz.w[j] + nz.sigma * hash_normal(nz.seed, ctr, (unsigned int)(g * P + j));
+      nz.out[(size_t)g * P + j] = v;
+      wn[lane] = v;
+    }
+    __syncthreads();
+    if (lane == 0) {   // every block read *counter above: the last to arrive advances it
+      const unsigned int prev = __hip_atomic_fetch_add(nz.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x * gridDim.y - 1) {
+        *nz.counter = ctr + 1;
+        __hip_atomic_store(nz.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else if (lane < 2 * N) {
+    wn[lane] = w[((size_t)g * L + l) * 2 * N + lane];
+  }
+  if (l == 0) return;
+  __syncthreads();
   if (lane < N) {
-    const float* wl = w + ((size_t)g * L + l) * 2 * N;
     float s, c, sp, cp;
-    __sincosf(0.5f * wl[2 * lane], &s, &c);
-    __sincosf(0.5f * wl[2 * lane + 1], &sp, &cp);
+    __sincosf(0.5f * wn[2 * lane], &s, &c);
+    __sincosf(0.5f * wn[2 * lane + 1], &sp, &cp);
     tr[lane] = make_float4(c, s, cp, sp);
   }
   __syncthreads();
@@ -293,7 +345,21 @@ QD_API long long qd_qsim_mfma_ops_halves(int G, int L) { return (long long)G * (
 // w (G, L, 8, 2) -> ops (qd_qsim_mfma_ops_halves fp16 values)
 QD_API int qd_qsim_mfma_prep(const float* w, void* ops, int G, int L, void* stream) {
   if (G < 1 || L < 2) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(prep_kernel, dim3(G, L - 1), dim3(64), 0, (hipStream_t)stream, w, (_Float16*)ops, L);
+  Noise nz{nullptr, nullptr, 0.f, 0ull, nullptr, nullptr};
+  // (without noise the layer-0 blocks of the (G, L) grid return at once)
+  hipLaunchKernelGGL(prep_kernel, dim3(G, L), dim3(64), 0, (hipStream_t)stream, w, (_Float16*)ops, L, nz);
+  return (int)hipGetLastError();
+}
+
+// QuantumNAT draw + operand images in ONE launch: out (G, L, 8, 2) = w (L, 8, 2) + sigma N(0, 1) -- bit-identical to
+// qd_qnoise with the same seed / counter -- and the images of the noisy layers 1..L-1.  done: zero-initialised
+// uint32 (re-armed by the kernel).
+QD_API int qd_qsim_mfma_prep_noise(const float* w, float* out, void* ops, int G, int L, float sigma,
+                                   unsigned long long seed, unsigned long long* counter, unsigned int* done,
+                                   void* stream) {
+  if (G < 1 || L < 2 || !w || !out || !counter || !done) return (int)hipErrorInvalidValue;
+  Noise nz{w, out, sigma, seed, counter, done};
+  hipLaunchKernelGGL(prep_kernel, dim3(G, L), dim3(64), 0, (hipStream_t)stream, out, (_Float16*)ops, L, nz);
   return (int)hipGetLastError();
 }
 

@@ -162,6 +162,21 @@ class QSCStepHIP:
         self.wnoisy = torch.empty((n_groups,) + tuple(wq.shape), **f32)
         self.noise_ctr = torch.zeros(1, dtype=torch.int64, device=dev)      # advanced by the kernel
         self.noise_seed = int(torch.randint(0, 2 ** 62, (1,)).item())       # from the (seeded) host RNG
+        # n = 8: the circuit forward on the matrix cores (csrc/hip/qsim_mfma.hip: each layer's rotations as
+        # Kronecker-factored complex products on mfma_f32_16x16x32_f16, fp16 hi/lo split = fp32-grade
+        # amplitudes); its per-step operand images are built in the QuantumNAT noise draw's launch
+        # (qd_qsim_mfma_prep_noise), so the step has no extra launch.  The adjoint backward reads the final
+        # state it saves (qsim.hip's layout).  QDML_QSIM_MFMA=0: the register forward (qsim.hip).
+        self.mfma = (dev.type == "cuda" and not self.big and self.n == 8 and 2 <= self.L <= 8
+                     and self.psave is not None and os.environ.get("QDML_QSIM_MFMA", "1") != "0")
+        if self.mfma:
+            halves = nat.fn(L, "qd_qsim_mfma_ops_halves", [_i, _i], ctypes.c_longlong)(max(1, n_groups), self.L)
+            self.qops = torch.empty(halves, dtype=torch.float16, device=dev)
+            self.qdone = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._mprep = nat.fn(L, "qd_qsim_mfma_prep", [_p, _p, _i, _i, _p])
+            self._mprep_noise = nat.fn(L, "qd_qsim_mfma_prep_noise",
+                                       [_p, _p, _p, _i, _i, _f, ctypes.c_ulonglong, _p, _p, _p])
+            self._mfwd = nat.fn(L, "qd_qsim_mfma_fwd", [_p, _p, _p, _p, _i, _i, _i, _p, _p])
 
     def quantum_weights(self) -> torch.Tensor:
         """Master weights, or (training + QuantumNAT) G per-stream noisy copies drawn in-kernel
@@ -169,9 +184,17 @@ class QSCStepHIP:
         m = self.m
         w = m.qlayer.weights.detach()
         if m.training and m.use_quantumnat and m.noise_level > 0:
-            nat.check(self._qnoise(nat.ptr(w), nat.ptr(self.wnoisy), self.G, w.numel(), float(m.noise_level),
-                                   self.noise_seed, nat.ptr(self.noise_ctr), nat.stream_ptr(w.device)), "qnoise")
+            if self.mfma:   # the draw + the MFMA forward's operand images of the noisy layers, one launch
+                nat.check(self._mprep_noise(nat.ptr(w), nat.ptr(self.wnoisy), nat.ptr(self.qops), self.G, self.L,
+                                            float(m.noise_level), self.noise_seed, nat.ptr(self.noise_ctr),
+                                            nat.ptr(self.qdone), nat.stream_ptr(w.device)), "qsim_mfma_prep_noise")
+            else:
+                nat.check(self._qnoise(nat.ptr(w), nat.ptr(self.wnoisy), self.G, w.numel(), float(m.noise_level),
+                                       self.noise_seed, nat.ptr(self.noise_ctr), nat.stream_ptr(w.device)), "qnoise")
             return self.wnoisy
+        if self.mfma:
+            w = w.contiguous()
+            nat.check(self._mprep(nat.ptr(w), nat.ptr(self.qops), 1, self.L, nat.stream_ptr(w.device)), "qsim_mfma_prep")
         return w
 
     @torch.no_grad()
@@ -222,8 +245,12 @@ class QSCStepHIP:
         extra = (nat.ptr(self.qws) if self.qws is not None else None,
                  nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
             (nat.ptr(self.psave) if self.psave is not None else None,)
-        nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, wgroup, *extra, st),
-                  "qsim_fwd")
+        if self.mfma:
+            nat.check(self._mfwd(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.qops), nat.ptr(self.E), B, L, wgroup,
+                                 nat.ptr(self.psave), st), "qsim_mfma_fwd")
+        else:
+            nat.check(self._qf(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.E), B, n, L, wgroup, *extra, st),
+                      "qsim_fwd")
         cls = m.classifier
         nat.check(self._head(nat.ptr(self.E), nat.ptr(cls.weight), nat.ptr(cls.bias), nat.ptr(labels),
                              nat.ptr(self.dE), nat.ptr(cls.weight.grad), nat.ptr(cls.bias.grad), nat.ptr(self.loss),

@@ -106,3 +106,36 @@ def test_qsc_bwd_bf16x3_matches_f32_kernel(cuda, n, B):
         err = float((g3[k] - g32[k]).abs().max() / g32[k].abs().max().clamp_min(1e-12))
         print(f"{k}: bf16x3 vs f32 max-rel {err:.2e}")
         assert err < 1e-4, (k, err)
+
+
+@pytest.mark.parametrize("noise", [False, True])
+def test_qsc_circuit_forward_on_mfma_matches_register_kernel(cuda, monkeypatch, noise):
+    """The flagship's 8-qubit circuit forward on the matrix cores (qsim_mfma.hip, operand images built in the
+    QuantumNAT draw's launch) == the register kernel (qsim.hip): the same noisy weights bit for bit, the same
+    draw counter, <Z> / loss / every gradient to fp32 accuracy, over two steps."""
+    G, B = 9, 2304
+    outs = []
+    for mf in ("1", "0"):
+        monkeypatch.setenv("QDML_QSIM_MFMA", mf)
+        torch.manual_seed(0)
+        a = QSC_P128(n_qubits=8, use_quantumnat=noise, use_gradient_pruning=False, pilot_num=128).to(cuda)
+        a.train()
+        space = FlatParamSpace(list(a.named_parameters()), cuda)
+        torch.manual_seed(1)
+        step = QSCStepHIP(a, space, B, n_groups=G)
+        assert step.mfma == (mf == "1")
+        x = torch.randn(B, 2, 16, 8, device=cuda)
+        y = torch.randint(0, 3, (B,), device=cuda)
+        rec = []
+        for _ in range(2):
+            space.zero_grad()
+            loss = step(x, y)
+            torch.cuda.synchronize()
+            rec.append((loss.clone(), step.E.clone(), space.grad.clone(), step.wnoisy.clone(), step.noise_ctr.clone()))
+        outs.append(rec)
+    for (la, ea, ga, wa, ca), (lb, eb, gb, wb, cb) in zip(*outs):
+        if noise:
+            assert torch.equal(wa, wb) and torch.equal(ca, cb)
+        assert torch.allclose(la, lb, rtol=1e-5, atol=1e-6), (la, lb)
+        assert float((ea - eb).abs().max()) < 2e-5
+        assert float((ga - gb).abs().max()) <= 1e-4 * float(gb.abs().max())
