@@ -236,6 +236,11 @@ def main() -> int:
                 "dist_backend": ctx.backend,
                 "steps_per_graph": tr._k(),
                 "quantumnat": cfg.use_quantumnat,
+                # which kernels the timed step ran: the FC forward (hand_plain / hand / hand_f8 / library), the
+                # FC gradients, the 8-qubit circuit forward on the matrix cores
+                "fc_forward": getattr(tr.hstep, "fc_path", None),
+                "fc_grad_gemms": sorted(tr.hstep.hand_gemm & {"wgrad", "dgrad"}) if tr.hstep.hip else None,
+                "qsim_mfma_forward": bool(getattr(getattr(tr.cstep, "hip", None), "mfma", False)),
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
         }

@@ -290,17 +290,20 @@ class HDCEStep:
         self.defer_loss = True   # (with bias_via_conv_slabs) loss finish hosted by the conv backward
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; QDML_HAND_GEMM=0: hipBLASLt) and their
-        # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d").  Default: the hand-written weight
-        # gradient (128 x 256 tiles, 8 waves) and data gradient (144 x 256 tiles, 8 waves along N: cfg 2) --
-        # in the step 0.4115 / 0.4116 vs 0.4180 / 0.4161 ms with the hipBLASLt data gradient (same box, 2
-        # rounds, profiles/r3_02_gemm_variants.txt).  The hand forward (with the loss epilogue; 8 waves as two
-        # K halves: cfg 2, 38.4 us isolated vs hipBLASLt 39.5) stays off: beside the concurrent QSC branch its
-        # whole-CU tiles and epilogue cost more than the separate loss pass (all-hand 0.4225-0.4238)
-        hg = os.environ.get("QDML_HAND_GEMM", "wgrad,dgrad").strip()
+        # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d").  Default: all three hand-written --
+        #   forward  "fwdplain", cfg 1: 192 x 128 tiles (192 workgroups: ~64 CUs stay free for the concurrent QSC
+        #            branch, as hipBLASLt's 234-tile MT128x160 kernel leaves 22), bias-only epilogue, the loss as
+        #            the separate one-pass NMSE kernel: 0.4095 / 0.4093 vs 0.4092 / 0.4070 ms with hipBLASLt (same
+        #            box, profiles/r3_17_fwd192.txt); with 256 tiles (cfg 0 / 2) 0.8-1.3 % slower (r3_16), with the
+        #            loss in the GEMM's epilogue ("fwd") 1.5-4 % slower (r3_02, r3_17): it keeps whole CUs from the
+        #            QSC backward that then lands on the weight gradient;
+        #   wgrad    cfg 1: 128 x 256 tiles, 8 waves;  dgrad  cfg 2: 144 x 256 tiles, 8 waves along N (0.4115 /
+        #            0.4116 vs 0.4180 / 0.4161 ms with the hipBLASLt data gradient, r3_02_gemm_variants.txt)
+        hg = os.environ.get("QDML_HAND_GEMM", "fwdplain,wgrad,dgrad").strip()
         hg = {"1": "fwd,wgrad,dgrad", "all": "fwd,wgrad,dgrad", "0": "", "none": ""}.get(hg, hg)
         self.hand_gemm = set(x for x in hg.split(",") if x) if self.hip else set()
-        assert self.hand_gemm <= {"fwd", "wgrad", "dgrad"}, self.hand_gemm
-        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "0,1,2").split(","))
+        assert self.hand_gemm <= {"fwd", "fwdplain", "wgrad", "dgrad"}, self.hand_gemm
+        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "1,1,2").split(","))
         # fp8 estimator: the FC weight / data gradients in e4m3 as well (see _fc_hand_f8; QDML_F8_BWD=0: bf16)
         self.f8_bwd = os.environ.get("QDML_F8_BWD", "1") != "0"
         if self.hip:
@@ -456,6 +459,11 @@ class HDCEStep:
         if not self.defer_dgrad:
             self.dgrad()
 
+    def _plain_fwd_ok(self, A: torch.Tensor, W: torch.Tensor) -> bool:
+        from ..ops.fc import gemm_fwd_ok
+        return A.is_contiguous() and W.is_contiguous() and gemm_fwd_ok(A.shape[0], W.shape[0], A.shape[1],
+                                                                        self.gemm_cfg[0])
+
     def _hand_f8_ok(self, A: torch.Tensor) -> bool:
         """The fp8 estimator's forward on the hand-written e4m3 GEMM with the loss epilogue
         (qd_gemm_fwd_nmse_f8): e4m3 activations from the conv stack, e4m3 weight shadow from the
@@ -541,6 +549,15 @@ class HDCEStep:
             Y = torch._scaled_mm(self.conv.h3_8, m._shadow_w8.t(), scale_a=sc[0], scale_b=sc[1], bias=b,
                                  out_dtype=dt)
             m.fp8_scales.update()
+        elif "fwdplain" in self.hand_gemm and dt == torch.bfloat16 and A.dtype == dt and W.dtype == dt \
+                and b is not None and b.dtype == dt and self._plain_fwd_ok(A, W):
+            # the hand-written forward GEMM with only the bias in its epilogue; the loss runs as the separate
+            # one-pass NMSE kernel below, as after a library GEMM
+            from ..ops.fc import gemm_fwd
+            if getattr(self, "_Y_buf", None) is None or self._Y_buf.shape != (A.shape[0], W.shape[0]):
+                self._Y_buf = torch.empty(A.shape[0], W.shape[0], device=A.device, dtype=dt)
+            Y = gemm_fwd(A, W, b, out=self._Y_buf, cfg=self.gemm_cfg[0])
+            self.fc_path = "hand_plain"
         else:
             Y = torch.nn.functional.linear(A.to(dt), W, b)
         if hook is not None:

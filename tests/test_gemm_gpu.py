@@ -162,6 +162,42 @@ def test_flagship_hand_gemm_matches_hipblaslt_path(cuda, monkeypatch):
         assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
 
 
+@pytest.mark.parametrize("cfg", ["2,1,2", None])
+def test_flagship_plain_hand_forward_matches_library_forward(cuda, monkeypatch, cfg):
+    """The hand-written FC forward with only the bias in its epilogue (QDML_HAND_GEMM=fwdplain: the loss as the
+    separate one-pass NMSE kernel, as after hipBLASLt) vs the hipBLASLt forward: one flagship step, loss and
+    every HDCE gradient to bf16 accuracy."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
+                                                                                                FlagshipTrainer)
+    ctx = DistContext(device=cuda)
+    if cfg is not None:
+        monkeypatch.setenv("QDML_GEMM_CFG", cfg)
+    trs = []
+    # (hg None: the defaults -- the shipped step runs this forward)
+    for hg, path in ((None if cfg is None else "fwdplain,wgrad,dgrad", "hand_plain"), ("wgrad,dgrad", "library")):
+        if hg is None:
+            monkeypatch.delenv("QDML_HAND_GEMM", raising=False)
+        else:
+            monkeypatch.setenv("QDML_HAND_GEMM", hg)
+        torch.manual_seed(0)
+        tr = FlagshipTrainer(FlagshipConfig(batch=192, data_len=800, hip_graphs=False, use_quantumnat=False,
+                                            stream_mode="serial"), ctx)
+        tr.next_batch()
+        tr._dp_g1()
+        tr._dp_g2()
+        torch.cuda.synchronize()
+        assert tr.hstep.fc_path == path
+        trs.append(tr)
+    a, b = trs
+    assert torch.allclose(a.hloss, b.hloss, rtol=1e-2), (a.hloss, b.hloss)
+    sp = a.hdce.space
+    for name, p in zip(sp.names, sp.params):
+        sl = sp.slice_of(p)
+        x, y = a.hdce.space.grad[sl], b.hdce.space.grad[sl]
+        assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
+
+
 @pytest.mark.parametrize("cfg", [0, 1])
 @pytest.mark.parametrize("M,N,K", [(576, 256, 256), (2304, 2048, 4096)])
 def test_gemm_fwd_f8_matches_fp32(cuda, M, N, K, cfg):
