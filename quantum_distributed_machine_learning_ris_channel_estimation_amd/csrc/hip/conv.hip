@@ -32,6 +32,7 @@
 //   bn_*             statistics finalisation (+ running-stat momentum updates in stream order),
 //                    backward reductions, and the final BN+ReLU apply that feeds the FC GEMM.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -1395,7 +1396,7 @@ __global__ void __launch_bounds__(64) bn_stats_finalize_kernel(FinJobs jobs, int
 // Backward reductions: per (u, chunk, ch): sum g, sum g*xhat.  grid (U*chunks, E), block 256.
 // 16-lane groups each own one (sample, channel) row of HW values (8 per lane per pass); a
 // group's rows alternate between channels g and g+16, so every lane keeps 2 x 2 partials.
-template <int HW, typename TDH>
+template <int HW, typename TDH, int UNR = (HW == 128 ? 4 : 2)>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restrict__ dh, const uint16_t* __restrict__ z,
                                                             const float* __restrict__ st, float* __restrict__ slab,
                                                             int E, int B, int chunks, int spb, LossFinish lf) {
@@ -1409,32 +1410,50 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restric
   const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
   const int rows = (nend - n0) * CO;
   float sg0 = 0.f, sgx0 = 0.f, sg1 = 0.f, sgx1 = 0.f;  // channels grp and grp+16
-  for (int it = 0; it * 16 < rows; ++it) {
-    const int r = it * 16 + grp;
-    if (r >= rows) break;
-    const int n = n0 + r / CO, c = r % CO, ch = e * CO + c;
-    const float* sc = st + ((size_t)u * EC + ch) * NST;
-    const float a = sc[ST_A], b = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
-    const size_t rb = ((size_t)n * EC + ch) * HW;
-    float tg = 0.f, tgx = 0.f;
+  // rows in rounds of UNR with every load of a round issued before its math (one row per round trip kept the
+  // kernel latency-bound); the per-row sums and their order into sg / sgx are the one-row loop's
+  constexpr int QN = HW / 128;   // 8-value passes per lane per row
+  const int nit = (rows + 15) / 16;
+  for (int it0 = 0; it0 < nit; it0 += UNR) {
+    float d[UNR][QN][8], zz[UNR][QN][8], a[UNR], b[UNR], mu[UNR], inv[UNR];
+    bool ok[UNR];
 #pragma unroll
-    for (int q = gl * 8; q < HW; q += 128) {
-      float d[8], zz[8];
-      load8(dh + rb + q, d);
-      load8(z + rb + q, zz);
+    for (int k = 0; k < UNR; ++k) {
+      const int r = (it0 + k) * 16 + grp;
+      ok[k] = it0 + k < nit && r < rows;
+      if (!ok[k]) continue;
+      const int n = n0 + r / CO, c = r % CO, ch = e * CO + c;
+      const float* sc = st + ((size_t)u * EC + ch) * NST;
+      a[k] = sc[ST_A];
+      b[k] = sc[ST_B];
+      mu[k] = sc[ST_MEAN];
+      inv[k] = sc[ST_INV];
+      const size_t rb = ((size_t)n * EC + ch) * HW;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float g = (a * zz[j] + b > 0.f) ? d[j] : 0.f;
-        tg += g;
-        tgx += g * (zz[j] - mu) * inv;
+      for (int qi = 0; qi < QN; ++qi) {
+        load8(dh + rb + gl * 8 + 128 * qi, d[k][qi]);
+        load8(z + rb + gl * 8 + 128 * qi, zz[k][qi]);
       }
     }
-    if (it & 1) {
-      sg1 += tg;
-      sgx1 += tgx;
-    } else {
-      sg0 += tg;
-      sgx0 += tgx;
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      if (!ok[k]) continue;
+      float tg = 0.f, tgx = 0.f;
+#pragma unroll
+      for (int qi = 0; qi < QN; ++qi)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float g = (a[k] * zz[k][qi][j] + b[k] > 0.f) ? d[k][qi][j] : 0.f;
+          tg += g;
+          tgx += g * (zz[k][qi][j] - mu[k]) * inv[k];
+        }
+      if ((it0 + k) & 1) {
+        sg1 += tg;
+        sgx1 += tgx;
+      } else {
+        sg0 += tg;
+        sgx0 += tgx;
+      }
     }
   }
 #pragma unroll
@@ -1542,7 +1561,7 @@ __global__ void __launch_bounds__(256) bn_relu_apply_kernel(const uint16_t* __re
 // h = relu(a z + b) for spb samples x 32 channels (32*HW contiguous bf16 per sample).  Workgroups
 // beyond: every layer's running statistics (+ num_batches_tracked), one (layer, channel) per wave --
 // jobs.st[2] is null there, the records of layer 3 come from the apply workgroups only.
-template <int HW>
+template <int HW, int UNR>
 __global__ void __launch_bounds__(256) bn_apply_tail_kernel(const uint16_t* __restrict__ z, uint16_t* __restrict__ h,
                                                             BnFwd bnf, FinJobs jobs, int U, int E, int B, int spb,
                                                             int ach, int chunks, int training,
@@ -1560,32 +1579,63 @@ __global__ void __launch_bounds__(256) bn_apply_tail_kernel(const uint16_t* __re
   }
   __shared__ float stl[CO * NST];
   const int e = blockIdx.x % E, rest = blockIdx.x / E, chunk = rest % ach, u = rest / ach;
+  const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
+  constexpr int ITEMS = CO * HW / 8;   // 8-value items per sample
+  // UNR items per thread per round, the next round's loads in flight behind this round's math and stores
+  // (one load per round trip kept the kernel latency-bound: 16 dependent round trips per thread at spb 8),
+  // and the first round's loads issued before the BN records are built (z does not depend on them)
+  const int total = (nend - n0) * ITEMS;
+  auto off = [&](int t) -> size_t {
+    const int n = n0 + t / ITEMS, i = t % ITEMS;
+    return ((size_t)n * EC + e * CO) * HW + (size_t)i * 8;
+  };
+  uint4 raw[UNR];
+#pragma unroll
+  for (int k = 0; k < UNR; ++k) {
+    const int t = threadIdx.x + 256 * k;
+    if (t < total) raw[k] = *reinterpret_cast<const uint4*>(z + off(t));
+  }
   bn_fwd_build(bnf, stl, u, e, EC, chunk == 0);
   __syncthreads();
   const float q = h8 ? qs[0] : 0.f;
   float mx = 0.f;
-  const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
-  constexpr int ITEMS = CO * HW / 8;   // 8-value items per sample
-  for (int t = threadIdx.x; t < (nend - n0) * ITEMS; t += 256) {
-    const int n = n0 + t / ITEMS, i = t % ITEMS;
-    const size_t e0 = ((size_t)n * EC + e * CO) * HW + (size_t)i * 8;
-    const int c = (i * 8) / HW;
-    const float a = stl[c * NST + ST_A], b = stl[c * NST + ST_B];
-    float v[8];
-    load8(z + e0, v);
-    uint32_t w[4];
+  for (int base = 0; base < total; base += 256 * UNR) {
+    uint4 nxt[UNR];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = relu_nan(a * v[j] + b);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
-    *reinterpret_cast<uint4*>(h + e0) = make_uint4(w[0], w[1], w[2], w[3]);
-    if (h8) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j]);
-      const uint32_t p0 = e4m3_pack4(v[0] * q, v[1] * q, v[2] * q, v[3] * q);
-      const uint32_t p1 = e4m3_pack4(v[4] * q, v[5] * q, v[6] * q, v[7] * q);
-      *reinterpret_cast<uint2*>(h8 + e0) = make_uint2(p0, p1);
+    for (int k = 0; k < UNR; ++k) {
+      const int t = base + 256 * UNR + threadIdx.x + 256 * k;
+      if (t < total) nxt[k] = *reinterpret_cast<const uint4*>(z + off(t));
     }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) {
+      const int t = base + threadIdx.x + 256 * k;
+      if (t >= total) continue;
+      const size_t e0 = off(t);
+      const int c = ((t % ITEMS) * 8) / HW;
+      const float a = stl[c * NST + ST_A], b = stl[c * NST + ST_B];
+      const uint32_t r4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = __uint_as_float(r4[j] << 16);
+        v[2 * j + 1] = __uint_as_float(r4[j] & 0xffff0000u);
+      }
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = relu_nan(a * v[j] + b);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = f32_to_bf16(v[2 * j]) | ((uint32_t)f32_to_bf16(v[2 * j + 1]) << 16);
+      *reinterpret_cast<uint4*>(h + e0) = make_uint4(w[0], w[1], w[2], w[3]);
+      if (h8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx = fmaxf(mx, v[j]);
+        const uint32_t p0 = e4m3_pack4(v[0] * q, v[1] * q, v[2] * q, v[3] * q);
+        const uint32_t p1 = e4m3_pack4(v[4] * q, v[5] * q, v[6] * q, v[7] * q);
+        *reinterpret_cast<uint2*>(h8 + e0) = make_uint2(p0, p1);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UNR; ++k) raw[k] = nxt[k];
   }
   if (h8) amax_block_store(amax, mx);
 }
@@ -1956,11 +2006,14 @@ QD_API int qd_bn_stats_finalize_multi(int n, const float* const* stats, const fl
 QD_API int qd_bn_bwd_reduce(const void* dh, int dh_bf16, const uint16_t* z, const float* st, float* slab, int N, int E,
                             int B, int H, int W, int chunks, int spb, const qd::LossFinish* lf_in, void* stream) {
   const qd::LossFinish lf = (lf_in && lf_in->part) ? *lf_in : qd::LossFinish{};
+  // QDML_TAIL_UNR=1: one row per round trip (the round-2 loop, for A/B; the same knob as the BN tail's)
+  static const bool unr1 = [] { const char* v = getenv("QDML_TAIL_UNR"); return v && atoi(v) == 1; }();
   dim3 grid((N / B) * chunks, E + (lf.part ? 1 : 0));
   hipStream_t s = (hipStream_t)stream;
   if (chunks * spb < B || H * W % 64) return (int)hipErrorInvalidValue;
   if (H * W == 128) {
-    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
+    if (dh_bf16 && unr1) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t, 1>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
+    else if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
     else hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb, lf);
   } else if (H * W == 256) {
     if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
@@ -2023,12 +2076,20 @@ QD_API int qd_bn_apply_tail(const uint16_t* z, uint16_t* h, const BnFwd* bnf, co
   if (napply > qd::kAmaxParts) return (int)hipErrorInvalidValue;
   const dim3 grid(napply + nfin);
   hipStream_t s = (hipStream_t)stream;
-  if (HW == 128)
-    hipLaunchKernelGGL((bn_apply_tail_kernel<128>), grid, dim3(256), 0, s, z, h, *bnf, jobs, U, E, B, spb, ach, chunks,
-                       training, nbt, n_nbt, nbt_inc, h8, qs, amax);
+  // QDML_TAIL_UNR=1: one load in flight per thread (the round-2 loop, for A/B)
+  static const bool unr1 = [] { const char* v = getenv("QDML_TAIL_UNR"); return v && atoi(v) == 1; }();
+#define QD_TAIL(HWV, U_)                                                                                          \
+  hipLaunchKernelGGL((bn_apply_tail_kernel<HWV, U_>), grid, dim3(256), 0, s, z, h, *bnf, jobs, U, E, B, spb, ach, \
+                     chunks, training, nbt, n_nbt, nbt_inc, h8, qs, amax)
+  if (HW == 128 && unr1)
+    QD_TAIL(128, 1);
+  else if (HW == 128)
+    QD_TAIL(128, 4);
+  else if (HW == 256 && unr1)
+    QD_TAIL(256, 1);
   else if (HW == 256)
-    hipLaunchKernelGGL((bn_apply_tail_kernel<256>), grid, dim3(256), 0, s, z, h, *bnf, jobs, U, E, B, spb, ach, chunks,
-                       training, nbt, n_nbt, nbt_inc, h8, qs, amax);
+    QD_TAIL(256, 4);
+#undef QD_TAIL
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
