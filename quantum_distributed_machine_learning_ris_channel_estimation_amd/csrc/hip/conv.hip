@@ -1663,6 +1663,7 @@ __global__ void __launch_bounds__(256) slab_rows_sum_kernel(const float* __restr
 // Vector variant (width % 4 == 0, 16-byte aligned rows): 16 column quads x 16 row phases per
 // block, float4 loads, unrolled so each thread keeps several independent loads in flight.
 // ld: row stride of the slab in floats (>= width; a group spans rows * ld floats).
+template <int SR = 8>
 __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
                                                     int width, int ld, int g, int bx, int accumulate);
 __global__ void __launch_bounds__(256) slab_rows_sum4_kernel(const float* __restrict__ slab, float* __restrict__ out,
@@ -1679,6 +1680,7 @@ struct SlabJobs {
   float* out[kSlabJobs];
   int groups[kSlabJobs], rows[kSlabJobs], width[kSlabJobs], ld[kSlabJobs], vec[kSlabJobs];
   int accumulate;
+  int sr1;   // (A/B, QDML_TAIL_UNR=1) one row per load round
 };
 __device__ __forceinline__ void slab_rows_sum1_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
                                                     int width, int ld, int g, int bx, int accumulate) {
@@ -1707,7 +1709,10 @@ __device__ __forceinline__ void slab_rows_sum1_body(const float* __restrict__ sl
 __global__ void __launch_bounds__(256) slab_rows_sum4_multi_kernel(SlabJobs jobs) {
   const int j = blockIdx.z;
   if (blockIdx.y >= jobs.groups[j] || blockIdx.x * 64 >= jobs.width[j]) return;
-  if (jobs.vec[j])
+  if (jobs.vec[j] && jobs.sr1)
+    slab_rows_sum4_body<1>(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], jobs.ld[j], blockIdx.y, blockIdx.x,
+                           jobs.accumulate);
+  else if (jobs.vec[j])
     slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], jobs.ld[j], blockIdx.y, blockIdx.x,
                         jobs.accumulate);
   else
@@ -1715,6 +1720,7 @@ __global__ void __launch_bounds__(256) slab_rows_sum4_multi_kernel(SlabJobs jobs
                         jobs.accumulate);
 }
 
+template <int SR>
 __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
                                                     int width, int ld, int g, int bx, int accumulate) {
   __shared__ float4 red[16][16];
@@ -1723,13 +1729,21 @@ __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ sl
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < width) {
     const float* s = slab + (size_t)g * rows * ld + i;
-#pragma unroll 4
-    for (int r = ty; r < rows; r += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(s + (size_t)r * ld);
-      t.x += v.x;
-      t.y += v.y;
-      t.z += v.z;
-      t.w += v.w;
+    // rounds of SR rows with every load of a round issued before its adds (same summation order as a
+    // row-at-a-time loop: bit-identical sums); QDML_TAIL_UNR=1 selects one row per round
+    for (int r0 = ty; r0 < rows; r0 += 16 * SR) {
+      float4 v[SR];
+#pragma unroll
+      for (int k = 0; k < SR; ++k)
+        if (r0 + 16 * k < rows) v[k] = *reinterpret_cast<const float4*>(s + (size_t)(r0 + 16 * k) * ld);
+#pragma unroll
+      for (int k = 0; k < SR; ++k)
+        if (r0 + 16 * k < rows) {
+          t.x += v[k].x;
+          t.y += v[k].y;
+          t.z += v[k].z;
+          t.w += v[k].w;
+        }
     }
   }
   red[ty][tq] = t;
@@ -2102,6 +2116,8 @@ QD_API int qd_slab_rows_sum_multi(int n, const float* const* slabs, float* const
   if (n < 1 || n > kSlabJobs) return (int)hipErrorInvalidValue;
   SlabJobs jobs{};
   jobs.accumulate = accumulate;
+  static const bool sr1 = [] { const char* v = getenv("QDML_TAIL_UNR"); return v && atoi(v) == 1; }();
+  jobs.sr1 = sr1;
   int gx = 0, gy = 0;
   for (int j = 0; j < n; ++j) {
     jobs.ld[j] = lds ? lds[j] : widths[j];
