@@ -101,7 +101,7 @@ def main() -> int:
     one_graph = args.dp_one_graph or args.dp_graph == "one"
     forced = world_env == 1 and os.environ.get("QDML_FORCE_DIST") == "1"   # (a one-rank RCCL group: rehearsal)
     if args.dp_graph == "auto" and not args.dp_one_graph and (world_env > 1 or forced) and not args.no_graphs \
-            and os.environ.get("QDML_DIST_BACKEND", "nccl") == "nccl":
+            and os.environ.get("QDML_DIST_BACKEND", "rccl") in ("rccl", "nccl"):
         # (before this process touches the GPU: the probe runs in a child of every rank)
         import torch
         n_dev = torch.cuda.device_count()   # (no GPU initialisation on this image)

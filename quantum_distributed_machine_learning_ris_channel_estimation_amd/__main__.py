@@ -71,7 +71,7 @@ def main(argv=None) -> int:
                 print(f"wrote scenario {s} user {u} -> {cfg.data_dir}")
         return 0
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and cfg.dp_graphs == "auto" and cfg.hip_graphs \
-            and cfg.device != "cpu" and os.environ.get("QDML_DIST_BACKEND", "nccl") == "nccl":
+            and cfg.device != "cpu" and os.environ.get("QDML_DIST_BACKEND", "rccl") in ("rccl", "nccl"):
         # (before anything touches the GPU: every rank's child captures the collective pattern, rank 0 decides)
         from .parallel.capture_probe import preflight
         os.environ["QDML_DP_GRAPHS"] = "1" if preflight() else "0"

@@ -3,11 +3,12 @@
 The one-graph data-parallel plan (``FlagshipConfig.dp_one_graph``) captures the step's all-reduces
 into its HIP graph.  That path is measured bit-exact over a one-rank RCCL group
 (``tests/test_flagship_gpu.py::test_dp_one_graph_matches_five_graphs_over_rccl``), but a runtime that
-cannot capture a collective fails hard (a segfault in ``hipStreamEndCapture``,
-``scripts/probe_rccl_capture.py``), not with an exception.  So before a multi-rank run commits to it,
+cannot capture a collective fails hard (a segfault in ``hipStreamEndCapture`` was
+seen with torch's process group in round 2), not with an exception.  So before a multi-rank run commits to it,
 every rank starts a CHILD process (the parent has not touched the GPU yet) that captures the plan's
-collective pattern -- two async all-reduces launched from the capturing stream, one waited for on a
-forked stream, and the ZeRO plan's reduce-scatter + all-gather -- replays it and checks the sums.  The
+collective pattern through the framework's own RCCL communicator (``parallel/comm.py``) and
+``GradBuckets`` -- two bucket all-reduces (one coalesced), one waited for on a forked stream, and the
+ZeRO plan's reduce-scatter + all-gather -- replays it and checks the sums.  The
 ranks then agree through a TCPStore: rank 0 publishes one decision (the plan is used only if every
 child succeeded) and every rank reads it; a rank that cannot read it exits non-zero.
 
@@ -24,40 +25,44 @@ import time
 
 def _child() -> int:
     import torch
-    import torch.distributed as dist
-    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
-    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
-    torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import (GradBuckets,
+                                                                                             init_distributed,
+                                                                                             shutdown)
+    ctx = init_distributed("cuda")
+    rank, world, dev = ctx.rank, ctx.world, ctx.device
     a = torch.full((1 << 20,), float(rank + 1), device=dev)
     b = torch.full((4096,), 1.0, device=dev)
+    c = torch.full((8,), 1.0, device=dev)
     out = torch.empty_like(a)
     # the ZeRO one-graph plan's collectives too: reduce-scatter of a region, all-gather of the shards
     full = torch.full((world * 8192,), float(rank + 1), device=dev)
-    shard = torch.empty(8192, device=dev)
-    gath = torch.empty(world * 8192, device=dev)
+    gath = torch.zeros(world * 8192, device=dev)
+    bk = GradBuckets(ctx, {"a": [a], "bc": [b, c]})
     side = torch.cuda.Stream(dev)
 
     def body():
         a.mul_(1.0)
-        w1 = dist.all_reduce(a, async_op=True)
-        w2 = dist.all_reduce(b, async_op=True)
-        w3 = dist.reduce_scatter_tensor(shard, full, async_op=True)
+        bk.launch("a")
+        bk.launch("bc")
+        bk.launch_reduce_scatter("rs", full)
         side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            w1.wait()
+        with torch.cuda.stream(side):   # (one bucket consumed on a forked stream)
+            bk.wait(("a",))
             out.copy_(a)
-        w2.wait()
-        w3.wait()
-        w4 = dist.all_gather_into_tensor(gath, shard, async_op=True)
-        w4.wait()
+        bk.wait(("bc", "rs"))
+        gath.copy_(full)
+        bk.launch_all_gather("ag", gath)
+        bk.wait(("ag",))
+        bk.pending.clear()
         torch.cuda.current_stream(dev).wait_stream(side)
 
     def reset():
         a.fill_(float(rank + 1))
         b.fill_(1.0)
+        c.fill_(1.0)
         full.fill_(float(rank + 1))
-        shard.zero_()
         gath.zero_()
 
     s = torch.cuda.Stream(dev)
@@ -68,16 +73,16 @@ def _child() -> int:
     torch.cuda.synchronize(dev)
     g = torch.cuda.CUDAGraph()
     reset()
-    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+    with torch.cuda.graph(g):
         body()
     reset()
     g.replay()
     torch.cuda.synchronize(dev)
     tri = world * (world + 1) / 2
-    ok = (bool((out == tri).all()) and bool((b == world).all()) and bool((shard == tri).all())
-          and bool((gath == tri).all()))
-    dist.barrier()
-    dist.destroy_process_group()
+    ok = (bool((out == tri).all()) and bool((b == world).all()) and bool((c == world).all())
+          and bool((gath.view(world, -1)[rank] == tri).all()))
+    ctx.barrier()
+    shutdown()
     return 0 if ok else 3
 
 

@@ -1,4 +1,4 @@
-"""SPMD data parallelism over RCCL (torch.distributed 'nccl' backend on ROCm) / Gloo on CPU.
+"""SPMD data parallelism over RCCL (our own communicator, ``parallel/comm.py``) / Gloo on CPU.
 
 Reference: the only multi-GPU mechanism is ``torch.nn.DataParallel`` over 4 GPUs
 (Runner_P128_QuantumNAT_onchipQNN.py:135-153, Test.py:70-97): single process, one
@@ -20,7 +20,12 @@ MI355X design:
     parameter grads coalesced into one second bucket;
   * metrics (NMSE numerators/denominators, correct/total counts, loss sums) are
     all-reduced as raw sums -- the global NMSE is sum(err)/sum(pow), never a mean of
-    per-rank ratios.
+    per-rank ratios;
+  * backends: "rccl" on GPUs -- one RCCL communicator per process (``parallel/comm.py``),
+    every collective a stream-ordered RCCL kernel on a dedicated comm stream, with no
+    process group, watchdog thread or work objects (so a HIP graph can capture the
+    collectives with nothing polling them: docs/CONCURRENCY.md "captured collectives");
+    "gloo" for CPU runs and the several-ranks-per-GPU rehearsal (torch.distributed).
 """
 from __future__ import annotations
 
@@ -33,14 +38,20 @@ import torch
 import torch.distributed as dist
 
 
+_GLOO_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
 @dataclass
 class DistContext:
     rank: int = 0
     world: int = 1
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
-    backend: str = "none"
-    forced: bool = False   # a process group even at world 1 (QDML_FORCE_DIST=1: rehearses the collectives)
+    backend: str = "none"   # none | rccl | gloo
+    forced: bool = False   # collectives even at world 1 (QDML_FORCE_DIST=1: rehearses them)
+    comm: Optional[object] = None    # (rccl) parallel.comm.RcclComm
+    store: Optional[object] = None   # (rccl) the c10d store the communicator id travelled through
+    _comm_stream: Optional[object] = None
 
     @property
     def is_main(self) -> bool:
@@ -50,22 +61,46 @@ class DistContext:
     def distributed(self) -> bool:
         return self.world > 1 or self.forced
 
+    @property
+    def comm_stream(self) -> "torch.cuda.Stream":
+        """(rccl) the one stream every gradient collective runs on: RCCL needs one issue order per
+        communicator, and a single stream gives every rank the same one."""
+        if self._comm_stream is None:
+            self._comm_stream = torch.cuda.Stream(self.device)
+        return self._comm_stream
+
+    def _device_op(self, t: torch.Tensor, fn) -> torch.Tensor:
+        """(rccl) run ``fn`` on a device tensor (host tensors round-trip through the device)."""
+        if t.is_cuda:
+            return fn(t)
+        d = t.to(self.device)
+        fn(d)
+        t.copy_(d.cpu())
+        return t
+
     def barrier(self) -> None:
-        if self.distributed:
-            if self.backend == "nccl":
-                dist.barrier(device_ids=[self.local_rank])
-            else:
-                dist.barrier()
+        if not self.distributed:
+            return
+        if self.backend == "rccl":
+            # a one-element all-reduce can only complete once every rank has issued it
+            x = torch.ones(1, device=self.device)
+            self.comm.all_reduce_(x)
+            torch.cuda.current_stream(self.device).synchronize()
+        else:
+            dist.barrier()
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.distributed:
+            if self.backend == "rccl":
+                return self._device_op(t, lambda d: self.comm.broadcast_(d, src))
             dist.broadcast(t, src)
         return t
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.distributed:
-            dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
-                                   "min": dist.ReduceOp.MIN}[op])
+            if self.backend == "rccl":
+                return self._device_op(t, lambda d: self.comm.all_reduce_(d, op))
+            dist.all_reduce(t, op=_GLOO_OPS[op])
         return t
 
     def max_scalar(self, v: float) -> float:
@@ -75,8 +110,8 @@ class DistContext:
         """Element-wise max over ranks of a short host vector (one collective)."""
         if not self.distributed:
             return [float(v) for v in vs]
-        t = torch.tensor(list(vs), dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor(list(vs), dtype=torch.float64)
+        self.all_reduce_(t, "max")
         return [float(x) for x in t.tolist()]
 
 
@@ -111,9 +146,15 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
         dev = torch.device("cpu")
     backend = "none"
     forced = world == 1 and os.environ.get("QDML_FORCE_DIST") == "1"
+    comm = store = None
     if world > 1 or forced:
-        backend = os.environ.get("QDML_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
-        if backend == "nccl":
+        backend = os.environ.get("QDML_DIST_BACKEND") or ("rccl" if use_cuda else "gloo")
+        backend = {"nccl": "rccl"}.get(backend, backend)   # (torch's name for it on ROCm)
+        if backend not in ("rccl", "gloo"):
+            raise ValueError(f"QDML_DIST_BACKEND={backend!r}: rccl or gloo")
+        if backend == "rccl":
+            if not use_cuda:
+                raise RuntimeError("the rccl backend needs a GPU")
             check_local_gpus(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)), torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if forced and "MASTER_PORT" not in os.environ:
@@ -121,12 +162,17 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
             with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
                 sk.bind(("127.0.0.1", 0))
                 os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
-        kw = {}
-        if backend == "nccl":
-            kw["device_id"] = dev
-        dist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s),
-                                **kw)
-    _CTX = DistContext(rank, world, local, dev, backend, forced)
+        tmo = datetime.timedelta(seconds=timeout_s)
+        if backend == "rccl":
+            from .comm import RcclComm
+            # (the env:// rendezvous: torchrun's agent store when there is one, else rank 0 hosts a TCPStore)
+            store, _, _ = next(dist.rendezvous("env://", rank=rank, world_size=world, timeout=tmo))
+            comm = RcclComm(rank, world, dev, store)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world, timeout=tmo)
+    _CTX = DistContext(rank, world, local, dev, backend, forced, comm, store)
+    if comm is not None:
+        _CTX.barrier()   # (every rank holds the communicator id: rank 0's store may go)
     return _CTX
 
 
@@ -136,8 +182,12 @@ def get_context() -> DistContext:
 
 def shutdown() -> None:
     global _CTX
-    if _CTX is not None and dist.is_initialized():
-        dist.destroy_process_group()
+    if _CTX is not None:
+        if _CTX.comm is not None:
+            torch.cuda.synchronize(_CTX.device)
+            _CTX.comm.close()
+        elif dist.is_initialized():
+            dist.destroy_process_group()
     _CTX = None
 
 
@@ -172,21 +222,45 @@ class GradBuckets:
                 self.staging[k] = torch.empty(sum(t.numel() for t in ts), device=ts[0].device, dtype=ts[0].dtype)
         self.pending: Dict[str, list] = {}
 
+    def assert_quiescent(self) -> None:
+        """Raise if a launched collective has not been waited for (a graph capture must not begin with one
+        in flight: its completion would be observed from inside the capture)."""
+        if self.pending:
+            raise RuntimeError(f"gradient collectives still pending: {sorted(self.pending)}")
+
     def bucket_bytes(self) -> Dict[str, int]:
         return {k: sum(t.numel() * t.element_size() for t in ts) for k, ts in self.buckets.items()}
+
+    def _collective(self, fn):
+        """Issue one collective.  gloo: ``fn(None)`` is a torch.distributed async call returning its work.
+        rccl: ``fn(stream)`` issues the RCCL kernel on the context's comm stream, forked from the current
+        stream (so it sees every gradient written so far); the returned handle is an event on the comm
+        stream that ``wait`` joins back -- under graph capture the fork and the join are graph edges."""
+        if self.ctx.backend != "rccl":
+            return fn(None)
+        cur = torch.cuda.current_stream(self.ctx.device)
+        cs = self.ctx.comm_stream
+        cs.wait_stream(cur)
+        fn(cs)
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        return ev
+
+    def _all_reduce(self, t: torch.Tensor):
+        if self.ctx.backend == "rccl":
+            return self._collective(lambda s: self.ctx.comm.all_reduce_(t, stream=s))
+        return dist.all_reduce(t, async_op=True)
 
     def launch(self, name: str) -> None:
         if not self.ctx.distributed or name not in self.buckets:
             return
         ts = self.buckets[name]
         if len(ts) == 1:
-            work = dist.all_reduce(ts[0], async_op=True)
-            self.pending[name] = [work, None, None]
+            self.pending[name] = [self._all_reduce(ts[0]), None, None]
         else:
             st = self.staging[name]
             torch.cat([t.reshape(-1) for t in ts], out=st)
-            work = dist.all_reduce(st, async_op=True)
-            self.pending[name] = [work, st, ts]
+            self.pending[name] = [self._all_reduce(st), st, ts]
 
     def launch_all(self) -> None:
         for k in self.buckets:
@@ -209,7 +283,10 @@ class GradBuckets:
         if not self.ctx.distributed:
             return
         st = self._shard_staging("rs:" + name, full)
-        work = dist.reduce_scatter_tensor(st, full, async_op=True)
+        if self.ctx.backend == "rccl":
+            work = self._collective(lambda s: self.ctx.comm.reduce_scatter(st, full, stream=s))
+        else:
+            work = dist.reduce_scatter_tensor(st, full, async_op=True)
         self.pending[name] = [work, st, [full.view(self.ctx.world, -1)[self.ctx.rank]]]
 
     def launch_all_gather(self, name: str, full: torch.Tensor) -> None:
@@ -219,7 +296,11 @@ class GradBuckets:
             return
         st = self._shard_staging("ag:" + name, full)
         st.copy_(full.view(self.ctx.world, -1)[self.ctx.rank])
-        self.pending[name] = [dist.all_gather_into_tensor(full, st, async_op=True), None, None]
+        if self.ctx.backend == "rccl":
+            work = self._collective(lambda s: self.ctx.comm.all_gather(full, st, stream=s))
+        else:
+            work = dist.all_gather_into_tensor(full, st, async_op=True)
+        self.pending[name] = [work, None, None]
 
     def wait(self, names: Optional[Sequence[str]] = None) -> None:
         """Make the CURRENT stream wait for the named (default: all) launched collectives; a coalesced
@@ -228,7 +309,10 @@ class GradBuckets:
         for from several streams."""
         for k in list(self.pending) if names is None else [n for n in names if n in self.pending]:
             ent = self.pending[k]
-            ent[0].wait()
+            if isinstance(ent[0], torch.cuda.Event):   # (rccl: join the comm stream's event)
+                torch.cuda.current_stream(self.ctx.device).wait_event(ent[0])
+            else:
+                ent[0].wait()
             if _GLOO_HOST_SYNC and self.ctx.backend == "gloo" and torch.cuda.is_available():
                 torch.cuda.current_stream().synchronize()
             if ent[1] is not None:

@@ -272,7 +272,7 @@ class FlagshipTrainer(DPPlan):
                     for i in range(k):
                         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr,
                                      fence=i == k - 1, first=i == 0)
-                gs = [GraphedStep(body, enabled=graphs, capture_error_mode="thread_local")]
+                gs = [GraphedStep(body, enabled=graphs, guards=(self.buckets.assert_quiescent,))]
                 self._graph_sets[k] = gs
                 return gs
             if k != 1:
@@ -281,7 +281,7 @@ class FlagshipTrainer(DPPlan):
             # graphs that replay concurrently (gf on the fc stream beside gr / the next g1a on main)
             # allocate nothing
             pool = torch.cuda.graph_pool_handle() if graphs else None
-            gs = [GraphedStep(f, enabled=graphs, pool=pool)
+            gs = [GraphedStep(f, enabled=graphs, pool=pool, guards=(self.buckets.assert_quiescent,))
                   for f in (self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)]
         self._graph_sets[k] = gs
         return gs

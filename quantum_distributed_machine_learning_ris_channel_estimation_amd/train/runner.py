@@ -177,7 +177,7 @@ class Y2HRunner:
         if self.dp_graphs not in ("on", "off", "auto"):
             raise ValueError(f"dp_graphs {self.dp_graphs!r}")
         on = self.dp_graphs == "on" or (self.dp_graphs == "auto" and os.environ.get("QDML_DP_GRAPHS") == "1")
-        return on and ctx.backend == "nccl"
+        return on and ctx.backend == "rccl"
 
     # ------------------------------------------------------------------ HDCE
     def build_hdce(self) -> HDCEModel:

@@ -15,7 +15,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import os
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
 
@@ -85,13 +85,15 @@ class GraphedStep:
     WARMUP = 3
 
     def __init__(self, fn: Callable[[], None], enabled: bool = True, warmup: Optional[int] = None, pool=None,
-                 capture_stream: Optional["torch.cuda.Stream"] = None, capture_error_mode: str = "global"):
+                 capture_stream: Optional["torch.cuda.Stream"] = None, capture_error_mode: str = "global",
+                 guards: Sequence[Callable[[], None]] = ()):
         """``capture_stream``: the stream the graph is captured on (e.g. a high-priority one, so the
-        nodes of its chain keep that priority over side branches forked from lower-priority streams)."""
+        nodes of its chain keep that priority over side branches forked from lower-priority streams).
+        ``guards``: checks run right before the capture begins (each raises if the process is not
+        quiescent, e.g. a gradient collective still pending)."""
         self.capture_stream = capture_stream
-        # "thread_local" when the captured body launches RCCL collectives: the process group's
-        # watchdog thread polls the events of earlier collectives, which a "global" capture forbids
         self.capture_error_mode = capture_error_mode
+        self.guards = list(guards)
         self.fn = fn
         self.enabled = enabled and torch.cuda.is_available()
         self.warmup = self.WARMUP if warmup is None else warmup
@@ -105,6 +107,7 @@ class GraphedStep:
             for _ in range(self.warmup):
                 self.fn()
         torch.cuda.current_stream().wait_stream(s)
+        self.pre_capture()
         g = torch.cuda.CUDAGraph()
         if self.capture_stream is not None:
             self.capture_stream.wait_stream(torch.cuda.current_stream())
@@ -112,6 +115,16 @@ class GraphedStep:
                               capture_error_mode=self.capture_error_mode):
             self.fn()
         self.graph = g
+
+    def pre_capture(self) -> None:
+        """The capture starts from a quiescent process: every warm-up kernel and collective has finished
+        on the device (host sync), and every guard passes.  (Round 3's captured-collective abort: a thread
+        other than the capturing one touched an event of a warm-up collective while the capture ran --
+        docs/CONCURRENCY.md "captured collectives".)"""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        for g in self.guards:
+            g()
 
     def __call__(self) -> None:
         if not self.enabled:
