@@ -865,6 +865,10 @@ QD_API int qd_gemm_fwd_nmse_f8(const uint8_t* A8, const uint8_t* W8, const float
          bias, na, nullptr, 0, deq};
   if (M % FwdA8::BM || (FwdA8::BM / (B * E) + 2) * E > 64 || B % 16 || FwdA8::BM % (16 * E))
     return (int)hipErrorInvalidValue;
+  // the dY amax partials go to amax8[blockIdx.x]: the 1-D grid must fit the kAmaxParts slots of slot 6
+  const long tiles = cfg == 1 ? (long)(M / FwdM8::BM) * ((N + FwdM8::BN - 1) / FwdM8::BN)
+                              : (long)(M / FwdA8::BM) * ((N + FwdA8::BN - 1) / FwdA8::BN);
+  if (dY8 != nullptr && tiles > qd::kAmaxParts) return (int)hipErrorInvalidValue;
   if (cfg == 1) return launch<FwdM8, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
   return launch<FwdA8, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
 }

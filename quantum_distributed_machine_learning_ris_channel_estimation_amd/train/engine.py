@@ -316,6 +316,30 @@ class HDCEStep:
             self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
 
+    def prime_fp8_dy(self, forward: Callable[[], None], state: Sequence[torch.Tensor], ctx=None) -> bool:
+        """(fp8 estimator with e4m3 FC gradients) seed the delayed scale of the loss gradient dY (fp8 slot 6).
+        The loss epilogue quantises dY with the PREVIOUS step's scale, and dY = 2 err / (S den) sits far below
+        e4m3's range at the initial unit scale: the first step's FC gradients would underflow.
+        ``forward`` runs one forward + loss pass (this step's bf16-gradient path) on the first batch; max |dY|
+        (max over ranks with ``ctx``) sets the slot; every tensor in ``state`` is restored afterwards, so the
+        run differs from an unprimed one only in slot 6.  Returns whether it primed."""
+        sc = getattr(self.m, "fp8_scales", None)
+        if sc is None or not self.hip or not self.f8_bwd:
+            return False
+        saved = [t.clone() for t in state]
+        self.f8_bwd = False
+        try:
+            forward()
+            amax = self._dYW[0].detach().abs().amax().float().clamp_min(1e-30).view(1)
+            if ctx is not None and ctx.distributed:
+                ctx.all_reduce_(amax, "max")
+        finally:
+            self.f8_bwd = True
+            for t, c in zip(state, saved):
+                t.copy_(c)
+        sc.set_from_tensor(6, amax)
+        return True
+
     def __call__(self, Yp: torch.Tensor, HL: torch.Tensor, HP: torch.Tensor) -> torch.Tensor:
         """Yp (E,U,B,2,H,W), HL/HP (E,U,B,2048) fp32.  Returns device loss[2] (loss, loss_perf)."""
         loss = self.forward_fc(Yp, HL, HP)

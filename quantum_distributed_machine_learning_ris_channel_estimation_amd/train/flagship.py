@@ -222,6 +222,8 @@ class FlagshipTrainer(DPPlan):
         else:
             mode = "serial"
         self.mode = mode
+        # (experiment, QDML_QSC_ORDER) capture order of the dagq step: qsc_first | hdce_first | own_gather
+        self.qsc_order = os.environ.get("QDML_QSC_ORDER", "qsc_first")
         # the FC weight's Adam in the weight-gradient GEMM's epilogue (world 1: no gradient collective between)
         self.fused_adam = bool((cfg.fused_fc_adam or os.environ.get("QDML_FUSED_ADAM") == "1")
                                and os.environ.get("QDML_FUSED_ADAM") != "0"
@@ -243,8 +245,19 @@ class FlagshipTrainer(DPPlan):
             self._tail_pack_launch(advance=False)   # the first step's images
         self._use_graphs = graphs
         self._phases = None   # (phase_times) per-step dicts of HIP events
+        self._prime_fp8()
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
+
+    def _prime_fp8(self) -> None:
+        """(fp8 estimator) seed the loss gradient's delayed e4m3 scale before the first step
+        (HDCEStep.prime_fp8_dy).  The primed slot is part of mutable_state(), so a capture(preserve=True)
+        restores it primed."""
+        def fwd():
+            self._gather(classifier=False)
+            self._hdce_forward()
+        if self.hstep.prime_fp8_dy(fwd, self.mutable_state() + [self.cur], self.ctx) and self.tail_pack:
+            self._tail_pack_launch(advance=False)   # (the packed conv images of the restored weights)
 
     def _graphs_for(self, k: int):
         """The graph set that runs ``k`` consecutive training steps per replay (world 1; the DP plan is
@@ -350,12 +363,30 @@ class FlagshipTrainer(DPPlan):
 
     def _step_body(self) -> None:
         if self.mode == "dagq":
-            # the QSC branch forks right after the batch gather: its latency-bound kernels share the GPU with
-            # the HDCE chain's, and it joins at the end of the step
-            self._gather()
-            with self._fork(self.streams["qsc"]):
-                self._qsc_branch(with_opt=True)
+            order = self.qsc_order
+            if order == "qsc_first":
+                # the QSC branch forks right after the batch gather: its latency-bound kernels share the GPU with
+                # the HDCE chain's, and it joins at the end of the step
+                self._gather()
+                with self._fork(self.streams["qsc"]):
+                    self._qsc_branch(with_opt=True)
+                self._hdce_graph()
+                self._join(("qsc",))
+                return
+            # HDCE chain captured first (it keeps the gather's queue); the QSC branch forks from an event
+            # recorded right after the HDCE gather.  own_gather: the QSC branch gathers its own half of the batch
+            # (cursor 1) on its queue, so no data crosses the executor's queues inside the step
+            own = order == "own_gather"
+            self._gather(classifier=not own)
+            ev = torch.cuda.Event()
+            ev.record()
             self._hdce_graph()
+            qs = self.streams["qsc"]
+            qs.wait_event(ev)
+            with torch.cuda.stream(qs):
+                if own:
+                    self._gather(hdce=False, classifier=True)
+                self._qsc_branch(with_opt=True)
             self._join(("qsc",))
             return
         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)

@@ -180,6 +180,16 @@ class Y2HRunner:
         return on and ctx.backend == "rccl"
 
     # ------------------------------------------------------------------ HDCE
+    def _sync_bn_buffers(self, model: HDCEModel) -> None:
+        """Every rank takes rank 0's BN running statistics and batch counters before evaluation and
+        checkpointing: DataParallel keeps replica 0's buffers (data_parallel.py:88-90), so the
+        evaluated / saved model is one model, not a per-rank mix.  (Training normalises with batch statistics:
+        the running buffers never feed back into a step.)"""
+        ctx = self._context()
+        if ctx.distributed:
+            for t in model.run_mean + model.run_var + [model._nbt]:
+                ctx.broadcast_(t)
+
     def build_hdce(self) -> HDCEModel:
         ctx = self._context()
         model = HDCEModel(self.Pilot_num, ctx.device, self.dtype, self.n_scenarios)
@@ -257,36 +267,68 @@ class Y2HRunner:
         static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
         gscale = 1.0 if ref else 1.0 / ctx.world
 
-        gathers = {}
+        def part(n: int) -> int:
+            """rows of a global batch of n this rank takes (torch.tensor_split's sizes in reference semantics)"""
+            return n // ctx.world + (1 if ctx.rank < n % ctx.world else 0) if ref else n
 
-        def run(idx):
-            sp.zero_grad()
+        # one step engine + gather per part size, ALL built here, before any capture (an HDCEStep's constructor
+        # synchronises the host): the full batch's part and the partial last batch's (drop_last=False)
+        steps, gathers = {}, {}
+        for n in sorted({B, tr.n % B or B}):
+            b = part(n)
+            if b > 0 and b not in steps:
+                steps[b] = step if b == Bl else HDCEStep(model, U, b, grad_hook=buckets.launch, skip=skip, hip=hip)
+                gathers[b] = StepGather(E, U, b, model.H, model.W, ctx.device, with_classifier=False)
+
+        def forward(idx):
+            """gather + forward + loss of this rank's part of ``idx``; returns (step engine, loss) or None
+            when the part is empty"""
             if ref:
                 den_global[:, 0] = tr.Hlabel.index_select(1, idx).pow(2).sum((1, 2))
                 den_global[:, 1] = tr.Hperf.index_select(1, idx).pow(2).sum((1, 2))
                 idx = self._local_part(idx)
             b = idx.numel()
-            if b not in gathers:
-                gathers[b] = StepGather(E, U, b, model.H, model.W, ctx.device, with_classifier=False)
-            g = gathers[b]
+            if b == 0:
+                return None
+            g, hs = gathers[b], steps[b]
             g(tr, idx)
-            hs = step if b == Bl else HDCEStep(model, U, b, grad_hook=buckets.launch, skip=skip, hip=hip)
             hs.nmse.den_global = den_global
             if rowpow is not None:   # (the one-pass NMSE reads per-row label powers, scaled to global sums)
                 g.rowpow = rowpow
                 o = g.rowoff.long()
                 g.rowden[:, 0] = rowpow[0][o]
                 g.rowden[:, 1] = rowpow[1][o]
-            loss = hs.forward_fc_gathered(g, tr)
-            if hs.grad_hook:
-                hs.grad_hook("fc")
-            hs.backward_conv()
-            if hs.grad_hook:
-                hs.grad_hook("conv")
-            last_loss.copy_(loss)
-            loss_acc.add_(loss)
+            return hs, hs.forward_fc_gathered(g, tr)
+
+        def run(idx):
+            sp.zero_grad()
+            out = forward(idx)
+            if out is None:
+                # a partial last batch smaller than the world: this rank holds no rows, but still takes part
+                # in every collective (zero gradients, a clear NaN flag) and in the optimizer step
+                if skip is not None:
+                    skip.zero_()
+                buckets.launch_all()
+            else:
+                hs, loss = out
+                if hs.grad_hook:
+                    hs.grad_hook("fc")
+                hs.backward_conv()
+                if hs.grad_hook:
+                    hs.grad_hook("conv")
+                last_loss.copy_(loss)
+                loss_acc.add_(loss)
             buckets.wait()
             opt.step(grad_scale=gscale, skip=skip)
+
+        def state():   # every tensor a step mutates
+            return ([sp.flat, opt.m, opt.v, opt.step_t] + model.run_mean + model.run_var + [model._nbt, loss_acc]
+                    + ([model.fc_shadow] if model.fc_shadow is not None else [])
+                    + ([model.fp8_scales.amax, model.fp8_scales.scale, model.fp8_scales.qs]
+                       if model.fp8_scales is not None else []))
+
+        # fp8 estimator: seed the loss gradient's e4m3 scale from a bf16-gradient pass on a first batch
+        step.prime_fp8_dy(lambda: forward(torch.arange(min(B, tr.n), device=ctx.device)), state(), ctx)
 
         graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
         # (reference semantics: one permutation for every rank -- each takes its part of each global batch)
@@ -325,12 +367,7 @@ class Y2HRunner:
                     if graphed.enabled and graphed.graph is None:
                         # (every tensor a step updates: incl. the optimizer-written bf16 FC shadow and
                         # the BN batch counters)
-                        _capture_preserving(graphed, [sp.flat, opt.m, opt.v, opt.step_t] + model.run_mean
-                                            + model.run_var + [model._nbt, loss_acc]
-                                            + ([model.fc_shadow] if model.fc_shadow is not None else [])
-                                            + ([model.fp8_scales.amax, model.fp8_scales.scale, model.fp8_scales.qs]
-                                               if model.fp8_scales is not None else []),
-                                            static_idx, idx)
+                        _capture_preserving(graphed, state(), static_idx, idx)
                     static_idx.copy_(idx)
                     graphed()
                 else:
@@ -348,6 +385,7 @@ class Y2HRunner:
             ctx.all_reduce_(loss_acc)
             tl = (loss_acc / (max(nb, 1) * (1 if ref else ctx.world))).tolist()
             self.train_HDCE_losses.append(tl[0])
+            self._sync_bn_buffers(model)
             nmse, nmse_perf = self.eval_hdce(model, va)
             self.val_HDCE_nmse.append(nmse)
             if ctx.is_main:
@@ -438,6 +476,16 @@ class Y2HRunner:
                 if share != 1.0:
                     cstep.grad_hook = None
             b = idx.numel()
+            if b == 0:
+                # a partial last batch smaller than the world: no rows here, but every collective and the
+                # optimizer step still run in lockstep (zero gradients, a clear NaN flag)
+                if skip is not None:
+                    skip.zero_()
+                cstep.grad_hook = buckets.launch
+                buckets.launch_all()
+                buckets.wait()
+                opt.step(grad_scale=gscale, skip=skip)
+                return
             x = tr.Yp.index_select(1, idx).reshape(S * b, *tr.Yp.shape[2:])
             labels = tr.scen.repeat_interleave(b)
             loss = cstep(x, labels)

@@ -5,7 +5,9 @@ stream; the result must equal a single process training on the whole global batc
 
 Classical SC (BN-free): every parameter after one epoch equals the 1-rank run within fp32 tolerance.
 HDCE: the run completes in lockstep (per-replica BatchNorm, as DataParallel, makes its parameters differ
-from a full-batch BN run by design), with rank-identical parameters."""
+from a full-batch BN run by design), with rank-identical parameters and BN buffers.  At world 3 the global
+batch of 8 splits 3/3/2 and at world 8 the partial last batch (6 rows) leaves two ranks with no rows: both
+must still run every collective in lockstep."""
 import os
 import sys
 
@@ -28,9 +30,11 @@ def main(out):
     ctx = r._context()
     same = True
     if ctx.world > 1:
-        g = [torch.empty_like(h) for _ in range(ctx.world)]
-        dist.all_gather(g, h)
-        same = all(torch.equal(g[0], x) for x in g[1:])
+        # weights AND the BN running buffers (rank 0's, broadcast before evaluation / checkpointing) agree
+        for t in (h, torch.cat(m.run_mean + m.run_var), m._nbt.double()):
+            g = [torch.empty_like(t) for _ in range(ctx.world)]
+            dist.all_gather(g, t)
+            same = same and all(torch.equal(g[0], x) for x in g[1:])
     torch.save({"sc": flat, "hdce_loss": torch.tensor(r.train_HDCE_losses), "sc_loss": torch.tensor(r.train_SC_losses)},
                f"{out}.{ctx.rank}.pt")
     with open(f"{out}.{ctx.rank}", "w") as f:

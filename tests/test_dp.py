@@ -122,7 +122,7 @@ def test_rccl_gpu_check_is_per_node():
             check_local_gpus(local_rank=lr, local_world=lw, n_gpus=8)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_reference_dp_semantics_matches_one_process(tmp_path, world):
     """dp_semantics="reference" (DataParallel's split of one global batch, R:144-148) == one process on the
     whole batch, for the BN-free classical SC; the HDCE trainer runs in lockstep (rank-identical weights)."""
