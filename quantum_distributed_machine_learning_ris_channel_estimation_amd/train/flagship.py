@@ -222,8 +222,6 @@ class FlagshipTrainer(DPPlan):
         else:
             mode = "serial"
         self.mode = mode
-        # (experiment, QDML_QSC_ORDER) capture order of the dagq step: qsc_first | hdce_first | own_gather
-        self.qsc_order = os.environ.get("QDML_QSC_ORDER", "qsc_first")
         # the FC weight's Adam in the weight-gradient GEMM's epilogue (world 1: no gradient collective between)
         self.fused_adam = bool((cfg.fused_fc_adam or os.environ.get("QDML_FUSED_ADAM") == "1")
                                and os.environ.get("QDML_FUSED_ADAM") != "0"
@@ -355,6 +353,10 @@ class FlagshipTrainer(DPPlan):
         """HDCE forward + backward + Adam (world 1): one Adam launch over the whole space, which also packs
         the next step's conv weight images and advances the batch cursor (tail_pack)."""
         self._hdce_forward()
+        self._hdce_backward_update()
+
+    def _hdce_backward_update(self) -> None:
+        """conv/BN backward + the one Adam launch over the whole HDCE space (+ the conv weight images)."""
         self.hstep.backward_conv()
         pk = self._adam_pack()
         self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
@@ -363,30 +365,14 @@ class FlagshipTrainer(DPPlan):
 
     def _step_body(self) -> None:
         if self.mode == "dagq":
-            order = self.qsc_order
-            if order == "qsc_first":
-                # the QSC branch forks right after the batch gather: its latency-bound kernels share the GPU with
-                # the HDCE chain's, and it joins at the end of the step
-                self._gather()
-                with self._fork(self.streams["qsc"]):
-                    self._qsc_branch(with_opt=True)
-                self._hdce_graph()
-                self._join(("qsc",))
-                return
-            # HDCE chain captured first (it keeps the gather's queue); the QSC branch forks from an event
-            # recorded right after the HDCE gather.  own_gather: the QSC branch gathers its own half of the batch
-            # (cursor 1) on its queue, so no data crosses the executor's queues inside the step
-            own = order == "own_gather"
-            self._gather(classifier=not own)
-            ev = torch.cuda.Event()
-            ev.record()
-            self._hdce_graph()
-            qs = self.streams["qsc"]
-            qs.wait_event(ev)
-            with torch.cuda.stream(qs):
-                if own:
-                    self._gather(hdce=False, classifier=True)
+            # the QSC branch forks right after the batch gather: its latency-bound kernels share the GPU with
+            # the HDCE chain's, and it joins at the end of the step.  (Measured alternatives, round 4,
+            # docs/CONCURRENCY.md: the HDCE chain captured first, the QSC branch gathering its own batch, the QSC
+            # step split around the FC GEMMs, the FC update on the QSC stream -- all slower.)
+            self._gather()
+            with self._fork(self.streams["qsc"]):
                 self._qsc_branch(with_opt=True)
+            self._hdce_graph()
             self._join(("qsc",))
             return
         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)
