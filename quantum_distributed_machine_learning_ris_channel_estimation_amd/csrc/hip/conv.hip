@@ -1680,7 +1680,6 @@ struct SlabJobs {
   float* out[kSlabJobs];
   int groups[kSlabJobs], rows[kSlabJobs], width[kSlabJobs], ld[kSlabJobs], vec[kSlabJobs];
   int accumulate;
-  int sr1;   // (A/B, QDML_TAIL_UNR=1) one row per load round
 };
 __device__ __forceinline__ void slab_rows_sum1_body(const float* __restrict__ slab, float* __restrict__ out, int rows,
                                                     int width, int ld, int g, int bx, int accumulate) {
@@ -1709,10 +1708,7 @@ __device__ __forceinline__ void slab_rows_sum1_body(const float* __restrict__ sl
 __global__ void __launch_bounds__(256) slab_rows_sum4_multi_kernel(SlabJobs jobs) {
   const int j = blockIdx.z;
   if (blockIdx.y >= jobs.groups[j] || blockIdx.x * 64 >= jobs.width[j]) return;
-  if (jobs.vec[j] && jobs.sr1)
-    slab_rows_sum4_body<1>(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], jobs.ld[j], blockIdx.y, blockIdx.x,
-                           jobs.accumulate);
-  else if (jobs.vec[j])
+  if (jobs.vec[j])
     slab_rows_sum4_body(jobs.slab[j], jobs.out[j], jobs.rows[j], jobs.width[j], jobs.ld[j], blockIdx.y, blockIdx.x,
                         jobs.accumulate);
   else
@@ -1730,7 +1726,7 @@ __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ sl
   if (i < width) {
     const float* s = slab + (size_t)g * rows * ld + i;
     // rounds of SR rows with every load of a round issued before its adds (same summation order as a
-    // row-at-a-time loop: bit-identical sums); QDML_TAIL_UNR=1 selects one row per round
+    // row-at-a-time loop: bit-identical sums)
     for (int r0 = ty; r0 < rows; r0 += 16 * SR) {
       float4 v[SR];
 #pragma unroll
@@ -2020,14 +2016,11 @@ QD_API int qd_bn_stats_finalize_multi(int n, const float* const* stats, const fl
 QD_API int qd_bn_bwd_reduce(const void* dh, int dh_bf16, const uint16_t* z, const float* st, float* slab, int N, int E,
                             int B, int H, int W, int chunks, int spb, const qd::LossFinish* lf_in, void* stream) {
   const qd::LossFinish lf = (lf_in && lf_in->part) ? *lf_in : qd::LossFinish{};
-  // QDML_TAIL_UNR=1: one row per round trip (the round-2 loop, for A/B; the same knob as the BN tail's)
-  static const bool unr1 = [] { const char* v = getenv("QDML_TAIL_UNR"); return v && atoi(v) == 1; }();
   dim3 grid((N / B) * chunks, E + (lf.part ? 1 : 0));
   hipStream_t s = (hipStream_t)stream;
   if (chunks * spb < B || H * W % 64) return (int)hipErrorInvalidValue;
   if (H * W == 128) {
-    if (dh_bf16 && unr1) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t, 1>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
-    else if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
+    if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
     else hipLaunchKernelGGL((bn_bwd_reduce_kernel<128, float>), grid, dim3(256), 0, s, (const float*)dh, z, st, slab, E, B, chunks, spb, lf);
   } else if (H * W == 256) {
     if (dh_bf16) hipLaunchKernelGGL((bn_bwd_reduce_kernel<256, uint16_t>), grid, dim3(256), 0, s, (const uint16_t*)dh, z, st, slab, E, B, chunks, spb, lf);
@@ -2090,17 +2083,11 @@ QD_API int qd_bn_apply_tail(const uint16_t* z, uint16_t* h, const BnFwd* bnf, co
   if (napply > qd::kAmaxParts) return (int)hipErrorInvalidValue;
   const dim3 grid(napply + nfin);
   hipStream_t s = (hipStream_t)stream;
-  // QDML_TAIL_UNR=1: one load in flight per thread (the round-2 loop, for A/B)
-  static const bool unr1 = [] { const char* v = getenv("QDML_TAIL_UNR"); return v && atoi(v) == 1; }();
 #define QD_TAIL(HWV, U_)                                                                                          \
   hipLaunchKernelGGL((bn_apply_tail_kernel<HWV, U_>), grid, dim3(256), 0, s, z, h, *bnf, jobs, U, E, B, spb, ach, \
                      chunks, training, nbt, n_nbt, nbt_inc, h8, qs, amax)
-  if (HW == 128 && unr1)
-    QD_TAIL(128, 1);
-  else if (HW == 128)
+  if (HW == 128)
     QD_TAIL(128, 4);
-  else if (HW == 256 && unr1)
-    QD_TAIL(256, 1);
   else if (HW == 256)
     QD_TAIL(256, 4);
 #undef QD_TAIL
@@ -2116,8 +2103,6 @@ QD_API int qd_slab_rows_sum_multi(int n, const float* const* slabs, float* const
   if (n < 1 || n > kSlabJobs) return (int)hipErrorInvalidValue;
   SlabJobs jobs{};
   jobs.accumulate = accumulate;
-  static const bool sr1 = [] { const char* v = getenv("QDML_TAIL_UNR"); return v && atoi(v) == 1; }();
-  jobs.sr1 = sr1;
   int gx = 0, gy = 0;
   for (int j = 0; j < n; ++j) {
     jobs.ld[j] = lds ? lds[j] : widths[j];

@@ -296,9 +296,8 @@ QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const fl
   Shadow sh{shadow, shadow_lo, shadow_hi, shadow8, qs, amax};
   // max_grid (0 = 2048): fewer workgroups stream the update more slowly but leave most CUs to
   // kernels running beside it (the FC Adam as a side branch of the step graph)
-  // streaming loads/stores for large ranges (QDML_ADAM_NT=0/1 overrides; measured in scripts/gpu_check.sh adamnt)
-  static const int nt_env = [] { const char* e = getenv("QDML_ADAM_NT"); return e ? atoi(e) : -1; }();
-  const bool nt = nt_env >= 0 ? nt_env != 0 : n - hole_n >= (1L << 20);
+  // streaming loads/stores for large ranges (profiles/r1_17_adam_nt.md)
+  const bool nt = n - hole_n >= (1L << 20);
   const dim3 grid(grid_for(n - hole_n, max_grid > 0 ? max_grid : 2048));
   if (nt)
     hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh,

@@ -800,11 +800,10 @@ QD_API long long qd_qsim_big_workspace(int n, int grid, int backward) {
 
 // Workgroups (= slab rows of the backward) for a batch of B: one sample in flight per workgroup.
 // The cap trades HBM workspace (2 / 4 states of 2^n complex per workgroup: 1 / 2 MiB at n = 16) for
-// occupancy (QDML_QSIM_BIG_GRID); measured at n = 16, B = 2304: 512 / 1152 / 2304 workgroups ->
-// 28.2 / 31.1 / 28.6 ms per flagship step -- not occupancy-bound, so the small workspace stays.
-static int g_big_grid_cap = 512;
-QD_API void qd_qsim_big_set_grid_cap(int cap) { g_big_grid_cap = cap > 0 ? cap : 512; }
-QD_API int qd_qsim_big_grid(int B) { return B < g_big_grid_cap ? B : g_big_grid_cap; }
+// occupancy; measured at n = 16, B = 2304: 512 / 1152 / 2304 workgroups -> 28.2 / 31.1 / 28.6 ms per
+// flagship step -- not occupancy-bound, so the small workspace stays.
+constexpr int kBigGridCap = 512;
+QD_API int qd_qsim_big_grid(int B) { return B < kBigGridCap ? B : kBigGridCap; }
 
 // psave (nullable): (B, 2^n) complex64 buffer keeping every sample's psi_final for qd_qsim_big_bwd.
 QD_API int qd_qsim_big_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,

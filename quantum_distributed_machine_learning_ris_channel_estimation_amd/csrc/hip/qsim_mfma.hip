@@ -364,24 +364,16 @@ QD_API int qd_qsim_mfma_prep_noise(const float* w, float* out, void* ops, int G,
 }
 
 // n = 8 only, 2 <= L <= 8.  psave nullable ((B, 256) complex64, qsim.hip's layout).
-// QDML_QSIM_MFMA_SPW (1 / 2 / 4; default 1: measured 11.1 / 12.5 / 16.6 us at the flagship shape): samples per wave, one group per wave (wgroup % SPW == 0)
+// samples per wave: 1 (measured 11.1 / 12.5 / 16.6 us at the flagship shape for 1 / 2 / 4)
 QD_API int qd_qsim_mfma_fwd(const float* x, const float* w, const void* ops, float* E, int B, int L, int wgroup,
                             void* psave, void* stream) {
   if (B < 1 || L < 2 || L > 8) return (int)hipErrorInvalidValue;
-  static const int spw_env = [] { const char* e = getenv("QDML_QSIM_MFMA_SPW"); return e ? atoi(e) : 1; }();
-  int spw = spw_env == 4 ? 4 : spw_env == 1 ? 1 : 2;
-  while (spw > 1 && wgroup > 0 && wgroup % spw) spw /= 2;
+  constexpr int spw = 1;
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((B + 4 * spw - 1) / (4 * spw));
   const _Float16* o = (const _Float16*)ops;
 #define QM_S(SPW) hipLaunchKernelGGL((fwd_kernel<SPW>), grid, dim3(256), 0, st, x, w, o, E, B, L, wgroup, (cf*)psave);
-  if (spw == 4) {
-    QM_S(4)
-  } else if (spw == 2) {
-    QM_S(2)
-  } else {
-    QM_S(1)
-  }
+  QM_S(1)
 #undef QM_S
   return (int)hipGetLastError();
 }

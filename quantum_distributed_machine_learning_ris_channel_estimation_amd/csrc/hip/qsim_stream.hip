@@ -694,12 +694,8 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     attr = true;
   }
   const dim3 ga(ROWS, B), gb(C::NTILE, B);
-  // bricks per workgroup of the reverse pass A (QDML_QS_BPB: 1, 2, 4; tuning knob)
-  static const int bpb = [] {
-    const char* e = getenv("QDML_QS_BPB");
-    const int v = e ? atoi(e) : 4;
-    return (v == 1 || v == 2 || v == 4) ? v : 4;
-  }();
+  // bricks per workgroup of the reverse pass A (1 / 2 / 4 instantiated; 4 measured fastest)
+  constexpr int bpb = 4;
   const cf* lin = nullptr;
   for (int l = L - 1; l >= 0; --l) {
     cf* lo = ((L - 1 - l) % 2 == 0) ? L1 : L2;

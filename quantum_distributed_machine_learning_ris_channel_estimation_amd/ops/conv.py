@@ -11,12 +11,12 @@ HIP graph.  Gradients are written straight into the model's flat gradient buffer
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import List, Optional
 
 import torch
 
 from .. import _native as nat
+from ..knobs import KNOBS
 from .slabsum import SlabBatch
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
@@ -66,10 +66,8 @@ class ConvStackHIP:
         # layer's BN partials from ONE staging of each sample, spb_f samples per workgroup (5: 468
         # workgroups, two resident per CU, one staging while the other computes; 8 = 288 workgroups
         # left half the CUs with one and measured slower than the side-by-side wd kernel).
-        # QDML_CONV_BWD_FUSED=0: wgrad and dgrad as separate workgroups of the wd kernel.
-        if bwd_fused is None:
-            bwd_fused = os.environ.get("QDML_CONV_BWD_FUSED", "1") != "0"
-        self.bwd_fused = bool(bwd_fused) and dx_bf16
+        # bwd_fused=False: wgrad and dgrad as separate workgroups of the wd kernel (tests compare the two).
+        self.bwd_fused = (True if bwd_fused is None else bool(bwd_fused)) and dx_bf16
         # layer 1 (2 input channels) is one accumulator tile: staging-bound, so more, shorter workgroups
         self.spb_wl = (spb_w1, spb_f, spb_f) if self.bwd_fused else (spb_w1, spb_w, spb_w)
         self.chunks_wl = tuple((B + s - 1) // s for s in self.spb_wl)
@@ -83,14 +81,14 @@ class ConvStackHIP:
         self.h3_8 = torch.empty(N * self.E, 32 * HW, device=dev, dtype=torch.float8_e4m3fn) if self.fp8 else None
         # fp8 estimator: the 32-channel forward convs (layers 2, 3) on e4m3 MFMA (conv3x3_f8_kernel) with
         # delayed per-tensor scales: slots 2..5 = [act2, w2, act3, w3] of the model's Fp8Scales (updated
-        # with the FC's).  Opt-in (QDML_FP8_CONV=1): in the step the e4m3 convs are no faster than the bf16 ones
+        # with the FC's).  Opt-in (knobs.KNOBS.fp8_conv): in the step the e4m3 convs are no faster than the bf16 ones
         # (latency-bound 32-channel layers; the weight quantisation sits in their prologue), so the default fp8
         # estimator runs the FC -- 78 % of the HDCE FLOPs -- in e4m3 (forward, weight and data gradients) and the
         # convs in bf16: 0.402-0.404 vs 0.410-0.413 ms/step with the e4m3 convs, bf16 0.409-0.410
         # (profiles/r3_07_fp8_step_variants.txt).
         f8m = getattr(model, "fp8_scales", None)
         self.f8conv = (self.fp8 and dev.type == "cuda" and f8m is not None and f8m.n >= 6
-                       and os.environ.get("QDML_FP8_CONV", "0") == "1")
+                       and KNOBS.fp8_conv)
         self.f8s, self.f8o = (f8m, 2) if self.f8conv else (None, 0)
         if self.f8conv:
             from .optim import FP8_E4M3_MAX
@@ -133,9 +131,9 @@ class ConvStackHIP:
         self._apply = nat.fn(L, "qd_bn_relu_apply", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p])
         self._apply_tail = nat.fn(L, "qd_bn_apply_tail", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i,
                                                            _i, _p, _i, ctypes.c_longlong, _p, _p, _p, _p])
-        # the BN tail (running statistics) and layer 3's BN/ReLU apply as ONE launch (QDML_BN_APPLY_TAIL=0:
-        # two launches, the tail publishing layer 3's records)
-        self.apply_tail = os.environ.get("QDML_BN_APPLY_TAIL", "1") != "0"
+        # the BN tail (running statistics) and layer 3's BN/ReLU apply as ONE launch (False: two launches, the
+        # tail publishing layer 3's records -- 1 launch more on the chain)
+        self.apply_tail = True
         self.spb_a = 8 if B % 8 == 0 else 1
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
         self._packm2 = nat.fn(L, "qd_conv_pack_weights_multi2", [_i, _p, _p, _p, _p, _i, _p, _i, _p])
@@ -144,8 +142,8 @@ class ConvStackHIP:
         self.pack_at_tail = False
         self._wd = nat.fn(L, "qd_conv_wgrad_dgrad", [_p, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _i,
                                                         _p, _p, _p])
-        # (bwd_fused off) wgrad + dgrad of layers 3 and 2 as one launch each (QDML_CONV_FUSE_WD=0: separate)
-        self.fuse_wd = os.environ.get("QDML_CONV_FUSE_WD", "1") != "0"
+        # (bwd_fused off) wgrad + dgrad of layers 3 and 2 as one launch each
+        self.fuse_wd = True
         self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p])
         self._fwd8 = nat.fn(L, "qd_conv_fwd_f8", [_p] * 4 + [_i] * 7 + [_p] * 6)
 

@@ -20,7 +20,6 @@ In data-parallel runs ``sums()`` + all-reduce + ``finalize()`` give the GLOBAL N
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -51,8 +50,8 @@ class StreamNMSE:
         self.skip = torch.zeros(1, device=dev, dtype=torch.float32)  # NaN guard flag (all-reduced in DP)
         self._rs_long = self.row_stream.long()
         # fused path: rows per block = E * rpc_mult (scripts/probe_nmse.py: 22.7 vs 24.2 us isolated at 4 vs 2;
-        # 0.7 % per step in 2 of 2 rounds, profiles/r2_20_variants.md; QDML_NMSE_RPC_MULT for sweeps)
-        self.rpc_mult = int(os.environ.get("QDML_NMSE_RPC_MULT", "4"))
+        # 0.7 % per step in 2 of 2 rounds, profiles/r2_20_variants.md)
+        self.rpc_mult = 4
         self.rowoff: Optional[torch.Tensor] = None
         # (S, 2) per-stream (label, perf) denominators of the GLOBAL batch, when this rank computes only part
         # of it (data parallelism with the reference's DataParallel semantics): the loss becomes this
@@ -259,8 +258,8 @@ class StreamNMSE:
         assert A.dtype == W.dtype == want and A.is_contiguous() and W.is_contiguous()
         f8cfg = 0
         if f8:
-            # (the e4m3 kernels have the cfg-0 tile; f8 cfg 1 = the MX-scaled MFMA when K allows, QDML_F8_MX=0: off)
-            f8cfg = 1 if (K % 256 == 0 and os.environ.get("QDML_F8_MX", "1") != "0") else 0
+            # (the e4m3 kernels have the cfg-0 tile; f8 cfg 1 = the MX-scaled MFMA when K allows)
+            f8cfg = 1 if K % 256 == 0 else 0
             cfg = 0
         self._check_labels(label)
         if perf is not None:

@@ -19,7 +19,6 @@ backward use it, the grads flow to the clean master.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional
 
 import torch
@@ -27,6 +26,7 @@ import torch
 from .. import _native as nat
 from .slabsum import SlabBatch
 from ..ops.optim import FlatParamSpace
+from ..knobs import KNOBS
 from ..ops.quantum import HIP_REG_MAX_QUBITS, stream_sim_ok
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
@@ -68,9 +68,8 @@ class QSCStepHIP:
             self.grid_fwd = -(-batch_total // wf(self.Ww, 0))      # one sample per wave
             # at most 256 workgroups (grid-stride loop over the samples): the forward runs beside the HDCE
             # conv forward and leaves it more CUs -- 1 % per step over one sample per wave (576 workgroups
-            # at 2304 samples) in 4 of 4 same-box rounds (profiles/r2_20_*); QDML_QSC_GRID_FWD overrides
-            self.grid_fwd = min(self.grid_fwd, int(os.environ.get("QDML_QSC_GRID_FWD", "256")))
-            grid_bwd = int(os.environ.get("QDML_QSC_GRID_BWD", grid_bwd))   # (tuning knob)
+            # at 2304 samples) in 4 of 4 same-box rounds (profiles/r2_20_*)
+            self.grid_fwd = min(self.grid_fwd, 256)
             self.grid_bwd = min(-(-batch_total // wf(self.Ww, 1)), grid_bwd)
             self.p2 = torch.empty(batch_total, feat, **f32)        # pool-2 features (linear weight grad)
             # saved by the forward for the backward: pool-1 map + both pools' argmax choices
@@ -108,19 +107,15 @@ class QSCStepHIP:
             self.qws = torch.empty(nb, dtype=torch.uint8, device=dev)
             # the forward keeps every layer's pass-A output (L - 1 states: the backward's psi, never un-applied)
             sv = nat.fn(L, "qd_qsim_stream_save_bytes", [_i, _i, _i], ctypes.c_longlong)(self.n, batch_total, self.L)
-            self.psave = torch.empty(sv, dtype=torch.uint8, device=dev) \
-                if os.environ.get("QDML_QSIM_SAVE_STATE", "1") != "0" else None
+            self.psave = torch.empty(sv, dtype=torch.uint8, device=dev)
         elif self.big:
-            cap = int(os.environ.get("QDML_QSIM_BIG_GRID", "0"))   # (0: the library default)
-            nat.fn(L, "qd_qsim_big_set_grid_cap", [_i], None)(cap)
             self.qrows = nat.fn(L, "qd_qsim_big_grid", [_i])(batch_total)
             ws = nat.fn(L, "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)
             nb = max(ws(self.n, self.qrows, 0), ws(self.n, self.qrows, 1))
             self.qws = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else None
             # every sample's final state, kept by the forward for the adjoint backward (which then
             # skips re-running the circuit): 2304 x 2^16 x 8 B = 1.2 GB at 16 qubits -- HBM has room
-            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev) \
-                if os.environ.get("QDML_QSIM_SAVE_STATE", "1") != "0" else None
+            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev)
         else:
             self.qrows = nat.fn(L, "qd_qsim_bwd_grid", [_i, _i])(self.n, batch_total)
             self.qws = None
@@ -132,12 +127,11 @@ class QSCStepHIP:
                                                    _i, _p])
         # the preprocess CNN's products on bf16x3 MFMAs (fp32-grade: hi/lo bf16 operands, three products):
         # the forward's conv2 (qd_qsc2_fwd3) and, at P128, the whole backward (qsc2_bwd3_kernel); the f32
-        # MFMA they replace runs at 1/16 of the bf16 rate.  QDML_QSC_F32=1: the f32-MFMA kernels.
+        # MFMA they replace runs at 1/16 of the bf16 rate.
         self._fwd3 = nat.fn(L, "qd_qsc2_fwd3", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p])
         self._bwd3 = nat.fn(L, "qd_qsc2_bwd3", [_p] * 12 + [_i] * 7 + [_p, _p])
-        x3 = os.environ.get("QDML_QSC_F32", "0") == "0"
-        self.fwd_x3 = x3 and (self.Hh, self.Ww) == (16, 8)   # (P256 at 256 VGPRs halves its occupancy)
-        self.bwd_x3 = x3 and (self.Hh, self.Ww) == (16, 8)
+        self.fwd_x3 = (self.Hh, self.Ww) == (16, 8)   # (P256 at 256 VGPRs halves its occupancy)
+        self.bwd_x3 = (self.Hh, self.Ww) == (16, 8)
         # the backward's bf16 hi / lo transposed conv2 weights, written by the bf16x3 forward each step
         self.w2t_img = torch.empty(2 * 9 * 16 * 48, device=self.p2.device, dtype=torch.bfloat16) \
             if (self.bwd_x3 and impl == "mfma") else None
@@ -150,8 +144,7 @@ class QSCStepHIP:
         else:
             # the forward keeps every sample's final state (2^n complex, 4.7 MB at 8 qubits) for the
             # adjoint backward, which then skips re-running the circuit
-            save = os.environ.get("QDML_QSIM_SAVE_STATE", "1") != "0"
-            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev) if save else None
+            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev)
             self._qf = nat.fn(L, "qd_qsim_fwd_save", [_p, _p, _p, _i, _i, _i, _i, _p, _p])
             self._qb = nat.fn(L, "qd_qsim_bwd_saved", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])
         self._rs = nat.fn(L, "qd_reduce_slab", [_p, _p, _i, _i, _f, _p])
@@ -166,9 +159,9 @@ class QSCStepHIP:
         # Kronecker-factored complex products on mfma_f32_16x16x32_f16, fp16 hi/lo split = fp32-grade
         # amplitudes); its per-step operand images are built in the QuantumNAT noise draw's launch
         # (qd_qsim_mfma_prep_noise), so the step has no extra launch.  The adjoint backward reads the final
-        # state it saves (qsim.hip's layout).  QDML_QSIM_MFMA=0: the register forward (qsim.hip).
+        # state it saves (qsim.hip's layout).  knobs.KNOBS.qsim_mfma = False: the register forward (qsim.hip).
         self.mfma = (dev.type == "cuda" and not self.big and self.n == 8 and 2 <= self.L <= 8
-                     and self.psave is not None and os.environ.get("QDML_QSIM_MFMA", "1") != "0")
+                     and self.psave is not None and KNOBS.qsim_mfma)
         if self.mfma:
             halves = nat.fn(L, "qd_qsim_mfma_ops_halves", [_i, _i], ctypes.c_longlong)(max(1, n_groups), self.L)
             self.qops = torch.empty(halves, dtype=torch.float16, device=dev)

@@ -20,7 +20,6 @@ Here three interchangeable backends implement the SAME function:
 from __future__ import annotations
 
 import ctypes
-import os
 import math
 from typing import Optional
 
@@ -38,10 +37,8 @@ HIP_MAX_QUBITS = 16       # workgroup-per-sample kernel above that
 
 def stream_sim_ok(n: int, L: int) -> bool:
     """(n, L) runs on the streamed simulator (csrc/hip/qsim_stream.hip: n = 13..16, L >= 2, one
-    workgroup per (sample, 4096-amplitude brick) per pass); QDML_QSIM_STREAM=0 keeps qsim_big.hip's
-    workgroup-per-sample kernels."""
-    if os.environ.get("QDML_QSIM_STREAM", "1") == "0":
-        return False
+    workgroup per (sample, 4096-amplitude brick) per pass); else qsim_big.hip's workgroup-per-sample
+    kernels run it."""
     return bool(nat.fn(nat.hip_lib(), "qd_qsim_stream_ok", [_i, _i])(n, L))
 
 

@@ -191,10 +191,6 @@ def shutdown() -> None:
     _CTX = None
 
 
-_FOREACH_ALWAYS = os.environ.get("QDML_BUCKET_FOREACH") == "1"   # (A/B: the single multi-tensor scatter-back)
-# (diagnosis of the gloo-on-one-GPU rehearsal, docs/CONCURRENCY.md: a host synchronisation of the waiting
-# stream after every gloo work.wait() -- separates gloo's device-copy completion semantics from our ordering)
-_GLOO_HOST_SYNC = os.environ.get("QDML_GLOO_HOST_SYNC") == "1"
 
 
 class GradBuckets:
@@ -313,8 +309,6 @@ class GradBuckets:
                 torch.cuda.current_stream(self.ctx.device).wait_event(ent[0])
             else:
                 ent[0].wait()
-            if _GLOO_HOST_SYNC and self.ctx.backend == "gloo" and torch.cuda.is_available():
-                torch.cuda.current_stream().synchronize()
             if ent[1] is not None:
                 # every member back from the staging buffer.  Few members: one copy launch each -- the
                 # multi-tensor launch gives each 64K-element chunk ONE workgroup, so the conv gradient
@@ -322,7 +316,7 @@ class GradBuckets:
                 # (profiles/r2_23_dp_one_graph_world1_kernel_stats.md); many members: one launch
                 sizes = [t.numel() for t in ent[2]]
                 parts = list(ent[1][:sum(sizes)].split(sizes))
-                if len(sizes) <= self.FOREACH_MIN and not _FOREACH_ALWAYS:
+                if len(sizes) <= self.FOREACH_MIN:
                     for t, src in zip(ent[2], parts):
                         t.view(-1).copy_(src)
                 else:

@@ -27,7 +27,7 @@ MI355X design implemented here:
 """
 from __future__ import annotations
 
-import os
+
 
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -36,6 +36,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native as nat
+from ..knobs import KNOBS
 from ..models.estimators import Conv_P128, FC_P128, QSC_P128, SC_P128, pilot_grid
 from ..ops.nmse import StreamNMSE
 from ..ops.optim import ALIGN, FlatParamSpace
@@ -289,8 +290,8 @@ class HDCEStep:
         self.bias_via_conv_slabs = False
         self.defer_loss = True   # (with bias_via_conv_slabs) loss finish hosted by the conv backward
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
-        # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; QDML_HAND_GEMM=0: hipBLASLt) and their
-        # tile configurations (forward, wgrad, dgrad; QDML_GEMM_CFG="f,w,d").  Default: all three hand-written --
+        # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; knobs.KNOBS.hand_gemm = "": hipBLASLt) and
+        # their tile configurations (forward, wgrad, dgrad; knobs.KNOBS.gemm_cfg).  Default: all three hand-written --
         #   forward  "fwdplain", cfg 1: 192 x 128 tiles (192 workgroups: ~64 CUs stay free for the concurrent QSC
         #            branch, as hipBLASLt's 234-tile MT128x160 kernel leaves 22), bias-only epilogue, the loss as
         #            the separate one-pass NMSE kernel: 0.4095 / 0.4093 vs 0.4092 / 0.4070 ms with hipBLASLt (same
@@ -299,20 +300,16 @@ class HDCEStep:
         #            QSC backward that then lands on the weight gradient;
         #   wgrad    cfg 1: 128 x 256 tiles, 8 waves;  dgrad  cfg 2: 144 x 256 tiles, 8 waves along N (0.4115 /
         #            0.4116 vs 0.4180 / 0.4161 ms with the hipBLASLt data gradient, r3_02_gemm_variants.txt)
-        hg = os.environ.get("QDML_HAND_GEMM", "fwdplain,wgrad,dgrad").strip()
+        hg = KNOBS.hand_gemm.strip()
         hg = {"1": "fwd,wgrad,dgrad", "all": "fwd,wgrad,dgrad", "0": "", "none": ""}.get(hg, hg)
         self.hand_gemm = set(x for x in hg.split(",") if x) if self.hip else set()
         assert self.hand_gemm <= {"fwd", "fwdplain", "wgrad", "dgrad"}, self.hand_gemm
-        self.gemm_cfg = tuple(int(c) for c in os.environ.get("QDML_GEMM_CFG", "1,1,2").split(","))
-        # fp8 estimator: the FC weight / data gradients in e4m3 as well (see _fc_hand_f8; QDML_F8_BWD=0: bf16)
-        self.f8_bwd = os.environ.get("QDML_F8_BWD", "1") != "0"
+        self.gemm_cfg = tuple(int(c) for c in KNOBS.gemm_cfg.split(","))
+        # fp8 estimator: the FC weight / data gradients in e4m3 as well (see _fc_hand_f8; KNOBS.f8_bwd)
+        self.f8_bwd = KNOBS.f8_bwd
         if self.hip:
             from ..ops.conv import ConvStackHIP
-            # launch knobs (samples per wave / per wgrad workgroup / per BN-reduction workgroup / layer-1
-            # wgrad); QDML_CONV_KNOBS="spw,spb_w,spb_r,spb_w1" overrides them for sweeps
-            kn = os.environ.get("QDML_CONV_KNOBS")
-            kw = dict(zip(("spw", "spb_w", "spb_r", "spb_w1"), map(int, kn.split(",")))) if kn else {}
-            self.conv = ConvStackHIP(model, n_users, batch, **kw)
+            self.conv = ConvStackHIP(model, n_users, batch)
             self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
 
@@ -441,7 +438,7 @@ class HDCEStep:
 
     def _hand_gemm_ok(self, A: torch.Tensor) -> bool:
         """The hand-written FC GEMMs (csrc/hip/gemm.hip) apply: bf16 estimator, labels gathered through
-        rowoff with per-row powers, a shape the kernels tile (QDML_HAND_GEMM=0: hipBLASLt instead)."""
+        rowoff with per-row powers, a shape the kernels tile (knobs.KNOBS.hand_gemm without "fwd": hipBLASLt)."""
         m = self.m
         if not ("fwd" in self.hand_gemm and m.compute_dtype == torch.bfloat16 and not m.fp8 and self.nmse.rowoff is not None
                 and getattr(self, "_rowden", None) is not None):
@@ -491,9 +488,9 @@ class HDCEStep:
     def _hand_f8_ok(self, A: torch.Tensor) -> bool:
         """The fp8 estimator's forward on the hand-written e4m3 GEMM with the loss epilogue
         (qd_gemm_fwd_nmse_f8): e4m3 activations from the conv stack, e4m3 weight shadow from the
-        optimizer, rowoff-gathered labels.  QDML_HAND_FP8=0: hipBLASLt (torch._scaled_mm) + the NMSE kernel."""
+        optimizer, rowoff-gathered labels.  KNOBS.hand_fp8 False: hipBLASLt (torch._scaled_mm) + the NMSE kernel."""
         m = self.m
-        if not (m.fp8 and m.fc_shadow is not None and os.environ.get("QDML_HAND_FP8", "1") != "0"
+        if not (m.fp8 and m.fc_shadow is not None and KNOBS.hand_fp8
                 and self.nmse.rowoff is not None and getattr(self, "_rowden", None) is not None
                 and getattr(self.conv, "h3_8", None) is not None):
             return False
@@ -505,7 +502,7 @@ class HDCEStep:
                 and self.B % 16 == 0 and tm % (16 * m.E) == 0)
 
     def _f8_bwd_ok(self, M: int, N: int, K: int) -> bool:
-        """The FC weight / data gradients in e4m3 too (QDML_F8_BWD=0: bf16): shapes the MX-scaled GEMMs tile
+        """The FC weight / data gradients in e4m3 too (KNOBS.f8_bwd False: bf16): shapes the MX-scaled GEMMs tile
         (dgrad 144 x 128 tiles over K = N, wgrad 128 x 256 tiles over K = M)."""
         return self.f8_bwd and M % 256 == 0 and N % 256 == 0 and K % 256 == 0 and M % 144 == 0
 

@@ -91,6 +91,7 @@ class model_val:
             setattr(self, k, v)
         self.device = resolve_device(cfg.device)
         self.epoch_tag = "epoch99"
+        self.hip_engine = True   # (GPU) the HIP inference engine; False: the models' torch forward
         self.results: Dict[str, List[float]] = {}
 
     def load_model_state_dict(self, model, filepath, fallback_key=None):
@@ -174,8 +175,8 @@ class model_val:
         return out
 
     def _hip_engine(self, sc, qsc, convs, fc):
-        """The HIP inference engine for these models (GPU; None on the CPU, or with QDML_EVAL_TORCH=1)."""
-        if self.device.type != "cuda" or os.environ.get("QDML_EVAL_TORCH") == "1":
+        """The HIP inference engine for these models (GPU; None on the CPU, or with ``hip_engine`` off)."""
+        if self.device.type != "cuda" or not self.hip_engine:
             return None
         # the engine keeps COPIES of the weights: key it on the modules themselves (strong references, so a
         # freed module's id can never be reused by a later model) and on the version counter of every

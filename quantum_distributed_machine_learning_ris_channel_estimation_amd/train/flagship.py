@@ -54,25 +54,6 @@ from .flagship_dp import DPPlan
 
 import os
 
-# hipBLASLt / rocBLAS solution choices for the FC GEMMs, picked on an MI355X by scripts/tune_gemm.py
-# (PyTorch TunableOp); replayed without tuning when present
-TUNABLEOP_FILE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning",
-                              "tunableop_gfx950.csv")
-
-
-def use_tuned_gemms(path: str = TUNABLEOP_FILE) -> bool:
-    """Replay the stored TunableOp GEMM choices (no tuning at run time).  Returns whether enabled."""
-    if not os.path.exists(path):
-        return False
-    tun = torch.cuda.tunable
-    tun.enable(True)
-    tun.tuning_enable(False)
-    tun.record_untuned_enable(False)
-    tun.set_filename(path, insert_device_ordinal=False)
-    tun.read_file(path)
-    return True
-
-
 @dataclass
 class FlagshipConfig:
     pilot_num: int = 128
@@ -95,7 +76,6 @@ class FlagshipConfig:
     #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
     #                              separate (profiles/r3_04_fused_adam.txt) -- 256 one-per-CU workgroups stream
     #                              the Adam state far slower than the 2048-workgroup update kernel
-    #                              (QDML_FUSED_ADAM=1 turns it on)
     dp_plan: str = "zero"        # world > 1: "zero" = ZeRO-1 FC optimizer (reduce-scatter the FC gradient,
     #                              Adam on this rank's 1/world shard, all-gather the bf16 weight shadow) or
     #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
@@ -108,7 +88,6 @@ class FlagshipConfig:
     #                              graph (the 5-graph plan launches the collectives between graph replays and
     #                              pays a graph boundary at each; this one pays one per step but fences the
     #                              FC update at the end of the step instead of overlapping the next gather)
-    tunableop: bool = True       # replay the stored hipBLASLt solution choices (TUNABLEOP_FILE)
     seed: int = 0
     n_scenarios: int = 3
     n_users: int = 3
@@ -119,7 +98,6 @@ class FlagshipTrainer(DPPlan):
         """``store``: share another trainer's HBM-resident dataset (same data_len / pilots / SNR / seed)."""
         self.cfg, self.ctx = cfg, ctx
         dev = ctx.device
-        self.tuned_gemms = dev.type == "cuda" and cfg.tunableop and use_tuned_gemms()
         if store is None:
             store, _ = make_dml_stores(cfg.data_len, cfg.pilot_num, cfg.snr_db, 0.9, dev, data_dir=None, synthetic=True,
                                        base_seed=cfg.seed + 1000 * ctx.rank, n_scenarios=cfg.n_scenarios,
@@ -223,9 +201,7 @@ class FlagshipTrainer(DPPlan):
             mode = "serial"
         self.mode = mode
         # the FC weight's Adam in the weight-gradient GEMM's epilogue (world 1: no gradient collective between)
-        self.fused_adam = bool((cfg.fused_fc_adam or os.environ.get("QDML_FUSED_ADAM") == "1")
-                               and os.environ.get("QDML_FUSED_ADAM") != "0"
-                               and dev.type == "cuda" and ctx.world == 1 and not cfg.split_graphs
+        self.fused_adam = bool(cfg.fused_fc_adam and dev.type == "cuda" and ctx.world == 1 and not cfg.split_graphs
                                and self.hstep.hip and "wgrad" in self.hstep.hand_gemm and not self.hdce.fp8
                                and cfg.dtype == "bf16" and len(self.hopt.bounds) == 1
                                and self.S * self.B % 64 == 0)   # (the hand weight-gradient GEMM's M tiling)
@@ -322,8 +298,8 @@ class FlagshipTrainer(DPPlan):
 
     def _adam_pack(self):
         """(tail_pack) the HDCE update writes the conv weight images and advances the batch cursor
-        itself (QDML_ADAM_PACK=0: a separate pack launch after it)."""
-        if not (self.tail_pack and os.environ.get("QDML_ADAM_PACK", "1") != "0"):
+        itself (no separate pack launch after it)."""
+        if not self.tail_pack:
             return None
         conv, flat, cur = self.hstep.conv, self.hdce.space.flat, self.cur[0, 0:1]
         return lambda lo, hi: conv.pack_scatter(flat, lo, hi, cursor=cur, cursor_inc=self.B)

@@ -29,14 +29,8 @@ for s in $STEPS; do
     bench_fp8) run bench_fp8 600 python bench.py --steps 50 --warmup 10 --dtype fp8 ;;
     bench_c5) run bench_c5 600 python bench.py --steps 10 --warmup 3 --qubits 16 --dtype fp8 ;;
     train) run train 1200 python scripts/train_eval.py --epochs ${EPOCHS:-100} --qubits 6 --qml-qubits 4,8 --out "$OUT/train" ;;
-    q16grid) for g in ${GRIDS:-512 1152 2304}; do QDML_QSIM_BIG_GRID=$g run bench_q16_$g 300 python bench.py --steps 6 --warmup 2 --steps-per-graph 1 --qubits 16 --dtype fp8; done ;;
-    convknobs) for k in ${KNOBS:-2,8,4,4 1,8,4,4 4,8,4,4 2,16,4,4 2,4,4,4 2,8,2,4 2,8,8,4 2,8,4,2 2,8,4,8}; do QDML_CONV_KNOBS=$k run bench_conv_${k//,/_} 300 python bench.py --steps 50 --warmup 10; done ;;
-    savestate) for v in 1 0 1 0; do QDML_QSIM_SAVE_STATE=$v run bench_save_$v 300 python bench.py --steps 100 --warmup 10; done ;;
-    qscgrid) for r in 1 2; do for g in 256 128 64 576; do QDML_QSC_GRID_BWD=$g timeout -k 10 300 python bench.py --steps 200 --warmup 10 > $OUT/cmp.log 2>&1 || exit 1; echo "$g $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/qscgrid.txt; done; done ;;
-    adamnt) for v in 0 1 0 1; do (cd /tmp && export TMPDIR=/tmp && QDML_ADAM_NT=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/adamnt_$v" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 > "$OUT/adamnt_$v.log" 2>&1) || exit 1; python scripts/prof_summary.py "$OUT/adamnt_$v/run_kernel_trace.csv" --tail 0.6 > "$OUT/adamnt_${v}_$RANDOM.md"; rm -rf "$OUT/adamnt_$v"; done ;;
     pmc) for pc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do n=${pc%% *}; (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $pc --output-format csv -d "$OUT/pmc_$n" -o run -- python "$ROOT/bench.py" --steps 10 --warmup 2 --steps-per-graph 1 > "$OUT/pmc_$n.log" 2>&1) || { echo "pmc $pc failed"; tail -5 "$OUT/pmc_$n.log"; exit 1; }; done; python scripts/pmc_summary.py "$OUT"/pmc_* > "$OUT/pmc_summary.md"; rm -rf "$OUT"/pmc_*/ ;;
     variants) IFS=';' read -ra VS <<< "${VARIANTS:-NONE=0|}"; for r in 1 2; do for v in "${VS[@]}"; do env ${v%%|*} timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-300} --warmup 10 ${v#*|} > $OUT/cmp.log 2>&1 || exit 1; echo "$v $(grep -o '"ms_per_step": [0-9.]*' $OUT/cmp.log)" | tee -a $OUT/variants.txt; done; done ;;
-    fusewd) for v in 1 0 1 0; do QDML_CONV_FUSE_WD=$v run bench_fwd_$v 300 python bench.py --steps 100 --warmup 10; mv $OUT/bench_fwd_$v.log $OUT/bench_fwd_${v}_$RANDOM.log; done ;;
     poison) run poison 600 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_lds_poison_gpu.py -m gpu ;;
     pytest_fl) run pytest_fl 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_flagship_gpu.py -m gpu ;;
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
@@ -50,7 +44,6 @@ for s in $STEPS; do
     gemmprobe) run gemmprobe 300 python scripts/probe_gemm.py ;;
     gemmtest) run gemmtest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_gpu.py -m gpu ;;
     nmseprobe) run nmseprobe 300 python scripts/probe_nmse.py ;;
-    tunegemm) run tunegemm 900 python scripts/tune_gemm.py --out "$OUT/tunableop_gfx950.csv" ;;
     diag) run diag 900 python scripts/diag_hdce.py --epochs ${DIAG_EPOCHS:-20} ;;
     gensweep) run gensweep 1500 python scripts/gen_sweep.py --epochs ${SWEEP_EPOCHS:-30} --sc-epochs 8 ;;
   esac

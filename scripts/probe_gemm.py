@@ -11,7 +11,6 @@ import torch  # noqa: E402
 
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import (  # noqa: E402
     gemm_dgrad, gemm_dgrad_f8, gemm_fwd, gemm_fwd_f8, gemm_nt_f8, gemm_wgrad, gemm_wgrad_f8, transpose_u8)
-from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import use_tuned_gemms  # noqa: E402
 
 
 def timeit(fn, iters=30):
@@ -26,7 +25,6 @@ def timeit(fn, iters=30):
 
 
 def main():
-    print("tuned gemms:", use_tuned_gemms())
     dev = torch.device("cuda")
     M, N, K = 2304, 2048, 4096
     A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()

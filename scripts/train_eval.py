@@ -71,7 +71,7 @@ def main():
         mva.test_for_CE_P128_for_all_scenarios()
         t["eval_bn_adapt_s"] = time.time() - t0
     summary = {**{k: round(v, 2) for k, v in t.items()},
-               "eval_engine": "torch" if os.environ.get("QDML_EVAL_TORCH") == "1" else "hip"}
+               "eval_engine": "hip"}
     with open(os.path.join(a.out, "run_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary))

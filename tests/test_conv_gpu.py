@@ -15,6 +15,7 @@ import torch.nn.functional as F
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.conv import ConvStackHIP
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEModel, HDCEStep
 
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
 pytestmark = pytest.mark.gpu
 
 
@@ -121,7 +122,7 @@ def test_conv_f8_forward_matches_quantised_reference(cuda, monkeypatch):
     same e4m3-quantised operands (h = BN+ReLU(z_prev) with the kernel's records, scaled by the delayed
     activation factor; W scaled by the weight factor) -- the kernel's tile swizzle, k order and
     dequantisation -- and the whole fp8 feature stack vs the fp32 model within e4m3 error."""
-    monkeypatch.setenv("QDML_FP8_CONV", "1")   # (opt-in: see ops/conv.py)
+    monkeypatch.setattr(KNOBS, "fp8_conv", True)   # (opt-in: see ops/conv.py)
     U, B = 3, 64
     a, b = pair(cuda)
     a8 = HDCEModel(128, cuda, "fp8")

@@ -7,6 +7,7 @@ import torch
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import (gemm_dgrad, gemm_fwd,
                                                                                   gemm_fwd_ok, gemm_wgrad)
 
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
 pytestmark = pytest.mark.gpu
 
 
@@ -144,7 +145,7 @@ def test_flagship_hand_gemm_matches_hipblaslt_path(cuda, monkeypatch):
     cfg = dict(batch=64, data_len=800, hip_graphs=False, use_quantumnat=False, stream_mode="serial")
     trs = []
     for hand in ("1", "0"):
-        monkeypatch.setenv("QDML_HAND_GEMM", hand)
+        monkeypatch.setattr(KNOBS, "hand_gemm", hand)
         tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
         assert bool(tr.hstep.hand_gemm) == (hand == "1")
         tr.next_batch()
@@ -164,7 +165,7 @@ def test_flagship_hand_gemm_matches_hipblaslt_path(cuda, monkeypatch):
 
 @pytest.mark.parametrize("cfg", ["2,1,2", None])
 def test_flagship_plain_hand_forward_matches_library_forward(cuda, monkeypatch, cfg):
-    """The hand-written FC forward with only the bias in its epilogue (QDML_HAND_GEMM=fwdplain: the loss as the
+    """The hand-written FC forward with only the bias in its epilogue (KNOBS.hand_gemm "fwdplain": the loss as the
     separate one-pass NMSE kernel, as after hipBLASLt) vs the hipBLASLt forward: one flagship step, loss and
     every HDCE gradient to bf16 accuracy."""
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext
@@ -172,14 +173,11 @@ def test_flagship_plain_hand_forward_matches_library_forward(cuda, monkeypatch, 
                                                                                                 FlagshipTrainer)
     ctx = DistContext(device=cuda)
     if cfg is not None:
-        monkeypatch.setenv("QDML_GEMM_CFG", cfg)
+        monkeypatch.setattr(KNOBS, "gemm_cfg", cfg)
     trs = []
     # (hg None: the defaults -- the shipped step runs this forward)
     for hg, path in ((None if cfg is None else "fwdplain,wgrad,dgrad", "hand_plain"), ("wgrad,dgrad", "library")):
-        if hg is None:
-            monkeypatch.delenv("QDML_HAND_GEMM", raising=False)
-        else:
-            monkeypatch.setenv("QDML_HAND_GEMM", hg)
+        monkeypatch.setattr(KNOBS, "hand_gemm", "fwdplain,wgrad,dgrad" if hg is None else hg)
         torch.manual_seed(0)
         tr = FlagshipTrainer(FlagshipConfig(batch=192, data_len=800, hip_graphs=False, use_quantumnat=False,
                                             stream_mode="serial"), ctx)
@@ -236,9 +234,9 @@ def test_flagship_fp8_hand_gemm_matches_scaled_mm_path(cuda, monkeypatch):
     ctx = DistContext(device=cuda)
     cfg = dict(batch=64, data_len=800, hip_graphs=False, use_quantumnat=False, stream_mode="serial", dtype="fp8")
     trs = []
-    monkeypatch.setenv("QDML_F8_BWD", "0")   # (bf16 gradients on both sides; the e4m3 backward: next test)
+    monkeypatch.setattr(KNOBS, "f8_bwd", False)   # (bf16 gradients on both sides; the e4m3 backward: next test)
     for hand in ("1", "0"):
-        monkeypatch.setenv("QDML_HAND_FP8", hand)
+        monkeypatch.setattr(KNOBS, "hand_fp8", hand == "1")
         tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
         tr.next_batch()
         tr._dp_g1()
@@ -288,7 +286,7 @@ def test_flagship_fp8_backward_matches_bf16_backward(cuda, monkeypatch):
     cfg = dict(batch=256, data_len=600, hip_graphs=False, use_quantumnat=False, stream_mode="serial", dtype="fp8")
     trs = {}
     for bwd in ("0", "1"):
-        monkeypatch.setenv("QDML_F8_BWD", bwd)
+        monkeypatch.setattr(KNOBS, "f8_bwd", bwd == "1")
         trs[bwd] = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
     b16, b8 = trs["0"], trs["1"]
     b16.next_batch()

@@ -7,6 +7,7 @@ from quantum_distributed_machine_learning_ris_channel_estimation_amd.models.esti
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.optim import FlatParamSpace
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.qsc import QSCStepHIP
 
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
 pytestmark = pytest.mark.gpu
 
 
@@ -116,7 +117,7 @@ def test_qsc_circuit_forward_on_mfma_matches_register_kernel(cuda, monkeypatch, 
     G, B = 9, 2304
     outs = []
     for mf in ("1", "0"):
-        monkeypatch.setenv("QDML_QSIM_MFMA", mf)
+        monkeypatch.setattr(KNOBS, "qsim_mfma", mf == "1")
         torch.manual_seed(0)
         a = QSC_P128(n_qubits=8, use_quantumnat=noise, use_gradient_pruning=False, pilot_num=128).to(cuda)
         a.train()
