@@ -67,6 +67,16 @@ def main():
         "dgrad_hand2_1x8": lambda: gemm_dgrad(dY, W, out=dA, cfg=2),
         "dgrad_hand3_ks2": lambda: gemm_dgrad(dY, W, out=dA, cfg=3),
     }
+    # cold-cache variants: a 512 MB write evicts L2 and the MALL before the GEMM (the step's FC operands
+    # arrive from HBM: the weight shadow was written a whole step earlier); subtract flush_only
+    flush = torch.empty(128 << 20, device=dev)
+    var["flush_only"] = lambda: flush.zero_()
+    var["fwd_hand1_cold"] = lambda: (flush.zero_(), gemm_fwd(A, W, b, out=Y, cfg=1))
+    var["wgrad_hand1_cold"] = lambda: (flush.zero_(), gemm_wgrad(dY, A, out=dW, cfg=1))
+    var["dgrad_hand2_cold"] = lambda: (flush.zero_(), gemm_dgrad(dY, W, out=dA, cfg=2))
+    if os.environ.get("PROBE_ONLY"):
+        keep = os.environ["PROBE_ONLY"].split(",")
+        var = {k: v for k, v in var.items() if k in keep}
     res = {k: [] for k in var}
     for _ in range(5):
         for k, f in var.items():

@@ -1,0 +1,78 @@
+"""Step-plan experiments without touching the product code: alternative capture structures of the world-1
+dagq step, as subclasses of FlagshipTrainer; prints ms/step for each (same timing contract as bench.py:
+warm-up, capture, settle, then a timed window).  Run under rocprofv3 --kernel-trace with PLAN=<name> to get
+the timeline of one plan.
+
+    python scripts/r4_plan_probe.py [steps]          # PLAN=all (default) or one plan name
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext  # noqa: E402
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (  # noqa: E402
+    FlagshipConfig, FlagshipTrainer)
+
+
+class HdceFirst(FlagshipTrainer):
+    """HDCE chain captured before the QSC branch (the QSC forks from an event after the gather)."""
+
+    def _step_body(self):
+        self._gather()
+        ev = torch.cuda.Event()
+        ev.record()
+        self._hdce_graph()
+        qs = self.streams["qsc"]
+        qs.wait_event(ev)
+        with torch.cuda.stream(qs):
+            self._qsc_branch(with_opt=True)
+        self._join(("qsc",))
+
+
+class JoinFirst(FlagshipTrainer):
+    """As shipped, but the join is issued BEFORE the HDCE chain's last node (the Adam): the next step's
+    gather then depends on the Adam only through the main stream."""
+
+    def _step_body(self):
+        self._gather()
+        with self._fork(self.streams["qsc"]):
+            self._qsc_branch(with_opt=True)
+        self._hdce_forward()
+        self.hstep.backward_conv()
+        self._join(("qsc",))
+        pk = self._adam_pack()
+        self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
+
+
+PLANS = {"shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_first": JoinFirst}
+
+
+def run(cls, steps):
+    ctx = DistContext(device=torch.device("cuda", 0))
+    tr = cls(FlagshipConfig(steps_per_graph=10), ctx)
+    tr.run(20)
+    tr.prepare(steps)
+    tr.run(30)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.run(steps)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3, tr
+
+
+def main(steps):
+    want = os.environ.get("PLAN", "all")
+    names = list(PLANS) if want == "all" else [want]
+    for rnd in range(2 if want == "all" else 1):
+        for n in names:
+            ms, tr = run(PLANS[n], steps)
+            print(f"{n:12s} {ms:.4f} ms/step  loss {tr.hloss.tolist()[0]:.5f}", flush=True)
+            del tr
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 300)
