@@ -757,6 +757,14 @@ using FwdC = Geo<9, 2, 1, 4, KC, KC, 4, 0, 0, 2>;   // fwd 144 x 128, 8 waves (1
 using DgrC = Geo<9, 2, 1, 8, KC, MC, 3>;            // dgrad 144 x 256, 8 waves (1 x 8)
 using DgrD = Geo<9, 4, 1, 4, KC, MC, 3, 0, 0, 2>;   // dgrad 144 x 256, 8 waves (1 x 4 x K2)
 using WgrC = Geo<8, 4, 1, 4, MC, MC, 3, 0, 0, 2>;   // wgrad 128 x 256, 8 waves (1 x 4 x K2)
+// round 4: wave grids that cut the LDS read traffic per K step.  With WM x WN waves over a BM x BN tile a K step
+// reads (WN BM + WM BN) fragment rows from LDS (every wave reads the A rows of its row band and the B rows of its
+// column band), so the 1 x 4 / 1 x 8 / 2 x 4 grids above read A four or eight times; the MFMA work is BM BN.
+// Counters (profiles/r4_08_*): the forward at 30 % MFMA busy, LDS-read bound.
+using FwdD = Geo<3, 8, 4, 1, KC, KC, 3>;            // fwd 192 x 128, 4 waves (4 x 1): A read once, B 4x
+using FwdE = Geo<6, 4, 2, 2, KC, KC, 3>;            // fwd 192 x 128, 4 waves (2 x 2)
+using WgrD = Geo<4, 8, 2, 2, MC, MC, 3>;            // wgrad 128 x 256, 4 waves (2 x 2)
+using DgrE = Geo<9, 4, 2, 2, KC, MC, 3>;            // dgrad 288 x 128, 4 waves (2 x 2): 256 tiles at the flagship shape
 
 }  // namespace gemm
 }  // namespace qd
@@ -764,7 +772,7 @@ using WgrC = Geo<8, 4, 1, 4, MC, MC, 3, 0, 0, 2>;   // wgrad 128 x 256, 8 waves 
 using namespace qd::gemm;
 
 // Which forward config applies to (M, N, K): 1 + cfg, or 0 (unsupported)
-QD_API int qd_gemm_tile_m(int cfg) { return cfg == 1 ? FwdB::BM : FwdA::BM; }
+QD_API int qd_gemm_tile_m(int cfg) { return (cfg == 1 || cfg == 3 || cfg == 4) ? FwdB::BM : FwdA::BM; }
 
 QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (K % BK || N % 128) return 0;
@@ -772,6 +780,7 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (cfg == 0) return M % FwdA::BM == 0;
   if (cfg == 2) return M % FwdC::BM == 0 && K % (2 * BK) == 0;
   if (cfg == 1) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
+  if (cfg == 3 || cfg == 4) return M % FwdD::BM == 0 && N % FwdD::BN == 0;
   return 0;
 }
 
@@ -783,6 +792,8 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   Args a{A, W, K, K, M, N, K, Y, N, bias, {}, expert, E, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
+  if (cfg == 3) return launch<FwdD, EPI_BF16, 1, 4>(a, st);
+  if (cfg == 4) return launch<FwdE, EPI_BF16, 1, 4>(a, st);
   if (M % FwdA::BM) return (int)hipErrorInvalidValue;
   if (cfg == 2) return launch<FwdC, EPI_BF16, 4, 8>(a, st);
   if (cfg == 101) return launch<Geo<9, 2, 1, 4, KC, KC, 4, 1>, EPI_BF16, 4, 8>(a, st);   // (diagnosis builds)
@@ -802,11 +813,32 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
               loss_scale};
   Args a{A, W, K, K, M, N, K, nullptr, N, bias, na, nullptr, 0, nullptr};
   hipStream_t st = (hipStream_t)stream;
-  const int bm = cfg == 1 ? FwdB::BM : FwdA::BM;
+  const int bm = qd_gemm_tile_m(cfg);
   if (M % bm || (bm / (B * E) + 2) * E > 64 || B % 16 || bm % (16 * E)) return (int)hipErrorInvalidValue;
   if (cfg == 1) return launch<FwdB, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 3) return launch<FwdD, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 4) return launch<FwdE, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 2) return launch<FwdC, EPI_NMSE, 4, 8>(a, st);
   return launch<FwdA, EPI_NMSE, 4, 8>(a, st);
+}
+
+// does the cfg tile this shape?  (I, J, K) of the kernel = (N, K, M) for wgrad and (M, K, N) for dgrad
+template <class G>
+static int tiles_ok(int I, int J, int K) {
+  return I % G::BM == 0 && J % G::BN == 0 && K % BK == 0 && K >= BK && (!G::STEP_LOOP || (K / BK) % 2 == 0);
+}
+QD_API int qd_gemm_wgrad_ok(int M, int N, int K, int cfg) {
+  if (cfg == 1) return tiles_ok<WgrB>(N, K, M);
+  if (cfg == 2) return tiles_ok<WgrC>(N, K, M);
+  if (cfg == 3) return tiles_ok<WgrD>(N, K, M);
+  return tiles_ok<WgrA>(N, K, M);
+}
+QD_API int qd_gemm_dgrad_ok(int M, int N, int K, int cfg) {
+  if (cfg == 1) return tiles_ok<DgrB>(M, K, N);
+  if (cfg == 2) return tiles_ok<DgrC>(M, K, N);
+  if (cfg == 3) return tiles_ok<DgrD>(M, K, N);
+  if (cfg == 4) return tiles_ok<DgrE>(M, K, N);
+  return tiles_ok<DgrA>(M, K, N);
 }
 
 // dW (N, K) fp32 = dY^T A: dY (M, N) bf16, A (M, K) bf16 row-major; reduction over M
@@ -816,6 +848,7 @@ QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<WgrB, EPI_F32, 2, 8>(a, st);
   if (cfg == 2) return launch<WgrC, EPI_F32, 2, 8>(a, st);
+  if (cfg == 3) return launch<WgrD, EPI_F32, 2, 8>(a, st);
   return launch<WgrA, EPI_F32, 2, 8>(a, st);
 }
 
@@ -841,6 +874,7 @@ QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, in
   if (cfg == 1) return launch<DgrB, EPI_BF16, 4, 8>(a, st);
   if (cfg == 2) return launch<DgrC, EPI_BF16, 4, 4>(a, st);
   if (cfg == 3) return launch<DgrD, EPI_BF16, 4, 4>(a, st);
+  if (cfg == 4) return launch<DgrE, EPI_BF16, 2, 4>(a, st);
   return launch<DgrA, EPI_BF16, 4, 4>(a, st);
 }
 

@@ -25,6 +25,16 @@ def gemm_fwd_ok(M: int, N: int, K: int, cfg: int = 0) -> bool:
     return bool(_gemm_fn("qd_gemm_fwd_ok", [_i, _i, _i, _i])(M, N, K, cfg))
 
 
+def gemm_wgrad_ok(M: int, N: int, K: int, cfg: int = 0) -> bool:
+    """dW (N, K) = dY (M, N)^T A (M, K): does tile configuration ``cfg`` cover this shape?"""
+    return bool(_gemm_fn("qd_gemm_wgrad_ok", [_i, _i, _i, _i])(M, N, K, cfg))
+
+
+def gemm_dgrad_ok(M: int, N: int, K: int, cfg: int = 0) -> bool:
+    """dA (M, K) = dY (M, N) W (N, K): does tile configuration ``cfg`` cover this shape?"""
+    return bool(_gemm_fn("qd_gemm_dgrad_ok", [_i, _i, _i, _i])(M, N, K, cfg))
+
+
 def gemm_tile_m(cfg: int = 0) -> int:
     return int(_gemm_fn("qd_gemm_tile_m", [_i])(cfg))
 

@@ -607,8 +607,9 @@ class HDCEStep:
         tiled shape, else hipBLASLt."""
         from ..ops.fc import gemm_wgrad
         m = self.m
-        hand = ("wgrad" in self.hand_gemm and dY.dtype == A.dtype == torch.bfloat16 and dY.shape[0] % 64 == 0
-                and dY.shape[1] % 128 == 0 and A.shape[1] % 256 == 0)
+        from ..ops.fc import gemm_wgrad_ok
+        hand = ("wgrad" in self.hand_gemm and dY.dtype == A.dtype == torch.bfloat16
+                and gemm_wgrad_ok(dY.shape[0], dY.shape[1], A.shape[1], self.gemm_cfg[1]))
 
         fa = self.fused_adam
         if fa is not None and not hand:
@@ -641,8 +642,9 @@ class HDCEStep:
             if self.stage_hook is not None:
                 self.stage_hook("dgrad")
             return
+        from ..ops.fc import gemm_dgrad_ok
         if "dgrad" in self.hand_gemm and dY.dtype == torch.bfloat16 and W.dtype == torch.bfloat16 \
-                and dY.shape[0] % 144 == 0 and W.shape[1] % 256 == 0 and W.shape[0] % 64 == 0:
+                and gemm_dgrad_ok(dY.shape[0], W.shape[0], W.shape[1], self.gemm_cfg[2]):
             if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
                 self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)
             self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
@@ -707,9 +709,14 @@ class ClassifierStep:
         self.is_sc = isinstance(model, SC_P128)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """Inference log-probabilities.  GPU: the HIP kernels (the SC's fused forward; for the QSC the
+        preprocess CNN + the circuit on the clean master weights + the inference head,
+        QSCStepHIP.infer) in chunks of the step's static batch; else the models' torch forward."""
         m = self.model
         if self.is_sc and self.hip is not None:
             return self.hip.forward(x)
+        if self.hip is not None and getattr(self.hip, "impl", None) == "mfma" and not m.training:
+            return self._infer_hip(x)
         if isinstance(m, QSC_P128) and m.use_quantum:
             angles = m.preprocess(x)
             w = m.qlayer.weights
@@ -719,6 +726,27 @@ class ClassifierStep:
             xq = m.qlayer(angles, w)
             return F.log_softmax(m.classifier(xq), dim=1)
         return m(x)
+
+    @torch.no_grad()
+    def _infer_hip(self, x: torch.Tensor) -> torch.Tensor:
+        """(QSC, GPU) log-probabilities of any number of samples through QSCStepHIP.infer, which runs exactly
+        its static batch: chunks of that size, the last one padded by repeating its final sample."""
+        h = self.hip
+        Bs = h.B
+        x = x.contiguous().float()
+        N = x.shape[0]
+        if getattr(self, "_xin", None) is None:
+            self._xin = torch.empty((Bs,) + tuple(x.shape[1:]), device=x.device)
+            self._logp = torch.empty(Bs, h.C, device=x.device)
+        out = torch.empty(N, h.C, device=x.device)
+        for lo in range(0, N, Bs):
+            n = min(Bs, N - lo)
+            self._xin[:n].copy_(x[lo:lo + n])
+            if n < Bs:
+                self._xin[n:].copy_(x[lo + n - 1:lo + n].expand(Bs - n, *x.shape[1:]))
+            h.infer(self._xin, None, self._logp)
+            out[lo:lo + n].copy_(self._logp[:n])
+        return out
 
     def forward_part(self, x: torch.Tensor, labels: torch.Tensor) -> None:
         """(HIP path) the step's forward half: loss, NaN flag, head grads (see QSCStepHIP.forward_part)."""

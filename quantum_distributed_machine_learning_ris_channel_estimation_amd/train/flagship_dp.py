@@ -89,6 +89,7 @@ class DPPlan:
             lo, hi = self.fc_region
             self.buckets.launch_all_gather("master", self.hdce.space.flat[lo:hi])
             self.buckets.wait(("master",))
+            self.buckets.pending.pop("master")   # (waited for by its only consumer: nothing stays in flight)
 
     def _mark(self, name: str, stream=None) -> None:
         """(phase timing) a HIP event on ``stream`` (default: current) under ``name``."""

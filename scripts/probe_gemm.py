@@ -55,17 +55,21 @@ def main():
         "fwd_hand0": lambda: gemm_fwd(A, W, b, out=Y, cfg=0),
         "fwd_hand1": lambda: gemm_fwd(A, W, b, out=Y, cfg=1),
         "fwd_hand2_ks2": lambda: gemm_fwd(A, W, b, out=Y, cfg=2),
+        "fwd_hand3_4x1": lambda: gemm_fwd(A, W, b, out=Y, cfg=3),
+        "fwd_hand4_2x2": lambda: gemm_fwd(A, W, b, out=Y, cfg=4),
         "fwd_hand0_noload": lambda: gemm_fwd(A, W, b, out=Y, cfg=101),
         "fwd_hand0_nomfma": lambda: gemm_fwd(A, W, b, out=Y, cfg=102),
         "wgrad_hipblaslt": lambda: torch.mm(dY.t(), A, out_dtype=torch.float32, out=dW),
         "wgrad_hand0": lambda: gemm_wgrad(dY, A, out=dW, cfg=0),
         "wgrad_hand1": lambda: gemm_wgrad(dY, A, out=dW, cfg=1),
         "wgrad_hand2_ks2": lambda: gemm_wgrad(dY, A, out=dW, cfg=2),
+        "wgrad_hand3_2x2": lambda: gemm_wgrad(dY, A, out=dW, cfg=3),
         "dgrad_hipblaslt": lambda: torch.mm(dY, W, out=dA),
         "dgrad_hand0": lambda: gemm_dgrad(dY, W, out=dA, cfg=0),
         "dgrad_hand1": lambda: gemm_dgrad(dY, W, out=dA, cfg=1),
         "dgrad_hand2_1x8": lambda: gemm_dgrad(dY, W, out=dA, cfg=2),
         "dgrad_hand3_ks2": lambda: gemm_dgrad(dY, W, out=dA, cfg=3),
+        "dgrad_hand4_288": lambda: gemm_dgrad(dY, W, out=dA, cfg=4),
     }
     # cold-cache variants: a 512 MB write evicts L2 and the MALL before the GEMM (the step's FC operands
     # arrive from HBM: the weight shadow was written a whole step earlier); subtract flush_only

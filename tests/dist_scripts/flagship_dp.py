@@ -20,6 +20,7 @@ from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flags
 
 def flat_all(tr):
     tr.sync_master()   # (ZeRO plan: each rank's fp32 FC master is current on its own shard only)
+    tr.buckets.assert_quiescent()   # (nothing left in flight: a later graph capture would refuse to start)
     ts = [tr.hdce.space.flat, tr.qspace.flat]
     if tr.hdce.fc_shadow is not None:   # the bf16 weights the forward reads
         ts.append(tr.hdce.fc_shadow.float())

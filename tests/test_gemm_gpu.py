@@ -15,7 +15,7 @@ def _rel(a, b):
     return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K", [(576, 256, 192), (576, 256, 256), (2304, 2048, 4096)])
 def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     if not gemm_fwd_ok(M, N, K, cfg):
@@ -37,7 +37,7 @@ def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     assert float(Y2[:, :5].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(192, 256, 512), (256, 256, 512), (2304, 2048, 4096)])
 def test_gemm_wgrad_matches_fp32(cuda, cfg, M, N, K):
     if cfg == 2 and M % 128:
@@ -60,7 +60,7 @@ def test_gemm_wgrad_matches_fp32(cuda, cfg, M, N, K):
     assert float(dW2[4:N - 1].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K", [(288, 192, 256), (288, 256, 256), (2304, 2048, 4096)])
 def test_gemm_dgrad_matches_fp32(cuda, cfg, M, N, K):
     if cfg in (0, 2, 3) and K % 256:

@@ -140,3 +140,24 @@ def test_qsc_circuit_forward_on_mfma_matches_register_kernel(cuda, monkeypatch, 
         assert torch.allclose(la, lb, rtol=1e-5, atol=1e-6), (la, lb)
         assert float((ea - eb).abs().max()) < 2e-5
         assert float((ga - gb).abs().max()) <= 1e-4 * float(gb.abs().max())
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_classifier_validation_runs_on_hip_kernels(cuda, n):
+    """The runner's QSC validation (ClassifierStep.forward in eval mode) runs the HIP inference kernels
+    (QSCStepHIP.infer: preprocess CNN, circuit on the clean weights, inference head) in chunks of the static
+    batch -- the last one padded -- and matches the models' torch forward (reference R:378-414)."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import ClassifierStep
+    torch.manual_seed(3)
+    m = QSC_P128(n_qubits=n, use_quantumnat=True, use_gradient_pruning=False, pilot_num=128).to(cuda)
+    space = FlatParamSpace(list(m.named_parameters()), cuda)
+    cs = ClassifierStep(m, 9, space=space, batch_total=9 * 32)
+    assert cs.hip is not None and cs.hip.impl == "mfma"
+    x = torch.randn(9 * 32 * 2 + 50, 2, 16, 8, device=cuda)      # two full chunks + a partial one
+    m.eval()
+    got = cs.forward(x)
+    ref = F.log_softmax(m.classifier(m.qlayer(m.preprocess(x))), dim=1)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    assert float((got - ref).abs().max()) < 2e-4, float((got - ref).abs().max())
+    assert torch.equal(got.argmax(1), ref.argmax(1))
