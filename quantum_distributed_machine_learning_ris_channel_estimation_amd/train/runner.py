@@ -240,10 +240,16 @@ class Y2HRunner:
         tr, va = self.device_stores()
         model = self.build_hdce()
         opt = make_optimizer(model.space, self.optimizer, self.lr)
-        model.attach_fc_shadow(opt)
         E, U, B = self.n_scenarios, self.n_users, self.batch_size_DML
         sp = model.space
         n_conv = sp.offsets[sp.names.index("CE.FC.weight")]
+        # N > 1: the update split at the conv / FC boundary (the flagship DP plan's split): the FC part steps as
+        # soon as its all-reduce -- launched before the conv backward, hidden behind it -- has landed, beside
+        # the conv bucket's all-reduce; elementwise, so the split changes no value
+        split = ctx.distributed
+        if split:
+            opt.partition([n_conv])
+        model.attach_fc_shadow(opt)
         if self.hdce_engine not in ("hip", "torch"):
             raise ValueError(f"hdce_engine {self.hdce_engine!r}")
         hip = None if self.hdce_engine == "hip" else False
@@ -260,8 +266,18 @@ class Y2HRunner:
         if ctx.device.type == "cuda" and step.hip:
             rowpow = (step.nmse._row_powers(tr.Hlabel), step.nmse._row_powers(tr.Hperf))
         # the NaN-guard flag rides in the conv bucket: all ranks skip (or step) together
-        buckets = GradBuckets(ctx, {"fc": [sp.grad[n_conv:]], "conv": [sp.grad[:n_conv]] + ([skip] if skip is not None else [])})
-        step.grad_hook = buckets.launch
+        # the NaN-guard flag (final once the loss pass ends) travels in its own bucket right before the FC one,
+        # so every rank skips -- or steps -- together, and the FC update need not wait for the conv bucket
+        bk = {"fc": [sp.grad[n_conv:]], "conv": [sp.grad[:n_conv]]}
+        if skip is not None:
+            bk["skip"] = [skip]
+        buckets = GradBuckets(ctx, bk)
+
+        def grad_hook(name: str) -> None:
+            if name == "fc":
+                buckets.launch("skip")
+            buckets.launch(name)
+        step.grad_hook = grad_hook
         loss_acc = torch.zeros(2, device=ctx.device)
         last_loss = torch.zeros(2, device=ctx.device)
         static_idx = torch.zeros(B, dtype=torch.long, device=ctx.device)
@@ -277,7 +293,7 @@ class Y2HRunner:
         for n in sorted({B, tr.n % B or B}):
             b = part(n)
             if b > 0 and b not in steps:
-                steps[b] = step if b == Bl else HDCEStep(model, U, b, grad_hook=buckets.launch, skip=skip, hip=hip)
+                steps[b] = step if b == Bl else HDCEStep(model, U, b, grad_hook=grad_hook, skip=skip, hip=hip)
                 gathers[b] = StepGather(E, U, b, model.H, model.W, ctx.device, with_classifier=False)
 
         def forward(idx):
@@ -308,7 +324,8 @@ class Y2HRunner:
                 # in every collective (zero gradients, a clear NaN flag) and in the optimizer step
                 if skip is not None:
                     skip.zero_()
-                buckets.launch_all()
+                grad_hook("fc")      # (the same collective order as every other rank)
+                grad_hook("conv")
             else:
                 hs, loss = out
                 if hs.grad_hook:
@@ -318,8 +335,15 @@ class Y2HRunner:
                     hs.grad_hook("conv")
                 last_loss.copy_(loss)
                 loss_acc.add_(loss)
-            buckets.wait()
-            opt.step(grad_scale=gscale, skip=skip)
+            if split:
+                buckets.wait(("skip", "fc"))
+                opt.step(grad_scale=gscale, skip=skip, part=1)
+                buckets.wait(("conv",))
+                opt.step(grad_scale=gscale, skip=skip, part=0)
+                buckets.pending.clear()
+            else:
+                buckets.wait()
+                opt.step(grad_scale=gscale, skip=skip)
 
         def state():   # every tensor a step mutates
             return ([sp.flat, opt.m, opt.v, opt.step_t] + model.run_mean + model.run_var + [model._nbt, loss_acc]
