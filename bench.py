@@ -79,6 +79,8 @@ def main() -> int:
                     help="untimed steps replayed right before the timed region, after the warm-up and the graph "
                          "capture (rounded up to whole graph replays): the first replays of a fresh graph run "
                          "slower (profiles/r3_01_window.txt); reported in the JSON line")
+    ap.add_argument("--spread-windows", type=int, default=8,
+                    help="extra event-timed windows after the timed region (step_spread in the JSON line); 0 = off")
     ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dagq"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, or the QSC branch "
                          "forked off the HDCE chain")
@@ -188,6 +190,27 @@ def main() -> int:
     settle = (max(0, args.settle_steps) + k - 1) // k * k
     elapsed, host = timed(tr, args.steps, settle)
 
+    # spread: after the timed window, 8 more windows of `steps_per_graph` steps each timed with HIP events (no
+    # host sync inside a window; the max over ranks per window) -- the run-to-run spread the single timed window
+    # cannot show
+    spread = None
+    if ctx.device.type == "cuda" and args.spread_windows > 0:
+        k = tr._k()
+        evs = []
+        for _ in range(args.spread_windows):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            tr.run(k)
+            b.record()
+            evs.append((a, b))
+        sync()
+        per = [x.elapsed_time(y) / k for x, y in evs]
+        per = ctx.max_vector(per)
+        srt = sorted(per)
+        spread = {"windows": len(per), "steps_per_window": k, "min_ms": round(srt[0], 4),
+                  "median_ms": round(srt[len(srt) // 2], 4), "max_ms": round(srt[-1], 4)}
+    hbm_peak = torch.cuda.max_memory_allocated(ctx.device) / 2 ** 30 if ctx.device.type == "cuda" else None
+
     hl = tr.hloss.tolist()
     ql = float(tr.qloss.item())
     n = ctx.world
@@ -243,6 +266,10 @@ def main() -> int:
                 "qsim_mfma_forward": bool(getattr(getattr(tr.cstep, "hip", None), "mfma", False)),
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
+            "step_spread": spread,
+            # (torch's caching allocator: everything the run allocated on this GPU -- dataset, weights, optimizer
+            # state, activations, graph pools -- out of 288 GB of HBM3E)
+            "hbm_peak_gib": round(hbm_peak, 3) if hbm_peak is not None else None,
         }
         if dp:
             rec["phases_ms"] = phases
