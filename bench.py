@@ -79,6 +79,8 @@ def main() -> int:
                     help="untimed steps replayed right before the timed region, after the warm-up and the graph "
                          "capture (rounded up to whole graph replays): the first replays of a fresh graph run "
                          "slower (profiles/r3_01_window.txt); reported in the JSON line")
+    ap.add_argument("--gemm-cfg", default=None,
+                    help="FC GEMM tile configurations 'fwd,wgrad,dgrad' (knobs.KNOBS.gemm_cfg; default: the shipped ones)")
     ap.add_argument("--spread-windows", type=int, default=8,
                     help="extra event-timed windows after the timed region (step_spread in the JSON line); 0 = off")
     ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dagq"],
@@ -120,6 +122,9 @@ def main() -> int:
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
                                                                                                 FlagshipTrainer)
 
+    if args.gemm_cfg:
+        from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
+        KNOBS.gemm_cfg = args.gemm_cfg
     ctx = init_distributed("auto", timeout_s=int(os.environ.get("QDML_PG_TIMEOUT", "600")))
     if ctx.world != args.gpus:
         print(f"error: --gpus {args.gpus} but the process group has {ctx.world} rank(s)", file=sys.stderr)
@@ -263,6 +268,7 @@ def main() -> int:
                 # FC gradients, the 8-qubit circuit forward on the matrix cores
                 "fc_forward": getattr(tr.hstep, "fc_path", None),
                 "fc_grad_gemms": sorted(tr.hstep.hand_gemm & {"wgrad", "dgrad"}) if tr.hstep.hip else None,
+                "fc_gemm_cfg": list(tr.hstep.gemm_cfg) if tr.hstep.hip else None,
                 "qsim_mfma_forward": bool(getattr(getattr(tr.cstep, "hip", None), "mfma", False)),
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
