@@ -57,7 +57,10 @@ typedef __attribute__((ext_vector_type(8))) int v8i;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
-enum { KC = 0, MC = 1, MC8 = 2 };
+// KCD: k-contiguous like KC, but read by each wave straight from global memory into its MFMA registers (no LDS
+// stage): with a WM x 1 wave grid every A row belongs to exactly one wave, so staging A through LDS only
+// costs LDS bandwidth (round 4, see the DA configurations below)
+enum { KC = 0, MC = 1, MC8 = 2, KCD = 3 };
 enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2, EPI_ADAM = 3 };
 constexpr int BK = 64;
 
@@ -129,15 +132,18 @@ struct Geo {
   static_assert(KS == 1 || KS == 2, "KS");
   static_assert(F8 != 2 || KS == 1, "MX fragments already span the K step");
   static constexpr bool MX = F8 == 2;
+  static constexpr bool ADIR = LA == KCD;   // A fragments direct from global memory (see KCD)
+  static_assert(!ADIR || (WN == 1 && F8 == 0 && KS == 1 && NSTAGE == 3 && (LB == KC || LB == MC)),
+                "direct A: one wave column, bf16, a 3-stage B ring");
   static constexpr bool STEP_LOOP = KS == 2 || MX;   // one fragment set per K step (see gemm_kernel)
   static constexpr int NW = WM * WN * KS, NT = 64 * NW;
   static constexpr int BM = 16 * MF * WM, BN = 16 * NJ * WN;
-  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_BYTES = ADIR ? 0 : BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   static constexpr int PA = A_BYTES / 1024, PB = B_BYTES / 1024, P = PA + PB;   // 1-KiB pieces per tile
   static constexpr int NPER = (P + NW - 1) / NW;      // pieces each wave issues per tile
   static constexpr int PITCH = BN + 4;               // fp32 epilogue tile row pitch
   static constexpr int LDS = (NSTAGE * STAGE > BM * PITCH * 4 + 8192) ? NSTAGE * STAGE : BM * PITCH * 4 + 8192;
-  static_assert(LA == KC || BM % 128 == 0, "MC operand tiles are whole 128-column panels");
+  static_assert(LA == KC || LA == KCD || BM % 128 == 0, "MC operand tiles are whole 128-column panels");
   static_assert(LB == KC || BN % 128 == 0, "MC operand tiles are whole 128-column panels");
   static_assert(BN % 128 == 0, "epilogue rows are 2 or 4 columns per lane");
   static_assert(LDS <= 160 * 1024, "LDS");
@@ -369,6 +375,12 @@ struct Stager {
       src[it] += adv[it];
     }
   }
+  // K tile `tile` (from the tile-0 pointers init() left in src; issue() must not have run)
+  __device__ __forceinline__ void issue_tile(char* st, int tile) {
+#pragma unroll
+    for (int it = 0; it < G::NPER; ++it)
+      __builtin_amdgcn_global_load_lds((glb_void*)(src[it] + (size_t)tile * adv[it]), (lds_void*)(st + dst[it]), 16, 0, 0);
+  }
 };
 
 struct Args {
@@ -386,6 +398,91 @@ struct Args {
   AdamEpi ad;           // EPI_ADAM
   const float* deq2;    // nullable: with deq, the scales are deq[0] and deq2[0] (two separate scale slots)
 };
+
+// Direct-A K loop (G::ADIR): B through the 3-stage global_load_lds ring as in the staged loop, A straight into
+// registers: wave wm owns A rows wm * 16 MF .. (its MF fragments); fragment f of sub-step s of K step t is lane
+// (fr, fq)'s 16 bytes A[row(f) * lda + 64 t + 32 s + 8 fq] (the KC LDS image's fragment, read from memory).
+// A is loaded two K steps ahead into a 2-slot register ring; the K loop is unrolled by two so the slot is a
+// compile-time index.  Per K step t (stage t % 3 holds B tile t):
+//   MFMAs of sub-step 0 (B fragments read one phase earlier) with sub-step 1's B reads issued first;
+//   wait for B tile t + 1 + barrier; refill the stage tile t - 1 used with tile t + 2; read tile t + 1's
+//   sub-step-0 B fragments; MFMAs of sub-step 1; load A of step t + 2 into the slot just consumed.
+// Every step issues the same memory operations -- past the last tile the loads repeat tile nk - 1 into a stage /
+// slot nobody reads again -- so the loop body is branch-free and the compiler's vmcnt bookkeeping for the
+// register loads stays exact (a data-dependent load count made it drain the memory queue every iteration); the
+// B stage wait is an explicit vmcnt (a tile's pieces are followed by one step's A loads).  LDS reads are inline
+// asm with explicit lgkmcnt waits, as in Readers::mma_read.
+// (inline asm: the compiler's own vmcnt bookkeeping for loop-carried register loads drained the whole memory queue
+// at the top of every iteration; da_loop's waits are exact because every step issues the same loads)
+template <int SL, int MF>
+__device__ __forceinline__ void da_load_a(bf16x8 (&ar)[2][2][MF], const uint16_t* const (&arow)[MF], int t) {
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ar[SL][sub][f]) : "v"(arow[f] + (size_t)t * BK + 32 * sub)
+                   : "memory");
+}
+
+template <class G>
+__device__ __forceinline__ void da_loop(f32x4 (&acc)[G::MF][G::NJ], const Args& a, const Readers<G>& rd,
+                                        Stager<G>& stg, char* smem, uint32_t lds0, int i0, int wm, int fr, int fq,
+                                        int nk) {
+  constexpr int MF = G::MF, NJ = G::NJ, RB = Readers<G>::RB;
+  constexpr int NA = 2 * MF;   // A loads per K step
+  const uint16_t* arow[MF];
+#pragma unroll
+  for (int f = 0; f < MF; ++f) arow[f] = a.P + (size_t)(i0 + wm * MF * 16 + 16 * f + fr) * a.ldp + 8 * fq;
+  bf16x8 ar[2][2][MF];
+  auto loadA = [&](auto slot, int t) __attribute__((always_inline)) {
+    da_load_a<decltype(slot)::value, MF>(ar, arow, t);
+  };
+  bf16x8 b0[NJ], b1[NJ];
+  auto readB = [&](bf16x8 (&b)[NJ], uint32_t st, int sub) __attribute__((always_inline)) {
+    static_for<0, NJ>([&](auto j) { b[decltype(j)::value] = rd.rb.template frag<decltype(j)::value>(st, sub); });
+  };
+  auto mfma = [&](const bf16x8 (&av)[MF], const bf16x8 (&b)[NJ]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], b[j], acc[i][j], 0, 0, 0);
+  };
+  const int last = nk - 1;
+  // prologue: B tiles 0, 1 and A of steps 0, 1 in flight (pieces, then A, per tile); wait for tile 0
+  stg.issue_tile(smem, 0);
+  loadA(std::integral_constant<int, 0>{}, 0);
+  stg.issue_tile(smem + G::STAGE, 1 < last ? 1 : last);
+  loadA(std::integral_constant<int, 1>{}, 1 < last ? 1 : last);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::NPER + 2 * NA) : "memory");
+  __builtin_amdgcn_s_barrier();
+  readB(b0, lds0, 0);
+  auto step = [&](auto slot, int t) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot)::value;
+    const uint32_t cur = lds0 + (t % 3) * G::STAGE, nxt = lds0 + ((t + 1) % 3) * G::STAGE;
+    readB(b1, cur, 1);
+    // A of step t (loaded at the end of step t - 2): followed by step t - 1's B pieces and A loads
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::NPER + NA) : "memory");
+    lgkm_wait<NJ * RB>();   // (b0 landed; b1 may still be in flight)
+    mfma(ar[SL][0], b0);
+    __builtin_amdgcn_sched_barrier(0);
+    // tile t + 1: its pieces were issued one step ago, followed only by that step's A loads
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA) : "memory");
+    __builtin_amdgcn_s_barrier();
+    const int tn = t + 2 < last ? t + 2 : last;
+    stg.issue_tile(smem + ((t + 2) % 3) * G::STAGE, tn);
+    __builtin_amdgcn_sched_barrier(0);
+    readB(b0, nxt, 0);
+    lgkm_wait<NJ * RB>();   // (b1 landed)
+    mfma(ar[SL][1], b1);
+    __builtin_amdgcn_sched_barrier(0);
+    loadA(slot, tn);
+  };
+  for (int t = 0; t < nk; t += 2) {   // (nk even: checked by the launcher)
+    step(std::integral_constant<int, 0>{}, t);
+    step(std::integral_constant<int, 1>{}, t + 1);
+  }
+}
 
 // tile order: blocks b, b+8, ... share an XCD; each XCD takes whole GM x GN tile groups (row-major
 // within the group) when the grid splits that way, else plain row-major
@@ -431,12 +528,16 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   Readers<G> rd;
   rd.ra.init(0, wm * G::MF * 16, fr, fq);
   rd.rb.init(G::A_BYTES, wn * G::NJ * 16, fr, fq);
-  // prologue: tiles 0 .. NS-2 in flight; wait for tile 0; its first fragments
-  for (int t = 0; t < NS - 1 && t < nk; ++t) stg.issue(smem + t * G::STAGE);
-  vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
-  __builtin_amdgcn_s_barrier();
+  // prologue: tiles 0 .. NS-2 in flight; wait for tile 0; its first fragments (the direct-A loop has its own)
+  if constexpr (!G::ADIR) {
+    for (int t = 0; t < NS - 1 && t < nk; ++t) stg.issue(smem + t * G::STAGE);
+    vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
+    __builtin_amdgcn_s_barrier();
+  }
   Frags<G> f0, f1;
-  if constexpr (!G::STEP_LOOP) {
+  if constexpr (G::ADIR) {
+    da_loop<G>(acc, a, rd, stg, smem, lds0, i0, wm, fr, fq, nk);
+  } else if constexpr (!G::STEP_LOOP) {
     rd.read_b(f0, lds0, 0);
     rd.read_a(f0, lds0, 0);
 
@@ -723,7 +824,8 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
 template <class G, int EPI, int GM, int GN>
 int launch(const Args& a, hipStream_t st) {
   if (a.I % G::BM || a.J % G::BN || a.K % BK || a.K < BK) return (int)hipErrorInvalidValue;
-  if (G::STEP_LOOP && (a.K / BK) % 2) return (int)hipErrorInvalidValue;   // (that loop runs K steps in pairs)
+  if ((G::STEP_LOOP || G::ADIR) && (a.K / BK) % 2) return (int)hipErrorInvalidValue;   // (K steps in pairs)
+  if (G::ADIR && a.pexp != nullptr) return (int)hipErrorInvalidValue;   // (no routed rows on the direct path)
   auto kern = &gemm_kernel<G, EPI, GM, GN>;
   static bool attr = false;
   if (!attr) {
@@ -765,6 +867,8 @@ using FwdD = Geo<3, 8, 4, 1, KC, KC, 3>;            // fwd 192 x 128, 4 waves (4
 using FwdE = Geo<6, 4, 2, 2, KC, KC, 3>;            // fwd 192 x 128, 4 waves (2 x 2)
 using WgrD = Geo<4, 8, 2, 2, MC, MC, 3>;            // wgrad 128 x 256, 4 waves (2 x 2)
 using DgrE = Geo<9, 4, 2, 2, KC, MC, 3>;            // dgrad 288 x 128, 4 waves (2 x 2): 256 tiles at the flagship shape
+// direct A (KCD): 4 x 1 waves, the A rows of a wave loaded straight into its registers, only B through LDS
+using FwdDA = Geo<3, 8, 4, 1, KCD, KC, 3>;          // fwd 192 x 128
 
 }  // namespace gemm
 }  // namespace qd
@@ -772,7 +876,7 @@ using DgrE = Geo<9, 4, 2, 2, KC, MC, 3>;            // dgrad 288 x 128, 4 waves 
 using namespace qd::gemm;
 
 // Which forward config applies to (M, N, K): 1 + cfg, or 0 (unsupported)
-QD_API int qd_gemm_tile_m(int cfg) { return (cfg == 1 || cfg == 3 || cfg == 4) ? FwdB::BM : FwdA::BM; }
+QD_API int qd_gemm_tile_m(int cfg) { return (cfg == 1 || cfg == 3 || cfg == 4 || cfg == 5) ? FwdB::BM : FwdA::BM; }
 
 QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (K % BK || N % 128) return 0;
@@ -781,6 +885,7 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (cfg == 2) return M % FwdC::BM == 0 && K % (2 * BK) == 0;
   if (cfg == 1) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
   if (cfg == 3 || cfg == 4) return M % FwdD::BM == 0 && N % FwdD::BN == 0;
+  if (cfg == 5) return M % FwdDA::BM == 0 && N % FwdDA::BN == 0 && (K / BK) % 2 == 0;
   return 0;
 }
 
@@ -794,6 +899,7 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_BF16, 1, 4>(a, st);
   if (cfg == 4) return launch<FwdE, EPI_BF16, 1, 4>(a, st);
+  if (cfg == 5) return launch<FwdDA, EPI_BF16, 1, 4>(a, st);
   if (M % FwdA::BM) return (int)hipErrorInvalidValue;
   if (cfg == 2) return launch<FwdC, EPI_BF16, 4, 8>(a, st);
   if (cfg == 101) return launch<Geo<9, 2, 1, 4, KC, KC, 4, 1>, EPI_BF16, 4, 8>(a, st);   // (diagnosis builds)
@@ -818,6 +924,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   if (cfg == 1) return launch<FwdB, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 4) return launch<FwdE, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 5) return launch<FwdDA, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 2) return launch<FwdC, EPI_NMSE, 4, 8>(a, st);
   return launch<FwdA, EPI_NMSE, 4, 8>(a, st);
 }
