@@ -30,8 +30,9 @@ At N > 1:
     all-reduce) are built on the graph mode the capture pre-flight allows, each timed over
     ``--select-steps`` steps after its warm-up (max over ranks), and the faster one is benchmarked;
     ``plan_select_ms`` records both.
-  * ``phases_ms``: per-phase HIP-event times (max over ranks) on extra steps AFTER the timed region --
-    for the 5-graph plan only; the one-graph plan reports null (no host-visible phase boundaries).
+  * ``phases_ms``: per-phase times (max over ranks) on extra steps AFTER the timed region: HIP events
+    between the 5-graph plan's replays, device clock stamps captured inside the one-graph plan's graph
+    (FlagshipTrainer.phase_times); ``phases_src`` says which.
 """
 from __future__ import annotations
 
@@ -223,8 +224,9 @@ def main() -> int:
     value = samples / elapsed
     dp = len(tr.graphs) == 5 or (one_graph and (ctx.world > 1 or cfg.split_graphs))
     phases = None
-    if args.phase_steps > 0 and dp and len(tr.graphs) == 5:   # (the 5-graph plan only: see FlagshipTrainer.phase_times)
+    if args.phase_steps > 0 and dp:
         phases = tr.phase_times(args.phase_steps)
+    if phases is not None:
         keys = sorted(phases)
         phases = dict(zip(keys, (round(v, 4) for v in ctx.max_vector([phases[k] for k in keys]))))
     if ctx.is_main:
@@ -279,6 +281,7 @@ def main() -> int:
         }
         if dp:
             rec["phases_ms"] = phases
+            rec["phases_src"] = None if phases is None else ("events" if len(tr.graphs) == 5 else "stamps")
         fb = os.environ.get("QDML_DP_FALLBACK")
         if ctx.world > 1:
             rec["dp_fallback"] = fb or None

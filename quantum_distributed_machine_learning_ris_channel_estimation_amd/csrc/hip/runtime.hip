@@ -74,3 +74,26 @@ extern "C" int qd_lds_peek(uint32_t* out, void* stream) {
   hipLaunchKernelGGL(qd::rt::lds_peek_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
   return (int)hipGetLastError();
 }
+
+// Phase stamps (FlagshipTrainer.phase_times under the one-graph DP plan, whose phases sit inside ONE graph
+// and so have no host-visible boundaries for HIP events): a one-wave kernel, captured as a graph node between
+// two phases on the phase's own stream, writes the chip's constant-rate wall clock into out[idx] once the work
+// ahead of it on that stream has finished.  The clock is shared by every XCD and queue, so stamps taken on
+// different streams of the same step are comparable; qd_wallclock_khz gives its rate.
+namespace qd {
+namespace rt {
+__global__ void __launch_bounds__(64) stamp_kernel(unsigned long long* __restrict__ out, int idx) {
+  const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) out[idx] = t;   // (a vector store: lane 0 of the wave)
+}
+}  // namespace rt
+}  // namespace qd
+
+extern "C" int qd_stamp(unsigned long long* out, int idx, void* stream) {
+  hipLaunchKernelGGL(qd::rt::stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out, idx);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qd_wallclock_khz(int device, int* khz) {
+  return (int)hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, device);
+}

@@ -219,6 +219,7 @@ class FlagshipTrainer(DPPlan):
             self._tail_pack_launch(advance=False)   # the first step's images
         self._use_graphs = graphs
         self._phases = None   # (phase_times) per-step dicts of HIP events
+        self._stamps = None   # (phase_times, one-graph plan) (device clock buffer, {phase: slot}) while capturing
         self._prime_fp8()
         self._graph_sets = {}            # steps per replay -> list of GraphedStep
         self.graphs = self._graphs_for(1)
@@ -378,7 +379,10 @@ class FlagshipTrainer(DPPlan):
     def capture(self, preserve: bool = True, k: int = 1) -> None:
         """Capture the ``k``-step graph set now.  Capturing runs warm-up steps; with ``preserve`` the
         model/optimizer state is restored afterwards, so the first real step is step 1."""
-        gs = self._graphs_for(k)
+        self._capture_set(self._graphs_for(k), k, preserve)
+
+    def _capture_set(self, gs, k: int, preserve: bool = True) -> None:
+        """Capture the graphs of ``gs`` (``k`` steps per replay) that are not captured yet."""
         if not any(g.enabled and g.graph is None for g in gs):
             return
         # the warm-up runs inside capture advance the device cursors: make room, restore them after

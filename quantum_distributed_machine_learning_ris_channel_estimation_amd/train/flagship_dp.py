@@ -1,6 +1,7 @@
 """The flagship trainer's data-parallel plan (world > 1; also world 1 with ``split_graphs``), as a mixin of
 ``train.flagship.FlagshipTrainer``: the step cut around its gradient collectives, the ZeRO-1 / all-reduce FC
-update on its own stream, and per-phase HIP-event timing.
+update on its own stream, and per-phase timing (HIP events between the
+5-graph plan's replays; device clock stamps captured inside the one-graph plan's graph).
 
 Reference: torch.nn.DataParallel over 4 GPUs in the HDCE trainer (Runner_P128_QuantumNAT_onchipQNN.py:135-153,
 SURVEY §2.4 C1-C7), re-designed as SPMD over RCCL: one process per GPU, bucketed collectives launched as soon
@@ -8,7 +9,12 @@ as their gradients are final and hidden behind the rest of the backward (see ``D
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
+
+from .. import _native as nat
+from ..utils.profiling import GraphedStep
 
 
 class DPPlan:
@@ -92,11 +98,20 @@ class DPPlan:
             self.buckets.pending.pop("master")   # (waited for by its only consumer: nothing stays in flight)
 
     def _mark(self, name: str, stream=None) -> None:
-        """(phase timing) a HIP event on ``stream`` (default: current) under ``name``."""
+        """(phase timing) a HIP event on ``stream`` (default: current) under ``name``; while the stamped
+        one-graph step is being captured, a clock-stamp node instead (csrc/hip/runtime.hip qd_stamp)."""
         if self._phases is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record(stream)
             self._phases[-1][name] = e
+        elif self._stamps is not None:
+            buf, slots = self._stamps
+            i = slots.setdefault(name, len(slots))
+            if i >= buf.numel():
+                raise RuntimeError(f"phase stamp buffer full at {name!r}")
+            s = stream if stream is not None else torch.cuda.current_stream(self.ctx.device)
+            f = nat.fn(nat.hip_lib(), "qd_stamp", [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p])
+            nat.check(f(nat.ptr(buf), i, ctypes.c_void_p(s.cuda_stream)), "qd_stamp")
 
     def _dp_run(self, g1a, g1b, g2, gf, gr, fence: bool = True, first: bool = True) -> None:
         """The DP step around the collectives.  RCCL runs every collective of the process group on one
@@ -108,10 +123,9 @@ class DPPlan:
         for the fc stream only before g1b reads the FC weights.  ``fence``: main also waits for it at the
         end of the step (the last step of a run(), every step()): afterwards the state is complete."""
         b, zero = self.buckets, self.zero
-        timed = self._phases is not None
-        if timed:
+        if self._phases is not None:
             self._phases.append({})
-            self._mark("start")
+        self._mark("start")
         g1a()
         self._mark("g1a")
         main = torch.cuda.current_stream(self.ctx.device) if self.streams is not None else None
@@ -179,28 +193,35 @@ class DPPlan:
                 main.wait_stream(fc)
                 b.launch_all_gather("ag", self._fc_weights_lp())
             b.wait(("ag",))
+            self._mark("ag")
         b.pending.clear()   # (every collective has been waited for by the stream that consumes it)
         if fence:
             main.wait_stream(fc)
         self._mark("end")
 
     def phase_times(self, steps: int):
-        """Run ``steps`` DP steps with HIP events around the phases and return the mean milliseconds of
-        each (diagnostic; the GPU 5-graph DP plan only): g1 (forward + FC wgrad), g2 (FC dgrad + conv
+        """Run ``steps`` DP steps with timers around the phases and return the mean milliseconds of each
+        (diagnostic): g1a (gather + conv forward), fc_prev_wait, g1 (forward + FC wgrad), g2 (FC dgrad + conv
         backward + QSC, hiding the FC collective), fc_exposed (FC collective time left after g2),
-        small_exposed, fc_adam, all_gather (ZeRO), conv_qsc_adam, step.  None for every other plan -- in
-        particular the one-graph DP plan, whose phases have no host-visible boundaries (its whole-step
-        time is what bench.py measures; the phases of a different plan are never reported for it)."""
-        if self.ctx.device.type != "cuda" or self.streams is None or len(self.graphs) != 5:
+        small_exposed, fc_adam, all_gather (ZeRO; the one-graph plan: its part left after gr),
+        conv_qsc_adam, step.
+          5-graph plan : HIP events between the graph replays (``run``: consecutive steps overlap, step =
+                         start to the next step's start).
+          one-graph    : a second capture of the one-step graph with a clock-stamp node at each phase
+                         boundary on the phase's own stream, replayed ``steps`` times with a host sync after
+                         each (step = its start to its fenced end).  The stamp nodes are extra graph nodes
+                         (a few us each): the phases are the plan's shape, bench.py's timed run its speed.
+        None for the world-1 single-chain plan and off the GPU."""
+        if self.ctx.device.type != "cuda" or self.streams is None:
             return None
-        self._phases = []
-        try:
-            self.run(steps)
-            torch.cuda.synchronize(self.ctx.device)
-            rows = self._phases
-        finally:
-            self._phases = None
-        el = lambda r, a, b_: r[a].elapsed_time(r[b_])
+        if len(self.graphs) == 5:
+            rows, chained = self._event_rows(steps), True
+        elif self.cfg.dp_one_graph and self._use_graphs and len(self.graphs) == 1 and \
+                (self.ctx.world > 1 or self.cfg.split_graphs):
+            rows, chained = self._stamped_rows(steps), False
+        else:
+            return None
+        el = lambda r, a, b_: r[b_] - r[a]
         out = {"g1a": [], "fc_prev_wait": [], "g1": [], "g2": [], "fc_exposed": [], "small_exposed": [],
                "fc_adam": [], "all_gather": [], "conv_qsc_adam": [], "step": []}
         for i, r in enumerate(rows):
@@ -211,8 +232,55 @@ class DPPlan:
             out["fc_exposed"].append(max(0.0, el(r, "g2", "fc_ready")))
             out["small_exposed"].append(max(0.0, el(r, "g2", "small_ready")))
             out["fc_adam"].append(el(r, "fc_ready", "gf"))
-            out["all_gather"].append(el(r, "gf", "ag") if "ag" in r else 0.0)
+            # (5-graph: the all-gather follows the shard Adam on the fc stream; one-graph: main launches it
+            # beside gr, and only what is left of it after gr is on the critical path)
+            ag_from = "gf" if chained else "gr"
+            out["all_gather"].append(max(0.0, el(r, ag_from, "ag")) if "ag" in r else 0.0)
             out["conv_qsc_adam"].append(el(r, "small_ready", "gr"))
-            # step = start to the next step's start (the FC update overlaps it), the last to its end
-            out["step"].append(r["start"].elapsed_time(rows[i + 1]["start"]) if i + 1 < len(rows) else el(r, "start", "end"))
+            nxt = rows[i + 1]["start"] if chained and i + 1 < len(rows) else r["end"]
+            out["step"].append(nxt - r["start"])
         return {k: sum(v) / len(v) for k, v in out.items()}
+
+    def _event_rows(self, steps: int):
+        """(5-graph plan) ``run(steps)`` with HIP events at the phase boundaries -> per-step {phase: ms}
+        relative to the first step's start."""
+        self._phases = []
+        try:
+            self.run(steps)
+            torch.cuda.synchronize(self.ctx.device)
+            rows = self._phases
+        finally:
+            self._phases = None
+        t0 = rows[0]["start"]
+        return [{k: t0.elapsed_time(e) for k, e in r.items()} for r in rows]
+
+    def _stamped_rows(self, steps: int):
+        """(one-graph plan) the one-step graph captured again with clock stamps (see ``_mark``), replayed
+        ``steps`` times -> per-step {phase: ms} on the device clock."""
+        dev = self.ctx.device
+        buf = torch.zeros(32, dtype=torch.int64, device=dev)
+        self._stamps = (buf, {})
+        gs = [GraphedStep(lambda: self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr),
+                          enabled=True, guards=(self.buckets.assert_quiescent,))]
+        try:
+            self._capture_set(gs, 1, preserve=True)
+            slots = dict(self._stamps[1])
+        finally:
+            self._stamps = None
+        khz = ctypes.c_int(0)
+        f = nat.fn(nat.hip_lib(), "qd_wallclock_khz", [ctypes.c_int, ctypes.POINTER(ctypes.c_int)])
+        nat.check(f(dev.index if dev.index is not None else torch.cuda.current_device(), ctypes.byref(khz)),
+                  "qd_wallclock_khz")
+        if khz.value <= 0:
+            raise RuntimeError(f"device wall clock rate {khz.value} kHz")
+        rows = []
+        try:
+            for _ in range(steps):
+                self.next_batch(1)
+                gs[0]()
+                torch.cuda.synchronize(dev)
+                t = buf.tolist()
+                rows.append({n: (t[i] - t[slots["start"]]) / khz.value for n, i in slots.items()})
+        finally:
+            del gs   # (the stamped graph and its pool)
+        return rows

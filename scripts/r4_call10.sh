@@ -11,4 +11,6 @@ timeout -k 10 120 python scripts/r4_adam_probe.py > $O/r4_10_adam_probe.txt 2>&1
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tl_p256 -o run -- python $R/bench.py --pilot 256 --qubits 12 --steps 30 --warmup 5 --steps-per-graph 1 > $O/tl_p256.log 2>&1) || exit 1
 python scripts/prof_timeline.py $O/tl_p256/run_kernel_trace.csv --marker "conv3x3_kernel<2," --back 5 > $O/r4_10_p256_timeline.md
 python scripts/prof_summary.py $O/tl_p256/run_kernel_trace.csv --tail 0.6 > $O/r4_10_p256_kernel_stats.md; rm -rf $O/tl_p256
-VARIANTS="N=0|;N=1|--gemm-cfg 3,1,2;N=2|--gemm-cfg 5,1,2;N=3|--gemm-cfg 1,3,4" bash scripts/r4_ab.sh $O/r4_10_gemm_cfg_ab.txt
+VARIANTS="N=0|;N=1|--gemm-cfg 3,1,2;N=2|--gemm-cfg 5,1,2;N=3|--gemm-cfg 1,3,4" bash scripts/r4_ab.sh $O/r4_10_gemm_cfg_ab.txt || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_runtime_gpu.py tests/test_flagship_gpu.py -v --timeout 200 --timeout-method thread -k "clock_stamps or one_graph" > $O/r4_10_stamps.log 2>&1 || exit 1
+QDML_FORCE_DIST=1 timeout -k 10 300 python bench.py --steps 200 --warmup 20 > $O/r4_10_bench_forced_stamps.json 2>$O/r4_10_bench_forced_stamps.err

@@ -5,7 +5,9 @@
 Run with QDML_FORCE_DIST=1 at world 1 on one GPU (a real RCCL process group of one rank: the
 collectives are launched and captured exactly as at world N) or with N ranks.  Both plans train the
 same model on the same batches for 6 steps; weights, moments and the bf16 FC shadow must agree
-exactly (the graphs hold the same kernels in the same dependency order)."""
+exactly (the graphs hold the same kernels in the same dependency order).  Then the one-graph trainer's
+phase_times (clock stamps captured in a second copy of its graph) must give finite phases that fit in
+the step."""
 import faulthandler
 import os
 import sys
@@ -26,20 +28,24 @@ def run(ctx, plan, one, k=1, steps=6):
     tr.run(steps)
     tr.sync_master()
     torch.cuda.synchronize()
-    return len(tr.graphs), [t.cpu().clone() for t in tr.mutable_state()], tr.hloss.cpu().clone()
+    return tr, len(tr.graphs), [t.cpu().clone() for t in tr.mutable_state()], tr.hloss.cpu().clone()
 
 
 def main(out, plan="zero", k=1):
     faulthandler.enable()
     ctx = init_distributed("cuda")
-    n5, s5, l5 = run(ctx, plan, False)
+    _, n5, s5, l5 = run(ctx, plan, False)
     print("five-graph plan done", flush=True)
-    n1, s1, l1 = run(ctx, plan, True, k)
+    t1, n1, s1, l1 = run(ctx, plan, True, k)
     print("one-graph plan done", flush=True)
     same = [torch.equal(a, b) for a, b in zip(s5, s1)]
     ok = ctx.distributed and n5 == 5 and n1 == 1 and all(same) and torch.equal(l5, l1) and bool(torch.isfinite(l1).all())
+    ph = t1.phase_times(3) if k == 1 else None
+    ph_ok = ph is None or (all(v == v and 0.0 <= v < 1e3 for v in ph.values()) and ph["step"] > 0
+                           and ph["g1"] <= ph["step"] and ph["g1"] + ph["g2"] <= ph["step"] + 1e-3)
+    print("phases", ph, flush=True)
     with open(f"{out}.{ctx.rank}", "w") as f:
-        f.write(f"{int(ok)} {n5} {n1} {''.join(str(int(x)) for x in same)} {l5.tolist()} {l1.tolist()}\n")
+        f.write(f"{int(ok and ph_ok)} {n5} {n1} {''.join(str(int(x)) for x in same)} {l5.tolist()} {l1.tolist()}\n")
     shutdown()
 
 

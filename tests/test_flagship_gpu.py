@@ -148,7 +148,8 @@ def test_dp_one_graph_matches_five_graphs_over_rccl(tmp_path, plan, k):
     """The DP step captured as ONE graph with its RCCL collectives inside == the 5-graph DP plan (which
     launches the collectives between replays), bit for bit over 6 steps: a real RCCL process group of
     one rank (QDML_FORCE_DIST=1), so the reduce-scatter / all-reduce / all-gather are captured.  k = 3:
-    three steps per replay, each step's FC update overlapping the next step's conv forward."""
+    three steps per replay, each step's FC update overlapping the next step's conv forward.  (k = 1: the
+    one-graph trainer's phase_times -- clock stamps captured inside the graph -- must also fit in its step.)"""
     import os
     import sys
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.launch import launch
