@@ -9,7 +9,7 @@ optimizer, on HBM-resident synthetic data.
 
 Execution plan (world = 1, default ``stream_mode="dagq"``): one HIP graph replay runs
 ``steps_per_graph`` consecutive training steps (5 in bench), each captured from two streams: the
-QSC branch forks off the HDCE chain after the batch gather and joins it at the end of the step.
+QSC branch forks off the HDCE chain after the batch gather and joins it before the HDCE update.
 Almost every kernel of this model is latency-bound and fills a fraction of the 256 CUs, so the
 QSC branch overlaps the HDCE chain.  (Plans that let the two chains run independently across step
 boundaries were ~1.5% faster but not bit-reproducible on ROCm 7.x; they were measured and removed --
@@ -17,7 +17,7 @@ docs/CONCURRENCY.md keeps the findings.)  Per step:
 
   main : gather -> conv fwd x3 -> BN/ReLU apply (+ BN tail) -> FC fwd GEMM -> one-pass NMSE ->
          FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce (+ loss finish) -> [wgrad|dgrad] L3 ->
-         [wgrad|dgrad] L2 -> wgrad L1 -> slab sums (conv, BN, FC bias) -> Adam (one launch over all
+         [wgrad|dgrad] L2 -> wgrad L1 -> slab sums (conv, BN, FC bias) -> (join) -> Adam (one launch over all
          HDCE parameters; also writes the bf16 FC shadow and the conv weights' MFMA B-fragment images
          for the NEXT step, and advances the batch cursor)
   qsc  : (after gather) QuantumNAT noise -> QSC fwd -> VQC fwd -> head -> VQC adjoint ->
@@ -51,8 +51,6 @@ from ..utils.profiling import GraphedStep
 from .engine import ClassifierStep, HDCEModel, HDCEStep
 from .flagship_dp import DPPlan
 
-
-import os
 
 @dataclass
 class FlagshipConfig:
@@ -335,6 +333,9 @@ class FlagshipTrainer(DPPlan):
     def _hdce_backward_update(self) -> None:
         """conv/BN backward + the one Adam launch over the whole HDCE space (+ the conv weight images)."""
         self.hstep.backward_conv()
+        self._hdce_update()
+
+    def _hdce_update(self) -> None:
         pk = self._adam_pack()
         self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
         if self.tail_pack and pk is None:
@@ -343,14 +344,21 @@ class FlagshipTrainer(DPPlan):
     def _step_body(self) -> None:
         if self.mode == "dagq":
             # the QSC branch forks right after the batch gather: its latency-bound kernels share the GPU with
-            # the HDCE chain's, and it joins at the end of the step.  (Measured alternatives, round 4,
-            # docs/CONCURRENCY.md: the HDCE chain captured first, the QSC branch gathering its own batch, the QSC
-            # step split around the FC GEMMs, the FC update on the QSC stream -- all slower.)
+            # the HDCE chain's, and it joins BEFORE the HDCE update (the QSC branch has long finished by then).
+            # The update is then the chain's last node with a single parent on its own queue, and the next
+            # step's gather follows it there; with the join after the update, the graph executor placed the
+            # gather on the QSC queue and every step paid two cross-queue hops (update -> gather -> conv
+            # forward, ~33 us idle: profiles/r3_23_step_timeline.md).  0.4176-0.4182 vs 0.4203-0.4223 ms/step
+            # (profiles/r4_08_plan_probe.txt).  (Measured alternatives, round 4, docs/CONCURRENCY.md: the HDCE
+            # chain captured first, the QSC branch gathering its own batch, the QSC step split around the FC
+            # GEMMs, the FC update on the QSC stream -- all slower.)
             self._gather()
             with self._fork(self.streams["qsc"]):
                 self._qsc_branch(with_opt=True)
-            self._hdce_graph()
+            self._hdce_forward()
+            self.hstep.backward_conv()
             self._join(("qsc",))
+            self._hdce_update()
             return
         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)
 

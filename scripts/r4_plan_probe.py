@@ -32,22 +32,20 @@ class HdceFirst(FlagshipTrainer):
         self._join(("qsc",))
 
 
-class JoinFirst(FlagshipTrainer):
-    """As shipped, but the join is issued BEFORE the HDCE chain's last node (the Adam): the next step's
-    gather then depends on the Adam only through the main stream."""
+class JoinLast(FlagshipTrainer):
+    """The round-3 plan: the QSC branch joins AFTER the HDCE chain's last node (the Adam), so the next step's
+    gather has two parents on two queues.  (Round 4 ships the join before the Adam, measured here as
+    'join_first' before it became the default: profiles/r4_08_plan_probe.txt.)"""
 
     def _step_body(self):
         self._gather()
         with self._fork(self.streams["qsc"]):
             self._qsc_branch(with_opt=True)
-        self._hdce_forward()
-        self.hstep.backward_conv()
+        self._hdce_graph()
         self._join(("qsc",))
-        pk = self._adam_pack()
-        self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
 
 
-PLANS = {"shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_first": JoinFirst}
+PLANS = {"shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast}
 
 
 def run(cls, steps):
