@@ -27,9 +27,10 @@ At N > 1:
     the JSON line then carries ``dp_fallback`` with the reason.  Only a fully successful attempt's
     JSON line is printed (rank 0's supervisor relays it), so stdout never holds two.
   * the DP plan is CHOSEN AT THE REAL WORLD SIZE: with ``--dp-plan auto`` both plans (ZeRO-1 and
-    all-reduce) are built on the graph mode the capture pre-flight allows, each timed over
-    ``--select-steps`` steps after its warm-up (max over ranks), and the faster one is benchmarked;
-    ``plan_select_ms`` records both.
+    all-reduce) are built on the graph mode the capture pre-flight allows -- on the one-graph plan
+    each with both QSC placements (``--dp-qsc auto``: beside the conv backward, or forked after the
+    gather) -- each timed over ``--select-steps`` steps after its warm-up (max over ranks), and the
+    fastest is benchmarked; ``plan_select_ms`` records every candidate.
   * ``phases_ms``: per-phase times (max over ranks) on extra steps AFTER the timed region: HIP events
     between the 5-graph plan's replays, device clock stamps captured inside the one-graph plan's graph
     (FlagshipTrainer.phase_times); ``phases_src`` says which.
@@ -71,6 +72,9 @@ def main() -> int:
                     help="DP plan: capture the whole step, RCCL collectives included, in one HIP graph")
     ap.add_argument("--phase-steps", type=int, default=20,
                     help="N > 1: extra steps (after the timed region) timed per phase with HIP events; 0 = off")
+    ap.add_argument("--dp-qsc", default="auto", choices=["auto", "g2", "fwd"],
+                    help="N > 1, one-graph DP plan: the QSC branch beside the conv backward (g2) or forked after the "
+                         "gather (fwd); auto = timed at the real world size with the plans (FlagshipConfig.dp_qsc)")
     ap.add_argument("--select-steps", type=int, default=10,
                     help="N > 1, --dp-plan auto: steps timed per candidate plan to choose the faster one (0 = no timing: "
                          "allreduce with the one-graph step, zero with the 5-graph step)")
@@ -132,12 +136,13 @@ def main() -> int:
         return 2
     sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
 
-    def make(plan: str, og: bool, store=None) -> FlagshipTrainer:
+    def make(cand, og: bool, store=None) -> FlagshipTrainer:
+        plan, qsc = cand
         cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch,
                              data_len=args.data_len, dtype=args.dtype, hip_graphs=not args.no_graphs,
                              use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
                              stream_mode=args.stream_mode, steps_per_graph=args.steps_per_graph,
-                             dp_plan=plan, dp_one_graph=og, lead_in=args.lead_in)
+                             dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in)
         return FlagshipTrainer(cfg, ctx, store=store)
 
     def timed(tr: FlagshipTrainer, n: int, settle: int = 0):
@@ -162,30 +167,39 @@ def main() -> int:
     # mode the pre-flight allows; a user-fixed plan is a single candidate
     dp_run = ctx.world > 1 or ctx.forced or args.split_graphs
     if not dp_run:
-        cands = ["allreduce"]   # (world 1: the plan field is unused)
+        plans = ["allreduce"]   # (world 1: the plan field is unused)
     elif args.dp_plan != "auto":
-        cands = [args.dp_plan]
+        plans = [args.dp_plan]
     elif args.select_steps <= 0 or args.dtype == "fp8":   # (fp8: no ZeRO plan, see FlagshipTrainer)
-        cands = ["allreduce" if one_graph or args.dtype == "fp8" else "zero"]
+        plans = ["allreduce" if one_graph or args.dtype == "fp8" else "zero"]
     else:
-        cands = ["allreduce", "zero"]
+        plans = ["allreduce", "zero"]
+    # the QSC branch's place in the DP step (one-graph plan only): timed with the plans unless fixed
+    if not (dp_run and one_graph and not args.no_graphs):
+        qscs = ["g2"]
+    elif args.dp_qsc != "auto":
+        qscs = [args.dp_qsc]
+    else:
+        qscs = ["g2", "fwd"] if args.select_steps > 0 else ["g2"]
+    cands = [(p, q) for p in plans for q in qscs]
     select = {}
     tr, store = None, None
-    for plan in cands:
-        t = make(plan, one_graph, store)
+    for cand in cands:
+        t = make(cand, one_graph, store)
         store = t.store
         if len(cands) > 1:
             t.run(args.warmup)
             el, _ = timed(t, args.select_steps)
-            select[plan] = round(el / args.select_steps * 1e3, 4)
-            if tr is None or select[plan] < select[tr_plan]:
+            key = cand[0] if len(qscs) == 1 else f"{cand[0]}/{cand[1]}"
+            select[key] = round(el / args.select_steps * 1e3, 4)
+            if tr is None or el < best:
                 if tr is not None:
                     del tr
-                tr, tr_plan = t, plan
+                tr, tr_cand, best = t, cand, el
             else:
                 del t
         else:
-            tr, tr_plan = t, plan
+            tr, tr_cand = t, cand
     cfg = tr.cfg
     t = None
     if len(cands) > 1 and ctx.device.type == "cuda":
@@ -261,6 +275,7 @@ def main() -> int:
                 "stream_mode": tr.mode,
                 "dp_plan": ("zero" if tr.zero else "allreduce") if dp else None,
                 "dp_graph": ("one" if one_graph else "five") if dp else None,
+                "dp_qsc": tr.cfg.dp_qsc if dp else None,
                 "capture_preflight": capture_ok,
                 "plan_select_ms": select or None,
                 "dist_backend": ctx.backend,

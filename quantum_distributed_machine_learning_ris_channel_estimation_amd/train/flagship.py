@@ -86,6 +86,11 @@ class FlagshipConfig:
     #                              graph (the 5-graph plan launches the collectives between graph replays and
     #                              pays a graph boundary at each; this one pays one per step but fences the
     #                              FC update at the end of the step instead of overlapping the next gather)
+    dp_qsc: str = "g2"           # DP plan, where the QSC branch runs: "g2" = forked beside the conv backward (the most
+    #                              work behind the FC gradient collective), "fwd" = forked right after the gather as in
+    #                              the world-1 step, joined before the small bucket (shorter g2: wins where the FC
+    #                              collective is short; one-graph plan only -- a fork cannot span two graphs).
+    #                              bench.py times both at the real world size.
     seed: int = 0
     n_scenarios: int = 3
     n_users: int = 3
@@ -108,6 +113,8 @@ class FlagshipTrainer(DPPlan):
         dp = ctx.world > 1 or cfg.split_graphs
         if cfg.dp_plan not in ("zero", "allreduce"):
             raise ValueError(f"dp_plan {cfg.dp_plan!r}")
+        if cfg.dp_qsc not in ("g2", "fwd") or (cfg.dp_qsc == "fwd" and not cfg.dp_one_graph):
+            raise ValueError(f"dp_qsc {cfg.dp_qsc!r} (\"fwd\" needs dp_one_graph)")
         # ZeRO-1 plan (see _dp_run); not with the fp8 estimator (its weight scale is a max over the
         # whole FC weight, which a sharded update would have to all-reduce)
         self.zero = dp and cfg.dp_plan == "zero" and cfg.dtype != "fp8"

@@ -28,9 +28,16 @@ class DPPlan:
     #        -> all-reduce 'small' (conv/BN + QSC grads + the QSC NaN flag)
     #   gf : (fc stream) FC Adam once 'skip' + 'fc' arrived and g2's dgrad read the weight shadow,
     #        beside the 'small' all-reduce;   gr : (main) conv/BN Adam + QSC AdamW after 'small'
+    def _qsc_fwd(self) -> bool:
+        """(cfg.dp_qsc "fwd", one-graph plan) the QSC branch forks after the gather and joins in g2."""
+        return self.cfg.dp_qsc == "fwd" and self.streams is not None and self._use_graphs
+
     def _dp_g1a(self) -> None:
         """gather + conv forward (reads no FC weight: overlaps the previous step's FC update)."""
         self._gather()
+        if self._qsc_fwd():
+            with self._fork(self.streams["qsc"]):
+                self._qsc_branch(with_opt=False)
         self.hstep.defer_dgrad = self.hstep.hip
         if self.hstep.hip:
             self.hstep.forward_conv_gathered(self.gat)
@@ -59,6 +66,10 @@ class DPPlan:
         # the QSC branch then read the previous step's gather output)
         if self.hstep.defer_dgrad:
             self.hstep.dgrad()
+        if self._qsc_fwd():   # (forked in g1a: joined before the small bucket, which carries its gradients)
+            self.hstep.backward_conv()
+            self._join(("qsc",))
+            return
         if self.streams is None:
             self.hstep.backward_conv()
             self._qsc_branch(with_opt=False)

@@ -12,3 +12,4 @@ python scripts/prof_summary.py $O/tl_step/run_kernel_trace.csv --tail 0.6 > $O/r
 timeout -k 10 400 python scripts/r4_qsc_gate_probe.py 256 12 100 2 > $O/r4_12_qsc_gate_p256.txt 2>&1 || exit 1
 timeout -k 10 300 python scripts/r4_qsc_gate_probe.py 128 8 300 2 > $O/r4_12_qsc_gate_p128.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py --qubits 16 --dtype fp8 --steps 20 --warmup 3 > $O/r4_12_bench_q16.json 2>$O/r4_12_bench_q16.err || exit 1
+QDML_FORCE_DIST=1 timeout -k 10 400 python bench.py --steps 200 --warmup 20 --select-steps 30 > $O/r4_12_bench_forced.json 2>$O/r4_12_bench_forced.err || exit 1

@@ -1,6 +1,6 @@
 """DP plan captured as ONE graph (RCCL collectives inside it) == the 5-graph DP plan, bit for bit.
 
-    dp_one_graph.py OUT [zero|allreduce] [steps per one-graph replay]
+    dp_one_graph.py OUT [zero|allreduce] [steps per one-graph replay] [g2|fwd: the one-graph plan's QSC placement]
 
 Run with QDML_FORCE_DIST=1 at world 1 on one GPU (a real RCCL process group of one rank: the
 collectives are launched and captured exactly as at world N) or with N ranks.  Both plans train the
@@ -21,9 +21,9 @@ from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flags
     FlagshipConfig, FlagshipTrainer)
 
 
-def run(ctx, plan, one, k=1, steps=6):
+def run(ctx, plan, one, k=1, steps=6, qsc="g2"):
     cfg = FlagshipConfig(n_qubits=8, batch=32, data_len=800, hip_graphs=True, dp_plan=plan,
-                         split_graphs=True, dp_one_graph=one, steps_per_graph=k)
+                         split_graphs=True, dp_one_graph=one, steps_per_graph=k, dp_qsc=qsc)
     tr = FlagshipTrainer(cfg, ctx)
     tr.run(steps)
     tr.sync_master()
@@ -31,12 +31,12 @@ def run(ctx, plan, one, k=1, steps=6):
     return tr, len(tr.graphs), [t.cpu().clone() for t in tr.mutable_state()], tr.hloss.cpu().clone()
 
 
-def main(out, plan="zero", k=1):
+def main(out, plan="zero", k=1, qsc="g2"):
     faulthandler.enable()
     ctx = init_distributed("cuda")
     _, n5, s5, l5 = run(ctx, plan, False)
     print("five-graph plan done", flush=True)
-    t1, n1, s1, l1 = run(ctx, plan, True, k)
+    t1, n1, s1, l1 = run(ctx, plan, True, k, qsc=qsc)
     print("one-graph plan done", flush=True)
     same = [torch.equal(a, b) for a, b in zip(s5, s1)]
     ok = ctx.distributed and n5 == 5 and n1 == 1 and all(same) and torch.equal(l5, l1) and bool(torch.isfinite(l1).all())
@@ -50,4 +50,5 @@ def main(out, plan="zero", k=1):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "zero", int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "zero", int(sys.argv[3]) if len(sys.argv) > 3 else 1,
+         sys.argv[4] if len(sys.argv) > 4 else "g2")

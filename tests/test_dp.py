@@ -140,3 +140,16 @@ def test_reference_dp_semantics_matches_one_process(tmp_path, world):
         assert torch.allclose(a["sc_loss"], b["sc_loss"], rtol=1e-5)
         same, hl, _ = open(f"{many}.{r}").read().split()
         assert same == "1" and float(hl) == float(hl)
+
+
+def test_dp_qsc_placement_needs_the_one_graph_plan():
+    """cfg.dp_qsc "fwd" forks the QSC branch in g1a and joins it in g2: only the one-graph DP plan holds both in
+    one capture, so any other plan refuses it (instead of silently running the "g2" placement)."""
+    import torch
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
+                                                                                                FlagshipTrainer)
+    ctx = DistContext(device=torch.device("cpu"))
+    for bad in (dict(dp_qsc="fwd", split_graphs=True), dict(dp_qsc="later")):
+        with pytest.raises(ValueError, match="dp_qsc"):
+            FlagshipTrainer(FlagshipConfig(n_qubits=4, batch=4, data_len=100, dtype="fp32", **bad), ctx)

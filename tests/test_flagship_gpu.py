@@ -143,19 +143,22 @@ def test_dp_plan_run_to_run_on_shared_gpu(tmp_path):
         assert rec[0] == "1", (r, rec)
 
 
-@pytest.mark.parametrize("plan,k", [("zero", 1), ("allreduce", 1), ("allreduce", 3)])
-def test_dp_one_graph_matches_five_graphs_over_rccl(tmp_path, plan, k):
+@pytest.mark.parametrize("plan,k,qsc", [("zero", 1, "g2"), ("allreduce", 1, "g2"), ("allreduce", 3, "g2"),
+                                        ("zero", 1, "fwd"), ("allreduce", 3, "fwd")])
+def test_dp_one_graph_matches_five_graphs_over_rccl(tmp_path, plan, k, qsc):
     """The DP step captured as ONE graph with its RCCL collectives inside == the 5-graph DP plan (which
     launches the collectives between replays), bit for bit over 6 steps: a real RCCL process group of
     one rank (QDML_FORCE_DIST=1), so the reduce-scatter / all-reduce / all-gather are captured.  k = 3:
-    three steps per replay, each step's FC update overlapping the next step's conv forward.  (k = 1: the
-    one-graph trainer's phase_times -- clock stamps captured inside the graph -- must also fit in its step.)"""
+    three steps per replay, each step's FC update overlapping the next step's conv forward.  qsc "fwd": the
+    one-graph plan's QSC branch forked after the gather (cfg.dp_qsc) -- the same kernels on the same inputs,
+    so still bit-exact.  (k = 1: the one-graph trainer's phase_times -- clock stamps captured inside the graph
+    -- must also fit in its step.)"""
     import os
     import sys
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.launch import launch
     here = os.path.dirname(os.path.abspath(__file__))
     out = str(tmp_path / "og")
-    rc = launch([sys.executable, os.path.join(here, "dist_scripts", "dp_one_graph.py"), out, plan, str(k)], nproc=1,
+    rc = launch([sys.executable, os.path.join(here, "dist_scripts", "dp_one_graph.py"), out, plan, str(k), qsc], nproc=1,
                 extra_env={"OMP_NUM_THREADS": "2", "QDML_FORCE_DIST": "1"})
     assert rc == 0
     rec = open(f"{out}.0").read().split()
