@@ -97,3 +97,70 @@ extern "C" int qd_stamp(unsigned long long* out, int idx, void* stream) {
 extern "C" int qd_wallclock_khz(int device, int* khz) {
   return (int)hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, device);
 }
+
+// Cross-queue coherence probe (scripts/probe_coherence.py; docs/CONCURRENCY.md, the stale-read diagnosis).
+// A producer grid writes buf[i] = tag * 2^20 + i with tag = *ctr (the step), a consumer grid forked onto
+// another stream of the same graph reads buf back and counts the elements that do not hold THIS step's value
+// (errs[0]; errs[1] = elements seen holding the PREVIOUS step's value, i.e. a stale cached line), and a tick
+// grid advances *ctr at the end of the step.  buf is small (it stays resident in the consumer XCDs' L2 between
+// steps), so a consumer that misses an L2 invalidate after the cross-queue edge reads last step's line.
+// mode 0: plain loads; 1: an agent-scope acquire fence at consumer entry; 2: system-scope (L2-coherent)
+// loads.  Counters are vector atomics.
+namespace qd {
+namespace rt {
+__global__ void __launch_bounds__(256) coh_produce_kernel(int* __restrict__ buf, int n, const int* __restrict__ ctr) {
+  const int tag = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (vector load: the tag
+  //                                                                                       itself is not under test)
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) buf[i] = (tag << 20) + i;
+}
+template <int MODE>
+__global__ void __launch_bounds__(256) coh_consume_kernel(const int* buf, int n, const int* __restrict__ ctr,
+                                                          unsigned int* __restrict__ errs) {
+  if constexpr (MODE == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int tag = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned int bad = 0, stale = 0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    int v;
+    if constexpr (MODE == 2) v = __hip_atomic_load(buf + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else v = buf[i];
+    bad += v != (tag << 20) + i;
+    stale += v == ((tag - 1) << 20) + i;
+  }
+  if (bad) atomicAdd(errs, bad);
+  if (stale) atomicAdd(errs + 1, stale);
+}
+__global__ void __launch_bounds__(64) coh_tick_kernel(int* __restrict__ ctr) {
+  if (threadIdx.x == 0) ctr[0] = ctr[0] + 1;
+}
+// keeps the producer's queue busy while the consumer runs (so the graph executor gives the branch its own queue)
+__global__ void __launch_bounds__(256) coh_busy_kernel(float* __restrict__ x, int n, int iters) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    float v = x[i];
+    for (int k = 0; k < iters; ++k) v = v * 0.999f + 0.001f;
+    x[i] = v;
+  }
+}
+}  // namespace rt
+}  // namespace qd
+
+QD_API int qd_coh_produce(int* buf, int n, const int* ctr, int grid, void* stream) {
+  hipLaunchKernelGGL(qd::rt::coh_produce_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, buf, n, ctr);
+  return (int)hipGetLastError();
+}
+QD_API int qd_coh_consume(const int* buf, int n, const int* ctr, unsigned int* errs, int mode, int grid,
+                          void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 0) hipLaunchKernelGGL(qd::rt::coh_consume_kernel<0>, dim3(grid), dim3(256), 0, s, buf, n, ctr, errs);
+  else if (mode == 1) hipLaunchKernelGGL(qd::rt::coh_consume_kernel<1>, dim3(grid), dim3(256), 0, s, buf, n, ctr, errs);
+  else if (mode == 2) hipLaunchKernelGGL(qd::rt::coh_consume_kernel<2>, dim3(grid), dim3(256), 0, s, buf, n, ctr, errs);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+QD_API int qd_coh_tick(int* ctr, void* stream) {
+  hipLaunchKernelGGL(qd::rt::coh_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ctr);
+  return (int)hipGetLastError();
+}
+QD_API int qd_coh_busy(float* x, int n, int iters, int grid, void* stream) {
+  hipLaunchKernelGGL(qd::rt::coh_busy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, iters);
+  return (int)hipGetLastError();
+}

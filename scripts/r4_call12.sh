@@ -13,3 +13,4 @@ timeout -k 10 400 python scripts/r4_qsc_gate_probe.py 256 12 100 2 > $O/r4_12_qs
 timeout -k 10 300 python scripts/r4_qsc_gate_probe.py 128 8 300 2 > $O/r4_12_qsc_gate_p128.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py --qubits 16 --dtype fp8 --steps 20 --warmup 3 > $O/r4_12_bench_q16.json 2>$O/r4_12_bench_q16.err || exit 1
 QDML_FORCE_DIST=1 timeout -k 10 400 python bench.py --steps 200 --warmup 20 --select-steps 30 > $O/r4_12_bench_forced.json 2>$O/r4_12_bench_forced.err || exit 1
+timeout -k 10 120 python scripts/probe_coherence.py 300 10 > $O/r4_12_coherence.txt 2>&1 || exit 1
