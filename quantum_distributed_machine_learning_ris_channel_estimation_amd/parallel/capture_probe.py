@@ -45,7 +45,7 @@ def _child() -> int:
     def body():
         a.mul_(1.0)
         bk.launch("a")
-        bk.launch("bc")
+        bk.launch("bc", inline=True)   # (the DP step's small bucket: inline on the issuing stream)
         bk.launch_reduce_scatter("rs", full)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):   # (one bucket consumed on a forked stream)
@@ -55,7 +55,7 @@ def _child() -> int:
         gath.copy_(full)
         bk.launch_all_gather("ag", gath)
         bk.wait(("ag",))
-        bk.pending.clear()
+        bk.clear()
         torch.cuda.current_stream(dev).wait_stream(side)
 
     def reset():

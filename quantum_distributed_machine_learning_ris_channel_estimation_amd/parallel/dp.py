@@ -217,46 +217,67 @@ class GradBuckets:
             if len(ts) > 1:
                 self.staging[k] = torch.empty(sum(t.numel() for t in ts), device=ts[0].device, dtype=ts[0].dtype)
         self.pending: Dict[str, list] = {}
+        # (rccl) the event of the last collective issued: RCCL needs the collectives of one communicator in one
+        # order on every rank and never two of them running at once, so each next collective -- on the comm
+        # stream or inline on the caller's stream -- is ordered after it.  Reset once nothing is pending.
+        self._last: Optional[torch.cuda.Event] = None
+
+    def clear(self) -> None:
+        """Forget every launched collective (each has been waited for by the stream that consumes it)."""
+        self.pending.clear()
+        self._last = None
 
     def assert_quiescent(self) -> None:
         """Raise if a launched collective has not been waited for (a graph capture must not begin with one
-        in flight: its completion would be observed from inside the capture)."""
+        in flight: its completion would be observed from inside the capture).  With nothing pending, the
+        ordering event of the last collective is dropped too (a capture must not wait on an event recorded
+        before it began)."""
         if self.pending:
             raise RuntimeError(f"gradient collectives still pending: {sorted(self.pending)}")
+        self._last = None
 
     def bucket_bytes(self) -> Dict[str, int]:
         return {k: sum(t.numel() * t.element_size() for t in ts) for k, ts in self.buckets.items()}
 
-    def _collective(self, fn):
+    def _collective(self, fn, inline: bool = False):
         """Issue one collective.  gloo: ``fn(None)`` is a torch.distributed async call returning its work.
         rccl: ``fn(stream)`` issues the RCCL kernel on the context's comm stream, forked from the current
         stream (so it sees every gradient written so far); the returned handle is an event on the comm
-        stream that ``wait`` joins back -- under graph capture the fork and the join are graph edges."""
+        stream that ``wait`` joins back -- under graph capture the fork and the join are graph edges.
+        ``inline``: the kernel runs on the CURRENT stream instead (for a collective its stream waits for right
+        away: no fork / join hop), after the previous collective."""
         if self.ctx.backend != "rccl":
             return fn(None)
         cur = torch.cuda.current_stream(self.ctx.device)
-        cs = self.ctx.comm_stream
-        cs.wait_stream(cur)
-        fn(cs)
+        if inline:
+            s = cur
+        else:
+            s = self.ctx.comm_stream
+            s.wait_stream(cur)
+        if self._last is not None:
+            s.wait_event(self._last)
+        fn(s)
         ev = torch.cuda.Event()
-        ev.record(cs)
+        ev.record(s)
+        self._last = ev
         return ev
 
-    def _all_reduce(self, t: torch.Tensor):
+    def _all_reduce(self, t: torch.Tensor, inline: bool = False):
         if self.ctx.backend == "rccl":
-            return self._collective(lambda s: self.ctx.comm.all_reduce_(t, stream=s))
+            return self._collective(lambda s: self.ctx.comm.all_reduce_(t, stream=s), inline)
         return dist.all_reduce(t, async_op=True)
 
-    def launch(self, name: str) -> None:
+    def launch(self, name: str, inline: bool = False) -> None:
+        """All-reduce bucket ``name``.  ``inline`` (rccl): on the current stream, which waits for it next."""
         if not self.ctx.distributed or name not in self.buckets:
             return
         ts = self.buckets[name]
         if len(ts) == 1:
-            self.pending[name] = [self._all_reduce(ts[0]), None, None]
+            self.pending[name] = [self._all_reduce(ts[0], inline), None, None]
         else:
             st = self.staging[name]
             torch.cat([t.reshape(-1) for t in ts], out=st)
-            self.pending[name] = [self._all_reduce(st), st, ts]
+            self.pending[name] = [self._all_reduce(st, inline), st, ts]
 
     def launch_all(self) -> None:
         for k in self.buckets:
@@ -329,7 +350,7 @@ class GradBuckets:
             elif len(ent) > 3:
                 torch.cuda.current_stream().wait_event(ent[3])
         if names is None:
-            self.pending.clear()
+            self.clear()
 
 
 class DeviceSampler:

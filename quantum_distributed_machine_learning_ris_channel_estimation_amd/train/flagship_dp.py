@@ -107,6 +107,8 @@ class DPPlan:
             self.buckets.launch_all_gather("master", self.hdce.space.flat[lo:hi])
             self.buckets.wait(("master",))
             self.buckets.pending.pop("master")   # (waited for by its only consumer: nothing stays in flight)
+            if not self.buckets.pending:
+                self.buckets.clear()
 
     def _mark(self, name: str, stream=None) -> None:
         """(phase timing) a HIP event on ``stream`` (default: current) under ``name``; while the stamped
@@ -155,7 +157,10 @@ class DPPlan:
             b.launch("fc")
         g2()
         self._mark("g2")
-        b.launch("small")
+        # (main waits for the small bucket right away: its all-reduce runs inline on main -- ordered after the
+        # FC collective -- instead of a fork / join through the comm stream, two cross-queue hops on the
+        # step's critical path)
+        b.launch("small", inline=True)
         fc_wait = ("fc", "small") if zero else ("skip", "fc")
         if self.streams is None:
             b.wait(fc_wait)
@@ -205,7 +210,7 @@ class DPPlan:
                 b.launch_all_gather("ag", self._fc_weights_lp())
             b.wait(("ag",))
             self._mark("ag")
-        b.pending.clear()   # (every collective has been waited for by the stream that consumes it)
+        b.clear()   # (every collective has been waited for by the stream that consumes it)
         if fence:
             main.wait_stream(fc)
         self._mark("end")

@@ -340,7 +340,7 @@ class Y2HRunner:
                 opt.step(grad_scale=gscale, skip=skip, part=1)
                 buckets.wait(("conv",))
                 opt.step(grad_scale=gscale, skip=skip, part=0)
-                buckets.pending.clear()
+                buckets.clear()
             else:
                 buckets.wait()
                 opt.step(grad_scale=gscale, skip=skip)

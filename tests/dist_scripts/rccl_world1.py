@@ -55,7 +55,7 @@ def collectives(ctx):
         g3.add_(3.0)
         full.add_(1.0)
         bk.launch("big")
-        bk.launch("small")
+        bk.launch("small", inline=True)   # (on the capturing stream, after "big": the DP step's small bucket)
         bk.launch_reduce_scatter("rs", full)
         bk.wait()
         bk.launch_all_gather("ag", full)
