@@ -33,6 +33,12 @@ def main():
     flush = torch.empty(128 << 20, device=dev)
     src = torch.empty(n * 4, device=dev)        # 4 fp32 streams read ...
     dst = torch.empty(n * 3, device=dev)        # ... 3 written (+ the bf16 shadow ~ 0.5 more)
+    def adam_grid(g):
+        def f():
+            opt.max_grid[0] = g
+            opt.step()
+        return f
+
     var = {
         "adam": lambda: opt.step(),
         "copy_r4w3": lambda: dst.copy_(src[:n * 3]),
@@ -40,6 +46,10 @@ def main():
         "flush_then_adam": lambda: (flush.zero_(), opt.step()),
         "flush_only": lambda: flush.zero_(),
     }
+    # launch sizes of the update (cold, as in the step: after a 512 MB flush), grid-stride over 8.4 M params
+    for g in (1024, 4096, 8192):
+        var[f"flush_then_adam_grid{g}"] = (lambda f: lambda: (flush.zero_(), f()))(adam_grid(g))
+    var["flush_then_adam_grid2048"] = (lambda f: lambda: (flush.zero_(), f()))(adam_grid(2048))
     bytes_adam = n * (4 * 4 + 3 * 4 + 2)
     res = {k: [] for k in var}
     for _ in range(5):
