@@ -35,17 +35,16 @@ class PackScatter(ctypes.Structure):
 
 
 class FlatParamSpace:
-    def __init__(self, params: Sequence[Tuple[str, nn.Parameter]], device=None, extra: int = 0):
+    def __init__(self, params: Sequence[Tuple[str, nn.Parameter]], device=None, extra: int = 0, front: int = 0,
+                 storage: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
         """``extra``: trailing scratch floats (one ALIGN block) after the last parameter; their grad
         slots ride along with the tail of the grad buffer (e.g. a NaN flag that then travels in the
-        same all-reduce as the last parameters' gradients).  ``extra_off`` is their offset."""
-        seen = set()
-        uniq = []
-        for name, p in params:
-            if id(p) in seen:
-                continue
-            seen.add(id(p))
-            uniq.append((name, p))
+        same all-reduce as the last parameters' gradients).  ``extra_off`` is their offset.
+        ``front``: floats reserved IN FRONT of this space in the same allocation (``front_views``: (flat, grad)
+        of that region) -- another space placed there with ``storage`` makes the two gradient buffers one
+        contiguous range (one in-place collective, no coalescing copies).  ``storage``: (flat, grad) views to
+        live in instead of a fresh allocation (zero-filled by their owner, at least ``size_of`` long)."""
+        uniq = self._uniq(params)
         self.names = [n for n, _ in uniq]
         self.params = [p for _, p in uniq]
         device = torch.device(device) if device is not None else self.params[0].device
@@ -58,14 +57,43 @@ class FlatParamSpace:
         off += (extra + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
         self.n_real = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(off, device=device, dtype=torch.float32)
-        self.grad = torch.zeros(off, device=device, dtype=torch.float32)
+        self.front_views = None
+        if storage is not None:
+            if front or storage[0].numel() < off or storage[1].numel() < off:
+                raise ValueError(f"storage of {storage[0].numel()} floats for a space of {off}")
+            self.flat, self.grad = storage[0][:off], storage[1][:off]
+            self.grad_base = None
+        else:
+            if front % ALIGN:
+                raise ValueError(f"front {front} not a multiple of {ALIGN}")
+            fa = torch.zeros(front + off, device=device, dtype=torch.float32)
+            ga = torch.zeros(front + off, device=device, dtype=torch.float32)
+            self.flat, self.grad = fa[front:], ga[front:]
+            self.grad_base = ga   # (front region + this space's gradients, contiguous)
+            if front:
+                self.front_views = (fa[:front], ga[:front])
         for p, o in zip(self.params, offs):
             n = p.numel()
             view = self.flat[o:o + n].view(p.shape)
             view.copy_(p.data.to(device, torch.float32))
             p.data = view
             p.grad = self.grad[o:o + n].view(p.shape)
+
+    @staticmethod
+    def _uniq(params):
+        seen, uniq = set(), []
+        for name, p in params:
+            if id(p) in seen:
+                continue
+            seen.add(id(p))
+            uniq.append((name, p))
+        return uniq
+
+    @classmethod
+    def size_of(cls, params: Sequence[Tuple[str, nn.Parameter]], extra: int = 0) -> int:
+        """Floats a space over ``params`` (+ ``extra``) occupies (shapes only: meta tensors will do)."""
+        al = lambda n: (n + ALIGN - 1) // ALIGN * ALIGN
+        return sum(al(p.numel()) for _, p in cls._uniq(params)) + al(extra)
 
     def slice_of(self, p: torch.Tensor) -> slice:
         for q, o in zip(self.params, self.offsets):

@@ -58,9 +58,11 @@ class HDCEModel:
     views into the flat buffer), so ``Conv0.state_dict()`` etc. remain reference-compatible."""
 
     def __init__(self, pilot_num: int = 128, device="cpu", dtype: str = "bf16", n_experts: int = 3,
-                 grad_extra: int = 0, fc_pad_multiple: int = 1):
+                 grad_extra: int = 0, fc_pad_multiple: int = 1, front: int = 0):
         """``fc_pad_multiple``: pad the flat space after the FC parameters so that the FC region
-        [FC.weight offset, end) has a multiple of this many elements (ZeRO-1 sharding over ranks)."""
+        [FC.weight offset, end) has a multiple of this many elements (ZeRO-1 sharding over ranks).
+        ``front``: floats reserved in front of the flat space in the same allocation
+        (``space.front_views``; FlatParamSpace)."""
         self.device = torch.device(device)
         self.E = n_experts
         self.H, self.W = pilot_grid(pilot_num)
@@ -86,7 +88,7 @@ class HDCEModel:
             al = lambda n: (n + ALIGN - 1) // ALIGN * ALIGN
             fc_len = al(self.fc.FC.weight.numel()) + al(self.fc.FC.bias.numel()) + al(grad_extra)
             grad_extra += (-fc_len) % (fc_pad_multiple * ALIGN)   # (every shard ALIGN-aligned)
-        self.space = FlatParamSpace(named, self.device, extra=grad_extra)
+        self.space = FlatParamSpace(named, self.device, extra=grad_extra, front=front)
         # grouped leaf views over the expert-consecutive parameter blocks
         self.conv_w, self.bn_w, self.bn_b = [], [], []
         for k in range(3):

@@ -122,11 +122,22 @@ class FlagshipTrainer(DPPlan):
         # travels in the FC all-reduce (one collective less ahead of it); ZeRO plan: in the small bucket
         # (every rank needs the summed flag, a reduce-scatter leaves it on one rank only)
         self.flag_in_fc = dp and not self.zero
+        # DP: the QSC space lives IN FRONT of the HDCE space in one allocation, and the NaN flags in its trailing
+        # scratch (QSC flag at +0, ZeRO's HDCE flag one 128-byte line later), so the small bucket -- QSC grads,
+        # flags, conv/BN grads -- is ONE contiguous range: all-reduced in place, no coalescing / scatter-back
+        # copies on the step's critical path.  (Sized on the meta device: no RNG draw, init order unchanged.)
+        qargs = (cfg.n_qubits, cfg.n_layers, cfg.n_classes, cfg.use_quantumnat, cfg.use_gradient_pruning,
+                 cfg.pilot_num)
+        q_extra = 64 if dp else 0
+        nq = 0
+        if dp:
+            with torch.device("meta"):
+                nq = FlatParamSpace.size_of(list(QSC_P128(*qargs).named_parameters()), extra=q_extra)
         self.hdce = HDCEModel(cfg.pilot_num, dev, cfg.dtype, cfg.n_scenarios, grad_extra=1 if self.flag_in_fc else 0,
-                              fc_pad_multiple=ctx.world if self.zero else 1)
-        self.qsc = QSC_P128(cfg.n_qubits, cfg.n_layers, cfg.n_classes, cfg.use_quantumnat,
-                            cfg.use_gradient_pruning, cfg.pilot_num).to(dev)
-        self.qspace = FlatParamSpace(list(self.qsc.named_parameters()), dev)
+                              fc_pad_multiple=ctx.world if self.zero else 1, front=nq)
+        self.qsc = QSC_P128(*qargs).to(dev)
+        self.qspace = FlatParamSpace(list(self.qsc.named_parameters()), dev, extra=q_extra,
+                                     storage=self.hdce.space.front_views)
         ctx.broadcast_(self.hdce.space.flat)
         ctx.broadcast_(self.qspace.flat)
         self.hopt = make_optimizer(self.hdce.space, "adam", cfg.lr)
@@ -152,19 +163,25 @@ class FlagshipTrainer(DPPlan):
         self.skip = torch.zeros(2, 64, device=dev, dtype=torch.float32)   # (own cache line per flag)
         self.qskip = self.skip[1, 0:1]
         self.hskip = sp.grad[sp.extra_off:sp.extra_off + 1] if self.flag_in_fc else self.skip[0, 0:1]
+        if dp:
+            qe = self.qspace.extra_off
+            self.qskip = self.qspace.grad[qe:qe + 1]
+            if self.zero:
+                self.hskip = self.qspace.grad[qe + 32:qe + 33]
         self.hstep.nmse.skip = self.hskip
         gb = cfg.qsc_grid_bwd or 256   # (QSC backward workgroups: fewer measured slower, profiles/r2_20_variants.md)
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B,
                                     skip=self.qskip, hip_kw={"grid_bwd": gb})
         self.cstep.skip_add = False
         self.cstep.writes_grads = self.cstep.hip is not None
-        # buckets (see _dp_run): "fc" = 33.6 MB FC grads (in place; + the HDCE NaN flag when flag_in_fc,
-        # else that flag is its own "skip" bucket), "small"
-        # = conv/BN + QSC grads + the QSC NaN flag (coalesced)
+        # buckets (see _dp_run): "fc" = 33.6 MB FC grads (in place; + the HDCE NaN flag in the all-reduce plan),
+        # "small" = QSC grads + NaN flags + conv/BN grads, one contiguous range in place (DP; see above)
         bk = {"fc": [sp.grad[n_conv:]], "small": [sp.grad[:n_conv], self.qspace.grad, self.qskip]}
-        if self.zero:
-            bk = {"small": bk["small"] + [self.hskip]}
-        elif not self.flag_in_fc:
+        if dp:
+            bk["small"] = [sp.grad_base[:nq + n_conv]]
+            if self.zero:
+                del bk["fc"]   # (its reduce-scatter is launched on the region directly)
+        else:
             bk["skip"] = [self.skip[0, 0:1]]
         self.buckets = GradBuckets(ctx, bk)
         self.gat = StepGather(self.E, self.U, self.B, self.hdce.H, self.hdce.W, dev, with_classifier=True)

@@ -143,3 +143,30 @@ def test_nmse_global_denominators_split_equals_whole():
         g = part.grad(sl(Y), sl(L)).view(U, hi - lo, E, cols)
         assert torch.allclose(g, gw[:, lo:hi], rtol=1e-5, atol=1e-7)
     assert torch.allclose(loss_sum, lw, rtol=1e-5)
+
+
+def test_flat_space_in_front_of_another_shares_one_contiguous_gradient_range():
+    """A space placed in another's ``front`` region (the DP trainer's QSC space before the HDCE space) makes the
+    two gradient buffers one contiguous range -- the small gradient bucket is all-reduced in place -- and each
+    module's parameters / grads are views of exactly their own slots."""
+    import torch
+    import torch.nn as nn
+    import pytest
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.optim import ALIGN, FlatParamSpace
+    torch.manual_seed(0)
+    a, b = nn.Linear(5, 3), nn.Conv2d(2, 4, 3)
+    with torch.device("meta"):
+        nq = FlatParamSpace.size_of(list(nn.Linear(5, 3).named_parameters()), extra=64)
+    assert nq % ALIGN == 0 and nq == 16 + 16 + 64
+    wa, wb = a.weight.detach().clone(), b.weight.detach().clone()
+    big = FlatParamSpace(list(b.named_parameters()), "cpu", front=nq)
+    small = FlatParamSpace(list(a.named_parameters()), "cpu", extra=64, storage=big.front_views)
+    assert torch.equal(a.weight, wa) and torch.equal(b.weight, wb)
+    base = big.grad_base
+    assert base.numel() == nq + big.numel
+    assert small.grad.data_ptr() == base.data_ptr() and big.grad.data_ptr() == base.data_ptr() + 4 * nq
+    base.copy_(torch.arange(base.numel(), dtype=torch.float32))
+    assert torch.equal(a.weight.grad.reshape(-1), torch.arange(15, dtype=torch.float32))
+    assert torch.equal(b.bias.grad, base[nq + big.offsets[1]:nq + big.offsets[1] + 4])
+    with pytest.raises(ValueError):
+        FlatParamSpace(list(nn.Linear(50, 3).named_parameters()), "cpu", storage=big.front_views)
