@@ -193,6 +193,14 @@ def shutdown() -> None:
 
 
 
+class _Issued:
+    """(rccl) a launched collective: the event recorded after it and the stream it ran on."""
+    __slots__ = ("event", "stream")
+
+    def __init__(self, event, stream):
+        self.event, self.stream = event, stream
+
+
 class GradBuckets:
     """Asynchronous all-reduce of named gradient buckets.
 
@@ -217,15 +225,19 @@ class GradBuckets:
             if len(ts) > 1:
                 self.staging[k] = torch.empty(sum(t.numel() for t in ts), device=ts[0].device, dtype=ts[0].dtype)
         self.pending: Dict[str, list] = {}
-        # (rccl) the event of the last collective issued: RCCL needs the collectives of one communicator in one
-        # order on every rank and never two of them running at once, so each next collective -- on the comm
-        # stream or inline on the caller's stream -- is ordered after it.  Reset once nothing is pending.
-        self._last: Optional[torch.cuda.Event] = None
+        # (rccl) the last collective issued: RCCL needs the collectives of one communicator in one order on every
+        # rank and never two of them running at once, so each next collective -- on the comm stream or inline on
+        # the caller's stream -- is ordered after it.  Reset once nothing is pending.
+        self._last: Optional[_Issued] = None
+        # (rccl) (stream handle, event id) pairs already waited for: under HIP graph capture a stream must not
+        # take the same node as a dependency twice (a duplicate edge crashed hipStreamEndCapture, r4_12)
+        self._waited = set()
 
     def clear(self) -> None:
         """Forget every launched collective (each has been waited for by the stream that consumes it)."""
         self.pending.clear()
         self._last = None
+        self._waited.clear()
 
     def assert_quiescent(self) -> None:
         """Raise if a launched collective has not been waited for (a graph capture must not begin with one
@@ -235,6 +247,16 @@ class GradBuckets:
         if self.pending:
             raise RuntimeError(f"gradient collectives still pending: {sorted(self.pending)}")
         self._last = None
+        self._waited.clear()
+
+    def _wait_on(self, s, rec: "_Issued") -> None:
+        """Make stream ``s`` wait for ``rec`` unless it already does: recorded on ``s`` itself (stream order) or
+        waited for before (no duplicate dependency edges under capture)."""
+        key = (s.cuda_stream, id(rec.event))
+        if rec.stream.cuda_stream == s.cuda_stream or key in self._waited:
+            return
+        s.wait_event(rec.event)
+        self._waited.add(key)
 
     def bucket_bytes(self) -> Dict[str, int]:
         return {k: sum(t.numel() * t.element_size() for t in ts) for k, ts in self.buckets.items()}
@@ -254,13 +276,15 @@ class GradBuckets:
         else:
             s = self.ctx.comm_stream
             s.wait_stream(cur)
-        if self._last is not None:
-            s.wait_event(self._last)
+        last = self._last
+        # ordered after the previous collective; nothing to add when it ran on s or on cur (which s just joined)
+        if last is not None and last.stream.cuda_stream not in (s.cuda_stream, cur.cuda_stream):
+            self._wait_on(s, last)
         fn(s)
         ev = torch.cuda.Event()
         ev.record(s)
-        self._last = ev
-        return ev
+        self._last = _Issued(ev, s)
+        return self._last
 
     def _all_reduce(self, t: torch.Tensor, inline: bool = False):
         if self.ctx.backend == "rccl":
@@ -326,8 +350,8 @@ class GradBuckets:
         for from several streams."""
         for k in list(self.pending) if names is None else [n for n in names if n in self.pending]:
             ent = self.pending[k]
-            if isinstance(ent[0], torch.cuda.Event):   # (rccl: join the comm stream's event)
-                torch.cuda.current_stream(self.ctx.device).wait_event(ent[0])
+            if isinstance(ent[0], _Issued):   # (rccl: join the collective's stream)
+                self._wait_on(torch.cuda.current_stream(self.ctx.device), ent[0])
             else:
                 ent[0].wait()
             if ent[1] is not None:
