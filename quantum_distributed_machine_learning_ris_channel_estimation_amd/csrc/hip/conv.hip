@@ -152,12 +152,20 @@ __device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, i
                                                int j) {
   float a = 0.f, b = 0.f;
   const float* p = part + (size_t)u * chunks * 2 * EC + ch;
+  // all 16 loads issued before the first add (a chunk past the end loads chunk 0 and is not added): guarded
+  // loads compiled to 8 dependent round trips, each behind its own vmcnt(0) -- most of every consumer's prologue
+  float pa[8], pb[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int k = j + 8 * i;
-    if (k < chunks) {
-      a += p[(size_t)k * 2 * EC];
-      b += p[(size_t)k * 2 * EC + EC];
+    const int k = j + 8 * i < chunks ? j + 8 * i : 0;
+    pa[i] = p[(size_t)k * 2 * EC];
+    pb[i] = p[(size_t)k * 2 * EC + EC];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (j + 8 * i < chunks) {   // (the same additions in the same order as before: bit-identical)
+      a += pa[i];
+      b += pb[i];
     }
   }
   for (int k = j + 64; k < chunks; k += 8) {

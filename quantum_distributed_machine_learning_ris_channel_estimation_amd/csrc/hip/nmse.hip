@@ -249,27 +249,41 @@ __global__ void __launch_bounds__(256) nmse_fused_kernel(const TY* __restrict__ 
   const int r1 = r0 + rpc;
   int ro[RT];
   float4 yv[RT], lv[RT], pv[RT];
+  // (branch-free: a row past the block's end re-loads row rb and is never used -- guarded loads compiled to one
+  // dependent round trip per rowoff, each behind its own vmcnt(0), before the first label load could issue)
   auto issue = [&](int rb) {
 #pragma unroll
-    for (int q = 0; q < RT; ++q)
-      if (rb + q < r1) ro[q] = rowoff[rb + q];
+    for (int q = 0; q < RT; ++q) ro[q] = rowoff[rb + q < r1 ? rb + q : rb];
 #pragma unroll
-    for (int q = 0; q < RT; ++q)
-      if (rb + q < r1) yv[q] = load4<TY>(Y + (size_t)(rb + q) * cols + c0);
+    for (int q = 0; q < RT; ++q) yv[q] = load4<TY>(Y + (size_t)(rb + q < r1 ? rb + q : rb) * cols + c0);
 #pragma unroll
-    for (int q = 0; q < RT; ++q)
-      if (rb + q < r1) {
-        const size_t le = (size_t)ro[q] * cols + c0;
-        lv[q] = *reinterpret_cast<const float4*>(Lb + le);
-        pv[q] = Pf ? *reinterpret_cast<const float4*>(Pf + le) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+    for (int q = 0; q < RT; ++q) {
+      const size_t le = (size_t)ro[q] * cols + c0;
+      lv[q] = *reinterpret_cast<const float4*>(Lb + le);
+      pv[q] = Pf ? *reinterpret_cast<const float4*>(Pf + le) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   if (act) issue(r0);
   // per-stream label powers of this u-block (wave e: stream e*U + u), fixed order
   for (int e = wv; e < E; e += 4) {
     float a = 0.f, ap = 0.f;
     if (rowden) {   // (gathered per-row powers: independent loads, no rowoff -> rowpow chain)
-      for (int b = lane; b < B; b += 64) {
+      // up to 8 rows per lane in flight at once (a loop of guarded loads waited one round trip per row), then
+      // the same additions in the same order; rows beyond 512 per stream in the tail loop
+      constexpr int NB = 8;
+      float2 rv[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int b = lane + 64 * i < B ? lane + 64 * i : lane < B ? lane : 0;
+        rv[i] = rowden[(u * B + b) * E + e];
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        if (lane + 64 * i < B) {
+          a += rv[i].x;
+          ap += Pf ? rv[i].y : 0.f;
+        }
+      for (int b = lane + 64 * NB; b < B; b += 64) {
         const float2 v = rowden[(u * B + b) * E + e];
         a += v.x;
         ap += Pf ? v.y : 0.f;

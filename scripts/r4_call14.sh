@@ -1,7 +1,13 @@
 #!/bin/bash
-# round-4 GPU call: captured-RCCL regression check (inline small bucket, ordering without duplicate waits)
+# round-4 GPU call: captured-RCCL regression check (inline small bucket, ordering without duplicate waits), the
+# serial-load fixes (BN partial sums, NMSE prologue) in the step: bench + timeline + full GPU suite
 cd "$(dirname "$0")/.." || exit 1
 R=$(pwd); O=$R/gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_comm_gpu.py tests/test_flagship_gpu.py -v --timeout 200 --timeout-method thread -k "rccl or one_graph" > $O/r4_14_pytest.log 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_comm_gpu.py tests/test_flagship_gpu.py -v --timeout 200 --timeout-method thread -k "rccl or one_graph" > $O/r4_14_pytest.log 2>&1; echo "pytest rc=$?" >> $O/r4_14_pytest.log
+timeout -k 10 300 python bench.py --steps 300 --warmup 20 > $O/r4_14_bench.json 2>$O/r4_14_bench.err || exit 1
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tl_step -o run -- python $R/bench.py --steps 100 --warmup 20 > $O/tl_step.log 2>&1) || exit 1
+python scripts/prof_timeline.py $O/tl_step/run_kernel_trace.csv --marker "conv3x3_kernel<2," --back 5 > $O/r4_14_step_timeline.md
+python scripts/prof_summary.py $O/tl_step/run_kernel_trace.csv --tail 0.6 > $O/r4_14_step_kernel_stats.md; rm -rf $O/tl_step
+timeout -k 10 120 python scripts/stamp_conv.py > $O/r4_14_stamp_conv.txt 2>&1 || exit 1
 QDML_FORCE_DIST=1 timeout -k 10 400 python bench.py --steps 200 --warmup 20 --select-steps 30 > $O/r4_14_bench_forced.json 2>$O/r4_14_bench_forced.err || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/r4_14_pytest_full.log 2>&1; echo "pytest rc=$?" >> $O/r4_14_pytest_full.log
