@@ -1427,9 +1427,11 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restric
     bool ok[UNR];
 #pragma unroll
     for (int k = 0; k < UNR; ++k) {
-      const int r = (it0 + k) * 16 + grp;
-      ok[k] = it0 + k < nit && r < rows;
-      if (!ok[k]) continue;
+      // (branch-free: a row past the end loads row grp -- rows >= CO > grp -- and is not added; guarded loads
+      // compiled to one round trip per row)
+      const int rr = (it0 + k) * 16 + grp;
+      ok[k] = it0 + k < nit && rr < rows;
+      const int r = ok[k] ? rr : grp;
       const int n = n0 + r / CO, c = r % CO, ch = e * CO + c;
       const float* sc = st + ((size_t)u * EC + ch) * NST;
       a[k] = sc[ST_A];
@@ -1445,7 +1447,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restric
     }
 #pragma unroll
     for (int k = 0; k < UNR; ++k) {
-      if (!ok[k]) continue;
+      // (the row sums unconditionally -- a row past the end sums its stand-in and is dropped below: a guarded
+      // body let the compiler sink each row's loads into it, one round trip per row again)
       float tg = 0.f, tgx = 0.f;
 #pragma unroll
       for (int qi = 0; qi < QN; ++qi)
@@ -1455,6 +1458,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restric
           tg += g;
           tgx += g * (zz[k][qi][j] - mu[k]) * inv[k];
         }
+      if (!ok[k]) continue;
       if ((it0 + k) & 1) {
         sg1 += tg;
         sgx1 += tgx;
@@ -1736,10 +1740,12 @@ __device__ __forceinline__ void slab_rows_sum4_body(const float* __restrict__ sl
     // rounds of SR rows with every load of a round issued before its adds (same summation order as a
     // row-at-a-time loop: bit-identical sums)
     for (int r0 = ty; r0 < rows; r0 += 16 * SR) {
+      // (branch-free: a row past the end re-loads row r0 and is not added -- guarded loads compiled to one
+      // round trip each)
       float4 v[SR];
 #pragma unroll
       for (int k = 0; k < SR; ++k)
-        if (r0 + 16 * k < rows) v[k] = *reinterpret_cast<const float4*>(s + (size_t)(r0 + 16 * k) * ld);
+        v[k] = *reinterpret_cast<const float4*>(s + (size_t)(r0 + 16 * k < rows ? r0 + 16 * k : r0) * ld);
 #pragma unroll
       for (int k = 0; k < SR; ++k)
         if (r0 + 16 * k < rows) {

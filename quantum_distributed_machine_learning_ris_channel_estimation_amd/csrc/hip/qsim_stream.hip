@@ -303,9 +303,17 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
       tp[e] = cmul(PL[k & 255], PH[k >> 8]);
     }
   } else {
+    // the whole brick's loads in flight before the first LDS store (a guarded copy loop waited out one
+    // round trip per 16 bytes)
     const cf* si = in + (size_t)s * C::D;
-    for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NT)
-      *reinterpret_cast<float4*>(tp + e) = *reinterpret_cast<const float4*>(si + brick_k(e, br));
+    constexpr int PT = C::AS / (2 * NT);
+    static_assert(C::AS % (2 * NT) == 0, "whole float4 rounds");
+    float4 v[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i)
+      v[i] = *reinterpret_cast<const float4*>(si + brick_k(2 * threadIdx.x + 2 * NT * i, br));
+#pragma unroll
+    for (int i = 0; i < PT; ++i) *reinterpret_cast<float4*>(tp + 2 * threadIdx.x + 2 * NT * i) = v[i];
   }
   __syncthreads();
   float dth[C::AB], dph[C::AB];
