@@ -45,7 +45,41 @@ class JoinLast(FlagshipTrainer):
         self._join(("qsc",))
 
 
-PLANS = {"shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast}
+class ForkAfter(FlagshipTrainer):
+    """As shipped, but the QSC branch's nodes are created AFTER the HDCE chain's first conv launch(es) -- its only
+    dependency is still the gather (an event recorded right after it).  The graph executor keeps a node's first
+    created child on the parent's queue: shipped, that child is the QSC branch and the conv forward hops queues
+    (~13 us after the gather, profiles/r4_14_step_timeline.md); here the conv forward is the first child."""
+    FORK_AT = "conv1"
+
+    def _step_body(self):
+        self._gather()
+        ev = torch.cuda.Event()
+        ev.record()
+        qs = self.streams["qsc"]
+
+        def hook(stage):
+            if stage == self.FORK_AT:
+                qs.wait_event(ev)
+                with torch.cuda.stream(qs):
+                    self._qsc_branch(with_opt=True)
+
+        self.hstep.stage_hook = hook
+        try:
+            self._hdce_forward()
+        finally:
+            self.hstep.stage_hook = None
+        self.hstep.backward_conv()
+        self._join(("qsc",))
+        self._hdce_update()
+
+
+class ForkAfterConv2(ForkAfter):
+    FORK_AT = "conv2"
+
+
+PLANS = {"shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
+         "fork_conv2": ForkAfterConv2}
 
 
 def run(cls, steps):
@@ -63,8 +97,8 @@ def run(cls, steps):
 
 def main(steps):
     want = os.environ.get("PLAN", "all")
-    names = list(PLANS) if want == "all" else [want]
-    for rnd in range(2 if want == "all" else 1):
+    names = list(PLANS) if want == "all" else want.split(",")
+    for rnd in range(2 if len(names) > 1 else 1):
         for n in names:
             ms, tr = run(PLANS[n], steps)
             print(f"{n:12s} {ms:.4f} ms/step  loss {tr.hloss.tolist()[0]:.5f}", flush=True)
