@@ -869,6 +869,10 @@ using WgrD = Geo<4, 8, 2, 2, MC, MC, 3>;            // wgrad 128 x 256, 4 waves 
 using DgrE = Geo<9, 4, 2, 2, KC, MC, 3>;            // dgrad 288 x 128, 4 waves (2 x 2): 256 tiles at the flagship shape
 // direct A (KCD): 4 x 1 waves, the A rows of a wave loaded straight into its registers, only B through LDS
 using FwdDA = Geo<3, 8, 4, 1, KCD, KC, 3>;          // fwd 192 x 128
+// the in-step forward's 192 x 128 tile with a 4-stage ring (exactly the 160 KiB of a CU's LDS): two tiles in flight
+// behind the MFMAs instead of one -- with three stages every K step waits vmcnt(0) for the tile issued one step
+// earlier, one L2 round trip per 64 k
+using FwdB4 = Geo<6, 2, 2, 4, KC, KC, 4>;
 
 }  // namespace gemm
 }  // namespace qd
@@ -876,14 +880,16 @@ using FwdDA = Geo<3, 8, 4, 1, KCD, KC, 3>;          // fwd 192 x 128
 using namespace qd::gemm;
 
 // Which forward config applies to (M, N, K): 1 + cfg, or 0 (unsupported)
-QD_API int qd_gemm_tile_m(int cfg) { return (cfg == 1 || cfg == 3 || cfg == 4 || cfg == 5) ? FwdB::BM : FwdA::BM; }
+QD_API int qd_gemm_tile_m(int cfg) {
+  return (cfg == 1 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 6) ? FwdB::BM : FwdA::BM;
+}
 
 QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (K % BK || N % 128) return 0;
   if (cfg == 101 || cfg == 102) return M % FwdA::BM == 0;
   if (cfg == 0) return M % FwdA::BM == 0;
   if (cfg == 2) return M % FwdC::BM == 0 && K % (2 * BK) == 0;
-  if (cfg == 1) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
+  if (cfg == 1 || cfg == 6) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
   if (cfg == 3 || cfg == 4) return M % FwdD::BM == 0 && N % FwdD::BN == 0;
   if (cfg == 5) return M % FwdDA::BM == 0 && N % FwdDA::BN == 0 && (K / BK) % 2 == 0;
   return 0;
@@ -897,6 +903,7 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   Args a{A, W, K, K, M, N, K, Y, N, bias, {}, expert, E, nullptr};
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
+  if (cfg == 6) return launch<FwdB4, EPI_BF16, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_BF16, 1, 4>(a, st);
   if (cfg == 4) return launch<FwdE, EPI_BF16, 1, 4>(a, st);
   if (cfg == 5) return launch<FwdDA, EPI_BF16, 1, 4>(a, st);
@@ -922,6 +929,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   const int bm = qd_gemm_tile_m(cfg);
   if (M % bm || (bm / (B * E) + 2) * E > 64 || B % 16 || bm % (16 * E)) return (int)hipErrorInvalidValue;
   if (cfg == 1) return launch<FwdB, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 6) return launch<FwdB4, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 4) return launch<FwdE, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 5) return launch<FwdDA, EPI_NMSE, 1, 4>(a, st);

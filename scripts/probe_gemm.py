@@ -58,6 +58,7 @@ def main():
         "fwd_hand3_4x1": lambda: gemm_fwd(A, W, b, out=Y, cfg=3),
         "fwd_hand4_2x2": lambda: gemm_fwd(A, W, b, out=Y, cfg=4),
         "fwd_hand5_directA": lambda: gemm_fwd(A, W, b, out=Y, cfg=5),
+        "fwd_hand6_b4": lambda: gemm_fwd(A, W, b, out=Y, cfg=6),
         "fwd_hand0_noload": lambda: gemm_fwd(A, W, b, out=Y, cfg=101),
         "fwd_hand0_nomfma": lambda: gemm_fwd(A, W, b, out=Y, cfg=102),
         "wgrad_hipblaslt": lambda: torch.mm(dY.t(), A, out_dtype=torch.float32, out=dW),
