@@ -873,6 +873,9 @@ using FwdDA = Geo<3, 8, 4, 1, KCD, KC, 3>;          // fwd 192 x 128
 // behind the MFMAs instead of one -- with three stages every K step waits vmcnt(0) for the tile issued one step
 // earlier, one L2 round trip per 64 k
 using FwdB4 = Geo<6, 2, 2, 4, KC, KC, 4>;
+// the weight gradient likewise: 128 x 128 tiles, 8 waves (2 x 4), 4 stages (128 KiB) -- the 128 x 256 3-stage tile
+// of cfg 1 takes 147 KiB, and a fourth stage would not fit
+using WgrB4 = Geo<4, 2, 2, 4, MC, MC, 4>;
 
 }  // namespace gemm
 }  // namespace qd
@@ -944,6 +947,7 @@ static int tiles_ok(int I, int J, int K) {
 }
 QD_API int qd_gemm_wgrad_ok(int M, int N, int K, int cfg) {
   if (cfg == 1) return tiles_ok<WgrB>(N, K, M);
+  if (cfg == 4) return tiles_ok<WgrB4>(N, K, M);
   if (cfg == 2) return tiles_ok<WgrC>(N, K, M);
   if (cfg == 3) return tiles_ok<WgrD>(N, K, M);
   return tiles_ok<WgrA>(N, K, M);
@@ -964,6 +968,7 @@ QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M
   if (cfg == 1) return launch<WgrB, EPI_F32, 2, 8>(a, st);
   if (cfg == 2) return launch<WgrC, EPI_F32, 2, 8>(a, st);
   if (cfg == 3) return launch<WgrD, EPI_F32, 2, 8>(a, st);
+  if (cfg == 4) return launch<WgrB4, EPI_F32, 2, 8>(a, st);
   return launch<WgrA, EPI_F32, 2, 8>(a, st);
 }
 

@@ -66,6 +66,7 @@ def main():
         "wgrad_hand1": lambda: gemm_wgrad(dY, A, out=dW, cfg=1),
         "wgrad_hand2_ks2": lambda: gemm_wgrad(dY, A, out=dW, cfg=2),
         "wgrad_hand3_2x2": lambda: gemm_wgrad(dY, A, out=dW, cfg=3),
+        "wgrad_hand4_b4": lambda: gemm_wgrad(dY, A, out=dW, cfg=4),
         "dgrad_hipblaslt": lambda: torch.mm(dY, W, out=dA),
         "dgrad_hand0": lambda: gemm_dgrad(dY, W, out=dA, cfg=0),
         "dgrad_hand1": lambda: gemm_dgrad(dY, W, out=dA, cfg=1),

@@ -37,7 +37,7 @@ def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     assert float(Y2[:, :5].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K", [(192, 256, 512), (256, 256, 512), (2304, 2048, 4096)])
 def test_gemm_wgrad_matches_fp32(cuda, cfg, M, N, K):
     if cfg == 2 and M % 128:
