@@ -384,7 +384,10 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
     // ---- stage the (transformed) input tile into LDS, channel-last, with zero halo ----
     if constexpr (PREF) {
       store_group(0);
-      if (n + 1 < nend) load_group(n + 1, 0);
+      // the next sample's loads, branch-free (the last sample re-loads itself, unused): a guarded prefetch made
+      // the compiler copy half-arrived registers at the branch join and wait for the loads right there, before
+      // this sample's MFMAs -- no overlap at all (profiles/r4_12_stamp_conv.txt: ~3500 cycles per sample)
+      load_group(n + 1 < nend ? n + 1 : n, 0);
     } else {
 #pragma unroll 1
       for (int g0 = 0; g0 < ITER; g0 += GR) {
@@ -418,7 +421,10 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
       }
       return a;
     };
-    constexpr int MG = G::MT < 4 ? G::MT : 4;
+    // (with the prefetch in flight: 2 position tiles at a time -- 4 accumulator tiles plus the held next sample
+    // exceed the 256-register budget of 2 workgroups per CU and spill, whose reload waits out the prefetch)
+    constexpr int MGMAX = PREF ? 2 : 4;
+    constexpr int MG = G::MT < MGMAX ? G::MT : MGMAX;
 #pragma unroll
     for (int g0 = 0; g0 < G::MT; g0 += MG) {
       // fused BN reduction: the previous layer's z at this lane's output positions, loaded now so
