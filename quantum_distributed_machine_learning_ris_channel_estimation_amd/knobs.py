@@ -16,7 +16,7 @@ class Knobs:
     # FC GEMMs (train/engine.py HDCEStep): which of forward / wgrad / dgrad run on the hand-written kernels
     # (csrc/hip/gemm.hip; the rest on hipBLASLt), and their tile configurations (forward, wgrad, dgrad)
     hand_gemm: str = "fwdplain,wgrad,dgrad"
-    gemm_cfg: str = "1,1,2"
+    gemm_cfg: str = "6,1,2"
     # fp8 estimator: the hand-written e4m3 forward (else torch._scaled_mm + the NMSE kernel), e4m3 FC gradients
     hand_fp8: bool = True
     f8_bwd: bool = True

@@ -294,13 +294,16 @@ class HDCEStep:
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; knobs.KNOBS.hand_gemm = "": hipBLASLt) and
         # their tile configurations (forward, wgrad, dgrad; knobs.KNOBS.gemm_cfg).  Default: all three hand-written --
-        #   forward  "fwdplain", cfg 1: 192 x 128 tiles (192 workgroups: ~64 CUs stay free for the concurrent QSC
-        #            branch, as hipBLASLt's 234-tile MT128x160 kernel leaves 22), bias-only epilogue, the loss as
+        #   forward  "fwdplain", cfg 6: 192 x 128 tiles on a 4-stage LDS ring (round 4: two tiles in flight behind
+        #            the MFMAs; isolated 43.5 vs 50.2 us for the 3-stage cfg 1, in the step 0.4012 / 0.3999 vs
+        #            0.4070 / 0.4068 ms, profiles/r4_16_*); 192 workgroups, so ~64 CUs stay free for the concurrent
+        #            QSC branch (hipBLASLt's 234-tile MT128x160 kernel leaves 22); bias-only epilogue, the loss as
         #            the separate one-pass NMSE kernel: 0.4095 / 0.4093 vs 0.4092 / 0.4070 ms with hipBLASLt (same
         #            box, profiles/r3_17_fwd192.txt); with 256 tiles (cfg 0 / 2) 0.8-1.3 % slower (r3_16), with the
         #            loss in the GEMM's epilogue ("fwd") 1.5-4 % slower (r3_02, r3_17): it keeps whole CUs from the
         #            QSC backward that then lands on the weight gradient;
-        #   wgrad    cfg 1: 128 x 256 tiles, 8 waves;  dgrad  cfg 2: 144 x 256 tiles, 8 waves along N (0.4115 /
+        #   wgrad    cfg 1: 128 x 256 tiles, 8 waves (the 4-stage 128 x 128 cfg 4: 0.4103 / 0.4109 ms, slower);
+        #   dgrad    cfg 2: 144 x 256 tiles, 8 waves along N (0.4115 /
         #            0.4116 vs 0.4180 / 0.4161 ms with the hipBLASLt data gradient, r3_02_gemm_variants.txt)
         hg = KNOBS.hand_gemm.strip()
         hg = {"1": "fwd,wgrad,dgrad", "all": "fwd,wgrad,dgrad", "0": "", "none": ""}.get(hg, hg)
