@@ -21,6 +21,16 @@
 // Every wave owns its sample from input to output, so waves never wait for each other.
 #include "common.h"
 
+// pins a loaded value at its load site: without a use there, the compiler sinks a batch of loads into the guarded
+// stores that consume them, one round trip each again
+template <typename T>
+__device__ __forceinline__ void keep_loaded(const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "dword values");
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) asm volatile("" ::"v"(w[i]));
+}
+
 namespace qd {
 namespace qsc2 {
 
@@ -882,19 +892,42 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
   float* DP1 = reinterpret_cast<float*>(DZC + B3::DZC);
   float* misc = DP1 + 16 * 32;
   {
-    const int q4 = G::F / 4;
+    const int q4 = G::F / 4, tot = n * q4;
     const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
-    for (int i = threadIdx.x; i < n * q4; i += blockDim.x) {
-      const int j = i / q4, c = i % q4;
-      *reinterpret_cast<float4*>(wl + j * wl_stride(G::F) + 4 * c) = src[i];
+    // (rounds of 4 loads per thread in flight: the one-at-a-time copy loop waited a round trip per float4)
+    for (int i0 = threadIdx.x; i0 < tot; i0 += 4 * blockDim.x) {
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + k * blockDim.x;
+        v[k] = src[i < tot ? i : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) keep_loaded(v[k]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + k * blockDim.x;
+        if (i < tot) *reinterpret_cast<float4*>(wl + (i / q4) * wl_stride(G::F) + 4 * (i % q4)) = v[k];
+      }
     }
     if (w2t_img) {   // this step's image from the forward (qd_qsc2_fwd3): one copy, one round trip
       const uint4* src = reinterpret_cast<const uint4*>(w2t_img);
       uint4* dst = reinterpret_cast<uint4*>(w2t);
+      // (every load issued before the first store -- an index past the end re-loads element 0, not stored: the
+      // guarded copy compiled to one round trip per 4 KiB)
+      constexpr int NCP = (B3::W2T * 2 / 16 + 255) / 256;
+      uint4 v[NCP];
 #pragma unroll
-      for (int k = 0; k < (B3::W2T * 2 / 16 + 255) / 256; ++k) {
+      for (int k = 0; k < NCP; ++k) {
         const int i = threadIdx.x + 256 * k;
-        if (i < B3::W2T * 2 / 16) dst[i] = src[i];
+        v[k] = src[i < B3::W2T * 2 / 16 ? i : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < NCP; ++k) keep_loaded(v[k]);
+#pragma unroll
+      for (int k = 0; k < NCP; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < B3::W2T * 2 / 16) dst[i] = v[k];
       }
     } else
     // W2 [co][ci][tap] -> W2T [tap][ci][co]: iterate in DESTINATION order, two co per dword (in source
