@@ -98,7 +98,7 @@ def run(cls, steps):
 def main(steps):
     want = os.environ.get("PLAN", "all")
     names = list(PLANS) if want == "all" else want.split(",")
-    for rnd in range(2 if len(names) > 1 else 1):
+    for rnd in range(int(os.environ.get("ROUNDS", "2")) if len(names) > 1 else 1):
         for n in names:
             ms, tr = run(PLANS[n], steps)
             print(f"{n:12s} {ms:.4f} ms/step  loss {tr.hloss.tolist()[0]:.5f}", flush=True)
