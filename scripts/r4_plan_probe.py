@@ -78,7 +78,17 @@ class ForkAfterConv2(ForkAfter):
     FORK_AT = "conv2"
 
 
-PLANS = {"shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
+def adam_grid(g):
+    class AdamGrid(FlagshipTrainer):
+        """As shipped, the HDCE update launched on at most ``g`` workgroups (default 2048)."""
+
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            self.hopt.max_grid[0] = g
+    return AdamGrid
+
+
+PLANS = {"adam1024": adam_grid(1024), "adam1536": adam_grid(1536), "shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
          "fork_conv2": ForkAfterConv2}
 
 
