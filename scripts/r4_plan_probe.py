@@ -88,7 +88,27 @@ def adam_grid(g):
     return AdamGrid
 
 
-PLANS = {"adam1024": adam_grid(1024), "adam1536": adam_grid(1536), "shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
+def knobs(**kw):
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
+
+    class WithKnobs(FlagshipTrainer):
+        """As shipped, built under other knobs.KNOBS values (restored after construction)."""
+
+        def __init__(self, *a, **k):
+            old = {n: getattr(KNOBS, n) for n in kw}
+            for n, v in kw.items():
+                setattr(KNOBS, n, v)
+            try:
+                super().__init__(*a, **k)
+            finally:
+                for n, v in old.items():
+                    setattr(KNOBS, n, v)
+    return WithKnobs
+
+
+PLANS = {"fused_loss6": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="6,1,2"),
+         "fused_loss1": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="1,1,2"),
+         "adam1024": adam_grid(1024), "adam1536": adam_grid(1536), "shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
          "fork_conv2": ForkAfterConv2}
 
 
