@@ -69,6 +69,25 @@ def new_unique_id() -> bytes:
     return bytes(buf)
 
 
+class _StdoutToStderr:
+    """fd-level redirect of stdout to stderr: RCCL prints its version banner on stdout at initialisation, and a
+    benchmark's stdout carries exactly one JSON line (bench.py)."""
+
+    def __enter__(self):
+        import sys
+        sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        import sys
+        sys.stdout.flush()
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
 class RcclComm:
     """One rank of an RCCL communicator on ``device``.  ``store``: a c10d Store shared by the ranks
     (the communicator id travels through it under ``key``)."""
@@ -85,7 +104,8 @@ class RcclComm:
         self._gs = nat.fn(L, "qd_comm_group_start", [])
         self._ge = nat.fn(L, "qd_comm_group_end", [])
         if rank == 0:
-            uid = new_unique_id()
+            with _StdoutToStderr():
+                uid = new_unique_id()
             store.set(key, uid)
         else:
             uid = store.get(key)   # (blocks until rank 0 has published it)
@@ -93,7 +113,7 @@ class RcclComm:
         if len(uid) != n:
             raise CommError(f"communicator id of {len(uid)} bytes, expected {n}")
         self.comm = ctypes.c_void_p()
-        with torch.cuda.device(device):
+        with torch.cuda.device(device), _StdoutToStderr():
             st = nat.fn(L, "qd_comm_init", [ctypes.POINTER(ctypes.c_void_p), i, ctypes.c_char_p, i])(
                 ctypes.byref(self.comm), world, uid, rank)
         _check(L, st, f"ncclCommInitRank(rank {rank} of {world})")
