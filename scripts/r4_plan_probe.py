@@ -106,7 +106,26 @@ def knobs(**kw):
     return WithKnobs
 
 
-PLANS = {"fused_loss6": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="6,1,2"),
+class HdceOnly(FlagshipTrainer):
+    """(diagnostic, not a training step) the HDCE chain alone: what the concurrent QSC branch costs it."""
+
+    def _step_body(self):
+        self._gather()
+        self._hdce_forward()
+        self.hstep.backward_conv()
+        self._hdce_update()
+
+
+class QscOnly(FlagshipTrainer):
+    """(diagnostic) the QSC branch alone, on the capturing stream."""
+
+    def _step_body(self):
+        self._gather()
+        self._qsc_branch(with_opt=True)
+
+
+PLANS = {"hdce_only": HdceOnly, "qsc_only": QscOnly,
+         "fused_loss6": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="6,1,2"),
          "fused_loss1": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="1,1,2"),
          "adam1024": adam_grid(1024), "adam1536": adam_grid(1536), "shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
          "fork_conv2": ForkAfterConv2}
