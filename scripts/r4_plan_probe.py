@@ -78,6 +78,10 @@ class ForkAfterConv2(ForkAfter):
     FORK_AT = "conv2"
 
 
+class ForkAfterConv3(ForkAfter):
+    FORK_AT = "conv3"
+
+
 def adam_grid(g):
     class AdamGrid(FlagshipTrainer):
         """As shipped, the HDCE update launched on at most ``g`` workgroups (default 2048)."""
@@ -128,12 +132,14 @@ PLANS = {"hdce_only": HdceOnly, "qsc_only": QscOnly,
          "fused_loss6": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="6,1,2"),
          "fused_loss1": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="1,1,2"),
          "adam1024": adam_grid(1024), "adam1536": adam_grid(1536), "shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
-         "fork_conv2": ForkAfterConv2}
+         "fork_conv2": ForkAfterConv2,
+         "fork_conv3": ForkAfterConv3}
 
 
 def run(cls, steps):
     ctx = DistContext(device=torch.device("cuda", 0))
-    tr = cls(FlagshipConfig(steps_per_graph=10), ctx)
+    tr = cls(FlagshipConfig(steps_per_graph=10, pilot_num=int(os.environ.get("PILOT", "128")),
+                            n_qubits=int(os.environ.get("QUBITS", "8"))), ctx)
     tr.run(20)
     tr.prepare(steps)
     tr.run(30)
