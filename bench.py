@@ -75,9 +75,9 @@ def main() -> int:
     ap.add_argument("--dp-qsc", default="auto", choices=["auto", "g2", "fwd"],
                     help="N > 1, one-graph DP plan: the QSC branch beside the conv backward (g2) or forked after the "
                          "gather (fwd); auto = timed at the real world size with the plans (FlagshipConfig.dp_qsc)")
-    ap.add_argument("--select-steps", type=int, default=10,
-                    help="N > 1, --dp-plan auto: steps timed per candidate plan to choose the faster one (0 = no timing: "
-                         "allreduce with the one-graph step, zero with the 5-graph step)")
+    ap.add_argument("--select-steps", type=int, default=30,
+                    help="N > 1, --dp-plan auto: steps timed per candidate plan to choose the fastest (three "
+                         "10-step replays; 0 = no timing: allreduce with the one-graph step, zero with the 5-graph step)")
     ap.add_argument("--lead-in", type=int, default=1,
                     help="steps replayed one per graph at the start of every run (FlagshipConfig.lead_in)")
     ap.add_argument("--settle-steps", type=int, default=25,
