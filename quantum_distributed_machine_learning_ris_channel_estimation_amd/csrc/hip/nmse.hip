@@ -245,8 +245,9 @@ __global__ void __launch_bounds__(256) nmse_fused_kernel(const TY* __restrict__ 
   // any of them is used (rowoff -> label is the only dependent pair), and the first batch is issued
   // BEFORE the per-stream label powers below, so the whole block pays ~2 memory round trips instead of
   // one per phase (rowden -> barrier -> rowoff -> label, per batch).
-  // (4E rows per round: the step's rpc = 4E rows of a block in ONE round -- one rowoff -> label round trip, not two)
-  constexpr int RT = 4 * E;
+  // (2E rows per round: 4E in one round measured 27.3 vs 16.5 us in the step -- 196 VGPRs halve the occupancy,
+  // profiles/r4_25_step_kernel_stats.md)
+  constexpr int RT = 2 * E;
   const int r1 = r0 + rpc;
   int ro[RT];
   float4 yv[RT], lv[RT], pv[RT];
