@@ -327,3 +327,76 @@ QD_API int qd_fp8_scale_update(float* amax_parts, float* scale, float* qs, int n
 }
 
 QD_API int qd_amax_parts() { return qd::kAmaxParts; }
+
+// ---------------------------------------------------------------------------------------------------------------
+// Probe-only (scripts/r4_adam_probe.py): the Adam update with a bf16 shadow, in access-pattern variants, to find what
+// limits adam_kernel at ~5 TB/s of its 30 bytes per parameter (6.3 TB/s is the measured float4-copy rate).
+//   LNT / SNT: non-temporal loads / stores;  U: parameter quads per thread per round, every load of a round in
+//   flight before its math.  Same arithmetic as adam_kernel (Adam, no weight decay / pruning); n % 4 == 0.
+namespace qd {
+namespace optim {
+template <bool LNT, bool SNT, int U>
+__global__ void __launch_bounds__(256) adam_probe_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v, long n,
+                                                         const float* __restrict__ lr_ptr, const float* step_ptr,
+                                                         AdamArgs a, uint16_t* __restrict__ shadow) {
+  const float lr = *lr_ptr;
+  const float t = *step_ptr + 1.f;
+  const float step_size = lr / (1.f - __powf(a.beta1, t));
+  const float rbc2 = rsqrtf(1.f - __powf(a.beta2, t));
+  const long lane0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long span = (long)gridDim.x * blockDim.x * 4;   // one quad per thread
+  for (long base = lane0; base < n; base += span * U) {
+    float4 pp[U], gg[U], mm[U], vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i0 = base + span * u < n ? base + span * u : lane0;
+      pp[u] = ldv<LNT>(p + i0);
+      gg[u] = ldv<LNT>(g + i0);
+      mm[u] = ldv<LNT>(m + i0);
+      vv[u] = ldv<LNT>(v + i0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i0 = base + span * u;
+      if (i0 >= n) continue;
+      float* pa = &pp[u].x; float* ga = &gg[u].x; float* ma = &mm[u].x; float* va = &vv[u].x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) adam_elem(pa[j], ma[j], va[j], ga[j] * a.grad_scale, a.beta1, a.beta2, a.eps,
+                                            step_size, rbc2);
+      stv<SNT>(p + i0, pp[u]);
+      stv<SNT>(m + i0, mm[u]);
+      stv<SNT>(v + i0, vv[u]);
+      ushort4 h;
+      h.x = f32_to_bf16(pp[u].x);
+      h.y = f32_to_bf16(pp[u].y);
+      h.z = f32_to_bf16(pp[u].z);
+      h.w = f32_to_bf16(pp[u].w);
+      *reinterpret_cast<ushort4*>(shadow + i0) = h;
+    }
+  }
+}
+}  // namespace optim
+}  // namespace qd
+
+QD_API int qd_adam_probe(int variant, float* p, const float* g, float* m, float* v, long n, const float* lr,
+                         const float* step, float beta1, float beta2, float eps, uint16_t* shadow, int grid,
+                         void* stream) {
+  if (n <= 0 || (n & 3) || grid <= 0) return (int)hipErrorInvalidValue;
+  const AdamArgs a{beta1, beta2, eps, 0.f, 1.f, 0.f, 0};
+  hipStream_t st = (hipStream_t)stream;
+#define QD_AP(L, S, U) \
+  hipLaunchKernelGGL((adam_probe_kernel<L, S, U>), dim3(grid), dim3(256), 0, st, p, g, m, v, n, lr, step, a, shadow)
+  switch (variant) {
+    case 0: QD_AP(true, true, 1); break;
+    case 1: QD_AP(true, true, 2); break;
+    case 2: QD_AP(false, true, 1); break;
+    case 3: QD_AP(true, false, 1); break;
+    case 4: QD_AP(false, false, 1); break;
+    case 5: QD_AP(true, true, 4); break;
+    case 6: QD_AP(false, false, 2); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef QD_AP
+  return (int)hipGetLastError();
+}

@@ -50,6 +50,26 @@ def main():
     for g in (1024, 4096, 8192):
         var[f"flush_then_adam_grid{g}"] = (lambda f: lambda: (flush.zero_(), f()))(adam_grid(g))
     var["flush_then_adam_grid2048"] = (lambda f: lambda: (flush.zero_(), f()))(adam_grid(2048))
+    # access-pattern variants of the same update (csrc/hip/optim.hip qd_adam_probe), cold
+    import ctypes
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    vp = ctypes.c_void_p
+    fprobe = nat.fn(nat.hip_lib(), "qd_adam_probe", [ctypes.c_int, vp, vp, vp, vp, ctypes.c_long, vp, vp,
+                                                     ctypes.c_float, ctypes.c_float, ctypes.c_float, vp,
+                                                     ctypes.c_int, vp])
+    shadow = torch.empty(n, device=dev, dtype=torch.bfloat16)
+
+    def probe(variant, grid):
+        def f():
+            flush.zero_()
+            nat.check(fprobe(variant, nat.ptr(space.flat), nat.ptr(space.grad), nat.ptr(opt.m), nat.ptr(opt.v), n,
+                             nat.ptr(opt.lr_t), nat.ptr(opt.step_t), 0.9, 0.999, 1e-8, nat.ptr(shadow), grid,
+                             nat.stream_ptr()), "adam_probe")
+        return f
+    names = {0: "nt_nt_u1", 1: "nt_nt_u2", 2: "ld_nt_u1", 3: "nt_st_u1", 4: "plain_u1", 5: "nt_nt_u4", 6: "plain_u2"}
+    for vnum, nm in names.items():
+        for grid in (2048, 8192):
+            var[f"flush_then_probe_{nm}_g{grid}"] = probe(vnum, grid)
     bytes_adam = n * (4 * 4 + 3 * 4 + 2)
     res = {k: [] for k in var}
     for _ in range(5):
