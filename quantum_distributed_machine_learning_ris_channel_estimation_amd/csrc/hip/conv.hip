@@ -41,6 +41,17 @@ namespace conv {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
+// two floats -> one word of two RNE bf16 (x low): a single v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack_bf16x2(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+// the two floats of a packed bf16 word
+__device__ __forceinline__ f32x2 unpack_bf16x2(uint32_t w) {
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
 
 constexpr int CO = 32;     // output channels of every layer (per expert)
 constexpr int NST = 8;     // floats per (group, channel) BN state record
@@ -250,6 +261,7 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
   float* stl = reinterpret_cast<float*>(wl + KS * 64);                                     // BN params
   // per-lane channel for the output/statistics: column of the MFMA tile
   float s1 = 0.f, s2 = 0.f;
+  f32x2 s1v = {0.f, 0.f}, s2v = {0.f, 0.f};   // (OUT_Z_STATS: packed partial sums, even / odd positions)
   [[maybe_unused]] float ra = 0.f, rb = 0.f, rmu = 0.f, rinv = 0.f;
   const bool fuse_red = DGRAD && OUTM == OUT_BF16 && brd.part != nullptr;
   if (fuse_red) {
@@ -311,6 +323,28 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
       if constexpr (RAWIN) {
         const int c = i / G::HW, p = i % G::HW;
         tile[((p / W + 1) * G::WP + (p % W) + 1) * CINP + c] = (__bf16)rr[k];
+      } else if constexpr (INM == IN_BNRELU && QV == 1) {
+        // the forward's bf16 input, a channel pair at a time: one packed FMA per position for both channels,
+        // a NaN-keeping max per value and one packed bf16 conversion per LDS word -- about half the vector
+        // instructions of the per-value path below, which made the staging VALU-bound (the same values: RNE
+        // rounding of relu(a z + b) either way)
+        const int pr = i % NPAIR, p0 = (i / NPAIR) * 8;
+        const float* s0 = stl + (2 * pr) * NST;
+        const f32x2 a2 = {s0[ST_A], s0[NST + ST_A]}, b2 = {s0[ST_B], s0[NST + ST_B]};
+        const uint32_t w0[4] = {rv[k][0][0].x, rv[k][0][0].y, rv[k][0][0].z, rv[k][0][0].w};
+        const uint32_t w1[4] = {rv[k][1][0].x, rv[k][1][0].y, rv[k][1][0].z, rv[k][1][0].w};
+        const int ph = p0 / W, pw = p0 % W;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t u0 = (j & 1) ? (w0[j >> 1] & 0xffff0000u) : (w0[j >> 1] << 16);
+          const uint32_t u1 = (j & 1) ? (w1[j >> 1] & 0xffff0000u) : (w1[j >> 1] << 16);
+          f32x2 y = f32x2{__uint_as_float(u0), __uint_as_float(u1)} * a2 + b2;
+          y.x = relu_max(y.x);
+          y.y = relu_max(y.y);
+          const int R = ph + 1, C = pw + j + 1;
+          *reinterpret_cast<uint32_t*>(tile + (R * G::WP + C) * CINP + 8 * ((pr >> 2) ^ tile_swz(R, C)) +
+                                       2 * (pr & 3)) = pack_bf16x2(y);
+        }
       } else {
         const int pr = i % NPAIR, p0 = (i / NPAIR) * 8;
         float v2[2][8];
@@ -477,19 +511,21 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
             *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + rbase + 8 * g + 4 * hh) =
                 make_float4(acc[j][4 * g], acc[j][4 * g + 1], acc[j][4 * g + 2], acc[j][4 * g + 3]);
         } else {
-          uint2 pk[4];
+          // packed conversions (one v_cvt_pk_bf16_f32 per two values) and packed statistics sums: the
+          // epilogue's vector instructions sat outside the MFMA stream, one per value or more
+          uint32_t pk[4][2];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const uint16_t h0 = f32_to_bf16(acc[j][4 * g]), h1 = f32_to_bf16(acc[j][4 * g + 1]);
-            const uint16_t h2 = f32_to_bf16(acc[j][4 * g + 2]), h3 = f32_to_bf16(acc[j][4 * g + 3]);
-            pk[g] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
+            pk[g][0] = pack_bf16x2(f32x2{acc[j][4 * g], acc[j][4 * g + 1]});
+            pk[g][1] = pack_bf16x2(f32x2{acc[j][4 * g + 2], acc[j][4 * g + 3]});
             if constexpr (OUTM == OUT_Z_STATS) {   // statistics of the stored (bf16-rounded) values
-              const float v0 = bf(h0), v1 = bf(h1), v2 = bf(h2), v3 = bf(h3);
-              s1 += v0 + v1 + v2 + v3;
-              s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+              const f32x2 v01 = unpack_bf16x2(pk[g][0]), v23 = unpack_bf16x2(pk[g][1]);
+              s1v += v01 + v23;
+              s2v += v01 * v01 + v23 * v23;
             } else if constexpr (DGRAD && OUTM == OUT_BF16) {   // fused BN reduction (stored values)
               if (fuse_red) {
-                const float d[4] = {bf(h0), bf(h1), bf(h2), bf(h3)};
+                const f32x2 d01 = unpack_bf16x2(pk[g][0]), d23 = unpack_bf16x2(pk[g][1]);
+                const float d[4] = {d01.x, d01.y, d23.x, d23.y};
                 const float zz[4] = {__uint_as_float(zq[j][g].x << 16), __uint_as_float(zq[j][g].x & 0xffff0000u),
                                      __uint_as_float(zq[j][g].y << 16), __uint_as_float(zq[j][g].y & 0xffff0000u)};
 #pragma unroll
@@ -503,11 +539,16 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
           }
 #pragma unroll
           for (int q = 0; q < 2; ++q) {   // pair (g = 2q, 2q + 1): half-wave hh stores g = 2q + hh
-            const uint2 send = hh ? pk[2 * q] : pk[2 * q + 1];
-            const uint2 recv = make_uint2(__shfl_xor(send.x, 32), __shfl_xor(send.y, 32));
-            const uint2 mine = hh ? pk[2 * q + 1] : pk[2 * q];
-            const uint4 row = hh ? make_uint4(recv.x, recv.y, mine.x, mine.y) : make_uint4(mine.x, mine.y, recv.x, recv.y);
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + rbase + 8 * (2 * q + hh)) = row;
+            // v_permlane32_swap: the upper half's group 2q goes down, the lower half's group 2q + 1 goes up, so
+            // each lane then holds its 8 consecutive positions (no bpermute through LDS, no selects)
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+              const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * q][w], pk[2 * q + 1][w], false, false);
+              pk[2 * q][w] = r[0];
+              pk[2 * q + 1][w] = r[1];
+            }
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(out) + rbase + 8 * (2 * q + hh)) =
+                make_uint4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
           }
         }
       }
@@ -517,6 +558,8 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
   if constexpr (STAMP) ts[4] = phase_stamp();
   if (OUTM == OUT_Z_STATS || fuse_red) {
     // combine the two half-waves (same channel), then the 4 waves through LDS
+    s1 += s1v.x + s1v.y;
+    s2 += s2v.x + s2v.y;
     s1 += __shfl_xor(s1, 32);
     s2 += __shfl_xor(s2, 32);
     __syncthreads();
@@ -683,6 +726,7 @@ __global__ void __launch_bounds__(256, 2) conv3x3_f8_kernel(const uint16_t* __re
   __syncthreads();
 
   float s1 = 0.f, s2 = 0.f;
+  f32x2 s1v = {0.f, 0.f}, s2v = {0.f, 0.f};
   for (int n = n0; n < nend; ++n) {
     wave_lds_fence();
     stage(n);
@@ -712,27 +756,31 @@ __global__ void __launch_bounds__(256, 2) conv3x3_f8_kernel(const uint16_t* __re
       for (int j = 0; j < MG; ++j) {
         const int mt = g0 + j;
         const size_t rbase = ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + mt * 32;
-        uint2 pk[4];
+        uint32_t pk[4][2];   // (conv3x3_body's packed epilogue)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const uint16_t h0 = f32_to_bf16(acc[j][4 * g] * deq), h1 = f32_to_bf16(acc[j][4 * g + 1] * deq);
-          const uint16_t h2 = f32_to_bf16(acc[j][4 * g + 2] * deq), h3 = f32_to_bf16(acc[j][4 * g + 3] * deq);
-          pk[g] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
-          const float v0 = bf(h0), v1 = bf(h1), v2 = bf(h2), v3 = bf(h3);
-          s1 += v0 + v1 + v2 + v3;
-          s2 += v0 * v0 + v1 * v1 + v2 * v2 + v3 * v3;
+          pk[g][0] = pack_bf16x2(f32x2{acc[j][4 * g], acc[j][4 * g + 1]} * deq);
+          pk[g][1] = pack_bf16x2(f32x2{acc[j][4 * g + 2], acc[j][4 * g + 3]} * deq);
+          const f32x2 v01 = unpack_bf16x2(pk[g][0]), v23 = unpack_bf16x2(pk[g][1]);
+          s1v += v01 + v23;
+          s2v += v01 * v01 + v23 * v23;
         }
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const uint2 send = hh ? pk[2 * q] : pk[2 * q + 1];
-          const uint2 recv = make_uint2(__shfl_xor(send.x, 32), __shfl_xor(send.y, 32));
-          const uint2 mine = hh ? pk[2 * q + 1] : pk[2 * q];
-          const uint4 row = hh ? make_uint4(recv.x, recv.y, mine.x, mine.y) : make_uint4(mine.x, mine.y, recv.x, recv.y);
-          *reinterpret_cast<uint4*>(out + rbase + 8 * (2 * q + hh)) = row;
+#pragma unroll
+          for (int w = 0; w < 2; ++w) {
+            const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * q][w], pk[2 * q + 1][w], false, false);
+            pk[2 * q][w] = r[0];
+            pk[2 * q + 1][w] = r[1];
+          }
+          *reinterpret_cast<uint4*>(out + rbase + 8 * (2 * q + hh)) =
+              make_uint4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
         }
       }
     }
   }
+  s1 += s1v.x + s1v.y;
+  s2 += s2v.x + s2v.y;
   s1 += __shfl_xor(s1, 32);
   s2 += __shfl_xor(s2, 32);
   __syncthreads();
@@ -1249,13 +1297,13 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
       }
       // ---- dgrad epilogue: lane holds input channel l32, positions mt*32 + 8g + 4hh + {0..3} ----
       const size_t rbase = ((size_t)n * E + e) * CO * HW + (size_t)l32 * HW + mt * 32;
-      uint2 pk[4];
+      uint32_t pk[4][2];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const uint16_t h0 = f32_to_bf16(acc[4 * g]), h1 = f32_to_bf16(acc[4 * g + 1]);
-        const uint16_t h2 = f32_to_bf16(acc[4 * g + 2]), h3 = f32_to_bf16(acc[4 * g + 3]);
-        pk[g] = make_uint2(h0 | ((uint32_t)h1 << 16), h2 | ((uint32_t)h3 << 16));
-        const float d[4] = {bf(h0), bf(h1), bf(h2), bf(h3)};
+        pk[g][0] = pack_bf16x2(f32x2{acc[4 * g], acc[4 * g + 1]});
+        pk[g][1] = pack_bf16x2(f32x2{acc[4 * g + 2], acc[4 * g + 3]});
+        const f32x2 d01 = unpack_bf16x2(pk[g][0]), d23 = unpack_bf16x2(pk[g][1]);
+        const float d[4] = {d01.x, d01.y, d23.x, d23.y};
         const float zz[4] = {__uint_as_float(zq[g].x << 16), __uint_as_float(zq[g].x & 0xffff0000u),
                              __uint_as_float(zq[g].y << 16), __uint_as_float(zq[g].y & 0xffff0000u)};
 #pragma unroll
@@ -1266,12 +1314,15 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
         }
       }
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {   // pair (g = 2q, 2q + 1): half-wave hh stores g = 2q + hh
-        const uint2 send = hh ? pk[2 * q] : pk[2 * q + 1];
-        const uint2 recv = make_uint2(__shfl_xor(send.x, 32), __shfl_xor(send.y, 32));
-        const uint2 mine = hh ? pk[2 * q + 1] : pk[2 * q];
-        const uint4 row = hh ? make_uint4(recv.x, recv.y, mine.x, mine.y) : make_uint4(mine.x, mine.y, recv.x, recv.y);
-        *reinterpret_cast<uint4*>(dx + rbase + 8 * (2 * q + hh)) = row;
+      for (int q = 0; q < 2; ++q) {   // pair (g = 2q, 2q + 1): half-wave hh stores g = 2q + hh (conv3x3_body's swap)
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * q][w], pk[2 * q + 1][w], false, false);
+          pk[2 * q][w] = r[0];
+          pk[2 * q + 1][w] = r[1];
+        }
+        *reinterpret_cast<uint4*>(dx + rbase + 8 * (2 * q + hh)) =
+            make_uint4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
       }
     }
   }

@@ -46,6 +46,22 @@ def main():
         d["wave_lifetime_median"] = float((t[:, 5] - t[:, 0]).median())
         d["wave_lifetime_max"] = float((t[:, 5] - t[:, 0]).max())
         out[("dgrad" if dg else "forward_layer2") + f"_spw{spw}"] = d
+    # isolated wall time of the whole stack (3 forward launches + BN tail; backward launches)
+    cs = ConvStackHIP(m, U, B)
+    for _ in range(5):
+        cs.forward(x1, True)
+        cs.backward(dh)
+    for nm, fn in (("forward", lambda: cs.forward(x1, True)), ("backward", lambda: cs.backward(dh))):
+        ts = []
+        for _ in range(30):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b) * 1e3)
+        ts.sort()
+        out[f"isolated_{nm}_us"] = {"median": ts[len(ts) // 2], "min": ts[0]}
     print(json.dumps(out, indent=1))
 
 
