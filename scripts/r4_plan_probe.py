@@ -133,13 +133,18 @@ PLANS = {"hdce_only": HdceOnly, "qsc_only": QscOnly,
          "fused_loss1": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="1,1,2"),
          "adam1024": adam_grid(1024), "adam1536": adam_grid(1536), "shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
          "fork_conv2": ForkAfterConv2,
-         "fork_conv3": ForkAfterConv3}
+         "fork_conv3": ForkAfterConv3,
+         # the FC weight's Adam in the weight-gradient GEMM's epilogue (round 3 measured it slower with the
+         # round-3 plan; re-measured after the join move), on the shipped and the 8-wave K-split wgrad tile
+         "fused_adam": (FlagshipTrainer, {"fused_fc_adam": True}),
+         "fused_adam_w2": (knobs(gemm_cfg="6,2,2"), {"fused_fc_adam": True})}
 
 
 def run(cls, steps):
+    cls, cfgkw = cls if isinstance(cls, tuple) else (cls, {})
     ctx = DistContext(device=torch.device("cuda", 0))
     tr = cls(FlagshipConfig(steps_per_graph=10, pilot_num=int(os.environ.get("PILOT", "128")),
-                            n_qubits=int(os.environ.get("QUBITS", "8"))), ctx)
+                            n_qubits=int(os.environ.get("QUBITS", "8")), **cfgkw), ctx)
     tr.run(20)
     tr.prepare(steps)
     tr.run(30)
