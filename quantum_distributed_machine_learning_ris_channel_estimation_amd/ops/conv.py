@@ -11,7 +11,7 @@ HIP graph.  Gradients are written straight into the model's flat gradient buffer
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional
+from typing import Optional
 
 import torch
 

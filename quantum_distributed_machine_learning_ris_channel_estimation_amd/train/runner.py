@@ -17,7 +17,6 @@ compatibility and tests.
 """
 from __future__ import annotations
 
-import math
 import os
 import time
 from typing import Dict, List, Optional, Tuple

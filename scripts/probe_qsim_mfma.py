@@ -30,7 +30,6 @@ cases = {
                                mf(nat.ptr(x), nat.ptr(w), nat.ptr(ops), nat.ptr(E), B, L, b, nat.ptr(ps), st)),
     "mfma(fwd only)": lambda: mf(nat.ptr(x), nat.ptr(w), nat.ptr(ops), nat.ptr(E), B, L, b, nat.ptr(ps), st),
 }
-import os
 for name, f in cases.items():
     for _ in range(20):
         f()

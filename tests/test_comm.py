@@ -2,7 +2,6 @@
 capture guard -- a graph capture must not begin while a gradient collective is still pending (round 3's
 captured-collective abort, docs/CONCURRENCY.md "captured collectives")."""
 import os
-import sys
 
 import pytest
 import torch
