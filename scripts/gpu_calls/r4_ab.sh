@@ -1,8 +1,8 @@
 #!/bin/bash
 # A/B bench of env-selected variants on one box, alternating, 2 rounds:
-#   VARIANTS="A=1|--flags;B=0|" bash scripts/r4_ab.sh OUTFILE
+#   VARIANTS="A=1|--flags;B=0|" bash scripts/gpu_calls/r4_ab.sh OUTFILE
 set -o pipefail
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 O=${1:-gpurun_out/ab.txt}
 IFS=';' read -ra VS <<< "${VARIANTS:-NONE=0|}"
 for r in 1 2; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-4 GPU call: clock-stamp phase tests, P256 large batch / 16-qubit benches, Adam probe, P256 timeline
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_runtime_gpu.py tests/test_flagship_gpu.py -v --timeout 200 --timeout-method thread -k "clock_stamps or one_graph" > $O/r4_11_stamps.log 2>&1 || exit 1
 QDML_FORCE_DIST=1 timeout -k 10 300 python bench.py --steps 200 --warmup 20 > $O/r4_11_bench_forced_stamps.json 2>$O/r4_11_bench_forced_stamps.err || exit 1

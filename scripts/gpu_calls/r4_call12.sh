@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 GPU call: full GPU suite on the join-before-update plan, bench + step timeline, QSC-gate probe (P256 / P128),
 # 16-qubit bench repeat
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/r4_12_pytest.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/r4_12_pytest.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 GPU call: captured-RCCL regression check (inline small bucket, ordering without duplicate waits), the
 # serial-load fixes (BN partial sums, NMSE prologue) in the step: bench + timeline + full GPU suite
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_comm_gpu.py tests/test_flagship_gpu.py -v --timeout 200 --timeout-method thread -k "rccl or one_graph" > $O/r4_14_pytest.log 2>&1; echo "pytest rc=$?" >> $O/r4_14_pytest.log
 timeout -k 10 300 python bench.py --steps 300 --warmup 20 > $O/r4_14_bench.json 2>$O/r4_14_bench.err || exit 1

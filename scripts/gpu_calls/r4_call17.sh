@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 GPU call: conv forward prefetch rework -- conv numerics + LDS-poison + bit-exact plans, phase stamps, bench +
 # step timeline
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_conv_gpu.py tests/test_lds_poison_gpu.py tests/test_flagship_gpu.py -q --timeout 200 --timeout-method thread > $O/r4_17_pytest.log 2>&1; echo "pytest rc=$?" >> $O/r4_17_pytest.log
 timeout -k 10 120 python scripts/stamp_conv.py > $O/r4_17_stamp_conv.txt 2>&1 || exit 1

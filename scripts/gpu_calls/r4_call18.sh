@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-4 consolidation: full GPU suite, bench, forced-DP bench, P256 / 16-qubit / fp8 benches, step profile
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/r4_18_pytest.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/r4_18_pytest.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-4 GPU call (diagnostic): the HDCE chain alone and the QSC branch alone vs the shipped step, + timelines
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 ROUNDS=2 PLAN=shipped,hdce_only,qsc_only timeout -k 10 400 python scripts/r4_plan_probe.py 400 > $O/r4_22_plans.txt 2>&1 || exit 1
 for p in hdce_only qsc_only; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-4 GPU call: NMSE rows in one round -- numerics + in-step kernel time (compare r4_18_step_kernel_stats.md)
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_flagship_gpu.py -q --timeout 200 --timeout-method thread -k "nmse or bit_exact" > $O/r4_25_pytest.log 2>&1; echo "pytest rc=$?" >> $O/r4_25_pytest.log
 timeout -k 10 300 python bench.py --steps 300 --warmup 20 > $O/r4_25_bench.json 2>$O/r4_25_bench.err || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # conv VALU diet (packed BN/ReLU staging, packed epilogue statistics, permlane32 stores): conv tests, an A/B of
 # the step against the previous library (lib_ab/libqdml_hip_base.so swapped in), and the new step's kernel stats
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out; L=$R/quantum_distributed_machine_learning_ris_channel_estimation_amd/lib
 timeout -k 10 400 python -u -m pytest tests/test_conv_gpu.py tests/test_kernels_gpu.py tests/test_flagship_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/r4_27_pytest.log 2>&1 || exit 1
 cp $L/libqdml_hip.so $R/lib_ab/libqdml_hip_new.so

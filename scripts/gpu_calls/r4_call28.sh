@@ -1,6 +1,6 @@
 #!/bin/bash
 # conv VALU diet: in-kernel phase stamps and isolated stack times, new library vs the previous one
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out; L=$R/quantum_distributed_machine_learning_ris_channel_estimation_amd/lib
 cp $L/libqdml_hip.so $R/lib_ab/libqdml_hip_new.so
 for v in new base new base; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # conv backward staging in packed pairs (dz = c1 g - (k3 z + k0)): conv tests, A/B vs the previous library, timeline
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/r4_30_pytest.log 2>&1 || exit 1
 bash scripts/ab_lib.sh r4_30 3 || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 counter passes over the 1-GPU flagship step (one pass per run, each under its own KILL timeout);
 # PASSES: ';'-separated counter lists.  Output: gpurun_out/<tag>_pmc_summary.md
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 ROOT=$(pwd)
 TAG=${TAG:-pmc}
 OUT=$ROOT/gpurun_out
