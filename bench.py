@@ -80,6 +80,9 @@ def main() -> int:
                          "10-step replays; 0 = no timing: allreduce with the one-graph step, zero with the 5-graph step)")
     ap.add_argument("--lead-in", type=int, default=1,
                     help="steps replayed one per graph at the start of every run (FlagshipConfig.lead_in)")
+    ap.add_argument("--ramp", type=int, default=4,
+                    help="steps of the one replay between the lead-in and the k-step replays (FlagshipConfig.ramp: "
+                         "keeps each graph's host submission behind the previous replay's GPU work; 0 = off)")
     ap.add_argument("--settle-steps", type=int, default=25,
                     help="untimed steps replayed right before the timed region, after the warm-up and the graph "
                          "capture (rounded up to whole graph replays): the first replays of a fresh graph run "
@@ -142,7 +145,8 @@ def main() -> int:
                              data_len=args.data_len, dtype=args.dtype, hip_graphs=not args.no_graphs,
                              use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
                              stream_mode=args.stream_mode, steps_per_graph=args.steps_per_graph,
-                             dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in)
+                             dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in,
+                             ramp=args.ramp)
         return FlagshipTrainer(cfg, ctx, store=store)
 
     def timed(tr: FlagshipTrainer, n: int, settle: int = 0):
@@ -254,6 +258,8 @@ def main() -> int:
             "warmup": args.warmup,
             "settle_steps": settle,
             "lead_in": args.lead_in,
+            "ramp": args.ramp,
+            "replays": tr._reps(args.steps),
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "host_ms_per_step": round(host / args.steps * 1e3, 4),
             "higher_is_better": True,

@@ -176,6 +176,7 @@ class FusedOptimizer:
         # with its own step counter / done counter, so independent ranges can update on different
         # streams as soon as their gradients are final (they always advance together: equal counts)
         self.bounds: List[Tuple[int, int]] = [(0, space.numel)]
+        self.end = space.numel   # stepped range ends here (limit())
         self.max_grid: Dict[int, int] = {}   # part -> workgroup cap of its update launch (0: default)
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
         self.pruned = torch.zeros(1, device=dev, dtype=torch.int32)
@@ -199,13 +200,25 @@ class FusedOptimizer:
 
     def partition(self, cuts: Sequence[int]) -> None:
         """Split the space at the (ALIGN-multiple) offsets ``cuts`` into independently launched parts."""
-        edges = [0] + sorted(int(c) for c in cuts) + [self.space.numel]
+        edges = [0] + sorted(int(c) for c in cuts) + [self.end]
         if any(e % 4 for e in edges) or any(a >= b for a, b in zip(edges, edges[1:])):
             raise ValueError(f"bad partition {edges}")
         self.bounds = list(zip(edges, edges[1:]))
         dev = self.space.flat.device
         self.step_t = self.step_t[:1].repeat(len(self.bounds)).contiguous()
         self.done = torch.zeros(len(self.bounds), device=dev, dtype=torch.int32)
+
+    def limit(self, end: int) -> None:
+        """Step nothing at or past ``end`` (an ALIGN-multiple offset): the space's trailing scratch there holds
+        flags that other kernels read while this optimizer runs (the DP plan's NaN flags ride in the gradient
+        buckets), and a step would rewrite them in place (grad_scale / pruning write the gradient back) and
+        count them in the pruning statistics."""
+        if end % 4 or end <= 0 or end > self.space.numel:
+            raise ValueError(f"limit {end} for a space of {self.space.numel}")
+        if self.bounds[-1][0] >= end:
+            raise ValueError(f"limit {end} would empty the last part {self.bounds[-1]}")
+        self.bounds = [(lo, min(hi, end)) for lo, hi in self.bounds if lo < end]
+        self.end = end
 
     def fuse_range(self, lo: int, hi: int) -> int:
         """Hand [lo, hi) (inside ONE part) to an external update kernel; returns the index of its step / done
@@ -350,7 +363,7 @@ class FusedOptimizer:
 
     def pruned_count(self, steps: int) -> int:
         """Pruned gradient elements over ``steps`` steps (alignment padding excluded; syncs)."""
-        return int(self.pruned.item()) - (self.space.numel - self.space.n_real) * steps
+        return int(self.pruned.item()) - (self.end - self.space.n_real) * steps
 
     def pruning_ratio(self, steps: int) -> float:
         return self.pruned_count(steps) / max(1, self.space.n_real * steps)

@@ -25,7 +25,12 @@ MI355X design:
     every collective a stream-ordered RCCL kernel on a dedicated comm stream, with no
     process group, watchdog thread or work objects (so a HIP graph can capture the
     collectives with nothing polling them: docs/CONCURRENCY.md "captured collectives");
-    "gloo" for CPU runs and the several-ranks-per-GPU rehearsal (torch.distributed).
+    "gloo" for CPU runs and the several-ranks-per-GPU rehearsal (torch.distributed);
+    "torch_nccl" (QDML_DIST_BACKEND=torch_nccl) keeps torch's own ProcessGroupNCCL selectable as a
+    fallback (eager / 5-graph plans only: its watchdog polls events, which a graph capture forbids);
+  * failure detection (rccl): ``parallel/watchdog.py`` -- a thread with no HIP calls watches the
+    heartbeat every completed host sync point bumps and RCCL's async-error state, and on a stall
+    longer than QDML_PG_TIMEOUT or an error aborts the communicator and exits non-zero.
 """
 from __future__ import annotations
 
@@ -51,6 +56,7 @@ class DistContext:
     forced: bool = False   # collectives even at world 1 (QDML_FORCE_DIST=1: rehearses them)
     comm: Optional[object] = None    # (rccl) parallel.comm.RcclComm
     store: Optional[object] = None   # (rccl) the c10d store the communicator id travelled through
+    watchdog: Optional[object] = None   # (rccl) parallel.watchdog.CommWatchdog
     _comm_stream: Optional[object] = None
 
     @property
@@ -78,6 +84,11 @@ class DistContext:
         t.copy_(d.cpu())
         return t
 
+    def heartbeat(self, phase: Optional[str] = None) -> None:
+        """A host sync point completed (the failure detector's heartbeat; ``phase``: what runs next)."""
+        if self.watchdog is not None:
+            self.watchdog.heartbeat(phase)
+
     def barrier(self) -> None:
         if not self.distributed:
             return
@@ -86,8 +97,11 @@ class DistContext:
             x = torch.ones(1, device=self.device)
             self.comm.all_reduce_(x)
             torch.cuda.current_stream(self.device).synchronize()
+        elif self.backend == "torch_nccl":
+            dist.barrier(device_ids=[self.device.index])
         else:
             dist.barrier()
+        self.heartbeat()
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.distributed:
@@ -99,7 +113,10 @@ class DistContext:
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.distributed:
             if self.backend == "rccl":
-                return self._device_op(t, lambda d: self.comm.all_reduce_(d, op))
+                self._device_op(t, lambda d: self.comm.all_reduce_(d, op))
+                if not t.is_cuda:   # (a host result: the collective has completed)
+                    self.heartbeat()
+                return t
             dist.all_reduce(t, op=_GLOO_OPS[op])
         return t
 
@@ -150,11 +167,11 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
     if world > 1 or forced:
         backend = os.environ.get("QDML_DIST_BACKEND") or ("rccl" if use_cuda else "gloo")
         backend = {"nccl": "rccl"}.get(backend, backend)   # (torch's name for it on ROCm)
-        if backend not in ("rccl", "gloo"):
-            raise ValueError(f"QDML_DIST_BACKEND={backend!r}: rccl or gloo")
-        if backend == "rccl":
+        if backend not in ("rccl", "gloo", "torch_nccl"):
+            raise ValueError(f"QDML_DIST_BACKEND={backend!r}: rccl, gloo or torch_nccl")
+        if backend in ("rccl", "torch_nccl"):
             if not use_cuda:
-                raise RuntimeError("the rccl backend needs a GPU")
+                raise RuntimeError(f"the {backend} backend needs a GPU")
             check_local_gpus(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)), torch.cuda.device_count())
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if forced and "MASTER_PORT" not in os.environ:
@@ -168,9 +185,16 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
             # (the env:// rendezvous: torchrun's agent store when there is one, else rank 0 hosts a TCPStore)
             store, _, _ = next(dist.rendezvous("env://", rank=rank, world_size=world, timeout=tmo))
             comm = RcclComm(rank, world, dev, store)
+        elif backend == "torch_nccl":
+            # (the fallback: torch's ProcessGroupNCCL = RCCL on ROCm, with torch's own watchdog)
+            dist.init_process_group("nccl", rank=rank, world_size=world, timeout=tmo, device_id=dev)
         else:
             dist.init_process_group(backend, rank=rank, world_size=world, timeout=tmo)
-    _CTX = DistContext(rank, world, local, dev, backend, forced, comm, store)
+    wd = None
+    if comm is not None and os.environ.get("QDML_WATCHDOG", "1") != "0":
+        from .watchdog import CommWatchdog
+        wd = CommWatchdog(comm, rank, timeout_s, poll_s=float(os.environ.get("QDML_WATCHDOG_POLL", "2"))).start()
+    _CTX = DistContext(rank, world, local, dev, backend, forced, comm, store, wd)
     if comm is not None:
         _CTX.barrier()   # (every rank holds the communicator id: rank 0's store may go)
     return _CTX
@@ -185,6 +209,8 @@ def shutdown() -> None:
     if _CTX is not None:
         if _CTX.comm is not None:
             torch.cuda.synchronize(_CTX.device)
+            if _CTX.watchdog is not None:   # (before the communicator goes: it must not abort a closed one)
+                _CTX.watchdog.stop()
             _CTX.comm.close()
         elif dist.is_initialized():
             dist.destroy_process_group()
@@ -194,11 +220,15 @@ def shutdown() -> None:
 
 
 class _Issued:
-    """(rccl) a launched collective: the event recorded after it and the stream it ran on."""
-    __slots__ = ("event", "stream")
+    """(rccl) a launched collective: the event recorded after it, the stream it ran on, and a process-wide
+    sequence number (the identity GradBuckets' wait dedupe keys on: an id() of a freed event can be reused)."""
+    __slots__ = ("event", "stream", "seq")
+    _next = 0
 
     def __init__(self, event, stream):
         self.event, self.stream = event, stream
+        self.seq = _Issued._next
+        _Issued._next += 1
 
 
 class GradBuckets:
@@ -229,8 +259,9 @@ class GradBuckets:
         # rank and never two of them running at once, so each next collective -- on the comm stream or inline on
         # the caller's stream -- is ordered after it.  Reset once nothing is pending.
         self._last: Optional[_Issued] = None
-        # (rccl) (stream handle, event id) pairs already waited for: under HIP graph capture a stream must not
-        # take the same node as a dependency twice (a duplicate edge crashed hipStreamEndCapture, r4_12)
+        # (rccl) (stream handle, collective sequence number) pairs already waited for: under HIP graph capture a
+        # stream must not take the same node as a dependency twice (a duplicate edge crashed hipStreamEndCapture,
+        # r4_12; docs/CONCURRENCY.md "duplicate dependency edges")
         self._waited = set()
 
     def clear(self) -> None:
@@ -252,7 +283,7 @@ class GradBuckets:
     def _wait_on(self, s, rec: "_Issued") -> None:
         """Make stream ``s`` wait for ``rec`` unless it already does: recorded on ``s`` itself (stream order) or
         waited for before (no duplicate dependency edges under capture)."""
-        key = (s.cuda_stream, id(rec.event))
+        key = (s.cuda_stream, rec.seq)
         if rec.stream.cuda_stream == s.cuda_stream or key in self._waited:
             return
         s.wait_event(rec.event)

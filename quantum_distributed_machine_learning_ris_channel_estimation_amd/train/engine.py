@@ -318,25 +318,37 @@ class HDCEStep:
             self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
 
-    def prime_fp8_dy(self, forward: Callable[[], None], state: Sequence[torch.Tensor], ctx=None) -> bool:
+    def prime_fp8_dy(self, forward: Callable[[], Optional["HDCEStep"]], state: Sequence[torch.Tensor], ctx=None,
+                     engines: Sequence["HDCEStep"] = ()) -> bool:
         """(fp8 estimator with e4m3 FC gradients) seed the delayed scale of the loss gradient dY (fp8 slot 6).
         The loss epilogue quantises dY with the PREVIOUS step's scale, and dY = 2 err / (S den) sits far below
         e4m3's range at the initial unit scale: the first step's FC gradients would underflow.
-        ``forward`` runs one forward + loss pass (this step's bf16-gradient path) on the first batch; max |dY|
-        (max over ranks with ``ctx``) sets the slot; every tensor in ``state`` is restored afterwards, so the
-        run differs from an unprimed one only in slot 6.  Returns whether it primed."""
+        ``forward`` runs one forward + loss pass (this step's bf16-gradient path) on the first batch and returns
+        the engine that ran it -- with several part sizes (runner.py) a rank's part may use another engine than
+        this one -- or None when this rank's part is empty (it then contributes amax 0).  ``engines``: every
+        engine forward may dispatch to (all are switched to bf16 gradients for the pass).  max |dY| (max over
+        ranks with ``ctx``: every rank enters the collective) sets the slot; every tensor in ``state`` is
+        restored afterwards, so the run differs from an unprimed one only in slot 6.  Returns whether it primed."""
         sc = getattr(self.m, "fp8_scales", None)
         if sc is None or not self.hip or not self.f8_bwd:
             return False
+        engs = list(dict.fromkeys([self, *engines]))
         saved = [t.clone() for t in state]
-        self.f8_bwd = False
+        flags = [e.f8_bwd for e in engs]
+        for e in engs:
+            e.f8_bwd = False
         try:
-            forward()
-            amax = self._dYW[0].detach().abs().amax().float().clamp_min(1e-30).view(1)
+            used = forward()
+            if used is None:
+                amax = torch.zeros(1, device=sc.amax.device, dtype=torch.float32)
+            else:
+                amax = used._dYW[0].detach().abs().amax().float().view(1)
             if ctx is not None and ctx.distributed:
                 ctx.all_reduce_(amax, "max")
+            amax = amax.clamp_min(1e-30)
         finally:
-            self.f8_bwd = True
+            for e, f in zip(engs, flags):
+                e.f8_bwd = f
             for t, c in zip(state, saved):
                 t.copy_(c)
         sc.set_from_tensor(6, amax)

@@ -82,6 +82,11 @@ class FlagshipConfig:
     lead_in: int = 1             # run(): the first lead_in steps replayed one step per graph -- a run that starts on
     #                              an idle GPU waits for its first graph's launch to be submitted, and a 1-step graph
     #                              is submitted in a fifth of a k-step one's time
+    ramp: int = 4                # run(): after the lead-in, one ramp-step replay before the k-step ones.  A replay is
+    #                              submitted by the host at ~0.08 ms per step while the GPU runs ~0.4 ms per step, and the
+    #                              GPU starts a replay only once it is submitted: a k-step replay right behind a 1-step
+    #                              one left the GPU idle for (0.08 k - 0.4) ms (0.35 ms of the driver's 20-step window,
+    #                              BENCH_r04.json); behind a ramp-step replay every submission hides (0 = off)
     dp_one_graph: bool = False   # DP plan: capture the whole step -- its RCCL collectives included -- in ONE
     #                              graph (the 5-graph plan launches the collectives between graph replays and
     #                              pays a graph boundary at each; this one pays one per step but fences the
@@ -156,6 +161,12 @@ class FlagshipTrainer(DPPlan):
         self.hdce.attach_fc_shadow(self.hopt, to_end=self.zero)
         self.qopt = make_optimizer(self.qspace, "adamw", cfg.lr, weight_decay=cfg.qsc_weight_decay,
                                    prune_thr=0.1 if cfg.use_gradient_pruning else 0.0)
+        # the NaN flags in the spaces' trailing scratch (below) are read by the update kernels while they run:
+        # neither optimizer steps them (a step writes grad_scale-d / pruned gradients back in place)
+        if dp:
+            self.qopt.limit(self.qspace.extra_off)
+        if self.flag_in_fc:
+            self.hopt.limit(sp.extra_off)
         self.hstep = HDCEStep(self.hdce, self.U, self.B)
         self.hstep.bias_via_conv_slabs = ctx.world == 1 and not cfg.split_graphs
         # NaN guards: the NMSE kernel sets skip[0] (HDCE), the QSC head skip[1]; they travel in the
@@ -253,6 +264,7 @@ class FlagshipTrainer(DPPlan):
         def fwd():
             self._gather(classifier=False)
             self._hdce_forward()
+            return self.hstep
         if self.hstep.prime_fp8_dy(fwd, self.mutable_state() + [self.cur], self.ctx) and self.tail_pack:
             self._tail_pack_launch(advance=False)   # (the packed conv images of the restored weights)
 
@@ -460,13 +472,24 @@ class FlagshipTrainer(DPPlan):
         return max(1, self.cfg.steps_per_graph) if one else 1
 
     def _reps(self, n: int):
-        """Steps per replay of ``run(n)``: lead_in single steps, then k-step replays, then the remainder as ONE
-        replay of a (n - lead_in) % k-step graph (single-step replays cost ~3 % more per step:
-        profiles/r3_12_window.txt)."""
+        """Steps per replay of ``run(n)``: lead_in single steps, one ``ramp``-step replay, then k-step replays, then
+        the remainder as ONE replay of a shorter graph (single-step replays cost ~3 % more per step:
+        profiles/r3_12_window.txt).  Each replay is submitted while the previous one runs, so the ramp keeps every
+        submission behind GPU work (FlagshipConfig.ramp)."""
         k = self._k()
-        lead = min(n, max(0, self.cfg.lead_in)) if k > 1 else 0
-        r = (n - lead) % k
-        return [1] * lead + [k] * ((n - lead) // k) + ([r] if r else [])
+        if k == 1:
+            return [1] * n
+        head = [1] * max(0, self.cfg.lead_in)
+        if head and 1 < self.cfg.ramp < k:
+            head.append(self.cfg.ramp)
+        reps, rem = [], n
+        for r in head:
+            if rem == 0:
+                break
+            reps.append(min(r, rem))
+            rem -= reps[-1]
+        reps += [k] * (rem // k)
+        return reps + ([rem % k] if rem % k else [])
 
     def prepare(self, n: int) -> None:
         """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""

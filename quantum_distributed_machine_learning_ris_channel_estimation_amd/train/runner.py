@@ -351,7 +351,10 @@ class Y2HRunner:
                        if model.fp8_scales is not None else []))
 
         # fp8 estimator: seed the loss gradient's e4m3 scale from a bf16-gradient pass on a first batch
-        step.prime_fp8_dy(lambda: forward(torch.arange(min(B, tr.n), device=ctx.device)), state(), ctx)
+        # (forward returns the engine of this rank's part, or None for an empty part: that rank contributes amax 0
+        # and still enters the max all-reduce, so no rank waits alone)
+        step.prime_fp8_dy(lambda: (forward(torch.arange(min(B, tr.n), device=ctx.device)) or (None,))[0], state(), ctx,
+                          engines=list(steps.values()))
 
         graphed = GraphedStep(lambda: run(static_idx), enabled=self._graphs_on())
         # (reference semantics: one permutation for every rank -- each takes its part of each global batch)
@@ -407,6 +410,7 @@ class Y2HRunner:
             # the epoch's loss over every rank: reference semantics -- shares of one loss (sum); weak -- mean
             ctx.all_reduce_(loss_acc)
             tl = (loss_acc / (max(nb, 1) * (1 if ref else ctx.world))).tolist()
+            ctx.heartbeat(f"hdce epoch {epoch}: validation")   # (failure detector: a sync point completed)
             self.train_HDCE_losses.append(tl[0])
             self._sync_bn_buffers(model)
             nmse, nmse_perf = self.eval_hdce(model, va)
@@ -437,6 +441,7 @@ class Y2HRunner:
                                run_var=[t.cpu() for t in model.run_var], nbt=[t.cpu() for t in model.nbt],
                                train_losses=torch.tensor(self.train_HDCE_losses, dtype=torch.float64),
                                val_nmse=torch.tensor(self.val_HDCE_nmse, dtype=torch.float64), rng=ck.rng_state())
+            ctx.heartbeat(f"hdce epoch {epoch + 1}")
             _maybe_fault(epoch)
         self.hdce_model = model
         return model
@@ -465,7 +470,9 @@ class Y2HRunner:
         ctx.all_reduce_(loss_sum)   # (per-rank val shards may differ in size: divide global sums)
         loss_sum[0] /= loss_sum[3].clamp_min(1)
         model.train()
-        return float(loss_sum[0]), float(loss_sum[1] / loss_sum[2])
+        out = float(loss_sum[0]), float(loss_sum[1] / loss_sum[2])
+        ctx.heartbeat()
+        return out
 
     def _train_classifier(self, model, kind: str, opt_name: str, wd: float, prune_thr: float,
                           on_epoch, histories: Tuple[List, List, List], extra: Optional[Dict] = None):
@@ -565,6 +572,7 @@ class Y2HRunner:
                 nb += 1
             ctx.all_reduce_(loss_acc)   # (the epoch's mean loss over every rank)
             avg = float(loss_acc.item()) / (max(nb, 1) * ctx.world)
+            ctx.heartbeat(f"{kind} epoch {epoch}: validation")
             dt = time.perf_counter() - t0
             train_losses.append(avg)
             self._print(f"Epoch {epoch + 1}/{self.n_epochs}, Average Loss: {avg:.4f}")

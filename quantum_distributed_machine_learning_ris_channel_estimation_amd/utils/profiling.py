@@ -101,6 +101,11 @@ class GraphedStep:
         self.pool = pool
 
     def capture(self) -> None:
+        from ..parallel.watchdog import capturing
+        with capturing():
+            self._capture()
+
+    def _capture(self) -> None:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

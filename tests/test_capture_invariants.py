@@ -1,0 +1,204 @@
+"""Capture invariants of the DP step's collective plumbing (parallel/dp.py GradBuckets, train/flagship_dp.py
+DPPlan._dp_run), on the CPU with stub streams and events.
+
+Round 4 found that a HIP graph capture in which a stream takes the SAME event as a dependency twice crashes
+``hipStreamEndCapture`` (a duplicate edge, gpurun_out/r4_12; docs/CONCURRENCY.md "duplicate dependency
+edges"), and that a capturing stream must never wait on an event recorded before the capture began.  This test
+drives the real ``_dp_run`` through the ZeRO-1 and all-reduce plans, one to three steps per capture (the
+one-graph plan), at simulated world 2 / 4 / 8, and checks both invariants on every ``wait_event``.  It fails if
+GradBuckets._wait_on's dedupe is removed or a capture begins with a collective pending
+(test_dedupe_is_what_keeps_it_clean)."""
+import contextlib
+import itertools
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel import dp as dpmod
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext, GradBuckets
+from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship_dp import DPPlan
+
+
+class Sim:
+    """Stub HIP runtime: streams, events, a current-stream stack and a capture epoch."""
+
+    def __init__(self):
+        self.ids = itertools.count(1)
+        self.epoch = 0            # capture number (0: not capturing)
+        self.waits = []           # (stream id, event id, event epoch, epoch of the wait)
+        self.main = self.Stream("main")
+        self.stack = [self.main]
+
+    def Stream(self, name):
+        sim = self
+
+        class S:
+            def __init__(self):
+                self.name, self.cuda_stream = name, next(sim.ids)
+
+            def wait_event(self, ev):
+                assert ev.recorded, "wait on an event that was never recorded"
+                sim.waits.append((self.cuda_stream, ev.id, ev.epoch, sim.epoch))
+
+            def wait_stream(self, other):   # (torch: records a fresh event on `other`, waits on it)
+                e = sim.Event()
+                e.record(other)
+                self.wait_event(e)
+        return S()
+
+    def Event(self, **kw):
+        sim = self
+
+        class E:
+            def __init__(self):
+                self.id, self.recorded, self.epoch = next(sim.ids), False, None
+
+            def record(self, stream=None):
+                self.recorded, self.epoch = True, sim.epoch
+                self.stream = stream if stream is not None else sim.stack[-1]
+        return E()
+
+    def current_stream(self, device=None):
+        return self.stack[-1]
+
+    @contextlib.contextmanager
+    def stream(self, s):
+        self.stack.append(s)
+        try:
+            yield
+        finally:
+            self.stack.pop()
+
+
+class FakeComm:
+    def __init__(self, log):
+        self.log = log
+
+    def all_reduce_(self, t, op="sum", stream=None):
+        self.log.append(("all_reduce", stream.name))
+        return t
+
+    def reduce_scatter(self, out, inp, stream=None):
+        self.log.append(("reduce_scatter", stream.name))
+        return out
+
+    def all_gather(self, out, inp, stream=None):
+        self.log.append(("all_gather", stream.name))
+        return out
+
+
+def make_plan(sim, world, zero, one_graph=True):
+    ctx = DistContext(rank=world - 1, world=world, backend="rccl", comm=FakeComm([]))
+    ctx._comm_stream = sim.Stream("comm")
+    n_conv, fc = 64, 64 * world
+    grad = torch.zeros(n_conv + fc + 32)
+    flat = torch.zeros_like(grad)
+    bk = {"small": [grad[:n_conv]]}
+    if not zero:
+        bk["fc"] = [grad[n_conv:n_conv + fc]]
+        bk["skip"] = [grad[-1:]]
+    p = DPPlan()
+    p.ctx, p.zero, p.buckets = ctx, zero, GradBuckets(ctx, bk)
+    p._phases = p._stamps = None
+    p.streams = {"fc": sim.Stream("fc"), "qsc": sim.Stream("qsc")}
+    p.cfg = SimpleNamespace(dp_one_graph=one_graph, dp_qsc="g2")
+    p.fc_region = (n_conv, n_conv + fc)
+    p.hdce = SimpleNamespace(space=SimpleNamespace(grad=grad, flat=flat), fc_shadow=None)
+    noop = lambda: None   # noqa: E731
+    # (g2: the QSC branch forked onto its stream and joined back, as the real _dp_g2 does)
+
+    def g2():
+        qs = p.streams["qsc"]
+        qs.wait_stream(sim.current_stream())
+        sim.current_stream().wait_stream(qs)
+    return p, (noop, noop, g2, noop, noop)
+
+
+def capture(sim, plan, gs, k):
+    """One graph capture of k DP steps (GraphedStep: guards first, then the body)."""
+    plan.buckets.assert_quiescent()
+    sim.epoch += 1
+    first = len(sim.waits)
+    for i in range(k):
+        plan._dp_run(*gs, fence=i == k - 1, first=i == 0)
+    assert not plan.buckets.pending
+    return sim.waits[first:]
+
+
+def check(waits):
+    seen = set()
+    for s, e, e_epoch, epoch in waits:
+        assert (s, e) not in seen, "a stream waited twice on the same event inside one capture (duplicate edge)"
+        seen.add((s, e))
+        assert e_epoch == epoch, "a captured wait on an event recorded before the capture began"
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("zero", [True, False])
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_no_duplicate_or_stale_waits(world, zero, k, monkeypatch):
+    sim = Sim()
+    monkeypatch.setattr(torch.cuda, "current_stream", sim.current_stream)
+    monkeypatch.setattr(torch.cuda, "stream", sim.stream)
+    monkeypatch.setattr(torch.cuda, "Event", sim.Event)
+    plan, gs = make_plan(sim, world, zero)
+    for _ in range(3):   # consecutive captures (k-step sets of the same trainer)
+        check(capture(sim, plan, gs, k))
+    ops = [o for o, _ in plan.ctx.comm.log]
+    per_step = ["reduce_scatter", "all_reduce", "all_gather"] if zero else ["all_reduce"] * 3
+    assert ops == per_step * (3 * k)   # (one issue order per step on every rank)
+
+
+def test_dedupe_is_what_keeps_it_clean(monkeypatch):
+    """Without the dedupe the all-reduce plan waits twice on the FC collective's event from main (once as the
+    ordering edge of the inline small-bucket all-reduce, once in wait()); a capture must not begin with a
+    collective pending (assert_quiescent), whose wait would be on an event recorded before the capture."""
+    sim = Sim()
+    monkeypatch.setattr(torch.cuda, "current_stream", sim.current_stream)
+    monkeypatch.setattr(torch.cuda, "stream", sim.stream)
+    monkeypatch.setattr(torch.cuda, "Event", sim.Event)
+    plan, gs = make_plan(sim, 4, zero=False)
+
+    def no_dedupe(self, s, rec):
+        if rec.stream.cuda_stream != s.cuda_stream:
+            s.wait_event(rec.event)
+    monkeypatch.setattr(GradBuckets, "_wait_on", no_dedupe)
+    with pytest.raises(AssertionError, match="duplicate edge"):
+        check(capture(sim, plan, gs, 1))
+    monkeypatch.undo()
+
+    sim = Sim()
+    monkeypatch.setattr(torch.cuda, "current_stream", sim.current_stream)
+    monkeypatch.setattr(torch.cuda, "stream", sim.stream)
+    monkeypatch.setattr(torch.cuda, "Event", sim.Event)
+    plan, gs = make_plan(sim, 4, zero=True)
+    check(capture(sim, plan, gs, 1))
+    plan.buckets.launch("small")   # (eager, outside any capture, and never waited for)
+    with pytest.raises(RuntimeError, match="still pending"):
+        capture(sim, plan, gs, 1)
+    sim.epoch += 1                 # (had the guard let the capture begin, its wait would be on a stale event)
+    n = len(sim.waits)
+    plan.buckets.wait()
+    with pytest.raises(AssertionError, match="before the capture began"):
+        check(sim.waits[n:])
+
+
+@pytest.mark.parametrize("n,k,lead,ramp,want", [
+    (20, 10, 1, 4, [1, 4, 10, 5]),       # the driver's window: every submission behind the previous replay
+    (300, 10, 1, 4, [1, 4] + [10] * 29 + [5]),
+    (30, 10, 1, 4, [1, 4, 10, 10, 5]),   # bench.py's settle run: warms every graph set the 20-step window uses
+    (20, 10, 1, 0, [1, 10, 9]),          # ramp off: round 4's plan
+    (3, 10, 1, 4, [1, 2]),
+    (20, 1, 1, 4, [1] * 20),
+    (25, 10, 0, 4, [10, 10, 5]),
+])
+def test_replay_plan(n, k, lead, ramp, want):
+    """FlagshipTrainer._reps: lead-in single step, one ramp replay, k-step replays, one remainder replay."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import FlagshipTrainer
+    fake = SimpleNamespace(cfg=SimpleNamespace(lead_in=lead, ramp=ramp), _k=lambda: k)
+    got = FlagshipTrainer._reps(fake, n)
+    assert got == want and sum(got) == n
+    # every graph set of the 20-step window is replayed by the 30-step settle run before it
+    if n == 20 and k == 10:
+        assert set(got) <= set(FlagshipTrainer._reps(fake, 30))

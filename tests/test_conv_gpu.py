@@ -164,7 +164,7 @@ COS_BOUND = (0.992, 0.996, 0.9988)
 
 
 def test_hdce_step_hip_vs_torch(cuda):
-    """Whole step (conv kernels + hipBLASLt FC + fused NMSE) vs the fp32 autograd step."""
+    """Whole step (conv kernels + the hand-written FC GEMMs of gemm.hip, the HDCEStep default + fused NMSE) vs the fp32 autograd step."""
     U, B = 3, 64
     a, b = pair(cuda)
     Yp = torch.randn(3, U, B, 2, 16, 8, device=cuda)
