@@ -94,6 +94,11 @@ def main() -> int:
     ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dagq"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, or the QSC branch "
                          "forked off the HDCE chain")
+    ap.add_argument("--fc-adam-side", type=int, default=0,
+                    help="world 1: the FC weight's Adam on a side stream beside the conv backward, capped at this many "
+                         "workgroups (FlagshipConfig.fc_adam_side; 0 = off)")
+    ap.add_argument("--f8-producers", type=int, default=None, choices=[0, 1],
+                    help="fp8 estimator: the e4m3 GEMMs with producer waves (knobs.KNOBS.f8_producers; default: shipped)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -130,9 +135,12 @@ def main() -> int:
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
                                                                                                 FlagshipTrainer)
 
-    if args.gemm_cfg:
+    if args.gemm_cfg or args.f8_producers is not None:
         from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
-        KNOBS.gemm_cfg = args.gemm_cfg
+        if args.gemm_cfg:
+            KNOBS.gemm_cfg = args.gemm_cfg
+        if args.f8_producers is not None:
+            KNOBS.f8_producers = bool(args.f8_producers)
     ctx = init_distributed("auto", timeout_s=int(os.environ.get("QDML_PG_TIMEOUT", "600")))
     if ctx.world != args.gpus:
         print(f"error: --gpus {args.gpus} but the process group has {ctx.world} rank(s)", file=sys.stderr)
@@ -146,7 +154,7 @@ def main() -> int:
                              use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
                              stream_mode=args.stream_mode, steps_per_graph=args.steps_per_graph,
                              dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in,
-                             ramp=args.ramp)
+                             ramp=args.ramp, fc_adam_side=args.fc_adam_side)
         return FlagshipTrainer(cfg, ctx, store=store)
 
     def timed(tr: FlagshipTrainer, n: int, settle: int = 0):
@@ -293,6 +301,7 @@ def main() -> int:
                 "fc_grad_gemms": sorted(tr.hstep.hand_gemm & {"wgrad", "dgrad"}) if tr.hstep.hip else None,
                 "fc_gemm_cfg": list(tr.hstep.gemm_cfg) if tr.hstep.hip else None,
                 "qsim_mfma_forward": bool(getattr(getattr(tr.cstep, "hip", None), "mfma", False)),
+                "fc_adam_side": cfg.fc_adam_side if getattr(tr, "fc_adam_side", False) else 0,
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
             "step_spread": spread,

@@ -122,10 +122,15 @@ struct AdamEpi {
 // per-wave output tile: wave group wk computes sub-step wk (32 k) of every K step, the two partial tiles
 // are summed (in a fixed order) in the epilogue.  Each SIMD then interleaves two waves' MFMA, LDS-read,
 // glds-issue and barrier streams, and each wave issues half the staging pieces per K step.
-template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int DBG_ = 0, int F8_ = 0, int KS_ = 1>
+// PW: producer waves (round 5).  PW > 0 adds PW waves that only issue the global_load_lds pieces of the ring (and
+// wait for them before each K step's barrier); the WM x WN compute waves then issue no vector-memory instruction at
+// all.  An LDS-DMA piece costs its issuing wave ~60 cycles among MFMAs (MI355X_MICROARCH "LDS-DMA piece"), so with
+// the compute waves issuing them a K step of the 192 x 128 tile paid ~600 cycles of issue beside ~768 of MFMA.
+template <int MF_, int NJ_, int WM_, int WN_, int LA_, int LB_, int NSTAGE_, int DBG_ = 0, int F8_ = 0, int KS_ = 1,
+          int PW_ = 0>
 struct Geo {
   static constexpr int MF = MF_, NJ = NJ_, WM = WM_, WN = WN_, LA = LA_, LB = LB_, NSTAGE = NSTAGE_, DBG = DBG_;
-  static constexpr int F8 = F8_, KS = KS_;
+  static constexpr int F8 = F8_, KS = KS_, PW = PW_;
   static_assert(!F8 || ((LA == KC || (F8 == 2 && LA == MC8)) && (LB == KC || (F8 == 2 && LB == MC8))),
                 "e4m3 operands: k-contiguous layouts (MX: also MC8)");
   static_assert((LA != MC8 && LB != MC8) || F8 == 2, "MC8 = e4m3 operands");
@@ -136,11 +141,13 @@ struct Geo {
   static_assert(!ADIR || (WN == 1 && F8 == 0 && KS == 1 && NSTAGE == 3 && (LB == KC || LB == MC)),
                 "direct A: one wave column, bf16, a 3-stage B ring");
   static constexpr bool STEP_LOOP = KS == 2 || MX;   // one fragment set per K step (see gemm_kernel)
-  static constexpr int NW = WM * WN * KS, NT = 64 * NW;
+  static_assert(PW == 0 || !ADIR, "producer waves: the staged loops");
+  static constexpr int NW = WM * WN * KS, NT = 64 * (NW + PW);
+  static constexpr int NLD = PW > 0 ? PW : NW;        // waves that issue the ring's pieces
   static constexpr int BM = 16 * MF * WM, BN = 16 * NJ * WN;
   static constexpr int A_BYTES = ADIR ? 0 : BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   static constexpr int PA = A_BYTES / 1024, PB = B_BYTES / 1024, P = PA + PB;   // 1-KiB pieces per tile
-  static constexpr int NPER = (P + NW - 1) / NW;      // pieces each wave issues per tile
+  static constexpr int NPER = (P + NLD - 1) / NLD;    // pieces each loading wave issues per tile
   static constexpr int PITCH = BN + 4;               // fp32 epilogue tile row pitch
   static constexpr int LDS = (NSTAGE * STAGE > BM * PITCH * 4 + 8192) ? NSTAGE * STAGE : BM * PITCH * 4 + 8192;
   static_assert(LA == KC || LA == KCD || BM % 128 == 0, "MC operand tiles are whole 128-column panels");
@@ -354,7 +361,7 @@ struct Stager {
                                        int wave, int lane, const long* pexp, int pe) {
 #pragma unroll
     for (int it = 0; it < G::NPER; ++it) {
-      int q = wave + it * G::NW;
+      int q = wave + it * G::NLD;
       q = q < G::P ? q : G::P - 1;
       const bool isA = q < G::PA;
       const int qq = isA ? q : q - G::PA;
@@ -524,14 +531,42 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
   constexpr int NS = G::NSTAGE;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   Stager<G> stg;
-  stg.init(a.P, a.ldp, a.Q, a.ldq, i0, j0, __builtin_amdgcn_readfirstlane(wave), lane, a.pexp, a.pe);
+  if constexpr (G::PW > 0) {
+    if (wave >= G::NW) {
+      // producer wave: the compute waves' barrier schedule (one in the prologue, one per K step but the last),
+      // each barrier preceded by the wait that publishes the tile the compute waves read next; then it ends (an
+      // ended wave no longer counts at a workgroup barrier, so the epilogue's barriers are the compute waves')
+      stg.init(a.P, a.ldp, a.Q, a.ldq, i0, j0, __builtin_amdgcn_readfirstlane(wave - G::NW), lane, a.pexp, a.pe);
+      for (int t = 0; t < NS - 1 && t < nk; ++t) stg.issue(smem + t * G::STAGE);
+      vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
+      __builtin_amdgcn_s_barrier();
+      // (the KS = 1 loop has nk - 1 K-step barriers, the one-fragment-set-per-step loop nk: the waits publish
+      // tile t + 1 before barrier t either way)
+      const int steps = G::STEP_LOOP ? nk : nk - 1;
+      int t = 0;
+      for (; t < nk - (NS - 1); ++t) {
+        vm_wait<G>(NS - 3 < 0 ? 0 : NS - 3);
+        __builtin_amdgcn_s_barrier();
+        stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
+      }
+      for (; t < steps; ++t) {
+        vm_wait<G>(nk - 2 - t);
+        __builtin_amdgcn_s_barrier();
+      }
+      return;
+    }
+  } else {
+    stg.init(a.P, a.ldp, a.Q, a.ldq, i0, j0, __builtin_amdgcn_readfirstlane(wave), lane, a.pexp, a.pe);
+  }
   Readers<G> rd;
   rd.ra.init(0, wm * G::MF * 16, fr, fq);
   rd.rb.init(G::A_BYTES, wn * G::NJ * 16, fr, fq);
   // prologue: tiles 0 .. NS-2 in flight; wait for tile 0; its first fragments (the direct-A loop has its own)
   if constexpr (!G::ADIR) {
-    for (int t = 0; t < NS - 1 && t < nk; ++t) stg.issue(smem + t * G::STAGE);
-    vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
+    if constexpr (G::PW == 0) {
+      for (int t = 0; t < NS - 1 && t < nk; ++t) stg.issue(smem + t * G::STAGE);
+      vm_wait<G>((NS - 1 < nk ? NS - 1 : nk) - 1);
+    }
     __builtin_amdgcn_s_barrier();
   }
   Frags<G> f0, f1;
@@ -548,9 +583,10 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     auto step = [&](int t, auto refill, int ahead) {
       const uint32_t cur = lds0 + (t % NS) * G::STAGE, nxt = lds0 + ((t + 1) % NS) * G::STAGE;
       rd.template mma_read<true>(acc, f0, f1, cur, 1);
-      if constexpr (G::DBG != 1) vm_wait<G>(ahead);
+      if constexpr (G::DBG != 1 && G::PW == 0) vm_wait<G>(ahead);
       __builtin_amdgcn_s_barrier();
-      if constexpr (decltype(refill)::value && G::DBG != 1) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
+      if constexpr (decltype(refill)::value && G::DBG != 1 && G::PW == 0)
+        stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
       __builtin_amdgcn_sched_barrier(0);
       rd.template mma_read<true>(acc, f1, f0, nxt, 0);
     };
@@ -574,9 +610,9 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     rd.read_a(f0, lds0, sk);
     auto step = [&](int t, Frags<G>& cur, Frags<G>& nxt) __attribute__((always_inline)) {
       const int ahead = nk - 2 - t < NS - 3 ? nk - 2 - t : NS - 3;
-      if constexpr (G::DBG != 1) vm_wait<G>(ahead);
+      if constexpr (G::DBG != 1 && G::PW == 0) vm_wait<G>(ahead);
       __builtin_amdgcn_s_barrier();
-      if (G::DBG != 1 && t + NS - 1 < nk) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
+      if (G::DBG != 1 && G::PW == 0 && t + NS - 1 < nk) stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
       __builtin_amdgcn_sched_barrier(0);
       rd.template mma_read<true>(acc, cur, nxt, lds0 + ((t + 1) % NS) * G::STAGE, sk);
     };
@@ -876,6 +912,21 @@ using FwdB4 = Geo<6, 2, 2, 4, KC, KC, 4>;
 // the weight gradient likewise: 128 x 128 tiles, 8 waves (2 x 4), 4 stages (128 KiB) -- the 128 x 256 3-stage tile
 // of cfg 1 takes 147 KiB, and a fourth stage would not fit
 using WgrB4 = Geo<4, 2, 2, 4, MC, MC, 4>;
+// round 5: producer waves (PW = 4, one per SIMD) issue the ring's LDS-DMA pieces; the compute waves only read LDS
+// and issue MFMAs
+using FwdP = Geo<6, 4, 2, 2, KC, KC, 4, 0, 0, 1, 4>;    // fwd 192 x 128, 2 x 2 compute waves (96 x 64), 4 stages
+using FwdP3 = Geo<6, 4, 2, 2, KC, KC, 3, 0, 0, 1, 4>;   // the same, 3 stages
+using FwdQ = Geo<9, 2, 1, 4, KC, KC, 4, 0, 0, 1, 4>;    // fwd 144 x 128 (256 tiles), 1 x 4 compute waves (144 x 32)
+using FwdR = Geo<6, 2, 2, 4, KC, KC, 4, 0, 0, 1, 4>;    // fwd 192 x 128, 2 x 4 compute waves (the cfg 6 tile) + 4
+using WgrP = Geo<8, 4, 2, 2, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 256 x 128 (256 tiles), 2 x 2 compute waves (128 x 64)
+using WgrQ = Geo<4, 8, 2, 2, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 2 compute waves (64 x 128)
+using WgrR = Geo<4, 4, 2, 4, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 4 compute waves (the cfg 1 tile) + 4
+using DgrP = Geo<9, 4, 1, 4, KC, MC, 3, 0, 0, 1, 4>;    // dgrad 144 x 256 (256 tiles), 1 x 4 compute waves (144 x 64)
+using DgrQ = Geo<9, 2, 1, 8, KC, MC, 3, 0, 0, 1, 4>;    // dgrad 144 x 256, 1 x 8 compute waves (the cfg 2 tile) + 4
+// the fp8 estimator's e4m3 MX GEMMs with producer waves (the FwdM8 / WgrM8C / DgrM8C tiles + 4 loading waves)
+using FwdM8P = Geo<9, 2, 1, 4, KC, KC, 4, 0, 2, 1, 4>;
+using WgrM8CP = Geo<4, 4, 2, 4, MC8, MC8, 3, 0, 2, 1, 4>;
+using DgrM8CP = Geo<9, 2, 1, 4, KC, MC8, 4, 0, 2, 1, 4>;
 
 }  // namespace gemm
 }  // namespace qd
@@ -884,7 +935,8 @@ using namespace qd::gemm;
 
 // Which forward config applies to (M, N, K): 1 + cfg, or 0 (unsupported)
 QD_API int qd_gemm_tile_m(int cfg) {
-  return (cfg == 1 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 6) ? FwdB::BM : FwdA::BM;
+  return (cfg == 1 || cfg == 3 || cfg == 4 || cfg == 5 || cfg == 6 || cfg == 7 || cfg == 9 || cfg == 10) ? FwdB::BM
+                                                                                                      : FwdA::BM;
 }
 
 QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
@@ -892,7 +944,8 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (cfg == 101 || cfg == 102) return M % FwdA::BM == 0;
   if (cfg == 0) return M % FwdA::BM == 0;
   if (cfg == 2) return M % FwdC::BM == 0 && K % (2 * BK) == 0;
-  if (cfg == 1 || cfg == 6) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
+  if (cfg == 1 || cfg == 6 || cfg == 7 || cfg == 9 || cfg == 10) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
+  if (cfg == 8) return M % FwdQ::BM == 0 && N % FwdQ::BN == 0;
   if (cfg == 3 || cfg == 4) return M % FwdD::BM == 0 && N % FwdD::BN == 0;
   if (cfg == 5) return M % FwdDA::BM == 0 && N % FwdDA::BN == 0 && (K / BK) % 2 == 0;
   return 0;
@@ -907,6 +960,10 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   hipStream_t st = (hipStream_t)stream;
   if (cfg == 1) return launch<FwdB, EPI_BF16, 1, 4>(a, st);
   if (cfg == 6) return launch<FwdB4, EPI_BF16, 1, 4>(a, st);
+  if (cfg == 7) return launch<FwdP, EPI_BF16, 1, 4>(a, st);
+  if (cfg == 8) return launch<FwdQ, EPI_BF16, 4, 8>(a, st);
+  if (cfg == 9) return launch<FwdP3, EPI_BF16, 1, 4>(a, st);
+  if (cfg == 10) return launch<FwdR, EPI_BF16, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_BF16, 1, 4>(a, st);
   if (cfg == 4) return launch<FwdE, EPI_BF16, 1, 4>(a, st);
   if (cfg == 5) return launch<FwdDA, EPI_BF16, 1, 4>(a, st);
@@ -933,6 +990,10 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   if (M % bm || (bm / (B * E) + 2) * E > 64 || B % 16 || bm % (16 * E)) return (int)hipErrorInvalidValue;
   if (cfg == 1) return launch<FwdB, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 6) return launch<FwdB4, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 7) return launch<FwdP, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 8) return launch<FwdQ, EPI_NMSE, 4, 8>(a, st);
+  if (cfg == 9) return launch<FwdP3, EPI_NMSE, 1, 4>(a, st);
+  if (cfg == 10) return launch<FwdR, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 4) return launch<FwdE, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 5) return launch<FwdDA, EPI_NMSE, 1, 4>(a, st);
@@ -947,6 +1008,9 @@ static int tiles_ok(int I, int J, int K) {
 }
 QD_API int qd_gemm_wgrad_ok(int M, int N, int K, int cfg) {
   if (cfg == 1) return tiles_ok<WgrB>(N, K, M);
+  if (cfg == 5) return tiles_ok<WgrP>(N, K, M);
+  if (cfg == 6) return tiles_ok<WgrQ>(N, K, M);
+  if (cfg == 7) return tiles_ok<WgrR>(N, K, M);
   if (cfg == 4) return tiles_ok<WgrB4>(N, K, M);
   if (cfg == 2) return tiles_ok<WgrC>(N, K, M);
   if (cfg == 3) return tiles_ok<WgrD>(N, K, M);
@@ -954,6 +1018,8 @@ QD_API int qd_gemm_wgrad_ok(int M, int N, int K, int cfg) {
 }
 QD_API int qd_gemm_dgrad_ok(int M, int N, int K, int cfg) {
   if (cfg == 1) return tiles_ok<DgrB>(M, K, N);
+  if (cfg == 5) return tiles_ok<DgrP>(M, K, N);
+  if (cfg == 6) return tiles_ok<DgrQ>(M, K, N);
   if (cfg == 2) return tiles_ok<DgrC>(M, K, N);
   if (cfg == 3) return tiles_ok<DgrD>(M, K, N);
   if (cfg == 4) return tiles_ok<DgrE>(M, K, N);
@@ -969,6 +1035,9 @@ QD_API int qd_gemm_wgrad(const uint16_t* dY, const uint16_t* A, float* dW, int M
   if (cfg == 2) return launch<WgrC, EPI_F32, 2, 8>(a, st);
   if (cfg == 3) return launch<WgrD, EPI_F32, 2, 8>(a, st);
   if (cfg == 4) return launch<WgrB4, EPI_F32, 2, 8>(a, st);
+  if (cfg == 5) return launch<WgrP, EPI_F32, 4, 8>(a, st);
+  if (cfg == 6) return launch<WgrQ, EPI_F32, 2, 8>(a, st);
+  if (cfg == 7) return launch<WgrR, EPI_F32, 2, 8>(a, st);
   return launch<WgrA, EPI_F32, 2, 8>(a, st);
 }
 
@@ -995,6 +1064,8 @@ QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, in
   if (cfg == 2) return launch<DgrC, EPI_BF16, 4, 4>(a, st);
   if (cfg == 3) return launch<DgrD, EPI_BF16, 4, 4>(a, st);
   if (cfg == 4) return launch<DgrE, EPI_BF16, 2, 4>(a, st);
+  if (cfg == 5) return launch<DgrP, EPI_BF16, 4, 4>(a, st);
+  if (cfg == 6) return launch<DgrQ, EPI_BF16, 4, 4>(a, st);
   return launch<DgrA, EPI_BF16, 4, 4>(a, st);
 }
 
@@ -1020,9 +1091,10 @@ QD_API int qd_gemm_fwd_nmse_f8(const uint8_t* A8, const uint8_t* W8, const float
   if (M % FwdA8::BM || (FwdA8::BM / (B * E) + 2) * E > 64 || B % 16 || FwdA8::BM % (16 * E))
     return (int)hipErrorInvalidValue;
   // the dY amax partials go to amax8[blockIdx.x]: the 1-D grid must fit the kAmaxParts slots of slot 6
-  const long tiles = cfg == 1 ? (long)(M / FwdM8::BM) * ((N + FwdM8::BN - 1) / FwdM8::BN)
+  const long tiles = cfg >= 1 ? (long)(M / FwdM8::BM) * ((N + FwdM8::BN - 1) / FwdM8::BN)
                               : (long)(M / FwdA8::BM) * ((N + FwdA8::BN - 1) / FwdA8::BN);
   if (dY8 != nullptr && tiles > qd::kAmaxParts) return (int)hipErrorInvalidValue;
+  if (cfg == 2) return launch<FwdM8P, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
   if (cfg == 1) return launch<FwdM8, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
   return launch<FwdA8, EPI_NMSE, 4, 8>(a, (hipStream_t)stream);
 }
@@ -1034,6 +1106,7 @@ QD_API int qd_gemm_fwd_bias_f8(const uint8_t* A8, const uint8_t* W8, const float
   const int K2 = K / 2;
   Args a{reinterpret_cast<const uint16_t*>(A8), reinterpret_cast<const uint16_t*>(W8), K2, K2, M, N, K2, Y, N, bias, {},
          nullptr, 0, deq};
+  if (cfg == 2) return launch<FwdM8P, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
   if (cfg == 1) return launch<FwdM8, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
   return launch<FwdA8, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
 }
@@ -1099,19 +1172,22 @@ QD_API int qd_transpose_u8(const uint8_t* src, uint8_t* dst, int R, int C, void*
 // The fp8 estimator's backward GEMMs straight from the row-major e4m3 tensors (MC8 operands, no transposed
 // copies).  sdy / sa / sw: device dequantisation scales.  M % 256 == 0 (wgrad), N % 256 == 0 (dgrad).
 // dW (N, K) fp32 (row stride ldw) = sdy sa dY8^T A8: dY8 (M, N), A8 (M, K)
+// cfg 1: the same tiles with producer waves
 QD_API int qd_gemm_wgrad_f8(const uint8_t* dY8, const uint8_t* A8, const float* sdy, const float* sa, float* dW, int M,
-                            int N, int K, int ldw, void* stream) {
+                            int N, int K, int ldw, int cfg, void* stream) {
   if (M % 256 || N % 128 || K % 256 || !sdy || !sa) return (int)hipErrorInvalidValue;
   Args a{reinterpret_cast<const uint16_t*>(dY8), reinterpret_cast<const uint16_t*>(A8), N / 2, K / 2, N, K, M / 2,
          dW, ldw, nullptr, {}, nullptr, 0, sdy, {}, sa};
+  if (cfg == 1) return launch<WgrM8CP, EPI_F32, 2, 8>(a, (hipStream_t)stream);
   return launch<WgrM8C, EPI_F32, 2, 8>(a, (hipStream_t)stream);
 }
 // dA (M, K) bf16 = sdy sw dY8 W8: dY8 (M, N), W8 (N, K)
 QD_API int qd_gemm_dgrad_f8(const uint8_t* dY8, const uint8_t* W8, const float* sdy, const float* sw, uint16_t* dA, int M,
-                            int N, int K, void* stream) {
+                            int N, int K, int cfg, void* stream) {
   if (N % 256 || M % 144 || K % 128 || !sdy || !sw) return (int)hipErrorInvalidValue;
   Args a{reinterpret_cast<const uint16_t*>(dY8), reinterpret_cast<const uint16_t*>(W8), N / 2, K / 2, M, K, N / 2,
          dA, K, nullptr, {}, nullptr, 0, sdy, {}, sw};
+  if (cfg == 1) return launch<DgrM8CP, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
   return launch<DgrM8C, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
 }
 

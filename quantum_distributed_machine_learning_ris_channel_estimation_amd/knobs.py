@@ -14,12 +14,16 @@ from dataclasses import dataclass
 @dataclass
 class Knobs:
     # FC GEMMs (train/engine.py HDCEStep): which of forward / wgrad / dgrad run on the hand-written kernels
-    # (csrc/hip/gemm.hip; the rest on hipBLASLt), and their tile configurations (forward, wgrad, dgrad)
+    # (csrc/hip/gemm.hip; the rest on hipBLASLt), and their tile configurations (forward, wgrad, dgrad).
+    # 8,7,6 (round 5) = the producer-wave tiles: isolated 33.0 / 38.8 / 35.1 us against 40.3 / 42.2 / 35.8 for round
+    # 4's 6,1,2; in the step 0.3958-0.3967 against 0.3992-0.4025 ms (profiles/r5_02_gemm_probe.txt, r5_03_ab.txt)
     hand_gemm: str = "fwdplain,wgrad,dgrad"
-    gemm_cfg: str = "6,1,2"
+    gemm_cfg: str = "8,7,6"
     # fp8 estimator: the hand-written e4m3 forward (else torch._scaled_mm + the NMSE kernel), e4m3 FC gradients
     hand_fp8: bool = True
     f8_bwd: bool = True
+    # the e4m3 GEMMs with producer waves (gemm.hip Geo PW = 4: loading waves beside the MFMA waves)
+    f8_producers: bool = False
     # e4m3 convs for layers 2 / 3 of the fp8 estimator (opt-in: a net loss in the step, profiles/r2_14_*)
     fp8_conv: bool = False
     # the 8-qubit circuit forward on the matrix cores (csrc/hip/qsim_mfma.hip; else the register kernel)

@@ -110,12 +110,13 @@ def gemm_fwd_f8(A8: torch.Tensor, W8: torch.Tensor, deq: torch.Tensor, b: Option
                 out: Optional[torch.Tensor] = None, cfg: int = 1) -> torch.Tensor:
     """Y (M, N) bf16 = deq[0] deq[1] A8 W8^T (+ b): OCP e4m3 operands (torch.float8_e4m3fn, row-major,
     K % 128 == 0), fp32 accumulation (csrc/hip/gemm.hip qd_gemm_fwd_bias_f8).  cfg 1: the MX-scaled
-    MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales, K % 256 == 0); 0: mfma_f32_16x16x32_fp8_fp8."""
+    MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales, K % 256 == 0); 2: the same with producer waves;
+    0: mfma_f32_16x16x32_fp8_fp8."""
     M, K = A8.shape
     N = W8.shape[0]
     assert A8.dtype == W8.dtype == torch.float8_e4m3fn and A8.is_contiguous() and W8.is_contiguous()
     assert deq.dtype == torch.float32 and deq.numel() >= 2
-    if cfg == 1 and K % 256:
+    if cfg >= 1 and K % 256:
         cfg = 0
     Y = out if out is not None else torch.empty(M, N, device=A8.device, dtype=torch.bfloat16)
     f = _gemm_fn("qd_gemm_fwd_bias_f8", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
@@ -152,31 +153,32 @@ def transpose_u8(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch
 
 
 def gemm_wgrad_f8(dY8: torch.Tensor, A8: torch.Tensor, s_dy: torch.Tensor, s_a: torch.Tensor,
-                  out: torch.Tensor) -> torch.Tensor:
+                  out: torch.Tensor, cfg: int = 0) -> torch.Tensor:
     """dW (N, K) fp32 = s_dy s_a dY8^T A8 from the row-major e4m3 dY8 (M, N) and A8 (M, K) (MX-scaled MFMA, both
-    operands read i-contiguous through ds_read_b64_tr_b8: csrc/hip/gemm.hip qd_gemm_wgrad_f8).  M % 256 == 0."""
+    operands read i-contiguous through ds_read_b64_tr_b8: csrc/hip/gemm.hip qd_gemm_wgrad_f8).  M % 256 == 0.
+    cfg 1: the same tiles with producer waves."""
     M, N = dY8.shape
     K = A8.shape[1]
     assert dY8.dtype == A8.dtype == torch.float8_e4m3fn and dY8.is_contiguous() and A8.is_contiguous()
     assert A8.shape[0] == M and out.dtype == torch.float32 and out.shape == (N, K) and out.stride(1) == 1
-    f = _gemm_fn("qd_gemm_wgrad_f8", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
-    nat.check(f(nat.ptr(dY8), nat.ptr(A8), nat.ptr(s_dy), nat.ptr(s_a), nat.ptr(out), M, N, K, out.stride(0),
+    f = _gemm_fn("qd_gemm_wgrad_f8", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(dY8), nat.ptr(A8), nat.ptr(s_dy), nat.ptr(s_a), nat.ptr(out), M, N, K, out.stride(0), cfg,
                 nat.stream_ptr(dY8.device)), "gemm_wgrad_f8")
     return out
 
 
 def gemm_dgrad_f8(dY8: torch.Tensor, W8: torch.Tensor, s_dy: torch.Tensor, s_w: torch.Tensor,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, cfg: int = 0) -> torch.Tensor:
     """dA (M, K) bf16 = s_dy s_w dY8 W8 from the row-major e4m3 dY8 (M, N) and W8 (N, K) (csrc/hip/gemm.hip
-    qd_gemm_dgrad_f8).  N % 256 == 0, M % 144 == 0."""
+    qd_gemm_dgrad_f8).  N % 256 == 0, M % 144 == 0.  cfg 1: the same tiles with producer waves."""
     M, N = dY8.shape
     K = W8.shape[1]
     assert dY8.dtype == W8.dtype == torch.float8_e4m3fn and dY8.is_contiguous() and W8.is_contiguous()
     assert W8.shape[0] == N
     dA = out if out is not None else torch.empty(M, K, device=dY8.device, dtype=torch.bfloat16)
     assert dA.dtype == torch.bfloat16 and dA.shape == (M, K) and dA.is_contiguous()
-    f = _gemm_fn("qd_gemm_dgrad_f8", [_p, _p, _p, _p, _p, _i, _i, _i, _p])
-    nat.check(f(nat.ptr(dY8), nat.ptr(W8), nat.ptr(s_dy), nat.ptr(s_w), nat.ptr(dA), M, N, K,
+    f = _gemm_fn("qd_gemm_dgrad_f8", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(dY8), nat.ptr(W8), nat.ptr(s_dy), nat.ptr(s_w), nat.ptr(dA), M, N, K, cfg,
                 nat.stream_ptr(dY8.device)), "gemm_dgrad_f8")
     return dA
 

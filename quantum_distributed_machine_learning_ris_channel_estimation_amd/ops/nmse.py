@@ -25,6 +25,7 @@ from typing import Optional, Tuple
 import torch
 
 from .. import _native as nat
+from ..knobs import KNOBS
 
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
@@ -259,7 +260,7 @@ class StreamNMSE:
         f8cfg = 0
         if f8:
             # (the e4m3 kernels have the cfg-0 tile; f8 cfg 1 = the MX-scaled MFMA when K allows)
-            f8cfg = 1 if K % 256 == 0 else 0
+            f8cfg = (2 if KNOBS.f8_producers else 1) if K % 256 == 0 else 0
             cfg = 0
         self._check_labels(label)
         if perf is not None:

@@ -283,9 +283,20 @@ class FusedOptimizer:
         for i in parts:
             self._step_part(i, grad_scale, skip, pack)
 
-    def _step_part(self, i: int, grad_scale: float, skip: Optional[torch.Tensor], pack=None) -> None:
+    def step_fused(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None, max_grid: int = 0) -> None:
+        """(GPU) one Adam launch over the ``fuse_range`` hole itself, on the current stream, with the hole's own
+        step / done slot: the range is then stepped apart from (and concurrently with) the other launches --
+        e.g. the FC weight's Adam on a side stream beside the conv backward (FlagshipConfig.fc_adam_side).
+        ``max_grid``: workgroup cap (0 = the default 2048)."""
+        if self.fused is None:
+            raise ValueError("step_fused needs a fuse_range")
+        lo, hi = self.fused
+        self._step_part(len(self.bounds), grad_scale, skip, None, rng=(lo, hi), max_grid=max_grid)
+
+    def _step_part(self, i: int, grad_scale: float, skip: Optional[torch.Tensor], pack=None, rng=None,
+                   max_grid: int = 0) -> None:
         s = self.space
-        lo, hi = self.bounds[i]
+        lo, hi = self.bounds[i] if rng is None else rng
         lib = nat.hip_lib()
         st = nat.stream_ptr(s.flat.device)
         skp = nat.ptr(skip) if skip is not None else None
@@ -301,7 +312,7 @@ class FusedOptimizer:
         f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
                                          _p, _p, _l, _l, _p, _p, _p, _i, _p, _l, _l, _p])
         hole_lo = hole_n = 0
-        if self.fused is not None and lo <= self.fused[0] and self.fused[1] <= hi:
+        if rng is None and self.fused is not None and lo <= self.fused[0] and self.fused[1] <= hi:
             hole_lo, hole_n = self.fused[0] - lo, self.fused[1] - self.fused[0]
         ps = pack(lo, hi) if pack is not None else None
         # the shadow range, clipped to this part and expressed relative to it
@@ -316,7 +327,7 @@ class FusedOptimizer:
                     self.betas[1], self.eps, self.weight_decay, int(self.kind == "adamw"), grad_scale,
                     self.prune_thr, done_p, sh_ptr, (sh_lo - lo) if has_sh else 0, (sh_hi - lo) if has_sh else 0,
                     sh8_ptr, nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
-                    nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, int(self.max_grid.get(i, 0)),
+                    nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, int(max_grid or self.max_grid.get(i, 0)),
                     ctypes.byref(ps) if ps is not None else None, hole_lo, hole_n, st),
                   "adam")
 

@@ -287,6 +287,7 @@ class HDCEStep:
         # (ops/fc.gemm_wgrad_adam) -- dW is never written; the data gradient then runs first (it reads the
         # bf16 weight copy the fused update rewrites)
         self.fused_adam = None
+        self.after_dgrad = None   # callable run right after the FC data gradient's launch (FlagshipConfig.fc_adam_side)
         # world-1 plans: the FC bias gradient's column reduction rides in the conv backward's slab launch
         # (never in DP: the FC gradient bucket is all-reduced before the conv backward runs)
         self.bias_via_conv_slabs = False
@@ -555,7 +556,8 @@ class HDCEStep:
         self._f8_bwd = bwd8
         if bwd8:
             from ..ops.fc import gemm_wgrad_f8
-            gemm_wgrad_f8(self._dY8, self.conv.h3_8.view(M, K), sc.scale[6:7], sc.scale[0:1], out=m.fc_w.grad)
+            gemm_wgrad_f8(self._dY8, self.conv.h3_8.view(M, K), sc.scale[6:7], sc.scale[0:1], out=m.fc_w.grad,
+                          cfg=int(KNOBS.f8_producers))
         else:
             self._wgrad(dY, A.to(m.compute_dtype))
         self._dYW = (dY, W)
@@ -654,7 +656,8 @@ class HDCEStep:
             sc = m.fp8_scales
             if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
                 self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)
-            self._dA = gemm_dgrad_f8(self._dY8, m._shadow_w8, sc.scale[6:7], sc.scale[1:2], out=self._dA_buf)
+            self._dA = gemm_dgrad_f8(self._dY8, m._shadow_w8, sc.scale[6:7], sc.scale[1:2], out=self._dA_buf,
+                                     cfg=int(KNOBS.f8_producers))
             sc.update()
             if self.stage_hook is not None:
                 self.stage_hook("dgrad")
@@ -667,6 +670,8 @@ class HDCEStep:
             self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
         else:
             self._dA = torch.mm(dY, W)                         # (rows, 4096) bf16
+        if self.after_dgrad is not None:   # (the FC weight's shadow has had its last reader of the step)
+            self.after_dgrad()
         if self.stage_hook is not None:
             self.stage_hook("dgrad")
 

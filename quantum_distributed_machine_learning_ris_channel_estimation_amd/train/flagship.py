@@ -74,6 +74,10 @@ class FlagshipConfig:
     #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
     #                              separate (profiles/r3_04_fused_adam.txt) -- 256 one-per-CU workgroups stream
     #                              the Adam state far slower than the 2048-workgroup update kernel
+    fc_adam_side: int = 0        # (world 1, dagq) > 0: the FC weight's Adam runs on the "fc" stream right after the FC
+    #                              data gradient -- the last reader of the bf16 shadow it rewrites -- beside the conv
+    #                              backward, on at most this many workgroups (so the conv kernels keep most CUs);
+    #                              joined before the step's other Adam launch.  0: one Adam launch at the tail
     dp_plan: str = "zero"        # world > 1: "zero" = ZeRO-1 FC optimizer (reduce-scatter the FC gradient,
     #                              Adam on this rank's 1/world shard, all-gather the bf16 weight shadow) or
     #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
@@ -245,6 +249,13 @@ class FlagshipTrainer(DPPlan):
             # the fused update reads this step's NaN flag: the loss finish (which sets it) runs right after the
             # loss pass, not deferred into the conv backward
             self.hstep.defer_loss = False
+        self.fc_adam_side = bool(cfg.fc_adam_side > 0 and not self.fused_adam and self.streams is not None
+                                 and cfg.dtype == "bf16" and self.hdce.fc_shadow is not None
+                                 and ctx.world == 1 and not cfg.split_graphs and len(self.hopt.bounds) == 1)
+        if self.fc_adam_side:
+            lo = sp.offsets[sp.names.index("CE.FC.weight")]
+            self.hopt.fuse_range(lo, lo + self.hdce.fc_w.numel())
+            self.hstep.after_dgrad = self._fc_adam_fork
         # end-of-step weight pack (GPU fused path)
         self.tail_pack = bool(self.hstep.hip and cfg.tail_pack)
         if self.tail_pack:
@@ -345,6 +356,12 @@ class FlagshipTrainer(DPPlan):
         self.hstep.conv.pack_weights(nat.stream_ptr(self.ctx.device), cursor=self.cur[0, 0:1] if advance else None,
                                      cursor_inc=self.B if advance else 0)
 
+    def _fc_adam_fork(self) -> None:
+        """(fc_adam_side) the FC weight's Adam on the fc stream, after the FC data gradient (its last reader of the
+        shadow) and the loss pass (its NaN flag); the step joins the stream before its other Adam launch."""
+        with self._fork(self.streams["fc"]):
+            self.hopt.step_fused(grad_scale=1.0, skip=self.hskip, max_grid=self.cfg.fc_adam_side)
+
     def _qsc_branch(self, with_opt: bool) -> None:
         """The QSC step (+ AdamW with ``with_opt``)."""
         q = self.cstep(self.gat.xq, self.labels, slabs=self.qslabs if self.cstep.writes_grads else None)
@@ -393,7 +410,7 @@ class FlagshipTrainer(DPPlan):
                 self._qsc_branch(with_opt=True)
             self._hdce_forward()
             self.hstep.backward_conv()
-            self._join(("qsc",))
+            self._join(("qsc", "fc") if self.fc_adam_side else ("qsc",))
             self._hdce_update()
             return
         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)

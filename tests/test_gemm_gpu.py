@@ -15,7 +15,7 @@ def _rel(a, b):
     return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("M,N,K", [(576, 256, 192), (576, 256, 256), (2304, 2048, 4096)])
 def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     if not gemm_fwd_ok(M, N, K, cfg):
@@ -37,7 +37,7 @@ def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     assert float(Y2[:, :5].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(192, 256, 512), (256, 256, 512), (2304, 2048, 4096)])
 def test_gemm_wgrad_matches_fp32(cuda, cfg, M, N, K):
     if cfg == 2 and M % 128:
@@ -60,7 +60,7 @@ def test_gemm_wgrad_matches_fp32(cuda, cfg, M, N, K):
     assert float(dW2[4:N - 1].abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("M,N,K", [(288, 192, 256), (288, 256, 256), (2304, 2048, 4096)])
 def test_gemm_dgrad_matches_fp32(cuda, cfg, M, N, K):
     if cfg in (0, 2, 3) and K % 256:
@@ -98,7 +98,7 @@ def _rows(E, U, B, N_store, cols, device):
     return L, P, rowoff, rowden, lab, per, stream
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 7, 8, 10])
 @pytest.mark.parametrize("E,U,B,N,K", [(3, 3, 64, 256, 320), (3, 3, 64, 256, 384), (3, 3, 256, 2048, 4096)])
 def test_gemm_nmse_epilogue_matches_fp32(cuda, cfg, E, U, B, N, K):
     """Forward GEMM with the HDCE loss epilogue + finish: loss, loss_perf, dY, bias gradient, NaN flag."""
@@ -196,7 +196,7 @@ def test_flagship_plain_hand_forward_matches_library_forward(cuda, monkeypatch, 
         assert float((x - y).abs().max()) <= 3e-2 * float(y.abs().max()) + 1e-8, name
 
 
-@pytest.mark.parametrize("cfg", [0, 1])
+@pytest.mark.parametrize("cfg", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K", [(576, 256, 256), (2304, 2048, 4096)])
 def test_gemm_fwd_f8_matches_fp32(cuda, M, N, K, cfg):
     """e4m3 forward (mfma_f32_16x16x32_fp8_fp8, two per 16-byte fragment) == the fp32 product of the SAME
@@ -316,11 +316,12 @@ def test_flagship_fp8_backward_matches_bf16_backward(cuda, monkeypatch):
         assert float((x - y).abs().max()) <= 0.15 * float(y.abs().max()) + 1e-8, name
 
 
+@pytest.mark.parametrize("cfg", [0, 1])
 @pytest.mark.parametrize("M,N,K", [(2304, 2048, 4096), (2304, 256, 512), (256, 256, 256)])
-def test_gemm_f8_grads_from_row_major(cuda, M, N, K):
+def test_gemm_f8_grads_from_row_major(cuda, M, N, K, cfg):
     """The fp8 backward GEMMs on the row-major e4m3 tensors (i-contiguous operands through ds_read_b64_tr_b8):
     dW = s s dY8^T A8 (fp32) and dA = s s dY8 W8 (bf16) == the fp32 products of the same dequantised operands;
-    one-hot operands check the layouts exactly."""
+    one-hot operands check the layouts exactly.  cfg 1: the same tiles with producer waves."""
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import gemm_dgrad_f8, gemm_wgrad_f8
     torch.manual_seed(4)
     q = lambda t, s: (t / s).to(torch.float8_e4m3fn)
@@ -329,12 +330,12 @@ def test_gemm_f8_grads_from_row_major(cuda, M, N, K):
     dY8, A8, W8 = q(dY, sy), q(A, sa), q(W, sw)
     t = lambda v: torch.tensor([v], device=cuda)
     dW = torch.empty(N, K, device=cuda)
-    gemm_wgrad_f8(dY8, A8, t(sy), t(sa), out=dW)
+    gemm_wgrad_f8(dY8, A8, t(sy), t(sa), out=dW, cfg=cfg)
     ref_w = (dY8.float() * sy).t() @ (A8.float() * sa)
     torch.cuda.synchronize()
     assert _rel(dW, ref_w) < 1e-4, _rel(dW, ref_w)
     if M % 144 == 0:
-        dA = gemm_dgrad_f8(dY8, W8, t(sy), t(sw))
+        dA = gemm_dgrad_f8(dY8, W8, t(sy), t(sw), cfg=cfg)
         ref_a = (dY8.float() * sy) @ (W8.float() * sw)
         torch.cuda.synchronize()
         assert _rel(dA, ref_a) < 8e-3, _rel(dA, ref_a)
@@ -342,7 +343,7 @@ def test_gemm_f8_grads_from_row_major(cuda, M, N, K):
     oh = torch.zeros(M, N, device=cuda)
     oh[M - 1, 3] = 1.0
     oh[5, N - 2] = 2.0
-    gemm_wgrad_f8(oh.to(torch.float8_e4m3fn), A8, t(1.0), t(1.0), out=dW)
+    gemm_wgrad_f8(oh.to(torch.float8_e4m3fn), A8, t(1.0), t(1.0), out=dW, cfg=cfg)
     torch.cuda.synchronize()
     assert torch.equal(dW[3], A8[M - 1].float()) and torch.equal(dW[N - 2], 2 * A8[5].float())
     assert float(dW[4].abs().sum()) == 0.0
