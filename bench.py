@@ -97,6 +97,8 @@ def main() -> int:
     ap.add_argument("--fc-adam-side", type=int, default=0,
                     help="world 1: the FC weight's Adam on a side stream beside the conv backward, capped at this many "
                          "workgroups (FlagshipConfig.fc_adam_side; 0 = off)")
+    ap.add_argument("--qsim-mfma12", type=int, default=None, choices=[0, 1],
+                    help="12 qubits: the MFMA simulator (knobs.KNOBS.qsim_mfma12) or qsim_big.hip's VALU kernels")
     ap.add_argument("--f8-producers", type=int, default=None, choices=[0, 1],
                     help="fp8 estimator: the e4m3 GEMMs with producer waves (knobs.KNOBS.f8_producers; default: shipped)")
     args = ap.parse_args()
@@ -135,12 +137,14 @@ def main() -> int:
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
                                                                                                 FlagshipTrainer)
 
-    if args.gemm_cfg or args.f8_producers is not None:
+    if args.gemm_cfg or args.f8_producers is not None or args.qsim_mfma12 is not None:
         from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
         if args.gemm_cfg:
             KNOBS.gemm_cfg = args.gemm_cfg
         if args.f8_producers is not None:
             KNOBS.f8_producers = bool(args.f8_producers)
+        if args.qsim_mfma12 is not None:
+            KNOBS.qsim_mfma12 = bool(args.qsim_mfma12)
     ctx = init_distributed("auto", timeout_s=int(os.environ.get("QDML_PG_TIMEOUT", "600")))
     if ctx.world != args.gpus:
         print(f"error: --gpus {args.gpus} but the process group has {ctx.world} rank(s)", file=sys.stderr)
@@ -301,6 +305,7 @@ def main() -> int:
                 "fc_grad_gemms": sorted(tr.hstep.hand_gemm & {"wgrad", "dgrad"}) if tr.hstep.hip else None,
                 "fc_gemm_cfg": list(tr.hstep.gemm_cfg) if tr.hstep.hip else None,
                 "qsim_mfma_forward": bool(getattr(getattr(tr.cstep, "hip", None), "mfma", False)),
+                "qsim_mfma12": bool(getattr(getattr(tr.cstep, "hip", None), "mfma12", False)),
                 "fc_adam_side": cfg.fc_adam_side if getattr(tr, "fc_adam_side", False) else 0,
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},

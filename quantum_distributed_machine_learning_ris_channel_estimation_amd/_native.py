@@ -79,7 +79,7 @@ def hipcc() -> Optional[str]:
 # qsim_stream.hip: no SLP vectorisation (packed-f32 pairs of the complex gate math doubled the register
 # demand: the adjoint passes spilled at 256 VGPRs, 86-92 without)
 PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "qsim_stream.hip": ["-fno-slp-vectorize"],
-                  "qsim_mfma.hip": ["-fno-slp-vectorize"]}
+                  "qsim_mfma.hip": ["-fno-slp-vectorize"], "qsim12_mfma.hip": ["-fno-slp-vectorize"]}
 
 
 def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:

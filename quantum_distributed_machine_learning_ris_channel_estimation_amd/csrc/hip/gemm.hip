@@ -923,9 +923,10 @@ using WgrQ = Geo<4, 8, 2, 2, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 
 using WgrR = Geo<4, 4, 2, 4, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 4 compute waves (the cfg 1 tile) + 4
 using DgrP = Geo<9, 4, 1, 4, KC, MC, 3, 0, 0, 1, 4>;    // dgrad 144 x 256 (256 tiles), 1 x 4 compute waves (144 x 64)
 using DgrQ = Geo<9, 2, 1, 8, KC, MC, 3, 0, 0, 1, 4>;    // dgrad 144 x 256, 1 x 8 compute waves (the cfg 2 tile) + 4
-// the fp8 estimator's e4m3 MX GEMMs with producer waves (the FwdM8 / WgrM8C / DgrM8C tiles + 4 loading waves)
+// the fp8 estimator's e4m3 MX GEMMs with producer waves (the FwdM8 / DgrM8C tiles + 4 loading waves).  (The
+// weight gradient's 8 compute waves + 4 producers cap a wave at 168 VGPRs, and its MX fragments then spilled 65:
+// it keeps WgrM8C.)
 using FwdM8P = Geo<9, 2, 1, 4, KC, KC, 4, 0, 2, 1, 4>;
-using WgrM8CP = Geo<4, 4, 2, 4, MC8, MC8, 3, 0, 2, 1, 4>;
 using DgrM8CP = Geo<9, 2, 1, 4, KC, MC8, 4, 0, 2, 1, 4>;
 
 }  // namespace gemm
@@ -1172,13 +1173,13 @@ QD_API int qd_transpose_u8(const uint8_t* src, uint8_t* dst, int R, int C, void*
 // The fp8 estimator's backward GEMMs straight from the row-major e4m3 tensors (MC8 operands, no transposed
 // copies).  sdy / sa / sw: device dequantisation scales.  M % 256 == 0 (wgrad), N % 256 == 0 (dgrad).
 // dW (N, K) fp32 (row stride ldw) = sdy sa dY8^T A8: dY8 (M, N), A8 (M, K)
-// cfg 1: the same tiles with producer waves
+// cfg: accepted for symmetry with qd_gemm_dgrad_f8 (one tile configuration: see WgrM8C / DgrM8CP)
 QD_API int qd_gemm_wgrad_f8(const uint8_t* dY8, const uint8_t* A8, const float* sdy, const float* sa, float* dW, int M,
                             int N, int K, int ldw, int cfg, void* stream) {
+  (void)cfg;
   if (M % 256 || N % 128 || K % 256 || !sdy || !sa) return (int)hipErrorInvalidValue;
   Args a{reinterpret_cast<const uint16_t*>(dY8), reinterpret_cast<const uint16_t*>(A8), N / 2, K / 2, N, K, M / 2,
          dW, ldw, nullptr, {}, nullptr, 0, sdy, {}, sa};
-  if (cfg == 1) return launch<WgrM8CP, EPI_F32, 2, 8>(a, (hipStream_t)stream);
   return launch<WgrM8C, EPI_F32, 2, 8>(a, (hipStream_t)stream);
 }
 // dA (M, K) bf16 = sdy sw dY8 W8: dY8 (M, N), W8 (N, K)

@@ -28,6 +28,8 @@ class Knobs:
     fp8_conv: bool = False
     # the 8-qubit circuit forward on the matrix cores (csrc/hip/qsim_mfma.hip; else the register kernel)
     qsim_mfma: bool = True
+    # the 12-qubit circuit, forward and adjoint, on the matrix cores (csrc/hip/qsim12_mfma.hip; else qsim_big.hip)
+    qsim_mfma12: bool = True
 
 
 KNOBS = Knobs()

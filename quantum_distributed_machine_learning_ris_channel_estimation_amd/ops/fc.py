@@ -156,7 +156,7 @@ def gemm_wgrad_f8(dY8: torch.Tensor, A8: torch.Tensor, s_dy: torch.Tensor, s_a: 
                   out: torch.Tensor, cfg: int = 0) -> torch.Tensor:
     """dW (N, K) fp32 = s_dy s_a dY8^T A8 from the row-major e4m3 dY8 (M, N) and A8 (M, K) (MX-scaled MFMA, both
     operands read i-contiguous through ds_read_b64_tr_b8: csrc/hip/gemm.hip qd_gemm_wgrad_f8).  M % 256 == 0.
-    cfg 1: the same tiles with producer waves."""
+    (``cfg`` is accepted for symmetry with gemm_dgrad_f8: one tile configuration.)"""
     M, N = dY8.shape
     K = A8.shape[1]
     assert dY8.dtype == A8.dtype == torch.float8_e4m3fn and dY8.is_contiguous() and A8.is_contiguous()

@@ -97,6 +97,9 @@ class QSCStepHIP:
         self.preslab = torch.empty(self.grid_bwd, row, **f32)
         L = nat.hip_lib()
         self.big = self.n > HIP_REG_MAX_QUBITS  # workgroup-per-sample simulator (qsim_big.hip)
+        # n = 12: every gate layer -- forward and adjoint -- as complex MFMA mode products (csrc/hip/qsim12_mfma.hip,
+        # same contract as qsim_big.hip's kernels); knobs.KNOBS.qsim_mfma12 = False: the VALU kernels
+        self.mfma12 = dev.type == "cuda" and self.n == 12 and 1 <= self.L <= 8 and KNOBS.qsim_mfma12
         # n = 13..16 with >= 2 layers: the streamed simulator (csrc/hip/qsim_stream.hip, one workgroup per
         # (sample, 4096-amplitude brick) per pass); else qsim_big.hip's workgroup-per-sample kernels
         self.stream = self.big and stream_sim_ok(self.n, self.L)
@@ -110,8 +113,12 @@ class QSCStepHIP:
             self.psave = torch.empty(sv, dtype=torch.uint8, device=dev)
         elif self.big:
             self.qrows = nat.fn(L, "qd_qsim_big_grid", [_i])(batch_total)
-            ws = nat.fn(L, "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)
-            nb = max(ws(self.n, self.qrows, 0), ws(self.n, self.qrows, 1))
+            if self.mfma12:
+                # the per-(group, layer) MFMA operand images of the 12-qubit simulator (csrc/hip/qsim12_mfma.hip)
+                nb = nat.fn(L, "qd_qsim_mfma12_workspace", [_i, _i], ctypes.c_longlong)(max(1, n_groups), self.L)
+            else:
+                ws = nat.fn(L, "qd_qsim_big_workspace", [_i, _i, _i], ctypes.c_longlong)
+                nb = max(ws(self.n, self.qrows, 0), ws(self.n, self.qrows, 1))
             self.qws = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else None
             # every sample's final state, kept by the forward for the adjoint backward (which then
             # skips re-running the circuit): 2304 x 2^16 x 8 B = 1.2 GB at 16 qubits -- HBM has room
@@ -138,7 +145,7 @@ class QSCStepHIP:
         self._img_step = False   # the image holds this step's weights (the last forward was fwd3)
         self._head = nat.fn(L, "qd_qsc_head", [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p])
         if self.big:
-            pre = "qd_qsim_stream" if self.stream else "qd_qsim_big"
+            pre = "qd_qsim_stream" if self.stream else ("qd_qsim_mfma12" if self.mfma12 else "qd_qsim_big")
             self._qf = nat.fn(L, pre + "_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
             self._qb = nat.fn(L, pre + "_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
         else:
