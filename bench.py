@@ -97,6 +97,8 @@ def main() -> int:
     ap.add_argument("--fc-adam-side", type=int, default=0,
                     help="world 1: the FC weight's Adam on a side stream beside the conv backward, capped at this many "
                          "workgroups (FlagshipConfig.fc_adam_side; 0 = off)")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="set a knobs.KNOBS switch for this run (repeatable; bools as 0/1), e.g. qsim_mfma_bwd=0")
     ap.add_argument("--qsim-mfma12", type=int, default=None, choices=[0, 1],
                     help="12 qubits: the MFMA simulator (knobs.KNOBS.qsim_mfma12) or qsim_big.hip's VALU kernels")
     ap.add_argument("--f8-producers", type=int, default=None, choices=[0, 1],
@@ -137,8 +139,12 @@ def main() -> int:
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
                                                                                                 FlagshipTrainer)
 
-    if args.gemm_cfg or args.f8_producers is not None or args.qsim_mfma12 is not None:
+    if args.gemm_cfg or args.f8_producers is not None or args.qsim_mfma12 is not None or args.knob:
         from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
+        for kv in args.knob:
+            name, val = kv.split("=", 1)
+            cur = getattr(KNOBS, name)   # (AttributeError for an unknown knob)
+            setattr(KNOBS, name, bool(int(val)) if isinstance(cur, bool) else type(cur)(val))
         if args.gemm_cfg:
             KNOBS.gemm_cfg = args.gemm_cfg
         if args.f8_producers is not None:
@@ -306,6 +312,7 @@ def main() -> int:
                 "fc_gemm_cfg": list(tr.hstep.gemm_cfg) if tr.hstep.hip else None,
                 "qsim_mfma_forward": bool(getattr(getattr(tr.cstep, "hip", None), "mfma", False)),
                 "qsim_mfma12": bool(getattr(getattr(tr.cstep, "hip", None), "mfma12", False)),
+                "qsim_mfma_bwd": bool(getattr(getattr(tr.cstep, "hip", None), "mfma_bwd", False)),
                 "fc_adam_side": cfg.fc_adam_side if getattr(tr, "fc_adam_side", False) else 0,
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},

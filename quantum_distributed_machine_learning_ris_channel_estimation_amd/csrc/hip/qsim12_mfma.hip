@@ -91,11 +91,13 @@ __device__ __forceinline__ int sidx(int o, int e) {
 // grid (G, L - 1), block 64: the operand images of layer l = 1 + blockIdx.y of weight group blockIdx.x.  For
 // lane (i, g) = (lane & 15, lane >> 4) and k = 8 g + j: form r = [Ar | -Ai][i][k], form i = [Ai | Ar][i][k] of the
 // mode's factor A (direction 0) or of its adjoint A^dagger[i][k'] = conj(A[k'][i]) (direction 1).
+template <int NQ>
 __global__ void __launch_bounds__(64) prep_kernel(const float* __restrict__ w, h8* __restrict__ img, int L) {
-  __shared__ float4 tr[N];
+  constexpr int NM = NQ / 4;   // modes
+  __shared__ float4 tr[NQ];
   const int g = blockIdx.x, l = 1 + blockIdx.y, lane = threadIdx.x;
-  if (lane < N) {
-    const float* wl = w + ((size_t)g * L + l) * 2 * N;
+  if (lane < NQ) {
+    const float* wl = w + ((size_t)g * L + l) * 2 * NQ;
     float s, c, sp, cp;
     __sincosf(0.5f * wl[2 * lane], &s, &c);
     __sincosf(0.5f * wl[2 * lane + 1], &sp, &cp);
@@ -103,9 +105,9 @@ __global__ void __launch_bounds__(64) prep_kernel(const float* __restrict__ w, h
   }
   __syncthreads();
   const int i = lane & 15, gq = lane >> 4;
-  h8* out = img + ((size_t)g * (L - 1) + (l - 1)) * LAYER_H8;
+  h8* out = img + ((size_t)g * (L - 1) + (l - 1)) * (NM * 2 * IMG_H8);
 #pragma unroll
-  for (int m = 0; m < 3; ++m)
+  for (int m = 0; m < NM; ++m)
 #pragma unroll
     for (int dir = 0; dir < 2; ++dir) {
       h8 rh, rl, ih, il;
@@ -451,6 +453,187 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
   for (int p = tid; p < P; p += NT) slab[(size_t)blockIdx.x * P + p] = acc[p];
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// 8 qubits: the adjoint backward of the flagship's circuit (its forward is csrc/hip/qsim_mfma.hip) in the same
+// formulation with two modes, X[b][a] (k = b << 4 | a), ONE WAVE PER SAMPLE (a mode product or a cross density
+// is a single 16 x 16 tile): per layer in reverse the ring undone through the wave's LDS planes, C_0 and C_1 (one
+// K step each, 6 MFMAs), the 16 gate gradients from their partial traces, and psi, lambda <- U^dagger (two mode
+// products each).  Replaces qsim.hip's register-resident VALU adjoint (qsim_bwd_kernel<8>); same contract as
+// qd_qsim_bwd_saved: psave in qsim.hip's layout (written by either forward), one slab row per wave.
+// ---------------------------------------------------------------------------------------------------------------
+namespace k8 {
+constexpr int N8 = 8, D8 = 256;
+constexpr int WAVE_F = 8 * D8 + 64 + 128;   // per-wave LDS floats: psi / lambda planes, C_0 / C_1, rho, acc
+template <int M>
+__device__ __forceinline__ int sidx8(int o, int e) {
+  if constexpr (M == 0) return (o << 4) | e;
+  else return (e << 4) | o;
+}
+__device__ __forceinline__ int ring8(int k) {
+#pragma unroll
+  for (int i = 0; i < N8 - 1; ++i) k ^= ((k >> i) & 1) << (i + 1);
+  k ^= (k >> (N8 - 1)) & 1;
+  return k;
+}
+// psi <- A psi along mode M (in place: the wave's one tile)
+template <int M>
+__device__ __forceinline__ void mode8(float* pr, float* pi, const Op& A, int lane) {
+  const int jj = lane & 15, gq = lane >> 4;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  const float* pl = (gq >> 1) ? pi : pr;
+  h8 bh, bl;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    _Float16 h, lo;
+    split(pl[sidx8<M>(jj, 8 * (gq & 1) + j)], h, lo);
+    bh[j] = h;
+    bl[j] = lo;
+  }
+  const f4 rc = mfma(A.rl, bh, mfma(A.rh, bl, z));
+  const f4 ic = mfma(A.il, bh, mfma(A.ih, bl, z));
+  f4 yr = mfma(A.rh, bh, z), yi = mfma(A.ih, bh, z);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k = sidx8<M>(jj, 4 * gq + r);
+    pr[k] = yr[r] + rc[r] * LO_INV;
+    pi[k] = yi[r] + ic[r] * LO_INV;
+  }
+}
+// C_M = sum_o conj(lambda[o, alpha]) psi[o, beta] -> c (Cr at +0, Ci at +256, [alpha][beta])
+template <int M>
+__device__ __forceinline__ void cross8(const float* pr, const float* pi, const float* lr, const float* li, float* c,
+                                       int lane) {
+  const int jj = lane & 15, gq = lane >> 4;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  const float* la = (gq >> 1) ? li : lr;
+  const float* pb = (gq >> 1) ? pi : pr;
+  const float* qb = (gq >> 1) ? pr : pi;
+  const float sq = (gq >> 1) ? -1.f : 1.f;
+  h8 ah, al, bh, bl, ch, cl;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = sidx8<M>(8 * (gq & 1) + j, jj);
+    _Float16 h, lo;
+    split(la[k], h, lo);
+    ah[j] = h;
+    al[j] = lo;
+    split(pb[k], h, lo);
+    bh[j] = h;
+    bl[j] = lo;
+    split(sq * qb[k], h, lo);
+    ch[j] = h;
+    cl[j] = lo;
+  }
+  const f4 crc = mfma(al, bh, mfma(ah, bl, z)), cic = mfma(al, ch, mfma(ah, cl, z));
+  const f4 cr = mfma(ah, bh, z), ci = mfma(ah, ch, z);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    c[(4 * gq + r) * 16 + jj] = cr[r] + crc[r] * LO_INV;
+    c[256 + (4 * gq + r) * 16 + jj] = ci[r] + cic[r] * LO_INV;
+  }
+}
+
+// block 256 = 4 waves; global wave gw < rows takes samples gw, gw + rows, ... and writes slab row gw.
+__global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                   const h8* __restrict__ img, const float* __restrict__ gE,
+                                                   float* __restrict__ dx, float* __restrict__ slab, int B, int L,
+                                                   int wgroup, const cf* __restrict__ psave, int rows) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + wv;
+  if (gw >= rows) return;   // (whole wave; the kernel has no workgroup barrier)
+  float* base = sm + wv * WAVE_F;
+  float *pr = base, *pi = base + D8, *lr = base + 2 * D8, *li = base + 3 * D8;
+  float* cm = base + 4 * D8;            // C_0 (512) | C_1 (512)
+  float* rho = base + 8 * D8;           // 64
+  float* acc = rho + 64;                // 2 n L <= 128
+  const int P = 2 * N8 * L;
+  for (int p = lane; p < P; p += 64) acc[p] = 0.f;
+  for (int s = gw; s < B; s += rows) {
+    const int grp = wgroup > 0 ? s / wgroup : 0;
+    const float* wg = w + (size_t)grp * L * 2 * N8;
+    float g[N8];
+#pragma unroll
+    for (int q = 0; q < N8; ++q) g[q] = gE[(size_t)s * N8 + q];
+    // psi_final in qsim.hip's layout: element r * 64 + lane is amplitude k = r | lane << 2
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = r | (lane << 2);
+      const cf v = psave[(size_t)s * D8 + r * 64 + lane];
+      float o = 0.f;
+#pragma unroll
+      for (int q = 0; q < N8; ++q) o += ((k >> q) & 1) ? -g[q] : g[q];
+      pr[k] = v.x;
+      pi[k] = v.y;
+      lr[k] = o * v.x;
+      li[k] = o * v.y;
+    }
+    wave_lds_fence();
+    for (int l = L - 1; l >= 0; --l) {
+      float v[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = ring8(lane + 64 * r);
+        v[0][r] = pr[j];
+        v[1][r] = pi[j];
+        v[2][r] = lr[j];
+        v[3][r] = li[j];
+      }
+      wave_lds_fence();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = lane + 64 * r;
+        pr[k] = v[0][r];
+        pi[k] = v[1][r];
+        lr[k] = v[2][r];
+        li[k] = v[3][r];
+      }
+      wave_lds_fence();
+      cross8<0>(pr, pi, lr, li, cm, lane);
+      cross8<1>(pr, pi, lr, li, cm + 512, lane);
+      wave_lds_fence();
+      {   // rho[m][ql][xy][c]: lane = m * 32 + ql * 8 + xy * 2 + c
+        const int m = lane >> 5, ql = (lane >> 3) & 3, xy = (lane >> 1) & 3, c = lane & 1;
+        const int xb = xy >> 1, yb = xy & 1;
+        const float* cc = cm + m * 512 + c * 256;
+        float t = 0.f;
+#pragma unroll
+        for (int o3 = 0; o3 < 8; ++o3) {
+          const int lo = o3 & ((1 << ql) - 1), hi = (o3 >> ql) << (ql + 1);
+          t += cc[(hi | (xb << ql) | lo) * 16 + (hi | (yb << ql) | lo)];
+        }
+        rho[lane] = t;
+      }
+      wave_lds_fence();
+      if (lane < N8) {
+        const int q = lane;
+        const float* rq = rho + q * 8;
+        float sp, cp;
+        __sincosf(wg[2 * N8 * l + 2 * q + 1], &sp, &cp);
+        const float dphi = rq[1] - rq[7];
+        const float dth = (cp * rq[4] - sp * rq[5]) - (cp * rq[2] + sp * rq[3]);
+        acc[(l * N8 + q) * 2] += dth;
+        acc[(l * N8 + q) * 2 + 1] += dphi;
+        if (l == 0) dx[(size_t)s * N8 + q] = dth;
+      }
+      wave_lds_fence();
+      if (l > 0) {
+        const h8* lm = img + ((size_t)grp * (L - 1) + (l - 1)) * (2 * 2 * IMG_H8);
+        const Op a0 = load_op(lm + (0 * 2 + 1) * IMG_H8, lane);
+        mode8<0>(pr, pi, a0, lane);
+        mode8<0>(lr, li, a0, lane);
+        wave_lds_fence();
+        const Op a1 = load_op(lm + (1 * 2 + 1) * IMG_H8, lane);
+        mode8<1>(pr, pi, a1, lane);
+        mode8<1>(lr, li, a1, lane);
+        wave_lds_fence();
+      }
+    }
+  }
+  for (int p = lane; p < P; p += 64) slab[(size_t)gw * P + p] = acc[p];
+}
+}  // namespace k8
+
 constexpr size_t FWD_SMEM = (2 * D + 64 + 2 * 48) * sizeof(float);
 constexpr size_t BWD_SMEM = (4 * D + 4 * 2 * 256 + 96 + 192) * sizeof(float);
 
@@ -472,7 +655,7 @@ QD_API int qd_qsim_mfma12_fwd(const float* x, const float* w, float* E, int B, i
   hipStream_t st = (hipStream_t)stream;
   const int G = wgroup > 0 ? (B + wgroup - 1) / wgroup : 1;
   if (L > 1) {
-    hipLaunchKernelGGL(prep_kernel, dim3(G, L - 1), dim3(64), 0, st, w, (h8*)ws, L);
+    hipLaunchKernelGGL(prep_kernel<N>, dim3(G, L - 1), dim3(64), 0, st, w, (h8*)ws, L);
     if (hipError_t e = hipGetLastError()) return (int)e;
   }
   if (hipError_t e = qd::allow_lds(fwd_kernel, FWD_SMEM)) return (int)e;
@@ -491,5 +674,29 @@ QD_API int qd_qsim_mfma12_bwd(const float* x, const float* w, const float* gE, f
   const int grid = B < 512 ? B : 512;   // = qd_qsim_big_grid(B): the slab rows the caller sums
   hipLaunchKernelGGL(bwd_kernel, dim3(grid), dim3(NT), BWD_SMEM, (hipStream_t)stream, x, w, (const h8*)ws, gE, dx,
                      slab, B, L, wgroup, (const float*)psave);
+  return (int)hipGetLastError();
+}
+
+// bytes of the 8-qubit adjoint's operand images (2 modes x {forward, adjoint} per (group, layer >= 1))
+QD_API long long qd_qsim_mfma8_workspace(int G, int L) {
+  return (long long)(G < 1 ? 1 : G) * (L > 1 ? L - 1 : 0) * (2 * 2 * IMG_H8) * (long long)sizeof(h8);
+}
+
+// The 8-qubit adjoint backward on the matrix cores: the contract of qd_qsim_bwd_saved (psave = the forward's
+// final states in qsim.hip's layout, dx (B, 8), slab rows = qd_qsim_bwd_grid(8, B)) plus ws for the operand
+// images, rebuilt here from w.
+QD_API int qd_qsim_mfma8_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n,
+                             int L, int wgroup, void* ws, const void* psave, void* stream) {
+  if (B < 1 || n != 8 || L < 1 || L > 8 || psave == nullptr || (L > 1 && ws == nullptr)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (L > 1) {
+    const int G = wgroup > 0 ? (B + wgroup - 1) / wgroup : 1;
+    hipLaunchKernelGGL(prep_kernel<8>, dim3(G, L - 1), dim3(64), 0, st, w, (h8*)ws, L);
+    if (hipError_t e = hipGetLastError()) return (int)e;
+  }
+  const int rows = B < 4096 ? B : 4096;   // = qd_qsim_bwd_grid(8, B)
+  const size_t smem = 4 * k8::WAVE_F * sizeof(float);
+  hipLaunchKernelGGL(k8::bwd8_kernel, dim3((rows + 3) / 4), dim3(256), smem, st, x, w, (const h8*)ws, gE, dx, slab, B,
+                     L, wgroup, (const cf*)psave, rows);
   return (int)hipGetLastError();
 }

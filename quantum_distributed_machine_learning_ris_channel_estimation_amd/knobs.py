@@ -22,14 +22,18 @@ class Knobs:
     # fp8 estimator: the hand-written e4m3 forward (else torch._scaled_mm + the NMSE kernel), e4m3 FC gradients
     hand_fp8: bool = True
     f8_bwd: bool = True
-    # the e4m3 GEMMs with producer waves (gemm.hip Geo PW = 4: loading waves beside the MFMA waves)
-    f8_producers: bool = False
+    # the e4m3 GEMMs with producer waves (gemm.hip Geo PW = 4: loading waves beside the MFMA waves): forward 20.6 us
+    # and data gradient 25.1 us isolated against 28.6 / 30.3; the fp8 step 0.3811-0.3819 ms against 0.3922-0.3946
+    # (profiles/r5_05_*)
+    f8_producers: bool = True
     # e4m3 convs for layers 2 / 3 of the fp8 estimator (opt-in: a net loss in the step, profiles/r2_14_*)
     fp8_conv: bool = False
     # the 8-qubit circuit forward on the matrix cores (csrc/hip/qsim_mfma.hip; else the register kernel)
     qsim_mfma: bool = True
     # the 12-qubit circuit, forward and adjoint, on the matrix cores (csrc/hip/qsim12_mfma.hip; else qsim_big.hip)
     qsim_mfma12: bool = True
+    # the 8-qubit adjoint backward on the matrix cores (qsim12_mfma.hip qd_qsim_mfma8_bwd; else qsim.hip's)
+    qsim_mfma_bwd: bool = True
 
 
 KNOBS = Knobs()

@@ -177,6 +177,14 @@ class QSCStepHIP:
             self._mprep_noise = nat.fn(L, "qd_qsim_mfma_prep_noise",
                                        [_p, _p, _p, _i, _i, _f, ctypes.c_ulonglong, _p, _p, _p])
             self._mfwd = nat.fn(L, "qd_qsim_mfma_fwd", [_p, _p, _p, _p, _i, _i, _i, _p, _p])
+        # n = 8: the adjoint backward on the matrix cores too (csrc/hip/qsim12_mfma.hip qd_qsim_mfma8_bwd: the same
+        # contract as qd_qsim_bwd_saved, plus its own operand images); knobs.KNOBS.qsim_mfma_bwd = False: qsim.hip
+        self.mfma_bwd = (dev.type == "cuda" and not self.big and self.n == 8 and 1 <= self.L <= 8
+                         and self.psave is not None and KNOBS.qsim_mfma_bwd)
+        if self.mfma_bwd:
+            nb = nat.fn(L, "qd_qsim_mfma8_workspace", [_i, _i], ctypes.c_longlong)(max(1, n_groups), self.L)
+            self.qops8 = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+            self._qb = nat.fn(L, "qd_qsim_mfma8_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
 
     def quantum_weights(self) -> torch.Tensor:
         """Master weights, or (training + QuantumNAT) G per-stream noisy copies drawn in-kernel
@@ -290,6 +298,8 @@ class QSCStepHIP:
         extra = (nat.ptr(self.qws) if self.qws is not None else None,
                  nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
             (nat.ptr(self.psave) if self.psave is not None else None,)
+        if self.mfma_bwd:
+            extra = (nat.ptr(self.qops8), nat.ptr(self.psave))
         nat.check(self._qb(nat.ptr(self.angles), nat.ptr(w), nat.ptr(self.dE), nat.ptr(self.dang),
                            nat.ptr(self.qslab), B, n, L, wgroup, *extra, st), "qsim_bwd")
         own = SlabBatch()

@@ -115,3 +115,62 @@ def test_qsim12_mfma_deterministic(cuda):
     b = _mfma12(x, w, gE, 0)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+def _bwd8(x, w, gE, wgroup, mfma):
+    """8 qubits: the register forward (qsim.hip, keeps psi_final) then the MFMA adjoint (qd_qsim_mfma8_bwd) or the
+    register adjoint (qd_qsim_bwd_saved) -> (E, dx, dw summed over the slab rows)."""
+    lib = nat.hip_lib()
+    B, n = x.shape
+    L = w.shape[-3]
+    G = w.shape[0] if w.dim() == 4 else 1
+    dev = x.device
+    ps = torch.empty(B * (8 << n), dtype=torch.uint8, device=dev)
+    rows = nat.fn(lib, "qd_qsim_bwd_grid", [_i, _i])(n, B)
+    E = torch.empty(B, n, device=dev)
+    dx = torch.empty(B, n, device=dev)
+    slab = torch.full((rows, 2 * n * L), float("nan"), device=dev)
+    st = nat.stream_ptr(dev)
+    nat.check(nat.fn(lib, "qd_qsim_fwd_save", [_p, _p, _p, _i, _i, _i, _i, _p, _p])(
+        nat.ptr(x), nat.ptr(w), nat.ptr(E), B, n, L, wgroup, nat.ptr(ps), st), "fwd_save")
+    if mfma:
+        wsb = nat.fn(lib, "qd_qsim_mfma8_workspace", [_i, _i], ctypes.c_longlong)(G, L)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        nat.check(nat.fn(lib, "qd_qsim_mfma8_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])(
+            nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup, nat.ptr(ws), nat.ptr(ps),
+            st), "mfma8 bwd")
+    else:
+        nat.check(nat.fn(lib, "qd_qsim_bwd_saved", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p])(
+            nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, n, L, wgroup, nat.ptr(ps), st),
+            "bwd_saved")
+    torch.cuda.synchronize()
+    return E, dx, slab.sum(0).view(L, n, 2)
+
+
+@pytest.mark.parametrize("L,B", [(1, 5), (3, 9), (4, 33)])
+def test_qsim8_mfma_adjoint_matches_cpp(cuda, L, B):
+    g = torch.Generator().manual_seed(3 * L + B)
+    x = torch.rand(B, 8, generator=g) * 2 - 1
+    w = torch.rand(L, 8, 2, generator=g) * 2 * math.pi
+    gE = torch.randn(B, 8, generator=g)
+    xc, wc = x.clone().requires_grad_(), w.clone().requires_grad_()
+    (qsim(xc, wc, "cpu") * gE).sum().backward()
+    _, dx, dw = _bwd8(x.to(cuda), w.to(cuda), gE.to(cuda), 0, True)
+    assert torch.allclose(dx.cpu(), xc.grad, atol=5e-5), float((dx.cpu() - xc.grad).abs().max())
+    assert torch.allclose(dw.cpu(), wc.grad, atol=5e-4), float((dw.cpu() - wc.grad).abs().max())
+
+
+@pytest.mark.parametrize("B,G", [(2304, 9), (5000, 1)])
+def test_qsim8_mfma_adjoint_matches_register_kernel(cuda, B, G):
+    """Flagship batch (9 QuantumNAT groups; and > 4096 samples: waves loop over samples) against qsim.hip's
+    register-resident adjoint on the same saved states."""
+    torch.manual_seed(B)
+    L = 3
+    x = torch.rand(B, 8, device=cuda) * 3.0
+    w = torch.rand(G, L, 8, 2, device=cuda) * 6.28
+    gE = torch.randn(B, 8, device=cuda) / B
+    wgroup = B // G if G > 1 else 0
+    _, dx, dw = _bwd8(x, w, gE, wgroup, True)
+    _, dx0, dw0 = _bwd8(x, w, gE, wgroup, False)
+    assert torch.allclose(dx, dx0, atol=1e-6), float((dx - dx0).abs().max())
+    assert torch.allclose(dw, dw0, atol=1e-5), float((dw - dw0).abs().max())
