@@ -262,10 +262,15 @@ def estimate_routed(convs: Sequence[nn.Module], fc: nn.Module, x: torch.Tensor, 
 class HDCEStep:
     """One fused HDCE training step over 9 stream batches (see module docstring).
 
+    ``DGRAD_BNRED`` (class default, read at construction): the last conv layer's BN backward reduction rides in
+    the FC data gradient's epilogue where the shapes allow it (tests construct steps both ways).
+
     GPU path (``hip=True``): the conv/BN/ReLU stack runs on the hand-written kernels of
     csrc/hip/conv.hip with a manual backward, the FC on hipBLASLt (bf16 operands, fp32
     weight-gradient output written straight into the flat gradient buffer), the loss on
     csrc/hip/nmse.hip.  CPU / reference path: the same math through torch autograd."""
+
+    DGRAD_BNRED = True
 
     def __init__(self, model: HDCEModel, n_users: int, batch: int, grad_hook: Optional[Callable] = None,
                  hip: Optional[bool] = None, skip: Optional[torch.Tensor] = None):
@@ -312,11 +317,20 @@ class HDCEStep:
         self.gemm_cfg = tuple(int(c) for c in KNOBS.gemm_cfg.split(","))
         # fp8 estimator: the FC weight / data gradients in e4m3 as well (see _fc_hand_f8; KNOBS.f8_bwd)
         self.f8_bwd = KNOBS.f8_bwd
+        self.dgrad_bnred = False
         if self.hip:
             from ..ops.conv import ConvStackHIP
             self.conv = ConvStackHIP(model, n_users, batch)
             self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
+            # layer 3's BN backward reduction in the FC data gradient's epilogue (ops.fc.gemm_dgrad_bnred): one
+            # launch fewer on the chain (the bf16 hand-written dgrad, 3 experts, 144-row tiles within 2 groups)
+            self.dgrad_bnred = bool(self.DGRAD_BNRED and "dgrad" in self.hand_gemm and not getattr(model, "fp8", False)
+                                    and self.conv.bwd_fused and self.gemm_cfg[2] in (0, 2) and model.E == 3
+                                    and self.conv.HW in (128, 256) and 3 * batch >= 144
+                                    and (n_users * batch * 3) % 144 == 0)
+            if self.dgrad_bnred:
+                self.conv.enable_dgrad_bnred(n_users * batch * 3 // 144)
 
     def prime_fp8_dy(self, forward: Callable[[], None], state: Sequence[torch.Tensor], ctx=None) -> bool:
         """(fp8 estimator with e4m3 FC gradients) seed the delayed scale of the loss gradient dY (fp8 slot 6).
@@ -652,8 +666,16 @@ class HDCEStep:
                 and gemm_dgrad_ok(dY.shape[0], W.shape[0], W.shape[1], self.gemm_cfg[2]):
             if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
                 self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)
-            self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
+            if self.dgrad_bnred:
+                from ..ops.fc import gemm_dgrad_bnred
+                c = self.conv
+                self._dA = gemm_dgrad_bnred(dY, W, self._dA_buf, self.gemm_cfg[2], c.z[2], c.st[2], c.rslab[2],
+                                            self.B, self.U, c.HW)
+            else:
+                self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
         else:
+            if self.dgrad_bnred:
+                raise RuntimeError("dgrad_bnred needs the hand-written bf16 data gradient")
             self._dA = torch.mm(dY, W)                         # (rows, 4096) bf16
         if self.stage_hook is not None:
             self.stage_hook("dgrad")

@@ -110,6 +110,19 @@ def knobs(**kw):
     return WithKnobs
 
 
+class NoDgradBnred(FlagshipTrainer):
+    """As shipped before round 4's last change: layer 3's BN backward reduction in a launch of its own instead of
+    the FC data gradient's epilogue."""
+
+    def __init__(self, *a, **k):
+        from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEStep
+        HDCEStep.DGRAD_BNRED = False
+        try:
+            super().__init__(*a, **k)
+        finally:
+            HDCEStep.DGRAD_BNRED = True
+
+
 class HdceOnly(FlagshipTrainer):
     """(diagnostic, not a training step) the HDCE chain alone: what the concurrent QSC branch costs it."""
 
@@ -128,7 +141,7 @@ class QscOnly(FlagshipTrainer):
         self._qsc_branch(with_opt=True)
 
 
-PLANS = {"hdce_only": HdceOnly, "qsc_only": QscOnly,
+PLANS = {"hdce_only": HdceOnly, "qsc_only": QscOnly, "no_dgrad_bnred": NoDgradBnred,
          "fused_loss6": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="6,1,2"),
          "fused_loss1": knobs(hand_gemm="fwd,wgrad,dgrad", gemm_cfg="1,1,2"),
          "adam1024": adam_grid(1024), "adam1536": adam_grid(1536), "shipped": FlagshipTrainer, "hdce_first": HdceFirst, "join_last": JoinLast, "fork_conv1": ForkAfter,
