@@ -1117,7 +1117,11 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
                                                           const uint16_t* __restrict__ z, const float* __restrict__ st,
                                                           float* __restrict__ slab, const uint16_t* __restrict__ wt,
                                                           uint16_t* __restrict__ dx, float* __restrict__ part, int E,
-                                                          int B, int chunks, int spb, BnBwd bnb) {
+                                                          int B, int chunks, int spb, BnBwd bnb, LossFinish lf) {
+  if ((int)blockIdx.y == E) {   // the extra row (lf.part set): block 0 hosts the HDCE loss finish (when layer 3's
+    if (blockIdx.x == 0) loss_finish_body(lf);   // BN reduction rode in the FC data gradient, the launch that
+    return;                                      // hosted it is gone)
+  }
   using BG = BwdGeo<W>;
   using G = typename BG::G;
   constexpr int HW = G::HW, HP = G::HP, WP = G::WP, XCS = BG::XCS, DZS = BG::DZS;
@@ -2031,16 +2035,18 @@ QD_API int qd_conv_wgrad_dgrad(const uint16_t* xin, const float* st_prev, const 
 // qd_conv_wgrad's with the same chunking.
 QD_API int qd_conv_bwd_fused(const uint16_t* zprev, const float* st_prev, const uint16_t* dh, const uint16_t* z,
                              const float* st, float* slab, const uint16_t* w, uint16_t* dx, float* part, int N, int E,
-                             int B, int H, int W, int chunks, int spb, const BnBwd* bnb, void* stream) {
+                             int B, int H, int W, int chunks, int spb, const BnBwd* bnb, const qd::LossFinish* lf,
+                             void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const BnBwd bb = bnb ? *bnb : BnBwd{};
+  const qd::LossFinish lff = lf ? *lf : qd::LossFinish{};
   if (chunks * spb < B || N % B) return (int)hipErrorInvalidValue;
-  dim3 grid((N / B) * chunks, E);
+  dim3 grid((N / B) * chunks, E + (lf ? 1 : 0));
   QD_GEOM(WW, {
     const size_t sm = BwdGeo<WW>::SMEM;
     if (hipError_t e = qd::allow_lds(conv3x3_bwd_kernel<WW>, sm)) return (int)e;
     hipLaunchKernelGGL((conv3x3_bwd_kernel<WW>), grid, dim3(256), sm, s, zprev, st_prev, dh, z, st, slab, w, dx, part,
-                       E, B, chunks, spb, bb);
+                       E, B, chunks, spb, bb, lff);
   })
   return (int)hipGetLastError();
 }

@@ -107,6 +107,20 @@ struct AdamEpi {
   unsigned int* done;       // zero-initialised arrival counter (re-armed by the last workgroup)
 };
 
+// BN backward reduction in the data gradient's epilogue (EPI_BF16, the HDCE FC dgrad): dA = dh3 is the gradient of
+// the last conv layer's BN+ReLU output h3 = relu(a z + b), row r = (u B + b) E + e (a virtual sample), column
+// c HW + p (channel c of expert e, position p), E = 3.  Per (group u, channel e * 32 + c) the epilogue sums
+// g = dh * [a z + b > 0] and g * (z - mean) * invstd over its rows and columns, from the STORED (bf16) dh -- what
+// csrc/hip/conv.hip bn_bwd_reduce_kernel computes in a launch of its own, which this replaces -- into partial rows
+// part[(u * MT + tile_i) * 2 + k][EC] (MT = M / BM; rows of (u, tile) pairs that share no row are never written:
+// zero from allocation).  z: the layer's pre-BN output (bf16, dA's layout); st: its BN records (U, EC, 8).
+struct BnRedEpi {
+  const uint16_t* z;        // null: plain EPI_BF16
+  const float* st;
+  float* part;
+  int B, U, HW, EC;
+};
+
 // DBG (diagnosis builds, scripts/probe_gemm.py): 1 = no global loads in the K loop (MFMAs on whatever the
 // stages hold), 2 = no MFMAs (loads and LDS reads only)
 // F8: OCP e4m3 operands (KC x KC only).  The kernel still moves 2-byte "elements" (a row of K e4m3
@@ -404,6 +418,7 @@ struct Args {
   const float* deq;     // nullable: (2,) dequantisation scales; the accumulators are multiplied by their product
   AdamEpi ad;           // EPI_ADAM
   const float* deq2;    // nullable: with deq, the scales are deq[0] and deq2[0] (two separate scale slots)
+  BnRedEpi br;          // EPI_BF16: nullable BN backward reduction (see BnRedEpi)
 };
 
 // Direct-A K loop (G::ADIR): B through the 3-stage global_load_lds ring as in the staged loop, A straight into
@@ -506,6 +521,105 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_i, int tiles
   } else {
     ti = bid / tiles_j;
     tj = bid % tiles_j;
+  }
+}
+
+// EPI_BF16 row passes with the BN backward reduction (BnRedEpi).  Wave w takes rows w + NW k; with i0 % 3 == 0 the
+// expert of row w + NW k is (w + NW k) % 3, so k % 3 is a fixed accumulator slot per wave (no runtime register
+// indexing).  A tile spans at most two statistics groups (BM <= B E): rows >= rb belong to group u_lo + 1.
+template <class G>
+__device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, uint16_t* C, const float* bv, int i0,
+                                               int j0, int ti, int c0, int wave, int lane, int tid) {
+  constexpr int PITCH = G::PITCH, RPW = G::BM / G::NW, NSTR = 8;
+  const BnRedEpi& br = a.br;
+  const int col = j0 + c0, c = col / br.HW;   // this lane's channel (within its expert)
+  const int ub = br.B * 3, u_lo = i0 / ub, rb = (u_lo + 1) * ub - i0;
+  const int u_hi = u_lo + 1 < br.U ? u_lo + 1 : u_lo;
+  float4 rec[2][3];   // (mean, invstd, a, b) of (u_lo + us, expert of slot j, c)
+#pragma unroll
+  for (int us = 0; us < 2; ++us)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int e = (wave + G::NW * j) % 3;
+      rec[us][j] = *reinterpret_cast<const float4*>(br.st + ((size_t)(us ? u_hi : u_lo) * br.EC + e * 32 + c) * NSTR);
+    }
+  uint2 zr[RPW];   // every row's z first (one round trip for the whole pass)
+#pragma unroll
+  for (int k = 0; k < RPW; ++k)
+    zr[k] = *reinterpret_cast<const uint2*>(br.z + (size_t)(i0 + wave + G::NW * k) * a.ldc + col);
+  float s[2][3][2];
+#pragma unroll
+  for (int us = 0; us < 2; ++us)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) s[us][j][0] = s[us][j][1] = 0.f;
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int row = wave + G::NW * k, j = k % 3;
+    const float4 v = *reinterpret_cast<const float4*>(ct + row * PITCH + c0);
+    uint2 w;
+    w.x = (uint32_t)f32_to_bf16(v.x + bv[0]) | ((uint32_t)f32_to_bf16(v.y + bv[1]) << 16);
+    w.y = (uint32_t)f32_to_bf16(v.z + bv[2]) | ((uint32_t)f32_to_bf16(v.w + bv[3]) << 16);
+    *reinterpret_cast<uint2*>(C + (size_t)(i0 + row) * a.ldc + col) = w;
+    const float d[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                        __uint_as_float(w.y & 0xffff0000u)};
+    const float zz[4] = {__uint_as_float(zr[k].x << 16), __uint_as_float(zr[k].x & 0xffff0000u),
+                         __uint_as_float(zr[k].y << 16), __uint_as_float(zr[k].y & 0xffff0000u)};
+    const bool hi = row >= rb;   // (wave-uniform)
+    const float4 r = hi ? rec[1][j] : rec[0][j];
+    float tg = 0.f, tgx = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float g = (r.z * zz[q] + r.w > 0.f) ? d[q] : 0.f;
+      tg += g;
+      tgx += g * (zz[q] - r.x) * r.y;
+    }
+    if (hi) {
+      s[1][j][0] += tg;
+      s[1][j][1] += tgx;
+    } else {
+      s[0][j][0] += tg;
+      s[0][j][1] += tgx;
+    }
+  }
+  // lanes of one channel: 32 (HW = 128: lane halves are two channels) or all 64 (HW = 256)
+  const int span = br.HW / 4;
+#pragma unroll
+  for (int us = 0; us < 2; ++us)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        float t = s[us][j][k];
+        for (int m = 1; m < span; m <<= 1) t += __shfl_xor(t, m);
+        s[us][j][k] = t;
+      }
+  float* red = const_cast<float*>(ct) + G::BM * PITCH;   // (the 8 KB after the tile)
+  if ((lane & (span - 1)) == 0) {
+    const int half = lane / span;
+#pragma unroll
+    for (int us = 0; us < 2; ++us)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) red[((wave * 2 + half) * 2 + us) * 6 + j * 2 + k] = s[us][j][k];
+  }
+  __syncthreads();
+  // (half, us, e, k) partials, summed over the waves in wave order
+  const int nhalf = 64 / span;
+  if (tid < nhalf * 12) {
+    const int half = tid / 12, us = (tid % 12) / 6, e = (tid % 6) / 2, k = tid % 2;
+    const int uu = u_lo + us;
+    const bool has = us == 0 ? rb > 0 : (rb < G::BM && uu < br.U);
+    if (has) {
+      float t = 0.f;
+      for (int w = 0; w < G::NW; ++w) {
+        int j = 0;
+        while ((w + G::NW * j) % 3 != e) ++j;
+        t += red[((w * 2 + half) * 2 + us) * 6 + j * 2 + k];
+      }
+      const int ch = e * 32 + (j0 + half * span * 4) / br.HW;
+      br.part[(((size_t)uu * (a.I / G::BM) + ti) * 2 + k) * br.EC + ch] = t;
+    }
   }
 }
 
@@ -710,6 +824,12 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     float bv[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) bv[v] = a.bias ? bf16_to_f32(a.bias[j0 + c0 + v]) : 0.f;
+    if constexpr (VEC == 4 && G::KS == 1 && !G::F8 && G::BM % (3 * G::NW) == 0 && G::NW % 3 != 0) {
+      if (a.br.z != nullptr) {
+        bnred_epilogue<G>(a, ct, C, bv, i0, j0, ti, c0, wave, lane, tid);
+        return;
+      }
+    }
     for (int row = wave; row < G::BM; row += G::NW) {
       const float* src = ct + row * PITCH + c0;
       uint16_t* dst = C + (size_t)(i0 + row) * a.ldc + j0 + c0;
@@ -1068,6 +1188,31 @@ QD_API int qd_gemm_dgrad(const uint16_t* dY, const uint16_t* W, uint16_t* dA, in
   if (cfg == 5) return launch<DgrP, EPI_BF16, 4, 4>(a, st);
   if (cfg == 6) return launch<DgrQ, EPI_BF16, 4, 4>(a, st);
   return launch<DgrA, EPI_BF16, 4, 4>(a, st);
+}
+
+// The data gradient with the last conv layer's BN backward reduction in its epilogue (BnRedEpi): dA as
+// qd_gemm_dgrad, plus part (U, M / BM, 2, EC) partial rows of sum g / sum g xhat.  E = 3 experts, rows
+// (u B + b) 3 + e, K = 32 HW columns per row; cfg 0 / 2 (256-column tiles).  Any other shape or cfg:
+// hipErrorInvalidValue (the caller then keeps the separate reduction launch).
+QD_API int qd_gemm_dgrad_bnred(const uint16_t* dY, const uint16_t* W, uint16_t* dA, int M, int N, int K, int cfg,
+                               const uint16_t* z, const float* st, float* part, int B, int U, int HW, void* stream) {
+  if (!z || !st || !part || (HW != 128 && HW != 256) || K != 32 * HW || M != U * B * 3 ||
+      (cfg != 0 && cfg != 2 && cfg != 5 && cfg != 6))
+    return (int)hipErrorInvalidValue;
+  Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}, nullptr, 0, nullptr};
+  a.br = BnRedEpi{z, st, part, B, U, HW, 96};
+  hipStream_t st_ = (hipStream_t)stream;
+  // (producer-wave tiles: the producers have ended before the epilogue, whose barriers are the compute waves')
+  if (cfg == 5 || cfg == 6) {
+    if (3 * B < DgrQ::BM) return (int)hipErrorInvalidValue;
+    return cfg == 6 ? launch<DgrQ, EPI_BF16, 4, 4>(a, st_) : launch<DgrP, EPI_BF16, 4, 4>(a, st_);
+  }
+  if (cfg == 2) {
+    if (3 * B < DgrC::BM) return (int)hipErrorInvalidValue;   // (a tile spans at most two statistics groups)
+    return launch<DgrC, EPI_BF16, 4, 4>(a, st_);
+  }
+  if (3 * B < DgrA::BM) return (int)hipErrorInvalidValue;
+  return launch<DgrA, EPI_BF16, 4, 4>(a, st_);
 }
 
 // e4m3 forward with the HDCE-loss epilogue: A8 (M, K) e4m3 activations, W8 (N, K) e4m3 weights (both

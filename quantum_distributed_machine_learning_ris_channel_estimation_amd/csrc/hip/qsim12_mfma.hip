@@ -72,6 +72,29 @@ __device__ __forceinline__ void split(float v, _Float16& hi, _Float16& lo) {
 }
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
 
+// 8 floats -> fp16 hi / lo operands in pairs: hi = v with its mantissa cut to fp16's 11 significant bits (exact in
+// fp16 over its normal range, so the packed round-toward-zero convert is exact), lo = (v - hi) 2^11: 4 vector
+// instructions per value instead of 5-6 for the per-value split (amplitudes below fp16's normal range, < 6e-5,
+// lose their bits below ~6e-8 absolute)
+typedef __attribute__((ext_vector_type(2))) __fp16 hp2;
+typedef __attribute__((ext_vector_type(4))) unsigned int u4;
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
+  u4 H, L;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = __uint_as_float(__float_as_uint(v[2 * p]) & 0xffffe000u);
+    const float b = __uint_as_float(__float_as_uint(v[2 * p + 1]) & 0xffffe000u);
+    H[p] = __builtin_bit_cast(unsigned int, __builtin_amdgcn_cvt_pkrtz(a, b));
+    L[p] = __builtin_bit_cast(unsigned int,
+                              __builtin_amdgcn_cvt_pkrtz((v[2 * p] - a) * LO_SCALE, (v[2 * p + 1] - b) * LO_SCALE));
+  }
+  hi = __builtin_bit_cast(h8, H);
+  lo = __builtin_bit_cast(h8, L);
+}
+// LDS plane address of amplitude k: one float of padding per 16 (a 17-float row; pad()), so the strided operand reads of
+// all three modes are at most 2-way bank conflicts (8-way on the unpadded mode-0 reads)
+__device__ __forceinline__ int pad(int k) { return k + (k >> 4); }
+
 // CNOT ring CNOT(0,1) .. CNOT(n-2,n-1), CNOT(n-1,0) as a basis map, and its inverse (qsim_big.hip's)
 __device__ __forceinline__ int ring_fwd(int k) {
 #pragma unroll
@@ -148,13 +171,10 @@ template <int M>
 __device__ __forceinline__ void load_b(const float* pr, const float* pi, int t, int jj, int gq, h8& bh, h8& bl) {
   const float* pl = (gq >> 1) ? pi : pr;
   const int o = t * 16 + jj;
+  float v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 h, lo;
-    split(pl[sidx<M>(o, 8 * (gq & 1) + j)], h, lo);
-    bh[j] = h;
-    bl[j] = lo;
-  }
+  for (int j = 0; j < 8; ++j) v[j] = pl[pad(sidx<M>(o, 8 * (gq & 1) + j))];
+  split8(v, bh, bl);
 }
 
 // Y = A X along mode M for the 4 tiles of wave wv; RING: written at the CNOT-ring images (after a workgroup
@@ -163,27 +183,30 @@ template <int M, bool RING>
 __device__ __forceinline__ void mode_apply(float* pr, float* pi, const Op& A, int wv, int lane) {
   const int jj = lane & 15, gq = lane >> 4;
   const f4 z = {0.f, 0.f, 0.f, 0.f};
-  f4 yr[4], yi[4];
-#pragma unroll
+  f4 yr[RING ? 4 : 1], yi[RING ? 4 : 1];
+  // (one tile at a time unless the ring needs all four held: unrolled, the compiler hoisted every tile's loads and
+  // the backward spilled)
+#pragma unroll RING ? 4 : 1
   for (int tt = 0; tt < 4; ++tt) {
     const int t = wv * 4 + tt;
+    const int ts = RING ? tt : 0;
     h8 bh, bl;
     load_b<M>(pr, pi, t, jj, gq, bh, bl);
     const f4 rc = mfma(A.rl, bh, mfma(A.rh, bl, z));
     const f4 ic = mfma(A.il, bh, mfma(A.ih, bl, z));
-    yr[tt] = mfma(A.rh, bh, z);
-    yi[tt] = mfma(A.ih, bh, z);
+    yr[ts] = mfma(A.rh, bh, z);
+    yi[ts] = mfma(A.ih, bh, z);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      yr[tt][r] += rc[r] * LO_INV;
-      yi[tt][r] += ic[r] * LO_INV;
+      yr[ts][r] += rc[r] * LO_INV;
+      yi[ts][r] += ic[r] * LO_INV;
     }
     if constexpr (!RING) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int k = sidx<M>(t * 16 + jj, 4 * gq + r);
-        pr[k] = yr[tt][r];
-        pi[k] = yi[tt][r];
+        const int k = pad(sidx<M>(t * 16 + jj, 4 * gq + r));
+        pr[k] = yr[0][r];
+        pi[k] = yi[0][r];
       }
     }
   }
@@ -193,7 +216,7 @@ __device__ __forceinline__ void mode_apply(float* pr, float* pi, const Op& A, in
     for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int k = ring_fwd(sidx<M>((wv * 4 + tt) * 16 + jj, 4 * gq + r));
+        const int k = pad(ring_fwd(sidx<M>((wv * 4 + tt) * 16 + jj, 4 * gq + r)));
         pr[k] = yr[tt][r];
         pi[k] = yi[tt][r];
       }
@@ -221,14 +244,15 @@ __device__ __forceinline__ void layer0(float* pr, float* pi, cf* tab, const floa
   for (int i = 0; i < D / NT; ++i) {
     const int k = tid + NT * i;
     const cf v = cmul(cmul(tab[k & 15], tab[16 + ((k >> 4) & 15)]), tab[32 + (k >> 8)]);
-    const int j = ring_fwd(k);
+    const int j = pad(ring_fwd(k));
     pr[j] = v.x;
     pi[j] = v.y;
   }
 }
 
-// LDS carve (floats): psi planes | lambda planes (backward) | scratch
-constexpr int F_PSI = 0, F_LAM = 2 * D, F_SCR = 4 * D;
+// LDS carve (floats): psi planes | lambda planes (backward) | scratch; a plane holds DP = D + D / 16 floats (pad)
+constexpr int DP = D + D / 16;
+constexpr int F_PSI = 0, F_LAM = 2 * DP, F_SCR = 4 * DP;
 
 // grid: samples looped; block 256.  x (B, 12) angles, w (G, L, 12, 2) (group of sample s = s / wgroup; wgroup 0:
 // one group), img from prep_kernel, E (B, 12), psave (B, 2, 4096) or null.
@@ -237,9 +261,9 @@ __global__ void __launch_bounds__(NT, 2) fwd_kernel(const float* __restrict__ x,
                                                     int wgroup, float* __restrict__ psave) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* pr = sm + F_PSI;
-  float* pi = pr + D;
-  float* red = sm + 2 * D;                             // 4 waves x 12
-  cf* tab = reinterpret_cast<cf*>(sm + 2 * D + 64);    // 48 complex
+  float* pi = pr + DP;
+  float* red = sm + 2 * DP;                            // 4 waves x 12
+  cf* tab = reinterpret_cast<cf*>(sm + 2 * DP + 64);   // 48 complex
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   for (int s = blockIdx.x; s < B; s += gridDim.x) {
     const int grp = wgroup > 0 ? s / wgroup : 0;
@@ -266,13 +290,14 @@ __global__ void __launch_bounds__(NT, 2) fwd_kernel(const float* __restrict__ x,
 #pragma unroll
     for (int i = 0; i < D / NT; ++i) {
       const int k = tid + NT * i;
-      const float p = pr[k] * pr[k] + pi[k] * pi[k];
+      const float re = pr[pad(k)], im = pi[pad(k)];
+      const float p = re * re + im * im;
       ptot += p;
 #pragma unroll
       for (int b = 0; b < 4; ++b) ph[b] += ((i >> b) & 1) ? -p : p;
       if (psave != nullptr) {
-        psave[(size_t)s * 2 * D + k] = pr[k];
-        psave[(size_t)s * 2 * D + D + k] = pi[k];
+        psave[(size_t)s * 2 * D + k] = re;
+        psave[(size_t)s * 2 * D + D + k] = im;
       }
     }
 #pragma unroll
@@ -304,24 +329,21 @@ __device__ __forceinline__ void cross_partial(const float* pr, const float* pi, 
   const float* pb = (gq >> 1) ? pi : pr;   // -> Cr
   const float* qb = (gq >> 1) ? pr : pi;   // -> Ci (negated for the im half)
   const float sq = (gq >> 1) ? -1.f : 1.f;
-#pragma unroll
+#pragma unroll 1
   for (int kt = 0; kt < 4; ++kt) {
     const int o0 = (wv * 4 + kt) * 16 + 8 * (gq & 1);
     h8 ah, al, bh, bl, ch, cl;
+    float va[8], vb[8], vc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int ka = sidx<M>(o0 + j, jj);   // (alpha = jj for the A operand, beta = jj for the B operands)
-      _Float16 h, lo;
-      split(la[ka], h, lo);
-      ah[j] = h;
-      al[j] = lo;
-      split(pb[ka], h, lo);
-      bh[j] = h;
-      bl[j] = lo;
-      split(sq * qb[ka], h, lo);
-      ch[j] = h;
-      cl[j] = lo;
+      const int ka = pad(sidx<M>(o0 + j, jj));   // (alpha = jj for the A operand, beta = jj for the B operands)
+      va[j] = la[ka];
+      vb[j] = pb[ka];
+      vc[j] = sq * qb[ka];
     }
+    split8(va, ah, al);
+    split8(vb, bh, bl);
+    split8(vc, ch, cl);
     cr = mfma(ah, bh, cr);
     crc = mfma(al, bh, mfma(ah, bl, crc));
     ci = mfma(ah, ch, ci);
@@ -341,9 +363,9 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
                                                     int wgroup, const float* __restrict__ psave) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* pr = sm + F_PSI;
-  float* pi = pr + D;
+  float* pi = pr + DP;
   float* lr = sm + F_LAM;
-  float* li = lr + D;
+  float* li = lr + DP;
   float* scr = sm + F_SCR;             // 4 waves x {Cr, Ci} x 256
   float* rho = scr + 4 * 2 * 256;      // 3 modes x 4 qubits x (x, y) 4 x {re, im}
   float* acc = rho + 96;               // 2 n L <= 192
@@ -364,10 +386,10 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
       float o = 0.f;
 #pragma unroll
       for (int q = 0; q < N; ++q) o += ((k >> q) & 1) ? -g[q] : g[q];
-      pr[k] = a;
-      pi[k] = b;
-      lr[k] = o * a;
-      li[k] = o * b;
+      pr[pad(k)] = a;
+      pi[pad(k)] = b;
+      lr[pad(k)] = o * a;
+      li[pad(k)] = o * b;
     }
     __syncthreads();
     for (int l = L - 1; l >= 0; --l) {
@@ -376,7 +398,7 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
         float v[4][D / NT];
 #pragma unroll
         for (int i = 0; i < D / NT; ++i) {
-          const int j = ring_fwd(tid + NT * i);
+          const int j = pad(ring_fwd(tid + NT * i));
           v[0][i] = pr[j];
           v[1][i] = pi[j];
           v[2][i] = lr[j];
@@ -385,7 +407,7 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < D / NT; ++i) {
-          const int k = tid + NT * i;
+          const int k = pad(tid + NT * i);
           pr[k] = v[0][i];
           pi[k] = v[1][i];
           lr[k] = v[2][i];
@@ -463,7 +485,8 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
 // ---------------------------------------------------------------------------------------------------------------
 namespace k8 {
 constexpr int N8 = 8, D8 = 256;
-constexpr int WAVE_F = 8 * D8 + 64 + 128;   // per-wave LDS floats: psi / lambda planes, C_0 / C_1, rho, acc
+constexpr int DP8 = D8 + D8 / 16;           // padded plane (pad)
+constexpr int WAVE_F = 4 * DP8 + 4 * D8 + 64 + 128;   // per-wave LDS floats: psi / lambda planes, C_0 / C_1, rho, acc
 template <int M>
 __device__ __forceinline__ int sidx8(int o, int e) {
   if constexpr (M == 0) return (o << 4) | e;
@@ -482,19 +505,16 @@ __device__ __forceinline__ void mode8(float* pr, float* pi, const Op& A, int lan
   const f4 z = {0.f, 0.f, 0.f, 0.f};
   const float* pl = (gq >> 1) ? pi : pr;
   h8 bh, bl;
+  float vv[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    _Float16 h, lo;
-    split(pl[sidx8<M>(jj, 8 * (gq & 1) + j)], h, lo);
-    bh[j] = h;
-    bl[j] = lo;
-  }
+  for (int j = 0; j < 8; ++j) vv[j] = pl[pad(sidx8<M>(jj, 8 * (gq & 1) + j))];
+  split8(vv, bh, bl);
   const f4 rc = mfma(A.rl, bh, mfma(A.rh, bl, z));
   const f4 ic = mfma(A.il, bh, mfma(A.ih, bl, z));
   f4 yr = mfma(A.rh, bh, z), yi = mfma(A.ih, bh, z);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int k = sidx8<M>(jj, 4 * gq + r);
+    const int k = pad(sidx8<M>(jj, 4 * gq + r));
     pr[k] = yr[r] + rc[r] * LO_INV;
     pi[k] = yi[r] + ic[r] * LO_INV;
   }
@@ -510,20 +530,17 @@ __device__ __forceinline__ void cross8(const float* pr, const float* pi, const f
   const float* qb = (gq >> 1) ? pr : pi;
   const float sq = (gq >> 1) ? -1.f : 1.f;
   h8 ah, al, bh, bl, ch, cl;
+  float va[8], vb[8], vc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int k = sidx8<M>(8 * (gq & 1) + j, jj);
-    _Float16 h, lo;
-    split(la[k], h, lo);
-    ah[j] = h;
-    al[j] = lo;
-    split(pb[k], h, lo);
-    bh[j] = h;
-    bl[j] = lo;
-    split(sq * qb[k], h, lo);
-    ch[j] = h;
-    cl[j] = lo;
+    const int k = pad(sidx8<M>(8 * (gq & 1) + j, jj));
+    va[j] = la[k];
+    vb[j] = pb[k];
+    vc[j] = sq * qb[k];
   }
+  split8(va, ah, al);
+  split8(vb, bh, bl);
+  split8(vc, ch, cl);
   const f4 crc = mfma(al, bh, mfma(ah, bl, z)), cic = mfma(al, ch, mfma(ah, cl, z));
   const f4 cr = mfma(ah, bh, z), ci = mfma(ah, ch, z);
 #pragma unroll
@@ -543,9 +560,9 @@ __global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, 
   const int gw = blockIdx.x * 4 + wv;
   if (gw >= rows) return;   // (whole wave; the kernel has no workgroup barrier)
   float* base = sm + wv * WAVE_F;
-  float *pr = base, *pi = base + D8, *lr = base + 2 * D8, *li = base + 3 * D8;
-  float* cm = base + 4 * D8;            // C_0 (512) | C_1 (512)
-  float* rho = base + 8 * D8;           // 64
+  float *pr = base, *pi = base + DP8, *lr = base + 2 * DP8, *li = base + 3 * DP8;
+  float* cm = base + 4 * DP8;           // C_0 (512) | C_1 (512)
+  float* rho = cm + 4 * D8;             // 64
   float* acc = rho + 64;                // 2 n L <= 128
   const int P = 2 * N8 * L;
   for (int p = lane; p < P; p += 64) acc[p] = 0.f;
@@ -563,17 +580,17 @@ __global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, 
       float o = 0.f;
 #pragma unroll
       for (int q = 0; q < N8; ++q) o += ((k >> q) & 1) ? -g[q] : g[q];
-      pr[k] = v.x;
-      pi[k] = v.y;
-      lr[k] = o * v.x;
-      li[k] = o * v.y;
+      pr[pad(k)] = v.x;
+      pi[pad(k)] = v.y;
+      lr[pad(k)] = o * v.x;
+      li[pad(k)] = o * v.y;
     }
     wave_lds_fence();
     for (int l = L - 1; l >= 0; --l) {
       float v[4][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int j = ring8(lane + 64 * r);
+        const int j = pad(ring8(lane + 64 * r));
         v[0][r] = pr[j];
         v[1][r] = pi[j];
         v[2][r] = lr[j];
@@ -582,7 +599,7 @@ __global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, 
       wave_lds_fence();
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int k = lane + 64 * r;
+        const int k = pad(lane + 64 * r);
         pr[k] = v[0][r];
         pi[k] = v[1][r];
         lr[k] = v[2][r];
@@ -634,8 +651,8 @@ __global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, 
 }
 }  // namespace k8
 
-constexpr size_t FWD_SMEM = (2 * D + 64 + 2 * 48) * sizeof(float);
-constexpr size_t BWD_SMEM = (4 * D + 4 * 2 * 256 + 96 + 192) * sizeof(float);
+constexpr size_t FWD_SMEM = (2 * DP + 64 + 2 * 48) * sizeof(float);
+constexpr size_t BWD_SMEM = (4 * DP + 4 * 2 * 256 + 96 + 192) * sizeof(float);
 
 }  // namespace qm12
 }  // namespace qd

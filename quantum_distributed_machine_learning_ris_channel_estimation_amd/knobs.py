@@ -30,6 +30,9 @@ class Knobs:
     fp8_conv: bool = False
     # the 8-qubit circuit forward on the matrix cores (csrc/hip/qsim_mfma.hip; else the register kernel)
     qsim_mfma: bool = True
+    # layer 3's BN backward reduction in the FC data gradient's epilogue (gemm.hip BnRedEpi; else its own launch,
+    # conv.hip bn_bwd_reduce_kernel)
+    dgrad_bnred: bool = True
     # the 12-qubit circuit, forward and adjoint, on the matrix cores (csrc/hip/qsim12_mfma.hip; else qsim_big.hip)
     qsim_mfma12: bool = True
     # the 8-qubit adjoint backward on the matrix cores (qsim12_mfma.hip qd_qsim_mfma8_bwd; else qsim.hip's)

@@ -144,8 +144,20 @@ class ConvStackHIP:
                                                         _p, _p, _p])
         # (bwd_fused off) wgrad + dgrad of layers 3 and 2 as one launch each
         self.fuse_wd = True
-        self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p])
+        self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p, _p])
+        # layer 3's BN backward partials from the FC data gradient's epilogue (enable_dgrad_bnred): 0 = own launch
+        self.bnred_mt = 0
         self._fwd8 = nat.fn(L, "qd_conv_fwd_f8", [_p] * 4 + [_i] * 7 + [_p] * 6)
+
+    def enable_dgrad_bnred(self, mt: int) -> None:
+        """Layer 3's BN backward partials come from the FC data gradient's epilogue (ops.fc.gemm_dgrad_bnred,
+        ``mt`` M tiles: partial rows (U, mt, 2, EC); rows of (group, tile) pairs that share no sample stay zero
+        from here), so backward() launches no reduction for layer 3 and hands the deferred loss finish to layer
+        3's fused backward kernel.  Needs the fused backward (bf16 dx)."""
+        assert self.bwd_fused and self.E == 3
+        self.bnred_mt = int(mt)
+        self.rchunks[2] = self.bnred_mt
+        self.rslab[2] = torch.zeros(self.U, self.bnred_mt, 2, self.EC, device=self.rslab[2].device)
 
     def pack_weights(self, st, cursor: Optional[torch.Tensor] = None, cursor_inc: int = 0) -> None:
         """Forward (3) and dgrad (2) B-fragment images of the current weights: one launch.
@@ -247,7 +259,7 @@ class ConvStackHIP:
         the current stream while wgrad(k) runs beside it; the current stream joins before the slab
         reduction.  Each of these kernels fills well under the 256 CUs, so they overlap.
         ``loss_finish`` (ops.nmse.LossFinish): the deferred HDCE loss finish, hosted by layer 3's BN
-        reduction launch as one extra workgroup."""
+        reduction launch as one extra workgroup (with ``bnred_mt``: by layer 3's fused backward launch)."""
         m, st = self.m, nat.stream_ptr(dh3.device)
         main = torch.cuda.current_stream(dh3.device) if side is not None else None
         dh, dh_bf = dh3, int(dh3.dtype == torch.bfloat16)
@@ -255,10 +267,12 @@ class ConvStackHIP:
         for k in (2, 1, 0):
             z, bst = self.z[k], self.st[k]
             rs = self.rslab[k]
-            if k == 2 or not self.fuse_bn_red:   # (else the previous dgrad produced these partials)
-                lf = ctypes.byref(loss_finish) if (loss_finish is not None and k == 2) else None
+            lf = ctypes.byref(loss_finish) if (loss_finish is not None and k == 2) else None
+            # (layer 3 with bnred_mt: the FC data gradient's epilogue produced them; else the previous dgrad)
+            if (k == 2 and not self.bnred_mt) or (k < 2 and not self.fuse_bn_red):
                 nat.check(self._bred(nat.ptr(dh), dh_bf, nat.ptr(z), nat.ptr(bst), nat.ptr(rs), self.N, self.E,
                                      self.B, self.H, self.W, self.chunks_r, self.spb_r, lf, st), f"bn_bwd_reduce{k + 1}")
+                lf = None
             # BN backward finalisation fused into this layer's wgrad and dgrad kernels
             bnb = BnBwd(nat.ptr(rs), nat.ptr(m.bn_w[k]), self.rchunks[k], float(self.B * self.HW))
             xin = self.x1 if k == 0 else self.z[k - 1]
@@ -269,10 +283,11 @@ class ConvStackHIP:
                 dx = self.dx[k - 1]
                 nat.check(self._bwdf(nat.ptr(xin), _ptr(st_prev), nat.ptr(dh), nat.ptr(z), nat.ptr(bst), nat.ptr(ws),
                                      nat.ptr(self.wpk_t[k]), nat.ptr(dx), nat.ptr(self.rslab[k - 1]), self.N, self.E,
-                                     self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k], ctypes.byref(bnb), st),
-                          f"conv_bwd_fused{k + 1}")
+                                     self.B, self.H, self.W, self.chunks_wl[k], self.spb_wl[k], ctypes.byref(bnb), lf,
+                                     st), f"conv_bwd_fused{k + 1}")
                 dh, dh_bf = dx, 1
                 continue
+            assert lf is None, "the deferred loss finish needs layer 3's fused backward launch"
             if k > 0 and self.fuse_wd and dh_bf and self.dx_bf16 and side is None:
                 # weight AND data gradient of this layer in one launch (independent: side by side)
                 dx = self.dx[k - 1]

@@ -106,6 +106,22 @@ def gemm_dgrad(dY: torch.Tensor, W: torch.Tensor, out: Optional[torch.Tensor] = 
     return dA
 
 
+def gemm_dgrad_bnred(dY: torch.Tensor, W: torch.Tensor, out: torch.Tensor, cfg: int, z: torch.Tensor,
+                     st: torch.Tensor, part: torch.Tensor, B: int, U: int, HW: int) -> torch.Tensor:
+    """gemm_dgrad with the last conv layer's BN backward reduction in the epilogue (csrc/hip/gemm.hip BnRedEpi):
+    part (U, M / 144, 2, 96) receives per (group, tile) sum g / sum g xhat of g = dA [a z + b > 0] -- the partial
+    rows csrc/hip/conv.hip bn_bwd_reduce_kernel would write.  z: the layer's pre-BN output in dA's layout;
+    st: its BN records (U, 96, 8).  3 experts, cfg 0, 2, 5 or 6."""
+    M, N = dY.shape
+    K = W.shape[1]
+    assert dY.dtype == W.dtype == z.dtype == torch.bfloat16 and dY.is_contiguous() and W.is_contiguous()
+    assert z.is_contiguous() and z.numel() == M * K and part.is_contiguous() and part.numel() == U * (M // 144) * 2 * 96
+    f = _gemm_fn("qd_gemm_dgrad_bnred", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(dY), nat.ptr(W), nat.ptr(out), M, N, K, cfg, nat.ptr(z), nat.ptr(st), nat.ptr(part), B, U, HW,
+                nat.stream_ptr(W.device)), "gemm_dgrad_bnred")
+    return out
+
+
 def gemm_fwd_f8(A8: torch.Tensor, W8: torch.Tensor, deq: torch.Tensor, b: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, cfg: int = 1) -> torch.Tensor:
     """Y (M, N) bf16 = deq[0] deq[1] A8 W8^T (+ b): OCP e4m3 operands (torch.float8_e4m3fn, row-major,

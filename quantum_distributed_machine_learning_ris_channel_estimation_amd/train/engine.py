@@ -313,11 +313,20 @@ class HDCEStep:
         self.gemm_cfg = tuple(int(c) for c in KNOBS.gemm_cfg.split(","))
         # fp8 estimator: the FC weight / data gradients in e4m3 as well (see _fc_hand_f8; KNOBS.f8_bwd)
         self.f8_bwd = KNOBS.f8_bwd
+        self.dgrad_bnred = False
         if self.hip:
             from ..ops.conv import ConvStackHIP
             self.conv = ConvStackHIP(model, n_users, batch)
             self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
+            # layer 3's BN backward reduction in the FC data gradient's epilogue (ops.fc.gemm_dgrad_bnred): one
+            # launch fewer on the chain (the bf16 hand-written dgrad, 3 experts, 144-row tiles within 2 groups)
+            self.dgrad_bnred = bool(KNOBS.dgrad_bnred and "dgrad" in self.hand_gemm and not getattr(model, "fp8", False)
+                                    and self.conv.bwd_fused and self.gemm_cfg[2] in (0, 2, 5, 6) and model.E == 3
+                                    and self.conv.HW in (128, 256) and 3 * batch >= 144
+                                    and (n_users * batch * 3) % 144 == 0)
+            if self.dgrad_bnred:
+                self.conv.enable_dgrad_bnred(n_users * batch * 3 // 144)
 
     def prime_fp8_dy(self, forward: Callable[[], Optional["HDCEStep"]], state: Sequence[torch.Tensor], ctx=None,
                      engines: Sequence["HDCEStep"] = ()) -> bool:
@@ -667,8 +676,16 @@ class HDCEStep:
                 and gemm_dgrad_ok(dY.shape[0], W.shape[0], W.shape[1], self.gemm_cfg[2]):
             if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
                 self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)
-            self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
+            if self.dgrad_bnred:
+                from ..ops.fc import gemm_dgrad_bnred
+                c = self.conv
+                self._dA = gemm_dgrad_bnred(dY, W, self._dA_buf, self.gemm_cfg[2], c.z[2], c.st[2], c.rslab[2],
+                                            self.B, self.U, c.HW)
+            else:
+                self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
         else:
+            if self.dgrad_bnred:
+                raise RuntimeError("dgrad_bnred needs the hand-written bf16 data gradient")
             self._dA = torch.mm(dY, W)                         # (rows, 4096) bf16
         if self.after_dgrad is not None:   # (the FC weight's shadow has had its last reader of the step)
             self.after_dgrad()

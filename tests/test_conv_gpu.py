@@ -267,3 +267,30 @@ def test_hdce_step_counts_batches_and_running_stats(cuda):
     for k in range(3):
         assert torch.allclose(a.run_mean[k], b.run_mean[k], rtol=2e-2, atol=2e-3)
         assert torch.allclose(a.run_var[k], b.run_var[k], rtol=5e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("pilot_num,B", [(128, 256), (128, 64), (256, 64)])
+def test_dgrad_bn_reduction_epilogue_matches_its_own_launch(cuda, monkeypatch, pilot_num, B):
+    """Layer 3's BN backward reduction in the FC data gradient's epilogue (gemm.hip BnRedEpi, the default) vs
+    its own launch (bn_bwd_reduce_kernel): the same sums over the same stored bf16 dh3 in another grouping, so
+    every gradient agrees to float rounding; the loss is the same launch's either way.  B = 64: 144-row tiles
+    straddle the 192-row statistics groups."""
+    U = 3
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(KNOBS, "dgrad_bnred", fused)
+        a, _ = pair(cuda, pilot_num)
+        torch.manual_seed(1)
+        Yp = torch.randn(3, U, B, 2, a.H, a.W, device=cuda)
+        HL = torch.randn(3, U, B, a.fc_w.shape[0], device=cuda)
+        s = HDCEStep(a, U, B, hip=True)
+        assert s.dgrad_bnred == fused
+        a.space.zero_grad()
+        loss = s(Yp, HL, HL + 0.1 * torch.randn_like(HL))
+        torch.cuda.synchronize()
+        outs.append((loss.clone(), a.space.grad.clone(), s.conv.dx[1].clone()))
+    (lf, gf, xf), (lr_, gr, xr) = outs
+    assert torch.equal(lf, lr_)
+    # (c2 / c3 of layer 3 come from the same sums in another order: a dz rounding may flip a bf16 dx here and there)
+    assert rel(xf, xr) < 1e-4, rel(xf, xr)
+    assert rel(gf, gr) < 1e-4, rel(gf, gr)
