@@ -51,7 +51,6 @@ def main():
             fb = nat.fn(lib, "qd_qsim_mfma12_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
             vf = nat.fn(lib, "qd_qsim_big_fwd", [_p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
             vb = nat.fn(lib, "qd_qsim_big_bwd", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p])
-            args = lambda t: (nat.ptr(t),)  # noqa: E731
             var["q12_fwd_mfma"] = lambda ff=ff, x=x, w=w, E=E, ws=ws, ps=ps, wg=wg: ff(
                 nat.ptr(x), nat.ptr(w), nat.ptr(E), B, 12, L, wg, nat.ptr(ws), nat.ptr(ps), st)
             var["q12_bwd_mfma"] = lambda fb=fb, x=x, w=w, gE=gE, dx=dx, slab=slab, ws=ws, ps=ps, wg=wg: fb(
@@ -63,9 +62,9 @@ def main():
                 nat.ptr(x), nat.ptr(w), nat.ptr(gE), nat.ptr(dx), nat.ptr(slab), B, 12, L, wg, None, nat.ptr(ps), st)
             # (the MFMA backward reads the MFMA forward's psave layout, the VALU backward its own: keep each pair's
             # state consistent by running the forward first in each timing)
-            var["q12_fb_mfma"] = lambda: (var["q12_fwd_mfma"](), var["q12_bwd_mfma"]())
-            var["q12_fb_valu"] = lambda: (var["q12_fwd_valu"](), var["q12_bwd_valu"]())
-            del var["q12_bwd_mfma"], var["q12_bwd_valu"]
+            fwm, bwm, fwv, bwv = var["q12_fwd_mfma"], var.pop("q12_bwd_mfma"), var["q12_fwd_valu"], var.pop("q12_bwd_valu")
+            var["q12_fb_mfma"] = lambda fwm=fwm, bwm=bwm: (fwm(), bwm())
+            var["q12_fb_valu"] = lambda fwv=fwv, bwv=bwv: (fwv(), bwv())
         else:
             rows = nat.fn(lib, "qd_qsim_bwd_grid", [_i, _i])(n, B)
             slab = torch.empty(rows, 2 * n * L, device=dev)
