@@ -73,6 +73,10 @@ class RunnerConfig:
     deterministic: bool = False
     nan_guard: bool = True
     resume: bool = False
+    # HDCE weight averaging: the mean of the estimator's weights over the last ``swa_epochs`` epochs (one snapshot
+    # per epoch end), with every expert's BN statistics re-estimated on its training streams, saved beside the
+    # epoch checkpoints under the tag "swa" (0: off; the reference evaluates the last epoch's weights)
+    swa_epochs: int = 0
 
     def update_from_dict(self, d: Dict[str, Any]) -> "RunnerConfig":
         names = {f.name: f for f in dataclasses.fields(self)}
@@ -109,6 +113,8 @@ class EvalConfig:
     # test-time BN adaptation: re-estimate each expert's BN statistics on the test pilots routed to it
     # (unsupervised; the reference keeps the 10 dB training statistics -- reports/r2_hdce_snr.md)
     bn_adapt: bool = False
+    # the HDCE checkpoint tag to evaluate ("": the classifiers' epoch tag; "swa": RunnerConfig.swa_epochs' average)
+    hdce_tag: str = ""
 
     def update_from_dict(self, d: Dict[str, Any]) -> "EvalConfig":
         names = {f.name for f in dataclasses.fields(self)}

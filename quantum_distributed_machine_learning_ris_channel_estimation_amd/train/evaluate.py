@@ -122,9 +122,13 @@ class model_val:
             qsc = None
         convs = [Conv_P128(self.Pilot_num).to(dev) for _ in range(3)]
         fc = FC_P128(self.Pilot_num).to(dev)
+        htag = self.hdce_tag or self.epoch_tag
         for name, model, key in [("Conv0", convs[0], "conv"), ("Conv1", convs[1], "conv"),
                                  ("Conv2", convs[2], "conv"), ("Linear", fc, "linear")]:
-            f = _epoch_file(d, f"{name}_{bs}_{snr}dB_{{tag}}_DML.pth", self.epoch_tag)
+            f = (_epoch_file(d, f"{name}_{bs}_{snr}dB_{{tag}}_DML.pth", htag) if htag.startswith("epoch")
+                 else os.path.join(d, f"{name}_{bs}_{snr}dB_{htag}_DML.pth"))
+            if not os.path.exists(f or ""):
+                f = None
             if f is None:
                 raise FileNotFoundError(f"{name} checkpoint not found in {d}")
             self.load_model_state_dict(model, f, fallback_key=key)

@@ -229,7 +229,7 @@ class FlagshipTrainer(DPPlan):
         # CU-masked streams for the two chains (ops/streams.py: every partition slower), and the DP plan's
         # QSC branch split around the HDCE forward.)
         mode = cfg.stream_mode
-        if mode not in ("serial", "dagq"):
+        if mode not in ("serial", "dagq", "indep"):
             raise ValueError(f"stream_mode {mode!r}")
         self.streams = None
         if dev.type == "cuda" and mode != "serial" and self.hstep.hip and self.cstep.hip is not None:
@@ -250,6 +250,7 @@ class FlagshipTrainer(DPPlan):
             # loss pass, not deferred into the conv backward
             self.hstep.defer_loss = False
         self.fc_adam_side = bool(cfg.fc_adam_side > 0 and not self.fused_adam and self.streams is not None
+                                 and mode == "dagq"
                                  and cfg.dtype == "bf16" and self.hdce.fc_shadow is not None
                                  and ctx.world == 1 and not cfg.split_graphs and len(self.hopt.bounds) == 1)
         if self.fc_adam_side:
@@ -293,7 +294,14 @@ class FlagshipTrainer(DPPlan):
                     fn()
             return body
 
-        if self.ctx.world == 1 and not cfg.split_graphs:
+        if self.ctx.world == 1 and not cfg.split_graphs and mode == "indep":
+            # the QSC and HDCE chains independent for the whole k-step replay (see _indep_step): one join at its end
+            def body():
+                for i in range(k):
+                    self._indep_step(first=i == 0)
+                self._join(("qsc",))
+            gs = [GraphedStep(body, enabled=graphs)]
+        elif self.ctx.world == 1 and not cfg.split_graphs:
             # one graph: gather, both forwards, NMSE, both backwards, the optimizers
             gs = [GraphedStep(rep(self._step_body), enabled=graphs)]
         else:
@@ -414,6 +422,26 @@ class FlagshipTrainer(DPPlan):
             self._hdce_update()
             return
         self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr)
+
+    def _indep_step(self, first: bool) -> None:
+        """(stream_mode "indep", world 1) one training step with the QSC chain fully independent of the HDCE
+        chain: the QSC branch gathers its own half of the batch (the same permutation through its own cursor,
+        cur[1], so both models see the same samples) on its own stream and is never joined inside the replay, so
+        the HDCE chain -- gather, forward, backward, Adam -- has no cross-queue edge at all (the dagq step pays
+        two queue hand-overs per step at its join, ~14 us).  The classifier input is written and read on the qsc
+        stream only (round 3's independent plans shared the gather's output across the streams: that race is why
+        they were not reproducible).  ``first``: the replay's first step orders the qsc stream after this step's
+        first node (a branch forked before any node would be a root of the graph)."""
+        self._gather(classifier=False)
+        q = self.streams["qsc"]
+        if first:
+            q.wait_stream(torch.cuda.current_stream(self.ctx.device))
+        with torch.cuda.stream(q):
+            self._gather(hdce=False, classifier=True)
+            self._qsc_branch(with_opt=True)
+        self._hdce_forward()
+        self.hstep.backward_conv()
+        self._hdce_update()
 
     def skip_flags(self) -> torch.Tensor:
         """(2,) the HDCE and QSC NaN-guard flags of the last step (after the all-reduce: summed)."""

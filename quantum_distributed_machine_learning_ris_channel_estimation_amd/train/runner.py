@@ -364,10 +364,15 @@ class Y2HRunner:
         best_nmse = 1000.0
         resume_path = os.path.join(ck.ckpt_dir(self.workspace, self.Pilot_num), f"HDCE_{B}_{self.SNRdb}dB_resume.pth")
         start = 0
+        # (swa_epochs) the running sum of the per-epoch weight snapshots and their count
+        swa = [torch.zeros_like(sp.flat), 0] if self.swa_epochs > 0 else None
         if self.resume:
             st = ck.load_resume(resume_path)
             if st is not None:
                 ck.load_into(sp.flat, st["flat"])
+                if swa is not None and "swa" in st:
+                    ck.load_into(swa[0], st["swa"])
+                    swa[1] = int(st["swa_n"])
                 opt.load_state_dict(st["optimizer"])
                 for t, v in zip(model.run_mean + model.run_var, st["run_mean"] + st["run_var"]):
                     ck.load_into(t, v)
@@ -430,6 +435,9 @@ class Y2HRunner:
             log.log(kind="hdce_epoch", epoch=epoch, loss=tl[0], loss_perf=tl[1], val_nmse=nmse,
                     val_nmse_db=to_db(nmse), val_nmse_perf_db=to_db(nmse_perf), lr=opt.lr, samples_per_sec=sps,
                     fc_path=getattr(step, "fc_path", None), f8_bwd=bool(getattr(step, "_f8_bwd", False)))
+            if swa is not None and epoch >= self.n_epochs - self.swa_epochs:
+                swa[0].add_(sp.flat)
+                swa[1] += 1
             if epoch > 0:
                 if epoch % self.lr_decay == 0:
                     opt.set_lr(opt.lr * 0.5)
@@ -440,11 +448,46 @@ class Y2HRunner:
                                flat=sp.flat.cpu(), run_mean=[t.cpu() for t in model.run_mean],
                                run_var=[t.cpu() for t in model.run_var], nbt=[t.cpu() for t in model.nbt],
                                train_losses=torch.tensor(self.train_HDCE_losses, dtype=torch.float64),
-                               val_nmse=torch.tensor(self.val_HDCE_nmse, dtype=torch.float64), rng=ck.rng_state())
+                               val_nmse=torch.tensor(self.val_HDCE_nmse, dtype=torch.float64), rng=ck.rng_state(),
+                               **({"swa": swa[0].cpu(), "swa_n": swa[1]} if swa is not None else {}))
             ctx.heartbeat(f"hdce epoch {epoch + 1}")
             _maybe_fault(epoch)
+        if swa is not None and swa[1] > 0 and ctx.is_main:
+            self._save_swa(model, tr, swa, d)
+            ctx.heartbeat("hdce swa")
         self.hdce_model = model
         return model
+
+    @torch.no_grad()
+    def _save_swa(self, model: HDCEModel, store: DMLStore, swa: list, d: str) -> None:
+        """``swa_epochs``: the mean of the last epochs' weight snapshots, with every expert's BN statistics
+        re-estimated on its own training streams -- torch's momentum=None cumulative average over batches of
+        n_users x batch_size_DML samples, the training step's BN batch (the running statistics of the trained
+        weights do not describe the averaged ones) -- saved under the tag "swa" for ``model_val(hdce_tag="swa")``.
+        The trained weights and statistics are put back afterwards.  (An estimator-side option beside the
+        reference protocol, which evaluates the last epoch: Test.py:64-100.)"""
+        from .evaluate import recalibrate_bn, restore_bn
+        sp = model.space
+        keep = sp.flat.clone()
+        sp.flat.copy_(swa[0] / swa[1])
+        xs, ex = [], []
+        for e in range(self.n_scenarios):
+            streams = (store.scen == e).nonzero().flatten().to(store.Yp.device)
+            Yp = store.Yp.index_select(0, streams)               # (U, n, ...): sample-major, the users of one
+            xs.append(Yp.transpose(0, 1).reshape(-1, *Yp.shape[2:]))   # index next to each other, as in a batch
+            ex.append(torch.full((xs[-1].shape[0],), e, dtype=torch.int64, device=store.Yp.device))
+        x, expert = torch.cat(xs), torch.cat(ex)
+        chunk = self.n_users * self.batch_size_DML
+        if store.Yp.is_cuda and self.hdce_engine == "hip":
+            from .infer import HIPInference
+            eng = HIPInference(model.convs, model.fc, self.Pilot_num, store.Yp.device)
+            saved = eng.recalibrate_bn(model.convs, x, expert, chunk=chunk)
+        else:
+            saved = recalibrate_bn(model.convs, x, expert, chunk=chunk)
+        ck.save_hdce(d, model.convs, model.fc, self.batch_size_DML, self.SNRdb, "swa")
+        restore_bn(model.convs, saved)
+        sp.flat.copy_(keep)
+        self._print(f"HDCE weight average over {swa[1]} epochs saved (tag swa)")
 
     # ------------------------------------------------------------------ classifiers
     @torch.no_grad()

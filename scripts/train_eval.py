@@ -28,13 +28,15 @@ def main():
                     help="HDCE training step: the fused HIP kernels, or torch autograd (with --dtype fp32: all fp32)")
     ap.add_argument("--bn-adapt", action="store_true", help="also run the sweep with test-time BN re-estimation "
                     "(written under <out>/bn_adapt)")
+    ap.add_argument("--swa-epochs", type=int, default=0, help="also average the HDCE weights over the last K epochs "
+                    "and run the sweep on the average (written under <out>/swa, and <out>/swa_bn_adapt with --bn-adapt)")
     a = ap.parse_args()
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.evaluate import model_val
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.runner import Y2HRunner
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.utils.plots import plot_fig2
     os.makedirs(a.out, exist_ok=True)
     common = dict(n_epochs=a.epochs, data_len=a.data_len, batch_size_DML=a.batch, workspace=a.workspace, dtype=a.dtype,
-                  hdce_engine=a.hdce_engine,
+                  hdce_engine=a.hdce_engine, swa_epochs=a.swa_epochs,
                   log_jsonl=os.path.join(a.out, "train_metrics.jsonl"))
     r = Y2HRunner(n_qubits=a.qubits, **common)
     t = {}
@@ -70,6 +72,15 @@ def main():
         t0 = time.time()
         mva.test_for_CE_P128_for_all_scenarios()
         t["eval_bn_adapt_s"] = time.time() - t0
+    if a.swa_epochs > 0:
+        for sub, bn in (("swa", False),) + ((("swa_bn_adapt", True),) if a.bn_adapt else ()):
+            mvs = model_val(workspace=a.workspace, results_dir=os.path.join(a.out, sub), data_len_for_test=a.test_len,
+                            training_data_len=a.data_len, batch_size_DML=a.batch, n_qubits=a.qubits, bn_adapt=bn,
+                            hdce_tag="swa")
+            mvs.epoch_tag = mv.epoch_tag
+            t0 = time.time()
+            mvs.test_for_CE_P128_for_all_scenarios()
+            t[f"eval_{sub}_s"] = time.time() - t0
     summary = {**{k: round(v, 2) for k, v in t.items()},
                "eval_engine": "hip"}
     with open(os.path.join(a.out, "run_summary.json"), "w") as f:

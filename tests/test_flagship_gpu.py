@@ -43,7 +43,7 @@ def _all_state(tr):
             tr.hdce.fc_shadow] + list(tr.hdce.run_mean) + list(tr.hdce.run_var)
 
 
-@pytest.mark.parametrize("mode,split,k", [("dagq", True, 1), ("dagq", False, 1), ("dagq", False, 3)])
+@pytest.mark.parametrize("mode,split,k", [("dagq", True, 1), ("dagq", False, 1), ("dagq", False, 3), ("indep", False, 3)])
 def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     """The multi-stream step (captured in one graph, or the 5-graph DP plan) computes exactly what the
     single-stream eager step computes: every kernel is deterministic (slab reductions, no float
@@ -70,13 +70,14 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     assert float(ref.hopt.step_t[0]) == 4.0 and bool((dag.hopt.step_t == 4.0).all())
 
 
-@pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1)])
+@pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1), ("indep", False, 4)])
 def test_shipped_plans_bit_exact_over_12_steps(cuda, mode, split, k):
     """The plans bench.py / the DP path run -- dagq (QSC branch forked and joined every step, k steps per
-    replay) and the 5-graph data-parallel plan -- reproduce the same plan run eagerly on one stream
-    BIT FOR BIT over 12 steps, in every one of 3 fresh trainer pairs (docs/CONCURRENCY.md: the
-    independent-chains plan dagi does not, in 10-25 of 25 trials on the boxes measured).  (The DP plan
-    reduces the FC bias gradient in its own launch, so its reference is the DP plan run eagerly.)"""
+    replay), indep (the two chains independent for the whole replay, each gathering its own half of the batch)
+    and the 5-graph data-parallel plan -- reproduce the same plan run eagerly on one stream BIT FOR BIT over 12
+    steps, in every one of 3 fresh trainer pairs (docs/CONCURRENCY.md: round 3's independent-chains plan dagi,
+    whose QSC branch read the classifier input the NEXT step's gather rewrote, did not, in 10-25 of 25 trials).
+    (The DP plan reduces the FC bias gradient in its own launch, so its reference is the DP plan run eagerly.)"""
     ctx = DistContext(device=cuda)
     base = dict(batch=32, data_len=800, use_quantumnat=True, qsc_grid_bwd=128)
     for trial in range(3):
