@@ -195,6 +195,9 @@ __device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, i
 // bn.st_out.  (The running statistics advance once per step in the BN tail launch.)
 __device__ void bn_fwd_build(const BnFwd& bn, float* rec, int u, int e, int EC, bool publish) {
   const int tid = threadIdx.x, c = tid >> 3, j = tid & 7, ch = e * CO + c;
+  // gamma / beta issued with the partial sums (loaded by lane j == 0 after the reduction they were one more
+  // dependent round trip of every consumer's prologue)
+  const float g = bn.gamma[ch], bt = bn.beta[ch];
   float mean, var;
   if (bn.training) {
     const float2 sm = bn_part_sums(bn.stats, u, bn.chunks, EC, ch, j);
@@ -205,8 +208,8 @@ __device__ void bn_fwd_build(const BnFwd& bn, float* rec, int u, int e, int EC, 
     var = bn.run_var[ch];
   }
   if (j == 0) {
-    const float g = bn.gamma[ch], inv = rsqrtf(var + bn.eps);
-    const float4 r = make_float4(mean, inv, g * inv, bn.beta[ch] - mean * g * inv);
+    const float inv = rsqrtf(var + bn.eps);
+    const float4 r = make_float4(mean, inv, g * inv, bt - mean * g * inv);
     *reinterpret_cast<float4*>(rec + c * NST) = r;
     if (publish) *reinterpret_cast<float4*>(bn.st_out + ((size_t)u * EC + ch) * NST) = r;
   }
@@ -216,10 +219,12 @@ __device__ void bn_fwd_build(const BnFwd& bn, float* rec, int u, int e, int EC, 
 // in.  (dgamma / dbeta: column sums of the same partials, in the step's batched slab reduction.)
 __device__ void bn_bwd_build(const BnBwd& bn, const float* __restrict__ st, float* rec, int u, int e, int EC) {
   const int tid = threadIdx.x, c = tid >> 3, j = tid & 7, ch = e * CO + c;
+  // the forward record and gamma issued with the partial sums (one round trip for the whole build)
+  const float4 f = *reinterpret_cast<const float4*>(st + ((size_t)u * EC + ch) * NST);
+  const float gm = bn.gamma[ch];
   const float2 sg = bn_part_sums(bn.rslab, u, bn.chunks, EC, ch, j);
   if (j == 0) {
-    const float4 f = *reinterpret_cast<const float4*>(st + ((size_t)u * EC + ch) * NST);
-    const float c1 = bn.gamma[ch] * f.y;
+    const float c1 = gm * f.y;
     *reinterpret_cast<float4*>(rec + c * NST) = f;
     *reinterpret_cast<float4*>(rec + c * NST + 4) = make_float4(c1, c1 * sg.x / bn.count, c1 * sg.y / bn.count, 0.f);
   }
@@ -399,14 +404,16 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
     const bool build = (INM == IN_BNRELU && bnf.stats) || (INM == IN_BNBWD && bnb.rslab);
     if constexpr (!RAWIN)
       if (!build && tid < CIN * NST) tp = st_in[((size_t)u * EC_in + e * CIN) * NST + tid];
-#pragma unroll
-    for (int k = 0; k < WPT; ++k)
-      if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) wl[tid + 256 * k] = tw[k];
+    // the BN build's loads go out behind the weight loads, before the weights' LDS stores wait for them (built
+    // after the stores, the partial sums were a second dependent round trip of the prologue)
     if constexpr (INM == IN_BNRELU) {
       if (build) bn_fwd_build(bnf, stl, u, e, EC_in, chunk == 0);
     } else if constexpr (INM == IN_BNBWD) {
       if (build) bn_bwd_build(bnb, st_in, stl, u, e, EC_in);
     }
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) wl[tid + 256 * k] = tw[k];
     if constexpr (!RAWIN)
       if (!build && tid < CIN * NST) stl[tid] = tp;
   }
@@ -902,19 +909,6 @@ __device__ __forceinline__ void conv3x3_wgrad_body(const TIN* __restrict__ xin, 
   for (int t = 0; t < MTW; ++t) acc[t] = f32x16{};
   const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb);
 
-  // ---- BN parameters of this block's (group, expert) channels -> LDS once: [x: CIN][dz: CO] x NST ----
-  float* prm = reinterpret_cast<float*>(DZ + CO * DZS);
-  if constexpr (INM == IN_BNRELU) {
-    const float* sp = st_prev + ((size_t)u * E * CIN + e * CIN) * NST;
-    for (int i = tid; i < CIN * NST; i += 256) prm[i] = sp[i];
-  }
-  if (bnb.rslab) {   // fused BN backward finalisation
-    bn_bwd_build(bnb, st, prm + CIN * NST, u, e, E * CO);
-  } else {
-    const float* sp = st + ((size_t)u * E * CO + e * CO) * NST;
-    for (int i = tid; i < CO * NST; i += 256) prm[CIN * NST + i] = sp[i];
-  }
-
   // ---- one-sample-ahead register prefetch: sample n+1's loads fly during sample n's MFMAs ----
   uint4 xr[XIT][XQ], dr[DIT][DQ], zr[DIT];
   auto prefetch = [&](int n) {
@@ -938,7 +932,20 @@ __device__ __forceinline__ void conv3x3_wgrad_body(const TIN* __restrict__ xin, 
       zr[k] = *reinterpret_cast<const uint4*>(z + off);
     }
   };
-  if (n0 < nend) prefetch(n0);
+  if (n0 < nend) prefetch(n0);   // (the first sample's loads fly while the BN records are built)
+
+  // ---- BN parameters of this block's (group, expert) channels -> LDS once: [x: CIN][dz: CO] x NST ----
+  float* prm = reinterpret_cast<float*>(DZ + CO * DZS);
+  if constexpr (INM == IN_BNRELU) {
+    const float* sp = st_prev + ((size_t)u * E * CIN + e * CIN) * NST;
+    for (int i = tid; i < CIN * NST; i += 256) prm[i] = sp[i];
+  }
+  if (bnb.rslab) {   // fused BN backward finalisation
+    bn_bwd_build(bnb, st, prm + CIN * NST, u, e, E * CO);
+  } else {
+    const float* sp = st + ((size_t)u * E * CO + e * CO) * NST;
+    for (int i = tid; i < CO * NST; i += 256) prm[CIN * NST + i] = sp[i];
+  }
 
   for (int n = n0; n < nend; ++n) {
     __syncthreads();   // the previous sample's MFMAs are done reading X / DZ

@@ -37,6 +37,11 @@ class Knobs:
     qsim_mfma12: bool = True
     # the 8-qubit adjoint backward on the matrix cores (qsim12_mfma.hip qd_qsim_mfma8_bwd; else qsim.hip's)
     qsim_mfma_bwd: bool = True
+    # conv stack launch shapes (ops/conv.py ConvStackHIP): samples per wave of the forward / dgrad kernels (4 waves per
+    # workgroup), samples per workgroup of the fused layer-3/2 backward and of layer 1's weight gradient
+    conv_spw: int = 2
+    conv_spb_f: int = 5
+    conv_spb_w1: int = 4
 
 
 KNOBS = Knobs()
