@@ -91,7 +91,7 @@ def main() -> int:
                     help="FC GEMM tile configurations 'fwd,wgrad,dgrad' (knobs.KNOBS.gemm_cfg; default: the shipped ones)")
     ap.add_argument("--spread-windows", type=int, default=8,
                     help="extra event-timed windows after the timed region (step_spread in the JSON line); 0 = off")
-    ap.add_argument("--stream-mode", default="dagq", choices=["serial", "dagq", "indep"],
+    ap.add_argument("--stream-mode", default="indep", choices=["serial", "dagq", "indep"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, or the QSC branch "
                          "forked off the HDCE chain")
     ap.add_argument("--fc-adam-side", type=int, default=0,

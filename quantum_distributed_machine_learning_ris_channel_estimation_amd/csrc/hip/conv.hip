@@ -157,8 +157,22 @@ struct BnRed {
   float* part;         // (U, chunks, 2, EC)
 };
 
+// COH: a value another workgroup of the SAME launch wrote (the persistent forward, conv_fwd_stack_kernel): an
+// agent-scope atomic access (coherent across the XCDs' L2s, no cache-wide writeback / invalidate); else a plain one
+template <bool COH>
+__device__ __forceinline__ float ld_part(const float* p) {
+  if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void st_part(float* p, float v) {
+  if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 // sums of the two planar partial rows of channel ch over the chunks of group u (8 lanes per
 // channel; up to 64 chunks with every load in flight at once)
+template <bool COH = false>
 __device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, int u, int chunks, int EC, int ch,
                                                int j) {
   float a = 0.f, b = 0.f;
@@ -169,8 +183,8 @@ __device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, i
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int k = j + 8 * i < chunks ? j + 8 * i : 0;
-    pa[i] = p[(size_t)k * 2 * EC];
-    pb[i] = p[(size_t)k * 2 * EC + EC];
+    pa[i] = ld_part<COH>(p + (size_t)k * 2 * EC);
+    pb[i] = ld_part<COH>(p + (size_t)k * 2 * EC + EC);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -180,8 +194,8 @@ __device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, i
     }
   }
   for (int k = j + 64; k < chunks; k += 8) {
-    a += p[(size_t)k * 2 * EC];
-    b += p[(size_t)k * 2 * EC + EC];
+    a += ld_part<COH>(p + (size_t)k * 2 * EC);
+    b += ld_part<COH>(p + (size_t)k * 2 * EC + EC);
   }
 #pragma unroll
   for (int m = 1; m < 8; m <<= 1) {
@@ -193,6 +207,7 @@ __device__ __forceinline__ float2 bn_part_sums(const float* __restrict__ part, i
 
 // rec[c * NST + ST_MEAN .. ST_B] for the 32 channels of (u, e); publish: also write the record to
 // bn.st_out.  (The running statistics advance once per step in the BN tail launch.)
+template <bool COH = false>
 __device__ void bn_fwd_build(const BnFwd& bn, float* rec, int u, int e, int EC, bool publish) {
   const int tid = threadIdx.x, c = tid >> 3, j = tid & 7, ch = e * CO + c;
   // gamma / beta issued with the partial sums (loaded by lane j == 0 after the reduction they were one more
@@ -200,7 +215,7 @@ __device__ void bn_fwd_build(const BnFwd& bn, float* rec, int u, int e, int EC, 
   const float g = bn.gamma[ch], bt = bn.beta[ch];
   float mean, var;
   if (bn.training) {
-    const float2 sm = bn_part_sums(bn.stats, u, bn.chunks, EC, ch, j);
+    const float2 sm = bn_part_sums<COH>(bn.stats, u, bn.chunks, EC, ch, j);
     mean = sm.x / bn.count;
     var = fmaxf(sm.y / bn.count - mean * mean, 0.f);
   } else {
@@ -237,7 +252,7 @@ __device__ void bn_bwd_build(const BnBwd& bn, const float* __restrict__ st, floa
 // DGRAD: weights used transposed + flipped (W[e*32+k][lane][8-tap]); output fp32.
 // wt: B fragments pre-packed by pack_weights_kernel (fwd or dgrad order).
 // ------------------------------------------------------------------------------------------
-template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN, bool STAMP = false>
+template <int CIN, int H, int W, int INM, int OUTM, bool DGRAD, typename TIN, bool STAMP = false, bool COH = false>
 __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const uint16_t* __restrict__ zaux,
                                              const float* __restrict__ st_in, const uint16_t* __restrict__ wt,
                                              void* __restrict__ out, float* __restrict__ stats, int E, int B,
@@ -407,7 +422,7 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
     // the BN build's loads go out behind the weight loads, before the weights' LDS stores wait for them (built
     // after the stores, the partial sums were a second dependent round trip of the prologue)
     if constexpr (INM == IN_BNRELU) {
-      if (build) bn_fwd_build(bnf, stl, u, e, EC_in, chunk == 0);
+      if (build) bn_fwd_build<COH>(bnf, stl, u, e, EC_in, chunk == 0);
     } else if constexpr (INM == IN_BNBWD) {
       if (build) bn_bwd_build(bnb, st_in, stl, u, e, EC_in);
     }
@@ -582,7 +597,7 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
 #pragma unroll
       for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
       float* dst = OUTM == OUT_Z_STATS ? stats : brd.part;
-      dst[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;   // planar [2][EC] rows
+      st_part<COH>(dst + (((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c, t);   // planar [2][EC] rows
     }
   }
   if constexpr (STAMP) {
@@ -600,6 +615,170 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
                                                       unsigned long long* __restrict__ stamps = nullptr) {
   conv3x3_body<CIN, H, W, INM, OUTM, DGRAD, TIN, STAMP>(xin, zaux, st_in, wt, out, stats, E, B, chunks, spw, bnf, bnb,
                                                         brd, stamps, blockIdx.x, blockIdx.y, gridDim.x);
+}
+
+// ------------------------------------------------------------------------------------------
+// conv_fwd_stack_kernel: the training forward of all three conv/BN/ReLU layers -- and the BN tail (layer 3's
+// records, h3 = relu(bn3(z3)) for the FC GEMM, the running statistics) -- as ONE persistent launch.
+// Workgroup (group u, chunk, expert e) runs conv3x3_body for layer 1, 2, 3 on the same samples, so each wave
+// re-reads only the z it wrote itself (through its CU's L2: no cross-XCD traffic, no writeback between layers);
+// between layers the `chunks` workgroups of stream (u, e) meet at a barrier, after which every one of them builds
+// the next BN records from the stream's statistics partials (agent-scope atomic stores / loads: coherent across
+// the XCDs).  Replaces 4 launches (3 conv + BN tail): no launch gaps, no per-kernel dispatch ramp and tail, no
+// end-of-kernel L2 writeback of the activations between layers.  Bitwise the same z / h3 / records as the
+// per-layer launches (same bodies, same partials, same summation order); the running statistics are summed in
+// the consumers' order (bn_part_sums) instead of bn_fin_body's.
+// Co-residency: the grid must fit the chip at once (checked on the host with the occupancy API, 2 workgroups per
+// CU by launch bounds / LDS), and every barrier wait gives up after kStackSpin polls (the error word is set and
+// the launch completes with wrong values instead of hanging).
+// ------------------------------------------------------------------------------------------
+constexpr int kStackSpin = 1 << 20;
+struct StackSync {
+  unsigned* bar;      // (U * E) x 2: arrivals, generation -- one barrier per stream (group u, expert e)
+  unsigned* arrive;   // E x 3: streams of expert e past layer l (the last one updates the running statistics)
+  int* err;           // set when a barrier wait gave up
+};
+struct StackFwd {
+  const float* x1;              // (N, E*2, H, W) f32 pilots
+  const uint16_t* w[3];         // packed forward B fragments (pack_weights)
+  uint16_t* z[3];               // pre-BN outputs (bf16)
+  float* stats[3];              // (U, chunks, 2, EC) statistics partials
+  const float* gamma[3];
+  const float* beta[3];
+  float* run_mean[3];
+  float* run_var[3];
+  float* st[3];                 // (U, EC, NST) published records
+  uint16_t* h3;                 // (N * E, 32 * HW) bf16: relu(bn3(z3)), the FC operand
+  long long* nbt;               // (E * 3) num_batches_tracked, or null
+  long long nbt_inc;
+  float count, momentum, eps;
+};
+
+__device__ __forceinline__ unsigned ld_agent_u(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the n workgroups of one stream: sense-reversal barrier on (arrivals, generation), agent-scope atomics.  Every
+// wave first waits for its own stores: the statistics partials are agent-scope atomic stores, complete = visible
+// to the other XCDs (z needs nothing: only the wave that wrote it reads it back)
+__device__ void stream_barrier(unsigned* bar, int n, int* err) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* cnt = bar;
+    unsigned* gen = bar + 1;
+    const unsigned g = ld_agent_u(gen);
+    __builtin_amdgcn_s_waitcnt(0);   // (the generation is read before this workgroup arrives)
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)n - 1) {    // the last arrival resets the count, then releases the others
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int it = 0;
+      while (ld_agent_u(gen) == g) {
+        if (++it > kStackSpin) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// running statistics of layer l, expert e, after every stream of the expert passed layer l's barrier: the groups'
+// mean / var as the consumers computed them (bn_part_sums), momentum-updated in group order (the reference's
+// per-stream BatchNorm calls); num_batches_tracked with layer 0
+__device__ void stack_running_stats(const StackFwd& a, int l, int e, int U, int chunks, int EC) {
+  const int tid = threadIdx.x, c = tid >> 3, j = tid & 7, ch = e * CO + c;
+  float rm = a.run_mean[l][ch], rv = a.run_var[l][ch];
+  for (int u = 0; u < U; ++u) {
+    const float2 sm = bn_part_sums<true>(a.stats[l], u, chunks, EC, ch, j);
+    const float mean = sm.x / a.count, var = fmaxf(sm.y / a.count - mean * mean, 0.f);
+    rm = (1.f - a.momentum) * rm + a.momentum * mean;
+    rv = (1.f - a.momentum) * rv + a.momentum * var * a.count / (a.count - 1.f);
+  }
+  if (j == 0) {
+    a.run_mean[l][ch] = rm;
+    a.run_var[l][ch] = rv;
+  }
+  if (l == 0 && a.nbt && tid < 3) a.nbt[e * 3 + tid] += a.nbt_inc;
+}
+
+template <int W>
+__global__ void __launch_bounds__(256, 2) conv_fwd_stack_kernel(StackFwd a, StackSync sy, int E, int B, int U,
+                                                                int chunks, int spw) {
+  __shared__ int last;
+  const int bx = blockIdx.x, e = blockIdx.y, u = bx / chunks, chunk = bx % chunks;
+  const int EC = E * CO;
+  unsigned* bar = sy.bar + 2 * (u * E + e);
+  auto bnf = [&](int l) {
+    return BnFwd{a.stats[l], a.gamma[l], a.beta[l], a.run_mean[l], a.run_var[l], a.st[l], chunks, a.count, a.momentum,
+                 a.eps, 1};
+  };
+  // after stream (u, e) passed layer l's barrier: its chunk-0 workgroup counts the stream in; the expert's last
+  // stream updates the layer's running statistics
+  auto arrive = [&](int l) {
+    if (threadIdx.x == 0) {
+      last = 0;
+      if (chunk == 0) {
+        unsigned* c = sy.arrive + e * 3 + l;
+        if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)U - 1) {
+          __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          last = 1;
+        }
+      }
+    }
+    __syncthreads();
+    if (last) stack_running_stats(a, l, e, U, chunks, EC);
+  };
+  conv3x3_body<2, 16, W, IN_RAW_F32, OUT_Z_STATS, false, float, false, true>(
+      a.x1, nullptr, nullptr, a.w[0], a.z[0], a.stats[0], E, B, chunks, spw, BnFwd{}, BnBwd{}, BnRed{}, nullptr, bx, e,
+      gridDim.x);
+  stream_barrier(bar, chunks, sy.err);
+  arrive(0);
+  conv3x3_body<32, 16, W, IN_BNRELU, OUT_Z_STATS, false, uint16_t, false, true>(
+      a.z[0], nullptr, nullptr, a.w[1], a.z[1], a.stats[1], E, B, chunks, spw, bnf(0), BnBwd{}, BnRed{}, nullptr, bx, e,
+      gridDim.x);
+  stream_barrier(bar, chunks, sy.err);
+  arrive(1);
+  conv3x3_body<32, 16, W, IN_BNRELU, OUT_Z_STATS, false, uint16_t, false, true>(
+      a.z[1], nullptr, nullptr, a.w[2], a.z[2], a.stats[2], E, B, chunks, spw, bnf(1), BnBwd{}, BnRed{}, nullptr, bx, e,
+      gridDim.x);
+  stream_barrier(bar, chunks, sy.err);
+  arrive(2);
+  // ---- tail: layer 3's records (chunk 0 publishes them for the backward), then h3 = relu(a z3 + b) for every
+  // wave's own samples (the z3 it wrote), 8 items of 8 values per lane and sample, all loads in flight ----
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* stl = reinterpret_cast<float*>(smem);
+  bn_fwd_build<true>(bnf(2), stl, u, e, EC, chunk == 0);
+  __syncthreads();
+  constexpr int HW = 16 * W, ITEMS = CO * HW / 8, PER = ITEMS / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n0 = u * B + (chunk * 4 + wv) * spw, nend = min((u + 1) * B, n0 + spw);
+  for (int n = n0; n < nend; ++n) {
+    const size_t base = ((size_t)n * E + e) * CO * HW;
+    uint4 raw[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) raw[k] = *reinterpret_cast<const uint4*>(a.z[2] + base + (size_t)(lane + 64 * k) * 8);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = lane + 64 * k, c = (i * 8) / HW;
+      const f32x2 a2 = {stl[c * NST + ST_A], stl[c * NST + ST_A]}, b2 = {stl[c * NST + ST_B], stl[c * NST + ST_B]};
+      const uint32_t r4[4] = {raw[k].x, raw[k].y, raw[k].z, raw[k].w};
+      uint32_t w4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x2 y = unpack_bf16x2(r4[q]) * a2 + b2;
+        y.x = relu_nan(y.x);
+        y.y = relu_nan(y.y);
+        w4[q] = pack_bf16x2(y);
+      }
+      *reinterpret_cast<uint4*>(a.h3 + base + (size_t)i * 8) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1919,6 +2098,45 @@ QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const u
                                     dim3(256), fwd_smem(32, H, W), s, (const uint16_t*)xin, nullptr, st_prev, w, z,
                                     stats, E, B, chunks, spw, bf, bb, BnRed{}))
   }
+  return (int)hipGetLastError();
+}
+
+// The persistent training forward (conv_fwd_stack_kernel).  sync: (U*E)*2 + E*3 + 1 zero-initialised words --
+// the barriers, the per-(expert, layer) arrival counts and the error word (all return to zero after a launch, the
+// error word excepted).  Returns hipErrorInvalidValue when the shapes do not fit and hipErrorInvalidConfiguration
+// when the grid cannot be resident all at once (the caller keeps the per-layer launches then);
+// qd_conv_fwd_stack_fits answers that without launching.
+template <int W>
+static int stack_fits(int grid) {
+  static int cap = -1;   // co-resident workgroups of this kernel on the device (per W)
+  if (cap < 0) {
+    int nb = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_fwd_stack_kernel<W>, 256, fwd_smem(32, 16, W)) !=
+            hipSuccess)
+      return 0;
+    cap = nb * cus;
+  }
+  return grid <= cap;
+}
+QD_API int qd_conv_fwd_stack_fits(int N, int E, int B, int H, int W, int chunks) {
+  if (H != 16 || N % B) return 0;
+  const int grid = (N / B) * chunks * E;
+  if (W == 8) return stack_fits<8>(grid);
+  if (W == 16) return stack_fits<16>(grid);
+  return 0;
+}
+QD_API int qd_conv_fwd_stack(const StackFwd* a, unsigned* sync, int N, int E, int B, int H, int W, int chunks, int spw,
+                             void* stream) {
+  if (!a || !sync || N % B || chunks * 4 * spw < B || (N / B) > kMaxGroups) return (int)hipErrorInvalidValue;
+  if (!qd_conv_fwd_stack_fits(N, E, B, H, W, chunks)) return (int)hipErrorInvalidConfiguration;
+  const int U = N / B;
+  StackSync sy{sync, sync + 2 * U * E, reinterpret_cast<int*>(sync + 2 * U * E + 3 * E)};
+  dim3 grid(U * chunks, E);
+  hipStream_t s = (hipStream_t)stream;
+  QD_GEOM(WW, hipLaunchKernelGGL((conv_fwd_stack_kernel<WW>), grid, dim3(256), fwd_smem(32, 16, WW), s, *a, sy, E, B,
+                                  U, chunks, spw))
   return (int)hipGetLastError();
 }
 

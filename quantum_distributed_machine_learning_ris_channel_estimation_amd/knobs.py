@@ -39,6 +39,9 @@ class Knobs:
     qsim_mfma_bwd: bool = True
     # conv stack launch shapes (ops/conv.py ConvStackHIP): samples per wave of the forward / dgrad kernels (4 waves per
     # workgroup), samples per workgroup of the fused layer-3/2 backward and of layer 1's weight gradient
+    # the conv stack's training forward as one persistent launch (conv.hip conv_fwd_stack_kernel; else 3 conv launches
+    # + the BN tail launch)
+    conv_stack: bool = False
     conv_spw: int = 2
     conv_spb_f: int = 5
     conv_spb_w1: int = 4

@@ -38,6 +38,13 @@ class BnRed(ctypes.Structure):
     _fields_ = [("z", _p), ("st", _p), ("part", _p)]
 
 
+class StackFwd(ctypes.Structure):
+    """csrc/hip/conv.hip ``StackFwd``: the persistent training forward's operands (conv_fwd_stack_kernel)."""
+    _fields_ = [("x1", _p), ("w", _p * 3), ("z", _p * 3), ("stats", _p * 3), ("gamma", _p * 3), ("beta", _p * 3),
+                ("run_mean", _p * 3), ("run_var", _p * 3), ("st", _p * 3), ("h3", _p), ("nbt", _p),
+                ("nbt_inc", ctypes.c_longlong), ("count", _f), ("momentum", _f), ("eps", _f)]
+
+
 class BnBwd(ctypes.Structure):
     """csrc/hip/conv.hip ``BnBwd``: BN backward finalisation fused into the wgrad / dgrad kernels."""
     _fields_ = [("rslab", _p), ("gamma", _p), ("chunks", _i), ("count", _f)]
@@ -148,6 +155,16 @@ class ConvStackHIP:
         # layer 3's BN backward partials from the FC data gradient's epilogue (enable_dgrad_bnred): 0 = own launch
         self.bnred_mt = 0
         self._fwd8 = nat.fn(L, "qd_conv_fwd_f8", [_p] * 4 + [_i] * 7 + [_p] * 6)
+        # the training forward as ONE persistent launch (conv_fwd_stack_kernel: the 3 layers + the BN tail, per-stream
+        # barriers between layers) when its grid fits the chip at once; the bf16 FC operand only (the fp8
+        # estimator's e4m3 copy and amax come from the per-layer path's BN tail)
+        self.stack = bool(KNOBS.conv_stack and dev.type == "cuda" and not self.fp8 and not self.f8conv
+                          and nat.fn(L, "qd_conv_fwd_stack_fits", [_i] * 6)(self.N, self.E, self.B, self.H, self.W,
+                                                                           self.chunks))
+        if self.stack:
+            self._stackf = nat.fn(L, "qd_conv_fwd_stack", [_p, _p] + [_i] * 7 + [_p])
+            # barriers (U*E x 2), per-(expert, layer) arrival counts (E x 3), the error word: zero between launches
+            self.stack_sync = torch.zeros(2 * U * self.E + 3 * self.E + 1, dtype=torch.int32, device=dev)
 
     def enable_dgrad_bnred(self, mt: int) -> None:
         """Layer 3's BN backward partials come from the FC data gradient's epilogue (ops.fc.gemm_dgrad_bnred,
@@ -200,6 +217,12 @@ class ConvStackHIP:
         hook = self.stage_hook
         if hook is not None:
             hook("packed")
+        if training and self.stack:
+            self._forward_stack(x1, st)
+            if hook is not None:
+                for k in range(3):
+                    hook(f"conv{k + 1}")
+            return self.h3
         f8 = self.f8s
         inp, st_prev = x1, None
         for k in range(3):
@@ -247,6 +270,28 @@ class ConvStackHIP:
                               self.HW, _ptr(self.h3_8), nat.ptr(f8.qs) if f8 else None,
                               nat.ptr(f8.amax[0]) if f8 else None, st), "bn_relu_apply")
         return self.h3
+
+    def _forward_stack(self, x1: torch.Tensor, st) -> None:
+        m = self.m
+        nbt = getattr(m, "_nbt", None) if self.count_batches else None
+        assert nbt is None or nbt.numel() == 3 * self.E, "num_batches_tracked: 3 counters per expert"
+        a = StackFwd()
+        a.x1 = nat.ptr(x1)
+        for k in range(3):
+            a.w[k], a.z[k], a.stats[k] = nat.ptr(self.wpk[k]), nat.ptr(self.z[k]), nat.ptr(self.stats[k])
+            a.gamma[k], a.beta[k] = nat.ptr(m.bn_w[k]), nat.ptr(m.bn_b[k])
+            a.run_mean[k], a.run_var[k], a.st[k] = nat.ptr(m.run_mean[k]), nat.ptr(m.run_var[k]), nat.ptr(self.st[k])
+        a.h3 = nat.ptr(self.h3)
+        a.nbt = _ptr(nbt)
+        a.nbt_inc = self.U
+        a.count, a.momentum, a.eps = float(self.B * self.HW), float(m.momentum), float(m.eps)
+        nat.check(self._stackf(ctypes.byref(a), nat.ptr(self.stack_sync), self.N, self.E, self.B, self.H, self.W,
+                               self.chunks, self.spw, st), "conv_fwd_stack")
+
+    def stack_error(self) -> bool:
+        """True when a persistent forward's barrier wait gave up (its outputs are then wrong): callers check it at
+        a synchronisation point (bench / epoch end)."""
+        return bool(self.stack and int(self.stack_sync[-1]) != 0)
 
     # --------------------------------------------------------------------- backward
     def backward(self, dh3: torch.Tensor, accumulate: bool = True, slabs: Optional["SlabBatch"] = None,

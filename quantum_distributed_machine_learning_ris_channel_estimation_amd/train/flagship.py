@@ -7,13 +7,17 @@ NLL, AdamW, optional QuantumNAT noise and gradient pruning) and the HDCE estimat
 (3 scenario experts + shared FC, per-stream NMSE, Adam), both forward + backward +
 optimizer, on HBM-resident synthetic data.
 
-Execution plan (world = 1, default ``stream_mode="dagq"``): one HIP graph replay runs
-``steps_per_graph`` consecutive training steps (5 in bench), each captured from two streams: the
-QSC branch forks off the HDCE chain after the batch gather and joins it before the HDCE update.
-Almost every kernel of this model is latency-bound and fills a fraction of the 256 CUs, so the
-QSC branch overlaps the HDCE chain.  (Plans that let the two chains run independently across step
-boundaries were ~1.5% faster but not bit-reproducible on ROCm 7.x; they were measured and removed --
-docs/CONCURRENCY.md keeps the findings.)  Per step:
+Execution plan (world = 1, default ``stream_mode="indep"``): one HIP graph replay runs
+``steps_per_graph`` consecutive training steps, captured from two streams that stay independent for the
+whole replay: the HDCE chain (its own gather, forward, backward, Adam) on one, the QSC chain (its own gather of
+the same batch through a second device cursor, forward, backward, AdamW) on the other, joined once at the end
+of the replay.  Almost every kernel of this model is latency-bound and fills a fraction of the 256 CUs, so the
+QSC chain overlaps the HDCE chain, and the HDCE chain has no cross-queue edge (each one costs a queue
+hand-over).  0.3997 / 0.4008 ms/step against 0.4104 / 0.4105 for ``"dagq"`` (the QSC branch forked after a
+shared gather and joined before the HDCE update every step) on one box (profiles/r5_10_ab.txt); bit-identical
+to the serial step.  (Round 3's independent plans shared the gather's classifier input across the streams --
+the next step's gather could rewrite it under the QSC forward -- and were not reproducible: docs/CONCURRENCY.md.)
+Per step:
 
   main : gather -> conv fwd x3 -> BN/ReLU apply (+ BN tail) -> FC fwd GEMM -> one-pass NMSE ->
          FC wgrad GEMM -> FC dgrad GEMM -> BN bwd reduce (+ loss finish) -> [wgrad|dgrad] L3 ->
@@ -68,7 +72,7 @@ class FlagshipConfig:
     qsc_weight_decay: float = 0.01
     hip_graphs: bool = True
     split_graphs: bool = False   # force the DP execution plan (5 graphs) even at world 1 (testing)
-    stream_mode: str = "dagq"    # serial | dagq (see FlagshipTrainer.__init__)
+    stream_mode: str = "indep"   # serial | dagq | indep (see FlagshipTrainer.__init__)
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
     fused_fc_adam: bool = False  # (world 1, GPU, bf16) the FC weight's Adam step in the weight-gradient GEMM's
     #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
@@ -222,6 +226,8 @@ class FlagshipTrainer(DPPlan):
         #   serial : one stream, one chain
         #   dagq   : ONE graph, the QSC branch forked after the gather and joined at the end of the step; the
         #            HDCE a single chain.  (The DP plan also forks the FC update onto the "fc" stream.)
+        #   indep  : (world 1) the QSC chain with its own gather, independent of the HDCE chain for the whole
+        #            k-step replay (_indep_step); world > 1 runs the DP plan as with dagq
         # (a HIP graph's executor maps parallel branches onto its own pool of queues and every edge that
         # crosses queues costs a barrier packet, so fewer, longer branches win.  Measured and removed in round 3
         # (docs/CONCURRENCY.md): HDCE side branches (FC wgrad / conv wgrads / FC Adam on their own streams),

@@ -91,6 +91,41 @@ def test_conv_stack_backward(cuda, pilot_num, B):
 
 
 @pytest.mark.parametrize("pilot_num,B", [(128, 256), (128, 40), (256, 64)])
+def test_conv_stack_persistent_matches_per_layer(cuda, monkeypatch, pilot_num, B):
+    """The training forward as one persistent launch (conv_fwd_stack_kernel: per-stream barriers between the layers)
+    against the per-layer launches, 3 consecutive steps on fresh inputs: z, h3 and the published BN records bit
+    for bit (the same bodies, partials and summation order), the running statistics to rounding (summed in the
+    consumers' order), the batch counters exactly; the barrier words back at zero and no barrier gave up."""
+    U = 3
+    outs = []
+    for stack in (False, True):
+        monkeypatch.setattr(KNOBS, "conv_stack", stack)
+        a, _ = pair(cuda, pilot_num)
+        conv = ConvStackHIP(a, U, B)
+        conv.count_batches = True
+        assert conv.stack == stack
+        steps = []
+        for step in range(3):
+            torch.manual_seed(10 + step)
+            Yp = torch.randn(3, U, B, 2, a.H, a.W, device=cuda) * (1 + step)
+            h3 = conv.forward(a.pack_input(Yp).contiguous(), training=True)
+            torch.cuda.synchronize()
+            steps.append(dict(h3=h3.clone(), **{f"z{k}": conv.z[k].clone() for k in range(3)},
+                              **{f"st{k}": conv.st[k][..., :4].clone() for k in range(3)}))
+        if stack:
+            assert not conv.stack_error()
+            assert int(conv.stack_sync.abs().sum()) == 0
+        outs.append((steps, [t.clone() for t in a.run_mean + a.run_var], a._nbt.clone()))
+    (s0, r0, n0), (s1, r1, n1) = outs
+    for i, (x, y) in enumerate(zip(s0, s1)):
+        for name in x:
+            assert torch.equal(x[name], y[name]), (i, name, float((x[name].float() - y[name].float()).abs().max()))
+    for x, y in zip(r0, r1):
+        assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), float((x - y).abs().max())
+    assert torch.equal(n0, n1) and int(n1[0]) == 3 * U
+
+
+@pytest.mark.parametrize("pilot_num,B", [(128, 256), (128, 40), (256, 64)])
 def test_conv_bwd_fused_matches_side_by_side(cuda, pilot_num, B):
     """conv3x3_bwd_kernel (one staging per sample feeds wgrad, dgrad and the previous layer's BN
     partials) vs conv3x3_wd_kernel (the two bodies as separate workgroups): the same formulas in the
