@@ -2369,7 +2369,7 @@ QD_API int qd_bn_apply_tail(const uint16_t* z, uint16_t* h, const BnFwd* bnf, co
                             float* const* run_var, float* const* st, int U, int E, int B, int HW, int spb, int chunks,
                             int training, long long* nbt, int n_nbt, long long nbt_inc, uint8_t* h8, const float* qs,
                             float* amax, void* stream) {
-  if (!bnf || U < 1 || U > kMaxGroups || n_nbt > 64 || spb < 1 || B % spb || (h8 && (!qs || !amax)))
+  if (!bnf || U < 1 || U > kMaxGroups || n_nbt > 64 || spb < 1 || (h8 && (!qs || !amax)))
     return (int)hipErrorInvalidValue;
   FinJobs jobs{};
   for (int l = 0; l < 3; ++l) {
@@ -2380,9 +2380,11 @@ QD_API int qd_bn_apply_tail(const uint16_t* z, uint16_t* h, const BnFwd* bnf, co
     jobs.run_var[l] = run_var[l];
     jobs.st[l] = l == 2 ? nullptr : st[l];
   }
-  const int ach = B / spb, EC = E * CO;
+  // (a group of B samples: ceil(B / spb) apply workgroups, the last one partial -- B need not divide: the test-time
+  // BN re-estimation's last chunk of an expert's samples has any size)
+  const int ach = (B + spb - 1) / spb, EC = E * CO;
   const int napply = U * ach * E, nfin = (3 * EC + 3) / 4;
-  if (napply > qd::kAmaxParts) return (int)hipErrorInvalidValue;
+  if (h8 && napply > qd::kAmaxParts) return (int)hipErrorInvalidValue;   // (one amax partial per apply workgroup)
   const dim3 grid(napply + nfin);
   hipStream_t s = (hipStream_t)stream;
 #define QD_TAIL(HWV, U_)                                                                                          \

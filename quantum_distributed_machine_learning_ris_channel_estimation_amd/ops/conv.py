@@ -141,7 +141,7 @@ class ConvStackHIP:
         # the BN tail (running statistics) and layer 3's BN/ReLU apply as ONE launch (False: two launches, the
         # tail publishing layer 3's records -- 1 launch more on the chain)
         self.apply_tail = True
-        self.spb_a = 8 if B % 8 == 0 else 1
+        self.spb_a = 8   # (samples per BN-apply workgroup; a group's last workgroup may be partial)
         self._packm = nat.fn(L, "qd_conv_pack_weights_multi", [_i, _p, _p, _p, _p, _i, _p])
         self._packm2 = nat.fn(L, "qd_conv_pack_weights_multi2", [_i, _p, _p, _p, _p, _i, _p, _i, _p])
         # pack_at_tail: the owner packs the weights at the END of each step (after the optimizer) and

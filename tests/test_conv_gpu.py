@@ -114,11 +114,21 @@ def test_conv_stack_persistent_matches_per_layer(cuda, monkeypatch, pilot_num, B
                               **{f"st{k}": conv.st[k][..., :4].clone() for k in range(3)}))
         if stack:
             assert not conv.stack_error()
-            assert int(conv.stack_sync.abs().sum()) == 0
+            sy = conv.stack_sync.cpu()
+            nb = 2 * U * conv.E
+            # arrivals and the per-(expert, layer) counts back at zero; every stream's generation advanced by
+            # 3 barriers per step
+            assert int(sy[0:nb:2].abs().sum()) == 0 and int(sy[nb:].abs().sum()) == 0, sy
+            assert bool((sy[1:nb:2] == 3 * 3).all()), sy
         outs.append((steps, [t.clone() for t in a.run_mean + a.run_var], a._nbt.clone()))
     (s0, r0, n0), (s1, r1, n1) = outs
     for i, (x, y) in enumerate(zip(s0, s1)):
         for name in x:
+            if name in ("st0", "st1"):
+                # (the per-layer path's BN tail re-publishes layers 1 / 2's records from its own sums -- bn_fin_body's
+                # order -- over the ones the consumers built and normalised with; the persistent launch keeps the latter)
+                assert torch.allclose(x[name], y[name], rtol=1e-5, atol=1e-6), (i, name)
+                continue
             assert torch.equal(x[name], y[name]), (i, name, float((x[name].float() - y[name].float()).abs().max()))
     for x, y in zip(r0, r1):
         assert torch.allclose(x, y, rtol=1e-5, atol=1e-6), float((x - y).abs().max())

@@ -64,12 +64,15 @@ def test_hip_bn_recalibration_matches_torch(cuda):
     ref_convs, hip_convs = copy.deepcopy(convs), copy.deepcopy(convs)
     eng = HIPInference(hip_convs, fc, 128, cuda, chunk=576)
     torch.manual_seed(1)
-    N = 2500
+    N = 10003
     x = torch.randn(N, 2, 16, 8, device=cuda) * 0.7 + 0.1
-    expert = torch.randint(0, 2, (N,), device=cuda)   # expert 2 gets nothing
+    expert = torch.arange(N, device=cuda) % 2          # expert 2 gets nothing
     expert[:1] = 2                                     # ... one sample: < 2, skipped
-    saved_ref = recalibrate_bn(ref_convs, x, expert, chunk=1000)
-    saved_hip = eng.recalibrate_bn(hip_convs, x, expert, chunk=1000)
+    # (5001 samples per expert: chunks of 3000 + 2001 -- the last not a multiple of the BN tail's 8 samples per
+    # workgroup, so its last workgroup is partial; rounds 3-4 refused such groups above 1365 samples, which broke
+    # FIG1's bn_adapt sweep)
+    saved_ref = recalibrate_bn(ref_convs, x, expert, chunk=3000)
+    saved_hip = eng.recalibrate_bn(hip_convs, x, expert, chunk=3000)
     bn = lambda cs: [m for c in cs for m in c.modules() if isinstance(m, torch.nn.BatchNorm2d)]
     for i, (a, b, o) in enumerate(zip(bn(ref_convs), bn(hip_convs), bn(convs))):
         e = i // 3
