@@ -94,6 +94,9 @@ def main() -> int:
     ap.add_argument("--stream-mode", default="indep", choices=["serial", "dagq", "indep"],
                     help="how the step's independent branches run (FlagshipTrainer): one chain, or the QSC branch "
                          "forked off the HDCE chain")
+    ap.add_argument("--qsc-start", default="step", choices=["step", "conv"],
+                    help="(stream mode indep) when each step's QSC chain starts: with the step, or after the HDCE conv "
+                         "forward (FlagshipConfig.qsc_start)")
     ap.add_argument("--fc-adam-side", type=int, default=0,
                     help="world 1: the FC weight's Adam on a side stream beside the conv backward, capped at this many "
                          "workgroups (FlagshipConfig.fc_adam_side; 0 = off)")
@@ -162,7 +165,8 @@ def main() -> int:
         cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch,
                              data_len=args.data_len, dtype=args.dtype, hip_graphs=not args.no_graphs,
                              use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
-                             stream_mode=args.stream_mode, steps_per_graph=args.steps_per_graph,
+                             stream_mode=args.stream_mode, qsc_start=args.qsc_start,
+                             steps_per_graph=args.steps_per_graph,
                              dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in,
                              ramp=args.ramp, fc_adam_side=args.fc_adam_side)
         return FlagshipTrainer(cfg, ctx, store=store)

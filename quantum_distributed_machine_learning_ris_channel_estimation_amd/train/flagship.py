@@ -73,6 +73,8 @@ class FlagshipConfig:
     hip_graphs: bool = True
     split_graphs: bool = False   # force the DP execution plan (5 graphs) even at world 1 (testing)
     stream_mode: str = "indep"   # serial | dagq | indep (see FlagshipTrainer.__init__)
+    qsc_start: str = "step"      # (indep) "conv": each step's QSC chain waits for the HDCE conv forward (one HDCE ->
+    #                              QSC edge, none on the HDCE chain), so the conv kernels have the chip to themselves
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
     fused_fc_adam: bool = False  # (world 1, GPU, bf16) the FC weight's Adam step in the weight-gradient GEMM's
     #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
@@ -440,12 +442,20 @@ class FlagshipTrainer(DPPlan):
         first node (a branch forked before any node would be a root of the graph)."""
         self._gather(classifier=False)
         q = self.streams["qsc"]
-        if first:
+        after_conv = self.cfg.qsc_start == "conv" and self.hstep.hip
+        if after_conv:
+            self.hstep.forward_conv_gathered(self.gat)
+        if first or after_conv:
             q.wait_stream(torch.cuda.current_stream(self.ctx.device))
         with torch.cuda.stream(q):
             self._gather(hdce=False, classifier=True)
             self._qsc_branch(with_opt=True)
-        self._hdce_forward()
+        if after_conv:
+            loss = self.hstep.forward_fc_after_conv(self.store)
+            if loss is not self.hloss:
+                self.hloss.copy_(loss)
+        else:
+            self._hdce_forward()
         self.hstep.backward_conv()
         self._hdce_update()
 

@@ -43,17 +43,20 @@ def _all_state(tr):
             tr.hdce.fc_shadow] + list(tr.hdce.run_mean) + list(tr.hdce.run_var)
 
 
-@pytest.mark.parametrize("mode,split,k", [("dagq", True, 1), ("dagq", False, 1), ("dagq", False, 3), ("indep", False, 3)])
+@pytest.mark.parametrize("mode,split,k", [("dagq", True, 1), ("dagq", False, 1), ("dagq", False, 3), ("indep", False, 3),
+                                         ("indep+conv", False, 3)])
 def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     """The multi-stream step (captured in one graph, or the 5-graph DP plan) computes exactly what the
     single-stream eager step computes: every kernel is deterministic (slab reductions, no float
-    atomics) and the DAG only reorders independent work."""
+    atomics) and the DAG only reorders independent work.  ("indep+conv": the QSC chain of each step starts after
+    the HDCE conv forward, FlagshipConfig.qsc_start.)"""
     ctx = DistContext(device=cuda)
+    mode, _, start = mode.partition("+")
     # (the same QSC backward grid on both sides: it fixes the slab reduction order)
     base = dict(batch=32, data_len=800, use_quantumnat=True, qsc_grid_bwd=128)
     ref = FlagshipTrainer(FlagshipConfig(hip_graphs=False, stream_mode="serial", **base), ctx)
     dag = FlagshipTrainer(FlagshipConfig(hip_graphs=True, stream_mode=mode, split_graphs=split,
-                                         steps_per_graph=k, **base), ctx)
+                                         steps_per_graph=k, qsc_start=start or "step", **base), ctx)
     assert dag.streams is not None and ref.streams is None
     dag.capture(preserve=True, k=k)   # (capturing runs warm-up steps; the state is restored)
     dag.capture(preserve=True, k=1)
@@ -70,7 +73,8 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     assert float(ref.hopt.step_t[0]) == 4.0 and bool((dag.hopt.step_t == 4.0).all())
 
 
-@pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1), ("indep", False, 4)])
+@pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1), ("indep", False, 4),
+                                         ("indep+conv", False, 4)])
 def test_shipped_plans_bit_exact_over_12_steps(cuda, mode, split, k):
     """The plans bench.py / the DP path run -- dagq (QSC branch forked and joined every step, k steps per
     replay), indep (the two chains independent for the whole replay, each gathering its own half of the batch)
@@ -80,11 +84,12 @@ def test_shipped_plans_bit_exact_over_12_steps(cuda, mode, split, k):
     (The DP plan reduces the FC bias gradient in its own launch, so its reference is the DP plan run eagerly.)"""
     import os
     ctx = DistContext(device=cuda)
+    mode, _, start = mode.partition("+")
     base = dict(batch=32, data_len=800, use_quantumnat=True, qsc_grid_bwd=128)
     for trial in range(int(os.environ.get("QDML_BITEXACT_TRIALS", "3"))):   # (more trials: a longer GPU call)
         ref = FlagshipTrainer(FlagshipConfig(hip_graphs=False, stream_mode="serial", split_graphs=split, **base), ctx)
         dag = FlagshipTrainer(FlagshipConfig(hip_graphs=True, stream_mode=mode, split_graphs=split,
-                                             steps_per_graph=k, **base), ctx)
+                                             steps_per_graph=k, qsc_start=start or "step", **base), ctx)
         dag.capture(preserve=True, k=k)
         for rep in range(12 // k):
             for _ in range(k):
