@@ -707,10 +707,15 @@ __device__ void stack_running_stats(const StackFwd& a, int l, int e, int U, int 
   if (l == 0 && a.nbt && tid < 3) a.nbt[e * 3 + tid] += a.nbt_inc;
 }
 
-template <int W>
+// STAMP (diagnostic build, qd_conv_fwd_stack_stamped): per workgroup 8 s_memtime stamps -- start, after each layer's
+// body, after each layer's barrier (+ running statistics), end
+template <int W, bool STAMP = false>
 __global__ void __launch_bounds__(256, 2) conv_fwd_stack_kernel(StackFwd a, StackSync sy, int E, int B, int U,
-                                                                int chunks, int spw) {
+                                                                int chunks, int spw,
+                                                                unsigned long long* __restrict__ stamps = nullptr) {
   __shared__ int last;
+  unsigned long long ts[8] = {};
+  if constexpr (STAMP) ts[0] = phase_stamp();
   const int bx = blockIdx.x, e = blockIdx.y, u = bx / chunks, chunk = bx % chunks;
   const int EC = E * CO;
   unsigned* bar = sy.bar + 2 * (u * E + e);
@@ -737,18 +742,24 @@ __global__ void __launch_bounds__(256, 2) conv_fwd_stack_kernel(StackFwd a, Stac
   conv3x3_body<2, 16, W, IN_RAW_F32, OUT_Z_STATS, false, float, false, true>(
       a.x1, nullptr, nullptr, a.w[0], a.z[0], a.stats[0], E, B, chunks, spw, BnFwd{}, BnBwd{}, BnRed{}, nullptr, bx, e,
       gridDim.x);
+  if constexpr (STAMP) ts[1] = phase_stamp();
   stream_barrier(bar, chunks, sy.err);
   arrive(0);
+  if constexpr (STAMP) ts[2] = phase_stamp();
   conv3x3_body<32, 16, W, IN_BNRELU, OUT_Z_STATS, false, uint16_t, false, true>(
       a.z[0], nullptr, nullptr, a.w[1], a.z[1], a.stats[1], E, B, chunks, spw, bnf(0), BnBwd{}, BnRed{}, nullptr, bx, e,
       gridDim.x);
+  if constexpr (STAMP) ts[3] = phase_stamp();
   stream_barrier(bar, chunks, sy.err);
   arrive(1);
+  if constexpr (STAMP) ts[4] = phase_stamp();
   conv3x3_body<32, 16, W, IN_BNRELU, OUT_Z_STATS, false, uint16_t, false, true>(
       a.z[1], nullptr, nullptr, a.w[2], a.z[2], a.stats[2], E, B, chunks, spw, bnf(1), BnBwd{}, BnRed{}, nullptr, bx, e,
       gridDim.x);
+  if constexpr (STAMP) ts[5] = phase_stamp();
   stream_barrier(bar, chunks, sy.err);
   arrive(2);
+  if constexpr (STAMP) ts[6] = phase_stamp();
   // ---- tail: layer 3's records (chunk 0 publishes them for the backward), then h3 = relu(a z3 + b) for every
   // wave's own samples (the z3 it wrote), 8 items of 8 values per lane and sample, all loads in flight ----
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -778,6 +789,11 @@ __global__ void __launch_bounds__(256, 2) conv_fwd_stack_kernel(StackFwd a, Stac
       }
       *reinterpret_cast<uint4*>(a.h3 + base + (size_t)i * 8) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
+  }
+  if constexpr (STAMP) {
+    ts[7] = phase_stamp();
+    if (threadIdx.x == 0)
+      for (int k = 0; k < 8; ++k) stamps[((size_t)e * gridDim.x + bx) * 8 + k] = ts[k];
   }
 }
 
@@ -2137,6 +2153,19 @@ QD_API int qd_conv_fwd_stack(const StackFwd* a, unsigned* sync, int N, int E, in
   hipStream_t s = (hipStream_t)stream;
   QD_GEOM(WW, hipLaunchKernelGGL((conv_fwd_stack_kernel<WW>), grid, dim3(256), fwd_smem(32, 16, WW), s, *a, sy, E, B,
                                   U, chunks, spw))
+  return (int)hipGetLastError();
+}
+
+// Diagnostic: the persistent forward with per-workgroup phase stamps (stamps: grid * 8 u64, see
+// conv_fwd_stack_kernel).  P128 geometry only.
+QD_API int qd_conv_fwd_stack_stamped(const StackFwd* a, unsigned* sync, int N, int E, int B, int chunks, int spw,
+                                     unsigned long long* stamps, void* stream) {
+  if (!a || !sync || !stamps || N % B || chunks * 4 * spw < B || (N / B) > kMaxGroups) return (int)hipErrorInvalidValue;
+  if (!stack_fits<8>((N / B) * chunks * E)) return (int)hipErrorInvalidConfiguration;
+  const int U = N / B;
+  StackSync sy{sync, sync + 2 * U * E, reinterpret_cast<int*>(sync + 2 * U * E + 3 * E)};
+  hipLaunchKernelGGL((conv_fwd_stack_kernel<8, true>), dim3(U * chunks, E), dim3(256), fwd_smem(32, 16, 8),
+                     (hipStream_t)stream, *a, sy, E, B, U, chunks, spw, stamps);
   return (int)hipGetLastError();
 }
 

@@ -272,6 +272,12 @@ class ConvStackHIP:
         return self.h3
 
     def _forward_stack(self, x1: torch.Tensor, st) -> None:
+        a = self.stack_args(x1)
+        nat.check(self._stackf(ctypes.byref(a), nat.ptr(self.stack_sync), self.N, self.E, self.B, self.H, self.W,
+                               self.chunks, self.spw, st), "conv_fwd_stack")
+
+    def stack_args(self, x1: torch.Tensor) -> "StackFwd":
+        """The persistent forward's operand struct for input ``x1`` (also the stamped diagnostic's)."""
         m = self.m
         nbt = getattr(m, "_nbt", None) if self.count_batches else None
         assert nbt is None or nbt.numel() == 3 * self.E, "num_batches_tracked: 3 counters per expert"
@@ -285,8 +291,7 @@ class ConvStackHIP:
         a.nbt = _ptr(nbt)
         a.nbt_inc = self.U
         a.count, a.momentum, a.eps = float(self.B * self.HW), float(m.momentum), float(m.eps)
-        nat.check(self._stackf(ctypes.byref(a), nat.ptr(self.stack_sync), self.N, self.E, self.B, self.H, self.W,
-                               self.chunks, self.spw, st), "conv_fwd_stack")
+        return a
 
     def stack_error(self) -> bool:
         """True when a persistent forward's barrier wait gave up (its outputs are then wrong): callers check it at

@@ -530,7 +530,12 @@ class FlagshipTrainer(DPPlan):
 
     def _k(self) -> int:
         one = (self.ctx.world == 1 and not self.cfg.split_graphs) or (self.cfg.dp_one_graph and self._use_graphs)
-        return max(1, self.cfg.steps_per_graph) if one else 1
+        if not one:
+            return 1
+        # (a capture runs WARMUP + 1 passes of the k steps inside one permutation of the stream: large batches --
+        # P256 x 1024 samples per stream -- get fewer steps per replay)
+        fit = self.store.n // ((GraphedStep.WARMUP + 1) * self.B)
+        return max(1, min(self.cfg.steps_per_graph, fit))
 
     def _reps(self, n: int):
         """Steps per replay of ``run(n)``: lead_in single steps, one ``ramp``-step replay, then k-step replays, then
