@@ -80,6 +80,9 @@ class FlagshipConfig:
     #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
     #                              separate (profiles/r3_04_fused_adam.txt) -- 256 one-per-CU workgroups stream
     #                              the Adam state far slower than the 2048-workgroup update kernel
+    fc_adam_next: bool = False   # (world 1, indep) the FC weight's Adam on the "fc" stream after the step's other Adam
+    #                              launch, overlapping the next step's gather + conv forward; the next FC forward waits
+    #                              for it (the DP plan's overlap, at world 1)
     fc_adam_side: int = 0        # (world 1, dagq) > 0: the FC weight's Adam runs on the "fc" stream right after the FC
     #                              data gradient -- the last reader of the bf16 shadow it rewrites -- beside the conv
     #                              backward, on at most this many workgroups (so the conv kernels keep most CUs);
@@ -265,6 +268,14 @@ class FlagshipTrainer(DPPlan):
             lo = sp.offsets[sp.names.index("CE.FC.weight")]
             self.hopt.fuse_range(lo, lo + self.hdce.fc_w.numel())
             self.hstep.after_dgrad = self._fc_adam_fork
+        self.fc_adam_next = bool(cfg.fc_adam_next and not self.fused_adam and not self.fc_adam_side
+                                 and self.streams is not None and mode == "indep" and self.hstep.hip
+                                 and cfg.dtype == "bf16" and self.hdce.fc_shadow is not None
+                                 and ctx.world == 1 and not cfg.split_graphs and len(self.hopt.bounds) == 1)
+        if self.fc_adam_next:
+            lo = sp.offsets[sp.names.index("CE.FC.weight")]
+            self.hopt.fuse_range(lo, lo + self.hdce.fc_w.numel())
+        self._fc_pending = False   # (fc_adam_next) an FC update forked in this replay that the next FC forward awaits
         # end-of-step weight pack (GPU fused path)
         self.tail_pack = bool(self.hstep.hip and cfg.tail_pack)
         if self.tail_pack:
@@ -305,9 +316,11 @@ class FlagshipTrainer(DPPlan):
         if self.ctx.world == 1 and not cfg.split_graphs and mode == "indep":
             # the QSC and HDCE chains independent for the whole k-step replay (see _indep_step): one join at its end
             def body():
+                self._fc_pending = False
                 for i in range(k):
                     self._indep_step(first=i == 0)
-                self._join(("qsc",))
+                self._join(("qsc", "fc") if self._fc_pending else ("qsc",))
+                self._fc_pending = False
             gs = [GraphedStep(body, enabled=graphs)]
         elif self.ctx.world == 1 and not cfg.split_graphs:
             # one graph: gather, both forwards, NMSE, both backwards, the optimizers
@@ -442,10 +455,12 @@ class FlagshipTrainer(DPPlan):
         first node (a branch forked before any node would be a root of the graph)."""
         self._gather(classifier=False)
         q = self.streams["qsc"]
-        after_conv = self.cfg.qsc_start == "conv" and self.hstep.hip
+        after_conv = (self.cfg.qsc_start == "conv" or self.fc_adam_next) and self.hstep.hip
         if after_conv:
             self.hstep.forward_conv_gathered(self.gat)
-        if first or after_conv:
+            if self._fc_pending:   # (fc_adam_next) the FC forward reads the weights the previous step's update wrote
+                torch.cuda.current_stream(self.ctx.device).wait_stream(self.streams["fc"])
+        if first or (after_conv and self.cfg.qsc_start == "conv"):
             q.wait_stream(torch.cuda.current_stream(self.ctx.device))
         with torch.cuda.stream(q):
             self._gather(hdce=False, classifier=True)
@@ -458,6 +473,10 @@ class FlagshipTrainer(DPPlan):
             self._hdce_forward()
         self.hstep.backward_conv()
         self._hdce_update()
+        if self.fc_adam_next:
+            with self._fork(self.streams["fc"]):
+                self.hopt.step_fused(grad_scale=1.0, skip=self.hskip)
+            self._fc_pending = True
 
     def skip_flags(self) -> torch.Tensor:
         """(2,) the HDCE and QSC NaN-guard flags of the last step (after the all-reduce: summed)."""

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 output: top kernels per training step.
 
     python scripts/prof_summary.py <kernel_stats.csv> [steps] [top]
-    python scripts/prof_summary.py <kernel_trace.csv> --marker adam_kernel [--per-step 2] [--tail 0.5] [--top 40]
+    python scripts/prof_summary.py <kernel_trace.csv> [--marker 'conv3x3_kernel<2,'] [--per-step 2] [--tail 0.5] [--top 40]
 
 With a kernel *trace*, only the steady-state tail of the run is used (the last ``--tail``
 fraction of dispatches by start time, so data generation / warm-up / graph capture drop out)
@@ -69,7 +69,8 @@ def main():
     ap.add_argument("path")
     ap.add_argument("steps", nargs="?", type=float, default=1.0)
     ap.add_argument("top_pos", nargs="?", type=int, default=None)
-    ap.add_argument("--marker", default="gather_step_kernel")
+    # (the layer-1 conv forward runs once per step in every plan; the batch gather runs twice per step in the indep plan)
+    ap.add_argument("--marker", default="conv3x3_kernel<2,")
     ap.add_argument("--per-step", type=float, default=1.0)
     ap.add_argument("--tail", type=float, default=0.5)
     ap.add_argument("--top", type=int, default=40)

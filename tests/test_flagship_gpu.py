@@ -38,26 +38,33 @@ def test_no_zero_grad_overwrites_every_gradient(cuda):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-7), (i, float((a - b).abs().max()))
 
 
+def _opts(opt: str) -> dict:
+    """'conv' / 'fcnext' (the part of a test mode after '+') -> the FlagshipConfig options they stand for"""
+    return {"conv": {"qsc_start": "conv"}, "fcnext": {"fc_adam_next": True}, "": {}}[opt]
+
+
 def _all_state(tr):
     return [tr.hdce.space.flat, tr.qspace.flat, tr.hopt.m, tr.hopt.v, tr.qopt.m, tr.qopt.v,
             tr.hdce.fc_shadow] + list(tr.hdce.run_mean) + list(tr.hdce.run_var)
 
 
 @pytest.mark.parametrize("mode,split,k", [("dagq", True, 1), ("dagq", False, 1), ("dagq", False, 3), ("indep", False, 3),
-                                         ("indep+conv", False, 3)])
+                                         ("indep+conv", False, 3), ("indep+fcnext", False, 3)])
 def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
     """The multi-stream step (captured in one graph, or the 5-graph DP plan) computes exactly what the
     single-stream eager step computes: every kernel is deterministic (slab reductions, no float
     atomics) and the DAG only reorders independent work.  ("indep+conv": the QSC chain of each step starts after
-    the HDCE conv forward, FlagshipConfig.qsc_start.)"""
+    the HDCE conv forward, FlagshipConfig.qsc_start; "indep+fcnext": the FC weight's Adam overlaps the next step's
+    conv forward, FlagshipConfig.fc_adam_next.)"""
     ctx = DistContext(device=cuda)
     mode, _, start = mode.partition("+")
     # (the same QSC backward grid on both sides: it fixes the slab reduction order)
     base = dict(batch=32, data_len=800, use_quantumnat=True, qsc_grid_bwd=128)
     ref = FlagshipTrainer(FlagshipConfig(hip_graphs=False, stream_mode="serial", **base), ctx)
     dag = FlagshipTrainer(FlagshipConfig(hip_graphs=True, stream_mode=mode, split_graphs=split,
-                                         steps_per_graph=k, qsc_start=start or "step", **base), ctx)
+                                         steps_per_graph=k, **_opts(start), **base), ctx)
     assert dag.streams is not None and ref.streams is None
+    assert dag.fc_adam_next == (start == "fcnext")
     dag.capture(preserve=True, k=k)   # (capturing runs warm-up steps; the state is restored)
     dag.capture(preserve=True, k=1)
     for _ in range(4):
@@ -74,7 +81,7 @@ def test_multistream_graph_matches_serial_eager(cuda, mode, split, k):
 
 
 @pytest.mark.parametrize("mode,split,k", [("dagq", False, 4), ("dagq", True, 1), ("indep", False, 4),
-                                         ("indep+conv", False, 4)])
+                                         ("indep+conv", False, 4), ("indep+fcnext", False, 4)])
 def test_shipped_plans_bit_exact_over_12_steps(cuda, mode, split, k):
     """The plans bench.py / the DP path run -- dagq (QSC branch forked and joined every step, k steps per
     replay), indep (the two chains independent for the whole replay, each gathering its own half of the batch)
@@ -89,7 +96,7 @@ def test_shipped_plans_bit_exact_over_12_steps(cuda, mode, split, k):
     for trial in range(int(os.environ.get("QDML_BITEXACT_TRIALS", "3"))):   # (more trials: a longer GPU call)
         ref = FlagshipTrainer(FlagshipConfig(hip_graphs=False, stream_mode="serial", split_graphs=split, **base), ctx)
         dag = FlagshipTrainer(FlagshipConfig(hip_graphs=True, stream_mode=mode, split_graphs=split,
-                                             steps_per_graph=k, qsc_start=start or "step", **base), ctx)
+                                             steps_per_graph=k, **_opts(start), **base), ctx)
         dag.capture(preserve=True, k=k)
         for rep in range(12 // k):
             for _ in range(k):
