@@ -97,9 +97,11 @@ def main() -> int:
     ap.add_argument("--qsc-start", default="step", choices=["step", "conv"],
                     help="(stream mode indep) when each step's QSC chain starts: with the step, or after the HDCE conv "
                          "forward (FlagshipConfig.qsc_start)")
-    ap.add_argument("--fc-adam-next", action="store_true",
-                    help="(stream mode indep) the FC weight's Adam on a side stream overlapping the next step's gather + "
-                         "conv forward (FlagshipConfig.fc_adam_next)")
+    ap.add_argument("--hdce-priority", action="store_true",
+                    help="(stream mode indep) capture on a high-priority stream (FlagshipConfig.hdce_priority)")
+    ap.add_argument("--fc-adam-next", type=int, default=0, metavar="WORKGROUPS",
+                    help="(stream mode indep) > 0: the FC weight's Adam on a side stream overlapping the next step's "
+                         "gather + conv forward, on at most this many workgroups (FlagshipConfig.fc_adam_next; 0 = off)")
     ap.add_argument("--fc-adam-side", type=int, default=0,
                     help="world 1: the FC weight's Adam on a side stream beside the conv backward, capped at this many "
                          "workgroups (FlagshipConfig.fc_adam_side; 0 = off)")
@@ -171,7 +173,8 @@ def main() -> int:
                              stream_mode=args.stream_mode, qsc_start=args.qsc_start,
                              steps_per_graph=args.steps_per_graph,
                              dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in,
-                             ramp=args.ramp, fc_adam_side=args.fc_adam_side, fc_adam_next=args.fc_adam_next)
+                             ramp=args.ramp, fc_adam_side=args.fc_adam_side, fc_adam_next=args.fc_adam_next,
+                             hdce_priority=args.hdce_priority)
         return FlagshipTrainer(cfg, ctx, store=store)
 
     def timed(tr: FlagshipTrainer, n: int, settle: int = 0):
@@ -321,7 +324,8 @@ def main() -> int:
                 "qsim_mfma12": bool(getattr(getattr(tr.cstep, "hip", None), "mfma12", False)),
                 "qsim_mfma_bwd": bool(getattr(getattr(tr.cstep, "hip", None), "mfma_bwd", False)),
                 "fc_adam_side": cfg.fc_adam_side if getattr(tr, "fc_adam_side", False) else 0,
-                "fc_adam_next": bool(getattr(tr, "fc_adam_next", False)),
+                "fc_adam_next": cfg.fc_adam_next if getattr(tr, "fc_adam_next", False) else 0,
+                "hdce_priority": bool(cfg.hdce_priority),
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
             "step_spread": spread,

@@ -73,6 +73,8 @@ class FlagshipConfig:
     hip_graphs: bool = True
     split_graphs: bool = False   # force the DP execution plan (5 graphs) even at world 1 (testing)
     stream_mode: str = "indep"   # serial | dagq | indep (see FlagshipTrainer.__init__)
+    hdce_priority: bool = False  # (indep) capture on a high-priority stream: the HDCE chain's nodes keep that priority
+    #                              over the QSC chain's (forked from a normal-priority stream) when both have work queued
     qsc_start: str = "step"      # (indep) "conv": each step's QSC chain waits for the HDCE conv forward (one HDCE ->
     #                              QSC edge, none on the HDCE chain), so the conv kernels have the chip to themselves
     tail_pack: bool = True       # pack the conv weights at the END of a step (not at the forward's head)
@@ -80,9 +82,10 @@ class FlagshipConfig:
     #                              epilogue (dW never written; bit-identical).  Off: 0.419-0.423 ms/step vs 0.412
     #                              separate (profiles/r3_04_fused_adam.txt) -- 256 one-per-CU workgroups stream
     #                              the Adam state far slower than the 2048-workgroup update kernel
-    fc_adam_next: bool = False   # (world 1, indep) the FC weight's Adam on the "fc" stream after the step's other Adam
-    #                              launch, overlapping the next step's gather + conv forward; the next FC forward waits
-    #                              for it (the DP plan's overlap, at world 1)
+    fc_adam_next: int = 0        # (world 1, indep) > 0: the FC weight's Adam on the "fc" stream after the step's other
+    #                              Adam launch, on at most this many workgroups, overlapping the next step's gather + conv
+    #                              forward; the next FC forward waits for it (the DP plan's overlap, at world 1).
+    #                              2048 (the default launch size): 0.405 against 0.394 ms (profiles/r5_15_*)
     fc_adam_side: int = 0        # (world 1, dagq) > 0: the FC weight's Adam runs on the "fc" stream right after the FC
     #                              data gradient -- the last reader of the bf16 shadow it rewrites -- beside the conv
     #                              backward, on at most this many workgroups (so the conv kernels keep most CUs);
@@ -268,7 +271,7 @@ class FlagshipTrainer(DPPlan):
             lo = sp.offsets[sp.names.index("CE.FC.weight")]
             self.hopt.fuse_range(lo, lo + self.hdce.fc_w.numel())
             self.hstep.after_dgrad = self._fc_adam_fork
-        self.fc_adam_next = bool(cfg.fc_adam_next and not self.fused_adam and not self.fc_adam_side
+        self.fc_adam_next = bool(cfg.fc_adam_next > 0 and not self.fused_adam and not self.fc_adam_side
                                  and self.streams is not None and mode == "indep" and self.hstep.hip
                                  and cfg.dtype == "bf16" and self.hdce.fc_shadow is not None
                                  and ctx.world == 1 and not cfg.split_graphs and len(self.hopt.bounds) == 1)
@@ -321,7 +324,8 @@ class FlagshipTrainer(DPPlan):
                     self._indep_step(first=i == 0)
                 self._join(("qsc", "fc") if self._fc_pending else ("qsc",))
                 self._fc_pending = False
-            gs = [GraphedStep(body, enabled=graphs)]
+            cs = torch.cuda.Stream(self.ctx.device, priority=-1) if (cfg.hdce_priority and graphs) else None
+            gs = [GraphedStep(body, enabled=graphs, capture_stream=cs)]
         elif self.ctx.world == 1 and not cfg.split_graphs:
             # one graph: gather, both forwards, NMSE, both backwards, the optimizers
             gs = [GraphedStep(rep(self._step_body), enabled=graphs)]
@@ -475,7 +479,7 @@ class FlagshipTrainer(DPPlan):
         self._hdce_update()
         if self.fc_adam_next:
             with self._fork(self.streams["fc"]):
-                self.hopt.step_fused(grad_scale=1.0, skip=self.hskip)
+                self.hopt.step_fused(grad_scale=1.0, skip=self.hskip, max_grid=self.cfg.fc_adam_next)
             self._fc_pending = True
 
     def skip_flags(self) -> torch.Tensor:

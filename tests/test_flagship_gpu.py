@@ -40,7 +40,7 @@ def test_no_zero_grad_overwrites_every_gradient(cuda):
 
 def _opts(opt: str) -> dict:
     """'conv' / 'fcnext' (the part of a test mode after '+') -> the FlagshipConfig options they stand for"""
-    return {"conv": {"qsc_start": "conv"}, "fcnext": {"fc_adam_next": True}, "": {}}[opt]
+    return {"conv": {"qsc_start": "conv"}, "fcnext": {"fc_adam_next": 256}, "": {}}[opt]
 
 
 def _all_state(tr):
