@@ -97,6 +97,8 @@ def main() -> int:
     ap.add_argument("--qsc-start", default="step", choices=["step", "conv"],
                     help="(stream mode indep) when each step's QSC chain starts: with the step, or after the HDCE conv "
                          "forward (FlagshipConfig.qsc_start)")
+    ap.add_argument("--qsc-grid-bwd", type=int, default=0,
+                    help="QSC backward workgroups (FlagshipConfig.qsc_grid_bwd; 0 = the default 256)")
     ap.add_argument("--hdce-priority", action="store_true",
                     help="(stream mode indep) capture on a high-priority stream (FlagshipConfig.hdce_priority)")
     ap.add_argument("--fc-adam-next", type=int, default=0, metavar="WORKGROUPS",
@@ -174,7 +176,7 @@ def main() -> int:
                              steps_per_graph=args.steps_per_graph,
                              dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in,
                              ramp=args.ramp, fc_adam_side=args.fc_adam_side, fc_adam_next=args.fc_adam_next,
-                             hdce_priority=args.hdce_priority)
+                             hdce_priority=args.hdce_priority, qsc_grid_bwd=args.qsc_grid_bwd)
         return FlagshipTrainer(cfg, ctx, store=store)
 
     def timed(tr: FlagshipTrainer, n: int, settle: int = 0):

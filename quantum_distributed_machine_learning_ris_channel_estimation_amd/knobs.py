@@ -42,6 +42,8 @@ class Knobs:
     # the conv stack's training forward as one persistent launch (conv.hip conv_fwd_stack_kernel; else 3 conv launches
     # + the BN tail launch)
     conv_stack: bool = False
+    # the QSC preprocess forward's workgroup cap (ops/qsc.py; one sample per wave beyond it, a grid-stride loop)
+    qsc_fwd_cap: int = 256
     conv_spw: int = 2
     conv_spb_f: int = 5
     conv_spb_w1: int = 4

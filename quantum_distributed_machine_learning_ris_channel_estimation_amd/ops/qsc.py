@@ -69,7 +69,7 @@ class QSCStepHIP:
             # at most 256 workgroups (grid-stride loop over the samples): the forward runs beside the HDCE
             # conv forward and leaves it more CUs -- 1 % per step over one sample per wave (576 workgroups
             # at 2304 samples) in 4 of 4 same-box rounds (profiles/r2_20_*)
-            self.grid_fwd = min(self.grid_fwd, 256)
+            self.grid_fwd = min(self.grid_fwd, KNOBS.qsc_fwd_cap)
             self.grid_bwd = min(-(-batch_total // wf(self.Ww, 1)), grid_bwd)
             self.p2 = torch.empty(batch_total, feat, **f32)        # pool-2 features (linear weight grad)
             # saved by the forward for the backward: pool-1 map + both pools' argmax choices

@@ -1,6 +1,8 @@
 #!/bin/bash
-# round-5 GPU call 17: the indep step with the HDCE chain captured on a high-priority stream (hdce_priority), and the
-# FC Adam overlapping the next conv forward on capped grids (fc_adam_next 256 / 512): tests + 3 alternating rounds
+# round-5 GPU call 17: the indep step with the HDCE chain captured on a high-priority stream (hdce_priority), the
+# FC Adam overlapping the next conv forward on capped grids (fc_adam_next 256 / 512), and the QSC chain's grids (the
+# preprocess forward's cap KNOBS.qsc_fwd_cap 256 -> 576, the backward's qsc_grid_bwd 256 -> 128 / 512): tests + 3
+# alternating rounds
 set -o pipefail
 cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
@@ -16,4 +18,7 @@ for r in 1 2 3; do
   run "r$r hdce_priority" --hdce-priority
   run "r$r fc_adam_next256" --fc-adam-next 256
   run "r$r fc_adam_next512" --fc-adam-next 512
+  run "r$r fwdcap576" --knob qsc_fwd_cap=576
+  run "r$r bwd512" --qsc-grid-bwd 512
+  run "r$r bwd128" --qsc-grid-bwd 128
 done
