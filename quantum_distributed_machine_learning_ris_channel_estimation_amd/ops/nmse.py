@@ -50,7 +50,7 @@ class StreamNMSE:
         self.coef = torch.zeros(n_streams, device=dev)
         self.skip = torch.zeros(1, device=dev, dtype=torch.float32)  # NaN guard flag (all-reduced in DP)
         self._rs_long = self.row_stream.long()
-        # fused path: rows per block = E * rpc_mult (scripts/probe_nmse.py: 22.7 vs 24.2 us isolated at 4 vs 2;
+        # fused path: rows per block = E * rpc_mult (scripts/probes/probe_nmse.py: 22.7 vs 24.2 us isolated at 4 vs 2;
         # 0.7 % per step in 2 of 2 rounds, profiles/r2_20_variants.md)
         self.rpc_mult = 4
         self.rowoff: Optional[torch.Tensor] = None

@@ -185,7 +185,7 @@ class DPPlan:
             self._mark("gf", fc)
             if zero and self.cfg.dp_one_graph:
                 # (captured: a collective launched from a forked stream crashes hipStreamEndCapture --
-                # scripts/probe_rccl_capture.py -- so main launches the all-gather; see below)
+                # scripts/probes/probe_rccl_capture.py -- so main launches the all-gather; see below)
                 pass
             elif zero:
                 b.launch_all_gather("ag", self._fc_weights_lp())

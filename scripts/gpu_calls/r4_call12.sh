@@ -9,11 +9,11 @@ timeout -k 10 300 python bench.py --steps 300 --warmup 20 > $O/r4_12_bench.json 
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tl_step -o run -- python $R/bench.py --steps 100 --warmup 20 > $O/tl_step.log 2>&1) || exit 1
 python scripts/prof_timeline.py $O/tl_step/run_kernel_trace.csv --marker "conv3x3_kernel<2," --back 5 > $O/r4_12_step_timeline.md
 python scripts/prof_summary.py $O/tl_step/run_kernel_trace.csv --tail 0.6 > $O/r4_12_step_kernel_stats.md; rm -rf $O/tl_step
-timeout -k 10 400 python scripts/r4_qsc_gate_probe.py 256 12 100 2 > $O/r4_12_qsc_gate_p256.txt 2>&1 || exit 1
-timeout -k 10 300 python scripts/r4_qsc_gate_probe.py 128 8 300 2 > $O/r4_12_qsc_gate_p128.txt 2>&1 || exit 1
+timeout -k 10 400 python scripts/probes/r4_qsc_gate_probe.py 256 12 100 2 > $O/r4_12_qsc_gate_p256.txt 2>&1 || exit 1
+timeout -k 10 300 python scripts/probes/r4_qsc_gate_probe.py 128 8 300 2 > $O/r4_12_qsc_gate_p128.txt 2>&1 || exit 1
 timeout -k 10 300 python bench.py --qubits 16 --dtype fp8 --steps 20 --warmup 3 > $O/r4_12_bench_q16.json 2>$O/r4_12_bench_q16.err || exit 1
 QDML_FORCE_DIST=1 timeout -k 10 400 python bench.py --steps 200 --warmup 20 --select-steps 30 > $O/r4_12_bench_forced.json 2>$O/r4_12_bench_forced.err || exit 1
-timeout -k 10 120 python scripts/probe_coherence.py 300 10 > $O/r4_12_coherence.txt 2>&1 || exit 1
-timeout -k 10 120 python scripts/stamp_conv.py > $O/r4_12_stamp_conv.txt 2>&1 || exit 1
-timeout -k 10 180 python scripts/r4_adam_probe.py > $O/r4_12_adam_probe.txt 2>&1 || exit 1
-timeout -k 10 180 python scripts/probe_qsc_determinism.py 40 > $O/r4_12_qsc_determinism.txt 2>&1 || exit 1
+timeout -k 10 120 python scripts/probes/probe_coherence.py 300 10 > $O/r4_12_coherence.txt 2>&1 || exit 1
+timeout -k 10 120 python scripts/probes/stamp_conv.py > $O/r4_12_stamp_conv.txt 2>&1 || exit 1
+timeout -k 10 180 python scripts/probes/r4_adam_probe.py > $O/r4_12_adam_probe.txt 2>&1 || exit 1
+timeout -k 10 180 python scripts/probes/probe_qsc_determinism.py 40 > $O/r4_12_qsc_determinism.txt 2>&1 || exit 1

@@ -8,6 +8,6 @@ timeout -k 10 300 python bench.py --steps 300 --warmup 20 > $O/r4_14_bench.json 
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tl_step -o run -- python $R/bench.py --steps 100 --warmup 20 > $O/tl_step.log 2>&1) || exit 1
 python scripts/prof_timeline.py $O/tl_step/run_kernel_trace.csv --marker "conv3x3_kernel<2," --back 5 > $O/r4_14_step_timeline.md
 python scripts/prof_summary.py $O/tl_step/run_kernel_trace.csv --tail 0.6 > $O/r4_14_step_kernel_stats.md; rm -rf $O/tl_step
-timeout -k 10 120 python scripts/stamp_conv.py > $O/r4_14_stamp_conv.txt 2>&1 || exit 1
+timeout -k 10 120 python scripts/probes/stamp_conv.py > $O/r4_14_stamp_conv.txt 2>&1 || exit 1
 QDML_FORCE_DIST=1 timeout -k 10 400 python bench.py --steps 200 --warmup 20 --select-steps 30 > $O/r4_14_bench_forced.json 2>$O/r4_14_bench_forced.err || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/r4_14_pytest_full.log 2>&1; echo "pytest rc=$?" >> $O/r4_14_pytest_full.log

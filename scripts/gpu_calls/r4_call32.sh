@@ -5,4 +5,4 @@ cd "$(dirname "$0")/../.." || exit 1
 O=$(pwd)/gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/r4_32_pytest.log 2>&1 || exit 1
 bash scripts/ab_lib.sh r4_32 3 || exit 1
-PLAN=shipped,fused_adam,fused_adam_w2 ROUNDS=2 timeout -k 10 500 python scripts/r4_plan_probe.py 300 > $O/r4_32_plans.txt 2>&1 || exit 1
+PLAN=shipped,fused_adam,fused_adam_w2 ROUNDS=2 timeout -k 10 500 python scripts/probes/r4_plan_probe.py 300 > $O/r4_32_plans.txt 2>&1 || exit 1

@@ -10,7 +10,7 @@ for r in 1 2; do
     echo "round $r [$v] $(python -c "import json; d=json.load(open('$O/r5_02_cur.json')); print(d['ms_per_step'], d['step_spread'])")" | tee -a $O/r5_02_window.txt
   done
 done
-timeout -k 10 300 python scripts/probe_gemm_r5.py 5 > $O/r5_02_gemm_probe.txt 2>&1; cat $O/r5_02_gemm_probe.txt
+timeout -k 10 300 python scripts/probes/probe_gemm_r5.py 5 > $O/r5_02_gemm_probe.txt 2>&1; cat $O/r5_02_gemm_probe.txt
 # the FC weight's Adam beside the conv backward (--fc-adam-side N workgroups) vs at the tail, 2 rounds, --steps 300
 for r in 1 2; do
   for v in "--fc-adam-side 0" "--fc-adam-side 64" "--fc-adam-side 128" "--fc-adam-side 256"; do

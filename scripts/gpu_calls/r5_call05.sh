@@ -7,7 +7,7 @@ cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py -x -q -k "f8" --timeout 120 --timeout-method thread > $O/r5_05_pytest.log 2>&1 || { tail -30 $O/r5_05_pytest.log; exit 1; }
 tail -2 $O/r5_05_pytest.log
-timeout -k 10 300 python scripts/probe_gemm_r5.py 5 fwd8,wgrad8,dgrad8,fwd_c8,wgrad_c7,dgrad_c6 > $O/r5_05_gemm_probe.txt 2>&1; cat $O/r5_05_gemm_probe.txt
+timeout -k 10 300 python scripts/probes/probe_gemm_r5.py 5 fwd8,wgrad8,dgrad8,fwd_c8,wgrad_c7,dgrad_c6 > $O/r5_05_gemm_probe.txt 2>&1; cat $O/r5_05_gemm_probe.txt
 for r in 1 2 3; do
   for v in "--dtype bf16" "--dtype fp8 --f8-producers 0" "--dtype fp8 --f8-producers 1"; do
     timeout -k 10 200 python bench.py --steps 300 --warmup 20 $v > $O/r5_05_cur.json 2> $O/r5_05_cur.err || { tail -20 $O/r5_05_cur.err; exit 1; }

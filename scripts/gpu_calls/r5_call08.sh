@@ -6,7 +6,7 @@ cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_qsim12_gpu.py -x -q --timeout 120 --timeout-method thread > $O/r5_08_pytest.log 2>&1 || { tail -40 $O/r5_08_pytest.log; exit 1; }
 tail -2 $O/r5_08_pytest.log
-timeout -k 10 300 python scripts/probe_qsim_mfma.py 5 > $O/r5_08_qsim_probe.txt 2>&1; cat $O/r5_08_qsim_probe.txt
+timeout -k 10 300 python scripts/probes/probe_qsim_mfma.py 5 > $O/r5_08_qsim_probe.txt 2>&1; cat $O/r5_08_qsim_probe.txt
 for r in 1 2; do
   for v in 1 0; do
     timeout -k 10 200 python bench.py --qsim-mfma12 $v --pilot 256 --qubits 12 --steps 100 --warmup 10 > $O/r5_08_cur.json 2> $O/r5_08_cur.err || { tail -20 $O/r5_08_cur.err; exit 1; }

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_infer_gpu.py -x -q --timeout 120 --timeout-method thread > $O/r5_12_pytest.log 2>&1 || { tail -40 $O/r5_12_pytest.log; exit 1; }
 tail -1 $O/r5_12_pytest.log
-timeout -k 10 120 python scripts/probe_conv_stack.py 400 > $O/r5_12_conv_stack_probe.txt 2>&1 || { cat $O/r5_12_conv_stack_probe.txt; exit 1; }
+timeout -k 10 120 python scripts/probes/probe_conv_stack.py 400 > $O/r5_12_conv_stack_probe.txt 2>&1 || { cat $O/r5_12_conv_stack_probe.txt; exit 1; }
 cat $O/r5_12_conv_stack_probe.txt
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_stack -o run -- python $R/bench.py --steps 40 --warmup 10 --knob conv_stack=1 > $O/prof_stack.log 2>&1) || exit 1
 python scripts/prof_summary.py $O/prof_stack/run_kernel_trace.csv --tail 0.6 > $O/r5_12_stack_kernel_stats.md

@@ -36,15 +36,15 @@ for s in $STEPS; do
     bench_split) run bench_split 600 python bench.py --steps 50 --warmup 10 --split-graphs ;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace ${PROF_EXTRA:-} --stats --output-format csv -d "$OUT/prof" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 ${BENCH_EXTRA:-}) && python scripts/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_summary.md" && python scripts/prof_timeline.py "$OUT/prof/run_kernel_trace.csv" --marker "conv3x3_kernel<2," > "$OUT/prof_timeline.md" ;;
     prof_fp8) (cd /tmp && export TMPDIR=/tmp && run prof_fp8 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_fp8" -o run -- python "$ROOT/bench.py" --steps 100 --warmup 5 --dtype fp8 --steps-per-graph 1) && python scripts/prof_summary.py "$OUT/prof_fp8/run_kernel_trace.csv" --tail 0.6 > "$OUT/prof_fp8_summary.md" && python scripts/prof_timeline.py "$OUT/prof_fp8/run_kernel_trace.csv" > "$OUT/prof_fp8_timeline.md" ;;
-    stamp) run stamp 300 python scripts/stamp_qsc.py ;;
-    stamp_conv) run stamp_conv 300 python scripts/stamp_conv.py ;;
+    stamp) run stamp 300 python scripts/probes/stamp_qsc.py ;;
+    stamp_conv) run stamp_conv 300 python scripts/probes/stamp_conv.py ;;
     tune) run tune 900 python scripts/tune_kernels.py --what ${TUNE_WHAT:-qsc,conv} ;;
-    fp8probe) run fp8probe 300 python scripts/probe_fp8.py ;;
-    fcprobe) run fcprobe 300 python scripts/probe_fc_gemm.py ;;
-    gemmprobe) run gemmprobe 300 python scripts/probe_gemm.py ;;
+    fp8probe) run fp8probe 300 python scripts/probes/probe_fp8.py ;;
+    fcprobe) run fcprobe 300 python scripts/probes/probe_fc_gemm.py ;;
+    gemmprobe) run gemmprobe 300 python scripts/probes/probe_gemm.py ;;
     gemmtest) run gemmtest 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_gpu.py -m gpu ;;
-    nmseprobe) run nmseprobe 300 python scripts/probe_nmse.py ;;
-    diag) run diag 900 python scripts/diag_hdce.py --epochs ${DIAG_EPOCHS:-20} ;;
+    nmseprobe) run nmseprobe 300 python scripts/probes/probe_nmse.py ;;
+    diag) run diag 900 python scripts/probes/diag_hdce.py --epochs ${DIAG_EPOCHS:-20} ;;
     gensweep) run gensweep 1500 python scripts/gen_sweep.py --epochs ${SWEEP_EPOCHS:-30} --sc-epochs 8 ;;
   esac
 done

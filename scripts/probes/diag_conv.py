@@ -1,5 +1,10 @@
-import torch, torch.nn.functional as F, sys
-sys.path.insert(0, '/root/repo')
+"""Diagnostic: the HIP conv stack (forward) against the fp32 torch model on one flagship batch."""
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.conv import ConvStackHIP
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.engine import HDCEModel
 cuda = torch.device('cuda')

@@ -13,7 +13,7 @@ the scenario classifier plays no part):
 
 Per variant: NMSE (dB) vs the perfect channel at SNR 5..15 dB, plus 20 / 30 dB (the model's floor).
 
-    python scripts/diag_hdce_snr.py --epochs 100 --out reports/r2_hdce_snr.jsonl
+    python scripts/probes/diag_hdce_snr.py --epochs 100 --out reports/r2_hdce_snr.jsonl
 """
 import argparse
 import json
@@ -25,7 +25,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -16,7 +16,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat  # noqa: E402
 
 _p, _i = ctypes.c_void_p, ctypes.c_int

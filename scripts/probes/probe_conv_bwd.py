@@ -2,14 +2,14 @@
 """Conv-stack backward alone (no QSC chain beside it): ConvStackHIP.backward in a loop, for rocprofv3
 kernel traces / PMC passes of the fused conv3x3_bwd_kernel vs the side-by-side wd kernel.
 
-    python scripts/probe_conv_bwd.py [--fused 0|1] [--spb-f S] [--iters N] [--pilot 128|256]"""
+    python scripts/probes/probe_conv_bwd.py [--fused 0|1] [--spb-f S] [--iters N] [--pilot 128|256]"""
 import argparse
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -3,15 +3,15 @@ persistent launch (conv.hip conv_fwd_stack_kernel), each captured in a HIP graph
 beside a concurrent load on a second stream (a QSC step of the flagship) to see how the persistent kernel's
 barriers fare when other kernels hold CUs.
 
-    python scripts/probe_conv_stack.py [reps]
-    QDML_STACK_STAMPS=1 python scripts/probe_conv_stack.py     # per-phase stamps of the persistent kernel
+    python scripts/probes/probe_conv_stack.py [reps]
+    QDML_STACK_STAMPS=1 python scripts/probes/probe_conv_stack.py     # per-phase stamps of the persistent kernel
 """
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS  # noqa: E402
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.conv import ConvStackHIP  # noqa: E402

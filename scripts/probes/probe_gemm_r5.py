@@ -3,12 +3,12 @@
 M=2304, N=2048, K=4096.  Each variant is first checked against an fp32 torch product (max |err| / max |ref|), then
 timed: rounds interleave the variants in one process, median and min over rounds are printed.
 
-    python scripts/probe_gemm_r5.py [rounds]"""
+    python scripts/probes/probe_gemm_r5.py [rounds]"""
 import os
 import statistics
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import (  # noqa: E402

@@ -4,7 +4,7 @@ choices) against the three-kernel path (row sums + reduce/finalize, grad_bias + 
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.nmse import StreamNMSE  # noqa: E402

@@ -13,7 +13,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat  # noqa: E402
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.models.estimators import QSC_P128  # noqa: E402
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.optim import FlatParamSpace  # noqa: E402

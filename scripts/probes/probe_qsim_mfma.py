@@ -3,13 +3,13 @@
 12 qubits -- csrc/hip/qsim12_mfma.hip (MFMA mode products) vs qsim_big.hip (VALU); 8 qubits -- the adjoint on the
 MFMA (qd_qsim_mfma8_bwd) vs qsim.hip's register kernel.  Median over rounds interleaving the variants.
 
-    python scripts/probe_qsim_mfma.py [rounds]"""
+    python scripts/probes/probe_qsim_mfma.py [rounds]"""
 import ctypes
 import os
 import statistics
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 
 from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat  # noqa: E402

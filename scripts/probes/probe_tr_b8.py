@@ -4,7 +4,7 @@ and lane i receives column i of the 8 rows (byte q = row q)."""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import ctypes  # noqa: E402
 
 import torch  # noqa: E402

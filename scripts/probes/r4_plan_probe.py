@@ -3,7 +3,7 @@ dagq step, as subclasses of FlagshipTrainer; prints ms/step for each (same timin
 warm-up, capture, settle, then a timed window).  Run under rocprofv3 --kernel-trace with PLAN=<name> to get
 the timeline of one plan.
 
-    python scripts/r4_plan_probe.py [steps]          # PLAN=all (default) or one plan name
+    python scripts/probes/r4_plan_probe.py [steps]          # PLAN=all (default) or one plan name
 """
 import os
 import sys
@@ -11,7 +11,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext  # noqa: E402
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (  # noqa: E402
     FlagshipConfig, FlagshipTrainer)

@@ -14,7 +14,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat  # noqa: E402
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext  # noqa: E402
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (  # noqa: E402
