@@ -465,7 +465,8 @@ class Y2HRunner:
         n_users x batch_size_DML samples, the training step's BN batch (the running statistics of the trained
         weights do not describe the averaged ones) -- saved under the tag "swa" for ``model_val(hdce_tag="swa")``.
         The trained weights and statistics are put back afterwards.  (An estimator-side option beside the
-        reference protocol, which evaluates the last epoch: Test.py:64-100.)"""
+        reference protocol, which evaluates the last epoch: Test.py:64-100.  Data parallel: rank 0 re-estimates the
+        statistics on its own training shard -- every rank holds the same averaged weights -- and saves.)"""
         from .evaluate import recalibrate_bn, restore_bn
         sp = model.space
         keep = sp.flat.clone()
