@@ -37,14 +37,17 @@ class Knobs:
     qsim_mfma12: bool = True
     # the 8-qubit adjoint backward on the matrix cores (qsim12_mfma.hip qd_qsim_mfma8_bwd; else qsim.hip's)
     qsim_mfma_bwd: bool = True
-    # conv stack launch shapes (ops/conv.py ConvStackHIP): samples per wave of the forward / dgrad kernels (4 waves per
-    # workgroup), samples per workgroup of the fused layer-3/2 backward and of layer 1's weight gradient
     # the conv stack's training forward as one persistent launch (conv.hip conv_fwd_stack_kernel; else 3 conv launches
-    # + the BN tail launch)
+    # + the BN tail launch).  Measured slower: 105 against 58 us alone (docs/CONCURRENCY.md)
     conv_stack: bool = False
     # the QSC preprocess forward's workgroup cap (ops/qsc.py; one sample per wave beyond it, a grid-stride loop)
     qsc_fwd_cap: int = 256
-    conv_spw: int = 2
+    # conv stack launch shapes (ops/conv.py ConvStackHIP): samples per wave of the forward / dgrad kernels (4 waves per
+    # workgroup), samples per workgroup of the fused layer-3/2 backward and of layer 1's weight gradient.
+    # spw 3 (round 5): 198 workgroups, one per CU -- spw 2's 288 put two on 32 CUs, whose workgroups then set each
+    # layer's time: 0.3869 / 0.3879 against 0.3909 / 0.3909 ms, and 0.4081 / 0.4066 against 0.4102 / 0.4084 on another
+    # box (profiles/r5_18_spw_stack_window_ab.txt, r5_10_ab.txt)
+    conv_spw: int = 3
     conv_spb_f: int = 5
     conv_spb_w1: int = 4
 

@@ -53,7 +53,7 @@ class BnBwd(ctypes.Structure):
 class ConvStackHIP:
     """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
 
-    def __init__(self, model, U: int, B: int, spw: int = 2, spb_w: int = 8, spb_r: int = 4, spb_w1: int = 4,
+    def __init__(self, model, U: int, B: int, spw: int = 3, spb_w: int = 8, spb_r: int = 4, spb_w1: int = 4,
                  dx_bf16: bool = True, bwd_fused: Optional[bool] = None, spb_f: int = 5):
         self.m = model
         self.count_batches = False   # set by the owner that stops counting num_batches_tracked itself
