@@ -17,6 +17,7 @@
 //   * an optional bf16 "shadow" of a parameter range (the FC weight): the forward GEMM reads
 //     the shadow instead of casting 8.4 M fp32 weights every step.
 #include <cstdlib>
+#include <utility>
 
 #include "common.h"
 
@@ -47,6 +48,30 @@ struct PackScatter {
   int* cursor;          // nullable: *cursor += cursor_inc once per launch (also when the step is skipped)
   int cursor_inc;
 };
+
+// Gradients the update sums itself (world 1): job k's gradient over the flat range [off[k], off[k] + groups * width)
+// (relative to the stepped part) is the row sum of a workgroup-partial slab -- out[g * width + i] = sum over r < rows
+// of slab[(g * rows + r) * ld + i] -- the deterministic slab reduction qd_slab_rows_sum_multi would have written
+// into the gradient (conv.hip slab_rows_sum4_body: the same rows per thread in the same order, the same combine, so
+// the sums are bit-identical).  The update's workgroups past the regular ones run these jobs, 64 columns each, and
+// the regular ones skip the ranges: the slab launch leaves the chain.  Vector jobs only (width, ld, off % 4 == 0).
+constexpr int kAdamSlabJobs = 16, kAdamSkips = 4;
+struct AdamSlabs {
+  const float* slab[kAdamSlabJobs];
+  int off[kAdamSlabJobs], groups[kAdamSlabJobs], rows[kAdamSlabJobs], width[kAdamSlabJobs], ld[kAdamSlabJobs];
+  int wg0[kAdamSlabJobs + 1];   // first extra workgroup of each job (prefix sums); wg0[n] = extra workgroups
+  int n;
+  // the regular workgroups skip [skip_lo[k], skip_hi[k]): the jobs' ranges merged across alignment gaps (a gap's
+  // elements are padding, never stepped apart from their zero gradient) -- 4 int compares per float4 (the job
+  // table itself in the loop cost 25 VGPRs and occupancy 7 -> 5)
+  int skip_lo[kAdamSkips], skip_hi[kAdamSkips];
+};
+__device__ __forceinline__ bool in_slab_job(const AdamSlabs& sj, long i0) {
+  bool in = false;
+#pragma unroll
+  for (int k = 0; k < kAdamSkips; ++k) in |= i0 >= sj.skip_lo[k] && i0 < sj.skip_hi[k];
+  return in;
+}
 
 __device__ __forceinline__ void pack_scatter(const PackScatter& ps, long i0, const float* v4) {
 #pragma unroll
@@ -127,18 +152,19 @@ __device__ __forceinline__ void stv(float* a, float4 v) {
   }
 }
 
-template <bool NT>
+template <bool NT, bool SLABS = false>
 __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long n,
                                                    const float* __restrict__ lr_ptr, const float* step_ptr,
                                                    const float* __restrict__ skip, unsigned int* __restrict__ pruned,
                                                    AdamArgs a, float* __restrict__ step_out,
                                                    unsigned int* __restrict__ done, Shadow sh, PackScatter ps,
-                                                   long hole_lo, long hole_n) {
+                                                   long hole_lo, long hole_n, AdamSlabs sj) {
   if (skip != nullptr && *skip != 0.f) {   // uniform across the grid: nobody ticks (the cursor still moves)
     if (ps.cursor && blockIdx.x == 0 && threadIdx.x == 0) *ps.cursor += ps.cursor_inc;
     return;
   }
+  const int nreg = SLABS ? (int)gridDim.x - sj.wg0[sj.n] : (int)gridDim.x;   // regular workgroups; then the slab jobs
   const float lr = *lr_ptr;
   const float t = *step_ptr + 1.f;  // step about to be taken
   const float bc1 = 1.f - __powf(a.beta1, t);
@@ -147,33 +173,83 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
   const float rbc2 = rsqrtf(bc2);
   unsigned int cnt = 0;
   float wmax = 0.f;
-  const long stride = (long)gridDim.x * blockDim.x * 4;
+  // one float4 of the update: p, m, v at i0 with gradient gg (already read / summed); returns the updated gg
+  auto update4 = [&](long i0, float4 gg) __attribute__((always_inline)) {
+    float4 pp = ldv<NT>(p + i0);
+    float4 mm = ldv<NT>(m + i0);
+    float4 vv = ldv<NT>(v + i0);
+    float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = ga[j] * a.grad_scale;
+      if (a.prune_thr > 0.f && !(fabsf(gj) > a.prune_thr)) { gj = 0.f; ++cnt; }
+      float pj = pa[j];
+      if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
+      else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
+      adam_elem(pj, ma[j], va[j], gj, a.beta1, a.beta2, a.eps, step_size, rbc2);
+      pa[j] = pj;
+      ga[j] = gj;
+    }
+    stv<NT>(p + i0, pp);
+    wmax = fmaxf(wmax, store_shadow(sh, i0, pp));
+    pack_scatter(ps, i0, &pp.x);
+    stv<NT>(m + i0, mm);
+    stv<NT>(v + i0, vv);
+    return gg;
+  };
+  if (SLABS && (int)blockIdx.x >= nreg) {
+    // ---- a slab job's 64 columns: 16 column quads x 16 row phases, rounds of 4 rows with every load in flight
+    // (conv.hip slab_rows_sum4_body's order: the same row sequence per thread whatever the round size), then the
+    // update of those 64 elements ----
+    const int b = (int)blockIdx.x - nreg;
+    int k = 0;
+    while (k + 1 < sj.n && b >= sj.wg0[k + 1]) ++k;
+    const int cpg = (sj.width[k] + 63) / 64, lb = b - sj.wg0[k], grp = lb / cpg, bx = lb % cpg;
+    const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int i = (bx * 16 + tq) * 4, rows = sj.rows[k], ld = sj.ld[k];
+    __shared__ float4 red[16][16];
+    float4 t4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < sj.width[k]) {
+      const float* sp = sj.slab[k] + (size_t)grp * rows * ld + i;
+      constexpr int SR = 4;   // (8 raised the kernel to 90 VGPRs: occupancy 5 instead of 7 for the HBM-bound update)
+      for (int r0 = ty; r0 < rows; r0 += 16 * SR) {
+        float4 vv[SR];
+#pragma unroll
+        for (int q = 0; q < SR; ++q)
+          vv[q] = *reinterpret_cast<const float4*>(sp + (size_t)(r0 + 16 * q < rows ? r0 + 16 * q : r0) * ld);
+#pragma unroll
+        for (int q = 0; q < SR; ++q)
+          if (r0 + 16 * q < rows) {
+            t4.x += vv[q].x;
+            t4.y += vv[q].y;
+            t4.z += vv[q].z;
+            t4.w += vv[q].w;
+          }
+      }
+    }
+    red[ty][tq] = t4;
+    __syncthreads();
+    if (ty == 0 && i < sj.width[k]) {
+      float4 acc = red[0][tq];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) {
+        acc.x += red[q][tq].x;
+        acc.y += red[q][tq].y;
+        acc.z += red[q][tq].z;
+        acc.w += red[q][tq].w;
+      }
+      const long i0 = sj.off[k] + (long)grp * sj.width[k] + i;
+      *reinterpret_cast<float4*>(g + i0) = update4(i0, acc);   // (the gradient as the update used it)
+    }
+  } else {
+  const long stride = (long)nreg * blockDim.x * 4;
   // [hole_lo, hole_lo + hole_n) (multiples of 4) is skipped: a range another kernel updates (the FC weight,
   // stepped inside its weight-gradient GEMM's epilogue); the loop runs over n - hole_n logical elements
   for (long il = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; il < n - hole_n; il += stride) {
     const long i0 = il < hole_lo ? il : il + hole_n;
+    if (SLABS && in_slab_job(sj, i0)) continue;   // (summed and stepped by the slab workgroups)
     if (i0 + 3 < n) {
-      float4 pp = ldv<NT>(p + i0);
-      float4 gg = ldv<NT>(g + i0);
-      float4 mm = ldv<NT>(m + i0);
-      float4 vv = ldv<NT>(v + i0);
-      float* pa = &pp.x; float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float gj = ga[j] * a.grad_scale;
-        if (a.prune_thr > 0.f && !(fabsf(gj) > a.prune_thr)) { gj = 0.f; ++cnt; }
-        float pj = pa[j];
-        if (a.decoupled) pj *= 1.f - lr * a.weight_decay;
-        else if (a.weight_decay != 0.f) gj += a.weight_decay * pj;
-        adam_elem(pj, ma[j], va[j], gj, a.beta1, a.beta2, a.eps, step_size, rbc2);
-        pa[j] = pj;
-        ga[j] = gj;
-      }
-      stv<NT>(p + i0, pp);
-      wmax = fmaxf(wmax, store_shadow(sh, i0, pp));
-      pack_scatter(ps, i0, &pp.x);
-      stv<NT>(m + i0, mm);
-      stv<NT>(v + i0, vv);
+      const float4 gg = update4(i0, ldv<NT>(g + i0));
       if (a.prune_thr > 0.f || a.grad_scale != 1.f) *reinterpret_cast<float4*>(g + i0) = gg;
     } else {
       for (long i = i0; i < n; ++i) {
@@ -197,6 +273,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
         }
       }
     }
+  }
   }
   if (pruned != nullptr && a.prune_thr > 0.f) {
     // one atomic per wave (the compiler's wave-level atomic coalescing would not sum counts)
@@ -278,12 +355,74 @@ using namespace qd::optim;
 // done: device uint32 counter, zero-initialised once (re-armed by the kernel).
 // shadow: optional bf16 copy of p[lo, hi) (lo, hi multiples of 4), written with the update;
 // shadow8/qs/amax: optional e4m3 copy of the same range (fp8 estimator).
+// nj slab jobs (nullable arrays; see AdamSlabs): job k sums slab[k] (groups[k] x rows[k] rows of ld[k] floats) into
+// the gradient of the flat range [off[k], off[k] + groups[k] * width[k]) of this part before updating it
+QD_API int qd_adam_step_slabs(float* p, float* g, float* m, float* v, long n, const float* lr, float* step,
+                              const float* skip, unsigned int* pruned, float beta1, float beta2, float eps,
+                              float weight_decay, int decoupled, float grad_scale, float prune_thr, unsigned int* done,
+                              uint16_t* shadow, long shadow_lo, long shadow_hi, uint8_t* shadow8, const float* qs,
+                              float* amax, int max_grid, const PackScatter* ps_in, long hole_lo, long hole_n, int nj,
+                              const float* const* slab, const long* off, const int* groups, const int* rows,
+                              const int* width, const int* ld, void* stream);
 QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const float* lr, float* step, const float* skip,
                         unsigned int* pruned, float beta1, float beta2, float eps, float weight_decay, int decoupled,
                         float grad_scale, float prune_thr, unsigned int* done, uint16_t* shadow, long shadow_lo,
                         long shadow_hi, uint8_t* shadow8, const float* qs, float* amax, int max_grid,
                         const PackScatter* ps_in, long hole_lo, long hole_n, void* stream) {
+  return qd_adam_step_slabs(p, g, m, v, n, lr, step, skip, pruned, beta1, beta2, eps, weight_decay, decoupled,
+                            grad_scale, prune_thr, done, shadow, shadow_lo, shadow_hi, shadow8, qs, amax, max_grid, ps_in,
+                            hole_lo, hole_n, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+QD_API int qd_adam_step_slabs(float* p, float* g, float* m, float* v, long n, const float* lr, float* step,
+                              const float* skip, unsigned int* pruned, float beta1, float beta2, float eps,
+                              float weight_decay, int decoupled, float grad_scale, float prune_thr, unsigned int* done,
+                              uint16_t* shadow, long shadow_lo, long shadow_hi, uint8_t* shadow8, const float* qs,
+                              float* amax, int max_grid, const PackScatter* ps_in, long hole_lo, long hole_n, int nj,
+                              const float* const* slab, const long* off, const int* groups, const int* rows,
+                              const int* width, const int* ld, void* stream) {
   const PackScatter ps = ps_in ? *ps_in : PackScatter{};
+  if (nj < 0 || nj > kAdamSlabJobs) return (int)hipErrorInvalidValue;
+  AdamSlabs sj{};
+  sj.n = nj;
+  if (nj && n >= (1L << 31)) return (int)hipErrorInvalidValue;
+  long lo_k[kAdamSlabJobs], hi_k[kAdamSlabJobs];
+  for (int k = 0; k < nj; ++k) {
+    if (!slab[k] || off[k] < 0 || groups[k] < 1 || rows[k] < 1 || width[k] < 4 || ld[k] < width[k] ||
+        ((off[k] | width[k] | ld[k]) & 3) || off[k] + (long)groups[k] * width[k] > n ||
+        (reinterpret_cast<uintptr_t>(slab[k]) & 15))
+      return (int)hipErrorInvalidValue;
+    // (a job inside the hole -- a range another kernel updates -- would be stepped twice)
+    if (hole_n && off[k] < hole_lo + hole_n && hole_lo < off[k] + (long)groups[k] * width[k])
+      return (int)hipErrorInvalidValue;
+    sj.slab[k] = slab[k];
+    sj.off[k] = (int)off[k];
+    sj.groups[k] = groups[k];
+    sj.rows[k] = rows[k];
+    sj.width[k] = width[k];
+    sj.ld[k] = ld[k];
+    sj.wg0[k + 1] = sj.wg0[k] + groups[k] * ((width[k] + 63) / 64);
+    lo_k[k] = off[k];
+    hi_k[k] = off[k] + (long)groups[k] * width[k];
+  }
+  // skip intervals: the job ranges sorted and merged across gaps of < 64 elements (alignment padding)
+  for (int a = 0; a < nj; ++a)
+    for (int b = a + 1; b < nj; ++b)
+      if (lo_k[b] < lo_k[a]) {
+        std::swap(lo_k[a], lo_k[b]);
+        std::swap(hi_k[a], hi_k[b]);
+      }
+  int ns = 0;
+  for (int k = 0; k < nj; ++k) {
+    if (k > 0 && lo_k[k] < hi_k[k - 1]) return (int)hipErrorInvalidValue;   // (overlapping jobs)
+    if (ns > 0 && lo_k[k] - sj.skip_hi[ns - 1] < 64 && (hole_n == 0 || !(sj.skip_hi[ns - 1] <= hole_lo && hole_lo < lo_k[k]))) {
+      sj.skip_hi[ns - 1] = (int)hi_k[k];
+    } else {
+      if (ns == kAdamSkips) return (int)hipErrorInvalidValue;
+      sj.skip_lo[ns] = (int)lo_k[k];
+      sj.skip_hi[ns] = (int)hi_k[k];
+      ++ns;
+    }
+  }
   for (int k = 0; k < 3; ++k)
     if (ps.n[k] && (ps.lo[k] < 0 || ps.lo[k] + ps.n[k] > n || (ps.lo[k] & 3) || (ps.n[k] & 3) || !ps.fwd[k]))
       return (int)hipErrorInvalidValue;
@@ -298,13 +437,16 @@ QD_API int qd_adam_step(float* p, float* g, float* m, float* v, long n, const fl
   // kernels running beside it (the FC Adam as a side branch of the step graph)
   // streaming loads/stores for large ranges (profiles/r1_17_adam_nt.md)
   const bool nt = n - hole_n >= (1L << 20);
-  const dim3 grid(grid_for(n - hole_n, max_grid > 0 ? max_grid : 2048));
-  if (nt)
-    hipLaunchKernelGGL(adam_kernel<true>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done, sh,
-                       ps, hole_lo, hole_n);
-  else
-    hipLaunchKernelGGL(adam_kernel<false>, grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, done,
-                       sh, ps, hole_lo, hole_n);
+  const dim3 grid(grid_for(n - hole_n, max_grid > 0 ? max_grid : 2048) + sj.wg0[nj]);
+#define QD_ADAM(NT_, SL_)                                                                                          \
+  hipLaunchKernelGGL((adam_kernel<NT_, SL_>), grid, dim3(256), 0, st, p, g, m, v, n, lr, step, skip, pruned, a, step, \
+                     done, sh, ps, hole_lo, hole_n, sj)
+  if (nj) {
+    if (nt) QD_ADAM(true, true); else QD_ADAM(false, true);
+  } else {
+    if (nt) QD_ADAM(true, false); else QD_ADAM(false, false);
+  }
+#undef QD_ADAM
   return (int)hipGetLastError();
 }
 

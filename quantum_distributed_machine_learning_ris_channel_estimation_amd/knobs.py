@@ -37,6 +37,9 @@ class Knobs:
     qsim_mfma12: bool = True
     # the 8-qubit adjoint backward on the matrix cores (qsim12_mfma.hip qd_qsim_mfma8_bwd; else qsim.hip's)
     qsim_mfma_bwd: bool = True
+    # (world 1) the HDCE Adam launch sums the step's gradient slabs (conv weights, BN, FC bias) in extra workgroups
+    # (optim.hip AdamSlabs) instead of a slab-reduction launch before it on the chain
+    adam_slabs: bool = True
     # the conv stack's training forward as one persistent launch (conv.hip conv_fwd_stack_kernel; else 3 conv launches
     # + the BN tail launch).  Measured slower: 105 against 58 us alone (docs/CONCURRENCY.md)
     conv_stack: bool = False

@@ -269,19 +269,25 @@ class FusedOptimizer:
 
     # ---------------------------------------------------------------- step
     def step(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None, part: Optional[int] = None,
-             pack=None) -> None:
+             pack=None, slabs=None) -> None:
         """One optimizer step over every part (``part=None``) or over part ``part`` only.  ``pack`` (GPU):
-        a callable (lo, hi) -> PackScatter for the range a launch updates (see ConvStackHIP.pack_scatter)."""
+        a callable (lo, hi) -> PackScatter for the range a launch updates (see ConvStackHIP.pack_scatter).
+        ``slabs`` (GPU, one part): an ops.slabsum.SlabBatch whose reductions write gradients of this space -- the
+        update sums them itself (optim.hip AdamSlabs) instead of a slab launch before it."""
         s = self.space
         parts = range(len(self.bounds)) if part is None else (part,)
         if not s.flat.is_cuda:
+            if slabs is not None:
+                raise ValueError("slab-fed updates are a GPU path")
             for i in parts:
                 self._step_host(i, grad_scale, skip)
             if self.shadow is not None:
                 self.refresh_shadow()
             return
+        if slabs is not None and (len(parts) != 1 or self.kind != "adam" and self.kind != "adamw"):
+            raise ValueError("slab-fed update: one Adam part per launch")
         for i in parts:
-            self._step_part(i, grad_scale, skip, pack)
+            self._step_part(i, grad_scale, skip, pack, slabs=slabs)
 
     def step_fused(self, grad_scale: float = 1.0, skip: Optional[torch.Tensor] = None, max_grid: int = 0) -> None:
         """(GPU) one Adam launch over the ``fuse_range`` hole itself, on the current stream, with the hole's own
@@ -294,7 +300,7 @@ class FusedOptimizer:
         self._step_part(len(self.bounds), grad_scale, skip, None, rng=(lo, hi), max_grid=max_grid)
 
     def _step_part(self, i: int, grad_scale: float, skip: Optional[torch.Tensor], pack=None, rng=None,
-                   max_grid: int = 0) -> None:
+                   max_grid: int = 0, slabs=None) -> None:
         s = self.space
         lo, hi = self.bounds[i] if rng is None else rng
         lib = nat.hip_lib()
@@ -309,8 +315,12 @@ class FusedOptimizer:
             if self.shadow is not None:
                 self.refresh_shadow()
             return
-        f = nat.fn(lib, "qd_adam_step", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
-                                         _p, _p, _l, _l, _p, _p, _p, _i, _p, _l, _l, _p])
+        f = nat.fn(lib, "qd_adam_step_slabs", [_p, _p, _p, _p, _l, _p, _p, _p, _p, _f, _f, _f, _f, _i, _f, _f,
+                                               _p, _p, _l, _l, _p, _p, _p, _i, _p, _l, _l,
+                                               _i, _p, _p, _p, _p, _p, _p, _p])
+        jobs = slabs.jobs_in(s.grad, lo, hi) if slabs is not None else []
+        nj = len(jobs)
+        col = lambda k, ty: (ty * max(nj, 1))(*[j[k] for j in jobs]) if nj else None
         hole_lo = hole_n = 0
         if rng is None and self.fused is not None and lo <= self.fused[0] and self.fused[1] <= hi:
             hole_lo, hole_n = self.fused[0] - lo, self.fused[1] - self.fused[0]
@@ -328,7 +338,9 @@ class FusedOptimizer:
                     self.prune_thr, done_p, sh_ptr, (sh_lo - lo) if has_sh else 0, (sh_hi - lo) if has_sh else 0,
                     sh8_ptr, nat.ptr(self.fp8.qs[self.fp8_slot:]) if f8 else None,
                     nat.ptr(self.fp8.amax[self.fp8_slot]) if f8 else None, int(max_grid or self.max_grid.get(i, 0)),
-                    ctypes.byref(ps) if ps is not None else None, hole_lo, hole_n, st),
+                    ctypes.byref(ps) if ps is not None else None, hole_lo, hole_n,
+                    nj, col(0, ctypes.c_void_p), col(1, ctypes.c_long), col(2, ctypes.c_int), col(3, ctypes.c_int),
+                    col(4, ctypes.c_int), col(5, ctypes.c_int), st),
                   "adam")
 
     @torch.no_grad()

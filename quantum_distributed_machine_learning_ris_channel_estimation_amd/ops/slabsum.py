@@ -35,6 +35,20 @@ class SlabBatch:
             raise RuntimeError(f"SlabBatch: more than {MAX_JOBS} reductions in one launch")
         self.jobs.append((slab.data_ptr() + 4 * offset, out, groups, rows, width, ld))
 
+    def jobs_in(self, flat_grad: torch.Tensor, lo: int, hi: int):
+        """The queued reductions as slab jobs of an optimizer launch over flat_grad[lo:hi] (ops/optim.py
+        ``step(slabs=...)``): (slab pointer, offset relative to lo, groups, rows, width, ld) per job.  Every output
+        must be a float32 view into flat_grad[lo:hi], and the whole batch is consumed (nothing is launched here)."""
+        base = flat_grad.data_ptr()
+        out = []
+        for slab_ptr, o, groups, rows, width, ld in self.jobs:
+            off = (o.data_ptr() - base) // 4
+            if o.dtype != torch.float32 or (o.data_ptr() - base) % 4 or off < lo or off + groups * width > hi:
+                raise ValueError("slab job output outside the optimizer's range")
+            out.append((slab_ptr, off - lo, groups, rows, width, ld))
+        self.jobs = []
+        return out
+
     def launch(self, accumulate: bool, stream) -> None:
         if not self.jobs:
             return

@@ -291,6 +291,9 @@ class HDCEStep:
         # world-1 plans: the FC bias gradient's column reduction rides in the conv backward's slab launch
         # (never in DP: the FC gradient bucket is all-reduced before the conv backward runs)
         self.bias_via_conv_slabs = False
+        # (world 1) backward_conv leaves the step's gradient slab reductions to the optimizer update (take_slabs)
+        self.defer_slabs = False
+        self._deferred = None
         self.defer_loss = True   # (with bias_via_conv_slabs) loss finish hosted by the conv backward
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; knobs.KNOBS.hand_gemm = "": hipBLASLt) and
@@ -442,9 +445,13 @@ class HDCEStep:
             lf = getattr(self.nmse, "pending_finish", None)
             self.nmse.pending_finish = None
             if pending is not None and slabs is None:
-                # the conv weight / BN slabs and the pending FC bias reduction: one overwrite launch
+                # the conv weight / BN slabs and the pending FC bias reduction: one overwrite launch -- or (defer_slabs)
+                # none: the caller's optimizer update sums them itself (take_slabs)
                 self.conv.backward(self._dA, accumulate=False, slabs=pending, side=side, loss_finish=lf)
-                pending.launch(accumulate=False, stream=nat.stream_ptr(self._dA.device))
+                if self.defer_slabs:
+                    self._deferred = pending
+                else:
+                    pending.launch(accumulate=False, stream=nat.stream_ptr(self._dA.device))
             else:
                 if pending is not None:
                     pending.launch(accumulate=False, stream=nat.stream_ptr(self._dA.device))
@@ -454,6 +461,12 @@ class HDCEStep:
             self._A = None
         if not (self.hip and self.conv.count_batches):   # the HIP forward counted them in-kernel
             self.m.count_batches(self.U)
+
+    def take_slabs(self):
+        """(defer_slabs) the SlabBatch the last backward_conv left unlaunched -- the conv weight / BN gradient slabs and
+        the FC bias reduction -- for ``FusedOptimizer.step(slabs=...)``; None when there is none."""
+        b, self._deferred = self._deferred, None
+        return b
 
     @torch.no_grad()
     def _forward_fc_hip(self, x1: torch.Tensor, label: torch.Tensor, perf: torch.Tensor) -> torch.Tensor:

@@ -48,6 +48,7 @@ from .. import _native as nat
 from ..data.datasets import DMLStore, make_dml_stores
 from ..models.estimators import QSC_P128
 from ..ops.gather import StepGather
+from ..knobs import KNOBS
 from ..ops.optim import FlatParamSpace, make_optimizer
 from ..ops.slabsum import SlabBatch
 from ..parallel.dp import DistContext, GradBuckets
@@ -279,6 +280,11 @@ class FlagshipTrainer(DPPlan):
             lo = sp.offsets[sp.names.index("CE.FC.weight")]
             self.hopt.fuse_range(lo, lo + self.hdce.fc_w.numel())
         self._fc_pending = False   # (fc_adam_next) an FC update forked in this replay that the next FC forward awaits
+        # (world 1) the HDCE update sums the step's gradient slabs itself: the slab launch leaves the chain
+        self.adam_slabs = bool(KNOBS.adam_slabs and self.hstep.hip and ctx.world == 1 and not cfg.split_graphs
+                               and self.hstep.writes_grads and self.hopt.kind in ("adam", "adamw")
+                               and len(self.hopt.bounds) == 1 and not self.fused_adam)
+        self.hstep.defer_slabs = self.adam_slabs
         # end-of-step weight pack (GPU fused path)
         self.tail_pack = bool(self.hstep.hip and cfg.tail_pack)
         if self.tail_pack:
@@ -423,7 +429,8 @@ class FlagshipTrainer(DPPlan):
 
     def _hdce_update(self) -> None:
         pk = self._adam_pack()
-        self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk)
+        sl = self.hstep.take_slabs() if self.adam_slabs else None
+        self.hopt.step(grad_scale=1.0, skip=self.hskip, pack=pk, slabs=sl)
         if self.tail_pack and pk is None:
             self._tail_pack_launch()
 

@@ -88,7 +88,9 @@ class DPPlan:
     def _dp_gr(self) -> None:
         g = 1.0 / self.ctx.world
         pk = self._adam_pack()
-        self.hopt.step(grad_scale=g, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None, pack=pk)
+        # (world-1 serial plan with adam_slabs: the update sums the step's gradient slabs itself)
+        sl = self.hstep.take_slabs() if getattr(self, "adam_slabs", False) else None
+        self.hopt.step(grad_scale=g, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None, pack=pk, slabs=sl)
         if self.tail_pack and pk is None:
             self._tail_pack_launch()
         self.qopt.step(grad_scale=g, skip=self.qskip)

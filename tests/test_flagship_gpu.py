@@ -264,3 +264,25 @@ def test_fused_fc_adam_matches_separate_adam(cuda, graphs):
     assert float(fus.hskip) != 0.0
     for i, (a, b) in enumerate(zip(before, _all_state(fus)[:7])):
         assert torch.equal(a, b), i   # (the whole HDCE step skipped, the fused FC update included)
+
+
+@pytest.mark.parametrize("mode", ["indep", "serial"])
+def test_slab_fed_adam_matches_slab_launch(cuda, monkeypatch, mode):
+    """The HDCE update summing the step's gradient slabs itself (knobs.KNOBS.adam_slabs: optim.hip AdamSlabs -- conv
+    weights, BN, FC bias) == the slab-reduction launch before a plain update, bit for bit over 6 steps: the same row
+    order per column and the same combine as conv.hip's slab_rows_sum4_body."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.knobs import KNOBS
+    ctx = DistContext(device=cuda)
+    base = dict(batch=32, data_len=800, use_quantumnat=True, qsc_grid_bwd=128, stream_mode=mode,
+                hip_graphs=mode != "serial")
+    trs = []
+    for on in (False, True):
+        monkeypatch.setattr(KNOBS, "adam_slabs", on)
+        tr = FlagshipTrainer(FlagshipConfig(steps_per_graph=3, **base), ctx)
+        assert tr.adam_slabs == on
+        tr.run(6)
+        torch.cuda.synchronize()
+        trs.append(tr)
+    for i, (a, b) in enumerate(zip(_all_state(trs[0]), _all_state(trs[1]))):
+        assert torch.equal(a, b), (i, float((a.float() - b.float()).abs().max()))
+    assert torch.equal(trs[0].hloss, trs[1].hloss)
