@@ -164,7 +164,9 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     if (ps.cursor && blockIdx.x == 0 && threadIdx.x == 0) *ps.cursor += ps.cursor_inc;
     return;
   }
-  const int nreg = SLABS ? (int)gridDim.x - sj.wg0[sj.n] : (int)gridDim.x;   // regular workgroups; then the slab jobs
+  // the slab jobs' workgroups come FIRST (dispatched in block order: appended after the 2048 regular ones they ran
+  // alone at the end of the launch -- measured no faster than the slab launch they replace)
+  const int nsl = SLABS ? sj.wg0[sj.n] : 0, nreg = (int)gridDim.x - nsl, rb = (int)blockIdx.x - nsl;
   const float lr = *lr_ptr;
   const float t = *step_ptr + 1.f;  // step about to be taken
   const float bc1 = 1.f - __powf(a.beta1, t);
@@ -197,11 +199,11 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
     stv<NT>(v + i0, vv);
     return gg;
   };
-  if (SLABS && (int)blockIdx.x >= nreg) {
+  if (SLABS && rb < 0) {
     // ---- a slab job's 64 columns: 16 column quads x 16 row phases, rounds of 4 rows with every load in flight
     // (conv.hip slab_rows_sum4_body's order: the same row sequence per thread whatever the round size), then the
     // update of those 64 elements ----
-    const int b = (int)blockIdx.x - nreg;
+    const int b = (int)blockIdx.x;
     int k = 0;
     while (k + 1 < sj.n && b >= sj.wg0[k + 1]) ++k;
     const int cpg = (sj.width[k] + 63) / 64, lb = b - sj.wg0[k], grp = lb / cpg, bx = lb % cpg;
@@ -245,7 +247,7 @@ __global__ void __launch_bounds__(256) adam_kernel(float* __restrict__ p, float*
   const long stride = (long)nreg * blockDim.x * 4;
   // [hole_lo, hole_lo + hole_n) (multiples of 4) is skipped: a range another kernel updates (the FC weight,
   // stepped inside its weight-gradient GEMM's epilogue); the loop runs over n - hole_n logical elements
-  for (long il = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4; il < n - hole_n; il += stride) {
+  for (long il = ((long)rb * blockDim.x + threadIdx.x) * 4; il < n - hole_n; il += stride) {
     const long i0 = il < hole_lo ? il : il + hole_n;
     if (SLABS && in_slab_job(sj, i0)) continue;   // (summed and stepped by the slab workgroups)
     if (i0 + 3 < n) {
