@@ -38,8 +38,11 @@ class Knobs:
     # the 8-qubit adjoint backward on the matrix cores (qsim12_mfma.hip qd_qsim_mfma8_bwd; else qsim.hip's)
     qsim_mfma_bwd: bool = True
     # (world 1) the HDCE Adam launch sums the step's gradient slabs (conv weights, BN, FC bias) in extra workgroups
-    # (optim.hip AdamSlabs) instead of a slab-reduction launch before it on the chain
-    adam_slabs: bool = True
+    # (optim.hip AdamSlabs) instead of a slab-reduction launch before it on the chain.  Off: bit-identical but not
+    # faster -- 0.3856-0.3876 against 0.3830-0.3852 ms with the slab workgroups first in block order, no gain with
+    # them last (profiles/r5_19_adam_slabs_ab_v*.txt); the slab-fed variant needs 90 VGPRs (occupancy 5 for the
+    # HBM-bound update instead of 7)
+    adam_slabs: bool = False
     # the conv stack's training forward as one persistent launch (conv.hip conv_fwd_stack_kernel; else 3 conv launches
     # + the BN tail launch).  Measured slower: 105 against 58 us alone (docs/CONCURRENCY.md)
     conv_stack: bool = False
