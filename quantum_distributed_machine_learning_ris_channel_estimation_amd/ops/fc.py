@@ -198,3 +198,20 @@ def gemm_dgrad_f8(dY8: torch.Tensor, W8: torch.Tensor, s_dy: torch.Tensor, s_w: 
                 nat.stream_ptr(dY8.device)), "gemm_dgrad_f8")
     return dA
 
+
+def gemm_dgrad_f8_bnred(dY8: torch.Tensor, W8: torch.Tensor, s_dy: torch.Tensor, s_w: torch.Tensor, out: torch.Tensor,
+                        cfg: int, z: torch.Tensor, st: torch.Tensor, part: torch.Tensor, B: int, U: int,
+                        HW: int) -> torch.Tensor:
+    """gemm_dgrad_f8 with gemm_dgrad_bnred's epilogue (csrc/hip/gemm.hip qd_gemm_dgrad_f8_bnred): the e4m3 data
+    gradient also writes layer 3's BN backward partial rows.  HW == 128, M == U B 3, 3 B >= 144; cfg 1 or 0."""
+    M, N = dY8.shape
+    K = W8.shape[1]
+    assert dY8.dtype == W8.dtype == torch.float8_e4m3fn and dY8.is_contiguous() and W8.is_contiguous()
+    assert W8.shape[0] == N and out.dtype == torch.bfloat16 and out.shape == (M, K) and out.is_contiguous()
+    assert z.dtype == torch.bfloat16 and z.is_contiguous() and z.numel() == M * K
+    assert part.is_contiguous() and part.numel() == U * (M // 144) * 2 * 96
+    f = _gemm_fn("qd_gemm_dgrad_f8_bnred", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _i, _i, _i, _p])
+    nat.check(f(nat.ptr(dY8), nat.ptr(W8), nat.ptr(s_dy), nat.ptr(s_w), nat.ptr(out), M, N, K, cfg, nat.ptr(z),
+                nat.ptr(st), nat.ptr(part), B, U, HW, nat.stream_ptr(dY8.device)), "gemm_dgrad_f8_bnred")
+    return out
+

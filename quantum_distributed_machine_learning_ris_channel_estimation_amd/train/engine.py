@@ -329,6 +329,13 @@ class HDCEStep:
                                     and self.conv.bwd_fused and self.gemm_cfg[2] in (0, 2, 5, 6) and model.E == 3
                                     and self.conv.HW in (128, 256) and 3 * batch >= 144
                                     and (n_users * batch * 3) % 144 == 0)
+            # the fp8 estimator's e4m3 data gradient carries the same epilogue (gemm.hip qd_gemm_dgrad_f8_bnred,
+            # 128-pixel maps only)
+            if (KNOBS.dgrad_bnred and getattr(model, "fp8", False) and KNOBS.hand_fp8 and self.conv.bwd_fused
+                    and model.E == 3 and self.conv.HW == 128 and 3 * batch >= 144
+                    and (n_users * batch * 3) % 144 == 0):
+                M = n_users * batch * 3
+                self.dgrad_bnred = self._f8_bwd_ok(M, model.fc_w.shape[0], model.fc_w.shape[1])
             if self.dgrad_bnred:
                 self.conv.enable_dgrad_bnred(n_users * batch * 3 // 144)
 
@@ -679,8 +686,15 @@ class HDCEStep:
             sc = m.fp8_scales
             if getattr(self, "_dA_buf", None) is None or self._dA_buf.shape != (dY.shape[0], W.shape[1]):
                 self._dA_buf = torch.empty(dY.shape[0], W.shape[1], device=dY.device, dtype=torch.bfloat16)
-            self._dA = gemm_dgrad_f8(self._dY8, m._shadow_w8, sc.scale[6:7], sc.scale[1:2], out=self._dA_buf,
-                                     cfg=int(KNOBS.f8_producers))
+            if self.dgrad_bnred:
+                from ..ops.fc import gemm_dgrad_f8_bnred
+                c = self.conv
+                self._dA = gemm_dgrad_f8_bnred(self._dY8, m._shadow_w8, sc.scale[6:7], sc.scale[1:2], self._dA_buf,
+                                               int(KNOBS.f8_producers), c.z[2], c.st[2], c.rslab[2], self.B, self.U,
+                                               c.HW)
+            else:
+                self._dA = gemm_dgrad_f8(self._dY8, m._shadow_w8, sc.scale[6:7], sc.scale[1:2], out=self._dA_buf,
+                                         cfg=int(KNOBS.f8_producers))
             sc.update()
             if self.stage_hook is not None:
                 self.stage_hook("dgrad")
@@ -699,7 +713,7 @@ class HDCEStep:
                 self._dA = gemm_dgrad(dY, W, out=self._dA_buf, cfg=self.gemm_cfg[2])
         else:
             if self.dgrad_bnred:
-                raise RuntimeError("dgrad_bnred needs the hand-written bf16 data gradient")
+                raise RuntimeError("dgrad_bnred needs the hand-written bf16 or e4m3 data gradient")
             self._dA = torch.mm(dY, W)                         # (rows, 4096) bf16
         if self.after_dgrad is not None:   # (the FC weight's shadow has had its last reader of the step)
             self.after_dgrad()

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import torch  # noqa: E402
 
 from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops.fc import (  # noqa: E402
-    gemm_dgrad, gemm_dgrad_f8, gemm_fwd, gemm_fwd_f8, gemm_wgrad, gemm_wgrad_f8)
+    gemm_dgrad, gemm_dgrad_bnred, gemm_dgrad_f8, gemm_dgrad_f8_bnred, gemm_fwd, gemm_fwd_f8, gemm_wgrad, gemm_wgrad_f8)
 
 
 def timeit(fn, iters=40):
@@ -60,6 +60,14 @@ def main():
     for c in (0, 1):
         var[f"wgrad8_c{c}"] = ("wgrad8", lambda c=c: gemm_wgrad_f8(dY8, A8, one, one, out=dW, cfg=c))
         var[f"dgrad8_c{c}"] = ("dgrad8", lambda c=c: gemm_dgrad_f8(dY8, W8, one, one, out=dA, cfg=c))
+    # the data gradients with layer 3's BN backward reduction in the epilogue (B 256, U 3, HW 128: M = 2304)
+    z = torch.randn(M, K, device=dev).bfloat16()
+    st = torch.rand(3, 96, 8, device=dev)
+    part = torch.empty(3 * (M // 144) * 2 * 96, device=dev)
+    var["dgrad_bnred_c6"] = ("dgrad", lambda: gemm_dgrad_bnred(dY, W, dA, 6, z, st, part, 256, 3, 128))
+    for c in (0, 1):
+        var[f"dgrad8_bnred_c{c}"] = ("dgrad8", lambda c=c: gemm_dgrad_f8_bnred(dY8, W8, one, one, dA, c, z, st, part,
+                                                                               256, 3, 128))
     if only:
         var = {k: v for k, v in var.items() if any(k.startswith(o) for o in only)}
     bad = []

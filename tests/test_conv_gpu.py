@@ -339,3 +339,34 @@ def test_dgrad_bn_reduction_epilogue_matches_its_own_launch(cuda, monkeypatch, p
     # (c2 / c3 of layer 3 come from the same sums in another order: a dz rounding may flip a bf16 dx here and there)
     assert rel(xf, xr) < 1e-4, rel(xf, xr)
     assert rel(gf, gr) < 1e-4, rel(gf, gr)
+
+
+def test_f8_dgrad_bn_reduction_epilogue_matches_its_own_launch(cuda, monkeypatch):
+    """The fp8 estimator's e4m3 data gradient with layer 3's BN backward reduction in its epilogue
+    (gemm.hip qd_gemm_dgrad_f8_bnred) vs the plain e4m3 data gradient + bn_bwd_reduce_kernel: same stored dh3,
+    other summation grouping.  A flagship step (the gathered path the hand-written e4m3 GEMMs need), batch 256:
+    M = 2304 rows tile the e4m3 gradients."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel.dp import DistContext
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import (FlagshipConfig,
+                                                                                                FlagshipTrainer)
+    ctx = DistContext(device=cuda)
+    cfg = dict(batch=256, data_len=1600, hip_graphs=False, use_quantumnat=False, stream_mode="serial", dtype="fp8")
+    outs = []
+    for fused in (True, False):
+        monkeypatch.setattr(KNOBS, "dgrad_bnred", fused)
+        tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
+        s = tr.hstep
+        assert s.dgrad_bnred == fused
+        for _ in range(2):   # (the second step runs on amax-set delayed scales)
+            tr.hdce.space.zero_grad()
+            tr.next_batch()
+            tr._dp_g1()
+            tr._dp_g2()
+        torch.cuda.synchronize()
+        assert s.fc_path == "hand_f8" and s._f8_bwd
+        outs.append((tr.hloss.clone(), tr.hdce.space.grad.clone(), s.conv.dx[1].clone()))
+    (lf, gf, xf), (lr_, gr, xr) = outs
+    assert torch.equal(lf, lr_)
+    assert float(gf.abs().max()) > 0
+    assert rel(xf, xr) < 1e-4, rel(xf, xr)
+    assert rel(gf, gr) < 1e-4, rel(gf, gr)
