@@ -61,7 +61,7 @@ typedef __attribute__((address_space(1))) void glb_void;
 // stage): with a WM x 1 wave grid every A row belongs to exactly one wave, so staging A through LDS only
 // costs LDS bandwidth (round 4, see the DA configurations below)
 enum { KC = 0, MC = 1, MC8 = 2, KCD = 3 };
-enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2, EPI_ADAM = 3, EPI_BF16_BNP = 4 };
+enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2, EPI_ADAM = 3 };
 constexpr int BK = 64;
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
@@ -524,20 +524,18 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_i, int tiles
   }
 }
 
-// EPI_BF16 row passes with the BN backward reduction (BnRedEpi), by NWE waves (index wv among them).  Wave wv takes
-// rows wv + NWE k; with i0 % 3 == 0 the expert of row wv + NWE k is (wv + NWE k) % 3, so k % 3 is a fixed accumulator
-// slot per wave (no runtime register indexing).  A tile spans at most two statistics groups (BM <= B E): rows >= rb
-// belong to group u_lo + 1.  VEC: columns per lane (4: 256-column tiles, the bf16 data gradients; 2: 128-column
-// tiles, the e4m3 one, HW = 128 only -- a channel's 128 columns are then the whole tile row).
-// Two forms: the compute waves after a plain K loop (NWE = NW, STORE: they also write dA, z loaded here), or the
-// producer waves of a PW > 0 tile (NWE = PW, z prefetched into zpre during the K loop's last steps -- see
-// gemm_kernel: the first NPRE rows), while the compute waves store dA beside them.
-template <class G, int VEC, int NWE, bool STORE, int NPRE = 0>
+// EPI_BF16 row passes with the BN backward reduction (BnRedEpi).  Wave w takes rows w + NW k; with i0 % 3 == 0 the
+// expert of row w + NW k is (w + NW k) % 3, so k % 3 is a fixed accumulator slot per wave (no runtime register
+// indexing).  A tile spans at most two statistics groups (BM <= B E): rows >= rb belong to group u_lo + 1.
+// VEC: columns per lane (4: 256-column tiles, the bf16 data gradients; 2: 128-column tiles, the e4m3 one, HW = 128
+// only -- a channel's 128 columns are then the whole tile row).
+// (Round 5 also ran it on a producer-wave tile's producers, z rows prefetched during the K loop's tail, while the
+// compute waves stored dA: slower, see qd_gemm_dgrad_bnred.)
+template <class G, int VEC>
 __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, uint16_t* C, const float* bv, int i0,
-                                               int j0, int ti, int c0, int wv, int lane, const uint2* zpre) {
+                                               int j0, int ti, int c0, int wave, int lane, int tid) {
   static_assert(VEC == 2 || VEC == 4, "bnred rows of 2 or 4 columns per lane");
-  static_assert(G::BM % (3 * NWE) == 0 && NWE % 3 != 0, "a fixed expert slot per (wave, k % 3)");
-  constexpr int PITCH = G::PITCH, RPW = G::BM / NWE, NSTR = 8;
+  constexpr int PITCH = G::PITCH, RPW = G::BM / G::NW, NSTR = 8;
   const BnRedEpi& br = a.br;
   const int col = j0 + c0, c = col / br.HW;   // this lane's channel (within its expert)
   const int ub = br.B * 3, u_lo = i0 / ub, rb = (u_lo + 1) * ub - i0;
@@ -547,68 +545,55 @@ __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, u
   for (int us = 0; us < 2; ++us)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const int e = (wv + NWE * j) % 3;
+      const int e = (wave + G::NW * j) % 3;
       rec[us][j] = *reinterpret_cast<const float4*>(br.st + ((size_t)(us ? u_hi : u_lo) * br.EC + e * 32 + c) * NSTR);
     }
+  uint2 zr[RPW];   // every row's z first (one round trip for the whole pass; VEC 2: .x only)
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const uint16_t* zp = br.z + (size_t)(i0 + wave + G::NW * k) * a.ldc + col;
+    if constexpr (VEC == 4) zr[k] = *reinterpret_cast<const uint2*>(zp);
+    else zr[k] = make_uint2(*reinterpret_cast<const uint32_t*>(zp), 0u);
+  }
   float s[2][3][2];
 #pragma unroll
   for (int us = 0; us < 2; ++us)
 #pragma unroll
     for (int j = 0; j < 3; ++j) s[us][j][0] = s[us][j][1] = 0.f;
-  // rows in chunks of CH (a multiple of 3), each chunk's z loads first (one round trip per chunk; VEC 2: .x only).
-  // One chunk up to 18 rows; the producer form's 36 rows of 8 bytes in 12-row chunks (72 VGPRs of z at once spilled)
-  constexpr int CH = RPW > 18 ? 12 : RPW;
-  static_assert(RPW % CH == 0 && CH % 3 == 0, "row chunks");
 #pragma unroll
-  for (int k0 = 0; k0 < RPW; k0 += CH) {
-    if constexpr (CH < RPW) __builtin_amdgcn_sched_barrier(0);   // (no chunk's loads hoisted above another's math)
-    uint2 zr[CH];
-#pragma unroll
-    for (int kk = 0; kk < CH; ++kk) {
-      const int k = k0 + kk;
-      if constexpr (NPRE > 0) if (k < NPRE) {
-        zr[kk] = zpre[k < NPRE ? k : 0];
-        continue;
-      }
-      const uint16_t* zp = br.z + (size_t)(i0 + wv + NWE * k) * a.ldc + col;
-      if constexpr (VEC == 4) zr[kk] = *reinterpret_cast<const uint2*>(zp);
-      else zr[kk] = make_uint2(*reinterpret_cast<const uint32_t*>(zp), 0u);
+  for (int k = 0; k < RPW; ++k) {
+    const int row = wave + G::NW * k, j = k % 3;
+    uint2 w;
+    if constexpr (VEC == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(ct + row * PITCH + c0);
+      w.x = (uint32_t)f32_to_bf16(v.x + bv[0]) | ((uint32_t)f32_to_bf16(v.y + bv[1]) << 16);
+      w.y = (uint32_t)f32_to_bf16(v.z + bv[2]) | ((uint32_t)f32_to_bf16(v.w + bv[3]) << 16);
+      *reinterpret_cast<uint2*>(C + (size_t)(i0 + row) * a.ldc + col) = w;
+    } else {
+      const float2 v = *reinterpret_cast<const float2*>(ct + row * PITCH + c0);
+      w.x = (uint32_t)f32_to_bf16(v.x + bv[0]) | ((uint32_t)f32_to_bf16(v.y + bv[1]) << 16);
+      w.y = 0u;
+      *reinterpret_cast<uint32_t*>(C + (size_t)(i0 + row) * a.ldc + col) = w.x;
     }
+    const float d[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                        __uint_as_float(w.y & 0xffff0000u)};
+    const float zz[4] = {__uint_as_float(zr[k].x << 16), __uint_as_float(zr[k].x & 0xffff0000u),
+                         __uint_as_float(zr[k].y << 16), __uint_as_float(zr[k].y & 0xffff0000u)};
+    const bool hi = row >= rb;   // (wave-uniform)
+    const float4 r = hi ? rec[1][j] : rec[0][j];
+    float tg = 0.f, tgx = 0.f;
 #pragma unroll
-    for (int kk = 0; kk < CH; ++kk) {
-      const int k = k0 + kk, row = wv + NWE * k, j = k % 3;
-      uint2 w;
-      if constexpr (VEC == 4) {
-        const float4 v = *reinterpret_cast<const float4*>(ct + row * PITCH + c0);
-        w.x = (uint32_t)f32_to_bf16(v.x + bv[0]) | ((uint32_t)f32_to_bf16(v.y + bv[1]) << 16);
-        w.y = (uint32_t)f32_to_bf16(v.z + bv[2]) | ((uint32_t)f32_to_bf16(v.w + bv[3]) << 16);
-        if constexpr (STORE) *reinterpret_cast<uint2*>(C + (size_t)(i0 + row) * a.ldc + col) = w;
-      } else {
-        const float2 v = *reinterpret_cast<const float2*>(ct + row * PITCH + c0);
-        w.x = (uint32_t)f32_to_bf16(v.x + bv[0]) | ((uint32_t)f32_to_bf16(v.y + bv[1]) << 16);
-        w.y = 0u;
-        if constexpr (STORE) *reinterpret_cast<uint32_t*>(C + (size_t)(i0 + row) * a.ldc + col) = w.x;
-      }
-      const float d[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
-                          __uint_as_float(w.y & 0xffff0000u)};
-      const float zz[4] = {__uint_as_float(zr[kk].x << 16), __uint_as_float(zr[kk].x & 0xffff0000u),
-                           __uint_as_float(zr[kk].y << 16), __uint_as_float(zr[kk].y & 0xffff0000u)};
-      const bool hi = row >= rb;   // (wave-uniform)
-      const float4 r = hi ? rec[1][j] : rec[0][j];
-      float tg = 0.f, tgx = 0.f;
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) {
-        const float g = (r.z * zz[q] + r.w > 0.f) ? d[q] : 0.f;
-        tg += g;
-        tgx += g * (zz[q] - r.x) * r.y;
-      }
-      if (hi) {
-        s[1][j][0] += tg;
-        s[1][j][1] += tgx;
-      } else {
-        s[0][j][0] += tg;
-        s[0][j][1] += tgx;
-      }
+    for (int q = 0; q < VEC; ++q) {
+      const float g = (r.z * zz[q] + r.w > 0.f) ? d[q] : 0.f;
+      tg += g;
+      tgx += g * (zz[q] - r.x) * r.y;
+    }
+    if (hi) {
+      s[1][j][0] += tg;
+      s[1][j][1] += tgx;
+    } else {
+      s[0][j][0] += tg;
+      s[0][j][1] += tgx;
     }
   }
   // lanes of one channel: HW / VEC -- 32 (VEC 4, HW 128: lane halves are two channels) or all 64
@@ -631,49 +616,26 @@ __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, u
 #pragma unroll
       for (int j = 0; j < 3; ++j)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) red[((wv * 2 + half) * 2 + us) * 6 + j * 2 + k] = s[us][j][k];
+        for (int k = 0; k < 2; ++k) red[((wave * 2 + half) * 2 + us) * 6 + j * 2 + k] = s[us][j][k];
   }
-  // (producer form: the compute waves pass no barrier after the tile's; an ended wave no longer counts at one)
   __syncthreads();
   // (half, us, e, k) partials, summed over the waves in wave order
-  const int nhalf = 64 / span, lt = wv * 64 + lane;
-  if (lt < nhalf * 12) {
-    const int half = lt / 12, us = (lt % 12) / 6, e = (lt % 6) / 2, k = lt % 2;
+  const int nhalf = 64 / span;
+  if (tid < nhalf * 12) {
+    const int half = tid / 12, us = (tid % 12) / 6, e = (tid % 6) / 2, k = tid % 2;
     const int uu = u_lo + us;
     const bool has = us == 0 ? rb > 0 : (rb < G::BM && uu < br.U);
     if (has) {
       float t = 0.f;
-      for (int w = 0; w < NWE; ++w) {
+      for (int w = 0; w < G::NW; ++w) {
         int j = 0;
-        while ((w + NWE * j) % 3 != e) ++j;
+        while ((w + G::NW * j) % 3 != e) ++j;
         t += red[((w * 2 + half) * 2 + us) * 6 + j * 2 + k];
       }
       const int ch = e * 32 + (j0 + half * span * VEC) / br.HW;
       br.part[(((size_t)uu * (a.I / G::BM) + ti) * 2 + k) * br.EC + ch] = t;
     }
   }
-}
-
-// the producer waves' form of the BN reduction epilogue (see bnred_epilogue): a PW > 0 one-K-group tile whose
-// producers can hold their rows' z while they wait out the K loop's last steps (vmcnt stays within its 6 bits)
-template <class G>
-struct BnPre {
-  static constexpr int VEC = G::BN / 64;
-  static constexpr int RPW = G::PW > 0 ? G::BM / G::PW : 1;
-  // rows whose z is prefetched (the rest load at the epilogue's start): all of them in 4-byte rows, 16 of the
-  // 8-byte ones (36 x 2 VGPRs beside the 12-wave tile's 168 spilled)
-  static constexpr int NPRE = VEC == 2 ? RPW : (RPW < 16 ? RPW : 16);
-  static constexpr bool ON = G::PW > 0 && G::KS == 1 && G::PW % 3 != 0 && G::BM % (3 * (G::PW > 0 ? G::PW : 1)) == 0 &&
-                             (G::NSTAGE - 3) * G::NPER + NPRE <= 63 && RPW <= 48;
-};
-
-template <class G, int X>
-__device__ __forceinline__ void vm_wait_x(int tiles) {   // vm_wait with X younger loads also left in flight
-  constexpr int N = G::NPER;
-  // (a count below the exact one only waits longer)
-  if (tiles >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N + X <= 63 ? 2 * N + X : 63) : "memory");
-  else if (tiles == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N + X <= 63 ? N + X : 63) : "memory");
-  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
 }
 
 template <class G, int EPI, int GM, int GN>
@@ -715,36 +677,6 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
         vm_wait<G>(NS - 3 < 0 ? 0 : NS - 3);
         __builtin_amdgcn_s_barrier();
         stg.issue(smem + ((t + NS - 1) % NS) * G::STAGE);
-      }
-      if constexpr (EPI == EPI_BF16_BNP) {
-        static_assert(BnPre<G>::ON, "EPI_BF16_BNP: a BnPre tile");
-        if (a.br.z != nullptr) {
-          // BN reduction epilogue (BnPre): this producer's rows of z in flight behind the ring's last pieces (loads
-          // return in issue order, so the ring waits below leave exactly these RPW younger loads outstanding)
-          constexpr int NPRE = BnPre<G>::NPRE, VEC = BnPre<G>::VEC;
-          const int wv = wave - G::NW, c0 = VEC * lane;
-          uint2 zpre[NPRE];
-#pragma unroll
-          for (int k = 0; k < NPRE; ++k) {
-            const uint16_t* zp = a.br.z + (size_t)(i0 + wv + G::PW * k) * a.ldc + j0 + c0;
-            if constexpr (VEC == 4) zpre[k] = *reinterpret_cast<const uint2*>(zp);
-            else zpre[k] = make_uint2(*reinterpret_cast<const uint32_t*>(zp), 0u);
-          }
-          for (; t < steps; ++t) {
-            vm_wait_x<G, NPRE>(nk - 2 - t);
-            __builtin_amdgcn_s_barrier();
-          }
-          // the compute waves' two barriers (K loop done, the ring becomes the fp32 tile; the tile written) -- raw, so
-          // the z loads stay in flight until their first use
-          __builtin_amdgcn_s_barrier();
-          __builtin_amdgcn_s_barrier();
-          float bv[VEC];
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) bv[v] = a.bias ? bf16_to_f32(a.bias[j0 + c0 + v]) : 0.f;
-          bnred_epilogue<G, VEC, G::PW, false, NPRE>(a, reinterpret_cast<const float*>(smem), nullptr, bv, i0, j0, ti,
-                                                     c0, wv, lane, zpre);
-          return;
-        }
       }
       for (; t < steps; ++t) {
         vm_wait<G>(nk - 2 - t);
@@ -902,16 +834,14 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
         __hip_atomic_store(ad.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-  } else if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_BNP) {
+  } else if constexpr (EPI == EPI_BF16) {
     uint16_t* C = reinterpret_cast<uint16_t*>(a.C);
     float bv[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) bv[v] = a.bias ? bf16_to_f32(a.bias[j0 + c0 + v]) : 0.f;
-    // (EPI_BF16_BNP: the producer waves reduce, these waves only store dA below)
-    if constexpr (EPI == EPI_BF16 && (VEC == 4 || VEC == 2) && G::KS == 1 && G::BM % (3 * G::NW) == 0 &&
-                  G::NW % 3 != 0) {
+    if constexpr ((VEC == 4 || VEC == 2) && G::KS == 1 && G::BM % (3 * G::NW) == 0 && G::NW % 3 != 0) {
       if (a.br.z != nullptr) {
-        bnred_epilogue<G, VEC, G::NW, true>(a, ct, C, bv, i0, j0, ti, c0, wave, lane, nullptr);
+        bnred_epilogue<G, VEC>(a, ct, C, bv, i0, j0, ti, c0, wave, lane, tid);
         return;
       }
     }
@@ -1287,8 +1217,9 @@ QD_API int qd_gemm_dgrad_bnred(const uint16_t* dY, const uint16_t* W, uint16_t* 
   Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}, nullptr, 0, nullptr};
   a.br = BnRedEpi{z, st, part, B, U, HW, 96};
   hipStream_t st_ = (hipStream_t)stream;
-  // (producer-wave tiles: the compute waves reduce after the producers have ended -- 36 rows of z per producer
-  // would not fit beside these tiles' registers, see BnPre)
+  // (producer-wave tiles: the compute waves reduce after the producers have ended.  Run by the producers instead,
+  // with z prefetched during the K loop's tail, the e4m3 tile's epilogue was slower: 46.8 against 44.3 us,
+  // profiles/r5_24_dgrad_bnred_probe.txt; the 12-wave bf16 tile spilled)
   if (cfg == 5 || cfg == 6) {
     if (3 * B < DgrQ::BM) return (int)hipErrorInvalidValue;
     return cfg == 6 ? launch<DgrQ, EPI_BF16, 4, 4>(a, st_) : launch<DgrP, EPI_BF16, 4, 4>(a, st_);
@@ -1424,7 +1355,7 @@ QD_API int qd_gemm_dgrad_f8_bnred(const uint8_t* dY8, const uint8_t* W8, const f
   Args a{reinterpret_cast<const uint16_t*>(dY8), reinterpret_cast<const uint16_t*>(W8), N / 2, K / 2, M, K, N / 2,
          dA, K, nullptr, {}, nullptr, 0, sdy, {}, sw};
   a.br = BnRedEpi{z, st, part, B, U, HW, 96};
-  if (cfg == 1) return launch<DgrM8CP, EPI_BF16_BNP, 4, 8>(a, (hipStream_t)stream);
+  if (cfg == 1) return launch<DgrM8CP, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
   return launch<DgrM8C, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
 }
 // dA (M, K) bf16 = sdy sw dY8 W8: dY8 (M, N), W8 (N, K)

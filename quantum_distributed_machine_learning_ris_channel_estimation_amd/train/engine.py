@@ -329,9 +329,9 @@ class HDCEStep:
                                     and self.conv.bwd_fused and self.gemm_cfg[2] in (0, 2, 5, 6) and model.E == 3
                                     and self.conv.HW in (128, 256) and 3 * batch >= 144
                                     and (n_users * batch * 3) % 144 == 0)
-            # the fp8 estimator's e4m3 data gradient carries the same epilogue (gemm.hip qd_gemm_dgrad_f8_bnred,
-            # 128-pixel maps only)
-            if (KNOBS.dgrad_bnred and getattr(model, "fp8", False) and KNOBS.hand_fp8 and self.conv.bwd_fused
+            # the fp8 estimator's e4m3 data gradient with the same epilogue (gemm.hip qd_gemm_dgrad_f8_bnred,
+            # 128-pixel maps only; KNOBS.dgrad_bnred_f8, off: measured no faster)
+            if (KNOBS.dgrad_bnred_f8 and getattr(model, "fp8", False) and KNOBS.hand_fp8 and self.conv.bwd_fused
                     and model.E == 3 and self.conv.HW == 128 and 3 * batch >= 144
                     and (n_users * batch * 3) % 144 == 0):
                 M = n_users * batch * 3

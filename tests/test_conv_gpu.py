@@ -353,7 +353,7 @@ def test_f8_dgrad_bn_reduction_epilogue_matches_its_own_launch(cuda, monkeypatch
     cfg = dict(batch=256, data_len=1600, hip_graphs=False, use_quantumnat=False, stream_mode="serial", dtype="fp8")
     outs = []
     for fused in (True, False):
-        monkeypatch.setattr(KNOBS, "dgrad_bnred", fused)
+        monkeypatch.setattr(KNOBS, "dgrad_bnred_f8", fused)
         tr = FlagshipTrainer(FlagshipConfig(**cfg), ctx)
         s = tr.hstep
         assert s.dgrad_bnred == fused
