@@ -62,6 +62,8 @@ typedef __attribute__((address_space(1))) void glb_void;
 // costs LDS bandwidth (round 4, see the DA configurations below)
 enum { KC = 0, MC = 1, MC8 = 2, KCD = 3 };
 enum { EPI_F32 = 0, EPI_BF16 = 1, EPI_NMSE = 2, EPI_ADAM = 3 };
+// (diagnosis builds: EPI_BF16 with the BN reduction epilogue's DBG = EPI - 4, see bnred_epilogue)
+enum { EPI_BF16_D1 = 5, EPI_BF16_D2 = 6, EPI_BF16_D3 = 7 };
 constexpr int BK = 64;
 
 __device__ __forceinline__ int kc_off(int row, int ch) { return row * 128 + ((ch ^ (row & 7)) << 4); }
@@ -531,7 +533,9 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_i, int tiles
 // only -- a channel's 128 columns are then the whole tile row).
 // (Round 5 also ran it on a producer-wave tile's producers, z rows prefetched during the K loop's tail, while the
 // compute waves stored dA: slower, see qd_gemm_dgrad_bnred.)
-template <class G, int VEC>
+// DBG (diagnosis builds, qd_gemm_dgrad_bnred_dbg): bit 0 = no z loads (a constant z), bit 1 = no cross-lane / cross-wave
+// reduction (each lane's sums kept alive by a never-taken store)
+template <class G, int VEC, int DBG = 0>
 __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, uint16_t* C, const float* bv, int i0,
                                                int j0, int ti, int c0, int wave, int lane, int tid) {
   static_assert(VEC == 2 || VEC == 4, "bnred rows of 2 or 4 columns per lane");
@@ -552,7 +556,8 @@ __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, u
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
     const uint16_t* zp = br.z + (size_t)(i0 + wave + G::NW * k) * a.ldc + col;
-    if constexpr (VEC == 4) zr[k] = *reinterpret_cast<const uint2*>(zp);
+    if constexpr (DBG & 1) zr[k] = make_uint2(0x3f803f80u + (uint32_t)k, 0x3f803f80u);
+    else if constexpr (VEC == 4) zr[k] = *reinterpret_cast<const uint2*>(zp);
     else zr[k] = make_uint2(*reinterpret_cast<const uint32_t*>(zp), 0u);
   }
   float s[2][3][2];
@@ -595,6 +600,15 @@ __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, u
       s[0][j][0] += tg;
       s[0][j][1] += tgx;
     }
+  }
+  if constexpr ((DBG & 2) != 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int us = 0; us < 2; ++us)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) t += s[us][j][0] + s[us][j][1];
+    if (t == 1234.5f) br.part[tid] = t;
+    return;
   }
   // lanes of one channel: HW / VEC -- 32 (VEC 4, HW 128: lane halves are two channels) or all 64
   const int span = br.HW / VEC;
@@ -834,14 +848,14 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
         __hip_atomic_store(ad.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-  } else if constexpr (EPI == EPI_BF16) {
+  } else if constexpr (EPI == EPI_BF16 || EPI >= EPI_BF16_D1) {
     uint16_t* C = reinterpret_cast<uint16_t*>(a.C);
     float bv[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) bv[v] = a.bias ? bf16_to_f32(a.bias[j0 + c0 + v]) : 0.f;
     if constexpr ((VEC == 4 || VEC == 2) && G::KS == 1 && G::BM % (3 * G::NW) == 0 && G::NW % 3 != 0) {
       if (a.br.z != nullptr) {
-        bnred_epilogue<G, VEC>(a, ct, C, bv, i0, j0, ti, c0, wave, lane, tid);
+        bnred_epilogue<G, VEC, (EPI >= EPI_BF16_D1 ? EPI - 4 : 0)>(a, ct, C, bv, i0, j0, ti, c0, wave, lane, tid);
         return;
       }
     }
@@ -1357,6 +1371,20 @@ QD_API int qd_gemm_dgrad_f8_bnred(const uint8_t* dY8, const uint8_t* W8, const f
   a.br = BnRedEpi{z, st, part, B, U, HW, 96};
   if (cfg == 1) return launch<DgrM8CP, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
   return launch<DgrM8C, EPI_BF16, 4, 8>(a, (hipStream_t)stream);
+}
+// (diagnosis builds) qd_gemm_dgrad_bnred, cfg 6, with the epilogue's DBG 1-3 (scripts/probes/probe_gemm_r5.py)
+QD_API int qd_gemm_dgrad_bnred_dbg(const uint16_t* dY, const uint16_t* W, uint16_t* dA, int M, int N, int K, int dbg,
+                                   const uint16_t* z, const float* st, float* part, int B, int U, int HW,
+                                   void* stream) {
+  if (!z || !st || !part || (HW != 128 && HW != 256) || K != 32 * HW || M != U * B * 3 || 3 * B < DgrQ::BM)
+    return (int)hipErrorInvalidValue;
+  Args a{dY, W, N, K, M, K, N, dA, K, nullptr, {}, nullptr, 0, nullptr};
+  a.br = BnRedEpi{z, st, part, B, U, HW, 96};
+  hipStream_t st_ = (hipStream_t)stream;
+  if (dbg == 1) return launch<DgrQ, EPI_BF16_D1, 4, 4>(a, st_);
+  if (dbg == 2) return launch<DgrQ, EPI_BF16_D2, 4, 4>(a, st_);
+  if (dbg == 3) return launch<DgrQ, EPI_BF16_D3, 4, 4>(a, st_);
+  return (int)hipErrorInvalidValue;
 }
 // dA (M, K) bf16 = sdy sw dY8 W8: dY8 (M, N), W8 (N, K)
 QD_API int qd_gemm_dgrad_f8(const uint8_t* dY8, const uint8_t* W8, const float* sdy, const float* sw, uint16_t* dA, int M,

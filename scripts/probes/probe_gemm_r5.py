@@ -65,6 +65,16 @@ def main():
     st = torch.rand(3, 96, 8, device=dev)
     part = torch.empty(3 * (M // 144) * 2 * 96, device=dev)
     var["dgrad_bnred_c6"] = ("dgrad", lambda: gemm_dgrad_bnred(dY, W, dA, 6, z, st, part, 256, 3, 128))
+    # (diagnosis) the bf16 epilogue with its z loads replaced by a constant (d1), without the cross-lane / cross-wave
+    # reduction (d2), both (d3)
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.ops import fc as _fc
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as _nat
+    fdbg = _fc._gemm_fn("qd_gemm_dgrad_bnred_dbg", [_fc._p, _fc._p, _fc._p] + [_fc._i] * 4 + [_fc._p] * 3 + [_fc._i] * 3
+                        + [_fc._p])
+    for d in (1, 2, 3):
+        var[f"dgrad_bnred_d{d}"] = ("dgrad", lambda d=d: _nat.check(fdbg(
+            _nat.ptr(dY), _nat.ptr(W), _nat.ptr(dA), M, N, K, d, _nat.ptr(z), _nat.ptr(st), _nat.ptr(part), 256, 3,
+            128, _nat.stream_ptr(dY.device)), "dbg"))
     for c in (0, 1):
         var[f"dgrad8_bnred_c{c}"] = ("dgrad8", lambda c=c: gemm_dgrad_f8_bnred(dY8, W8, one, one, dA, c, z, st, part,
                                                                                256, 3, 128))
