@@ -611,17 +611,23 @@ __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, u
     return;
   }
   // lanes of one channel: HW / VEC -- 32 (VEC 4, HW 128: lane halves are two channels) or all 64
+  // (butterfly steps unrolled with the 12 sums side by side: a rolled step loop per sum serialised 60 lane exchanges,
+  // 6 us of a 47 us launch -- profiles/r5_25_dgrad_bnred_dbg.txt)
   const int span = br.HW / VEC;
+  auto xstep = [&](int m) __attribute__((always_inline)) {
 #pragma unroll
-  for (int us = 0; us < 2; ++us)
+    for (int us = 0; us < 2; ++us)
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+      for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        float t = s[us][j][k];
-        for (int m = 1; m < span; m <<= 1) t += __shfl_xor(t, m);
-        s[us][j][k] = t;
-      }
+        for (int k = 0; k < 2; ++k) s[us][j][k] += __shfl_xor(s[us][j][k], m);
+  };
+  xstep(1);
+  xstep(2);
+  xstep(4);
+  xstep(8);
+  xstep(16);
+  if (span == 64) xstep(32);   // (wave-uniform)
   float* red = const_cast<float*>(ct) + G::BM * PITCH;   // (the 8 KB after the tile)
   if ((lane & (span - 1)) == 0) {
     const int half = lane / span;
@@ -641,9 +647,10 @@ __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, u
     const bool has = us == 0 ? rb > 0 : (rb < G::BM && uu < br.U);
     if (has) {
       float t = 0.f;
+#pragma unroll
       for (int w = 0; w < G::NW; ++w) {
-        int j = 0;
-        while ((w + G::NW * j) % 3 != e) ++j;
+        // the slot j with (w + NW j) % 3 == e: j = (e - w) (NW % 3) mod 3, as (NW % 3)^2 = 1 mod 3
+        const int j = ((e - w % 3 + 3) * (G::NW % 3)) % 3;
         t += red[((w * 2 + half) * 2 + us) * 6 + j * 2 + k];
       }
       const int ch = e * 32 + (j0 + half * span * VEC) / br.HW;
