@@ -33,11 +33,10 @@ class Knobs:
     # layer 3's BN backward reduction in the FC data gradient's epilogue (gemm.hip BnRedEpi; else its own launch,
     # conv.hip bn_bwd_reduce_kernel)
     dgrad_bnred: bool = True
-    # the same epilogue on the fp8 estimator's e4m3 data gradient (gemm.hip qd_gemm_dgrad_f8_bnred).  Off: the
-    # epilogue costs the 144 x 128 e4m3 tile 17 us (27.7 -> 44.3 us alone, its 256-byte z row pieces) against the
-    # 13 us launch it replaces, and the fp8 step is no faster: 0.3765-0.3767 against 0.3747-0.3771 ms
-    # (profiles/r5_21_fp8_dgrad_bnred_ab.txt, r5_23_dgrad_bnred_probe.txt)
-    dgrad_bnred_f8: bool = False
+    # the same epilogue on the fp8 estimator's e4m3 data gradient (gemm.hip qd_gemm_dgrad_f8_bnred): 27.7 -> 36.9 us
+    # alone against the 13 us launch it replaces; the fp8 step 0.3718-0.3730 against 0.3766-0.3772 ms
+    # (profiles/r5_27_*; with the epilogue's rolled butterfly it was +17 us and no faster, r5_21 / r5_23)
+    dgrad_bnred_f8: bool = True
     # the 12-qubit circuit, forward and adjoint, on the matrix cores (csrc/hip/qsim12_mfma.hip; else qsim_big.hip)
     qsim_mfma12: bool = True
     # the 8-qubit adjoint backward on the matrix cores (qsim12_mfma.hip qd_qsim_mfma8_bwd; else qsim.hip's)

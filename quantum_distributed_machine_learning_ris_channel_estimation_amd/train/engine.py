@@ -330,7 +330,7 @@ class HDCEStep:
                                     and self.conv.HW in (128, 256) and 3 * batch >= 144
                                     and (n_users * batch * 3) % 144 == 0)
             # the fp8 estimator's e4m3 data gradient with the same epilogue (gemm.hip qd_gemm_dgrad_f8_bnred,
-            # 128-pixel maps only; KNOBS.dgrad_bnred_f8, off: measured no faster)
+            # 128-pixel maps only; KNOBS.dgrad_bnred_f8)
             if (KNOBS.dgrad_bnred_f8 and getattr(model, "fp8", False) and KNOBS.hand_fp8 and self.conv.bwd_fused
                     and model.E == 3 and self.conv.HW == 128 and 3 * batch >= 144
                     and (n_users * batch * 3) % 144 == 0):
