@@ -916,7 +916,21 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     float mx8 = 0.f;
     constexpr int RU = G::BM % (G::NW * 12) == 0 ? 12 : G::BM % (G::NW * 9) == 0 ? 9 : 6;   // rows per batch
     static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
-    for (int r0 = wave * RU; r0 < G::BM; r0 += G::NW * RU) {
+    // FAST (3 experts, the waves' batch round = one 48-row chunk of 16 samples): a lane keeps its error sums per
+    // (batch, expert) -- row q of a batch is expert q % 3 -- and the wave reduces them once, all side by side,
+    // after the rows; else every row's sums go through the wave on their own (2 dependent 6-step lane-exchange
+    // chains per row: 20 of the e4m3 forward's 43 us, profiles/r5_28_nmse_epi_stats.txt)
+    constexpr int NBW = G::BM / (G::NW * RU);   // batches per wave
+    constexpr bool FAST_OK = G::NW * RU == 48 && RU % 3 == 0 && G::BM % 48 == 0;
+    const bool fast = FAST_OK && E == 3;
+    float pe[FAST_OK ? NBW : 1][3][2];
+#pragma unroll
+    for (int it = 0; it < (FAST_OK ? NBW : 1); ++it)
+#pragma unroll
+      for (int e3 = 0; e3 < 3; ++e3) pe[it][e3][0] = pe[it][e3][1] = 0.f;
+#pragma unroll
+    for (int it = 0; it < NBW; ++it) {
+      const int r0 = wave * RU + it * G::NW * RU;
       float2 l[RU], pv[RU];
       int ro[RU];
 #pragma unroll
@@ -951,9 +965,34 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
               (uint16_t)(e4m3_pack4(g0 * q8, g1 * q8, 0.f, 0.f) & 0xffffu);
           *reinterpret_cast<float2*>(ct + (r0 + q) * PITCH + c0) = make_float2(g0, g1);   // (for the dYt8 pass)
         }
+        if constexpr (FAST_OK) {
+          if (fast) {
+            pe[it][q % 3][0] += se;
+            pe[it][q % 3][1] += sp;
+            continue;
+          }
+        }
         se = wave_sum(se);
         sp = wave_sum(sp);
         if (lane == 0) rsum[r0 + q] = make_float2(se, sp);
+      }
+    }
+    if constexpr (FAST_OK) {
+      if (fast) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+          for (int it = 0; it < NBW; ++it)
+#pragma unroll
+            for (int e3 = 0; e3 < 3; ++e3) {
+              pe[it][e3][0] += __shfl_xor(pe[it][e3][0], m);
+              pe[it][e3][1] += __shfl_xor(pe[it][e3][1], m);
+            }
+        if (lane == 0)   // (batch it of every wave = chunk it of the tile)
+#pragma unroll
+          for (int it = 0; it < NBW; ++it)
+#pragma unroll
+            for (int e3 = 0; e3 < 3; ++e3) rsum[(it * G::NW + wave) * 3 + e3] = make_float2(pe[it][e3][0], pe[it][e3][1]);
       }
     }
     // column sums of dY over the tile: the waves' partials combined in a fixed order
@@ -990,10 +1029,18 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     for (int sl = tid; sl < (G::BM / CR) * E; sl += G::NT) {
       const int c = sl / E, e = sl % E;
       float2 o = make_float2(0.f, 0.f);
-      for (int b = 0; b < 16; ++b) {
-        const float2 v = rsum[c * CR + b * E + e];
-        o.x += v.x;
-        o.y += v.y;
+      if (fast) {
+        for (int w = 0; w < G::NW; ++w) {
+          const float2 v = rsum[(c * G::NW + w) * 3 + e];
+          o.x += v.x;
+          o.y += v.y;
+        }
+      } else {
+        for (int b = 0; b < 16; ++b) {
+          const float2 v = rsum[c * CR + b * E + e];
+          o.x += v.x;
+          o.y += v.y;
+        }
       }
       *reinterpret_cast<float2*>(na.part + (((size_t)((i0 + c * CR) / CR) * tiles_j + tj) * E + e) * 2) = o;
     }
