@@ -297,7 +297,9 @@ class HDCEStep:
         self.defer_loss = True   # (with bias_via_conv_slabs) loss finish hosted by the conv backward
         self.stage_hook = None  # optional callable(stage) between forward launches (stream forks)
         # the FC GEMMs: hand-written MFMA kernels (csrc/hip/gemm.hip; knobs.KNOBS.hand_gemm = "": hipBLASLt) and
-        # their tile configurations (forward, wgrad, dgrad; knobs.KNOBS.gemm_cfg).  Default: all three hand-written --
+        # their tile configurations (forward, wgrad, dgrad; knobs.KNOBS.gemm_cfg).  Default: all three hand-written,
+        # round 5: the producer-wave tiles (cfg 8, 7, 6) and the forward with the loss in its epilogue ("fwd", see
+        # knobs.py); the round-4 notes below are the history of that choice --
         #   forward  "fwdplain", cfg 6: 192 x 128 tiles on a 4-stage LDS ring (round 4: two tiles in flight behind
         #            the MFMAs; isolated 43.5 vs 50.2 us for the 3-stage cfg 1, in the step 0.4012 / 0.3999 vs
         #            0.4070 / 0.4068 ms, profiles/r4_16_*); 192 workgroups, so ~64 CUs stay free for the concurrent
