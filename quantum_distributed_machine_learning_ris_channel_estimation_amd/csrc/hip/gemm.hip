@@ -205,22 +205,6 @@ __device__ __forceinline__ void vm_wait(int tiles) {   // leave `tiles` tiles of
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// a workgroup barrier that waits for this wave's LDS operations only (__syncthreads() also waits for every global
-// load in flight): the loss epilogue's prefetched reads stay in flight across the fp32 tile's barriers
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// the loss epilogue's row batches (EPI_NMSE): RU rows per batch, NBW batches per wave
-template <class G>
-struct NmseGeo {
-  static constexpr int RU = G::BM % (G::NW * 12) == 0 ? 12 : G::BM % (G::NW * 9) == 0 ? 9 : 6;
-  static constexpr int NBW = G::BM / (G::NW * RU);
-  static constexpr int NRD = 4;   // prefetched label powers per lane and stream (B <= 256 in one round)
-};
-
 // LDS reads as inline asm: the compiler's own LDS wait counting turned conservative in this loop
 // (lgkmcnt(0) before every MFMA group, i.e. no read/MFMA overlap), so the K loop places its waits
 // itself -- the counts are exact because LDS reads return in issue order -- each followed by a
@@ -794,29 +778,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
 
   // ---------------------------------------------------------------- epilogue
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  // (EPI_NMSE) the loss epilogue's first global reads go out now, ahead of the fp32 tile's LDS round: the label
-  // powers of the (at most 2 per wave) streams the tile touches and the row offsets of the wave's first row batch
-  [[maybe_unused]] float2 pre_rd[2][NmseGeo<G>::NRD];
-  [[maybe_unused]] int pre_ro[NmseGeo<G>::RU];
-  if constexpr (EPI == EPI_NMSE) {
-    const NmseArgs& na = a.na;
-    const int ub = na.B * na.E, u_lo = i0 / ub, nst = ((i0 + G::BM - 1) / ub - u_lo + 1) * na.E;
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      const int q = wave + G::NW * qq < nst ? wave + G::NW * qq : 0;   // (branch-free; unused when past nst)
-      const int u = u_lo + q / na.E, e = q % na.E;
-#pragma unroll
-      for (int i = 0; i < NmseGeo<G>::NRD; ++i) {
-        const int b = lane + 64 * i < na.B ? lane + 64 * i : 0;
-        pre_rd[qq][i] = na.rowden[(u * na.B + b) * na.E + e];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NmseGeo<G>::RU; ++q) pre_ro[q] = na.rowoff[i0 + wave * NmseGeo<G>::RU + q];
-    lds_barrier();
-  } else {
-    __syncthreads();   // (every wave is done with the stage ring: it becomes the fp32 tile)
-  }
+  __syncthreads();   // (every wave is done with the stage ring: it becomes the fp32 tile)
   float* ct = reinterpret_cast<float*>(smem);
   constexpr int PITCH = G::PITCH;
   const float dq = a.deq ? a.deq[0] * (a.deq2 ? a.deq2[0] : a.deq[1]) : 1.f;
@@ -836,8 +798,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
           }
       }
     }
-    if constexpr (EPI == EPI_NMSE) lds_barrier();
-    else __syncthreads();
+    __syncthreads();
   }
   constexpr int VEC = G::BN / 64;   // columns per lane in a row pass (2 or 4)
   const int c0 = VEC * lane;
@@ -933,55 +894,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     const int ub = B * E;
     const int u_lo = i0 / ub, u_hi = (i0 + G::BM - 1) / ub;
     const int nst = (u_hi - u_lo + 1) * E;
-    constexpr int RU = NmseGeo<G>::RU, NBW = NmseGeo<G>::NBW, NRD = NmseGeo<G>::NRD;   // rows per batch, batches
-    static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
-    // every batch's row offsets (the first batch's were prefetched), then the first batch's labels: in flight
-    // while the coefficients below reduce; batch it + 1's labels are issued before batch it's math
-    int ro[NBW][RU];
-#pragma unroll
-    for (int q = 0; q < RU; ++q) ro[0][q] = pre_ro[q];
-#pragma unroll
-    for (int it = 1; it < NBW; ++it)
-#pragma unroll
-      for (int q = 0; q < RU; ++q) ro[it][q] = na.rowoff[i0 + wave * RU + it * G::NW * RU + q];
-    float2 l[2][RU], pv[2][RU];
-    auto issue = [&](int it, int buf) __attribute__((always_inline)) {
-#pragma unroll
-      for (int q = 0; q < RU; ++q) {
-        const size_t o = (size_t)ro[it][q] * N + j0 + c0;
-        l[buf][q] = *reinterpret_cast<const float2*>(na.label + o);
-        pv[buf][q] = na.perf ? *reinterpret_cast<const float2*>(na.perf + o) : make_float2(0.f, 0.f);
-      }
-    };
-    issue(0, 0);
-    // per-stream coefficients of the streams this tile touches (den_s summed over the stream's B rows in a fixed
-    // order: every block gets bitwise-identical values), from the prefetched powers
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      const int q = wave + G::NW * qq;
-      if (q < nst) {
-        const int u = u_lo + q / E, e = q % E;
-        float s = 0.f, sp = 0.f;
-#pragma unroll
-        for (int i = 0; i < NRD; ++i)
-          if (lane + 64 * i < B) {
-            s += pre_rd[qq][i].x;
-            sp += na.perf ? pre_rd[qq][i].y : 0.f;
-          }
-        for (int b = lane + 64 * NRD; b < B; b += 64) {
-          const float2 v = na.rowden[(u * B + b) * E + e];
-          s += v.x;
-          sp += na.perf ? v.y : 0.f;
-        }
-        s = wave_sum(s);
-        sp = wave_sum(sp);
-        if (lane == 0) {
-          red[q] = na.loss_scale * 2.f / ((float)S * s);
-          if (tj == 0 && u * ub >= i0) *reinterpret_cast<float2*>(na.dens + (e * U + u) * 2) = make_float2(s, sp);
-        }
-      }
-    }
-    for (int q = wave + 2 * G::NW; q < nst; q += G::NW) {   // (more streams than 2 per wave)
+    for (int q = wave; q < nst; q += G::NW) {
       const int u = u_lo + q / E, e = q % E;
       float s = 0.f, sp = 0.f;
       for (int b = lane; b < B; b += 64) {
@@ -996,15 +909,18 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
         if (tj == 0 && u * ub >= i0) *reinterpret_cast<float2*>(na.dens + (e * U + u) * 2) = make_float2(s, sp);
       }
     }
-    lds_barrier();   // (red; the first batch's labels stay in flight)
+    __syncthreads();
     float2* rsum = reinterpret_cast<float2*>(red + 64 + G::NW * 128);   // per-row (err^2, errperf^2)
     float cs0 = 0.f, cs1 = 0.f;
     const float q8 = na.dY8 != nullptr ? *na.qs8 : 0.f;
     float mx8 = 0.f;
+    constexpr int RU = G::BM % (G::NW * 12) == 0 ? 12 : G::BM % (G::NW * 9) == 0 ? 9 : 6;   // rows per batch
+    static_assert(G::BM % (G::NW * RU) == 0, "rows per wave");
     // FAST (3 experts, the waves' batch round = one 48-row chunk of 16 samples): a lane keeps its error sums per
     // (batch, expert) -- row q of a batch is expert q % 3 -- and the wave reduces them once, all side by side,
     // after the rows; else every row's sums go through the wave on their own (2 dependent 6-step lane-exchange
     // chains per row: 20 of the e4m3 forward's 43 us, profiles/r5_28_nmse_epi_stats.txt)
+    constexpr int NBW = G::BM / (G::NW * RU);   // batches per wave
     constexpr bool FAST_OK = G::NW * RU == 48 && RU % 3 == 0 && G::BM % 48 == 0;
     const bool fast = FAST_OK && E == 3;
     float pe[FAST_OK ? NBW : 1][3][2];
@@ -1015,8 +931,16 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
 #pragma unroll
     for (int it = 0; it < NBW; ++it) {
       const int r0 = wave * RU + it * G::NW * RU;
-      if (it + 1 < NBW) issue(it + 1 < NBW ? it + 1 : 0, (it + 1) % 2);
-      const int bf = it % 2;
+      float2 l[RU], pv[RU];
+      int ro[RU];
+#pragma unroll
+      for (int q = 0; q < RU; ++q) ro[q] = na.rowoff[i0 + r0 + q];
+#pragma unroll
+      for (int q = 0; q < RU; ++q) {
+        const size_t o = (size_t)ro[q] * N + j0 + c0;
+        l[q] = *reinterpret_cast<const float2*>(na.label + o);
+        pv[q] = na.perf ? *reinterpret_cast<const float2*>(na.perf + o) : make_float2(0.f, 0.f);
+      }
 #pragma unroll
       for (int q = 0; q < RU; ++q) {
         const int row = i0 + r0 + q;
@@ -1024,10 +948,10 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
         y.x += bv0;
         y.y += bv1;
         const float coef = red[(row / ub - u_lo) * E + row % E];
-        const float d0 = y.x - l[bf][q].x, d1 = y.y - l[bf][q].y;
+        const float d0 = y.x - l[q].x, d1 = y.y - l[q].y;
         float se = d0 * d0 + d1 * d1, sp = 0.f;
         if (na.perf) {
-          const float p0 = y.x - pv[bf][q].x, p1 = y.y - pv[bf][q].y;
+          const float p0 = y.x - pv[q].x, p1 = y.y - pv[q].y;
           sp = p0 * p0 + p1 * p1;
         }
         const float g0 = coef * d0, g1 = coef * d1;

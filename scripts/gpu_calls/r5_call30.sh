@@ -1,7 +1,9 @@
 #!/bin/bash
 # round-5 GPU call 30: the loss epilogue's global reads prefetched (label powers + first batch's row offsets before
 # the fp32 tile's LDS round, LDS-only barriers; every batch's offsets up front, labels one batch ahead): tests,
-# epilogue probe, fp8 and bf16 step A/B against the previous library
+# epilogue probe, fp8 and bf16 step A/B against the previous library.
+# RESULT: the direct-A tile (cfg 5) faulted in test_gemm_nmse_epilogue_matches_fp32 (profiles/r5_30_prefetch_fault_pytest.log);
+# the change was reverted (gemm.hip as of the call-29 tree) -- cause not found by inspection
 set -o pipefail
 cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out
