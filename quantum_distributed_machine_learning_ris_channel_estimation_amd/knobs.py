@@ -17,13 +17,13 @@ class Knobs:
     # (csrc/hip/gemm.hip; the rest on hipBLASLt), and their tile configurations (forward, wgrad, dgrad).
     # 8,7,6 (round 5) = the producer-wave tiles: isolated 33.0 / 38.8 / 35.1 us against 40.3 / 42.2 / 35.8 for round
     # 4's 6,1,2; in the step 0.3958-0.3967 against 0.3992-0.4025 ms (profiles/r5_02_gemm_probe.txt, r5_03_ab.txt)
-    # "fwd" instead of "fwdplain": the forward with the loss in its epilogue (gemm.hip EPI_NMSE) instead of the plain
-    # forward + the one-pass NMSE kernel -- 0.3721 / 0.3726 against 0.3745 / 0.3737 ms since the epilogue reduces
-    # its error sums per (batch, expert) rather than per row (profiles/r5_29_nmse_epilogue_ab.txt).  Not the default:
-    # with it, the plans that split the HDCE forward around the QSC fork (qsc_start="conv", fc_adam_next) end with
-    # QSC weights 3e-3 off the serial step in test_multistream_graph_matches_serial_eager (profiles/r5_32_*; cause
-    # open), while fwdplain passes them all
-    hand_gemm: str = "fwdplain,wgrad,dgrad"
+    # "fwd" (round 5): the forward with the loss in its epilogue (gemm.hip EPI_NMSE) where it tiles, else the plain
+    # hand-written forward + the one-pass NMSE kernel ("fwdplain") -- 0.3721 / 0.3726 against 0.3745 / 0.3737 ms
+    # since the epilogue reduces its error sums per (batch, expert) rather than per row
+    # (profiles/r5_29_nmse_epilogue_ab.txt; rounds 3-4 measured it 1.5-4 % slower with the per-row reductions).
+    # (Shapes the epilogue does not tile used to fall back to hipBLASLt, which broke the split-forward plans'
+    # equality with the serial step at the tests' batch 32: profiles/r5_32_*, r5_41_map.txt)
+    hand_gemm: str = "fwd,wgrad,dgrad"
     gemm_cfg: str = "8,7,6"
     # fp8 estimator: the hand-written e4m3 forward (else torch._scaled_mm + the NMSE kernel), e4m3 FC gradients
     hand_fp8: bool = True

@@ -621,10 +621,12 @@ class HDCEStep:
             Y = torch._scaled_mm(self.conv.h3_8, m._shadow_w8.t(), scale_a=sc[0], scale_b=sc[1], bias=b,
                                  out_dtype=dt)
             m.fp8_scales.update()
-        elif "fwdplain" in self.hand_gemm and dt == torch.bfloat16 and A.dtype == dt and W.dtype == dt \
-                and b is not None and b.dtype == dt and self._plain_fwd_ok(A, W):
+        elif ("fwdplain" in self.hand_gemm or "fwd" in self.hand_gemm) and dt == torch.bfloat16 and A.dtype == dt \
+                and W.dtype == dt and b is not None and b.dtype == dt and self._plain_fwd_ok(A, W):
             # the hand-written forward GEMM with only the bias in its epilogue; the loss runs as the separate
-            # one-pass NMSE kernel below, as after a library GEMM
+            # one-pass NMSE kernel below, as after a library GEMM.  ("fwd" too, for shapes the loss epilogue does not
+            # tile, e.g. M % 128 != 0 at small batches: its hipBLASLt fallback broke the split-forward plans'
+            # equality with the serial step -- profiles/r5_41_map.txt)
             from ..ops.fc import gemm_fwd
             if getattr(self, "_Y_buf", None) is None or self._Y_buf.shape != (A.shape[0], W.shape[0]):
                 self._Y_buf = torch.empty(A.shape[0], W.shape[0], device=A.device, dtype=dt)
