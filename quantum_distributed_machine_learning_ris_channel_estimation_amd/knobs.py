@@ -17,13 +17,13 @@ class Knobs:
     # (csrc/hip/gemm.hip; the rest on hipBLASLt), and their tile configurations (forward, wgrad, dgrad).
     # 8,7,6 (round 5) = the producer-wave tiles: isolated 33.0 / 38.8 / 35.1 us against 40.3 / 42.2 / 35.8 for round
     # 4's 6,1,2; in the step 0.3958-0.3967 against 0.3992-0.4025 ms (profiles/r5_02_gemm_probe.txt, r5_03_ab.txt)
-    # "fwd" (round 5): the forward with the loss in its epilogue (gemm.hip EPI_NMSE) where it tiles, else the plain
-    # hand-written forward + the one-pass NMSE kernel ("fwdplain") -- 0.3721 / 0.3726 against 0.3745 / 0.3737 ms
-    # since the epilogue reduces its error sums per (batch, expert) rather than per row
-    # (profiles/r5_29_nmse_epilogue_ab.txt; rounds 3-4 measured it 1.5-4 % slower with the per-row reductions).
-    # (Shapes the epilogue does not tile used to fall back to hipBLASLt, which broke the split-forward plans'
-    # equality with the serial step at the tests' batch 32: profiles/r5_32_*, r5_41_map.txt)
-    hand_gemm: str = "fwd,wgrad,dgrad"
+    # "fwd" instead of "fwdplain": the forward with the loss in its epilogue (gemm.hip EPI_NMSE) where it tiles, else
+    # the plain hand-written forward + the one-pass NMSE kernel.  Since the epilogue reduces its error sums per (batch,
+    # expert) rather than per row the two are level: 0.3721 / 0.3726 against 0.3745 / 0.3737 ms on one box, 0.3842-
+    # 0.3847 against 0.3839-0.3845 on another (profiles/r5_29_nmse_epilogue_ab.txt, r5_42_fused_fwd_ab.txt) -- the
+    # plain forward stays.  (Shapes the epilogue does not tile fell back to hipBLASLt, whose forward breaks the
+    # split-forward plans' equality with the serial step: profiles/r5_32_*, r5_41_map.txt, r5_42_library_fwd.log)
+    hand_gemm: str = "fwdplain,wgrad,dgrad"
     gemm_cfg: str = "8,7,6"
     # fp8 estimator: the hand-written e4m3 forward (else torch._scaled_mm + the NMSE kernel), e4m3 FC gradients
     hand_fp8: bool = True
