@@ -1121,6 +1121,11 @@ using FwdP = Geo<6, 4, 2, 2, KC, KC, 4, 0, 0, 1, 4>;    // fwd 192 x 128, 2 x 2 
 using FwdP3 = Geo<6, 4, 2, 2, KC, KC, 3, 0, 0, 1, 4>;   // the same, 3 stages
 using FwdQ = Geo<9, 2, 1, 4, KC, KC, 4, 0, 0, 1, 4>;    // fwd 144 x 128 (256 tiles), 1 x 4 compute waves (144 x 32)
 using FwdR = Geo<6, 2, 2, 4, KC, KC, 4, 0, 0, 1, 4>;    // fwd 192 x 128, 2 x 4 compute waves (the cfg 6 tile) + 4
+// FwdQ on a 3-stage ring (cfg 11): 102 KB of LDS instead of 136, so a workgroup fits beside one of the QSC preprocess
+// forward's (54 KB) -- with the 4-stage ring the FC forward can wait ~14 us for that kernel to leave the CUs
+// (profiles/r5_33_step_timeline.md).  Measured slower: 49.0 against 37.4 us alone, the step 0.4009-0.4020 against
+// 0.3974-0.3985 ms (profiles/r5_43_*): it starts at once but runs beside the preprocess kernel at 74 us
+using FwdQ3 = Geo<9, 2, 1, 4, KC, KC, 3, 0, 0, 1, 4>;
 using WgrP = Geo<8, 4, 2, 2, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 256 x 128 (256 tiles), 2 x 2 compute waves (128 x 64)
 using WgrQ = Geo<4, 8, 2, 2, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 2 compute waves (64 x 128)
 using WgrR = Geo<4, 4, 2, 4, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 4 compute waves (the cfg 1 tile) + 4
@@ -1150,6 +1155,7 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (cfg == 2) return M % FwdC::BM == 0 && K % (2 * BK) == 0;
   if (cfg == 1 || cfg == 6 || cfg == 7 || cfg == 9 || cfg == 10) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
   if (cfg == 8) return M % FwdQ::BM == 0 && N % FwdQ::BN == 0;
+  if (cfg == 11) return M % FwdQ3::BM == 0 && N % FwdQ3::BN == 0;
   if (cfg == 3 || cfg == 4) return M % FwdD::BM == 0 && N % FwdD::BN == 0;
   if (cfg == 5) return M % FwdDA::BM == 0 && N % FwdDA::BN == 0 && (K / BK) % 2 == 0;
   return 0;
@@ -1166,6 +1172,7 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   if (cfg == 6) return launch<FwdB4, EPI_BF16, 1, 4>(a, st);
   if (cfg == 7) return launch<FwdP, EPI_BF16, 1, 4>(a, st);
   if (cfg == 8) return launch<FwdQ, EPI_BF16, 4, 8>(a, st);
+  if (cfg == 11) return launch<FwdQ3, EPI_BF16, 4, 8>(a, st);
   if (cfg == 9) return launch<FwdP3, EPI_BF16, 1, 4>(a, st);
   if (cfg == 10) return launch<FwdR, EPI_BF16, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_BF16, 1, 4>(a, st);
@@ -1196,6 +1203,7 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   if (cfg == 6) return launch<FwdB4, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 7) return launch<FwdP, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 8) return launch<FwdQ, EPI_NMSE, 4, 8>(a, st);
+  if (cfg == 11) return launch<FwdQ3, EPI_NMSE, 4, 8>(a, st);
   if (cfg == 9) return launch<FwdP3, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 10) return launch<FwdR, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_NMSE, 1, 4>(a, st);
