@@ -897,7 +897,22 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     for (int q = wave; q < nst; q += G::NW) {
       const int u = u_lo + q / E, e = q % E;
       float s = 0.f, sp = 0.f;
-      for (int b = lane; b < B; b += 64) {
+      int b0 = lane;
+      if constexpr (!G::ADIR) {
+        // the first 4 rows per lane in flight at once (the rolled loop waited one round trip per 64 rows); the same
+        // additions in the same order.  (Not on the direct-A tile: r5_30's fault there is unexplained.)
+        float2 rv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[i] = na.rowden[(u * B + (lane + 64 * i < B ? lane + 64 * i : 0)) * E + e];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (lane + 64 * i < B) {
+            s += rv[i].x;
+            sp += na.perf ? rv[i].y : 0.f;
+          }
+        b0 = lane + 256;
+      }
+      for (int b = b0; b < B; b += 64) {
         const float2 v = na.rowden[(u * B + b) * E + e];
         s += v.x;
         sp += na.perf ? v.y : 0.f;
@@ -928,13 +943,29 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     for (int it = 0; it < (FAST_OK ? NBW : 1); ++it)
 #pragma unroll
       for (int e3 = 0; e3 < 3; ++e3) pe[it][e3][0] = pe[it][e3][1] = 0.f;
+    // (not on the direct-A tile) the next batch's row offsets are loaded before this batch's labels: one round trip
+    // per batch instead of two
+    [[maybe_unused]] int ro_nx[RU];
+    if constexpr (!G::ADIR) {
+#pragma unroll
+      for (int q = 0; q < RU; ++q) ro_nx[q] = na.rowoff[i0 + wave * RU + q];
+    }
 #pragma unroll
     for (int it = 0; it < NBW; ++it) {
       const int r0 = wave * RU + it * G::NW * RU;
       float2 l[RU], pv[RU];
       int ro[RU];
+      if constexpr (!G::ADIR) {
 #pragma unroll
-      for (int q = 0; q < RU; ++q) ro[q] = na.rowoff[i0 + r0 + q];
+        for (int q = 0; q < RU; ++q) ro[q] = ro_nx[q];
+        if (it + 1 < NBW) {
+#pragma unroll
+          for (int q = 0; q < RU; ++q) ro_nx[q] = na.rowoff[i0 + r0 + G::NW * RU + q];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < RU; ++q) ro[q] = na.rowoff[i0 + r0 + q];
+      }
 #pragma unroll
       for (int q = 0; q < RU; ++q) {
         const size_t o = (size_t)ro[q] * N + j0 + c0;
