@@ -897,22 +897,7 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     for (int q = wave; q < nst; q += G::NW) {
       const int u = u_lo + q / E, e = q % E;
       float s = 0.f, sp = 0.f;
-      int b0 = lane;
-      if constexpr (!G::ADIR) {
-        // the first 4 rows per lane in flight at once (the rolled loop waited one round trip per 64 rows); the same
-        // additions in the same order.  (Not on the direct-A tile: r5_30's fault there is unexplained.)
-        float2 rv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rv[i] = na.rowden[(u * B + (lane + 64 * i < B ? lane + 64 * i : 0)) * E + e];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (lane + 64 * i < B) {
-            s += rv[i].x;
-            sp += na.perf ? rv[i].y : 0.f;
-          }
-        b0 = lane + 256;
-      }
-      for (int b = b0; b < B; b += 64) {
+      for (int b = lane; b < B; b += 64) {
         const float2 v = na.rowden[(u * B + b) * E + e];
         s += v.x;
         sp += na.perf ? v.y : 0.f;
@@ -943,29 +928,13 @@ __global__ void __launch_bounds__(G::NT, 1) gemm_kernel(Args a) {
     for (int it = 0; it < (FAST_OK ? NBW : 1); ++it)
 #pragma unroll
       for (int e3 = 0; e3 < 3; ++e3) pe[it][e3][0] = pe[it][e3][1] = 0.f;
-    // (not on the direct-A tile) the next batch's row offsets are loaded before this batch's labels: one round trip
-    // per batch instead of two
-    [[maybe_unused]] int ro_nx[RU];
-    if constexpr (!G::ADIR) {
-#pragma unroll
-      for (int q = 0; q < RU; ++q) ro_nx[q] = na.rowoff[i0 + wave * RU + q];
-    }
 #pragma unroll
     for (int it = 0; it < NBW; ++it) {
       const int r0 = wave * RU + it * G::NW * RU;
       float2 l[RU], pv[RU];
       int ro[RU];
-      if constexpr (!G::ADIR) {
 #pragma unroll
-        for (int q = 0; q < RU; ++q) ro[q] = ro_nx[q];
-        if (it + 1 < NBW) {
-#pragma unroll
-          for (int q = 0; q < RU; ++q) ro_nx[q] = na.rowoff[i0 + r0 + G::NW * RU + q];
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < RU; ++q) ro[q] = na.rowoff[i0 + r0 + q];
-      }
+      for (int q = 0; q < RU; ++q) ro[q] = na.rowoff[i0 + r0 + q];
 #pragma unroll
       for (int q = 0; q < RU; ++q) {
         const size_t o = (size_t)ro[q] * N + j0 + c0;
@@ -1152,11 +1121,6 @@ using FwdP = Geo<6, 4, 2, 2, KC, KC, 4, 0, 0, 1, 4>;    // fwd 192 x 128, 2 x 2 
 using FwdP3 = Geo<6, 4, 2, 2, KC, KC, 3, 0, 0, 1, 4>;   // the same, 3 stages
 using FwdQ = Geo<9, 2, 1, 4, KC, KC, 4, 0, 0, 1, 4>;    // fwd 144 x 128 (256 tiles), 1 x 4 compute waves (144 x 32)
 using FwdR = Geo<6, 2, 2, 4, KC, KC, 4, 0, 0, 1, 4>;    // fwd 192 x 128, 2 x 4 compute waves (the cfg 6 tile) + 4
-// FwdQ on a 3-stage ring (cfg 11): 102 KB of LDS instead of 136, so a workgroup fits beside one of the QSC preprocess
-// forward's (54 KB) -- with the 4-stage ring the FC forward can wait ~14 us for that kernel to leave the CUs
-// (profiles/r5_33_step_timeline.md).  Measured slower: 49.0 against 37.4 us alone, the step 0.4009-0.4020 against
-// 0.3974-0.3985 ms (profiles/r5_43_*): it starts at once but runs beside the preprocess kernel at 74 us
-using FwdQ3 = Geo<9, 2, 1, 4, KC, KC, 3, 0, 0, 1, 4>;
 using WgrP = Geo<8, 4, 2, 2, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 256 x 128 (256 tiles), 2 x 2 compute waves (128 x 64)
 using WgrQ = Geo<4, 8, 2, 2, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 2 compute waves (64 x 128)
 using WgrR = Geo<4, 4, 2, 4, MC, MC, 3, 0, 0, 1, 4>;    // wgrad 128 x 256, 2 x 4 compute waves (the cfg 1 tile) + 4
@@ -1186,7 +1150,6 @@ QD_API int qd_gemm_fwd_ok(int M, int N, int K, int cfg) {
   if (cfg == 2) return M % FwdC::BM == 0 && K % (2 * BK) == 0;
   if (cfg == 1 || cfg == 6 || cfg == 7 || cfg == 9 || cfg == 10) return M % FwdB::BM == 0 && N % FwdB::BN == 0;
   if (cfg == 8) return M % FwdQ::BM == 0 && N % FwdQ::BN == 0;
-  if (cfg == 11) return M % FwdQ3::BM == 0 && N % FwdQ3::BN == 0;
   if (cfg == 3 || cfg == 4) return M % FwdD::BM == 0 && N % FwdD::BN == 0;
   if (cfg == 5) return M % FwdDA::BM == 0 && N % FwdDA::BN == 0 && (K / BK) % 2 == 0;
   return 0;
@@ -1203,7 +1166,6 @@ QD_API int qd_gemm_fwd_bias(const uint16_t* A, const uint16_t* W, const uint16_t
   if (cfg == 6) return launch<FwdB4, EPI_BF16, 1, 4>(a, st);
   if (cfg == 7) return launch<FwdP, EPI_BF16, 1, 4>(a, st);
   if (cfg == 8) return launch<FwdQ, EPI_BF16, 4, 8>(a, st);
-  if (cfg == 11) return launch<FwdQ3, EPI_BF16, 4, 8>(a, st);
   if (cfg == 9) return launch<FwdP3, EPI_BF16, 1, 4>(a, st);
   if (cfg == 10) return launch<FwdR, EPI_BF16, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_BF16, 1, 4>(a, st);
@@ -1234,7 +1196,6 @@ QD_API int qd_gemm_fwd_nmse(const uint16_t* A, const uint16_t* W, const uint16_t
   if (cfg == 6) return launch<FwdB4, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 7) return launch<FwdP, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 8) return launch<FwdQ, EPI_NMSE, 4, 8>(a, st);
-  if (cfg == 11) return launch<FwdQ3, EPI_NMSE, 4, 8>(a, st);
   if (cfg == 9) return launch<FwdP3, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 10) return launch<FwdR, EPI_NMSE, 1, 4>(a, st);
   if (cfg == 3) return launch<FwdD, EPI_NMSE, 1, 4>(a, st);

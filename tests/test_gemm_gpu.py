@@ -15,7 +15,7 @@ def _rel(a, b):
     return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-30))
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("M,N,K", [(576, 256, 192), (576, 256, 256), (2304, 2048, 4096)])
 def test_gemm_fwd_matches_fp32(cuda, cfg, M, N, K):
     if not gemm_fwd_ok(M, N, K, cfg):
@@ -98,7 +98,7 @@ def _rows(E, U, B, N_store, cols, device):
     return L, P, rowoff, rowden, lab, per, stream
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 7, 8, 10, 11])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 5, 6, 7, 8, 10])
 @pytest.mark.parametrize("E,U,B,N,K", [(3, 3, 64, 256, 320), (3, 3, 64, 256, 384), (3, 3, 256, 2048, 4096)])
 def test_gemm_nmse_epilogue_matches_fp32(cuda, cfg, E, U, B, N, K):
     """Forward GEMM with the HDCE loss epilogue + finish: loss, loss_perf, dY, bias gradient, NaN flag."""
