@@ -170,6 +170,11 @@ __device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Of
   if (threadIdx.x < n) ws[S_WEND + n * wl_stride(F) + threadIdx.x] = flat[o.bl + threadIdx.x];
 }
 
+// a wave-uniform value from the first active lane, in an SGPR (conv1's weights: see conv1_half)
+__device__ __forceinline__ float uniform(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
 // conv1 pre-activations (+bias) of one ROW of pool window `win` (hw = 0 top, 1 bottom): all 16
 // channels x 2 positions.  The whole wave walks the channels in lockstep, so every weight is
 // wave-uniform: LDS broadcast reads of the workgroup's staged copy (w1g = W1 transposed [k][co], b1g).
@@ -180,7 +185,7 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
   const int qy = win / G::W2, qx = win % G::W2;
 #pragma unroll
   for (int co = 0; co < C1; ++co) {
-    const float b = b1g[co];
+    const float b = uniform(b1g[co]);
     acc[co][0] = b;
     acc[co][1] = b;
   }
@@ -195,7 +200,8 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
     const float4* wk = reinterpret_cast<const float4*>(w1g + k * C1);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 w = wk[q];
+      const float4 wv = wk[q];
+      const float4 w = make_float4(uniform(wv.x), uniform(wv.y), uniform(wv.z), uniform(wv.w));
       acc[4 * q][0] += w.x * p0;
       acc[4 * q][1] += w.x * p1;
       acc[4 * q + 1][0] += w.y * p0;

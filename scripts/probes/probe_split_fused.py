@@ -104,6 +104,32 @@ def main():
                 torch.cuda.synchronize()
                 print(f"   {lab}: eager recompute vs its step: p1s {d(run_p1, h.p1s):.3e} angles {d(run_ang, h.angles):.3e}",
                       flush=True)
+                per = (run_p1 - h.p1s).abs().amax(dim=1)
+                bad = torch.nonzero(per > 0).flatten().tolist()
+                if bad:   # which samples, their workgroup (4 waves each) and its XCD (block % 8)
+                    print(f"   {lab}: {len(bad)} of {per.numel()} samples differ; first: "
+                          f"{[(b, b // 4, (b // 4) % 8) for b in bad[:24]]}", flush=True)
+                    xcds = torch.tensor([(b // 4) % 8 for b in bad]).bincount(minlength=8).tolist()
+                    print(f"   {lab}: differing samples per XCD of their workgroup: {xcds}", flush=True)
+                    rows = torch.tensor(bad, device=dev)
+                    dif = (run_p1[rows] - h.p1s[rows]).abs() > 0
+                    print(f"   {lab}: per differing sample, entries that differ: {dif.sum(1).tolist()[:24]} of "
+                          f"{run_p1.shape[1]}; step min p1 {float(run_p1.min()):.3e}", flush=True)
+                    for b in bad[:3]:   # the differing entries (window, channel): step value / recompute value
+                        ent = torch.nonzero((run_p1[b] - h.p1s[b]).abs() > 0).flatten().tolist()
+                        print(f"   {lab}: sample {b}: " + ", ".join(
+                            f"(w{e // 16} c{e % 16}) {float(run_p1[b, e]):.4f}/{float(h.p1s[b, e]):.4f}" for e in ent),
+                            flush=True)
+                    # the same forward from the POST-step weights: do the differing samples match that instead?
+                    pre_p1 = h.p1s.clone()
+                    h._fwd_mfma(tr.gat.xq, tr.qspace.flat, nat.stream_ptr(dev))
+                    torch.cuda.synchronize()
+                    per2 = (run_p1 - h.p1s).abs().amax(dim=1)
+                    post_ok = [b for b in bad if float(per2[b]) == 0.0]
+                    print(f"   {lab}: of the differing samples, {len(post_ok)} match a forward from the post-step "
+                          f"weights; samples that differ from that one: {int((per2 > 0).sum())}", flush=True)
+                    # the previous step's batch (the cursor one batch back) is not at hand; the c1 codes are
+                    h.p1s.copy_(pre_p1)
         if s == 0:   # every QSC buffer of the first step: which one differs first
             for owner in ("cstep", "cstep.hip"):
                 ra, da = ref, dag
