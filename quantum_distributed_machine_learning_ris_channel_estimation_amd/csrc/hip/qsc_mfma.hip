@@ -177,7 +177,11 @@ __device__ __forceinline__ float uniform(float v) {
 
 // conv1 pre-activations (+bias) of one ROW of pool window `win` (hw = 0 top, 1 bottom): all 16
 // channels x 2 positions.  The whole wave walks the channels in lockstep, so every weight is
-// wave-uniform: LDS broadcast reads of the workgroup's staged copy (w1g = W1 transposed [k][co], b1g).
+// wave-uniform: LDS broadcast reads of the workgroup's staged copy (w1g = W1 transposed [k][co], b1g),
+// each value taken from lane 0 into an SGPR (uniform()).  With the per-lane copies, under concurrent work
+// in the graph plans lanes 48-63 used a wrong channel-5 weight in 20-30 of 288 samples; lane 0's copy
+// removes it (docs/CONCURRENCY.md, profiles/r5_55_entries.txt, r5_56_uniform_probe.txt); same registers and
+// step time.
 template <int H, int W>
 __device__ __forceinline__ void conv1_half(const float* act, const float* __restrict__ w1g,
                                            const float* __restrict__ b1g, int win, int hw, float (&acc)[16][2]) {
