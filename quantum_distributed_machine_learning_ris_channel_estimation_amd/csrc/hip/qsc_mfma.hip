@@ -197,7 +197,7 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
   // ds_read_b128 of the transposed copy [k][co] and its two input values two LDS reads, consumed right
   // away (unrolled, the compiler hoisted all 288 weights into VGPRs and halved the occupancy).  3 k per
   // iteration since the weights live in SGPRs: 232 VGPRs (2 waves / SIMD as with 2), step 0.3841-0.3856 vs
-  // 0.3856-0.3867 ms (profiles/r5_62_ab.txt); fully unrolled it spills
+  // 0.3856-0.3867 ms on one box (profiles/r5_62_ab.txt), level on another (r5_64_ab.txt); fully unrolled it spills
 #pragma unroll 3
   for (int k = 0; k < K1; ++k) {
     const int ci = k / 9, t = k % 9;
