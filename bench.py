@@ -58,6 +58,14 @@ def main() -> int:
                     help="estimator compute dtype (fp8: e4m3 FC forward GEMM, bf16 convs/backward)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-quantumnat", action="store_true")
+    ap.add_argument("--gradient-pruning", action="store_true",
+                    help="the QSC's on-chip gradient pruning (|g| > 0.1 mask fused into its AdamW, reference "
+                         "apply_gradient_pruning E:205-228; FlagshipConfig.use_gradient_pruning): BASELINE config 5's "
+                         "\"on-chip QNN\"")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = batch_size_DML per stream on EVERY rank (each rank its own data); strong = "
+                         "the reference's DataParallel semantics (R:144-148): ONE global batch of batch_size_DML per "
+                         "stream per step, cut into N contiguous parts (FlagshipConfig.scaling)")
     ap.add_argument("--split-graphs", action="store_true", help="the DP plan (5 graphs around the collectives) even at 1 GPU")
     ap.add_argument("--steps-per-graph", type=int, default=10,
                     help="training steps captured per graph replay at world 1 (each gathers its own batch)")
@@ -161,7 +169,7 @@ def main() -> int:
             KNOBS.f8_producers = bool(args.f8_producers)
         if args.qsim_mfma12 is not None:
             KNOBS.qsim_mfma12 = bool(args.qsim_mfma12)
-    ctx = init_distributed("auto", timeout_s=int(os.environ.get("QDML_PG_TIMEOUT", "600")))
+    ctx = init_distributed("auto")   # (rendezvous + failure-detector timeout: QDML_PG_TIMEOUT, default 600 s)
     if ctx.world != args.gpus:
         print(f"error: --gpus {args.gpus} but the process group has {ctx.world} rank(s)", file=sys.stderr)
         return 2
@@ -171,7 +179,8 @@ def main() -> int:
         plan, qsc = cand
         cfg = FlagshipConfig(pilot_num=args.pilot, n_qubits=args.qubits, n_layers=args.layers, batch=args.batch,
                              data_len=args.data_len, dtype=args.dtype, hip_graphs=not args.no_graphs,
-                             use_quantumnat=not args.no_quantumnat, split_graphs=args.split_graphs or ctx.forced,
+                             use_quantumnat=not args.no_quantumnat, use_gradient_pruning=args.gradient_pruning,
+                             scaling=args.scaling, split_graphs=args.split_graphs or ctx.forced,
                              stream_mode=args.stream_mode, qsc_start=args.qsc_start,
                              steps_per_graph=args.steps_per_graph,
                              dp_plan=plan, dp_one_graph=og, dp_qsc=qsc, lead_in=args.lead_in,
@@ -228,10 +237,10 @@ def main() -> int:
             select[key] = round(el / args.select_steps * 1e3, 4)
             if tr is None or el < best:
                 if tr is not None:
-                    del tr
+                    tr.close()   # (its graphs released now, after a device sync: not by a later GC)
                 tr, tr_cand, best = t, cand, el
             else:
-                del t
+                t.close()
         else:
             tr, tr_cand = t, cand
     cfg = tr.cfg
@@ -293,7 +302,7 @@ def main() -> int:
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "host_ms_per_step": round(host / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": cfg.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (DeepMIMO-shaped geometric channels, HBM-resident), random-init weights",
@@ -302,6 +311,7 @@ def main() -> int:
                      f"estimator (HDCE: 3x Conv_P{args.pilot} + FC_P{args.pilot})",
                 "global_batch": tr.samples_per_step * n,
                 "per_gpu_batch": tr.samples_per_step,
+                "per_rank_stream_batch": tr.B,
                 "streams": tr.S,
                 "batch_size_DML": args.batch,
                 "seq_len": None,
@@ -317,6 +327,7 @@ def main() -> int:
                 "dist_backend": ctx.backend,
                 "steps_per_graph": tr._k(),
                 "quantumnat": cfg.use_quantumnat,
+                "gradient_pruning": cfg.use_gradient_pruning,
                 # which kernels the timed step ran: the FC forward (hand_plain / hand / hand_f8 / library), the
                 # FC gradients, the 8-qubit circuit forward on the matrix cores
                 "fc_forward": getattr(tr.hstep, "fc_path", None),
@@ -348,6 +359,7 @@ def main() -> int:
                 f.write(line + "\n")
         else:
             print(line, flush=True)
+    tr.close()
     shutdown()
     return 0
 

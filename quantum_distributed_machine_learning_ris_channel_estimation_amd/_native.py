@@ -147,7 +147,11 @@ def hip_lib(build_if_missing: bool = True) -> ctypes.CDLL:
             if not build_if_missing:
                 raise NativeUnavailable(f"{HIP_LIB} missing; run __graft_entry__.build()")
             build_hip(verbose=False)
-        _hip = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL)
+        lib = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL)
+        # native frames on a host crash (csrc/hip/runtime.hip qd_install_crash_handler), ahead of faulthandler
+        if os.environ.get("QDML_CRASH_HANDLER", "1") == "1" and hasattr(lib, "qd_install_crash_handler"):
+            lib.qd_install_crash_handler()
+        _hip = lib
     return _hip
 
 

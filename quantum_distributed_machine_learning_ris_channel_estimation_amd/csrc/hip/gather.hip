@@ -22,17 +22,23 @@
 namespace qd {
 namespace gather {
 
+// Strong scaling (the reference's DataParallel semantics, R:144-148: ONE global batch of Bg rows per stream,
+// cut into contiguous parts): this rank's part starts `off` rows into the global batch, the cursor advances by
+// `adv` = Bg, and -- with `scale` set (den_scale_kernel) -- the per-row label powers are scaled so that the NMSE
+// kernels' per-stream sums over this rank's rows ARE the global batch's denominators.  Weak: off 0, adv B.
 __global__ void __launch_bounds__(256) gather_step_kernel(const long* __restrict__ idx, const float* __restrict__ Yp,
                                                           long yp_stream_stride, float* __restrict__ x1,
                                                           float* __restrict__ xq, int* __restrict__ rowoff,
                                                           long lab_stream_rows, int E, int U, int B, int plane,
                                                           int* __restrict__ cursor, unsigned int* __restrict__ done,
                                                           long nperm, const float* __restrict__ rowpow_l,
-                                                          const float* __restrict__ rowpow_p, float2* __restrict__ rowden) {
+                                                          const float* __restrict__ rowpow_p, float2* __restrict__ rowden,
+                                                          int off, int adv, const float2* __restrict__ scale) {
   const int lane = threadIdx.x & 63;
   const int S = E * U;
   int c = cursor ? *cursor : 0;
-  if (c < 0 || c + B > nperm) c = 0;   // (never out of the permutation, whatever the host did)
+  if (c < 0 || c + adv > nperm) c = 0;   // (never out of the permutation, whatever the host did)
+  c += off;
   // grid-stride over (stream, sample) waves: a capped grid keeps the cursor protocol's
   // same-address atomics (one per workgroup, serialised in L2) few
   for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < S * B; wid += gridDim.x * 4) {
@@ -50,7 +56,13 @@ __global__ void __launch_bounds__(256) gather_step_kernel(const long* __restrict
     if (lane == 0 && rowoff) rowoff[(size_t)(u * B + b) * E + e] = (int)(s * lab_stream_rows + n);
     if (lane == 1 && rowden) {   // per-row label / perfect-channel power for the NMSE kernel's denominators
       const long ro = s * lab_stream_rows + n;
-      rowden[(size_t)(u * B + b) * E + e] = make_float2(rowpow_l[ro], rowpow_p ? rowpow_p[ro] : 0.f);
+      float2 d = make_float2(rowpow_l[ro], rowpow_p ? rowpow_p[ro] : 0.f);
+      if (scale) {
+        const float2 f = scale[s];
+        d.x *= f.x;
+        d.y *= f.y;
+      }
+      rowden[(size_t)(u * B + b) * E + e] = d;
     }
   }
   if (cursor == nullptr || done == nullptr) return;   // (read-only cursor: someone else advances it)
@@ -64,8 +76,50 @@ __global__ void __launch_bounds__(256) gather_step_kernel(const long* __restrict
   }
   __syncthreads();
   if (last && threadIdx.x == 0) {
-    *cursor = c + B;
+    *cursor = c - off + adv;
     __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// (strong scaling) per stream s: the global batch's label / perfect-channel power (rows perm[c .. c + Bg)) over this
+// rank's part's (rows perm[c + off .. c + off + B)) -> scale[s], which gather_step_kernel multiplies into the
+// part's rowden.  One workgroup per stream, a fixed-order reduction (deterministic); reads the cursor before the
+// gather that follows it on the stream advances it.
+__global__ void __launch_bounds__(256) den_scale_kernel(const long* __restrict__ perm, const int* __restrict__ cursor,
+                                                        long nperm, int Bg, int off, int B,
+                                                        const float* __restrict__ rowpow_l,
+                                                        const float* __restrict__ rowpow_p, long lab_stream_rows,
+                                                        float2* __restrict__ scale) {
+  __shared__ float4 red[256];
+  const int s = blockIdx.x, t = threadIdx.x;
+  int c = *cursor;
+  if (c < 0 || c + Bg > nperm) c = 0;   // (the gather's own guard)
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);   // (global l, global p, part l, part p)
+  for (int b = t; b < Bg; b += 256) {
+    const long ro = s * lab_stream_rows + perm[c + b];
+    const float l = rowpow_l[ro], p = rowpow_p ? rowpow_p[ro] : 0.f;
+    a.x += l;
+    a.y += p;
+    if (b >= off && b < off + B) {
+      a.z += l;
+      a.w += p;
+    }
+  }
+  red[t] = a;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h) {
+      const float4 o = red[t + h];
+      red[t].x += o.x;
+      red[t].y += o.y;
+      red[t].z += o.z;
+      red[t].w += o.w;
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const float4 r = red[0];
+    scale[s] = make_float2(r.z > 0.f ? r.x / r.z : 1.f, r.w > 0.f ? r.y / r.w : 1.f);
   }
 }
 
@@ -80,7 +134,8 @@ QD_API int qd_gather_step(const long* idx, const float* Yp, long yp_stream_strid
   if (plane % 4 || E < 1 || U < 1 || B < 1) return (int)hipErrorInvalidValue;
   const int waves = E * U * B;
   hipLaunchKernelGGL(gather_step_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)stream, idx, Yp,
-                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, nullptr, nullptr, (long)B, nullptr, nullptr, nullptr);
+                     yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, nullptr, nullptr, (long)B, nullptr,
+                     nullptr, nullptr, 0, B, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -88,19 +143,34 @@ QD_API int qd_gather_step(const long* idx, const float* Yp, long yp_stream_strid
 // advanced by B in-kernel); done: device uint32 zero-initialised once.  x1 / xq / rowoff nullable.
 // The caller guarantees *cursor + B <= n (it re-arms the cursor when it regenerates perm).
 // rowpow_l / rowpow_p / rowden (nullable, HDCE half only): rowden[r] = (|label row|^2, |perf row|^2)
+// off / adv / scale (strong scaling, see gather_step_kernel): this rank's part of the global batch starts off rows
+// in, the cursor advances by adv (>= off + B), scale (nullable, S float2) from qd_den_scale.  Weak: 0 / B / null.
 QD_API int qd_gather_cursor(const long* perm, long nperm, int* cursor, unsigned int* done, const float* rowpow_l,
                             const float* rowpow_p, float* rowden, const float* Yp, long yp_stream_stride,
                             float* x1, float* xq, int* rowoff, long lab_stream_rows, int E, int U, int B, int plane,
-                            void* stream) {
+                            int off, int adv, const float* scale, void* stream) {
   // done == null: the cursor is only read (the caller advances it later in the step, e.g. the
   // end-of-step weight pack) -- no same-address atomics, so the grid need not be capped
-  if (plane % 4 || E < 1 || U < 1 || B < 1 || !cursor || nperm < B) return (int)hipErrorInvalidValue;
+  if (plane % 4 || E < 1 || U < 1 || B < 1 || !cursor || off < 0 || adv < off + B || nperm < adv)
+    return (int)hipErrorInvalidValue;
   if ((x1 == nullptr) != (rowoff == nullptr) || (rowden && (!rowoff || !rowpow_l))) return (int)hipErrorInvalidValue;
   const int waves = E * U * B;
   const int cap = done ? 128 : 4096;
   const int grid = (waves + 3) / 4 < cap ? (waves + 3) / 4 : cap;
   hipLaunchKernelGGL(gather_step_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, perm, Yp,
                      yp_stream_stride, x1, xq, rowoff, lab_stream_rows, E, U, B, plane, cursor, done, nperm,
-                     rowpow_l, rowpow_p, reinterpret_cast<float2*>(rowden));
+                     rowpow_l, rowpow_p, reinterpret_cast<float2*>(rowden), off, adv,
+                     reinterpret_cast<const float2*>(scale));
+  return (int)hipGetLastError();
+}
+
+// (strong scaling) scale (S, 2) for this rank's part [off, off + B) of the global batch perm[*cursor .. + Bg)
+QD_API int qd_den_scale(const long* perm, long nperm, const int* cursor, int Bg, int off, int B,
+                        const float* rowpow_l, const float* rowpow_p, long lab_stream_rows, int S, float* scale,
+                        void* stream) {
+  if (!perm || !cursor || !rowpow_l || !scale || S < 1 || Bg < 1 || off < 0 || off + B > Bg || nperm < Bg)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(den_scale_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, perm, cursor, nperm, Bg, off, B,
+                     rowpow_l, rowpow_p, lab_stream_rows, reinterpret_cast<float2*>(scale));
   return (int)hipGetLastError();
 }

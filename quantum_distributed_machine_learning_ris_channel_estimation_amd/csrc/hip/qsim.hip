@@ -387,6 +387,7 @@ QD_API int qd_qsim_bwd_grid(int n, int B) {
 
 // wgroup > 0: sample b uses weights w[b / wgroup] (per-stream QuantumNAT noise); 0: shared.
 QD_API int qd_qsim_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   hipStream_t st = (hipStream_t)stream;
 #define CALL_F(NN) launch_fwd<NN>(x, w, E, B, L, wgroup, 0, st)
   QD_DISPATCH_N(n, CALL_F)
@@ -395,6 +396,7 @@ QD_API int qd_qsim_fwd(const float* x, const float* w, float* E, int B, int n, i
 
 QD_API int qd_qsim_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n, int L,
                        int wgroup, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   hipStream_t st = (hipStream_t)stream;
   const int grid = qd_qsim_bwd_grid(n, B);
 #define CALL_B(NN) launch_bwd<NN>(x, w, gE, dx, slab, B, L, wgroup, grid, st)
@@ -406,6 +408,7 @@ QD_API int qd_qsim_bwd(const float* x, const float* w, const float* gE, float* d
 // sample's final state there and the backward starts from it (no circuit recompute).
 QD_API int qd_qsim_fwd_save(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* psave,
                             void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   hipStream_t st = (hipStream_t)stream;
 #define CALL_F(NN) launch_fwd<NN>(x, w, E, B, L, wgroup, 0, st, (cf*)psave)
   QD_DISPATCH_N(n, CALL_F)
@@ -414,6 +417,7 @@ QD_API int qd_qsim_fwd_save(const float* x, const float* w, float* E, int B, int
 
 QD_API int qd_qsim_bwd_saved(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n,
                              int L, int wgroup, const void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   hipStream_t st = (hipStream_t)stream;
   const int grid = qd_qsim_bwd_grid(n, B);
 #define CALL_B(NN) launch_bwd<NN>(x, w, gE, dx, slab, B, L, wgroup, grid, st, (const cf*)psave)

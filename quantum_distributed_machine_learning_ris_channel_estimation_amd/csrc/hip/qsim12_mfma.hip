@@ -667,6 +667,7 @@ QD_API long long qd_qsim_mfma12_workspace(int G, int L) {
 // psave (B, 2, 4096) fp32 for qd_qsim_mfma12_bwd).  grid: one workgroup per sample up to 512.
 QD_API int qd_qsim_mfma12_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
                               void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (B < 1 || n != N || L < 1 || L > 8 || (L > 1 && ws == nullptr)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   const int G = wgroup > 0 ? (B + wgroup - 1) / wgroup : 1;
@@ -685,6 +686,7 @@ QD_API int qd_qsim_mfma12_fwd(const float* x, const float* w, float* E, int B, i
 // as the forward left them (same x, w).
 QD_API int qd_qsim_mfma12_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n,
                               int L, int wgroup, void* ws, void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (B < 1 || n != N || L < 1 || L > 8 || psave == nullptr || (L > 1 && ws == nullptr)) return (int)hipErrorInvalidValue;
   if (hipError_t e = qd::allow_lds(bwd_kernel, BWD_SMEM)) return (int)e;
   const int grid = B < 512 ? B : 512;   // = qd_qsim_big_grid(B): the slab rows the caller sums
@@ -703,6 +705,7 @@ QD_API long long qd_qsim_mfma8_workspace(int G, int L) {
 // images, rebuilt here from w.
 QD_API int qd_qsim_mfma8_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n,
                              int L, int wgroup, void* ws, const void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (B < 1 || n != 8 || L < 1 || L > 8 || psave == nullptr || (L > 1 && ws == nullptr)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (L > 1) {

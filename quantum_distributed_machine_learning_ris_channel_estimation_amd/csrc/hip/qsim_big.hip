@@ -808,6 +808,7 @@ QD_API int qd_qsim_big_grid(int B) { return B < kBigGridCap ? B : kBigGridCap; }
 // psave (nullable): (B, 2^n) complex64 buffer keeping every sample's psi_final for qd_qsim_big_bwd.
 QD_API int qd_qsim_big_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
                            void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (B < 1 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
   // (n <= 12: one 32 KiB state per workgroup, 4 resident per CU -- 768 workgroups, 3 samples each at B = 2304)
   const int grid = n <= 12 ? (B < 768 ? B : 768) : qd_qsim_big_grid(B);
@@ -820,6 +821,7 @@ QD_API int qd_qsim_big_fwd(const float* x, const float* w, float* E, int B, int 
 // psave (nullable): the forward's saved psi_final (same x, w); consumed (may be overwritten).
 QD_API int qd_qsim_big_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n, int L,
                            int wgroup, void* ws, void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (B < 1 || L < 1 || 2 * n * L > 256) return (int)hipErrorInvalidValue;
   const int grid = qd_qsim_big_grid(B);
 #define CALL_B(NN) \

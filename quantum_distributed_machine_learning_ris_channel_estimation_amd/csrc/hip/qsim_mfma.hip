@@ -367,6 +367,7 @@ QD_API int qd_qsim_mfma_prep_noise(const float* w, float* out, void* ops, int G,
 // samples per wave: 1 (measured 11.1 / 12.5 / 16.6 us at the flagship shape for 1 / 2 / 4)
 QD_API int qd_qsim_mfma_fwd(const float* x, const float* w, const void* ops, float* E, int B, int L, int wgroup,
                             void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (B < 1 || L < 2 || L > 8) return (int)hipErrorInvalidValue;
   constexpr int spw = 1;
   hipStream_t st = (hipStream_t)stream;

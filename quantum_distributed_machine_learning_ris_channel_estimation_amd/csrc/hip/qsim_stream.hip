@@ -775,6 +775,7 @@ QD_API long long qd_qsim_stream_save_bytes(int n, int B, int L) {
 // E (B, n) = <Z>; psave (nullable): qd_qsim_stream_save_bytes of kept states for qd_qsim_stream_bwd.
 QD_API int qd_qsim_stream_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
                               void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (!qd_qsim_stream_ok(n, L) || B < 1 || ws == nullptr) return (int)hipErrorInvalidValue;
 #define CALL_F(NN) fwd<NN>(x, w, E, B, L, wgroup, (char*)ws, (cf*)psave, (hipStream_t)stream)
   QD_STREAM_DISPATCH(n, CALL_F)
@@ -784,6 +785,7 @@ QD_API int qd_qsim_stream_fwd(const float* x, const float* w, float* E, int B, i
 // dx (B, n), slab (16 B, 2 n L) weight-gradient partials; psave (nullable) is consumed.
 QD_API int qd_qsim_stream_bwd(const float* x, const float* w, const float* gE, float* dx, float* slab, int B, int n,
                               int L, int wgroup, void* ws, void* psave, void* stream) {
+  if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
   if (!qd_qsim_stream_ok(n, L) || B < 1 || ws == nullptr) return (int)hipErrorInvalidValue;
 #define CALL_B(NN) bwd<NN>(x, w, gE, dx, slab, B, L, wgroup, (char*)ws, (cf*)psave, (hipStream_t)stream)
   QD_STREAM_DISPATCH(n, CALL_B)

@@ -164,3 +164,77 @@ QD_API int qd_coh_busy(float* x, int n, int iters, int grid, void* stream) {
   hipLaunchKernelGGL(qd::rt::coh_busy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, iters);
   return (int)hipGetLastError();
 }
+
+// Native crash report (round 6).  A host segfault inside the HIP runtime (round 5: rc 139 in
+// hipGraphLaunch under torch.cuda.CUDAGraph.replay, profiles/r5_46_pytest_segfault*.log) showed only the
+// Python frames faulthandler prints.  qd_install_crash_handler (called once by _native.hip_lib) puts a
+// SIGSEGV / SIGBUS / SIGABRT handler in front of whatever was installed before: it writes the native frames
+// (backtrace_symbols_fd: library + offset of every frame) to stderr, restores the previous action and
+// returns, so the fault re-raises into the previous handler (Python's faulthandler: the Python frames) and
+// finally the default action (exit status 139 / 134).  Async-signal-safe calls only.
+#include <execinfo.h>
+#include <signal.h>
+#include <string.h>
+#include <unistd.h>
+
+namespace qd {
+namespace rt {
+constexpr int kCrashSigs[3] = {SIGSEGV, SIGBUS, SIGABRT};
+struct sigaction g_prev[3];
+volatile sig_atomic_t g_installed = 0;
+
+void crash_write(const char* s) {
+  ssize_t r = write(2, s, strlen(s));
+  (void)r;
+}
+
+void crash_handler(int sig, siginfo_t* info, void* uctx) {
+  (void)uctx;
+  int k = 0;
+  while (k < 3 && kCrashSigs[k] != sig) ++k;
+  crash_write(sig == SIGSEGV ? "\n[qdml] SIGSEGV" : sig == SIGBUS ? "\n[qdml] SIGBUS" : "\n[qdml] SIGABRT");
+  char hex[32];
+  uintptr_t a = info ? (uintptr_t)info->si_addr : 0;
+  int n = 0;
+  hex[n++] = ' ';
+  hex[n++] = '@';
+  hex[n++] = '0';
+  hex[n++] = 'x';
+  for (int i = (int)sizeof(a) * 2 - 1; i >= 0; --i) hex[n++] = "0123456789abcdef"[(a >> (4 * i)) & 0xf];
+  hex[n++] = '\n';
+  hex[n] = 0;
+  crash_write(hex);
+  crash_write("[qdml] native frames (libqdml_hip crash handler):\n");
+  void* frames[64];
+  const int nf = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, nf, 2);
+  crash_write("[qdml] end of native frames\n");
+  // hand the signal on: the previous action (faulthandler, then the default) runs when the fault re-raises
+  if (k < 3) sigaction(sig, &g_prev[k], nullptr);
+  if (sig == SIGABRT) raise(sig);   // (abort() re-raises by itself too; a raised SIGABRT is not re-executed)
+}
+}  // namespace rt
+}  // namespace qd
+
+extern "C" int qd_install_crash_handler() {
+  using namespace qd::rt;
+  if (g_installed) return 0;
+  void* warm[2];
+  backtrace(warm, 2);   // (loads libgcc's unwinder now: backtrace() may allocate on its first call)
+  for (int k = 0; k < 3; ++k) {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = crash_handler;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    if (sigaction(kCrashSigs[k], &sa, &g_prev[k]) != 0) return -1;
+  }
+  g_installed = 1;
+  return 0;
+}
+
+// (test hook) fault on purpose in native code: tests/test_runtime_crash.py checks the report in a child process
+extern "C" void qd_crash_for_test() {
+  volatile int* p = nullptr;
+  *p = 1;
+}

@@ -250,6 +250,8 @@ class QSCStepHIP:
                                     self.Ww, self.grid_fwd, st), "qsc_pre_fwd")
         w = self.quantum_weights().contiguous()
         wgroup = B // w.shape[0] if w.dim() == 4 else 0
+        if wgroup and wgroup * w.shape[0] != B:   # (the kernels map sample s to group s // wgroup: G must divide B)
+            raise ValueError(f"{w.shape[0]} QuantumNAT weight groups do not divide the batch of {B}")
         extra = (nat.ptr(self.qws) if self.qws is not None else None,
                  nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
             (nat.ptr(self.psave) if self.psave is not None else None,)
@@ -295,6 +297,8 @@ class QSCStepHIP:
         flat = sp.flat
         w = self._w_cur
         wgroup = B // w.shape[0] if w.dim() == 4 else 0
+        if wgroup and wgroup * w.shape[0] != B:   # (the kernels map sample s to group s // wgroup: G must divide B)
+            raise ValueError(f"{w.shape[0]} QuantumNAT weight groups do not divide the batch of {B}")
         extra = (nat.ptr(self.qws) if self.qws is not None else None,
                  nat.ptr(self.psave) if self.psave is not None else None) if self.big else \
             (nat.ptr(self.psave) if self.psave is not None else None,)

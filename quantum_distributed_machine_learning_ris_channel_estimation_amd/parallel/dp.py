@@ -145,11 +145,21 @@ def check_local_gpus(local_rank: int, local_world: int, n_gpus: int) -> None:
                            "ranks per GPU)")
 
 
-def init_distributed(device: str = "auto", timeout_s: int = 600) -> DistContext:
-    """Initialise from torchrun-style env vars; world 1 needs no process group."""
+def resolve_timeout(timeout_s: Optional[float] = None) -> float:
+    """The rendezvous bound and the failure detector's stall timeout: ``timeout_s``, else ``QDML_PG_TIMEOUT``."""
+    if timeout_s is not None:
+        return float(timeout_s)
+    from .watchdog import default_timeout_s
+    return default_timeout_s()
+
+
+def init_distributed(device: str = "auto", timeout_s: Optional[float] = None) -> DistContext:
+    """Initialise from torchrun-style env vars; world 1 needs no process group.  ``timeout_s`` bounds the
+    rendezvous and is the failure detector's stall timeout; default ``QDML_PG_TIMEOUT`` (600 s)."""
     global _CTX
     if _CTX is not None:
         return _CTX
+    timeout_s = resolve_timeout(timeout_s)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))

@@ -32,19 +32,45 @@ EXIT_STALL = 75       # (EX_TEMPFAIL) a peer stopped answering: the job can be r
 EXIT_COMM_ERROR = 76  # RCCL reported an asynchronous error
 
 _capture_depth = 0   # HIP graph captures in progress in this process (utils.profiling.GraphedStep)
+_active: Optional["CommWatchdog"] = None   # the running watchdog of this process (one communicator per rank)
 
 
 @contextlib.contextmanager
 def capturing():
-    """Around a HIP graph capture: the watchdog makes no RCCL call meanwhile (belt and braces -- the async-error
-    read is host-only, but a capture is exactly where round 3's process-group watchdog broke things), and the
-    capture's warm-up is not mistaken for a stall."""
+    """Around a HIP graph capture -- the ``torch.cuda.graph`` block only, not its eager warm-ups: the watchdog makes
+    no RCCL call meanwhile (belt and braces: the async-error read is host-only, but a capture is exactly where round
+    3's process-group watchdog broke things).  The heartbeat-age check keeps running: it reads host memory only."""
     global _capture_depth
     _capture_depth += 1
     try:
         yield
     finally:
         _capture_depth -= 1
+
+
+def heartbeat(phase: Optional[str] = None) -> None:
+    """Bump the running watchdog's heartbeat, if there is one (a host sync point completed; ``phase``: what runs
+    next).  Cheap and safe to call from any host code."""
+    wd = _active
+    if wd is not None:
+        wd.heartbeat(phase)
+
+
+@contextlib.contextmanager
+def disarmed(phase: str):
+    """Around host-only work that may legitimately outlast the timeout with no collective in flight (data
+    generation, rank-0-only checkpointing / evaluation while the other ranks wait at the next barrier): the stall
+    check is off meanwhile (async errors still fire), and re-armed with a fresh heartbeat afterwards."""
+    wd = _active
+    if wd is None:
+        yield
+        return
+    wd.arm(False)
+    wd.heartbeat(phase)
+    try:
+        yield
+    finally:
+        wd.arm(True)
 
 
 class CommWatchdog:
@@ -67,7 +93,9 @@ class CommWatchdog:
 
     # -- training-loop side (cheap: a lock and two stores) -------------------------------------------
     def start(self) -> "CommWatchdog":
+        global _active
         self._thread.start()
+        _active = self
         return self
 
     def heartbeat(self, phase: Optional[str] = None) -> None:
@@ -84,6 +112,9 @@ class CommWatchdog:
             self._beat = self.clock()
 
     def stop(self) -> None:
+        global _active
+        if _active is self:
+            _active = None
         self._stop.set()
         if self._thread.is_alive() and threading.current_thread() is not self._thread:
             self._thread.join(timeout=self.poll_s + 1.0)
@@ -91,16 +122,15 @@ class CommWatchdog:
     # -- watchdog thread ------------------------------------------------------------------------------
     def check_once(self) -> Optional[str]:
         """One poll: the failure message, or None.  (Exposed for tests; the thread calls it every poll_s.)"""
-        if _capture_depth > 0:
-            return None
-        try:
-            err = int(self.comm.async_error())
-        except Exception as e:   # (a destroyed communicator while shutting down is not a failure)
-            if self._stop.is_set():
-                return None
-            return f"ncclCommGetAsyncError raised {e!r}"
-        if err != 0:
-            return f"RCCL asynchronous error {err}"
+        if _capture_depth == 0:   # (no RCCL call while a graph is being captured; the stall check below stays)
+            try:
+                err = int(self.comm.async_error())
+            except Exception as e:   # (a destroyed communicator while shutting down is not a failure)
+                if self._stop.is_set():
+                    return None
+                return f"ncclCommGetAsyncError raised {e!r}"
+            if err != 0:
+                return f"RCCL asynchronous error {err}"
         with self._lock:
             age, phase, armed = self.clock() - self._beat, self._phase, self._armed
         if armed and age > self.timeout_s:

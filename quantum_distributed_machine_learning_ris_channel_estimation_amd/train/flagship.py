@@ -113,6 +113,12 @@ class FlagshipConfig:
     #                              the world-1 step, joined before the small bucket (shorter g2: wins where the FC
     #                              collective is short; one-graph plan only -- a fork cannot span two graphs).
     #                              bench.py times both at the real world size.
+    scaling: str = "weak"        # world > 1: "weak" = batch per stream on EVERY rank, each rank its own data; "strong" =
+    #                              the reference's DataParallel semantics (R:144-148): ONE global batch of ``batch`` rows
+    #                              per stream per step (same data and permutation on every rank) cut into world
+    #                              contiguous parts of batch / world rows; the NMSE denominators are the global batch's
+    #                              (gather.hip den_scale_kernel), so the ranks' losses are shares of one loss and the
+    #                              HDCE gradients are SUMMED; per-rank BatchNorm (as DataParallel's replicas)
     seed: int = 0
     n_scenarios: int = 3
     n_users: int = 3
@@ -123,12 +129,22 @@ class FlagshipTrainer(DPPlan):
         """``store``: share another trainer's HBM-resident dataset (same data_len / pilots / SNR / seed)."""
         self.cfg, self.ctx = cfg, ctx
         dev = ctx.device
+        if cfg.scaling not in ("weak", "strong"):
+            raise ValueError(f"scaling {cfg.scaling!r}")
+        self.strong = cfg.scaling == "strong" and ctx.world > 1
+        if self.strong and cfg.batch % ctx.world:
+            raise ValueError(f"scaling 'strong': batch {cfg.batch} is not split evenly over {ctx.world} ranks")
         if store is None:
+            # (strong: every rank holds the same data -- its part of each global batch comes from it)
             store, _ = make_dml_stores(cfg.data_len, cfg.pilot_num, cfg.snr_db, 0.9, dev, data_dir=None, synthetic=True,
-                                       base_seed=cfg.seed + 1000 * ctx.rank, n_scenarios=cfg.n_scenarios,
-                                       n_users=cfg.n_users)
+                                       base_seed=cfg.seed + (0 if self.strong else 1000 * ctx.rank),
+                                       n_scenarios=cfg.n_scenarios, n_users=cfg.n_users)
         self.store = store
-        self.E, self.U, self.B = cfg.n_scenarios, cfg.n_users, cfg.batch
+        self.E, self.U = cfg.n_scenarios, cfg.n_users
+        self.Bg = cfg.batch                                           # rows per stream of one step's (global) batch
+        self.B = cfg.batch // ctx.world if self.strong else cfg.batch   # this rank's rows per stream
+        # HDCE gradient scale: weak -- the mean of the ranks' losses; strong -- shares of ONE loss, summed
+        self._hgs = 1.0 if self.strong else 1.0 / ctx.world
         self.S = self.E * self.U
         # --- models (weights broadcast from rank 0 once; then resident)
         torch.manual_seed(cfg.seed)
@@ -216,10 +232,18 @@ class FlagshipTrainer(DPPlan):
         if dev.type == "cuda" and self.hstep.hip:   # per-row label powers ride along with the gather
             nm = self.hstep.nmse
             self.gat.rowpow = (nm._row_powers(self.store.Hlabel), nm._row_powers(self.store.Hperf))
+        if self.strong:
+            self.gat.set_part(ctx.rank * self.B, self.Bg)
+            if dev.type == "cuda" and not self.hstep.hip:
+                raise ValueError("scaling 'strong' on a GPU needs the HIP HDCE step (its NMSE reads scaled row powers)")
+            if dev.type != "cuda":   # (the torch NMSE takes the global denominators directly)
+                self.hstep.nmse.den_global = self.gat.den_global
         # batch selection on the device: the gather kernels read perm[cur : cur + B] and advance cur
         # themselves (cur[0]: HDCE / whole-step gather, cur[1]: the QSC graph's own gather); the host
         # only tracks the epoch position to regenerate perm in place when it runs out
         self.perm = torch.randperm(self.store.n, device=dev)
+        if self.strong:
+            ctx.broadcast_(self.perm)   # (one permutation: the ranks take parts of the same global batches)
         # (one 256-byte row each: the HDCE and QSC chains run concurrently and update their own
         # cursor / arrival counter, so the two never share a cache line)
         self.cur = torch.zeros(2, 64, dtype=torch.int32, device=dev)
@@ -387,13 +411,13 @@ class FlagshipTrainer(DPPlan):
         if not self.tail_pack:
             return None
         conv, flat, cur = self.hstep.conv, self.hdce.space.flat, self.cur[0, 0:1]
-        return lambda lo, hi: conv.pack_scatter(flat, lo, hi, cursor=cur, cursor_inc=self.B)
+        return lambda lo, hi: conv.pack_scatter(flat, lo, hi, cursor=cur, cursor_inc=self.Bg)
 
     def _tail_pack_launch(self, advance: bool = True) -> None:
         """Pack the (just updated) conv weights into the MFMA B-fragment images the next forward reads,
         and advance the batch cursor -- one launch at the end of the step."""
         self.hstep.conv.pack_weights(nat.stream_ptr(self.ctx.device), cursor=self.cur[0, 0:1] if advance else None,
-                                     cursor_inc=self.B if advance else 0)
+                                     cursor_inc=self.Bg if advance else 0)
 
     def _fc_adam_fork(self) -> None:
         """(fc_adam_side) the FC weight's Adam on the fc stream, after the FC data gradient (its last reader of the
@@ -521,9 +545,9 @@ class FlagshipTrainer(DPPlan):
         if not any(g.enabled and g.graph is None for g in gs):
             return
         # the warm-up runs inside capture advance the device cursors: make room, restore them after
-        if self.cursor + (GraphedStep.WARMUP + 1) * k * self.B > self.store.n:
+        if self.cursor + (GraphedStep.WARMUP + 1) * k * self.Bg > self.store.n:
             self._new_epoch()
-        if self.cursor + (GraphedStep.WARMUP + 1) * k * self.B > self.store.n:
+        if self.cursor + (GraphedStep.WARMUP + 1) * k * self.Bg > self.store.n:
             raise ValueError(f"{k} steps per graph need more than the {self.store.n} samples per stream")
         cur = self.cur.clone()
         saved = [t.clone() for t in self.mutable_state()] if preserve else None
@@ -544,15 +568,17 @@ class FlagshipTrainer(DPPlan):
     def _new_epoch(self) -> None:
         # in place: the graphs hold its address; the previous replays were joined on this stream
         torch.randperm(self.store.n, device=self.ctx.device, out=self.perm)
+        if self.strong:
+            self.ctx.broadcast_(self.perm)
         self.cur.zero_()
         self.cursor = 0
 
     def next_batch(self, k: int = 1) -> None:
         """Advance the host mirror of the batch cursor by ``k`` batches; when the permutation cannot
         hold them, draw a new one and re-arm the device cursors (the short tail is dropped)."""
-        if self.cursor + k * self.B > self.store.n:
+        if self.cursor + k * self.Bg > self.store.n:
             self._new_epoch()
-        self.cursor += k * self.B
+        self.cursor += k * self.Bg
 
     def step(self) -> None:
         """One training step."""
@@ -564,14 +590,16 @@ class FlagshipTrainer(DPPlan):
             return 1
         # (a capture runs WARMUP + 1 passes of the k steps inside one permutation of the stream: large batches --
         # P256 x 1024 samples per stream -- get fewer steps per replay)
-        fit = self.store.n // ((GraphedStep.WARMUP + 1) * self.B)
+        fit = self.store.n // ((GraphedStep.WARMUP + 1) * self.Bg)
         return max(1, min(self.cfg.steps_per_graph, fit))
 
     def _reps(self, n: int):
-        """Steps per replay of ``run(n)``: lead_in single steps, one ``ramp``-step replay, then k-step replays, then
-        the remainder as ONE replay of a shorter graph (single-step replays cost ~3 % more per step:
-        profiles/r3_12_window.txt).  Each replay is submitted while the previous one runs, so the ramp keeps every
-        submission behind GPU work (FlagshipConfig.ramp)."""
+        """Steps per replay of ``run(n)``: lead_in single steps, one ``ramp``-step replay, then k-step replays; a
+        remainder r rides in the LAST of them as one (k + r)-step graph where the dataset holds that capture
+        (every replay boundary drains both chains and re-fills them, ~30 us: profiles/r5_46_bench*.json), else it
+        is one replay of its own.  Each replay is submitted while the previous one runs, so the ramp keeps every
+        submission behind GPU work (FlagshipConfig.ramp).  The driver's 20-step window is [1, 4, 15]: three
+        boundaries instead of [1, 4, 10, 5]'s four."""
         k = self._k()
         if k == 1:
             return [1] * n
@@ -584,8 +612,12 @@ class FlagshipTrainer(DPPlan):
                 break
             reps.append(min(r, rem))
             rem -= reps[-1]
-        reps += [k] * (rem // k)
-        return reps + ([rem % k] if rem % k else [])
+        body, tail = [k] * (rem // k), rem % k
+        fit = self.store.n // ((GraphedStep.WARMUP + 1) * self.Bg)   # (what _capture_set can hold: see _k)
+        if tail and body and k + tail <= fit:
+            body[-1] += tail
+            tail = 0
+        return reps + body + ([tail] if tail else [])
 
     def prepare(self, n: int) -> None:
         """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""
@@ -600,6 +632,8 @@ class FlagshipTrainer(DPPlan):
             self._replay(kk, fence=i == len(reps) - 1)
 
     def _replay(self, k: int, fence: bool = True) -> None:
+        if getattr(self, "_closed", False):
+            raise RuntimeError("FlagshipTrainer used after close()")
         gs = self._graphs_for(k)
         if any(g.enabled and g.graph is None for g in gs):
             # (preserve: the capture warm-ups run optimizer steps on rank-local gradients; restoring
@@ -614,3 +648,14 @@ class FlagshipTrainer(DPPlan):
     @property
     def samples_per_step(self) -> int:
         return self.S * self.B
+
+    def close(self) -> None:
+        """Release every captured graph set now (GraphedStep.close: device sync, then the executables and their
+        pools), instead of whenever the garbage collector reaches them -- possibly in the middle of another
+        trainer's capture or replay.  Idempotent; the trainer cannot step afterwards."""
+        for gs in list(getattr(self, "_graph_sets", {}).values()):
+            for g in gs:
+                g.close()
+        self._graph_sets = {}
+        self.graphs = []
+        self._closed = True

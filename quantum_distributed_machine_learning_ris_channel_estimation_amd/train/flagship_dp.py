@@ -80,20 +80,21 @@ class DPPlan:
         self._join(("qsc",))
 
     def _dp_gf(self) -> None:
+        # (HDCE gradient scale _hgs: 1 / world for weak scaling, 1 for strong -- the ranks' losses are shares of one)
         if self.zero:   # this rank's shard of the FC region only
-            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.hskip, part=1 + self.ctx.rank)
+            self.hopt.step(grad_scale=self._hgs, skip=self.hskip, part=1 + self.ctx.rank)
         elif len(self.hopt.bounds) > 1:   # (unpartitioned -- serial world 1 -- gr steps everything)
-            self.hopt.step(grad_scale=1.0 / self.ctx.world, skip=self.hskip, part=1)
+            self.hopt.step(grad_scale=self._hgs, skip=self.hskip, part=1)
 
     def _dp_gr(self) -> None:
-        g = 1.0 / self.ctx.world
         pk = self._adam_pack()
         # (world-1 serial plan with adam_slabs: the update sums the step's gradient slabs itself)
         sl = self.hstep.take_slabs() if getattr(self, "adam_slabs", False) else None
-        self.hopt.step(grad_scale=g, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None, pack=pk, slabs=sl)
+        self.hopt.step(grad_scale=self._hgs, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None, pack=pk,
+                       slabs=sl)
         if self.tail_pack and pk is None:
             self._tail_pack_launch()
-        self.qopt.step(grad_scale=g, skip=self.qskip)
+        self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.qskip)   # (QSC: the mean of equal-size parts)
 
     def _fc_weights_lp(self) -> torch.Tensor:
         """(ZeRO) the FC region's copy the forward / data gradient read: the bf16 shadow (GPU bf16),

@@ -34,6 +34,7 @@ from ..models.estimators import NMSELoss, QSC_P128, SC_P128
 from ..ops.gather import StepGather
 from ..ops.optim import FlatParamSpace, make_optimizer
 from ..parallel.dp import DeviceSampler, GradBuckets, init_distributed
+from ..parallel.watchdog import disarmed
 from ..utils.metrics import MetricsLogger, to_db
 from ..utils.profiling import GraphedStep
 from . import checkpoint as ck
@@ -139,8 +140,9 @@ class Y2HRunner:
         """HBM-resident train/val stores (this rank's shard)."""
         if self._stores is None:
             ctx = self._context()
-            tr, va = make_dml_stores(self.data_len, self.Pilot_num, self.SNRdb, self.train_test_ratio, ctx.device,
-                                     self.data_dir, self.synthetic, self.seed, self.n_scenarios, self.n_users)
+            with disarmed("data generation"):   # (host-only, may outlast the stall timeout on a big data_len)
+                tr, va = make_dml_stores(self.data_len, self.Pilot_num, self.SNRdb, self.train_test_ratio, ctx.device,
+                                         self.data_dir, self.synthetic, self.seed, self.n_scenarios, self.n_users)
             if ctx.world > 1:
                 if not self._dp_reference():   # (reference semantics: every rank slices the same global batches)
                     tr = tr.shard(ctx.rank, ctx.world)
@@ -421,12 +423,13 @@ class Y2HRunner:
             nmse, nmse_perf = self.eval_hdce(model, va)
             self.val_HDCE_nmse.append(nmse)
             if ctx.is_main:
-                if epoch == self.n_epochs - 1:
-                    ck.save_hdce(d, model.convs, model.fc, B, self.SNRdb, f"epoch{epoch}")
-                    print("HDCE finally saved!")
-                if nmse < best_nmse:
-                    ck.save_hdce(d, model.convs, model.fc, B, self.SNRdb, "best")
-                    print("HDCE saved!")
+                with disarmed("hdce checkpoint"):
+                    if epoch == self.n_epochs - 1:
+                        ck.save_hdce(d, model.convs, model.fc, B, self.SNRdb, f"epoch{epoch}")
+                        print("HDCE finally saved!")
+                    if nmse < best_nmse:
+                        ck.save_hdce(d, model.convs, model.fc, B, self.SNRdb, "best")
+                        print("HDCE saved!")
             if nmse < best_nmse:
                 best_nmse = nmse
             self._print(f"Epoch [{epoch}]/[{self.n_epochs}] || NMSE {nmse:.5f}, NMSE_perf {nmse_perf:.5f}, "
@@ -444,16 +447,19 @@ class Y2HRunner:
                 if opt.lr < self.lr_threshold:
                     opt.set_lr(self.lr_threshold)
             if ctx.is_main:
-                ck.save_resume(resume_path, epoch=epoch, best=best_nmse, optimizer=opt.state_dict(),
-                               flat=sp.flat.cpu(), run_mean=[t.cpu() for t in model.run_mean],
-                               run_var=[t.cpu() for t in model.run_var], nbt=[t.cpu() for t in model.nbt],
-                               train_losses=torch.tensor(self.train_HDCE_losses, dtype=torch.float64),
-                               val_nmse=torch.tensor(self.val_HDCE_nmse, dtype=torch.float64), rng=ck.rng_state(),
-                               **({"swa": swa[0].cpu(), "swa_n": swa[1]} if swa is not None else {}))
+                with disarmed("hdce resume file"):
+                    ck.save_resume(resume_path, epoch=epoch, best=best_nmse, optimizer=opt.state_dict(),
+                                   flat=sp.flat.cpu(), run_mean=[t.cpu() for t in model.run_mean],
+                                   run_var=[t.cpu() for t in model.run_var], nbt=[t.cpu() for t in model.nbt],
+                                   train_losses=torch.tensor(self.train_HDCE_losses, dtype=torch.float64),
+                                   val_nmse=torch.tensor(self.val_HDCE_nmse, dtype=torch.float64),
+                                   rng=ck.rng_state(),
+                                   **({"swa": swa[0].cpu(), "swa_n": swa[1]} if swa is not None else {}))
             ctx.heartbeat(f"hdce epoch {epoch + 1}")
             _maybe_fault(epoch)
         if swa is not None and swa[1] > 0 and ctx.is_main:
-            self._save_swa(model, tr, swa, d)
+            with disarmed("hdce swa (rank 0)"):
+                self._save_swa(model, tr, swa, d)
             ctx.heartbeat("hdce swa")
         self.hdce_model = model
         return model

@@ -101,11 +101,9 @@ class GraphedStep:
         self.pool = pool
 
     def capture(self) -> None:
-        from ..parallel.watchdog import capturing
-        with capturing():
-            self._capture()
-
-    def _capture(self) -> None:
+        from ..parallel.watchdog import capturing, heartbeat
+        # eager warm-ups (real collectives under the DP plans) stay visible to the failure detector: only the
+        # capture itself pauses it (a peer that dies during a warm-up or the pre-capture sync is a stall)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -113,13 +111,37 @@ class GraphedStep:
                 self.fn()
         torch.cuda.current_stream().wait_stream(s)
         self.pre_capture()
+        heartbeat("graph capture")
         g = torch.cuda.CUDAGraph()
         if self.capture_stream is not None:
             self.capture_stream.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.graph(g, pool=self.pool, stream=self.capture_stream,
-                              capture_error_mode=self.capture_error_mode):
-            self.fn()
+        with capturing():
+            with torch.cuda.graph(g, pool=self.pool, stream=self.capture_stream,
+                                  capture_error_mode=self.capture_error_mode):
+                self.fn()
+        heartbeat("graph replay")
         self.graph = g
+
+    def close(self) -> None:
+        """Release the graph executable (and its hold on the memory pool) deterministically: the device is
+        synchronised first, so no replay of it can still be running when HIP destroys the executable.  (Round 5:
+        a host segfault in a later hipGraphLaunch, with earlier tests' graphs dropped by whichever garbage
+        collection ran next -- the test suite had to synchronise and collect between tests, tests/conftest.py.)
+        Idempotent; calling the step afterwards raises."""
+        g, self.graph = self.graph, None
+        self.enabled = False
+        self.fn = None   # (breaks the trainer -> graph set -> step -> bound method cycle)
+        if g is not None:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            g.reset()
+
+    def __del__(self) -> None:
+        try:
+            if self.graph is not None:
+                self.close()
+        except Exception:   # (interpreter shutdown: torch may already be gone)
+            pass
 
     def pre_capture(self) -> None:
         """The capture starts from a quiescent process: every warm-up kernel and collective has finished
@@ -133,6 +155,8 @@ class GraphedStep:
 
     def __call__(self) -> None:
         if not self.enabled:
+            if self.fn is None:
+                raise RuntimeError("GraphedStep used after close()")
             self.fn()
             return
         if self.graph is None:

@@ -185,18 +185,21 @@ def test_dedupe_is_what_keeps_it_clean(monkeypatch):
 
 
 @pytest.mark.parametrize("n,k,lead,ramp,want", [
-    (20, 10, 1, 4, [1, 4, 10, 5]),       # the driver's window: every submission behind the previous replay
-    (300, 10, 1, 4, [1, 4] + [10] * 29 + [5]),
-    (30, 10, 1, 4, [1, 4, 10, 10, 5]),   # bench.py's settle run: warms every graph set the 20-step window uses
-    (20, 10, 1, 0, [1, 10, 9]),          # ramp off: round 4's plan
+    (20, 10, 1, 4, [1, 4, 15]),          # the driver's window: the remainder rides in the last replay (3 boundaries)
+    (300, 10, 1, 4, [1, 4] + [10] * 28 + [15]),
+    (30, 10, 1, 4, [1, 4, 10, 15]),      # bench.py's settle run: warms every graph set the 20-step window uses
+    (20, 10, 1, 0, [1, 10, 9]),          # ramp off: a merged 19-step graph exceeds one capture's data (fit 17)
     (3, 10, 1, 4, [1, 2]),
     (20, 1, 1, 4, [1] * 20),
-    (25, 10, 0, 4, [10, 10, 5]),
+    (25, 10, 0, 4, [10, 15]),
+    (39, 10, 1, 4, [1, 4, 10, 10, 14]),
 ])
 def test_replay_plan(n, k, lead, ramp, want):
-    """FlagshipTrainer._reps: lead-in single step, one ramp replay, k-step replays, one remainder replay."""
+    """FlagshipTrainer._reps: lead-in single step, one ramp replay, k-step replays, the remainder merged into the
+    last one while the dataset holds that capture (else one remainder replay)."""
     from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import FlagshipTrainer
-    fake = SimpleNamespace(cfg=SimpleNamespace(lead_in=lead, ramp=ramp), _k=lambda: k)
+    fake = SimpleNamespace(cfg=SimpleNamespace(lead_in=lead, ramp=ramp), _k=lambda: k, store=SimpleNamespace(n=18000),
+                           Bg=256)   # (fit = 18000 // (4 * 256) = 17 steps per capture)
     got = FlagshipTrainer._reps(fake, n)
     assert got == want and sum(got) == n
     # every graph set of the 20-step window is replayed by the 30-step settle run before it

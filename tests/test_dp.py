@@ -81,6 +81,18 @@ def test_bench_self_launches_n_ranks():
     assert r["dp_fallback"] is None
 
 
+def test_bench_strong_scaling_line():
+    """`bench.py --gpus 2 --scaling strong`: one global batch of 9 x batch rows per step, split over the ranks
+    (the reference's DataParallel semantics) -- the line says "strong" and the per-rank batch."""
+    rc, recs, err = _bench(["--gpus", "2", "--scaling", "strong", "--dp-plan", "allreduce"] + SMALL +
+                           ["--phase-steps", "0"])
+    assert rc == 0, err[-2000:]
+    assert len(recs) == 1, recs
+    r = recs[0]
+    assert r["scaling"] == "strong" and r["config"]["per_rank_stream_batch"] == 2
+    assert r["config"]["global_batch"] == 9 * 4 and r["config"]["per_gpu_batch"] == 9 * 2
+
+
 def test_bench_supervisor_falls_back_when_a_rank_fails():
     """A rank that fails in the first attempt makes EVERY rank restart with the 5-graph plan; exactly one
     JSON line (the successful attempt's) is printed, and it names the fallback."""

@@ -33,3 +33,17 @@ def test_flagship_lockstep_and_nan_skip_world_n(tmp_path, world, plan):
     for r in range(world):
         same, skipped, flag = open(f"{out}.{r}").read().split()
         assert same == "1" and skipped == "1" and float(flag) >= 1.0
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_flagship_strong_scaling_is_dataparallel_semantics(tmp_path, world):
+    """FlagshipConfig.scaling="strong" (bench.py --scaling strong): each rank holds its contiguous part of ONE
+    global batch, the NMSE denominators are the global batch's, the QSC matches a 1-process run on the whole
+    batch, and the ranks stay bit-identical (tests/dist_scripts/flagship_strong.py)."""
+    out = str(tmp_path / "st")
+    rc = launch([sys.executable, os.path.join(HERE, "dist_scripts", "flagship_strong.py"), out], nproc=world,
+                extra_env=ENV)
+    assert rc == 0
+    for r in range(world):
+        row = open(f"{out}.{r}").read()
+        assert row.split()[0] == "1", row

@@ -304,3 +304,28 @@ def test_slab_fed_adam_matches_slab_launch(cuda, monkeypatch, mode):
     for i, (a, b) in enumerate(zip(_all_state(trs[0]), _all_state(trs[1]))):
         assert torch.equal(a, b), (i, float((a.float() - b.float()).abs().max()))
     assert torch.equal(trs[0].hloss, trs[1].hloss)
+
+
+def test_dropped_trainer_then_new_capture_and_replay(cuda):
+    """Graph lifetime in the product code: a trainer dropped right after run() -- no sync, its
+    replays possibly still on the device -- releases its graph executables itself (GraphedStep.__del__ ->
+    close(): device sync first), so another trainer can capture and replay at once.  Also the explicit close()
+    bench.py's plan selection uses.  (tests/conftest.py no longer synchronises / collects between tests.)"""
+    import gc
+    ctx = DistContext(device=cuda)
+    cfg = FlagshipConfig(batch=32, data_len=400, steps_per_graph=3)
+    a = FlagshipTrainer(cfg, ctx)
+    a.run(7)                       # (graph sets 1, 3 and a merged tail; nothing synchronised after the replays)
+    del a
+    gc.collect()                   # (the trainer <-> graph-set cycle goes here, with replays maybe in flight)
+    b = FlagshipTrainer(cfg, ctx)
+    b.run(5)
+    c = FlagshipTrainer(cfg, ctx)
+    c.run(4)
+    b.close()                      # (explicit release while c's graphs stay alive)
+    c.run(4)
+    torch.cuda.synchronize()
+    assert torch.isfinite(c.hloss).all() and torch.isfinite(c.qloss).all()
+    with pytest.raises(RuntimeError):
+        b.run(1)                   # (a closed trainer cannot step)
+    c.close()

@@ -106,6 +106,85 @@ def test_capture_pauses_async_error_polling():
     assert "asynchronous error 7" in w.check_once()
 
 
+def test_stall_inside_a_capture_window_still_fires():
+    """the capture window pauses only the RCCL call -- a stall (a peer dead during the warm-up
+    collectives or the pre-capture sync) is still detected."""
+    c, clk = FakeComm(), Clock()
+    w = wdm.CommWatchdog(c, rank=2, timeout_s=5, clock=clk)
+    w.heartbeat("graph capture")
+    with wdm.capturing():
+        clk.t += 6
+        msg = w.check_once()
+    assert msg is not None and "graph capture" in msg
+
+
+def test_graphed_step_capture_window_is_the_graph_block_only(monkeypatch):
+    """GraphedStep.capture: the eager warm-ups run OUTSIDE capturing() (a stall there is visible), and the
+    heartbeat is bumped right before and after the graph block."""
+    import torch
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.utils import profiling
+    seen = []
+
+    class G:
+        def reset(self):
+            pass
+
+    @__import__("contextlib").contextmanager
+    def fake_graph(g, **kw):
+        seen.append(("graph", wdm._capture_depth))
+        yield
+
+    class S:
+        def wait_stream(self, other):
+            pass
+
+    monkeypatch.setattr(torch.cuda, "Stream", lambda *a, **k: S())
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a, **k: S())
+    monkeypatch.setattr(torch.cuda, "stream", lambda s: __import__("contextlib").nullcontext())
+    monkeypatch.setattr(torch.cuda, "CUDAGraph", G)
+    monkeypatch.setattr(torch.cuda, "graph", fake_graph)
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    beats = []
+    monkeypatch.setattr(wdm, "heartbeat", lambda phase=None: beats.append(phase))
+    gs = profiling.GraphedStep(lambda: seen.append(("fn", wdm._capture_depth)), warmup=2)
+    gs.capture()
+    assert seen == [("fn", 0), ("fn", 0), ("graph", 1), ("fn", 1)]
+    assert beats == ["graph capture", "graph replay"] and wdm._capture_depth == 0
+    gs.close()
+    with pytest.raises(RuntimeError, match="after close"):
+        gs()
+
+
+def test_module_heartbeat_and_disarmed_reach_the_running_watchdog():
+    c, clk = FakeComm(), Clock()
+    w = wdm.CommWatchdog(c, rank=0, timeout_s=5, poll_s=3600, clock=clk).start()
+    try:
+        assert wdm._active is w
+        clk.t += 4
+        wdm.heartbeat("epoch 3")
+        clk.t += 4
+        assert w.check_once() is None                # (the module-level heartbeat reached it)
+        with wdm.disarmed("data generation"):
+            clk.t += 1000
+            assert w.check_once() is None            # host-only phase: no stall
+        assert w._armed and w.check_once() is None   # re-armed with a fresh heartbeat
+        clk.t += 6
+        assert "data generation" in w.check_once()
+    finally:
+        w.stop()
+    assert wdm._active is None
+
+
+def test_pg_timeout_env_reaches_the_watchdog_timeout(monkeypatch):
+    """QDML_PG_TIMEOUT is the default of init_distributed's timeout (rendezvous AND the watchdog), not
+    only bench.py's."""
+    import inspect
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.parallel import dp
+    monkeypatch.setenv("QDML_PG_TIMEOUT", "1234")
+    assert dp.resolve_timeout() == 1234.0 and dp.resolve_timeout(7) == 7.0
+    assert inspect.signature(dp.init_distributed).parameters["timeout_s"].default is None
+
+
 def test_hung_abort_is_not_waited_for():
     class Stuck(FakeComm):
         def close(self, abort=False):
