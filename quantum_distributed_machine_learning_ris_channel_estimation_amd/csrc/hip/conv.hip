@@ -618,6 +618,205 @@ __global__ void __launch_bounds__(256, 2) conv3x3_kernel(const TIN* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------
+// conv3x3_fwd_db_kernel (round 6): the training forward of a 32-channel layer (2, 3) at P128, software-pipelined
+// per wave over TWO LDS tiles.  conv3x3_body runs each sample's phases back to back -- stage (BN + ReLU of the
+// previous layer's z, bf16 pack, 32 ds_write_b32 per lane), then 72 MFMAs, then the epilogue -- so with about one
+// wave per SIMD the MFMA pipe idles through every staging (profiles/r4_28_stamp_conv.txt: ~2,800 cycles of vector
+// issue beside 2,300 of MFMA per sample).  Here, while sample n's MFMAs run on tile[n & 1], the wave stages sample
+// n + 1 into the other tile from the registers its loads landed in, a piece (2 positions of one channel-pair item:
+// 2 packed FMAs, the NaN-keeping ReLU, 2 ds_write_b32) after each k-step's MFMA pair -- inside the MFMA shadow
+// (an MFMA holds the SIMD's vector issue for 8 of its 32 cycles: MI355X_MICROARCH "vector-instruction ISSUE cost")
+// -- and issues sample n + 2's global loads as soon as the last piece has consumed the registers.  Only the first
+// sample's staging is exposed.  The arithmetic is conv3x3_body's (same k order, same accumulation, same statistics
+// order): z and the BN partials are bit-identical to it.  One workgroup per CU (two tiles per wave: 111 KB of LDS).
+// ------------------------------------------------------------------------------------------
+template <int W>
+__global__ void __launch_bounds__(256, 1) conv3x3_fwd_db_kernel(const uint16_t* __restrict__ xin,
+                                                             const float* __restrict__ st_in,
+                                                             const uint16_t* __restrict__ wt, uint16_t* __restrict__ out,
+                                                             float* __restrict__ stats, int E, int B, int chunks,
+                                                             int spw, BnFwd bnf) {
+  using G = Geo<16, W>;
+  constexpr int CIN = 32, KS = 18;                    // 16-deep k steps of K = 9 taps x 32 channels
+  constexpr int TILE = G::HP * G::WP * CIN;           // bf16 elements per tile
+  // staging items per lane: (channel pair, 8 positions) -- CIN * HW / 8 single-channel 8-position units, two per
+  // item, 64 lanes
+  constexpr int ITER = CIN * G::HW / 8 / 2 / 64;
+  constexpr int NPIECE = ITER * 4;                    // pieces: 2 positions of one item
+  constexpr int MG = 2, NG = G::MT / MG;               // position tiles per MFMA group, groups per sample
+  static_assert(NPIECE < NG * KS, "the staging pieces and the next loads fit in one sample's k-steps");
+  static_assert((CIN * G::HW / 8) % 128 == 0 && G::MT % MG == 0, "geometry");
+  static_assert(32 * ITER == G::HW, "item k of lane l: positions 8 ((l >> 4) + 4 k) .. + 8 -- 4 lane groups x ITER");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
+  const int EC_in = E * CIN;
+  __bf16* tiles = reinterpret_cast<__bf16*>(smem) + wv * 2 * TILE;
+  for (int i = lane; i < 2 * TILE / 8; i += 64) reinterpret_cast<bf16x8*>(tiles)[i] = bf16x8{};
+  bf16x8* wl = reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(smem) + 8 * TILE);   // B fragments
+  float* stl = reinterpret_cast<float*>(wl + KS * 64);                                     // BN records
+  const int n0 = u * B + (chunk * 4 + wv) * spw;
+  const int nend = min((u + 1) * B, n0 + spw);
+  const int nlast = nend - 1;
+
+  // item k of this lane: channel pair pr = lane % 16 (the same for every k), positions [8 sg, 8 sg + 8)
+  const int pr = lane & 15;
+  // two register sets: the loads of sample n + 2 are issued during sample n, so every sample's data has a whole
+  // sample period (~1 us) to arrive before its staging reads it (one sample ahead it waited out the HBM latency)
+  uint4 ra[ITER][2], rb[ITER][2];
+  auto load = [&](uint4 (&rv)[ITER][2], int n) {
+    const size_t base = ((size_t)n * E + e) * CIN * G::HW;
+#pragma unroll
+    for (int k = 0; k < ITER; ++k) {
+      const int sg = (lane >> 4) + 4 * k;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+        rv[k][h2] = *reinterpret_cast<const uint4*>(xin + base + (size_t)(2 * pr + h2) * G::HW + 8 * sg);
+    }
+  };
+  f32x2 a2, b2;   // this lane's channel pair's BN affine (after the prologue)
+  // positions 2 jp, 2 jp + 1 of item k: BN + ReLU of both channels, one packed bf16 word per position
+  auto piece = [&](const uint4 (&rv)[ITER][2], __bf16* tile, int k, int jp) {
+    const int sg = (lane >> 4) + 4 * k, ph = (8 * sg) / W, pw = (8 * sg) % W;
+    const uint32_t w0 = (&rv[k][0].x)[jp], w1 = (&rv[k][1].x)[jp];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const uint32_t u0 = q ? (w0 & 0xffff0000u) : (w0 << 16);
+      const uint32_t u1 = q ? (w1 & 0xffff0000u) : (w1 << 16);
+      f32x2 y = f32x2{__uint_as_float(u0), __uint_as_float(u1)} * a2 + b2;
+      y.x = relu_max(y.x);
+      y.y = relu_max(y.y);
+      const int R = ph + 1, C = pw + 2 * jp + q + 1;
+      *reinterpret_cast<uint32_t*>(tile + (R * G::WP + C) * CIN + 8 * ((pr >> 2) ^ tile_swz(R, C)) + 2 * (pr & 3)) =
+          pack_bf16x2(y);
+    }
+  };
+
+  // the first two samples' loads fly during the prologue (branch-free: past the wave's last sample, re-load it)
+  if (n0 < nend) {
+    load(ra, n0);
+    load(rb, n0 + 1 <= nlast ? n0 + 1 : nlast);
+  }
+  {  // prologue: B fragments and the input BN records (conv3x3_body's)
+    constexpr int WPT = (KS * 64 + 255) / 256;
+    const bf16x8* wp = reinterpret_cast<const bf16x8*>(wt) + (size_t)e * KS * 64;
+    bf16x8 tw[WPT];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (tid + 256 * k < KS * 64) tw[k] = wp[tid + 256 * k];
+    float tp = 0.f;
+    const bool build = bnf.stats != nullptr;
+    if (!build) tp = st_in[((size_t)u * EC_in + e * CIN) * NST + tid];
+    if (build) bn_fwd_build<false>(bnf, stl, u, e, EC_in, chunk == 0);
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (tid + 256 * k < KS * 64) wl[tid + 256 * k] = tw[k];
+    if (!build) stl[tid] = tp;
+  }
+  __syncthreads();
+  a2 = f32x2{stl[(2 * pr) * NST + ST_A], stl[(2 * pr + 1) * NST + ST_A]};
+  b2 = f32x2{stl[(2 * pr) * NST + ST_B], stl[(2 * pr + 1) * NST + ST_B]};
+  if (n0 < nend) {   // the first sample staged up front (exposed), then set a takes sample n0 + 2
+#pragma unroll
+    for (int p = 0; p < NPIECE; ++p) piece(ra, tiles, p >> 2, p & 3);
+    load(ra, n0 + 2 <= nlast ? n0 + 2 : nlast);
+  }
+  f32x2 s1v = {0.f, 0.f}, s2v = {0.f, 0.f};
+  // sample n (tile cb): MFMAs over it; in their shadow sample n + 1 is staged from set `nx` into the other tile, and
+  // set nx then takes sample n + 3
+  auto sample = [&](int n, int cb, uint4 (&nx)[ITER][2]) {
+    const __bf16* cur = tiles + cb * TILE;
+    __bf16* nxt = tiles + (cb ^ 1) * TILE;
+    wave_lds_fence();   // this sample's tile is written (by this wave alone) and the other one free to rewrite
+    auto load_a = [&](int mt, int s) -> bf16x8 {
+      const int p = mt * 32 + l32, ph = p / W, pw = p % W;
+      const int tap = (16 * s) / CIN, q = ((16 * s) % CIN) / 8 + hh;
+      const int R = ph + tap / 3, C = pw + tap % 3;
+      return *reinterpret_cast<const bf16x8*>(cur + (R * G::WP + C) * CIN + 8 * (q ^ tile_swz(R, C)));
+    };
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      f32x16 acc[MG];
+      bf16x8 a_cur[MG], b_cur = wl[lane];
+#pragma unroll
+      for (int j = 0; j < MG; ++j) {
+        acc[j] = f32x16{};
+        a_cur[j] = load_a(g * MG + j, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        bf16x8 a_nxt[MG], b_nxt;
+        if (s + 1 < KS) {
+          b_nxt = wl[(s + 1) * 64 + lane];
+#pragma unroll
+          for (int j = 0; j < MG; ++j) a_nxt[j] = load_a(g * MG + j, s + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < MG; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_cur[j], b_cur, acc[j], 0, 0, 0);
+        // the next sample's staging in this k-step's MFMA shadow, then (registers free) the loads after it
+        const int p = g * KS + s;
+        if (p < NPIECE) piece(nx, nxt, p >> 2, p & 3);
+        if (p == NPIECE) load(nx, n + 3 <= nlast ? n + 3 : nlast);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < KS) {
+          b_cur = b_nxt;
+#pragma unroll
+          for (int j = 0; j < MG; ++j) a_cur[j] = a_nxt[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MG; ++j) {   // epilogue (conv3x3_body's OUT_Z_STATS)
+        const int mt = g * MG + j;
+        const size_t rbase = ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + mt * 32;
+        uint32_t pk[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pk[q][0] = pack_bf16x2(f32x2{acc[j][4 * q], acc[j][4 * q + 1]});
+          pk[q][1] = pack_bf16x2(f32x2{acc[j][4 * q + 2], acc[j][4 * q + 3]});
+          const f32x2 v01 = unpack_bf16x2(pk[q][0]), v23 = unpack_bf16x2(pk[q][1]);
+          s1v += v01 + v23;
+          s2v += v01 * v01 + v23 * v23;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+          for (int w = 0; w < 2; ++w) {
+            const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * q][w], pk[2 * q + 1][w], false, false);
+            pk[2 * q][w] = r[0];
+            pk[2 * q + 1][w] = r[1];
+          }
+          *reinterpret_cast<uint4*>(out + rbase + 8 * (2 * q + hh)) =
+              make_uint4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
+        }
+      }
+    }
+  };
+  for (int n = n0; n < nend; n += 2) {   // (by two: the register sets are named statically)
+    sample(n, 0, rb);                    // stages n + 1 from b, b takes n + 3
+    if (n + 1 < nend) sample(n + 1, 1, ra);   // stages n + 2 from a, a takes n + 4
+  }
+  float s1 = s1v.x + s1v.y, s2 = s2v.x + s2v.y;
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 32);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  if (hh == 0) {
+    red[(wv * 32 + l32) * 2] = s1;
+    red[(wv * 32 + l32) * 2 + 1] = s2;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = tid >> 1, k = tid & 1;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
+    stats[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;   // planar [2][EC] rows
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // conv_fwd_stack_kernel: the training forward of all three conv/BN/ReLU layers -- and the BN tail (layer 3's
 // records, h3 = relu(bn3(z3)) for the FC GEMM, the running statistics) -- as ONE persistent launch.
 // Workgroup (group u, chunk, expert e) runs conv3x3_body for layer 1, 2, 3 on the same samples, so each wave
@@ -1580,6 +1779,306 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
 }
 
 // ------------------------------------------------------------------------------------------
+// conv3x3_bwd_db_kernel (round 6): conv3x3_bwd_kernel (P128) software-pipelined over TWO stage buffers.  In
+// conv3x3_bwd_kernel every sample is staged by the whole workgroup between two barriers, and only then do the 4
+// waves run their 36 MFMAs; two workgroups per CU were meant to fill each other's gaps, but the kernel ran at
+// ~2.4 TB/s of its ~75 MB (31 us per layer, profiles/r5_46_step_kernel_stats.md).  Here one workgroup per CU
+// (136 KB of LDS) holds two buffers: while the MFMAs of sample n read buffer n & 1, every thread stages sample n + 1
+// into the other one in six pieces placed between the k-steps' MFMA pairs (the dz item's two 4-position halves, the
+// two x items' raw copy + transform and their shifted copies), and then issues sample n + 3's loads (two register
+// sets: each sample's loads get two sample periods to land).  One barrier per sample instead of two.  The
+// arithmetic and every summation order are conv3x3_bwd_kernel's: dx, the slab row and the BN partials are
+// bit-identical to it at the same chunking.
+// ------------------------------------------------------------------------------------------
+template <int W>
+struct BwdDbGeo {
+  using BG = BwdGeo<W>;
+  static constexpr int STG = BG::X_EL + BG::DZ_EL + BG::T_EL + BG::ZP_EL;   // 16-bit elements per stage buffer
+  static constexpr size_t SMEM_STAGE = 2 * (size_t)STG * 2 + BG::KSD * 64 * 16 + 2 * CO * NST * 4;
+  static constexpr size_t SMEM = SMEM_STAGE > BG::RED ? SMEM_STAGE : BG::RED;
+};
+
+template <int W>
+__global__ void __launch_bounds__(256, 1) conv3x3_bwd_db_kernel(const uint16_t* __restrict__ zprev,
+                                                             const float* __restrict__ st_prev,
+                                                             const uint16_t* __restrict__ dh,
+                                                             const uint16_t* __restrict__ z,
+                                                             const float* __restrict__ st, float* __restrict__ slab,
+                                                             const uint16_t* __restrict__ wt,
+                                                             uint16_t* __restrict__ dx, float* __restrict__ part, int E,
+                                                             int B, int chunks, int spb, BnBwd bnb, LossFinish lf) {
+  if ((int)blockIdx.y == E) {   // (as conv3x3_bwd_kernel: the extra row hosts the HDCE loss finish)
+    if (blockIdx.x == 0) loss_finish_body(lf);
+    return;
+  }
+  using BG = BwdGeo<W>;
+  using DB = BwdDbGeo<W>;
+  using G = typename BG::G;
+  constexpr int HW = G::HW, HP = G::HP, WP = G::WP, XCS = BG::XCS, DZS = BG::DZS;
+  constexpr int KSA = HW / 16;                  // wgrad k-steps (16 positions) per sample
+  static_assert(W == 8 && G::MT == 4, "P128: one dgrad position tile per wave, one dz item / two x items per thread");
+  static_assert(2 * KSA + KSA / 4 == 18, "wgrad steps pair with dgrad k-steps");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  auto X_of = [&](int b) { return reinterpret_cast<__bf16*>(smem) + b * DB::STG; };        // [kw][ci][row][w]
+  auto DZ_of = [&](int b) { return X_of(b) + BG::X_EL; };                                  // [co][p]
+  auto T_of = [&](int b) { return DZ_of(b) + BG::DZ_EL; };                                 // [pixel][32] swizzled
+  auto ZP_of = [&](int b) { return reinterpret_cast<uint16_t*>(T_of(b) + BG::T_EL); };     // [ci][p] raw z_prev
+  bf16x8* WB = reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(smem) + 2 * DB::STG);
+  float* prm = reinterpret_cast<float*>(WB + BG::KSD * 64);   // this layer's records (dz)
+  float* prp = prm + CO * NST;                               // previous layer's records (x, reduction)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int bx = blockIdx.x, e = blockIdx.y, u = bx / chunks, chunk = bx % chunks;
+  const int EC = E * CO;
+  const int n0 = u * B + chunk * spb, nend = min((u + 1) * B, n0 + spb), nlast = nend - 1;
+
+  // ---- zero both buffers' tiles (halos stay zero) and the halo rows of their shifted copies ----
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    for (int i = tid; i < BG::T_EL / 8; i += 256) reinterpret_cast<bf16x8*>(T_of(b))[i] = bf16x8{};
+    for (int i = tid; i < 3 * CO * 2; i += 256) {
+      const int cc = i >> 1, r = i & 1;
+      *reinterpret_cast<bf16x8*>(X_of(b) + cc * XCS + r * (HP - 1) * W) = bf16x8{};
+    }
+  }
+  // this thread's staging items: dz (channels 2 pr, 2 pr + 1; positions [p0, p0 + 8)), x rows (channel cx[j], row
+  // phx[j])
+  const int pr = tid & 15, p0 = (tid >> 4) * 8;
+  int cx[2], phx[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = tid + 256 * j;
+    cx[j] = i >> 4;
+    phx[j] = i & 15;
+  }
+  struct Set {
+    uint4 rd[2], rz[2], rx[2];
+  };
+  Set sa, sb;
+  auto load = [&](Set& r, int n) {
+    const size_t sbase = ((size_t)n * E + e) * CO * HW;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const size_t off = sbase + (size_t)(2 * pr + h2) * HW + p0;
+      r.rd[h2] = *reinterpret_cast<const uint4*>(dh + off);
+      r.rz[h2] = *reinterpret_cast<const uint4*>(z + off);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) r.rx[j] = *reinterpret_cast<const uint4*>(zprev + sbase + (size_t)cx[j] * HW + phx[j] * W);
+  };
+  // piece 0 / 1: dz of positions [p0 + 4 q, + 4), both channels -> DZ (two 8-byte rows) and T (4 words)
+  auto piece_dz = [&](const Set& r, int b, int q) {
+    __bf16* DZ = DZ_of(b);
+    __bf16* T = T_of(b);
+    float v[2][4];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int c = 2 * pr + h2;
+      const float* sc = prm + c * NST;
+      const float a = sc[ST_A], bb = sc[ST_B], mu = sc[ST_MEAN], inv = sc[ST_INV];
+      const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
+      const uint32_t dw[2] = {(&r.rd[h2].x)[2 * q], (&r.rd[h2].x)[2 * q + 1]};
+      const uint32_t zw[2] = {(&r.rz[h2].x)[2 * q], (&r.rz[h2].x)[2 * q + 1]};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t dk = dw[k >> 1], zk = zw[k >> 1];
+        const float d = __uint_as_float((k & 1) ? (dk & 0xffff0000u) : (dk << 16));
+        const float zz = __uint_as_float((k & 1) ? (zk & 0xffff0000u) : (zk << 16));
+        const float g = (a * zz + bb > 0.f) ? d : 0.f;
+        v[h2][k] = c1 * g - c2 - c3 * (zz - mu) * inv;
+      }
+      const uint32_t w0 = f32_to_bf16(v[h2][0]) | ((uint32_t)f32_to_bf16(v[h2][1]) << 16);
+      const uint32_t w1 = f32_to_bf16(v[h2][2]) | ((uint32_t)f32_to_bf16(v[h2][3]) << 16);
+      *reinterpret_cast<uint2*>(DZ + c * DZS + p0 + 4 * q) = make_uint2(w0, w1);
+    }
+    const int ph = p0 / W, pw = p0 % W;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t w2 = f32_to_bf16(v[0][k]) | ((uint32_t)f32_to_bf16(v[1][k]) << 16);
+      const int R = ph + 1, C = pw + 4 * q + k + 1;
+      *reinterpret_cast<uint32_t*>(T + (R * WP + C) * CO + 8 * ((pr >> 2) ^ tile_swz(R, C)) + 2 * (pr & 3)) = w2;
+    }
+  };
+  // piece 2 + j: x item j -- the raw z_prev row (for the reduction) and BN + ReLU into the 3 column-shifted copies
+  auto piece_x = [&](const Set& r, int b, int j) {
+    __bf16* X = X_of(b);
+    uint16_t* ZP = ZP_of(b);
+    const int c = cx[j], ph = phx[j];
+    float v[W + 2];
+    v[0] = 0.f;
+    v[W + 1] = 0.f;
+    unpack_q(r.rx[j], v + 1, (const uint16_t*)nullptr);
+    uint2* zp = reinterpret_cast<uint2*>(ZP + c * BG::ZPS + ph * W);
+    zp[0] = make_uint2(r.rx[j].x, r.rx[j].y);
+    zp[1] = make_uint2(r.rx[j].z, r.rx[j].w);
+    const float xa = prp[c * NST + ST_A], xb = prp[c * NST + ST_B];
+#pragma unroll
+    for (int q = 1; q <= W; ++q) v[q] = relu_nan(xa * v[q] + xb);
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = (__bf16)v[k + kw];   // column w holds x[w + kw - 1]
+      *reinterpret_cast<bf16x8*>(X + (kw * CO + c) * XCS + (ph + 1) * W) = o;
+    }
+  };
+
+  // ---- prologue: the first two samples' loads, the dgrad B fragments, both layers' BN records ----
+  if (n0 < nend) {
+    load(sa, n0);
+    load(sb, n0 + 1 <= nlast ? n0 + 1 : nlast);
+  }
+  {
+    constexpr int NW = BG::KSD * 64, WPT = (NW + 255) / 256;
+    const bf16x8* wp = reinterpret_cast<const bf16x8*>(wt) + (size_t)e * NW;
+    bf16x8 tw[WPT];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (tid + 256 * k < NW) tw[k] = wp[tid + 256 * k];
+    const float pv = st_prev[((size_t)u * EC + e * CO) * NST + tid];   // 32 channels x NST = one per thread
+    float cv = 0.f;
+    if (bnb.rslab) bn_bwd_build(bnb, st, prm, u, e, EC);
+    else cv = st[((size_t)u * EC + e * CO) * NST + tid];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (tid + 256 * k < NW) WB[tid + 256 * k] = tw[k];
+    prp[tid] = pv;
+    if (!bnb.rslab) prm[tid] = cv;
+  }
+  __syncthreads();
+  const float rmu = prp[l32 * NST + ST_MEAN], rinv = prp[l32 * NST + ST_INV];
+  const float ra = prp[l32 * NST + ST_A], rb = prp[l32 * NST + ST_B];
+  bf16x8 wreg[BG::KSD];   // the dgrad B fragments stay in registers (each wave reads them once)
+#pragma unroll
+  for (int k = 0; k < BG::KSD; ++k) wreg[k] = WB[k * 64 + lane];
+  if (n0 < nend) {   // the first sample staged up front (exposed), then set a takes sample n0 + 2
+    piece_dz(sa, 0, 0);
+    piece_dz(sa, 0, 1);
+    piece_x(sa, 0, 0);
+    piece_x(sa, 0, 1);
+    load(sa, n0 + 2 <= nlast ? n0 + 2 : nlast);
+  }
+
+  f32x16 accw[3];   // taps wv, wv + 4, and this wave's share of tap 8
+#pragma unroll
+  for (int t = 0; t < 3; ++t) accw[t] = f32x16{};
+  float s1 = 0.f, s2 = 0.f;
+  const int mt = wv;                             // this wave's dgrad position tile
+  auto sample = [&](int n, int cb, Set& nx) {
+    __syncthreads();   // buffer cb staged by every thread; everyone is done reading buffer cb ^ 1 (sample n - 1)
+    const __bf16* X = X_of(cb);
+    const __bf16* DZ = DZ_of(cb);
+    const __bf16* T = T_of(cb);
+    const uint16_t* ZP = ZP_of(cb);
+    uint2 zq[4];   // the previous layer's z at this lane's dx positions (for the reduction)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) zq[g] = *reinterpret_cast<const uint2*>(ZP + l32 * BG::ZPS + mt * 32 + 8 * g + 4 * hh);
+    const int p = mt * 32 + l32, ph = p / W, pw = p % W;
+    f32x16 acc = f32x16{};
+#pragma unroll
+    for (int s = 0; s < BG::KSD; ++s) {
+      const int tap = s >> 1, q = ((s & 1) << 1) + hh;
+      const int R = ph + tap / 3, C = pw + tap % 3;
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(T + (R * WP + C) * CO + 8 * (q ^ tile_swz(R, C)));
+      const int ws = s;   // (one dgrad tile per wave: the wgrad step index is the k-step's)
+      const int j = ws < 2 * KSA ? (ws & 1) : 2;
+      const int wtp = j == 0 ? wv : (j == 1 ? wv + 4 : 8);
+      const int ks = ws < 2 * KSA ? (ws >> 1) : wv * (KSA / 4) + ws - 2 * KSA;
+      const int q0 = ks * 16 + 8 * hh, xh = q0 / W, xw = q0 % W;
+      const bf16x8 bz = *reinterpret_cast<const bf16x8*>(DZ + l32 * DZS + q0);
+      const bf16x8 ax = *reinterpret_cast<const bf16x8*>(X + ((wtp % 3) * CO + l32) * XCS + (xh + wtp / 3) * W + xw);
+      __builtin_amdgcn_sched_barrier(0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, wreg[s], acc, 0, 0, 0);
+      accw[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, bz, accw[j], 0, 0, 0);
+      // the next sample's staging in this k-step's MFMA shadow (writes the other buffer), then its registers reload
+      if (s == 0) piece_dz(nx, cb ^ 1, 0);
+      if (s == 3) piece_dz(nx, cb ^ 1, 1);
+      if (s == 6) piece_x(nx, cb ^ 1, 0);
+      if (s == 9) piece_x(nx, cb ^ 1, 1);
+      if (s == 12) load(nx, n + 3 <= nlast ? n + 3 : nlast);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- dgrad epilogue (conv3x3_bwd_kernel's): lane holds input channel l32, positions mt*32 + 8g + 4hh + {0..3}
+    const size_t rbase = ((size_t)n * E + e) * CO * HW + (size_t)l32 * HW + mt * 32;
+    uint32_t pk[4][2];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      pk[g][0] = pack_bf16x2(f32x2{acc[4 * g], acc[4 * g + 1]});
+      pk[g][1] = pack_bf16x2(f32x2{acc[4 * g + 2], acc[4 * g + 3]});
+      const f32x2 d01 = unpack_bf16x2(pk[g][0]), d23 = unpack_bf16x2(pk[g][1]);
+      const float d[4] = {d01.x, d01.y, d23.x, d23.y};
+      const float zz[4] = {__uint_as_float(zq[g].x << 16), __uint_as_float(zq[g].x & 0xffff0000u),
+                           __uint_as_float(zq[g].y << 16), __uint_as_float(zq[g].y & 0xffff0000u)};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gg = (ra * zz[k] + rb > 0.f) ? d[k] : 0.f;
+        s1 += gg;
+        s2 += gg * (zz[k] - rmu) * rinv;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * q][w], pk[2 * q + 1][w], false, false);
+        pk[2 * q][w] = r[0];
+        pk[2 * q + 1][w] = r[1];
+      }
+      *reinterpret_cast<uint4*>(dx + rbase + 8 * (2 * q + hh)) =
+          make_uint4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
+    }
+  };
+  for (int n = n0; n < nend; n += 2) {          // (by two: the register sets are named statically)
+    sample(n, 0, sb);                           // stages n + 1 from b, b takes n + 3
+    if (n + 1 < nend) sample(n + 1, 1, sa);     // stages n + 2 from a, a takes n + 4
+  }
+
+  // ---- the previous layer's BN backward partials: half-waves, then the 4 waves through LDS ----
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 32);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  if (hh == 0) {
+    red[(wv * 32 + l32) * 2] = s1;
+    red[(wv * 32 + l32) * 2 + 1] = s2;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = tid >> 1, k = tid & 1;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
+    part[(((size_t)u * chunks + chunk) * 2 + k) * EC + e * CO + c] = t;   // planar [2][EC] rows
+  }
+  // ---- weight gradient rows (conv3x3_bwd_kernel's) ----
+  constexpr int RS = 9 * CO + 1;
+  __syncthreads();
+  float* wr = reinterpret_cast<float*>(smem);
+  float* p8 = wr + CO * RS;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ci = (r & 3) + 8 * (r >> 2) + 4 * hh;
+    wr[l32 * RS + ci * 9 + wv] = accw[0][r];
+    wr[l32 * RS + ci * 9 + wv + 4] = accw[1][r];
+    p8[(wv * CO + l32) * (CO + 1) + ci] = accw[2][r];
+  }
+  __syncthreads();
+  float* srow = slab + ((size_t)e * gridDim.x + bx) * CO * CO * 9;
+  for (int i = tid; i < CO * CO * 9; i += 256) {
+    const int co = i / (CO * 9), m = i % (CO * 9);
+    float v;
+    if (m % 9 == 8) {
+      const int ci = m / 9;
+      constexpr int P8 = CO + 1;
+      v = ((p8[co * P8 + ci] + p8[(CO + co) * P8 + ci]) + p8[(2 * CO + co) * P8 + ci]) + p8[(3 * CO + co) * P8 + ci];
+    } else {
+      v = wr[co * RS + m];
+    }
+    srow[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // BatchNorm pieces
 // ------------------------------------------------------------------------------------------
 // Forward statistics: per (u, ch) mean/invstd/(a,b); running stats updated in u order.
@@ -2117,6 +2616,20 @@ QD_API int qd_conv_fwd(int layer, const void* xin, const float* st_prev, const u
   return (int)hipGetLastError();
 }
 
+// qd_conv_fwd for layers 2 / 3 at P128 on the software-pipelined kernel (conv3x3_fwd_db_kernel): same arguments,
+// bit-identical outputs; hipErrorInvalidValue for other geometries (the caller keeps qd_conv_fwd then).
+QD_API int qd_conv_fwd_db(const uint16_t* xin, const float* st_prev, const uint16_t* w, uint16_t* z, float* stats,
+                          int N, int E, int B, int H, int W, int chunks, int spw, const BnFwd* bnf, void* stream) {
+  if (H != 16 || W != 8 || B <= 0 || N % B || chunks * 4 * spw < B) return (int)hipErrorInvalidValue;
+  const BnFwd bf = bnf ? *bnf : BnFwd{};
+  if (!bnf && !st_prev) return (int)hipErrorInvalidValue;
+  constexpr size_t smem = 8 * (size_t)18 * 10 * 32 * 2 + 18 * 64 * 16 + 32 * NST * sizeof(float);
+  if (hipError_t e = qd::allow_lds(conv3x3_fwd_db_kernel<8>, smem)) return (int)e;
+  hipLaunchKernelGGL(conv3x3_fwd_db_kernel<8>, dim3((N / B) * chunks, E), dim3(256), smem, (hipStream_t)stream, xin,
+                     st_prev, w, z, stats, E, B, chunks, spw, bf);
+  return (int)hipGetLastError();
+}
+
 // The persistent training forward (conv_fwd_stack_kernel).  sync: (U*E)*2 + E*3 + 1 zero-initialised words --
 // the barriers, the per-(expert, layer) arrival counts and the error word (all return to zero after a launch, the
 // error word excepted).  Returns hipErrorInvalidValue when the shapes do not fit and hipErrorInvalidConfiguration
@@ -2302,6 +2815,23 @@ QD_API int qd_conv_bwd_fused(const uint16_t* zprev, const float* st_prev, const 
     hipLaunchKernelGGL((conv3x3_bwd_kernel<WW>), grid, dim3(256), sm, s, zprev, st_prev, dh, z, st, slab, w, dx, part,
                        E, B, chunks, spb, bb, lff);
   })
+  return (int)hipGetLastError();
+}
+
+// qd_conv_bwd_fused at P128 on the software-pipelined kernel (conv3x3_bwd_db_kernel): same arguments and outputs
+// (bit-identical at the same chunking); hipErrorInvalidValue for other geometries.
+QD_API int qd_conv_bwd_db(const uint16_t* zprev, const float* st_prev, const uint16_t* dh, const uint16_t* z,
+                          const float* st, float* slab, const uint16_t* w, uint16_t* dx, float* part, int N, int E,
+                          int B, int H, int W, int chunks, int spb, const BnBwd* bnb, const qd::LossFinish* lf,
+                          void* stream) {
+  if (H != 16 || W != 8 || chunks * spb < B || N % B) return (int)hipErrorInvalidValue;
+  const BnBwd bb = bnb ? *bnb : BnBwd{};
+  const qd::LossFinish lff = lf ? *lf : qd::LossFinish{};
+  const size_t sm = BwdDbGeo<8>::SMEM;
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (hipError_t e = qd::allow_lds(conv3x3_bwd_db_kernel<8>, sm)) return (int)e;
+  hipLaunchKernelGGL(conv3x3_bwd_db_kernel<8>, dim3((N / B) * chunks, E + (lf ? 1 : 0)), dim3(256), sm,
+                     (hipStream_t)stream, zprev, st_prev, dh, z, st, slab, w, dx, part, E, B, chunks, spb, bb, lff);
   return (int)hipGetLastError();
 }
 

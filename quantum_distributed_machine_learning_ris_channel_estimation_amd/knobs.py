@@ -64,6 +64,13 @@ class Knobs:
     # layer's time: 0.3869 / 0.3879 against 0.3909 / 0.3909 ms, and 0.4081 / 0.4066 against 0.4102 / 0.4084 on another
     # box (profiles/r5_18_spw_stack_window_ab.txt, r5_10_ab.txt)
     conv_spw: int = 3
+    # (round 6) layers 2 / 3 of the P128 training forward on conv3x3_fwd_db_kernel: per wave, the next sample's staging
+    # runs in the current sample's MFMA shadow (two LDS tiles); bit-identical to conv3x3_kernel
+    conv_fwd_db: bool = False
+    # (round 6) layers 3 / 2's fused backward at P128 on conv3x3_bwd_db_kernel (two stage buffers: the next sample staged
+    # in the current one's MFMA shadow), conv_spb_db samples per workgroup -- 10: 234 workgroups, one per CU
+    conv_bwd_db: bool = False
+    conv_spb_db: int = 10
     conv_spb_f: int = 5
     conv_spb_w1: int = 4
 

@@ -54,7 +54,8 @@ class ConvStackHIP:
     """Grouped (experts-in-channels) 3-layer conv/BN/ReLU on (N, E*2, H, W) pilots."""
 
     def __init__(self, model, U: int, B: int, spw: int = 3, spb_w: int = 8, spb_r: int = 4, spb_w1: int = 4,
-                 dx_bf16: bool = True, bwd_fused: Optional[bool] = None, spb_f: int = 5):
+                 dx_bf16: bool = True, bwd_fused: Optional[bool] = None, spb_f: int = 5,
+                 spb_db: Optional[int] = None):
         self.m = model
         self.count_batches = False   # set by the owner that stops counting num_batches_tracked itself
         self.stage_hook = None       # optional callable(stage name) between forward launches
@@ -75,6 +76,11 @@ class ConvStackHIP:
         # left half the CUs with one and measured slower than the side-by-side wd kernel).
         # bwd_fused=False: wgrad and dgrad as separate workgroups of the wd kernel (tests compare the two).
         self.bwd_fused = (True if bwd_fused is None else bool(bwd_fused)) and dx_bf16
+        # (round 6) P128: the fused backward software-pipelined over two stage buffers (conv3x3_bwd_db_kernel), one
+        # workgroup per CU with spb_db samples each (bit-identical to conv3x3_bwd_kernel at the same chunking)
+        self.bwd_db = self.bwd_fused and bool(KNOBS.conv_bwd_db) and model.H == 16 and model.W == 8
+        if self.bwd_db:
+            spb_f = KNOBS.conv_spb_db if spb_db is None else spb_db
         # layer 1 (2 input channels) is one accumulator tile: staging-bound, so more, shorter workgroups
         self.spb_wl = (spb_w1, spb_f, spb_f) if self.bwd_fused else (spb_w1, spb_w, spb_w)
         self.chunks_wl = tuple((B + s - 1) // s for s in self.spb_wl)
@@ -129,6 +135,9 @@ class ConvStackHIP:
         self.lib = nat.hip_lib()
         L = self.lib
         self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
+        # layers 2 / 3 at P128: the software-pipelined forward (two LDS tiles per wave; bit-identical outputs)
+        self._fwd_db = nat.fn(L, "qd_conv_fwd_db", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
+        self.fwd_db = bool(KNOBS.conv_fwd_db) and self.W == 8 and self.H == 16
         self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p])
         self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
         self._fin = nat.fn(L, "qd_bn_stats_finalize_multi", [_i, _p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _f, _f, _i,
@@ -151,7 +160,7 @@ class ConvStackHIP:
                                                         _p, _p, _p])
         # (bwd_fused off) wgrad + dgrad of layers 3 and 2 as one launch each
         self.fuse_wd = True
-        self._bwdf = nat.fn(L, "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p, _p])
+        self._bwdf = nat.fn(L, "qd_conv_bwd_db" if self.bwd_db else "qd_conv_bwd_fused", [_p] * 9 + [_i] * 7 + [_p, _p, _p])
         # layer 3's BN backward partials from the FC data gradient's epilogue (enable_dgrad_bnred): 0 = own launch
         self.bnred_mt = 0
         self._fwd8 = nat.fn(L, "qd_conv_fwd_f8", [_p] * 4 + [_i] * 7 + [_p] * 6)
@@ -240,6 +249,11 @@ class ConvStackHIP:
                                      self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw, ctypes.byref(bnf),
                                      nat.ptr(f8.qs[j:]), nat.ptr(f8.scale[j:]), nat.ptr(f8.amax[j]),
                                      nat.ptr(f8.amax[j + 1]), st), f"conv_fwd_f8_{k + 1}")
+            elif k > 0 and self.fwd_db:
+                nat.check(self._fwd_db(nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
+                                       nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks,
+                                       self.spw, ctypes.byref(bnf) if bnf is not None else None, st),
+                          f"conv_fwd_db{k + 1}")
             else:
                 nat.check(self._fwd(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
                                     nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks,

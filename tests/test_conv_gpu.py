@@ -370,3 +370,64 @@ def test_f8_dgrad_bn_reduction_epilogue_matches_its_own_launch(cuda, monkeypatch
     assert float(gf.abs().max()) > 0
     assert rel(xf, xr) < 1e-4, rel(xf, xr)
     assert rel(gf, gr) < 1e-4, rel(gf, gr)
+
+
+@pytest.mark.parametrize("B", [256, 40, 7])
+def test_conv_forward_pipelined_matches_conv3x3_kernel(cuda, monkeypatch, B):
+    """Round 6: layers 2 / 3 on conv3x3_fwd_db_kernel (the next sample staged in the current one's MFMA shadow, two
+    LDS tiles per wave) against conv3x3_kernel, 3 steps on fresh inputs: z, h3, the BN records and the running
+    statistics bit for bit (the same MFMA order, statistics order and partials).  B 40 / 7: partial chunks and
+    waves with one or no sample."""
+    U = 3
+    outs = []
+    for db in (False, True):
+        monkeypatch.setattr(KNOBS, "conv_fwd_db", db)
+        a, _ = pair(cuda, 128)
+        conv = ConvStackHIP(a, U, B)
+        assert conv.fwd_db == db
+        steps = []
+        for step in range(3):
+            torch.manual_seed(20 + step)
+            Yp = torch.randn(3, U, B, 2, a.H, a.W, device=cuda) * (1 + step)
+            h3 = conv.forward(a.pack_input(Yp).contiguous(), training=True)
+            torch.cuda.synchronize()
+            steps.append([h3.clone()] + [conv.z[k].clone() for k in range(3)] + [conv.st[k].clone() for k in range(3)]
+                         + [conv.stats[k].clone() for k in range(3)])
+        outs.append((steps, [t.clone() for t in a.run_mean + a.run_var]))
+    (s0, r0), (s1, r1) = outs
+    for i, (x, y) in enumerate(zip(s0, s1)):
+        for j, (p, q) in enumerate(zip(x, y)):
+            assert torch.equal(p, q), (i, j, float((p.float() - q.float()).abs().max()))
+    for x, y in zip(r0, r1):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("B,spb", [(256, 10), (40, 10), (256, 7), (9, 4)])
+def test_conv_backward_pipelined_matches_conv3x3_bwd_kernel(cuda, monkeypatch, B, spb):
+    """Round 6: layers 3 / 2's fused backward on conv3x3_bwd_db_kernel (two stage buffers, the next sample staged in
+    the current one's MFMA shadow) against conv3x3_bwd_kernel at the same chunking: dx, every weight / BN gradient
+    bit for bit (same MFMA order, same slab and partial layout and summation order).  Odd spb / small B: a partial
+    last workgroup, odd sample counts (the by-two sample loop's tail)."""
+    U = 3
+    outs = []
+    for db in (False, True):
+        monkeypatch.setattr(KNOBS, "conv_bwd_db", db)
+        a, _ = pair(cuda, 128)
+        torch.manual_seed(1)
+        Yp = torch.randn(3, U, B, 2, a.H, a.W, device=cuda)
+        conv = ConvStackHIP(a, U, B, spb_f=spb, spb_db=spb)
+        assert conv.bwd_db == db and conv.spb_wl[1:] == (spb, spb)
+        conv.forward(a.pack_input(Yp).contiguous(), training=True)
+        res = []
+        for step in range(2):
+            torch.manual_seed(5 + step)
+            dh = torch.randn(U * B * 3, 32 * a.H * a.W, device=cuda).to(torch.bfloat16)
+            a.space.zero_grad()
+            conv.backward(dh)
+            torch.cuda.synchronize()
+            res.append([conv.dx[0].clone(), conv.dx[1].clone()] + [a.conv_w[k].grad.clone() for k in range(3)]
+                       + [a.bn_w[k].grad.clone() for k in range(3)] + [a.bn_b[k].grad.clone() for k in range(3)])
+        outs.append(res)
+    for i, (x, y) in enumerate(zip(*outs)):
+        for j, (p, q) in enumerate(zip(x, y)):
+            assert torch.equal(p, q), (i, j, float((p.float() - q.float()).abs().max()))
