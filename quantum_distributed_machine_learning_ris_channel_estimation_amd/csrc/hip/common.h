@@ -50,6 +50,23 @@ __device__ __forceinline__ unsigned long long phase_stamp() {
   return t;
 }
 
+// BatchNorm + ReLU backward pieces with every rounding explicit.  The same quantities are computed in several kernels
+// (conv.hip: the dgrad / wgrad / fused-backward stagings, the BN-reduction epilogues and launch; gemm.hip: the FC data
+// gradient's BN-reduction epilogue); with plain expressions each kernel's FMA contraction (-ffp-contract=fast) was
+// the compiler's choice in that context, so a dz could differ by one bf16 rounding between two kernels computing
+// the same thing.  Explicit: bitwise the same values in every kernel.
+//   gate  : the ReLU passed, a z + b > 0 (fma)           xhat : (z - mean) * invstd
+//   dz    : c1 g - c2 - c3 xhat                           red  : s1 += g, s2 += g xhat (fma)
+__device__ __forceinline__ bool bn_gate(float a, float z, float b) { return __fmaf_rn(a, z, b) > 0.f; }
+__device__ __forceinline__ float bn_xhat(float z, float mu, float inv) { return __fmul_rn(__fsub_rn(z, mu), inv); }
+__device__ __forceinline__ float bn_dz(float g, float xh, float c1, float c2, float c3) {
+  return __fsub_rn(__fsub_rn(__fmul_rn(c1, g), c2), __fmul_rn(c3, xh));
+}
+__device__ __forceinline__ void bn_red(float& s1, float& s2, float g, float xh) {
+  s1 = __fadd_rn(s1, g);
+  s2 = __fmaf_rn(g, xh, s2);
+}
+
 // torch semantics for non-finite inputs: relu / max propagate NaN (v_max_f32 would return the non-NaN
 // operand and silently turn a NaN batch into zeros -- and a finite loss the NaN guard never sees)
 __device__ __forceinline__ float relu_nan(float v) { return v < 0.f ? 0.f : v; }

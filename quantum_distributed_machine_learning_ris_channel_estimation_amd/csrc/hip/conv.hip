@@ -385,8 +385,8 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
             const float c1 = sc[ST_C1], c2 = sc[ST_C2], c3 = sc[ST_C3];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              const float g = (a * z[j] + b > 0.f) ? v[j] : 0.f;
-              v[j] = c1 * g - c2 - c3 * (z[j] - mu) * inv;
+              const float g = bn_gate(a, z[j], b) ? v[j] : 0.f;
+              v[j] = bn_dz(g, bn_xhat(z[j], mu, inv), c1, c2, c3);
             }
           }
         }
@@ -552,9 +552,8 @@ __device__ __forceinline__ void conv3x3_body(const TIN* __restrict__ xin, const 
                                      __uint_as_float(zq[j][g].y << 16), __uint_as_float(zq[j][g].y & 0xffff0000u)};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                  const float gg = (ra * zz[q] + rb > 0.f) ? d[q] : 0.f;
-                  s1 += gg;
-                  s2 += gg * (zz[q] - rmu) * rinv;
+                  const float gg = bn_gate(ra, zz[q], rb) ? d[q] : 0.f;
+                  bn_red(s1, s2, gg, bn_xhat(zz[q], rmu, rinv));
                 }
               }
             }
@@ -1387,8 +1386,8 @@ __device__ __forceinline__ void conv3x3_wgrad_body(const TIN* __restrict__ xin, 
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float g = (da * zz[j] + db > 0.f) ? d[j] : 0.f;
-        o[j] = (__bf16)(dc1 * g - dc2 - dc3 * (zz[j] - dmu) * dinv);
+        const float g = bn_gate(da, zz[j], db) ? d[j] : 0.f;
+        o[j] = (__bf16)bn_dz(g, bn_xhat(zz[j], dmu, dinv), dc1, dc2, dc3);
       }
       *reinterpret_cast<bf16x8*>(DZ + c * DZS + p0) = o;
     }
@@ -1592,8 +1591,8 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
         uint32_t w4[4];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float g = (a * zz[k] + b > 0.f) ? d[k] : 0.f;
-          v[h2][k] = c1 * g - c2 - c3 * (zz[k] - mu) * inv;
+          const float g = bn_gate(a, zz[k], b) ? d[k] : 0.f;
+          v[h2][k] = bn_dz(g, bn_xhat(zz[k], mu, inv), c1, c2, c3);
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -1713,9 +1712,8 @@ __global__ void __launch_bounds__(256, W == 8 ? 2 : 1) conv3x3_bwd_kernel(const 
                              __uint_as_float(zq[g].y << 16), __uint_as_float(zq[g].y & 0xffff0000u)};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float gg = (ra * zz[k] + rb > 0.f) ? d[k] : 0.f;
-          s1 += gg;
-          s2 += gg * (zz[k] - rmu) * rinv;
+          const float gg = bn_gate(ra, zz[k], rb) ? d[k] : 0.f;
+          bn_red(s1, s2, gg, bn_xhat(zz[k], rmu, rinv));
         }
       }
 #pragma unroll
@@ -1884,8 +1882,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_bwd_db_kernel(const uint16_t* 
         const uint32_t dk = dw[k >> 1], zk = zw[k >> 1];
         const float d = __uint_as_float((k & 1) ? (dk & 0xffff0000u) : (dk << 16));
         const float zz = __uint_as_float((k & 1) ? (zk & 0xffff0000u) : (zk << 16));
-        const float g = (a * zz + bb > 0.f) ? d : 0.f;
-        v[h2][k] = c1 * g - c2 - c3 * (zz - mu) * inv;
+        const float g = bn_gate(a, zz, bb) ? d : 0.f;
+        v[h2][k] = bn_dz(g, bn_xhat(zz, mu, inv), c1, c2, c3);
       }
       const uint32_t w0 = f32_to_bf16(v[h2][0]) | ((uint32_t)f32_to_bf16(v[h2][1]) << 16);
       const uint32_t w1 = f32_to_bf16(v[h2][2]) | ((uint32_t)f32_to_bf16(v[h2][3]) << 16);
@@ -2011,9 +2009,8 @@ __global__ void __launch_bounds__(256, 1) conv3x3_bwd_db_kernel(const uint16_t* 
                            __uint_as_float(zq[g].y << 16), __uint_as_float(zq[g].y & 0xffff0000u)};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float gg = (ra * zz[k] + rb > 0.f) ? d[k] : 0.f;
-        s1 += gg;
-        s2 += gg * (zz[k] - rmu) * rinv;
+        const float gg = bn_gate(ra, zz[k], rb) ? d[k] : 0.f;
+        bn_red(s1, s2, gg, bn_xhat(zz[k], rmu, rinv));
       }
     }
 #pragma unroll
@@ -2216,9 +2213,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const TDH* __restric
       for (int qi = 0; qi < QN; ++qi)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float g = (a[k] * zz[k][qi][j] + b[k] > 0.f) ? d[k][qi][j] : 0.f;
-          tg += g;
-          tgx += g * (zz[k][qi][j] - mu[k]) * inv[k];
+          const float g = bn_gate(a[k], zz[k][qi][j], b[k]) ? d[k][qi][j] : 0.f;
+          bn_red(tg, tgx, g, bn_xhat(zz[k][qi][j], mu[k], inv[k]));
         }
       if (!ok[k]) continue;
       if ((it0 + k) & 1) {

@@ -589,9 +589,8 @@ __device__ __forceinline__ void bnred_epilogue(const Args& a, const float* ct, u
     float tg = 0.f, tgx = 0.f;
 #pragma unroll
     for (int q = 0; q < VEC; ++q) {
-      const float g = (r.z * zz[q] + r.w > 0.f) ? d[q] : 0.f;
-      tg += g;
-      tgx += g * (zz[q] - r.x) * r.y;
+      const float g = bn_gate(r.z, zz[q], r.w) ? d[q] : 0.f;
+      bn_red(tg, tgx, g, bn_xhat(zz[q], r.x, r.y));
     }
     if (hi) {
       s[1][j][0] += tg;
