@@ -5,6 +5,8 @@
 set -o pipefail
 cd "$(dirname "$0")/../.." || exit 1
 R=$(pwd); O=$R/gpurun_out; P=r6_01
+timeout -k 10 120 python scripts/probes/probe_pkfma_war.py 4000 256 > $O/${P}_pkfma_war.txt 2>&1 || { tail -20 $O/${P}_pkfma_war.txt; exit 1; }
+cat $O/${P}_pkfma_war.txt
 timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread -k pipelined > $O/${P}_pytest_db.log 2>&1 || { tail -30 $O/${P}_pytest_db.log; exit 1; }
 tail -2 $O/${P}_pytest_db.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/${P}_pytest.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/${P}_pytest.log
