@@ -188,13 +188,28 @@ def main() -> int:
                              hdce_priority=args.hdce_priority, qsc_grid_bwd=args.qsc_grid_bwd)
         return FlagshipTrainer(cfg, ctx, store=store)
 
+    def warm(tr: FlagshipTrainer, n: int) -> None:
+        """Capture every graph set run(n) will replay and replay each once (a fresh graph's first replays run
+        slower, profiles/r3_01_window.txt): untimed steps."""
+        tr.prepare(n)
+        for kk in sorted(set(tr._reps(n))):
+            tr._replay(kk)
+
     def timed(tr: FlagshipTrainer, n: int, settle: int = 0):
         """(seconds of n timed steps, max over ranks; host enqueue seconds).  ``settle``: untimed steps
         replayed first, after any capture (every rank runs the same count: they hold collectives)."""
         tr.prepare(n)   # (graph capture, if the timed run needs a set the warm-up did not)
         if settle > 0:
             k = tr._k()
-            tr.run((settle + k - 1) // k * k)
+            ns = (settle + k - 1) // k * k
+            sync()
+            t0 = time.perf_counter()
+            tr.run(ns)
+            sync()
+            # the replay plan from this box's measured rates: GPU seconds per step (this settle run, 5 % margin) and
+            # host submission seconds per step (its small replays) -- FlagshipTrainer._reps_calibrated
+            tr.calibrate(0.95 * (time.perf_counter() - t0) / ns)
+            warm(tr, n)
         sync()
         ctx.barrier()
         sync()
@@ -259,6 +274,7 @@ def main() -> int:
     spread = None
     if ctx.device.type == "cuda" and args.spread_windows > 0:
         k = tr._k()
+        warm(tr, k)   # (the windows' graph sets captured and warmed outside them)
         evs = []
         for _ in range(args.spread_windows):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -299,6 +315,8 @@ def main() -> int:
             "lead_in": args.lead_in,
             "ramp": args.ramp,
             "replays": tr._reps(args.steps),
+            "replay_rates_ms": [round(1e3 * v, 4) if v else None for v in (getattr(tr, "_h_est", None),
+                                                                           getattr(tr, "_g_est", None))],
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "host_ms_per_step": round(host / args.steps * 1e3, 4),
             "higher_is_better": True,

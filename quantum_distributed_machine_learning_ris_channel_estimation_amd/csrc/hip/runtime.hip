@@ -340,6 +340,10 @@ __global__ void __launch_bounds__(512) pkfma_war_probe_kernel(int mode, int iter
     const float a0 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, acc.x)));
     const float a1 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, acc.y)));
     const bool bad = acc.x != a0 || acc.y != a1;
+    if (it == 0 && blockIdx.x == 0 && wv == 0) {   // (diagnostic dump: wave 0's lanes, first iteration)
+      out[4 + 2 * (threadIdx.x & 63)] = __builtin_bit_cast(unsigned int, acc.x);
+      out[5 + 2 * (threadIdx.x & 63)] = __builtin_bit_cast(unsigned int, acc.y);
+    }
     const unsigned long long m = __ballot(bad);
     if (m != 0ull) {
       ++events;
@@ -352,8 +356,9 @@ __global__ void __launch_bounds__(512) pkfma_war_probe_kernel(int mode, int iter
 }  // namespace rt
 }  // namespace qd
 
-// out: 4 zero-initialised u32 -- [0] non-uniform (iteration, wave) events, [1] (iteration, wave) pairs run,
-// [2] (unused), [3] OR of the lane masks (both halves folded) of the events.  grid workgroups of 8 waves.
+// out: 132 zero-initialised u32 -- [0] non-uniform (iteration, wave) events, [1] (iteration, wave) pairs run,
+// [2] (unused), [3] OR of the lane masks (both halves folded) of the events, [4 + 2 l .. +1] lane l's (acc.x, acc.y)
+// of block 0 / wave 0 / iteration 0 (as float bits).  grid workgroups of 8 waves.
 extern "C" int qd_pkfma_war_probe(int mode, int iters, int grid, unsigned int* out, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int pad = (mode & 8) ? 2 : (mode & 4) ? 1 : 0;

@@ -39,6 +39,7 @@ its own stream and overlaps the next step's gather + conv forward.
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -606,6 +607,10 @@ class FlagshipTrainer(DPPlan):
         head = [1] * max(0, self.cfg.lead_in)
         if head and 1 < self.cfg.ramp < k:
             head.append(self.cfg.ramp)
+        fit = self.store.n // ((GraphedStep.WARMUP + 1) * self.Bg)   # (what _capture_set can hold: see _k)
+        h, g = getattr(self, "_h_est", None), getattr(self, "_g_est", None)
+        if head and h and g and g > h:
+            return self._reps_calibrated(n, k, fit, h, g)
         reps, rem = [], n
         for r in head:
             if rem == 0:
@@ -613,11 +618,53 @@ class FlagshipTrainer(DPPlan):
             reps.append(min(r, rem))
             rem -= reps[-1]
         body, tail = [k] * (rem // k), rem % k
-        fit = self.store.n // ((GraphedStep.WARMUP + 1) * self.Bg)   # (what _capture_set can hold: see _k)
         if tail and body and k + tail <= fit:
             body[-1] += tail
             tail = 0
         return reps + body + ([tail] if tail else [])
+
+    BOUNDARY_S = 30e-6   # what a replay boundary costs the GPU (both chains drain and refill): bench windows, r5-r6
+
+    def _reps_calibrated(self, n: int, k: int, fit: int, h: float, g: float):
+        """The replay plan from measured rates (``calibrate``): h host seconds to submit one step of a graph, g GPU
+        seconds per step.  A replay only starts on the GPU once its submission is complete, so after the 1-step lead-in
+        each replay is as long as the GPU work already queued can hide:  h (S + r) <= h + g S + b i  for the steps S
+        submitted before it (i replays, b a boundary) -- growing geometrically at ratio ~g / h -- capped at ``fit``
+        steps per graph, and the steady state in k-step (or longer, up to fit) replays.  With h 0.07 and g 0.39 ms the
+        driver's 20-step window is [1, 5, 14]; with h 0.125 it is [1, 2, 6, 11] (round 6: a fixed [1, 4, 15] left the
+        GPU idle 0.4 ms for the 15-step submission at h 0.125, profiles/r6_01_bench20_2.json)."""
+        b = self.BOUNDARY_S
+        h = 1.2 * h   # (a 20 % margin: the host's pace varies between replays)
+        reps, S = [1], 1
+        while S < n:
+            allowed = int((h + (g - h) * S + b * len(reps)) / h)
+            r = max(1, min(allowed, fit, n - S))
+            if n - S - r and n - S - r < max(2, k // 2) and n - S <= fit:   # (no tiny tail replay)
+                r = n - S
+            reps.append(r)
+            S += r
+        return reps
+
+    def note_submission(self, k: int, seconds: float) -> None:
+        """(host submission rate) seconds the host spent submitting a k-step replay; small replays only -- a long run
+        blocks on the full launch queue, which is not submission cost."""
+        subs = getattr(self, "_subs", None)
+        if subs is None:
+            subs = self._subs = []
+        if k <= 4:
+            subs.append(seconds / k)
+            del subs[:-32]
+
+    def calibrate(self, gpu_s_per_step: float, host_s_per_step: Optional[float] = None) -> None:
+        """Rates for the replay plan (``_reps_calibrated``): the GPU's seconds per step (e.g. a synchronised run's wall
+        time per step) and the host's submission seconds per step (default: the median of the small replays
+        submitted so far).  World > 1: the slowest rank's host and GPU rates, so every rank runs the same plan."""
+        if host_s_per_step is None:
+            subs = sorted(getattr(self, "_subs", []) or [0.1e-3])
+            host_s_per_step = subs[len(subs) // 2]
+        h = self.ctx.max_scalar(float(host_s_per_step)) if self.ctx.world > 1 else float(host_s_per_step)
+        g = self.ctx.max_scalar(float(gpu_s_per_step)) if self.ctx.world > 1 else float(gpu_s_per_step)
+        self._h_est, self._g_est = h, g
 
     def prepare(self, n: int) -> None:
         """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""
@@ -641,7 +688,9 @@ class FlagshipTrainer(DPPlan):
             self.capture(preserve=True, k=k)
         self.next_batch(k)
         if len(gs) == 1:
+            t0 = time.perf_counter()
             gs[0]()
+            self.note_submission(k, time.perf_counter() - t0)
             return
         self._dp_run(*gs, fence=fence)
 

@@ -22,11 +22,12 @@ MODES = [(0, "v_pk_fma_f32, idle partners"), (1, "v_pk_fma_f32, MFMA partners"),
 
 def run(mode: int, iters: int, grid: int):
     f = nat.fn(nat.hip_lib(), "qd_pkfma_war_probe", [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p])
-    out = torch.zeros(4, dtype=torch.int32, device="cuda")
+    out = torch.zeros(132, dtype=torch.int32, device="cuda")
     nat.check(f(mode, iters, grid, nat.ptr(out), nat.stream_ptr(out.device)), "pkfma_war_probe")
     torch.cuda.synchronize()
-    ev, n, _, mask = [int(v) & 0xffffffff for v in out.tolist()]
-    return ev, n, mask
+    ev, n, _, mask = [int(v) & 0xffffffff for v in out[:4].tolist()]
+    lanes = out[4:].view(torch.float32).view(64, 2).cpu()
+    return ev, n, mask, lanes
 
 
 def main():
@@ -34,9 +35,12 @@ def main():
     grid = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     print(f"iters {iters} per probe wave, grid {grid} x (4 probe + 4 partner waves)")
     for mode, name in MODES:
-        ev, n, mask = run(mode, iters, grid)
+        ev, n, mask, vals = run(mode, iters, grid)
         lanes = [i for i in range(32) if mask >> i & 1]
         print(f"mode {mode:2d} {name:46s} events {ev:8d} / {n:9d}  lanes (mod 32) {lanes}", flush=True)
+        if ev:
+            print("   wave 0, iteration 0, acc (x, y) of lanes 0 / 15 / 16 / 31 / 32 / 47 / 48 / 63:",
+                  [tuple(round(float(v), 6) for v in vals[i]) for i in (0, 15, 16, 31, 32, 47, 48, 63)], flush=True)
 
 
 if __name__ == "__main__":

@@ -14,6 +14,18 @@ import csv
 from collections import defaultdict
 
 
+def load_trace(path):
+    """Kernel dispatch rows {Kernel_Name, Start_Timestamp, End_Timestamp}: from rocprofv3's CSV kernel trace, or
+    from its rocpd SQLite database (ROCm 7.2's default output: the ``kernels`` view)."""
+    if path.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(path)
+        return [{"Kernel_Name": n, "Start_Timestamp": str(a), "End_Timestamp": str(b)}
+                for n, a, b in con.execute("select name, start, end from kernels")]
+    return list(csv.DictReader(open(path)))
+
+
+
 def from_stats(path, steps, top):
     rows = list(csv.DictReader(open(path)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
@@ -26,7 +38,7 @@ def from_stats(path, steps, top):
 
 
 def from_trace(path, marker, per_step, tail, top):
-    rows = list(csv.DictReader(open(path)))
+    rows = load_trace(path)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = rows[int(len(rows) * (1 - tail)):]
     # start the window at a marker so partial steps at the edge do not skew the counts
@@ -76,7 +88,7 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     a = ap.parse_args()
     top = a.top_pos or a.top
-    if "trace" in a.path:
+    if "trace" in a.path or a.path.endswith(".db"):
         from_trace(a.path, a.marker, a.per_step, a.tail, top)
     else:
         from_stats(a.path, a.steps, top)

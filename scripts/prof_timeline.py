@@ -8,13 +8,25 @@ import argparse
 import csv
 
 
+def load_trace(path):
+    """Kernel dispatch rows {Kernel_Name, Start_Timestamp, End_Timestamp}: from rocprofv3's CSV kernel trace, or
+    from its rocpd SQLite database (ROCm 7.2's default output: the ``kernels`` view)."""
+    if path.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(path)
+        return [{"Kernel_Name": n, "Start_Timestamp": str(a), "End_Timestamp": str(b)}
+                for n, a, b in con.execute("select name, start, end from kernels")]
+    return list(csv.DictReader(open(path)))
+
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
     ap.add_argument("--marker", default="gather_step_kernel")
     ap.add_argument("--back", type=int, default=20, help="which step, counted from the end")
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.path)))
+    rows = load_trace(a.path)
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     lo, hi = idx[-a.back], idx[-a.back + 1]

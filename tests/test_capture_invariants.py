@@ -205,3 +205,27 @@ def test_replay_plan(n, k, lead, ramp, want):
     # every graph set of the 20-step window is replayed by the 30-step settle run before it
     if n == 20 and k == 10:
         assert set(got) <= set(FlagshipTrainer._reps(fake, 30))
+
+
+@pytest.mark.parametrize("h,g,n,want", [
+    (0.07e-3, 0.39e-3, 20, [1, 5, 14]),        # a fast host: the 20-step window in 3 replays
+    (0.125e-3, 0.39e-3, 20, [1, 2, 6, 11]),    # a slow one: no replay waits for its own submission
+    (0.07e-3, 0.39e-3, 300, None),
+])
+def test_calibrated_replay_plan_never_waits_for_submission(h, g, n, want):
+    """FlagshipTrainer._reps_calibrated: every replay's submission ends before the GPU runs out of queued work
+    (simulated with the same rates), sizes capped at what one capture holds."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import FlagshipTrainer
+    fake = SimpleNamespace(cfg=SimpleNamespace(lead_in=1, ramp=4), _k=lambda: 10, store=SimpleNamespace(n=18000),
+                           Bg=256, _h_est=h, _g_est=g, BOUNDARY_S=FlagshipTrainer.BOUNDARY_S)
+    fake._reps_calibrated = lambda *a: FlagshipTrainer._reps_calibrated(fake, *a)
+    got = FlagshipTrainer._reps(fake, n)
+    assert sum(got) == n and max(got) <= 17
+    host = gpu = 0.0
+    for i, r in enumerate(got):
+        host += h * r
+        if i:
+            assert host <= gpu + 1e-12, (got, i)   # submitted before the GPU drained what was queued
+        gpu = max(gpu, host if i == 0 else gpu) + g * r + FlagshipTrainer.BOUNDARY_S
+    if want is not None and n == 20:
+        assert got == want
