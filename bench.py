@@ -202,12 +202,13 @@ def main() -> int:
         if settle > 0:
             k = tr._k()
             ns = (settle + k - 1) // k * k
+            warm(tr, ns)   # (the settle run's own graph sets captured and warm: its wall time is the GPU's rate)
             sync()
             t0 = time.perf_counter()
             tr.run(ns)
             sync()
             # the replay plan from this box's measured rates: GPU seconds per step (this settle run, 5 % margin) and
-            # host submission seconds per step (its small replays) -- FlagshipTrainer._reps_calibrated
+            # the host's submission cost (fitted over the replays so far) -- FlagshipTrainer._reps_calibrated
             tr.calibrate(0.95 * (time.perf_counter() - t0) / ns)
             warm(tr, n)
         sync()
@@ -315,8 +316,9 @@ def main() -> int:
             "lead_in": args.lead_in,
             "ramp": args.ramp,
             "replays": tr._reps(args.steps),
-            "replay_rates_ms": [round(1e3 * v, 4) if v else None for v in (getattr(tr, "_h_est", None),
-                                                                           getattr(tr, "_g_est", None))],
+            # (the calibrated plan's inputs: host submit ms = a + c * steps, GPU ms per step)
+            "replay_rates_ms": {"submit_a": round(1e3 * tr._sub_est[0], 4), "submit_c": round(1e3 * tr._sub_est[1], 4),
+                                "gpu": round(1e3 * tr._g_est, 4)} if getattr(tr, "_g_est", None) else None,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "host_ms_per_step": round(host / args.steps * 1e3, 4),
             "higher_is_better": True,

@@ -336,9 +336,12 @@ __global__ void __launch_bounds__(512) pkfma_war_probe_kernel(int mode, int iter
     asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(base) : "memory");
 #pragma unroll 8
     for (int k = 1; k <= 64; ++k) war_step<PAD, PLAIN>(acc, w, x, base + 8u * (uint32_t)(k & 63));
-    // all lanes read the same addresses: acc must be wave-uniform
-    const float a0 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, acc.x)));
-    const float a1 = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, acc.y)));
+    // all lanes read the same addresses: acc must be wave-uniform.  (Lane 0's value through ds_bpermute, after a
+    // pad: the hazard recognizer does not see the inline asm's last VALU write, and a v_readfirstlane right behind
+    // it read a stale value in every mode of the first version of this probe, profiles/r6_01_pkfma_war.txt.)
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    const float a0 = __shfl(acc.x, 0);
+    const float a1 = __shfl(acc.y, 0);
     const bool bad = acc.x != a0 || acc.y != a1;
     if (it == 0 && blockIdx.x == 0 && wv == 0) {   // (diagnostic dump: wave 0's lanes, first iteration)
       out[4 + 2 * (threadIdx.x & 63)] = __builtin_bit_cast(unsigned int, acc.x);

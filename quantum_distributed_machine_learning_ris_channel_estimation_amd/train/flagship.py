@@ -608,9 +608,9 @@ class FlagshipTrainer(DPPlan):
         if head and 1 < self.cfg.ramp < k:
             head.append(self.cfg.ramp)
         fit = self.store.n // ((GraphedStep.WARMUP + 1) * self.Bg)   # (what _capture_set can hold: see _k)
-        h, g = getattr(self, "_h_est", None), getattr(self, "_g_est", None)
-        if head and h and g and g > h:
-            return self._reps_calibrated(n, k, fit, h, g)
+        sub, g = getattr(self, "_sub_est", None), getattr(self, "_g_est", None)
+        if head and sub and g and g > sub[1]:
+            return self._reps_calibrated(n, k, fit, sub, g)
         reps, rem = [], n
         for r in head:
             if rem == 0:
@@ -624,47 +624,68 @@ class FlagshipTrainer(DPPlan):
         return reps + body + ([tail] if tail else [])
 
     BOUNDARY_S = 30e-6   # what a replay boundary costs the GPU (both chains drain and refill): bench windows, r5-r6
+    SUBMIT_MARGIN = 1.2  # the host's submission pace varies between replays
 
-    def _reps_calibrated(self, n: int, k: int, fit: int, h: float, g: float):
-        """The replay plan from measured rates (``calibrate``): h host seconds to submit one step of a graph, g GPU
-        seconds per step.  A replay only starts on the GPU once its submission is complete, so after the 1-step lead-in
-        each replay is as long as the GPU work already queued can hide:  h (S + r) <= h + g S + b i  for the steps S
-        submitted before it (i replays, b a boundary) -- growing geometrically at ratio ~g / h -- capped at ``fit``
-        steps per graph, and the steady state in k-step (or longer, up to fit) replays.  With h 0.07 and g 0.39 ms the
-        driver's 20-step window is [1, 5, 14]; with h 0.125 it is [1, 2, 6, 11] (round 6: a fixed [1, 4, 15] left the
-        GPU idle 0.4 ms for the 15-step submission at h 0.125, profiles/r6_01_bench20_2.json)."""
+    def _reps_calibrated(self, n: int, k: int, fit: int, sub, g: float):
+        """The replay plan from measured rates (``calibrate``): submitting an r-step replay takes the host
+        ``a + c r`` seconds (``sub`` = (a, c)), the GPU runs g seconds per step and b per replay boundary.  A replay
+        starts on the GPU only once its submission is complete, so after the 1-step lead-in every replay is as long
+        as the GPU work queued ahead of it can hide: its submission must end before the GPU finishes the replays
+        before it -- the sizes grow roughly geometrically at ratio g / c -- capped at ``fit`` steps per graph.  (A fixed
+        [1, 4, 15] left the GPU idle 0.3 ms behind the 15-step submission on a slow-host box, 0.4162 against 0.3956
+        ms/step: profiles/r6_01_bench20*.json.)"""
         b = self.BOUNDARY_S
-        h = 1.2 * h   # (a 20 % margin: the host's pace varies between replays)
-        reps, S = [1], 1
+        a, c = (self.SUBMIT_MARGIN * v for v in sub)
+        reps = [1]
+        host = a + c           # the lead-in's submission ends
+        gpu = host + g + b     # ... and the GPU finishes it
+        S = 1
         while S < n:
-            allowed = int((h + (g - h) * S + b * len(reps)) / h)
+            allowed = int((gpu - host - a) / c) if c > 0 else fit
             r = max(1, min(allowed, fit, n - S))
-            if n - S - r and n - S - r < max(2, k // 2) and n - S <= fit:   # (no tiny tail replay)
+            if 0 < n - S - r < max(2, k // 2) and n - S <= fit:   # (no tiny tail replay)
                 r = n - S
+            host += a + c * r
+            gpu = max(gpu, host) + g * r + b
             reps.append(r)
             S += r
         return reps
 
     def note_submission(self, k: int, seconds: float) -> None:
-        """(host submission rate) seconds the host spent submitting a k-step replay; small replays only -- a long run
-        blocks on the full launch queue, which is not submission cost."""
+        """(host submission rate) seconds the host spent submitting a k-step replay (kept: the last 64)."""
         subs = getattr(self, "_subs", None)
         if subs is None:
             subs = self._subs = []
-        if k <= 4:
-            subs.append(seconds / k)
-            del subs[:-32]
+        subs.append((k, seconds))
+        del subs[:-64]
 
-    def calibrate(self, gpu_s_per_step: float, host_s_per_step: Optional[float] = None) -> None:
+    @staticmethod
+    def _fit_submission(subs):
+        """(a, c): least-squares fit of submit seconds = a + c k over the noted replays (fixed cost + per step)."""
+        if not subs:
+            return 0.0, 0.1e-3
+        ks = sorted({k for k, _ in subs})
+        if len(ks) < 2:
+            return 0.0, sorted(t / k for k, t in subs)[len(subs) // 2]
+        n = len(subs)
+        mk = sum(k for k, _ in subs) / n
+        mt = sum(t for _, t in subs) / n
+        var = sum((k - mk) ** 2 for k, _ in subs)
+        c = sum((k - mk) * (t - mt) for k, t in subs) / var
+        a = mt - c * mk
+        if c <= 0:
+            return 0.0, mt / mk
+        return max(a, 0.0), c
+
+    def calibrate(self, gpu_s_per_step: float) -> None:
         """Rates for the replay plan (``_reps_calibrated``): the GPU's seconds per step (e.g. a synchronised run's wall
-        time per step) and the host's submission seconds per step (default: the median of the small replays
-        submitted so far).  World > 1: the slowest rank's host and GPU rates, so every rank runs the same plan."""
-        if host_s_per_step is None:
-            subs = sorted(getattr(self, "_subs", []) or [0.1e-3])
-            host_s_per_step = subs[len(subs) // 2]
-        h = self.ctx.max_scalar(float(host_s_per_step)) if self.ctx.world > 1 else float(host_s_per_step)
-        g = self.ctx.max_scalar(float(gpu_s_per_step)) if self.ctx.world > 1 else float(gpu_s_per_step)
-        self._h_est, self._g_est = h, g
+        time per step, every graph set of it captured beforehand) and the host's submission cost (fitted over the
+        replays submitted so far).  World > 1: the slowest rank's rates, so every rank runs the same plan."""
+        a, c = self._fit_submission(getattr(self, "_subs", []))
+        g = float(gpu_s_per_step)
+        if self.ctx.world > 1:
+            a, c, g = self.ctx.max_vector([a, c, g])
+        self._sub_est, self._g_est = (a, c), g
 
     def prepare(self, n: int) -> None:
         """Capture every graph set ``run(n)`` will replay (keeps capture out of a timed region)."""

@@ -207,25 +207,36 @@ def test_replay_plan(n, k, lead, ramp, want):
         assert set(got) <= set(FlagshipTrainer._reps(fake, 30))
 
 
-@pytest.mark.parametrize("h,g,n,want", [
-    (0.07e-3, 0.39e-3, 20, [1, 5, 14]),        # a fast host: the 20-step window in 3 replays
-    (0.125e-3, 0.39e-3, 20, [1, 2, 6, 11]),    # a slow one: no replay waits for its own submission
-    (0.07e-3, 0.39e-3, 300, None),
+@pytest.mark.parametrize("a,c,g,n,want", [
+    (0.03e-3, 0.06e-3, 0.39e-3, 20, None),     # a fast host: few replays
+    (0.05e-3, 0.11e-3, 0.39e-3, 20, None),     # a slow one: no replay waits for its own submission
+    (0.03e-3, 0.06e-3, 0.39e-3, 300, None),
+    (0.0, 0.0, 0.39e-3, 20, [1, 17, 2]),        # free submission: the largest graphs (a tail of 2 is allowed)
 ])
-def test_calibrated_replay_plan_never_waits_for_submission(h, g, n, want):
-    """FlagshipTrainer._reps_calibrated: every replay's submission ends before the GPU runs out of queued work
-    (simulated with the same rates), sizes capped at what one capture holds."""
-    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import FlagshipTrainer
+def test_calibrated_replay_plan_never_waits_for_submission(a, c, g, n, want):
+    """FlagshipTrainer._reps_calibrated: every replay's submission (a + c r, with the plan's margin) ends before the
+    GPU runs out of the work queued ahead of it, sizes capped at what one capture holds."""
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import FlagshipTrainer as F
     fake = SimpleNamespace(cfg=SimpleNamespace(lead_in=1, ramp=4), _k=lambda: 10, store=SimpleNamespace(n=18000),
-                           Bg=256, _h_est=h, _g_est=g, BOUNDARY_S=FlagshipTrainer.BOUNDARY_S)
-    fake._reps_calibrated = lambda *a: FlagshipTrainer._reps_calibrated(fake, *a)
-    got = FlagshipTrainer._reps(fake, n)
-    assert sum(got) == n and max(got) <= 17
-    host = gpu = 0.0
-    for i, r in enumerate(got):
-        host += h * r
-        if i:
-            assert host <= gpu + 1e-12, (got, i)   # submitted before the GPU drained what was queued
-        gpu = max(gpu, host if i == 0 else gpu) + g * r + FlagshipTrainer.BOUNDARY_S
-    if want is not None and n == 20:
+                           Bg=256, _sub_est=(a, c), _g_est=g, BOUNDARY_S=F.BOUNDARY_S, SUBMIT_MARGIN=F.SUBMIT_MARGIN)
+    fake._reps_calibrated = lambda *args: F._reps_calibrated(fake, *args)
+    got = F._reps(fake, n) if c > 0 else F._reps_calibrated(fake, n, 10, 17, (a, c), g)
+    assert sum(got) == n and max(got) <= 17 and got[0] == 1
+    A, C = F.SUBMIT_MARGIN * a, F.SUBMIT_MARGIN * c
+    host = A + C
+    gpu = host + g + F.BOUNDARY_S
+    for r in got[1:]:
+        host += A + C * r
+        assert host <= gpu + 1e-12, got   # submitted before the GPU drained the replays queued ahead of it
+        gpu += g * r + F.BOUNDARY_S
+    if want is not None:
         assert got == want
+    if n == 20 and c > 0:
+        assert len(got) <= 4
+
+
+def test_submission_fit():
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd.train.flagship import FlagshipTrainer as F
+    a, c = F._fit_submission([(1, 0.11e-3), (4, 0.29e-3), (10, 0.65e-3), (15, 0.95e-3), (1, 0.12e-3)])
+    assert abs(c - 0.06e-3) < 0.005e-3 and 0.03e-3 < a < 0.07e-3
+    assert F._fit_submission([(1, 2e-4), (1, 1e-4), (1, 3e-4)]) == (0.0, 2e-4)
