@@ -28,9 +28,9 @@ At N > 1:
     JSON line is printed (rank 0's supervisor relays it), so stdout never holds two.
   * the DP plan is CHOSEN AT THE REAL WORLD SIZE: with ``--dp-plan auto`` both plans (ZeRO-1 and
     all-reduce) are built on the graph mode the capture pre-flight allows -- on the one-graph plan
-    each with both QSC placements (``--dp-qsc auto``: beside the conv backward, or forked after the
-    gather) -- each timed over ``--select-steps`` steps after its warm-up (max over ranks), and the
-    fastest is benchmarked; ``plan_select_ms`` records every candidate.
+    each with its QSC placements (``--dp-qsc auto``: beside the conv backward, forked after the gather, or --
+    all-reduce plan -- the independent QSC chain with its own bucket) -- each timed over ``--select-steps`` steps
+    after its warm-up (max over ranks), and the fastest is benchmarked; ``plan_select_ms`` records every candidate.
   * ``phases_ms``: per-phase times (max over ranks) on extra steps AFTER the timed region: HIP events
     between the 5-graph plan's replays, device clock stamps captured inside the one-graph plan's graph
     (FlagshipTrainer.phase_times); ``phases_src`` says which.
@@ -80,9 +80,10 @@ def main() -> int:
                     help="DP plan: capture the whole step, RCCL collectives included, in one HIP graph")
     ap.add_argument("--phase-steps", type=int, default=20,
                     help="N > 1: extra steps (after the timed region) timed per phase with HIP events; 0 = off")
-    ap.add_argument("--dp-qsc", default="auto", choices=["auto", "g2", "fwd"],
-                    help="N > 1, one-graph DP plan: the QSC branch beside the conv backward (g2) or forked after the "
-                         "gather (fwd); auto = timed at the real world size with the plans (FlagshipConfig.dp_qsc)")
+    ap.add_argument("--dp-qsc", default="auto", choices=["auto", "g2", "fwd", "indep"],
+                    help="N > 1, one-graph DP plan: the QSC branch beside the conv backward (g2), forked after the "
+                         "gather (fwd), or an independent chain with its own bucket (indep, all-reduce plan); auto = "
+                         "timed at the real world size with the plans (FlagshipConfig.dp_qsc)")
     ap.add_argument("--select-steps", type=int, default=30,
                     help="N > 1, --dp-plan auto: steps timed per candidate plan to choose the fastest (three "
                          "10-step replays; 0 = no timing: allreduce with the one-graph step, zero with the 5-graph step)")
@@ -239,8 +240,11 @@ def main() -> int:
     elif args.dp_qsc != "auto":
         qscs = [args.dp_qsc]
     else:
-        qscs = ["g2", "fwd"] if args.select_steps > 0 else ["g2"]
-    cands = [(p, q) for p in plans for q in qscs]
+        qscs = ["g2", "fwd", "indep"] if args.select_steps > 0 else ["g2"]
+    cands = [(p, q) for p in plans for q in qscs if not (q == "indep" and p != "allreduce")]
+    if not cands:
+        print("error: --dp-qsc indep runs on the all-reduce plan (--dp-plan allreduce)", file=sys.stderr)
+        return 2
     select = {}
     tr, store = None, None
     for cand in cands:

@@ -112,8 +112,11 @@ class FlagshipConfig:
     dp_qsc: str = "g2"           # DP plan, where the QSC branch runs: "g2" = forked beside the conv backward (the most
     #                              work behind the FC gradient collective), "fwd" = forked right after the gather as in
     #                              the world-1 step, joined before the small bucket (shorter g2: wins where the FC
-    #                              collective is short; one-graph plan only -- a fork cannot span two graphs).
-    #                              bench.py times both at the real world size.
+    #                              collective is short; one-graph plan only -- a fork cannot span two graphs);
+    #                              "indep" (round 6) = the world-1 independent chains: the QSC chain with its own
+    #                              gather, never joined inside the step, its gradients in a bucket of their own
+    #                              all-reduced at the next step's start (DPPlan._dp_run_indep; all-reduce plan).
+    #                              bench.py times them at the real world size.
     scaling: str = "weak"        # world > 1: "weak" = batch per stream on EVERY rank, each rank its own data; "strong" =
     #                              the reference's DataParallel semantics (R:144-148): ONE global batch of ``batch`` rows
     #                              per stream per step (same data and permutation on every rank) cut into world
@@ -152,8 +155,10 @@ class FlagshipTrainer(DPPlan):
         dp = ctx.world > 1 or cfg.split_graphs
         if cfg.dp_plan not in ("zero", "allreduce"):
             raise ValueError(f"dp_plan {cfg.dp_plan!r}")
-        if cfg.dp_qsc not in ("g2", "fwd") or (cfg.dp_qsc == "fwd" and not cfg.dp_one_graph):
-            raise ValueError(f"dp_qsc {cfg.dp_qsc!r} (\"fwd\" needs dp_one_graph)")
+        if cfg.dp_qsc not in ("g2", "fwd", "indep") or (cfg.dp_qsc in ("fwd", "indep") and not cfg.dp_one_graph):
+            raise ValueError(f"dp_qsc {cfg.dp_qsc!r} (\"fwd\" / \"indep\" need dp_one_graph)")
+        if cfg.dp_qsc == "indep" and cfg.dp_plan != "allreduce":
+            raise ValueError("dp_qsc 'indep' runs on the all-reduce plan (ZeRO's HDCE NaN flag rides in the QSC bucket)")
         # ZeRO-1 plan (see _dp_run); not with the fp8 estimator (its weight scale is a max over the
         # whole FC weight, which a sharded update would have to all-reduce)
         self.zero = dp and cfg.dp_plan == "zero" and cfg.dtype != "fp8"
@@ -224,6 +229,8 @@ class FlagshipTrainer(DPPlan):
         bk = {"fc": [sp.grad[n_conv:]], "small": [sp.grad[:n_conv], self.qspace.grad, self.qskip]}
         if dp:
             bk["small"] = [sp.grad_base[:nq + n_conv]]
+            if cfg.dp_qsc == "indep":   # (the QSC chain's own bucket: its gradients + NaN flag, all-reduced apart)
+                bk["small"], bk["q"] = [sp.grad_base[nq:nq + n_conv]], [sp.grad_base[:nq]]
             if self.zero:
                 del bk["fc"]   # (its reduce-scatter is launched on the region directly)
         else:
@@ -367,8 +374,11 @@ class FlagshipTrainer(DPPlan):
                 # replay: step i's FC update (fc stream) overlaps step i + 1's gather + conv forward
                 def body():
                     for i in range(k):
-                        self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr,
-                                     fence=i == k - 1, first=i == 0)
+                        if cfg.dp_qsc == "indep" and self.streams is not None:
+                            self._dp_run_indep(fence=i == k - 1, first=i == 0)
+                        else:
+                            self._dp_run(self._dp_g1a, self._dp_g1b, self._dp_g2, self._dp_gf, self._dp_gr,
+                                         fence=i == k - 1, first=i == 0)
                 gs = [GraphedStep(body, enabled=graphs, guards=(self.buckets.assert_quiescent,))]
                 self._graph_sets[k] = gs
                 return gs

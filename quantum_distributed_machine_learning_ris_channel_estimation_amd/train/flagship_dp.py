@@ -96,6 +96,68 @@ class DPPlan:
             self._tail_pack_launch()
         self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.qskip)   # (QSC: the mean of equal-size parts)
 
+    def _dp_run_indep(self, fence: bool = True, first: bool = True) -> None:
+        """(cfg.dp_qsc "indep": the one-graph all-reduce plan) the world-1 step's independent chains inside the DP
+        step.  The QSC chain gathers its own copy of the batch (device cursor cur[1]) and runs forward + backward
+        on its stream without joining the HDCE chain; its gradients (bucket "q": QSC gradients + its NaN flag) are
+        all-reduced at the START of the next step -- launched from main, as every captured collective must be
+        (one launched from a forked stream crashed hipStreamEndCapture, scripts/probes/probe_rccl_capture.py) -- after
+        main waits for the QSC chain of the previous step (long finished: ~150 us of QSC work against ~330 of HDCE
+        work per step), and the QSC stream runs AdamW once it has landed, then the next QSC step.  The last step of
+        a replay all-reduces and updates its own QSC gradients before the replay's join.  The HDCE chain has no QSC
+        kernel and one cross-stream edge per step; every value is the serial step's (AdamW(i - 1) still runs before
+        the QSC forward of step i).  ``fence``/``first`` as _dp_run.  (Reference DP site:
+        Runner_P128_QuantumNAT_onchipQNN.py:135-153.)"""
+        b = self.buckets
+        main = torch.cuda.current_stream(self.ctx.device)
+        q, fc = self.streams["qsc"], self.streams["fc"]
+
+        def q_update():   # the QSC gradients of the step the qsc stream last ran: all-reduce, then AdamW
+            main.wait_stream(q)
+            b.launch("q")
+            with torch.cuda.stream(q):
+                b.wait(("q",))
+                self.qopt.step(grad_scale=1.0 / self.ctx.world, skip=self.qskip)
+
+        self._mark("start")
+        if first:
+            q.wait_stream(main)   # (a branch forked before any node would be a root of the graph)
+        else:
+            q_update()
+        self._gather(classifier=False)
+        with torch.cuda.stream(q):
+            self._gather(hdce=False, classifier=True)
+            self._qsc_branch(with_opt=False)
+        self.hstep.defer_dgrad = self.hstep.hip
+        if self.hstep.hip:
+            self.hstep.forward_conv_gathered(self.gat)
+        else:
+            self._hdce_forward()
+        if not first:   # (the previous step's FC update on the fc stream)
+            main.wait_stream(fc)
+        self._dp_g1b()
+        b.launch("skip")
+        b.launch("fc")
+        if self.hstep.defer_dgrad:
+            self.hstep.dgrad()
+        self.hstep.backward_conv()
+        b.launch("small", inline=True)
+        fc.wait_stream(main)
+        with torch.cuda.stream(fc):
+            b.wait(("skip", "fc"))
+            self._dp_gf()
+        b.wait(("skip", "fc", "small"))
+        pk = self._adam_pack()
+        self.hopt.step(grad_scale=self._hgs, skip=self.hskip, part=0 if len(self.hopt.bounds) > 1 else None, pack=pk)
+        if self.tail_pack and pk is None:
+            self._tail_pack_launch()
+        if fence:
+            q_update()
+            main.wait_stream(q)
+            main.wait_stream(fc)
+        b.clear()   # (every collective has been waited for by the stream that consumes it)
+        self._mark("end")
+
     def _fc_weights_lp(self) -> torch.Tensor:
         """(ZeRO) the FC region's copy the forward / data gradient read: the bf16 shadow (GPU bf16),
         else the fp32 master weights themselves."""
@@ -164,6 +226,7 @@ class DPPlan:
         # FC collective -- instead of a fork / join through the comm stream, two cross-queue hops on the
         # step's critical path)
         b.launch("small", inline=True)
+        b.launch("q", inline=True)   # (dp_qsc "indep" off the GPU streams: the QSC bucket beside the small one)
         fc_wait = ("fc", "small") if zero else ("skip", "fc")
         if self.streams is None:
             b.wait(fc_wait)
@@ -178,7 +241,7 @@ class DPPlan:
             # ZeRO: main takes the small bucket (collective + scatter-back) BEFORE forking the fc stream,
             # which needs its HDCE NaN flag: one stream owns each scatter-back, and the fc stream inherits
             # it through the fork (no second-waiter path across streams)
-            b.wait(("small",))
+            b.wait(("small", "q"))
             fc_wait = ("fc",)
         fc.wait_stream(main)
         with torch.cuda.stream(fc):
@@ -196,7 +259,7 @@ class DPPlan:
                 self._mark("ag", fc)
         # (allreduce plan: the HDCE NaN flag rides in the fc bucket -- wait for it before the conv Adam
         # reads it; free under RCCL, whose in-order stream finished fc before small)
-        b.wait(("small",) if zero else ("skip", "fc", "small"))
+        b.wait(("small", "q") if zero else ("skip", "fc", "small", "q"))
         self._mark("small_ready")
         og_ag = zero and self.cfg.dp_one_graph
         # the shadow all-gather from main once the shard is updated: before gr (it overlaps gr; the shard
@@ -231,7 +294,7 @@ class DPPlan:
                          each (step = its start to its fenced end).  The stamp nodes are extra graph nodes
                          (a few us each): the phases are the plan's shape, bench.py's timed run its speed.
         None for the world-1 single-chain plan and off the GPU."""
-        if self.ctx.device.type != "cuda" or self.streams is None:
+        if self.ctx.device.type != "cuda" or self.streams is None or self.cfg.dp_qsc == "indep":
             return None
         if len(self.graphs) == 5:
             rows, chained = self._event_rows(steps), True

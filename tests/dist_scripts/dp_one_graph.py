@@ -1,6 +1,6 @@
 """DP plan captured as ONE graph (RCCL collectives inside it) == the 5-graph DP plan, bit for bit.
 
-    dp_one_graph.py OUT [zero|allreduce] [steps per one-graph replay] [g2|fwd: the one-graph plan's QSC placement]
+    dp_one_graph.py OUT [zero|allreduce] [steps per one-graph replay] [g2|fwd|indep: the one-graph plan's QSC placement]
 
 Run with QDML_FORCE_DIST=1 at world 1 on one GPU (a real RCCL process group of one rank: the
 collectives are launched and captured exactly as at world N) or with N ranks.  Both plans train the

@@ -240,3 +240,54 @@ def test_submission_fit():
     a, c = F._fit_submission([(1, 0.11e-3), (4, 0.29e-3), (10, 0.65e-3), (15, 0.95e-3), (1, 0.12e-3)])
     assert abs(c - 0.06e-3) < 0.005e-3 and 0.03e-3 < a < 0.07e-3
     assert F._fit_submission([(1, 2e-4), (1, 1e-4), (1, 3e-4)]) == (0.0, 2e-4)
+
+
+
+def make_indep_plan(sim, world):
+    """The DP plan with dp_qsc "indep" (DPPlan._dp_run_indep): stub kernels; the real stream / event / collective
+    plumbing."""
+    p, _ = make_plan(sim, world, zero=False)
+    grad = p.hdce.space.grad
+    p.buckets = GradBuckets(p.ctx, {"small": [grad[:48]], "q": [grad[48:64]], "fc": [grad[64:64 + 64 * world]],
+                                    "skip": [grad[-1:]]})
+    p.cfg = SimpleNamespace(dp_one_graph=True, dp_qsc="indep")
+    noop = lambda *a, **k: None   # noqa: E731
+    p._gather = noop
+    p._qsc_branch = noop
+    p._dp_g1b = noop
+    p._dp_gf = noop
+    p._adam_pack = lambda: None
+    p._tail_pack_launch = noop
+    p.tail_pack = False
+    p._hgs = 1.0 / world
+    p.qskip = p.hskip = None
+    p.gat = None
+    p.hstep = SimpleNamespace(hip=True, defer_dgrad=False, forward_conv_gathered=noop, dgrad=noop, backward_conv=noop)
+    opt = SimpleNamespace(step=noop, bounds=[0, 1])
+    p.hopt = p.qopt = opt
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_indep_dp_plan_capture_invariants(world, k, monkeypatch):
+    """dp_qsc "indep" (round 6): the QSC chain's own bucket all-reduced from main at the next step's start (and at
+    the replay's last step), waited for on the QSC stream -- no duplicate or stale waits over consecutive captures,
+    and one collective order on every rank: [q of the previous step] skip, fc, small per step, q at the end."""
+    sim = Sim()
+    monkeypatch.setattr(torch.cuda, "current_stream", sim.current_stream)
+    monkeypatch.setattr(torch.cuda, "stream", sim.stream)
+    monkeypatch.setattr(torch.cuda, "Event", sim.Event)
+    plan = make_indep_plan(sim, world)
+    for _ in range(3):
+        plan.buckets.assert_quiescent()
+        sim.epoch += 1
+        first = len(sim.waits)
+        for i in range(k):
+            plan._dp_run_indep(fence=i == k - 1, first=i == 0)
+        assert not plan.buckets.pending
+        check(sim.waits[first:])
+    ops = [o for o, _ in plan.ctx.comm.log]
+    assert ops == ["all_reduce"] * (3 * (4 * k))   # skip, fc, small per step + q once per step
+    # the QSC bucket's collective is issued on the comm stream (forked from main), never from the qsc stream
+    assert all(s != "qsc" for _, s in plan.ctx.comm.log)

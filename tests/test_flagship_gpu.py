@@ -176,14 +176,16 @@ def test_dp_plan_run_to_run_on_shared_gpu(tmp_path):
 
 
 @pytest.mark.parametrize("plan,k,qsc", [("zero", 1, "g2"), ("allreduce", 1, "g2"), ("allreduce", 3, "g2"),
-                                        ("zero", 1, "fwd"), ("allreduce", 3, "fwd")])
+                                        ("zero", 1, "fwd"), ("allreduce", 3, "fwd"), ("allreduce", 1, "indep"),
+                                        ("allreduce", 3, "indep")])
 def test_dp_one_graph_matches_five_graphs_over_rccl(tmp_path, plan, k, qsc):
     """The DP step captured as ONE graph with its RCCL collectives inside == the 5-graph DP plan (which
     launches the collectives between replays), bit for bit over 6 steps: a real RCCL process group of
     one rank (QDML_FORCE_DIST=1), so the reduce-scatter / all-reduce / all-gather are captured.  k = 3:
     three steps per replay, each step's FC update overlapping the next step's conv forward.  qsc "fwd": the
     one-graph plan's QSC branch forked after the gather (cfg.dp_qsc) -- the same kernels on the same inputs,
-    so still bit-exact.  (k = 1: the one-graph trainer's phase_times -- clock stamps captured inside the graph
+    so still bit-exact; qsc "indep" (round 6): the QSC chain independent, its bucket all-reduced at the next step's
+    start (DPPlan._dp_run_indep).  (k = 1: the one-graph trainer's phase_times -- clock stamps captured inside the graph
     -- must also fit in its step.)"""
     import os
     import sys
