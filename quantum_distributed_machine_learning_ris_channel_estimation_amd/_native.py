@@ -78,8 +78,17 @@ def hipcc() -> Optional[str]:
 # tiles between the register files every K step)
 # qsim_stream.hip: no SLP vectorisation (packed-f32 pairs of the complex gate math doubled the register
 # demand: the adjoint passes spilled at 256 VGPRs, 86-92 without)
+# hazard_probe.hip: the one file WITH packed-FP32 instructions (its inline asm demonstrates their hazard; see below)
 PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "qsim_stream.hip": ["-fno-slp-vectorize"],
-                  "qsim_mfma.hip": ["-fno-slp-vectorize"], "qsim12_mfma.hip": ["-fno-slp-vectorize"]}
+                  "qsim_mfma.hip": ["-fno-slp-vectorize"], "qsim12_mfma.hip": ["-fno-slp-vectorize"],
+                  "hazard_probe.hip": ["-Xclang", "-target-feature", "-Xclang", "+packed-fp32-ops"]}
+# No packed-FP32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) anywhere else (round 6).  On gfx950 a packed-FP32
+# instruction whose source registers are rewritten by a younger LDS read can -- while another wave on its SIMD is
+# issuing MFMAs -- read the NEW value in its last quarter-wave (lanes 48-63): 44,687 of 2,048,000 probe iterations
+# with MFMA partners, 0 without, 0 with plain v_fma_f32 (csrc/hip/hazard_probe.hip, profiles/r6_03_pkfma_war.txt).
+# That was the QSC preprocess forward's lanes-48..63 misread (docs/CONCURRENCY.md).  The compiler forms these
+# instructions on its own (vector types, SLP), so the feature is off for the whole library.
+NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
@@ -90,7 +99,7 @@ def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     srcs = _sources("hip", ".hip")
     hdrs = _headers("hip")
     flags = [f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
-             "-Wno-unused-result", "-I", os.path.join(CSRC, "hip")]
+             "-Wno-unused-result", "-I", os.path.join(CSRC, "hip")] + NO_PACKED_F32
     flags += os.environ.get("QDML_HIPCC_EXTRA", "").split()   # (tuning sweeps: extra -D defines)
     # a changed flag set (a tuning build, then the default again) rebuilds every object
     stamp = os.path.join(OBJ_DIR, "flags.txt")

@@ -62,3 +62,22 @@ def test_clock_stamps_time_stream_ordered_work(cuda):
     t2 = buf.tolist()
     assert t2[1] > t2[0] > t[1]
     assert (t2[1] - t2[0]) / khz >= 0.5 * ev_ms
+
+
+def test_packed_f32_war_probe_plain_fma_is_safe(cuda):
+    """csrc/hip/hazard_probe.hip (round 6): the instruction pattern of the QSC preprocess forward's misread -- an
+    FMA reading registers that the next ds_read rewrites -- with MFMA partner waves on every SIMD.  With plain
+    v_fma_f32 (what the library is built to emit: _native.NO_PACKED_F32) the result is wave-uniform in every
+    iteration.  (The packed form is only reported, not asserted: profiles/r6_03_pkfma_war.txt.)"""
+    import ctypes
+    import torch
+    from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+    f = nat.fn(nat.hip_lib(), "qd_pkfma_war_probe", [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p])
+    res = {}
+    for mode in (2 | 1, 1):
+        out = torch.zeros(132, dtype=torch.int32, device=cuda)
+        nat.check(f(mode, 500, 256, nat.ptr(out), nat.stream_ptr(out.device)), "pkfma_war_probe")
+        torch.cuda.synchronize()
+        res[mode] = (int(out[0]), int(out[1]))
+    print("pkfma WAR probe (events, iterations):", res)
+    assert res[3][1] == 500 * 256 * 4 and res[3][0] == 0
