@@ -365,6 +365,7 @@ def main() -> int:
                 "hdce_priority": bool(cfg.hdce_priority),
             },
             "final_losses": {"hdce_nmse": hl[0], "hdce_nmse_perf": hl[1], "qsc_nll": ql},
+            "steps_trained": getattr(tr, "steps_done", None),   # (the losses' step count: the warm-ups vary with the plan)
             "step_spread": spread,
             # (torch's caching allocator: everything the run allocated on this GPU -- dataset, weights, optimizer
             # state, activations, graph pools -- out of 288 GB of HBM3E)

@@ -27,7 +27,7 @@ from typing import List, Optional
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
-LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_DIR = os.environ.get("QDML_LIB_DIR") or os.path.join(PKG_DIR, "lib")   # (override: A/B builds side by side)
 OBJ_DIR = os.path.join(LIB_DIR, "obj")
 HIP_LIB = os.path.join(LIB_DIR, "libqdml_hip.so")
 CPU_LIB = os.path.join(LIB_DIR, "libqdml_cpu.so")
@@ -89,6 +89,8 @@ PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "qsim_stream
 # That was the QSC preprocess forward's lanes-48..63 misread (docs/CONCURRENCY.md).  The compiler forms these
 # instructions on its own (vector types, SLP), so the feature is off for the whole library.
 NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+if os.environ.get("QDML_PACKED_F32") == "1":   # (measurement only: the hazard-exposed build, for its A/B)
+    NO_PACKED_F32 = []
 
 
 def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:

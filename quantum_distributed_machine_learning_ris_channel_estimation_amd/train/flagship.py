@@ -718,6 +718,7 @@ class FlagshipTrainer(DPPlan):
             # the state keeps the ranks bit-identical)
             self.capture(preserve=True, k=k)
         self.next_batch(k)
+        self.steps_done = getattr(self, "steps_done", 0) + k   # (optimizer steps applied: capture warm-ups excluded)
         if len(gs) == 1:
             t0 = time.perf_counter()
             gs[0]()
