@@ -107,7 +107,7 @@ def main() -> int:
                     help="(stream mode indep) when each step's QSC chain starts: with the step, or after the HDCE conv "
                          "forward (FlagshipConfig.qsc_start)")
     ap.add_argument("--qsc-grid-bwd", type=int, default=0,
-                    help="QSC backward workgroups (FlagshipConfig.qsc_grid_bwd; 0 = the default 256)")
+                    help="QSC backward workgroups (FlagshipConfig.qsc_grid_bwd; 0 = at most 256, balanced: 192 at 2304 samples)")
     ap.add_argument("--hdce-priority", action="store_true",
                     help="(stream mode indep) capture on a high-priority stream (FlagshipConfig.hdce_priority)")
     ap.add_argument("--fc-adam-next", type=int, default=0, metavar="WORKGROUPS",

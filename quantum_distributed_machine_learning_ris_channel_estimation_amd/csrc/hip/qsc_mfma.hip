@@ -143,16 +143,6 @@ __device__ __forceinline__ void stage4(float* dst, const float* __restrict__ src
 // v_readlane / v_writelane per sample), then the per-wave images
 __host__ __device__ constexpr int fwd_w1_base(int n, int F) { return (n * (F + 4) + 16 + 3) & ~3; }
 __host__ __device__ constexpr int fwd_act_base(int n, int F) { return fwd_w1_base(n, F) + ((C1 * K1 + C1 + 3) & ~3); }
-__device__ __forceinline__ void stage_linear(const float* __restrict__ flat, Offs o, float* ws, int n, int F) {
-  const int q4 = F / 4;
-  const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
-  for (int i = threadIdx.x; i < n * q4; i += blockDim.x) {
-    const int j = i / q4, c = i % q4;
-    *reinterpret_cast<float4*>(ws + j * (F + 4) + 4 * c) = src[i];
-  }
-  if (threadIdx.x < n) ws[n * (F + 4) + threadIdx.x] = flat[o.bl + threadIdx.x];
-}
-
 // (all offsets are multiples of 16 floats: FlatParamSpace ALIGN; LDS slots multiples of 4)
 __device__ __forceinline__ void stage_weights(const float* __restrict__ flat, Offs o, float* ws, int n, int F) {
   stage4(ws + S_W1, flat + o.w1, C1 * K1);
@@ -384,17 +374,35 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   // registers (loaded straight from the flat buffer), conv2 bias is one value per lane
   float* act = sm + fwd_act_base(n, G::F) + wv * G::FWD;
   float* w1s = sm + fwd_w1_base(n, G::F);
-  stage_linear(flat, o, ws, n, G::F);
-  for (int i = threadIdx.x; i < C1 * K1 + C1; i += blockDim.x)   // W1 [co][k] -> [k][co] (+ bias)
-    w1s[i < C1 * K1 ? (i % K1) * C1 + i / K1 : i] = i < C1 * K1 ? flat[o.w1 + i] : flat[o.b1 + i - C1 * K1];
-  static_assert(G::FWD % 4 == 0 && G::BWD % 4 == 0, "float4 image fills");
-  for (int i = lane; i < G::FWD / 4; i += 64)   // zero halos once; interiors rewritten per sample
-    reinterpret_cast<float4*>(act)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // Every weight load of the prologue in flight together, one round trip (round 6: the linear layer's copy loop,
+  // conv1's transposing loop and the conv2 register loads waited for 4-5 round trips in turn, ~10k cycles per
+  // workgroup: profiles/r2_18_qsc_fwd_conv1_lds.md "stage weights").
+  constexpr int NTH = 64 * NWV;
+  constexpr int WLQ = (16 * (G::F / 4) + NTH - 1) / NTH;   // linear-layer float4 per thread (n <= 16)
+  constexpr int W1Q = (C1 * K1 + C1 + NTH - 1) / NTH;      // conv1 weights + bias per thread
+  const int q4 = G::F / 4, wl_tot = n * q4;
+  float4 vwl[WLQ];
+  float vw1[W1Q];
+  float vbl = 0.f;
+  {
+    const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
+#pragma unroll
+    for (int k = 0; k < WLQ; ++k) {
+      const int i = threadIdx.x + k * NTH;
+      vwl[k] = src[i < wl_tot ? i : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < W1Q; ++k) {
+      const int i = threadIdx.x + k * NTH;
+      vw1[k] = flat[i < C1 * K1 ? o.w1 + i : (i < C1 * K1 + C1 ? o.b1 + i - C1 * K1 : o.w1)];
+    }
+    if (threadIdx.x < n) vbl = flat[o.bl + threadIdx.x];
+  }
   // this lane's weights W2[co][8h .. 8h+7][0..8] are 72 contiguous floats: 18 float4 loads
   float wreg[72];
+  float tmp[72];
   {
     const float4* wp = reinterpret_cast<const float4*>(flat + o.w2 + (lane & 31) * K2 + 72 * (lane >> 5));
-    float tmp[72];
 #pragma unroll
     for (int q = 0; q < 18; ++q) {
       const float4 v = wp[q];
@@ -403,12 +411,28 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
       tmp[4 * q + 2] = v.z;
       tmp[4 * q + 3] = v.w;
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int t = 0; t < 9; ++t) wreg[t * 8 + j] = tmp[j * 9 + t];
   }
   const float bias2 = flat[o.b2 + (lane & 31)];
+#pragma unroll
+  for (int k = 0; k < WLQ; ++k) keep_loaded(vwl[k]);
+#pragma unroll
+  for (int k = 0; k < WLQ; ++k) {
+    const int i = threadIdx.x + k * NTH;
+    if (i < wl_tot) *reinterpret_cast<float4*>(ws + (i / q4) * (G::F + 4) + 4 * (i % q4)) = vwl[k];
+  }
+  if (threadIdx.x < n) ws[n * (G::F + 4) + threadIdx.x] = vbl;
+#pragma unroll
+  for (int k = 0; k < W1Q; ++k) {   // W1 [co][k] -> [k][co] (+ bias)
+    const int i = threadIdx.x + k * NTH;
+    if (i < C1 * K1 + C1) w1s[i < C1 * K1 ? (i % K1) * C1 + i / K1 : i] = vw1[k];
+  }
+  static_assert(G::FWD % 4 == 0 && G::BWD % 4 == 0, "float4 image fills");
+  for (int i = lane; i < G::FWD / 4; i += 64)   // zero halos once; interiors rewritten per sample
+    reinterpret_cast<float4*>(act)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wreg[t * 8 + j] = tmp[j * 9 + t];
   [[maybe_unused]] bf16x8_t wx3[X3 ? 18 : 1];
   if constexpr (X3) {
 #pragma unroll
@@ -909,43 +933,56 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
   __bf16* DZ1 = DZT;   // (alias: dz2 images are dead once the conv2 data gradient is done)
   float* DP1 = reinterpret_cast<float*>(DZC + B3::DZC);
   float* misc = DP1 + 16 * 32;
+  // this workgroup's share of the quantum layer's adjoint slab rows (summed into its slab row at the end): the
+  // loads fly with the weight loads below -- at the end they cost the workgroup's last wave a round trip per
+  // 4 rows (round 6)
+  const int q0 = (int)((long long)qs.rows * blockIdx.x / gridDim.x);
+  const int q1 = (int)((long long)qs.rows * (blockIdx.x + 1) / gridDim.x);
+  constexpr int QPF = 16;   // rows prefetched; a longer share sums the rest at the end
+  const bool q_mine = qs.slab && (int)threadIdx.x < qs.width;
+  float qv[QPF];
   {
-    const int q4 = G::F / 4, tot = n * q4;
+    const float* qc = qs.slab + (q_mine ? threadIdx.x : 0);
+#pragma unroll
+    for (int k = 0; k < QPF; ++k) qv[k] = q_mine && q0 + k < q1 ? qc[(size_t)(q0 + k) * qs.width] : 0.f;
+  }
+  {
+    // the linear layer and (when the forward wrote it) the W2T image: every load in flight together, then the
+    // stores -- one round trip (an index past the end re-loads element 0, not stored; round 6 merged the two
+    // copies' round trips)
+    const int q4 = G::F / 4, tot = n * q4;   // (n <= 16: tot <= 4 x 256)
     const float4* src = reinterpret_cast<const float4*>(flat + o.wl);
-    // (rounds of 4 loads per thread in flight: the one-at-a-time copy loop waited a round trip per float4)
-    for (int i0 = threadIdx.x; i0 < tot; i0 += 4 * blockDim.x) {
-      float4 v[4];
+    float4 v[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int i = i0 + k * blockDim.x;
-        v[k] = src[i < tot ? i : 0];
-      }
+    for (int k = 0; k < 4; ++k) {
+      const int i = threadIdx.x + k * 256;
+      v[k] = src[i < tot ? i : 0];
+    }
+    constexpr int NCP = (B3::W2T * 2 / 16 + 255) / 256;
+    uint4 vi[NCP];
+    if (w2t_img) {
+      const uint4* isrc = reinterpret_cast<const uint4*>(w2t_img);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) keep_loaded(v[k]);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int i = i0 + k * blockDim.x;
-        if (i < tot) *reinterpret_cast<float4*>(wl + (i / q4) * wl_stride(G::F) + 4 * (i % q4)) = v[k];
+      for (int k = 0; k < NCP; ++k) {
+        const int i = threadIdx.x + 256 * k;
+        vi[k] = isrc[i < B3::W2T * 2 / 16 ? i : 0];
       }
     }
-    if (w2t_img) {   // this step's image from the forward (qd_qsc2_fwd3): one copy, one round trip
-      const uint4* src = reinterpret_cast<const uint4*>(w2t_img);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) keep_loaded(v[k]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = threadIdx.x + k * 256;
+      if (i < tot) *reinterpret_cast<float4*>(wl + (i / q4) * wl_stride(G::F) + 4 * (i % q4)) = v[k];
+    }
+    if (w2t_img) {   // this step's image from the forward (qd_qsc2_fwd3)
       uint4* dst = reinterpret_cast<uint4*>(w2t);
-      // (every load issued before the first store -- an index past the end re-loads element 0, not stored: the
-      // guarded copy compiled to one round trip per 4 KiB)
-      constexpr int NCP = (B3::W2T * 2 / 16 + 255) / 256;
-      uint4 v[NCP];
+#pragma unroll
+      for (int k = 0; k < NCP; ++k) keep_loaded(vi[k]);
 #pragma unroll
       for (int k = 0; k < NCP; ++k) {
         const int i = threadIdx.x + 256 * k;
-        v[k] = src[i < B3::W2T * 2 / 16 ? i : 0];
-      }
-#pragma unroll
-      for (int k = 0; k < NCP; ++k) keep_loaded(v[k]);
-#pragma unroll
-      for (int k = 0; k < NCP; ++k) {
-        const int i = threadIdx.x + 256 * k;
-        if (i < B3::W2T * 2 / 16) dst[i] = v[k];
+        if (i < B3::W2T * 2 / 16) dst[i] = vi[k];
       }
     } else
     // W2 [co][ci][tap] -> W2T [tap][ci][co]: iterate in DESTINATION order, two co per dword (in source
@@ -1248,10 +1285,17 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
     if ((lane & 1) == 0) mine[C2 * K2 + C1 * K1 + C1 + (lane >> 1)] = v;
   }
   if (lane < 16) mine[C2 * K2 + C1 * K1 + C1 + C2 + lane] = lane < n ? gbl : 0.f;
+  float* qred = red + NWV * RW;   // the quantum slab columns' sums, by column (bwd3_smem counts 256 floats)
+  if (q_mine) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < QPF; ++k) v += qv[k];
+    const float* qc = qs.slab + threadIdx.x;
+    for (int r = q0 + QPF; r < q1; ++r) v += qc[(size_t)r * qs.width];
+    qred[threadIdx.x] = v;
+  }
   __syncthreads();
   float* row = slab + (size_t)blockIdx.x * o.row;
-  const int q0 = (int)((long long)qs.rows * blockIdx.x / gridDim.x);
-  const int q1 = (int)((long long)qs.rows * (blockIdx.x + 1) / gridDim.x);
   for (int i = threadIdx.x; i < o.row; i += 64 * NWV) {
     float v = 0.f;
     int src = -1;
@@ -1266,9 +1310,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
 #pragma unroll
       for (int w = 0; w < NWV; ++w) v += red[w * RW + src];
     } else if (qs.slab && a >= o.qw && a < o.qw + qs.width) {
-      const float* qc = qs.slab + (a - o.qw);
-#pragma unroll 4
-      for (int r = q0; r < q1; ++r) v += qc[(size_t)r * qs.width];
+      v = qred[a - o.qw];
     }
     row[i] = v;
   }
@@ -1283,7 +1325,7 @@ inline size_t bwd3_smem(int n) {
   using G = Geo<16, 8>;
   const size_t shared = (size_t)((n * wl_stride(G::F) + 16 + 3) & ~3) * 4 + (size_t)B3::W2T * 2;
   const size_t act = shared + 4 * (size_t)B3::WAVE_BYTES;
-  const size_t red = sizeof(float) * 4 * (C2 * K2 + C1 * K1 + C1 + C2 + 16 + (size_t)n * G::F);
+  const size_t red = sizeof(float) * (4 * (C2 * K2 + C1 * K1 + C1 + C2 + 16 + (size_t)n * G::F) + 256);   // (+ qred)
   return act > red ? act : red;
 }
 
@@ -1405,6 +1447,7 @@ QD_API int qd_qsc2_bwd3(const float* x, const float* flat, const int* offs, cons
                         const void* w2t_img, void* stream) {
   if (H != 16 || W != 8 || n < 1 || n > 16 || B <= 0 || grid <= 0 || !p2 || !p1s || !c1 || !c2)
     return (int)hipErrorInvalidValue;
+  if (qslab && (qwidth < 1 || qwidth > 256)) return (int)hipErrorInvalidValue;   // (one column per thread: qred)
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   const size_t sm = bwd3_smem(n);
@@ -1421,6 +1464,7 @@ QD_API int qd_qsc2_bwd3_stamped(const float* x, const float* flat, const int* of
                                 const float* dang, float* dpre, float* slab, const float* p2, float* p1s, uint32_t* c1,
                                 uint8_t* c2, const float* qslab, int qrows, int qwidth, int B, int n, int grid,
                                 unsigned long long* stamps, void* stream) {
+  if (n < 1 || n > 16 || B <= 0 || grid <= 0 || (qslab && (qwidth < 1 || qwidth > 256))) return (int)hipErrorInvalidValue;
   Offs o{offs[0], offs[1], offs[2], offs[3], offs[4], offs[5], offs[6], offs[7], offs[8]};
   Saved sv{p1s, c1, c2};
   const size_t sm = bwd3_smem(n);

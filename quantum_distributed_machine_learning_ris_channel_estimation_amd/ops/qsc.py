@@ -32,11 +32,19 @@ from ..ops.quantum import HIP_REG_MAX_QUBITS, stream_sim_ok
 _p, _i, _f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
 
+def balanced_grid(samples: int, waves: int, cap: int) -> int:
+    """The fewest workgroups (<= cap) of ``waves`` one-sample-at-a-time waves that give every wave the same number
+    of samples as a grid of ``cap`` gives its busiest wave: 192 for 2304 samples, 4 waves, cap 256."""
+    spw = -(-samples // (waves * cap))
+    return -(-samples // (waves * spw))
+
+
 class QSCStepHIP:
     def __init__(self, model, space: FlatParamSpace, batch_total: int, n_groups: int = 1,
-                 grid_fwd: int = 512, grid_bwd: int = 256, impl: str = "mfma"):
+                 grid_fwd: int = 512, grid_bwd: int = 256, impl: str = "mfma", balance_bwd: bool = True):
         """impl: "mfma" (csrc/hip/qsc_mfma.hip: one wave per sample, fp32 MFMA convs; default) or
-        "ref" (csrc/hip/qsc.hip: one workgroup per sample, VALU convs)."""
+        "ref" (csrc/hip/qsc.hip: one workgroup per sample, VALU convs).  balance_bwd (mfma): shrink the
+        backward's grid below ``grid_bwd`` until every wave takes the same number of samples."""
         self.m = model
         self.space = space
         dev = space.flat.device
@@ -71,6 +79,11 @@ class QSCStepHIP:
             # at 2304 samples) in 4 of 4 same-box rounds (profiles/r2_20_*)
             self.grid_fwd = min(self.grid_fwd, KNOBS.qsc_fwd_cap)
             self.grid_bwd = min(-(-batch_total // wf(self.Ww, 1)), grid_bwd)
+            if balance_bwd:
+                # the workgroup's slab reduction waits for its slowest wave: at 2304 samples 256 workgroups of
+                # 4 waves give a quarter of the waves a third sample; 192 give every wave 3 (same box, 3 alternating
+                # rounds: 0.3780-0.3792 against 0.3806-0.3825 ms, profiles/r6_06_qsc_grid_fp8_ab.txt)
+                self.grid_bwd = balanced_grid(batch_total, wf(self.Ww, 1), self.grid_bwd)
             self.p2 = torch.empty(batch_total, feat, **f32)        # pool-2 features (linear weight grad)
             # saved by the forward for the backward: pool-1 map + both pools' argmax choices
             hw2 = self.Hh * self.Ww // 4

@@ -95,7 +95,7 @@ class FlagshipConfig:
     dp_plan: str = "zero"        # world > 1: "zero" = ZeRO-1 FC optimizer (reduce-scatter the FC gradient,
     #                              Adam on this rank's 1/world shard, all-gather the bf16 weight shadow) or
     #                              "allreduce" (all-reduce the FC gradient, every rank steps all of it)
-    qsc_grid_bwd: int = 0        # QSC backward workgroups (0: 256)
+    qsc_grid_bwd: int = 0        # QSC backward workgroups (0: at most 256, balanced to equal samples per wave)
     steps_per_graph: int = 1     # world 1: training steps captured per graph replay (run())
     lead_in: int = 1             # run(): the first lead_in steps replayed one step per graph -- a run that starts on
     #                              an idle GPU waits for its first graph's launch to be submitted, and a 1-step graph
@@ -219,9 +219,11 @@ class FlagshipTrainer(DPPlan):
             if self.zero:
                 self.hskip = self.qspace.grad[qe + 32:qe + 33]
         self.hstep.nmse.skip = self.hskip
-        gb = cfg.qsc_grid_bwd or 256   # (QSC backward workgroups: fewer measured slower, profiles/r2_20_variants.md)
+        # (QSC backward workgroups: at most 256, balanced to the same samples per wave -- 192 at 2304 samples --
+        # unless set; fewer measured slower, profiles/r2_20_variants.md, r6_06_qsc_grid_fp8_ab.txt)
+        gb = cfg.qsc_grid_bwd or 256
         self.cstep = ClassifierStep(self.qsc, self.S, space=self.qspace, batch_total=self.S * self.B,
-                                    skip=self.qskip, hip_kw={"grid_bwd": gb})
+                                    skip=self.qskip, hip_kw={"grid_bwd": gb, "balance_bwd": not cfg.qsc_grid_bwd})
         self.cstep.skip_add = False
         self.cstep.writes_grads = self.cstep.hip is not None
         # buckets (see _dp_run): "fc" = 33.6 MB FC grads (in place; + the HDCE NaN flag in the all-reduce plan),
