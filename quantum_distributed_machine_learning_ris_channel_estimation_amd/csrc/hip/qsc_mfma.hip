@@ -507,6 +507,54 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   }
 }
 
+// The workgroup's slab row from its waves' partial rows (red: NWV rows of RW floats, w2 | w1 | b1 | b2 | bl (16 slots) |
+// wl [n][F] from RW0 when wl_here) and the quantum-slab column sums (qred: 256 floats, zero past qs.width; null: summed
+// here from the rows [q0, q1) of qs), four columns per thread and step (round 6: one column per step ran a ~90-instruction
+// range search per column, ~17k cycles per workgroup, profiles/r6_07_*).  Every flat range starts on a 16-float boundary
+// (FlatParamSpace ALIGN) and the partial rows hold zeros past a range's end up to its 4-float boundary, so a 4-column
+// chunk never mixes two ranges; every sum runs in the order of the one-column loop (bit-identical slab rows).
+template <int NWV>
+__device__ __forceinline__ void slab_row_out(float* __restrict__ row, const float* red, int RW, int RW0,
+                                             const float* qred, QSlab qs, int q0, int q1, Offs o, int n, int F,
+                                             bool wl_here) {
+  for (int i = 4 * threadIdx.x; i < o.row; i += 4 * 64 * NWV) {
+    const int a = i + o.base;   // flat offset of the chunk's first column
+    int src = -1;
+    if (a >= o.w2 && a < o.w2 + C2 * K2) src = a - o.w2;
+    else if (a >= o.w1 && a < o.w1 + C1 * K1) src = C2 * K2 + (a - o.w1);
+    else if (a >= o.b1 && a < o.b1 + C1) src = C2 * K2 + C1 * K1 + (a - o.b1);
+    else if (a >= o.b2 && a < o.b2 + C2) src = C2 * K2 + C1 * K1 + C1 + (a - o.b2);
+    else if (a >= o.bl && a < o.bl + n) src = C2 * K2 + C1 * K1 + C1 + C2 + (a - o.bl);
+    else if (wl_here && a >= o.wl && a < o.wl + n * F) src = RW0 + (a - o.wl);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (src >= 0) {
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) {
+        const float4 r = *reinterpret_cast<const float4*>(red + w * RW + src);
+        v.x += r.x;
+        v.y += r.y;
+        v.z += r.z;
+        v.w += r.w;
+      }
+    } else if (qs.slab && a >= o.qw && a < o.qw + qs.width) {
+      if (qred) {
+        v = *reinterpret_cast<const float4*>(qred + (a - o.qw));
+      } else {
+        float e[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (a + c < o.qw + qs.width) {
+            const float* qc = qs.slab + (a + c - o.qw);
+#pragma unroll 4
+            for (int r = q0; r < q1; ++r) e[c] += qc[(size_t)r * qs.width];
+          }
+        v = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+    *reinterpret_cast<float4*>(row + i) = v;
+  }
+}
+
 // Backward.  dang (B, n) = dL/d(angles).  Outputs: dpre (B, n) = dL/d(pre-tanh), slab row per
 // workgroup = grads of [w1 | b1 | w2 | b2 | wl | bl] in the flat layout starting at o.w1 (wl
 // columns zero when n > 64 / (F / 64): the caller then forms dWl = dpre^T p2 with a GEMM).
@@ -815,26 +863,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd_kernel(const float* __restr
   // this workgroup's share of the quantum-layer slab rows
   const int q0 = (int)((long long)qs.rows * blockIdx.x / gridDim.x);
   const int q1 = (int)((long long)qs.rows * (blockIdx.x + 1) / gridDim.x);
-  for (int i = threadIdx.x; i < o.row; i += 64 * NWV) {
-    float v = 0.f;
-    int src = -1;
-    const int a = i + o.base;   // flat offset of this column
-    if (a >= o.w2 && a < o.w2 + C2 * K2) src = a - o.w2;
-    else if (a >= o.w1 && a < o.w1 + C1 * K1) src = C2 * K2 + (a - o.w1);
-    else if (a >= o.b1 && a < o.b1 + C1) src = C2 * K2 + C1 * K1 + (a - o.b1);
-    else if (a >= o.b2 && a < o.b2 + C2) src = C2 * K2 + C1 * K1 + C1 + (a - o.b2);
-    else if (a >= o.bl && a < o.bl + n) src = C2 * K2 + C1 * K1 + C1 + C2 + (a - o.bl);
-    else if (wl_here && a >= o.wl && a < o.wl + n * G::F) src = RW0 + (a - o.wl);
-    if (src >= 0) {
-#pragma unroll
-      for (int w = 0; w < NWV; ++w) v += red[w * RW + src];
-    } else if (qs.slab && a >= o.qw && a < o.qw + qs.width) {
-      const float* qc = qs.slab + (a - o.qw);
-#pragma unroll 4
-      for (int r = q0; r < q1; ++r) v += qc[(size_t)r * qs.width];
-    }
-    row[i] = v;
-  }
+  slab_row_out<NWV>(row, red, RW, RW0, nullptr, qs, q0, q1, o, n, G::F, wl_here);
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -1285,35 +1314,20 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_bwd3_kernel(const float* __rest
     if ((lane & 1) == 0) mine[C2 * K2 + C1 * K1 + C1 + (lane >> 1)] = v;
   }
   if (lane < 16) mine[C2 * K2 + C1 * K1 + C1 + C2 + lane] = lane < n ? gbl : 0.f;
-  float* qred = red + NWV * RW;   // the quantum slab columns' sums, by column (bwd3_smem counts 256 floats)
-  if (q_mine) {
+  float* qred = red + NWV * RW;   // the quantum slab columns' sums by column, zero past qs.width (bwd3_smem: 256 floats)
+  {
     float v = 0.f;
+    if (q_mine) {
 #pragma unroll
-    for (int k = 0; k < QPF; ++k) v += qv[k];
-    const float* qc = qs.slab + threadIdx.x;
-    for (int r = q0 + QPF; r < q1; ++r) v += qc[(size_t)r * qs.width];
+      for (int k = 0; k < QPF; ++k) v += qv[k];
+      const float* qc = qs.slab + threadIdx.x;
+      for (int r = q0 + QPF; r < q1; ++r) v += qc[(size_t)r * qs.width];
+    }
     qred[threadIdx.x] = v;
   }
   __syncthreads();
   float* row = slab + (size_t)blockIdx.x * o.row;
-  for (int i = threadIdx.x; i < o.row; i += 64 * NWV) {
-    float v = 0.f;
-    int src = -1;
-    const int a = i + o.base;
-    if (a >= o.w2 && a < o.w2 + C2 * K2) src = a - o.w2;
-    else if (a >= o.w1 && a < o.w1 + C1 * K1) src = C2 * K2 + (a - o.w1);
-    else if (a >= o.b1 && a < o.b1 + C1) src = C2 * K2 + C1 * K1 + (a - o.b1);
-    else if (a >= o.b2 && a < o.b2 + C2) src = C2 * K2 + C1 * K1 + C1 + (a - o.b2);
-    else if (a >= o.bl && a < o.bl + n) src = C2 * K2 + C1 * K1 + C1 + C2 + (a - o.bl);
-    else if (wl_here && a >= o.wl && a < o.wl + n * G::F) src = RW0 + (a - o.wl);
-    if (src >= 0) {
-#pragma unroll
-      for (int w = 0; w < NWV; ++w) v += red[w * RW + src];
-    } else if (qs.slab && a >= o.qw && a < o.qw + qs.width) {
-      v = qred[a - o.qw];
-    }
-    row[i] = v;
-  }
+  slab_row_out<NWV>(row, red, RW, RW0, qred, qs, q0, q1, o, n, G::F, wl_here);
   if constexpr (STAMP) {
     ts[9] = stamp();
     if (lane == 0)
