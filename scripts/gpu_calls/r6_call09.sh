@@ -1,0 +1,23 @@
+#!/bin/bash
+# round-6 GPU call 9 (call 8 got no box; this one covers it): the P128 QSC forward's conv1 + ReLU + pool 1 on bf16x3
+# MFMAs (conv1_mfma) and the backward's 4-column slab rows: QSC + flagship GPU tests, forward and bwd3 phase stamps
+# new vs base (lib_base), bench --steps 300 alternating new / base, 3 rounds
+set -o pipefail
+cd "$(dirname "$0")/../.." || exit 1
+R=$(pwd); O=$R/gpurun_out; P=r6_09
+BASE=$R/quantum_distributed_machine_learning_ris_channel_estimation_amd/lib_base
+timeout -k 10 600 python -u -m pytest tests/test_qsc_gpu.py tests/test_flagship_gpu.py tests/test_lds_poison_gpu.py -x -q -s --timeout 240 --timeout-method thread > $O/${P}_pytest.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/${P}_pytest.log
+tail -3 $O/${P}_pytest.log; grep "conv1 MFMA\|angles:" $O/${P}_pytest.log
+[ $rc -eq 0 ] || exit 1
+for v in new base; do
+  if [ $v = base ]; then export QDML_LIB_DIR=$BASE; fi
+  timeout -k 10 120 python scripts/probes/stamp_qsc.py > $O/${P}_stamp_fwd_$v.json 2>$O/${P}_stamp_fwd_$v.err || { tail -5 $O/${P}_stamp_fwd_$v.err; exit 1; }
+  timeout -k 10 120 python scripts/probes/stamp_qsc_bwd3.py > $O/${P}_stamp_bwd3_$v.json 2>$O/${P}_stamp_bwd3_$v.err || { tail -5 $O/${P}_stamp_bwd3_$v.err; exit 1; }
+  python -c "import json; a=json.load(open('$O/${P}_stamp_fwd_$v.json')); b=json.load(open('$O/${P}_stamp_bwd3_$v.json')); print('$v fwd', {k: v['median_cycles'] for k, v in a.items() if isinstance(v, dict) and 'median_cycles' in v}, a['wave_lifetime_median_cycles']); print('$v bwd3', b)"
+done
+unset QDML_LIB_DIR
+B() { n=$1; shift; timeout -k 10 300 "$@" > $O/${P}_$n.json 2>$O/${P}_$n.err || { tail -5 $O/${P}_$n.err; exit 1; }; python -c "import json; d=json.load(open('$O/${P}_$n.json')); print('$n', d['ms_per_step'], d['replays'][:3], d['replay_rates_ms']['gpu'], d['step_spread']['median_ms'], d['steps_trained'], d['final_losses']['qsc_nll'], d['final_losses']['hdce_nmse'])" | tee -a $O/${P}_ab.txt; }
+for r in 1 2 3; do
+  B new_$r python bench.py --steps 300 --warmup 20
+  B base_$r env QDML_LIB_DIR=$BASE python bench.py --steps 300 --warmup 20
+done

@@ -161,3 +161,33 @@ def test_classifier_validation_runs_on_hip_kernels(cuda, n):
     assert got.shape == ref.shape
     assert float((got - ref).abs().max()) < 2e-4, float((got - ref).abs().max())
     assert torch.equal(got.argmax(1), ref.argmax(1))
+
+
+def test_qsc_fwd_conv1_on_mfma_matches_f32_forward(cuda):
+    """Round 6: the P128 forward's conv1 + ReLU + pool 1 on bf16x3 MFMAs (qsc_mfma.hip conv1_mfma) vs the f32
+    forward's VALU conv1: the saved pool-1 map agrees to fp32 grade and the saved window choices (2-bit codes per
+    channel) everywhere but near-ties."""
+    torch.manual_seed(1)
+    B = 2304
+    a = QSC_P128(n_qubits=8, use_quantumnat=False, use_gradient_pruning=False).to(cuda)
+    space = FlatParamSpace(list(a.named_parameters()), cuda)
+    x = torch.randn(B, 2, 16, 8, device=cuda)
+    y = torch.randint(0, 3, (B,), device=cuda)
+    step = QSCStepHIP(a, space, B)
+    assert step.fwd_x3
+    saved = []
+    for x3 in (True, False):
+        step.fwd_x3 = x3
+        step.forward_part(x, y)
+        torch.cuda.synchronize()
+        saved.append((step.p1s.clone(), step.c1.clone(), step.angles.clone()))
+    (p3, c3, a3), (pf, cf, af) = saved
+    shifts = torch.arange(0, 32, 2, device=cuda, dtype=torch.int32)
+    k3 = (c3.unsqueeze(-1) >> shifts) & 3
+    kf = (cf.unsqueeze(-1) >> shifts) & 3
+    diff = float((k3 != kf).float().mean())
+    err = float((p3 - pf).abs().max() / pf.abs().max())
+    print(f"conv1 MFMA vs f32: window-choice mismatch {diff:.2e}, pool-1 max-rel {err:.2e}")
+    assert diff < 1e-4, diff
+    assert err < 1e-5, err
+    assert float((a3 - af).abs().max()) < 1e-4
