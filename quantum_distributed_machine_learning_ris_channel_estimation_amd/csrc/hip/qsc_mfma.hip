@@ -216,42 +216,36 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
   }
 }
 
-// conv1 (+bias) + ReLU + pool 1 on bf16x3 MFMAs (P128, W = 8; round 6).  Per band of two image rows one
-// 16x16x32 tile: rows = the band's 16 positions (row r: image row 2 band + r / 8, column r % 8), columns = the 16
-// output channels, K = the 18 (ci, tap) padded to 32; three MFMAs (hi.hi + hi.lo + lo.hi: fp32-grade, as conv2) in
-// place of conv1_half's 576 VALU FMAs and 288 readfirstlanes per lane.  The accumulator gives lane (channel
+// conv1 (+bias) + ReLU + pool 1 on f32 MFMAs (P128, W = 8; round 6).  Per band of two image rows one 16x16 tile:
+// rows = the band's 16 positions (row r: image row 2 band + r / 8, column r % 8), columns = the 16 output channels,
+// K = the 18 (ci, tap) in five 16x16x4 f32 steps (fp32 products, as the VALU loop: a bf16x3 form measured 2.4e-3
+// max-rel on conv1's weight gradient against autograd at B = 300 through flipped near-tie pool choices) in place
+// of conv1_half's 576 VALU FMAs and 288 readfirstlanes per lane.  The accumulator gives lane (channel
 // c = lane & 15, group g = lane >> 4) the positions 4 g .. 4 g + 3 -- two horizontal pool pairs of one row -- and
 // lanes l, l ^ 32 hold the two rows of the same windows.  Same outputs and tie rules as the conv1_half loop:
-// the padded channel-last pool-1 image, p1g and the window codes c1g.  w1x3: this lane's B fragment
-// W1[c][8 g .. 8 g + 7] (zero past k = 17) as bf16 hi / lo; b1c = b1[c].
+// the padded channel-last pool-1 image, p1g and the window codes c1g.  w1f: this lane's B operands
+// W1[c][4 i + g] (zero past k = 17), i = 0..4; b1c = b1[c].
 template <int H, int W>
-__device__ __forceinline__ void conv1_mfma(float* act, int lane, const bf16x8_t (&w1x3)[2], float b1c,
+__device__ __forceinline__ void conv1_mfma(float* act, int lane, const float (&w1f)[5], float b1c,
                                            float* __restrict__ p1g, uint32_t* __restrict__ c1g) {
   using G = Geo<H, W>;
   static_assert(W == 8 && H % 2 == 0, "bands of two 8-wide rows");
   const int g = lane >> 4, c = lane & 15;
   const int ry = c >> 3, rx = c & 7;   // (A operand: this lane's position row = lane & 15)
-  int aoff[8];
+  int aoff[5];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * g + j, ci = k / 9, t = k % 9;
-    aoff[j] = k < K1 ? G::o_x + ci * G::XP + (ry + t / 3) * G::XW + rx + t % 3 : -1;
+  for (int i = 0; i < 5; ++i) {
+    const int k = 4 * i + g, ci = k / 9, t = k % 9;
+    aoff[i] = k < K1 ? G::o_x + ci * G::XP + (ry + t / 3) * G::XW + rx + t % 3 : -1;
   }
 #pragma unroll 2
   for (int band = 0; band < H / 2; ++band) {
-    bf16x8_t ah, al;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float a = aoff[j] >= 0 ? act[aoff[j] + 2 * band * G::XW] : 0.f;
-      __bf16 h, l;
-      split_bf16(a, h, l);
-      ah[j] = h;
-      al[j] = l;
-    }
     f32x4 acc = {b1c, b1c, b1c, b1c};
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w1x3[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, w1x3[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, w1x3[0], acc, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const float av = aoff[i] >= 0 ? act[aoff[i] + 2 * band * G::XW] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w1f[i], acc, 0, 0, 0);
+    }
     float v[2];
     uint32_t rt[2];
 #pragma unroll
@@ -294,7 +288,7 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
                                                const float* __restrict__ b1g, float bias2,
                                                float* __restrict__ p1g, uint32_t* __restrict__ c1g,
                                                unsigned long long* ts = nullptr, const bf16x8_t* wx3 = nullptr,
-                                               const float4* xpre = nullptr, const bf16x8_t* w1x3 = nullptr,
+                                               const float4* xpre = nullptr, const float* w1f = nullptr,
                                                float b1c = 0.f) {
   using G = Geo<H, W>;
   static_assert(W % 4 == 0, "float4 rows");
@@ -312,7 +306,7 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
   wave_lds_fence();
   if constexpr (STAMP) ts[2] = stamp();
   if constexpr (X3 && W == 8) {
-    conv1_mfma<H, W>(act, lane, *reinterpret_cast<const bf16x8_t(*)[2]>(w1x3), b1c, p1g, c1g);
+    conv1_mfma<H, W>(act, lane, *reinterpret_cast<const float(*)[5]>(w1f), b1c, p1g, c1g);
   } else {
   // conv1 + ReLU + pool: lane = (window, row of the window); the two rows meet with one shuffle
   static_assert((2 * G::HW2) % 64 == 0, "whole waves per conv1 pass");
@@ -482,15 +476,14 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
     }
   }
   const float bias2 = flat[o.b2 + (lane & 31)];
-  // conv1 on MFMAs (X3, W = 8: conv1_mfma): this lane's B fragment W1[c][8 g ..] and b1[c], c = lane & 15
+  // conv1 on MFMAs (X3, W = 8: conv1_mfma): this lane's B operands W1[c][4 i + g] and b1[c], c = lane & 15
   constexpr bool C1M = X3 && W == 8;
-  [[maybe_unused]] bf16x8_t w1x3[2];
-  [[maybe_unused]] float vw1x[8], b1c = 0.f;
+  [[maybe_unused]] float w1f[5], b1c = 0.f;
   if constexpr (C1M) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * (lane >> 4) + j;
-      vw1x[j] = k < K1 ? flat[o.w1 + (lane & 15) * K1 + k] : 0.f;
+    for (int i = 0; i < 5; ++i) {
+      const int k = 4 * i + (lane >> 4);
+      w1f[i] = k < K1 ? flat[o.w1 + (lane & 15) * K1 + k] : 0.f;
     }
     b1c = flat[o.b1 + (lane & 15)];
   }
@@ -514,15 +507,7 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
   for (int j = 0; j < 8; ++j)
 #pragma unroll
     for (int t = 0; t < 9; ++t) wreg[t * 8 + j] = tmp[j * 9 + t];
-  if constexpr (C1M) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      __bf16 h, l;
-      split_bf16(vw1x[j], h, l);
-      w1x3[0][j] = h;
-      w1x3[1][j] = l;
-    }
-  }
+
   [[maybe_unused]] bf16x8_t wx3[X3 ? 18 : 1];
   if constexpr (X3) {
 #pragma unroll
@@ -558,10 +543,10 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
     const float4* xp = s == blockIdx.x * NWV + wv ? &xpre : nullptr;
     if (STAMP && first)
       sample_forward<H, W, true, true, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, w1s, w1s + C1 * K1,
-                                           bias2, p1g, c1g, ts, wx3, xp, w1x3, b1c);
+                                           bias2, p1g, c1g, ts, wx3, xp, w1f, b1c);
     else
       sample_forward<H, W, true, false, X3>(x + (size_t)s * 2 * G::HW, ws, act, lane, wreg, w1s, w1s + C1 * K1,
-                                            bias2, p1g, c1g, nullptr, wx3, xp, w1x3, b1c);
+                                            bias2, p1g, c1g, nullptr, wx3, xp, w1f, b1c);
     float* p2s = act + G::o_p2f;
 #pragma unroll
     for (int i = 0; i < G::F / 64; ++i) {

@@ -164,9 +164,9 @@ def test_classifier_validation_runs_on_hip_kernels(cuda, n):
 
 
 def test_qsc_fwd_conv1_on_mfma_matches_f32_forward(cuda):
-    """Round 6: the P128 forward's conv1 + ReLU + pool 1 on bf16x3 MFMAs (qsc_mfma.hip conv1_mfma) vs the f32
-    forward's VALU conv1: the saved pool-1 map agrees to fp32 grade and the saved window choices (2-bit codes per
-    channel) everywhere but near-ties."""
+    """Round 6: the P128 forward's conv1 + ReLU + pool 1 on f32 MFMAs (qsc_mfma.hip conv1_mfma, the bf16x3 forward)
+    vs the f32 forward's VALU conv1: the saved pool-1 map agrees to fp32 grade and the saved window choices (2-bit
+    codes per channel) everywhere but near-ties."""
     torch.manual_seed(1)
     B = 2304
     a = QSC_P128(n_qubits=8, use_quantumnat=False, use_gradient_pruning=False).to(cuda)
