@@ -225,50 +225,61 @@ __device__ __forceinline__ void conv1_half(const float* act, const float* __rest
 // lanes l, l ^ 32 hold the two rows of the same windows.  Same outputs and tie rules as the conv1_half loop:
 // the padded channel-last pool-1 image, p1g and the window codes c1g.  w1f: this lane's B operands
 // W1[c][4 i + g] (zero past k = 17), i = 0..4; b1c = b1[c].
+__device__ __forceinline__ uint32_t spread_even16(uint32_t x) {   // bit i -> bit 2 i (16 bits)
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  return (x | (x << 1)) & 0x55555555u;
+}
 template <int H, int W>
 __device__ __forceinline__ void conv1_mfma(float* act, int lane, const float (&w1f)[5], float b1c,
                                            float* __restrict__ p1g, uint32_t* __restrict__ c1g) {
   using G = Geo<H, W>;
   static_assert(W == 8 && H % 2 == 0, "bands of two 8-wide rows");
+  constexpr int NB = H / 2;
   const int g = lane >> 4, c = lane & 15;
+  const bool top = g < 2;
   const int ry = c >> 3, rx = c & 7;   // (A operand: this lane's position row = lane & 15)
-  int aoff[5];
+  // every band's A operands first (40 LDS reads in flight), then the MFMA chains
+  float av[NB][5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
     const int k = 4 * i + g, ci = k / 9, t = k % 9;
-    aoff[i] = k < K1 ? G::o_x + ci * G::XP + (ry + t / 3) * G::XW + rx + t % 3 : -1;
+    const int off = G::o_x + ci * G::XP + (ry + t / 3) * G::XW + rx + t % 3;
+#pragma unroll
+    for (int band = 0; band < NB; ++band) av[band][i] = k < K1 ? act[off + 2 * band * G::XW] : 0.f;
   }
-#pragma unroll 2
-  for (int band = 0; band < H / 2; ++band) {
+#pragma unroll
+  for (int band = 0; band < NB; ++band) {
     f32x4 acc = {b1c, b1c, b1c, b1c};
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const float av = aoff[i] >= 0 ? act[aoff[i] + 2 * band * G::XW] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w1f[i], acc, 0, 0, 0);
-    }
-    float v[2];
-    uint32_t rt[2];
+    for (int i = 0; i < 5; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[band][i], w1f[i], acc, 0, 0, 0);
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
       const float r0 = relu(acc[2 * w]), r1 = relu(acc[2 * w + 1]);
-      v[w] = max_nan(r0, r1);
-      rt[w] = (uint32_t)(r1 > r0);   // ties go to the left column
-    }
-#pragma unroll
-    for (int w = 0; w < 2; ++w) {
-      const float pv = __shfl_xor(v[w], 32);             // the other row of the window
-      const uint32_t prt = (uint32_t)__shfl_xor((int)rt[w], 32);
-      const float m = g < 2 ? max_nan(v[w], pv) : max_nan(pv, v[w]);
-      const bool bottom = g < 2 ? pv > v[w] : v[w] > pv;   // ties go to the top row
-      const uint32_t rtop = g < 2 ? rt[w] : prt, rbot = g < 2 ? prt : rt[w];
-      uint32_t code = (bottom ? 2u + rbot : rtop) << (2 * c);
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) code |= (uint32_t)__shfl_xor((int)code, off);
-      if (g < 2) {
+      const float v = max_nan(r0, r1);
+      const uint32_t rt = (uint32_t)(r1 > r0);   // ties go to the left column
+      // the other row of the window: lanes l and l ^ 32 swap (v_permlane32_swap, no LDS round trip)
+      const auto sv = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, v),
+                                                       __builtin_bit_cast(uint32_t, v), false, false);
+      const auto sr = __builtin_amdgcn_permlane32_swap(rt, rt, false, false);
+      const float pv = __builtin_bit_cast(float, top ? sv[1] : sv[0]);
+      const uint32_t prt = top ? sr[1] : sr[0];
+      const float m = top ? max_nan(v, pv) : max_nan(pv, v);
+      const bool bottom = top ? pv > v : v > pv;   // ties go to the top row
+      const uint32_t rtop = top ? rt : prt, rbot = top ? prt : rt;
+      // window codes: 2 bits per channel = per lane of a group -- two ballots, the bits interleaved in SGPRs
+      const unsigned long long b1 = __ballot(bottom);
+      const unsigned long long b0 = __ballot(bottom ? rbot != 0u : rtop != 0u);
+      if (top) {
         const int qx = 2 * g + w, win = band * G::W2 + qx;
         act[G::o_p1 + ((band + 1) * G::PW + qx + 1) * G::PC + c] = m;
         p1g[win * C1 + c] = m;
-        if (c == 0) c1g[win] = code;
+        if (c == 0) {
+          const uint32_t sh = 16u * (uint32_t)g;
+          c1g[win] = spread_even16((uint32_t)(b0 >> sh) & 0xFFFFu) |
+                     (spread_even16((uint32_t)(b1 >> sh) & 0xFFFFu) << 1);
+        }
       }
     }
   }
