@@ -585,7 +585,21 @@ __global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, 
       li[pad(k)] = o * v.y;
     }
     wave_lds_fence();
+    // (round 6: every global load of the layer loop issued ahead of its use -- the gate angles of all layers here,
+    // each layer's two operand images at the layer's top, behind the ring / cross-density work; loaded where
+    // they were used, each was one exposed round trip, seven per sample at L = 3)
+    float th[8];
+    if (lane < N8) {
+#pragma unroll
+      for (int l = 0; l < 8; ++l) th[l] = l < L ? wg[2 * N8 * l + 2 * lane + 1] : 0.f;
+    }
     for (int l = L - 1; l >= 0; --l) {
+      Op a0, a1;
+      if (l > 0) {
+        const h8* lm = img + ((size_t)grp * (L - 1) + (l - 1)) * (2 * 2 * IMG_H8);
+        a0 = load_op(lm + (0 * 2 + 1) * IMG_H8, lane);
+        a1 = load_op(lm + (1 * 2 + 1) * IMG_H8, lane);
+      }
       float v[4][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -624,8 +638,10 @@ __global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, 
       if (lane < N8) {
         const int q = lane;
         const float* rq = rho + q * 8;
-        float sp, cp;
-        __sincosf(wg[2 * N8 * l + 2 * q + 1], &sp, &cp);
+        float sp, cp, t = th[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) t = l == k ? th[k] : t;   // (static register index: no scratch)
+        __sincosf(t, &sp, &cp);
         const float dphi = rq[1] - rq[7];
         const float dth = (cp * rq[4] - sp * rq[5]) - (cp * rq[2] + sp * rq[3]);
         acc[(l * N8 + q) * 2] += dth;
@@ -634,12 +650,9 @@ __global__ void __launch_bounds__(256) bwd8_kernel(const float* __restrict__ x, 
       }
       wave_lds_fence();
       if (l > 0) {
-        const h8* lm = img + ((size_t)grp * (L - 1) + (l - 1)) * (2 * 2 * IMG_H8);
-        const Op a0 = load_op(lm + (0 * 2 + 1) * IMG_H8, lane);
         mode8<0>(pr, pi, a0, lane);
         mode8<0>(lr, li, a0, lane);
         wave_lds_fence();
-        const Op a1 = load_op(lm + (1 * 2 + 1) * IMG_H8, lane);
         mode8<1>(pr, pi, a1, lane);
         mode8<1>(lr, li, a1, lane);
         wave_lds_fence();

@@ -172,8 +172,12 @@ QD_API int qd_coh_busy(float* x, int n, int iters, int grid, void* stream) {
 // (backtrace_symbols_fd: library + offset of every frame) to stderr, restores the previous action and
 // returns, so the fault re-raises into the previous handler (Python's faulthandler: the Python frames) and
 // finally the default action (exit status 139 / 134).  Async-signal-safe calls only.
+// QDML_CRASH_LOG (a file path) also sends the report to that file: under pytest's output capture fd 2 is a
+// temporary file that dies with the process (round 6, profiles/r6_11_pytest.log: faulthandler's frames only).
 #include <execinfo.h>
+#include <fcntl.h>
 #include <signal.h>
+#include <stdlib.h>
 #include <string.h>
 #include <unistd.h>
 
@@ -182,9 +186,11 @@ namespace rt {
 constexpr int kCrashSigs[3] = {SIGSEGV, SIGBUS, SIGABRT};
 struct sigaction g_prev[3];
 volatile sig_atomic_t g_installed = 0;
+int g_logfd = -1;
 
 void crash_write(const char* s) {
   ssize_t r = write(2, s, strlen(s));
+  if (g_logfd >= 0) r = write(g_logfd, s, strlen(s));
   (void)r;
 }
 
@@ -208,6 +214,7 @@ void crash_handler(int sig, siginfo_t* info, void* uctx) {
   void* frames[64];
   const int nf = backtrace(frames, 64);
   backtrace_symbols_fd(frames, nf, 2);
+  if (g_logfd >= 0) backtrace_symbols_fd(frames, nf, g_logfd);
   crash_write("[qdml] end of native frames\n");
   // hand the signal on: the previous action (faulthandler, then the default) runs when the fault re-raises
   if (k < 3) sigaction(sig, &g_prev[k], nullptr);
@@ -221,6 +228,8 @@ extern "C" int qd_install_crash_handler() {
   if (g_installed) return 0;
   void* warm[2];
   backtrace(warm, 2);   // (loads libgcc's unwinder now: backtrace() may allocate on its first call)
+  if (const char* path = getenv("QDML_CRASH_LOG"))
+    if (path[0]) g_logfd = open(path, O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
   for (int k = 0; k < 3; ++k) {
     struct sigaction sa;
     memset(&sa, 0, sizeof(sa));

@@ -12,6 +12,7 @@ timestamp per HDCE epoch (R:173).  Here:
 """
 from __future__ import annotations
 
+import atexit
 import contextlib
 import ctypes
 import os
@@ -74,6 +75,25 @@ class EventTimer:
         return {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in self.events.items()}
 
 
+_GRAVEYARD: list = []   # graph executables of dropped GraphedSteps, destroyed at the next safe point
+
+
+def release_dropped_graphs() -> None:
+    """Destroy the parked graph executables (GraphedStep.close / __del__) after a device sync -- from a safe point
+    only: never while a capture is running (a sync there invalidates it), never from a finaliser."""
+    if not _GRAVEYARD:
+        return
+    if torch.cuda.is_available():
+        if torch.cuda.is_current_stream_capturing():
+            return
+        torch.cuda.synchronize()
+    while _GRAVEYARD:
+        _GRAVEYARD.pop().reset()
+
+
+atexit.register(release_dropped_graphs)
+
+
 class GraphedStep:
     """Capture ``fn`` (which reads/writes only static tensors) into a HIP graph.
 
@@ -102,6 +122,7 @@ class GraphedStep:
 
     def capture(self) -> None:
         from ..parallel.watchdog import capturing, heartbeat
+        release_dropped_graphs()   # (a safe point: no capture or replay of ours is running)
         # eager warm-ups (real collectives under the DP plans) stay visible to the failure detector: only the
         # capture itself pauses it (a peer that dies during a warm-up or the pre-capture sync is a stall)
         s = torch.cuda.Stream()
@@ -132,15 +153,19 @@ class GraphedStep:
         self.enabled = False
         self.fn = None   # (breaks the trainer -> graph set -> step -> bound method cycle)
         if g is not None:
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-            g.reset()
+            _GRAVEYARD.append(g)
+        release_dropped_graphs()
 
     def __del__(self) -> None:
+        # no HIP call here: the garbage collector can run this in the middle of another graph's capture or replay
+        # (round 6: the round-5 hipGraphLaunch segfault recurred in a replay after earlier tests' graphs were
+        # dropped by collection, profiles/r6_11_pytest.log).  The executable is parked and destroyed at the next
+        # safe point (release_dropped_graphs: the next capture, close(), exit).
         try:
             if self.graph is not None:
-                self.close()
-        except Exception:   # (interpreter shutdown: torch may already be gone)
+                _GRAVEYARD.append(self.graph)
+                self.graph = None
+        except Exception:   # (interpreter shutdown)
             pass
 
     def pre_capture(self) -> None:

@@ -5,6 +5,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# on a GPU box: the native crash report (csrc/hip/runtime.hip crash_handler) also goes to a file that outlives
+# pytest's capture of fd 2 (a host fault kills the process before the captured output is shown)
+if os.environ.get("GRAFT_REPO_ROOT") and "QDML_CRASH_LOG" not in os.environ:
+    _out = os.path.join(os.environ["GRAFT_REPO_ROOT"], "gpurun_out")
+    os.makedirs(_out, exist_ok=True)
+    os.environ["QDML_CRASH_LOG"] = os.path.join(_out, "native_crash.log")
 
 
 def pytest_configure(config):

@@ -45,3 +45,20 @@ def test_crash_handler_can_be_turned_off():
     p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, QDML_CRASH_HANDLER="0"))
     assert p.returncode == -11 and "[qdml] SIGSEGV" not in p.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libqdml_hip.so not built")
+def test_crash_report_also_goes_to_the_crash_log(tmp_path):
+    """QDML_CRASH_LOG: the native frames also land in a file (pytest's capture of fd 2 dies with the process)."""
+    log = tmp_path / "crash.log"
+    script = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {REPO!r})
+        from quantum_distributed_machine_learning_ris_channel_estimation_amd import _native as nat
+        nat.hip_lib(build_if_missing=False).qd_crash_for_test()
+    """)
+    p = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, QDML_CRASH_LOG=str(log)))
+    assert p.returncode == -11
+    text = log.read_text()
+    assert "[qdml] SIGSEGV" in text and "libqdml_hip.so" in text and "end of native frames" in text, text
