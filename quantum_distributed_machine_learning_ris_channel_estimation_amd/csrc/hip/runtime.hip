@@ -173,7 +173,7 @@ QD_API int qd_coh_busy(float* x, int n, int iters, int grid, void* stream) {
 // returns, so the fault re-raises into the previous handler (Python's faulthandler: the Python frames) and
 // finally the default action (exit status 139 / 134).  Async-signal-safe calls only.
 // QDML_CRASH_LOG (a file path) also sends the report to that file: under pytest's output capture fd 2 is a
-// temporary file that dies with the process (round 6, profiles/r6_11_pytest.log: faulthandler's frames only).
+// temporary file that dies with the process (round 6, profiles/r6_11a_pytest_segfault.log: faulthandler's frames only).
 #include <execinfo.h>
 #include <fcntl.h>
 #include <signal.h>

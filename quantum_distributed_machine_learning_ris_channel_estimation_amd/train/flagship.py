@@ -733,9 +733,9 @@ class FlagshipTrainer(DPPlan):
         return self.S * self.B
 
     def close(self) -> None:
-        """Release every captured graph set now (GraphedStep.close: device sync, then the executables and their
-        pools), instead of whenever the garbage collector reaches them -- possibly in the middle of another
-        trainer's capture or replay.  Idempotent; the trainer cannot step afterwards."""
+        """Retire every captured graph set now (GraphedStep.close: the executables are parked and destroyed at exit
+        -- utils/profiling.py GRAPH_RELEASE -- never by whichever garbage collection reaches them, possibly in the
+        middle of another trainer's capture or replay).  Idempotent; the trainer cannot step afterwards."""
         for gs in list(getattr(self, "_graph_sets", {}).values()):
             for g in gs:
                 g.close()

@@ -75,13 +75,21 @@ class EventTimer:
         return {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in self.events.items()}
 
 
-_GRAVEYARD: list = []   # graph executables of dropped GraphedSteps, destroyed at the next safe point
+_GRAVEYARD: list = []   # graph executables of closed / dropped GraphedSteps, destroyed at exit (or a safe point)
+# When a parked executable is destroyed.  "exit" (default): at interpreter exit only.  Round 6's native crash
+# report (profiles/r6_11b_bench_forced_segfault.txt) put the recurring host segfault of hipGraphLaunch (rounds 5
+# and 6, multi-stream graphs) inside the HIP runtime's graph scheduling (hip_graph_internal.cpp: a node pointer
+# read as 0x21, then +0x1a8 dereferenced), and every occurrence followed the destruction of OTHER graph executables
+# in the same process (earlier tests' trainers, bench.py's losing plan candidates).  Their device memory stays
+# reserved until exit (a few GB per flagship trainer: HBM has room).  "sync": destroy at the next safe point.
+GRAPH_RELEASE = os.environ.get("QDML_GRAPH_RELEASE", "exit")
 
 
-def release_dropped_graphs() -> None:
-    """Destroy the parked graph executables (GraphedStep.close / __del__) after a device sync -- from a safe point
-    only: never while a capture is running (a sync there invalidates it), never from a finaliser."""
-    if not _GRAVEYARD:
+def release_dropped_graphs(final: bool = False) -> None:
+    """Destroy the parked graph executables (GraphedStep.close / __del__) after a device sync -- at exit
+    (``final``), or at a safe point when QDML_GRAPH_RELEASE=sync: never while a capture is running (a sync there
+    invalidates it), never from a finaliser."""
+    if not _GRAVEYARD or (GRAPH_RELEASE != "sync" and not final):
         return
     if torch.cuda.is_available():
         if torch.cuda.is_current_stream_capturing():
@@ -91,7 +99,7 @@ def release_dropped_graphs() -> None:
         _GRAVEYARD.pop().reset()
 
 
-atexit.register(release_dropped_graphs)
+atexit.register(release_dropped_graphs, True)
 
 
 class GraphedStep:
@@ -144,11 +152,10 @@ class GraphedStep:
         self.graph = g
 
     def close(self) -> None:
-        """Release the graph executable (and its hold on the memory pool) deterministically: the device is
-        synchronised first, so no replay of it can still be running when HIP destroys the executable.  (Round 5:
-        a host segfault in a later hipGraphLaunch, with earlier tests' graphs dropped by whichever garbage
-        collection ran next -- the test suite had to synchronise and collect between tests, tests/conftest.py.)
-        Idempotent; calling the step afterwards raises."""
+        """Retire the step: the graph executable is parked (destroyed at exit, or -- QDML_GRAPH_RELEASE=sync -- right
+        here after a device sync, so no replay of it can still be running when HIP destroys it).  (Rounds 5 and 6: a
+        host segfault in a later hipGraphLaunch of another graph after executables were destroyed, see
+        GRAPH_RELEASE.)  Idempotent; calling the step afterwards raises."""
         g, self.graph = self.graph, None
         self.enabled = False
         self.fn = None   # (breaks the trainer -> graph set -> step -> bound method cycle)
@@ -159,8 +166,8 @@ class GraphedStep:
     def __del__(self) -> None:
         # no HIP call here: the garbage collector can run this in the middle of another graph's capture or replay
         # (round 6: the round-5 hipGraphLaunch segfault recurred in a replay after earlier tests' graphs were
-        # dropped by collection, profiles/r6_11_pytest.log).  The executable is parked and destroyed at the next
-        # safe point (release_dropped_graphs: the next capture, close(), exit).
+        # dropped by collection, profiles/r6_11a_pytest_segfault.log).  The executable is parked and destroyed at exit
+        # (release_dropped_graphs; QDML_GRAPH_RELEASE).
         try:
             if self.graph is not None:
                 _GRAVEYARD.append(self.graph)

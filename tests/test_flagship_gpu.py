@@ -312,9 +312,9 @@ def test_slab_fed_adam_matches_slab_launch(cuda, monkeypatch, mode):
 def test_dropped_trainer_then_new_capture_and_replay(cuda):
     """Graph lifetime in the product code: a trainer dropped right after run() -- no sync, its
     replays possibly still on the device -- parks its graph executables (GraphedStep.__del__ makes no HIP call:
-    a collection can run inside another graph's capture or replay) and the next capture destroys them after a
-    device sync, so another trainer can capture and replay at once.  Also the explicit close() bench.py's plan
-    selection uses.  (tests/conftest.py no longer synchronises / collects between tests.)"""
+    a collection can run inside another graph's capture or replay; they are destroyed at exit), so another
+    trainer can capture and replay at once.  Also the explicit close() bench.py's plan selection uses.
+    (tests/conftest.py no longer synchronises / collects between tests.)"""
     import gc
     ctx = DistContext(device=cuda)
     cfg = FlagshipConfig(batch=32, data_len=400, steps_per_graph=3)
