@@ -35,6 +35,10 @@
 // 21, with psi un-applied and re-stored in every backward pass).
 #include "common.h"
 
+#ifndef QD_STREAM_SWEEP
+#define QD_STREAM_SWEEP 0   // (1: pass A's adjoint sweeps psi and lambda together, as before round 6 -- A/B builds)
+#endif
+
 namespace qd {
 namespace qstream {
 
@@ -275,6 +279,81 @@ __device__ __forceinline__ void lds_gates_adj_acc(cf* tp, cf* tq, const float4* 
     }
     __syncthreads();
   });
+}
+
+// The same d(theta) partials and lambda result without sweeping psi (round 6).  Every d(theta_b) is a pair sum
+// <lambda| G_b |psi> with G_b acting on qubit b alone, and G_b commutes with every RY of the layer (the other
+// qubits' and its own: same axis), so undoing gates on BOTH states never changes it: all of them come from the
+// brick as loaded (the pass's RZ phases undone), in a read-only pass over 4-bit groups; then RY^dagger is undone on
+// lambda only (psi is never written back: nothing reads it after this pass), three bits at a time.  UNDO = false
+// (layer 0: its lambda is not stored) skips the second half.  Same wacc slots as lds_gates_adj_acc.
+template <int TOT, int NBITS, int NTH, bool UNDO>
+__device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float4* trig, float* wacc) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int NG4 = (NBITS + 3) / 4;
+  static_for<0, NG4>([&](auto gc) {
+    constexpr int r0 = 4 * decltype(gc)::value;
+    constexpr int NB = (NBITS - r0) < 4 ? (NBITS - r0) : 4;
+    constexpr int ACT = (1 << TOT) >> NB;
+    float dth[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) dth[b] = 0.f;
+#pragma unroll 1
+    for (int t = threadIdx.x; t < ACT; t += NTH) {
+      const int base = ins_bits<r0, NB>(t);
+      cf p[1 << NB], m[1 << NB];
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) {
+        p[j] = tp[padx(base | (j << r0))];
+        m[j] = tq[padx(base | (j << r0))];
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j)
+          if (!((j >> b) & 1)) {
+            const cf p0 = p[j], p1 = p[j | (1 << b)], l0 = m[j], l1 = m[j | (1 << b)];
+            dth[b] += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+          }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float s1 = wave_sum(dth[b]);
+      if (lane == 0) wacc[wv * 2 * NBITS + 2 * (r0 + b)] += s1;
+    }
+  });
+  if constexpr (UNDO) {
+    __syncthreads();   // (every wave done reading lambda)
+    constexpr int NGRP = (NBITS + 2) / 3;
+    static_for<0, NGRP>([&](auto gc) {
+      constexpr int r0 = 3 * decltype(gc)::value;
+      constexpr int NB = (NBITS - r0) < 3 ? (NBITS - r0) : 3;
+      constexpr int ACT = (1 << TOT) >> NB;
+#pragma unroll 1
+      for (int t = threadIdx.x; t < ACT; t += NTH) {
+        const int base = ins_bits<r0, NB>(t);
+        cf m[1 << NB];
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j) m[j] = tq[padx(base | (j << r0))];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const float4 tg = trig[brick_q(r0 + b)];
+#pragma unroll
+          for (int j = 0; j < (1 << NB); ++j)
+            if (!((j >> b) & 1)) {
+              const cf m0 = m[j], m1 = m[j | (1 << b)];
+              m[j] = {tg.x * m0.x + tg.y * m1.x, tg.x * m0.y + tg.y * m1.y};
+              m[j | (1 << b)] = {tg.x * m1.x - tg.y * m0.x, tg.x * m1.y - tg.y * m0.y};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j) tq[padx(base | (j << r0))] = m[j];
+      }
+      __syncthreads();
+    });
+  } else {
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------------------------------ forward
@@ -601,7 +680,8 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
         if (lane == 0) red[wv * 2 * C::AB + 2 * b + 1] = sz;
       }
     }
-    lds_gates_adj_acc<C::AB, C::AB, NTA>(tp, tq, trig, red);
+    if constexpr (QD_STREAM_SWEEP) lds_gates_adj_acc<C::AB, C::AB, NTA>(tp, tq, trig, red);   // (the round-5 sweep)
+    else lds_dtheta_then_undo<C::AB, C::AB, NTA, STORE>(tp, tq, trig, red);
     if constexpr (STORE) {
       for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
         const cf u = tq[padx(e)], v = tq[padx(e) + 1];
