@@ -285,6 +285,57 @@ __device__ __forceinline__ void conv1_mfma(float* act, int lane, const float (&w
   }
 }
 
+// conv1_mfma for P256 (W = 16): one 16x16 tile per image row (row = the row's 16 columns), so the two rows of a
+// window are the same lane's accumulators in the tiles of rows 2 qy and 2 qy + 1: lane (c, g) holds columns
+// 4 g .. 4 g + 3 of both, i.e. windows (qy, 2 g) and (qy, 2 g + 1) of channel c -- no exchange across lanes.
+// The two rows' tiles are computed together, the row pairs in turn (accumulators of one pair live).
+template <int H, int W>
+__device__ __forceinline__ void conv1_mfma16(float* act, int lane, const float (&w1f)[5], float b1c,
+                                             float* __restrict__ p1g, uint32_t* __restrict__ c1g) {
+  using G = Geo<H, W>;
+  static_assert(W == 16 && H % 2 == 0, "one 16-wide row per tile");
+  const int g = lane >> 4, c = lane & 15;
+  int aoff[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int k = 4 * i + g, ci = k / 9, t = k % 9;
+    aoff[i] = k < K1 ? G::o_x + ci * G::XP + (t / 3) * G::XW + c + t % 3 : -1;   // (row 0; + y XW per row)
+  }
+#pragma unroll 2
+  for (int qy = 0; qy < H / 2; ++qy) {
+    float av[2][5];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 5; ++i) av[h][i] = aoff[i] >= 0 ? act[aoff[i] + (2 * qy + h) * G::XW] : 0.f;
+    f32x4 acc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      acc[h] = (f32x4){b1c, b1c, b1c, b1c};
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[h][i], w1f[i], acc[h], 0, 0, 0);
+    }
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const float t0 = relu(acc[0][2 * w]), t1 = relu(acc[0][2 * w + 1]);
+      const float u0 = relu(acc[1][2 * w]), u1 = relu(acc[1][2 * w + 1]);
+      const float v = max_nan(t0, t1), pv = max_nan(u0, u1);   // top / bottom row of the window
+      const uint32_t rtop = (uint32_t)(t1 > t0), rbot = (uint32_t)(u1 > u0);   // ties go to the left column
+      const float m = max_nan(v, pv);
+      const bool bottom = pv > v;                                             // ties go to the top row
+      const unsigned long long b1 = __ballot(bottom);
+      const unsigned long long b0 = __ballot(bottom ? rbot != 0u : rtop != 0u);
+      const int qx = 2 * g + w, win = qy * G::W2 + qx;
+      act[G::o_p1 + ((qy + 1) * G::PW + qx + 1) * G::PC + c] = m;
+      p1g[win * C1 + c] = m;
+      if (c == 0) {
+        const uint32_t sh = 16u * (uint32_t)g;
+        c1g[win] = spread_even16((uint32_t)(b0 >> sh) & 0xFFFFu) | (spread_even16((uint32_t)(b1 >> sh) & 0xFFFFu) << 1);
+      }
+    }
+  }
+}
+
 // Forward of one sample into the wave's LDS image: x -> p1 (padded) -> z2 (pre-activation).
 // wreg (optional): this lane's 72 conv2 weights W2[co = lane&31][ci = 8*(lane>>5) + j][t] at
 // [t*8 + j], register-resident across samples (forward kernel); null = read them from LDS.
@@ -318,6 +369,8 @@ __device__ __forceinline__ void sample_forward(const float* __restrict__ xs, con
   if constexpr (STAMP) ts[2] = stamp();
   if constexpr (X3 && W == 8) {
     conv1_mfma<H, W>(act, lane, *reinterpret_cast<const float(*)[5]>(w1f), b1c, p1g, c1g);
+  } else if constexpr (W == 16 && WREG) {
+    conv1_mfma16<H, W>(act, lane, *reinterpret_cast<const float(*)[5]>(w1f), b1c, p1g, c1g);
   } else {
   // conv1 + ReLU + pool: lane = (window, row of the window); the two rows meet with one shuffle
   static_assert((2 * G::HW2) % 64 == 0, "whole waves per conv1 pass");
@@ -487,8 +540,9 @@ __global__ void __launch_bounds__(64 * NWV) qsc2_fwd_kernel(const float* __restr
     }
   }
   const float bias2 = flat[o.b2 + (lane & 31)];
-  // conv1 on MFMAs (X3, W = 8: conv1_mfma): this lane's B operands W1[c][4 i + g] and b1[c], c = lane & 15
-  constexpr bool C1M = X3 && W == 8;
+  // conv1 on MFMAs (X3 at W = 8: conv1_mfma; W = 16: conv1_mfma16): this lane's B operands W1[c][4 i + g] and
+  // b1[c], c = lane & 15
+  constexpr bool C1M = (X3 && W == 8) || W == 16;
   [[maybe_unused]] float w1f[5], b1c = 0.f;
   if constexpr (C1M) {
 #pragma unroll

@@ -58,6 +58,10 @@ class Knobs:
     conv_stack: bool = False
     # the QSC preprocess forward's workgroup cap (ops/qsc.py; one sample per wave beyond it, a grid-stride loop)
     qsc_fwd_cap: int = 256
+    # P256: the QSC preprocess forward's conv2 on bf16x3 MFMAs too (qd_qsc2_fwd3).  Round 6's conv1 on MFMAs took
+    # the P256 forward kernels to 186 / 193 VGPRs (2 waves per SIMD; before: 248 + 16, 1 wave), which the bf16x3
+    # form was turned down for
+    qsc_fwd3_p256: bool = False
     # conv stack launch shapes (ops/conv.py ConvStackHIP): samples per wave of the forward / dgrad kernels (4 waves per
     # workgroup), samples per workgroup of the fused layer-3/2 backward and of layer 1's weight gradient.
     # spw 3 (round 5): 198 workgroups, one per CU -- spw 2's 288 put two on 32 CUs, whose workgroups then set each

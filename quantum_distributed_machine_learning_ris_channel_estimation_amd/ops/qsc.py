@@ -150,7 +150,8 @@ class QSCStepHIP:
         # MFMA they replace runs at 1/16 of the bf16 rate.
         self._fwd3 = nat.fn(L, "qd_qsc2_fwd3", [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _p, _p])
         self._bwd3 = nat.fn(L, "qd_qsc2_bwd3", [_p] * 12 + [_i] * 7 + [_p, _p])
-        self.fwd_x3 = (self.Hh, self.Ww) == (16, 8)   # (P256 at 256 VGPRs halves its occupancy)
+        # (P256: KNOBS.qsc_fwd3_p256 -- the bf16x3 forward at 256 VGPRs halved its occupancy before round 6)
+        self.fwd_x3 = (self.Hh, self.Ww) == (16, 8) or ((self.Hh, self.Ww) == (16, 16) and KNOBS.qsc_fwd3_p256)
         self.bwd_x3 = (self.Hh, self.Ww) == (16, 8)
         # the backward's bf16 hi / lo transposed conv2 weights, written by the bf16x3 forward each step
         self.w2t_img = torch.empty(2 * 9 * 16 * 48, device=self.p2.device, dtype=torch.bfloat16) \

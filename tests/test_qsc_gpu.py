@@ -191,3 +191,38 @@ def test_qsc_fwd_conv1_on_mfma_matches_f32_forward(cuda):
     assert diff < 1e-4, diff
     assert err < 1e-5, err
     assert float((a3 - af).abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("pilot", [128, 256])
+def test_qsc_pool1_map_and_choices_match_torch(cuda, pilot):
+    """Round 6: the QSC forward's conv1 + ReLU + pool 1 on f32 MFMAs (P128: conv1_mfma, P256: conv1_mfma16) against
+    torch's conv2d / relu / max_pool2d on the same input: the saved pool-1 map (the backward's ReLU mask) to fp32
+    grade and the saved window choices (2-bit codes, first max in scan order) equal to max_pool2d's indices but for
+    near-ties."""
+    import torch.nn.functional as F
+    torch.manual_seed(3)
+    B = 288
+    H, W = (16, 8) if pilot == 128 else (16, 16)
+    m = QSC_P128(n_qubits=8, use_quantumnat=False, use_gradient_pruning=False, pilot_num=pilot).to(cuda)
+    space = FlatParamSpace(list(m.named_parameters()), cuda)
+    x = torch.randn(B, 2, H, W, device=cuda)
+    y = torch.randint(0, 3, (B,), device=cuda)
+    step = QSCStepHIP(m, space, B)
+    step.forward_part(x, y)
+    torch.cuda.synchronize()
+    conv = m.preprocess[0]
+    with torch.no_grad():
+        z = F.relu(F.conv2d(x, conv.weight, conv.bias, padding=1))
+        pooled, idx = F.max_pool2d(z, 2, return_indices=True)          # (B, 16, H/2, W/2)
+    ref = pooled.permute(0, 2, 3, 1).reshape(B, -1)                     # [window][channel]
+    err = float((step.p1s - ref).abs().max() / ref.abs().max())
+    qy = torch.arange(H // 2, device=cuda).view(1, 1, -1, 1)
+    qx = torch.arange(W // 2, device=cuda).view(1, 1, 1, -1)
+    code_ref = 2 * (idx // W - 2 * qy) + (idx % W - 2 * qx)            # 0 TL, 1 TR, 2 BL, 3 BR
+    code_ref = code_ref.permute(0, 2, 3, 1).reshape(B, -1, 16)          # [sample][window][channel]
+    shifts = torch.arange(0, 32, 2, device=cuda, dtype=torch.int32)
+    code = (step.c1.unsqueeze(-1) >> shifts) & 3
+    diff = float((code != code_ref).float().mean())
+    print(f"P{pilot} pool-1 vs torch: max-rel {err:.2e}, window-choice mismatch {diff:.2e}")
+    assert err < 1e-5, err
+    assert diff < 1e-3, diff
