@@ -264,7 +264,6 @@ __global__ void __launch_bounds__(NT, 2) fwd_kernel(const float* __restrict__ x,
   float* red = sm + 2 * DP;                            // 4 waves x 12
   cf* tab = reinterpret_cast<cf*>(sm + 2 * DP + 64);   // 48 complex
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const size_t fin = (size_t)(L > 1 ? L - 2 : 0) * B * 2 * D;   // psave slot of the final state
   for (int s = blockIdx.x; s < B; s += gridDim.x) {
     const int grp = wgroup > 0 ? s / wgroup : 0;
     const float* wg = w + (size_t)grp * L * 2 * N;
@@ -284,15 +283,6 @@ __global__ void __launch_bounds__(NT, 2) fwd_kernel(const float* __restrict__ x,
       __syncthreads();
       mode_apply<2, true>(pr, pi, a2, wv, lane);
       __syncthreads();
-      if (psave != nullptr && l < L - 1) {   // S_l kept for the adjoint (slot l - 1; the final state: slot L - 2)
-        float* sl = psave + (size_t)(l - 1) * B * 2 * D + (size_t)s * 2 * D;
-#pragma unroll 4
-        for (int i = 0; i < D / NT; ++i) {
-          const int k = tid + NT * i;
-          sl[k] = pr[pad(k)];
-          sl[D + k] = pi[pad(k)];
-        }
-      }
     }
     // <Z_q>: thread tid owns k = tid + 256 i, so bit q < 8 of k is bit q of tid, bit q >= 8 is bit q - 8 of i
     float ptot = 0.f, ph[4] = {0.f, 0.f, 0.f, 0.f};
@@ -305,8 +295,8 @@ __global__ void __launch_bounds__(NT, 2) fwd_kernel(const float* __restrict__ x,
 #pragma unroll
       for (int b = 0; b < 4; ++b) ph[b] += ((i >> b) & 1) ? -p : p;
       if (psave != nullptr) {
-        psave[fin + (size_t)s * 2 * D + k] = re;
-        psave[fin + (size_t)s * 2 * D + D + k] = im;
+        psave[(size_t)s * 2 * D + k] = re;
+        psave[(size_t)s * 2 * D + D + k] = im;
       }
     }
 #pragma unroll
@@ -388,11 +378,10 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
 #pragma unroll
     for (int q = 0; q < N; ++q) g[q] = gE[(size_t)s * N + q];
     // psi = the forward's final state; lambda = (sum_q g_q Z_q) psi
-    const size_t fin = (size_t)(L > 1 ? L - 2 : 0) * B * 2 * D;
 #pragma unroll 4
     for (int i = 0; i < D / NT; ++i) {
       const int k = tid + NT * i;
-      const float a = psave[fin + (size_t)s * 2 * D + k], b = psave[fin + (size_t)s * 2 * D + D + k];
+      const float a = psave[(size_t)s * 2 * D + k], b = psave[(size_t)s * 2 * D + D + k];
       float o = 0.f;
 #pragma unroll
       for (int q = 0; q < N; ++q) o += ((k >> q) & 1) ? -g[q] : g[q];
@@ -403,27 +392,6 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
     }
     __syncthreads();
     for (int l = L - 1; l >= 0; --l) {
-      // psi of a lower layer: the forward's kept S_l (slot l - 1), or S_0 regenerated -- never un-applied (round 6:
-      // half the mode products; the loaded state is also the forward's exact one)
-      if (l < L - 1) {
-        if (l > 0) {
-          const float* sl = psave + (size_t)(l - 1) * B * 2 * D + (size_t)s * 2 * D;
-#pragma unroll 4
-          for (int i = 0; i < D / NT; ++i) {
-            const int k = tid + NT * i;
-            pr[pad(k)] = sl[k];
-            pi[pad(k)] = sl[D + k];
-          }
-          __syncthreads();
-        } else {
-          float xs[N];
-#pragma unroll
-          for (int q = 0; q < N; ++q) xs[q] = x[(size_t)s * N + q];
-          __syncthreads();   // (tab aliases the cross-density scratch)
-          layer0(pr, pi, reinterpret_cast<cf*>(scr), xs, wg, tid);
-          __syncthreads();
-        }
-      }
       // undo the ring: state[k] <- state[f(k)]
       {
         float v[4][D / NT];
@@ -486,14 +454,17 @@ __global__ void __launch_bounds__(NT, 2) bwd_kernel(const float* __restrict__ x,
         if (l == 0) dx[(size_t)s * N + q] = dth;
       }
       if (l > 0) {
-        const h8* lm = img + ((size_t)grp * (L - 1) + (l - 1)) * LAYER_H8;   // (lambda only: psi is reloaded)
+        const h8* lm = img + ((size_t)grp * (L - 1) + (l - 1)) * LAYER_H8;
         const Op a0 = load_op(lm + (0 * 2 + 1) * IMG_H8, lane);
-        const Op a1 = load_op(lm + (1 * 2 + 1) * IMG_H8, lane);
-        const Op a2 = load_op(lm + (2 * 2 + 1) * IMG_H8, lane);
+        mode_apply<0, false>(pr, pi, a0, wv, lane);
         mode_apply<0, false>(lr, li, a0, wv, lane);
         __syncthreads();
+        const Op a1 = load_op(lm + (1 * 2 + 1) * IMG_H8, lane);
+        mode_apply<1, false>(pr, pi, a1, wv, lane);
         mode_apply<1, false>(lr, li, a1, wv, lane);
         __syncthreads();
+        const Op a2 = load_op(lm + (2 * 2 + 1) * IMG_H8, lane);
+        mode_apply<2, false>(pr, pi, a2, wv, lane);
         mode_apply<2, false>(lr, li, a2, wv, lane);
         __syncthreads();
       }
@@ -706,7 +677,7 @@ QD_API long long qd_qsim_mfma12_workspace(int G, int L) {
 }
 
 // The same contract as qd_qsim_big_fwd at n = 12 (ws = the qd_qsim_mfma12_workspace images, rebuilt here from w;
-// psave: qd_qsim_mfma12_save_bytes of kept states for qd_qsim_mfma12_bwd).  grid: one workgroup per sample up to 512.
+// psave (B, 2, 4096) fp32 for qd_qsim_mfma12_bwd).  grid: one workgroup per sample up to 512.
 QD_API int qd_qsim_mfma12_fwd(const float* x, const float* w, float* E, int B, int n, int L, int wgroup, void* ws,
                               void* psave, void* stream) {
   if (wgroup > 0 && B % wgroup != 0) return (int)hipErrorInvalidValue;   // (G = B / wgroup weight groups, workspace)
@@ -735,13 +706,6 @@ QD_API int qd_qsim_mfma12_bwd(const float* x, const float* w, const float* gE, f
   hipLaunchKernelGGL(bwd_kernel, dim3(grid), dim3(NT), BWD_SMEM, (hipStream_t)stream, x, w, (const h8*)ws, gE, dx,
                      slab, B, L, wgroup, (const float*)psave);
   return (int)hipGetLastError();
-}
-
-// bytes of qd_qsim_mfma12_fwd's kept states (psave): max(1, L - 1) states of B x 2 x 4096 fp32 -- S_1 .. S_{L-2}
-// (the state after layer l, slot l - 1) and the final state (slot L - 2; L = 1: slot 0).  The adjoint reloads psi
-// per layer instead of un-applying it (round 6).
-QD_API long long qd_qsim_mfma12_save_bytes(int B, int L) {
-  return (long long)(L > 1 ? L - 1 : 1) * B * 2 * D * (long long)sizeof(float);
 }
 
 // bytes of the 8-qubit adjoint's operand images (2 modes x {forward, adjoint} per (group, layer >= 1))

@@ -134,11 +134,8 @@ class QSCStepHIP:
                 nb = max(ws(self.n, self.qrows, 0), ws(self.n, self.qrows, 1))
             self.qws = torch.empty(nb, dtype=torch.uint8, device=dev) if nb else None
             # every sample's final state, kept by the forward for the adjoint backward (which then
-            # skips re-running the circuit): 2304 x 2^16 x 8 B = 1.2 GB at 16 qubits -- HBM has room.  The 12-qubit
-            # MFMA simulator also keeps every intermediate layer's state (qd_qsim_mfma12_save_bytes: its adjoint
-            # reloads psi per layer instead of un-applying it)
-            nsv = batch_total * (8 << self.n) * (max(1, self.L - 1) if self.mfma12 else 1)   # (= qd_qsim_mfma12_save_bytes)
-            self.psave = torch.empty(nsv, dtype=torch.uint8, device=dev)
+            # skips re-running the circuit): 2304 x 2^16 x 8 B = 1.2 GB at 16 qubits -- HBM has room
+            self.psave = torch.empty(batch_total * (8 << self.n), dtype=torch.uint8, device=dev)
         else:
             self.qrows = nat.fn(L, "qd_qsim_bwd_grid", [_i, _i])(self.n, batch_total)
             self.qws = None
