@@ -1,11 +1,11 @@
 #!/bin/bash
-# round-6 GPU call 11 (rerun as call 17 on the final tree): consolidation of the tree -- full GPU suite + LDS poison + smoke; the headline benches (the
+# round-6 GPU call 17: call 11 on the final tree: consolidation of the tree -- full GPU suite + LDS poison + smoke; the headline benches (the
 # driver's command twice, --steps 300, no arguments, fp8, P256, P256 x 1024, BASELINE config 5 = 16 qubits + noise +
 # gradient pruning + fp8, forced world-1 DP with plan selection, --scaling strong); the default step's kernel stats
 # and timeline
 set -o pipefail
 cd "$(dirname "$0")/../.." || exit 1
-R=$(pwd); O=$R/gpurun_out; P=r6_11
+R=$(pwd); O=$R/gpurun_out; P=r6_17
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "not test_lds_poison" > $O/${P}_pytest.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/${P}_pytest.log
 tail -3 $O/${P}_pytest.log
 [ $rc -eq 0 ] || exit 1
