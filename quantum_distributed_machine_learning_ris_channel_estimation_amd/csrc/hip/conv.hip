@@ -815,6 +815,232 @@ __global__ void __launch_bounds__(256, 1) conv3x3_fwd_db_kernel(const uint16_t* 
   }
 }
 
+// LDS writes of this workgroup visible to all its waves, WITHOUT waiting for outstanding global loads (a
+// __syncthreads() drains vmcnt too, i.e. the next sample's prefetch)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ------------------------------------------------------------------------------------------
+// conv3x3_split_kernel (round 6): the training forward of a layer (1: raw f32 pilots; 2, 3: BN + ReLU of the previous
+// z) with every SAMPLE split over the workgroup's 4 waves.  conv3x3_body gives a wave whole samples -- the whole
+// staging (BN + ReLU + bf16 pack + LDS writes) and all 72 MFMAs of each -- and at the step's 2,304 virtual samples
+// that is about one wave per SIMD, which alternates its staging (vector issue), its MFMAs and its HBM waits with
+// nothing beside it (profiles/r4_28_stamp_conv.txt).  Here the 4 waves stage a sample together (one channel-pair item
+// per lane at P128), meet at ONE barrier, and each runs the MFMAs of its own position tile(s) -- a quarter of the
+// sample -- while the next sample's loads fly; two tiles alternate, so that barrier is the only one per sample.  A
+// workgroup is small (two sample tiles + the B fragments: 42 KB at P128) and short (sps samples), so three share a
+// CU and its SIMDs interleave one workgroup's staging with another's MFMAs and HBM waits.  conv3x3_body's k order,
+// MFMA shape and epilogue: z is bit-identical to it; the BN statistics partials come as ceil(B / sps) rows per group
+// (another grouping of the same sums).
+// ------------------------------------------------------------------------------------------
+template <int CIN, int W, int INM, typename TIN, int SPS, int D>
+__global__ void __launch_bounds__(256, W == 8 ? 3 : 2) conv3x3_split_kernel(const TIN* __restrict__ xin,
+                                                                         const float* __restrict__ st_in,
+                                                                         const uint16_t* __restrict__ wt,
+                                                                         uint16_t* __restrict__ out,
+                                                                         float* __restrict__ stats, int E, int B,
+                                                                         int chunks, BnFwd bnf) {
+  using G = Geo<16, W>;
+  constexpr bool RAWIN = INM == IN_RAW_F32;
+  static_assert(RAWIN ? CIN == 2 : (CIN == 32 && INM == IN_BNRELU), "layer 1 (raw pilots) or a 32-channel layer");
+  static_assert(D >= 1 && D <= SPS, "prefetch depth");
+  constexpr int KS = (9 * CIN + 15) / 16;             // 16-deep k steps
+  constexpr int TILE = G::HP * G::WP * CIN;           // bf16 elements per sample tile
+  constexpr int MTW = G::MT / 4;                      // 32-position tiles per wave
+  // staging items per thread: raw input -- single values; else (channel pair, 8 positions) = two 16-byte vectors
+  constexpr int IPT = RAWIN ? CIN * G::HW / 256 : 2 * G::HW / 256;
+  static_assert(IPT >= 1 && G::MT % 4 == 0 && TILE % 8 == 0, "geometry");
+  static_assert(2 * TILE * 2 >= 4 * 32 * 2 * (int)sizeof(float), "the statistics reduction reuses the tiles");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int hh = lane >> 5, l32 = lane & 31;
+  const int u = blockIdx.x / chunks, chunk = blockIdx.x % chunks, e = blockIdx.y;
+  const int EC_in = E * CIN;
+  __bf16* tiles = reinterpret_cast<__bf16*>(smem);
+  bf16x8* wl = reinterpret_cast<bf16x8*>(tiles + 2 * TILE);    // B fragments
+  float* stl = reinterpret_cast<float*>(wl + KS * 64);          // BN records of the input channels
+  const int n0 = u * B + chunk * SPS, cnt = min((u + 1) * B, n0 + SPS) - n0, nlast = n0 + cnt - 1;
+  const int pr = tid & 15;   // (bf16 input) this thread's channel pair, the same for all its items
+
+  // D samples' loads in flight (a ring of register sets, static indices: the sample loop is unrolled): one sample's
+  // MFMAs are a quarter of conv3x3_body's, far shorter than an HBM round trip, so one sample ahead exposed it
+  [[maybe_unused]] uint4 rv[RAWIN ? 1 : D][RAWIN ? 1 : IPT][2];
+  [[maybe_unused]] float rr[RAWIN ? D : 1][RAWIN ? IPT : 1];
+  auto load = [&](auto slot, int n) {
+    constexpr int S = decltype(slot)::value;
+    const size_t base = ((size_t)n * E + e) * CIN * G::HW;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = tid + 256 * k;
+      if constexpr (RAWIN) {
+        rr[S][k] = xin[base + i];
+      } else {
+        const int sg = i >> 4;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          rv[S][k][h2] = *reinterpret_cast<const uint4*>(xin + base + (size_t)(2 * pr + h2) * G::HW + 8 * sg);
+      }
+    }
+  };
+  f32x2 a2 = {0.f, 0.f}, b2 = {0.f, 0.f};   // (bf16 input) this pair's BN affine, after the prologue
+  auto stage = [&](auto slot, __bf16* tile) {
+    constexpr int S = decltype(slot)::value;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = tid + 256 * k;
+      if constexpr (RAWIN) {
+        const int c = i / G::HW, p = i % G::HW;
+        tile[((p / W + 1) * G::WP + (p % W) + 1) * CIN + c] = (__bf16)rr[S][k];
+      } else {   // conv3x3_body's channel-pair staging: packed FMA, NaN-keeping max, one packed bf16 word per position
+        const int p0 = (i >> 4) * 8, ph = p0 / W, pw = p0 % W;
+        const uint32_t w0[4] = {rv[S][k][0].x, rv[S][k][0].y, rv[S][k][0].z, rv[S][k][0].w};
+        const uint32_t w1[4] = {rv[S][k][1].x, rv[S][k][1].y, rv[S][k][1].z, rv[S][k][1].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t u0 = (j & 1) ? (w0[j >> 1] & 0xffff0000u) : (w0[j >> 1] << 16);
+          const uint32_t u1 = (j & 1) ? (w1[j >> 1] & 0xffff0000u) : (w1[j >> 1] << 16);
+          f32x2 y = f32x2{__uint_as_float(u0), __uint_as_float(u1)} * a2 + b2;
+          y.x = relu_max(y.x);
+          y.y = relu_max(y.y);
+          const int R = ph + 1, C = pw + j + 1;
+          *reinterpret_cast<uint32_t*>(tile + (R * G::WP + C) * CIN + 8 * ((pr >> 2) ^ tile_swz(R, C)) +
+                                       2 * (pr & 3)) = pack_bf16x2(y);
+        }
+      }
+    }
+  };
+
+  if (cnt > 0)   // the first D samples' loads fly during the prologue (past the last sample: re-load it, unused)
+    static_for<0, D>([&](auto I) { load(I, min(n0 + (int)I, nlast)); });
+  for (int i = tid; i < 2 * TILE / 8; i += 256) reinterpret_cast<bf16x8*>(tiles)[i] = bf16x8{};   // zero halos
+  {  // prologue: B fragments -> LDS, the input BN records (built from the producer's partials or read as published)
+    constexpr int WPT = (KS * 64 + 255) / 256;
+    const bf16x8* wp = reinterpret_cast<const bf16x8*>(wt) + (size_t)e * KS * 64;
+    bf16x8 tw[WPT];
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) tw[k] = wp[tid + 256 * k];
+    if constexpr (!RAWIN) {
+      if (bnf.stats) {
+        bn_fwd_build<false>(bnf, stl, u, e, EC_in, chunk == 0);
+      } else if (tid < CIN * NST) {
+        stl[tid] = st_in[((size_t)u * EC_in + e * CIN) * NST + tid];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if ((KS * 64) % 256 == 0 || tid + 256 * k < KS * 64) wl[tid + 256 * k] = tw[k];
+  }
+  __syncthreads();
+  if constexpr (!RAWIN) {
+    a2 = f32x2{stl[(2 * pr) * NST + ST_A], stl[(2 * pr + 1) * NST + ST_A]};
+    b2 = f32x2{stl[(2 * pr) * NST + ST_B], stl[(2 * pr + 1) * NST + ST_B]};
+  }
+  f32x2 s1v = {0.f, 0.f}, s2v = {0.f, 0.f};
+  static_for<0, SPS>([&](auto I) {
+    constexpr int i = I;
+    if (i < cnt) {   // (uniform over the workgroup)
+      const int n = n0 + i;
+      __bf16* tile = tiles + (i & 1) * TILE;
+      stage(std::integral_constant<int, i % D>{}, tile);
+      if constexpr (i + D < SPS) load(std::integral_constant<int, i % D>{}, min(n + D, nlast));   // refill the slot
+      lds_barrier();
+      auto load_a = [&](int mt, int s) -> bf16x8 {
+        const int p = mt * 32 + l32, ph = p / W, pw = p % W;
+        bf16x8 a;
+        if constexpr (CIN % 16 == 0) {
+          const int tap = (16 * s) / CIN, q = ((16 * s) % CIN) / 8 + hh;
+          const int R = ph + tap / 3, C = pw + tap % 3;
+          a = *reinterpret_cast<const bf16x8*>(tile + (R * G::WP + C) * CIN + 8 * (q ^ tile_swz(R, C)));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int k = 16 * s + 8 * hh + j;
+            if (k < 9 * CIN) {
+              const int tap = k / CIN, c = k % CIN;
+              a[j] = tile[((ph + tap / 3) * G::WP + pw + tap % 3) * CIN + c];
+            } else {
+              a[j] = (__bf16)0.f;
+            }
+          }
+        }
+        return a;
+      };
+      f32x16 acc[MTW];
+      bf16x8 a_cur[MTW], b_cur = wl[lane];
+#pragma unroll
+      for (int j = 0; j < MTW; ++j) {
+        acc[j] = f32x16{};
+        a_cur[j] = load_a(wv + 4 * j, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        bf16x8 a_nxt[MTW], b_nxt;
+        if (s + 1 < KS) {
+          b_nxt = wl[(s + 1) * 64 + lane];
+#pragma unroll
+          for (int j = 0; j < MTW; ++j) a_nxt[j] = load_a(wv + 4 * j, s + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < MTW; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_cur[j], b_cur, acc[j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < KS) {
+          b_cur = b_nxt;
+#pragma unroll
+          for (int j = 0; j < MTW; ++j) a_cur[j] = a_nxt[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MTW; ++j) {   // epilogue (conv3x3_body's OUT_Z_STATS)
+        const int mt = wv + 4 * j;
+        const size_t rbase = ((size_t)n * E + e) * CO * G::HW + (size_t)l32 * G::HW + mt * 32;
+        uint32_t pk[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          pk[q][0] = pack_bf16x2(f32x2{acc[j][4 * q], acc[j][4 * q + 1]});
+          pk[q][1] = pack_bf16x2(f32x2{acc[j][4 * q + 2], acc[j][4 * q + 3]});
+          const f32x2 v01 = unpack_bf16x2(pk[q][0]), v23 = unpack_bf16x2(pk[q][1]);
+          s1v += v01 + v23;
+          s2v += v01 * v01 + v23 * v23;
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+          for (int w = 0; w < 2; ++w) {
+            const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * q][w], pk[2 * q + 1][w], false, false);
+            pk[2 * q][w] = r[0];
+            pk[2 * q + 1][w] = r[1];
+          }
+          *reinterpret_cast<uint4*>(out + rbase + 8 * (2 * q + hh)) =
+              make_uint4(pk[2 * q][0], pk[2 * q][1], pk[2 * q + 1][0], pk[2 * q + 1][1]);
+        }
+      }
+    }
+  });
+  float s1 = s1v.x + s1v.y, s2 = s2v.x + s2v.y;
+  s1 += __shfl_xor(s1, 32);
+  s2 += __shfl_xor(s2, 32);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  if (hh == 0) {
+    red[(wv * 32 + l32) * 2] = s1;
+    red[(wv * 32 + l32) * 2 + 1] = s2;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = tid >> 1, k = tid & 1;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[(w * 32 + c) * 2 + k];
+    stats[(((size_t)u * chunks + chunk) * 2 + k) * E * CO + e * CO + c] = t;   // planar [2][EC] rows
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // conv_fwd_stack_kernel: the training forward of all three conv/BN/ReLU layers -- and the BN tail (layer 3's
 // records, h3 = relu(bn3(z3)) for the FC GEMM, the running statistics) -- as ONE persistent launch.
@@ -2623,6 +2849,37 @@ QD_API int qd_conv_fwd_db(const uint16_t* xin, const float* st_prev, const uint1
   if (hipError_t e = qd::allow_lds(conv3x3_fwd_db_kernel<8>, smem)) return (int)e;
   hipLaunchKernelGGL(conv3x3_fwd_db_kernel<8>, dim3((N / B) * chunks, E), dim3(256), smem, (hipStream_t)stream, xin,
                      st_prev, w, z, stats, E, B, chunks, spw, bf);
+  return (int)hipGetLastError();
+}
+
+// qd_conv_fwd on the sample-split kernel (conv3x3_split_kernel): `sps` samples per workgroup, `chunks` = workgroups
+// per group (chunks * sps >= B) = the statistics partial rows per group.  Same z as qd_conv_fwd.
+static size_t split_smem(int cin, int H, int W) {
+  // 2 sample tiles | B fragments | BN records
+  return 2 * (size_t)(H + 2) * (W + 2) * cin * 2 + (size_t)((9 * cin + 15) / 16) * 64 * 16 + (size_t)cin * NST * 4;
+}
+QD_API int qd_conv_fwd_split(int layer, const void* xin, const float* st_prev, const uint16_t* w, uint16_t* z,
+                             float* stats, int N, int E, int B, int H, int W, int chunks, int sps, const BnFwd* bnf,
+                             void* stream) {
+  if (B <= 0 || N % B || sps < 4 || sps > 6 || chunks <= 0 || (long)chunks * sps < B ||
+      (layer != 1 && !bnf && !st_prev))
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const BnFwd bf = bnf ? *bnf : BnFwd{};
+  dim3 grid((N / B) * chunks, E);
+  // P128: every sample's loads in flight from the start (D = SPS); P256 (twice the registers per sample): 2 ahead
+#define QD_SPLIT(SPS_)                                                                                                \
+  if (layer == 1) {                                                                                                   \
+    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_split_kernel<2, WW, IN_RAW_F32, float, SPS_, WW == 8 ? SPS_ : 2>), grid, \
+                                    dim3(256), split_smem(2, H, W), s, (const float*)xin, nullptr, w, z, stats, E, B, \
+                                    chunks, bf))                                                                      \
+  } else {                                                                                                            \
+    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_split_kernel<32, WW, IN_BNRELU, uint16_t, SPS_, WW == 8 ? SPS_ : 2>),    \
+                                    grid, dim3(256), split_smem(32, H, W), s, (const uint16_t*)xin, st_prev, w, z,    \
+                                    stats, E, B, chunks, bf))                                                         \
+  }
+  if (sps == 4) { QD_SPLIT(4) } else if (sps == 5) { QD_SPLIT(5) } else { QD_SPLIT(6) }
+#undef QD_SPLIT
   return (int)hipGetLastError();
 }
 

@@ -75,6 +75,12 @@ class Knobs:
     # in the current one's MFMA shadow), conv_spb_db samples per workgroup -- 10: 234 workgroups, one per CU
     conv_bwd_db: bool = False
     conv_spb_db: int = 10
+    # (round 6) the training / eval forward of all three layers on conv3x3_split_kernel: each sample split over a
+    # workgroup's 4 waves (one position tile each), conv_sps (4..6) samples per workgroup, several workgroups per CU.
+    # Off: level alone at P128 and 14 % faster at P256, but slower in both steps (P128 0.3834-0.3859 against
+    # 0.3807-0.3827 ms, P256 1.105-1.109 against 1.089-1.092: profiles/r6_18_conv_split_ab.txt, r6_20_*)
+    conv_fwd_split: bool = False
+    conv_sps: int = 5
     conv_spb_f: int = 5
     conv_spb_w1: int = 4
 

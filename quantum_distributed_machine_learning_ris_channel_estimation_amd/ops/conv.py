@@ -112,7 +112,12 @@ class ConvStackHIP:
                 self.f8s.scale[2 + 2 * j] = a
                 self.f8s.qs[2 + 2 * j] = 1.0 / a
         self.st = [torch.zeros(U, EC, NST, device=dev) for _ in range(3)]
-        self.stats = [torch.zeros(U, self.chunks, EC, 2, device=dev) for _ in range(3)]   # per layer
+        # the forward on conv3x3_split_kernel (KNOBS.conv_fwd_split): sps samples per workgroup; its workgroups per group
+        # (chunks_f) are the statistics partial rows every BN consumer sums
+        self.fwd_split = bool(KNOBS.conv_fwd_split) and not self.f8conv
+        self.sps = max(1, int(KNOBS.conv_sps))
+        self.chunks_f = (B + self.sps - 1) // self.sps if self.fwd_split else self.chunks
+        self.stats = [torch.zeros(U, self.chunks_f, EC, 2, device=dev) for _ in range(3)]   # per layer
         # BN backward partials per layer, planar rows [sum g | sum g*xhat] x EC (their column sums are
         # dbeta / dgamma: jobs of the step's batched slab reduction)
         # (layers 1, 2: produced by the next layer's fused backward / dgrad kernel, chunked like it;
@@ -137,6 +142,7 @@ class ConvStackHIP:
         self._fwd = nat.fn(L, "qd_conv_fwd", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
         # layers 2 / 3 at P128: the software-pipelined forward (two LDS tiles per wave; bit-identical outputs)
         self._fwd_db = nat.fn(L, "qd_conv_fwd_db", [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
+        self._fwd_split = nat.fn(L, "qd_conv_fwd_split", [_i, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
         self.fwd_db = bool(KNOBS.conv_fwd_db) and self.W == 8 and self.H == 16
         self._dgrad = nat.fn(L, "qd_conv_dgrad", [_p, _i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p])
         self._wgrad = nat.fn(L, "qd_conv_wgrad", [_i, _p, _p, _p, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p])
@@ -168,6 +174,7 @@ class ConvStackHIP:
         # barriers between layers) when its grid fits the chip at once; the bf16 FC operand only (the fp8
         # estimator's e4m3 copy and amax come from the per-layer path's BN tail)
         self.stack = bool(KNOBS.conv_stack and dev.type == "cuda" and not self.fp8 and not self.f8conv
+                          and not self.fwd_split
                           and nat.fn(L, "qd_conv_fwd_stack_fits", [_i] * 6)(self.N, self.E, self.B, self.H, self.W,
                                                                            self.chunks))
         if self.stack:
@@ -241,9 +248,14 @@ class ConvStackHIP:
             if k > 0:
                 j = k - 1
                 bnf = BnFwd(nat.ptr(self.stats[j]), nat.ptr(m.bn_w[j]), nat.ptr(m.bn_b[j]), nat.ptr(m.run_mean[j]),
-                            nat.ptr(m.run_var[j]), nat.ptr(self.st[j]), self.chunks, float(self.B * self.HW),
+                            nat.ptr(m.run_var[j]), nat.ptr(self.st[j]), self.chunks_f, float(self.B * self.HW),
                             m.momentum, m.eps, int(training))
-            if self.f8conv and k > 0:
+            if self.fwd_split:
+                nat.check(self._fwd_split(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
+                                          nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks_f,
+                                          self.sps, ctypes.byref(bnf) if bnf is not None else None, st),
+                          f"conv_fwd_split{k + 1}")
+            elif self.f8conv and k > 0:
                 j = 2 + 2 * (k - 1)
                 nat.check(self._fwd8(nat.ptr(inp), nat.ptr(m.conv_w[k]), nat.ptr(self.z[k]), nat.ptr(self.stats[k]),
                                      self.N, self.E, self.B, self.H, self.W, self.chunks, self.spw, ctypes.byref(bnf),
@@ -268,17 +280,17 @@ class ConvStackHIP:
         f8 = self.m.fp8_scales if self.fp8 else None
         if self.apply_tail:
             bnf3 = BnFwd(nat.ptr(self.stats[2]), nat.ptr(m.bn_w[2]), nat.ptr(m.bn_b[2]), nat.ptr(m.run_mean[2]),
-                         nat.ptr(m.run_var[2]), nat.ptr(self.st[2]), self.chunks, float(self.B * self.HW),
+                         nat.ptr(m.run_var[2]), nat.ptr(self.st[2]), self.chunks_f, float(self.B * self.HW),
                          m.momentum, m.eps, int(training))
             nat.check(self._apply_tail(nat.ptr(self.z[2]), nat.ptr(self.h3), ctypes.byref(bnf3), arr(self.stats),
                                        arr(m.bn_w), arr(m.bn_b), arr(m.run_mean), arr(m.run_var), arr(self.st),
-                                       self.U, self.E, self.B, self.HW, self.spb_a, self.chunks, int(training),
+                                       self.U, self.E, self.B, self.HW, self.spb_a, self.chunks_f, int(training),
                                        _ptr(nbt), nbt.numel() if nbt is not None else 0, self.U, _ptr(self.h3_8),
                                        nat.ptr(f8.qs) if f8 else None, nat.ptr(f8.amax[0]) if f8 else None, st),
                       "bn_apply_tail")
             return self.h3
         nat.check(self._fin(3, arr(self.stats), arr(m.bn_w), arr(m.bn_b), arr(m.run_mean), arr(m.run_var), arr(self.st),
-                            self.U, self.chunks, self.EC, float(self.B * self.HW), m.momentum, m.eps, int(training),
+                            self.U, self.chunks_f, self.EC, float(self.B * self.HW), m.momentum, m.eps, int(training),
                             _ptr(nbt), nbt.numel() if nbt is not None else 0, self.U, st), "bn_tail")
         nat.check(self._apply(nat.ptr(self.z[2]), nat.ptr(self.st[2]), nat.ptr(self.h3), self.N, self.EC, self.B,
                               self.HW, _ptr(self.h3_8), nat.ptr(f8.qs) if f8 else None,

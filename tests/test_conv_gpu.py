@@ -431,3 +431,40 @@ def test_conv_backward_pipelined_matches_conv3x3_bwd_kernel(cuda, monkeypatch, B
     for i, (x, y) in enumerate(zip(*outs)):
         for j, (p, q) in enumerate(zip(x, y)):
             assert torch.equal(p, q), (i, j, float((p.float() - q.float()).abs().max()))
+
+
+@pytest.mark.parametrize("pilot_num,B,sps", [(128, 256, 5), (128, 40, 4), (256, 64, 6), (128, 7, 4)])
+def test_conv_forward_split_matches_conv3x3_kernel(cuda, monkeypatch, pilot_num, B, sps):
+    """Round 6: the forward on conv3x3_split_kernel (each sample split over a workgroup's 4 waves, sps samples per
+    workgroup) against conv3x3_kernel: layer 1's z bit for bit (same MFMAs, no BN input); the later layers, h3, the
+    BN records and running statistics to a bf16 flip here and there (the statistics partials are grouped by the
+    split kernel's chunking); the backward on top of either forward alike; and the split forward against the fp32
+    model.  B 40 / 7: partial last workgroups."""
+    U = 3
+    outs = []
+    for split in (False, True):
+        monkeypatch.setattr(KNOBS, "conv_fwd_split", split)
+        monkeypatch.setattr(KNOBS, "conv_sps", sps)
+        a, b = pair(cuda, pilot_num)
+        conv = ConvStackHIP(a, U, B)
+        assert conv.fwd_split == split
+        torch.manual_seed(20)
+        Yp = torch.randn(3, U, B, 2, a.H, a.W, device=cuda)
+        h3 = conv.forward(a.pack_input(Yp).contiguous(), training=True)
+        torch.manual_seed(5)
+        dh = torch.randn(U * B * 3, 32 * a.H * a.W, device=cuda).to(torch.bfloat16)
+        a.space.zero_grad()
+        conv.backward(dh)
+        torch.cuda.synchronize()
+        fwd = [h3.clone()] + [conv.z[k].clone() for k in range(3)] + [conv.st[k][..., :4].clone() for k in range(3)]
+        bwd = [conv.dx[0].clone(), conv.dx[1].clone()] + [a.conv_w[k].grad.clone() for k in range(3)]
+        outs.append((fwd, [t.clone() for t in a.run_mean + a.run_var], bwd, b, Yp))
+    (f0, r0, g0, _, _), (f1, r1, g1, b, Yp) = outs
+    assert torch.equal(f0[1], f1[1])
+    for j, (p, q) in enumerate(zip(f0, f1)):
+        assert rel(q, p) < 1e-3, (j, rel(q, p))
+    for p, q in zip(r0, r1):
+        assert torch.allclose(p, q, rtol=1e-4, atol=1e-5), float((p - q).abs().max())
+    for j, (p, q) in enumerate(zip(g0, g1)):
+        assert rel(q, p) < 1e-2, (j, rel(q, p))
+    assert rel(f1[0], b.features(Yp, training=True)) < 2e-2
