@@ -38,6 +38,9 @@
 #ifndef QD_STREAM_SWEEP
 #define QD_STREAM_SWEEP 0   // (1: pass A's adjoint sweeps psi and lambda together, as before round 6 -- A/B builds)
 #endif
+#ifndef QD_STREAM_A4
+#define QD_STREAM_A4 1      // (0: pass A's adjoint in LDS passes only, read-only d(theta) then the lambda undo -- A/B builds)
+#endif
 
 namespace qd {
 namespace qstream {
@@ -236,6 +239,7 @@ __device__ __forceinline__ void lds_gates(cf* tp, cf* tq, const float4* trig, fl
 // bits 0..2 and 3..5 -- whose threads own 8 contiguous / 8-strided amplitudes -- read and write conflict-free
 // (unpadded, a wave's 8-byte accesses 64 bytes apart hit 4 bank pairs: 8-way conflicts)
 __device__ __forceinline__ int padx(int e) { return e + (e >> 3); }
+constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
 
 template <int TOT, int NBITS, int NTH>
 __device__ __forceinline__ void lds_gates_adj_acc(cf* tp, cf* tq, const float4* trig, float* wacc) {
@@ -354,6 +358,63 @@ __device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float
   } else {
     __syncthreads();
   }
+}
+
+// Pass A's adjoint in three steps (round 6, QD_STREAM_A4): the bits a thread holds from its coalesced loads -- bit
+// 0 and bits RLO.. of the brick (float4 pairs 2 NTA apart) -- are handled in registers before the brick reaches LDS
+// (d(theta), then RY^dagger on psi AND lambda: every later d(theta) is the same on both undone, see
+// lds_dtheta_then_undo); the other bits in two LDS groups of up to four, each a single sweep (the first writes both
+// states back, the second stores lambda straight to HBM).  Against lds_dtheta_then_undo: 2 LDS sweeps per brick
+// instead of 7 plus the store loop, 4 barriers instead of 9, and 256 instead of 544 KB of LDS traffic at n = 16; the
+// 16-qubit pass 1.11 against 1.23 ms, config 5's step 6.91-6.97 against 7.17-7.25 ms
+// (profiles/r6_21_q16_pass_a_regs_ab.txt, r6_22_*).  LDS image: one pad amplitude per 32 (padq), so the group on
+// bits 1..4 -- lanes 32 amplitudes apart -- hits distinct banks.
+__device__ __forceinline__ int padq(int e) { return e + (e >> 5); }
+
+// OUT: 0 = both states back to LDS, 1 = lambda back to LDS, 2 = lambda straight to its state in HBM (gdst, brick br:
+// for a fixed register index the lanes hold runs of 32 consecutive amplitudes, 256-byte pieces of the state)
+template <int TOT, int LO, int NB, int NTH, int OUT>
+__device__ __forceinline__ void lds_group_adj(cf* tp, cf* tq, const float4* trig, float* wacc, cf* gdst = nullptr,
+                                              int br = 0) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int ACT = (1 << TOT) >> NB;
+  // the group's amplitudes sit at padq(base) + j STR: base has the group's bits clear, so with the group below bit 5
+  // or from bit 5 up no carry crosses the pad (one address register, the rest immediate offsets)
+  static_assert(LO + NB <= 5 || LO >= 5, "a group either below or from bit 5");
+  constexpr int STR = (1 << LO) + ((1 << LO) >> 5);
+  float dth[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) dth[b] = 0.f;
+#pragma unroll 1
+  for (int t = threadIdx.x; t < ACT; t += NTH) {
+    const int eb = ins_bits<LO, NB>(t), pb = padq(eb);
+    cf p[1 << NB], m[1 << NB];
+#pragma unroll
+    for (int j = 0; j < (1 << NB); ++j) {
+      p[j] = tp[pb + j * STR];
+      m[j] = tq[pb + j * STR];
+    }
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+      const int b = NB - 1 - bb;
+      const float4 tg = trig[brick_q(LO + b)];
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j)
+        if (!((j >> b) & 1)) gate_adj_ry(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dth[b]);
+    }
+#pragma unroll
+    for (int j = 0; j < (1 << NB); ++j) {
+      if constexpr (OUT == 0) tp[pb + j * STR] = p[j];
+      if constexpr (OUT == 2) *reinterpret_cast<float2*>(gdst + brick_k(eb | (j << LO), br)) = make_float2(m[j].x, m[j].y);
+      else tq[pb + j * STR] = m[j];
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const float s1 = wave_sum(dth[b]);
+    if (lane == 0) wacc[wv * 2 * TOT + 2 * (LO + b)] += s1;
+  }
+  __syncthreads();
 }
 
 // ------------------------------------------------------------------------------------------ forward
@@ -651,6 +712,10 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
       tp[padx(e)] = cmul(p, z);
       tq[padx(e)] = cmul(m, z);
     };
+    // (A4) the register group: bit 0 and bits RLO .. AB - 1 of this thread's NPAIR float4 pairs, j = h | (i << 1)
+    constexpr bool A4 = !GEN0 && QD_STREAM_A4 && !QD_STREAM_SWEEP;
+    constexpr int RLO = ilog2c(2 * NTA), NRB = 1 + ilog2c(NPAIR);
+    [[maybe_unused]] float dthr[NRB];
     if constexpr (GEN0) {
       cf* PL = tq + C::AS + C::AS / 8;
       cf* PH = PL + 256;
@@ -660,6 +725,81 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
         const int k = brick_k(e, 0);
         take(e, cmul(PL[k & 255], PH[k >> 8]), ls[k]);
       }
+    } else if constexpr (A4) {   // (the phase tables: written before the brick loop, whose top barrier orders them)
+      cf p[2 * NPAIR], m[2 * NPAIR];
+      // the RZ diagonal at e = 2 t + 2 NTA i + h: with 2 NTA a multiple of 256 its low factor depends on h only and its
+      // high factor on i only -- 2 + NPAIR table reads instead of 2 per amplitude (all of them hoisted by the compiler
+      // spilled at n = 16)
+      constexpr bool ZSEP = (2 * NTA) % 256 == 0;
+      [[maybe_unused]] cf zl[2], zh[NPAIR];
+      if constexpr (ZSEP) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) zl[h] = ZL[(2 * threadIdx.x + h) & 255];
+#pragma unroll
+        for (int i = 0; i < NPAIR; ++i) zh[i] = ZH[(2 * threadIdx.x + 2 * NTA * i) >> 8];
+      }
+      // every d(phi) of the pass: Im<lam| Z_b |psi> summed with the sign of bit b -- which for bits 1 .. RLO - 1 is
+      // this thread's (of 2 t) for all its amplitudes, so one plain sum serves them; bit 0 and bits RLO.. are the
+      // register index's (compile-time signs)
+      float csum = 0.f, cb[NRB];
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) cb[b] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i) {
+        p[2 * i] = cf{na[i].x, na[i].y};
+        m[2 * i] = cf{nb[i].x, nb[i].y};
+        p[2 * i + 1] = cf{na[i].z, na[i].w};
+        m[2 * i + 1] = cf{nb[i].z, nb[i].w};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * i + h;
+          const float c = m[j].x * p[j].y - m[j].y * p[j].x;
+          csum += c;
+#pragma unroll
+          for (int b = 0; b < NRB; ++b) cb[b] += ((j >> b) & 1) ? -c : c;
+        }
+      }
+      asm volatile("" : "+v"(csum));
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) asm volatile("" : "+v"(cb[b]));
+#pragma unroll
+      for (int j = 0; j < 2 * NPAIR; ++j) {   // then the pass's RZ phases undone (take's arithmetic)
+        const int i = j >> 1, h = j & 1;
+        const int eh = 2 * threadIdx.x + 2 * NTA * i + h;
+        const cf z = ZSEP ? cmul(zl[h], zh[i]) : cmul(ZL[eh & 255], ZH[eh >> 8]);
+        p[j] = cmul(p[j], z);
+        m[j] = cmul(m[j], z);
+      }
+#pragma unroll
+      for (int b = 0; b < C::AB; ++b) {
+        if (b == 0) dz[b] = cb[0];
+        else if (b < RLO) dz[b] = ((2 * threadIdx.x) >> b) & 1 ? -csum : csum;
+        else dz[b] = cb[b - RLO + 1];
+      }
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) dthr[b] = 0.f;
+#pragma unroll
+      for (int bb = 0; bb < NRB; ++bb) {
+        const int b = NRB - 1 - bb;
+        const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
+#pragma unroll
+        for (int j = 0; j < 2 * NPAIR; ++j)
+          if (!((j >> b) & 1)) gate_adj_ry(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dthr[b]);
+      }
+      // the sums pinned here: left alone, the compiler sank their adds past the barrier below to the wave reductions,
+      // keeping every product alive across the LDS write (spilled at n = 16)
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) asm volatile("" : "+v"(dthr[b]));
+      // (e = 2 t + 2 NTA i + h: padq(e) = padq(2 t) + h + i (2 NTA + 2 NTA / 32) -- 2 t + 1 crosses no pad)
+      const int pb = padq(2 * threadIdx.x);
+#pragma unroll
+      for (int j = 0; j < 2 * NPAIR; ++j) {
+        const int o = pb + (j & 1) + (j >> 1) * (2 * NTA + (2 * NTA) / 32);
+        tp[o] = p[j];
+        tq[o] = m[j];
+      }
+      // the next brick's loads only now (the registers were this brick's): they fly during the LDS groups
+      if (bi + 1 < BPB) prefetch(br + 1);
     } else {
       __syncthreads();   // (the phase tables)
 #pragma unroll
@@ -679,12 +819,28 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
         const float sz = wave_sum(dz[b]);
         if (lane == 0) red[wv * 2 * C::AB + 2 * b + 1] = sz;
       }
+      if constexpr (A4) {
+#pragma unroll
+        for (int b = 0; b < NRB; ++b) {
+          const float st = wave_sum(dthr[b]);
+          if (lane == 0) red[wv * 2 * C::AB + 2 * (b == 0 ? 0 : RLO + b - 1)] = st;
+        }
+      }
     }
-    if constexpr (QD_STREAM_SWEEP) lds_gates_adj_acc<C::AB, C::AB, NTA>(tp, tq, trig, red);   // (the round-5 sweep)
-    else lds_dtheta_then_undo<C::AB, C::AB, NTA, STORE>(tp, tq, trig, red);
-    if constexpr (STORE) {
+    if constexpr (A4) {   // (the barrier above: every thread's brick image is in LDS; each wave adds to its own slots)
+      constexpr int NB1 = RLO - 1 < 4 ? RLO - 1 : 4;
+      static_assert(RLO > 1 + NB1 && STORE, "two LDS groups; lambda stored by the second");
+      lds_group_adj<C::AB, 1, NB1, NTA, 0>(tp, tq, trig, red);
+      lds_group_adj<C::AB, 1 + NB1, RLO - 1 - NB1, NTA, 2>(tp, tq, trig, red, ls, br);
+    } else if constexpr (QD_STREAM_SWEEP) {
+      lds_gates_adj_acc<C::AB, C::AB, NTA>(tp, tq, trig, red);   // (the round-5 sweep)
+    } else {
+      lds_dtheta_then_undo<C::AB, C::AB, NTA, STORE>(tp, tq, trig, red);
+    }
+    if constexpr (STORE && !A4) {
       for (int e = 2 * threadIdx.x; e < C::AS; e += 2 * NTA) {
-        const cf u = tq[padx(e)], v = tq[padx(e) + 1];
+        const int pe = padx(e);
+        const cf u = tq[pe], v = tq[pe + 1];
         *reinterpret_cast<float4*>(ls + brick_k(e, br)) = make_float4(u.x, u.y, v.x, v.y);
       }
     }
