@@ -41,6 +41,9 @@
 #ifndef QD_STREAM_A4
 #define QD_STREAM_A4 1      // (0: pass A's adjoint in LDS passes only, read-only d(theta) then the lambda undo -- A/B builds)
 #endif
+#ifndef QD_STREAM_B4
+#define QD_STREAM_B4 1      // (0: reverse pass B's adjoint of qubits 8..11 over the LDS tile -- A/B builds)
+#endif
 
 namespace qd {
 namespace qstream {
@@ -536,7 +539,7 @@ __global__ void __launch_bounds__(256) reduce_e(const float* __restrict__ epart,
 // layer 0's pass A reads).  Slab row s*16 + t*(16/NTILE) gets the 8 partials of qubits 8..11 (the other rows
 // of the tile's group get zeros in those columns).
 template <int N, bool FIRST, bool GEN0>
-__global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x, const float* __restrict__ w,
+__global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const float* __restrict__ x, const float* __restrict__ w,
                                                  const float* __restrict__ gE, int L, int l, int wgroup,
                                                  const cf* __restrict__ psi, const cf* __restrict__ lin,
                                                  cf* __restrict__ lout, float* __restrict__ slab) {
@@ -545,8 +548,8 @@ __global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x,
   float4* trig = reinterpret_cast<float4*>(smem);
   float* gq = reinterpret_cast<float*>(smem + 256);       // 16
   float* red = reinterpret_cast<float*>(smem + 320);      // NWV * 8
-  cf* tp = reinterpret_cast<cf*>(smem + 512);             // psi, pre-ring tile order
-  cf* tq = tp + 4096;                                     // lambda, pre-ring tile order
+  cf* tp = reinterpret_cast<cf*>(smem + 512);             // psi, pre-ring tile order (not with QD_STREAM_B4)
+  cf* tq = QD_STREAM_B4 ? tp : tp + 4096;                 // lambda, pre-ring tile order
   float* OL = reinterpret_cast<float*>(tq + 4096);        // (FIRST) observable tables
   float* OH = OL + 256;
   cf* PL = reinterpret_cast<cf*>(OH + 256);               // (GEN0) product tables
@@ -566,6 +569,86 @@ __global__ void __launch_bounds__(NT, 2) pass_b_bwd(const float* __restrict__ x,
     if (i < (1 << (N - 8))) OH[i] = oh;
   }
   if constexpr (GEN0) product_tables<N, NT>(trig, PL, PH, 0);
+  if constexpr (QD_STREAM_B4) {
+    // (round 6) the adjoint of qubits 8..11 in registers: thread c holds psi AND lambda at (h << 8) | c, h = 0..15 --
+    // psi as loaded (or generated), lambda read back from the ring scatter (or formed from psi) -- and stores lambda
+    // from there, 16 runs of 512 bytes per wave.  The LDS tile carried psi, the two-group adjoint sweep over both
+    // states and the store loop before: 1 LDS scatter + 1 gather and 2 barriers now, against 6 sweeps and 4.
+    cf p[16], m[16];
+    if constexpr (!GEN0) {   // psi = S_l: loads in flight across the lambda scatter below
+      const cf* src = psi + (size_t)s * C::D + ((size_t)t << 12);
+#pragma unroll
+      for (int h = 0; h < 16; ++h) p[h] = src[(h << 8) | c];
+    }
+    if constexpr (!FIRST) {   // lambda at the ring images -> pre-ring order in LDS
+      const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
+      const cf* ls = lin + (size_t)s * C::D;
+#pragma unroll 4
+      for (int i = threadIdx.x; i < 4096; i += NT) {
+        const int j = i | ((i & 2048 ? A1 : A0) << 12);
+        tq[ring_inv<N>(j) & 4095] = ls[j];
+      }
+    }
+    __syncthreads();   // (the scatter; FIRST: the observable tables; GEN0: the product tables)
+    if constexpr (GEN0) {
+#pragma unroll
+      for (int h = 0; h < 16; ++h) p[h] = cmul(PL[c], PH[(t << 4) | h]);
+    } else {   // this layer's rotations 8..11 re-applied
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float4 tg = trig[8 + b];
+#pragma unroll
+        for (int h = 0; h < 16; ++h)
+          if (!((h >> b) & 1)) gate_fwd(p[h], p[h | (1 << b)], tg);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      if constexpr (FIRST) {   // lambda = O psi_final, psi_final(ring(k)) = psi(k)
+        const int j = ring_fwd<N>((t << 12) | (h << 8) | c);
+        const float o = OL[j & 255] + OH[j >> 8];
+        m[h] = {p[h].x * o, p[h].y * o};
+      } else {
+        m[h] = tq[(h << 8) | c];
+      }
+    }
+    float dth[4], dph[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) dth[b] = dph[b] = 0.f;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {   // undo rotations 11..8 (lds_gates' adjoint order)
+      const int b = 3 - bb;
+      const float4 tg = trig[8 + b];
+#pragma unroll
+      for (int h = 0; h < 16; ++h)
+        if (!((h >> b) & 1)) gate_adj(p[h], p[h | (1 << b)], m[h], m[h | (1 << b)], tg, dth[b], dph[b]);
+    }
+    // the sums pinned here (sunk past block_sum_vec's barrier they kept every product alive: 249 VGPRs spilled)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) asm volatile("" : "+v"(dth[b]), "+v"(dph[b]));
+    cf* lo = lout + (size_t)s * C::D + ((size_t)t << 12);
+#pragma unroll
+    for (int h = 0; h < (GEN0 ? 1 : 16); ++h)   // (GEN0: only bits 8..11 = 0, the part layer 0's pass A reads)
+      *reinterpret_cast<float2*>(lo + ((h << 8) | c)) = make_float2(m[h].x, m[h].y);
+    float v[8];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      v[2 * b] = dth[b];
+      v[2 * b + 1] = dph[b];
+    }
+    float o[8];
+    block_sum_vec<8>(v, red, o);
+    if (threadIdx.x < 8) {
+      constexpr int PER = ROWS / C::NTILE;
+      const int P = 2 * N * L;
+      const int col = (l * N + 8 + threadIdx.x / 2) * 2 + (threadIdx.x & 1);
+      float* row = slab + ((size_t)s * ROWS + t * PER) * P + col;
+      row[0] = o[threadIdx.x];
+#pragma unroll
+      for (int r = 1; r < PER; ++r) row[(size_t)r * P] = 0.f;
+    }
+    return;
+  }
   if constexpr (!FIRST) {   // lambda at the ring images -> pre-ring order in LDS
     const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
     const cf* ls = lin + (size_t)s * C::D;
@@ -870,7 +953,8 @@ template <int N>
 struct Smem {
   static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + 512);   // (+ the GEN product tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
-  static constexpr size_t B_BWD = 512 + 2 * sizeof(cf) * 4096 + 2048 + sizeof(cf) * 512;   // (+ FIRST / GEN0 tables)
+  // (QD_STREAM_B4: lambda's tile only -- 39 KB, four workgroups per CU)
+  static constexpr size_t B_BWD = 512 + (QD_STREAM_B4 ? 1 : 2) * sizeof(cf) * 4096 + 2048 + sizeof(cf) * 512;   // (+ FIRST / GEN0 tables)
   static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * (SG<N>::AS + SG<N>::AS / 8) + sizeof(cf) * 512   // (+ GEN0 tables)
                                   + sizeof(cf) * (256 + 16);                                           // (+ RZ tables)
 };
