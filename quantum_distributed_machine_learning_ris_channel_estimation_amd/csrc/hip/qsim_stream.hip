@@ -44,6 +44,9 @@
 #ifndef QD_STREAM_B4
 #define QD_STREAM_B4 1      // (0: reverse pass B's adjoint of qubits 8..11 over the LDS tile -- A/B builds)
 #endif
+#ifndef QD_STREAM_A4F
+#define QD_STREAM_A4F 1     // (0: forward pass A in four LDS sweeps of three bits -- A/B builds)
+#endif
 
 namespace qd {
 namespace qstream {
@@ -420,6 +423,35 @@ __device__ __forceinline__ void lds_group_adj(cf* tp, cf* tq, const float4* trig
   __syncthreads();
 }
 
+// The forward counterpart (pass A, QD_STREAM_A4F): RZ RY on bits [LO, LO + NB) of the LDS brick, one sweep; TOG:
+// the result straight to the state in HBM (gdst, brick br) instead of back to LDS.
+template <int TOT, int LO, int NB, int NTH, bool TOG>
+__device__ __forceinline__ void lds_group_fwd(cf* tp, const float4* trig, cf* gdst = nullptr, int br = 0) {
+  constexpr int ACT = (1 << TOT) >> NB;
+  static_assert(LO + NB <= 5 || LO >= 5, "a group either below or from bit 5");
+  constexpr int STR = (1 << LO) + ((1 << LO) >> 5);
+#pragma unroll 1
+  for (int t = threadIdx.x; t < ACT; t += NTH) {
+    const int eb = ins_bits<LO, NB>(t), pb = padq(eb);
+    cf p[1 << NB];
+#pragma unroll
+    for (int j = 0; j < (1 << NB); ++j) p[j] = tp[pb + j * STR];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float4 tg = trig[brick_q(LO + b)];
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j)
+        if (!((j >> b) & 1)) gate_fwd(p[j], p[j | (1 << b)], tg);
+    }
+#pragma unroll
+    for (int j = 0; j < (1 << NB); ++j) {
+      if constexpr (TOG) *reinterpret_cast<float2*>(gdst + brick_k(eb | (j << LO), br)) = make_float2(p[j].x, p[j].y);
+      else tp[pb + j * STR] = p[j];
+    }
+  }
+  if constexpr (!TOG) __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------ forward
 // pass A of layer l (GEN: layer 1, its input generated: the ring image of the layer-0 product state)
 template <int N, bool GEN>
@@ -435,6 +467,52 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
   if constexpr (GEN) load_trig<N>(trig0, x, w, s, L, 0, wgroup);
   __syncthreads();
   cf* st = out + (size_t)s * C::D;
+  if constexpr (QD_STREAM_A4F) {
+    // (round 6) as the reverse pass A: the bits a thread holds from its coalesced loads (bit 0 and bits RLO.., 2 NT
+    // apart) in registers, the rest in two LDS groups, the second storing straight to HBM -- 2 LDS sweeps and the
+    // barriers of 2 instead of 4 sweeps + the store loop
+    constexpr int NPAIR = C::AS / (2 * NT), RLO = ilog2c(2 * NT), NRB = 1 + ilog2c(NPAIR);
+    cf p[2 * NPAIR];
+    if constexpr (GEN) {   // the ring image of the layer-0 product state, generated in registers
+      cf* PL = tp + C::AS + C::AS / 32;   // (past the padded image)
+      cf* PH = PL + 256;
+      product_tables<N, NT>(trig0, PL, PH, 0);
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 2 * NPAIR; ++j) {
+        const int k = ring_inv<N>(brick_k(2 * threadIdx.x + 2 * NT * (j >> 1) + (j & 1), br));
+        p[j] = cmul(PL[k & 255], PH[k >> 8]);
+      }
+    } else {
+      const cf* si = in + (size_t)s * C::D;
+      float4 v[NPAIR];
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i)
+        v[i] = *reinterpret_cast<const float4*>(si + brick_k(2 * threadIdx.x + 2 * NT * i, br));
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i) {
+        p[2 * i] = cf{v[i].x, v[i].y};
+        p[2 * i + 1] = cf{v[i].z, v[i].w};
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) {
+      const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
+#pragma unroll
+      for (int j = 0; j < 2 * NPAIR; ++j)
+        if (!((j >> b) & 1)) gate_fwd(p[j], p[j | (1 << b)], tg);
+    }
+    const int pb = padq(2 * threadIdx.x);
+#pragma unroll
+    for (int j = 0; j < 2 * NPAIR; ++j) tp[pb + (j & 1) + (j >> 1) * (2 * NT + (2 * NT) / 32)] = p[j];
+    __syncthreads();
+    constexpr int NB1 = RLO - 1 < 4 ? RLO - 1 : 4;
+    static_assert(RLO > 1 + NB1, "two LDS groups");
+    constexpr int NB2 = (C::AB < RLO ? C::AB : RLO) - 1 - NB1;   // (n = 13: the brick ends at bit 8)
+    lds_group_fwd<C::AB, 1, NB1, NT, false>(tp, trig);
+    lds_group_fwd<C::AB, 1 + NB1, NB2, NT, true>(tp, trig, st, br);
+    return;
+  }
   if constexpr (GEN) {
     // the ring image of the layer-0 product state: amplitude at k = product at ring^-1(k)
     cf* PL = tp + C::AS;
@@ -583,10 +661,18 @@ __global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const flo
     if constexpr (!FIRST) {   // lambda at the ring images -> pre-ring order in LDS
       const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
       const cf* ls = lin + (size_t)s * C::D;
-#pragma unroll 4
-      for (int i = threadIdx.x; i < 4096; i += NT) {
-        const int j = i | ((i & 2048 ? A1 : A0) << 12);
-        tq[ring_inv<N>(j) & 4095] = ls[j];
+      // all 16 loads in flight before the scatter (4 at a time, layer 0's pass -- no psi loads beside them -- ran
+      // at 2.8 TB/s)
+      cf lv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = threadIdx.x + NT * u;
+        lv[u] = ls[i | ((i & 2048 ? A1 : A0) << 12)];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = threadIdx.x + NT * u;
+        tq[ring_inv<N>(i | ((i & 2048 ? A1 : A0) << 12)) & 4095] = lv[u];
       }
     }
     __syncthreads();   // (the scatter; FIRST: the observable tables; GEN0: the product tables)
@@ -951,7 +1037,7 @@ __global__ void __launch_bounds__(256) reduce_dx(const float* __restrict__ slab,
 // ------------------------------------------------------------------------------------------ host
 template <int N>
 struct Smem {
-  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + 512);   // (+ the GEN product tables)
+  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 32 + 512);   // (padq image + the GEN tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
   // (QD_STREAM_B4: lambda's tile only -- 39 KB, four workgroups per CU)
   static constexpr size_t B_BWD = 512 + (QD_STREAM_B4 ? 1 : 2) * sizeof(cf) * 4096 + 2048 + sizeof(cf) * 512;   // (+ FIRST / GEN0 tables)
