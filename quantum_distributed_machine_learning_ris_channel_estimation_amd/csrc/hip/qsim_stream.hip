@@ -39,7 +39,7 @@
 #define QD_STREAM_SWEEP 0   // (1: pass A's adjoint sweeps psi and lambda together, as before round 6 -- A/B builds)
 #endif
 #ifndef QD_STREAM_A4
-#define QD_STREAM_A4 1      // (0: pass A's adjoint in LDS passes only, read-only d(theta) then the lambda undo -- A/B builds)
+#define QD_STREAM_A4 3      // (2: the register group undoes psi too; 1: the LDS groups too; 0: LDS passes only, read-only d(theta) then the lambda undo -- A/B builds)
 #endif
 #ifndef QD_STREAM_B4
 #define QD_STREAM_B4 1      // (0: reverse pass B's adjoint of qubits 8..11 over the LDS tile -- A/B builds)
@@ -366,7 +366,12 @@ __device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float
   }
 }
 
-// Pass A's adjoint in three steps (round 6, QD_STREAM_A4): the bits a thread holds from its coalesced loads -- bit
+// Pass A's adjoint without sweeping the brick bit by bit (round 6).  QD_STREAM_A4 = 3 (the default): psi is never
+// undone -- every d(theta) is taken from the loaded pair (the register bits in registers at load, the second LDS
+// group's in a read-only sweep, the first group's before it undoes lambda), lambda is undone group by group and on
+// the register bits last, then stored with 16-byte writes; 12 vector operations per pair and bit (lds_group_lam).
+// QD_STREAM_A4 = 2: the register group undoes psi and lambda, the LDS groups lambda only.  QD_STREAM_A4 = 1 (below):
+// the bits a thread holds from its coalesced loads -- bit
 // 0 and bits RLO.. of the brick (float4 pairs 2 NTA apart) -- are handled in registers before the brick reaches LDS
 // (d(theta), then RY^dagger on psi AND lambda: every later d(theta) is the same on both undone, see
 // lds_dtheta_then_undo); the other bits in two LDS groups of up to four, each a single sweep (the first writes both
@@ -419,6 +424,70 @@ __device__ __forceinline__ void lds_group_adj(cf* tp, cf* tq, const float4* trig
   for (int b = 0; b < NB; ++b) {
     const float s1 = wave_sum(dth[b]);
     if (lane == 0) wacc[wv * 2 * TOT + 2 * (LO + b)] += s1;
+  }
+  __syncthreads();
+}
+
+// (QD_STREAM_A4 == 2) the LDS groups without any psi undo: DTH -- read psi and lambda and take every d(theta) of the
+// group from them as they are (one consistent pair of states), then (OUT >= 0) undo RY on lambda only, written back to
+// LDS (OUT 1) or stored to HBM (OUT 2); without DTH only lambda is read.  Per pair and bit 4 (d(theta)) + 8 (lambda)
+// vector operations instead of lds_group_adj's 20.
+template <int TOT, int LO, int NB, int NTH, bool DTH, int OUT>
+__device__ __forceinline__ void lds_group_lam(cf* tp, cf* tq, const float4* trig, float* wacc, cf* gdst = nullptr,
+                                              int br = 0) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int ACT = (1 << TOT) >> NB;
+  static_assert(LO + NB <= 5 || LO >= 5, "a group either below or from bit 5");
+  constexpr int STR = (1 << LO) + ((1 << LO) >> 5);
+  [[maybe_unused]] float dth[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) dth[b] = 0.f;
+#pragma unroll 1
+  for (int t = threadIdx.x; t < ACT; t += NTH) {
+    const int eb = ins_bits<LO, NB>(t), pb = padq(eb);
+    cf m[1 << NB];
+#pragma unroll
+    for (int j = 0; j < (1 << NB); ++j) m[j] = tq[pb + j * STR];
+    if constexpr (DTH) {
+      cf p[1 << NB];
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) p[j] = tp[pb + j * STR];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j)
+          if (!((j >> b) & 1)) {
+            const cf p0 = p[j], p1 = p[j | (1 << b)], l0 = m[j], l1 = m[j | (1 << b)];
+            dth[b] += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+          }
+    }
+    if constexpr (OUT >= 0) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const float4 tg = trig[brick_q(LO + b)];
+#pragma unroll
+        for (int j = 0; j < (1 << NB); ++j)
+          if (!((j >> b) & 1)) {
+            const cf m0 = m[j], m1 = m[j | (1 << b)];
+            m[j] = {tg.x * m0.x + tg.y * m1.x, tg.x * m0.y + tg.y * m1.y};
+            m[j | (1 << b)] = {tg.x * m1.x - tg.y * m0.x, tg.x * m1.y - tg.y * m0.y};
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < (1 << NB); ++j) {
+        if constexpr (OUT == 2)
+          *reinterpret_cast<float2*>(gdst + brick_k(eb | (j << LO), br)) = make_float2(m[j].x, m[j].y);
+        else
+          tq[pb + j * STR] = m[j];
+      }
+    }
+  }
+  if constexpr (DTH) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float s1 = wave_sum(dth[b]);
+      if (lane == 0) wacc[wv * 2 * TOT + 2 * (LO + b)] += s1;
+    }
   }
   __syncthreads();
 }
@@ -947,13 +1016,24 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
       }
 #pragma unroll
       for (int b = 0; b < NRB; ++b) dthr[b] = 0.f;
+      if constexpr (QD_STREAM_A4 == 3) {   // d(theta) only: the register bits are undone on lambda at the end
 #pragma unroll
-      for (int bb = 0; bb < NRB; ++bb) {
-        const int b = NRB - 1 - bb;
-        const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
+        for (int b = 0; b < NRB; ++b)
 #pragma unroll
-        for (int j = 0; j < 2 * NPAIR; ++j)
-          if (!((j >> b) & 1)) gate_adj_ry(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dthr[b]);
+          for (int j = 0; j < 2 * NPAIR; ++j)
+            if (!((j >> b) & 1)) {
+              const cf p0 = p[j], p1 = p[j | (1 << b)], l0 = m[j], l1 = m[j | (1 << b)];
+              dthr[b] += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+            }
+      } else {
+#pragma unroll
+        for (int bb = 0; bb < NRB; ++bb) {
+          const int b = NRB - 1 - bb;
+          const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
+#pragma unroll
+          for (int j = 0; j < 2 * NPAIR; ++j)
+            if (!((j >> b) & 1)) gate_adj_ry(p[j], p[j | (1 << b)], m[j], m[j | (1 << b)], tg, dthr[b]);
+        }
       }
       // the sums pinned here: left alone, the compiler sank their adds past the barrier below to the wave reductions,
       // keeping every product alive across the LDS write (spilled at n = 16)
@@ -999,8 +1079,39 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
     if constexpr (A4) {   // (the barrier above: every thread's brick image is in LDS; each wave adds to its own slots)
       constexpr int NB1 = RLO - 1 < 4 ? RLO - 1 : 4;
       static_assert(RLO > 1 + NB1 && STORE, "two LDS groups; lambda stored by the second");
-      lds_group_adj<C::AB, 1, NB1, NTA, 0>(tp, tq, trig, red);
-      lds_group_adj<C::AB, 1 + NB1, RLO - 1 - NB1, NTA, 2>(tp, tq, trig, red, ls, br);
+      constexpr int NB2 = RLO - 1 - NB1;
+      if constexpr (QD_STREAM_A4 == 3) {   // psi never undone: every d(theta) from the loaded pair, lambda undone last
+        lds_group_lam<C::AB, 1 + NB1, NB2, NTA, true, -1>(tp, tq, trig, red);
+        lds_group_lam<C::AB, 1, NB1, NTA, true, 1>(tp, tq, trig, red);
+        lds_group_lam<C::AB, 1 + NB1, NB2, NTA, false, 1>(tp, tq, trig, red);
+        // lambda back in the load layout: the register bits undone, coalesced 16-byte stores
+        const int pb = padq(2 * threadIdx.x);
+        cf m[2 * NPAIR];
+#pragma unroll
+        for (int j = 0; j < 2 * NPAIR; ++j) m[j] = tq[pb + (j & 1) + (j >> 1) * (2 * NTA + (2 * NTA) / 32)];
+#pragma unroll
+        for (int b = 0; b < NRB; ++b) {
+          const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
+#pragma unroll
+          for (int j = 0; j < 2 * NPAIR; ++j)
+            if (!((j >> b) & 1)) {
+              const cf m0 = m[j], m1 = m[j | (1 << b)];
+              m[j] = {tg.x * m0.x + tg.y * m1.x, tg.x * m0.y + tg.y * m1.y};
+              m[j | (1 << b)] = {tg.x * m1.x - tg.y * m0.x, tg.x * m1.y - tg.y * m0.y};
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NPAIR; ++i)
+          *reinterpret_cast<float4*>(ls + brick_k(2 * threadIdx.x + 2 * NTA * i, br)) =
+              make_float4(m[2 * i].x, m[2 * i].y, m[2 * i + 1].x, m[2 * i + 1].y);
+      } else if constexpr (QD_STREAM_A4 == 2) {   // the second group's d(theta) first, then lambda-only undo sweeps
+        lds_group_lam<C::AB, 1 + NB1, NB2, NTA, true, -1>(tp, tq, trig, red);
+        lds_group_lam<C::AB, 1, NB1, NTA, true, 1>(tp, tq, trig, red);
+        lds_group_lam<C::AB, 1 + NB1, NB2, NTA, false, 2>(tp, tq, trig, red, ls, br);
+      } else {
+        lds_group_adj<C::AB, 1, NB1, NTA, 0>(tp, tq, trig, red);
+        lds_group_adj<C::AB, 1 + NB1, NB2, NTA, 2>(tp, tq, trig, red, ls, br);
+      }
     } else if constexpr (QD_STREAM_SWEEP) {
       lds_gates_adj_acc<C::AB, C::AB, NTA>(tp, tq, trig, red);   // (the round-5 sweep)
     } else {
