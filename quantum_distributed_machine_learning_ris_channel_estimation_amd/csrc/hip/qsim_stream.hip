@@ -42,7 +42,7 @@
 #define QD_STREAM_A4 3      // (2: the register group undoes psi too; 1: the LDS groups too; 0: LDS passes only, read-only d(theta) then the lambda undo -- A/B builds)
 #endif
 #ifndef QD_STREAM_B4
-#define QD_STREAM_B4 1      // (0: reverse pass B's adjoint of qubits 8..11 over the LDS tile -- A/B builds)
+#define QD_STREAM_B4 2      // (1: the register adjoint undoes psi too, gate by gate; 0: over the LDS tile -- A/B builds)
 #endif
 #ifndef QD_STREAM_A4F
 #define QD_STREAM_A4F 1     // (0: forward pass A in four LDS sweeps of three bits -- A/B builds)
@@ -701,10 +701,22 @@ __global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const flo
   float* OH = OL + 256;
   cf* PL = reinterpret_cast<cf*>(OH + 256);               // (GEN0) product tables
   cf* PH = PL + 256;
+  [[maybe_unused]] cf* ZT = PH + 256;                     // (QD_STREAM_B4 == 2) the 16 RZ undo phases of qubits 8..11
   const int t = blockIdx.x, s = blockIdx.y, c = threadIdx.x;
   load_trig<N>(trig, x, w, s, L, l, wgroup);
   if (FIRST && threadIdx.x < N) gq[threadIdx.x] = gE[(size_t)s * N + threadIdx.x];
   __syncthreads();
+  if constexpr (QD_STREAM_B4 == 2) {   // ZT[h] = prod_b (cos phi_b/2, -+ sin phi_b/2) over qubits 8 + b (+ for bit b = 0)
+    if (threadIdx.x < 16) {
+      cf z = {1.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float4 tg = trig[8 + b];
+        z = cmul(z, cf{tg.z, ((threadIdx.x >> b) & 1) ? -tg.w : tg.w});
+      }
+      ZT[threadIdx.x] = z;
+    }
+  }
   if constexpr (FIRST) {   // o(j) = sum_q g_q (1 - 2 bit_q(j)) = OL[j & 255] + OH[j >> 8]
     const int i = threadIdx.x;
     float ol = 0.f, oh = 0.f;
@@ -770,13 +782,51 @@ __global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const flo
     float dth[4], dph[4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) dth[b] = dph[b] = 0.f;
+    if constexpr (QD_STREAM_B4 == 2) {
+      // every d(phi) from the pair as it is (Z_b commutes with the layer's gates on other qubits and with RZ_b), the four
+      // RZ undone on both at once (one phase per amplitude), every d(theta) from that pair (J_b commutes with RY on
+      // other qubits and its own), then RY undone on lambda alone -- 12 vector operations per pair and bit after the
+      // phases, against gate_adj's 36
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {   // undo rotations 11..8 (lds_gates' adjoint order)
-      const int b = 3 - bb;
-      const float4 tg = trig[8 + b];
+      for (int h = 0; h < 16; ++h) {
+        const float cc = m[h].x * p[h].y - m[h].y * p[h].x;
 #pragma unroll
-      for (int h = 0; h < 16; ++h)
-        if (!((h >> b) & 1)) gate_adj(p[h], p[h | (1 << b)], m[h], m[h | (1 << b)], tg, dth[b], dph[b]);
+        for (int b = 0; b < 4; ++b) dph[b] += ((h >> b) & 1) ? -cc : cc;
+      }
+#pragma unroll
+      for (int h = 0; h < 16; ++h) {
+        const cf z = ZT[h];
+        p[h] = cmul(p[h], z);
+        m[h] = cmul(m[h], z);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int h = 0; h < 16; ++h)
+          if (!((h >> b) & 1)) {
+            const cf p0 = p[h], p1 = p[h | (1 << b)], l0 = m[h], l1 = m[h | (1 << b)];
+            dth[b] += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+          }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float4 tg = trig[8 + b];
+#pragma unroll
+        for (int h = 0; h < 16; ++h)
+          if (!((h >> b) & 1)) {
+            const cf m0 = m[h], m1 = m[h | (1 << b)];
+            m[h] = {tg.x * m0.x + tg.y * m1.x, tg.x * m0.y + tg.y * m1.y};
+            m[h | (1 << b)] = {tg.x * m1.x - tg.y * m0.x, tg.x * m1.y - tg.y * m0.y};
+          }
+      }
+    } else {
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {   // undo rotations 11..8 (lds_gates' adjoint order)
+        const int b = 3 - bb;
+        const float4 tg = trig[8 + b];
+#pragma unroll
+        for (int h = 0; h < 16; ++h)
+          if (!((h >> b) & 1)) gate_adj(p[h], p[h | (1 << b)], m[h], m[h | (1 << b)], tg, dth[b], dph[b]);
+      }
     }
     // the sums pinned here (sunk past block_sum_vec's barrier they kept every product alive: 249 VGPRs spilled)
 #pragma unroll
@@ -1151,7 +1201,7 @@ struct Smem {
   static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 32 + 512);   // (padq image + the GEN tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
   // (QD_STREAM_B4: lambda's tile only -- 39 KB, four workgroups per CU)
-  static constexpr size_t B_BWD = 512 + (QD_STREAM_B4 ? 1 : 2) * sizeof(cf) * 4096 + 2048 + sizeof(cf) * 512;   // (+ FIRST / GEN0 tables)
+  static constexpr size_t B_BWD = 512 + (QD_STREAM_B4 ? 1 : 2) * sizeof(cf) * 4096 + 2048 + sizeof(cf) * (512 + 16);   // (+ FIRST / GEN0 / RZ tables)
   static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * (SG<N>::AS + SG<N>::AS / 8) + sizeof(cf) * 512   // (+ GEN0 tables)
                                   + sizeof(cf) * (256 + 16);                                           // (+ RZ tables)
 };
