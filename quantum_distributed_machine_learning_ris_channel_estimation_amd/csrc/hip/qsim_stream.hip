@@ -47,6 +47,9 @@
 #ifndef QD_STREAM_A4F
 #define QD_STREAM_A4F 1     // (0: forward pass A in four LDS sweeps of three bits -- A/B builds)
 #endif
+#ifndef QD_STREAM_F2
+#define QD_STREAM_F2 1      // (0: the forward passes apply RZ gate by gate instead of one phase per amplitude -- A/B builds)
+#endif
 
 namespace qd {
 namespace qstream {
@@ -135,6 +138,13 @@ __device__ __forceinline__ void gate_fwd(cf& a0, cf& a1, float4 t) {
   const cf t1 = {t.y * a0.x + t.x * a1.x, t.y * a0.y + t.x * a1.y};
   a0 = cmul(t0, cf{t.z, -t.w});
   a1 = cmul(t1, cf{t.z, t.w});
+}
+// RY(theta) alone on the pair (the forward's RZ phases applied afterwards, one per amplitude: QD_STREAM_F2)
+__device__ __forceinline__ void gate_ry(cf& a0, cf& a1, float4 t) {
+  const cf t0 = {t.x * a0.x - t.y * a1.x, t.x * a0.y - t.y * a1.y};
+  const cf t1 = {t.y * a0.x + t.x * a1.x, t.y * a0.y + t.x * a1.y};
+  a0 = t0;
+  a1 = t1;
 }
 // adjoint step on psi / lambda AFTER the gate: accumulate d(theta), d(phi), undo the gate on both
 __device__ __forceinline__ void gate_adj(cf& p0, cf& p1, cf& l0, cf& l1, float4 t, float& dth, float& dph) {
@@ -494,8 +504,11 @@ __device__ __forceinline__ void lds_group_lam(cf* tp, cf* tq, const float4* trig
 
 // The forward counterpart (pass A, QD_STREAM_A4F): RZ RY on bits [LO, LO + NB) of the LDS brick, one sweep; TOG:
 // the result straight to the state in HBM (gdst, brick br) instead of back to LDS.
+// QD_STREAM_F2: RY only per bit; the store (TOG) multiplies every amplitude by the pass's whole RZ diagonal
+// ZL[e & 255] ZH[e >> 8] (RZ of a qubit commutes with every other qubit's RY, so the phases may wait for the last RY).
 template <int TOT, int LO, int NB, int NTH, bool TOG>
-__device__ __forceinline__ void lds_group_fwd(cf* tp, const float4* trig, cf* gdst = nullptr, int br = 0) {
+__device__ __forceinline__ void lds_group_fwd(cf* tp, const float4* trig, cf* gdst = nullptr, int br = 0,
+                                              const cf* ZL = nullptr, const cf* ZH = nullptr) {
   constexpr int ACT = (1 << TOT) >> NB;
   static_assert(LO + NB <= 5 || LO >= 5, "a group either below or from bit 5");
   constexpr int STR = (1 << LO) + ((1 << LO) >> 5);
@@ -510,12 +523,21 @@ __device__ __forceinline__ void lds_group_fwd(cf* tp, const float4* trig, cf* gd
       const float4 tg = trig[brick_q(LO + b)];
 #pragma unroll
       for (int j = 0; j < (1 << NB); ++j)
-        if (!((j >> b) & 1)) gate_fwd(p[j], p[j | (1 << b)], tg);
+        if (!((j >> b) & 1)) {
+          if constexpr (QD_STREAM_F2) gate_ry(p[j], p[j | (1 << b)], tg);
+          else gate_fwd(p[j], p[j | (1 << b)], tg);
+        }
     }
 #pragma unroll
     for (int j = 0; j < (1 << NB); ++j) {
-      if constexpr (TOG) *reinterpret_cast<float2*>(gdst + brick_k(eb | (j << LO), br)) = make_float2(p[j].x, p[j].y);
-      else tp[pb + j * STR] = p[j];
+      if constexpr (TOG) {
+        const int e = eb | (j << LO);
+        cf v = p[j];
+        if constexpr (QD_STREAM_F2) v = cmul(v, cmul(ZL[e & 255], ZH[e >> 8]));
+        *reinterpret_cast<float2*>(gdst + brick_k(e, br)) = make_float2(v.x, v.y);
+      } else {
+        tp[pb + j * STR] = p[j];
+      }
     }
   }
   if constexpr (!TOG) __syncthreads();
@@ -541,6 +563,29 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     // apart) in registers, the rest in two LDS groups, the second storing straight to HBM -- 2 LDS sweeps and the
     // barriers of 2 instead of 4 sweeps + the store loop
     constexpr int NPAIR = C::AS / (2 * NT), RLO = ilog2c(2 * NT), NRB = 1 + ilog2c(NPAIR);
+    // (F2) the pass's RZ diagonal: ZL over brick bits 0..7, ZH over 8.. (qubit q's factor cos(phi/2) -+ i sin(phi/2),
+    // - for bit 0), past the padded image and the GEN tables; read by the last group after two barriers
+    cf* ZLf = tp + C::AS + C::AS / 32 + 512;
+    cf* ZHf = ZLf + 256;
+    if constexpr (QD_STREAM_F2) {
+      const int i = threadIdx.x;
+      cf a = {1.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const float4 tq4 = trig[b];
+        a = cmul(a, cf{tq4.z, ((i >> b) & 1) ? tq4.w : -tq4.w});
+      }
+      ZLf[i] = a;
+      if (i < (1 << (C::AB - 8))) {
+        cf h = {1.f, 0.f};
+#pragma unroll
+        for (int b = 8; b < C::AB; ++b) {
+          const float4 tq4 = trig[brick_q(b)];
+          h = cmul(h, cf{tq4.z, ((i >> (b - 8)) & 1) ? tq4.w : -tq4.w});
+        }
+        ZHf[i] = h;
+      }
+    }
     cf p[2 * NPAIR];
     if constexpr (GEN) {   // the ring image of the layer-0 product state, generated in registers
       cf* PL = tp + C::AS + C::AS / 32;   // (past the padded image)
@@ -569,7 +614,10 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
       const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
 #pragma unroll
       for (int j = 0; j < 2 * NPAIR; ++j)
-        if (!((j >> b) & 1)) gate_fwd(p[j], p[j | (1 << b)], tg);
+        if (!((j >> b) & 1)) {
+          if constexpr (QD_STREAM_F2) gate_ry(p[j], p[j | (1 << b)], tg);
+          else gate_fwd(p[j], p[j | (1 << b)], tg);
+        }
     }
     const int pb = padq(2 * threadIdx.x);
 #pragma unroll
@@ -579,7 +627,7 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     static_assert(RLO > 1 + NB1, "two LDS groups");
     constexpr int NB2 = (C::AB < RLO ? C::AB : RLO) - 1 - NB1;   // (n = 13: the brick ends at bit 8)
     lds_group_fwd<C::AB, 1, NB1, NT, false>(tp, trig);
-    lds_group_fwd<C::AB, 1 + NB1, NB2, NT, true>(tp, trig, st, br);
+    lds_group_fwd<C::AB, 1 + NB1, NB2, NT, true>(tp, trig, st, br, ZLf, ZHf);
     return;
   }
   if constexpr (GEN) {
@@ -625,6 +673,22 @@ __global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x,
   cf* tp = reinterpret_cast<cf*>(smem + 512);
   const int t = blockIdx.x, s = blockIdx.y, c = threadIdx.x;
   load_trig<N>(trig, x, w, s, L, l, wgroup);
+  // (F2, not LAST) the four RZ of qubits 8..11 as one phase per amplitude: ZT[h] built by threads 0..15 from the
+  // weights directly, so the one barrier below covers it too.  LAST: the phases do not change |amplitude|^2 -- none.
+  [[maybe_unused]] cf* ZT = reinterpret_cast<cf*>(smem + 512 - 16 * sizeof(cf));
+  if constexpr (QD_STREAM_F2 && !LAST) {
+    if (threadIdx.x < 16) {
+      const float* wl = w + (wgroup > 0 ? (size_t)(s / wgroup) * 2 * N * L : 0) + 2 * N * l;
+      cf z = {1.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        float sp, cp;
+        __sincosf(0.5f * wl[2 * (8 + b) + 1], &sp, &cp);
+        z = cmul(z, cf{cp, ((threadIdx.x >> b) & 1) ? sp : -sp});
+      }
+      ZT[threadIdx.x] = z;
+    }
+  }
   const cf* src = in + (size_t)s * C::D + ((size_t)t << 12);
   cf a[16];
 #pragma unroll
@@ -635,7 +699,14 @@ __global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x,
     const float4 tg = trig[8 + b];
 #pragma unroll
     for (int h = 0; h < 16; ++h)
-      if (!((h >> b) & 1)) gate_fwd(a[h], a[h | (1 << b)], tg);
+      if (!((h >> b) & 1)) {
+        if constexpr (QD_STREAM_F2) gate_ry(a[h], a[h | (1 << b)], tg);
+        else gate_fwd(a[h], a[h | (1 << b)], tg);
+      }
+  }
+  if constexpr (QD_STREAM_F2 && !LAST) {
+#pragma unroll
+    for (int h = 0; h < 16; ++h) a[h] = cmul(a[h], ZT[h]);
   }
 #pragma unroll
   for (int h = 0; h < 16; ++h) tp[ring_fwd<N>((t << 12) | (h << 8) | c) & 4095] = a[h];
@@ -1198,7 +1269,8 @@ __global__ void __launch_bounds__(256) reduce_dx(const float* __restrict__ slab,
 // ------------------------------------------------------------------------------------------ host
 template <int N>
 struct Smem {
-  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 32 + 512);   // (padq image + the GEN tables)
+  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 32 + 512 + 256 + 16);   // (padq image + the GEN
+                                                                                                    // and RZ tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
   // (QD_STREAM_B4: lambda's tile only -- 39 KB, four workgroups per CU)
   static constexpr size_t B_BWD = 512 + (QD_STREAM_B4 ? 1 : 2) * sizeof(cf) * 4096 + 2048 + sizeof(cf) * (512 + 16);   // (+ FIRST / GEN0 / RZ tables)
