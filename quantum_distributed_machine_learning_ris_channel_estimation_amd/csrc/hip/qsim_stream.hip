@@ -33,6 +33,8 @@
 //
 // State traffic at n = 16, L = 3 (1.2 GB per state): forward 6 state passes, backward ~12 (round 2: 7 and
 // 21, with psi un-applied and re-stored in every backward pass).
+#include <cstdlib>
+
 #include "common.h"
 
 #ifndef QD_STREAM_SWEEP
@@ -708,6 +710,40 @@ __global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x,
 #pragma unroll
     for (int h = 0; h < 16; ++h) a[h] = cmul(a[h], ZT[h]);
   }
+  if constexpr (QD_STREAM_F2 && LAST) {
+    // <Z_q> straight from the registers: amplitude k = (t << 12) | (h << 8) | c lands at j = ring(k), and bit q of j
+    // is the parity of k's bits 0..q (bit 0: of bits 1..N-1) -- for q <= 7 this thread's constant, for q = 8..11 that
+    // constant times a sign pattern over h, above that also the tile's -- so 5 signed sums of |a_h|^2 give all N
+    // partials (no ring scatter through LDS, no barrier, no 16-way sign loop per amplitude)
+    float S = 0.f, Sh[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      const float pw = a[h].x * a[h].x + a[h].y * a[h].y;
+      S += pw;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) Sh[m] += (__builtin_popcount(h & ((2 << m) - 1)) & 1) ? -pw : pw;
+    }
+    const int pc = __popc(c & 255) & 1;   // parity of k's bits 0..7
+    float part[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      if (q == 0) {
+        const int par = (__popc(c & 254) + __popc(t)) & 1;   // bits 1..7 and the tile's; h's parity in Sh[3]
+        part[q] = par ? -Sh[3] : Sh[3];
+      } else if (q < 8) {
+        part[q] = (__popc(c & ((2 << q) - 1)) & 1) ? -S : S;
+      } else if (q < 12) {
+        part[q] = pc ? -Sh[q - 8] : Sh[q - 8];
+      } else {
+        const int par = (pc + __popc(t & ((2 << (q - 12)) - 1))) & 1;
+        part[q] = par ? -Sh[3] : Sh[3];
+      }
+    }
+    float o[N];
+    block_sum_vec<N>(part, red, o);
+    if (threadIdx.x < N) epart[((size_t)s * C::NTILE + t) * N + threadIdx.x] = o[threadIdx.x];
+    return;
+  }
 #pragma unroll
   for (int h = 0; h < 16; ++h) tp[ring_fwd<N>((t << 12) | (h << 8) | c) & 4095] = a[h];
   __syncthreads();
@@ -1341,8 +1377,13 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     attr = true;
   }
   const dim3 ga(ROWS, B), gb(C::NTILE, B);
-  // bricks per workgroup of the reverse pass A (1 / 2 / 4 instantiated; 4 measured fastest)
-  constexpr int bpb = 4;
+  // bricks per workgroup of the reverse pass A (1 / 2 / 4 instantiated; 4 measured fastest in round 3; QDML_QSTREAM_BPB
+  // overrides it for measurements)
+  static const int bpb = [] {
+    const char* e = std::getenv("QDML_QSTREAM_BPB");
+    const int v = e ? std::atoi(e) : 4;
+    return (v == 1 || v == 2) ? v : 4;
+  }();
   const cf* lin = nullptr;
   for (int l = L - 1; l >= 0; --l) {
     cf* lo = ((L - 1 - l) % 2 == 0) ? L1 : L2;
