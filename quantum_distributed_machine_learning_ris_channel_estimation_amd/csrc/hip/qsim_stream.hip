@@ -392,7 +392,14 @@ __device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float
 // 16-qubit pass 1.11 against 1.23 ms, config 5's step 6.91-6.97 against 7.17-7.25 ms
 // (profiles/r6_21_q16_pass_a_regs_ab.txt, r6_22_*).  LDS image: one pad amplitude per 32 (padq), so the group on
 // bits 1..4 -- lanes 32 amplitudes apart -- hits distinct banks.
-__device__ __forceinline__ int padq(int e) { return e + (e >> 5); }
+// (two pad amplitudes per 32: a half-wave of the bits-1..4 group -- lanes 32 amplitudes apart, and bit 0 -- then hits
+// 32 distinct 8-byte slots; with one per 32, pairs of lanes shared a slot: 22 % of the pass's LDS cycles were bank
+// conflicts, profiles/r6_35_qstream_pmc_b.md)
+#ifndef QD_STREAM_PADQ
+#define QD_STREAM_PADQ 2
+#endif
+constexpr int PADQ = QD_STREAM_PADQ;
+__device__ __forceinline__ int padq(int e) { return e + PADQ * (e >> 5); }
 
 // OUT: 0 = both states back to LDS, 1 = lambda back to LDS, 2 = lambda straight to its state in HBM (gdst, brick br:
 // for a fixed register index the lanes hold runs of 32 consecutive amplitudes, 256-byte pieces of the state)
@@ -404,7 +411,7 @@ __device__ __forceinline__ void lds_group_adj(cf* tp, cf* tq, const float4* trig
   // the group's amplitudes sit at padq(base) + j STR: base has the group's bits clear, so with the group below bit 5
   // or from bit 5 up no carry crosses the pad (one address register, the rest immediate offsets)
   static_assert(LO + NB <= 5 || LO >= 5, "a group either below or from bit 5");
-  constexpr int STR = (1 << LO) + ((1 << LO) >> 5);
+  constexpr int STR = (1 << LO) + PADQ * ((1 << LO) >> 5);
   float dth[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) dth[b] = 0.f;
@@ -450,7 +457,7 @@ __device__ __forceinline__ void lds_group_lam(cf* tp, cf* tq, const float4* trig
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int ACT = (1 << TOT) >> NB;
   static_assert(LO + NB <= 5 || LO >= 5, "a group either below or from bit 5");
-  constexpr int STR = (1 << LO) + ((1 << LO) >> 5);
+  constexpr int STR = (1 << LO) + PADQ * ((1 << LO) >> 5);
   [[maybe_unused]] float dth[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) dth[b] = 0.f;
@@ -513,7 +520,7 @@ __device__ __forceinline__ void lds_group_fwd(cf* tp, const float4* trig, cf* gd
                                               const cf* ZL = nullptr, const cf* ZH = nullptr) {
   constexpr int ACT = (1 << TOT) >> NB;
   static_assert(LO + NB <= 5 || LO >= 5, "a group either below or from bit 5");
-  constexpr int STR = (1 << LO) + ((1 << LO) >> 5);
+  constexpr int STR = (1 << LO) + PADQ * ((1 << LO) >> 5);
 #pragma unroll 1
   for (int t = threadIdx.x; t < ACT; t += NTH) {
     const int eb = ins_bits<LO, NB>(t), pb = padq(eb);
@@ -567,7 +574,7 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     constexpr int NPAIR = C::AS / (2 * NT), RLO = ilog2c(2 * NT), NRB = 1 + ilog2c(NPAIR);
     // (F2) the pass's RZ diagonal: ZL over brick bits 0..7, ZH over 8.. (qubit q's factor cos(phi/2) -+ i sin(phi/2),
     // - for bit 0), past the padded image and the GEN tables; read by the last group after two barriers
-    cf* ZLf = tp + C::AS + C::AS / 32 + 512;
+    cf* ZLf = tp + C::AS + PADQ * (C::AS / 32) + 512;
     cf* ZHf = ZLf + 256;
     if constexpr (QD_STREAM_F2) {
       const int i = threadIdx.x;
@@ -590,7 +597,7 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     }
     cf p[2 * NPAIR];
     if constexpr (GEN) {   // the ring image of the layer-0 product state, generated in registers
-      cf* PL = tp + C::AS + C::AS / 32;   // (past the padded image)
+      cf* PL = tp + C::AS + PADQ * (C::AS / 32);   // (past the padded image)
       cf* PH = PL + 256;
       product_tables<N, NT>(trig0, PL, PH, 0);
       __syncthreads();
@@ -623,7 +630,7 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     }
     const int pb = padq(2 * threadIdx.x);
 #pragma unroll
-    for (int j = 0; j < 2 * NPAIR; ++j) tp[pb + (j & 1) + (j >> 1) * (2 * NT + (2 * NT) / 32)] = p[j];
+    for (int j = 0; j < 2 * NPAIR; ++j) tp[pb + (j & 1) + (j >> 1) * (2 * NT + PADQ * ((2 * NT) / 32))] = p[j];
     __syncthreads();
     constexpr int NB1 = RLO - 1 < 4 ? RLO - 1 : 4;
     static_assert(RLO > 1 + NB1, "two LDS groups");
@@ -1196,11 +1203,11 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
       // keeping every product alive across the LDS write (spilled at n = 16)
 #pragma unroll
       for (int b = 0; b < NRB; ++b) asm volatile("" : "+v"(dthr[b]));
-      // (e = 2 t + 2 NTA i + h: padq(e) = padq(2 t) + h + i (2 NTA + 2 NTA / 32) -- 2 t + 1 crosses no pad)
+      // (e = 2 t + 2 NTA i + h: padq(e) = padq(2 t) + h + i (2 NTA + PADQ 2 NTA / 32) -- 2 t + 1 crosses no pad)
       const int pb = padq(2 * threadIdx.x);
 #pragma unroll
       for (int j = 0; j < 2 * NPAIR; ++j) {
-        const int o = pb + (j & 1) + (j >> 1) * (2 * NTA + (2 * NTA) / 32);
+        const int o = pb + (j & 1) + (j >> 1) * (2 * NTA + PADQ * ((2 * NTA) / 32));
         tp[o] = p[j];
         tq[o] = m[j];
       }
@@ -1245,7 +1252,7 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
         const int pb = padq(2 * threadIdx.x);
         cf m[2 * NPAIR];
 #pragma unroll
-        for (int j = 0; j < 2 * NPAIR; ++j) m[j] = tq[pb + (j & 1) + (j >> 1) * (2 * NTA + (2 * NTA) / 32)];
+        for (int j = 0; j < 2 * NPAIR; ++j) m[j] = tq[pb + (j & 1) + (j >> 1) * (2 * NTA + PADQ * ((2 * NTA) / 32))];
 #pragma unroll
         for (int b = 0; b < NRB; ++b) {
           const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
@@ -1305,7 +1312,7 @@ __global__ void __launch_bounds__(256) reduce_dx(const float* __restrict__ slab,
 // ------------------------------------------------------------------------------------------ host
 template <int N>
 struct Smem {
-  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 32 + 512 + 256 + 16);   // (padq image + the GEN
+  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 16 + 512 + 256 + 16);   // (padq image + the GEN
                                                                                                     // and RZ tables)
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
   // (QD_STREAM_B4: lambda's tile only -- 39 KB, four workgroups per CU)
