@@ -2861,7 +2861,9 @@ static size_t split_smem(int cin, int H, int W) {
 QD_API int qd_conv_fwd_split(int layer, const void* xin, const float* st_prev, const uint16_t* w, uint16_t* z,
                              float* stats, int N, int E, int B, int H, int W, int chunks, int sps, const BnFwd* bnf,
                              void* stream) {
-  if (B <= 0 || N % B || sps < 4 || sps > 6 || chunks <= 0 || (long)chunks * sps < B ||
+  // (layer 1 also at sps 12 = 4 waves x the per-wave kernel's 3 samples: the same statistics chunking as conv3x3_kernel,
+  // so it can replace that layer alone)
+  if (B <= 0 || N % B || ((sps < 4 || sps > 6) && !(layer == 1 && sps == 12)) || chunks <= 0 || (long)chunks * sps < B ||
       (layer != 1 && !bnf && !st_prev))
     return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
@@ -2878,7 +2880,11 @@ QD_API int qd_conv_fwd_split(int layer, const void* xin, const float* st_prev, c
                                     grid, dim3(256), split_smem(32, H, W), s, (const uint16_t*)xin, st_prev, w, z,    \
                                     stats, E, B, chunks, bf))                                                         \
   }
-  if (sps == 4) { QD_SPLIT(4) } else if (sps == 5) { QD_SPLIT(5) } else { QD_SPLIT(6) }
+  if (sps == 12) {   // (layer 1 only, checked above)
+    QD_GEOM(WW, hipLaunchKernelGGL((conv3x3_split_kernel<2, WW, IN_RAW_F32, float, 12, WW == 8 ? 12 : 2>), grid,
+                                    dim3(256), split_smem(2, H, W), s, (const float*)xin, nullptr, w, z, stats, E, B,
+                                    chunks, bf))
+  } else if (sps == 4) { QD_SPLIT(4) } else if (sps == 5) { QD_SPLIT(5) } else { QD_SPLIT(6) }
 #undef QD_SPLIT
   return (int)hipGetLastError();
 }

@@ -81,6 +81,10 @@ class Knobs:
     # 0.3807-0.3827 ms, P256 1.105-1.109 against 1.089-1.092: profiles/r6_18_conv_split_ab.txt, r6_20_*)
     conv_fwd_split: bool = False
     conv_sps: int = 5
+    # (round 6) layer 1 alone on conv3x3_split_kernel at 4 x conv_spw samples per workgroup (the statistics chunking of
+    # conv3x3_kernel, so layers 2 / 3 and the BN tail are unchanged).  Off: level in the step, 0.3775-0.3820 against
+    # 0.3768-0.3801 ms (profiles/r6_37_conv_l1_split_ab.txt)
+    conv_l1_split: bool = False
     conv_spb_f: int = 5
     conv_spb_w1: int = 4
 

@@ -117,6 +117,8 @@ class ConvStackHIP:
         self.fwd_split = bool(KNOBS.conv_fwd_split) and not self.f8conv
         self.sps = max(1, int(KNOBS.conv_sps))
         self.chunks_f = (B + self.sps - 1) // self.sps if self.fwd_split else self.chunks
+        # layer 1 alone on the split kernel at 4 spw samples per workgroup: conv3x3_kernel's chunking (KNOBS.conv_l1_split)
+        self.l1_split = bool(KNOBS.conv_l1_split) and not self.fwd_split and 4 * spw == 12
         self.stats = [torch.zeros(U, self.chunks_f, EC, 2, device=dev) for _ in range(3)]   # per layer
         # BN backward partials per layer, planar rows [sum g | sum g*xhat] x EC (their column sums are
         # dbeta / dgamma: jobs of the step's batched slab reduction)
@@ -250,7 +252,11 @@ class ConvStackHIP:
                 bnf = BnFwd(nat.ptr(self.stats[j]), nat.ptr(m.bn_w[j]), nat.ptr(m.bn_b[j]), nat.ptr(m.run_mean[j]),
                             nat.ptr(m.run_var[j]), nat.ptr(self.st[j]), self.chunks_f, float(self.B * self.HW),
                             m.momentum, m.eps, int(training))
-            if self.fwd_split:
+            if self.l1_split and k == 0:
+                nat.check(self._fwd_split(1, nat.ptr(inp), None, nat.ptr(self.wpk[0]), nat.ptr(self.z[0]),
+                                          nat.ptr(self.stats[0]), self.N, self.E, self.B, self.H, self.W, self.chunks,
+                                          12, None, st), "conv_fwd_split1")
+            elif self.fwd_split:
                 nat.check(self._fwd_split(k + 1, nat.ptr(inp), _ptr(st_prev), nat.ptr(self.wpk[k]), nat.ptr(self.z[k]),
                                           nat.ptr(self.stats[k]), self.N, self.E, self.B, self.H, self.W, self.chunks_f,
                                           self.sps, ctypes.byref(bnf) if bnf is not None else None, st),

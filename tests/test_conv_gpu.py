@@ -468,3 +468,27 @@ def test_conv_forward_split_matches_conv3x3_kernel(cuda, monkeypatch, pilot_num,
     for j, (p, q) in enumerate(zip(g0, g1)):
         assert rel(q, p) < 1e-2, (j, rel(q, p))
     assert rel(f1[0], b.features(Yp, training=True)) < 2e-2
+
+
+@pytest.mark.parametrize("pilot_num,B", [(128, 256), (128, 40), (256, 64)])
+def test_conv_layer1_split_matches_conv3x3_kernel(cuda, monkeypatch, pilot_num, B):
+    """Round 6: layer 1 alone on conv3x3_split_kernel at 12 samples per workgroup (KNOBS.conv_l1_split: the statistics
+    chunking of conv3x3_kernel, whose layers 2 / 3 and BN tail then run unchanged) against conv3x3_kernel: layer 1's
+    z bit for bit, the rest of the forward to a bf16 flip (the per-chunk statistics summed in another order)."""
+    U = 3
+    outs = []
+    for l1 in (False, True):
+        monkeypatch.setattr(KNOBS, "conv_l1_split", l1)
+        a, _ = pair(cuda, pilot_num)
+        conv = ConvStackHIP(a, U, B)
+        assert conv.l1_split == l1
+        torch.manual_seed(21)
+        Yp = torch.randn(3, U, B, 2, a.H, a.W, device=cuda)
+        h3 = conv.forward(a.pack_input(Yp).contiguous(), training=True)
+        torch.cuda.synchronize()
+        outs.append([h3.clone()] + [conv.z[k].clone() for k in range(3)] + [conv.stats[0].clone()])
+    x0, x1 = outs
+    assert torch.equal(x0[1], x1[1])
+    assert torch.allclose(x0[4], x1[4], rtol=1e-5, atol=1e-3)
+    for j, (p, q) in enumerate(zip(x0[:4], x1[:4])):
+        assert rel(q, p) < 1e-3, (j, rel(q, p))
