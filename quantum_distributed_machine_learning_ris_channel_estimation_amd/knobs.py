@@ -86,6 +86,10 @@ class Knobs:
     # 0.3768-0.3801 ms (profiles/r6_37_conv_l1_split_ab.txt)
     conv_l1_split: bool = False
     conv_spb_f: int = 5
+    # (round 6) the same at P256 (W = 16): its fused backward holds 131 KB of LDS, one workgroup per CU, so spb 5's 468
+    # workgroups ran in two rounds; 10 (234) is one -- the P256 step 1.109-1.118 against 1.128-1.138 ms alternating,
+    # 1.077-1.078 against 1.098-1.103 on another box (profiles/r6_40_p256_conv_spb10_ab.txt, r6_38_*, r6_39_*)
+    conv_spb_f_w16: int = 10
     conv_spb_w1: int = 4
 
 

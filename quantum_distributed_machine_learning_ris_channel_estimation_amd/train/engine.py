@@ -321,7 +321,8 @@ class HDCEStep:
         self.dgrad_bnred = False
         if self.hip:
             from ..ops.conv import ConvStackHIP
-            self.conv = ConvStackHIP(model, n_users, batch, spw=KNOBS.conv_spw, spb_f=KNOBS.conv_spb_f,
+            self.conv = ConvStackHIP(model, n_users, batch, spw=KNOBS.conv_spw,
+                                     spb_f=KNOBS.conv_spb_f_w16 if model.W == 16 else KNOBS.conv_spb_f,
                                      spb_w1=KNOBS.conv_spb_w1)
             self.conv.count_batches = True   # num_batches_tracked advanced inside the first BN launch
             self.fc_b_lp = None
