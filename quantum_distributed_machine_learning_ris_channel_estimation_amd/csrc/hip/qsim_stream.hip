@@ -1383,7 +1383,6 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     (void)allow_lds(pass_a_bwd<N, false, true, 1>, S::A_BWD);
     attr = true;
   }
-  const dim3 ga(ROWS, B), gb(C::NTILE, B);
   // bricks per workgroup of the reverse pass A (1 / 2 / 4 instantiated; 4 measured fastest in round 3; QDML_QSTREAM_BPB
   // overrides it for measurements)
   static const int bpb = [] {
@@ -1391,35 +1390,57 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     const int v = e ? std::atoi(e) : 4;
     return (v == 1 || v == 2) ? v : 4;
   }();
-  const cf* lin = nullptr;
-  for (int l = L - 1; l >= 0; --l) {
-    cf* lo = ((L - 1 - l) % 2 == 0) ? L1 : L2;
-    const cf* ps = l > 0 ? reinterpret_cast<const cf*>(reinterpret_cast<const char*>(psave) + (size_t)(l - 1) * sb)
-                         : nullptr;
-    if (l == L - 1)
-      hipLaunchKernelGGL((pass_b_bwd<N, true, false>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, ps, lin, lo,
-                         slab);
-    else if (l > 0)
-      hipLaunchKernelGGL((pass_b_bwd<N, false, false>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, ps, lin, lo,
-                         slab);
-    else
-      hipLaunchKernelGGL((pass_b_bwd<N, false, true>), gb, dim3(NT), S::B_BWD, st, x, w, gE, L, l, wgroup, ps, lin, lo,
-                         slab);
-    if (l > 0) {
-      if (bpb == 4)
-        hipLaunchKernelGGL((pass_a_bwd<N, true, false, 4>), dim3(ROWS / 4, B), dim3(C::NTA), S::A_BWD, st, x, w, L, l,
-                           wgroup, ps, lo, slab);
-      else if (bpb == 2)
-        hipLaunchKernelGGL((pass_a_bwd<N, true, false, 2>), dim3(ROWS / 2, B), dim3(C::NTA), S::A_BWD, st, x, w, L, l,
-                           wgroup, ps, lo, slab);
+  // (round 6) samples per backward chunk: the whole adjoint (all layers) runs chunk by chunk, so the two lambda
+  // buffers -- chunk-sized, reused -- stay in the 256 MB Infinity Cache between the passes instead of streaming 1.2 GB
+  // each through HBM per pass.  A chunk never straddles a QuantumNAT weight group (it divides wgroup).  0: one chunk,
+  // the default: measured slower at every size -- backward 3.60 / 3.93 / 5.83 ms at 256 / 128 / 64 samples against
+  // 3.42 unchunked, config 5 5.45-5.46 / 5.84-5.90 against 5.20-5.23 ms (the smaller grids leave CUs idle and add
+  // launches; the cache saves less than that, profiles/r6_46_*)
+  static const int chunk_env = [] {
+    const char* e = std::getenv("QDML_QSTREAM_CHUNK");
+    return e ? std::atoi(e) : 0;
+  }();
+  int CH = chunk_env > 0 && chunk_env < B ? chunk_env : B;
+  if (wgroup > 0 && CH < B && wgroup % CH != 0) CH = B;
+  const int P2 = 2 * N * L;
+  for (int s0 = 0; s0 < B; s0 += CH) {
+    const int Bc = B - s0 < CH ? B - s0 : CH;
+    const float* xc = x + (size_t)s0 * N;
+    const float* wc = w + (wgroup > 0 ? (size_t)(s0 / wgroup) * P2 : 0);
+    const float* gc = gE + (size_t)s0 * N;
+    float* slc = slab + (size_t)s0 * ROWS * P2;
+    const dim3 ga(ROWS, Bc), gb(C::NTILE, Bc);
+    const cf* lin = nullptr;
+    for (int l = L - 1; l >= 0; --l) {
+      cf* lo = ((L - 1 - l) % 2 == 0) ? L1 : L2;
+      const cf* ps = l > 0 ? reinterpret_cast<const cf*>(reinterpret_cast<const char*>(psave) + (size_t)(l - 1) * sb) +
+                                 (size_t)s0 * C::D
+                           : nullptr;
+      if (l == L - 1)
+        hipLaunchKernelGGL((pass_b_bwd<N, true, false>), gb, dim3(NT), S::B_BWD, st, xc, wc, gc, L, l, wgroup, ps, lin,
+                           lo, slc);
+      else if (l > 0)
+        hipLaunchKernelGGL((pass_b_bwd<N, false, false>), gb, dim3(NT), S::B_BWD, st, xc, wc, gc, L, l, wgroup, ps, lin,
+                           lo, slc);
       else
-        hipLaunchKernelGGL((pass_a_bwd<N, true, false, 1>), ga, dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps, lo,
-                           slab);
-    } else {
-      hipLaunchKernelGGL((pass_a_bwd<N, false, true, 1>), dim3(1, B), dim3(C::NTA), S::A_BWD, st, x, w, L, l, wgroup, ps,
-                         lo, slab);
+        hipLaunchKernelGGL((pass_b_bwd<N, false, true>), gb, dim3(NT), S::B_BWD, st, xc, wc, gc, L, l, wgroup, ps, lin,
+                           lo, slc);
+      if (l > 0) {
+        if (bpb == 4)
+          hipLaunchKernelGGL((pass_a_bwd<N, true, false, 4>), dim3(ROWS / 4, Bc), dim3(C::NTA), S::A_BWD, st, xc, wc, L,
+                             l, wgroup, ps, lo, slc);
+        else if (bpb == 2)
+          hipLaunchKernelGGL((pass_a_bwd<N, true, false, 2>), dim3(ROWS / 2, Bc), dim3(C::NTA), S::A_BWD, st, xc, wc, L,
+                             l, wgroup, ps, lo, slc);
+        else
+          hipLaunchKernelGGL((pass_a_bwd<N, true, false, 1>), ga, dim3(C::NTA), S::A_BWD, st, xc, wc, L, l, wgroup, ps,
+                             lo, slc);
+      } else {
+        hipLaunchKernelGGL((pass_a_bwd<N, false, true, 1>), dim3(1, Bc), dim3(C::NTA), S::A_BWD, st, xc, wc, L, l,
+                           wgroup, ps, lo, slc);
+      }
+      lin = lo;
     }
-    lin = lo;
   }
   hipLaunchKernelGGL(reduce_dx, dim3((B * N + 255) / 256), dim3(256), 0, st, slab, dx, B, N, 2 * N * L);
   return (int)hipGetLastError();
