@@ -395,6 +395,12 @@ __device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float
 // (two pad amplitudes per 32: a half-wave of the bits-1..4 group -- lanes 32 amplitudes apart, and bit 0 -- then hits
 // 32 distinct 8-byte slots; with one per 32, pairs of lanes shared a slot: 22 % of the pass's LDS cycles were bank
 // conflicts, profiles/r6_35_qstream_pmc_b.md)
+#ifndef QD_STREAM_A1T
+#define QD_STREAM_A1T 1
+#endif
+#ifndef QD_STREAM_A1T_OCC
+#define QD_STREAM_A1T_OCC 3
+#endif
 #ifndef QD_STREAM_PADQ
 #define QD_STREAM_PADQ 2
 #endif
@@ -1298,6 +1304,180 @@ __global__ void __launch_bounds__(SG<N>::NTA, 2) pass_a_bwd(const float* __restr
   }
 }
 
+// (QD_STREAM_A1T) the reverse pass A (layers l > 0) on ONE LDS tile instead of psi's and lambda's: lambda stays in
+// registers in its load layout while psi goes through the tile, and every d(theta) of the LDS bits 1 .. RLO - 1 comes
+// from psi's partner amplitudes read there -- for bit b the thread's pairs (2 t, 2 t + 1) + 2 NTA i meet psi at
+// 2 t ^ 2^b, one 16-byte read per pair and bit, sign = bit b of 2 t (constant over i).  Then lambda takes the tile and
+// is undone group by group (lds_group_lam without d(theta)), read back and finished on its register bits as in
+// pass_a_bwd.  Same sums from the same phase-undone loaded pair as QD_STREAM_A4 = 3; ~38 KB of LDS and no
+// next-brick registers instead of 79 KB + 64 prefetch VGPRs: up to four workgroups per CU instead of two.
+template <int N, int BPB>
+__global__ void __launch_bounds__(SG<N>::NTA, QD_STREAM_A1T_OCC) pass_a_bwd1(const float* __restrict__ x, const float* __restrict__ w,
+                                                           int L, int l, int wgroup, const cf* __restrict__ pst,
+                                                           cf* __restrict__ lst, float* __restrict__ slab) {
+  using C = SG<N>;
+  constexpr int NTA = C::NTA, AB = C::AB, AS = C::AS;
+  constexpr int NPAIR = AS / (2 * NTA);
+  constexpr int RLO = ilog2c(2 * NTA), NRB = 1 + ilog2c(NPAIR);
+  constexpr int NB1 = RLO - 1 < 4 ? RLO - 1 : 4, NB2 = RLO - 1 - NB1;
+  static_assert(NB2 > 0 && (2 * NTA) % 32 == 0, "two LDS groups; register index strides whole pad blocks");
+  constexpr int IST = 2 * NTA + PADQ * ((2 * NTA) / 32);   // tile stride of register index i
+  constexpr bool ZSEP = (2 * NTA) % 256 == 0;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* trig = reinterpret_cast<float4*>(smem);
+  float* red = reinterpret_cast<float*>(smem + 256);   // (NTA / 64) * 2 AB floats, every slot written each brick
+  cf* T = reinterpret_cast<cf*>(smem + 1024);
+  cf* ZL = T + AS + PADQ * (AS / 32);
+  cf* ZH = ZL + 256;
+  const int s = blockIdx.y;
+  const int P = 2 * N * L;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  load_trig<N>(trig, x, w, s, L, l, wgroup);
+  char* lc = reinterpret_cast<char*>(lst + (size_t)s * C::D);
+  const char* pc = reinterpret_cast<const char*>(pst + (size_t)s * C::D);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += NTA) {   // the pass's RZ diagonal (pass_a_bwd's tables)
+    cf a = {1.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const float4 t = trig[b];
+      a = cmul(a, cf{t.z, ((i >> b) & 1) ? -t.w : t.w});
+    }
+    ZL[i] = a;
+    if (i < (1 << (AB - 8))) {
+      cf h = {1.f, 0.f};
+#pragma unroll
+      for (int b = 8; b < AB; ++b) {
+        const float4 t = trig[brick_q(b)];
+        h = cmul(h, cf{t.z, ((i >> (b - 8)) & 1) ? -t.w : t.w});
+      }
+      ZH[i] = h;
+    }
+  }
+  const int t2 = 2 * threadIdx.x;
+#pragma unroll 1
+  for (int bi = 0; bi < BPB; ++bi) {
+    const int br = blockIdx.x * BPB + bi;
+    // (the thread's index opaque per brick: the addresses derived from it recomputed, not hoisted out of the loop --
+    // LICM'd, two dozen of them spilled at n = 16)
+    int tt = t2;
+    asm volatile("" : "+v"(tt));
+    const int pbb = padq(tt);
+    float4 na[NPAIR], nb[NPAIR];
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {   // (32-bit byte offsets from the sample's uniform base: one VGPR per address,
+                                        // 64-bit per-pair addresses kept live to the stores spilled)
+      const unsigned o = (unsigned)brick_k(tt + 2 * NTA * i, br) * (unsigned)sizeof(cf);
+      na[i] = *reinterpret_cast<const float4*>(pc + o);
+      nb[i] = *reinterpret_cast<const float4*>(lc + o);
+    }
+    __syncthreads();   // (the tables; the previous brick's tile and slab reads are done)
+    asm volatile("" : : : "memory");   // (the RZ factors re-read per brick: hoisted out of the loop they spilled)
+    cf p[2 * NPAIR], m[2 * NPAIR];
+    float csum = 0.f, cb[NRB];
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) cb[b] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      p[2 * i] = cf{na[i].x, na[i].y};
+      m[2 * i] = cf{nb[i].x, nb[i].y};
+      p[2 * i + 1] = cf{na[i].z, na[i].w};
+      m[2 * i + 1] = cf{nb[i].z, nb[i].w};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * i + h;
+        const float c = m[j].x * p[j].y - m[j].y * p[j].x;
+        csum += c;
+#pragma unroll
+        for (int b = 0; b < NRB; ++b) cb[b] += ((j >> b) & 1) ? -c : c;
+      }
+    }
+    asm volatile("" : "+v"(csum));
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) asm volatile("" : "+v"(cb[b]));
+#pragma unroll
+    for (int j = 0; j < 2 * NPAIR; ++j) {   // the pass's RZ phases undone on both states
+      const int i = j >> 1, h = j & 1;
+      const int eh = tt + 2 * NTA * i + h;
+      const cf z = ZSEP ? cmul(ZL[(tt + h) & 255], ZH[eh >> 8]) : cmul(ZL[eh & 255], ZH[eh >> 8]);
+      p[j] = cmul(p[j], z);
+      m[j] = cmul(m[j], z);
+    }
+    float dthr[NRB];   // d(theta) of the register bits (bit 0, bits RLO ..) from the pair as loaded
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) {
+      dthr[b] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2 * NPAIR; ++j)
+        if (!((j >> b) & 1)) {
+          const cf p0 = p[j], p1 = p[j | (1 << b)], l0 = m[j], l1 = m[j | (1 << b)];
+          dthr[b] += -(l0.x * p1.x + l0.y * p1.y) + (l1.x * p0.x + l1.y * p0.y);
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) asm volatile("" : "+v"(dthr[b]));
+#pragma unroll
+    for (int j = 0; j < 2 * NPAIR; ++j) T[pbb + (j & 1) + (j >> 1) * IST] = p[j];   // psi to the tile
+    // every d(phi): bit 0 and bits RLO.. by register index, bits 1 .. RLO - 1 by this thread's sign
+#pragma unroll
+    for (int b = 0; b < AB; ++b) {
+      const float dz = b == 0 ? cb[0] : b < RLO ? (((tt >> b) & 1) ? -csum : csum) : cb[b - RLO + 1];
+      const float sz = wave_sum(dz);
+      if (lane == 0) red[wv * 2 * AB + 2 * b + 1] = sz;
+    }
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) {
+      const float st = wave_sum(dthr[b]);
+      if (lane == 0) red[wv * 2 * AB + 2 * (b == 0 ? 0 : RLO + b - 1)] = st;
+    }
+    __syncthreads();   // psi's tile complete
+#pragma unroll 1
+    for (int b = 1; b < RLO; ++b) {   // d(theta) of the LDS bits: lambda here against psi's partners (rolled: one bit's
+                                      // NPAIR reads in flight -- all of them hoisted spilled at n = 16)
+      const int qb = padq(tt ^ (1 << b));
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i) {
+        const float4 q = *reinterpret_cast<const float4*>(T + qb + i * IST);
+        acc += m[2 * i].x * q.x + m[2 * i].y * q.y + m[2 * i + 1].x * q.z + m[2 * i + 1].y * q.w;
+      }
+      const float st = wave_sum(((tt >> b) & 1) ? acc : -acc);
+      if (lane == 0) red[wv * 2 * AB + 2 * b] = st;
+    }
+    __syncthreads();   // every partner read done: lambda takes the tile
+#pragma unroll
+    for (int j = 0; j < 2 * NPAIR; ++j) T[pbb + (j & 1) + (j >> 1) * IST] = m[j];
+    __syncthreads();
+    lds_group_lam<AB, 1, NB1, NTA, false, 1>(T, T, trig, red);
+    lds_group_lam<AB, 1 + NB1, NB2, NTA, false, 1>(T, T, trig, red);
+#pragma unroll
+    for (int j = 0; j < 2 * NPAIR; ++j) m[j] = T[pbb + (j & 1) + (j >> 1) * IST];
+#pragma unroll
+    for (int b = 0; b < NRB; ++b) {   // the register bits undone on lambda, then 16-byte stores in the load layout
+      const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
+#pragma unroll
+      for (int j = 0; j < 2 * NPAIR; ++j)
+        if (!((j >> b) & 1)) {
+          const cf m0 = m[j], m1 = m[j | (1 << b)];
+          m[j] = {tg.x * m0.x + tg.y * m1.x, tg.x * m0.y + tg.y * m1.y};
+          m[j | (1 << b)] = {tg.x * m1.x - tg.y * m0.x, tg.x * m1.y - tg.y * m0.y};
+        }
+    }
+    int ts = t2;   // (opaque again: the load addresses are not kept live for the stores)
+    asm volatile("" : "+v"(ts));
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i)
+      *reinterpret_cast<float4*>(lc + (unsigned)brick_k(ts + 2 * NTA * i, br) * (unsigned)sizeof(cf)) =
+          make_float4(m[2 * i].x, m[2 * i].y, m[2 * i + 1].x, m[2 * i + 1].y);
+    if (threadIdx.x < 2 * AB) {   // (the last group sweep ended with a barrier: every wave's slot is final)
+      float o = 0.f;
+#pragma unroll
+      for (int k = 0; k < NTA / 64; ++k) o += red[k * 2 * AB + threadIdx.x];
+      slab[((size_t)s * ROWS + br) * P + (l * N + brick_q(threadIdx.x / 2)) * 2 + (threadIdx.x & 1)] = o;
+    }
+  }
+}
+
 // dx[s][q] = sum over the sample's 16 slab rows of the layer-0 theta column
 __global__ void __launch_bounds__(256) reduce_dx(const float* __restrict__ slab, float* __restrict__ dx, int B, int N,
                                                  int P) {
@@ -1319,6 +1499,8 @@ struct Smem {
   static constexpr size_t B_BWD = 512 + (QD_STREAM_B4 ? 1 : 2) * sizeof(cf) * 4096 + 2048 + sizeof(cf) * (512 + 16);   // (+ FIRST / GEN0 / RZ tables)
   static constexpr size_t A_BWD = 1024 + 2 * sizeof(cf) * (SG<N>::AS + SG<N>::AS / 8) + sizeof(cf) * 512   // (+ GEN0 tables)
                                   + sizeof(cf) * (256 + 16);                                           // (+ RZ tables)
+  // pass_a_bwd1: one padq tile + the RZ tables
+  static constexpr size_t A_BWD1 = 1024 + sizeof(cf) * (SG<N>::AS + PADQ * (SG<N>::AS / 32) + 256 + 16);
 };
 
 inline size_t state_bytes(int n, int B) { return (size_t)B * (8ull << n); }
@@ -1381,6 +1563,9 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     (void)allow_lds(pass_a_bwd<N, true, false, 2>, S::A_BWD);
     (void)allow_lds(pass_a_bwd<N, true, false, 4>, S::A_BWD);
     (void)allow_lds(pass_a_bwd<N, false, true, 1>, S::A_BWD);
+    (void)allow_lds(pass_a_bwd1<N, 1>, S::A_BWD1);
+    (void)allow_lds(pass_a_bwd1<N, 2>, S::A_BWD1);
+    (void)allow_lds(pass_a_bwd1<N, 4>, S::A_BWD1);
     attr = true;
   }
   // bricks per workgroup of the reverse pass A (1 / 2 / 4 instantiated; 4 measured fastest in round 3; QDML_QSTREAM_BPB
@@ -1425,7 +1610,16 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
       else
         hipLaunchKernelGGL((pass_b_bwd<N, false, true>), gb, dim3(NT), S::B_BWD, st, xc, wc, gc, L, l, wgroup, ps, lin,
                            lo, slc);
-      if (l > 0) {
+      if (l > 0 && QD_STREAM_A1T) {
+        if (bpb == 4)
+          hipLaunchKernelGGL((pass_a_bwd1<N, 4>), dim3(ROWS / 4, Bc), dim3(C::NTA), S::A_BWD1, st, xc, wc, L, l, wgroup,
+                             ps, lo, slc);
+        else if (bpb == 2)
+          hipLaunchKernelGGL((pass_a_bwd1<N, 2>), dim3(ROWS / 2, Bc), dim3(C::NTA), S::A_BWD1, st, xc, wc, L, l, wgroup,
+                             ps, lo, slc);
+        else
+          hipLaunchKernelGGL((pass_a_bwd1<N, 1>), ga, dim3(C::NTA), S::A_BWD1, st, xc, wc, L, l, wgroup, ps, lo, slc);
+      } else if (l > 0) {
         if (bpb == 4)
           hipLaunchKernelGGL((pass_a_bwd<N, true, false, 4>), dim3(ROWS / 4, Bc), dim3(C::NTA), S::A_BWD, st, xc, wc, L,
                              l, wgroup, ps, lo, slc);
