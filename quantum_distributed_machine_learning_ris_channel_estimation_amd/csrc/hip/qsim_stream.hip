@@ -579,8 +579,9 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     // barriers of 2 instead of 4 sweeps + the store loop
     constexpr int NPAIR = C::AS / (2 * NT), RLO = ilog2c(2 * NT), NRB = 1 + ilog2c(NPAIR);
     // (F2) the pass's RZ diagonal: ZL over brick bits 0..7, ZH over 8.. (qubit q's factor cos(phi/2) -+ i sin(phi/2),
-    // - for bit 0), past the padded image and the GEN tables; read by the last group after two barriers
-    cf* ZLf = tp + C::AS + PADQ * (C::AS / 32) + 512;
+    // - for bit 0), right past the padded image (the GEN tables after them: without them the pass holds 37.5 KB of
+    // LDS, four workgroups per CU); read by the last group after two barriers
+    cf* ZLf = tp + C::AS + PADQ * (C::AS / 32);
     cf* ZHf = ZLf + 256;
     if constexpr (QD_STREAM_F2) {
       const int i = threadIdx.x;
@@ -603,7 +604,7 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     }
     cf p[2 * NPAIR];
     if constexpr (GEN) {   // the ring image of the layer-0 product state, generated in registers
-      cf* PL = tp + C::AS + PADQ * (C::AS / 32);   // (past the padded image)
+      cf* PL = tp + C::AS + PADQ * (C::AS / 32) + 256 + 16;   // (past the padded image and the RZ tables)
       cf* PH = PL + 256;
       product_tables<N, NT>(trig0, PL, PH, 0);
       __syncthreads();
@@ -854,21 +855,23 @@ __global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const flo
     // from there, 16 runs of 512 bytes per wave.  The LDS tile carried psi, the two-group adjoint sweep over both
     // states and the store loop before: 1 LDS scatter + 1 gather and 2 barriers now, against 6 sweeps and 4.
     cf p[16], m[16];
+    // (32-bit byte offsets from uniform bases below: one VGPR per address instead of a 64-bit pair -- with those the
+    // kernel spilled at its 128-VGPR bound)
     if constexpr (!GEN0) {   // psi = S_l: loads in flight across the lambda scatter below
-      const cf* src = psi + (size_t)s * C::D + ((size_t)t << 12);
+      const char* src = reinterpret_cast<const char*>(psi + (size_t)s * C::D + ((size_t)t << 12));
 #pragma unroll
-      for (int h = 0; h < 16; ++h) p[h] = src[(h << 8) | c];
+      for (int h = 0; h < 16; ++h) p[h] = *reinterpret_cast<const cf*>(src + (unsigned)((h << 8) | c) * 8u);
     }
     if constexpr (!FIRST) {   // lambda at the ring images -> pre-ring order in LDS
       const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
-      const cf* ls = lin + (size_t)s * C::D;
+      const char* ls = reinterpret_cast<const char*>(lin + (size_t)s * C::D);
       // all 16 loads in flight before the scatter (4 at a time, layer 0's pass -- no psi loads beside them -- ran
       // at 2.8 TB/s)
       cf lv[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int i = threadIdx.x + NT * u;
-        lv[u] = ls[i | ((i & 2048 ? A1 : A0) << 12)];
+        lv[u] = *reinterpret_cast<const cf*>(ls + (unsigned)(i | ((i & 2048 ? A1 : A0) << 12)) * 8u);
       }
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
@@ -951,10 +954,12 @@ __global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const flo
     // the sums pinned here (sunk past block_sum_vec's barrier they kept every product alive: 249 VGPRs spilled)
 #pragma unroll
     for (int b = 0; b < 4; ++b) asm volatile("" : "+v"(dth[b]), "+v"(dph[b]));
-    cf* lo = lout + (size_t)s * C::D + ((size_t)t << 12);
+    char* lo = reinterpret_cast<char*>(lout + (size_t)s * C::D + ((size_t)t << 12));
+    int cs = c;   // (opaque: the psi loads' offsets are not kept live -- spilled -- for these stores)
+    asm volatile("" : "+v"(cs));
 #pragma unroll
     for (int h = 0; h < (GEN0 ? 1 : 16); ++h)   // (GEN0: only bits 8..11 = 0, the part layer 0's pass A reads)
-      *reinterpret_cast<float2*>(lo + ((h << 8) | c)) = make_float2(m[h].x, m[h].y);
+      *reinterpret_cast<float2*>(lo + (unsigned)((h << 8) | cs) * 8u) = make_float2(m[h].x, m[h].y);
     float v[8];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -1492,8 +1497,10 @@ __global__ void __launch_bounds__(256) reduce_dx(const float* __restrict__ slab,
 // ------------------------------------------------------------------------------------------ host
 template <int N>
 struct Smem {
-  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 16 + 512 + 256 + 16);   // (padq image + the GEN
-                                                                                                    // and RZ tables)
+  // pass A forward: the padq image + the RZ tables (37.5 KB at n = 16: four workgroups per CU), + the GEN tables
+  static_assert(PADQ <= 2, "the images are sized for at most two pad amplitudes per 32");
+  static constexpr size_t A_FWD = 512 + sizeof(cf) * (SG<N>::AS + SG<N>::AS / 16 + 256 + 16);
+  static constexpr size_t A_FWD_GEN = A_FWD + sizeof(cf) * 512;
   static constexpr size_t B_FWD = 512 + sizeof(cf) * 4096;
   // (QD_STREAM_B4: lambda's tile only -- 39 KB, four workgroups per CU)
   static constexpr size_t B_BWD = 512 + (QD_STREAM_B4 ? 1 : 2) * sizeof(cf) * 4096 + 2048 + sizeof(cf) * (512 + 16);   // (+ FIRST / GEN0 / RZ tables)
@@ -1519,7 +1526,7 @@ static int fwd(const float* x, const float* w, float* E, int B, int L, int wgrou
   cf* S0 = reinterpret_cast<cf*>(ws + sb + epart_bytes(N, B));
   static bool attr = false;
   if (!attr) {
-    (void)allow_lds(pass_a_fwd<N, true>, S::A_FWD);
+    (void)allow_lds(pass_a_fwd<N, true>, S::A_FWD_GEN);
     (void)allow_lds(pass_a_fwd<N, false>, S::A_FWD);
     (void)allow_lds(pass_b_fwd<N, true>, S::B_FWD);
     (void)allow_lds(pass_b_fwd<N, false>, S::B_FWD);
@@ -1529,7 +1536,7 @@ static int fwd(const float* x, const float* w, float* E, int B, int L, int wgrou
   for (int l = 1; l < L; ++l) {
     cf* a_out = psave ? reinterpret_cast<cf*>(reinterpret_cast<char*>(psave) + (size_t)(l - 1) * sb) : S0;
     if (l == 1)
-      hipLaunchKernelGGL((pass_a_fwd<N, true>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, nullptr, a_out);
+      hipLaunchKernelGGL((pass_a_fwd<N, true>), ga, dim3(NT), S::A_FWD_GEN, st, x, w, L, l, wgroup, nullptr, a_out);
     else
       hipLaunchKernelGGL((pass_a_fwd<N, false>), ga, dim3(NT), S::A_FWD, st, x, w, L, l, wgroup, T, a_out);
     if (l == L - 1)
@@ -1568,11 +1575,12 @@ static int bwd(const float* x, const float* w, const float* gE, float* dx, float
     (void)allow_lds(pass_a_bwd1<N, 4>, S::A_BWD1);
     attr = true;
   }
-  // bricks per workgroup of the reverse pass A (1 / 2 / 4 instantiated; 4 measured fastest in round 3; QDML_QSTREAM_BPB
-  // overrides it for measurements)
+  // bricks per workgroup of the reverse pass A (1 / 2 / 4 instantiated; QDML_QSTREAM_BPB overrides it for
+  // measurements): 4 for the two-tile kernel (measured fastest in round 3), 1 for the one-tile kernel (three
+  // workgroups per CU): backward 3.04-3.06 against 3.10-3.11 ms at 4 (profiles/r6_50_qstream_bpb_probe.txt)
   static const int bpb = [] {
     const char* e = std::getenv("QDML_QSTREAM_BPB");
-    const int v = e ? std::atoi(e) : 4;
+    const int v = e ? std::atoi(e) : (QD_STREAM_A1T ? 1 : 4);
     return (v == 1 || v == 2) ? v : 4;
   }();
   // (round 6) samples per backward chunk: the whole adjoint (all layers) runs chunk by chunk, so the two lambda
