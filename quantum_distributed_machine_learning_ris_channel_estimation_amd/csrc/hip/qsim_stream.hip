@@ -569,6 +569,16 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
   float4* trig0 = trig + 16;                                 // 16 (GEN)
   cf* tp = reinterpret_cast<cf*>(smem + 512);
   const int br = blockIdx.x, s = blockIdx.y;
+  // (A4F, not GEN) the brick's loads issued first: in flight across the angle loads and the tables (behind them they
+  // were a second round trip per workgroup)
+  constexpr int NPAIRF = C::AS / (2 * NT);
+  [[maybe_unused]] float4 v0[NPAIRF];
+  if constexpr (QD_STREAM_A4F && !GEN) {
+    const cf* si = in + (size_t)s * C::D;
+#pragma unroll
+    for (int i = 0; i < NPAIRF; ++i)
+      v0[i] = *reinterpret_cast<const float4*>(si + brick_k(2 * threadIdx.x + 2 * NT * i, br));
+  }
   load_trig<N>(trig, x, w, s, L, l, wgroup);
   if constexpr (GEN) load_trig<N>(trig0, x, w, s, L, 0, wgroup);
   __syncthreads();
@@ -614,15 +624,10 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
         p[j] = cmul(PL[k & 255], PH[k >> 8]);
       }
     } else {
-      const cf* si = in + (size_t)s * C::D;
-      float4 v[NPAIR];
-#pragma unroll
-      for (int i = 0; i < NPAIR; ++i)
-        v[i] = *reinterpret_cast<const float4*>(si + brick_k(2 * threadIdx.x + 2 * NT * i, br));
 #pragma unroll
       for (int i = 0; i < NPAIR; ++i) {
-        p[2 * i] = cf{v[i].x, v[i].y};
-        p[2 * i + 1] = cf{v[i].z, v[i].w};
+        p[2 * i] = cf{v0[i].x, v0[i].y};
+        p[2 * i + 1] = cf{v0[i].z, v0[i].w};
       }
     }
 #pragma unroll
@@ -688,6 +693,12 @@ __global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x,
   float* red = reinterpret_cast<float*>(smem + 256);          // NWV * N floats
   cf* tp = reinterpret_cast<cf*>(smem + 512);
   const int t = blockIdx.x, s = blockIdx.y, c = threadIdx.x;
+  // the tile's loads first: in flight across the angle loads (behind them, a second round trip for wave 0 that the
+  // barrier below made every wave wait out)
+  const cf* src = in + (size_t)s * C::D + ((size_t)t << 12);
+  cf a[16];
+#pragma unroll
+  for (int h = 0; h < 16; ++h) a[h] = src[(h << 8) | c];
   load_trig<N>(trig, x, w, s, L, l, wgroup);
   // (F2, not LAST) the four RZ of qubits 8..11 as one phase per amplitude: ZT[h] built by threads 0..15 from the
   // weights directly, so the one barrier below covers it too.  LAST: the phases do not change |amplitude|^2 -- none.
@@ -705,10 +716,6 @@ __global__ void __launch_bounds__(NT, 2) pass_b_fwd(const float* __restrict__ x,
       ZT[threadIdx.x] = z;
     }
   }
-  const cf* src = in + (size_t)s * C::D + ((size_t)t << 12);
-  cf a[16];
-#pragma unroll
-  for (int h = 0; h < 16; ++h) a[h] = src[(h << 8) | c];
   __syncthreads();
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
@@ -824,6 +831,24 @@ __global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const flo
   cf* PH = PL + 256;
   [[maybe_unused]] cf* ZT = PH + 256;                     // (QD_STREAM_B4 == 2) the 16 RZ undo phases of qubits 8..11
   const int t = blockIdx.x, s = blockIdx.y, c = threadIdx.x;
+  // (B4) the tile's psi and lambda loads first: in flight across the angle / dL/dE loads and the tables (behind them,
+  // a second round trip for wave 0 that the barrier made every wave wait out).  32-bit byte offsets from uniform
+  // bases: one VGPR per address instead of a 64-bit pair.
+  [[maybe_unused]] cf p[16], lv[16];
+  if constexpr (QD_STREAM_B4 && !GEN0) {   // psi = S_l
+    const char* src = reinterpret_cast<const char*>(psi + (size_t)s * C::D + ((size_t)t << 12));
+#pragma unroll
+    for (int h = 0; h < 16; ++h) p[h] = *reinterpret_cast<const cf*>(src + (unsigned)((h << 8) | c) * 8u);
+  }
+  if constexpr (QD_STREAM_B4 && !FIRST) {   // lambda at the ring images of this tile's pre-ring amplitudes
+    const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
+    const char* ls = reinterpret_cast<const char*>(lin + (size_t)s * C::D);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = threadIdx.x + NT * u;
+      lv[u] = *reinterpret_cast<const cf*>(ls + (unsigned)(i | ((i & 2048 ? A1 : A0) << 12)) * 8u);
+    }
+  }
   load_trig<N>(trig, x, w, s, L, l, wgroup);
   if (FIRST && threadIdx.x < N) gq[threadIdx.x] = gE[(size_t)s * N + threadIdx.x];
   __syncthreads();
@@ -854,25 +879,9 @@ __global__ void __launch_bounds__(NT, QD_STREAM_B4 ? 4 : 2) pass_b_bwd(const flo
     // psi as loaded (or generated), lambda read back from the ring scatter (or formed from psi) -- and stores lambda
     // from there, 16 runs of 512 bytes per wave.  The LDS tile carried psi, the two-group adjoint sweep over both
     // states and the store loop before: 1 LDS scatter + 1 gather and 2 barriers now, against 6 sweeps and 4.
-    cf p[16], m[16];
-    // (32-bit byte offsets from uniform bases below: one VGPR per address instead of a 64-bit pair -- with those the
-    // kernel spilled at its 128-VGPR bound)
-    if constexpr (!GEN0) {   // psi = S_l: loads in flight across the lambda scatter below
-      const char* src = reinterpret_cast<const char*>(psi + (size_t)s * C::D + ((size_t)t << 12));
-#pragma unroll
-      for (int h = 0; h < 16; ++h) p[h] = *reinterpret_cast<const cf*>(src + (unsigned)((h << 8) | c) * 8u);
-    }
-    if constexpr (!FIRST) {   // lambda at the ring images -> pre-ring order in LDS
+    cf m[16];
+    if constexpr (!FIRST) {   // lambda (loaded at the top, all 16 in flight) -> pre-ring order in LDS
       const int A0 = ring_fwd<N>(t << 12) >> 12, A1 = ring_fwd<N>((t << 12) | 2048) >> 12;
-      const char* ls = reinterpret_cast<const char*>(lin + (size_t)s * C::D);
-      // all 16 loads in flight before the scatter (4 at a time, layer 0's pass -- no psi loads beside them -- ran
-      // at 2.8 TB/s)
-      cf lv[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = threadIdx.x + NT * u;
-        lv[u] = *reinterpret_cast<const cf*>(ls + (unsigned)(i | ((i & 2048 ? A1 : A0) << 12)) * 8u);
-      }
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int i = threadIdx.x + NT * u;
@@ -1337,9 +1346,23 @@ __global__ void __launch_bounds__(SG<N>::NTA, QD_STREAM_A1T_OCC) pass_a_bwd1(con
   const int s = blockIdx.y;
   const int P = 2 * N * L;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  load_trig<N>(trig, x, w, s, L, l, wgroup);
   char* lc = reinterpret_cast<char*>(lst + (size_t)s * C::D);
   const char* pc = reinterpret_cast<const char*>(pst + (size_t)s * C::D);
+  const int t2 = 2 * threadIdx.x;
+  // psi / lambda pairs of a brick (32-bit byte offsets from the sample's uniform bases: one VGPR per address, the
+  // 64-bit per-pair addresses kept live to the stores spilled); the first brick's issued before the angle loads and
+  // the tables, in flight across them
+  float4 na[NPAIR], nb[NPAIR];
+  auto load_brick = [&](int br, int tt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      const unsigned o = (unsigned)brick_k(tt + 2 * NTA * i, br) * (unsigned)sizeof(cf);
+      na[i] = *reinterpret_cast<const float4*>(pc + o);
+      nb[i] = *reinterpret_cast<const float4*>(lc + o);
+    }
+  };
+  load_brick(blockIdx.x * BPB, t2);
+  load_trig<N>(trig, x, w, s, L, l, wgroup);
   __syncthreads();
   for (int i = threadIdx.x; i < 256; i += NTA) {   // the pass's RZ diagonal (pass_a_bwd's tables)
     cf a = {1.f, 0.f};
@@ -1359,7 +1382,6 @@ __global__ void __launch_bounds__(SG<N>::NTA, QD_STREAM_A1T_OCC) pass_a_bwd1(con
       ZH[i] = h;
     }
   }
-  const int t2 = 2 * threadIdx.x;
 #pragma unroll 1
   for (int bi = 0; bi < BPB; ++bi) {
     const int br = blockIdx.x * BPB + bi;
@@ -1368,14 +1390,7 @@ __global__ void __launch_bounds__(SG<N>::NTA, QD_STREAM_A1T_OCC) pass_a_bwd1(con
     int tt = t2;
     asm volatile("" : "+v"(tt));
     const int pbb = padq(tt);
-    float4 na[NPAIR], nb[NPAIR];
-#pragma unroll
-    for (int i = 0; i < NPAIR; ++i) {   // (32-bit byte offsets from the sample's uniform base: one VGPR per address,
-                                        // 64-bit per-pair addresses kept live to the stores spilled)
-      const unsigned o = (unsigned)brick_k(tt + 2 * NTA * i, br) * (unsigned)sizeof(cf);
-      na[i] = *reinterpret_cast<const float4*>(pc + o);
-      nb[i] = *reinterpret_cast<const float4*>(lc + o);
-    }
+    if (bi > 0) load_brick(br, tt);
     __syncthreads();   // (the tables; the previous brick's tile and slab reads are done)
     asm volatile("" : : : "memory");   // (the RZ factors re-read per brick: hoisted out of the loop they spilled)
     cf p[2 * NPAIR], m[2 * NPAIR];
