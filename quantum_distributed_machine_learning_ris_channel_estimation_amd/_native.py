@@ -79,7 +79,11 @@ def hipcc() -> Optional[str]:
 # qsim_stream.hip: no SLP vectorisation (packed-f32 pairs of the complex gate math doubled the register
 # demand: the adjoint passes spilled at 256 VGPRs, 86-92 without)
 # hazard_probe.hip: the one file WITH packed-FP32 instructions (its inline asm demonstrates their hazard; see below)
-PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "qsim_stream.hip": ["-fno-slp-vectorize"],
+# qsim_stream.hip also without the SI load/store optimizer: it pairs the streamed passes' 8-byte LDS accesses into
+# ds_read2_b64 / ds_write2_b64, whose banks wrap every 32 dwords -- 24 % of the reverse pass A's LDS cycles were bank
+# conflicts (profiles/r6_54_qstream_pmc_b.md); single ds_read_b64 bank on 64 (QDML_QSTREAM_LSO=1: the paired build)
+_QS_LSO = [] if os.environ.get("QDML_QSTREAM_LSO") == "1" else ["-Xclang", "-target-feature", "-Xclang", "-load-store-opt"]
+PER_FILE_FLAGS = {"gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"], "qsim_stream.hip": ["-fno-slp-vectorize"] + _QS_LSO,
                   "qsim_mfma.hip": ["-fno-slp-vectorize"], "qsim12_mfma.hip": ["-fno-slp-vectorize"],
                   "hazard_probe.hip": ["-Xclang", "-target-feature", "-Xclang", "+packed-fp32-ops"]}
 # No packed-FP32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) anywhere else (round 6).  On gfx950 a packed-FP32
@@ -106,6 +110,7 @@ def build_hip(force: bool = False, verbose: bool = True, jobs: int = 8) -> str:
     # a changed flag set (a tuning build, then the default again) rebuilds every object
     stamp = os.path.join(OBJ_DIR, "flags.txt")
     want = " ".join(f for f in flags if not f.startswith("/"))   # (not the include path: the tree moves)
+    want += " " + repr(sorted(PER_FILE_FLAGS.items()))
     if not force and (not os.path.exists(stamp) or open(stamp).read() != want):
         force = True
     objs = []

@@ -406,6 +406,10 @@ __device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float
 #endif
 constexpr int PADQ = QD_STREAM_PADQ;
 __device__ __forceinline__ int padq(int e) { return e + PADQ * (e >> 5); }
+// a 16-byte aligned pair of amplitudes in an LDS image (even padq index): one ds_read_b128 / ds_write_b128 per lane
+// instead of the ds_read2_b64 / ds_write2_b64 the compiler forms from two 8-byte accesses (whose banks wrap every
+// 32 dwords: 4x the LDS cycles of b128 for the same 16 bytes)
+__device__ __forceinline__ float4* lds16(cf* p) { return reinterpret_cast<float4*>(__builtin_assume_aligned(p, 16)); }
 
 // OUT: 0 = both states back to LDS, 1 = lambda back to LDS, 2 = lambda straight to its state in HBM (gdst, brick br:
 // for a fixed register index the lanes hold runs of 32 consecutive amplitudes, 256-byte pieces of the state)
@@ -642,7 +646,9 @@ __global__ void __launch_bounds__(NT, 2) pass_a_fwd(const float* __restrict__ x,
     }
     const int pb = padq(2 * threadIdx.x);
 #pragma unroll
-    for (int j = 0; j < 2 * NPAIR; ++j) tp[pb + (j & 1) + (j >> 1) * (2 * NT + PADQ * ((2 * NT) / 32))] = p[j];
+    for (int i = 0; i < NPAIR; ++i)
+      *lds16(tp + pb + i * (2 * NT + PADQ * ((2 * NT) / 32))) = make_float4(p[2 * i].x, p[2 * i].y, p[2 * i + 1].x,
+                                                                             p[2 * i + 1].y);
     __syncthreads();
     constexpr int NB1 = RLO - 1 < 4 ? RLO - 1 : 4;
     static_assert(RLO > 1 + NB1, "two LDS groups");
@@ -1437,7 +1443,8 @@ __global__ void __launch_bounds__(SG<N>::NTA, QD_STREAM_A1T_OCC) pass_a_bwd1(con
 #pragma unroll
     for (int b = 0; b < NRB; ++b) asm volatile("" : "+v"(dthr[b]));
 #pragma unroll
-    for (int j = 0; j < 2 * NPAIR; ++j) T[pbb + (j & 1) + (j >> 1) * IST] = p[j];   // psi to the tile
+    for (int i = 0; i < NPAIR; ++i)   // psi to the tile
+      *lds16(T + pbb + i * IST) = make_float4(p[2 * i].x, p[2 * i].y, p[2 * i + 1].x, p[2 * i + 1].y);
     // every d(phi): bit 0 and bits RLO.. by register index, bits 1 .. RLO - 1 by this thread's sign
 #pragma unroll
     for (int b = 0; b < AB; ++b) {
@@ -1466,12 +1473,17 @@ __global__ void __launch_bounds__(SG<N>::NTA, QD_STREAM_A1T_OCC) pass_a_bwd1(con
     }
     __syncthreads();   // every partner read done: lambda takes the tile
 #pragma unroll
-    for (int j = 0; j < 2 * NPAIR; ++j) T[pbb + (j & 1) + (j >> 1) * IST] = m[j];
+    for (int i = 0; i < NPAIR; ++i)
+      *lds16(T + pbb + i * IST) = make_float4(m[2 * i].x, m[2 * i].y, m[2 * i + 1].x, m[2 * i + 1].y);
     __syncthreads();
     lds_group_lam<AB, 1, NB1, NTA, false, 1>(T, T, trig, red);
     lds_group_lam<AB, 1 + NB1, NB2, NTA, false, 1>(T, T, trig, red);
 #pragma unroll
-    for (int j = 0; j < 2 * NPAIR; ++j) m[j] = T[pbb + (j & 1) + (j >> 1) * IST];
+    for (int i = 0; i < NPAIR; ++i) {
+      const float4 q = *lds16(T + pbb + i * IST);
+      m[2 * i] = cf{q.x, q.y};
+      m[2 * i + 1] = cf{q.z, q.w};
+    }
 #pragma unroll
     for (int b = 0; b < NRB; ++b) {   // the register bits undone on lambda, then 16-byte stores in the load layout
       const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
