@@ -398,6 +398,9 @@ __device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float
 #ifndef QD_STREAM_A1T
 #define QD_STREAM_A1T 1
 #endif
+#ifndef QD_STREAM_A1T_OUT2
+#define QD_STREAM_A1T_OUT2 1
+#endif
 #ifndef QD_STREAM_A1T_OCC
 #define QD_STREAM_A1T_OCC 3
 #endif
@@ -1471,36 +1474,47 @@ __global__ void __launch_bounds__(SG<N>::NTA, QD_STREAM_A1T_OCC) pass_a_bwd1(con
       const float st = wave_sum(((tt >> b) & 1) ? acc : -acc);
       if (lane == 0) red[wv * 2 * AB + 2 * b] = st;
     }
+    // the register bits undone on lambda here or after the LDS groups: RY of different qubits commute
+    auto undo_reg = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int b = 0; b < NRB; ++b) {
+        const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
+#pragma unroll
+        for (int j = 0; j < 2 * NPAIR; ++j)
+          if (!((j >> b) & 1)) {
+            const cf m0 = m[j], m1 = m[j | (1 << b)];
+            m[j] = {tg.x * m0.x + tg.y * m1.x, tg.x * m0.y + tg.y * m1.y};
+            m[j | (1 << b)] = {tg.x * m1.x - tg.y * m0.x, tg.x * m1.y - tg.y * m0.y};
+          }
+      }
+    };
+    if constexpr (QD_STREAM_A1T_OUT2) undo_reg();
     __syncthreads();   // every partner read done: lambda takes the tile
 #pragma unroll
     for (int i = 0; i < NPAIR; ++i)
       *lds16(T + pbb + i * IST) = make_float4(m[2 * i].x, m[2 * i].y, m[2 * i + 1].x, m[2 * i + 1].y);
     __syncthreads();
     lds_group_lam<AB, 1, NB1, NTA, false, 1>(T, T, trig, red);
-    lds_group_lam<AB, 1 + NB1, NB2, NTA, false, 1>(T, T, trig, red);
+    if constexpr (QD_STREAM_A1T_OUT2) {
+      // (OUT2) the second group stores lambda straight to HBM -- runs of 32 amplitudes per register index -- instead of
+      // writing the tile back for a read-back in the load layout
+      lds_group_lam<AB, 1 + NB1, NB2, NTA, false, 2>(T, T, trig, red, reinterpret_cast<cf*>(lc), br);
+    } else {
+      lds_group_lam<AB, 1 + NB1, NB2, NTA, false, 1>(T, T, trig, red);
 #pragma unroll
-    for (int i = 0; i < NPAIR; ++i) {
-      const float4 q = *lds16(T + pbb + i * IST);
-      m[2 * i] = cf{q.x, q.y};
-      m[2 * i + 1] = cf{q.z, q.w};
+      for (int i = 0; i < NPAIR; ++i) {
+        const float4 q = *lds16(T + pbb + i * IST);
+        m[2 * i] = cf{q.x, q.y};
+        m[2 * i + 1] = cf{q.z, q.w};
+      }
+      undo_reg();   // then 16-byte stores in the load layout
+      int ts = t2;   // (opaque again: the load addresses are not kept live for the stores)
+      asm volatile("" : "+v"(ts));
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i)
+        *reinterpret_cast<float4*>(lc + (unsigned)brick_k(ts + 2 * NTA * i, br) * (unsigned)sizeof(cf)) =
+            make_float4(m[2 * i].x, m[2 * i].y, m[2 * i + 1].x, m[2 * i + 1].y);
     }
-#pragma unroll
-    for (int b = 0; b < NRB; ++b) {   // the register bits undone on lambda, then 16-byte stores in the load layout
-      const float4 tg = trig[brick_q(b == 0 ? 0 : RLO + b - 1)];
-#pragma unroll
-      for (int j = 0; j < 2 * NPAIR; ++j)
-        if (!((j >> b) & 1)) {
-          const cf m0 = m[j], m1 = m[j | (1 << b)];
-          m[j] = {tg.x * m0.x + tg.y * m1.x, tg.x * m0.y + tg.y * m1.y};
-          m[j | (1 << b)] = {tg.x * m1.x - tg.y * m0.x, tg.x * m1.y - tg.y * m0.y};
-        }
-    }
-    int ts = t2;   // (opaque again: the load addresses are not kept live for the stores)
-    asm volatile("" : "+v"(ts));
-#pragma unroll
-    for (int i = 0; i < NPAIR; ++i)
-      *reinterpret_cast<float4*>(lc + (unsigned)brick_k(ts + 2 * NTA * i, br) * (unsigned)sizeof(cf)) =
-          make_float4(m[2 * i].x, m[2 * i].y, m[2 * i + 1].x, m[2 * i + 1].y);
     if (threadIdx.x < 2 * AB) {   // (the last group sweep ended with a barrier: every wave's slot is final)
       float o = 0.f;
 #pragma unroll
