@@ -401,6 +401,8 @@ __device__ __forceinline__ void lds_dtheta_then_undo(cf* tp, cf* tq, const float
 #ifndef QD_STREAM_A1T_OUT2
 #define QD_STREAM_A1T_OUT2 1
 #endif
+// pass_a_bwd1's launch-bounds workgroups per CU (its register budget): the library build needs 89 VGPRs at n = 16, so
+// its 38 KB of LDS sets the occupancy -- four workgroups per CU; 4 here measured level (profiles/r6_50_*)
 #ifndef QD_STREAM_A1T_OCC
 #define QD_STREAM_A1T_OCC 3
 #endif
